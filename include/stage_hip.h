@@ -1,0 +1,199 @@
+/*
+ * stage_hip.h -- C-ABI of the MI355X-native index-organized probe/scan path.
+ *
+ * This is the drop-in boundary for the hot path of sheepTnT/Stage-IndexOrganized
+ * (reference @ 2024-12-18).  Every entry point below names the reference interface it
+ * replaces (file:line inside the reference checkout).  All types are plain C: fixed-width
+ * integers and pointers; no C++ exceptions cross this boundary.  Device pointers are
+ * HIP device allocations (stage_dev_alloc or any hipMalloc'd buffer of the same
+ * process); `stream` is a hipStream_t passed as void* (NULL = the table's own stream).
+ *
+ * Return value of every int function: STAGE_OK (0) or a negative STAGE_E_* code;
+ * stage_last_error() gives the message for the calling thread.
+ */
+#ifndef STAGE_HIP_H_
+#define STAGE_HIP_H_
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define STAGE_OK 0
+#define STAGE_E_ARG (-1)
+#define STAGE_E_HIP (-2)
+#define STAGE_E_NOMEM (-3)
+#define STAGE_E_STATE (-4)
+#define STAGE_E_UNSUPPORTED (-5)
+#define STAGE_E_RCCL (-6)
+
+/* ReturnCode (include/vstore/b_tree.h:42-54), reported by the host write path */
+#define STAGE_RC_INVALID 0
+#define STAGE_RC_OK 1
+#define STAGE_RC_KEY_EXISTS 2
+#define STAGE_RC_NOT_FOUND 3
+#define STAGE_RC_NODE_FROZEN 4
+#define STAGE_RC_CAS_FAIL 5
+#define STAGE_RC_NOT_ENOUGH_SPACE 6
+#define STAGE_RC_NOT_NEEDED_UPDATE 7
+#define STAGE_RC_RETRY_FAILURE 8
+#define STAGE_RC_DIRTY 9
+
+/* per-probe status (canonical outcome of BTree::Read b_tree.cpp:2066-2129 followed by the
+ * point-lookup branch of IndexScanExecutor::Execute, executor.h:374-454) */
+#define STAGE_ST_NOT_FOUND 0      /* Read returned nullptr                                */
+#define STAGE_ST_LATEST 1         /* txn_id >= meta cstamp, tuple from the leaf            */
+#define STAGE_ST_COPY 2           /* in-flight update: tuple from the overwrite copy       */
+#define STAGE_ST_OLD 3            /* retired version from the TupleHeader chain            */
+#define STAGE_ST_FAIL_INVALID_TS 4/* chain hit begin/end == INVALID_CID -> ResultType::FAILURE */
+#define STAGE_ST_CHAIN_MISS 5     /* no version visible to txn_id (tuple stays null)       */
+
+#define STAGE_FLAG_COPY_PRESENT 1u /* PerformRead would find an overwrite header (tm.cpp:379-399) */
+
+typedef struct stage_table stage_table; /* one index-organized table: BTree + device image */
+
+/* ParameterSet (b_tree.h:23-40) plus the key column width of the Catalog */
+typedef struct stage_params {
+    uint32_t split_threshold; /* inner-node split threshold (YCSB: 16 KiB, ycsb.cpp:72)   */
+    uint32_t merge_threshold; /* (YCSB: 32 KiB)                                          */
+    uint32_t leaf_node_size;  /* leaf block == leaf split threshold (YCSB: 64 KiB)       */
+    uint32_t payload_size;    /* bytes after the 8-byte padded key (YCSB: 1000)          */
+    uint32_t key_width;       /* 1..8 = every key has this many bytes; 0 = variable 1..8 */
+    int32_t device;           /* HIP device ordinal for the device image                  */
+} stage_params;
+
+/* one probe result (32 B) */
+typedef struct stage_probe_out {
+    uint8_t status;       /* STAGE_ST_*                                                    */
+    uint8_t flags;        /* STAGE_FLAG_*                                                  */
+    uint16_t hops;        /* TupleHeader hops walked                                       */
+    uint32_t leaf;        /* leaf index in key order                                       */
+    uint16_t slot;        /* record slot inside the leaf (0xFFFF if none)                  */
+    uint16_t key_len;     /* key length of the hit record                                  */
+    uint32_t cstamp;      /* Record cstamp handed to PerformRead: latest -> read id,
+                             copy -> overwrite rstamp, old -> TupleHeader begin            */
+    uint32_t rec_cstamp;  /* meta.GetTxnCommitId() of the hit slot (executor.h:383)        */
+    uint32_t copy_sstamp; /* overwrite header sstamp, 0xFFFFFFFF when none                 */
+    uint32_t image;       /* record-heap row that supplied the tuple (0xFFFFFFFF if none)  */
+    uint32_t reserved;
+} stage_probe_out;
+
+const char *stage_last_error(void);
+const char *stage_version(void);
+
+/* ---- table lifecycle ------------------------------------------------------------------
+ * replaces: BTree::BTree (b_tree.h:793-803), ParameterSet (b_tree.h:23-40) */
+int stage_table_create(const stage_params *params, stage_table **out);
+int stage_table_destroy(stage_table *t);
+
+/* ---- host write path (kept on host per the north star) ---------------------------------
+ * stage_insert      = BTree::Insert + BTree::FinalizeInsert (b_tree.cpp:1849-2020, 2238-2251)
+ *                     payload == NULL inserts the generated payload of `gen_rowid`.
+ * stage_load_ycsb   = LoadYCSBRows (benchmark/ycsb/ycsb_loader.cpp:93-171), one loader,
+ *                     rows [begin,end) with key = rowid (key_size 4 or 8 bytes), payload
+ *                     mode 0 = memset(rowid) as the reference, 1 = per-word pattern.
+ * stage_load_keys   = the same for an explicit key order (keys are rowids).
+ * stage_update      = BTree::Update / LeafNode::Update (b_tree.cpp:2132-2160, 1061-1163)
+ * stage_commit_update = CommitTransaction UPDATE entry (transaction_manager.cpp:610-676)
+ * stage_finalize_update = BTree::FinalizeUpdate (b_tree.cpp:2252-2268)
+ * stage_delete      = BTree::Delete + FinalizeDelete (b_tree.cpp:2184-2237, 2275-2310)
+ * rc_out receives the reference ReturnCode (STAGE_RC_*). */
+int stage_insert(stage_table *t, uint64_t key, uint16_t key_size, const uint8_t *payload,
+                 uint64_t gen_rowid, int payload_mode, uint32_t commit_id, uint8_t *rc_out);
+int stage_load_ycsb(stage_table *t, uint64_t begin_rowid, uint64_t end_rowid, uint32_t key_size,
+                    int payload_mode, uint64_t *inserted);
+int stage_load_keys(stage_table *t, const uint64_t *keys, uint64_t n, uint32_t key_size,
+                    int payload_mode, uint64_t *inserted);
+int stage_update(stage_table *t, uint64_t key, uint16_t key_size, uint32_t payload_off,
+                 const uint8_t *delta, uint32_t delta_len, uint32_t writer_id, uint8_t *rc_out);
+int stage_commit_update(stage_table *t, uint64_t key, uint16_t key_size, uint32_t commit_id,
+                        uint32_t sstamp, uint8_t *rc_out);
+int stage_finalize_update(stage_table *t, uint64_t key, uint16_t key_size, uint32_t commit_id,
+                          uint8_t *rc_out);
+int stage_delete(stage_table *t, uint64_t key, uint16_t key_size, uint32_t commit_id,
+                 uint8_t *rc_out);
+
+/* publish the host layout to HBM (leaf key columns, slot words, visibility masks, the
+ * separator search tree, record heap, overwrite copies and retired versions). */
+int stage_sync(stage_table *t);
+
+/* stats[0]=height(host equivalent: 1 + ceil(log_fanout)) stats[1]=0 stats[2]=leaves
+ * stats[3]=records stats[4]=sorted slots stats[5]=unsorted slots stats[6]=max records/leaf
+ * stats[7]=retired versions */
+int stage_stats(stage_table *t, uint64_t *stats);
+uint32_t stage_record_stride(stage_table *t); /* bytes between output/heap rows */
+uint32_t stage_leaf_capacity(stage_table *t); /* slots per leaf on the device (64/128) */
+
+/* host traversal -> leaf index in key order (BTree::TraverseToLeaf, b_tree.cpp:1804-1846) */
+int stage_traverse_batch(stage_table *t, const uint64_t *keys, const uint16_t *lens, uint64_t n,
+                         int le_child, uint32_t *leaf_out);
+/* export the leaf layout (key order) for layout parity against a reference tree:
+ * rc/sc = record_count/sorted_count, meta words and key bytes per slot (cap slots) */
+int64_t stage_export_leaves(stage_table *t, uint32_t cap, uint64_t max_leaves, uint32_t *rc,
+                            uint32_t *sc, uint64_t *meta, uint64_t *keyw);
+
+/* ---- device batch path (the replaced hot path) ------------------------------------------
+ * stage_probe_batch  replaces LeafNode::Read/SearchRecordMeta (b_tree.cpp:1042-1051, 18-122),
+ *   Record::New/Neww (b_tree.h:407-448), BTree::Read (b_tree.cpp:2066-2129) and the
+ *   visibility walk of IndexScanExecutor (executor.h:374-454), batched.
+ *   d_keys[i]: key bytes little-endian in a u64; d_lens NULL -> table key_width;
+ *   d_read_ids NULL -> 0xFFFFFFFE; d_leaf_ids NULL -> device traversal of the separator
+ *   mirror, else host-traversed leaf indices (stage_traverse_batch).
+ *   d_records: n rows of stage_record_stride() bytes = [key padded to 8][payload]; NULL to
+ *   skip the tuple copy.
+ * stage_scan_batch replaces BTree::RangeScanBySize + Iterator::GetNext + TableScanExecutor
+ *   (b_tree.h:830-953, b_tree.cpp:1261-1315, executor.h:611-642): for each start key up to
+ *   scan_size tuples in KeyCompare order into d_records[i*scan_size + j], count in d_counts.
+ * stage_resolve_batch: device traversal only (le_child as TraverseToLeaf). */
+int stage_probe_batch(stage_table *t, const uint64_t *d_keys, const uint16_t *d_lens,
+                      const uint32_t *d_read_ids, const uint32_t *d_leaf_ids, uint64_t n,
+                      stage_probe_out *d_out, uint8_t *d_records, void *stream);
+int stage_scan_batch(stage_table *t, const uint64_t *d_start_keys, const uint16_t *d_lens,
+                     uint64_t n, uint32_t scan_size, uint32_t *d_counts, uint8_t *d_records,
+                     void *stream);
+int stage_resolve_batch(stage_table *t, const uint64_t *d_keys, const uint16_t *d_lens, uint64_t n,
+                        int le_child, uint32_t *d_leaf, void *stream);
+
+/* MurmurHash64A (misc/murmur/MurmurHash2.cpp:99-147) over n keys of key_len bytes laid out
+ * key_stride bytes apart; d_out[i] = hash.  Used as the multi-GPU shard router. */
+int stage_murmur64a_batch(const void *d_keys, uint32_t key_len, uint32_t key_stride, uint64_t seed,
+                          uint64_t n, uint64_t *d_out, void *stream);
+
+/* ---- multi-GPU: hash-sharded probe front-end over RCCL (one process per GPU) ------------
+ * stage_comm_unique_id fills 128 bytes on rank 0 (broadcast them out of band);
+ * stage_comm_init joins the communicator; stage_probe_sharded routes each key to rank
+ * MurmurHash64A(key, key_width, 0) % world, probes it there and returns the results in the
+ * caller's order (all-to-all-v out, local probe, all-to-all-v back). */
+int stage_comm_unique_id(uint8_t *id128);
+int stage_comm_init(stage_table *t, const uint8_t *id128, int rank, int world);
+int stage_comm_destroy(stage_table *t);
+int stage_probe_sharded(stage_table *t, const uint64_t *d_keys, const uint32_t *d_read_ids,
+                        uint64_t n, stage_probe_out *d_out, uint8_t *d_records, void *stream);
+
+/* ---- plumbing for callers without their own HIP binding (ctypes) ----------------------- */
+int stage_set_device(int device);
+int stage_device_count(int *count);
+int stage_dev_alloc(uint64_t bytes, void **ptr);
+int stage_dev_free(void *ptr);
+int stage_dev_memset(void *ptr, int value, uint64_t bytes, void *stream);
+int stage_memcpy_h2d(void *dst, const void *src, uint64_t bytes, void *stream);
+int stage_memcpy_d2h(void *dst, const void *src, uint64_t bytes, void *stream);
+int stage_stream_create(void **stream);
+int stage_stream_destroy(void *stream);
+int stage_stream_sync(void *stream);
+int stage_device_sync(void);
+/* event pair timing on `stream`: returns the elapsed milliseconds between two records */
+int stage_event_create(void **ev);
+int stage_event_destroy(void *ev);
+int stage_event_record(void *ev, void *stream);
+int stage_event_elapsed(void *ev_start, void *ev_stop, float *ms);
+
+/* ---- YCSB harness generators (benchmark/benchmark_common.h:12-105) -----------------------
+ * FastRandom(seed) stream and ZipfDistribution(n, theta).GetNextNumber() draws in [1, n]. */
+int stage_fastrandom_next(uint64_t seed, uint64_t count, uint64_t *out);
+int stage_zipf_draws(uint64_t n, double theta, uint64_t seed, uint64_t count, uint64_t *out,
+                     int nthreads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

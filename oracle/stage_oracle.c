@@ -1,0 +1,1173 @@
+/*
+ * stage_oracle.c -- TEST INFRASTRUCTURE ONLY: the parity checker and the CPU baseline.
+ *
+ * A plain-C restatement of the reference's index-organized read path (and of the small
+ * part of its write path needed to build the same leaf layouts and version chains).
+ * Every function cites the reference file:line it follows (paths relative to the
+ * reference checkout sheepTnT/Stage-IndexOrganized @ 2024-12-18).  Nothing here is
+ * compiled into, linked with or called by the product library; the product path
+ * (stage-indexorganized_amd/) is an independent implementation that is checked
+ * against this one.
+ *
+ * Single writer: the reference's CAS/retry/freeze loops collapse to their
+ * single-threaded outcome (every CAS succeeds, no node is frozen by another thread).
+ */
+#define _GNU_SOURCE
+#include "stage_oracle.h"
+
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#define MAX_CID 0xFFFFFFFFu
+#define INVALID_CID 0u
+
+/* ---------------------------------------------------------------- key order */
+/* my_memcmp, b_tree.h:99-106: plain char is signed on the reference's x86 target */
+static int my_memcmp(const uint8_t *k1, const uint8_t *k2, uint32_t size) {
+    for (uint32_t i = 0; i < size; i++) {
+        signed char a = (signed char)k1[i], b = (signed char)k2[i];
+        if (a != b) return (int)a - (int)b;
+    }
+    return 0;
+}
+
+/* BaseNode::KeyCompare, b_tree.h:116-134 (memcmp -- unsigned -- only from 16 bytes up) */
+int orc_key_compare(const uint8_t *k1, uint32_t s1, const uint8_t *k2, uint32_t s2) {
+    if (!k1) return -1;
+    if (!k2) return 1;
+    uint32_t m = s1 < s2 ? s1 : s2;
+    int cmp = (m < 16) ? my_memcmp(k1, k2, m) : memcmp(k1, k2, m);
+    if (cmp == 0) return (int)(s1 - s2);
+    return cmp;
+}
+
+/* ---------------------------------------------------------------- metadata */
+/* RecordMetadata masks, record_meta.h:66-70 */
+#define M_CONTROL (1ull << 63)
+#define M_VISIBLE (1ull << 62)
+#define M_KEYLEN (0x2FFFull << 48)
+#define M_OFFSET (0xFFFFull << 32)
+#define M_TXN 0xFFFFFFFFull
+
+static inline uint16_t m_keylen(uint64_t m) { return (uint16_t)((m & M_KEYLEN) >> 48); }
+static inline uint16_t pad_key(uint32_t k) { return (uint16_t)((k + 7) / 8 * 8); } /* :89-91 */
+static inline uint16_t m_padded(uint64_t m) { return pad_key(m_keylen(m)); }
+static inline uint16_t m_offset(uint64_t m) { return (uint16_t)((m & M_OFFSET) >> 32); }
+static inline int m_visible(uint64_t m) { return (m & M_VISIBLE) != 0; }
+static inline int m_inserting(uint64_t m) { return m_visible(m) && (m & M_CONTROL); } /* :178-181 */
+static inline uint32_t m_cstamp(uint64_t m) { return (uint32_t)(m & M_TXN); }
+/* FinalizeForInsert(offset,key_len,commit_id), record_meta.h:128-137 */
+static inline uint64_t m_finalize_insert(uint64_t off, uint64_t klen, uint64_t cid) {
+    uint64_t m = (klen << 48) | (1ull << 62) | (off << 32) | cid;
+    return m & ~M_CONTROL;
+}
+
+/* next_ptr handles: the reference stores raw pointers (copy-buffer location while an
+ * update is in flight, TupleHeader* after commit).  Tagged here so a reader can tell
+ * them apart (the reference cannot; see DESIGN.md "chain walk on a copy pointer"). */
+#define NEXT_COPY 1ull
+#define NEXT_TH 2ull
+#define NEXT_KIND(x) ((x) & 3ull)
+#define NEXT_PTR(x) ((void *)(uintptr_t)((x) & ~3ull))
+
+typedef struct orc_loc { uint8_t *leaf; uint32_t slot; } orc_loc; /* RecordLocation */
+
+typedef struct orc_copy { /* EphemeralPool::OverwriteVersionHeader, ephemeral_pool.h:26-150 */
+    uint32_t cstamp, pstamp, rstamp, sstamp;
+    uint64_t next; /* old TupleHeader chain at update time */
+    uint64_t pre;
+    uint16_t key_len;
+    uint32_t payload_size;
+    int live, waiting;
+    uint8_t *image; /* [key(key_len)][payload] (b_tree.cpp:1143-1144) */
+    struct orc_copy *reg_next;
+} orc_copy;
+
+typedef struct orc_th { /* TupleHeader, version_store.h:28-155 */
+    uint32_t begin_id, comm_id;
+    uint64_t next;
+    uint8_t *slot; /* [key(key_len)][payload] (transaction_manager.cpp:639-640) */
+    uint16_t key_len;
+    struct orc_th *reg_next;
+} orc_th;
+
+/* ---------------------------------------------------------------- leaf image */
+/* sizeof(LeafNode) == 40: vptr(8) is_leaf(1,+7) NodeHeader{size u32, sorted_count u32,
+ * next_record_slot u32 (+4), StatusWord u64} (b_tree.h:109-113, version_store.h:158-231) */
+#define LEAF_HDR 40u
+#define META_SZ 24u
+#define OFF_ISLEAF 8
+#define OFF_SIZE 16
+#define OFF_SORTED 20
+#define OFF_STATUS 32
+
+typedef struct { uint64_t meta, next; orc_loc *loc; } orc_rmeta; /* 24 B */
+
+static inline uint32_t *l_size(uint8_t *n) { return (uint32_t *)(n + OFF_SIZE); }
+static inline uint32_t *l_sorted(uint8_t *n) { return (uint32_t *)(n + OFF_SORTED); }
+static inline uint64_t *l_status(uint8_t *n) { return (uint64_t *)(n + OFF_STATUS); }
+static inline orc_rmeta *l_meta(uint8_t *n, uint32_t i) { return (orc_rmeta *)(n + LEAF_HDR + META_SZ * i); }
+/* StatusWord, version_store.h:167-214 */
+static inline uint32_t st_count(uint64_t s) { return (uint32_t)((s >> 44) & 0xFFFF); }
+static inline uint32_t st_block(uint64_t s) { return (uint32_t)((s >> 22) & 0x3FFFFF); }
+static inline uint32_t st_deleted(uint64_t s) { return (uint32_t)(s & 0x3FFFFF); }
+static inline int st_frozen(uint64_t s) { return (s >> 60) & 1; }
+static inline uint64_t st_set_count(uint64_t s, uint32_t c) { return (s & ~(0xFFFFull << 44)) | ((uint64_t)c << 44); }
+static inline uint64_t st_set_block(uint64_t s, uint32_t b) { return (s & ~(0x3FFFFFull << 22)) | ((uint64_t)b << 22); }
+static inline uint64_t st_set_deleted(uint64_t s, uint32_t d) { return (s & ~0x3FFFFFull) | d; }
+/* LeafNode::GetUsedSpace, b_tree.h:577-582 */
+static inline uint32_t used_space(uint64_t s) { return LEAF_HDR + st_block(s) + st_count(s) * META_SZ; }
+/* BaseNode::GetKey, b_tree.h:188-193 */
+static inline const uint8_t *l_key(uint8_t *n, uint64_t m) { return m_visible(m) ? n + m_offset(m) : NULL; }
+
+/* ---------------------------------------------------------------- inner node */
+typedef struct orc_inner { /* InternalNode (b_tree.h:213-398): immutable once built */
+    uint8_t hdr[16];       /* hdr[OFF_ISLEAF] == 0 */
+    uint32_t size;         /* header.size == the node's allocation size */
+    uint32_t count;        /* header.sorted_count */
+    int frozen;
+    uint16_t *klen;
+    uint8_t **key;         /* NULL for the dummy slot-0 key */
+    void **child;
+    uint8_t *keybuf;
+} orc_inner;
+
+static inline int is_leaf(void *p) { return ((uint8_t *)p)[OFF_ISLEAF] != 0; }
+
+struct orc_tree {
+    uint32_t leaf_node_size, split_threshold, payload_size, merge_threshold;
+    void *root;
+    orc_copy *copies;
+    orc_th *ths;
+    orc_loc **locs;
+    uint64_t nlocs, caplocs;
+    void **garbage; /* nodes replaced during the current Insert (released after install) */
+    uint64_t ngarbage, capgarbage;
+    uint64_t retired;
+};
+
+typedef struct { orc_inner *node; uint32_t meta_index; } frame_t;
+typedef struct { frame_t f[32]; uint32_t n; void *root; } stack_t_; /* Stack, b_tree.h:743-784 */
+
+static void push(stack_t_ *s, orc_inner *n, uint32_t i) { s->f[s->n].node = n; s->f[s->n].meta_index = i; s->n++; }
+static frame_t *pop(stack_t_ *s) { return s->n == 0 ? NULL : &s->f[--s->n]; }
+static frame_t *top(stack_t_ *s) { return s->n == 0 ? NULL : &s->f[s->n - 1]; }
+
+static void *xmalloc(size_t n) {
+    void *p = malloc(n);
+    if (!p) abort();
+    return p;
+}
+
+static void garbage_add(orc_tree *t, void *p) {
+    if (t->ngarbage == t->capgarbage) {
+        t->capgarbage = t->capgarbage ? 2 * t->capgarbage : 64;
+        t->garbage = realloc(t->garbage, t->capgarbage * sizeof(void *));
+    }
+    t->garbage[t->ngarbage++] = p;
+}
+
+static void inner_free(orc_inner *n) {
+    free(n->klen);
+    free(n->key);
+    free(n->child);
+    free(n->keybuf);
+    free(n);
+}
+
+static void garbage_release(orc_tree *t) {
+    for (uint64_t i = 0; i < t->ngarbage; i++) {
+        void *p = t->garbage[i];
+        if (is_leaf(p)) free(p);
+        else inner_free((orc_inner *)p);
+    }
+    t->ngarbage = 0;
+}
+
+static orc_inner *inner_alloc(uint32_t cap, uint32_t keybytes) {
+    orc_inner *n = xmalloc(sizeof(orc_inner));
+    memset(n, 0, sizeof(*n));
+    n->klen = xmalloc(sizeof(uint16_t) * cap);
+    n->key = xmalloc(sizeof(uint8_t *) * cap);
+    n->child = xmalloc(sizeof(void *) * cap);
+    n->keybuf = xmalloc(keybytes ? keybytes : 1);
+    return n;
+}
+
+typedef struct { uint32_t used; } kb_t;
+static void inner_set(orc_inner *n, kb_t *kb, uint32_t idx, const uint8_t *key, uint16_t klen, void *child) {
+    n->klen[idx] = klen;
+    if (klen && key) {
+        memcpy(n->keybuf + kb->used, key, klen);
+        n->key[idx] = n->keybuf + kb->used;
+        kb->used += klen;
+    } else {
+        n->key[idx] = NULL; /* GetRawRecord: zero-length key -> nullptr (b_tree.h:378-382) */
+    }
+    n->child[idx] = child;
+}
+
+static uint32_t inner_keybytes(orc_inner *src, uint32_t b, uint32_t nr, uint32_t extra) {
+    uint32_t s = extra;
+    if (src)
+        for (uint32_t i = b; i < b + nr; i++) s += src->klen[i];
+    return s;
+}
+
+/* InternalNode(node_size, key, key_size, left, right), b_tree.cpp:363-389; alloc b_tree.h:249-265 */
+static orc_inner *inner_new_root(const uint8_t *key, uint16_t ks, void *left, void *right) {
+    orc_inner *n = inner_alloc(2, ks);
+    kb_t kb = {0};
+    n->size = 48 + pad_key(ks) + 8 + 8 + 2 * META_SZ;
+    inner_set(n, &kb, 0, NULL, 0, left);
+    inner_set(n, &kb, 1, key, ks, right);
+    n->count = 2;
+    return n;
+}
+
+/* InternalNode(node_size, src, begin, nr, key, key_size, left, right, left_most),
+ * b_tree.cpp:391-497 */
+static void inner_build(orc_inner *n, orc_inner *src, uint32_t begin, uint32_t nr, const uint8_t *key,
+                        uint16_t ks, void *left, void *right, void *left_most) {
+    kb_t kb = {0};
+    int need_insert_new = key != NULL;
+    uint32_t idx = 0;
+    if (left_most) {
+        inner_set(n, &kb, 0, NULL, 0, left_most);
+        idx++;
+    }
+    for (uint32_t i = begin; i < begin + nr; i++) {
+        const uint8_t *mk = src->key[i];
+        uint16_t mks = src->klen[i];
+        if (!need_insert_new) {
+            inner_set(n, &kb, idx, mk, mks, src->child[i]);
+        } else {
+            int cmp = orc_key_compare(mk, mks, key, ks);
+            if (cmp > 0) {
+                n->child[idx - 1] = left; /* previous key's payload := left child */
+                inner_set(n, &kb, idx, key, ks, right);
+                idx++;
+                inner_set(n, &kb, idx, mk, mks, src->child[i]);
+                need_insert_new = 0;
+            } else {
+                inner_set(n, &kb, idx, mk, mks, src->child[i]);
+            }
+        }
+        idx++;
+    }
+    if (need_insert_new) { /* new key is the right-most */
+        inner_set(n, &kb, idx, key, ks, right);
+        n->child[idx - 1] = left;
+        idx++;
+    }
+    n->count = idx;
+}
+
+/* InternalNode::New(src, key, ...) b_tree.h:230-246 */
+static orc_inner *inner_new_insert(orc_inner *src, const uint8_t *key, uint16_t ks, void *left, void *right) {
+    orc_inner *n = inner_alloc(src->count + 1, inner_keybytes(src, 0, src->count, ks));
+    n->size = src->size + pad_key(ks) + 8 + META_SZ;
+    inner_build(n, src, 0, src->count, key, ks, left, right, NULL);
+    return n;
+}
+
+/* InternalNode::New(src, begin, nr, key, ...) b_tree.h:266-303 */
+static orc_inner *inner_new_range(orc_inner *src, uint32_t begin, uint32_t nr, const uint8_t *key, uint16_t ks,
+                                  void *left, void *right, void *left_most) {
+    uint32_t alloc = 48;
+    if (begin > 0) alloc += pad_key(src->klen[0]) + 8 + META_SZ;
+    for (uint32_t i = begin; i < begin + nr; i++) alloc += pad_key(src->klen[i]) + 8 + META_SZ;
+    if (key) alloc += pad_key(ks) + 8 + META_SZ;
+    orc_inner *n = inner_alloc(nr + 2, inner_keybytes(src, begin, nr, key ? ks : 0));
+    n->size = alloc;
+    inner_build(n, src, begin, nr, key, ks, left, right, left_most);
+    return n;
+}
+
+/* InternalNode::GetChildIndex, b_tree.cpp:664-702 (reproduced literally) */
+static uint32_t get_child_index(orc_inner *n, const uint8_t *key, uint16_t ks, int get_le) {
+    int32_t left = 0, right = (int32_t)n->count - 1, mid = 0;
+    for (;;) {
+        mid = (left + right) / 2;
+        int cmp = orc_key_compare(key, ks, n->key[mid], n->klen[mid]);
+        if (cmp == 0) return get_le ? (uint32_t)(mid - 1) : (uint32_t)mid;
+        if (left > right) {
+            if (cmp <= 0 && get_le) return (uint32_t)(mid - 1);
+            return (uint32_t)mid;
+        }
+        if (cmp > 0) left = mid + 1;
+        else right = mid - 1;
+    }
+}
+
+/* BTree::TraverseToLeaf, b_tree.cpp:1804-1846 */
+static uint8_t *traverse_to_leaf(orc_tree *t, stack_t_ *st, const uint8_t *key, uint16_t ks, int le_child) {
+    void *node = t->root;
+    if (st) st->root = node;
+    while (!is_leaf(node)) {
+        orc_inner *p = (orc_inner *)node;
+        uint32_t idx = get_child_index(p, key, ks, le_child);
+        node = p->child[idx];
+        if (st) push(st, p, idx);
+    }
+    return (uint8_t *)node;
+}
+
+/* InternalNode::PrepareForSplit, b_tree.cpp:500-598 */
+static orc_inner *inner_prepare_for_split(orc_tree *t, orc_inner *n, stack_t_ *st, const uint8_t *key,
+                                          uint16_t ks, void *left, void *right) {
+    uint32_t data_size = n->size + ks + 8 + META_SZ;
+    uint32_t new_node_size = 48 + data_size;
+    if (new_node_size < t->split_threshold) return inner_new_insert(n, key, ks, left, right);
+
+    uint32_t n_left = n->count >> 1;
+    const uint8_t *sep_key = n->key[n_left];
+    uint16_t sep_ks = n->klen[n_left];
+    void *sep_child = n->child[n_left];
+    int cmp = orc_key_compare(key, ks, sep_key, sep_ks);
+    if (cmp == 0) cmp = (int)ks - (int)sep_ks;
+    orc_inner *l, *r;
+    if (cmp < 0) {
+        l = inner_new_range(n, 0, n_left, key, ks, left, right, NULL);
+        r = inner_new_range(n, n_left + 1, n->count - n_left - 1, NULL, 0, NULL, NULL, sep_child);
+    } else {
+        l = inner_new_range(n, 0, n_left, NULL, 0, NULL, NULL, NULL);
+        r = inner_new_range(n, n_left + 1, n->count - n_left - 1, key, ks, left, right, sep_child);
+    }
+    garbage_add(t, n); /* this node is replaced by l and r */
+    pop(st);
+    frame_t *pf = top(st);
+    if (!pf) return inner_new_root(sep_key, sep_ks, l, r);
+    pf->node->frozen = 1;
+    return inner_prepare_for_split(t, pf->node, st, sep_key, sep_ks, l, r);
+}
+
+static uint8_t *leaf_new(orc_tree *t) { /* LeafNode::New, b_tree.cpp:791-797 */
+    uint8_t *n = aligned_alloc(64, t->leaf_node_size);
+    if (!n) abort();
+    memset(n, 0, t->leaf_node_size);
+    n[OFF_ISLEAF] = 1;
+    *l_size(n) = t->leaf_node_size;
+    return n;
+}
+
+/* BaseNode::SearchRecordMeta, b_tree.cpp:18-122 (called with check_concurrency == true by
+ * LeafNode::Read because of the argument shift at b_tree.cpp:1044-1045). */
+static int64_t search_record_meta(uint8_t *n, const uint8_t *key, uint16_t ks, int check_concurrency) {
+    uint32_t sorted = *l_sorted(n);
+    for (uint32_t i = 0; i < sorted; i++) {
+        uint64_t m = l_meta(n, i)->meta;
+        if (m == 0) continue;
+        const uint8_t *ck = l_key(n, m);
+        int cmp = orc_key_compare(key, ks, ck, m_keylen(m));
+        if (cmp == 0 && m_visible(m)) return i;
+    }
+    uint32_t cnt = st_count(*l_status(n));
+    for (uint32_t i = sorted; i < cnt; i++) {
+        uint64_t m = l_meta(n, i)->meta;
+        if (m_visible(m)) {
+            uint16_t cs = m_keylen(m);
+            if (cs == ks && orc_key_compare(key, ks, l_key(n, m), cs) == 0) return i;
+        } else if (!check_concurrency) {
+            return i;
+        }
+    }
+    return -1;
+}
+
+/* LeafNode::Insert, b_tree.cpp:809-947 (single writer) */
+static int leaf_insert(orc_tree *t, uint8_t *n, const uint8_t *key, uint16_t ks, const uint8_t *payload,
+                       uint32_t commit_id, orc_loc *loc, orc_rmeta **out) {
+    uint64_t status = *l_status(n);
+    if (st_frozen(status)) return ORC_RET_NODE_FROZEN;
+    /* CheckUnique, b_tree.cpp:1395-1417 */
+    int64_t hit = search_record_meta(n, key, ks, 1);
+    if (hit >= 0) {
+        uint64_t m = l_meta(n, (uint32_t)hit)->meta;
+        if (m_inserting(m)) return ORC_RET_INVALID; /* ReCheck vs an in-flight update: unsupported */
+        if (orc_key_compare(key, ks, l_key(n, m), m_keylen(m)) == 0) return ORC_RET_KEY_EXISTS;
+    }
+    uint32_t new_size = used_space(status) + META_SZ + pad_key(ks) + t->payload_size;
+    if (new_size >= t->leaf_node_size) return ORC_RET_NOT_ENOUGH_SPACE; /* split_threshold == leaf_node_size (:1869-1871) */
+    uint32_t total = pad_key(ks) + t->payload_size;
+    uint64_t desired = status + ((1ull << 44) + ((uint64_t)total << 22)); /* PrepareForInsert */
+    uint32_t slot = st_count(status);
+    orc_rmeta *mp = l_meta(n, slot);
+    if (mp->meta != 0) return ORC_RET_RETRY_FAILURE;
+    uint64_t offset = *l_size(n) - st_block(desired);
+    /* PrepareForInsert(offset,key_len,commit_id), record_meta.h:114-120 */
+    mp->meta = ((uint64_t)ks << 48) | (offset << 32) | commit_id | M_CONTROL | M_VISIBLE;
+    *l_status(n) = desired;
+    loc->leaf = n;
+    loc->slot = slot;
+    mp->loc = loc;
+    memcpy(n + offset, key, ks);
+    memcpy(n + offset + pad_key(ks), payload, t->payload_size);
+    *out = mp;
+    return ORC_RET_OK;
+}
+
+typedef struct { const uint8_t *k; uint16_t ks; orc_rmeta *m; } sortrec_t;
+static int sortrec_cmp(const void *a, const void *b) {
+    const sortrec_t *x = a, *y = b;
+    int c = orc_key_compare(x->k, x->ks, y->k, y->ks);
+    return (c > 0) - (c < 0);
+}
+
+/* LeafNode::CopyFrom, b_tree.cpp:1486-1545 */
+static void leaf_copy_from(orc_tree *t, uint8_t *dst, uint8_t *src, sortrec_t *v, uint32_t nv) {
+    uint32_t offset = *l_size(dst);
+    uint32_t nrec = 0;
+    for (uint32_t i = 0; i < nv; i++) {
+        orc_rmeta mm = *v[i].m;
+        if (mm.meta == 0) continue;
+        if (m_padded(mm.meta) == 0) continue; /* GetRawRecord false */
+        uint32_t total = m_padded(mm.meta) + t->payload_size;
+        offset -= total;
+        memcpy(dst + offset, src + m_offset(mm.meta), total);
+        orc_rmeta *dm = l_meta(dst, nrec);
+        orc_loc *loc = mm.loc;
+        if (loc) {
+            loc->leaf = dst;
+            loc->slot = nrec;
+        }
+        dm->loc = loc;
+        dm->next = mm.next;
+        dm->meta = m_finalize_insert(offset, m_keylen(mm.meta), m_cstamp(mm.meta));
+        nrec++;
+    }
+    uint64_t s = *l_status(dst);
+    s = st_set_block(s, *l_size(dst) - offset);
+    s = st_set_count(s, nrec);
+    *l_status(dst) = s;
+    *l_sorted(dst) = nrec;
+}
+
+/* LeafNode::PrepareForSplit, b_tree.cpp:1558-1690 */
+static int leaf_prepare_for_split(orc_tree *t, uint8_t *n, stack_t_ *st, uint8_t **pl, uint8_t **pr,
+                                  orc_inner **new_parent) {
+    uint32_t cnt = st_count(*l_status(n));
+    if (cnt < 3) return 0;
+    uint8_t *l = leaf_new(t), *r = leaf_new(t);
+    sortrec_t *v = xmalloc(sizeof(sortrec_t) * (cnt + 1));
+    uint32_t nv = 0, total = 0;
+    for (uint32_t i = 0; i < cnt; i++) {
+        orc_rmeta *mp = l_meta(n, i);
+        if (mp->meta == 0) continue;
+        if (m_visible(mp->meta) && m_keylen(mp->meta) > 0) {
+            v[nv].k = n + m_offset(mp->meta);
+            v[nv].ks = m_keylen(mp->meta);
+            v[nv].m = mp;
+            nv++;
+            total += m_padded(mp->meta) + t->payload_size;
+        }
+    }
+    qsort(v, nv, sizeof(sortrec_t), sortrec_cmp); /* Sorter::Sort (unique keys -> same order as std::sort) */
+    if (total == 0) {
+        free(v);
+        free(l);
+        free(r);
+        return 0;
+    }
+    int32_t left_size = (int32_t)(total / 2);
+    uint32_t nleft = 0;
+    for (uint32_t i = 0; i < nv; i++) {
+        ++nleft;
+        left_size -= (int32_t)(m_padded(v[i].m->meta) + t->payload_size);
+        if (left_size <= 0) break;
+    }
+    leaf_copy_from(t, l, n, v, nleft);
+    leaf_copy_from(t, r, n, v + nleft, nv - nleft);
+    /* separator = last key of the left node (in the frozen old node) */
+    const uint8_t *sep = v[nleft - 1].k;
+    uint16_t sep_ks = v[nleft - 1].ks;
+    frame_t *pf = top(st);
+    if (!pf) {
+        *new_parent = inner_new_root(sep, sep_ks, l, r);
+    } else {
+        pf->node->frozen = 1;
+        *new_parent = inner_prepare_for_split(t, pf->node, st, sep, sep_ks, l, r);
+    }
+    free(v);
+    *pl = l;
+    *pr = r;
+    return 1;
+}
+
+static orc_loc *new_loc(orc_tree *t) { /* BTree::RecordIndirectLocation */
+    orc_loc *l = xmalloc(sizeof(orc_loc));
+    l->leaf = NULL;
+    l->slot = 0;
+    if (t->nlocs == t->caplocs) {
+        t->caplocs = t->caplocs ? 2 * t->caplocs : 1024;
+        t->locs = realloc(t->locs, t->caplocs * sizeof(orc_loc *));
+    }
+    t->locs[t->nlocs++] = l;
+    return l;
+}
+
+/* BTree::Insert, b_tree.cpp:1849-2020 */
+static int btree_insert(orc_tree *t, const uint8_t *key, uint16_t ks, const uint8_t *payload, uint32_t commit_id,
+                        orc_rmeta **out) {
+    stack_t_ st;
+    for (int guard = 0; guard < 64; guard++) {
+        st.n = 0;
+        uint8_t *leaf = traverse_to_leaf(t, &st, key, ks, 1);
+        orc_loc *loc = new_loc(t);
+        int rc = leaf_insert(t, leaf, key, ks, payload, commit_id, loc, out);
+        if (rc == ORC_RET_OK) return rc;
+        if (rc == ORC_RET_KEY_EXISTS || rc == ORC_RET_RETRY_FAILURE || rc == ORC_RET_INVALID) return rc;
+        /* NotEnoughSpace: freeze and split */
+        *l_status(leaf) |= (1ull << 60);
+        uint8_t *l = NULL, *r = NULL;
+        orc_inner *np = NULL;
+        if (!leaf_prepare_for_split(t, leaf, &st, &l, &r, &np)) return ORC_RET_RETRY_FAILURE;
+        frame_t *f = pop(&st);
+        orc_inner *old_parent = f ? f->node : NULL;
+        f = pop(&st);
+        orc_inner *grand = f ? f->node : NULL;
+        if (grand) {
+            grand->child[f->meta_index] = np; /* InternalNode::Update, b_tree.cpp:635-662 */
+        } else {
+            t->root = np; /* ChangeRoot */
+        }
+        garbage_add(t, leaf);
+        if (old_parent) garbage_add(t, old_parent);
+        garbage_release(t);
+    }
+    return ORC_RET_RETRY_FAILURE;
+}
+
+/* ---------------------------------------------------------------- public: build */
+orc_tree *orc_tree_new(uint32_t leaf_node_size, uint32_t split_threshold, uint32_t payload_size) {
+    orc_tree *t = xmalloc(sizeof(orc_tree));
+    memset(t, 0, sizeof(*t));
+    t->leaf_node_size = leaf_node_size;
+    t->split_threshold = split_threshold;
+    t->payload_size = payload_size;
+    t->merge_threshold = 32 * 1024;
+    t->root = leaf_new(t);
+    return t;
+}
+
+void orc_tree_set_merge_threshold(orc_tree *t, uint32_t merge_threshold) { t->merge_threshold = merge_threshold; }
+
+static void free_subtree(void *n) {
+    if (is_leaf(n)) {
+        free(n);
+        return;
+    }
+    orc_inner *p = n;
+    for (uint32_t i = 0; i < p->count; i++) free_subtree(p->child[i]);
+    inner_free(p);
+}
+
+void orc_tree_free(orc_tree *t) {
+    if (!t) return;
+    free_subtree(t->root);
+    for (orc_copy *c = t->copies; c;) {
+        orc_copy *nx = c->reg_next;
+        free(c->image);
+        free(c);
+        c = nx;
+    }
+    for (orc_th *h = t->ths; h;) {
+        orc_th *nx = h->reg_next;
+        free(h->slot);
+        free(h);
+        h = nx;
+    }
+    for (uint64_t i = 0; i < t->nlocs; i++) free(t->locs[i]);
+    free(t->locs);
+    free(t->garbage);
+    free(t);
+}
+
+int orc_insert(orc_tree *t, const uint8_t *key, uint32_t key_size, const uint8_t *payload, uint32_t commit_id) {
+    orc_rmeta *mp = NULL;
+    int rc = btree_insert(t, key, (uint16_t)key_size, payload, commit_id, &mp);
+    if (rc == ORC_RET_OK) {
+        /* BTree::FinalizeInsert, b_tree.cpp:2238-2251 */
+        mp->meta = m_finalize_insert(m_offset(mp->meta), m_keylen(mp->meta), commit_id);
+    }
+    return rc;
+}
+
+static uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+uint64_t orc_payload_word(uint64_t rowid, uint32_t j) { return splitmix64((rowid << 8) ^ j); }
+
+void orc_fill_payload(uint64_t rowid, int mode, uint8_t *dst, uint32_t payload_size) {
+    if (mode == 0) { /* memset(tuple.cols[i], rowid, ...) ycsb_loader.cpp:149-150 */
+        memset(dst, (int)(rowid & 0xFF), payload_size);
+        return;
+    }
+    for (uint32_t j = 0; j * 8 < payload_size; j++) {
+        uint64_t w = orc_payload_word(rowid, j);
+        uint32_t nb = payload_size - j * 8 < 8 ? payload_size - j * 8 : 8;
+        memcpy(dst + j * 8, &w, nb);
+    }
+}
+
+uint64_t orc_load_keys(orc_tree *t, const uint64_t *keys, uint64_t n, uint32_t key_size, int payload_mode) {
+    uint8_t *payload = xmalloc(t->payload_size + 8);
+    uint64_t ok = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        uint64_t k = keys[i];
+        orc_fill_payload(k, payload_mode, payload, t->payload_size);
+        if (orc_insert(t, (const uint8_t *)&k, key_size, payload, INVALID_CID) == ORC_RET_OK) ok++;
+    }
+    free(payload);
+    return ok;
+}
+
+uint64_t orc_load_ycsb(orc_tree *t, uint64_t begin, uint64_t end, uint32_t key_size, int payload_mode) {
+    uint8_t *payload = xmalloc(t->payload_size + 8);
+    uint64_t ok = 0;
+    for (uint64_t rowid = begin; rowid < end; rowid++) {
+        uint64_t k = rowid; /* uint32_t k_ = rowid for the 4-byte driver (ycsb_loader.cpp:152) */
+        orc_fill_payload(rowid, payload_mode, payload, t->payload_size);
+        if (orc_insert(t, (const uint8_t *)&k, key_size, payload, INVALID_CID) == ORC_RET_OK) ok++;
+    }
+    free(payload);
+    return ok;
+}
+
+/* ---------------------------------------------------------------- read path */
+static orc_copy *copy_of(uint64_t next) {
+    if (next == 0 || NEXT_KIND(next) != NEXT_COPY) return NULL;
+    orc_copy *c = NEXT_PTR(next);
+    return c->live ? c : NULL; /* EphemeralPool::GetOversionHeader (ephemeral_pool.cpp:110-123) */
+}
+
+static void emit_canonical(orc_tree *t, uint8_t *rec, const uint8_t *key, uint16_t ks, const uint8_t *payload) {
+    if (!rec) return;
+    memset(rec, 0, 8);
+    memcpy(rec, key, ks > 8 ? 8 : ks);
+    memcpy(rec + 8, payload, t->payload_size);
+}
+
+/* BTree::Read (b_tree.cpp:2066-2129) followed by the point-lookup branch of
+ * IndexScanExecutor::Execute (executor.h:374-454), canonical output. */
+static int read_one(orc_tree *t, const uint8_t *key, uint16_t ks, uint32_t read_id, orc_read_out *o, uint8_t *rec) {
+    memset(o, 0, sizeof(*o));
+    o->copy_sstamp = MAX_CID;
+    uint32_t rs = 8 + t->payload_size;
+    if (rec) memset(rec, 0, rs);
+    uint8_t *leaf = traverse_to_leaf(t, NULL, key, ks, 1);
+    int64_t slot = search_record_meta(leaf, key, ks, 1);
+    if (slot < 0) {
+        o->status = ORC_ST_NOT_FOUND;
+        return 0;
+    }
+    orc_rmeta *mp = l_meta(leaf, (uint32_t)slot);
+    uint64_t m = mp->meta;
+    o->rec_cstamp = m_cstamp(m);
+    orc_copy *pc = copy_of(mp->next); /* PerformRead's GetOversionHeader(meta.next_ptr) */
+    if (pc) {
+        o->copy_present = 1;
+        o->copy_sstamp = pc->sstamp;
+    }
+    const uint8_t *rkey, *rpay;
+    uint64_t next_tuple;
+    int from_copy = 0;
+    if (m_inserting(m)) {
+        orc_copy *c = pc;
+        if (!c) { /* copy location 0 / header gone: Read returns nullptr */
+            o->status = ORC_ST_NOT_FOUND;
+            return 0;
+        }
+        rkey = c->image; /* Record::Neww: key(keylen) then payload */
+        rpay = c->image + c->key_len;
+        o->cstamp = c->rstamp;
+        next_tuple = c->next;
+        from_copy = 1;
+    } else {
+        rkey = leaf + m_offset(m);
+        rpay = leaf + m_offset(m) + m_padded(m);
+        o->cstamp = read_id;
+        next_tuple = mp->next;
+    }
+    if (read_id >= o->rec_cstamp) {
+        o->status = from_copy ? ORC_ST_COPY : ORC_ST_LATEST;
+        emit_canonical(t, rec, rkey, m_keylen(m), rpay);
+        return 0;
+    }
+    /* older snapshot: walk the TupleHeader chain (executor.h:407-449) */
+    if (next_tuple == 0 || NEXT_KIND(next_tuple) != NEXT_TH) {
+        o->status = ORC_ST_CHAIN_MISS;
+        return 0;
+    }
+    orc_th *th = NEXT_PTR(next_tuple);
+    for (;;) {
+        o->hops++;
+        if (th->begin_id == INVALID_CID || th->comm_id == INVALID_CID) {
+            o->status = ORC_ST_FAIL_INVALID_TS;
+            return 0;
+        }
+        if (read_id >= th->begin_id && read_id <= th->comm_id) {
+            o->status = ORC_ST_OLD;
+            o->cstamp = th->begin_id;
+            emit_canonical(t, rec, th->slot, th->key_len, th->slot + th->key_len);
+            return 0;
+        }
+        uint64_t nx = th->next;
+        if (nx == 0 || nx == ~0ull || NEXT_KIND(nx) != NEXT_TH) {
+            o->status = ORC_ST_CHAIN_MISS;
+            return 0;
+        }
+        th = NEXT_PTR(nx);
+    }
+}
+
+int orc_read(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t read_id, orc_read_out *out, uint8_t *rec) {
+    return read_one(t, key, (uint16_t)key_size, read_id, out, rec);
+}
+
+typedef struct {
+    orc_tree *t;
+    const uint64_t *keys;
+    uint32_t ks;
+    const uint32_t *rids;
+    uint64_t b, e;
+    orc_read_out *outs;
+    uint8_t *recs;
+    uint32_t scan_size;
+    uint32_t *counts;
+    uint64_t sum;
+} job_t;
+
+static void *read_worker(void *arg) {
+    job_t *j = arg;
+    uint32_t rs = 8 + j->t->payload_size;
+    for (uint64_t i = j->b; i < j->e; i++) {
+        uint64_t k = j->keys[i];
+        read_one(j->t, (const uint8_t *)&k, (uint16_t)j->ks, j->rids ? j->rids[i] : 0xFFFFFFFEu, &j->outs[i],
+                 j->recs ? j->recs + i * rs : NULL);
+    }
+    return NULL;
+}
+
+static void run_jobs(void *(*fn)(void *), job_t *proto, uint64_t n, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if ((uint64_t)nthreads > n) nthreads = n ? (int)n : 1;
+    pthread_t th[256];
+    job_t jobs[256];
+    if (nthreads > 256) nthreads = 256;
+    for (int i = 0; i < nthreads; i++) {
+        jobs[i] = *proto;
+        jobs[i].b = n * (uint64_t)i / nthreads;
+        jobs[i].e = n * (uint64_t)(i + 1) / nthreads;
+        jobs[i].sum = 0;
+        pthread_create(&th[i], NULL, fn, &jobs[i]);
+    }
+    proto->sum = 0;
+    for (int i = 0; i < nthreads; i++) {
+        pthread_join(th[i], NULL);
+        proto->sum += jobs[i].sum;
+    }
+}
+
+int orc_read_batch(orc_tree *t, const uint64_t *keys, uint32_t key_size, const uint32_t *read_ids, uint64_t n,
+                   orc_read_out *outs, uint8_t *recs, int nthreads) {
+    job_t j = {t, keys, key_size, read_ids, 0, n, outs, recs, 0, NULL, 0};
+    run_jobs(read_worker, &j, n, nthreads);
+    return 0;
+}
+
+/* CPU baseline worker: the reference's work per read -- traverse, leaf probe, heap Record
+ * (Record::New, b_tree.h:407-428) and the executor's `new T` + memcpy (executor.h:396-401),
+ * both freed afterwards -- without the txn bookkeeping. */
+static void *timed_worker(void *arg) {
+    job_t *j = arg;
+    orc_tree *t = j->t;
+    uint64_t sum = 0;
+    orc_read_out o;
+    for (uint64_t i = j->b; i < j->e; i++) {
+        uint64_t k = j->keys[i];
+        const uint8_t *key = (const uint8_t *)&k;
+        uint16_t ks = (uint16_t)j->ks;
+        uint32_t rid = j->rids ? j->rids[i] : 0xFFFFFFFEu;
+        uint8_t *leaf = traverse_to_leaf(t, NULL, key, ks, 1);
+        int64_t slot = search_record_meta(leaf, key, ks, 1);
+        if (slot < 0) continue;
+        orc_rmeta *mp = l_meta(leaf, (uint32_t)slot);
+        uint64_t m = mp->meta;
+        if (m_inserting(m)) { /* rare: fall back to the full restatement */
+            uint8_t *rec = xmalloc(8 + t->payload_size);
+            read_one(t, key, ks, rid, &o, rec);
+            sum += rec[8];
+            free(rec);
+            continue;
+        }
+        size_t rsz = 48 + 4 + m_padded(m) + t->payload_size;
+        uint8_t *r = xmalloc(rsz);
+        memcpy(r + 52, leaf + m_offset(m), m_padded(m));
+        memcpy(r + 52 + m_padded(m), leaf + m_offset(m) + m_padded(m), t->payload_size);
+        if (rid >= m_cstamp(m)) {
+            uint8_t *tup = xmalloc(4 + t->payload_size);
+            memcpy(tup, r + 52, 4 + t->payload_size);
+            sum += tup[4 + (i % t->payload_size)];
+            free(tup);
+        } else {
+            read_one(t, key, ks, rid, &o, NULL);
+            sum += o.status;
+        }
+        free(r);
+    }
+    j->sum = sum;
+    return NULL;
+}
+
+uint64_t orc_read_batch_timed(orc_tree *t, const uint64_t *keys, uint32_t key_size, const uint32_t *read_ids,
+                              uint64_t n, int nthreads, double *seconds) {
+    job_t j = {t, keys, key_size, read_ids, 0, n, NULL, NULL, 0, NULL, 0};
+    struct timespec a, b;
+    clock_gettime(CLOCK_MONOTONIC, &a);
+    run_jobs(timed_worker, &j, n, nthreads);
+    clock_gettime(CLOCK_MONOTONIC, &b);
+    if (seconds) *seconds = (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
+    return j.sum;
+}
+
+/* ---------------------------------------------------------------- scans */
+typedef struct { uint8_t *leaf; uint32_t slot; const uint8_t *k; uint16_t ks; } scanrec_t;
+static int scanrec_cmp(const void *a, const void *b) {
+    const scanrec_t *x = a, *y = b;
+    int c = orc_key_compare(x->k, x->ks, y->k, y->ks);
+    return (c > 0) - (c < 0);
+}
+
+/* LeafNode::RangeScanBySize, b_tree.cpp:1261-1315: slot order, stop once > to_scan
+ * collected, then sort by KeyCompare. */
+static uint32_t range_scan_by_size(uint8_t *n, const uint8_t *key, uint16_t ks, uint32_t to_scan, scanrec_t *out) {
+    if (to_scan == 0) return 0;
+    uint32_t cnt = st_count(*l_status(n)), m = 0;
+    for (uint32_t i = 0; i < cnt; i++) {
+        if (m > to_scan) break;
+        uint64_t mm = l_meta(n, i)->meta;
+        if (m_visible(mm)) {
+            int cmp = orc_key_compare(key, ks, l_key(n, mm), m_keylen(mm));
+            if (cmp <= 0) {
+                out[m].leaf = n;
+                out[m].slot = i;
+                out[m].k = n + m_offset(mm);
+                out[m].ks = m_keylen(mm);
+                m++;
+            }
+        }
+    }
+    qsort(out, m, sizeof(scanrec_t), scanrec_cmp);
+    return m;
+}
+
+static void emit_scan_rec(orc_tree *t, uint8_t *dst, scanrec_t *r) {
+    uint64_t mm = l_meta(r->leaf, r->slot)->meta;
+    memset(dst, 0, 8);
+    memcpy(dst, r->leaf + m_offset(mm), m_padded(mm) > 8 ? 8 : m_padded(mm));
+    memcpy(dst + 8, r->leaf + m_offset(mm) + m_padded(mm), t->payload_size);
+}
+
+/* TableScanExecutor::Execute (executor.h:620-639) driving Iterator::GetNext (b_tree.h:899-941) */
+static uint32_t scan_one(orc_tree *t, const uint8_t *key, uint16_t ks, uint32_t scan_size, uint8_t *recs,
+                         scanrec_t *buf, uint32_t bufcap) {
+    uint32_t rs = 8 + t->payload_size, produced = 0;
+    uint32_t remaining = scan_size;
+    uint8_t lastkey[64];
+    uint16_t lastks = 0;
+    uint8_t *leaf = traverse_to_leaf(t, NULL, key, ks, 1);
+    uint32_t m = range_scan_by_size(leaf, key, ks, scan_size < bufcap ? scan_size : bufcap - 1, buf);
+    uint32_t head = 0;
+    for (uint32_t scanned = 0; scanned < scan_size; scanned++) {
+        /* GetNext */
+        if (head >= m || remaining == 0) continue; /* nullptr -> fail_num++ */
+        remaining -= 1;
+        if (m - head > 1) {
+            if (recs) emit_scan_rec(t, recs + (uint64_t)produced * rs, &buf[head]);
+            produced++;
+            head++;
+            continue;
+        }
+        scanrec_t last = buf[head];
+        head++;
+        if (recs) emit_scan_rec(t, recs + (uint64_t)produced * rs, &last);
+        produced++;
+        lastks = last.ks > 64 ? 64 : last.ks;
+        memcpy(lastkey, last.k, lastks);
+        uint8_t *nl = traverse_to_leaf(t, NULL, lastkey, lastks, 0);
+        m = range_scan_by_size(nl, lastkey, lastks, remaining < bufcap ? remaining : bufcap - 1, buf);
+        head = 0;
+        if (m > 0 && orc_key_compare(buf[0].k, buf[0].ks, lastkey, lastks) == 0) m = 0; /* item_vec.clear() */
+    }
+    return produced;
+}
+
+uint32_t orc_scan(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t scan_size, uint8_t *recs) {
+    uint32_t cap = 4096;
+    scanrec_t *buf = xmalloc(sizeof(scanrec_t) * cap);
+    uint32_t r = scan_one(t, key, (uint16_t)key_size, scan_size, recs, buf, cap);
+    free(buf);
+    return r;
+}
+
+static void *scan_worker(void *arg) {
+    job_t *j = arg;
+    uint32_t cap = 4096;
+    scanrec_t *buf = xmalloc(sizeof(scanrec_t) * cap);
+    uint64_t rs = 8 + j->t->payload_size, sum = 0;
+    for (uint64_t i = j->b; i < j->e; i++) {
+        uint64_t k = j->keys[i];
+        uint32_t c = scan_one(j->t, (const uint8_t *)&k, (uint16_t)j->ks, j->scan_size,
+                              j->recs ? j->recs + i * rs * j->scan_size : NULL, buf, cap);
+        if (j->counts) j->counts[i] = c;
+        sum += c;
+    }
+    free(buf);
+    j->sum = sum;
+    return NULL;
+}
+
+uint64_t orc_scan_batch(orc_tree *t, const uint64_t *keys, uint32_t key_size, uint64_t n, uint32_t scan_size,
+                        uint32_t *counts, uint8_t *recs, int nthreads) {
+    job_t j = {t, keys, key_size, NULL, 0, n, NULL, recs, scan_size, counts, 0};
+    run_jobs(scan_worker, &j, n, nthreads);
+    return j.sum;
+}
+
+/* ---------------------------------------------------------------- traversal export */
+static int64_t leaf_index_rec(void *node, uint8_t *target, int64_t *counter) {
+    if (is_leaf(node)) {
+        int64_t me = (*counter)++;
+        return node == target ? me : -1;
+    }
+    orc_inner *p = node;
+    for (uint32_t i = 0; i < p->count; i++) {
+        int64_t r = leaf_index_rec(p->child[i], target, counter);
+        if (r >= 0) return r;
+    }
+    return -1;
+}
+
+int64_t orc_traverse_leaf_index(orc_tree *t, const uint8_t *key, uint32_t key_size, int le_child) {
+    uint8_t *leaf = traverse_to_leaf(t, NULL, key, (uint16_t)key_size, le_child);
+    int64_t c = 0;
+    return leaf_index_rec(t->root, leaf, &c);
+}
+
+typedef struct {
+    uint32_t cap;
+    uint64_t max, n;
+    uint32_t *rc, *sc;
+    uint64_t *meta, *keyw;
+} export_t;
+
+static void export_rec(void *node, export_t *e, uint64_t *stats, uint32_t depth) {
+    if (is_leaf(node)) {
+        uint8_t *n = node;
+        uint32_t cnt = st_count(*l_status(n)), sorted = *l_sorted(n);
+        if (stats) {
+            if (depth + 1 > stats[0]) stats[0] = depth + 1;
+            stats[2]++;
+            for (uint32_t i = 0; i < cnt; i++)
+                if (m_visible(l_meta(n, i)->meta)) {
+                    stats[3]++;
+                    if (i < sorted) stats[4]++;
+                    else stats[5]++;
+                }
+            if (cnt > stats[6]) stats[6] = cnt;
+        }
+        if (e) {
+            if (e->n < e->max) {
+                e->rc[e->n] = cnt;
+                e->sc[e->n] = sorted;
+                for (uint32_t i = 0; i < e->cap; i++) {
+                    uint64_t mm = i < cnt ? l_meta(n, i)->meta : 0;
+                    uint64_t kw = 0;
+                    if (mm) memcpy(&kw, n + m_offset(mm), m_keylen(mm) > 8 ? 8 : m_keylen(mm));
+                    e->meta[e->n * (uint64_t)e->cap + i] = mm;
+                    e->keyw[e->n * (uint64_t)e->cap + i] = kw;
+                }
+            }
+            e->n++;
+        }
+        return;
+    }
+    orc_inner *p = node;
+    if (stats) stats[1]++;
+    for (uint32_t i = 0; i < p->count; i++) export_rec(p->child[i], e, stats, depth + 1);
+}
+
+void orc_stats(orc_tree *t, uint64_t *stats) {
+    memset(stats, 0, 8 * sizeof(uint64_t));
+    export_rec(t->root, NULL, stats, 0);
+    stats[7] = t->retired;
+}
+
+int64_t orc_export_leaves(orc_tree *t, uint32_t cap, uint64_t max_leaves, uint32_t *rc, uint32_t *sc,
+                          uint64_t *meta, uint64_t *keyw) {
+    export_t e = {cap, max_leaves, 0, rc, sc, meta, keyw};
+    export_rec(t->root, &e, NULL, 0);
+    if (e.n > max_leaves) return -(int64_t)e.n;
+    return (int64_t)e.n;
+}
+
+/* ---------------------------------------------------------------- write path (scenarios) */
+static orc_rmeta *find_meta(orc_tree *t, const uint8_t *key, uint16_t ks, uint8_t **leafp) {
+    uint8_t *leaf = traverse_to_leaf(t, NULL, key, ks, 1);
+    int64_t slot = search_record_meta(leaf, key, ks, 1);
+    if (leafp) *leafp = leaf;
+    return slot < 0 ? NULL : l_meta(leaf, (uint32_t)slot);
+}
+
+static orc_copy *copy_alloc(orc_tree *t, const uint8_t *src_key, uint16_t klen, uint64_t next, uint32_t cstamp,
+                            uint32_t rstamp) {
+    /* EphemeralPool::Allocate, ephemeral_pool.cpp:17-44 */
+    orc_copy *c = xmalloc(sizeof(orc_copy));
+    memset(c, 0, sizeof(*c));
+    c->cstamp = cstamp;
+    c->pstamp = cstamp;
+    c->rstamp = rstamp;
+    c->sstamp = MAX_CID;
+    c->next = next;
+    c->key_len = klen;
+    c->payload_size = t->payload_size;
+    c->live = 1;
+    c->image = xmalloc(klen + t->payload_size);
+    memcpy(c->image, src_key, klen);                                   /* b_tree.cpp:1143 */
+    memcpy(c->image + klen, src_key + pad_key(klen), t->payload_size); /* b_tree.cpp:1144 */
+    c->reg_next = t->copies;
+    t->copies = c;
+    return c;
+}
+
+/* LeafNode::Update, b_tree.cpp:1061-1163 (is_for_update == false) */
+int orc_update(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t payload_off, const uint8_t *delta,
+               uint32_t delta_len, uint32_t writer_id) {
+    uint16_t ks = (uint16_t)key_size;
+    uint8_t *leaf;
+    orc_rmeta *mp = find_meta(t, key, ks, &leaf);
+    if (!mp) return ORC_RET_NOT_FOUND;
+    if (m_inserting(mp->meta)) return ORC_RET_DIRTY;
+    uint8_t *rk = leaf + m_offset(mp->meta);
+    uint8_t *col = rk + 8 + payload_off; /* Catalog: 8-byte key column then payload columns */
+    if (payload_off + delta_len > t->payload_size) return ORC_RET_INVALID;
+    if (memcmp(col, delta, delta_len) == 0) return ORC_RET_NOT_NEEDED_UPDATE; /* ComparePayload */
+    if (m_cstamp(mp->meta) > writer_id) return ORC_RET_NOT_NEEDED_UPDATE;
+    uint64_t old = mp->meta;
+    mp->meta = old | M_CONTROL | M_VISIBLE; /* PrepareForUpdate */
+    orc_copy *c = copy_alloc(t, rk, m_keylen(old), mp->next, writer_id, m_cstamp(old));
+    mp->next = (uint64_t)(uintptr_t)c | NEXT_COPY;
+    memcpy(col, delta, delta_len); /* CopyPayload */
+    return ORC_RET_OK;
+}
+
+/* CommitTransaction, UPDATE entry (transaction_manager.cpp:610-676) for a single writer
+ * whose t_sstamp is `sstamp` (FindMinSstamp starts it at t_cstamp, :113-121). */
+int orc_commit_update(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t commit_id, uint32_t sstamp) {
+    orc_rmeta *mp = find_meta(t, key, (uint16_t)key_size, NULL);
+    if (!mp || !m_inserting(mp->meta)) return ORC_RET_NOT_FOUND;
+    orc_copy *c = copy_of(mp->next);
+    if (!c) return ORC_RET_NOT_FOUND;
+    orc_th *th = xmalloc(sizeof(orc_th)); /* AcquireVersion + PerformUpdate (:435-491) */
+    memset(th, 0, sizeof(*th));
+    th->next = c->next;
+    th->begin_id = c->rstamp;
+    c->sstamp = sstamp;
+    c->waiting = 1;
+    th->comm_id = c->sstamp;
+    th->key_len = c->key_len;
+    th->slot = xmalloc(c->key_len + t->payload_size);
+    memcpy(th->slot, c->image, c->key_len + t->payload_size);
+    th->reg_next = t->ths;
+    t->ths = th;
+    t->retired++;
+    c->pre = (uint64_t)(uintptr_t)th;
+    uint64_t m = mp->meta;
+    m = (m & ~M_TXN) | commit_id; /* FinalizeForUpdate(t_cstamp), record_meta.h:146-151 */
+    m &= ~M_CONTROL;
+    mp->meta = m;
+    mp->next = (uint64_t)(uintptr_t)th | NEXT_TH;
+    return ORC_RET_OK;
+}
+
+/* BTree::FinalizeUpdate, b_tree.cpp:2252-2268: cstamp := commit_id, next_ptr untouched */
+int orc_finalize_update(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t commit_id) {
+    orc_rmeta *mp = find_meta(t, key, (uint16_t)key_size, NULL);
+    if (!mp) return ORC_RET_NOT_FOUND;
+    uint64_t m = mp->meta;
+    m = (m & ~M_TXN) | commit_id;
+    m &= ~M_CONTROL;
+    mp->meta = m;
+    return ORC_RET_OK;
+}
+
+/* LeafNode::Delete (b_tree.cpp:1171-1251, is_for_update == false) + BTree::FinalizeDelete
+ * (:2275-2310).  BaseNode::CheckMerge (:150-318) is not restated: a delete that would merge
+ * siblings returns ORC_RET_INVALID after deleting. */
+int orc_delete(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t commit_id) {
+    (void)commit_id;
+    uint16_t ks = (uint16_t)key_size;
+    uint8_t *leaf;
+    orc_rmeta *mp = find_meta(t, key, ks, &leaf);
+    if (!mp) return ORC_RET_NOT_FOUND;
+    if (m_inserting(mp->meta)) return ORC_RET_DIRTY;
+    uint8_t *rk = leaf + m_offset(mp->meta);
+    orc_copy *c = copy_alloc(t, rk, m_keylen(mp->meta), mp->next, commit_id, m_cstamp(mp->meta));
+    uint32_t padded = m_padded(mp->meta);
+    mp->next = (uint64_t)(uintptr_t)c | NEXT_COPY;
+    mp->meta = 0;
+    uint64_t s = *l_status(leaf);
+    *l_status(leaf) = st_set_deleted(s, st_deleted(s) + padded + t->payload_size);
+    /* CheckMerge gate (b_tree.cpp:155-173) */
+    s = *l_status(leaf);
+    uint32_t valid = used_space(s) - st_deleted(s);
+    if (leaf != t->root && valid <= t->merge_threshold)
+        return ORC_RET_INVALID;
+    return ORC_RET_OK;
+}
+
+/* ---------------------------------------------------------------- murmur */
+/* MurmurHash64A, misc/murmur/MurmurHash2.cpp:99-147 (little-endian, unaligned) */
+uint64_t orc_murmur64a(const void *key, int len, uint64_t seed) {
+    const uint64_t m = 0xc6a4a7935bd1e995ull;
+    const int r = 47;
+    uint64_t h = seed ^ ((uint64_t)(int64_t)len * m);
+    const uint8_t *p = key;
+    int nblocks = len / 8;
+    for (int i = 0; i < nblocks; i++) {
+        uint64_t k;
+        memcpy(&k, p + 8 * i, 8);
+        k *= m;
+        k ^= k >> r;
+        k *= m;
+        h ^= k;
+        h *= m;
+    }
+    const uint8_t *d2 = p + 8 * nblocks;
+    switch (len & 7) {
+    case 7: h ^= (uint64_t)d2[6] << 48; /* fallthrough */
+    case 6: h ^= (uint64_t)d2[5] << 40; /* fallthrough */
+    case 5: h ^= (uint64_t)d2[4] << 32; /* fallthrough */
+    case 4: h ^= (uint64_t)d2[3] << 24; /* fallthrough */
+    case 3: h ^= (uint64_t)d2[2] << 16; /* fallthrough */
+    case 2: h ^= (uint64_t)d2[1] << 8;  /* fallthrough */
+    case 1:
+        h ^= (uint64_t)d2[0];
+        h *= m;
+    }
+    h ^= h >> r;
+    h *= m;
+    h ^= h >> r;
+    return h;
+}
+
+void orc_murmur64a_batch(const uint64_t *keys, uint64_t n, int len, uint64_t seed, uint64_t *out) {
+    for (uint64_t i = 0; i < n; i++) out[i] = orc_murmur64a(&keys[i], len, seed);
+}

@@ -1,0 +1,125 @@
+/*
+ * stage_oracle.h -- TEST INFRASTRUCTURE ONLY (parity checker, never product code).
+ *
+ * Plain-C restatement of the reference's index-organized hot path
+ * (sheepTnT/Stage-IndexOrganized @ 2024-12-18):
+ *   - signed-byte key order            include/vstore/b_tree.h:99-134
+ *   - 64-bit RecordMetadata word       include/vstore/record_meta.h:30-204
+ *   - BzTree leaf image / insert/split src/vstore/b_tree.cpp:809-947, 1558-1690, 1849-2020
+ *   - inner nodes + GetChildIndex      src/vstore/b_tree.cpp:363-702
+ *   - leaf probe SearchRecordMeta      src/vstore/b_tree.cpp:18-122, 1042-1051
+ *   - BTree::Read (+copy path)         src/vstore/b_tree.cpp:2066-2129
+ *   - point-lookup visibility          include/execute/executor.h:374-454
+ *   - RangeScanBySize + Iterator       src/vstore/b_tree.cpp:1261-1315, b_tree.h:883-953,
+ *                                      executor.h:611-642 (TableScanExecutor)
+ *   - update/commit (version chain)    b_tree.cpp:1061-1163, transaction_manager.cpp:610-676
+ *   - MurmurHash64A                    misc/murmur/MurmurHash2.cpp:99-147
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load
+ * this library, and only as the checker / the timed CPU baseline.
+ */
+#ifndef STAGE_ORACLE_H_
+#define STAGE_ORACLE_H_
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ReturnCode values, b_tree.h:42-54 */
+enum { ORC_RET_INVALID = 0, ORC_RET_OK = 1, ORC_RET_KEY_EXISTS = 2, ORC_RET_NOT_FOUND = 3,
+       ORC_RET_NODE_FROZEN = 4, ORC_RET_CAS_FAIL = 5, ORC_RET_NOT_ENOUGH_SPACE = 6,
+       ORC_RET_NOT_NEEDED_UPDATE = 7, ORC_RET_RETRY_FAILURE = 8, ORC_RET_DIRTY = 9 };
+
+/* canonical per-probe outcome of BTree::Read + IndexScanExecutor */
+enum { ORC_ST_NOT_FOUND = 0, ORC_ST_LATEST = 1, ORC_ST_COPY = 2, ORC_ST_OLD = 3,
+       ORC_ST_FAIL_INVALID_TS = 4, ORC_ST_CHAIN_MISS = 5 };
+
+typedef struct orc_read_out {
+    uint8_t status;        /* ORC_ST_* */
+    uint8_t copy_present;  /* PerformRead found an overwrite header for meta.next_ptr */
+    uint16_t hops;         /* TupleHeader hops walked */
+    uint32_t cstamp;       /* Record cstamp: latest -> reader id, copy -> rstamp, old -> begin */
+    uint32_t rec_cstamp;   /* meta.GetTxnCommitId() of the hit slot */
+    uint32_t copy_sstamp;  /* overwrite header sstamp (MAX_CID if none) */
+} orc_read_out;
+
+typedef struct orc_tree orc_tree;
+
+/* ParameterSet(split_threshold, merge_threshold, leaf_node_size, payload_size), b_tree.h:23-40 */
+orc_tree *orc_tree_new(uint32_t leaf_node_size, uint32_t split_threshold, uint32_t payload_size);
+void orc_tree_set_merge_threshold(orc_tree *t, uint32_t merge_threshold);
+void orc_tree_free(orc_tree *t);
+
+/* BTree::Insert + BTree::FinalizeInsert (loader semantics, ycsb_loader.cpp:152-171) */
+int orc_insert(orc_tree *t, const uint8_t *key, uint32_t key_size, const uint8_t *payload,
+               uint32_t commit_id);
+/* LoadYCSBRows (ycsb_loader.cpp:93-171) single loader, rows [begin,end), key = rowid as
+ * key_size (4 or 8) little-endian bytes.  payload_mode 0 = reference memset(rowid),
+ * 1 = "strong" per-word pattern (stage_payload_word).  Returns rows inserted. */
+uint64_t orc_load_ycsb(orc_tree *t, uint64_t begin, uint64_t end, uint32_t key_size,
+                       int payload_mode);
+/* insert keys[i] (key_size-byte little-endian) in the given order, payload from rowid=keys[i] */
+uint64_t orc_load_keys(orc_tree *t, const uint64_t *keys, uint64_t n, uint32_t key_size,
+                       int payload_mode);
+
+/* point lookup: rec receives [key padded to 8][payload] (8 + payload_size bytes), zeroed
+ * when no tuple is produced. */
+int orc_read(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t read_id,
+             orc_read_out *out, uint8_t *rec);
+/* batch of little-endian u64 keys of key_size bytes; rec may be NULL (only outs). */
+int orc_read_batch(orc_tree *t, const uint64_t *keys, uint32_t key_size, const uint32_t *read_ids,
+                   uint64_t n, orc_read_out *outs, uint8_t *recs, int nthreads);
+/* timing helper for the CPU baseline: same work as orc_read_batch, records written to a
+ * per-thread scratch row (the reference hands every Record to the caller and frees it).
+ * Returns a checksum of the records so nothing is optimised away. */
+uint64_t orc_read_batch_timed(orc_tree *t, const uint64_t *keys, uint32_t key_size,
+                              const uint32_t *read_ids, uint64_t n, int nthreads,
+                              double *seconds);
+
+/* TableScanExecutor (scan_sz >= 0) over RangeScanBySize/Iterator.  recs receives up to
+ * scan_size rows of [key padded 8][payload]; returns the number of records produced. */
+uint32_t orc_scan(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t scan_size,
+                  uint8_t *recs);
+uint64_t orc_scan_batch(orc_tree *t, const uint64_t *keys, uint32_t key_size, uint64_t n,
+                        uint32_t scan_size, uint32_t *counts, uint8_t *recs, int nthreads);
+
+/* host-side traversal result (BTree::TraverseToLeaf): leaf index in key order */
+int64_t orc_traverse_leaf_index(orc_tree *t, const uint8_t *key, uint32_t key_size, int le_child);
+
+/* write path used to construct visibility scenarios (single writer):
+ *   orc_update        = BTree::Update / LeafNode::Update (b_tree.cpp:1061-1163): in-place column
+ *                       patch of payload[payload_off, +delta_len), old image into a copy buffer.
+ *   orc_commit_update = CommitTransaction UPDATE branch (transaction_manager.cpp:610-676):
+ *                       TupleHeader{begin=rstamp, end=sstamp}, meta cstamp := commit_id,
+ *                       next := TupleHeader.
+ *   orc_finalize_update = BTree::FinalizeUpdate (b_tree.cpp:2252-2268, test style).
+ *   orc_delete          = BTree::Delete + FinalizeDelete (no merge). */
+int orc_update(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t payload_off,
+               const uint8_t *delta, uint32_t delta_len, uint32_t writer_id);
+int orc_commit_update(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t commit_id,
+                      uint32_t sstamp);
+int orc_finalize_update(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t commit_id);
+int orc_delete(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t commit_id);
+
+/* stats[0]=height stats[1]=inner nodes stats[2]=leaves stats[3]=records stats[4]=sorted slots
+ * stats[5]=unsorted slots stats[6]=max records/leaf stats[7]=retired versions */
+void orc_stats(orc_tree *t, uint64_t *stats);
+/* leaves in key order: rc[i]=record_count, sc[i]=sorted_count; slot arrays (cap per leaf):
+ * meta[i*cap+s], key bytes as little-endian u64 keyw[i*cap+s]; returns number of leaves,
+ * or -(needed) when max_leaves is too small. */
+int64_t orc_export_leaves(orc_tree *t, uint32_t cap, uint64_t max_leaves, uint32_t *rc,
+                          uint32_t *sc, uint64_t *meta, uint64_t *keyw);
+
+/* KeyCompare (b_tree.h:116-134) */
+int orc_key_compare(const uint8_t *k1, uint32_t s1, const uint8_t *k2, uint32_t s2);
+/* MurmurHash64A (misc/murmur/MurmurHash2.cpp:99-147) */
+uint64_t orc_murmur64a(const void *key, int len, uint64_t seed);
+void orc_murmur64a_batch(const uint64_t *keys, uint64_t n, int len, uint64_t seed, uint64_t *out);
+/* payload generator shared by both sides' loaders (data, not algorithm) */
+uint64_t orc_payload_word(uint64_t rowid, uint32_t j);
+void orc_fill_payload(uint64_t rowid, int mode, uint8_t *dst, uint32_t payload_size);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,326 @@
+// capi.cpp -- the extern "C" boundary (include/stage_hip.h).  No exception crosses it.
+#include <hip/hip_runtime_api.h>
+
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/stage_hip.h"
+#include "device_image.hpp"
+#include "dist.hpp"
+#include "host_table.hpp"
+#include "kernel_api.hpp"
+
+struct stage_table {
+    std::unique_ptr<stage::HostTable> host;
+    stage::DeviceImage dev;
+    stage::ProbeTuning tune;
+    std::unique_ptr<stage::ShardComm> comm;
+};
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+template <class F>
+int guarded(F fn) {
+    try {
+        return fn();
+    } catch (const std::bad_alloc &) {
+        return fail(STAGE_E_NOMEM, "host allocation failed");
+    } catch (const std::invalid_argument &e) {
+        return fail(STAGE_E_ARG, e.what());
+    } catch (const std::exception &e) {
+        return fail(STAGE_E_HIP, e.what());
+    }
+}
+
+int need_synced(stage_table *t) {
+    if (!t) return fail(STAGE_E_ARG, "null table");
+    if (!t->dev.valid || t->host->layout_dirty_)
+        return fail(STAGE_E_STATE, "device image is stale: call stage_sync after host writes");
+    return STAGE_OK;
+}
+
+hipStream_t pick(stage_table *t, void *stream) { return stream ? (hipStream_t)stream : t->dev.stream; }
+
+int hip_rc(hipError_t e, const char *what) {
+    if (e == hipSuccess) return STAGE_OK;
+    return fail(STAGE_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+}  // namespace
+
+extern "C" {
+
+const char *stage_last_error(void) { return g_err.c_str(); }
+const char *stage_version(void) { return "stage-hip 0.1 (gfx950)"; }
+
+int stage_table_create(const stage_params *params, stage_table **out) {
+    if (!params || !out) return fail(STAGE_E_ARG, "null argument");
+    return guarded([&] {
+        auto t = std::make_unique<stage_table>();
+        t->host = std::make_unique<stage::HostTable>(*params);
+        t->dev.device = params->device;
+        if (const char *g = std::getenv("STAGE_PROBE_GROUP")) t->tune.group = std::atoi(g);
+        if (const char *g = std::getenv("STAGE_PROBE_MAX_BLOCKS")) t->tune.max_blocks = std::atoi(g);
+        *out = t.release();
+        return STAGE_OK;
+    });
+}
+
+int stage_table_destroy(stage_table *t) {
+    if (!t) return STAGE_OK;
+    return guarded([&] {
+        if (t->dev.stream) (void)hipSetDevice(t->dev.device);
+        delete t;
+        return STAGE_OK;
+    });
+}
+
+int stage_insert(stage_table *t, uint64_t key, uint16_t key_size, const uint8_t *payload, uint64_t gen_rowid,
+                 int payload_mode, uint32_t commit_id, uint8_t *rc_out) {
+    if (!t) return fail(STAGE_E_ARG, "null table");
+    return guarded([&] {
+        int rc = t->host->insert(key, key_size, payload, gen_rowid, payload_mode, commit_id);
+        if (rc_out) *rc_out = (uint8_t)rc;
+        return STAGE_OK;
+    });
+}
+
+int stage_load_ycsb(stage_table *t, uint64_t begin_rowid, uint64_t end_rowid, uint32_t key_size, int payload_mode,
+                    uint64_t *inserted) {
+    if (!t || key_size == 0 || key_size > 8) return fail(STAGE_E_ARG, "bad arguments");
+    return guarded([&] {
+        uint64_t n = t->host->load_ycsb(begin_rowid, end_rowid, key_size, payload_mode);
+        if (inserted) *inserted = n;
+        return STAGE_OK;
+    });
+}
+
+int stage_load_keys(stage_table *t, const uint64_t *keys, uint64_t n, uint32_t key_size, int payload_mode,
+                    uint64_t *inserted) {
+    if (!t || (!keys && n) || key_size == 0 || key_size > 8) return fail(STAGE_E_ARG, "bad arguments");
+    return guarded([&] {
+        uint64_t c = t->host->load_keys(keys, n, key_size, payload_mode);
+        if (inserted) *inserted = c;
+        return STAGE_OK;
+    });
+}
+
+int stage_update(stage_table *t, uint64_t key, uint16_t key_size, uint32_t payload_off, const uint8_t *delta,
+                 uint32_t delta_len, uint32_t writer_id, uint8_t *rc_out) {
+    if (!t || (!delta && delta_len)) return fail(STAGE_E_ARG, "bad arguments");
+    return guarded([&] {
+        int rc = t->host->update(key, key_size, payload_off, delta, delta_len, writer_id);
+        if (rc_out) *rc_out = (uint8_t)rc;
+        return STAGE_OK;
+    });
+}
+
+int stage_commit_update(stage_table *t, uint64_t key, uint16_t key_size, uint32_t commit_id, uint32_t sstamp,
+                        uint8_t *rc_out) {
+    if (!t) return fail(STAGE_E_ARG, "null table");
+    return guarded([&] {
+        int rc = t->host->commit_update(key, key_size, commit_id, sstamp);
+        if (rc_out) *rc_out = (uint8_t)rc;
+        return STAGE_OK;
+    });
+}
+
+int stage_finalize_update(stage_table *t, uint64_t key, uint16_t key_size, uint32_t commit_id, uint8_t *rc_out) {
+    if (!t) return fail(STAGE_E_ARG, "null table");
+    return guarded([&] {
+        int rc = t->host->finalize_update(key, key_size, commit_id);
+        if (rc_out) *rc_out = (uint8_t)rc;
+        return STAGE_OK;
+    });
+}
+
+int stage_delete(stage_table *t, uint64_t key, uint16_t key_size, uint32_t commit_id, uint8_t *rc_out) {
+    if (!t) return fail(STAGE_E_ARG, "null table");
+    return guarded([&] {
+        int rc = t->host->remove(key, key_size, commit_id);
+        if (rc_out) *rc_out = (uint8_t)rc;
+        return STAGE_OK;
+    });
+}
+
+int stage_sync(stage_table *t) {
+    if (!t) return fail(STAGE_E_ARG, "null table");
+    return guarded([&] {
+        stage::sync_device(*t->host, t->dev);
+        return STAGE_OK;
+    });
+}
+
+int stage_stats(stage_table *t, uint64_t *stats) {
+    if (!t || !stats) return fail(STAGE_E_ARG, "null argument");
+    return guarded([&] {
+        t->host->stats(stats);
+        return STAGE_OK;
+    });
+}
+
+uint32_t stage_record_stride(stage_table *t) { return t ? t->host->stride() : 0; }
+uint32_t stage_leaf_capacity(stage_table *t) { return t ? t->host->cap() : 0; }
+
+int stage_traverse_batch(stage_table *t, const uint64_t *keys, const uint16_t *lens, uint64_t n, int le_child,
+                         uint32_t *leaf_out) {
+    if (!t) return fail(STAGE_E_ARG, "null table");
+    if ((!keys || !leaf_out) && n) return fail(STAGE_E_ARG, "null argument");
+    return guarded([&] {
+        // leaf index in key order: from the published image, or recomputed if host writes
+        // happened since (the traversal itself never needs the device)
+        std::vector<uint32_t> local;
+        const std::vector<uint32_t> *map = &t->dev.host_to_dev;
+        if (!t->dev.valid || t->host->layout_dirty_) {
+            std::vector<uint32_t> order;
+            t->host->key_order(order);
+            local.assign(t->host->leaves_.size(), 0xFFFFFFFFu);
+            for (size_t i = 0; i < order.size(); ++i) local[order[i]] = (uint32_t)i;
+            map = &local;
+        }
+        const uint32_t kw = t->host->params().key_width;
+        for (uint64_t i = 0; i < n; ++i) {
+            const uint32_t len = kw ? kw : (lens ? lens[i] : 8u);
+            const uint64_t mask = len >= 8 ? ~0ull : ((1ull << (8 * len)) - 1);
+            stage::Key k{stage::order_key(keys[i] & mask, len), len};
+            leaf_out[i] = (*map)[t->host->route(k, le_child != 0)];
+        }
+        return STAGE_OK;
+    });
+}
+
+int64_t stage_export_leaves(stage_table *t, uint32_t cap, uint64_t max_leaves, uint32_t *rc, uint32_t *sc,
+                            uint64_t *meta, uint64_t *keyw) {
+    if (!t || !rc || !sc || !meta || !keyw) return fail(STAGE_E_ARG, "null argument");
+    try {
+        return t->host->export_leaves(cap, max_leaves, rc, sc, meta, keyw);
+    } catch (const std::exception &e) {
+        return fail(STAGE_E_HIP, e.what());
+    }
+}
+
+int stage_probe_batch(stage_table *t, const uint64_t *d_keys, const uint16_t *d_lens, const uint32_t *d_read_ids,
+                      const uint32_t *d_leaf_ids, uint64_t n, stage_probe_out *d_out, uint8_t *d_records,
+                      void *stream) {
+    int rc = need_synced(t);
+    if (rc) return rc;
+    if (n && (!d_keys || !d_out)) return fail(STAGE_E_ARG, "null device buffer");
+    hipError_t e = hipSetDevice(t->dev.device);
+    if (e != hipSuccess) return hip_rc(e, "hipSetDevice");
+    e = stage::launch_probe(t->dev.view, d_keys, d_lens, d_read_ids, d_leaf_ids, n,
+                            reinterpret_cast<stage::stage_probe_out_dev *>(d_out), d_records, pick(t, stream), t->tune);
+    return hip_rc(e, "probe kernel");
+}
+
+int stage_scan_batch(stage_table *t, const uint64_t *d_start_keys, const uint16_t *d_lens, uint64_t n,
+                     uint32_t scan_size, uint32_t *d_counts, uint8_t *d_records, void *stream) {
+    int rc = need_synced(t);
+    if (rc) return rc;
+    if (n && (!d_start_keys || !d_counts || (!d_records && scan_size))) return fail(STAGE_E_ARG, "null device buffer");
+    hipError_t e = hipSetDevice(t->dev.device);
+    if (e != hipSuccess) return hip_rc(e, "hipSetDevice");
+    e = stage::launch_scan(t->dev.view, d_start_keys, d_lens, n, scan_size, d_counts, d_records, pick(t, stream));
+    return hip_rc(e, "scan kernel");
+}
+
+int stage_resolve_batch(stage_table *t, const uint64_t *d_keys, const uint16_t *d_lens, uint64_t n, int le_child,
+                        uint32_t *d_leaf, void *stream) {
+    int rc = need_synced(t);
+    if (rc) return rc;
+    if (n && (!d_keys || !d_leaf)) return fail(STAGE_E_ARG, "null device buffer");
+    hipError_t e = hipSetDevice(t->dev.device);
+    if (e != hipSuccess) return hip_rc(e, "hipSetDevice");
+    e = stage::launch_resolve(t->dev.view, d_keys, d_lens, n, le_child, d_leaf, pick(t, stream));
+    return hip_rc(e, "resolve kernel");
+}
+
+int stage_murmur64a_batch(const void *d_keys, uint32_t key_len, uint32_t key_stride, uint64_t seed, uint64_t n,
+                          uint64_t *d_out, void *stream) {
+    if (n && (!d_keys || !d_out || key_stride < key_len)) return fail(STAGE_E_ARG, "bad arguments");
+    return hip_rc(stage::launch_murmur(d_keys, key_len, key_stride, seed, n, d_out, (hipStream_t)stream),
+                  "murmur kernel");
+}
+
+// ---- plumbing
+int stage_set_device(int device) { return hip_rc(hipSetDevice(device), "hipSetDevice"); }
+int stage_device_count(int *count) { return hip_rc(hipGetDeviceCount(count), "hipGetDeviceCount"); }
+int stage_dev_alloc(uint64_t bytes, void **ptr) { return hip_rc(hipMalloc(ptr, bytes ? bytes : 16), "hipMalloc"); }
+int stage_dev_free(void *ptr) { return hip_rc(hipFree(ptr), "hipFree"); }
+int stage_dev_memset(void *ptr, int value, uint64_t bytes, void *stream) {
+    return hip_rc(hipMemsetAsync(ptr, value, bytes, (hipStream_t)stream), "hipMemsetAsync");
+}
+int stage_memcpy_h2d(void *dst, const void *src, uint64_t bytes, void *stream) {
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream);
+    if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)stream);
+    return hip_rc(e, "h2d");
+}
+int stage_memcpy_d2h(void *dst, const void *src, uint64_t bytes, void *stream) {
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream);
+    if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)stream);
+    return hip_rc(e, "d2h");
+}
+int stage_stream_create(void **stream) {
+    return hip_rc(hipStreamCreateWithFlags((hipStream_t *)stream, hipStreamNonBlocking), "hipStreamCreate");
+}
+int stage_stream_destroy(void *stream) { return hip_rc(hipStreamDestroy((hipStream_t)stream), "hipStreamDestroy"); }
+int stage_stream_sync(void *stream) { return hip_rc(hipStreamSynchronize((hipStream_t)stream), "hipStreamSynchronize"); }
+int stage_device_sync(void) { return hip_rc(hipDeviceSynchronize(), "hipDeviceSynchronize"); }
+int stage_event_create(void **ev) { return hip_rc(hipEventCreate((hipEvent_t *)ev), "hipEventCreate"); }
+int stage_event_destroy(void *ev) { return hip_rc(hipEventDestroy((hipEvent_t)ev), "hipEventDestroy"); }
+int stage_event_record(void *ev, void *stream) {
+    return hip_rc(hipEventRecord((hipEvent_t)ev, (hipStream_t)stream), "hipEventRecord");
+}
+int stage_event_elapsed(void *a, void *b, float *ms) {
+    hipError_t e = hipEventSynchronize((hipEvent_t)b);
+    if (e == hipSuccess) e = hipEventElapsedTime(ms, (hipEvent_t)a, (hipEvent_t)b);
+    return hip_rc(e, "hipEventElapsedTime");
+}
+
+// ---- multi-GPU
+int stage_comm_unique_id(uint8_t *id128) {
+    if (!id128) return fail(STAGE_E_ARG, "null argument");
+    return guarded([&] { return stage::shard_unique_id(id128); });
+}
+
+int stage_comm_init(stage_table *t, const uint8_t *id128, int rank, int world) {
+    if (!t || !id128 || world < 1 || rank < 0 || rank >= world) return fail(STAGE_E_ARG, "bad arguments");
+    return guarded([&] {
+        (void)hipSetDevice(t->dev.device);
+        t->comm = std::make_unique<stage::ShardComm>();
+        return stage::shard_init(*t->comm, id128, rank, world);
+    });
+}
+
+int stage_comm_destroy(stage_table *t) {
+    if (!t) return fail(STAGE_E_ARG, "null table");
+    return guarded([&] {
+        t->comm.reset();
+        return STAGE_OK;
+    });
+}
+
+int stage_probe_sharded(stage_table *t, const uint64_t *d_keys, const uint32_t *d_read_ids, uint64_t n,
+                        stage_probe_out *d_out, uint8_t *d_records, void *stream) {
+    int rc = need_synced(t);
+    if (rc) return rc;
+    if (!t->comm) return fail(STAGE_E_STATE, "stage_comm_init first");
+    return guarded([&] {
+        (void)hipSetDevice(t->dev.device);
+        return stage::shard_probe(*t->comm, t->dev.view, t->tune, d_keys, d_read_ids, n,
+                                  reinterpret_cast<stage::stage_probe_out_dev *>(d_out), d_records, pick(t, stream));
+    });
+}
+
+}  // extern "C"
+
+namespace stage {
+void set_error(const std::string &msg) { g_err = msg; }
+}  // namespace stage

@@ -1,0 +1,231 @@
+// device_image.cpp -- builds the HBM image of a table from its host layout.
+#include "device_image.hpp"
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <thread>
+
+namespace stage {
+
+void hip_check(hipError_t e, const char *what) {
+    if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+static void dev_ensure(DevBuf &b, uint64_t bytes, const char *what) {
+    if (bytes == 0) bytes = 16;
+    if (b.cap >= bytes) return;
+    if (b.p) hip_check(hipFree(b.p), "hipFree");
+    b.p = nullptr;
+    b.cap = 0;
+    hip_check(hipMalloc(&b.p, bytes), what);
+    b.cap = bytes;
+}
+
+DeviceImage::~DeviceImage() { release(); }
+
+void DeviceImage::release() {
+    for (DevBuf *b : {&okey, &slot, &vis, &tree, &tree_len, &heap, &chdr, &vhdr, &arena, &descs}) {
+        if (b->p) (void)hipFree(b->p);
+        b->p = nullptr;
+        b->cap = 0;
+    }
+    if (stream) (void)hipStreamDestroy(stream);
+    stream = nullptr;
+    valid = false;
+}
+
+template <class F>
+static void parallel_for(uint64_t n, F fn) {
+    unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (n < (1u << 16)) nt = 1;
+    std::vector<std::thread> th;
+    for (unsigned k = 0; k < nt; ++k)
+        th.emplace_back([=] {
+            uint64_t b = n * k / nt, e = n * (k + 1) / nt;
+            for (uint64_t i = b; i < e; ++i) fn(i);
+        });
+    for (auto &x : th) x.join();
+}
+
+static void upload(DevBuf &b, const void *src, uint64_t bytes, hipStream_t s, const char *what) {
+    dev_ensure(b, bytes, what);
+    if (bytes) hip_check(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, s), what);
+}
+
+void sync_device(HostTable &h, DeviceImage &d) {
+    auto t0 = std::chrono::steady_clock::now();
+    hip_check(hipSetDevice(d.device), "hipSetDevice");
+    if (!d.stream) hip_check(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking), "hipStreamCreate");
+    const stage_params &p = h.params();
+    const uint32_t cap = h.cap(), spl = cap / 64;
+
+    // ---- leaves in key order
+    std::vector<uint32_t> order;
+    h.key_order(order);
+    const uint64_t L = order.size();
+    d.host_to_dev.assign(h.leaves_.size(), 0xFFFFFFFFu);
+    for (uint64_t i = 0; i < L; ++i) d.host_to_dev[order[i]] = (uint32_t)i;
+
+    std::vector<uint64_t> okey(L * cap), vis(L * spl, 0);
+    std::vector<SlotInfo> slot(L * cap);
+    parallel_for(L, [&](uint64_t di) {
+        const uint64_t hb = (uint64_t)order[di] * cap, db = di * cap;
+        const uint32_t count = h.leaves_[order[di]].count;
+        for (uint32_t s = 0; s < cap; ++s) {
+            const bool live = s < count;
+            const uint64_t m = live ? h.meta_[hb + s] : 0;
+            okey[db + s] = live ? h.okey_[hb + s] : 0;
+            slot[db + s].meta = m;
+            slot[db + s].next = live ? h.next_[hb + s] : 0;
+            slot[db + s].image = live ? h.image_[hb + s] : 0;
+            if (meta_visible(m) && (p.key_width == 0 || meta_keylen(m) == p.key_width))
+                vis[di * spl + s / 64] |= 1ull << (s % 64);
+        }
+    });
+
+    // ---- implicit 8-ary separator tree: level 0 = separators, level k+1 = max of each
+    // 8-entry node of level k, every level padded with +inf, top level one node.
+    const uint64_t S = L ? L - 1 : 0;
+    std::vector<std::vector<uint64_t>> lv;
+    std::vector<std::vector<uint8_t>> lvlen;
+    {
+        const uint64_t n0 = (S + 1 + 7) / 8 * 8;
+        std::vector<uint64_t> l0(n0, ~0ull);
+        std::vector<uint8_t> l0len(n0, 0xFF);
+        for (uint64_t i = 0; i < S; ++i) {
+            const auto &sep = h.leaves_[order[i]].sep;
+            l0[i] = sep.okey;
+            l0len[i] = (uint8_t)sep.len;
+        }
+        lv.push_back(std::move(l0));
+        lvlen.push_back(std::move(l0len));
+        while (lv.back().size() > (uint64_t)kTreeFanout) {
+            const auto &prev = lv.back();
+            const auto &prevlen = lvlen.back();
+            const uint64_t nodes = prev.size() / kTreeFanout;
+            const uint64_t nn = (nodes + 7) / 8 * 8;
+            std::vector<uint64_t> nx(nn, ~0ull);
+            std::vector<uint8_t> nxlen(nn, 0xFF);
+            for (uint64_t j = 0; j < nodes; ++j) {
+                nx[j] = prev[j * kTreeFanout + kTreeFanout - 1];
+                nxlen[j] = prevlen[j * kTreeFanout + kTreeFanout - 1];
+            }
+            lv.push_back(std::move(nx));
+            lvlen.push_back(std::move(nxlen));
+        }
+    }
+    if (lv.size() > (size_t)kMaxTreeLevels) throw std::runtime_error("separator tree too deep");
+    std::vector<uint64_t> tree;
+    std::vector<uint8_t> tree_len;
+    uint64_t level_off[kMaxTreeLevels] = {0};
+    for (size_t k = 0; k < lv.size(); ++k) {
+        level_off[k] = tree.size();
+        tree.insert(tree.end(), lv[k].begin(), lv[k].end());
+        tree_len.insert(tree_len.end(), lvlen[k].begin(), lvlen[k].end());
+    }
+
+    hipStream_t s = d.stream;
+    upload(d.okey, okey.data(), okey.size() * 8, s, "okey");
+    upload(d.slot, slot.data(), slot.size() * sizeof(SlotInfo), s, "slot");
+    upload(d.vis, vis.data(), vis.size() * 8, s, "vis");
+    upload(d.tree, tree.data(), tree.size() * 8, s, "tree");
+    upload(d.tree_len, tree_len.data(), tree_len.size(), s, "tree_len");
+    upload(d.chdr, h.copies_.data(), h.copies_.size() * sizeof(CopyHdr), s, "chdr");
+    upload(d.vhdr, h.versions_.data(), h.versions_.size() * sizeof(VersionHdr), s, "vhdr");
+
+    // ---- record heap: fill the rows of images created since the last sync
+    const uint32_t stride = h.stride();
+    const uint64_t nimg = h.images_.size();
+    if (nimg > d.heap_rows) {
+        const uint64_t rows = nimg + std::max<uint64_t>(nimg / 16, 1024);
+        DevBuf nb;
+        hip_check(hipMalloc(&nb.p, rows * stride), "record heap");
+        nb.cap = rows * stride;
+        if (d.heap.p && h.images_synced_) {
+            hip_check(hipMemcpyAsync(nb.p, d.heap.p, h.images_synced_ * stride, hipMemcpyDeviceToDevice, s),
+                      "heap grow");
+            hip_check(hipStreamSynchronize(s), "heap grow sync");
+        }
+        if (d.heap.p) hip_check(hipFree(d.heap.p), "hipFree heap");
+        d.heap = nb;
+        d.heap_rows = rows;
+    }
+    if (h.arena_.size() > h.arena_synced_) {
+        // the device arena mirrors the host arena; grow keeps the already uploaded prefix
+        if (d.arena.cap < h.arena_.size()) {
+            DevBuf nb;
+            const uint64_t bytes = h.arena_.size() + h.arena_.size() / 4 + 4096;
+            hip_check(hipMalloc(&nb.p, bytes), "arena");
+            nb.cap = bytes;
+            if (d.arena.p && h.arena_synced_)
+                hip_check(hipMemcpyAsync(nb.p, d.arena.p, h.arena_synced_, hipMemcpyDeviceToDevice, s), "arena grow");
+            hip_check(hipStreamSynchronize(s), "arena sync");
+            if (d.arena.p) hip_check(hipFree(d.arena.p), "hipFree arena");
+            d.arena = nb;
+        }
+        hip_check(hipMemcpyAsync((uint8_t *)d.arena.p + h.arena_synced_, h.arena_.data() + h.arena_synced_,
+                                 h.arena_.size() - h.arena_synced_, hipMemcpyHostToDevice, s),
+                  "arena upload");
+        h.arena_synced_ = h.arena_.size();
+    }
+    const uint64_t first = h.images_synced_, count = nimg - first;
+    if (count) {
+        // identity run (LoadYCSBRows): image r = rowid0 + r, key = rowid, one payload mode
+        const ImageDesc &d0 = h.images_[first];
+        bool ident = d0.kind == 0;
+        uint32_t kw = 8;
+        if (ident) {
+            const uint64_t kmask_bits = d0.key_le;
+            (void)kmask_bits;
+            kw = p.key_width ? p.key_width : 8;
+            const uint64_t kmask = kw >= 8 ? ~0ull : ((1ull << (8 * kw)) - 1);
+            for (uint64_t r = 0; r < count && ident; ++r) {
+                const ImageDesc &e = h.images_[first + r];
+                ident = e.kind == 0 && e.mode == d0.mode && e.arg == d0.arg + r && e.key_le == (e.arg & kmask);
+            }
+        }
+        if (ident) {
+            hip_check(launch_fill((uint8_t *)d.heap.p, stride, p.payload_size, nullptr, nullptr, first, count, d0.arg,
+                                  kw, (int)d0.mode, s),
+                      "fill (identity)");
+        } else {
+            std::vector<ImageDescDev> dd(count);
+            for (uint64_t r = 0; r < count; ++r) {
+                const ImageDesc &e = h.images_[first + r];
+                dd[r] = ImageDescDev{e.key_le, e.arg, e.kind, e.mode};
+            }
+            upload(d.descs, dd.data(), count * sizeof(ImageDescDev), s, "descs");
+            hip_check(launch_fill((uint8_t *)d.heap.p, stride, p.payload_size, (const ImageDescDev *)d.descs.p,
+                                  (const uint8_t *)d.arena.p, first, count, 0, 0, 0, s),
+                      "fill");
+        }
+        h.images_synced_ = nimg;
+    }
+    hip_check(hipStreamSynchronize(s), "sync");
+
+    DevTable &v = d.view;
+    v.okey = (const uint64_t *)d.okey.p;
+    v.slot = (const SlotInfo *)d.slot.p;
+    v.vis = (const uint64_t *)d.vis.p;
+    v.tree = (const uint64_t *)d.tree.p;
+    v.tree_len = (const uint8_t *)d.tree_len.p;
+    v.heap = (const uint8_t *)d.heap.p;
+    v.chdr = (const CopyHdr *)d.chdr.p;
+    v.vhdr = (const VersionHdr *)d.vhdr.p;
+    for (int k = 0; k < kMaxTreeLevels; ++k) v.level_off[k] = level_off[k];
+    v.levels = (uint32_t)lv.size();
+    v.nleaves = (uint32_t)L;
+    v.nseps = (uint32_t)S;
+    v.cap = cap;
+    v.stride = stride;
+    v.payload_size = p.payload_size;
+    v.key_width = p.key_width;
+    h.layout_dirty_ = false;
+    d.valid = true;
+    d.last_sync_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+}  // namespace stage

@@ -1,0 +1,217 @@
+// dist.hip -- multi-GPU YCSB-C front-end: route every key to shard
+// MurmurHash64A(key, 8, 0) % world (misc/murmur/MurmurHash2.cpp:99-147 as the router),
+// exchange keys with one RCCL all-to-all-v (grouped ncclSend/ncclRecv over xGMI), probe the
+// local shard, return results with the reverse all-to-all-v and scatter them back into the
+// caller's order.  The reference has no distributed layer; this is the
+// build's own exchange step for the 8-GPU config.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/stage_hip.h"
+#include "dist.hpp"
+
+namespace stage {
+
+namespace {
+
+void chk(hipError_t e, const char *what) {
+    if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+void nchk(ncclResult_t r, const char *what) {
+    if (r != ncclSuccess) throw std::runtime_error(std::string(what) + ": " + ncclGetErrorString(r));
+}
+
+struct alignas(16) SendRec {
+    uint64_t key;
+    uint32_t rid;
+    uint32_t pad;
+};
+
+__device__ __forceinline__ uint64_t mm64a_8(uint64_t k) {
+    const uint64_t m = 0xc6a4a7935bd1e995ull;
+    uint64_t h = 0 ^ (8ull * m);
+    k *= m;
+    k ^= k >> 47;
+    k *= m;
+    h ^= k;
+    h *= m;
+    h ^= h >> 47;
+    h *= m;
+    h ^= h >> 47;
+    return h;
+}
+
+__global__ void route_count(const uint64_t *__restrict__ keys, uint64_t n, int world, uint32_t *__restrict__ dest,
+                            uint32_t *__restrict__ counts) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t d = (uint32_t)(mm64a_8(keys[i]) % (uint64_t)world);
+    dest[i] = d;
+    atomicAdd(&counts[d], 1u);
+}
+
+__global__ void route_scatter(const uint64_t *__restrict__ keys, const uint32_t *__restrict__ rids, uint64_t n,
+                              const uint32_t *__restrict__ dest, uint32_t *__restrict__ cursor,
+                              SendRec *__restrict__ send, uint32_t *__restrict__ perm) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t pos = atomicAdd(&cursor[dest[i]], 1u);
+    send[pos] = SendRec{keys[i], rids ? rids[i] : 0xFFFFFFFEu, 0};
+    perm[pos] = (uint32_t)i;
+}
+
+__global__ void unpack_keys(const SendRec *__restrict__ recv, uint64_t n, uint64_t *__restrict__ keys,
+                            uint32_t *__restrict__ rids) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    keys[i] = recv[i].key;
+    rids[i] = recv[i].rid;
+}
+
+// back in the caller's order: out[perm[p]] = bout[p], row copy by one wave per probe
+__global__ void unpermute(const stage_probe_out_dev *__restrict__ bout, const uint8_t *__restrict__ brec,
+                          const uint32_t *__restrict__ perm, uint64_t n, uint32_t stride,
+                          stage_probe_out_dev *__restrict__ out, uint8_t *__restrict__ recs) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    for (uint64_t p = w; p < n; p += nw) {
+        const uint32_t dst = perm[p];
+        if (lane < 2) reinterpret_cast<uint4 *>(out + dst)[lane] = reinterpret_cast<const uint4 *>(bout + p)[lane];
+        if (recs) {
+            const uint4 *s = reinterpret_cast<const uint4 *>(brec + p * (uint64_t)stride);
+            uint4 *d = reinterpret_cast<uint4 *>(recs + (uint64_t)dst * stride);
+            for (uint32_t c = lane; c < (stride >> 4); c += 64) d[c] = s[c];
+        }
+    }
+}
+
+void grow(void *&p, uint64_t bytes) {
+    if (p) chk(hipFree(p), "hipFree");
+    p = nullptr;
+    chk(hipMalloc(&p, bytes ? bytes : 16), "hipMalloc");
+}
+
+}  // namespace
+
+ShardComm::~ShardComm() {
+    if (comm) ncclCommDestroy((ncclComm_t)comm);
+    for (void *p : {dest, cursor, perm, send, recv, rout, rrec, bout, brec, cnt, lkeys, lrids})
+        if (p) (void)hipFree(p);
+}
+
+int shard_unique_id(uint8_t *id128) {
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    ncclUniqueId id;
+    nchk(ncclGetUniqueId(&id), "ncclGetUniqueId");
+    std::memcpy(id128, &id, 128);
+    return STAGE_OK;
+}
+
+int shard_init(ShardComm &c, const uint8_t *id128, int rank, int world) {
+    ncclUniqueId id;
+    std::memcpy(&id, id128, 128);
+    ncclComm_t comm;
+    nchk(ncclCommInitRank(&comm, world, id, rank), "ncclCommInitRank");
+    c.comm = comm;
+    c.rank = rank;
+    c.world = world;
+    grow(c.cnt, 4 * sizeof(uint32_t) * (uint64_t)world);
+    return STAGE_OK;
+}
+
+int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const uint64_t *d_keys,
+                const uint32_t *d_rids, uint64_t n, stage_probe_out_dev *d_out, uint8_t *d_recs, hipStream_t s) {
+    const int W = c.world;
+    const uint32_t stride = t.stride;
+    if (n > 0xFFFFFFFFull) throw std::invalid_argument("batch too large");
+    if (n > c.cap_local || stride != c.rec_stride) {
+        const uint64_t cap = n + n / 8 + 1024;
+        grow(c.dest, cap * 4);
+        grow(c.perm, cap * 4);
+        grow(c.send, cap * sizeof(SendRec));
+        grow(c.bout, cap * sizeof(stage_probe_out_dev));
+        grow(c.brec, cap * stride);
+        c.cap_local = cap;
+        c.rec_stride = stride;
+    }
+    uint32_t *counts = (uint32_t *)c.cnt;  // [0,W) send counts, [W,2W) cursor, [2W,3W) recv counts
+    chk(hipMemsetAsync(counts, 0, 2 * W * sizeof(uint32_t), s), "memset");
+    const unsigned blocks = (unsigned)((n + 255) / 256);
+    if (n) route_count<<<blocks, 256, 0, s>>>(d_keys, n, W, (uint32_t *)c.dest, counts);
+    std::vector<uint32_t> sc(W), rc(W);
+    chk(hipMemcpyAsync(sc.data(), counts, W * 4, hipMemcpyDeviceToHost, s), "counts d2h");
+    chk(hipStreamSynchronize(s), "sync");
+    std::vector<uint32_t> soff(W + 1, 0);
+    for (int r = 0; r < W; ++r) soff[r + 1] = soff[r] + sc[r];
+    chk(hipMemcpyAsync(counts + W, soff.data(), W * 4, hipMemcpyHostToDevice, s), "cursor h2d");
+    if (n)
+        route_scatter<<<blocks, 256, 0, s>>>(d_keys, d_rids, n, (const uint32_t *)c.dest, counts + W,
+                                             (SendRec *)c.send, (uint32_t *)c.perm);
+    // exchange the per-destination counts
+    ncclComm_t comm = (ncclComm_t)c.comm;
+    nchk(ncclAllToAll(counts, counts + 2 * W, 1, ncclUint32, comm, s), "ncclAllToAll counts");
+    chk(hipMemcpyAsync(rc.data(), counts + 2 * W, W * 4, hipMemcpyDeviceToHost, s), "recv counts d2h");
+    chk(hipStreamSynchronize(s), "sync");
+    std::vector<uint64_t> roff(W + 1, 0);
+    for (int r = 0; r < W; ++r) roff[r + 1] = roff[r] + rc[r];
+    const uint64_t m = roff[W];
+    if (m > c.cap_remote || stride != c.rec_stride) {
+        const uint64_t cap = m + m / 8 + 1024;
+        grow(c.recv, cap * sizeof(SendRec));
+        grow(c.rout, cap * sizeof(stage_probe_out_dev));
+        grow(c.rrec, cap * stride);
+        grow(c.lkeys, cap * 8);
+        grow(c.lrids, cap * 4);
+        c.cap_remote = cap;
+    }
+    // keys out: all-to-all-v as grouped point-to-point transfers
+    nchk(ncclGroupStart(), "group");
+    for (int r = 0; r < W; ++r) {
+        if (sc[r]) nchk(ncclSend((const uint8_t *)c.send + (uint64_t)soff[r] * sizeof(SendRec), (uint64_t)sc[r] * sizeof(SendRec),
+                                 ncclUint8, r, comm, s), "send keys");
+        if (rc[r]) nchk(ncclRecv((uint8_t *)c.recv + roff[r] * sizeof(SendRec), (uint64_t)rc[r] * sizeof(SendRec), ncclUint8,
+                                 r, comm, s), "recv keys");
+    }
+    nchk(ncclGroupEnd(), "group end");
+    // local probe of everything this shard owns
+    uint64_t *lk = (uint64_t *)c.lkeys;
+    uint32_t *lr = (uint32_t *)c.lrids;
+    if (m) {
+        unpack_keys<<<(unsigned)((m + 255) / 256), 256, 0, s>>>((const SendRec *)c.recv, m, lk, lr);
+        chk(launch_probe(t, lk, nullptr, lr, nullptr, m, (stage_probe_out_dev *)c.rout,
+                         d_recs ? (uint8_t *)c.rrec : nullptr, s, tune),
+            "probe");
+    }
+    // results back
+    const uint64_t ob = sizeof(stage_probe_out_dev);
+    nchk(ncclGroupStart(), "group");
+    for (int r = 0; r < W; ++r) {
+        if (rc[r]) {
+            nchk(ncclSend((const uint8_t *)c.rout + roff[r] * ob, (uint64_t)rc[r] * ob, ncclUint8, r, comm, s), "send out");
+            if (d_recs)
+                nchk(ncclSend((const uint8_t *)c.rrec + roff[r] * stride, (uint64_t)rc[r] * stride, ncclUint8, r, comm, s),
+                     "send rows");
+        }
+        if (sc[r]) {
+            nchk(ncclRecv((uint8_t *)c.bout + (uint64_t)soff[r] * ob, (uint64_t)sc[r] * ob, ncclUint8, r, comm, s), "recv out");
+            if (d_recs)
+                nchk(ncclRecv((uint8_t *)c.brec + (uint64_t)soff[r] * stride, (uint64_t)sc[r] * stride, ncclUint8, r, comm, s),
+                     "recv rows");
+        }
+    }
+    nchk(ncclGroupEnd(), "group end");
+    if (n)
+        unpermute<<<(unsigned)std::min<uint64_t>((n + 3) / 4, 8192), 256, 0, s>>>(
+            (const stage_probe_out_dev *)c.bout, (const uint8_t *)c.brec, (const uint32_t *)c.perm, n, stride, d_out,
+            d_recs);
+    chk(hipGetLastError(), "unpermute");
+    return STAGE_OK;
+}
+
+}  // namespace stage

@@ -1,0 +1,33 @@
+// dist.hpp -- hash-sharded multi-GPU probe front-end (one process per GPU, RCCL over xGMI).
+#pragma once
+#include <hip/hip_runtime_api.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "kernel_api.hpp"
+#include "stage_core.hpp"
+
+namespace stage {
+
+struct ShardComm {
+    void *comm = nullptr;  // ncclComm_t
+    int rank = 0, world = 1;
+    // device scratch (grown on demand)
+    void *dest = nullptr, *cursor = nullptr, *perm = nullptr, *send = nullptr, *recv = nullptr;
+    void *rout = nullptr, *rrec = nullptr, *bout = nullptr, *brec = nullptr, *cnt = nullptr;
+    void *lkeys = nullptr, *lrids = nullptr;
+    uint64_t cap_local = 0, cap_remote = 0;
+    uint32_t rec_stride = 0;
+    ~ShardComm();
+};
+
+int shard_unique_id(uint8_t *id128);
+int shard_init(ShardComm &c, const uint8_t *id128, int rank, int world);
+int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const uint64_t *d_keys,
+                const uint32_t *d_rids, uint64_t n, stage_probe_out_dev *d_out, uint8_t *d_recs, hipStream_t s);
+
+void set_error(const std::string &msg);
+
+}  // namespace stage

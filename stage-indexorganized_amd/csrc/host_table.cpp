@@ -1,0 +1,424 @@
+// host_table.cpp -- reference-exact leaf layout, built in structure-of-arrays form.
+//
+// Leaf contents, slot order, sorted_count and RecordMetadata words follow the reference's
+// single-loader write path:
+//   LeafNode::Insert       src/vstore/b_tree.cpp:809-947   (append in slot order, offsets
+//                                                            grow down from leaf_node_size)
+//   BTree::Insert          src/vstore/b_tree.cpp:1849-2020 (split on NotEnoughSpace, retry)
+//   LeafNode::PrepareForSplit / CopyFrom  b_tree.cpp:1558-1690, 1486-1545
+//   FinalizeForInsert      include/vstore/record_meta.h:128-137
+// The inner levels are not materialised: a leaf's key range is (previous separator,
+// own separator], which is exactly what InternalNode::GetChildIndex resolves to
+// (b_tree.cpp:664-702: an equal key goes to the left child with le_child, right without).
+#include "host_table.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <stdexcept>
+
+namespace stage {
+
+static uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+void gen_payload(uint64_t rowid, int mode, uint8_t *dst, uint32_t payload_size) {
+    if (mode == 0) {  // memset(tuple.cols[i], rowid, ...)  (ycsb_loader.cpp:149-150)
+        std::memset(dst, (int)(rowid & 0xFF), payload_size);
+        return;
+    }
+    for (uint32_t j = 0; j * 8 < payload_size; j++) {
+        uint64_t w = splitmix64((rowid << 8) ^ j);
+        uint32_t nb = std::min<uint32_t>(8, payload_size - j * 8);
+        std::memcpy(dst + j * 8, &w, nb);
+    }
+}
+
+static uint64_t key_mask(uint32_t len) { return len >= 8 ? ~0ull : ((1ull << (8 * len)) - 1); }
+
+HostTable::HostTable(const stage_params &p) : p_(p) {
+    if (p.payload_size == 0 || p.leaf_node_size < 256 || p.key_width > 8)
+        throw std::invalid_argument("bad table parameters");
+    const uint32_t rec = 8 + p.payload_size;  // keys are at most 8 bytes -> padded to 8
+    // largest record count c with 40 + c*(24+rec) < leaf_node_size (the Insert space check)
+    const uint32_t room = p.leaf_node_size - 40;
+    max_records_ = (room + (24 + rec) - 1) / (24 + rec) - 1;
+    if (max_records_ < 3) throw std::invalid_argument("leaf holds fewer than 3 records");
+    if (max_records_ <= 64) cap_ = 64;
+    else if (max_records_ <= 128) cap_ = 128;
+    else throw std::invalid_argument("more than 128 records per leaf is not supported");
+    stride_ = (8 + p.payload_size + 15) & ~15u;
+    buckets_.resize(1u << 16);
+    uint32_t root = alloc_leaf();
+    head_ = (int32_t)root;
+    for (auto &b : buckets_) b.push_back(RouteEntry{~0ull, root, kInfLen});
+}
+
+uint32_t HostTable::alloc_leaf() {
+    uint32_t id;
+    if (!free_leaves_.empty()) {
+        id = free_leaves_.back();
+        free_leaves_.pop_back();
+        leaves_[id] = Leaf();
+    } else {
+        id = (uint32_t)leaves_.size();
+        leaves_.emplace_back();
+        size_t n = (size_t)leaves_.size() * cap_;
+        okey_.resize(n, 0);
+        meta_.resize(n, 0);
+        next_.resize(n, 0);
+        image_.resize(n, 0);
+    }
+    size_t b = (size_t)id * cap_;
+    std::fill(okey_.begin() + b, okey_.begin() + b + cap_, 0);
+    std::fill(meta_.begin() + b, meta_.begin() + b + cap_, 0);
+    std::fill(next_.begin() + b, next_.begin() + b + cap_, 0);
+    std::fill(image_.begin() + b, image_.begin() + b + cap_, 0);
+    leaves_[id].live = true;
+    nleaves_live_++;
+    return id;
+}
+
+uint32_t HostTable::route(const Key &k, bool le_child) const {
+    for (uint32_t b = bucket_of(k.okey); b < buckets_.size(); ++b) {
+        const auto &v = buckets_[b];
+        auto it = le_child ? std::lower_bound(v.begin(), v.end(), k, entry_lt_key)
+                           : std::upper_bound(v.begin(), v.end(), k, [](const Key &kk, const RouteEntry &e) {
+                                 return kk.okey < e.sep_okey || (kk.okey == e.sep_okey && kk.len < e.sep_len);
+                             });
+        if (it != v.end()) return it->leaf;
+    }
+    return buckets_.back().back().leaf;  // the +inf leaf
+}
+
+// First visible slot holding k.  Equivalent to BaseNode::SearchRecordMeta with
+// check_concurrency (b_tree.cpp:61-121): the sorted pass and the unsorted pass both accept
+// only visible slots whose key bytes and key size equal the probe, first in slot order.
+int64_t HostTable::search(uint32_t leaf, const Key &k) const {
+    const Leaf &L = leaves_[leaf];
+    const size_t b = (size_t)leaf * cap_;
+    const uint64_t *ok = okey_.data() + b;
+    for (uint32_t s = 0; s < L.count; ++s) {
+        if (ok[s] != k.okey) continue;
+        uint64_t m = meta_[b + s];
+        if (meta_visible(m) && meta_keylen(m) == k.len) return s;
+    }
+    return -1;
+}
+
+uint32_t HostTable::new_image(uint64_t key_le, const uint8_t *payload, uint64_t gen_rowid, int mode) {
+    ImageDesc d;
+    d.key_le = key_le;
+    d.mode = (uint32_t)mode;
+    if (payload) {
+        d.kind = 1;
+        d.arg = arena_.size();
+        arena_.insert(arena_.end(), payload, payload + p_.payload_size);
+    } else {
+        d.kind = 0;
+        d.arg = gen_rowid;
+    }
+    images_.push_back(d);
+    if (images_.size() > kNextIndexMask) throw std::runtime_error("record heap index overflow");
+    return (uint32_t)(images_.size() - 1);
+}
+
+void HostTable::image_payload(uint32_t img, uint8_t *dst) const {
+    const ImageDesc &d = images_[img];
+    if (d.kind == 0) gen_payload(d.arg, (int)d.mode, dst, p_.payload_size);
+    else std::memcpy(dst, arena_.data() + d.arg, p_.payload_size);
+}
+
+int HostTable::insert(uint64_t key_le, uint32_t len, const uint8_t *payload, uint64_t gen_rowid, int mode,
+                      uint32_t commit_id) {
+    if (len == 0 || len > 8) return STAGE_RC_INVALID;
+    if (p_.key_width && len != p_.key_width) return STAGE_RC_INVALID;
+    key_le &= key_mask(len);
+    const Key k{order_key(key_le, len), len};
+    const uint32_t rec = pad8(len) + p_.payload_size;
+    for (int guard = 0; guard < 64; ++guard) {
+        uint32_t leaf = route(k, true);
+        int64_t hit = search(leaf, k);  // CheckUnique (b_tree.cpp:1395-1417)
+        if (hit >= 0) {
+            if (meta_inserting(meta_[(size_t)leaf * cap_ + hit])) return STAGE_RC_INVALID;  // ReCheck path
+            return STAGE_RC_KEY_EXISTS;
+        }
+        Leaf &L = leaves_[leaf];
+        if (used_space(L) + 24u + rec >= p_.leaf_node_size) {  // NotEnoughSpace (b_tree.cpp:829-836)
+            if (!split(leaf)) return STAGE_RC_RETRY_FAILURE;
+            continue;
+        }
+        const uint32_t slot = L.count++;
+        L.block += rec;
+        const uint64_t offset = p_.leaf_node_size - L.block;
+        const size_t i = (size_t)leaf * cap_ + slot;
+        okey_[i] = k.okey;
+        // PrepareForInsert then FinalizeInsert: control bit cleared, cstamp = commit_id
+        meta_[i] = ((uint64_t)len << 48) | kMetaVisible | (offset << 32) | commit_id;
+        next_[i] = 0;
+        image_[i] = new_image(key_le, payload, gen_rowid, mode);
+        layout_dirty_ = true;
+        return STAGE_RC_OK;
+    }
+    return STAGE_RC_RETRY_FAILURE;
+}
+
+bool HostTable::split(uint32_t p) {
+    if (leaves_[p].count < 3) return false;
+    struct Rec {
+        uint64_t okey, meta;
+        uint32_t next, image;
+    };
+    const size_t pb = (size_t)p * cap_;
+    std::vector<Rec> v;
+    v.reserve(leaves_[p].count);
+    uint32_t total = 0;
+    for (uint32_t s = 0; s < leaves_[p].count; ++s) {
+        uint64_t m = meta_[pb + s];
+        if (m == 0) continue;
+        if (meta_visible(m) && meta_keylen(m) > 0) {
+            v.push_back(Rec{okey_[pb + s], m, next_[pb + s], image_[pb + s]});
+            total += pad8(meta_keylen(m)) + p_.payload_size;
+        }
+    }
+    if (total == 0) return false;
+    std::sort(v.begin(), v.end(), [](const Rec &a, const Rec &b) {
+        return a.okey < b.okey || (a.okey == b.okey && meta_keylen(a.meta) < meta_keylen(b.meta));
+    });
+    int32_t left_size = (int32_t)(total / 2);
+    uint32_t nleft = 0;
+    for (size_t i = 0; i < v.size(); ++i) {
+        ++nleft;
+        left_size -= (int32_t)(pad8(meta_keylen(v[i].meta)) + p_.payload_size);
+        if (left_size <= 0) break;
+    }
+    const Key sep{v[nleft - 1].okey, meta_keylen(v[nleft - 1].meta)};
+    const Key hi = leaves_[p].sep;
+    const Key lo = leaves_[p].prev >= 0 ? leaves_[leaves_[p].prev].sep : Key{0, 0};
+    const bool lo_inf = leaves_[p].prev < 0;
+
+    const uint32_t r = alloc_leaf();  // may reallocate the arrays
+    auto fill = [&](uint32_t leaf, size_t from, size_t to) {
+        Leaf &L = leaves_[leaf];
+        const size_t b = (size_t)leaf * cap_;
+        uint32_t offset = p_.leaf_node_size, n = 0;
+        for (size_t i = from; i < to; ++i) {
+            const uint32_t kl = meta_keylen(v[i].meta);
+            offset -= pad8(kl) + p_.payload_size;
+            okey_[b + n] = v[i].okey;
+            meta_[b + n] = ((uint64_t)kl << 48) | kMetaVisible | ((uint64_t)offset << 32) | meta_cstamp(v[i].meta);
+            next_[b + n] = v[i].next;
+            image_[b + n] = v[i].image;
+            ++n;
+        }
+        for (uint32_t s = n; s < cap_; ++s) {
+            okey_[b + s] = 0;
+            meta_[b + s] = 0;
+            next_[b + s] = 0;
+            image_[b + s] = 0;
+        }
+        L.count = L.sorted = n;
+        L.block = p_.leaf_node_size - offset;
+        L.deleted = 0;
+    };
+    fill(p, 0, nleft);
+    fill(r, nleft, v.size());
+    Leaf &P = leaves_[p];
+    Leaf &R = leaves_[r];
+    R.sep = hi;
+    P.sep = sep;
+    R.prev = (int32_t)p;
+    R.next = P.next;
+    if (P.next >= 0) leaves_[P.next].prev = (int32_t)r;
+    P.next = (int32_t)r;
+    route_split(p, r, lo_inf ? Key{0, 0} : lo, sep, hi);
+    layout_dirty_ = true;
+    return true;
+}
+
+void HostTable::route_split(uint32_t p, uint32_t r, const Key &lo, const Key &s, const Key &hi) {
+    const uint32_t b_lo = bucket_of(lo.okey);
+    const uint32_t b_hi = key_is_inf(hi) ? (uint32_t)buckets_.size() - 1 : bucket_of(hi.okey);
+    const uint32_t b_s = bucket_of(s.okey);
+    for (uint32_t b = b_lo; b <= b_hi; ++b) {
+        auto &v = buckets_[b];
+        auto it = std::lower_bound(v.begin(), v.end(), hi, entry_lt_key);
+        while (it != v.end() && it->leaf != p) ++it;
+        if (it == v.end()) continue;  // p does not reach this bucket
+        if (b < b_s) {
+            it->sep_okey = s.okey;
+            it->sep_len = s.len;
+        } else if (b > b_s) {
+            it->leaf = r;
+        } else {
+            it->leaf = r;
+            v.insert(it, RouteEntry{s.okey, p, s.len});
+        }
+    }
+}
+
+uint64_t HostTable::load_ycsb(uint64_t begin, uint64_t end, uint32_t key_size, int mode) {
+    if (end > begin) images_.reserve(images_.size() + (end - begin));
+    uint64_t ok = 0;
+    for (uint64_t rowid = begin; rowid < end; ++rowid)
+        if (insert(rowid & key_mask(key_size), key_size, nullptr, rowid, mode, kInvalidCid) == STAGE_RC_OK) ++ok;
+    return ok;
+}
+
+uint64_t HostTable::load_keys(const uint64_t *keys, uint64_t n, uint32_t key_size, int mode) {
+    images_.reserve(images_.size() + n);
+    uint64_t ok = 0;
+    for (uint64_t i = 0; i < n; ++i)
+        if (insert(keys[i] & key_mask(key_size), key_size, nullptr, keys[i], mode, kInvalidCid) == STAGE_RC_OK) ++ok;
+    return ok;
+}
+
+int HostTable::find(uint64_t key_le, uint32_t len, uint32_t *leaf, uint32_t *slot) const {
+    if (len == 0 || len > 8) return -1;
+    key_le &= key_mask(len);
+    const Key k{order_key(key_le, len), len};
+    uint32_t lf = route(k, true);
+    int64_t s = search(lf, k);
+    if (s < 0) return -1;
+    *leaf = lf;
+    *slot = (uint32_t)s;
+    return 0;
+}
+
+// LeafNode::Update, b_tree.cpp:1061-1163 (is_for_update == false): the old image becomes the
+// overwrite copy (its image row is immutable), the record gets a new patched image.
+int HostTable::update(uint64_t key_le, uint32_t len, uint32_t payload_off, const uint8_t *delta, uint32_t delta_len,
+                      uint32_t writer_id) {
+    uint32_t leaf, slot;
+    if (find(key_le, len, &leaf, &slot) < 0) return STAGE_RC_NOT_FOUND;
+    const size_t i = (size_t)leaf * cap_ + slot;
+    const uint64_t m = meta_[i];
+    if (meta_inserting(m)) return STAGE_RC_DIRTY;
+    if ((uint64_t)payload_off + delta_len > p_.payload_size) return STAGE_RC_INVALID;
+    std::vector<uint8_t> pay(p_.payload_size);
+    image_payload(image_[i], pay.data());
+    if (std::memcmp(pay.data() + payload_off, delta, delta_len) == 0) return STAGE_RC_NOT_NEEDED_UPDATE;
+    if (meta_cstamp(m) > writer_id) return STAGE_RC_NOT_NEEDED_UPDATE;
+    meta_[i] = m | kMetaControl | kMetaVisible;  // PrepareForUpdate
+    CopyHdr c;
+    c.rstamp = meta_cstamp(m);
+    c.sstamp = kMaxCid;
+    c.next = next_[i];
+    c.image = image_[i];
+    copies_.push_back(c);
+    copy_live_.push_back(1);
+    if (copies_.size() > kNextIndexMask) throw std::runtime_error("copy index overflow");
+    next_[i] = kNextCopy | (uint32_t)(copies_.size() - 1);
+    std::memcpy(pay.data() + payload_off, delta, delta_len);  // CopyPayload
+    image_[i] = new_image(images_[image_[i]].key_le, pay.data(), 0, 0);
+    layout_dirty_ = true;
+    return STAGE_RC_OK;
+}
+
+// CommitTransaction UPDATE entry (transaction_manager.cpp:610-676), single writer.
+int HostTable::commit_update(uint64_t key_le, uint32_t len, uint32_t commit_id, uint32_t sstamp) {
+    uint32_t leaf, slot;
+    if (find(key_le, len, &leaf, &slot) < 0) return STAGE_RC_NOT_FOUND;
+    const size_t i = (size_t)leaf * cap_ + slot;
+    if (!meta_inserting(meta_[i]) || (next_[i] & kNextKindMask) != kNextCopy) return STAGE_RC_NOT_FOUND;
+    CopyHdr &c = copies_[next_[i] & kNextIndexMask];
+    c.sstamp = sstamp;
+    VersionHdr v;
+    v.begin_id = c.rstamp;
+    v.comm_id = c.sstamp;
+    v.next = c.next;
+    v.image = c.image;
+    versions_.push_back(v);
+    if (versions_.size() > kNextIndexMask) throw std::runtime_error("version index overflow");
+    uint64_t m = (meta_[i] & ~kMetaTxn) | commit_id;  // FinalizeForUpdate(t_cstamp)
+    meta_[i] = m & ~kMetaControl;
+    next_[i] = kNextVersion | (uint32_t)(versions_.size() - 1);
+    layout_dirty_ = true;
+    return STAGE_RC_OK;
+}
+
+// BTree::FinalizeUpdate (b_tree.cpp:2252-2268): cstamp := commit_id, next untouched.
+int HostTable::finalize_update(uint64_t key_le, uint32_t len, uint32_t commit_id) {
+    uint32_t leaf, slot;
+    if (find(key_le, len, &leaf, &slot) < 0) return STAGE_RC_NOT_FOUND;
+    const size_t i = (size_t)leaf * cap_ + slot;
+    meta_[i] = ((meta_[i] & ~kMetaTxn) | commit_id) & ~kMetaControl;
+    layout_dirty_ = true;
+    return STAGE_RC_OK;
+}
+
+// LeafNode::Delete (b_tree.cpp:1171-1251) + FinalizeDelete (b_tree.cpp:2275-2310).  Sibling
+// merges (BaseNode::CheckMerge) are not supported: such a delete reports RC_INVALID.
+int HostTable::remove(uint64_t key_le, uint32_t len, uint32_t commit_id) {
+    uint32_t leaf, slot;
+    if (find(key_le, len, &leaf, &slot) < 0) return STAGE_RC_NOT_FOUND;
+    const size_t i = (size_t)leaf * cap_ + slot;
+    const uint64_t m = meta_[i];
+    if (meta_inserting(m)) return STAGE_RC_DIRTY;
+    CopyHdr c;
+    c.rstamp = meta_cstamp(m);
+    c.sstamp = kMaxCid;
+    c.next = next_[i];
+    c.image = image_[i];
+    copies_.push_back(c);
+    copy_live_.push_back(1);
+    next_[i] = kNextCopy | (uint32_t)(copies_.size() - 1);
+    meta_[i] = 0;
+    Leaf &L = leaves_[leaf];
+    L.deleted += pad8(meta_keylen(m)) + p_.payload_size;
+    layout_dirty_ = true;
+    (void)commit_id;
+    if (nleaves_live_ > 1 && used_space(L) - L.deleted <= p_.merge_threshold) return STAGE_RC_INVALID;
+    return STAGE_RC_OK;
+}
+
+void HostTable::key_order(std::vector<uint32_t> &order) const {
+    order.clear();
+    order.reserve(nleaves_live_);
+    for (int32_t l = head_; l >= 0; l = leaves_[l].next) order.push_back((uint32_t)l);
+}
+
+void HostTable::stats(uint64_t *out) const {
+    for (int i = 0; i < 8; ++i) out[i] = 0;
+    std::vector<uint32_t> order;
+    key_order(order);
+    out[2] = order.size();
+    for (uint32_t l : order) {
+        const Leaf &L = leaves_[l];
+        for (uint32_t s = 0; s < L.count; ++s)
+            if (meta_visible(meta_[(size_t)l * cap_ + s])) {
+                out[3]++;
+                if (s < L.sorted) out[4]++;
+                else out[5]++;
+            }
+        out[6] = std::max<uint64_t>(out[6], L.count);
+    }
+    out[7] = versions_.size();
+}
+
+int64_t HostTable::export_leaves(uint32_t cap, uint64_t max_leaves, uint32_t *rc, uint32_t *sc, uint64_t *meta,
+                                 uint64_t *keyw) const {
+    std::vector<uint32_t> order;
+    key_order(order);
+    if (order.size() > max_leaves) return -(int64_t)order.size();
+    for (size_t d = 0; d < order.size(); ++d) {
+        const Leaf &L = leaves_[order[d]];
+        rc[d] = L.count;
+        sc[d] = L.sorted;
+        for (uint32_t s = 0; s < cap; ++s) {
+            uint64_t m = 0, kw = 0;
+            if (s < L.count && s < cap_) {
+                m = meta_[(size_t)order[d] * cap_ + s];
+                if (m) kw = key_bytes_from_order(okey_[(size_t)order[d] * cap_ + s], meta_keylen(m));
+            }
+            meta[d * cap + s] = m;
+            keyw[d * cap + s] = kw;
+        }
+    }
+    return (int64_t)order.size();
+}
+
+}  // namespace stage

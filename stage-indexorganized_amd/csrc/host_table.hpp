@@ -1,0 +1,121 @@
+// host_table.hpp -- the host side of one index-organized table.
+//
+// Keeps the reference's leaf layout (which records live in which leaf, in which slot, the
+// sorted/unsorted split, the RecordMetadata words) exactly as the reference's single-loader
+// write path would produce it, but in structure-of-arrays form with no payload bytes:
+// payloads live in the device record heap and are produced there from their sources.
+// Inner-node traversal is replaced on the host by a bucketed separator router (same leaf for
+// every key as BTree::TraverseToLeaf) and on the device by an implicit separator tree.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "stage_core.hpp"
+#include "../../include/stage_hip.h"
+
+namespace stage {
+
+struct Key {
+    uint64_t okey;
+    uint32_t len;
+};
+inline bool key_lt(const Key &a, const Key &b) { return a.okey < b.okey || (a.okey == b.okey && a.len < b.len); }
+inline bool key_eq(const Key &a, const Key &b) { return a.okey == b.okey && a.len == b.len; }
+inline bool key_le(const Key &a, const Key &b) { return !key_lt(b, a); }
+constexpr uint32_t kInfLen = 0xFFFF;
+inline Key key_inf() { return Key{~0ull, kInfLen}; }
+inline bool key_is_inf(const Key &k) { return k.len == kInfLen; }
+
+// Source of one record-heap image: generated from a rowid, or explicit bytes in the arena.
+struct ImageDesc {
+    uint64_t key_le;  // key bytes (little-endian, zero above key_len)
+    uint64_t arg;     // rowid (generated) or arena byte offset (explicit)
+    uint32_t kind;    // 0 = generated, 1 = arena
+    uint32_t mode;    // payload generator mode (generated images)
+};
+
+class HostTable {
+public:
+    explicit HostTable(const stage_params &p);
+
+    const stage_params &params() const { return p_; }
+    uint32_t cap() const { return cap_; }
+    uint32_t stride() const { return stride_; }
+
+    // write path, reference ReturnCode values
+    int insert(uint64_t key_le, uint32_t len, const uint8_t *payload, uint64_t gen_rowid, int mode,
+               uint32_t commit_id);
+    uint64_t load_ycsb(uint64_t begin, uint64_t end, uint32_t key_size, int mode);
+    uint64_t load_keys(const uint64_t *keys, uint64_t n, uint32_t key_size, int mode);
+    int update(uint64_t key_le, uint32_t len, uint32_t payload_off, const uint8_t *delta, uint32_t delta_len,
+               uint32_t writer_id);
+    int commit_update(uint64_t key_le, uint32_t len, uint32_t commit_id, uint32_t sstamp);
+    int finalize_update(uint64_t key_le, uint32_t len, uint32_t commit_id);
+    int remove(uint64_t key_le, uint32_t len, uint32_t commit_id);
+
+    // host traversal (TraverseToLeaf equivalent) -> host leaf id
+    uint32_t route(const Key &k, bool le_child) const;
+
+    void stats(uint64_t *out) const;
+    // leaves in key order
+    void key_order(std::vector<uint32_t> &order) const;
+    int64_t export_leaves(uint32_t cap, uint64_t max_leaves, uint32_t *rc, uint32_t *sc, uint64_t *meta,
+                          uint64_t *keyw) const;
+
+    // storage (read by the device-image builder)
+    struct Leaf {
+        uint32_t count = 0, sorted = 0, block = 0, deleted = 0;
+        int32_t prev = -1, next = -1;   // key-order neighbours
+        Key sep = key_inf();            // inclusive upper bound of the leaf's key range
+        bool live = false;
+    };
+    std::vector<Leaf> leaves_;
+    std::vector<uint64_t> okey_;   // [leaf*cap + slot]
+    std::vector<uint64_t> meta_;
+    std::vector<uint32_t> next_;
+    std::vector<uint32_t> image_;
+    int32_t head_ = 0;
+    uint32_t nleaves_live_ = 0;
+
+    std::vector<ImageDesc> images_;
+    std::vector<uint8_t> arena_;
+    std::vector<CopyHdr> copies_;
+    std::vector<uint8_t> copy_live_;
+    std::vector<VersionHdr> versions_;
+    uint64_t images_synced_ = 0;     // images already present on the device
+    uint64_t arena_synced_ = 0;
+    bool layout_dirty_ = true;
+
+private:
+    struct RouteEntry {
+        uint64_t sep_okey;
+        uint32_t leaf;
+        uint32_t sep_len;
+    };
+    static uint32_t bucket_of(uint64_t okey) { return (uint32_t)(okey >> 48); }
+    static bool entry_lt_key(const RouteEntry &e, const Key &k) {
+        return e.sep_okey < k.okey || (e.sep_okey == k.okey && e.sep_len < k.len);
+    }
+
+    uint32_t alloc_leaf();
+    int64_t search(uint32_t leaf, const Key &k) const;  // SearchRecordMeta (check_concurrency)
+    uint32_t used_space(const Leaf &l) const { return 40u + l.block + l.count * 24u; }
+    bool split(uint32_t leaf);
+    void route_split(uint32_t p, uint32_t r, const Key &lo, const Key &s, const Key &hi);
+    uint32_t new_image(uint64_t key_le, const uint8_t *payload, uint64_t gen_rowid, int mode);
+    void image_payload(uint32_t img, uint8_t *dst) const;
+    int find(uint64_t key_le, uint32_t len, uint32_t *leaf, uint32_t *slot) const;
+
+    stage_params p_;
+    uint32_t cap_ = 64;
+    uint32_t stride_ = 1008;
+    uint32_t max_records_ = 63;
+    std::vector<std::vector<RouteEntry>> buckets_;
+    std::vector<uint32_t> free_leaves_;
+};
+
+// payload generator (data only; same definition as the test oracle's)
+void gen_payload(uint64_t rowid, int mode, uint8_t *dst, uint32_t payload_size);
+
+}  // namespace stage

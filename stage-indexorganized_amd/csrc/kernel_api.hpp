@@ -1,0 +1,42 @@
+// kernel_api.hpp -- launchers of the gfx950 kernels (kernels.hip), called by the host side.
+#pragma once
+#include <hip/hip_runtime_api.h>
+
+#include <cstdint>
+
+#include "stage_core.hpp"
+
+namespace stage {
+
+// same bytes as stage_probe_out (include/stage_hip.h)
+struct alignas(16) stage_probe_out_dev {
+    uint32_t w[8];
+};
+
+// device copy of ImageDesc (host_table.hpp)
+struct alignas(8) ImageDescDev {
+    uint64_t key_le;
+    uint64_t arg;
+    uint32_t kind;
+    uint32_t mode;
+};
+
+struct ProbeTuning {
+    int group = 4;       // probes per wave in flight
+    int max_blocks = 0;  // 0 = default grid cap
+};
+
+hipError_t launch_resolve(const DevTable &t, const uint64_t *keys, const uint16_t *lens, uint64_t n, int le_child,
+                          uint32_t *out, hipStream_t s);
+hipError_t launch_probe(const DevTable &t, const uint64_t *keys, const uint16_t *lens, const uint32_t *rids,
+                        const uint32_t *leaf_in, uint64_t n, stage_probe_out_dev *out, uint8_t *recs, hipStream_t s,
+                        const ProbeTuning &tune);
+hipError_t launch_scan(const DevTable &t, const uint64_t *keys, const uint16_t *lens, uint64_t n, uint32_t scan_size,
+                       uint32_t *counts, uint8_t *recs, hipStream_t s);
+hipError_t launch_murmur(const void *keys, uint32_t key_len, uint32_t key_stride, uint64_t seed, uint64_t n,
+                         uint64_t *out, hipStream_t s);
+hipError_t launch_fill(uint8_t *heap, uint32_t stride, uint32_t payload_size, const ImageDescDev *descs,
+                       const uint8_t *arena, uint64_t first, uint64_t count, uint64_t ident_rowid0,
+                       uint32_t ident_key_width, int ident_mode, hipStream_t s);
+
+}  // namespace stage

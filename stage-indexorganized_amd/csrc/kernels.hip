@@ -1,0 +1,643 @@
+// kernels.hip -- gfx950 (CDNA4, wave64) kernels of the index-organized read path.
+//
+// Integer/pointer work only (no MFMA).  Mapping:
+//   * leaf resolve: lane-per-probe descent of the implicit 8-ary separator tree (one 64-B
+//     node per level = 4 x 16-B loads per lane), replaces InternalNode::GetChildIndex
+//     (b_tree.cpp:664-702) / BTree::TraverseToLeaf (b_tree.cpp:1804-1846).
+//   * leaf probe: wave-per-probe.  64 lanes read the leaf's key column (one coalesced 512-B
+//     read) and a scalar visible-slot mask; __ballot + ffs gives the first visible slot
+//     holding the key in slot order -- BaseNode::SearchRecordMeta (b_tree.cpp:18-122).
+//   * visibility: wave-uniform scalar walk (BTree::Read copy path b_tree.cpp:2087-2123,
+//     IndexScanExecutor executor.h:383-450).
+//   * tuple copy: 63 lanes x 16 B = the 1008-B [key|payload] row (Record::New b_tree.h:407-428).
+//   * range scan: ballot + mbcnt prefix counts give RangeScanBySize's slot-order truncation
+//     (b_tree.cpp:1276-1302), an in-wave rank sort replaces std::sort, continuation as
+//     Iterator::GetNext (b_tree.h:899-941).
+#include <hip/hip_runtime.h>
+
+#include "kernel_api.hpp"
+#include "stage_core.hpp"
+
+namespace stage {
+
+__device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+__device__ __forceinline__ uint32_t rl32(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+__device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
+    return ((uint64_t)rl32((uint32_t)(v >> 32), l) << 32) | rl32((uint32_t)v, l);
+}
+__device__ __forceinline__ uint32_t uni32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+    return ((uint64_t)uni32((uint32_t)(v >> 32)) << 32) | uni32((uint32_t)v);
+}
+// popcount of mask bits below this lane
+__device__ __forceinline__ uint32_t count_below(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+struct KeyV {
+    uint64_t okey;
+    uint32_t len;
+};
+__device__ __forceinline__ bool kv_lt(uint64_t ao, uint32_t al, uint64_t bo, uint32_t bl) {
+    return ao < bo || (ao == bo && al < bl);
+}
+
+// lower_bound over the separators: number of separators < x, i.e. the leaf whose range
+// (sep[i-1], sep[i]] holds x (le_child semantics).  Upper-bound callers pass succ(x).
+template <bool VARLEN>
+__device__ __forceinline__ uint32_t tree_lower_bound(const DevTable &t, uint64_t x, uint32_t xl) {
+    uint32_t node = 0;
+    for (int lvl = (int)t.levels - 1; lvl >= 0; --lvl) {
+        const uint64_t *e = t.tree + t.level_off[lvl] + (uint64_t)node * kTreeFanout;
+        const ulonglong2 *e2 = reinterpret_cast<const ulonglong2 *>(e);
+        ulonglong2 a = e2[0], b = e2[1], c = e2[2], d = e2[3];
+        uint64_t v[8] = {a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y};
+        uint32_t cnt = 0;
+        if (VARLEN) {
+            const uint8_t *ln = t.tree_len + t.level_off[lvl] + (uint64_t)node * kTreeFanout;
+            uint64_t lw = *reinterpret_cast<const uint64_t *>(ln);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) cnt += kv_lt(v[i], (uint32_t)((lw >> (8 * i)) & 0xFF), x, xl) ? 1u : 0u;
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) cnt += (v[i] < x) ? 1u : 0u;
+        }
+        node = node * kTreeFanout + cnt;
+    }
+    return node < t.nseps ? node : t.nseps;
+}
+
+template <bool VARLEN>
+__device__ __forceinline__ uint32_t resolve_leaf(const DevTable &t, uint64_t okey, uint32_t len, bool le_child) {
+    if (le_child) return tree_lower_bound<VARLEN>(t, okey, len);
+    if (VARLEN) return tree_lower_bound<VARLEN>(t, okey, len + 1);  // (okey, len+1) = succ
+    if (okey == ~0ull) return t.nseps;
+    return tree_lower_bound<VARLEN>(t, okey + 1, len);
+}
+
+__global__ __launch_bounds__(256) void resolve_kernel(DevTable t, const uint64_t *__restrict__ keys,
+                                                      const uint16_t *__restrict__ lens, uint64_t n, int le_child,
+                                                      uint32_t *__restrict__ out) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t len = t.key_width ? t.key_width : (lens ? lens[i] : 8u);
+    uint64_t ok = order_key(keys[i], len);
+    out[i] = t.key_width ? resolve_leaf<false>(t, ok, len, le_child != 0)
+                         : resolve_leaf<true>(t, ok, len, le_child != 0);
+}
+
+// ----------------------------------------------------------------------------------------
+// point probe
+
+struct ProbeRes {
+    uint32_t status, flags, hops, slot, key_len, cstamp, rec_cstamp, copy_sstamp, image;
+};
+
+// first visible slot of `leaf` holding (x, xl) in slot order, or -1
+template <bool VARLEN, int SPL>
+__device__ __forceinline__ int find_slot(const DevTable &t, uint32_t leaf, uint64_t x, uint32_t xl, uint32_t lane) {
+    const uint64_t base = (uint64_t)leaf * t.cap;
+    uint64_t col[SPL];
+#pragma unroll
+    for (int s = 0; s < SPL; ++s) col[s] = t.okey[base + s * 64 + lane];
+#pragma unroll
+    for (int s = 0; s < SPL; ++s) {
+        uint64_t vm = t.vis[(uint64_t)leaf * SPL + s];
+        uint64_t hit = ballot(col[s] == x) & vm;
+        if (VARLEN) {
+            while (hit) {  // candidates with the same order key: check the key length
+                int b = __builtin_ctzll(hit);
+                hit &= hit - 1;
+                uint64_t m = t.slot[base + s * 64 + b].meta;
+                if (meta_keylen(m) == xl) return s * 64 + b;
+            }
+        } else if (hit) {
+            return s * 64 + __builtin_ctzll(hit);
+        }
+    }
+    return -1;
+}
+
+// BTree::Read + IndexScanExecutor visibility for one wave-uniform probe
+__device__ __forceinline__ void visibility(const DevTable &t, uint32_t leaf, int slot, uint32_t rid, ProbeRes &r) {
+    r.flags = 0;
+    r.hops = 0;
+    r.copy_sstamp = kMaxCid;
+    r.image = 0xFFFFFFFFu;
+    r.cstamp = 0;
+    r.rec_cstamp = 0;
+    r.key_len = 0;
+    r.slot = 0xFFFF;
+    if (slot < 0) {
+        r.status = ST_NOT_FOUND;
+        return;
+    }
+    r.slot = (uint32_t)slot;
+    const SlotInfo si = t.slot[(uint64_t)leaf * t.cap + slot];
+    const uint64_t m = si.meta;
+    r.rec_cstamp = meta_cstamp(m);
+    r.key_len = meta_keylen(m);
+    CopyHdr c = {0, kMaxCid, 0, 0};
+    const bool has_copy = (si.next & kNextKindMask) == kNextCopy;
+    if (has_copy) {  // PerformRead: GetOversionHeader(meta.next_ptr) != nullptr
+        c = t.chdr[si.next & kNextIndexMask];
+        r.flags |= 1u;
+        r.copy_sstamp = c.sstamp;
+    }
+    uint32_t img, chain;
+    bool from_copy = false;
+    if (meta_inserting(m)) {
+        if (!has_copy) {  // copy location 0 / header gone: Read returns nullptr
+            r.status = ST_NOT_FOUND;
+            return;
+        }
+        img = c.image;
+        r.cstamp = c.rstamp;
+        chain = c.next;
+        from_copy = true;
+    } else {
+        img = si.image;
+        r.cstamp = rid;
+        chain = si.next;
+    }
+    if (rid >= r.rec_cstamp) {
+        r.status = from_copy ? ST_COPY : ST_LATEST;
+        r.image = img;
+        return;
+    }
+    // older snapshot: TupleHeader chain (executor.h:407-449)
+    if ((chain & kNextKindMask) != kNextVersion) {
+        r.status = ST_CHAIN_MISS;
+        return;
+    }
+    for (uint32_t guard = 0; guard < (1u << 24); ++guard) {
+        const VersionHdr v = t.vhdr[chain & kNextIndexMask];
+        r.hops++;
+        if (v.begin_id == kInvalidCid || v.comm_id == kInvalidCid) {
+            r.status = ST_FAIL_INVALID_TS;
+            return;
+        }
+        if (rid >= v.begin_id && rid <= v.comm_id) {
+            r.status = ST_OLD;
+            r.cstamp = v.begin_id;
+            r.image = v.image;
+            return;
+        }
+        if ((v.next & kNextKindMask) != kNextVersion) break;
+        chain = v.next;
+    }
+    r.status = ST_CHAIN_MISS;
+}
+
+__device__ __forceinline__ void copy_row(const DevTable &t, uint32_t img, uint8_t *dst, uint32_t lane) {
+    const uint32_t chunks = t.stride >> 4;
+    const uint4 *src = reinterpret_cast<const uint4 *>(t.heap + (uint64_t)img * t.stride);
+    uint4 *d = reinterpret_cast<uint4 *>(dst);
+    for (uint32_t c = lane; c < chunks; c += 64) {
+        uint4 v = img == 0xFFFFFFFFu ? make_uint4(0, 0, 0, 0) : src[c];
+        d[c] = v;
+    }
+}
+
+__device__ __forceinline__ void store_out(stage_probe_out_dev *out, uint32_t leaf, const ProbeRes &r) {
+    uint4 a, b;
+    a.x = (r.status & 0xFF) | ((r.flags & 0xFF) << 8) | ((r.hops > 0xFFFF ? 0xFFFF : r.hops) << 16);
+    a.y = leaf;
+    a.z = (r.slot & 0xFFFF) | (r.key_len << 16);
+    a.w = r.cstamp;
+    b.x = r.rec_cstamp;
+    b.y = r.copy_sstamp;
+    b.z = r.image;
+    b.w = 0;
+    uint4 *o = reinterpret_cast<uint4 *>(out);
+    o[0] = a;
+    o[1] = b;
+}
+
+// G probes per wave in flight: the G key-column loads, then the G slot-word loads, then the
+// G tuple loads are issued back to back, so each wave keeps G independent misses in flight.
+template <bool VARLEN, int SPL, int G>
+__global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *__restrict__ keys,
+                                                    const uint16_t *__restrict__ lens,
+                                                    const uint32_t *__restrict__ rids,
+                                                    const uint32_t *__restrict__ leaf_in, uint64_t n,
+                                                    stage_probe_out_dev *__restrict__ out,
+                                                    uint8_t *__restrict__ recs) {
+    const uint32_t lane = lane_id();
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint32_t chunks = t.stride >> 4;
+    for (uint64_t base = wave * 64; base < n; base += nwaves * 64) {
+        const uint64_t i = base + lane;
+        const bool valid = i < n;
+        const uint64_t kle = valid ? keys[i] : 0;
+        const uint32_t len = t.key_width ? t.key_width : (lens && valid ? (uint32_t)lens[i] : 8u);
+        const uint32_t rid = rids ? (valid ? rids[i] : 0u) : 0xFFFFFFFEu;
+        const uint64_t ok = order_key(kle, len);
+        uint32_t leaf = 0;
+        if (valid) leaf = leaf_in ? leaf_in[i] : resolve_leaf<VARLEN>(t, ok, len, true);
+        if (leaf > t.nseps) leaf = t.nseps;  // host-supplied ids are clamped to the table
+        const int cnt = (int)((n - base) < 64 ? (n - base) : 64);
+        for (int j0 = 0; j0 < cnt; j0 += G) {
+            uint32_t lf[G], rd[G];
+            int slot[G];
+            ProbeRes r[G];
+            if (VARLEN) {
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    const int j = j0 + g < cnt ? j0 + g : cnt - 1;
+                    lf[g] = rl32(leaf, j);
+                    rd[g] = rl32(rid, j);
+                    slot[g] = find_slot<VARLEN, SPL>(t, lf[g], rl64(ok, j), rl32(len, j), lane);
+                }
+#pragma unroll
+                for (int g = 0; g < G; ++g) visibility(t, lf[g], slot[g], rd[g], r[g]);
+            } else {
+                // phase 1: key columns and visible masks of G leaves
+                uint64_t x[G], col[G][SPL], vm[G][SPL];
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    const int j = j0 + g < cnt ? j0 + g : cnt - 1;
+                    lf[g] = rl32(leaf, j);
+                    rd[g] = rl32(rid, j);
+                    x[g] = rl64(ok, j);
+                    const uint64_t b = (uint64_t)lf[g] * t.cap;
+#pragma unroll
+                    for (int s = 0; s < SPL; ++s) {
+                        col[g][s] = t.okey[b + s * 64 + lane];
+                        vm[g][s] = t.vis[(uint64_t)lf[g] * SPL + s];
+                    }
+                }
+                // phase 2: first visible slot holding the key (ballot, slot order)
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    slot[g] = -1;
+#pragma unroll
+                    for (int s = SPL - 1; s >= 0; --s) {
+                        const uint64_t hit = ballot(col[g][s] == x[g]) & vm[g][s];
+                        if (hit) slot[g] = s * 64 + __builtin_ctzll(hit);
+                    }
+                }
+                // phase 3: slot words of the G hits (scalar loads)
+                SlotInfo si[G];
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    const uint64_t idx = (uint64_t)lf[g] * t.cap + (slot[g] < 0 ? 0 : slot[g]);
+                    si[g] = t.slot[idx];
+                }
+                // phase 4: the latest-version fast path, everything else through visibility()
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    const uint64_t m = si[g].meta;
+                    const bool fast = slot[g] >= 0 && !meta_inserting(m) && rd[g] >= meta_cstamp(m) &&
+                                      (si[g].next & kNextKindMask) != kNextCopy;
+                    if (fast) {
+                        r[g].status = ST_LATEST;
+                        r[g].flags = 0;
+                        r[g].hops = 0;
+                        r[g].slot = (uint32_t)slot[g];
+                        r[g].key_len = meta_keylen(m);
+                        r[g].cstamp = rd[g];
+                        r[g].rec_cstamp = meta_cstamp(m);
+                        r[g].copy_sstamp = kMaxCid;
+                        r[g].image = si[g].image;
+                    } else {
+                        visibility(t, lf[g], slot[g], rd[g], r[g]);
+                    }
+                }
+            }
+            // phase 5: tuple rows (G x 1008 B in flight), then stores
+            if (recs) {
+                for (uint32_t c0 = 0; c0 < chunks; c0 += 64) {
+                    const uint32_t c = c0 + lane;
+                    uint4 v[G];
+#pragma unroll
+                    for (int g = 0; g < G; ++g) {
+                        v[g] = make_uint4(0, 0, 0, 0);
+                        if (c < chunks && r[g].image != 0xFFFFFFFFu)
+                            v[g] = reinterpret_cast<const uint4 *>(t.heap + (uint64_t)r[g].image * t.stride)[c];
+                    }
+#pragma unroll
+                    for (int g = 0; g < G; ++g) {
+                        const int j = j0 + g;
+                        if (j < cnt && c < chunks)
+                            reinterpret_cast<uint4 *>(recs + (base + j) * (uint64_t)t.stride)[c] = v[g];
+                    }
+                }
+            }
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const int j = j0 + g;
+                if (j < cnt && lane == 0) store_out(out + base + j, lf[g], r[g]);
+            }
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------------------
+// range scan (TableScanExecutor over Iterator), one wave per scan
+
+template <bool VARLEN, int SPL>
+__device__ void scan_one(const DevTable &t, uint64_t x, uint32_t xl, uint32_t leaf, uint32_t scan_size,
+                         uint8_t *recs, uint32_t *count_out, uint32_t lane) {
+    uint32_t remaining = scan_size, produced = 0;
+    bool cont = false;
+    for (uint32_t guard = 0; guard < scan_size + 2 && remaining > 0; ++guard) {
+        const uint64_t base = (uint64_t)leaf * t.cap;
+        uint64_t col[SPL];
+        uint32_t kl[SPL];
+        uint64_t q[SPL];
+#pragma unroll
+        for (int s = 0; s < SPL; ++s) col[s] = t.okey[base + s * 64 + lane];
+#pragma unroll
+        for (int s = 0; s < SPL; ++s) {
+            const uint64_t vm = t.vis[(uint64_t)leaf * SPL + s];
+            const bool vis = (vm >> lane) & 1;
+            kl[s] = t.key_width;
+            if (VARLEN) kl[s] = vis ? meta_keylen(t.slot[base + s * 64 + lane].meta) : 0u;
+            // RangeScanBySize keeps visible records with KeyCompare(start, key) <= 0
+            q[s] = ballot(vis && !kv_lt(col[s], kl[s], x, xl));
+        }
+        // slot-order truncation: records are collected until more than to_scan are held
+        const uint32_t to_scan = remaining;
+        uint32_t before = 0, m = 0;
+        bool keep[SPL];
+#pragma unroll
+        for (int s = 0; s < SPL; ++s) {
+            const uint32_t rank = before + count_below(q[s]);
+            keep[s] = ((q[s] >> lane) & 1) && rank <= to_scan;
+            before += (uint32_t)__builtin_popcountll(q[s]);
+        }
+        uint64_t km[SPL];
+#pragma unroll
+        for (int s = 0; s < SPL; ++s) {
+            km[s] = ballot(keep[s]);
+            m += (uint32_t)__builtin_popcountll(km[s]);
+        }
+        if (m == 0) break;
+        // key rank among the kept records (std::sort by KeyCompare; keys are unique)
+        uint32_t kr[SPL];
+#pragma unroll
+        for (int s = 0; s < SPL; ++s) kr[s] = 0;
+#pragma unroll
+        for (int s2 = 0; s2 < SPL; ++s2) {
+            uint64_t mm = km[s2];
+            while (mm) {
+                const int b = __builtin_ctzll(mm);
+                mm &= mm - 1;
+                const uint64_t ko = rl64(col[s2], b);
+                const uint32_t kll = rl32(kl[s2], b);
+#pragma unroll
+                for (int s = 0; s < SPL; ++s) kr[s] += kv_lt(ko, kll, col[s], kl[s]) ? 1u : 0u;
+            }
+        }
+        // continuation: if the new batch starts with the last key, the iterator stops
+        if (cont) {
+            bool dup = false;
+#pragma unroll
+            for (int s = 0; s < SPL; ++s) dup |= keep[s] && kr[s] == 0 && col[s] == x && kl[s] == xl;
+            if (ballot(dup)) break;
+        }
+        const uint32_t e = m < remaining ? m : remaining;
+        // emit the e smallest kept records at produced + rank
+#pragma unroll
+        for (int s = 0; s < SPL; ++s) {
+            const bool emit = keep[s] && kr[s] < e;
+            uint32_t img = 0;
+            if (emit) img = t.slot[base + s * 64 + lane].image;
+            uint64_t em = ballot(emit);
+            while (em) {
+                const int b = __builtin_ctzll(em);
+                em &= em - 1;
+                const uint32_t im = rl32(img, b);
+                const uint32_t dst = produced + rl32(kr[s], b);
+                copy_row(t, im, recs + (uint64_t)dst * t.stride, lane);
+            }
+        }
+        produced += e;
+        remaining -= e;
+        if (e < m) break;
+        // last record popped: re-traverse from its key with le_child = false
+        uint64_t lastk = 0;
+        uint32_t lastl = 0;
+#pragma unroll
+        for (int s = 0; s < SPL; ++s) {
+            const uint64_t lm = ballot(keep[s] && kr[s] == m - 1);
+            if (lm) {
+                const int b = __builtin_ctzll(lm);
+                lastk = rl64(col[s], b);
+                lastl = rl32(kl[s], b);
+            }
+        }
+        x = lastk;
+        xl = lastl;
+        leaf = uni32(resolve_leaf<VARLEN>(t, x, xl, false));
+        cont = true;
+    }
+    if (lane == 0) *count_out = produced;
+}
+
+template <bool VARLEN, int SPL>
+__global__ __launch_bounds__(256) void scan_kernel(DevTable t, const uint64_t *__restrict__ keys,
+                                                   const uint16_t *__restrict__ lens, uint64_t n, uint32_t scan_size,
+                                                   uint32_t *__restrict__ counts, uint8_t *__restrict__ recs) {
+    const uint32_t lane = lane_id();
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    for (uint64_t base = wave * 64; base < n; base += nwaves * 64) {
+        const uint64_t i = base + lane;
+        const bool valid = i < n;
+        const uint32_t len = t.key_width ? t.key_width : (lens && valid ? (uint32_t)lens[i] : 8u);
+        const uint64_t ok = order_key(valid ? keys[i] : 0, len);
+        const uint32_t leaf = valid ? resolve_leaf<VARLEN>(t, ok, len, true) : 0u;
+        const int cnt = (int)((n - base) < 64 ? (n - base) : 64);
+        for (int j = 0; j < cnt; ++j) {
+            scan_one<VARLEN, SPL>(t, rl64(ok, j), rl32(len, j), rl32(leaf, j), scan_size,
+                                  recs + (base + j) * (uint64_t)scan_size * t.stride, counts + base + j, lane);
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------------------
+// MurmurHash64A (misc/murmur/MurmurHash2.cpp:99-147), lane per key
+
+__device__ __forceinline__ uint64_t murmur64a_dev(const uint8_t *p, uint32_t len, uint64_t seed) {
+    const uint64_t m = 0xc6a4a7935bd1e995ull;
+    const int r = 47;
+    uint64_t h = seed ^ ((uint64_t)len * m);
+    const uint32_t nb = len / 8;
+    for (uint32_t i = 0; i < nb; ++i) {
+        uint64_t k = 0;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) k |= (uint64_t)p[8 * i + b] << (8 * b);
+        k *= m;
+        k ^= k >> r;
+        k *= m;
+        h ^= k;
+        h *= m;
+    }
+    const uint8_t *d2 = p + 8 * nb;
+    const uint32_t rem = len & 7;
+    if (rem) {
+        for (int b = (int)rem - 1; b >= 0; --b) h ^= (uint64_t)d2[b] << (8 * b);
+        h *= m;
+    }
+    h ^= h >> r;
+    h *= m;
+    h ^= h >> r;
+    return h;
+}
+
+__global__ __launch_bounds__(256) void murmur_kernel(const uint8_t *__restrict__ keys, uint32_t key_len,
+                                                     uint32_t key_stride, uint64_t seed, uint64_t n,
+                                                     uint64_t *__restrict__ out) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint8_t *p = keys + i * key_stride;
+    if (key_len == 8 && (key_stride & 7) == 0) {  // the router's case: one aligned word
+        const uint64_t m = 0xc6a4a7935bd1e995ull;
+        uint64_t h = seed ^ (8ull * m);
+        uint64_t k = *reinterpret_cast<const uint64_t *>(p);
+        k *= m;
+        k ^= k >> 47;
+        k *= m;
+        h ^= k;
+        h *= m;
+        h ^= h >> 47;
+        h *= m;
+        h ^= h >> 47;
+        out[i] = h;
+    } else {
+        out[i] = murmur64a_dev(p, key_len, seed);
+    }
+}
+
+// ----------------------------------------------------------------------------------------
+// record-heap fill: row = [key padded to 8][payload][zero pad to stride]
+
+__device__ __forceinline__ uint64_t splitmix64_dev(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ uint64_t payload_word(const ImageDescDev &d, const uint8_t *arena, uint32_t j,
+                                                 uint32_t payload_size) {
+    const uint32_t off = j * 8;
+    if (off >= payload_size) return 0;
+    const uint32_t nb = payload_size - off < 8 ? payload_size - off : 8;
+    uint64_t w;
+    if (d.kind == 1) {
+        w = 0;
+        const uint8_t *s = arena + d.arg + off;
+        for (uint32_t b = 0; b < nb; ++b) w |= (uint64_t)s[b] << (8 * b);
+        return w;
+    }
+    if (d.mode == 0) w = 0x0101010101010101ull * (d.arg & 0xFF);
+    else w = splitmix64_dev((d.arg << 8) ^ j);
+    if (nb < 8) w &= (1ull << (8 * nb)) - 1;
+    return w;
+}
+
+__global__ __launch_bounds__(256) void fill_kernel(uint8_t *__restrict__ heap, uint32_t stride, uint32_t payload_size,
+                                                   const ImageDescDev *__restrict__ descs, const uint8_t *__restrict__ arena,
+                                                   uint64_t first, uint64_t count, uint64_t ident_rowid0,
+                                                   uint32_t ident_key_width, int ident_mode) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint32_t chunks = stride >> 4;
+    for (uint64_t r = wave; r < count; r += nwaves) {
+        ImageDescDev d;
+        if (descs) {
+            d = descs[r];
+        } else {  // identity run: image = rowid = key (LoadYCSBRows)
+            d.arg = ident_rowid0 + r;
+            d.key_le = ident_key_width >= 8 ? d.arg : (d.arg & ((1ull << (8 * ident_key_width)) - 1));
+            d.kind = 0;
+            d.mode = (uint32_t)ident_mode;
+        }
+        uint4 *row = reinterpret_cast<uint4 *>(heap + (first + r) * stride);
+        for (uint32_t c = lane; c < chunks; c += 64) {
+            uint64_t w0 = c == 0 ? d.key_le : payload_word(d, arena, 2 * c - 1, payload_size);
+            uint64_t w1 = payload_word(d, arena, 2 * c, payload_size);
+            row[c] = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------------------
+// launchers
+
+static int grid_for(uint64_t waves_needed, int waves_per_block, int max_blocks) {
+    uint64_t b = (waves_needed + waves_per_block - 1) / waves_per_block;
+    if (b < 1) b = 1;
+    if (b > (uint64_t)max_blocks) b = (uint64_t)max_blocks;
+    return (int)b;
+}
+
+hipError_t launch_resolve(const DevTable &t, const uint64_t *keys, const uint16_t *lens, uint64_t n, int le_child,
+                          uint32_t *out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    resolve_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(t, keys, lens, n, le_child, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_probe(const DevTable &t, const uint64_t *keys, const uint16_t *lens, const uint32_t *rids,
+                       const uint32_t *leaf_in, uint64_t n, stage_probe_out_dev *out, uint8_t *recs, hipStream_t s,
+                       const ProbeTuning &tune) {
+    if (n == 0) return hipSuccess;
+    const uint64_t chunks = (n + 63) / 64;
+    const int blocks = grid_for(chunks, 4, tune.max_blocks > 0 ? tune.max_blocks : 4096);
+    const bool var = t.key_width == 0;
+#define STAGE_PROBE(V, S, G) probe_kernel<V, S, G><<<blocks, 256, 0, s>>>(t, keys, lens, rids, leaf_in, n, out, recs)
+    if (t.cap == 64) {
+        if (var) STAGE_PROBE(true, 1, 4);
+        else if (tune.group == 1) STAGE_PROBE(false, 1, 1);
+        else if (tune.group == 2) STAGE_PROBE(false, 1, 2);
+        else if (tune.group == 8) STAGE_PROBE(false, 1, 8);
+        else STAGE_PROBE(false, 1, 4);
+    } else {
+        if (var) STAGE_PROBE(true, 2, 4);
+        else STAGE_PROBE(false, 2, 4);
+    }
+#undef STAGE_PROBE
+    return hipGetLastError();
+}
+
+hipError_t launch_scan(const DevTable &t, const uint64_t *keys, const uint16_t *lens, uint64_t n, uint32_t scan_size,
+                      uint32_t *counts, uint8_t *recs, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint64_t chunks = (n + 63) / 64;
+    const int blocks = grid_for(chunks, 4, 4096);
+    const bool var = t.key_width == 0;
+    if (t.cap == 64) {
+        if (var) scan_kernel<true, 1><<<blocks, 256, 0, s>>>(t, keys, lens, n, scan_size, counts, recs);
+        else scan_kernel<false, 1><<<blocks, 256, 0, s>>>(t, keys, lens, n, scan_size, counts, recs);
+    } else {
+        if (var) scan_kernel<true, 2><<<blocks, 256, 0, s>>>(t, keys, lens, n, scan_size, counts, recs);
+        else scan_kernel<false, 2><<<blocks, 256, 0, s>>>(t, keys, lens, n, scan_size, counts, recs);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_murmur(const void *keys, uint32_t key_len, uint32_t key_stride, uint64_t seed, uint64_t n,
+                        uint64_t *out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    murmur_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>((const uint8_t *)keys, key_len, key_stride, seed, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_fill(uint8_t *heap, uint32_t stride, uint32_t payload_size, const ImageDescDev *descs,
+                       const uint8_t *arena, uint64_t first, uint64_t count, uint64_t ident_rowid0,
+                       uint32_t ident_key_width, int ident_mode, hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    const int blocks = grid_for(count, 4, 8192);
+    fill_kernel<<<blocks, 256, 0, s>>>(heap, stride, payload_size, descs, arena, first, count, ident_rowid0,
+                                       ident_key_width, ident_mode);
+    return hipGetLastError();
+}
+
+}  // namespace stage

@@ -1,0 +1,115 @@
+// stage_core.hpp -- definitions shared by the host table builder and the gfx950 kernels.
+//
+// Device image of one index-organized table (DESIGN.md "Data layout in HBM"):
+//   okey[L*cap]    u64  order key of every leaf slot (coalesced key column, 512 B/leaf)
+//   slot[L*cap]    16 B {meta word, next handle, image id}  (read for the hit slot only)
+//   vis[L*cap/64]  u64  visible-slot masks (one wave-uniform scalar load per leaf)
+//   tree           u64  implicit 8-ary separator search tree (64-B nodes), all levels
+//   heap[I*stride] u8   record images [key padded to 8][payload] (current, copies, versions)
+//   chdr[C]        16 B overwrite-copy headers   (EphemeralPool::OverwriteVersionHeader)
+//   vhdr[V]        16 B retired-version headers  (TupleHeader)
+#pragma once
+#include <cstdint>
+
+#if defined(__HIPCC__) || defined(__HIP_DEVICE_COMPILE__)
+#define STAGE_HD __host__ __device__ __forceinline__
+#else
+#define STAGE_HD inline
+#endif
+
+namespace stage {
+
+// RecordMetadata word, bit-identical to the reference (record_meta.h:66-70) so a device
+// leaf can be compared word-for-word with a reference leaf.
+constexpr uint64_t kMetaControl = 1ull << 63;
+constexpr uint64_t kMetaVisible = 1ull << 62;
+constexpr uint64_t kMetaKeyLen = 0x2FFFull << 48;
+constexpr uint64_t kMetaOffset = 0xFFFFull << 32;
+constexpr uint64_t kMetaTxn = 0xFFFFFFFFull;
+constexpr uint32_t kMaxCid = 0xFFFFFFFFu;
+constexpr uint32_t kInvalidCid = 0u;
+
+STAGE_HD uint32_t meta_keylen(uint64_t m) { return (uint32_t)((m & kMetaKeyLen) >> 48); }
+STAGE_HD uint32_t meta_offset(uint64_t m) { return (uint32_t)((m & kMetaOffset) >> 32); }
+STAGE_HD bool meta_visible(uint64_t m) { return (m & kMetaVisible) != 0; }
+STAGE_HD bool meta_inserting(uint64_t m) { return (m & kMetaVisible) && (m & kMetaControl); }
+STAGE_HD uint32_t meta_cstamp(uint64_t m) { return (uint32_t)(m & kMetaTxn); }
+STAGE_HD uint32_t pad8(uint32_t n) { return (n + 7u) & ~7u; }
+
+// 32-bit next handle: kind in bits 30-31, index below.  The reference stores a raw pointer
+// (copy-buffer location while an update is in flight, TupleHeader* after commit).
+constexpr uint32_t kNextKindMask = 3u << 30;
+constexpr uint32_t kNextCopy = 1u << 30;
+constexpr uint32_t kNextVersion = 2u << 30;
+constexpr uint32_t kNextIndexMask = (1u << 30) - 1;
+
+// Order key: the reference orders keys by signed-byte lexicographic compare of the first
+// min(len) bytes, then by length (BaseNode::KeyCompare, b_tree.h:99-134).  For keys of at
+// most 8 bytes that order is the unsigned order of (okey, len) where okey holds byte i ^ 0x80
+// at big-endian position i and zero below the key.
+STAGE_HD uint64_t bswap64(uint64_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_bswap64(x);
+#else
+    return __builtin_bswap64(x);
+#endif
+}
+STAGE_HD uint64_t order_key(uint64_t le_bytes, uint32_t len) {
+    const uint64_t mask = len >= 8 ? ~0ull : ((1ull << (8u * len)) - 1ull);
+    return bswap64((le_bytes & mask) ^ (0x8080808080808080ull & mask));
+}
+STAGE_HD uint64_t key_bytes_from_order(uint64_t okey, uint32_t len) {
+    const uint64_t mask = len >= 8 ? ~0ull : ((1ull << (8u * len)) - 1ull);
+    return (bswap64(okey) ^ 0x8080808080808080ull) & mask;
+}
+
+// per-slot word read for the hit slot
+struct alignas(16) SlotInfo {
+    uint64_t meta;  // reference RecordMetadata.meta
+    uint32_t next;  // tagged next handle
+    uint32_t image; // record-heap row of the current image
+};
+
+struct alignas(16) CopyHdr {  // EphemeralPool::OverwriteVersionHeader (ephemeral_pool.h:26-150)
+    uint32_t rstamp;          // old cstamp (lower bound of the copy's visibility)
+    uint32_t sstamp;          // successor stamp (MAX_CID until the writer commits)
+    uint32_t next;            // TupleHeader chain at update time (tagged)
+    uint32_t image;           // record-heap row of the old image
+};
+
+struct alignas(16) VersionHdr { // TupleHeader (version_store.h:28-155)
+    uint32_t begin_id;
+    uint32_t comm_id;
+    uint32_t next;              // tagged (kNextVersion | idx) or 0
+    uint32_t image;
+};
+
+// probe statuses (mirror of include/stage_hip.h)
+enum : uint8_t { ST_NOT_FOUND = 0, ST_LATEST = 1, ST_COPY = 2, ST_OLD = 3, ST_FAIL_INVALID_TS = 4,
+                 ST_CHAIN_MISS = 5 };
+
+constexpr int kTreeFanout = 8;         // keys per separator-tree node (one 64-B line)
+constexpr int kMaxTreeLevels = 16;
+
+// Everything a kernel needs to read one table (passed by value).
+struct DevTable {
+    const uint64_t *okey;
+    const SlotInfo *slot;
+    const uint64_t *vis;
+    const uint64_t *tree;       // all levels, level 0 (leaf separators) first
+    const uint8_t *tree_len;    // variable-length tables only: key length per tree entry
+    const uint8_t *heap;
+    const CopyHdr *chdr;
+    const VersionHdr *vhdr;
+    uint64_t level_off[kMaxTreeLevels]; // entry offset of each level inside `tree`
+    uint32_t levels;            // number of levels (top = levels-1 has one node)
+    uint32_t nleaves;
+    uint32_t nseps;             // nleaves - 1
+    uint32_t cap;               // slots per leaf (64 or 128)
+    uint32_t stride;            // heap/output row bytes (multiple of 16, >= 8 + payload)
+    uint32_t payload_size;
+    uint32_t key_width;         // 0 = variable
+    uint32_t pad_;
+};
+
+}  // namespace stage

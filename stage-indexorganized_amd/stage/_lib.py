@@ -1,0 +1,108 @@
+"""ctypes binding of libstage_hip.so (include/stage_hip.h).
+
+The library is the product: if it is missing or fails to load, every entry point raises.
+There is no CPU fallback anywhere in this package.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libstage_hip.so")
+
+c_u8p = ctypes.POINTER(ctypes.c_uint8)
+c_u16p = ctypes.POINTER(ctypes.c_uint16)
+c_u32p = ctypes.POINTER(ctypes.c_uint32)
+c_u64p = ctypes.POINTER(ctypes.c_uint64)
+c_vp = ctypes.c_void_p
+
+
+class StageParams(ctypes.Structure):
+    _fields_ = [
+        ("split_threshold", ctypes.c_uint32),
+        ("merge_threshold", ctypes.c_uint32),
+        ("leaf_node_size", ctypes.c_uint32),
+        ("payload_size", ctypes.c_uint32),
+        ("key_width", ctypes.c_uint32),
+        ("device", ctypes.c_int32),
+    ]
+
+
+# every exported symbol: name -> (restype, argtypes)
+SIGNATURES = {
+    "stage_last_error": (ctypes.c_char_p, []),
+    "stage_version": (ctypes.c_char_p, []),
+    "stage_table_create": (ctypes.c_int, [ctypes.POINTER(StageParams), ctypes.POINTER(c_vp)]),
+    "stage_table_destroy": (ctypes.c_int, [c_vp]),
+    "stage_insert": (ctypes.c_int, [c_vp, ctypes.c_uint64, ctypes.c_uint16, c_vp, ctypes.c_uint64, ctypes.c_int,
+                                    ctypes.c_uint32, c_u8p]),
+    "stage_load_ycsb": (ctypes.c_int, [c_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, c_u64p]),
+    "stage_load_keys": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, c_u64p]),
+    "stage_update": (ctypes.c_int, [c_vp, ctypes.c_uint64, ctypes.c_uint16, ctypes.c_uint32, c_vp, ctypes.c_uint32,
+                                    ctypes.c_uint32, c_u8p]),
+    "stage_commit_update": (ctypes.c_int, [c_vp, ctypes.c_uint64, ctypes.c_uint16, ctypes.c_uint32, ctypes.c_uint32,
+                                           c_u8p]),
+    "stage_finalize_update": (ctypes.c_int, [c_vp, ctypes.c_uint64, ctypes.c_uint16, ctypes.c_uint32, c_u8p]),
+    "stage_delete": (ctypes.c_int, [c_vp, ctypes.c_uint64, ctypes.c_uint16, ctypes.c_uint32, c_u8p]),
+    "stage_sync": (ctypes.c_int, [c_vp]),
+    "stage_stats": (ctypes.c_int, [c_vp, c_vp]),
+    "stage_record_stride": (ctypes.c_uint32, [c_vp]),
+    "stage_leaf_capacity": (ctypes.c_uint32, [c_vp]),
+    "stage_traverse_batch": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_uint64, ctypes.c_int, c_vp]),
+    "stage_export_leaves": (ctypes.c_int64, [c_vp, ctypes.c_uint32, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp]),
+    "stage_probe_batch": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_uint64, c_vp, c_vp, c_vp]),
+    "stage_scan_batch": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_uint64, ctypes.c_uint32, c_vp, c_vp, c_vp]),
+    "stage_resolve_batch": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_uint64, ctypes.c_int, c_vp, c_vp]),
+    "stage_murmur64a_batch": (ctypes.c_int, [c_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64,
+                                             ctypes.c_uint64, c_vp, c_vp]),
+    "stage_comm_unique_id": (ctypes.c_int, [c_vp]),
+    "stage_comm_init": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int, ctypes.c_int]),
+    "stage_comm_destroy": (ctypes.c_int, [c_vp]),
+    "stage_probe_sharded": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_uint64, c_vp, c_vp, c_vp]),
+    "stage_set_device": (ctypes.c_int, [ctypes.c_int]),
+    "stage_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "stage_dev_alloc": (ctypes.c_int, [ctypes.c_uint64, ctypes.POINTER(c_vp)]),
+    "stage_dev_free": (ctypes.c_int, [c_vp]),
+    "stage_dev_memset": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_uint64, c_vp]),
+    "stage_memcpy_h2d": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64, c_vp]),
+    "stage_memcpy_d2h": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64, c_vp]),
+    "stage_stream_create": (ctypes.c_int, [ctypes.POINTER(c_vp)]),
+    "stage_stream_destroy": (ctypes.c_int, [c_vp]),
+    "stage_stream_sync": (ctypes.c_int, [c_vp]),
+    "stage_device_sync": (ctypes.c_int, []),
+    "stage_event_create": (ctypes.c_int, [ctypes.POINTER(c_vp)]),
+    "stage_event_destroy": (ctypes.c_int, [c_vp]),
+    "stage_event_record": (ctypes.c_int, [c_vp, c_vp]),
+    "stage_event_elapsed": (ctypes.c_int, [c_vp, c_vp, ctypes.POINTER(ctypes.c_float)]),
+    "stage_fastrandom_next": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint64, c_vp]),
+    "stage_zipf_draws": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_double, ctypes.c_uint64, ctypes.c_uint64, c_vp,
+                                        ctypes.c_int]),
+}
+
+
+class StageError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    """Load libstage_hip.so once; raise if it is absent (no fallback path exists)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise StageError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = lib().stage_last_error().decode(errors="replace")
+        raise StageError(f"{what}: rc={rc}: {msg}")
+    return rc

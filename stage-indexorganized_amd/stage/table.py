@@ -1,0 +1,296 @@
+"""Host-side mirror of the reference's table interface over the C-ABI.
+
+`Table` plays the role of the reference's `BTree` (include/vstore/b_tree.h:789-880) for the
+read path: `read`/`probe` = BTree::Read + IndexScanExecutor point lookup (batched),
+`range_scan` = RangeScanBySize + Iterator + TableScanExecutor, `insert`/`update`/... = the
+host write path.  Numpy arrays in, numpy arrays out; device buffers are managed here.
+"""
+import ctypes
+
+import numpy as np
+
+from ._lib import StageParams, c_vp, check, lib
+
+PROBE_OUT_DTYPE = np.dtype([
+    ("status", "u1"), ("flags", "u1"), ("hops", "u2"), ("leaf", "u4"), ("slot", "u2"), ("key_len", "u2"),
+    ("cstamp", "u4"), ("rec_cstamp", "u4"), ("copy_sstamp", "u4"), ("image", "u4"), ("reserved", "u4"),
+])
+assert PROBE_OUT_DTYPE.itemsize == 32
+
+ST_NOT_FOUND, ST_LATEST, ST_COPY, ST_OLD, ST_FAIL_INVALID_TS, ST_CHAIN_MISS = range(6)
+RC_INVALID, RC_OK, RC_KEY_EXISTS, RC_NOT_FOUND = 0, 1, 2, 3
+RC_NOT_NEEDED_UPDATE, RC_DIRTY = 7, 9
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+
+class DeviceBuffer:
+    """A hipMalloc'd buffer owned by Python."""
+
+    def __init__(self, nbytes):
+        self.nbytes = int(nbytes)
+        p = c_vp()
+        check(lib().stage_dev_alloc(max(self.nbytes, 16), ctypes.byref(p)), "stage_dev_alloc")
+        self.ptr = p.value
+
+    @classmethod
+    def from_numpy(cls, arr, stream=None):
+        arr = np.ascontiguousarray(arr)
+        b = cls(arr.nbytes)
+        if arr.nbytes:
+            check(lib().stage_memcpy_h2d(b.ptr, arr.ctypes.data, arr.nbytes, stream), "h2d")
+        return b
+
+    def to_numpy(self, dtype, count, stream=None):
+        out = np.empty(count, dtype=dtype)
+        if out.nbytes:
+            check(lib().stage_memcpy_d2h(out.ctypes.data, self.ptr, out.nbytes, stream), "d2h")
+        return out
+
+    def memset(self, value=0, stream=None):
+        check(lib().stage_dev_memset(self.ptr, value, self.nbytes, stream), "memset")
+
+    def free(self):
+        if self.ptr:
+            lib().stage_dev_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Stream:
+    def __init__(self):
+        p = c_vp()
+        check(lib().stage_stream_create(ctypes.byref(p)), "stream")
+        self.ptr = p.value
+
+    def sync(self):
+        check(lib().stage_stream_sync(self.ptr), "stream sync")
+
+    def __del__(self):
+        try:
+            lib().stage_stream_destroy(self.ptr)
+        except Exception:
+            pass
+
+
+class Event:
+    def __init__(self):
+        p = c_vp()
+        check(lib().stage_event_create(ctypes.byref(p)), "event")
+        self.ptr = p.value
+
+    def record(self, stream):
+        check(lib().stage_event_record(self.ptr, stream.ptr if stream else None), "event record")
+
+    def elapsed_ms(self, other):
+        ms = ctypes.c_float()
+        check(lib().stage_event_elapsed(self.ptr, other.ptr, ctypes.byref(ms)), "event elapsed")
+        return ms.value
+
+    def __del__(self):
+        try:
+            lib().stage_event_destroy(self.ptr)
+        except Exception:
+            pass
+
+
+class Table:
+    """One index-organized table.  Defaults = the YCSB table (ycsb.cpp:72, ycsb_loader.cpp:27-57)."""
+
+    def __init__(self, payload_size=1000, leaf_node_size=64 * 1024, split_threshold=16 * 1024,
+                 merge_threshold=32 * 1024, key_width=8, device=0):
+        p = StageParams(split_threshold, merge_threshold, leaf_node_size, payload_size, key_width, device)
+        h = c_vp()
+        check(lib().stage_table_create(ctypes.byref(p), ctypes.byref(h)), "stage_table_create")
+        self.h = h.value
+        self.payload_size = payload_size
+        self.key_width = key_width
+        self.device = device
+
+    def close(self):
+        if self.h:
+            lib().stage_table_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---------------------------------------------------------------- properties
+    @property
+    def stride(self):
+        return lib().stage_record_stride(self.h)
+
+    @property
+    def leaf_capacity(self):
+        return lib().stage_leaf_capacity(self.h)
+
+    def stats(self):
+        s = np.zeros(8, np.uint64)
+        check(lib().stage_stats(self.h, s.ctypes.data), "stats")
+        keys = ["height", "inner", "leaves", "records", "sorted", "unsorted", "max_count", "versions"]
+        return {k: int(v) for k, v in zip(keys, s)}
+
+    # ---------------------------------------------------------------- host write path
+    def insert(self, key, key_size=None, payload=None, gen_rowid=0, mode=0, commit_id=0):
+        ks = key_size or self.key_width
+        rc = ctypes.c_uint8()
+        buf = None
+        if payload is not None:
+            buf = np.frombuffer(bytes(payload), np.uint8)
+            assert buf.size == self.payload_size
+        check(lib().stage_insert(self.h, int(key), ks, _ptr(buf), gen_rowid, mode, commit_id, ctypes.byref(rc)),
+              "insert")
+        return rc.value
+
+    def load_ycsb(self, begin, end, key_size=None, mode=0):
+        n = ctypes.c_uint64()
+        check(lib().stage_load_ycsb(self.h, begin, end, key_size or self.key_width, mode, ctypes.byref(n)),
+              "load_ycsb")
+        return n.value
+
+    def load_keys(self, keys, key_size=None, mode=0):
+        keys = np.ascontiguousarray(keys, np.uint64)
+        n = ctypes.c_uint64()
+        check(lib().stage_load_keys(self.h, keys.ctypes.data, keys.size, key_size or self.key_width, mode,
+                                    ctypes.byref(n)), "load_keys")
+        return n.value
+
+    def update(self, key, payload_off, delta, writer_id, key_size=None):
+        d = np.frombuffer(bytes(delta), np.uint8)
+        rc = ctypes.c_uint8()
+        check(lib().stage_update(self.h, int(key), key_size or self.key_width, payload_off, d.ctypes.data, d.size,
+                                 writer_id, ctypes.byref(rc)), "update")
+        return rc.value
+
+    def commit_update(self, key, commit_id, sstamp, key_size=None):
+        rc = ctypes.c_uint8()
+        check(lib().stage_commit_update(self.h, int(key), key_size or self.key_width, commit_id, sstamp,
+                                        ctypes.byref(rc)), "commit_update")
+        return rc.value
+
+    def finalize_update(self, key, commit_id, key_size=None):
+        rc = ctypes.c_uint8()
+        check(lib().stage_finalize_update(self.h, int(key), key_size or self.key_width, commit_id, ctypes.byref(rc)),
+              "finalize_update")
+        return rc.value
+
+    def delete(self, key, commit_id=0, key_size=None):
+        rc = ctypes.c_uint8()
+        check(lib().stage_delete(self.h, int(key), key_size or self.key_width, commit_id, ctypes.byref(rc)), "delete")
+        return rc.value
+
+    def sync(self):
+        check(lib().stage_sync(self.h), "stage_sync")
+
+    def export_leaves(self, cap=None):
+        cap = cap or self.leaf_capacity
+        nl = self.stats()["leaves"]
+        rc = np.zeros(nl, np.uint32)
+        sc = np.zeros(nl, np.uint32)
+        meta = np.zeros(nl * cap, np.uint64)
+        keyw = np.zeros(nl * cap, np.uint64)
+        got = lib().stage_export_leaves(self.h, cap, nl, rc.ctypes.data, sc.ctypes.data, meta.ctypes.data,
+                                        keyw.ctypes.data)
+        if got < 0:
+            raise RuntimeError("export_leaves failed")
+        return rc, sc, meta.reshape(nl, cap), keyw.reshape(nl, cap)
+
+    def traverse(self, keys, lens=None, le_child=True):
+        keys = np.ascontiguousarray(keys, np.uint64)
+        lens = None if lens is None else np.ascontiguousarray(lens, np.uint16)
+        out = np.zeros(keys.size, np.uint32)
+        check(lib().stage_traverse_batch(self.h, keys.ctypes.data, _ptr(lens), keys.size, int(le_child),
+                                         out.ctypes.data), "traverse")
+        return out
+
+    # ---------------------------------------------------------------- device read path
+    def probe_device(self, d_keys, n, d_out, d_records=None, d_read_ids=None, d_lens=None, d_leaf_ids=None,
+                     stream=None):
+        check(lib().stage_probe_batch(self.h, d_keys, d_lens, d_read_ids, d_leaf_ids, n, d_out, d_records,
+                                      stream), "stage_probe_batch")
+
+    def probe(self, keys, read_ids=None, lens=None, leaf_ids=None, records=True):
+        """Batched BTree::Read + visibility.  Returns (out[n] PROBE_OUT_DTYPE, rows[n, stride] or None)."""
+        keys = np.ascontiguousarray(keys, np.uint64)
+        n = keys.size
+        bufs = [DeviceBuffer.from_numpy(keys)]
+        d_rids = d_lens = d_leaf = None
+        if read_ids is not None:
+            bufs.append(DeviceBuffer.from_numpy(np.ascontiguousarray(read_ids, np.uint32)))
+            d_rids = bufs[-1].ptr
+        if lens is not None:
+            bufs.append(DeviceBuffer.from_numpy(np.ascontiguousarray(lens, np.uint16)))
+            d_lens = bufs[-1].ptr
+        if leaf_ids is not None:
+            bufs.append(DeviceBuffer.from_numpy(np.ascontiguousarray(leaf_ids, np.uint32)))
+            d_leaf = bufs[-1].ptr
+        d_out = DeviceBuffer(n * 32)
+        d_rec = DeviceBuffer(n * self.stride) if records else None
+        self.probe_device(bufs[0].ptr, n, d_out.ptr, d_rec.ptr if d_rec else None, d_rids, d_lens, d_leaf)
+        check(lib().stage_device_sync(), "sync")
+        out = d_out.to_numpy(PROBE_OUT_DTYPE, n)
+        rows = d_rec.to_numpy(np.uint8, n * self.stride).reshape(n, self.stride) if d_rec else None
+        return out, rows
+
+    def range_scan(self, start_keys, scan_size, lens=None):
+        """TableScanExecutor over RangeScanBySize/Iterator.  Returns (counts[n], rows[n, scan_size, stride])."""
+        keys = np.ascontiguousarray(start_keys, np.uint64)
+        n = keys.size
+        d_keys = DeviceBuffer.from_numpy(keys)
+        d_lens = DeviceBuffer.from_numpy(np.ascontiguousarray(lens, np.uint16)) if lens is not None else None
+        d_cnt = DeviceBuffer(n * 4)
+        d_rec = DeviceBuffer(max(1, n * scan_size * self.stride))
+        d_rec.memset(0)
+        check(lib().stage_scan_batch(self.h, d_keys.ptr, d_lens.ptr if d_lens else None, n, scan_size, d_cnt.ptr,
+                                     d_rec.ptr, None), "stage_scan_batch")
+        check(lib().stage_device_sync(), "sync")
+        counts = d_cnt.to_numpy(np.uint32, n)
+        rows = d_rec.to_numpy(np.uint8, n * scan_size * self.stride).reshape(n, scan_size, self.stride)
+        return counts, rows
+
+    def resolve(self, keys, lens=None, le_child=True):
+        keys = np.ascontiguousarray(keys, np.uint64)
+        d_keys = DeviceBuffer.from_numpy(keys)
+        d_lens = DeviceBuffer.from_numpy(np.ascontiguousarray(lens, np.uint16)) if lens is not None else None
+        d_out = DeviceBuffer(keys.size * 4)
+        check(lib().stage_resolve_batch(self.h, d_keys.ptr, d_lens.ptr if d_lens else None, keys.size,
+                                        int(le_child), d_out.ptr, None), "resolve")
+        check(lib().stage_device_sync(), "sync")
+        return d_out.to_numpy(np.uint32, keys.size)
+
+
+def murmur64a_device(keys, key_len=8, seed=0):
+    keys = np.ascontiguousarray(keys, np.uint64)
+    d_keys = DeviceBuffer.from_numpy(keys)
+    d_out = DeviceBuffer(keys.size * 8)
+    check(lib().stage_murmur64a_batch(d_keys.ptr, key_len, 8, seed, keys.size, d_out.ptr, None), "murmur")
+    check(lib().stage_device_sync(), "sync")
+    return d_out.to_numpy(np.uint64, keys.size)
+
+
+def zipf_draws(n, theta, seed, count, nthreads=8):
+    out = np.empty(count, np.uint64)
+    check(lib().stage_zipf_draws(n, theta, seed, count, out.ctypes.data, nthreads), "zipf")
+    return out
+
+
+def fastrandom(seed, count):
+    out = np.empty(count, np.uint64)
+    check(lib().stage_fastrandom_next(seed, count, out.ctypes.data), "fastrandom")
+    return out
+
+
+def device_count():
+    c = ctypes.c_int(0)
+    rc = lib().stage_device_count(ctypes.byref(c))
+    return c.value if rc == 0 else 0

@@ -1,0 +1,195 @@
+"""ctypes binding of the test oracle (oracle/stage_oracle.c) -- TEST INFRASTRUCTURE ONLY.
+
+The oracle is the CPU restatement of the reference path; tests use it as the checker.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(REPO, "oracle")
+ORACLE_SO = os.path.join(ORACLE_DIR, "_build", "libstage_oracle.so")
+REF_MURMUR_SO = os.path.join(ORACLE_DIR, "_ref", "libref_murmur.so")
+
+READ_OUT_DTYPE = np.dtype([("status", "u1"), ("copy_present", "u1"), ("hops", "u2"), ("cstamp", "u4"),
+                           ("rec_cstamp", "u4"), ("copy_sstamp", "u4")])
+
+vp = ctypes.c_void_p
+u32, u64 = ctypes.c_uint32, ctypes.c_uint64
+
+_SIG = {
+    "orc_tree_new": (vp, [u32, u32, u32]),
+    "orc_tree_set_merge_threshold": (None, [vp, u32]),
+    "orc_tree_free": (None, [vp]),
+    "orc_insert": (ctypes.c_int, [vp, vp, u32, vp, u32]),
+    "orc_load_ycsb": (u64, [vp, u64, u64, u32, ctypes.c_int]),
+    "orc_load_keys": (u64, [vp, vp, u64, u32, ctypes.c_int]),
+    "orc_read": (ctypes.c_int, [vp, vp, u32, u32, vp, vp]),
+    "orc_read_batch": (ctypes.c_int, [vp, vp, u32, vp, u64, vp, vp, ctypes.c_int]),
+    "orc_read_batch_timed": (u64, [vp, vp, u32, vp, u64, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]),
+    "orc_scan": (u32, [vp, vp, u32, u32, vp]),
+    "orc_scan_batch": (u64, [vp, vp, u32, u64, u32, vp, vp, ctypes.c_int]),
+    "orc_traverse_leaf_index": (ctypes.c_int64, [vp, vp, u32, ctypes.c_int]),
+    "orc_update": (ctypes.c_int, [vp, vp, u32, u32, vp, u32, u32]),
+    "orc_commit_update": (ctypes.c_int, [vp, vp, u32, u32, u32]),
+    "orc_finalize_update": (ctypes.c_int, [vp, vp, u32, u32]),
+    "orc_delete": (ctypes.c_int, [vp, vp, u32, u32]),
+    "orc_stats": (None, [vp, vp]),
+    "orc_export_leaves": (ctypes.c_int64, [vp, u32, u64, vp, vp, vp, vp]),
+    "orc_key_compare": (ctypes.c_int, [vp, u32, vp, u32]),
+    "orc_murmur64a": (u64, [vp, ctypes.c_int, u64]),
+    "orc_murmur64a_batch": (None, [vp, u64, ctypes.c_int, u64, vp]),
+    "orc_payload_word": (u64, [u64, u32]),
+    "orc_fill_payload": (None, [u64, ctypes.c_int, vp, u32]),
+}
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE_SO):
+            build()
+        L = ctypes.CDLL(ORACLE_SO)
+        for name, (res, args) in _SIG.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def key_bytes(key, size):
+    return np.array([int(key)], np.uint64).tobytes()[:size] if isinstance(key, (int, np.integer)) else bytes(key)
+
+
+class OracleTree:
+    def __init__(self, leaf_node_size=64 * 1024, split_threshold=16 * 1024, payload_size=1000,
+                 merge_threshold=32 * 1024):
+        self.t = lib().orc_tree_new(leaf_node_size, split_threshold, payload_size)
+        lib().orc_tree_set_merge_threshold(self.t, merge_threshold)
+        self.payload_size = payload_size
+        self.row = 8 + payload_size
+
+    def __del__(self):
+        try:
+            lib().orc_tree_free(self.t)
+        except Exception:
+            pass
+
+    def insert(self, key, key_size, payload, commit_id=0):
+        kb = key_bytes(key, key_size)
+        pb = bytes(payload)
+        assert len(pb) == self.payload_size
+        return lib().orc_insert(self.t, kb, key_size, pb, commit_id)
+
+    def load_ycsb(self, begin, end, key_size, mode=0):
+        return lib().orc_load_ycsb(self.t, begin, end, key_size, mode)
+
+    def load_keys(self, keys, key_size, mode=0):
+        keys = np.ascontiguousarray(keys, np.uint64)
+        return lib().orc_load_keys(self.t, keys.ctypes.data, keys.size, key_size, mode)
+
+    def read(self, key, key_size, read_id=0xFFFFFFFE):
+        kb = key_bytes(key, key_size)
+        out = np.zeros(1, READ_OUT_DTYPE)
+        rec = np.zeros(self.row, np.uint8)
+        lib().orc_read(self.t, kb, key_size, read_id, out.ctypes.data, rec.ctypes.data)
+        return out[0], rec
+
+    def read_batch(self, keys, key_size, read_ids=None, records=True, nthreads=8):
+        keys = np.ascontiguousarray(keys, np.uint64)
+        n = keys.size
+        rids = None if read_ids is None else np.ascontiguousarray(read_ids, np.uint32)
+        outs = np.zeros(n, READ_OUT_DTYPE)
+        recs = np.zeros((n, self.row), np.uint8) if records else None
+        lib().orc_read_batch(self.t, keys.ctypes.data, key_size, rids.ctypes.data if rids is not None else None, n,
+                             outs.ctypes.data, recs.ctypes.data if recs is not None else None, nthreads)
+        return outs, recs
+
+    def scan(self, key, key_size, scan_size):
+        kb = key_bytes(key, key_size)
+        recs = np.zeros((max(scan_size, 1), self.row), np.uint8)
+        c = lib().orc_scan(self.t, kb, key_size, scan_size, recs.ctypes.data)
+        return c, recs[:c]
+
+    def scan_batch(self, keys, key_size, scan_size, nthreads=8):
+        keys = np.ascontiguousarray(keys, np.uint64)
+        counts = np.zeros(keys.size, np.uint32)
+        recs = np.zeros((keys.size, scan_size, self.row), np.uint8)
+        lib().orc_scan_batch(self.t, keys.ctypes.data, key_size, keys.size, scan_size, counts.ctypes.data,
+                             recs.ctypes.data, nthreads)
+        return counts, recs
+
+    def traverse(self, key, key_size, le_child=True):
+        return lib().orc_traverse_leaf_index(self.t, key_bytes(key, key_size), key_size, int(le_child))
+
+    def update(self, key, key_size, payload_off, delta, writer_id):
+        d = bytes(delta)
+        return lib().orc_update(self.t, key_bytes(key, key_size), key_size, payload_off, d, len(d), writer_id)
+
+    def commit_update(self, key, key_size, commit_id, sstamp):
+        return lib().orc_commit_update(self.t, key_bytes(key, key_size), key_size, commit_id, sstamp)
+
+    def finalize_update(self, key, key_size, commit_id):
+        return lib().orc_finalize_update(self.t, key_bytes(key, key_size), key_size, commit_id)
+
+    def delete(self, key, key_size, commit_id=0):
+        return lib().orc_delete(self.t, key_bytes(key, key_size), key_size, commit_id)
+
+    def stats(self):
+        s = np.zeros(8, np.uint64)
+        lib().orc_stats(self.t, s.ctypes.data)
+        keys = ["height", "inner", "leaves", "records", "sorted", "unsorted", "max_count", "versions"]
+        return {k: int(v) for k, v in zip(keys, s)}
+
+    def export_leaves(self, cap):
+        nl = self.stats()["leaves"]
+        rc = np.zeros(nl, np.uint32)
+        sc = np.zeros(nl, np.uint32)
+        meta = np.zeros(nl * cap, np.uint64)
+        keyw = np.zeros(nl * cap, np.uint64)
+        got = lib().orc_export_leaves(self.t, cap, nl, rc.ctypes.data, sc.ctypes.data, meta.ctypes.data,
+                                      keyw.ctypes.data)
+        assert got == nl
+        return rc, sc, meta.reshape(nl, cap), keyw.reshape(nl, cap)
+
+
+def key_compare(k1, k2):
+    a, b = bytes(k1), bytes(k2)
+    return lib().orc_key_compare(a, len(a), b, len(b))
+
+
+def murmur64a(data, seed=0):
+    b = bytes(data)
+    return lib().orc_murmur64a(b, len(b), seed)
+
+
+def murmur64a_keys(keys, length=8, seed=0):
+    keys = np.ascontiguousarray(keys, np.uint64)
+    out = np.zeros(keys.size, np.uint64)
+    lib().orc_murmur64a_batch(keys.ctypes.data, keys.size, length, seed, out.ctypes.data)
+    return out
+
+
+def payload(rowid, mode, size=1000):
+    out = np.zeros(size, np.uint8)
+    lib().orc_fill_payload(rowid, mode, out.ctypes.data, size)
+    return out
+
+
+def ref_murmur_lib():
+    """The reference's own MurmurHash64A compiled from /root/reference (oracle/_ref), if present."""
+    if not os.path.exists(REF_MURMUR_SO):
+        return None
+    L = ctypes.CDLL(REF_MURMUR_SO)
+    L.ref_murmur64a.restype = u64
+    L.ref_murmur64a.argtypes = [vp, ctypes.c_int, u64]
+    return L
