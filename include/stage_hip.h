@@ -153,6 +153,10 @@ int stage_scan_batch(stage_table *t, const uint64_t *d_start_keys, const uint16_
 int stage_resolve_batch(stage_table *t, const uint64_t *d_keys, const uint16_t *d_lens, uint64_t n,
                         int le_child, uint32_t *d_leaf, void *stream);
 
+/* launch shape of stage_probe_batch: probes in flight per wave (1, 2, 4 or 8) and the grid
+ * cap in 256-thread blocks (0 = default).  A tuning knob, not a semantic one. */
+int stage_set_probe_tuning(stage_table *t, int group, int max_blocks);
+
 /* MurmurHash64A (misc/murmur/MurmurHash2.cpp:99-147) over n keys of key_len bytes laid out
  * key_stride bytes apart; d_out[i] = hash.  Used as the multi-GPU shard router. */
 int stage_murmur64a_batch(const void *d_keys, uint32_t key_len, uint32_t key_stride, uint64_t seed,

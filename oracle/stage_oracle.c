@@ -934,6 +934,33 @@ static void *scan_worker(void *arg) {
     return NULL;
 }
 
+static void *scan_timed_worker(void *arg) {
+    job_t *j = arg;
+    uint32_t cap = 4096;
+    scanrec_t *buf = xmalloc(sizeof(scanrec_t) * cap);
+    uint64_t rs = 8 + j->t->payload_size, sum = 0;
+    uint8_t *scratch = xmalloc(rs * (j->scan_size ? j->scan_size : 1));
+    for (uint64_t i = j->b; i < j->e; i++) {
+        uint64_t k = j->keys[i];
+        sum += scan_one(j->t, (const uint8_t *)&k, (uint16_t)j->ks, j->scan_size, scratch, buf, cap);
+    }
+    free(scratch);
+    free(buf);
+    j->sum = sum;
+    return NULL;
+}
+
+uint64_t orc_scan_batch_timed(orc_tree *t, const uint64_t *keys, uint32_t key_size, uint64_t n, uint32_t scan_size,
+                              int nthreads, double *seconds) {
+    job_t j = {t, keys, key_size, NULL, 0, n, NULL, NULL, scan_size, NULL, 0};
+    struct timespec a, b;
+    clock_gettime(CLOCK_MONOTONIC, &a);
+    run_jobs(scan_timed_worker, &j, n, nthreads);
+    clock_gettime(CLOCK_MONOTONIC, &b);
+    if (seconds) *seconds = (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
+    return j.sum;
+}
+
 uint64_t orc_scan_batch(orc_tree *t, const uint64_t *keys, uint32_t key_size, uint64_t n, uint32_t scan_size,
                         uint32_t *counts, uint8_t *recs, int nthreads) {
     job_t j = {t, keys, key_size, NULL, 0, n, NULL, recs, scan_size, counts, 0};

@@ -82,6 +82,10 @@ uint32_t orc_scan(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t s
                   uint8_t *recs);
 uint64_t orc_scan_batch(orc_tree *t, const uint64_t *keys, uint32_t key_size, uint64_t n,
                         uint32_t scan_size, uint32_t *counts, uint8_t *recs, int nthreads);
+/* CPU baseline for scans: TableScanExecutor copies every record into its result vector
+ * (executor.h:637); rows go to a per-thread scratch buffer.  Returns records produced. */
+uint64_t orc_scan_batch_timed(orc_tree *t, const uint64_t *keys, uint32_t key_size, uint64_t n,
+                              uint32_t scan_size, int nthreads, double *seconds);
 
 /* host-side traversal result (BTree::TraverseToLeaf): leaf index in key order */
 int64_t orc_traverse_leaf_index(orc_tree *t, const uint8_t *key, uint32_t key_size, int le_child);

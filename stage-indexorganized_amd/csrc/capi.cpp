@@ -17,6 +17,7 @@ struct stage_table {
     std::unique_ptr<stage::HostTable> host;
     stage::DeviceImage dev;
     stage::ProbeTuning tune;
+    uint32_t out_stride = 0;  // 0 = stride of the canonical row; STAGE_OUT_STRIDE overrides (A/B)
     std::unique_ptr<stage::ShardComm> comm;
 };
 
@@ -69,6 +70,10 @@ int stage_table_create(const stage_params *params, stage_table **out) {
         t->dev.device = params->device;
         if (const char *g = std::getenv("STAGE_PROBE_GROUP")) t->tune.group = std::atoi(g);
         if (const char *g = std::getenv("STAGE_PROBE_MAX_BLOCKS")) t->tune.max_blocks = std::atoi(g);
+        if (const char *g = std::getenv("STAGE_OUT_STRIDE")) {
+            uint32_t v = (uint32_t)std::atoi(g);
+            if (v >= t->host->stride() && v % 16 == 0) t->out_stride = v;
+        }
         *out = t.release();
         return STAGE_OK;
     });
@@ -167,7 +172,7 @@ int stage_stats(stage_table *t, uint64_t *stats) {
     });
 }
 
-uint32_t stage_record_stride(stage_table *t) { return t ? t->host->stride() : 0; }
+uint32_t stage_record_stride(stage_table *t) { return t ? (t->out_stride ? t->out_stride : t->host->stride()) : 0; }
 uint32_t stage_leaf_capacity(stage_table *t) { return t ? t->host->cap() : 0; }
 
 int stage_traverse_batch(stage_table *t, const uint64_t *keys, const uint16_t *lens, uint64_t n, int le_child,
@@ -215,7 +220,9 @@ int stage_probe_batch(stage_table *t, const uint64_t *d_keys, const uint16_t *d_
     if (n && (!d_keys || !d_out)) return fail(STAGE_E_ARG, "null device buffer");
     hipError_t e = hipSetDevice(t->dev.device);
     if (e != hipSuccess) return hip_rc(e, "hipSetDevice");
-    e = stage::launch_probe(t->dev.view, d_keys, d_lens, d_read_ids, d_leaf_ids, n,
+    stage::DevTable view = t->dev.view;
+    if (t->out_stride) view.stride = t->out_stride;
+    e = stage::launch_probe(view, d_keys, d_lens, d_read_ids, d_leaf_ids, n,
                             reinterpret_cast<stage::stage_probe_out_dev *>(d_out), d_records, pick(t, stream), t->tune);
     return hip_rc(e, "probe kernel");
 }
@@ -240,6 +247,16 @@ int stage_resolve_batch(stage_table *t, const uint64_t *d_keys, const uint16_t *
     if (e != hipSuccess) return hip_rc(e, "hipSetDevice");
     e = stage::launch_resolve(t->dev.view, d_keys, d_lens, n, le_child, d_leaf, pick(t, stream));
     return hip_rc(e, "resolve kernel");
+}
+
+int stage_set_probe_tuning(stage_table *t, int group, int max_blocks) {
+    if (!t || (group != 1 && group != 2 && group != 4 && group != 8 && group != 104) || max_blocks < 0)
+        return fail(STAGE_E_ARG, "bad tuning");
+    // group 104 = 4 in flight with ordinary (temporal) output stores (A/B knob)
+    t->tune.nt_store = group == 104 ? 0 : 1;  // (probe_kernel<.., 4, false>)
+    t->tune.group = group == 104 ? 4 : group;
+    t->tune.max_blocks = max_blocks;
+    return STAGE_OK;
 }
 
 int stage_murmur64a_batch(const void *d_keys, uint32_t key_len, uint32_t key_stride, uint64_t seed, uint64_t n,

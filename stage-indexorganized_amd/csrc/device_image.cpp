@@ -27,7 +27,7 @@ static void dev_ensure(DevBuf &b, uint64_t bytes, const char *what) {
 DeviceImage::~DeviceImage() { release(); }
 
 void DeviceImage::release() {
-    for (DevBuf *b : {&okey, &slot, &vis, &tree, &tree_len, &heap, &chdr, &vhdr, &arena, &descs}) {
+    for (DevBuf *b : {&head, &okey, &slot, &tree, &tree_len, &heap, &chdr, &vhdr, &arena, &descs}) {
         if (b->p) (void)hipFree(b->p);
         b->p = nullptr;
         b->cap = 0;
@@ -69,30 +69,40 @@ void sync_device(HostTable &h, DeviceImage &d) {
     d.host_to_dev.assign(h.leaves_.size(), 0xFFFFFFFFu);
     for (uint64_t i = 0; i < L; ++i) d.host_to_dev[order[i]] = (uint32_t)i;
 
-    std::vector<uint64_t> okey(L * cap), vis(L * spl, 0);
+    const uint32_t hb = leaf_head_bytes(cap);
+    std::vector<uint64_t> okey(L * cap);
+    std::vector<uint8_t> head(L * hb, 0);
     std::vector<SlotInfo> slot(L * cap);
     parallel_for(L, [&](uint64_t di) {
-        const uint64_t hb = (uint64_t)order[di] * cap, db = di * cap;
+        const uint64_t hbase = (uint64_t)order[di] * cap, db = di * cap;
         const uint32_t count = h.leaves_[order[di]].count;
+        uint8_t *hd = head.data() + di * hb;
+        uint64_t vis[2] = {0, 0};
         for (uint32_t s = 0; s < cap; ++s) {
             const bool live = s < count;
-            const uint64_t m = live ? h.meta_[hb + s] : 0;
-            okey[db + s] = live ? h.okey_[hb + s] : 0;
+            const uint64_t m = live ? h.meta_[hbase + s] : 0;
+            const uint64_t ok = live ? h.okey_[hbase + s] : 0;
+            okey[db + s] = ok;
+            slot[db + s].okey = ok;
             slot[db + s].meta = m;
-            slot[db + s].next = live ? h.next_[hb + s] : 0;
-            slot[db + s].image = live ? h.image_[hb + s] : 0;
-            if (meta_visible(m) && (p.key_width == 0 || meta_keylen(m) == p.key_width))
-                vis[di * spl + s / 64] |= 1ull << (s % 64);
+            slot[db + s].next = live ? h.next_[hbase + s] : 0;
+            slot[db + s].image = live ? h.image_[hbase + s] : 0;
+            slot[db + s].pad = 0;
+            if (meta_visible(m) && (p.key_width == 0 || meta_keylen(m) == p.key_width)) {
+                vis[s / 64] |= 1ull << (s % 64);
+                hd[s] = (uint8_t)key_fp(ok);
+            }
         }
+        std::memcpy(hd + cap, vis, 8 * spl);
     });
 
-    // ---- implicit 8-ary separator tree: level 0 = separators, level k+1 = max of each
-    // 8-entry node of level k, every level padded with +inf, top level one node.
+    // ---- implicit 16-ary separator tree: level 0 = separators, level k+1 = max of each
+    // 16-entry node of level k, every level padded with +inf, top level one node.
     const uint64_t S = L ? L - 1 : 0;
     std::vector<std::vector<uint64_t>> lv;
     std::vector<std::vector<uint8_t>> lvlen;
     {
-        const uint64_t n0 = (S + 1 + 7) / 8 * 8;
+        const uint64_t n0 = (S + 1 + kTreeFanout - 1) / kTreeFanout * kTreeFanout;
         std::vector<uint64_t> l0(n0, ~0ull);
         std::vector<uint8_t> l0len(n0, 0xFF);
         for (uint64_t i = 0; i < S; ++i) {
@@ -106,7 +116,7 @@ void sync_device(HostTable &h, DeviceImage &d) {
             const auto &prev = lv.back();
             const auto &prevlen = lvlen.back();
             const uint64_t nodes = prev.size() / kTreeFanout;
-            const uint64_t nn = (nodes + 7) / 8 * 8;
+            const uint64_t nn = (nodes + kTreeFanout - 1) / kTreeFanout * kTreeFanout;
             std::vector<uint64_t> nx(nn, ~0ull);
             std::vector<uint8_t> nxlen(nn, 0xFF);
             for (uint64_t j = 0; j < nodes; ++j) {
@@ -128,16 +138,16 @@ void sync_device(HostTable &h, DeviceImage &d) {
     }
 
     hipStream_t s = d.stream;
+    upload(d.head, head.data(), head.size(), s, "head");
     upload(d.okey, okey.data(), okey.size() * 8, s, "okey");
     upload(d.slot, slot.data(), slot.size() * sizeof(SlotInfo), s, "slot");
-    upload(d.vis, vis.data(), vis.size() * 8, s, "vis");
     upload(d.tree, tree.data(), tree.size() * 8, s, "tree");
     upload(d.tree_len, tree_len.data(), tree_len.size(), s, "tree_len");
     upload(d.chdr, h.copies_.data(), h.copies_.size() * sizeof(CopyHdr), s, "chdr");
     upload(d.vhdr, h.versions_.data(), h.versions_.size() * sizeof(VersionHdr), s, "vhdr");
 
     // ---- record heap: fill the rows of images created since the last sync
-    const uint32_t stride = h.stride();
+    const uint32_t stride = h.hstride();
     const uint64_t nimg = h.images_.size();
     if (nimg > d.heap_rows) {
         const uint64_t rows = nimg + std::max<uint64_t>(nimg / 16, 1024);
@@ -207,9 +217,9 @@ void sync_device(HostTable &h, DeviceImage &d) {
     hip_check(hipStreamSynchronize(s), "sync");
 
     DevTable &v = d.view;
+    v.head = (const uint8_t *)d.head.p;
     v.okey = (const uint64_t *)d.okey.p;
     v.slot = (const SlotInfo *)d.slot.p;
-    v.vis = (const uint64_t *)d.vis.p;
     v.tree = (const uint64_t *)d.tree.p;
     v.tree_len = (const uint8_t *)d.tree_len.p;
     v.heap = (const uint8_t *)d.heap.p;
@@ -220,7 +230,9 @@ void sync_device(HostTable &h, DeviceImage &d) {
     v.nleaves = (uint32_t)L;
     v.nseps = (uint32_t)S;
     v.cap = cap;
-    v.stride = stride;
+    v.stride = h.stride();
+    v.hstride = stride;
+    v.head_bytes = hb;
     v.payload_size = p.payload_size;
     v.key_width = p.key_width;
     h.layout_dirty_ = false;

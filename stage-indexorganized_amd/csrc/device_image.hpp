@@ -19,7 +19,7 @@ struct DevBuf {
 struct DeviceImage {
     int device = 0;
     hipStream_t stream = nullptr;
-    DevBuf okey, slot, vis, tree, tree_len, heap, chdr, vhdr, arena, descs;
+    DevBuf head, okey, slot, tree, tree_len, heap, chdr, vhdr, arena, descs;
     uint64_t heap_rows = 0;  // rows the heap buffer can hold
     DevTable view{};
     std::vector<uint32_t> host_to_dev;  // host leaf id -> leaf index in key order

@@ -50,7 +50,10 @@ HostTable::HostTable(const stage_params &p) : p_(p) {
     if (max_records_ <= 64) cap_ = 64;
     else if (max_records_ <= 128) cap_ = 128;
     else throw std::invalid_argument("more than 128 records per leaf is not supported");
+    // output/heap row: [key padded to 8][payload], 16-B multiple; rows above 128 B are
+    // 128-B multiples so every row starts on an L2 line (a 1008-B tuple = 8 whole lines)
     stride_ = (8 + p.payload_size + 15) & ~15u;
+    if (stride_ > 128) stride_ = (stride_ + 127) & ~127u;
     buckets_.resize(1u << 16);
     uint32_t root = alloc_leaf();
     head_ = (int32_t)root;

@@ -42,6 +42,7 @@ public:
     const stage_params &params() const { return p_; }
     uint32_t cap() const { return cap_; }
     uint32_t stride() const { return stride_; }
+    uint32_t hstride() const { return stride_; }
 
     // write path, reference ReturnCode values
     int insert(uint64_t key_le, uint32_t len, const uint8_t *payload, uint64_t gen_rowid, int mode,

@@ -22,8 +22,9 @@ struct alignas(8) ImageDescDev {
 };
 
 struct ProbeTuning {
-    int group = 4;       // probes per wave in flight
-    int max_blocks = 0;  // 0 = default grid cap
+    int group = 8;         // probes per wave in flight (swept: 8 > 4 > 2 > 1 at 100M rows)
+    int max_blocks = 0;    // 0 = default grid cap (16384 blocks of 256 threads)
+    int nt_store = 1;      // nontemporal output stores
 };
 
 hipError_t launch_resolve(const DevTable &t, const uint64_t *keys, const uint16_t *lens, uint64_t n, int le_child,

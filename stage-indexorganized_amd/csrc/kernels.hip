@@ -1,15 +1,18 @@
 // kernels.hip -- gfx950 (CDNA4, wave64) kernels of the index-organized read path.
 //
-// Integer/pointer work only (no MFMA).  Mapping (DESIGN.md):
+// Integer/pointer work only (no MFMA).  Mapping (DESIGN.md §4):
 //   * leaf resolve: lane-per-probe descent of the implicit 8-ary separator tree (one 64-B
 //     node per level = 4 x 16-B loads per lane), replaces InternalNode::GetChildIndex
 //     (b_tree.cpp:664-702) / BTree::TraverseToLeaf (b_tree.cpp:1804-1846).
-//   * leaf probe: wave-per-probe.  64 lanes read the leaf's key column (one coalesced 512-B
-//     read) and a scalar visible-slot mask; __ballot + ffs gives the first visible slot
-//     holding the key in slot order -- BaseNode::SearchRecordMeta (b_tree.cpp:18-122).
+//   * leaf probe: wave-per-probe.  64 lanes read the leaf head (1-byte key fingerprint per
+//     slot + visible mask, one 128-B line); ballot gives the fingerprint candidates, the
+//     candidate lanes read their 32-B slot words and a second ballot confirms the order key:
+//     first visible slot holding the key in slot order == BaseNode::SearchRecordMeta
+//     (b_tree.cpp:18-122).
 //   * visibility: wave-uniform scalar walk (BTree::Read copy path b_tree.cpp:2087-2123,
-//     IndexScanExecutor executor.h:383-450).
-//   * tuple copy: 63 lanes x 16 B = the 1008-B [key|payload] row (Record::New b_tree.h:407-428).
+//     IndexScanExecutor executor.h:383-450); latest-version fast path inline.
+//   * tuple copy: 63 lanes x 16 B = the 1008-B [key|payload] row (Record::New b_tree.h:407-428),
+//     read from a 128-B aligned heap row, written with nontemporal stores.
 //   * range scan: ballot + mbcnt prefix counts give RangeScanBySize's slot-order truncation
 //     (b_tree.cpp:1276-1302), an in-wave rank sort replaces std::sort, continuation as
 //     Iterator::GetNext (b_tree.h:899-941).
@@ -20,6 +23,8 @@
 
 namespace stage {
 
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 __device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 __device__ __forceinline__ uint32_t rl32(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
@@ -27,41 +32,47 @@ __device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
     return ((uint64_t)rl32((uint32_t)(v >> 32), l) << 32) | rl32((uint32_t)v, l);
 }
 __device__ __forceinline__ uint32_t uni32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
-__device__ __forceinline__ uint64_t uni64(uint64_t v) {
-    return ((uint64_t)uni32((uint32_t)(v >> 32)) << 32) | uni32((uint32_t)v);
-}
 // popcount of mask bits below this lane
 __device__ __forceinline__ uint32_t count_below(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
-
-struct KeyV {
-    uint64_t okey;
-    uint32_t len;
-};
 __device__ __forceinline__ bool kv_lt(uint64_t ao, uint32_t al, uint64_t bo, uint32_t bl) {
     return ao < bo || (ao == bo && al < bl);
+}
+__device__ __forceinline__ uint64_t head_vis(const DevTable &t, uint32_t leaf, int s) {
+    return *reinterpret_cast<const uint64_t *>(t.head + (uint64_t)leaf * t.head_bytes + t.cap + 8 * s);
 }
 
 // lower_bound over the separators: number of separators < x, i.e. the leaf whose range
 // (sep[i-1], sep[i]] holds x (le_child semantics).  Upper-bound callers pass succ(x).
 template <bool VARLEN>
 __device__ __forceinline__ uint32_t tree_lower_bound(const DevTable &t, uint64_t x, uint32_t xl) {
+    static_assert(kTreeFanout == 16, "node = 8 x 16-B loads");
     uint32_t node = 0;
     for (int lvl = (int)t.levels - 1; lvl >= 0; --lvl) {
-        const uint64_t *e = t.tree + t.level_off[lvl] + (uint64_t)node * kTreeFanout;
-        const ulonglong2 *e2 = reinterpret_cast<const ulonglong2 *>(e);
-        ulonglong2 a = e2[0], b = e2[1], c = e2[2], d = e2[3];
-        uint64_t v[8] = {a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y};
+        const uint64_t off = t.level_off[lvl] + (uint64_t)node * kTreeFanout;
+        const u32x4 *e = reinterpret_cast<const u32x4 *>(t.tree + off);
+        u32x4 q[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) q[k] = e[k];
         uint32_t cnt = 0;
         if (VARLEN) {
-            const uint8_t *ln = t.tree_len + t.level_off[lvl] + (uint64_t)node * kTreeFanout;
-            uint64_t lw = *reinterpret_cast<const uint64_t *>(ln);
+            const uint64_t *lp = reinterpret_cast<const uint64_t *>(t.tree_len + off);
+            const uint64_t lw0 = lp[0], lw1 = lp[1];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) cnt += kv_lt(v[i], (uint32_t)((lw >> (8 * i)) & 0xFF), x, xl) ? 1u : 0u;
+            for (int k = 0; k < 8; ++k) {
+                const uint64_t lw = k < 4 ? lw0 : lw1;
+                const int sh = 16 * (k & 3);
+                const uint64_t v0 = ((uint64_t)q[k].y << 32) | q[k].x, v1 = ((uint64_t)q[k].w << 32) | q[k].z;
+                cnt += kv_lt(v0, (uint32_t)((lw >> sh) & 0xFF), x, xl) ? 1u : 0u;
+                cnt += kv_lt(v1, (uint32_t)((lw >> (sh + 8)) & 0xFF), x, xl) ? 1u : 0u;
+            }
         } else {
 #pragma unroll
-            for (int i = 0; i < 8; ++i) cnt += (v[i] < x) ? 1u : 0u;
+            for (int k = 0; k < 8; ++k) {
+                cnt += ((((uint64_t)q[k].y << 32) | q[k].x) < x) ? 1u : 0u;
+                cnt += ((((uint64_t)q[k].w << 32) | q[k].z) < x) ? 1u : 0u;
+            }
         }
         node = node * kTreeFanout + cnt;
     }
@@ -94,33 +105,10 @@ struct ProbeRes {
     uint32_t status, flags, hops, slot, key_len, cstamp, rec_cstamp, copy_sstamp, image;
 };
 
-// first visible slot of `leaf` holding (x, xl) in slot order, or -1
-template <bool VARLEN, int SPL>
-__device__ __forceinline__ int find_slot(const DevTable &t, uint32_t leaf, uint64_t x, uint32_t xl, uint32_t lane) {
-    const uint64_t base = (uint64_t)leaf * t.cap;
-    uint64_t col[SPL];
-#pragma unroll
-    for (int s = 0; s < SPL; ++s) col[s] = t.okey[base + s * 64 + lane];
-#pragma unroll
-    for (int s = 0; s < SPL; ++s) {
-        uint64_t vm = t.vis[(uint64_t)leaf * SPL + s];
-        uint64_t hit = ballot(col[s] == x) & vm;
-        if (VARLEN) {
-            while (hit) {  // candidates with the same order key: check the key length
-                int b = __builtin_ctzll(hit);
-                hit &= hit - 1;
-                uint64_t m = t.slot[base + s * 64 + b].meta;
-                if (meta_keylen(m) == xl) return s * 64 + b;
-            }
-        } else if (hit) {
-            return s * 64 + __builtin_ctzll(hit);
-        }
-    }
-    return -1;
-}
-
-// BTree::Read + IndexScanExecutor visibility for one wave-uniform probe
-__device__ __forceinline__ void visibility(const DevTable &t, uint32_t leaf, int slot, uint32_t rid, ProbeRes &r) {
+// BTree::Read + IndexScanExecutor visibility for one wave-uniform probe whose slot word
+// (meta, next, image) is already known.
+__device__ __forceinline__ void visibility(const DevTable &t, int slot, uint64_t m, uint32_t next, uint32_t image,
+                                           uint32_t rid, ProbeRes &r) {
     r.flags = 0;
     r.hops = 0;
     r.copy_sstamp = kMaxCid;
@@ -134,14 +122,12 @@ __device__ __forceinline__ void visibility(const DevTable &t, uint32_t leaf, int
         return;
     }
     r.slot = (uint32_t)slot;
-    const SlotInfo si = t.slot[(uint64_t)leaf * t.cap + slot];
-    const uint64_t m = si.meta;
     r.rec_cstamp = meta_cstamp(m);
     r.key_len = meta_keylen(m);
     CopyHdr c = {0, kMaxCid, 0, 0};
-    const bool has_copy = (si.next & kNextKindMask) == kNextCopy;
+    const bool has_copy = (next & kNextKindMask) == kNextCopy;
     if (has_copy) {  // PerformRead: GetOversionHeader(meta.next_ptr) != nullptr
-        c = t.chdr[si.next & kNextIndexMask];
+        c = t.chdr[next & kNextIndexMask];
         r.flags |= 1u;
         r.copy_sstamp = c.sstamp;
     }
@@ -157,9 +143,9 @@ __device__ __forceinline__ void visibility(const DevTable &t, uint32_t leaf, int
         chain = c.next;
         from_copy = true;
     } else {
-        img = si.image;
+        img = image;
         r.cstamp = rid;
-        chain = si.next;
+        chain = next;
     }
     if (rid >= r.rec_cstamp) {
         r.status = from_copy ? ST_COPY : ST_LATEST;
@@ -190,18 +176,7 @@ __device__ __forceinline__ void visibility(const DevTable &t, uint32_t leaf, int
     r.status = ST_CHAIN_MISS;
 }
 
-__device__ __forceinline__ void copy_row(const DevTable &t, uint32_t img, uint8_t *dst, uint32_t lane) {
-    const uint32_t chunks = t.stride >> 4;
-    const uint4 *src = reinterpret_cast<const uint4 *>(t.heap + (uint64_t)img * t.stride);
-    uint4 *d = reinterpret_cast<uint4 *>(dst);
-    for (uint32_t c = lane; c < chunks; c += 64) {
-        uint4 v = img == 0xFFFFFFFFu ? make_uint4(0, 0, 0, 0) : src[c];
-        d[c] = v;
-    }
-}
-
-__device__ __forceinline__ void store_out(stage_probe_out_dev *out, uint32_t leaf, const ProbeRes &r) {
-    uint4 a, b;
+__device__ __forceinline__ void pack_out(uint32_t leaf, const ProbeRes &r, u32x4 &a, u32x4 &b) {
     a.x = (r.status & 0xFF) | ((r.flags & 0xFF) << 8) | ((r.hops > 0xFFFF ? 0xFFFF : r.hops) << 16);
     a.y = leaf;
     a.z = (r.slot & 0xFFFF) | (r.key_len << 16);
@@ -210,14 +185,15 @@ __device__ __forceinline__ void store_out(stage_probe_out_dev *out, uint32_t lea
     b.y = r.copy_sstamp;
     b.z = r.image;
     b.w = 0;
-    uint4 *o = reinterpret_cast<uint4 *>(out);
-    o[0] = a;
-    o[1] = b;
 }
 
-// G probes per wave in flight: the G key-column loads, then the G slot-word loads, then the
-// G tuple loads are issued back to back, so each wave keeps G independent misses in flight.
-template <bool VARLEN, int SPL, int G>
+template <bool NT, class T>
+__device__ __forceinline__ void st16(T v, T *p) {
+    if (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+template <bool VARLEN, int SPL, int G, bool NT = true>
 __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *__restrict__ keys,
                                                     const uint16_t *__restrict__ lens,
                                                     const uint32_t *__restrict__ rids,
@@ -227,10 +203,11 @@ __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *
     const uint32_t lane = lane_id();
     const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    const uint32_t chunks = t.stride >> 4;
+    const uint32_t out_chunks = t.stride >> 4;
     for (uint64_t base = wave * 64; base < n; base += nwaves * 64) {
         const uint64_t i = base + lane;
         const bool valid = i < n;
+        u32x4 my_a = u32x4{0, 0, 0, 0}, my_b = u32x4{0, 0, 0, 0};  // this lane's probe result
         const uint64_t kle = valid ? keys[i] : 0;
         const uint32_t len = t.key_width ? t.key_width : (lens && valid ? (uint32_t)lens[i] : 8u);
         const uint32_t rid = rids ? (valid ? rids[i] : 0u) : 0xFFFFFFFEu;
@@ -240,103 +217,142 @@ __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *
         if (leaf > t.nseps) leaf = t.nseps;  // host-supplied ids are clamped to the table
         const int cnt = (int)((n - base) < 64 ? (n - base) : 64);
         for (int j0 = 0; j0 < cnt; j0 += G) {
-            uint32_t lf[G], rd[G];
-            int slot[G];
-            ProbeRes r[G];
-            if (VARLEN) {
+            uint32_t lf[G], rd[G], xl[G];
+            uint64_t x[G];
+            uint32_t fpb[G][SPL];
+            uint64_t vm[G][SPL];
+            // phase 1: leaf heads (fingerprints + visible masks) of G probes
 #pragma unroll
-                for (int g = 0; g < G; ++g) {
-                    const int j = j0 + g < cnt ? j0 + g : cnt - 1;
-                    lf[g] = rl32(leaf, j);
-                    rd[g] = rl32(rid, j);
-                    slot[g] = find_slot<VARLEN, SPL>(t, lf[g], rl64(ok, j), rl32(len, j), lane);
+            for (int g = 0; g < G; ++g) {
+                const int j = j0 + g < cnt ? j0 + g : cnt - 1;
+                lf[g] = rl32(leaf, j);
+                rd[g] = rl32(rid, j);
+                x[g] = rl64(ok, j);
+                xl[g] = VARLEN ? rl32(len, j) : t.key_width;
+                const uint8_t *h = t.head + (uint64_t)lf[g] * t.head_bytes;
+#pragma unroll
+                for (int s = 0; s < SPL; ++s) {
+                    fpb[g][s] = h[s * 64 + lane];
+                    vm[g][s] = head_vis(t, lf[g], s);
                 }
+            }
+            // phase 2: fingerprint candidates read their slot words
+            uint64_t wok[G][SPL], wmeta[G][SPL];
+            uint32_t wnext[G][SPL], wimg[G][SPL];
+            bool cand[G][SPL];
 #pragma unroll
-                for (int g = 0; g < G; ++g) visibility(t, lf[g], slot[g], rd[g], r[g]);
-            } else {
-                // phase 1: key columns and visible masks of G leaves
-                uint64_t x[G], col[G][SPL], vm[G][SPL];
+            for (int g = 0; g < G; ++g) {
+                const uint32_t fx = key_fp(x[g]);
 #pragma unroll
-                for (int g = 0; g < G; ++g) {
-                    const int j = j0 + g < cnt ? j0 + g : cnt - 1;
-                    lf[g] = rl32(leaf, j);
-                    rd[g] = rl32(rid, j);
-                    x[g] = rl64(ok, j);
-                    const uint64_t b = (uint64_t)lf[g] * t.cap;
-#pragma unroll
-                    for (int s = 0; s < SPL; ++s) {
-                        col[g][s] = t.okey[b + s * 64 + lane];
-                        vm[g][s] = t.vis[(uint64_t)lf[g] * SPL + s];
-                    }
-                }
-                // phase 2: first visible slot holding the key (ballot, slot order)
-#pragma unroll
-                for (int g = 0; g < G; ++g) {
-                    slot[g] = -1;
-#pragma unroll
-                    for (int s = SPL - 1; s >= 0; --s) {
-                        const uint64_t hit = ballot(col[g][s] == x[g]) & vm[g][s];
-                        if (hit) slot[g] = s * 64 + __builtin_ctzll(hit);
-                    }
-                }
-                // phase 3: slot words of the G hits (scalar loads)
-                SlotInfo si[G];
-#pragma unroll
-                for (int g = 0; g < G; ++g) {
-                    const uint64_t idx = (uint64_t)lf[g] * t.cap + (slot[g] < 0 ? 0 : slot[g]);
-                    si[g] = t.slot[idx];
-                }
-                // phase 4: the latest-version fast path, everything else through visibility()
-#pragma unroll
-                for (int g = 0; g < G; ++g) {
-                    const uint64_t m = si[g].meta;
-                    const bool fast = slot[g] >= 0 && !meta_inserting(m) && rd[g] >= meta_cstamp(m) &&
-                                      (si[g].next & kNextKindMask) != kNextCopy;
-                    if (fast) {
-                        r[g].status = ST_LATEST;
-                        r[g].flags = 0;
-                        r[g].hops = 0;
-                        r[g].slot = (uint32_t)slot[g];
-                        r[g].key_len = meta_keylen(m);
-                        r[g].cstamp = rd[g];
-                        r[g].rec_cstamp = meta_cstamp(m);
-                        r[g].copy_sstamp = kMaxCid;
-                        r[g].image = si[g].image;
-                    } else {
-                        visibility(t, lf[g], slot[g], rd[g], r[g]);
+                for (int s = 0; s < SPL; ++s) {
+                    cand[g][s] = ((vm[g][s] >> lane) & 1) && fpb[g][s] == fx;
+                    wok[g][s] = 0;
+                    wmeta[g][s] = 0;
+                    wnext[g][s] = 0;
+                    wimg[g][s] = 0;
+                    if (cand[g][s]) {
+                        const u32x4 *w = reinterpret_cast<const u32x4 *>(t.slot + (uint64_t)lf[g] * t.cap + s * 64 + lane);
+                        const u32x4 w0 = w[0], w1 = w[1];
+                        wok[g][s] = ((uint64_t)w0.y << 32) | w0.x;
+                        wmeta[g][s] = ((uint64_t)w0.w << 32) | w0.z;
+                        wnext[g][s] = w1.x;
+                        wimg[g][s] = w1.y;
                     }
                 }
             }
-            // phase 5: tuple rows (G x 1008 B in flight), then stores
+            // phase 3: confirm (order key, key length), first hit in slot order, visibility
+            ProbeRes r[G];
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                int slot = -1;
+                uint64_t m = 0;
+                uint32_t nx = 0, im = 0;
+#pragma unroll
+                for (int s = SPL - 1; s >= 0; --s) {
+                    const bool hitl = cand[g][s] && wok[g][s] == x[g] && (!VARLEN || meta_keylen(wmeta[g][s]) == xl[g]);
+                    const uint64_t hit = ballot(hitl);
+                    if (hit) {
+                        const int b = __builtin_ctzll(hit);
+                        slot = s * 64 + b;
+                        m = rl64(wmeta[g][s], b);
+                        nx = rl32(wnext[g][s], b);
+                        im = rl32(wimg[g][s], b);
+                    }
+                }
+                const bool fast = slot >= 0 && !meta_inserting(m) && rd[g] >= meta_cstamp(m) &&
+                                  (nx & kNextKindMask) != kNextCopy;
+                if (fast) {
+                    r[g].status = ST_LATEST;
+                    r[g].flags = 0;
+                    r[g].hops = 0;
+                    r[g].slot = (uint32_t)slot;
+                    r[g].key_len = meta_keylen(m);
+                    r[g].cstamp = rd[g];
+                    r[g].rec_cstamp = meta_cstamp(m);
+                    r[g].copy_sstamp = kMaxCid;
+                    r[g].image = im;
+                } else {
+                    visibility(t, slot, m, nx, im, rd[g], r[g]);
+                }
+            }
+            // phase 4: tuple rows (G rows in flight), then nontemporal stores
             if (recs) {
-                for (uint32_t c0 = 0; c0 < chunks; c0 += 64) {
+                for (uint32_t c0 = 0; c0 < out_chunks; c0 += 64) {
                     const uint32_t c = c0 + lane;
-                    uint4 v[G];
+                    u32x4 v[G];
 #pragma unroll
                     for (int g = 0; g < G; ++g) {
-                        v[g] = make_uint4(0, 0, 0, 0);
-                        if (c < chunks && r[g].image != 0xFFFFFFFFu)
-                            v[g] = reinterpret_cast<const uint4 *>(t.heap + (uint64_t)r[g].image * t.stride)[c];
+                        v[g] = u32x4{0, 0, 0, 0};
+                        if (c < out_chunks && r[g].image != 0xFFFFFFFFu)
+                            v[g] = reinterpret_cast<const u32x4 *>(t.heap + (uint64_t)r[g].image * t.hstride)[c];
                     }
 #pragma unroll
                     for (int g = 0; g < G; ++g) {
                         const int j = j0 + g;
-                        if (j < cnt && c < chunks)
-                            reinterpret_cast<uint4 *>(recs + (base + j) * (uint64_t)t.stride)[c] = v[g];
+                        if (j < cnt && c < out_chunks)
+                            st16<NT>(v[g], reinterpret_cast<u32x4 *>(recs + (base + j) * (uint64_t)t.stride) + c);
                     }
                 }
             }
 #pragma unroll
             for (int g = 0; g < G; ++g) {
-                const int j = j0 + g;
-                if (j < cnt && lane == 0) store_out(out + base + j, lf[g], r[g]);
+                u32x4 a, b;
+                pack_out(lf[g], r[g], a, b);
+                if (lane == (uint32_t)(j0 + g)) {
+                    my_a = a;
+                    my_b = b;
+                }
             }
+        }
+        // one coalesced 2-KiB store of the chunk's 64 results
+        if (valid) {
+            u32x4 *o = reinterpret_cast<u32x4 *>(out + i);
+            st16<NT>(my_a, o);
+            st16<NT>(my_b, o + 1);
         }
     }
 }
 
 // ----------------------------------------------------------------------------------------
 // range scan (TableScanExecutor over Iterator), one wave per scan
+
+__device__ __forceinline__ void copy_rows4(const DevTable &t, const uint32_t *img, const uint32_t *dst, int n,
+                                           uint8_t *recs, uint32_t lane) {
+    const uint32_t chunks = t.stride >> 4;
+    for (uint32_t c0 = 0; c0 < chunks; c0 += 64) {
+        const uint32_t c = c0 + lane;
+        u32x4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            v[k] = u32x4{0, 0, 0, 0};
+            if (k < n && c < chunks) v[k] = reinterpret_cast<const u32x4 *>(t.heap + (uint64_t)img[k] * t.hstride)[c];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (k < n && c < chunks)
+                __builtin_nontemporal_store(v[k], reinterpret_cast<u32x4 *>(recs + (uint64_t)dst[k] * t.stride) + c);
+    }
+}
 
 template <bool VARLEN, int SPL>
 __device__ void scan_one(const DevTable &t, uint64_t x, uint32_t xl, uint32_t leaf, uint32_t scan_size,
@@ -352,7 +368,7 @@ __device__ void scan_one(const DevTable &t, uint64_t x, uint32_t xl, uint32_t le
         for (int s = 0; s < SPL; ++s) col[s] = t.okey[base + s * 64 + lane];
 #pragma unroll
         for (int s = 0; s < SPL; ++s) {
-            const uint64_t vm = t.vis[(uint64_t)leaf * SPL + s];
+            const uint64_t vm = head_vis(t, leaf, s);
             const bool vis = (vm >> lane) & 1;
             kl[s] = t.key_width;
             if (VARLEN) kl[s] = vis ? meta_keylen(t.slot[base + s * 64 + lane].meta) : 0u;
@@ -400,7 +416,7 @@ __device__ void scan_one(const DevTable &t, uint64_t x, uint32_t xl, uint32_t le
             if (ballot(dup)) break;
         }
         const uint32_t e = m < remaining ? m : remaining;
-        // emit the e smallest kept records at produced + rank
+        // emit the e smallest kept records at produced + rank, four rows in flight
 #pragma unroll
         for (int s = 0; s < SPL; ++s) {
             const bool emit = keep[s] && kr[s] < e;
@@ -408,11 +424,15 @@ __device__ void scan_one(const DevTable &t, uint64_t x, uint32_t xl, uint32_t le
             if (emit) img = t.slot[base + s * 64 + lane].image;
             uint64_t em = ballot(emit);
             while (em) {
-                const int b = __builtin_ctzll(em);
-                em &= em - 1;
-                const uint32_t im = rl32(img, b);
-                const uint32_t dst = produced + rl32(kr[s], b);
-                copy_row(t, im, recs + (uint64_t)dst * t.stride, lane);
+                uint32_t im4[4], d4[4];
+                int nk = 0;
+                for (; nk < 4 && em; ++nk) {
+                    const int b = __builtin_ctzll(em);
+                    em &= em - 1;
+                    im4[nk] = rl32(img, b);
+                    d4[nk] = produced + rl32(kr[s], b);
+                }
+                copy_rows4(t, im4, d4, nk, recs, lane);
             }
         }
         produced += e;
@@ -559,11 +579,11 @@ __global__ __launch_bounds__(256) void fill_kernel(uint8_t *__restrict__ heap, u
             d.kind = 0;
             d.mode = (uint32_t)ident_mode;
         }
-        uint4 *row = reinterpret_cast<uint4 *>(heap + (first + r) * stride);
+        u32x4 *row = reinterpret_cast<u32x4 *>(heap + (first + r) * stride);
         for (uint32_t c = lane; c < chunks; c += 64) {
             uint64_t w0 = c == 0 ? d.key_le : payload_word(d, arena, 2 * c - 1, payload_size);
             uint64_t w1 = payload_word(d, arena, 2 * c, payload_size);
-            row[c] = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
+            row[c] = u32x4{(uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32)};
         }
     }
 }
@@ -586,19 +606,21 @@ hipError_t launch_resolve(const DevTable &t, const uint64_t *keys, const uint16_
 }
 
 hipError_t launch_probe(const DevTable &t, const uint64_t *keys, const uint16_t *lens, const uint32_t *rids,
-                       const uint32_t *leaf_in, uint64_t n, stage_probe_out_dev *out, uint8_t *recs, hipStream_t s,
-                       const ProbeTuning &tune) {
+                        const uint32_t *leaf_in, uint64_t n, stage_probe_out_dev *out, uint8_t *recs, hipStream_t s,
+                        const ProbeTuning &tune) {
     if (n == 0) return hipSuccess;
     const uint64_t chunks = (n + 63) / 64;
-    const int blocks = grid_for(chunks, 4, tune.max_blocks > 0 ? tune.max_blocks : 4096);
+    const int blocks = grid_for(chunks, 4, tune.max_blocks > 0 ? tune.max_blocks : 16384);
     const bool var = t.key_width == 0;
 #define STAGE_PROBE(V, S, G) probe_kernel<V, S, G><<<blocks, 256, 0, s>>>(t, keys, lens, rids, leaf_in, n, out, recs)
     if (t.cap == 64) {
         if (var) STAGE_PROBE(true, 1, 4);
         else if (tune.group == 1) STAGE_PROBE(false, 1, 1);
         else if (tune.group == 2) STAGE_PROBE(false, 1, 2);
-        else if (tune.group == 8) STAGE_PROBE(false, 1, 8);
-        else STAGE_PROBE(false, 1, 4);
+        else if (tune.group == 4 && !tune.nt_store)
+            probe_kernel<false, 1, 4, false><<<blocks, 256, 0, s>>>(t, keys, lens, rids, leaf_in, n, out, recs);
+        else if (tune.group == 4) STAGE_PROBE(false, 1, 4);
+        else STAGE_PROBE(false, 1, 8);
     } else {
         if (var) STAGE_PROBE(true, 2, 4);
         else STAGE_PROBE(false, 2, 4);
@@ -608,7 +630,7 @@ hipError_t launch_probe(const DevTable &t, const uint64_t *keys, const uint16_t 
 }
 
 hipError_t launch_scan(const DevTable &t, const uint64_t *keys, const uint16_t *lens, uint64_t n, uint32_t scan_size,
-                      uint32_t *counts, uint8_t *recs, hipStream_t s) {
+                       uint32_t *counts, uint8_t *recs, hipStream_t s) {
     if (n == 0) return hipSuccess;
     const uint64_t chunks = (n + 63) / 64;
     const int blocks = grid_for(chunks, 4, 4096);
@@ -624,7 +646,7 @@ hipError_t launch_scan(const DevTable &t, const uint64_t *keys, const uint16_t *
 }
 
 hipError_t launch_murmur(const void *keys, uint32_t key_len, uint32_t key_stride, uint64_t seed, uint64_t n,
-                        uint64_t *out, hipStream_t s) {
+                         uint64_t *out, hipStream_t s) {
     if (n == 0) return hipSuccess;
     murmur_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>((const uint8_t *)keys, key_len, key_stride, seed, n, out);
     return hipGetLastError();

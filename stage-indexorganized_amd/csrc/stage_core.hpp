@@ -1,13 +1,15 @@
 // stage_core.hpp -- definitions shared by the host table builder and the gfx950 kernels.
 //
 // Device image of one index-organized table (DESIGN.md "Data layout in HBM"):
-//   okey[L*cap]    u64  order key of every leaf slot (coalesced key column, 512 B/leaf)
-//   slot[L*cap]    16 B {meta word, next handle, image id}  (read for the hit slot only)
-//   vis[L*cap/64]  u64  visible-slot masks (one wave-uniform scalar load per leaf)
-//   tree           u64  implicit 8-ary separator search tree (64-B nodes), all levels
-//   heap[I*stride] u8   record images [key padded to 8][payload] (current, copies, versions)
-//   chdr[C]        16 B overwrite-copy headers   (EphemeralPool::OverwriteVersionHeader)
-//   vhdr[V]        16 B retired-version headers  (TupleHeader)
+//   head[L]         cap+cap/8 B rounded to 128: 1-byte key fingerprint per slot, then the
+//                   visible-slot masks -- the only per-leaf bytes a point probe reads
+//   okey[L*cap]     u64  order key column (range scans read it whole, 512 B/leaf)
+//   slot[L*cap]     32 B {okey, meta word, next handle, image id} (probe: candidates only)
+//   tree            u64  implicit 16-ary separator tree (128-B nodes), all levels
+//   heap[I*hstride] u8   record images [key padded to 8][payload] (current, copies,
+//                   versions); rows 128-B aligned when larger than 128 B
+//   chdr[C]         16 B overwrite-copy headers   (EphemeralPool::OverwriteVersionHeader)
+//   vhdr[V]         16 B retired-version headers  (TupleHeader)
 #pragma once
 #include <cstdint>
 
@@ -63,12 +65,18 @@ STAGE_HD uint64_t key_bytes_from_order(uint64_t okey, uint32_t len) {
     return (bswap64(okey) ^ 0x8080808080808080ull) & mask;
 }
 
-// per-slot word read for the hit slot
-struct alignas(16) SlotInfo {
+// per-slot word, read by the fingerprint candidates of a probe
+struct alignas(32) SlotInfo {
+    uint64_t okey;  // order key (confirms a fingerprint match)
     uint64_t meta;  // reference RecordMetadata.meta
     uint32_t next;  // tagged next handle
     uint32_t image; // record-heap row of the current image
+    uint64_t pad;
 };
+
+// 1-byte key fingerprint stored per slot in the leaf head
+STAGE_HD uint32_t key_fp(uint64_t okey) { return (uint32_t)((okey * 0x9E3779B97F4A7C15ull) >> 56); }
+STAGE_HD uint32_t leaf_head_bytes(uint32_t cap) { return (cap + cap / 8 + 127u) & ~127u; }
 
 struct alignas(16) CopyHdr {  // EphemeralPool::OverwriteVersionHeader (ephemeral_pool.h:26-150)
     uint32_t rstamp;          // old cstamp (lower bound of the copy's visibility)
@@ -88,14 +96,14 @@ struct alignas(16) VersionHdr { // TupleHeader (version_store.h:28-155)
 enum : uint8_t { ST_NOT_FOUND = 0, ST_LATEST = 1, ST_COPY = 2, ST_OLD = 3, ST_FAIL_INVALID_TS = 4,
                  ST_CHAIN_MISS = 5 };
 
-constexpr int kTreeFanout = 8;         // keys per separator-tree node (one 64-B line)
+constexpr int kTreeFanout = 16;        // keys per separator-tree node (one 128-B line)
 constexpr int kMaxTreeLevels = 16;
 
 // Everything a kernel needs to read one table (passed by value).
 struct DevTable {
+    const uint8_t *head;        // [L * head_bytes]: fp[cap] then vis[cap/64]
     const uint64_t *okey;
     const SlotInfo *slot;
-    const uint64_t *vis;
     const uint64_t *tree;       // all levels, level 0 (leaf separators) first
     const uint8_t *tree_len;    // variable-length tables only: key length per tree entry
     const uint8_t *heap;
@@ -106,10 +114,11 @@ struct DevTable {
     uint32_t nleaves;
     uint32_t nseps;             // nleaves - 1
     uint32_t cap;               // slots per leaf (64 or 128)
-    uint32_t stride;            // heap/output row bytes (multiple of 16, >= 8 + payload)
+    uint32_t stride;            // output row bytes (multiple of 16, >= 8 + payload)
+    uint32_t hstride;           // heap row bytes (stride, rounded to 128 when above 128)
+    uint32_t head_bytes;        // bytes per leaf head
     uint32_t payload_size;
     uint32_t key_width;         // 0 = variable
-    uint32_t pad_;
 };
 
 }  // namespace stage

@@ -31,6 +31,7 @@ _SIG = {
     "orc_read_batch_timed": (u64, [vp, vp, u32, vp, u64, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]),
     "orc_scan": (u32, [vp, vp, u32, u32, vp]),
     "orc_scan_batch": (u64, [vp, vp, u32, u64, u32, vp, vp, ctypes.c_int]),
+    "orc_scan_batch_timed": (u64, [vp, vp, u32, u64, u32, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]),
     "orc_traverse_leaf_index": (ctypes.c_int64, [vp, vp, u32, ctypes.c_int]),
     "orc_update": (ctypes.c_int, [vp, vp, u32, u32, vp, u32, u32]),
     "orc_commit_update": (ctypes.c_int, [vp, vp, u32, u32, u32]),
