@@ -242,8 +242,12 @@ def main():
             draws = stage.zipf_draws(total_rows - 1, args.theta, args.seed + rank, B, nthreads=nthreads)
             rids = None
             n_ops = B
-        d_keys = stage.DeviceBuffer.from_numpy(draws)
-        d_rid = stage.DeviceBuffer.from_numpy(rids) if rids is not None else None
+        d_keys = stage.DeviceBuffer(B * 8)
+        check(L.stage_memcpy_h2d(d_keys.ptr, draws.ctypes.data, draws.nbytes, None), "h2d")
+        d_rid = None
+        if rids is not None:  # YCSB-B: the read share varies per epoch, buffers hold a whole batch
+            d_rid = stage.DeviceBuffer(B * 4)
+            check(L.stage_memcpy_h2d(d_rid.ptr, rids.ctypes.data, rids.nbytes, None), "h2d")
         d_out = stage.DeviceBuffer(B * 32)
         d_rec = stage.DeviceBuffer(B * tab.stride)
     d_leaf = None
