@@ -163,6 +163,8 @@ class YcsbB:
         self.epoch = 0
         self.updates = 0
         self.host_s = 0.0
+        self.sync_s = 0.0
+        self.last_sync = None
 
     def next_batch(self):
         a = self.args
@@ -171,18 +173,19 @@ class YcsbB:
         rng = np.random.default_rng(a.seed + self.epoch)
         is_upd = rng.random(a.batch) < a.update_ratio
         t0 = time.time()
-        first_id = self.counter
-        col = np.full(100, 0, np.uint8)
-        for k in draws[is_upd]:
-            rid = self.counter
-            cid = self.counter + 1
-            self.counter += 2
-            col[:] = (int(k) + self.epoch + 1) & 0xFF
-            rc = self.tab.update(int(k), 0, col.tobytes(), rid)
-            if rc == stage.RC_OK:
-                self.tab.commit_update(int(k), cid, cid)
-                self.updates += 1
+        keys = draws[is_upd]
+        m = keys.size
+        # read id / commit id pairs from one counter (tid_counter), one 100-B column patch each
+        rid = (self.counter + 2 * np.arange(m, dtype=np.uint64)).astype(np.uint32)
+        cid = rid + np.uint32(1)
+        self.counter += 2 * m
+        cols = np.repeat(((keys + np.uint64(self.epoch + 1)) & np.uint64(0xFF)).astype(np.uint8)[:, None], 100, 1)
+        _, ok = self.tab.update_batch(keys, 0, cols, rid, cid)
+        self.updates += ok
+        t1 = time.time()
         self.tab.sync()
+        self.sync_s += time.time() - t1
+        self.last_sync = self.tab.sync_info()
         self.host_s += time.time() - t0
         reads = draws[~is_upd]
         rids = np.full(reads.size, self.counter, np.uint32)
@@ -370,7 +373,10 @@ def main():
             config["theta"] = args.theta
         if ycsb_b is not None:
             config.update({"update_ratio": args.update_ratio, "updates_applied": ycsb_b.updates,
-                           "host_write_and_publish_s": round(ycsb_b.host_s, 1),
+                           "host_write_and_publish_s": round(ycsb_b.host_s, 2),
+                           "publish_s": round(ycsb_b.sync_s, 3), "last_publish": ycsb_b.last_sync,
+                           "ops_per_s_incl_host_writes": round((ops_done + ycsb_b.updates) /
+                                                               (elapsed + ycsb_b.host_s), 1),
                            "read_status_counts": {"latest": int(status_hist[1]), "copy": int(status_hist[2]),
                                                   "old": int(status_hist[3]), "fail": int(status_hist[4]),
                                                   "chain_miss": int(status_hist[5]),

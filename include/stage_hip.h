@@ -111,10 +111,22 @@ int stage_finalize_update(stage_table *t, uint64_t key, uint16_t key_size, uint3
                           uint8_t *rc_out);
 int stage_delete(stage_table *t, uint64_t key, uint16_t key_size, uint32_t commit_id,
                  uint8_t *rc_out);
+/* batched write path of one transaction epoch (the YCSB-B writers, ycsb.cpp:200-260): for
+ * key i, stage_update(keys[i], payload_off, deltas + i*delta_len, writer_ids[i]) and, when it
+ * succeeded and commit_ids[i] != 0, stage_commit_update(keys[i], commit_ids[i], sstamps[i]
+ * (or commit_ids[i] when sstamps is NULL)).  rc_out[i] (optional) = the last ReturnCode;
+ * *n_ok (optional) = keys whose update (and commit) returned STAGE_RC_OK. */
+int stage_update_batch(stage_table *t, const uint64_t *keys, uint64_t n, uint16_t key_size,
+                       uint32_t payload_off, const uint8_t *deltas, uint32_t delta_len,
+                       const uint32_t *writer_ids, const uint32_t *commit_ids,
+                       const uint32_t *sstamps, uint8_t *rc_out, uint64_t *n_ok);
 
 /* publish the host layout to HBM (leaf key columns, slot words, visibility masks, the
  * separator search tree, record heap, overwrite copies and retired versions). */
 int stage_sync(stage_table *t);
+/* what the last stage_sync did: info[0] = 1 if it patched in place (no split since the
+ * previous publish), info[1] = leaves re-headed, info[2] = slots patched; *seconds = wall time */
+int stage_sync_info(stage_table *t, double *seconds, uint64_t *info);
 
 /* stats[0]=height(host equivalent: 1 + ceil(log_fanout)) stats[1]=0 stats[2]=leaves
  * stats[3]=records stats[4]=sorted slots stats[5]=unsorted slots stats[6]=max records/leaf

@@ -138,6 +138,18 @@ int stage_commit_update(stage_table *t, uint64_t key, uint16_t key_size, uint32_
     });
 }
 
+int stage_update_batch(stage_table *t, const uint64_t *keys, uint64_t n, uint16_t key_size, uint32_t payload_off,
+                       const uint8_t *deltas, uint32_t delta_len, const uint32_t *writer_ids,
+                       const uint32_t *commit_ids, const uint32_t *sstamps, uint8_t *rc_out, uint64_t *n_ok) {
+    if (!t || (n && (!keys || !writer_ids || (!deltas && delta_len)))) return fail(STAGE_E_ARG, "bad arguments");
+    return guarded([&] {
+        uint64_t ok = t->host->update_batch(keys, n, key_size, payload_off, deltas, delta_len, writer_ids, commit_ids,
+                                            sstamps, rc_out);
+        if (n_ok) *n_ok = ok;
+        return STAGE_OK;
+    });
+}
+
 int stage_finalize_update(stage_table *t, uint64_t key, uint16_t key_size, uint32_t commit_id, uint8_t *rc_out) {
     if (!t) return fail(STAGE_E_ARG, "null table");
     return guarded([&] {
@@ -162,6 +174,17 @@ int stage_sync(stage_table *t) {
         stage::sync_device(*t->host, t->dev);
         return STAGE_OK;
     });
+}
+
+int stage_sync_info(stage_table *t, double *seconds, uint64_t *info) {
+    if (!t) return fail(STAGE_E_ARG, "null table");
+    if (seconds) *seconds = t->dev.last_sync_seconds;
+    if (info) {
+        info[0] = t->dev.last_sync_incremental ? 1 : 0;
+        info[1] = t->dev.last_patch_leaves;
+        info[2] = t->dev.last_patch_slots;
+    }
+    return STAGE_OK;
 }
 
 int stage_stats(stage_table *t, uint64_t *stats) {

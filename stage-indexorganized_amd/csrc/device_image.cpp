@@ -27,7 +27,7 @@ static void dev_ensure(DevBuf &b, uint64_t bytes, const char *what) {
 DeviceImage::~DeviceImage() { release(); }
 
 void DeviceImage::release() {
-    for (DevBuf *b : {&head, &okey, &slot, &tree, &tree_len, &heap, &chdr, &vhdr, &arena, &descs}) {
+    for (DevBuf *b : {&head, &okey, &slot, &tree, &tree_len, &heap, &chdr, &vhdr, &arena, &descs, &patch}) {
         if (b->p) (void)hipFree(b->p);
         b->p = nullptr;
         b->cap = 0;
@@ -55,98 +55,108 @@ static void upload(DevBuf &b, const void *src, uint64_t bytes, hipStream_t s, co
     if (bytes) hip_check(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, s), what);
 }
 
-void sync_device(HostTable &h, DeviceImage &d) {
-    auto t0 = std::chrono::steady_clock::now();
-    hip_check(hipSetDevice(d.device), "hipSetDevice");
-    if (!d.stream) hip_check(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking), "hipStreamCreate");
+// One leaf's head (fingerprints + visible mask) and slot words, reference slot order.
+static void build_leaf(const HostTable &h, uint32_t hl, uint8_t *hd, uint64_t *okey, SlotInfo *slot) {
     const stage_params &p = h.params();
-    const uint32_t cap = h.cap(), spl = cap / 64;
-
-    // ---- leaves in key order
-    std::vector<uint32_t> order;
-    h.key_order(order);
-    const uint64_t L = order.size();
-    d.host_to_dev.assign(h.leaves_.size(), 0xFFFFFFFFu);
-    for (uint64_t i = 0; i < L; ++i) d.host_to_dev[order[i]] = (uint32_t)i;
-
-    const uint32_t hb = leaf_head_bytes(cap);
-    std::vector<uint64_t> okey(L * cap);
-    std::vector<uint8_t> head(L * hb, 0);
-    std::vector<SlotInfo> slot(L * cap);
-    parallel_for(L, [&](uint64_t di) {
-        const uint64_t hbase = (uint64_t)order[di] * cap, db = di * cap;
-        const uint32_t count = h.leaves_[order[di]].count;
-        uint8_t *hd = head.data() + di * hb;
-        uint64_t vis[2] = {0, 0};
-        for (uint32_t s = 0; s < cap; ++s) {
-            const bool live = s < count;
-            const uint64_t m = live ? h.meta_[hbase + s] : 0;
-            const uint64_t ok = live ? h.okey_[hbase + s] : 0;
-            okey[db + s] = ok;
-            slot[db + s].okey = ok;
-            slot[db + s].meta = m;
-            slot[db + s].next = live ? h.next_[hbase + s] : 0;
-            slot[db + s].image = live ? h.image_[hbase + s] : 0;
-            slot[db + s].pad = 0;
-            if (meta_visible(m) && (p.key_width == 0 || meta_keylen(m) == p.key_width)) {
-                vis[s / 64] |= 1ull << (s % 64);
-                hd[s] = (uint8_t)key_fp(ok);
-            }
-        }
-        std::memcpy(hd + cap, vis, 8 * spl);
-    });
-
-    // ---- implicit 16-ary separator tree: level 0 = separators, level k+1 = max of each
-    // 16-entry node of level k, every level padded with +inf, top level one node.
-    const uint64_t S = L ? L - 1 : 0;
-    std::vector<std::vector<uint64_t>> lv;
-    std::vector<std::vector<uint8_t>> lvlen;
-    {
-        const uint64_t n0 = (S + 1 + kTreeFanout - 1) / kTreeFanout * kTreeFanout;
-        std::vector<uint64_t> l0(n0, ~0ull);
-        std::vector<uint8_t> l0len(n0, 0xFF);
-        for (uint64_t i = 0; i < S; ++i) {
-            const auto &sep = h.leaves_[order[i]].sep;
-            l0[i] = sep.okey;
-            l0len[i] = (uint8_t)sep.len;
-        }
-        lv.push_back(std::move(l0));
-        lvlen.push_back(std::move(l0len));
-        while (lv.back().size() > (uint64_t)kTreeFanout) {
-            const auto &prev = lv.back();
-            const auto &prevlen = lvlen.back();
-            const uint64_t nodes = prev.size() / kTreeFanout;
-            const uint64_t nn = (nodes + kTreeFanout - 1) / kTreeFanout * kTreeFanout;
-            std::vector<uint64_t> nx(nn, ~0ull);
-            std::vector<uint8_t> nxlen(nn, 0xFF);
-            for (uint64_t j = 0; j < nodes; ++j) {
-                nx[j] = prev[j * kTreeFanout + kTreeFanout - 1];
-                nxlen[j] = prevlen[j * kTreeFanout + kTreeFanout - 1];
-            }
-            lv.push_back(std::move(nx));
-            lvlen.push_back(std::move(nxlen));
+    const uint32_t cap = h.cap(), spl = cap / 64, hb = leaf_head_bytes(cap);
+    const uint64_t hbase = (uint64_t)hl * cap;
+    const uint32_t count = h.leaves_[hl].count;
+    std::memset(hd, 0, hb);
+    uint64_t vis[2] = {0, 0};
+    for (uint32_t s = 0; s < cap; ++s) {
+        const bool live = s < count;
+        const uint64_t m = live ? h.meta_[hbase + s] : 0;
+        const uint64_t ok = live ? h.okey_[hbase + s] : 0;
+        okey[s] = ok;
+        slot[s].okey = ok;
+        slot[s].meta = m;
+        slot[s].next = live ? h.next_[hbase + s] : 0;
+        slot[s].image = live ? h.image_[hbase + s] : 0;
+        slot[s].pad = 0;
+        if (meta_visible(m) && (p.key_width == 0 || meta_keylen(m) == p.key_width)) {
+            vis[s / 64] |= 1ull << (s % 64);
+            hd[s] = (uint8_t)key_fp(ok);
         }
     }
-    if (lv.size() > (size_t)kMaxTreeLevels) throw std::runtime_error("separator tree too deep");
-    std::vector<uint64_t> tree;
-    std::vector<uint8_t> tree_len;
-    uint64_t level_off[kMaxTreeLevels] = {0};
-    for (size_t k = 0; k < lv.size(); ++k) {
-        level_off[k] = tree.size();
-        tree.insert(tree.end(), lv[k].begin(), lv[k].end());
-        tree_len.insert(tree_len.end(), lvlen[k].begin(), lvlen[k].end());
+    std::memcpy(hd + cap, vis, 8 * spl);
+}
+
+// Copy/version headers: append the new tail, re-send the rewritten range of copy headers.
+static void sync_headers(HostTable &h, DeviceImage &d, hipStream_t s) {
+    const uint64_t nc = h.copies_.size(), nv = h.versions_.size();
+    auto grow = [&](DevBuf &b, uint64_t bytes, uint64_t keep, const char *what) {
+        if (b.cap >= bytes && b.p) return;
+        DevBuf nb;
+        const uint64_t want = std::max<uint64_t>(bytes + bytes / 4, 4096);
+        hip_check(hipMalloc(&nb.p, want), what);
+        nb.cap = want;
+        if (b.p && keep) hip_check(hipMemcpyAsync(nb.p, b.p, keep, hipMemcpyDeviceToDevice, s), what);
+        hip_check(hipStreamSynchronize(s), what);
+        if (b.p) hip_check(hipFree(b.p), "hipFree hdr");
+        b = nb;
+    };
+    grow(d.chdr, nc * sizeof(CopyHdr), h.copies_synced_ * sizeof(CopyHdr), "chdr");
+    grow(d.vhdr, nv * sizeof(VersionHdr), h.versions_synced_ * sizeof(VersionHdr), "vhdr");
+    const uint64_t c0 = std::min<uint64_t>(h.copies_synced_, h.copies_dirty_from_);
+    if (nc > c0)
+        hip_check(hipMemcpyAsync((CopyHdr *)d.chdr.p + c0, h.copies_.data() + c0, (nc - c0) * sizeof(CopyHdr),
+                                 hipMemcpyHostToDevice, s),
+                  "chdr upload");
+    if (nv > h.versions_synced_)
+        hip_check(hipMemcpyAsync((VersionHdr *)d.vhdr.p + h.versions_synced_, h.versions_.data() + h.versions_synced_,
+                                 (nv - h.versions_synced_) * sizeof(VersionHdr), hipMemcpyHostToDevice, s),
+                  "vhdr upload");
+    h.copies_synced_ = nc;
+    h.versions_synced_ = nv;
+    h.copies_dirty_from_ = ~0ull;
+}
+
+// Incremental publish (no split since the last publish): leaf order and separators are
+// unchanged, so only the written slots and their leaves' heads are patched in place.
+static void patch_device(HostTable &h, DeviceImage &d, hipStream_t s) {
+    const uint32_t cap = h.cap(), hb = leaf_head_bytes(cap);
+    std::vector<uint64_t> &ds = h.dirty_slots_;
+    std::sort(ds.begin(), ds.end());
+    ds.erase(std::unique(ds.begin(), ds.end()), ds.end());
+    std::vector<uint32_t> leaves;
+    for (uint64_t x : ds)
+        if (leaves.empty() || leaves.back() != x / cap) leaves.push_back((uint32_t)(x / cap));
+    const uint64_t nl = leaves.size(), ns = ds.size();
+    if (nl == 0) return;
+    // staging: [dev leaf u32 ...][heads nl*hb][slot idx u64 ...][SlotInfo ...], 32-B aligned parts
+    auto al = [](uint64_t x) { return (x + 31) & ~31ull; };
+    const uint64_t o_head = al(nl * 4), o_idx = o_head + al(nl * hb), o_src = o_idx + al(ns * 8);
+    const uint64_t bytes = o_src + ns * sizeof(SlotInfo);
+    d.staging.resize(bytes);
+    uint8_t *st = d.staging.data();
+    uint32_t *dleaf = (uint32_t *)st;
+    uint64_t *sidx = (uint64_t *)(st + o_idx);
+    SlotInfo *ssrc = (SlotInfo *)(st + o_src);
+    std::vector<uint64_t> okey_tmp(cap);
+    std::vector<SlotInfo> slot_tmp(cap);
+    uint64_t k = 0;
+    for (uint64_t li = 0; li < nl; ++li) {
+        const uint32_t hl = leaves[li], dl = d.host_to_dev[hl];
+        dleaf[li] = dl;
+        build_leaf(h, hl, st + o_head + li * hb, okey_tmp.data(), slot_tmp.data());
+        for (; k < ns && ds[k] / cap == hl; ++k) {
+            const uint32_t sl = (uint32_t)(ds[k] % cap);
+            sidx[k] = (uint64_t)dl * cap + sl;
+            ssrc[k] = slot_tmp[sl];
+        }
     }
+    upload(d.patch, st, bytes, s, "patch staging");
+    uint8_t *dp = (uint8_t *)d.patch.p;
+    hip_check(launch_patch((uint8_t *)d.head.p, (uint64_t *)d.okey.p, (SlotInfo *)d.slot.p, hb, (const uint32_t *)dp,
+                           dp + o_head, nl, (const uint64_t *)(dp + o_idx), (const SlotInfo *)(dp + o_src), ns, s),
+              "patch");
+    d.last_patch_leaves = nl;
+    d.last_patch_slots = ns;
+}
 
-    hipStream_t s = d.stream;
-    upload(d.head, head.data(), head.size(), s, "head");
-    upload(d.okey, okey.data(), okey.size() * 8, s, "okey");
-    upload(d.slot, slot.data(), slot.size() * sizeof(SlotInfo), s, "slot");
-    upload(d.tree, tree.data(), tree.size() * 8, s, "tree");
-    upload(d.tree_len, tree_len.data(), tree_len.size(), s, "tree_len");
-    upload(d.chdr, h.copies_.data(), h.copies_.size() * sizeof(CopyHdr), s, "chdr");
-    upload(d.vhdr, h.versions_.data(), h.versions_.size() * sizeof(VersionHdr), s, "vhdr");
-
-    // ---- record heap: fill the rows of images created since the last sync
+// ---- record heap: fill the rows of images created since the last sync
+static void sync_heap(HostTable &h, DeviceImage &d, hipStream_t s) {
+    const stage_params &p = h.params();
     const uint32_t stride = h.hstride();
     const uint64_t nimg = h.images_.size();
     if (nimg > d.heap_rows) {
@@ -211,9 +221,97 @@ void sync_device(HostTable &h, DeviceImage &d) {
             hip_check(launch_fill((uint8_t *)d.heap.p, stride, p.payload_size, (const ImageDescDev *)d.descs.p,
                                   (const uint8_t *)d.arena.p, first, count, 0, 0, 0, s),
                       "fill");
+            hip_check(hipStreamSynchronize(s), "fill sync");  // dd is pageable and local
         }
         h.images_synced_ = nimg;
     }
+}
+
+void sync_device(HostTable &h, DeviceImage &d) {
+    auto t0 = std::chrono::steady_clock::now();
+    hip_check(hipSetDevice(d.device), "hipSetDevice");
+    if (!d.stream) hip_check(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking), "hipStreamCreate");
+    hipStream_t s = d.stream;
+    if (d.valid && !h.structure_dirty_ && d.host_to_dev.size() == h.leaves_.size()) {
+        patch_device(h, d, s);
+        sync_headers(h, d, s);
+        sync_heap(h, d, s);
+        hip_check(hipStreamSynchronize(s), "sync");
+        d.view.heap = (const uint8_t *)d.heap.p;
+        d.view.chdr = (const CopyHdr *)d.chdr.p;
+        d.view.vhdr = (const VersionHdr *)d.vhdr.p;
+        h.dirty_slots_.clear();
+        h.layout_dirty_ = false;
+        d.last_sync_incremental = true;
+        d.last_sync_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        return;
+    }
+    const stage_params &p = h.params();
+    const uint32_t cap = h.cap();
+
+    // ---- leaves in key order
+    std::vector<uint32_t> order;
+    h.key_order(order);
+    const uint64_t L = order.size();
+    d.host_to_dev.assign(h.leaves_.size(), 0xFFFFFFFFu);
+    for (uint64_t i = 0; i < L; ++i) d.host_to_dev[order[i]] = (uint32_t)i;
+
+    const uint32_t hb = leaf_head_bytes(cap);
+    std::vector<uint64_t> okey(L * cap);
+    std::vector<uint8_t> head(L * hb, 0);
+    std::vector<SlotInfo> slot(L * cap);
+    parallel_for(L, [&](uint64_t di) {
+        build_leaf(h, order[di], head.data() + di * hb, okey.data() + di * cap, slot.data() + di * cap);
+    });
+
+    // ---- implicit 16-ary separator tree: level 0 = separators, level k+1 = max of each
+    // 16-entry node of level k, every level padded with +inf, top level one node.
+    const uint64_t S = L ? L - 1 : 0;
+    std::vector<std::vector<uint64_t>> lv;
+    std::vector<std::vector<uint8_t>> lvlen;
+    {
+        const uint64_t n0 = (S + 1 + kTreeFanout - 1) / kTreeFanout * kTreeFanout;
+        std::vector<uint64_t> l0(n0, ~0ull);
+        std::vector<uint8_t> l0len(n0, 0xFF);
+        for (uint64_t i = 0; i < S; ++i) {
+            const auto &sep = h.leaves_[order[i]].sep;
+            l0[i] = sep.okey;
+            l0len[i] = (uint8_t)sep.len;
+        }
+        lv.push_back(std::move(l0));
+        lvlen.push_back(std::move(l0len));
+        while (lv.back().size() > (uint64_t)kTreeFanout) {
+            const auto &prev = lv.back();
+            const auto &prevlen = lvlen.back();
+            const uint64_t nodes = prev.size() / kTreeFanout;
+            const uint64_t nn = (nodes + kTreeFanout - 1) / kTreeFanout * kTreeFanout;
+            std::vector<uint64_t> nx(nn, ~0ull);
+            std::vector<uint8_t> nxlen(nn, 0xFF);
+            for (uint64_t j = 0; j < nodes; ++j) {
+                nx[j] = prev[j * kTreeFanout + kTreeFanout - 1];
+                nxlen[j] = prevlen[j * kTreeFanout + kTreeFanout - 1];
+            }
+            lv.push_back(std::move(nx));
+            lvlen.push_back(std::move(nxlen));
+        }
+    }
+    if (lv.size() > (size_t)kMaxTreeLevels) throw std::runtime_error("separator tree too deep");
+    std::vector<uint64_t> tree;
+    std::vector<uint8_t> tree_len;
+    uint64_t level_off[kMaxTreeLevels] = {0};
+    for (size_t k = 0; k < lv.size(); ++k) {
+        level_off[k] = tree.size();
+        tree.insert(tree.end(), lv[k].begin(), lv[k].end());
+        tree_len.insert(tree_len.end(), lvlen[k].begin(), lvlen[k].end());
+    }
+
+    upload(d.head, head.data(), head.size(), s, "head");
+    upload(d.okey, okey.data(), okey.size() * 8, s, "okey");
+    upload(d.slot, slot.data(), slot.size() * sizeof(SlotInfo), s, "slot");
+    upload(d.tree, tree.data(), tree.size() * 8, s, "tree");
+    upload(d.tree_len, tree_len.data(), tree_len.size(), s, "tree_len");
+    sync_headers(h, d, s);
+    sync_heap(h, d, s);
     hip_check(hipStreamSynchronize(s), "sync");
 
     DevTable &v = d.view;
@@ -231,12 +329,16 @@ void sync_device(HostTable &h, DeviceImage &d) {
     v.nseps = (uint32_t)S;
     v.cap = cap;
     v.stride = h.stride();
-    v.hstride = stride;
+    v.hstride = h.hstride();
     v.head_bytes = hb;
     v.payload_size = p.payload_size;
     v.key_width = p.key_width;
     h.layout_dirty_ = false;
+    h.structure_dirty_ = false;
+    h.dirty_slots_.clear();
     d.valid = true;
+    d.last_sync_incremental = false;
+    d.last_patch_leaves = d.last_patch_slots = 0;
     d.last_sync_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 

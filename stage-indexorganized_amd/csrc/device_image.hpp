@@ -19,12 +19,15 @@ struct DevBuf {
 struct DeviceImage {
     int device = 0;
     hipStream_t stream = nullptr;
-    DevBuf head, okey, slot, tree, tree_len, heap, chdr, vhdr, arena, descs;
+    DevBuf head, okey, slot, tree, tree_len, heap, chdr, vhdr, arena, descs, patch;
+    std::vector<uint8_t> staging;  // host staging of incremental patches
     uint64_t heap_rows = 0;  // rows the heap buffer can hold
     DevTable view{};
     std::vector<uint32_t> host_to_dev;  // host leaf id -> leaf index in key order
     bool valid = false;
     double last_sync_seconds = 0;
+    bool last_sync_incremental = false;
+    uint64_t last_patch_leaves = 0, last_patch_slots = 0;
 
     ~DeviceImage();
     void release();

@@ -46,23 +46,72 @@ __device__ __forceinline__ uint64_t mm64a_8(uint64_t k) {
     return h;
 }
 
-__global__ void route_count(const uint64_t *__restrict__ keys, uint64_t n, int world, uint32_t *__restrict__ dest,
-                            uint32_t *__restrict__ counts) {
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    uint32_t d = (uint32_t)(mm64a_8(keys[i]) % (uint64_t)world);
-    dest[i] = d;
-    atomicAdd(&counts[d], 1u);
+// Routing without global atomics: per-block LDS histograms (blk[d*NB + b]), one exclusive
+// scan over them (dest-major, so offsets come out grouped by destination rank), then a
+// scatter that claims positions with LDS atomics inside each block's range.
+constexpr int kRouteBlocks = 1024;
+constexpr int kMaxWorld = 64;
+
+__global__ __launch_bounds__(256) void route_hist(const uint64_t *__restrict__ keys, uint64_t n, int world,
+                                                  uint8_t *__restrict__ dest, uint32_t *__restrict__ blk) {
+    __shared__ uint32_t h[kMaxWorld];
+    if (threadIdx.x < (unsigned)world) h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const uint64_t b0 = (uint64_t)blockIdx.x * per, b1 = b0 + per < n ? b0 + per : n;
+    for (uint64_t i = b0 + threadIdx.x; i < b1; i += blockDim.x) {
+        const uint32_t d = (uint32_t)(mm64a_8(keys[i]) % (uint64_t)world);
+        dest[i] = (uint8_t)d;
+        atomicAdd(&h[d], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < (unsigned)world) blk[threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];
 }
 
-__global__ void route_scatter(const uint64_t *__restrict__ keys, const uint32_t *__restrict__ rids, uint64_t n,
-                              const uint32_t *__restrict__ dest, uint32_t *__restrict__ cursor,
-                              SendRec *__restrict__ send, uint32_t *__restrict__ perm) {
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    uint32_t pos = atomicAdd(&cursor[dest[i]], 1u);
-    send[pos] = SendRec{keys[i], rids ? rids[i] : 0xFFFFFFFEu, 0};
-    perm[pos] = (uint32_t)i;
+// exclusive scan of m = world*NB counters in one 1024-thread block; counts[d] = per-rank totals
+__global__ __launch_bounds__(1024) void route_scan(const uint32_t *__restrict__ blk, uint32_t m, int world, int nb,
+                                                   uint32_t *__restrict__ offs, uint32_t *__restrict__ counts) {
+    __shared__ uint32_t part[1024];
+    const uint32_t per = (m + 1023) / 1024;
+    const uint32_t b0 = threadIdx.x * per, b1 = b0 + per < m ? b0 + per : m;
+    uint32_t s = 0;
+    for (uint32_t i = b0; i < b1; ++i) s += blk[i];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
+        const uint32_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0u;
+        __syncthreads();
+        part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint32_t run = threadIdx.x ? part[threadIdx.x - 1] : 0u;
+    for (uint32_t i = b0; i < b1; ++i) {
+        offs[i] = run;
+        run += blk[i];
+    }
+    if (threadIdx.x == 1023) offs[m] = part[1023];
+    __syncthreads();
+    if (threadIdx.x < (unsigned)world) {
+        const uint32_t lo = offs[threadIdx.x * nb];
+        const uint32_t hi = (int)threadIdx.x + 1 < world ? offs[(threadIdx.x + 1) * nb] : part[1023];
+        counts[threadIdx.x] = hi - lo;
+    }
+}
+
+__global__ __launch_bounds__(256) void route_scatter(const uint64_t *__restrict__ keys, const uint32_t *__restrict__ rids,
+                                                     uint64_t n, int world, const uint8_t *__restrict__ dest,
+                                                     const uint32_t *__restrict__ offs, SendRec *__restrict__ send,
+                                                     uint32_t *__restrict__ perm) {
+    __shared__ uint32_t cur[kMaxWorld];
+    if (threadIdx.x < (unsigned)world) cur[threadIdx.x] = offs[threadIdx.x * gridDim.x + blockIdx.x];
+    __syncthreads();
+    const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const uint64_t b0 = (uint64_t)blockIdx.x * per, b1 = b0 + per < n ? b0 + per : n;
+    for (uint64_t i = b0 + threadIdx.x; i < b1; i += blockDim.x) {
+        const uint32_t pos = atomicAdd(&cur[dest[i]], 1u);
+        send[pos] = SendRec{keys[i], rids ? rids[i] : 0xFFFFFFFEu, 0};
+        perm[pos] = (uint32_t)i;
+    }
 }
 
 __global__ void unpack_keys(const SendRec *__restrict__ recv, uint64_t n, uint64_t *__restrict__ keys,
@@ -121,7 +170,9 @@ int shard_init(ShardComm &c, const uint8_t *id128, int rank, int world) {
     c.comm = comm;
     c.rank = rank;
     c.world = world;
+    if (world > kMaxWorld) throw std::invalid_argument("world size above 64");
     grow(c.cnt, 4 * sizeof(uint32_t) * (uint64_t)world);
+    grow(c.cursor, (2ull * world * kRouteBlocks + 16) * sizeof(uint32_t));
     return STAGE_OK;
 }
 
@@ -132,7 +183,7 @@ int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const 
     if (n > 0xFFFFFFFFull) throw std::invalid_argument("batch too large");
     if (n > c.cap_local || stride != c.rec_stride) {
         const uint64_t cap = n + n / 8 + 1024;
-        grow(c.dest, cap * 4);
+        grow(c.dest, cap);
         grow(c.perm, cap * 4);
         grow(c.send, cap * sizeof(SendRec));
         grow(c.bout, cap * sizeof(stage_probe_out_dev));
@@ -140,19 +191,21 @@ int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const 
         c.cap_local = cap;
         c.rec_stride = stride;
     }
-    uint32_t *counts = (uint32_t *)c.cnt;  // [0,W) send counts, [W,2W) cursor, [2W,3W) recv counts
-    chk(hipMemsetAsync(counts, 0, 2 * W * sizeof(uint32_t), s), "memset");
-    const unsigned blocks = (unsigned)((n + 255) / 256);
-    if (n) route_count<<<blocks, 256, 0, s>>>(d_keys, n, W, (uint32_t *)c.dest, counts);
+    uint32_t *counts = (uint32_t *)c.cnt;  // [0,W) send counts, [2W,3W) recv counts
+    uint32_t *blk = (uint32_t *)c.cursor, *offs = blk + (uint64_t)W * kRouteBlocks;
+    if (n) {
+        route_hist<<<kRouteBlocks, 256, 0, s>>>(d_keys, n, W, (uint8_t *)c.dest, blk);
+        route_scan<<<1, 1024, 0, s>>>(blk, (uint32_t)(W * kRouteBlocks), W, kRouteBlocks, offs, counts);
+        route_scatter<<<kRouteBlocks, 256, 0, s>>>(d_keys, d_rids, n, W, (const uint8_t *)c.dest, offs,
+                                                   (SendRec *)c.send, (uint32_t *)c.perm);
+    } else {
+        chk(hipMemsetAsync(counts, 0, W * sizeof(uint32_t), s), "memset");
+    }
     std::vector<uint32_t> sc(W), rc(W);
     chk(hipMemcpyAsync(sc.data(), counts, W * 4, hipMemcpyDeviceToHost, s), "counts d2h");
     chk(hipStreamSynchronize(s), "sync");
     std::vector<uint32_t> soff(W + 1, 0);
     for (int r = 0; r < W; ++r) soff[r + 1] = soff[r] + sc[r];
-    chk(hipMemcpyAsync(counts + W, soff.data(), W * 4, hipMemcpyHostToDevice, s), "cursor h2d");
-    if (n)
-        route_scatter<<<blocks, 256, 0, s>>>(d_keys, d_rids, n, (const uint32_t *)c.dest, counts + W,
-                                             (SendRec *)c.send, (uint32_t *)c.perm);
     // exchange the per-destination counts
     ncclComm_t comm = (ncclComm_t)c.comm;
     nchk(ncclAllToAll(counts, counts + 2 * W, 1, ncclUint32, comm, s), "ncclAllToAll counts");

@@ -163,7 +163,7 @@ int HostTable::insert(uint64_t key_le, uint32_t len, const uint8_t *payload, uin
         meta_[i] = ((uint64_t)len << 48) | kMetaVisible | (offset << 32) | commit_id;
         next_[i] = 0;
         image_[i] = new_image(key_le, payload, gen_rowid, mode);
-        layout_dirty_ = true;
+        touch(leaf, slot);
         return STAGE_RC_OK;
     }
     return STAGE_RC_RETRY_FAILURE;
@@ -239,6 +239,8 @@ bool HostTable::split(uint32_t p) {
     P.next = (int32_t)r;
     route_split(p, r, lo_inf ? Key{0, 0} : lo, sep, hi);
     layout_dirty_ = true;
+    structure_dirty_ = true;
+    dirty_slots_.clear();
     return true;
 }
 
@@ -317,7 +319,7 @@ int HostTable::update(uint64_t key_le, uint32_t len, uint32_t payload_off, const
     next_[i] = kNextCopy | (uint32_t)(copies_.size() - 1);
     std::memcpy(pay.data() + payload_off, delta, delta_len);  // CopyPayload
     image_[i] = new_image(images_[image_[i]].key_le, pay.data(), 0, 0);
-    layout_dirty_ = true;
+    touch(leaf, slot);
     return STAGE_RC_OK;
 }
 
@@ -327,8 +329,10 @@ int HostTable::commit_update(uint64_t key_le, uint32_t len, uint32_t commit_id, 
     if (find(key_le, len, &leaf, &slot) < 0) return STAGE_RC_NOT_FOUND;
     const size_t i = (size_t)leaf * cap_ + slot;
     if (!meta_inserting(meta_[i]) || (next_[i] & kNextKindMask) != kNextCopy) return STAGE_RC_NOT_FOUND;
-    CopyHdr &c = copies_[next_[i] & kNextIndexMask];
+    const uint64_t ci = next_[i] & kNextIndexMask;
+    CopyHdr &c = copies_[ci];
     c.sstamp = sstamp;
+    if (ci < copies_dirty_from_) copies_dirty_from_ = ci;
     VersionHdr v;
     v.begin_id = c.rstamp;
     v.comm_id = c.sstamp;
@@ -339,7 +343,7 @@ int HostTable::commit_update(uint64_t key_le, uint32_t len, uint32_t commit_id, 
     uint64_t m = (meta_[i] & ~kMetaTxn) | commit_id;  // FinalizeForUpdate(t_cstamp)
     meta_[i] = m & ~kMetaControl;
     next_[i] = kNextVersion | (uint32_t)(versions_.size() - 1);
-    layout_dirty_ = true;
+    touch(leaf, slot);
     return STAGE_RC_OK;
 }
 
@@ -349,7 +353,7 @@ int HostTable::finalize_update(uint64_t key_le, uint32_t len, uint32_t commit_id
     if (find(key_le, len, &leaf, &slot) < 0) return STAGE_RC_NOT_FOUND;
     const size_t i = (size_t)leaf * cap_ + slot;
     meta_[i] = ((meta_[i] & ~kMetaTxn) | commit_id) & ~kMetaControl;
-    layout_dirty_ = true;
+    touch(leaf, slot);
     return STAGE_RC_OK;
 }
 
@@ -372,10 +376,25 @@ int HostTable::remove(uint64_t key_le, uint32_t len, uint32_t commit_id) {
     meta_[i] = 0;
     Leaf &L = leaves_[leaf];
     L.deleted += pad8(meta_keylen(m)) + p_.payload_size;
-    layout_dirty_ = true;
+    touch(leaf, slot);
     (void)commit_id;
     if (nleaves_live_ > 1 && used_space(L) - L.deleted <= p_.merge_threshold) return STAGE_RC_INVALID;
     return STAGE_RC_OK;
+}
+
+uint64_t HostTable::update_batch(const uint64_t *keys, uint64_t n, uint32_t len, uint32_t payload_off,
+                                 const uint8_t *deltas, uint32_t delta_len, const uint32_t *writer_ids,
+                                 const uint32_t *commit_ids, const uint32_t *sstamps, uint8_t *rc_out) {
+    uint64_t ok = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        int rc = update(keys[i], len, payload_off, deltas + i * (uint64_t)delta_len, delta_len, writer_ids[i]);
+        if (rc == STAGE_RC_OK && commit_ids && commit_ids[i]) {
+            rc = commit_update(keys[i], len, commit_ids[i], sstamps ? sstamps[i] : commit_ids[i]);
+        }
+        if (rc == STAGE_RC_OK) ++ok;
+        if (rc_out) rc_out[i] = (uint8_t)rc;
+    }
+    return ok;
 }
 
 void HostTable::key_order(std::vector<uint32_t> &order) const {

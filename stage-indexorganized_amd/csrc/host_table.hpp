@@ -86,7 +86,16 @@ public:
     std::vector<VersionHdr> versions_;
     uint64_t images_synced_ = 0;     // images already present on the device
     uint64_t arena_synced_ = 0;
-    bool layout_dirty_ = true;
+    bool layout_dirty_ = true;       // any host write since the last publish
+    bool structure_dirty_ = true;    // a split (or the first load) changed the leaf set/order
+    std::vector<uint64_t> dirty_slots_;  // leaf*cap + slot written since the last publish
+    uint64_t copies_synced_ = 0, versions_synced_ = 0;  // headers already on the device
+    uint64_t copies_dirty_from_ = ~0ull;                 // lowest synced copy header rewritten since
+
+    // batched write path (one call per YCSB-B epoch): update + optional commit per key
+    uint64_t update_batch(const uint64_t *keys, uint64_t n, uint32_t len, uint32_t payload_off, const uint8_t *deltas,
+                          uint32_t delta_len, const uint32_t *writer_ids, const uint32_t *commit_ids,
+                          const uint32_t *sstamps, uint8_t *rc_out);
 
 private:
     struct RouteEntry {
@@ -99,6 +108,10 @@ private:
         return e.sep_okey < k.okey || (e.sep_okey == k.okey && e.sep_len < k.len);
     }
 
+    void touch(uint32_t leaf, uint32_t slot) {
+        layout_dirty_ = true;
+        if (!structure_dirty_) dirty_slots_.push_back((uint64_t)leaf * cap_ + slot);
+    }
     uint32_t alloc_leaf();
     int64_t search(uint32_t leaf, const Key &k) const;  // SearchRecordMeta (check_concurrency)
     uint32_t used_space(const Leaf &l) const { return 40u + l.block + l.count * 24u; }

@@ -588,6 +588,30 @@ __global__ __launch_bounds__(256) void fill_kernel(uint8_t *__restrict__ heap, u
     }
 }
 
+// Incremental publish: rewrite the heads of dirty leaves (16-B chunks) and the dirty slot
+// words + key-column entries in place.  One thread per chunk / slot, grid-stride.
+__global__ __launch_bounds__(256) void patch_kernel(uint8_t *__restrict__ head, uint64_t *__restrict__ okey,
+                                                    SlotInfo *__restrict__ slot, uint32_t head_bytes,
+                                                    const uint32_t *__restrict__ head_leaf,
+                                                    const u32x4 *__restrict__ head_src, uint64_t nhead,
+                                                    const uint64_t *__restrict__ slot_idx,
+                                                    const SlotInfo *__restrict__ slot_src, uint64_t nslot) {
+    const uint32_t cpl = head_bytes >> 4;
+    const uint64_t nchunk = nhead * cpl;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nchunk + nslot; i += stride) {
+        if (i < nchunk) {
+            const uint64_t l = i / cpl, c = i % cpl;
+            reinterpret_cast<u32x4 *>(head + (uint64_t)head_leaf[l] * head_bytes)[c] = head_src[i];
+        } else {
+            const uint64_t k = i - nchunk, d = slot_idx[k];
+            const SlotInfo v = slot_src[k];
+            slot[d] = v;
+            okey[d] = v.okey;
+        }
+    }
+}
+
 // ----------------------------------------------------------------------------------------
 // launchers
 
@@ -659,6 +683,18 @@ hipError_t launch_fill(uint8_t *heap, uint32_t stride, uint32_t payload_size, co
     const int blocks = grid_for(count, 4, 8192);
     fill_kernel<<<blocks, 256, 0, s>>>(heap, stride, payload_size, descs, arena, first, count, ident_rowid0,
                                        ident_key_width, ident_mode);
+    return hipGetLastError();
+}
+
+hipError_t launch_patch(uint8_t *head, uint64_t *okey, SlotInfo *slot, uint32_t head_bytes, const uint32_t *head_leaf,
+                        const void *head_src, uint64_t nhead, const uint64_t *slot_idx, const SlotInfo *slot_src,
+                        uint64_t nslot, hipStream_t s) {
+    const uint64_t work = nhead * (head_bytes >> 4) + nslot;
+    if (work == 0) return hipSuccess;
+    uint64_t blocks = (work + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    patch_kernel<<<(unsigned)blocks, 256, 0, s>>>(head, okey, slot, head_bytes, head_leaf, (const u32x4 *)head_src,
+                                                  nhead, slot_idx, slot_src, nslot);
     return hipGetLastError();
 }
 

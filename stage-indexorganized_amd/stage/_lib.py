@@ -43,7 +43,10 @@ SIGNATURES = {
                                            c_u8p]),
     "stage_finalize_update": (ctypes.c_int, [c_vp, ctypes.c_uint64, ctypes.c_uint16, ctypes.c_uint32, c_u8p]),
     "stage_delete": (ctypes.c_int, [c_vp, ctypes.c_uint64, ctypes.c_uint16, ctypes.c_uint32, c_u8p]),
+    "stage_update_batch": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64, ctypes.c_uint16, ctypes.c_uint32, c_vp,
+                                          ctypes.c_uint32, c_vp, c_vp, c_vp, c_vp, c_u64p]),
     "stage_sync": (ctypes.c_int, [c_vp]),
+    "stage_sync_info": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_double), c_vp]),
     "stage_stats": (ctypes.c_int, [c_vp, c_vp]),
     "stage_record_stride": (ctypes.c_uint32, [c_vp]),
     "stage_leaf_capacity": (ctypes.c_uint32, [c_vp]),

@@ -178,6 +178,26 @@ class Table:
                                         ctypes.byref(rc)), "commit_update")
         return rc.value
 
+    def update_batch(self, keys, payload_off, deltas, writer_ids, commit_ids=None, sstamps=None, key_size=None):
+        """Batched update (+ commit where commit_ids[i] != 0); returns (rc per key, number OK).
+
+        ``deltas`` is an (n, delta_len) uint8 array, one patch per key."""
+        keys = np.ascontiguousarray(keys, np.uint64)
+        n = keys.size
+        deltas = np.ascontiguousarray(deltas, np.uint8).reshape(n, -1) if n else np.zeros((0, 0), np.uint8)
+        wid = np.ascontiguousarray(np.broadcast_to(np.asarray(writer_ids, np.uint32), (n,)))
+        cid = None if commit_ids is None else np.ascontiguousarray(np.broadcast_to(np.asarray(commit_ids, np.uint32),
+                                                                                    (n,)))
+        sst = None if sstamps is None else np.ascontiguousarray(np.broadcast_to(np.asarray(sstamps, np.uint32), (n,)))
+        rc = np.zeros(n, np.uint8)
+        ok = ctypes.c_uint64()
+        check(lib().stage_update_batch(self.h, keys.ctypes.data, n, key_size or self.key_width, payload_off,
+                                       deltas.ctypes.data, deltas.shape[1] if n else 0, wid.ctypes.data,
+                                       cid.ctypes.data if cid is not None else None,
+                                       sst.ctypes.data if sst is not None else None, rc.ctypes.data,
+                                       ctypes.byref(ok)), "update_batch")
+        return rc, ok.value
+
     def finalize_update(self, key, commit_id, key_size=None):
         rc = ctypes.c_uint8()
         check(lib().stage_finalize_update(self.h, int(key), key_size or self.key_width, commit_id, ctypes.byref(rc)),
@@ -191,6 +211,13 @@ class Table:
 
     def sync(self):
         check(lib().stage_sync(self.h), "stage_sync")
+
+    def sync_info(self):
+        """What the last sync did: {'incremental', 'leaves', 'slots', 'seconds'}."""
+        sec = ctypes.c_double()
+        info = np.zeros(3, np.uint64)
+        check(lib().stage_sync_info(self.h, ctypes.byref(sec), info.ctypes.data), "sync_info")
+        return {"incremental": bool(info[0]), "leaves": int(info[1]), "slots": int(info[2]), "seconds": sec.value}
 
     def export_leaves(self, cap=None):
         cap = cap or self.leaf_capacity

@@ -105,3 +105,34 @@ def test_updates_and_deletes_keep_layout():
     tab.load_keys(more, 8, 0)
     orc.load_keys(more, 8, 0)
     compare_layout(tab, orc)
+
+
+def test_update_batch_matches_per_key_oracle():
+    # one YCSB-B writer epoch through the batched entry point (stage_update_batch), with
+    # duplicate keys, absent keys, no-op deltas and stale writer ids, against the oracle's
+    # per-key LeafNode::Update + CommitTransaction calls
+    tab = stage.Table(key_width=8)
+    orc = O.OracleTree()
+    tab.load_ycsb(0, 30000, 8, mode=1)
+    orc.load_ycsb(0, 30000, 8, 1)
+    rng = np.random.default_rng(21)
+    for epoch in range(3):
+        n = 4000
+        keys = np.concatenate([rng.integers(0, 30000, n - 50), rng.integers(30000, 40000, 50)]).astype(np.uint64)
+        deltas = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+        deltas[::97] = 0  # payload mode 1 words are random: zero patches still change bytes
+        wid = np.full(n, 100 + 10 * epoch, np.uint32)
+        wid[::53] = 1  # stale writers -> NOT_NEEDED_UPDATE once a key has a newer cstamp
+        cid = np.where(np.arange(n) % 5 == 4, 0, 101 + 10 * epoch).astype(np.uint32)  # 20% stay in flight
+        off = 8 * epoch
+        rc, ok = tab.update_batch(keys, off, deltas, wid, cid)
+        exp = np.zeros(n, np.uint8)
+        for i in range(n):
+            r = orc.update(int(keys[i]), 8, off, deltas[i].tobytes(), int(wid[i]))
+            if r == stage.RC_OK and cid[i]:
+                r = orc.commit_update(int(keys[i]), 8, int(cid[i]), int(cid[i]))
+            exp[i] = r
+        assert (rc == exp).all(), np.nonzero(rc != exp)[0][:5]
+        assert ok == int((exp == stage.RC_OK).sum())
+        assert len(set(rc.tolist())) >= 3
+    compare_layout(tab, orc)
