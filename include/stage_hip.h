@@ -165,6 +165,31 @@ int stage_scan_batch(stage_table *t, const uint64_t *d_start_keys, const uint16_
 int stage_resolve_batch(stage_table *t, const uint64_t *d_keys, const uint16_t *d_lens, uint64_t n,
                         int le_child, uint32_t *d_leaf, void *stream);
 
+/* ---- host-buffer forms (keys and results in host memory) --------------------------------
+ * stage_probe_host: stage_probe_batch for host buffers; the batch is cut into chunks that
+ *   rotate over three streams so H2D, probe and D2H overlap.  Pass pinned buffers
+ *   (stage_host_alloc) for full PCIe rate; pageable buffers work but copy through HIP's staging.
+ *   Calls on one table are serialised.
+ * stage_reader_*: the single-key adapter for BTree::Read callers (b_tree.cpp:2066-2129 as used
+ *   by IndexScanExecutor::Execute, executor.h:374-454, from every worker thread).  Thread-safe:
+ *   concurrent stage_reader_read calls are coalesced into one device batch of up to max_batch
+ *   keys, shipped when full or when its oldest request has waited max_wait_us; each call
+ *   blocks until its own result (stage_probe_out + [key padded to 8][payload] in `record`,
+ *   either may be NULL) is filled.  stats[0] = batches, [1] = reads, [2] = full batches.
+ *   Writers must not stage_sync while readers are running (the host is the single writer and
+ *   publishes between epochs, as for every other device entry point). */
+typedef struct stage_reader stage_reader;
+int stage_host_alloc(uint64_t bytes, void **ptr);
+int stage_host_free(void *ptr);
+int stage_probe_host(stage_table *t, const uint64_t *keys, const uint16_t *lens,
+                     const uint32_t *read_ids, uint64_t n, stage_probe_out *out, uint8_t *records);
+int stage_reader_create(stage_table *t, uint32_t max_batch, uint32_t max_wait_us,
+                        stage_reader **out);
+int stage_reader_read(stage_reader *r, uint64_t key, uint16_t key_size, uint32_t read_id,
+                      stage_probe_out *out, uint8_t *record);
+int stage_reader_stats(stage_reader *r, uint64_t *stats);
+int stage_reader_destroy(stage_reader *r);
+
 /* launch shape of stage_probe_batch: probes in flight per wave (1, 2, 4 or 8) and the grid
  * cap in 256-thread blocks (0 = default).  A tuning knob, not a semantic one. */
 int stage_set_probe_tuning(stage_table *t, int group, int max_blocks);

@@ -7,55 +7,12 @@
 #include <string>
 #include <vector>
 
-#include "../../include/stage_hip.h"
-#include "device_image.hpp"
-#include "dist.hpp"
-#include "host_table.hpp"
-#include "kernel_api.hpp"
+#include "handle.hpp"
 
-struct stage_table {
-    std::unique_ptr<stage::HostTable> host;
-    stage::DeviceImage dev;
-    stage::ProbeTuning tune;
-    uint32_t out_stride = 0;  // 0 = stride of the canonical row; STAGE_OUT_STRIDE overrides (A/B)
-    std::unique_ptr<stage::ShardComm> comm;
-};
-
-namespace {
+namespace stage_capi {
 thread_local std::string g_err;
-
-int fail(int code, const std::string &msg) {
-    g_err = msg;
-    return code;
 }
-
-template <class F>
-int guarded(F fn) {
-    try {
-        return fn();
-    } catch (const std::bad_alloc &) {
-        return fail(STAGE_E_NOMEM, "host allocation failed");
-    } catch (const std::invalid_argument &e) {
-        return fail(STAGE_E_ARG, e.what());
-    } catch (const std::exception &e) {
-        return fail(STAGE_E_HIP, e.what());
-    }
-}
-
-int need_synced(stage_table *t) {
-    if (!t) return fail(STAGE_E_ARG, "null table");
-    if (!t->dev.valid || t->host->layout_dirty_)
-        return fail(STAGE_E_STATE, "device image is stale: call stage_sync after host writes");
-    return STAGE_OK;
-}
-
-hipStream_t pick(stage_table *t, void *stream) { return stream ? (hipStream_t)stream : t->dev.stream; }
-
-int hip_rc(hipError_t e, const char *what) {
-    if (e == hipSuccess) return STAGE_OK;
-    return fail(STAGE_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
-}
-}  // namespace
+using namespace stage_capi;
 
 extern "C" {
 

@@ -1,0 +1,69 @@
+// handle.hpp -- the table handle behind the C-ABI and the error helpers shared by the
+// translation units that implement include/stage_hip.h (capi.cpp, host_io.cpp).
+#pragma once
+#include <hip/hip_runtime_api.h>
+
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+
+#include "../../include/stage_hip.h"
+#include "device_image.hpp"
+#include "dist.hpp"
+#include "host_table.hpp"
+#include "kernel_api.hpp"
+
+namespace stage {
+struct HostPipe;  // host_io.cpp: pinned staging + streams of stage_probe_host
+void host_pipe_release(HostPipe *p);
+struct HostPipeDeleter {
+    void operator()(HostPipe *p) const { host_pipe_release(p); }
+};
+}  // namespace stage
+
+struct stage_table {
+    std::unique_ptr<stage::HostTable> host;
+    stage::DeviceImage dev;
+    stage::ProbeTuning tune;
+    uint32_t out_stride = 0;  // 0 = stride of the canonical row; STAGE_OUT_STRIDE overrides (A/B)
+    std::unique_ptr<stage::ShardComm> comm;
+    std::mutex pipe_mu;  // serialises stage_probe_host calls on this table
+    std::unique_ptr<stage::HostPipe, stage::HostPipeDeleter> pipe;
+};
+
+namespace stage_capi {
+extern thread_local std::string g_err;
+
+inline int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+template <class F>
+int guarded(F fn) {
+    try {
+        return fn();
+    } catch (const std::bad_alloc &) {
+        return fail(STAGE_E_NOMEM, "host allocation failed");
+    } catch (const std::invalid_argument &e) {
+        return fail(STAGE_E_ARG, e.what());
+    } catch (const std::exception &e) {
+        return fail(STAGE_E_HIP, e.what());
+    }
+}
+
+inline int need_synced(stage_table *t) {
+    if (!t) return fail(STAGE_E_ARG, "null table");
+    if (!t->dev.valid || t->host->layout_dirty_)
+        return fail(STAGE_E_STATE, "device image is stale: call stage_sync after host writes");
+    return STAGE_OK;
+}
+
+inline hipStream_t pick(stage_table *t, void *stream) { return stream ? (hipStream_t)stream : t->dev.stream; }
+
+inline int hip_rc(hipError_t e, const char *what) {
+    if (e == hipSuccess) return STAGE_OK;
+    return fail(STAGE_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+}  // namespace stage_capi

@@ -46,6 +46,13 @@ SIGNATURES = {
     "stage_update_batch": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64, ctypes.c_uint16, ctypes.c_uint32, c_vp,
                                           ctypes.c_uint32, c_vp, c_vp, c_vp, c_vp, c_u64p]),
     "stage_sync": (ctypes.c_int, [c_vp]),
+    "stage_host_alloc": (ctypes.c_int, [ctypes.c_uint64, ctypes.POINTER(c_vp)]),
+    "stage_host_free": (ctypes.c_int, [c_vp]),
+    "stage_probe_host": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, ctypes.c_uint64, c_vp, c_vp]),
+    "stage_reader_create": (ctypes.c_int, [c_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(c_vp)]),
+    "stage_reader_read": (ctypes.c_int, [c_vp, ctypes.c_uint64, ctypes.c_uint16, ctypes.c_uint32, c_vp, c_vp]),
+    "stage_reader_stats": (ctypes.c_int, [c_vp, c_vp]),
+    "stage_reader_destroy": (ctypes.c_int, [c_vp]),
     "stage_sync_info": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_double), c_vp]),
     "stage_stats": (ctypes.c_int, [c_vp, c_vp]),
     "stage_record_stride": (ctypes.c_uint32, [c_vp]),

@@ -269,6 +269,21 @@ class Table:
         rows = d_rec.to_numpy(np.uint8, n * self.stride).reshape(n, self.stride) if d_rec else None
         return out, rows
 
+    def probe_host(self, keys, read_ids=None, lens=None, records=True):
+        """stage_probe_host: the same probe with host-memory inputs and outputs (pipelined)."""
+        keys = np.ascontiguousarray(keys, np.uint64)
+        n = keys.size
+        rids = None if read_ids is None else np.ascontiguousarray(read_ids, np.uint32)
+        ln = None if lens is None else np.ascontiguousarray(lens, np.uint16)
+        out = np.zeros(n, PROBE_OUT_DTYPE)
+        rows = np.zeros((n, self.stride), np.uint8) if records else None
+        check(lib().stage_probe_host(self.h, keys.ctypes.data, _ptr(ln), _ptr(rids), n, out.ctypes.data, _ptr(rows)),
+              "probe_host")
+        return out, rows
+
+    def reader(self, max_batch=1024, max_wait_us=50):
+        return Reader(self, max_batch, max_wait_us)
+
     def range_scan(self, start_keys, scan_size, lens=None):
         """TableScanExecutor over RangeScanBySize/Iterator.  Returns (counts[n], rows[n, scan_size, stride])."""
         keys = np.ascontiguousarray(start_keys, np.uint64)
@@ -294,6 +309,41 @@ class Table:
                                         int(le_child), d_out.ptr, None), "resolve")
         check(lib().stage_device_sync(), "sync")
         return d_out.to_numpy(np.uint32, keys.size)
+
+
+class Reader:
+    """stage_reader: thread-safe single-key BTree::Read adapter (calls are coalesced into
+    device batches).  ``read`` releases the GIL inside the library, so Python threads
+    calling it concurrently are batched together."""
+
+    def __init__(self, table, max_batch=1024, max_wait_us=50):
+        self.table = table
+        h = ctypes.c_void_p()
+        check(lib().stage_reader_create(table.h, max_batch, max_wait_us, ctypes.byref(h)), "reader_create")
+        self.h = h
+
+    def read(self, key, read_id=0xFFFFFFFE, key_size=None, record=True):
+        out = np.zeros(1, PROBE_OUT_DTYPE)
+        row = np.zeros(8 + self.table.payload_size, np.uint8) if record else None
+        check(lib().stage_reader_read(self.h, int(key), key_size or self.table.key_width, read_id, out.ctypes.data,
+                                      _ptr(row)), "reader_read")
+        return out[0], row
+
+    def stats(self):
+        s = np.zeros(3, np.uint64)
+        check(lib().stage_reader_stats(self.h, s.ctypes.data), "reader_stats")
+        return {"batches": int(s[0]), "reads": int(s[1]), "full_batches": int(s[2])}
+
+    def close(self):
+        if self.h:
+            lib().stage_reader_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def murmur64a_device(keys, key_len=8, seed=0):

@@ -1,0 +1,104 @@
+"""GPU parity of the host-buffer entry points: stage_probe_host (chunked, three streams) and the
+coalescing single-key reader (stage_reader_*, the BTree::Read adapter of SURVEY §8(b)), both
+against the oracle and against the device-buffer probe."""
+import threading
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import stage
+from test_gpu_parity import check_probe
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def chains(gpu):
+    n = 300000
+    tab = stage.Table(key_width=8)
+    orc = O.OracleTree()
+    tab.load_ycsb(0, n, 8, mode=1)
+    orc.load_ycsb(0, n, 8, 1)
+    rng = np.random.default_rng(41)
+    hot = rng.choice(n, 5000, replace=False).astype(np.uint64)
+    for ep in range(3):
+        d = np.full((hot.size, 16), 0x30 + ep, np.uint8)
+        rc, _ = tab.update_batch(hot, 16 * ep, d, 10 + 10 * ep, 11 + 10 * ep)
+        for k in hot:
+            orc.update(int(k), 8, 16 * ep, bytes([0x30 + ep]) * 16, 10 + 10 * ep)
+            orc.commit_update(int(k), 8, 11 + 10 * ep, 11 + 10 * ep)
+    for k in hot[:500]:
+        assert tab.update(int(k), 100, b"\x99" * 4, 40) == orc.update(int(k), 8, 100, b"\x99" * 4, 40)
+    tab.sync()
+    return tab, orc, hot, n
+
+
+def test_probe_host_matches_device_and_oracle(chains):
+    tab, orc, hot, n = chains
+    rng = np.random.default_rng(42)
+    # > 3 chunks of 2^17 so every lane is reused
+    keys = np.concatenate([rng.integers(0, n + 1000, 450000), hot]).astype(np.uint64)
+    rids = rng.integers(0, 45, keys.size).astype(np.uint32)
+    out_h, rows_h = tab.probe_host(keys, read_ids=rids)
+    out_d, rows_d = tab.probe(keys, read_ids=rids)
+    assert (out_h == out_d).all()
+    assert (rows_h == rows_d).all()
+    sel = rng.choice(keys.size, 60000, replace=False)
+    check_probe(tab, orc, keys[sel], 8, read_ids=rids[sel])
+    # outputs only, no rows
+    out2, none = tab.probe_host(keys[:1000], read_ids=rids[:1000], records=False)
+    assert none is None and (out2 == out_h[:1000]).all()
+
+
+def test_reader_concurrent_threads_match_oracle(chains):
+    tab, orc, hot, n = chains
+    rng = np.random.default_rng(43)
+    keys = np.concatenate([rng.integers(0, n + 100, 6000), rng.choice(hot, 2000)]).astype(np.uint64)
+    rids = rng.integers(0, 45, keys.size).astype(np.uint32)
+    o_out, o_rec = orc.read_batch(keys, 8, rids)
+    r = tab.reader(max_batch=64, max_wait_us=200)
+    got_out = np.zeros(keys.size, stage.PROBE_OUT_DTYPE)
+    got_rec = np.zeros((keys.size, orc.row), np.uint8)
+    T = 16
+    errs = []
+
+    def work(t):
+        try:
+            for i in range(t, keys.size, T):
+                got_out[i], got_rec[i] = r.read(int(keys[i]), int(rids[i]))
+        except Exception as e:  # surfaced below
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(T)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errs, errs
+    for f in ("status", "hops", "cstamp", "rec_cstamp", "copy_sstamp"):
+        assert (got_out[f] == o_out[f]).all(), f
+    assert ((got_out["flags"] & 1) == o_out["copy_present"]).all()
+    assert (got_rec == o_rec).all()
+    st = r.stats()
+    assert st["reads"] == keys.size
+    assert st["batches"] < keys.size  # requests were actually coalesced
+    r.close()
+
+
+def test_reader_single_caller_and_stale_image(gpu):
+    tab = stage.Table(key_width=4)
+    tab.load_ycsb(0, 1000, 4)
+    tab.sync()
+    r = tab.reader(max_batch=8, max_wait_us=10)
+    out, row = r.read(7)
+    assert out["status"] == stage.ST_LATEST and row[0] == 7 and (row[8:1008] == 7).all()
+    out, row = r.read(5000)
+    assert out["status"] == stage.ST_NOT_FOUND
+    assert tab.update(7, 0, b"\x01", 5) == stage.RC_OK
+    with pytest.raises(RuntimeError):
+        r.read(7)  # host wrote since the last publish
+    tab.sync()
+    out, row = r.read(7, read_id=10)
+    assert out["status"] == stage.ST_COPY and row[8] == 7
+    r.close()
