@@ -7,15 +7,22 @@
 //    BTree::Read (b_tree.cpp:2066-2129) one key at a time from every worker thread
 //    (IndexScanExecutor::Execute, executor.h:374-454); a reader coalesces those concurrent
 //    calls into one device batch (group probe): callers append to the open batch and block,
-//    a dispatcher thread ships a batch when it is full or its oldest request has waited
-//    `max_wait_us`, and fills every caller's result before waking it.  While one batch is on
-//    the device the next one fills, so the device and the callers overlap.
+//    a dispatcher thread ships a batch when it is full, when its oldest request has waited
+//    `max_wait_us` or when arrivals have paused, and fills every caller's result before
+//    waking it.  The batch is one probe launch reading keys from and writing results to
+//    pinned, device-mapped host memory (no separate copies).  While one batch is on the
+//    device the next one fills.
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <climits>
 #include <cstring>
+#include <linux/futex.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -96,6 +103,19 @@ hipError_t pipe_chunk(stage_table *t, stage::PipeLane &l, uint64_t stride, const
 // ---------------------------------------------------------------------------------------
 // the coalescing reader
 
+namespace {
+
+long futex(std::atomic<uint32_t> *addr, int op, uint32_t val) {
+    return syscall(SYS_futex, reinterpret_cast<uint32_t *>(addr), op, val, nullptr, nullptr, 0);
+}
+
+int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+}  // namespace
+
 struct stage_reader {
     struct Req {
         uint64_t key;
@@ -105,6 +125,18 @@ struct stage_reader {
         uint8_t *rec;
         int *rc;
     };
+    // one batch buffer: a pinned, device-mapped block the probe kernel reads the keys from and
+    // writes the results to directly over PCIe (zero-copy: one launch, no copies)
+    struct Slot {
+        hipStream_t s = nullptr;
+        hipEvent_t ev = nullptr;
+        uint8_t *h = nullptr;   // keys | lens | read ids | out | rows
+        uint8_t *hd = nullptr;  // the same block as the device sees it
+        std::vector<Req> reqs;
+        uint32_t seq = 0;
+        bool busy = false;
+    };
+    static constexpr int kSlots = 2;
 
     stage_table *t = nullptr;
     uint32_t max_batch = 0;
@@ -112,84 +144,122 @@ struct stage_reader {
     uint32_t row_bytes = 0;  // bytes handed to a caller: key padded to 8 + payload
     uint64_t stride = 0;
 
-    std::mutex mu;
-    std::condition_variable cv_work, cv_space, cv_done;
+    std::mutex mu;  // guards open/stop; callers hold it only to append
+    std::condition_variable cv_work, cv_space;
     std::vector<Req> open;
-    std::chrono::steady_clock::time_point open_since;
-    uint64_t open_gen = 1, done_gen = 0;
+    uint32_t open_seq = 1;  // sequence number the open batch will carry
+    std::atomic<uint32_t> open_count{0};
+    std::atomic<int64_t> first_arrival_ns{0}, last_arrival_ns{0};
+    std::atomic<uint32_t> done_seq{0};  // every batch with seq <= done_seq is complete (futex word)
     bool stop = false;
     std::thread worker;
+    Slot slot[kSlots];
 
-    hipStream_t s = nullptr;
-    uint64_t *h_keys = nullptr;
-    uint16_t *h_lens = nullptr;
-    uint32_t *h_rids = nullptr;
-    stage_probe_out *h_out = nullptr;
-    uint8_t *h_rows = nullptr;
-    uint8_t *d = nullptr;
-
-    uint64_t n_batches = 0, n_reads = 0, n_full = 0;
+    std::atomic<uint64_t> n_batches{0}, n_reads{0}, n_full{0};
 
     void run();
-    int ship(std::vector<Req> &cur);
+    void launch(Slot &sl);
+    void complete(Slot &sl);
 };
 
-int stage_reader::ship(std::vector<Req> &cur) {
-    const uint64_t n = cur.size();
+void stage_reader::launch(Slot &sl) {
+    const uint64_t n = sl.reqs.size(), mb = max_batch;
+    uint64_t *keys = (uint64_t *)sl.h;
+    uint16_t *lens = (uint16_t *)(sl.h + 8 * mb);
+    uint32_t *rids = (uint32_t *)(sl.h + 10 * mb);
     for (uint64_t i = 0; i < n; ++i) {
-        h_keys[i] = cur[i].key;
-        h_lens[i] = cur[i].len;
-        h_rids[i] = cur[i].rid;
+        keys[i] = sl.reqs[i].key;
+        lens[i] = sl.reqs[i].len;
+        rids[i] = sl.reqs[i].rid;
     }
-    const uint64_t mb = max_batch;
-    uint8_t *dk = d, *dl = dk + 8 * mb, *dr = dl + 2 * mb, *dout = dr + 4 * mb, *drow = dout + 32 * mb;
-    hipError_t e = hipSetDevice(t->dev.device);
-    if (!e) e = hipMemcpyAsync(dk, h_keys, 8 * n, hipMemcpyHostToDevice, s);
-    if (!e) e = hipMemcpyAsync(dl, h_lens, 2 * n, hipMemcpyHostToDevice, s);
-    if (!e) e = hipMemcpyAsync(dr, h_rids, 4 * n, hipMemcpyHostToDevice, s);
-    if (!e) {
-        stage::DevTable view = t->dev.view;
-        view.stride = (uint32_t)stride;
-        e = stage::launch_probe(view, (const uint64_t *)dk, (const uint16_t *)dl, (const uint32_t *)dr, nullptr, n,
-                                (stage::stage_probe_out_dev *)dout, drow, s, t->tune);
+    stage::DevTable view = t->dev.view;
+    view.stride = (uint32_t)stride;
+    hipError_t e = stage_capi::need_synced(t) ? hipErrorInvalidValue : hipSuccess;
+    const int stale = e != hipSuccess;
+    if (!e)
+        e = stage::launch_probe(view, (const uint64_t *)sl.hd, (const uint16_t *)(sl.hd + 8 * mb),
+                                (const uint32_t *)(sl.hd + 10 * mb), nullptr, n,
+                                (stage::stage_probe_out_dev *)(sl.hd + 14 * mb), sl.hd + 46 * mb, sl.s, t->tune);
+    if (!e) e = hipEventRecord(sl.ev, sl.s);
+    if (e) {  // fail the batch now; complete() only delivers
+        for (auto &r : sl.reqs) *r.rc = stale ? STAGE_E_STATE : STAGE_E_HIP;
+        sl.reqs.clear();
     }
-    if (!e) e = hipMemcpyAsync(h_out, dout, 32 * n, hipMemcpyDeviceToHost, s);
-    if (!e) e = hipMemcpyAsync(h_rows, drow, stride * n, hipMemcpyDeviceToHost, s);
-    if (!e) e = hipStreamSynchronize(s);
-    if (e) return STAGE_E_HIP;
-    for (uint64_t i = 0; i < n; ++i) {
-        if (cur[i].out) *cur[i].out = h_out[i];
-        if (cur[i].rec) std::memcpy(cur[i].rec, h_rows + i * stride, row_bytes);
-    }
-    return STAGE_OK;
+    sl.busy = true;
 }
 
+void stage_reader::complete(Slot &sl) {
+    const uint64_t n = sl.reqs.size(), mb = max_batch;
+    const stage_probe_out *out = (const stage_probe_out *)(sl.h + 14 * mb);
+    const uint8_t *rows = sl.h + 46 * mb;
+    if (n && hipEventSynchronize(sl.ev) != hipSuccess) {
+        for (auto &r : sl.reqs) *r.rc = STAGE_E_HIP;
+    } else {
+        for (uint64_t i = 0; i < n; ++i) {
+            const Req &r = sl.reqs[i];
+            if (r.out) *r.out = out[i];
+            if (r.rec) std::memcpy(r.rec, rows + i * stride, row_bytes);
+            *r.rc = STAGE_OK;
+        }
+    }
+    n_batches++;
+    n_reads += n;
+    if (n >= max_batch) n_full++;
+    sl.reqs.clear();
+    sl.busy = false;
+    done_seq.store(sl.seq, std::memory_order_release);
+    futex(&done_seq, FUTEX_WAKE_PRIVATE, INT32_MAX);
+}
+
+// Dispatch rule: a batch leaves when it is full, when its oldest request has waited
+// max_wait_us, or when no request has arrived for kGapNs (the callers of the previous batch
+// have come back).  Two batches can be in flight; they complete in launch order.  The
+// dispatcher sleeps only when nothing is open or in flight.
+constexpr int64_t kGapNs = 3000;
+
 void stage_reader::run() {
-    std::vector<Req> cur;
-    cur.reserve(max_batch);
+    (void)hipSetDevice(t->dev.device);
+    int next = 0;  // slot the next batch goes to (slots are used round robin)
+    int oldest = 0;
     for (;;) {
-        uint64_t gen;
-        {
+        // deliver the oldest in-flight batch once its event has fired
+        if (slot[oldest].busy && (slot[oldest].reqs.empty() || hipEventQuery(slot[oldest].ev) != hipErrorNotReady)) {
+            complete(slot[oldest]);
+            oldest ^= 1;
+            continue;
+        }
+        const bool any_busy = slot[0].busy || slot[1].busy;
+        const uint32_t cnt = open_count.load(std::memory_order_acquire);
+        if (cnt == 0) {
+            if (any_busy) {
+                std::this_thread::yield();
+                continue;
+            }
             std::unique_lock<std::mutex> lk(mu);
             cv_work.wait(lk, [&] { return stop || !open.empty(); });
             if (open.empty() && stop) return;
-            const auto deadline = open_since + std::chrono::microseconds(max_wait_us);
-            cv_work.wait_until(lk, deadline, [&] { return stop || open.size() >= max_batch; });
-            cur.swap(open);
-            gen = open_gen++;
+            continue;
         }
-        cv_space.notify_all();
-        const int rc = stage_capi::need_synced(t) ? STAGE_E_STATE : ship(cur);
-        for (auto &r : cur) *r.rc = rc;
+        if (slot[next].busy) {  // both slots in flight: wait for the oldest
+            std::this_thread::yield();
+            continue;
+        }
+        const int64_t now = now_ns();
+        if (cnt < max_batch && now < first_arrival_ns.load(std::memory_order_acquire) + (int64_t)max_wait_us * 1000 &&
+            now - last_arrival_ns.load(std::memory_order_acquire) < kGapNs) {
+            std::this_thread::yield();
+            continue;
+        }
+        Slot &sl = slot[next];
         {
             std::lock_guard<std::mutex> lk(mu);
-            done_gen = gen;
-            ++n_batches;
-            n_reads += cur.size();
-            if (cur.size() >= max_batch) ++n_full;
+            sl.reqs.swap(open);
+            sl.seq = open_seq++;
+            open_count.store(0, std::memory_order_release);
         }
-        cv_done.notify_all();
-        cur.clear();
+        cv_space.notify_all();
+        launch(sl);
+        next ^= 1;
     }
 }
 
@@ -237,15 +307,16 @@ int stage_reader_create(stage_table *t, uint32_t max_batch, uint32_t max_wait_us
         r->max_wait_us = max_wait_us;
         r->stride = t->host->stride();
         r->row_bytes = 8 + t->host->params().payload_size;
-        const uint64_t mb = max_batch;
+        const uint64_t mb = max_batch, bytes = mb * (8 + 2 + 4 + 32 + r->stride);
         stage::hip_check(hipSetDevice(t->dev.device), "hipSetDevice");
-        stage::hip_check(hipStreamCreateWithFlags(&r->s, hipStreamNonBlocking), "reader stream");
-        stage::hip_check(hipHostMalloc((void **)&r->h_keys, 8 * mb, hipHostMallocDefault), "reader pinned");
-        stage::hip_check(hipHostMalloc((void **)&r->h_lens, 2 * mb, hipHostMallocDefault), "reader pinned");
-        stage::hip_check(hipHostMalloc((void **)&r->h_rids, 4 * mb, hipHostMallocDefault), "reader pinned");
-        stage::hip_check(hipHostMalloc((void **)&r->h_out, 32 * mb, hipHostMallocDefault), "reader pinned");
-        stage::hip_check(hipHostMalloc((void **)&r->h_rows, r->stride * mb, hipHostMallocDefault), "reader pinned");
-        stage::hip_check(hipMalloc((void **)&r->d, mb * (8 + 2 + 4 + 32 + r->stride)), "reader device");
+        for (auto &sl : r->slot) {
+            stage::hip_check(hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking), "reader stream");
+            stage::hip_check(hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming), "reader event");
+            stage::hip_check(hipHostMalloc((void **)&sl.h, bytes, hipHostMallocMapped | hipHostMallocPortable),
+                             "reader pinned");
+            stage::hip_check(hipHostGetDevicePointer((void **)&sl.hd, sl.h, 0), "reader mapped pointer");
+            sl.reqs.reserve(max_batch);
+        }
         r->open.reserve(max_batch);
         stage_reader *raw = r.get();
         r->worker = std::thread([raw] { raw->run(); });
@@ -259,15 +330,23 @@ int stage_reader_read(stage_reader *r, uint64_t key, uint16_t key_size, uint32_t
     if (!r) return fail(STAGE_E_ARG, "null reader");
     if (key_size == 0 || key_size > 8) return fail(STAGE_E_ARG, "key_size must be 1..8");
     int rc = STAGE_E_STATE;
+    uint32_t seq;
     {
         std::unique_lock<std::mutex> lk(r->mu);
         r->cv_space.wait(lk, [&] { return r->stop || r->open.size() < r->max_batch; });
         if (r->stop) return fail(STAGE_E_STATE, "reader is closing");
-        if (r->open.empty()) r->open_since = std::chrono::steady_clock::now();
         r->open.push_back({key, key_size, read_id, out, record, &rc});
-        const uint64_t gen = r->open_gen;
-        if (r->open.size() == 1 || r->open.size() >= r->max_batch) r->cv_work.notify_one();
-        r->cv_done.wait(lk, [&] { return r->done_gen >= gen; });
+        const int64_t now = now_ns();
+        if (r->open.size() == 1) r->first_arrival_ns.store(now, std::memory_order_release);
+        r->last_arrival_ns.store(now, std::memory_order_release);
+        r->open_count.store((uint32_t)r->open.size(), std::memory_order_release);
+        seq = r->open_seq;
+        if (r->open.size() == 1) r->cv_work.notify_one();
+    }
+    for (;;) {  // wait for batch `seq` (sequence numbers wrap: compare as a signed distance)
+        const uint32_t d = r->done_seq.load(std::memory_order_acquire);
+        if ((int32_t)(d - seq) >= 0) break;
+        futex(&r->done_seq, FUTEX_WAIT_PRIVATE, d);
     }
     if (rc) return fail(rc, rc == STAGE_E_STATE ? "device image is stale: call stage_sync after host writes"
                                                 : "reader batch failed on the device");
@@ -276,10 +355,9 @@ int stage_reader_read(stage_reader *r, uint64_t key, uint16_t key_size, uint32_t
 
 int stage_reader_stats(stage_reader *r, uint64_t *stats) {
     if (!r || !stats) return fail(STAGE_E_ARG, "null argument");
-    std::lock_guard<std::mutex> lk(r->mu);
-    stats[0] = r->n_batches;
-    stats[1] = r->n_reads;
-    stats[2] = r->n_full;
+    stats[0] = r->n_batches.load();
+    stats[1] = r->n_reads.load();
+    stats[2] = r->n_full.load();
     return STAGE_OK;
 }
 
@@ -293,10 +371,11 @@ int stage_reader_destroy(stage_reader *r) {
     r->cv_space.notify_all();
     if (r->worker.joinable()) r->worker.join();
     (void)hipSetDevice(r->t->dev.device);
-    if (r->s) (void)hipStreamDestroy(r->s);
-    for (void *p : {(void *)r->h_keys, (void *)r->h_lens, (void *)r->h_rids, (void *)r->h_out, (void *)r->h_rows})
-        if (p) (void)hipHostFree(p);
-    if (r->d) (void)hipFree(r->d);
+    for (auto &sl : r->slot) {
+        if (sl.s) (void)hipStreamSynchronize(sl.s), (void)hipStreamDestroy(sl.s);
+        if (sl.ev) (void)hipEventDestroy(sl.ev);
+        if (sl.h) (void)hipHostFree(sl.h);
+    }
     delete r;
     return STAGE_OK;
 }
