@@ -143,6 +143,26 @@ int stage_traverse_batch(stage_table *t, const uint64_t *keys, const uint16_t *l
 int64_t stage_export_leaves(stage_table *t, uint32_t cap, uint64_t max_leaves, uint32_t *rc,
                             uint32_t *sc, uint64_t *meta, uint64_t *keyw);
 
+/* ---- leaf-level snapshot in the reference's block format -----------
+ * A block is one LeafNode of leaf_node_size bytes exactly as the reference lays it out
+ * (b_tree.h:571-740: BaseNode{is_leaf, NodeHeader{size, sorted_count, next_record_slot,
+ * StatusWord}} b_tree.h:109-113 / version_store.h:158-231, RecordMetadata{meta, next_ptr,
+ * loc_ptr} record_meta.h:30-60 per slot, records [key][pad to 8][payload] growing down).
+ * Canonical form: next_ptr and loc_ptr (process pointers: TupleHeader / copy buffer /
+ * RecordLocation, record_location.h:13-42) are 0 and unreferenced record bytes are 0.
+ * sep_keys[i]/sep_lens[i] = leaf i's upper bound, the inner-node key that routes to it
+ * (GetChildIndex, b_tree.cpp:664-702), len 0xFFFF = +inf for the last leaf.
+ * stage_export_leaf_images returns the number of leaves (STAGE_E_ARG if max_leaves is below
+ *   stage_stats[2]); blocks holds max_leaves * leaf_node_size bytes; seps may be NULL (both).
+ * stage_import_leaf_images loads such a snapshot into an EMPTY table (a quiesced leaf level:
+ *   no control bits; version chains are not part of the format).  sep_keys NULL -> each
+ *   leaf's largest visible key.  *n_records = visible records imported. */
+int64_t stage_export_leaf_images(stage_table *t, uint64_t max_leaves, uint8_t *blocks,
+                                 uint64_t *sep_keys, uint16_t *sep_lens);
+int stage_import_leaf_images(stage_table *t, const uint8_t *blocks, uint64_t n_leaves,
+                             uint32_t block_size, const uint64_t *sep_keys,
+                             const uint16_t *sep_lens, uint64_t *n_records);
+
 /* ---- device batch path (the replaced hot path) ------------------------------------------
  * stage_probe_batch  replaces LeafNode::Read/SearchRecordMeta (b_tree.cpp:1042-1051, 18-122),
  *   Record::New/Neww (b_tree.h:407-448), BTree::Read (b_tree.cpp:2066-2129) and the

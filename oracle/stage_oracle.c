@@ -1031,6 +1031,62 @@ static void export_rec(void *node, export_t *e, uint64_t *stats, uint32_t depth)
     for (uint32_t i = 0; i < p->count; i++) export_rec(p->child[i], e, stats, depth + 1);
 }
 
+/* Leaf-level snapshot in the reference's own block format (LeafNode, b_tree.h:571-740;
+ * BaseNode{is_leaf, NodeHeader} b_tree.h:109-113; StatusWord version_store.h:158-231;
+ * RecordMetadata{meta, next_ptr, loc_ptr} record_meta.h:30-60).  Canonical form: the process
+ * pointers (next_ptr, loc_ptr) are written as 0 and record bytes no live metadata entry
+ * references (deleted records) are zeroed.  Leaf i's separator is the inner-node key that
+ * bounds it from above: child j of an inner node covers (key[j], key[j+1]] (GetChildIndex,
+ * b_tree.cpp:664-702), the last child inherits its parent's bound; the last leaf gets
+ * len 0xFFFF (+inf). */
+typedef struct {
+    uint64_t max, n;
+    uint32_t block, payload;
+    uint8_t *blocks;
+    uint64_t *sep_key;
+    uint16_t *sep_len;
+} image_export_t;
+
+static void image_rec(void *node, image_export_t *e, const uint8_t *ub, uint16_t ub_len, int ub_inf) {
+    if (is_leaf(node)) {
+        if (e->n < e->max) {
+            uint8_t *n = node, *dst = e->blocks + e->n * (uint64_t)e->block;
+            uint32_t cnt = st_count(*l_status(n));
+            memcpy(dst, n, LEAF_HDR);
+            memset(dst, 0, 8); /* vptr */
+            memset(dst + LEAF_HDR, 0, e->block - LEAF_HDR);
+            for (uint32_t i = 0; i < cnt; i++) {
+                uint64_t m = l_meta(n, i)->meta;
+                memcpy(dst + LEAF_HDR + META_SZ * i, &m, 8);
+                if (m) {
+                    uint32_t off = m_offset(m), len = pad_key(m_keylen(m)) + e->payload;
+                    memcpy(dst + off, n + off, len);
+                }
+            }
+            if (e->sep_key) {
+                uint64_t kw = 0;
+                if (!ub_inf) memcpy(&kw, ub, ub_len > 8 ? 8 : ub_len);
+                e->sep_key[e->n] = kw;
+                e->sep_len[e->n] = ub_inf ? 0xFFFF : ub_len;
+            }
+        }
+        e->n++;
+        return;
+    }
+    orc_inner *p = node;
+    for (uint32_t i = 0; i < p->count; i++) {
+        if (i + 1 < p->count) image_rec(p->child[i], e, p->key[i + 1], p->klen[i + 1], 0);
+        else image_rec(p->child[i], e, ub, ub_len, ub_inf);
+    }
+}
+
+int64_t orc_export_leaf_images(orc_tree *t, uint64_t max_leaves, uint8_t *blocks, uint64_t *sep_key,
+                               uint16_t *sep_len) {
+    image_export_t e = {max_leaves, 0, t->leaf_node_size, t->payload_size, blocks, sep_key, sep_len};
+    image_rec(t->root, &e, NULL, 0, 1);
+    return (int64_t)e.n;
+}
+
 void orc_stats(orc_tree *t, uint64_t *stats) {
     memset(stats, 0, 8 * sizeof(uint64_t));
     export_rec(t->root, NULL, stats, 0);

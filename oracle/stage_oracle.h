@@ -111,6 +111,10 @@ void orc_stats(orc_tree *t, uint64_t *stats);
 /* leaves in key order: rc[i]=record_count, sc[i]=sorted_count; slot arrays (cap per leaf):
  * meta[i*cap+s], key bytes as little-endian u64 keyw[i*cap+s]; returns number of leaves,
  * or -(needed) when max_leaves is too small. */
+/* leaves in key order as reference-format blocks of leaf_node_size bytes (pointers zeroed,
+ * dead record bytes zeroed) + each leaf's upper separator (len 0xFFFF = +inf) */
+int64_t orc_export_leaf_images(orc_tree *t, uint64_t max_leaves, uint8_t *blocks, uint64_t *sep_key,
+                               uint16_t *sep_len);
 int64_t orc_export_leaves(orc_tree *t, uint32_t cap, uint64_t max_leaves, uint32_t *rc,
                           uint32_t *sc, uint64_t *meta, uint64_t *keyw);
 

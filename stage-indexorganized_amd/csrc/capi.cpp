@@ -192,6 +192,30 @@ int64_t stage_export_leaves(stage_table *t, uint32_t cap, uint64_t max_leaves, u
     }
 }
 
+int64_t stage_export_leaf_images(stage_table *t, uint64_t max_leaves, uint8_t *blocks, uint64_t *sep_keys,
+                                 uint16_t *sep_lens) {
+    if (!t || !blocks || (!sep_keys != !sep_lens)) return fail(STAGE_E_ARG, "bad arguments");
+    try {
+        const int64_t n = t->host->export_leaf_images(max_leaves, blocks, sep_keys, sep_lens);
+        if (n < 0) return fail(STAGE_E_ARG, "max_leaves is smaller than the leaf count (stage_stats[2])");
+        return n;
+    } catch (const std::bad_alloc &) {
+        return fail(STAGE_E_NOMEM, "host allocation failed");
+    } catch (const std::exception &e) {
+        return fail(STAGE_E_HIP, e.what());
+    }
+}
+
+int stage_import_leaf_images(stage_table *t, const uint8_t *blocks, uint64_t n_leaves, uint32_t block_size,
+                             const uint64_t *sep_keys, const uint16_t *sep_lens, uint64_t *n_records) {
+    if (!t || !blocks || (!sep_keys != !sep_lens)) return fail(STAGE_E_ARG, "bad arguments");
+    return guarded([&] {
+        const uint64_t n = t->host->import_leaf_images(blocks, n_leaves, block_size, sep_keys, sep_lens);
+        if (n_records) *n_records = n;
+        return STAGE_OK;
+    });
+}
+
 int stage_probe_batch(stage_table *t, const uint64_t *d_keys, const uint16_t *d_lens, const uint32_t *d_read_ids,
                       const uint32_t *d_leaf_ids, uint64_t n, stage_probe_out *d_out, uint8_t *d_records,
                       void *stream) {

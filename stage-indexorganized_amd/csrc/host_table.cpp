@@ -443,4 +443,156 @@ int64_t HostTable::export_leaves(uint32_t cap, uint64_t max_leaves, uint32_t *rc
     return (int64_t)order.size();
 }
 
+// ---- leaf-level snapshot in the reference's block format --------------------------------
+// Block = LeafNode (b_tree.h:571-740): [vptr 8][is_leaf 1 + pad 7][NodeHeader: size u32,
+// sorted_count u32, next_record_slot u32 + pad 4, StatusWord u64 (version_store.h:158-231:
+// frozen bit 60, record count 44-59, block size 22-43, delete size 0-21)], then
+// RecordMetadata{meta, next_ptr, loc_ptr} (record_meta.h:30-60) per slot, records
+// [key][pad to 8][payload] at meta.offset growing down from `size`.  Canonical form (the
+// oracle's orc_export_leaf_images uses the same): next_ptr / loc_ptr = 0, record bytes not
+// referenced by a non-zero meta word = 0.
+static constexpr uint32_t kLeafHdr = 40, kOffIsLeaf = 8, kOffSize = 16, kOffSorted = 20, kOffStatus = 32;
+
+int64_t HostTable::export_leaf_images(uint64_t max_leaves, uint8_t *blocks, uint64_t *sep_key_le,
+                                      uint16_t *sep_len) const {
+    std::vector<uint32_t> order;
+    key_order(order);
+    if (order.size() > max_leaves) return -(int64_t)order.size();
+    const uint32_t B = p_.leaf_node_size;
+    std::vector<uint8_t> pay(p_.payload_size);
+    for (size_t d = 0; d < order.size(); ++d) {
+        const Leaf &L = leaves_[order[d]];
+        uint8_t *dst = blocks + d * (uint64_t)B;
+        std::memset(dst, 0, B);
+        dst[kOffIsLeaf] = 1;
+        std::memcpy(dst + kOffSize, &B, 4);
+        std::memcpy(dst + kOffSorted, &L.sorted, 4);
+        const uint64_t status = ((uint64_t)L.count << 44) | ((uint64_t)L.block << 22) | L.deleted;
+        std::memcpy(dst + kOffStatus, &status, 8);
+        const size_t b = (size_t)order[d] * cap_;
+        for (uint32_t s = 0; s < L.count; ++s) {
+            const uint64_t m = meta_[b + s];
+            std::memcpy(dst + kLeafHdr + 24 * s, &m, 8);
+            if (!m) continue;
+            const uint32_t off = meta_offset(m), kl = meta_keylen(m);
+            const uint64_t kw = key_bytes_from_order(okey_[b + s], kl);
+            std::memcpy(dst + off, &kw, kl);
+            image_payload(image_[b + s], pay.data());
+            std::memcpy(dst + off + pad8(kl), pay.data(), p_.payload_size);
+        }
+        if (sep_key_le) {
+            sep_key_le[d] = key_is_inf(L.sep) ? 0 : key_bytes_from_order(L.sep.okey, L.sep.len);
+            sep_len[d] = key_is_inf(L.sep) ? (uint16_t)kInfLen : (uint16_t)L.sep.len;
+        }
+    }
+    return (int64_t)order.size();
+}
+
+uint64_t HostTable::import_leaf_images(const uint8_t *blocks, uint64_t n, uint32_t block_size,
+                                       const uint64_t *sep_key_le, const uint16_t *sep_len) {
+    auto bad = [](const std::string &w) { throw std::invalid_argument("leaf image import: " + w); };
+    if (nleaves_live_ != 1 || head_ != 0 || leaves_.size() != 1 || leaves_[0].count != 0 || !images_.empty())
+        bad("the table must be empty");
+    if (block_size != p_.leaf_node_size) bad("block size differs from the table's leaf_node_size");
+    if (n == 0) bad("no leaves");
+    if (n > 0x7FFFFFFFull) bad("too many leaves");
+    // separators: given (the inner-node keys) or derived as each leaf's largest visible key
+    std::vector<Key> sep(n, key_inf());
+    uint64_t nrec = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint8_t *blk = blocks + i * (uint64_t)block_size;
+        uint32_t size, sorted;
+        uint64_t status;
+        std::memcpy(&size, blk + kOffSize, 4);
+        std::memcpy(&sorted, blk + kOffSorted, 4);
+        std::memcpy(&status, blk + kOffStatus, 8);
+        const uint32_t count = (uint32_t)((status >> 44) & 0xFFFF);
+        if (!blk[kOffIsLeaf]) bad("block " + std::to_string(i) + " is not a leaf");
+        if (size != block_size) bad("block " + std::to_string(i) + ": header size != block size");
+        if ((status >> 60) & 1) bad("block " + std::to_string(i) + " is frozen (mid-split)");
+        if (count > cap_ || count > max_records_ || sorted > count) bad("block " + std::to_string(i) + ": bad counts");
+        Key mx{0, 0}, mn{0, 0};
+        bool any = false;
+        for (uint32_t s = 0; s < count; ++s) {
+            uint64_t m;
+            std::memcpy(&m, blk + kLeafHdr + 24 * s, 8);
+            if (!m) continue;
+            if (m & kMetaControl) bad("block " + std::to_string(i) + ": in-flight record (control bit)");
+            const uint32_t kl = meta_keylen(m), off = meta_offset(m);
+            if (kl == 0 || kl > 8) bad("block " + std::to_string(i) + ": key length outside 1..8");
+            if (p_.key_width && kl != p_.key_width) bad("block " + std::to_string(i) + ": key width");
+            if (off < kLeafHdr + 24 * count || (uint64_t)off + pad8(kl) + p_.payload_size > size)
+                bad("block " + std::to_string(i) + ": record offset out of range");
+            if (!meta_visible(m)) continue;
+            uint64_t kw = 0;
+            std::memcpy(&kw, blk + off, kl);
+            const Key k{order_key(kw, kl), kl};
+            if (!any || key_lt(mx, k)) mx = k;
+            if (!any || key_lt(k, mn)) mn = k;
+            any = true;
+            ++nrec;
+        }
+        if (i + 1 < n) {
+            if (sep_key_le) {
+                if (sep_len[i] == 0 || sep_len[i] > 8) bad("separator " + std::to_string(i) + ": length");
+                sep[i] = Key{order_key(sep_key_le[i], sep_len[i]), sep_len[i]};
+            } else {
+                if (!any) bad("block " + std::to_string(i) + ": empty leaf needs an explicit separator");
+                sep[i] = mx;
+            }
+            if (i > 0 && !key_lt(sep[i - 1], sep[i])) bad("separators are not increasing");
+        }
+        if (any && !key_le(mx, sep[i])) bad("block " + std::to_string(i) + ": key above its separator");
+        if (any && i > 0 && !key_lt(sep[i - 1], mn)) bad("block " + std::to_string(i) + ": key below its range");
+    }
+    // second pass: fill the SoA leaves and images (first leaf reuses the empty root)
+    images_.reserve(nrec);
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint32_t id = i == 0 ? (uint32_t)head_ : alloc_leaf();
+        const uint8_t *blk = blocks + i * (uint64_t)block_size;
+        uint32_t sorted;
+        uint64_t status;
+        std::memcpy(&sorted, blk + kOffSorted, 4);
+        std::memcpy(&status, blk + kOffStatus, 8);
+        Leaf &L = leaves_[id];
+        L.count = (uint32_t)((status >> 44) & 0xFFFF);
+        L.sorted = sorted;
+        L.block = (uint32_t)((status >> 22) & 0x3FFFFF);
+        L.deleted = (uint32_t)(status & 0x3FFFFF);
+        L.sep = sep[i];
+        L.prev = i == 0 ? -1 : (int32_t)(id - 1);
+        L.next = -1;
+        if (i > 0) leaves_[id - 1].next = (int32_t)id;
+        const size_t b = (size_t)id * cap_;
+        for (uint32_t s = 0; s < L.count; ++s) {
+            uint64_t m;
+            std::memcpy(&m, blk + kLeafHdr + 24 * s, 8);
+            meta_[b + s] = m;
+            next_[b + s] = 0;
+            if (!m) {
+                okey_[b + s] = 0;
+                image_[b + s] = 0;
+                continue;
+            }
+            const uint32_t kl = meta_keylen(m), off = meta_offset(m);
+            uint64_t kw = 0;
+            std::memcpy(&kw, blk + off, kl);
+            okey_[b + s] = order_key(kw, kl);
+            image_[b + s] = new_image(kw, blk + off + pad8(kl), 0, 0);
+        }
+    }
+    // router: every bucket lists, in key order, each leaf whose range (sep[i-1], sep[i]] meets it
+    for (auto &v : buckets_) v.clear();
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint32_t id = (uint32_t)(head_ + i);
+        const uint32_t b_lo = i == 0 ? 0 : bucket_of(sep[i - 1].okey);
+        const uint32_t b_hi = key_is_inf(sep[i]) ? (uint32_t)buckets_.size() - 1 : bucket_of(sep[i].okey);
+        for (uint32_t bk = b_lo; bk <= b_hi; ++bk) buckets_[bk].push_back(RouteEntry{sep[i].okey, id, sep[i].len});
+    }
+    layout_dirty_ = true;
+    structure_dirty_ = true;
+    dirty_slots_.clear();
+    return nrec;
+}
+
 }  // namespace stage

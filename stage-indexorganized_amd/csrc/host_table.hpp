@@ -64,6 +64,11 @@ public:
     int64_t export_leaves(uint32_t cap, uint64_t max_leaves, uint32_t *rc, uint32_t *sc, uint64_t *meta,
                           uint64_t *keyw) const;
 
+    // leaf-level snapshot in the reference's 64 KiB block format (see host_table.cpp)
+    int64_t export_leaf_images(uint64_t max_leaves, uint8_t *blocks, uint64_t *sep_key_le, uint16_t *sep_len) const;
+    uint64_t import_leaf_images(const uint8_t *blocks, uint64_t n, uint32_t block_size, const uint64_t *sep_key_le,
+                                const uint16_t *sep_len);
+
     // storage (read by the device-image builder)
     struct Leaf {
         uint32_t count = 0, sorted = 0, block = 0, deleted = 0;

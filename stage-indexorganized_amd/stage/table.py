@@ -111,6 +111,7 @@ class Table:
         check(lib().stage_table_create(ctypes.byref(p), ctypes.byref(h)), "stage_table_create")
         self.h = h.value
         self.payload_size = payload_size
+        self.leaf_node_size = leaf_node_size
         self.key_width = key_width
         self.device = device
 
@@ -231,6 +232,26 @@ class Table:
         if got < 0:
             raise RuntimeError("export_leaves failed")
         return rc, sc, meta.reshape(nl, cap), keyw.reshape(nl, cap)
+
+    def export_leaf_images(self):
+        """Reference-format leaf blocks in key order + upper separators (key_le, len; 0xFFFF = +inf)."""
+        nl = self.stats()["leaves"]
+        blocks = np.zeros((nl, self.leaf_node_size), np.uint8)
+        sk = np.zeros(nl, np.uint64)
+        sl = np.zeros(nl, np.uint16)
+        got = lib().stage_export_leaf_images(self.h, nl, blocks.ctypes.data, sk.ctypes.data, sl.ctypes.data)
+        if got < 0:
+            check(int(got), "export_leaf_images")
+        return blocks[:got], sk[:got], sl[:got]
+
+    def import_leaf_images(self, blocks, sep_keys=None, sep_lens=None):
+        blocks = np.ascontiguousarray(blocks, np.uint8)
+        n = ctypes.c_uint64()
+        sk = None if sep_keys is None else np.ascontiguousarray(sep_keys, np.uint64)
+        sl = None if sep_lens is None else np.ascontiguousarray(sep_lens, np.uint16)
+        check(lib().stage_import_leaf_images(self.h, blocks.ctypes.data, blocks.shape[0], blocks.shape[1], _ptr(sk),
+                                             _ptr(sl), ctypes.byref(n)), "import_leaf_images")
+        return n.value
 
     def traverse(self, keys, lens=None, le_child=True):
         keys = np.ascontiguousarray(keys, np.uint64)

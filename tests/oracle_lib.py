@@ -39,6 +39,7 @@ _SIG = {
     "orc_delete": (ctypes.c_int, [vp, vp, u32, u32]),
     "orc_stats": (None, [vp, vp]),
     "orc_export_leaves": (ctypes.c_int64, [vp, u32, u64, vp, vp, vp, vp]),
+    "orc_export_leaf_images": (ctypes.c_int64, [vp, u64, vp, vp, vp]),
     "orc_key_compare": (ctypes.c_int, [vp, u32, vp, u32]),
     "orc_murmur64a": (u64, [vp, ctypes.c_int, u64]),
     "orc_murmur64a_batch": (None, [vp, u64, ctypes.c_int, u64, vp]),
@@ -77,6 +78,7 @@ class OracleTree:
         self.t = lib().orc_tree_new(leaf_node_size, split_threshold, payload_size)
         lib().orc_tree_set_merge_threshold(self.t, merge_threshold)
         self.payload_size = payload_size
+        self.leaf_node_size = leaf_node_size
         self.row = 8 + payload_size
 
     def __del__(self):
@@ -150,6 +152,15 @@ class OracleTree:
         lib().orc_stats(self.t, s.ctypes.data)
         keys = ["height", "inner", "leaves", "records", "sorted", "unsorted", "max_count", "versions"]
         return {k: int(v) for k, v in zip(keys, s)}
+
+    def export_leaf_images(self):
+        nl = self.stats()["leaves"]
+        blocks = np.zeros((nl, self.leaf_node_size), np.uint8)
+        sk = np.zeros(nl, np.uint64)
+        sl = np.zeros(nl, np.uint16)
+        got = lib().orc_export_leaf_images(self.t, nl, blocks.ctypes.data, sk.ctypes.data, sl.ctypes.data)
+        assert got == nl
+        return blocks, sk, sl
 
     def export_leaves(self, cap):
         nl = self.stats()["leaves"]
