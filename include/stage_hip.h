@@ -230,6 +230,16 @@ int stage_comm_destroy(stage_table *t);
 int stage_probe_sharded(stage_table *t, const uint64_t *d_keys, const uint32_t *d_read_ids,
                         uint64_t n, stage_probe_out *d_out, uint8_t *d_records, void *stream);
 
+/* single-process rehearsal of stage_probe_sharded: `world` shard tables on ONE device play the
+ * ranks; the routing, count exchange, offsets, local probes and un-permutation are the same
+ * code, with device-to-device copies where the RCCL path has ncclSend/ncclRecv.  Arrays are
+ * indexed by rank (d_read_ids may be NULL; d_records all NULL or none).  For testing the
+ * multi-GPU data path on one GPU. */
+int stage_probe_sharded_loopback(stage_table *const *shards, int world, const uint64_t *const *d_keys,
+                                 const uint32_t *const *d_read_ids, const uint64_t *n,
+                                 stage_probe_out *const *d_out, uint8_t *const *d_records,
+                                 void *stream);
+
 /* ---- plumbing for callers without their own HIP binding (ctypes) ----------------------- */
 int stage_set_device(int device);
 int stage_device_count(int *count);

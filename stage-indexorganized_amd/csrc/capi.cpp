@@ -27,6 +27,8 @@ int stage_table_create(const stage_params *params, stage_table **out) {
         t->dev.device = params->device;
         if (const char *g = std::getenv("STAGE_PROBE_GROUP")) t->tune.group = std::atoi(g);
         if (const char *g = std::getenv("STAGE_PROBE_MAX_BLOCKS")) t->tune.max_blocks = std::atoi(g);
+        if (const char *g = std::getenv("STAGE_SCAN_ROWS")) t->scan_tune.rows = std::atoi(g);
+        if (const char *g = std::getenv("STAGE_SCAN_MAX_BLOCKS")) t->scan_tune.max_blocks = std::atoi(g);
         if (const char *g = std::getenv("STAGE_OUT_STRIDE")) {
             uint32_t v = (uint32_t)std::atoi(g);
             if (v >= t->host->stride() && v % 16 == 0) t->out_stride = v;
@@ -238,7 +240,8 @@ int stage_scan_batch(stage_table *t, const uint64_t *d_start_keys, const uint16_
     if (n && (!d_start_keys || !d_counts || (!d_records && scan_size))) return fail(STAGE_E_ARG, "null device buffer");
     hipError_t e = hipSetDevice(t->dev.device);
     if (e != hipSuccess) return hip_rc(e, "hipSetDevice");
-    e = stage::launch_scan(t->dev.view, d_start_keys, d_lens, n, scan_size, d_counts, d_records, pick(t, stream));
+    e = stage::launch_scan(t->dev.view, d_start_keys, d_lens, n, scan_size, d_counts, d_records, pick(t, stream),
+                          t->scan_tune);
     return hip_rc(e, "scan kernel");
 }
 
@@ -337,6 +340,43 @@ int stage_probe_sharded(stage_table *t, const uint64_t *d_keys, const uint32_t *
         (void)hipSetDevice(t->dev.device);
         return stage::shard_probe(*t->comm, t->dev.view, t->tune, d_keys, d_read_ids, n,
                                   reinterpret_cast<stage::stage_probe_out_dev *>(d_out), d_records, pick(t, stream));
+    });
+}
+
+int stage_probe_sharded_loopback(stage_table *const *shards, int world, const uint64_t *const *d_keys,
+                                 const uint32_t *const *d_read_ids, const uint64_t *n, stage_probe_out *const *d_out,
+                                 uint8_t *const *d_records, void *stream) {
+    if (!shards || world < 1 || !d_keys || !n || !d_out || !d_records) return fail(STAGE_E_ARG, "null argument");
+    for (int r = 0; r < world; ++r) {
+        int rc = need_synced(shards[r]);
+        if (rc) return rc;
+        if (shards[r]->dev.device != shards[0]->dev.device) return fail(STAGE_E_ARG, "shards on different devices");
+        if ((d_records[r] == nullptr) != (d_records[0] == nullptr)) return fail(STAGE_E_ARG, "rows for all or none");
+    }
+    return guarded([&] {
+        (void)hipSetDevice(shards[0]->dev.device);
+        std::vector<stage::ShardComm *> cs(world);
+        std::vector<const stage::DevTable *> ts(world);
+        std::vector<const uint64_t *> ks(world);
+        std::vector<const uint32_t *> rs(world);
+        std::vector<uint64_t> ns(world);
+        std::vector<stage::stage_probe_out_dev *> os(world);
+        std::vector<uint8_t *> recs(world);
+        for (int r = 0; r < world; ++r) {
+            stage_table *t = shards[r];
+            if (!t->loop_comm || t->loop_comm->world != world || t->loop_comm->rank != r) {
+                t->loop_comm = std::make_unique<stage::ShardComm>();
+                stage::shard_init_loopback(*t->loop_comm, r, world);
+            }
+            cs[r] = t->loop_comm.get();
+            ts[r] = &t->dev.view;
+            ks[r] = d_keys[r];
+            rs[r] = d_read_ids ? d_read_ids[r] : nullptr;
+            ns[r] = n[r];
+            os[r] = reinterpret_cast<stage::stage_probe_out_dev *>(d_out[r]);
+            recs[r] = d_records[r];
+        }
+        return stage::shard_probe_loopback(cs, ts, shards[0]->tune, ks, rs, ns, os, recs, pick(shards[0], stream));
     });
 }
 

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -176,10 +177,13 @@ int shard_init(ShardComm &c, const uint8_t *id128, int rank, int world) {
     return STAGE_OK;
 }
 
-int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const uint64_t *d_keys,
-                const uint32_t *d_rids, uint64_t n, stage_probe_out_dev *d_out, uint8_t *d_recs, hipStream_t s) {
+// ---- the phases of one sharded probe (shared by the RCCL path and the loopback rehearsal)
+
+// route the caller's keys: send buffer grouped by destination, perm = caller index of each
+// send slot; returns the per-destination counts (host)
+static std::vector<uint32_t> phase_route(ShardComm &c, const uint64_t *d_keys, const uint32_t *d_rids, uint64_t n,
+                                         uint32_t stride, hipStream_t s) {
     const int W = c.world;
-    const uint32_t stride = t.stride;
     if (n > 0xFFFFFFFFull) throw std::invalid_argument("batch too large");
     if (n > c.cap_local || stride != c.rec_stride) {
         const uint64_t cap = n + n / 8 + 1024;
@@ -190,6 +194,7 @@ int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const 
         grow(c.brec, cap * stride);
         c.cap_local = cap;
         c.rec_stride = stride;
+        c.cap_remote = 0;  // remote buffers follow the stride too
     }
     uint32_t *counts = (uint32_t *)c.cnt;  // [0,W) send counts, [2W,3W) recv counts
     uint32_t *blk = (uint32_t *)c.cursor, *offs = blk + (uint64_t)W * kRouteBlocks;
@@ -201,46 +206,77 @@ int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const 
     } else {
         chk(hipMemsetAsync(counts, 0, W * sizeof(uint32_t), s), "memset");
     }
-    std::vector<uint32_t> sc(W), rc(W);
+    std::vector<uint32_t> sc(W);
     chk(hipMemcpyAsync(sc.data(), counts, W * 4, hipMemcpyDeviceToHost, s), "counts d2h");
     chk(hipStreamSynchronize(s), "sync");
-    std::vector<uint32_t> soff(W + 1, 0);
-    for (int r = 0; r < W; ++r) soff[r + 1] = soff[r] + sc[r];
+    return sc;
+}
+
+static void ensure_remote(ShardComm &c, uint64_t m, uint32_t stride) {
+    if (m <= c.cap_remote) return;
+    const uint64_t cap = m + m / 8 + 1024;
+    grow(c.recv, cap * sizeof(SendRec));
+    grow(c.rout, cap * sizeof(stage_probe_out_dev));
+    grow(c.rrec, cap * stride);
+    grow(c.lkeys, cap * 8);
+    grow(c.lrids, cap * 4);
+    c.cap_remote = cap;
+}
+
+// probe the m keys this shard received (recv buffer) into rout / rrec
+static void phase_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, uint64_t m, bool rows,
+                        hipStream_t s) {
+    if (!m) return;
+    uint64_t *lk = (uint64_t *)c.lkeys;
+    uint32_t *lr = (uint32_t *)c.lrids;
+    unpack_keys<<<(unsigned)((m + 255) / 256), 256, 0, s>>>((const SendRec *)c.recv, m, lk, lr);
+    chk(launch_probe(t, lk, nullptr, lr, nullptr, m, (stage_probe_out_dev *)c.rout, rows ? (uint8_t *)c.rrec : nullptr,
+                     s, tune),
+        "probe");
+}
+
+static void phase_unpermute(ShardComm &c, uint64_t n, uint32_t stride, stage_probe_out_dev *d_out, uint8_t *d_recs,
+                            hipStream_t s) {
+    if (n)
+        unpermute<<<(unsigned)std::min<uint64_t>((n + 3) / 4, 8192), 256, 0, s>>>(
+            (const stage_probe_out_dev *)c.bout, (const uint8_t *)c.brec, (const uint32_t *)c.perm, n, stride, d_out,
+            d_recs);
+    chk(hipGetLastError(), "unpermute");
+}
+
+static std::vector<uint64_t> prefix(const std::vector<uint32_t> &v) {
+    std::vector<uint64_t> o(v.size() + 1, 0);
+    for (size_t r = 0; r < v.size(); ++r) o[r + 1] = o[r] + v[r];
+    return o;
+}
+
+int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const uint64_t *d_keys,
+                const uint32_t *d_rids, uint64_t n, stage_probe_out_dev *d_out, uint8_t *d_recs, hipStream_t s) {
+    if (!c.comm) throw std::invalid_argument("not an RCCL communicator");
+    const int W = c.world;
+    const uint32_t stride = t.stride;
+    const std::vector<uint32_t> sc = phase_route(c, d_keys, d_rids, n, stride, s);
+    const std::vector<uint64_t> soff = prefix(sc);
     // exchange the per-destination counts
+    uint32_t *counts = (uint32_t *)c.cnt;
     ncclComm_t comm = (ncclComm_t)c.comm;
     nchk(ncclAllToAll(counts, counts + 2 * W, 1, ncclUint32, comm, s), "ncclAllToAll counts");
+    std::vector<uint32_t> rc(W);
     chk(hipMemcpyAsync(rc.data(), counts + 2 * W, W * 4, hipMemcpyDeviceToHost, s), "recv counts d2h");
     chk(hipStreamSynchronize(s), "sync");
-    std::vector<uint64_t> roff(W + 1, 0);
-    for (int r = 0; r < W; ++r) roff[r + 1] = roff[r] + rc[r];
+    const std::vector<uint64_t> roff = prefix(rc);
     const uint64_t m = roff[W];
-    if (m > c.cap_remote || stride != c.rec_stride) {
-        const uint64_t cap = m + m / 8 + 1024;
-        grow(c.recv, cap * sizeof(SendRec));
-        grow(c.rout, cap * sizeof(stage_probe_out_dev));
-        grow(c.rrec, cap * stride);
-        grow(c.lkeys, cap * 8);
-        grow(c.lrids, cap * 4);
-        c.cap_remote = cap;
-    }
+    ensure_remote(c, m, stride);
     // keys out: all-to-all-v as grouped point-to-point transfers
     nchk(ncclGroupStart(), "group");
     for (int r = 0; r < W; ++r) {
-        if (sc[r]) nchk(ncclSend((const uint8_t *)c.send + (uint64_t)soff[r] * sizeof(SendRec), (uint64_t)sc[r] * sizeof(SendRec),
+        if (sc[r]) nchk(ncclSend((const uint8_t *)c.send + soff[r] * sizeof(SendRec), (uint64_t)sc[r] * sizeof(SendRec),
                                  ncclUint8, r, comm, s), "send keys");
         if (rc[r]) nchk(ncclRecv((uint8_t *)c.recv + roff[r] * sizeof(SendRec), (uint64_t)rc[r] * sizeof(SendRec), ncclUint8,
                                  r, comm, s), "recv keys");
     }
     nchk(ncclGroupEnd(), "group end");
-    // local probe of everything this shard owns
-    uint64_t *lk = (uint64_t *)c.lkeys;
-    uint32_t *lr = (uint32_t *)c.lrids;
-    if (m) {
-        unpack_keys<<<(unsigned)((m + 255) / 256), 256, 0, s>>>((const SendRec *)c.recv, m, lk, lr);
-        chk(launch_probe(t, lk, nullptr, lr, nullptr, m, (stage_probe_out_dev *)c.rout,
-                         d_recs ? (uint8_t *)c.rrec : nullptr, s, tune),
-            "probe");
-    }
+    phase_probe(c, t, tune, m, d_recs != nullptr, s);
     // results back
     const uint64_t ob = sizeof(stage_probe_out_dev);
     nchk(ncclGroupStart(), "group");
@@ -252,18 +288,75 @@ int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const 
                      "send rows");
         }
         if (sc[r]) {
-            nchk(ncclRecv((uint8_t *)c.bout + (uint64_t)soff[r] * ob, (uint64_t)sc[r] * ob, ncclUint8, r, comm, s), "recv out");
+            nchk(ncclRecv((uint8_t *)c.bout + soff[r] * ob, (uint64_t)sc[r] * ob, ncclUint8, r, comm, s), "recv out");
             if (d_recs)
-                nchk(ncclRecv((uint8_t *)c.brec + (uint64_t)soff[r] * stride, (uint64_t)sc[r] * stride, ncclUint8, r, comm, s),
+                nchk(ncclRecv((uint8_t *)c.brec + soff[r] * stride, (uint64_t)sc[r] * stride, ncclUint8, r, comm, s),
                      "recv rows");
         }
     }
     nchk(ncclGroupEnd(), "group end");
-    if (n)
-        unpermute<<<(unsigned)std::min<uint64_t>((n + 3) / 4, 8192), 256, 0, s>>>(
-            (const stage_probe_out_dev *)c.bout, (const uint8_t *)c.brec, (const uint32_t *)c.perm, n, stride, d_out,
-            d_recs);
-    chk(hipGetLastError(), "unpermute");
+    phase_unpermute(c, n, stride, d_out, d_recs, s);
+    return STAGE_OK;
+}
+
+int shard_init_loopback(ShardComm &c, int rank, int world) {
+    if (world < 1 || world > kMaxWorld || rank < 0 || rank >= world) throw std::invalid_argument("bad rank/world");
+    c.comm = nullptr;
+    c.rank = rank;
+    c.world = world;
+    grow(c.cnt, 4 * sizeof(uint32_t) * (uint64_t)world);
+    grow(c.cursor, (2ull * world * kRouteBlocks + 16) * sizeof(uint32_t));
+    return STAGE_OK;
+}
+
+// The same phases for W shards held by one process on one device, with device-to-device
+// copies where shard_probe has RCCL transfers (same offsets, same order).  Every shard's
+// stride must be equal.
+int shard_probe_loopback(const std::vector<ShardComm *> &cs, const std::vector<const DevTable *> &ts,
+                         const ProbeTuning &tune, const std::vector<const uint64_t *> &keys,
+                         const std::vector<const uint32_t *> &rids, const std::vector<uint64_t> &n,
+                         const std::vector<stage_probe_out_dev *> &outs, const std::vector<uint8_t *> &recs,
+                         hipStream_t s) {
+    const int W = (int)cs.size();
+    const uint32_t stride = ts[0]->stride;
+    for (int r = 0; r < W; ++r)
+        if (ts[r]->stride != stride || cs[r]->world != W || cs[r]->rank != r)
+            throw std::invalid_argument("loopback shards disagree on stride / rank / world");
+    const bool rows = recs[0] != nullptr;
+    std::vector<std::vector<uint32_t>> sc(W), rc(W, std::vector<uint32_t>(W));
+    std::vector<std::vector<uint64_t>> soff(W), roff(W);
+    for (int r = 0; r < W; ++r) {
+        sc[r] = phase_route(*cs[r], keys[r], rids[r], n[r], stride, s);
+        soff[r] = prefix(sc[r]);
+    }
+    for (int r = 0; r < W; ++r)
+        for (int q = 0; q < W; ++q) rc[r][q] = sc[q][r];  // what the count all-to-all delivers
+    for (int r = 0; r < W; ++r) {
+        roff[r] = prefix(rc[r]);
+        ensure_remote(*cs[r], roff[r][W], stride);
+    }
+    for (int r = 0; r < W; ++r)  // keys: q's send segment for r -> r's receive segment from q
+        for (int q = 0; q < W; ++q)
+            if (sc[q][r])
+                chk(hipMemcpyAsync((uint8_t *)cs[r]->recv + roff[r][q] * sizeof(SendRec),
+                                   (const uint8_t *)cs[q]->send + soff[q][r] * sizeof(SendRec),
+                                   (uint64_t)sc[q][r] * sizeof(SendRec), hipMemcpyDeviceToDevice, s),
+                    "loopback keys");
+    for (int r = 0; r < W; ++r) phase_probe(*cs[r], *ts[r], tune, roff[r][W], rows, s);
+    const uint64_t ob = sizeof(stage_probe_out_dev);
+    for (int q = 0; q < W; ++q)  // results: owner q's segment for origin r -> r's slots of q
+        for (int r = 0; r < W; ++r)
+            if (rc[q][r]) {
+                chk(hipMemcpyAsync((uint8_t *)cs[r]->bout + soff[r][q] * ob, (const uint8_t *)cs[q]->rout + roff[q][r] * ob,
+                                   (uint64_t)rc[q][r] * ob, hipMemcpyDeviceToDevice, s),
+                    "loopback out");
+                if (rows)
+                    chk(hipMemcpyAsync((uint8_t *)cs[r]->brec + soff[r][q] * stride,
+                                       (const uint8_t *)cs[q]->rrec + roff[q][r] * stride, (uint64_t)rc[q][r] * stride,
+                                       hipMemcpyDeviceToDevice, s),
+                        "loopback rows");
+            }
+    for (int r = 0; r < W; ++r) phase_unpermute(*cs[r], n[r], stride, outs[r], recs[r], s);
     return STAGE_OK;
 }
 

@@ -28,6 +28,15 @@ int shard_init(ShardComm &c, const uint8_t *id128, int rank, int world);
 int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const uint64_t *d_keys,
                 const uint32_t *d_rids, uint64_t n, stage_probe_out_dev *d_out, uint8_t *d_recs, hipStream_t s);
 
+// single-process rehearsal of shard_probe for W shards on one device (device copies in place
+// of the RCCL transfers): the routing, offsets and permutations are the same code
+int shard_init_loopback(ShardComm &c, int rank, int world);
+int shard_probe_loopback(const std::vector<ShardComm *> &cs, const std::vector<const DevTable *> &ts,
+                         const ProbeTuning &tune, const std::vector<const uint64_t *> &keys,
+                         const std::vector<const uint32_t *> &rids, const std::vector<uint64_t> &n,
+                         const std::vector<stage_probe_out_dev *> &outs, const std::vector<uint8_t *> &recs,
+                         hipStream_t s);
+
 void set_error(const std::string &msg);
 
 }  // namespace stage

@@ -26,8 +26,10 @@ struct stage_table {
     std::unique_ptr<stage::HostTable> host;
     stage::DeviceImage dev;
     stage::ProbeTuning tune;
+    stage::ScanTuning scan_tune;
     uint32_t out_stride = 0;  // 0 = stride of the canonical row; STAGE_OUT_STRIDE overrides (A/B)
     std::unique_ptr<stage::ShardComm> comm;
+    std::unique_ptr<stage::ShardComm> loop_comm;  // stage_probe_sharded_loopback state
     std::mutex pipe_mu;  // serialises stage_probe_host calls on this table
     std::unique_ptr<stage::HostPipe, stage::HostPipeDeleter> pipe;
 };

@@ -32,8 +32,13 @@ hipError_t launch_resolve(const DevTable &t, const uint64_t *keys, const uint16_
 hipError_t launch_probe(const DevTable &t, const uint64_t *keys, const uint16_t *lens, const uint32_t *rids,
                         const uint32_t *leaf_in, uint64_t n, stage_probe_out_dev *out, uint8_t *recs, hipStream_t s,
                         const ProbeTuning &tune);
+struct ScanTuning {
+    int rows = 4;        // tuple rows in flight per wave (2, 4 or 8)
+    int max_blocks = 0;  // 0 = default grid cap (16384 blocks of 256 threads)
+};
+
 hipError_t launch_scan(const DevTable &t, const uint64_t *keys, const uint16_t *lens, uint64_t n, uint32_t scan_size,
-                       uint32_t *counts, uint8_t *recs, hipStream_t s);
+                       uint32_t *counts, uint8_t *recs, hipStream_t s, const ScanTuning &tune);
 hipError_t launch_murmur(const void *keys, uint32_t key_len, uint32_t key_stride, uint64_t seed, uint64_t n,
                          uint64_t *out, hipStream_t s);
 hipError_t launch_fill(uint8_t *heap, uint32_t stride, uint32_t payload_size, const ImageDescDev *descs,

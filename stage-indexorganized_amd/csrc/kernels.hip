@@ -336,25 +336,26 @@ __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *
 // ----------------------------------------------------------------------------------------
 // range scan (TableScanExecutor over Iterator), one wave per scan
 
-__device__ __forceinline__ void copy_rows4(const DevTable &t, const uint32_t *img, const uint32_t *dst, int n,
-                                           uint8_t *recs, uint32_t lane) {
+template <int R>
+__device__ __forceinline__ void copy_rows(const DevTable &t, const uint32_t *img, const uint32_t *dst, int n,
+                                          uint8_t *recs, uint32_t lane) {
     const uint32_t chunks = t.stride >> 4;
     for (uint32_t c0 = 0; c0 < chunks; c0 += 64) {
         const uint32_t c = c0 + lane;
-        u32x4 v[4];
+        u32x4 v[R];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < R; ++k) {
             v[k] = u32x4{0, 0, 0, 0};
             if (k < n && c < chunks) v[k] = reinterpret_cast<const u32x4 *>(t.heap + (uint64_t)img[k] * t.hstride)[c];
         }
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
+        for (int k = 0; k < R; ++k)
             if (k < n && c < chunks)
                 __builtin_nontemporal_store(v[k], reinterpret_cast<u32x4 *>(recs + (uint64_t)dst[k] * t.stride) + c);
     }
 }
 
-template <bool VARLEN, int SPL>
+template <bool VARLEN, int SPL, int R>
 __device__ void scan_one(const DevTable &t, uint64_t x, uint32_t xl, uint32_t leaf, uint32_t scan_size,
                          uint8_t *recs, uint32_t *count_out, uint32_t lane) {
     uint32_t remaining = scan_size, produced = 0;
@@ -424,15 +425,15 @@ __device__ void scan_one(const DevTable &t, uint64_t x, uint32_t xl, uint32_t le
             if (emit) img = t.slot[base + s * 64 + lane].image;
             uint64_t em = ballot(emit);
             while (em) {
-                uint32_t im4[4], d4[4];
+                uint32_t imr[R], dr[R];
                 int nk = 0;
-                for (; nk < 4 && em; ++nk) {
+                for (; nk < R && em; ++nk) {
                     const int b = __builtin_ctzll(em);
                     em &= em - 1;
-                    im4[nk] = rl32(img, b);
-                    d4[nk] = produced + rl32(kr[s], b);
+                    imr[nk] = rl32(img, b);
+                    dr[nk] = produced + rl32(kr[s], b);
                 }
-                copy_rows4(t, im4, d4, nk, recs, lane);
+                copy_rows<R>(t, imr, dr, nk, recs, lane);
             }
         }
         produced += e;
@@ -458,24 +459,21 @@ __device__ void scan_one(const DevTable &t, uint64_t x, uint32_t xl, uint32_t le
     if (lane == 0) *count_out = produced;
 }
 
-template <bool VARLEN, int SPL>
+// One wave per scan (grid-stride over scans): the start key's descent is wave-uniform, and a
+// wide grid keeps many scans -- and their R rows in flight each -- resident per CU.
+template <bool VARLEN, int SPL, int R>
 __global__ __launch_bounds__(256) void scan_kernel(DevTable t, const uint64_t *__restrict__ keys,
                                                    const uint16_t *__restrict__ lens, uint64_t n, uint32_t scan_size,
                                                    uint32_t *__restrict__ counts, uint8_t *__restrict__ recs) {
     const uint32_t lane = lane_id();
     const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    for (uint64_t base = wave * 64; base < n; base += nwaves * 64) {
-        const uint64_t i = base + lane;
-        const bool valid = i < n;
-        const uint32_t len = t.key_width ? t.key_width : (lens && valid ? (uint32_t)lens[i] : 8u);
-        const uint64_t ok = order_key(valid ? keys[i] : 0, len);
-        const uint32_t leaf = valid ? resolve_leaf<VARLEN>(t, ok, len, true) : 0u;
-        const int cnt = (int)((n - base) < 64 ? (n - base) : 64);
-        for (int j = 0; j < cnt; ++j) {
-            scan_one<VARLEN, SPL>(t, rl64(ok, j), rl32(len, j), rl32(leaf, j), scan_size,
-                                  recs + (base + j) * (uint64_t)scan_size * t.stride, counts + base + j, lane);
-        }
+    for (uint64_t i = wave; i < n; i += nwaves) {
+        const uint32_t len = t.key_width ? t.key_width : (lens ? (uint32_t)lens[i] : 8u);
+        const uint64_t ok = order_key(keys[i], len);
+        const uint32_t leaf = uni32(resolve_leaf<VARLEN>(t, ok, len, true));
+        scan_one<VARLEN, SPL, R>(t, ok, len, leaf, scan_size, recs + i * (uint64_t)scan_size * t.stride, counts + i,
+                                 lane);
     }
 }
 
@@ -653,19 +651,26 @@ hipError_t launch_probe(const DevTable &t, const uint64_t *keys, const uint16_t 
     return hipGetLastError();
 }
 
-hipError_t launch_scan(const DevTable &t, const uint64_t *keys, const uint16_t *lens, uint64_t n, uint32_t scan_size,
-                       uint32_t *counts, uint8_t *recs, hipStream_t s) {
-    if (n == 0) return hipSuccess;
-    const uint64_t chunks = (n + 63) / 64;
-    const int blocks = grid_for(chunks, 4, 4096);
+template <int R>
+static void launch_scan_r(const DevTable &t, const uint64_t *keys, const uint16_t *lens, uint64_t n,
+                          uint32_t scan_size, uint32_t *counts, uint8_t *recs, hipStream_t s, int blocks) {
     const bool var = t.key_width == 0;
     if (t.cap == 64) {
-        if (var) scan_kernel<true, 1><<<blocks, 256, 0, s>>>(t, keys, lens, n, scan_size, counts, recs);
-        else scan_kernel<false, 1><<<blocks, 256, 0, s>>>(t, keys, lens, n, scan_size, counts, recs);
+        if (var) scan_kernel<true, 1, R><<<blocks, 256, 0, s>>>(t, keys, lens, n, scan_size, counts, recs);
+        else scan_kernel<false, 1, R><<<blocks, 256, 0, s>>>(t, keys, lens, n, scan_size, counts, recs);
     } else {
-        if (var) scan_kernel<true, 2><<<blocks, 256, 0, s>>>(t, keys, lens, n, scan_size, counts, recs);
-        else scan_kernel<false, 2><<<blocks, 256, 0, s>>>(t, keys, lens, n, scan_size, counts, recs);
+        if (var) scan_kernel<true, 2, R><<<blocks, 256, 0, s>>>(t, keys, lens, n, scan_size, counts, recs);
+        else scan_kernel<false, 2, R><<<blocks, 256, 0, s>>>(t, keys, lens, n, scan_size, counts, recs);
     }
+}
+
+hipError_t launch_scan(const DevTable &t, const uint64_t *keys, const uint16_t *lens, uint64_t n, uint32_t scan_size,
+                       uint32_t *counts, uint8_t *recs, hipStream_t s, const ScanTuning &tune) {
+    if (n == 0) return hipSuccess;
+    const int blocks = grid_for(n, 4, tune.max_blocks > 0 ? tune.max_blocks : 16384);
+    if (tune.rows == 8) launch_scan_r<8>(t, keys, lens, n, scan_size, counts, recs, s, blocks);
+    else if (tune.rows == 2) launch_scan_r<2>(t, keys, lens, n, scan_size, counts, recs, s, blocks);
+    else launch_scan_r<4>(t, keys, lens, n, scan_size, counts, recs, s, blocks);
     return hipGetLastError();
 }
 

@@ -367,6 +367,48 @@ class Reader:
             pass
 
 
+def probe_sharded_loopback(tables, keys_per_rank, read_ids_per_rank=None, records=True):
+    """stage_probe_sharded_loopback: rank r's keys are routed across the shard tables (all on
+    one device) exactly as stage_probe_sharded routes them over RCCL; returns per-rank
+    (out, rows) in each rank's own key order."""
+    W = len(tables)
+    keep = []
+    k_ptrs, r_ptrs, o_ptrs, rec_ptrs, ns = [], [], [], [], []
+    stride = tables[0].stride
+    for r in range(W):
+        k = np.ascontiguousarray(keys_per_rank[r], np.uint64)
+        n = k.size
+        dk = DeviceBuffer.from_numpy(k) if n else DeviceBuffer(8)
+        do = DeviceBuffer(max(n, 1) * 32)
+        dr = DeviceBuffer(max(n, 1) * stride) if records else None
+        keep.append((dk, do, dr))
+        k_ptrs.append(dk.ptr)
+        o_ptrs.append(do.ptr)
+        rec_ptrs.append(dr.ptr if dr else None)
+        ns.append(n)
+        if read_ids_per_rank is not None:
+            ri = np.ascontiguousarray(read_ids_per_rank[r], np.uint32)
+            drid = DeviceBuffer.from_numpy(ri) if n else DeviceBuffer(4)
+            keep.append((drid,))
+            r_ptrs.append(drid.ptr)
+    arr = lambda v: (ctypes.c_void_p * W)(*v)
+    hs = (ctypes.c_void_p * W)(*[t.h for t in tables])
+    n_arr = (ctypes.c_uint64 * W)(*ns)
+    check(lib().stage_probe_sharded_loopback(hs, W, arr(k_ptrs), arr(r_ptrs) if r_ptrs else None, n_arr, arr(o_ptrs),
+                                             arr(rec_ptrs), None), "probe_sharded_loopback")
+    check(lib().stage_device_sync(), "sync")
+    res = []
+    trip = [x for x in keep if len(x) == 3]
+    for r in range(W):
+        n = ns[r]
+        _, do, dr = trip[r]
+        out = do.to_numpy(PROBE_OUT_DTYPE, n) if n else np.zeros(0, PROBE_OUT_DTYPE)
+        rows = (dr.to_numpy(np.uint8, n * stride).reshape(n, stride) if n else np.zeros((0, stride), np.uint8)) \
+            if records else None
+        res.append((out, rows))
+    return res
+
+
 def murmur64a_device(keys, key_len=8, seed=0):
     keys = np.ascontiguousarray(keys, np.uint64)
     d_keys = DeviceBuffer.from_numpy(keys)

@@ -1,10 +1,13 @@
-"""GPU: the RCCL sharded probe front-end (stage_probe_sharded) on a one-rank communicator
-returns exactly what the direct probe returns (routing, all-to-all-v to self, unpermute)."""
+"""GPU: the sharded probe front-end.  stage_probe_sharded on a one-rank RCCL communicator
+returns exactly what the direct probe returns (routing, all-to-all-v to self, unpermute); the
+same data path with W = 2, 3, 8 shards on one device (stage_probe_sharded_loopback) returns
+what one table holding every key returns."""
 import ctypes
 
 import numpy as np
 import pytest
 
+import oracle_lib as O
 import stage
 from stage._lib import check
 
@@ -36,3 +39,56 @@ def test_sharded_world1_equals_direct(gpu):
         assert (rows == ref_rows).all()
     finally:
         check(L.stage_comm_destroy(tab.h), "destroy")
+
+
+def shard_tables(keys, world, mode=1):
+    """Rank r's shard: the keys with MurmurHash64A(key, 8, 0) % world == r, in ascending order."""
+    h = O.murmur64a_keys(keys, 8, 0)
+    tabs = []
+    for r in range(world):
+        t = stage.Table(key_width=8)
+        t.load_keys(keys[(h % np.uint64(world)) == np.uint64(r)], 8, mode=mode)
+        tabs.append(t)
+    return tabs, h
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_sharded_data_path_loopback_equals_single_table(gpu, world):
+    # the multi-GPU data path (routing, count exchange, all-to-all-v offsets, local probes,
+    # reverse exchange, un-permutation) with W shards on one device, against one table
+    # holding every key; version chains on some keys so statuses and rows vary
+    n = 400_000
+    keys = np.arange(n, dtype=np.uint64)
+    tabs, h = shard_tables(keys, world)
+    full = stage.Table(key_width=8)
+    full.load_keys(keys, 8, mode=1)
+    rng = np.random.default_rng(world)
+    hot = rng.choice(n, 3000, replace=False).astype(np.uint64)
+    for k in hot:
+        owner = tabs[int(h[int(k)] % np.uint64(world))]
+        for t in (owner, full):
+            assert t.update(int(k), 16, b"\x42" * 32, 10) == stage.RC_OK
+            assert t.commit_update(int(k), 11, 11) == stage.RC_OK
+    for t in tabs + [full]:
+        t.sync()
+    sizes = [int(x) for x in rng.integers(1, 120_000, world)]
+    sizes[-1] = 0  # a rank with nothing to probe still takes part in the exchange
+    per_keys = [np.concatenate([rng.integers(0, n + 20_000, s), rng.choice(hot, min(s, 500))]).astype(np.uint64)
+                if s else np.zeros(0, np.uint64) for s in sizes]
+    per_rids = [rng.integers(0, 14, k.size).astype(np.uint32) for k in per_keys]
+    res = stage.probe_sharded_loopback(tabs, per_keys, per_rids)
+    for r in range(world):
+        out, rows = res[r]
+        if per_keys[r].size == 0:
+            assert out.size == 0
+            continue
+        ref_out, ref_rows = full.probe(per_keys[r], read_ids=per_rids[r])
+        for f in ("status", "flags", "hops", "key_len", "cstamp", "rec_cstamp", "copy_sstamp"):
+            assert (out[f] == ref_out[f]).all(), (world, r, f)
+        assert (rows == ref_rows).all(), (world, r)
+    # and a second round reuses the grown scratch buffers, without rows
+    res2 = stage.probe_sharded_loopback(tabs, per_keys, None, records=False)
+    for r in range(world):
+        if per_keys[r].size:
+            ref_out, _ = full.probe(per_keys[r], records=False)
+            assert (res2[r][0]["status"] == ref_out["status"]).all()
