@@ -225,6 +225,10 @@ int stage_murmur64a_batch(const void *d_keys, uint32_t key_len, uint32_t key_str
  * MurmurHash64A(key, key_width, 0) % world, probes it there and returns the results in the
  * caller's order (all-to-all-v out, local probe, all-to-all-v back). */
 int stage_comm_unique_id(uint8_t *id128);
+/* the sharded batch is exchanged in `chunks` pieces whose result transfers overlap the next
+ * piece's probe (0 = STAGE_SHARD_CHUNKS env or 4); set before stage_comm_init, same value on
+ * every rank */
+int stage_set_shard_chunks(stage_table *t, int chunks);
 int stage_comm_init(stage_table *t, const uint8_t *id128, int rank, int world);
 int stage_comm_destroy(stage_table *t);
 int stage_probe_sharded(stage_table *t, const uint64_t *d_keys, const uint32_t *d_read_ids,

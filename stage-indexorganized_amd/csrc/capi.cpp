@@ -319,8 +319,14 @@ int stage_comm_init(stage_table *t, const uint8_t *id128, int rank, int world) {
     return guarded([&] {
         (void)hipSetDevice(t->dev.device);
         t->comm = std::make_unique<stage::ShardComm>();
-        return stage::shard_init(*t->comm, id128, rank, world);
+        return stage::shard_init(*t->comm, id128, rank, world, t->shard_chunks);
     });
+}
+
+int stage_set_shard_chunks(stage_table *t, int chunks) {
+    if (!t || chunks < 0 || chunks > 64) return fail(STAGE_E_ARG, "chunks must be 0..64");
+    t->shard_chunks = chunks;
+    return STAGE_OK;
 }
 
 int stage_comm_destroy(stage_table *t) {
@@ -364,9 +370,11 @@ int stage_probe_sharded_loopback(stage_table *const *shards, int world, const ui
         std::vector<uint8_t *> recs(world);
         for (int r = 0; r < world; ++r) {
             stage_table *t = shards[r];
-            if (!t->loop_comm || t->loop_comm->world != world || t->loop_comm->rank != r) {
+            const int want = shards[0]->shard_chunks > 0 ? shards[0]->shard_chunks : stage::shard_default_chunks();
+            if (!t->loop_comm || t->loop_comm->world != world || t->loop_comm->rank != r ||
+                t->loop_comm->chunks != want) {
                 t->loop_comm = std::make_unique<stage::ShardComm>();
-                stage::shard_init_loopback(*t->loop_comm, r, world);
+                stage::shard_init_loopback(*t->loop_comm, r, world, want);
             }
             cs[r] = t->loop_comm.get();
             ts[r] = &t->dev.view;

@@ -8,6 +8,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -52,6 +53,7 @@ __device__ __forceinline__ uint64_t mm64a_8(uint64_t k) {
 // scatter that claims positions with LDS atomics inside each block's range.
 constexpr int kRouteBlocks = 1024;
 constexpr int kMaxWorld = 64;
+constexpr int kDefaultChunks = 4;  // sharded batches are exchanged in this many overlapped chunks
 
 __global__ __launch_bounds__(256) void route_hist(const uint64_t *__restrict__ keys, uint64_t n, int world,
                                                   uint8_t *__restrict__ dest, uint32_t *__restrict__ blk) {
@@ -102,7 +104,7 @@ __global__ __launch_bounds__(1024) void route_scan(const uint32_t *__restrict__ 
 __global__ __launch_bounds__(256) void route_scatter(const uint64_t *__restrict__ keys, const uint32_t *__restrict__ rids,
                                                      uint64_t n, int world, const uint8_t *__restrict__ dest,
                                                      const uint32_t *__restrict__ offs, SendRec *__restrict__ send,
-                                                     uint32_t *__restrict__ perm) {
+                                                     uint32_t *__restrict__ perm, uint32_t idx_base) {
     __shared__ uint32_t cur[kMaxWorld];
     if (threadIdx.x < (unsigned)world) cur[threadIdx.x] = offs[threadIdx.x * gridDim.x + blockIdx.x];
     __syncthreads();
@@ -111,7 +113,7 @@ __global__ __launch_bounds__(256) void route_scatter(const uint64_t *__restrict_
     for (uint64_t i = b0 + threadIdx.x; i < b1; i += blockDim.x) {
         const uint32_t pos = atomicAdd(&cur[dest[i]], 1u);
         send[pos] = SendRec{keys[i], rids ? rids[i] : 0xFFFFFFFEu, 0};
-        perm[pos] = (uint32_t)i;
+        perm[pos] = idx_base + (uint32_t)i;
     }
 }
 
@@ -123,14 +125,14 @@ __global__ void unpack_keys(const SendRec *__restrict__ recv, uint64_t n, uint64
     rids[i] = recv[i].rid;
 }
 
-// back in the caller's order: out[perm[p]] = bout[p], row copy by one wave per probe
+// back in the caller's order: out[perm[p]] = bout[p] for p in [p0, p1), one wave per probe
 __global__ void unpermute(const stage_probe_out_dev *__restrict__ bout, const uint8_t *__restrict__ brec,
-                          const uint32_t *__restrict__ perm, uint64_t n, uint32_t stride,
+                          const uint32_t *__restrict__ perm, uint64_t p0, uint64_t p1, uint32_t stride,
                           stage_probe_out_dev *__restrict__ out, uint8_t *__restrict__ recs) {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    for (uint64_t p = w; p < n; p += nw) {
+    for (uint64_t p = p0 + w; p < p1; p += nw) {
         const uint32_t dst = perm[p];
         if (lane < 2) reinterpret_cast<uint4 *>(out + dst)[lane] = reinterpret_cast<const uint4 *>(bout + p)[lane];
         if (recs) {
@@ -150,6 +152,9 @@ void grow(void *&p, uint64_t bytes) {
 }  // namespace
 
 ShardComm::~ShardComm() {
+    if (cs) (void)hipStreamSynchronize(cs), (void)hipStreamDestroy(cs);
+    if (us) (void)hipStreamSynchronize(us), (void)hipStreamDestroy(us);
+    for (hipEvent_t e : evs) (void)hipEventDestroy(e);
     if (comm) ncclCommDestroy((ncclComm_t)comm);
     for (void *p : {dest, cursor, perm, send, recv, rout, rrec, bout, brec, cnt, lkeys, lrids})
         if (p) (void)hipFree(p);
@@ -163,27 +168,60 @@ int shard_unique_id(uint8_t *id128) {
     return STAGE_OK;
 }
 
-int shard_init(ShardComm &c, const uint8_t *id128, int rank, int world) {
+static void init_common(ShardComm &c, int rank, int world, int chunks) {
+    if (world < 1 || world > kMaxWorld || rank < 0 || rank >= world) throw std::invalid_argument("bad rank/world");
+    if (chunks < 1 || chunks > 64) throw std::invalid_argument("chunks must be 1..64");
+    c.rank = rank;
+    c.world = world;
+    c.chunks = chunks;
+    grow(c.cnt, 4ull * sizeof(uint32_t) * (uint64_t)world * chunks);
+    grow(c.cursor, (2ull * world * kRouteBlocks + 16) * sizeof(uint32_t));
+    chk(hipStreamCreateWithFlags(&c.cs, hipStreamNonBlocking), "comm stream");
+    chk(hipStreamCreateWithFlags(&c.us, hipStreamNonBlocking), "unpermute stream");
+    c.evs.resize(3 * chunks + 2);
+    for (auto &e : c.evs) chk(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
+}
+
+static int env_chunks() {
+    const char *e = std::getenv("STAGE_SHARD_CHUNKS");
+    return e ? std::max(1, std::min(64, std::atoi(e))) : kDefaultChunks;
+}
+
+int shard_default_chunks() { return env_chunks(); }
+
+int shard_init(ShardComm &c, const uint8_t *id128, int rank, int world, int chunks) {
+    init_common(c, rank, world, chunks > 0 ? chunks : env_chunks());
     ncclUniqueId id;
     std::memcpy(&id, id128, 128);
     ncclComm_t comm;
     nchk(ncclCommInitRank(&comm, world, id, rank), "ncclCommInitRank");
     c.comm = comm;
-    c.rank = rank;
-    c.world = world;
-    if (world > kMaxWorld) throw std::invalid_argument("world size above 64");
-    grow(c.cnt, 4 * sizeof(uint32_t) * (uint64_t)world);
-    grow(c.cursor, (2ull * world * kRouteBlocks + 16) * sizeof(uint32_t));
     return STAGE_OK;
 }
 
-// ---- the phases of one sharded probe (shared by the RCCL path and the loopback rehearsal)
+int shard_init_loopback(ShardComm &c, int rank, int world, int chunks) {
+    init_common(c, rank, world, chunks > 0 ? chunks : env_chunks());
+    c.comm = nullptr;
+    return STAGE_OK;
+}
 
-// route the caller's keys: send buffer grouped by destination, perm = caller index of each
-// send slot; returns the per-destination counts (host)
-static std::vector<uint32_t> phase_route(ShardComm &c, const uint64_t *d_keys, const uint32_t *d_rids, uint64_t n,
-                                         uint32_t stride, hipStream_t s) {
-    const int W = c.world;
+// ---- the plan of one sharded probe, shared by the RCCL path and the loopback rehearsal.
+// The caller's batch is cut into C chunks (C is the same on every rank, fixed at init, so the
+// ranks issue matching transfers).  Chunk i's keys are routed into send/perm positions
+// [cb_i, cb_{i+1}), grouped by destination; what arrives lands in recv positions
+// [rb_i, rb_{i+1}), grouped by source.  All offsets are absolute.
+struct Plan {
+    int W = 1, C = 1;
+    std::vector<uint64_t> cb, rb;           // chunk bases (send side / receive side), C+1
+    std::vector<uint32_t> sc, rc;           // [i*W + r] counts sent to / received from r
+    std::vector<uint64_t> soff, roff;       // [i*(W+1) + r] absolute segment starts
+    uint64_t m() const { return rb[C]; }
+};
+
+// route every chunk (caller stream), return the send counts [C][W] (host, synchronised)
+static void plan_route(ShardComm &c, Plan &P, const uint64_t *d_keys, const uint32_t *d_rids, uint64_t n,
+                       uint32_t stride, hipStream_t s) {
+    const int W = c.world, C = c.chunks;
     if (n > 0xFFFFFFFFull) throw std::invalid_argument("batch too large");
     if (n > c.cap_local || stride != c.rec_stride) {
         const uint64_t cap = n + n / 8 + 1024;
@@ -196,122 +234,157 @@ static std::vector<uint32_t> phase_route(ShardComm &c, const uint64_t *d_keys, c
         c.rec_stride = stride;
         c.cap_remote = 0;  // remote buffers follow the stride too
     }
-    uint32_t *counts = (uint32_t *)c.cnt;  // [0,W) send counts, [2W,3W) recv counts
+    P.W = W;
+    P.C = C;
+    P.cb.resize(C + 1);
+    for (int i = 0; i <= C; ++i) P.cb[i] = n * (uint64_t)i / (uint64_t)C;
+    uint32_t *counts = (uint32_t *)c.cnt;  // [C][W] send counts
     uint32_t *blk = (uint32_t *)c.cursor, *offs = blk + (uint64_t)W * kRouteBlocks;
-    if (n) {
-        route_hist<<<kRouteBlocks, 256, 0, s>>>(d_keys, n, W, (uint8_t *)c.dest, blk);
-        route_scan<<<1, 1024, 0, s>>>(blk, (uint32_t)(W * kRouteBlocks), W, kRouteBlocks, offs, counts);
-        route_scatter<<<kRouteBlocks, 256, 0, s>>>(d_keys, d_rids, n, W, (const uint8_t *)c.dest, offs,
-                                                   (SendRec *)c.send, (uint32_t *)c.perm);
-    } else {
-        chk(hipMemsetAsync(counts, 0, W * sizeof(uint32_t), s), "memset");
+    chk(hipMemsetAsync(counts, 0, (uint64_t)C * W * sizeof(uint32_t), s), "memset counts");
+    for (int i = 0; i < C; ++i) {
+        const uint64_t b = P.cb[i], len = P.cb[i + 1] - b;
+        if (!len) continue;
+        route_hist<<<kRouteBlocks, 256, 0, s>>>(d_keys + b, len, W, (uint8_t *)c.dest + b, blk);
+        route_scan<<<1, 1024, 0, s>>>(blk, (uint32_t)(W * kRouteBlocks), W, kRouteBlocks, offs, counts + i * W);
+        route_scatter<<<kRouteBlocks, 256, 0, s>>>(d_keys + b, d_rids ? d_rids + b : nullptr, len, W,
+                                                   (const uint8_t *)c.dest + b, offs, (SendRec *)c.send + b,
+                                                   (uint32_t *)c.perm + b, (uint32_t)b);
     }
-    std::vector<uint32_t> sc(W);
-    chk(hipMemcpyAsync(sc.data(), counts, W * 4, hipMemcpyDeviceToHost, s), "counts d2h");
+    chk(hipGetLastError(), "route");
+    P.sc.resize((size_t)C * W);
+    chk(hipMemcpyAsync(P.sc.data(), counts, (uint64_t)C * W * 4, hipMemcpyDeviceToHost, s), "counts d2h");
     chk(hipStreamSynchronize(s), "sync");
-    return sc;
+    P.soff.assign((size_t)C * (W + 1), 0);
+    for (int i = 0; i < C; ++i) {
+        P.soff[i * (W + 1)] = P.cb[i];
+        for (int r = 0; r < W; ++r) P.soff[i * (W + 1) + r + 1] = P.soff[i * (W + 1) + r] + P.sc[i * W + r];
+    }
 }
 
-static void ensure_remote(ShardComm &c, uint64_t m, uint32_t stride) {
-    if (m <= c.cap_remote) return;
-    const uint64_t cap = m + m / 8 + 1024;
-    grow(c.recv, cap * sizeof(SendRec));
-    grow(c.rout, cap * sizeof(stage_probe_out_dev));
-    grow(c.rrec, cap * stride);
-    grow(c.lkeys, cap * 8);
-    grow(c.lrids, cap * 4);
-    c.cap_remote = cap;
+// receive side of the plan from rc (filled by the transport's count exchange)
+static void plan_receive(ShardComm &c, Plan &P, uint32_t stride) {
+    const int W = P.W, C = P.C;
+    P.rb.assign(C + 1, 0);
+    P.roff.assign((size_t)C * (W + 1), 0);
+    for (int i = 0; i < C; ++i) {
+        P.roff[i * (W + 1)] = P.rb[i];
+        for (int r = 0; r < W; ++r) P.roff[i * (W + 1) + r + 1] = P.roff[i * (W + 1) + r] + P.rc[i * W + r];
+        P.rb[i + 1] = P.roff[i * (W + 1) + W];
+    }
+    const uint64_t m = P.m();
+    if (m > c.cap_remote) {
+        const uint64_t cap = m + m / 8 + 1024;
+        grow(c.recv, cap * sizeof(SendRec));
+        grow(c.rout, cap * sizeof(stage_probe_out_dev));
+        grow(c.rrec, cap * stride);
+        grow(c.lkeys, cap * 8);
+        grow(c.lrids, cap * 4);
+        c.cap_remote = cap;
+    }
 }
 
-// probe the m keys this shard received (recv buffer) into rout / rrec
-static void phase_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, uint64_t m, bool rows,
+// probe what arrived in chunk i
+static void chunk_probe(ShardComm &c, const Plan &P, int i, const DevTable &t, const ProbeTuning &tune, bool rows,
                         hipStream_t s) {
+    const uint64_t b = P.rb[i], m = P.rb[i + 1] - b;
     if (!m) return;
-    uint64_t *lk = (uint64_t *)c.lkeys;
-    uint32_t *lr = (uint32_t *)c.lrids;
-    unpack_keys<<<(unsigned)((m + 255) / 256), 256, 0, s>>>((const SendRec *)c.recv, m, lk, lr);
-    chk(launch_probe(t, lk, nullptr, lr, nullptr, m, (stage_probe_out_dev *)c.rout, rows ? (uint8_t *)c.rrec : nullptr,
-                     s, tune),
+    uint64_t *lk = (uint64_t *)c.lkeys + b;
+    uint32_t *lr = (uint32_t *)c.lrids + b;
+    unpack_keys<<<(unsigned)((m + 255) / 256), 256, 0, s>>>((const SendRec *)c.recv + b, m, lk, lr);
+    chk(launch_probe(t, lk, nullptr, lr, nullptr, m, (stage_probe_out_dev *)c.rout + b,
+                     rows ? (uint8_t *)c.rrec + b * (uint64_t)t.stride : nullptr, s, tune),
         "probe");
 }
 
-static void phase_unpermute(ShardComm &c, uint64_t n, uint32_t stride, stage_probe_out_dev *d_out, uint8_t *d_recs,
-                            hipStream_t s) {
-    if (n)
-        unpermute<<<(unsigned)std::min<uint64_t>((n + 3) / 4, 8192), 256, 0, s>>>(
-            (const stage_probe_out_dev *)c.bout, (const uint8_t *)c.brec, (const uint32_t *)c.perm, n, stride, d_out,
-            d_recs);
+static void chunk_unpermute(ShardComm &c, const Plan &P, int i, uint32_t stride, stage_probe_out_dev *d_out,
+                            uint8_t *d_recs, hipStream_t s) {
+    const uint64_t p0 = P.cb[i], p1 = P.cb[i + 1];
+    if (p1 > p0)
+        unpermute<<<(unsigned)std::min<uint64_t>((p1 - p0 + 3) / 4, 8192), 256, 0, s>>>(
+            (const stage_probe_out_dev *)c.bout, (const uint8_t *)c.brec, (const uint32_t *)c.perm, p0, p1, stride,
+            d_out, d_recs);
     chk(hipGetLastError(), "unpermute");
 }
 
-static std::vector<uint64_t> prefix(const std::vector<uint32_t> &v) {
-    std::vector<uint64_t> o(v.size() + 1, 0);
-    for (size_t r = 0; r < v.size(); ++r) o[r + 1] = o[r] + v[r];
-    return o;
-}
-
+// RCCL path.  Streams: the caller's stream s routes and probes; c.cs carries the RCCL
+// transfers; c.us un-permutes.  Order: all key exchanges first (16 B/key), then for each
+// chunk the probe (s) and, as soon as it is done, its result exchange (cs) -- so the return
+// of chunk i over xGMI overlaps the probe of chunk i+1 in HBM -- and its un-permutation (us).
 int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const uint64_t *d_keys,
                 const uint32_t *d_rids, uint64_t n, stage_probe_out_dev *d_out, uint8_t *d_recs, hipStream_t s) {
     if (!c.comm) throw std::invalid_argument("not an RCCL communicator");
-    const int W = c.world;
+    const int W = c.world, C = c.chunks;
     const uint32_t stride = t.stride;
-    const std::vector<uint32_t> sc = phase_route(c, d_keys, d_rids, n, stride, s);
-    const std::vector<uint64_t> soff = prefix(sc);
-    // exchange the per-destination counts
-    uint32_t *counts = (uint32_t *)c.cnt;
     ncclComm_t comm = (ncclComm_t)c.comm;
-    nchk(ncclAllToAll(counts, counts + 2 * W, 1, ncclUint32, comm, s), "ncclAllToAll counts");
-    std::vector<uint32_t> rc(W);
-    chk(hipMemcpyAsync(rc.data(), counts + 2 * W, W * 4, hipMemcpyDeviceToHost, s), "recv counts d2h");
+    Plan P;
+    plan_route(c, P, d_keys, d_rids, n, stride, s);
+    // count exchange: peer-major [W][C] so one all-to-all of C counts per peer carries all chunks
+    uint32_t *cnt = (uint32_t *)c.cnt, *sendT = cnt + (uint64_t)C * W, *recvT = sendT + (uint64_t)C * W;
+    std::vector<uint32_t> hT((size_t)C * W);
+    for (int i = 0; i < C; ++i)
+        for (int r = 0; r < W; ++r) hT[(size_t)r * C + i] = P.sc[(size_t)i * W + r];
+    chk(hipMemcpyAsync(sendT, hT.data(), hT.size() * 4, hipMemcpyHostToDevice, s), "counts h2d");
+    nchk(ncclAllToAll(sendT, recvT, (size_t)C, ncclUint32, comm, s), "ncclAllToAll counts");
+    chk(hipMemcpyAsync(hT.data(), recvT, hT.size() * 4, hipMemcpyDeviceToHost, s), "counts d2h");
     chk(hipStreamSynchronize(s), "sync");
-    const std::vector<uint64_t> roff = prefix(rc);
-    const uint64_t m = roff[W];
-    ensure_remote(c, m, stride);
-    // keys out: all-to-all-v as grouped point-to-point transfers
-    nchk(ncclGroupStart(), "group");
-    for (int r = 0; r < W; ++r) {
-        if (sc[r]) nchk(ncclSend((const uint8_t *)c.send + soff[r] * sizeof(SendRec), (uint64_t)sc[r] * sizeof(SendRec),
-                                 ncclUint8, r, comm, s), "send keys");
-        if (rc[r]) nchk(ncclRecv((uint8_t *)c.recv + roff[r] * sizeof(SendRec), (uint64_t)rc[r] * sizeof(SendRec), ncclUint8,
-                                 r, comm, s), "recv keys");
+    P.rc.resize((size_t)C * W);
+    for (int i = 0; i < C; ++i)
+        for (int r = 0; r < W; ++r) P.rc[(size_t)i * W + r] = hT[(size_t)r * C + i];
+    plan_receive(c, P, stride);
+    hipEvent_t *ev_keys = c.evs.data(), *ev_probe = ev_keys + C, *ev_res = ev_probe + C, ev_start = ev_res[C];
+    // the comm stream starts after the routing (done: s was synchronised) -- keys of all chunks
+    for (int i = 0; i < C; ++i) {
+        nchk(ncclGroupStart(), "group");
+        for (int r = 0; r < W; ++r) {
+            const uint32_t sn = P.sc[(size_t)i * W + r], rn = P.rc[(size_t)i * W + r];
+            if (sn)
+                nchk(ncclSend((const SendRec *)c.send + P.soff[(size_t)i * (W + 1) + r], (uint64_t)sn * sizeof(SendRec),
+                              ncclUint8, r, comm, c.cs),
+                     "send keys");
+            if (rn)
+                nchk(ncclRecv((SendRec *)c.recv + P.roff[(size_t)i * (W + 1) + r], (uint64_t)rn * sizeof(SendRec),
+                              ncclUint8, r, comm, c.cs),
+                     "recv keys");
+        }
+        nchk(ncclGroupEnd(), "group end");
+        chk(hipEventRecord(ev_keys[i], c.cs), "event");
     }
-    nchk(ncclGroupEnd(), "group end");
-    phase_probe(c, t, tune, m, d_recs != nullptr, s);
-    // results back
     const uint64_t ob = sizeof(stage_probe_out_dev);
-    nchk(ncclGroupStart(), "group");
-    for (int r = 0; r < W; ++r) {
-        if (rc[r]) {
-            nchk(ncclSend((const uint8_t *)c.rout + roff[r] * ob, (uint64_t)rc[r] * ob, ncclUint8, r, comm, s), "send out");
-            if (d_recs)
-                nchk(ncclSend((const uint8_t *)c.rrec + roff[r] * stride, (uint64_t)rc[r] * stride, ncclUint8, r, comm, s),
-                     "send rows");
+    for (int i = 0; i < C; ++i) {
+        chk(hipStreamWaitEvent(s, ev_keys[i], 0), "wait keys");
+        chunk_probe(c, P, i, t, tune, d_recs != nullptr, s);
+        chk(hipEventRecord(ev_probe[i], s), "event");
+        chk(hipStreamWaitEvent(c.cs, ev_probe[i], 0), "wait probe");
+        nchk(ncclGroupStart(), "group");
+        for (int r = 0; r < W; ++r) {
+            const uint32_t sn = P.sc[(size_t)i * W + r], rn = P.rc[(size_t)i * W + r];
+            const uint64_t so = P.soff[(size_t)i * (W + 1) + r], ro = P.roff[(size_t)i * (W + 1) + r];
+            if (rn) {
+                nchk(ncclSend((const uint8_t *)c.rout + ro * ob, (uint64_t)rn * ob, ncclUint8, r, comm, c.cs), "send out");
+                if (d_recs)
+                    nchk(ncclSend((const uint8_t *)c.rrec + ro * stride, (uint64_t)rn * stride, ncclUint8, r, comm, c.cs),
+                         "send rows");
+            }
+            if (sn) {
+                nchk(ncclRecv((uint8_t *)c.bout + so * ob, (uint64_t)sn * ob, ncclUint8, r, comm, c.cs), "recv out");
+                if (d_recs)
+                    nchk(ncclRecv((uint8_t *)c.brec + so * stride, (uint64_t)sn * stride, ncclUint8, r, comm, c.cs),
+                         "recv rows");
+            }
         }
-        if (sc[r]) {
-            nchk(ncclRecv((uint8_t *)c.bout + soff[r] * ob, (uint64_t)sc[r] * ob, ncclUint8, r, comm, s), "recv out");
-            if (d_recs)
-                nchk(ncclRecv((uint8_t *)c.brec + soff[r] * stride, (uint64_t)sc[r] * stride, ncclUint8, r, comm, s),
-                     "recv rows");
-        }
+        nchk(ncclGroupEnd(), "group end");
+        chk(hipEventRecord(ev_res[i], c.cs), "event");
+        chk(hipStreamWaitEvent(c.us, ev_res[i], 0), "wait results");
+        chunk_unpermute(c, P, i, stride, d_out, d_recs, c.us);
     }
-    nchk(ncclGroupEnd(), "group end");
-    phase_unpermute(c, n, stride, d_out, d_recs, s);
+    // the caller's stream completes after the last un-permutation
+    chk(hipEventRecord(ev_start, c.us), "event");
+    chk(hipStreamWaitEvent(s, ev_start, 0), "join");
     return STAGE_OK;
 }
 
-int shard_init_loopback(ShardComm &c, int rank, int world) {
-    if (world < 1 || world > kMaxWorld || rank < 0 || rank >= world) throw std::invalid_argument("bad rank/world");
-    c.comm = nullptr;
-    c.rank = rank;
-    c.world = world;
-    grow(c.cnt, 4 * sizeof(uint32_t) * (uint64_t)world);
-    grow(c.cursor, (2ull * world * kRouteBlocks + 16) * sizeof(uint32_t));
-    return STAGE_OK;
-}
-
-// The same phases for W shards held by one process on one device, with device-to-device
-// copies where shard_probe has RCCL transfers (same offsets, same order).  Every shard's
-// stride must be equal.
+// The same plan for W shards held by one process on one device, with device-to-device copies
+// where shard_probe has RCCL transfers (same chunks, same offsets), all on one stream.
 int shard_probe_loopback(const std::vector<ShardComm *> &cs, const std::vector<const DevTable *> &ts,
                          const ProbeTuning &tune, const std::vector<const uint64_t *> &keys,
                          const std::vector<const uint32_t *> &rids, const std::vector<uint64_t> &n,
@@ -320,43 +393,41 @@ int shard_probe_loopback(const std::vector<ShardComm *> &cs, const std::vector<c
     const int W = (int)cs.size();
     const uint32_t stride = ts[0]->stride;
     for (int r = 0; r < W; ++r)
-        if (ts[r]->stride != stride || cs[r]->world != W || cs[r]->rank != r)
-            throw std::invalid_argument("loopback shards disagree on stride / rank / world");
+        if (ts[r]->stride != stride || cs[r]->world != W || cs[r]->rank != r || cs[r]->chunks != cs[0]->chunks)
+            throw std::invalid_argument("loopback shards disagree on stride / rank / world / chunks");
+    const int C = cs[0]->chunks;
     const bool rows = recs[0] != nullptr;
-    std::vector<std::vector<uint32_t>> sc(W), rc(W, std::vector<uint32_t>(W));
-    std::vector<std::vector<uint64_t>> soff(W), roff(W);
+    std::vector<Plan> P(W);
+    for (int r = 0; r < W; ++r) plan_route(*cs[r], P[r], keys[r], rids[r], n[r], stride, s);
     for (int r = 0; r < W; ++r) {
-        sc[r] = phase_route(*cs[r], keys[r], rids[r], n[r], stride, s);
-        soff[r] = prefix(sc[r]);
+        P[r].rc.resize((size_t)C * W);
+        for (int i = 0; i < C; ++i)
+            for (int q = 0; q < W; ++q) P[r].rc[(size_t)i * W + q] = P[q].sc[(size_t)i * W + r];
+        plan_receive(*cs[r], P[r], stride);
     }
-    for (int r = 0; r < W; ++r)
-        for (int q = 0; q < W; ++q) rc[r][q] = sc[q][r];  // what the count all-to-all delivers
-    for (int r = 0; r < W; ++r) {
-        roff[r] = prefix(rc[r]);
-        ensure_remote(*cs[r], roff[r][W], stride);
-    }
-    for (int r = 0; r < W; ++r)  // keys: q's send segment for r -> r's receive segment from q
-        for (int q = 0; q < W; ++q)
-            if (sc[q][r])
-                chk(hipMemcpyAsync((uint8_t *)cs[r]->recv + roff[r][q] * sizeof(SendRec),
-                                   (const uint8_t *)cs[q]->send + soff[q][r] * sizeof(SendRec),
-                                   (uint64_t)sc[q][r] * sizeof(SendRec), hipMemcpyDeviceToDevice, s),
-                    "loopback keys");
-    for (int r = 0; r < W; ++r) phase_probe(*cs[r], *ts[r], tune, roff[r][W], rows, s);
-    const uint64_t ob = sizeof(stage_probe_out_dev);
-    for (int q = 0; q < W; ++q)  // results: owner q's segment for origin r -> r's slots of q
+    auto copy = [&](void *dst, const void *src, uint64_t bytes, const char *what) {
+        if (bytes) chk(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s), what);
+    };
+    for (int i = 0; i < C; ++i)  // keys: q's chunk-i segment for r -> r's chunk-i segment from q
         for (int r = 0; r < W; ++r)
-            if (rc[q][r]) {
-                chk(hipMemcpyAsync((uint8_t *)cs[r]->bout + soff[r][q] * ob, (const uint8_t *)cs[q]->rout + roff[q][r] * ob,
-                                   (uint64_t)rc[q][r] * ob, hipMemcpyDeviceToDevice, s),
-                    "loopback out");
+            for (int q = 0; q < W; ++q)
+                copy((SendRec *)cs[r]->recv + P[r].roff[(size_t)i * (W + 1) + q],
+                     (const SendRec *)cs[q]->send + P[q].soff[(size_t)i * (W + 1) + r],
+                     (uint64_t)P[q].sc[(size_t)i * W + r] * sizeof(SendRec), "loopback keys");
+    const uint64_t ob = sizeof(stage_probe_out_dev);
+    for (int i = 0; i < C; ++i) {
+        for (int r = 0; r < W; ++r) chunk_probe(*cs[r], P[r], i, *ts[r], tune, rows, s);
+        for (int q = 0; q < W; ++q)  // results: owner q's chunk-i segment for r -> r's chunk-i slots of q
+            for (int r = 0; r < W; ++r) {
+                const uint64_t cnt = P[q].rc[(size_t)i * W + r];
+                const uint64_t ro = P[q].roff[(size_t)i * (W + 1) + r], so = P[r].soff[(size_t)i * (W + 1) + q];
+                copy((uint8_t *)cs[r]->bout + so * ob, (const uint8_t *)cs[q]->rout + ro * ob, cnt * ob, "loopback out");
                 if (rows)
-                    chk(hipMemcpyAsync((uint8_t *)cs[r]->brec + soff[r][q] * stride,
-                                       (const uint8_t *)cs[q]->rrec + roff[q][r] * stride, (uint64_t)rc[q][r] * stride,
-                                       hipMemcpyDeviceToDevice, s),
-                        "loopback rows");
+                    copy((uint8_t *)cs[r]->brec + so * stride, (const uint8_t *)cs[q]->rrec + ro * stride,
+                         cnt * stride, "loopback rows");
             }
-    for (int r = 0; r < W; ++r) phase_unpermute(*cs[r], n[r], stride, outs[r], recs[r], s);
+        for (int r = 0; r < W; ++r) chunk_unpermute(*cs[r], P[r], i, stride, outs[r], recs[r], s);
+    }
     return STAGE_OK;
 }
 

@@ -20,17 +20,23 @@ struct ShardComm {
     void *lkeys = nullptr, *lrids = nullptr;
     uint64_t cap_local = 0, cap_remote = 0;
     uint32_t rec_stride = 0;
+    int chunks = 1;                  // overlapped exchange chunks (same on every rank)
+    hipStream_t cs = nullptr;        // RCCL transfers
+    hipStream_t us = nullptr;        // un-permutation
+    std::vector<hipEvent_t> evs;     // per-chunk keys / probe / results events + join
     ~ShardComm();
 };
 
 int shard_unique_id(uint8_t *id128);
-int shard_init(ShardComm &c, const uint8_t *id128, int rank, int world);
+// chunks: overlapped exchange chunks, identical on every rank (<= 0: STAGE_SHARD_CHUNKS or 4)
+int shard_init(ShardComm &c, const uint8_t *id128, int rank, int world, int chunks);
+int shard_default_chunks();
 int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const uint64_t *d_keys,
                 const uint32_t *d_rids, uint64_t n, stage_probe_out_dev *d_out, uint8_t *d_recs, hipStream_t s);
 
 // single-process rehearsal of shard_probe for W shards on one device (device copies in place
 // of the RCCL transfers): the routing, offsets and permutations are the same code
-int shard_init_loopback(ShardComm &c, int rank, int world);
+int shard_init_loopback(ShardComm &c, int rank, int world, int chunks);
 int shard_probe_loopback(const std::vector<ShardComm *> &cs, const std::vector<const DevTable *> &ts,
                          const ProbeTuning &tune, const std::vector<const uint64_t *> &keys,
                          const std::vector<const uint32_t *> &rids, const std::vector<uint64_t> &n,

@@ -30,6 +30,7 @@ struct stage_table {
     uint32_t out_stride = 0;  // 0 = stride of the canonical row; STAGE_OUT_STRIDE overrides (A/B)
     std::unique_ptr<stage::ShardComm> comm;
     std::unique_ptr<stage::ShardComm> loop_comm;  // stage_probe_sharded_loopback state
+    int shard_chunks = 0;                          // 0 = STAGE_SHARD_CHUNKS or the default
     std::mutex pipe_mu;  // serialises stage_probe_host calls on this table
     std::unique_ptr<stage::HostPipe, stage::HostPipeDeleter> pipe;
 };

@@ -52,8 +52,8 @@ def shard_tables(keys, world, mode=1):
     return tabs, h
 
 
-@pytest.mark.parametrize("world", [2, 3, 8])
-def test_sharded_data_path_loopback_equals_single_table(gpu, world):
+@pytest.mark.parametrize("world,chunks", [(2, 1), (3, 4), (8, 7)])
+def test_sharded_data_path_loopback_equals_single_table(gpu, world, chunks):
     # the multi-GPU data path (routing, count exchange, all-to-all-v offsets, local probes,
     # reverse exchange, un-permutation) with W shards on one device, against one table
     # holding every key; version chains on some keys so statuses and rows vary
@@ -71,6 +71,8 @@ def test_sharded_data_path_loopback_equals_single_table(gpu, world):
             assert t.commit_update(int(k), 11, 11) == stage.RC_OK
     for t in tabs + [full]:
         t.sync()
+    for t in tabs:
+        check(stage.lib().stage_set_shard_chunks(t.h, chunks), "chunks")
     sizes = [int(x) for x in rng.integers(1, 120_000, world)]
     sizes[-1] = 0  # a rank with nothing to probe still takes part in the exchange
     per_keys = [np.concatenate([rng.integers(0, n + 20_000, s), rng.choice(hot, min(s, 500))]).astype(np.uint64)
