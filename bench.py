@@ -314,12 +314,31 @@ def main():
             ops_done += n_ops
             o = d_out.to_numpy(stage.PROBE_OUT_DTYPE, n_ops)
             status_hist += np.bincount(o["status"], minlength=6)[:6]
+    owner = None
     if dist:
         dist.barrier()
         import torch
         tt = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
+        # the same steps with STAGE_REPLY_OWNER: rows stay in the owner's HBM, only the 32-B
+        # status records return -- the HBM-side scaling without the xGMI tuple return
+        for _ in range(max(1, args.warmup)):
+            check(L.stage_probe_sharded_ex(tab.h, d_keys.ptr, None, B, d_out.ptr, None, stage.REPLY_OWNER, stream.ptr),
+                  "sharded owner")
+        stream.sync()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            check(L.stage_probe_sharded_ex(tab.h, d_keys.ptr, None, B, d_out.ptr, None, stage.REPLY_OWNER, stream.ptr),
+                  "sharded owner")
+        stream.sync()
+        t_own = time.perf_counter() - t0
+        tt = torch.tensor([t_own], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_own = float(tt.item())
+        owner = {"value": round(B * args.steps * world / t_own, 1), "ms_per_step": round(t_own / args.steps * 1e3, 4),
+                 "reply": "32-B status records to the caller, tuple rows materialised on the owner"}
     step_ms = [evs[2 * i].elapsed_ms(evs[2 * i + 1]) for i in range(args.steps)]
     kern_ms = float(np.mean(step_ms))
 
@@ -387,6 +406,7 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic (LoadYCSBRows keys/payloads)",
             "config": config, "roofline": roof, "cpu_baseline": cpu, "self_check": ok,
+            **({"owner_reply": owner} if owner else {}),
             "setup_s": {"load": round(t_load, 1), "sync": round(t_sync, 1)},
         }
         print(json.dumps(result), flush=True)

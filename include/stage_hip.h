@@ -233,6 +233,18 @@ int stage_comm_init(stage_table *t, const uint8_t *id128, int rank, int world);
 int stage_comm_destroy(stage_table *t);
 int stage_probe_sharded(stage_table *t, const uint64_t *d_keys, const uint32_t *d_read_ids,
                         uint64_t n, stage_probe_out *d_out, uint8_t *d_records, void *stream);
+/* reply modes: STAGE_REPLY_ROWS = status records and tuple rows come back to the caller (what
+ * stage_probe_sharded does); STAGE_REPLY_OWNER = the owner materialises the tuple rows in its
+ * own HBM result buffer and only the 32-B status records come back, each carrying the row's
+ * owner-local index in `reserved` (owner rank = MurmurHash64A(key, 8, 0) % world); the owner
+ * reads its buffer with stage_sharded_owner_rows (valid until its next sharded probe). */
+#define STAGE_REPLY_ROWS 0
+#define STAGE_REPLY_OWNER 1
+int stage_probe_sharded_ex(stage_table *t, const uint64_t *d_keys, const uint32_t *d_read_ids,
+                           uint64_t n, stage_probe_out *d_out, uint8_t *d_records, int reply_mode,
+                           void *stream);
+/* loopback != 0: the buffer of stage_probe_sharded_loopback's shard state */
+int stage_sharded_owner_rows(stage_table *t, int loopback, uint8_t **d_rows, uint64_t *n_rows);
 
 /* single-process rehearsal of stage_probe_sharded: `world` shard tables on ONE device play the
  * ranks; the routing, count exchange, offsets, local probes and un-permutation are the same
@@ -242,7 +254,7 @@ int stage_probe_sharded(stage_table *t, const uint64_t *d_keys, const uint32_t *
 int stage_probe_sharded_loopback(stage_table *const *shards, int world, const uint64_t *const *d_keys,
                                  const uint32_t *const *d_read_ids, const uint64_t *n,
                                  stage_probe_out *const *d_out, uint8_t *const *d_records,
-                                 void *stream);
+                                 int reply_mode, void *stream);
 
 /* ---- plumbing for callers without their own HIP binding (ctypes) ----------------------- */
 int stage_set_device(int device);

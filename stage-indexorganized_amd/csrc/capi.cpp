@@ -345,14 +345,39 @@ int stage_probe_sharded(stage_table *t, const uint64_t *d_keys, const uint32_t *
     return guarded([&] {
         (void)hipSetDevice(t->dev.device);
         return stage::shard_probe(*t->comm, t->dev.view, t->tune, d_keys, d_read_ids, n,
-                                  reinterpret_cast<stage::stage_probe_out_dev *>(d_out), d_records, pick(t, stream));
+                                  reinterpret_cast<stage::stage_probe_out_dev *>(d_out), d_records, STAGE_REPLY_ROWS,
+                                  pick(t, stream));
     });
+}
+
+int stage_probe_sharded_ex(stage_table *t, const uint64_t *d_keys, const uint32_t *d_read_ids, uint64_t n,
+                           stage_probe_out *d_out, uint8_t *d_records, int reply_mode, void *stream) {
+    int rc = need_synced(t);
+    if (rc) return rc;
+    if (!t->comm) return fail(STAGE_E_STATE, "stage_comm_init first");
+    if (reply_mode != STAGE_REPLY_ROWS && reply_mode != STAGE_REPLY_OWNER) return fail(STAGE_E_ARG, "bad reply mode");
+    return guarded([&] {
+        (void)hipSetDevice(t->dev.device);
+        return stage::shard_probe(*t->comm, t->dev.view, t->tune, d_keys, d_read_ids, n,
+                                  reinterpret_cast<stage::stage_probe_out_dev *>(d_out), d_records, reply_mode,
+                                  pick(t, stream));
+    });
+}
+
+int stage_sharded_owner_rows(stage_table *t, int loopback, uint8_t **d_rows, uint64_t *n_rows) {
+    if (!t || !d_rows || !n_rows) return fail(STAGE_E_ARG, "null argument");
+    stage::ShardComm *c = loopback ? t->loop_comm.get() : t->comm.get();
+    if (!c) return fail(STAGE_E_STATE, "no sharded probe has run");
+    *d_rows = (uint8_t *)c->rrec;
+    *n_rows = c->owner_rows;
+    return STAGE_OK;
 }
 
 int stage_probe_sharded_loopback(stage_table *const *shards, int world, const uint64_t *const *d_keys,
                                  const uint32_t *const *d_read_ids, const uint64_t *n, stage_probe_out *const *d_out,
-                                 uint8_t *const *d_records, void *stream) {
+                                 uint8_t *const *d_records, int reply_mode, void *stream) {
     if (!shards || world < 1 || !d_keys || !n || !d_out || !d_records) return fail(STAGE_E_ARG, "null argument");
+    if (reply_mode != STAGE_REPLY_ROWS && reply_mode != STAGE_REPLY_OWNER) return fail(STAGE_E_ARG, "bad reply mode");
     for (int r = 0; r < world; ++r) {
         int rc = need_synced(shards[r]);
         if (rc) return rc;
@@ -384,7 +409,8 @@ int stage_probe_sharded_loopback(stage_table *const *shards, int world, const ui
             os[r] = reinterpret_cast<stage::stage_probe_out_dev *>(d_out[r]);
             recs[r] = d_records[r];
         }
-        return stage::shard_probe_loopback(cs, ts, shards[0]->tune, ks, rs, ns, os, recs, pick(shards[0], stream));
+        return stage::shard_probe_loopback(cs, ts, shards[0]->tune, ks, rs, ns, os, recs, reply_mode,
+                                           pick(shards[0], stream));
     });
 }
 

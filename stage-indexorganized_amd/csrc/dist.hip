@@ -143,6 +143,13 @@ __global__ void unpermute(const stage_probe_out_dev *__restrict__ bout, const ui
     }
 }
 
+// reply mode "owner": the row stays in the owner's result buffer; the status record carries
+// its owner-local index in the reserved word
+__global__ void tag_rows(stage_probe_out_dev *__restrict__ out, uint64_t m, uint32_t base) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) out[i].w[7] = base + (uint32_t)i;
+}
+
 void grow(void *&p, uint64_t bytes) {
     if (p) chk(hipFree(p), "hipFree");
     p = nullptr;
@@ -285,7 +292,7 @@ static void plan_receive(ShardComm &c, Plan &P, uint32_t stride) {
 
 // probe what arrived in chunk i
 static void chunk_probe(ShardComm &c, const Plan &P, int i, const DevTable &t, const ProbeTuning &tune, bool rows,
-                        hipStream_t s) {
+                        bool tag, hipStream_t s) {
     const uint64_t b = P.rb[i], m = P.rb[i + 1] - b;
     if (!m) return;
     uint64_t *lk = (uint64_t *)c.lkeys + b;
@@ -294,6 +301,7 @@ static void chunk_probe(ShardComm &c, const Plan &P, int i, const DevTable &t, c
     chk(launch_probe(t, lk, nullptr, lr, nullptr, m, (stage_probe_out_dev *)c.rout + b,
                      rows ? (uint8_t *)c.rrec + b * (uint64_t)t.stride : nullptr, s, tune),
         "probe");
+    if (tag) tag_rows<<<(unsigned)((m + 255) / 256), 256, 0, s>>>((stage_probe_out_dev *)c.rout + b, m, (uint32_t)b);
 }
 
 static void chunk_unpermute(ShardComm &c, const Plan &P, int i, uint32_t stride, stage_probe_out_dev *d_out,
@@ -311,8 +319,12 @@ static void chunk_unpermute(ShardComm &c, const Plan &P, int i, uint32_t stride,
 // chunk the probe (s) and, as soon as it is done, its result exchange (cs) -- so the return
 // of chunk i over xGMI overlaps the probe of chunk i+1 in HBM -- and its un-permutation (us).
 int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const uint64_t *d_keys,
-                const uint32_t *d_rids, uint64_t n, stage_probe_out_dev *d_out, uint8_t *d_recs, hipStream_t s) {
+                const uint32_t *d_rids, uint64_t n, stage_probe_out_dev *d_out, uint8_t *d_recs, int reply,
+                hipStream_t s) {
     if (!c.comm) throw std::invalid_argument("not an RCCL communicator");
+    const bool owner = reply == STAGE_REPLY_OWNER;
+    if (owner) d_recs = nullptr;  // rows stay on the owner
+    c.owner_rows = 0;
     const int W = c.world, C = c.chunks;
     const uint32_t stride = t.stride;
     ncclComm_t comm = (ncclComm_t)c.comm;
@@ -352,7 +364,7 @@ int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const 
     const uint64_t ob = sizeof(stage_probe_out_dev);
     for (int i = 0; i < C; ++i) {
         chk(hipStreamWaitEvent(s, ev_keys[i], 0), "wait keys");
-        chunk_probe(c, P, i, t, tune, d_recs != nullptr, s);
+        chunk_probe(c, P, i, t, tune, owner || d_recs != nullptr, owner, s);
         chk(hipEventRecord(ev_probe[i], s), "event");
         chk(hipStreamWaitEvent(c.cs, ev_probe[i], 0), "wait probe");
         nchk(ncclGroupStart(), "group");
@@ -380,6 +392,7 @@ int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const 
     // the caller's stream completes after the last un-permutation
     chk(hipEventRecord(ev_start, c.us), "event");
     chk(hipStreamWaitEvent(s, ev_start, 0), "join");
+    if (owner) c.owner_rows = P.m();
     return STAGE_OK;
 }
 
@@ -388,10 +401,13 @@ int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const 
 int shard_probe_loopback(const std::vector<ShardComm *> &cs, const std::vector<const DevTable *> &ts,
                          const ProbeTuning &tune, const std::vector<const uint64_t *> &keys,
                          const std::vector<const uint32_t *> &rids, const std::vector<uint64_t> &n,
-                         const std::vector<stage_probe_out_dev *> &outs, const std::vector<uint8_t *> &recs,
+                         const std::vector<stage_probe_out_dev *> &outs, std::vector<uint8_t *> recs, int reply,
                          hipStream_t s) {
     const int W = (int)cs.size();
     const uint32_t stride = ts[0]->stride;
+    const bool owner = reply == STAGE_REPLY_OWNER;
+    if (owner)
+        for (auto &r : recs) r = nullptr;
     for (int r = 0; r < W; ++r)
         if (ts[r]->stride != stride || cs[r]->world != W || cs[r]->rank != r || cs[r]->chunks != cs[0]->chunks)
             throw std::invalid_argument("loopback shards disagree on stride / rank / world / chunks");
@@ -416,7 +432,7 @@ int shard_probe_loopback(const std::vector<ShardComm *> &cs, const std::vector<c
                      (uint64_t)P[q].sc[(size_t)i * W + r] * sizeof(SendRec), "loopback keys");
     const uint64_t ob = sizeof(stage_probe_out_dev);
     for (int i = 0; i < C; ++i) {
-        for (int r = 0; r < W; ++r) chunk_probe(*cs[r], P[r], i, *ts[r], tune, rows, s);
+        for (int r = 0; r < W; ++r) chunk_probe(*cs[r], P[r], i, *ts[r], tune, rows || owner, owner, s);
         for (int q = 0; q < W; ++q)  // results: owner q's chunk-i segment for r -> r's chunk-i slots of q
             for (int r = 0; r < W; ++r) {
                 const uint64_t cnt = P[q].rc[(size_t)i * W + r];
@@ -428,6 +444,7 @@ int shard_probe_loopback(const std::vector<ShardComm *> &cs, const std::vector<c
             }
         for (int r = 0; r < W; ++r) chunk_unpermute(*cs[r], P[r], i, stride, outs[r], recs[r], s);
     }
+    for (int r = 0; r < W; ++r) cs[r]->owner_rows = owner ? P[r].m() : 0;
     return STAGE_OK;
 }
 

@@ -24,6 +24,7 @@ struct ShardComm {
     hipStream_t cs = nullptr;        // RCCL transfers
     hipStream_t us = nullptr;        // un-permutation
     std::vector<hipEvent_t> evs;     // per-chunk keys / probe / results events + join
+    uint64_t owner_rows = 0;         // rows left in rrec by the last owner-reply probe
     ~ShardComm();
 };
 
@@ -32,7 +33,8 @@ int shard_unique_id(uint8_t *id128);
 int shard_init(ShardComm &c, const uint8_t *id128, int rank, int world, int chunks);
 int shard_default_chunks();
 int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const uint64_t *d_keys,
-                const uint32_t *d_rids, uint64_t n, stage_probe_out_dev *d_out, uint8_t *d_recs, hipStream_t s);
+                const uint32_t *d_rids, uint64_t n, stage_probe_out_dev *d_out, uint8_t *d_recs, int reply,
+                hipStream_t s);
 
 // single-process rehearsal of shard_probe for W shards on one device (device copies in place
 // of the RCCL transfers): the routing, offsets and permutations are the same code
@@ -40,7 +42,7 @@ int shard_init_loopback(ShardComm &c, int rank, int world, int chunks);
 int shard_probe_loopback(const std::vector<ShardComm *> &cs, const std::vector<const DevTable *> &ts,
                          const ProbeTuning &tune, const std::vector<const uint64_t *> &keys,
                          const std::vector<const uint32_t *> &rids, const std::vector<uint64_t> &n,
-                         const std::vector<stage_probe_out_dev *> &outs, const std::vector<uint8_t *> &recs,
+                         const std::vector<stage_probe_out_dev *> &outs, std::vector<uint8_t *> recs, int reply,
                          hipStream_t s);
 
 void set_error(const std::string &msg);

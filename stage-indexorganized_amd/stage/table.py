@@ -367,7 +367,18 @@ class Reader:
             pass
 
 
-def probe_sharded_loopback(tables, keys_per_rank, read_ids_per_rank=None, records=True):
+REPLY_ROWS, REPLY_OWNER = 0, 1
+
+
+def owner_rows(table, loopback=True):
+    """(device pointer, row count) of the rows an owner-reply sharded probe left on `table`."""
+    p = ctypes.c_void_p()
+    n = ctypes.c_uint64()
+    check(lib().stage_sharded_owner_rows(table.h, int(loopback), ctypes.byref(p), ctypes.byref(n)), "owner_rows")
+    return p.value, n.value
+
+
+def probe_sharded_loopback(tables, keys_per_rank, read_ids_per_rank=None, records=True, reply=REPLY_ROWS):
     """stage_probe_sharded_loopback: rank r's keys are routed across the shard tables (all on
     one device) exactly as stage_probe_sharded routes them over RCCL; returns per-rank
     (out, rows) in each rank's own key order."""
@@ -395,7 +406,7 @@ def probe_sharded_loopback(tables, keys_per_rank, read_ids_per_rank=None, record
     hs = (ctypes.c_void_p * W)(*[t.h for t in tables])
     n_arr = (ctypes.c_uint64 * W)(*ns)
     check(lib().stage_probe_sharded_loopback(hs, W, arr(k_ptrs), arr(r_ptrs) if r_ptrs else None, n_arr, arr(o_ptrs),
-                                             arr(rec_ptrs), None), "probe_sharded_loopback")
+                                             arr(rec_ptrs), reply, None), "probe_sharded_loopback")
     check(lib().stage_device_sync(), "sync")
     res = []
     trip = [x for x in keep if len(x) == 3]

@@ -94,3 +94,35 @@ def test_sharded_data_path_loopback_equals_single_table(gpu, world, chunks):
         if per_keys[r].size:
             ref_out, _ = full.probe(per_keys[r], records=False)
             assert (res2[r][0]["status"] == ref_out["status"]).all()
+
+
+def test_owner_reply_mode_loopback(gpu):
+    # STAGE_REPLY_OWNER: only status records travel back; each row stays in its owner's result
+    # buffer at the index the record carries
+    world, n = 4, 200_000
+    keys = np.arange(n, dtype=np.uint64)
+    tabs, h = shard_tables(keys, world)
+    full = stage.Table(key_width=8)
+    full.load_keys(keys, 8, mode=1)
+    for t in tabs + [full]:
+        t.sync()
+    rng = np.random.default_rng(77)
+    per_keys = [rng.integers(0, n + 5000, 30_000 + 1000 * r).astype(np.uint64) for r in range(world)]
+    res = stage.probe_sharded_loopback(tabs, per_keys, None, records=True, reply=stage.REPLY_OWNER)
+    owner_bufs = []
+    for t in tabs:
+        ptr, cnt = stage.owner_rows(t, loopback=True)
+        buf = np.zeros(cnt * t.stride, np.uint8)
+        check(stage.lib().stage_memcpy_d2h(buf.ctypes.data, ptr, buf.nbytes, None), "d2h")
+        owner_bufs.append(buf.reshape(cnt, t.stride))
+    assert sum(b.shape[0] for b in owner_bufs) == sum(k.size for k in per_keys)
+    for r in range(world):
+        out, rows = res[r]
+        ref_out, ref_rows = full.probe(per_keys[r])
+        assert (out["status"] == ref_out["status"]).all() and (out["cstamp"] == ref_out["cstamp"]).all()
+        own = (O.murmur64a_keys(per_keys[r], 8, 0) % np.uint64(world)).astype(np.int64)
+        for o in range(world):
+            sel = np.nonzero(own == o)[0]
+            got = owner_bufs[o][out["reserved"][sel]]
+            hit = out["status"][sel] != stage.ST_NOT_FOUND
+            assert (got[hit] == ref_rows[sel][hit]).all()
