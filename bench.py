@@ -71,6 +71,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--host-traversal", action="store_true", help="leaf ids from the host router instead")
+    p.add_argument("--force-sharded", action="store_true",
+                   help="run the multi-GPU (RCCL) code path even with one rank -- a rehearsal, not a config")
     a = p.parse_args()
     a.steps = a.steps if a.steps is not None else (5 if a.config == "c3" else 20)
     a.warmup = a.warmup if a.warmup is not None else (1 if a.config == "c3" else 3)
@@ -201,7 +203,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
     dist = None
-    if world > 1:
+    sharded = world > 1 or args.force_sharded
+    if sharded:
         import torch.distributed as tdist
         tdist.init_process_group("gloo")  # control plane only; the data path is RCCL in the library
         dist = tdist
@@ -213,7 +216,7 @@ def main():
     total_rows = args.rows * world
     t0 = time.time()
     tab = stage.Table(key_width=8, device=local)
-    if world == 1:
+    if not sharded:
         loaded = tab.load_ycsb(0, total_rows, 8, mode=0)
     else:
         keys = owned_keys(total_rows, world, rank)
@@ -257,7 +260,7 @@ def main():
     if args.host_traversal and world == 1 and args.config == "c2":
         d_leaf = stage.DeviceBuffer.from_numpy(tab.traverse(draws))
 
-    if world > 1:
+    if sharded:
         uid = (ctypes.c_uint8 * 128)()
         if rank == 0:
             check(L.stage_comm_unique_id(uid), "unique id")
@@ -270,7 +273,7 @@ def main():
         if args.config == "c4":
             check(L.stage_scan_batch(tab.h, d_keys.ptr, None, B, args.scan_size, d_cnt.ptr, d_rec.ptr, stream.ptr),
                   "scan")
-        elif world == 1:
+        elif not sharded:
             tab.probe_device(d_keys.ptr, n_ops, d_out.ptr, d_rec.ptr, d_read_ids=d_rid.ptr if d_rid else None,
                              d_leaf_ids=d_leaf.ptr if d_leaf else None, stream=stream.ptr)
         else:
@@ -369,10 +372,10 @@ def main():
         else:
             per_unit = BYTES_PER_LOOKUP
             unit = "ops/s"
-            kernel = "probe_kernel" if world == 1 else "sharded step (route + RCCL + probe_kernel)"
+            kernel = "probe_kernel" if not sharded else "sharded step (route + RCCL + probe_kernel)"
         units_per_launch = ops_done / args.steps
         achieved = per_unit * units_per_launch / (kern_ms * 1e-3) / 1e9
-        traffic, tsrc = (traffic_from_profile(B, args.rows) if args.config == "c2" and world == 1 else (None, None))
+        traffic, tsrc = (traffic_from_profile(B, args.rows) if args.config == "c2" and not sharded else (None, None))
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kernel,
                 "algorithmic_bytes_per_unit": per_unit, "units_per_launch": units_per_launch,
@@ -380,9 +383,9 @@ def main():
         if tsrc:
             roof["traffic_source"] = tsrc
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
+        if not sharded and not args.no_cpu_baseline:
             cpu = cpu_baseline(args, nthreads)
-        wl = WORKLOADS[args.config] if world == 1 else WORKLOADS["c5"]
+        wl = WORKLOADS[args.config] if not sharded else WORKLOADS["c5"]
         config = {"workload": wl, "rows_per_gpu": args.rows, "rows_total": total_rows, "batch_per_gpu": B,
                   "key_bytes": 8, "payload_bytes": 1000, "leaf_bytes": 65536,
                   "parallelism": f"hash-shard x{world}", "traversal": "host" if d_leaf else "device"}
