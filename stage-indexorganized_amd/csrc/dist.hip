@@ -125,20 +125,26 @@ __global__ void unpack_keys(const SendRec *__restrict__ recv, uint64_t n, uint64
     rids[i] = recv[i].rid;
 }
 
-// back in the caller's order: out[perm[p]] = bout[p] for p in [p0, p1), one wave per probe
+// back in the caller's order: out[perm[p]] = bout[p] for p in [p0, p1), one wave per probe.
+// Positions [q0, q1) are this rank's own keys: they never left the device, so they are read
+// straight from the local probe's output (qout / qrec) instead of a received copy.
 __global__ void unpermute(const stage_probe_out_dev *__restrict__ bout, const uint8_t *__restrict__ brec,
                           const uint32_t *__restrict__ perm, uint64_t p0, uint64_t p1, uint32_t stride,
-                          stage_probe_out_dev *__restrict__ out, uint8_t *__restrict__ recs) {
+                          stage_probe_out_dev *__restrict__ out, uint8_t *__restrict__ recs, uint64_t q0, uint64_t q1,
+                          const stage_probe_out_dev *__restrict__ qout, const uint8_t *__restrict__ qrec) {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
     for (uint64_t p = p0 + w; p < p1; p += nw) {
         const uint32_t dst = perm[p];
-        if (lane < 2) reinterpret_cast<uint4 *>(out + dst)[lane] = reinterpret_cast<const uint4 *>(bout + p)[lane];
+        const bool own = p >= q0 && p < q1;
+        const stage_probe_out_dev *so = own ? qout + (p - q0) : bout + p;
+        if (lane < 2) reinterpret_cast<uint4 *>(out + dst)[lane] = reinterpret_cast<const uint4 *>(so)[lane];
         if (recs) {
-            const uint4 *s = reinterpret_cast<const uint4 *>(brec + p * (uint64_t)stride);
+            const uint4 *sr = reinterpret_cast<const uint4 *>(own ? qrec + (p - q0) * (uint64_t)stride
+                                                                   : brec + p * (uint64_t)stride);
             uint4 *d = reinterpret_cast<uint4 *>(recs + (uint64_t)dst * stride);
-            for (uint32_t c = lane; c < (stride >> 4); c += 64) d[c] = s[c];
+            for (uint32_t c = lane; c < (stride >> 4); c += 64) d[c] = sr[c];
         }
     }
 }
@@ -307,10 +313,13 @@ static void chunk_probe(ShardComm &c, const Plan &P, int i, const DevTable &t, c
 static void chunk_unpermute(ShardComm &c, const Plan &P, int i, uint32_t stride, stage_probe_out_dev *d_out,
                             uint8_t *d_recs, hipStream_t s) {
     const uint64_t p0 = P.cb[i], p1 = P.cb[i + 1];
+    const int W = P.W, me = c.rank;
+    const uint64_t q0 = P.soff[(size_t)i * (W + 1) + me], q1 = P.soff[(size_t)i * (W + 1) + me + 1];
+    const uint64_t ro = P.roff[(size_t)i * (W + 1) + me];  // where the local probe wrote them
     if (p1 > p0)
         unpermute<<<(unsigned)std::min<uint64_t>((p1 - p0 + 3) / 4, 8192), 256, 0, s>>>(
             (const stage_probe_out_dev *)c.bout, (const uint8_t *)c.brec, (const uint32_t *)c.perm, p0, p1, stride,
-            d_out, d_recs);
+            d_out, d_recs, q0, q1, (const stage_probe_out_dev *)c.rout + ro, (const uint8_t *)c.rrec + ro * stride);
     chk(hipGetLastError(), "unpermute");
 }
 
@@ -369,6 +378,7 @@ int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const 
         chk(hipStreamWaitEvent(c.cs, ev_probe[i], 0), "wait probe");
         nchk(ncclGroupStart(), "group");
         for (int r = 0; r < W; ++r) {
+            if (r == c.rank) continue;  // own results are read in place by the un-permutation
             const uint32_t sn = P.sc[(size_t)i * W + r], rn = P.rc[(size_t)i * W + r];
             const uint64_t so = P.soff[(size_t)i * (W + 1) + r], ro = P.roff[(size_t)i * (W + 1) + r];
             if (rn) {
@@ -435,6 +445,7 @@ int shard_probe_loopback(const std::vector<ShardComm *> &cs, const std::vector<c
         for (int r = 0; r < W; ++r) chunk_probe(*cs[r], P[r], i, *ts[r], tune, rows || owner, owner, s);
         for (int q = 0; q < W; ++q)  // results: owner q's chunk-i segment for r -> r's chunk-i slots of q
             for (int r = 0; r < W; ++r) {
+                if (r == q) continue;  // as shard_probe: own results are read in place
                 const uint64_t cnt = P[q].rc[(size_t)i * W + r];
                 const uint64_t ro = P[q].roff[(size_t)i * (W + 1) + r], so = P[r].soff[(size_t)i * (W + 1) + q];
                 copy((uint8_t *)cs[r]->bout + so * ob, (const uint8_t *)cs[q]->rout + ro * ob, cnt * ob, "loopback out");
