@@ -57,7 +57,7 @@ typedef struct stage_params {
     uint32_t merge_threshold; /* (YCSB: 32 KiB)                                          */
     uint32_t leaf_node_size;  /* leaf block == leaf split threshold (YCSB: 64 KiB)       */
     uint32_t payload_size;    /* bytes after the 8-byte padded key (YCSB: 1000)          */
-    uint32_t key_width;       /* 1..8 = every key has this many bytes; 0 = variable 1..8 */
+    uint32_t key_width;       /* 1..32 = every key has this many bytes; 0 = variable 1..8 */
     int32_t device;           /* HIP device ordinal for the device image                  */
 } stage_params;
 
@@ -112,14 +112,36 @@ int stage_finalize_update(stage_table *t, uint64_t key, uint16_t key_size, uint3
 int stage_delete(stage_table *t, uint64_t key, uint16_t key_size, uint32_t commit_id,
                  uint8_t *rc_out);
 /* batched write path of one transaction epoch (the YCSB-B writers, ycsb.cpp:200-260): for
- * key i, stage_update(keys[i], payload_off, deltas + i*delta_len, writer_ids[i]) and, when it
- * succeeded and commit_ids[i] != 0, stage_commit_update(keys[i], commit_ids[i], sstamps[i]
+ * key i (key_size bytes at keys + i*key_stride; u64 keys of <= 8 bytes: key_stride 8),
+ * stage_update(key i, payload_off, deltas + i*delta_len, writer_ids[i]) and, when it
+ * succeeded and commit_ids[i] != 0, stage_commit_update(key i, commit_ids[i], sstamps[i]
  * (or commit_ids[i] when sstamps is NULL)).  rc_out[i] (optional) = the last ReturnCode;
  * *n_ok (optional) = keys whose update (and commit) returned STAGE_RC_OK. */
-int stage_update_batch(stage_table *t, const uint64_t *keys, uint64_t n, uint16_t key_size,
-                       uint32_t payload_off, const uint8_t *deltas, uint32_t delta_len,
-                       const uint32_t *writer_ids, const uint32_t *commit_ids,
+int stage_update_batch(stage_table *t, const void *keys, uint32_t key_stride, uint64_t n,
+                       uint16_t key_size, uint32_t payload_off, const uint8_t *deltas,
+                       uint32_t delta_len, const uint32_t *writer_ids, const uint32_t *commit_ids,
                        const uint32_t *sstamps, uint8_t *rc_out, uint64_t *n_ok);
+
+/* byte-key forms, for every key width a table takes: 1..8 bytes (key_width 1..8 or 0 =
+ * variable) or a fixed width of 9..32 bytes (TPC-C composite keys, tpcc_record.h: int64
+ * fields, e.g. OrderLineKey = 32 bytes).  Same ReturnCodes as the u64 forms above.
+ * stage_load_rows inserts n rows in order (key i at keys + i*key_stride, payload i at
+ * payloads + i*payload_stride), rc_out[i] optional.
+ * Device key buffers (stage_probe_batch, stage_scan_batch, stage_resolve_batch,
+ * stage_traverse_batch) hold stage_key_words(t) u64 words per key: the key bytes
+ * little-endian, zero padded (1 word for keys of <= 8 bytes, 2 for 9..16, 4 for 17..32). */
+int stage_insert_key(stage_table *t, const uint8_t *key, uint16_t key_size, const uint8_t *payload,
+                     uint32_t commit_id, uint8_t *rc_out);
+int stage_load_rows(stage_table *t, const uint8_t *keys, uint32_t key_stride, uint16_t key_size,
+                    const uint8_t *payloads, uint32_t payload_stride, uint64_t n, uint32_t commit_id,
+                    uint8_t *rc_out, uint64_t *inserted);
+int stage_update_key(stage_table *t, const uint8_t *key, uint16_t key_size, uint32_t payload_off,
+                     const uint8_t *delta, uint32_t delta_len, uint32_t writer_id, uint8_t *rc_out);
+int stage_commit_update_key(stage_table *t, const uint8_t *key, uint16_t key_size,
+                            uint32_t commit_id, uint32_t sstamp, uint8_t *rc_out);
+int stage_delete_key(stage_table *t, const uint8_t *key, uint16_t key_size, uint32_t commit_id,
+                     uint8_t *rc_out);
+uint32_t stage_key_words(stage_table *t);
 
 /* publish the host layout to HBM (leaf key columns, slot words, visibility masks, the
  * separator search tree, record heap, overwrite copies and retired versions). */
@@ -167,7 +189,8 @@ int stage_import_leaf_images(stage_table *t, const uint8_t *blocks, uint64_t n_l
  * stage_probe_batch  replaces LeafNode::Read/SearchRecordMeta (b_tree.cpp:1042-1051, 18-122),
  *   Record::New/Neww (b_tree.h:407-448), BTree::Read (b_tree.cpp:2066-2129) and the
  *   visibility walk of IndexScanExecutor (executor.h:374-454), batched.
- *   d_keys[i]: key bytes little-endian in a u64; d_lens NULL -> table key_width;
+ *   d_keys: stage_key_words(t) u64 words per key, key bytes little-endian (one word for
+ *   keys of <= 8 bytes); d_lens NULL -> table key_width;
  *   d_read_ids NULL -> 0xFFFFFFFE; d_leaf_ids NULL -> device traversal of the separator
  *   mirror, else host-traversed leaf indices (stage_traverse_batch).
  *   d_records: n rows of stage_record_stride() bytes = [key padded to 8][payload]; NULL to

@@ -138,6 +138,7 @@ static inline int is_leaf(void *p) { return ((uint8_t *)p)[OFF_ISLEAF] != 0; }
 
 struct orc_tree {
     uint32_t leaf_node_size, split_threshold, payload_size, merge_threshold;
+    uint32_t key_pad; /* key bytes of a canonical tuple row (8, or the padded wide key width) */
     void *root;
     orc_copy *copies;
     orc_th *ths;
@@ -548,11 +549,13 @@ orc_tree *orc_tree_new(uint32_t leaf_node_size, uint32_t split_threshold, uint32
     t->split_threshold = split_threshold;
     t->payload_size = payload_size;
     t->merge_threshold = 32 * 1024;
+    t->key_pad = 8;
     t->root = leaf_new(t);
     return t;
 }
 
 void orc_tree_set_merge_threshold(orc_tree *t, uint32_t merge_threshold) { t->merge_threshold = merge_threshold; }
+void orc_tree_set_key_pad(orc_tree *t, uint32_t key_pad) { t->key_pad = key_pad < 8 ? 8 : key_pad; }
 
 static void free_subtree(void *n) {
     if (is_leaf(n)) {
@@ -647,11 +650,13 @@ static orc_copy *copy_of(uint64_t next) {
     return c->live ? c : NULL; /* EphemeralPool::GetOversionHeader (ephemeral_pool.cpp:110-123) */
 }
 
+/* canonical tuple row: [key padded to key_pad][payload] (key_pad = 8 for keys of <= 8 bytes,
+ * the padded key width for wider fixed-width keys) */
 static void emit_canonical(orc_tree *t, uint8_t *rec, const uint8_t *key, uint16_t ks, const uint8_t *payload) {
     if (!rec) return;
-    memset(rec, 0, 8);
-    memcpy(rec, key, ks > 8 ? 8 : ks);
-    memcpy(rec + 8, payload, t->payload_size);
+    memset(rec, 0, t->key_pad);
+    memcpy(rec, key, ks > t->key_pad ? t->key_pad : ks);
+    memcpy(rec + t->key_pad, payload, t->payload_size);
 }
 
 /* BTree::Read (b_tree.cpp:2066-2129) followed by the point-lookup branch of
@@ -659,7 +664,7 @@ static void emit_canonical(orc_tree *t, uint8_t *rec, const uint8_t *key, uint16
 static int read_one(orc_tree *t, const uint8_t *key, uint16_t ks, uint32_t read_id, orc_read_out *o, uint8_t *rec) {
     memset(o, 0, sizeof(*o));
     o->copy_sstamp = MAX_CID;
-    uint32_t rs = 8 + t->payload_size;
+    uint32_t rs = t->key_pad + t->payload_size;
     if (rec) memset(rec, 0, rs);
     uint8_t *leaf = traverse_to_leaf(t, NULL, key, ks, 1);
     int64_t slot = search_record_meta(leaf, key, ks, 1);
@@ -742,14 +747,22 @@ typedef struct {
     uint32_t scan_size;
     uint32_t *counts;
     uint64_t sum;
+    const uint8_t *kbytes; /* byte keys (kstride apart) instead of u64 keys */
+    uint32_t kstride;
 } job_t;
+
+static const uint8_t *job_key(job_t *j, uint64_t i, uint64_t *tmp) {
+    if (j->kbytes) return j->kbytes + i * j->kstride;
+    *tmp = j->keys[i];
+    return (const uint8_t *)tmp;
+}
 
 static void *read_worker(void *arg) {
     job_t *j = arg;
-    uint32_t rs = 8 + j->t->payload_size;
+    uint32_t rs = j->t->key_pad + j->t->payload_size;
     for (uint64_t i = j->b; i < j->e; i++) {
-        uint64_t k = j->keys[i];
-        read_one(j->t, (const uint8_t *)&k, (uint16_t)j->ks, j->rids ? j->rids[i] : 0xFFFFFFFEu, &j->outs[i],
+        uint64_t k;
+        read_one(j->t, job_key(j, i, &k), (uint16_t)j->ks, j->rids ? j->rids[i] : 0xFFFFFFFEu, &j->outs[i],
                  j->recs ? j->recs + i * rs : NULL);
     }
     return NULL;
@@ -777,7 +790,14 @@ static void run_jobs(void *(*fn)(void *), job_t *proto, uint64_t n, int nthreads
 
 int orc_read_batch(orc_tree *t, const uint64_t *keys, uint32_t key_size, const uint32_t *read_ids, uint64_t n,
                    orc_read_out *outs, uint8_t *recs, int nthreads) {
-    job_t j = {t, keys, key_size, read_ids, 0, n, outs, recs, 0, NULL, 0};
+    job_t j = {t, keys, key_size, read_ids, 0, n, outs, recs, 0, NULL, 0, NULL, 0};
+    run_jobs(read_worker, &j, n, nthreads);
+    return 0;
+}
+
+int orc_read_batch_k(orc_tree *t, const uint8_t *keys, uint32_t key_stride, uint32_t key_size,
+                     const uint32_t *read_ids, uint64_t n, orc_read_out *outs, uint8_t *recs, int nthreads) {
+    job_t j = {t, NULL, key_size, read_ids, 0, n, outs, recs, 0, NULL, 0, keys, key_stride};
     run_jobs(read_worker, &j, n, nthreads);
     return 0;
 }
@@ -828,7 +848,7 @@ static void *timed_worker(void *arg) {
 
 uint64_t orc_read_batch_timed(orc_tree *t, const uint64_t *keys, uint32_t key_size, const uint32_t *read_ids,
                               uint64_t n, int nthreads, double *seconds) {
-    job_t j = {t, keys, key_size, read_ids, 0, n, NULL, NULL, 0, NULL, 0};
+    job_t j = {t, keys, key_size, read_ids, 0, n, NULL, NULL, 0, NULL, 0, NULL, 0};
     struct timespec a, b;
     clock_gettime(CLOCK_MONOTONIC, &a);
     run_jobs(timed_worker, &j, n, nthreads);
@@ -870,15 +890,15 @@ static uint32_t range_scan_by_size(uint8_t *n, const uint8_t *key, uint16_t ks, 
 
 static void emit_scan_rec(orc_tree *t, uint8_t *dst, scanrec_t *r) {
     uint64_t mm = l_meta(r->leaf, r->slot)->meta;
-    memset(dst, 0, 8);
-    memcpy(dst, r->leaf + m_offset(mm), m_padded(mm) > 8 ? 8 : m_padded(mm));
-    memcpy(dst + 8, r->leaf + m_offset(mm) + m_padded(mm), t->payload_size);
+    memset(dst, 0, t->key_pad);
+    memcpy(dst, r->leaf + m_offset(mm), m_padded(mm) > t->key_pad ? t->key_pad : m_padded(mm));
+    memcpy(dst + t->key_pad, r->leaf + m_offset(mm) + m_padded(mm), t->payload_size);
 }
 
 /* TableScanExecutor::Execute (executor.h:620-639) driving Iterator::GetNext (b_tree.h:899-941) */
 static uint32_t scan_one(orc_tree *t, const uint8_t *key, uint16_t ks, uint32_t scan_size, uint8_t *recs,
                          scanrec_t *buf, uint32_t bufcap) {
-    uint32_t rs = 8 + t->payload_size, produced = 0;
+    uint32_t rs = t->key_pad + t->payload_size, produced = 0;
     uint32_t remaining = scan_size;
     uint8_t lastkey[64];
     uint16_t lastks = 0;
@@ -921,10 +941,10 @@ static void *scan_worker(void *arg) {
     job_t *j = arg;
     uint32_t cap = 4096;
     scanrec_t *buf = xmalloc(sizeof(scanrec_t) * cap);
-    uint64_t rs = 8 + j->t->payload_size, sum = 0;
+    uint64_t rs = j->t->key_pad + j->t->payload_size, sum = 0;
     for (uint64_t i = j->b; i < j->e; i++) {
-        uint64_t k = j->keys[i];
-        uint32_t c = scan_one(j->t, (const uint8_t *)&k, (uint16_t)j->ks, j->scan_size,
+        uint64_t k;
+        uint32_t c = scan_one(j->t, job_key(j, i, &k), (uint16_t)j->ks, j->scan_size,
                               j->recs ? j->recs + i * rs * j->scan_size : NULL, buf, cap);
         if (j->counts) j->counts[i] = c;
         sum += c;
@@ -952,7 +972,7 @@ static void *scan_timed_worker(void *arg) {
 
 uint64_t orc_scan_batch_timed(orc_tree *t, const uint64_t *keys, uint32_t key_size, uint64_t n, uint32_t scan_size,
                               int nthreads, double *seconds) {
-    job_t j = {t, keys, key_size, NULL, 0, n, NULL, NULL, scan_size, NULL, 0};
+    job_t j = {t, keys, key_size, NULL, 0, n, NULL, NULL, scan_size, NULL, 0, NULL, 0};
     struct timespec a, b;
     clock_gettime(CLOCK_MONOTONIC, &a);
     run_jobs(scan_timed_worker, &j, n, nthreads);
@@ -963,7 +983,14 @@ uint64_t orc_scan_batch_timed(orc_tree *t, const uint64_t *keys, uint32_t key_si
 
 uint64_t orc_scan_batch(orc_tree *t, const uint64_t *keys, uint32_t key_size, uint64_t n, uint32_t scan_size,
                         uint32_t *counts, uint8_t *recs, int nthreads) {
-    job_t j = {t, keys, key_size, NULL, 0, n, NULL, recs, scan_size, counts, 0};
+    job_t j = {t, keys, key_size, NULL, 0, n, NULL, recs, scan_size, counts, 0, NULL, 0};
+    run_jobs(scan_worker, &j, n, nthreads);
+    return j.sum;
+}
+
+uint64_t orc_scan_batch_k(orc_tree *t, const uint8_t *keys, uint32_t key_stride, uint32_t key_size, uint64_t n,
+                          uint32_t scan_size, uint32_t *counts, uint8_t *recs, int nthreads) {
+    job_t j = {t, NULL, key_size, NULL, 0, n, NULL, recs, scan_size, counts, 0, keys, key_stride};
     run_jobs(scan_worker, &j, n, nthreads);
     return j.sum;
 }
@@ -1043,8 +1070,9 @@ typedef struct {
     uint64_t max, n;
     uint32_t block, payload;
     uint8_t *blocks;
-    uint64_t *sep_key;
+    uint64_t *sep_key; /* kwords u64 words of key bytes per leaf */
     uint16_t *sep_len;
+    uint32_t kwords;
 } image_export_t;
 
 static void image_rec(void *node, image_export_t *e, const uint8_t *ub, uint16_t ub_len, int ub_inf) {
@@ -1064,9 +1092,9 @@ static void image_rec(void *node, image_export_t *e, const uint8_t *ub, uint16_t
                 }
             }
             if (e->sep_key) {
-                uint64_t kw = 0;
-                if (!ub_inf) memcpy(&kw, ub, ub_len > 8 ? 8 : ub_len);
-                e->sep_key[e->n] = kw;
+                uint64_t *kw = e->sep_key + e->n * (uint64_t)e->kwords;
+                memset(kw, 0, 8 * e->kwords);
+                if (!ub_inf) memcpy(kw, ub, ub_len > 8 * e->kwords ? 8 * e->kwords : ub_len);
                 e->sep_len[e->n] = ub_inf ? 0xFFFF : ub_len;
             }
         }
@@ -1080,11 +1108,16 @@ static void image_rec(void *node, image_export_t *e, const uint8_t *ub, uint16_t
     }
 }
 
-int64_t orc_export_leaf_images(orc_tree *t, uint64_t max_leaves, uint8_t *blocks, uint64_t *sep_key,
-                               uint16_t *sep_len) {
-    image_export_t e = {max_leaves, 0, t->leaf_node_size, t->payload_size, blocks, sep_key, sep_len};
+int64_t orc_export_leaf_images_k(orc_tree *t, uint64_t max_leaves, uint8_t *blocks, uint64_t *sep_key,
+                                 uint32_t kwords, uint16_t *sep_len) {
+    image_export_t e = {max_leaves, 0, t->leaf_node_size, t->payload_size, blocks, sep_key, sep_len, kwords};
     image_rec(t->root, &e, NULL, 0, 1);
     return (int64_t)e.n;
+}
+
+int64_t orc_export_leaf_images(orc_tree *t, uint64_t max_leaves, uint8_t *blocks, uint64_t *sep_key,
+                               uint16_t *sep_len) {
+    return orc_export_leaf_images_k(t, max_leaves, blocks, sep_key, 1, sep_len);
 }
 
 void orc_stats(orc_tree *t, uint64_t *stats) {
@@ -1139,7 +1172,10 @@ int orc_update(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t payl
     if (!mp) return ORC_RET_NOT_FOUND;
     if (m_inserting(mp->meta)) return ORC_RET_DIRTY;
     uint8_t *rk = leaf + m_offset(mp->meta);
-    uint8_t *col = rk + 8 + payload_off; /* Catalog: 8-byte key column then payload columns */
+    /* Catalog::get_field_index of a payload column = the key columns' width (8 for the YCSB
+     * key column, 16/24/32 for TPC-C int64 key fields) + its offset inside the payload
+     * (ComparePayload / CopyPayload, b_tree.h:661-695) */
+    uint8_t *col = rk + m_padded(mp->meta) + payload_off;
     if (payload_off + delta_len > t->payload_size) return ORC_RET_INVALID;
     if (memcmp(col, delta, delta_len) == 0) return ORC_RET_NOT_NEEDED_UPDATE; /* ComparePayload */
     if (m_cstamp(mp->meta) > writer_id) return ORC_RET_NOT_NEEDED_UPDATE;

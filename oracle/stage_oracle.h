@@ -115,6 +115,16 @@ void orc_stats(orc_tree *t, uint64_t *stats);
  * dead record bytes zeroed) + each leaf's upper separator (len 0xFFFF = +inf) */
 int64_t orc_export_leaf_images(orc_tree *t, uint64_t max_leaves, uint8_t *blocks, uint64_t *sep_key,
                                uint16_t *sep_len);
+/* the same with kwords u64 words of separator key bytes per leaf (keys above 8 bytes) */
+int64_t orc_export_leaf_images_k(orc_tree *t, uint64_t max_leaves, uint8_t *blocks, uint64_t *sep_key,
+                                 uint32_t kwords, uint16_t *sep_len);
+/* canonical tuple rows [key padded to key_pad][payload]; default 8 (keys of <= 8 bytes) */
+void orc_tree_set_key_pad(orc_tree *t, uint32_t key_pad);
+/* batch forms over byte keys (key i at keys + i*key_stride) */
+int orc_read_batch_k(orc_tree *t, const uint8_t *keys, uint32_t key_stride, uint32_t key_size,
+                     const uint32_t *read_ids, uint64_t n, orc_read_out *outs, uint8_t *recs, int nthreads);
+uint64_t orc_scan_batch_k(orc_tree *t, const uint8_t *keys, uint32_t key_stride, uint32_t key_size, uint64_t n,
+                          uint32_t scan_size, uint32_t *counts, uint8_t *recs, int nthreads);
 int64_t orc_export_leaves(orc_tree *t, uint32_t cap, uint64_t max_leaves, uint32_t *rc,
                           uint32_t *sc, uint64_t *meta, uint64_t *keyw);
 

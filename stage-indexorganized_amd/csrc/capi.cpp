@@ -97,13 +97,14 @@ int stage_commit_update(stage_table *t, uint64_t key, uint16_t key_size, uint32_
     });
 }
 
-int stage_update_batch(stage_table *t, const uint64_t *keys, uint64_t n, uint16_t key_size, uint32_t payload_off,
-                       const uint8_t *deltas, uint32_t delta_len, const uint32_t *writer_ids,
+int stage_update_batch(stage_table *t, const void *keys, uint32_t key_stride, uint64_t n, uint16_t key_size,
+                       uint32_t payload_off, const uint8_t *deltas, uint32_t delta_len, const uint32_t *writer_ids,
                        const uint32_t *commit_ids, const uint32_t *sstamps, uint8_t *rc_out, uint64_t *n_ok) {
-    if (!t || (n && (!keys || !writer_ids || (!deltas && delta_len)))) return fail(STAGE_E_ARG, "bad arguments");
+    if (!t || (n && (!keys || !writer_ids || (!deltas && delta_len))) || key_stride < key_size)
+        return fail(STAGE_E_ARG, "bad arguments");
     return guarded([&] {
-        uint64_t ok = t->host->update_batch(keys, n, key_size, payload_off, deltas, delta_len, writer_ids, commit_ids,
-                                            sstamps, rc_out);
+        uint64_t ok = t->host->update_batch((const uint8_t *)keys, key_stride, n, key_size, payload_off, deltas,
+                                            delta_len, writer_ids, commit_ids, sstamps, rc_out);
         if (n_ok) *n_ok = ok;
         return STAGE_OK;
     });
@@ -126,6 +127,60 @@ int stage_delete(stage_table *t, uint64_t key, uint16_t key_size, uint32_t commi
         return STAGE_OK;
     });
 }
+
+// ---- byte-key forms (any key width of the table, up to 32 bytes)
+int stage_insert_key(stage_table *t, const uint8_t *key, uint16_t key_size, const uint8_t *payload, uint32_t commit_id,
+                     uint8_t *rc_out) {
+    if (!t || !key || !payload) return fail(STAGE_E_ARG, "null argument");
+    return guarded([&] {
+        int rc = t->host->insert(key, key_size, payload, 0, 0, commit_id);
+        if (rc_out) *rc_out = (uint8_t)rc;
+        return STAGE_OK;
+    });
+}
+
+int stage_load_rows(stage_table *t, const uint8_t *keys, uint32_t key_stride, uint16_t key_size,
+                    const uint8_t *payloads, uint32_t payload_stride, uint64_t n, uint32_t commit_id,
+                    uint8_t *rc_out, uint64_t *inserted) {
+    if (!t || (n && (!keys || !payloads)) || key_stride < key_size) return fail(STAGE_E_ARG, "bad arguments");
+    if (payload_stride < t->host->params().payload_size) return fail(STAGE_E_ARG, "payload stride < payload size");
+    return guarded([&] {
+        uint64_t c = t->host->load_rows(keys, key_stride, key_size, payloads, payload_stride, n, commit_id, rc_out);
+        if (inserted) *inserted = c;
+        return STAGE_OK;
+    });
+}
+
+int stage_update_key(stage_table *t, const uint8_t *key, uint16_t key_size, uint32_t payload_off,
+                     const uint8_t *delta, uint32_t delta_len, uint32_t writer_id, uint8_t *rc_out) {
+    if (!t || !key || (!delta && delta_len)) return fail(STAGE_E_ARG, "bad arguments");
+    return guarded([&] {
+        int rc = t->host->update(key, key_size, payload_off, delta, delta_len, writer_id);
+        if (rc_out) *rc_out = (uint8_t)rc;
+        return STAGE_OK;
+    });
+}
+
+int stage_commit_update_key(stage_table *t, const uint8_t *key, uint16_t key_size, uint32_t commit_id,
+                            uint32_t sstamp, uint8_t *rc_out) {
+    if (!t || !key) return fail(STAGE_E_ARG, "null argument");
+    return guarded([&] {
+        int rc = t->host->commit_update(key, key_size, commit_id, sstamp);
+        if (rc_out) *rc_out = (uint8_t)rc;
+        return STAGE_OK;
+    });
+}
+
+int stage_delete_key(stage_table *t, const uint8_t *key, uint16_t key_size, uint32_t commit_id, uint8_t *rc_out) {
+    if (!t || !key) return fail(STAGE_E_ARG, "null argument");
+    return guarded([&] {
+        int rc = t->host->remove(key, key_size, commit_id);
+        if (rc_out) *rc_out = (uint8_t)rc;
+        return STAGE_OK;
+    });
+}
+
+uint32_t stage_key_words(stage_table *t) { return t ? t->host->key_words() : 0; }
 
 int stage_sync(stage_table *t) {
     if (!t) return fail(STAGE_E_ARG, "null table");
@@ -173,11 +228,10 @@ int stage_traverse_batch(stage_table *t, const uint64_t *keys, const uint16_t *l
             for (size_t i = 0; i < order.size(); ++i) local[order[i]] = (uint32_t)i;
             map = &local;
         }
-        const uint32_t kw = t->host->params().key_width;
+        const uint32_t width = t->host->params().key_width, kwords = t->host->key_words();
         for (uint64_t i = 0; i < n; ++i) {
-            const uint32_t len = kw ? kw : (lens ? lens[i] : 8u);
-            const uint64_t mask = len >= 8 ? ~0ull : ((1ull << (8 * len)) - 1);
-            stage::Key k{stage::order_key(keys[i] & mask, len), len};
+            const uint32_t len = width ? width : (lens ? lens[i] : 8u);
+            const stage::Key k = t->host->key_of(reinterpret_cast<const uint8_t *>(keys + i * kwords), len);
             leaf_out[i] = (*map)[t->host->route(k, le_child != 0)];
         }
         return STAGE_OK;
@@ -316,6 +370,7 @@ int stage_comm_unique_id(uint8_t *id128) {
 
 int stage_comm_init(stage_table *t, const uint8_t *id128, int rank, int world) {
     if (!t || !id128 || world < 1 || rank < 0 || rank >= world) return fail(STAGE_E_ARG, "bad arguments");
+    if (t->host->key_words() != 1) return fail(STAGE_E_ARG, "the sharded front-end routes keys of <= 8 bytes");
     return guarded([&] {
         (void)hipSetDevice(t->dev.device);
         t->comm = std::make_unique<stage::ShardComm>();
@@ -381,6 +436,7 @@ int stage_probe_sharded_loopback(stage_table *const *shards, int world, const ui
     for (int r = 0; r < world; ++r) {
         int rc = need_synced(shards[r]);
         if (rc) return rc;
+        if (shards[r]->host->key_words() != 1) return fail(STAGE_E_ARG, "the sharded front-end routes keys of <= 8 bytes");
         if (shards[r]->dev.device != shards[0]->dev.device) return fail(STAGE_E_ARG, "shards on different devices");
         if ((d_records[r] == nullptr) != (d_records[0] == nullptr)) return fail(STAGE_E_ARG, "rows for all or none");
     }

@@ -55,10 +55,11 @@ static void upload(DevBuf &b, const void *src, uint64_t bytes, hipStream_t s, co
     if (bytes) hip_check(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, s), what);
 }
 
-// One leaf's head (fingerprints + visible mask) and slot words, reference slot order.
+// One leaf's head (fingerprints + visible mask), key planes and slot words, reference slot
+// order.  okey points at the leaf's KW planes of cap words.
 static void build_leaf(const HostTable &h, uint32_t hl, uint8_t *hd, uint64_t *okey, SlotInfo *slot) {
     const stage_params &p = h.params();
-    const uint32_t cap = h.cap(), spl = cap / 64, hb = leaf_head_bytes(cap);
+    const uint32_t cap = h.cap(), spl = cap / 64, hb = leaf_head_bytes(cap), kw = h.key_words();
     const uint64_t hbase = (uint64_t)hl * cap;
     const uint32_t count = h.leaves_[hl].count;
     std::memset(hd, 0, hb);
@@ -66,16 +67,18 @@ static void build_leaf(const HostTable &h, uint32_t hl, uint8_t *hd, uint64_t *o
     for (uint32_t s = 0; s < cap; ++s) {
         const bool live = s < count;
         const uint64_t m = live ? h.meta_[hbase + s] : 0;
-        const uint64_t ok = live ? h.okey_[hbase + s] : 0;
-        okey[s] = ok;
-        slot[s].okey = ok;
+        uint64_t w[kMaxKeyWords] = {0, 0, 0, 0};
+        if (live)
+            for (uint32_t j = 0; j < kw; ++j) w[j] = h.okey_[(hbase + s) * kw + j];
+        for (uint32_t j = 0; j < kw; ++j) okey[(uint64_t)j * cap + s] = w[j];
+        slot[s].okey = w[0];
         slot[s].meta = m;
         slot[s].next = live ? h.next_[hbase + s] : 0;
         slot[s].image = live ? h.image_[hbase + s] : 0;
         slot[s].pad = 0;
         if (meta_visible(m) && (p.key_width == 0 || meta_keylen(m) == p.key_width)) {
             vis[s / 64] |= 1ull << (s % 64);
-            hd[s] = (uint8_t)key_fp(ok);
+            hd[s] = (uint8_t)key_fp_words(w, kw);
         }
     }
     std::memcpy(hd + cap, vis, 8 * spl);
@@ -123,16 +126,20 @@ static void patch_device(HostTable &h, DeviceImage &d, hipStream_t s) {
         if (leaves.empty() || leaves.back() != x / cap) leaves.push_back((uint32_t)(x / cap));
     const uint64_t nl = leaves.size(), ns = ds.size();
     if (nl == 0) return;
-    // staging: [dev leaf u32 ...][heads nl*hb][slot idx u64 ...][SlotInfo ...], 32-B aligned parts
+    // staging: [dev leaf u32 ...][heads nl*hb][slot idx u64 ...][SlotInfo ...][key words ns*kw],
+    // 32-B aligned parts
+    const uint32_t kw = h.key_words();
     auto al = [](uint64_t x) { return (x + 31) & ~31ull; };
     const uint64_t o_head = al(nl * 4), o_idx = o_head + al(nl * hb), o_src = o_idx + al(ns * 8);
-    const uint64_t bytes = o_src + ns * sizeof(SlotInfo);
+    const uint64_t o_words = o_src + al(ns * sizeof(SlotInfo));
+    const uint64_t bytes = o_words + ns * kw * 8;
     d.staging.resize(bytes);
     uint8_t *st = d.staging.data();
     uint32_t *dleaf = (uint32_t *)st;
     uint64_t *sidx = (uint64_t *)(st + o_idx);
     SlotInfo *ssrc = (SlotInfo *)(st + o_src);
-    std::vector<uint64_t> okey_tmp(cap);
+    uint64_t *swords = (uint64_t *)(st + o_words);
+    std::vector<uint64_t> okey_tmp((uint64_t)cap * kw);
     std::vector<SlotInfo> slot_tmp(cap);
     uint64_t k = 0;
     for (uint64_t li = 0; li < nl; ++li) {
@@ -143,12 +150,14 @@ static void patch_device(HostTable &h, DeviceImage &d, hipStream_t s) {
             const uint32_t sl = (uint32_t)(ds[k] % cap);
             sidx[k] = (uint64_t)dl * cap + sl;
             ssrc[k] = slot_tmp[sl];
+            for (uint32_t j = 0; j < kw; ++j) swords[k * kw + j] = okey_tmp[(uint64_t)j * cap + sl];
         }
     }
     upload(d.patch, st, bytes, s, "patch staging");
     uint8_t *dp = (uint8_t *)d.patch.p;
-    hip_check(launch_patch((uint8_t *)d.head.p, (uint64_t *)d.okey.p, (SlotInfo *)d.slot.p, hb, (const uint32_t *)dp,
-                           dp + o_head, nl, (const uint64_t *)(dp + o_idx), (const SlotInfo *)(dp + o_src), ns, s),
+    hip_check(launch_patch((uint8_t *)d.head.p, (uint64_t *)d.okey.p, (SlotInfo *)d.slot.p, hb, cap, kw,
+                           (const uint32_t *)dp, dp + o_head, nl, (const uint64_t *)(dp + o_idx),
+                           (const SlotInfo *)(dp + o_src), (const uint64_t *)(dp + o_words), ns, s),
               "patch");
     d.last_patch_leaves = nl;
     d.last_patch_slots = ns;
@@ -208,8 +217,8 @@ static void sync_heap(HostTable &h, DeviceImage &d, hipStream_t s) {
             }
         }
         if (ident) {
-            hip_check(launch_fill((uint8_t *)d.heap.p, stride, p.payload_size, nullptr, nullptr, first, count, d0.arg,
-                                  kw, (int)d0.mode, s),
+            hip_check(launch_fill((uint8_t *)d.heap.p, stride, p.payload_size, h.key_pad() + p.payload_size, nullptr,
+                                  nullptr, first, count, d0.arg, kw, (int)d0.mode, s),
                       "fill (identity)");
         } else {
             std::vector<ImageDescDev> dd(count);
@@ -218,8 +227,9 @@ static void sync_heap(HostTable &h, DeviceImage &d, hipStream_t s) {
                 dd[r] = ImageDescDev{e.key_le, e.arg, e.kind, e.mode};
             }
             upload(d.descs, dd.data(), count * sizeof(ImageDescDev), s, "descs");
-            hip_check(launch_fill((uint8_t *)d.heap.p, stride, p.payload_size, (const ImageDescDev *)d.descs.p,
-                                  (const uint8_t *)d.arena.p, first, count, 0, 0, 0, s),
+            hip_check(launch_fill((uint8_t *)d.heap.p, stride, p.payload_size, h.key_pad() + p.payload_size,
+                                  (const ImageDescDev *)d.descs.p, (const uint8_t *)d.arena.p, first, count, 0, 0, 0,
+                                  s),
                       "fill");
             hip_check(hipStreamSynchronize(s), "fill sync");  // dd is pageable and local
         }
@@ -256,40 +266,42 @@ void sync_device(HostTable &h, DeviceImage &d) {
     d.host_to_dev.assign(h.leaves_.size(), 0xFFFFFFFFu);
     for (uint64_t i = 0; i < L; ++i) d.host_to_dev[order[i]] = (uint32_t)i;
 
-    const uint32_t hb = leaf_head_bytes(cap);
-    std::vector<uint64_t> okey(L * cap);
+    const uint32_t hb = leaf_head_bytes(cap), kw = h.key_words();
+    std::vector<uint64_t> okey(L * cap * kw);
     std::vector<uint8_t> head(L * hb, 0);
     std::vector<SlotInfo> slot(L * cap);
     parallel_for(L, [&](uint64_t di) {
-        build_leaf(h, order[di], head.data() + di * hb, okey.data() + di * cap, slot.data() + di * cap);
+        build_leaf(h, order[di], head.data() + di * hb, okey.data() + di * cap * kw, slot.data() + di * cap);
     });
 
     // ---- implicit 16-ary separator tree: level 0 = separators, level k+1 = max of each
-    // 16-entry node of level k, every level padded with +inf, top level one node.
+    // 16-entry node of level k, every level padded with +inf, top level one node.  An entry
+    // is kw order words (entry-major); lengths ride along for variable-length tables.
     const uint64_t S = L ? L - 1 : 0;
     std::vector<std::vector<uint64_t>> lv;
     std::vector<std::vector<uint8_t>> lvlen;
     {
         const uint64_t n0 = (S + 1 + kTreeFanout - 1) / kTreeFanout * kTreeFanout;
-        std::vector<uint64_t> l0(n0, ~0ull);
+        std::vector<uint64_t> l0(n0 * kw, ~0ull);
         std::vector<uint8_t> l0len(n0, 0xFF);
         for (uint64_t i = 0; i < S; ++i) {
             const auto &sep = h.leaves_[order[i]].sep;
-            l0[i] = sep.okey;
+            for (uint32_t j = 0; j < kw; ++j) l0[i * kw + j] = sep.w[j];
             l0len[i] = (uint8_t)sep.len;
         }
         lv.push_back(std::move(l0));
         lvlen.push_back(std::move(l0len));
-        while (lv.back().size() > (uint64_t)kTreeFanout) {
+        while (lvlen.back().size() > (uint64_t)kTreeFanout) {
             const auto &prev = lv.back();
             const auto &prevlen = lvlen.back();
-            const uint64_t nodes = prev.size() / kTreeFanout;
+            const uint64_t nodes = prevlen.size() / kTreeFanout;
             const uint64_t nn = (nodes + kTreeFanout - 1) / kTreeFanout * kTreeFanout;
-            std::vector<uint64_t> nx(nn, ~0ull);
+            std::vector<uint64_t> nx(nn * kw, ~0ull);
             std::vector<uint8_t> nxlen(nn, 0xFF);
             for (uint64_t j = 0; j < nodes; ++j) {
-                nx[j] = prev[j * kTreeFanout + kTreeFanout - 1];
-                nxlen[j] = prevlen[j * kTreeFanout + kTreeFanout - 1];
+                const uint64_t last = j * kTreeFanout + kTreeFanout - 1;
+                for (uint32_t w = 0; w < kw; ++w) nx[j * kw + w] = prev[last * kw + w];
+                nxlen[j] = prevlen[last];
             }
             lv.push_back(std::move(nx));
             lvlen.push_back(std::move(nxlen));
@@ -300,7 +312,7 @@ void sync_device(HostTable &h, DeviceImage &d) {
     std::vector<uint8_t> tree_len;
     uint64_t level_off[kMaxTreeLevels] = {0};
     for (size_t k = 0; k < lv.size(); ++k) {
-        level_off[k] = tree.size();
+        level_off[k] = tree_len.size();  // in entries
         tree.insert(tree.end(), lv[k].begin(), lv[k].end());
         tree_len.insert(tree_len.end(), lvlen[k].begin(), lvlen[k].end());
     }
@@ -333,6 +345,7 @@ void sync_device(HostTable &h, DeviceImage &d) {
     v.head_bytes = hb;
     v.payload_size = p.payload_size;
     v.key_width = p.key_width;
+    v.key_words = kw;
     h.layout_dirty_ = false;
     h.structure_dirty_ = false;
     h.dirty_slots_.clear();

@@ -44,10 +44,11 @@ struct PipeLane {
 struct HostPipe {
     int device = 0;
     uint64_t stride = 0;
+    uint32_t kw = 1;  // u64 key words per probe
     PipeLane lane[kPipeLanes];
 };
 
-static uint64_t lane_bytes(uint64_t stride) { return kPipeChunk * (8 + 2 + 4 + 32 + stride); }
+static uint64_t lane_bytes(uint64_t stride, uint32_t kw) { return kPipeChunk * (8ull * kw + 2 + 4 + 32 + stride); }
 
 void host_pipe_release(HostPipe *p) {
     if (!p) return;
@@ -61,14 +62,17 @@ void host_pipe_release(HostPipe *p) {
 
 static HostPipe *get_pipe(stage_table *t) {
     const uint64_t stride = t->out_stride ? t->out_stride : t->dev.view.stride;
-    if (t->pipe && t->pipe->stride == stride && t->pipe->device == t->dev.device) return t->pipe.get();
+    const uint32_t kw = t->host->key_words();
+    if (t->pipe && t->pipe->stride == stride && t->pipe->kw == kw && t->pipe->device == t->dev.device)
+        return t->pipe.get();
     t->pipe.reset();
     std::unique_ptr<HostPipe, HostPipeDeleter> p(new HostPipe);
     p->device = t->dev.device;
     p->stride = stride;
+    p->kw = kw;
     for (auto &l : p->lane) {
         hip_check(hipStreamCreateWithFlags(&l.s, hipStreamNonBlocking), "pipe stream");
-        hip_check(hipMalloc(&l.d, lane_bytes(stride)), "pipe buffers");
+        hip_check(hipMalloc(&l.d, lane_bytes(stride, kw)), "pipe buffers");
     }
     t->pipe = std::move(p);
     return t->pipe.get();
@@ -79,12 +83,12 @@ static HostPipe *get_pipe(stage_table *t) {
 namespace {
 
 // one probe of n <= kPipeChunk keys on a lane: H2D inputs, probe, D2H results (all async)
-hipError_t pipe_chunk(stage_table *t, stage::PipeLane &l, uint64_t stride, const uint64_t *keys, const uint16_t *lens,
-                      const uint32_t *rids, uint64_t n, stage_probe_out *out, uint8_t *rows) {
+hipError_t pipe_chunk(stage_table *t, stage::PipeLane &l, uint64_t stride, uint32_t kw, const uint64_t *keys,
+                      const uint16_t *lens, const uint32_t *rids, uint64_t n, stage_probe_out *out, uint8_t *rows) {
     using stage::kPipeChunk;
-    uint8_t *dk = l.d, *dl = dk + 8 * kPipeChunk, *dr = dl + 2 * kPipeChunk, *dout = dr + 4 * kPipeChunk,
+    uint8_t *dk = l.d, *dl = dk + 8ull * kw * kPipeChunk, *dr = dl + 2 * kPipeChunk, *dout = dr + 4 * kPipeChunk,
             *drow = dout + 32 * kPipeChunk;
-    hipError_t e = hipMemcpyAsync(dk, keys, 8 * n, hipMemcpyHostToDevice, l.s);
+    hipError_t e = hipMemcpyAsync(dk, keys, 8ull * kw * n, hipMemcpyHostToDevice, l.s);
     if (!e && lens) e = hipMemcpyAsync(dl, lens, 2 * n, hipMemcpyHostToDevice, l.s);
     if (!e && rids) e = hipMemcpyAsync(dr, rids, 4 * n, hipMemcpyHostToDevice, l.s);
     if (e) return e;
@@ -287,7 +291,7 @@ int stage_probe_host(stage_table *t, const uint64_t *keys, const uint16_t *lens,
             stage::PipeLane &l = p->lane[c % stage::kPipeLanes];
             if (c >= (uint64_t)stage::kPipeLanes) stage::hip_check(hipStreamSynchronize(l.s), "pipe lane");
             const uint64_t b = c * stage::kPipeChunk, m = std::min<uint64_t>(stage::kPipeChunk, n - b);
-            stage::hip_check(pipe_chunk(t, l, p->stride, keys + b, lens ? lens + b : nullptr,
+            stage::hip_check(pipe_chunk(t, l, p->stride, p->kw, keys + b * p->kw, lens ? lens + b : nullptr,
                                         read_ids ? read_ids + b : nullptr, m, out + b,
                                         records ? records + b * p->stride : nullptr),
                              "probe_host chunk");
@@ -299,6 +303,7 @@ int stage_probe_host(stage_table *t, const uint64_t *keys, const uint16_t *lens,
 
 int stage_reader_create(stage_table *t, uint32_t max_batch, uint32_t max_wait_us, stage_reader **out) {
     if (!t || !out || max_batch == 0 || max_batch > (1u << 20)) return fail(STAGE_E_ARG, "bad reader arguments");
+    if (t->host->key_words() != 1) return fail(STAGE_E_ARG, "the single-key reader takes keys of <= 8 bytes");
     *out = nullptr;
     return guarded([&] {
         std::unique_ptr<stage_reader> r(new stage_reader);

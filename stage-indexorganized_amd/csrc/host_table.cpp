@@ -39,25 +39,57 @@ void gen_payload(uint64_t rowid, int mode, uint8_t *dst, uint32_t payload_size) 
 
 static uint64_t key_mask(uint32_t len) { return len >= 8 ? ~0ull : ((1ull << (8 * len)) - 1); }
 
+Key make_key(const uint8_t *bytes, uint32_t len, bool uns) {
+    Key k = key_zero();
+    k.len = len;
+    for (uint32_t j = 0; j < (uint32_t)kMaxKeyWords && 8 * j < len; ++j) {
+        const uint32_t nb = std::min<uint32_t>(8, len - 8 * j);
+        uint64_t w = 0;
+        std::memcpy(&w, bytes + 8 * j, nb);
+        k.w[j] = order_word(w, len, j, uns);
+    }
+    return k;
+}
+
+void key_to_bytes(const Key &k, uint8_t *out, bool uns) {
+    for (uint32_t j = 0; 8 * j < k.len; ++j) {
+        const uint32_t nb = std::min<uint32_t>(8, k.len - 8 * j);
+        const uint64_t w = uns ? bswap64(k.w[j]) : key_bytes_from_order(k.w[j], nb);
+        std::memcpy(out + 8 * j, &w, nb);
+    }
+}
+
 HostTable::HostTable(const stage_params &p) : p_(p) {
-    if (p.payload_size == 0 || p.leaf_node_size < 256 || p.key_width > 8)
+    if (p.payload_size == 0 || p.leaf_node_size < 256 || p.key_width > kMaxKeyBytes)
         throw std::invalid_argument("bad table parameters");
-    const uint32_t rec = 8 + p.payload_size;  // keys are at most 8 bytes -> padded to 8
+    kw_ = table_key_words(p.key_width);
+    uns_ = key_order_unsigned(p.key_width);
+    kpad_ = p.key_width > 8 ? pad8(p.key_width) : 8u;  // keys of <= 8 bytes pad to 8
+    const uint32_t rec = kpad_ + p.payload_size;
     // largest record count c with 40 + c*(24+rec) < leaf_node_size (the Insert space check)
     const uint32_t room = p.leaf_node_size - 40;
     max_records_ = (room + (24 + rec) - 1) / (24 + rec) - 1;
     if (max_records_ < 3) throw std::invalid_argument("leaf holds fewer than 3 records");
-    if (max_records_ <= 64) cap_ = 64;
-    else if (max_records_ <= 128) cap_ = 128;
-    else throw std::invalid_argument("more than 128 records per leaf is not supported");
+    // slots per device leaf: 64 * a power of two (the kernels' slot groups); keys of <= 8 bytes
+    // up to 128, wide keys (small TPC-C rows) up to 1024
+    cap_ = 64;
+    while (cap_ < max_records_) cap_ *= 2;
+    if (cap_ > (kw_ == 1 ? 128u : 1024u))
+        throw std::invalid_argument("too many records per leaf for the device layout (payload too small)");
     // output/heap row: [key padded to 8][payload], 16-B multiple; rows above 128 B are
     // 128-B multiples so every row starts on an L2 line (a 1008-B tuple = 8 whole lines)
-    stride_ = (8 + p.payload_size + 15) & ~15u;
+    stride_ = (kpad_ + p.payload_size + 15) & ~15u;
     if (stride_ > 128) stride_ = (stride_ + 127) & ~127u;
     buckets_.resize(1u << 16);
     uint32_t root = alloc_leaf();
     head_ = (int32_t)root;
-    for (auto &b : buckets_) b.push_back(RouteEntry{~0ull, root, kInfLen});
+    for (auto &b : buckets_) b.push_back(RouteEntry{key_inf(), root});
+}
+
+bool HostTable::key_ok(uint32_t len) const {
+    if (len == 0 || len > kMaxKeyBytes) return false;
+    if (p_.key_width) return len == p_.key_width;
+    return len <= 8;  // variable-length tables hold keys of 1..8 bytes
 }
 
 uint32_t HostTable::alloc_leaf() {
@@ -70,13 +102,13 @@ uint32_t HostTable::alloc_leaf() {
         id = (uint32_t)leaves_.size();
         leaves_.emplace_back();
         size_t n = (size_t)leaves_.size() * cap_;
-        okey_.resize(n, 0);
+        okey_.resize(n * kw_, 0);
         meta_.resize(n, 0);
         next_.resize(n, 0);
         image_.resize(n, 0);
     }
     size_t b = (size_t)id * cap_;
-    std::fill(okey_.begin() + b, okey_.begin() + b + cap_, 0);
+    std::fill(okey_.begin() + b * kw_, okey_.begin() + (b + cap_) * kw_, 0);
     std::fill(meta_.begin() + b, meta_.begin() + b + cap_, 0);
     std::fill(next_.begin() + b, next_.begin() + b + cap_, 0);
     std::fill(image_.begin() + b, image_.begin() + b + cap_, 0);
@@ -86,12 +118,11 @@ uint32_t HostTable::alloc_leaf() {
 }
 
 uint32_t HostTable::route(const Key &k, bool le_child) const {
-    for (uint32_t b = bucket_of(k.okey); b < buckets_.size(); ++b) {
+    for (uint32_t b = bucket_of(k); b < buckets_.size(); ++b) {
         const auto &v = buckets_[b];
         auto it = le_child ? std::lower_bound(v.begin(), v.end(), k, entry_lt_key)
-                           : std::upper_bound(v.begin(), v.end(), k, [](const Key &kk, const RouteEntry &e) {
-                                 return kk.okey < e.sep_okey || (kk.okey == e.sep_okey && kk.len < e.sep_len);
-                             });
+                           : std::upper_bound(v.begin(), v.end(), k,
+                                              [](const Key &kk, const RouteEntry &e) { return key_lt(kk, e.sep); });
         if (it != v.end()) return it->leaf;
     }
     return buckets_.back().back().leaf;  // the +inf leaf
@@ -103,26 +134,41 @@ uint32_t HostTable::route(const Key &k, bool le_child) const {
 int64_t HostTable::search(uint32_t leaf, const Key &k) const {
     const Leaf &L = leaves_[leaf];
     const size_t b = (size_t)leaf * cap_;
-    const uint64_t *ok = okey_.data() + b;
+    const uint64_t *ok = okey_.data() + b * kw_;
     for (uint32_t s = 0; s < L.count; ++s) {
-        if (ok[s] != k.okey) continue;
+        const uint64_t *w = ok + (size_t)s * kw_;
+        if (w[0] != k.w[0]) continue;
+        bool eq = true;
+        for (uint32_t j = 1; j < kw_; ++j) eq &= w[j] == k.w[j];
+        if (!eq) continue;
         uint64_t m = meta_[b + s];
         if (meta_visible(m) && meta_keylen(m) == k.len) return s;
     }
     return -1;
 }
 
-uint32_t HostTable::new_image(uint64_t key_le, const uint8_t *payload, uint64_t gen_rowid, int mode) {
+uint32_t HostTable::new_image(const uint8_t *key, uint32_t len, const uint8_t *payload, uint64_t gen_rowid,
+                              int mode) {
     ImageDesc d;
-    d.key_le = key_le;
+    d.key_le = 0;
     d.mode = (uint32_t)mode;
-    if (payload) {
-        d.kind = 1;
+    if (len > 8) {  // wide key: the arena holds the whole row [key padded][payload]
+        if (!payload) throw std::invalid_argument("keys above 8 bytes need an explicit payload");
+        d.kind = 2;
         d.arg = arena_.size();
-        arena_.insert(arena_.end(), payload, payload + p_.payload_size);
+        arena_.resize(arena_.size() + kpad_ + p_.payload_size, 0);
+        std::memcpy(arena_.data() + d.arg, key, len);
+        std::memcpy(arena_.data() + d.arg + kpad_, payload, p_.payload_size);
     } else {
-        d.kind = 0;
-        d.arg = gen_rowid;
+        std::memcpy(&d.key_le, key, len);
+        if (payload) {
+            d.kind = 1;
+            d.arg = arena_.size();
+            arena_.insert(arena_.end(), payload, payload + p_.payload_size);
+        } else {
+            d.kind = 0;
+            d.arg = gen_rowid;
+        }
     }
     images_.push_back(d);
     if (images_.size() > kNextIndexMask) throw std::runtime_error("record heap index overflow");
@@ -132,16 +178,15 @@ uint32_t HostTable::new_image(uint64_t key_le, const uint8_t *payload, uint64_t 
 void HostTable::image_payload(uint32_t img, uint8_t *dst) const {
     const ImageDesc &d = images_[img];
     if (d.kind == 0) gen_payload(d.arg, (int)d.mode, dst, p_.payload_size);
-    else std::memcpy(dst, arena_.data() + d.arg, p_.payload_size);
+    else if (d.kind == 1) std::memcpy(dst, arena_.data() + d.arg, p_.payload_size);
+    else std::memcpy(dst, arena_.data() + d.arg + kpad_, p_.payload_size);
 }
 
-int HostTable::insert(uint64_t key_le, uint32_t len, const uint8_t *payload, uint64_t gen_rowid, int mode,
+int HostTable::insert(const uint8_t *key, uint32_t len, const uint8_t *payload, uint64_t gen_rowid, int mode,
                       uint32_t commit_id) {
-    if (len == 0 || len > 8) return STAGE_RC_INVALID;
-    if (p_.key_width && len != p_.key_width) return STAGE_RC_INVALID;
-    key_le &= key_mask(len);
-    const Key k{order_key(key_le, len), len};
-    const uint32_t rec = pad8(len) + p_.payload_size;
+    if (!key_ok(len)) return STAGE_RC_INVALID;
+    const Key k = make_key(key, len, uns_);
+    const uint32_t rec = (len > 8 ? pad8(len) : 8u) + p_.payload_size;
     for (int guard = 0; guard < 64; ++guard) {
         uint32_t leaf = route(k, true);
         int64_t hit = search(leaf, k);  // CheckUnique (b_tree.cpp:1395-1417)
@@ -158,11 +203,11 @@ int HostTable::insert(uint64_t key_le, uint32_t len, const uint8_t *payload, uin
         L.block += rec;
         const uint64_t offset = p_.leaf_node_size - L.block;
         const size_t i = (size_t)leaf * cap_ + slot;
-        okey_[i] = k.okey;
+        set_slot_key(i, k);
         // PrepareForInsert then FinalizeInsert: control bit cleared, cstamp = commit_id
         meta_[i] = ((uint64_t)len << 48) | kMetaVisible | (offset << 32) | commit_id;
         next_[i] = 0;
-        image_[i] = new_image(key_le, payload, gen_rowid, mode);
+        image_[i] = new_image(key, len, payload, gen_rowid, mode);
         touch(leaf, slot);
         return STAGE_RC_OK;
     }
@@ -172,7 +217,8 @@ int HostTable::insert(uint64_t key_le, uint32_t len, const uint8_t *payload, uin
 bool HostTable::split(uint32_t p) {
     if (leaves_[p].count < 3) return false;
     struct Rec {
-        uint64_t okey, meta;
+        Key key;
+        uint64_t meta;
         uint32_t next, image;
     };
     const size_t pb = (size_t)p * cap_;
@@ -183,14 +229,12 @@ bool HostTable::split(uint32_t p) {
         uint64_t m = meta_[pb + s];
         if (m == 0) continue;
         if (meta_visible(m) && meta_keylen(m) > 0) {
-            v.push_back(Rec{okey_[pb + s], m, next_[pb + s], image_[pb + s]});
+            v.push_back(Rec{slot_key(pb + s), m, next_[pb + s], image_[pb + s]});
             total += pad8(meta_keylen(m)) + p_.payload_size;
         }
     }
     if (total == 0) return false;
-    std::sort(v.begin(), v.end(), [](const Rec &a, const Rec &b) {
-        return a.okey < b.okey || (a.okey == b.okey && meta_keylen(a.meta) < meta_keylen(b.meta));
-    });
+    std::sort(v.begin(), v.end(), [](const Rec &a, const Rec &b) { return key_lt(a.key, b.key); });
     int32_t left_size = (int32_t)(total / 2);
     uint32_t nleft = 0;
     for (size_t i = 0; i < v.size(); ++i) {
@@ -198,10 +242,9 @@ bool HostTable::split(uint32_t p) {
         left_size -= (int32_t)(pad8(meta_keylen(v[i].meta)) + p_.payload_size);
         if (left_size <= 0) break;
     }
-    const Key sep{v[nleft - 1].okey, meta_keylen(v[nleft - 1].meta)};
+    const Key sep = v[nleft - 1].key;
     const Key hi = leaves_[p].sep;
-    const Key lo = leaves_[p].prev >= 0 ? leaves_[leaves_[p].prev].sep : Key{0, 0};
-    const bool lo_inf = leaves_[p].prev < 0;
+    const Key lo = leaves_[p].prev >= 0 ? leaves_[leaves_[p].prev].sep : key_zero();
 
     const uint32_t r = alloc_leaf();  // may reallocate the arrays
     auto fill = [&](uint32_t leaf, size_t from, size_t to) {
@@ -211,14 +254,14 @@ bool HostTable::split(uint32_t p) {
         for (size_t i = from; i < to; ++i) {
             const uint32_t kl = meta_keylen(v[i].meta);
             offset -= pad8(kl) + p_.payload_size;
-            okey_[b + n] = v[i].okey;
+            set_slot_key(b + n, v[i].key);
             meta_[b + n] = ((uint64_t)kl << 48) | kMetaVisible | ((uint64_t)offset << 32) | meta_cstamp(v[i].meta);
             next_[b + n] = v[i].next;
             image_[b + n] = v[i].image;
             ++n;
         }
         for (uint32_t s = n; s < cap_; ++s) {
-            okey_[b + s] = 0;
+            clear_slot_key(b + s);
             meta_[b + s] = 0;
             next_[b + s] = 0;
             image_[b + s] = 0;
@@ -237,7 +280,7 @@ bool HostTable::split(uint32_t p) {
     R.next = P.next;
     if (P.next >= 0) leaves_[P.next].prev = (int32_t)r;
     P.next = (int32_t)r;
-    route_split(p, r, lo_inf ? Key{0, 0} : lo, sep, hi);
+    route_split(p, r, lo, sep, hi);
     layout_dirty_ = true;
     structure_dirty_ = true;
     dirty_slots_.clear();
@@ -245,27 +288,27 @@ bool HostTable::split(uint32_t p) {
 }
 
 void HostTable::route_split(uint32_t p, uint32_t r, const Key &lo, const Key &s, const Key &hi) {
-    const uint32_t b_lo = bucket_of(lo.okey);
-    const uint32_t b_hi = key_is_inf(hi) ? (uint32_t)buckets_.size() - 1 : bucket_of(hi.okey);
-    const uint32_t b_s = bucket_of(s.okey);
+    const uint32_t b_lo = bucket_of(lo);
+    const uint32_t b_hi = key_is_inf(hi) ? (uint32_t)buckets_.size() - 1 : bucket_of(hi);
+    const uint32_t b_s = bucket_of(s);
     for (uint32_t b = b_lo; b <= b_hi; ++b) {
         auto &v = buckets_[b];
         auto it = std::lower_bound(v.begin(), v.end(), hi, entry_lt_key);
         while (it != v.end() && it->leaf != p) ++it;
         if (it == v.end()) continue;  // p does not reach this bucket
         if (b < b_s) {
-            it->sep_okey = s.okey;
-            it->sep_len = s.len;
+            it->sep = s;
         } else if (b > b_s) {
             it->leaf = r;
         } else {
             it->leaf = r;
-            v.insert(it, RouteEntry{s.okey, p, s.len});
+            v.insert(it, RouteEntry{s, p});
         }
     }
 }
 
 uint64_t HostTable::load_ycsb(uint64_t begin, uint64_t end, uint32_t key_size, int mode) {
+    if (key_size > 8) return 0;
     if (end > begin) images_.reserve(images_.size() + (end - begin));
     uint64_t ok = 0;
     for (uint64_t rowid = begin; rowid < end; ++rowid)
@@ -274,6 +317,7 @@ uint64_t HostTable::load_ycsb(uint64_t begin, uint64_t end, uint32_t key_size, i
 }
 
 uint64_t HostTable::load_keys(const uint64_t *keys, uint64_t n, uint32_t key_size, int mode) {
+    if (key_size > 8) return 0;
     images_.reserve(images_.size() + n);
     uint64_t ok = 0;
     for (uint64_t i = 0; i < n; ++i)
@@ -281,10 +325,23 @@ uint64_t HostTable::load_keys(const uint64_t *keys, uint64_t n, uint32_t key_siz
     return ok;
 }
 
-int HostTable::find(uint64_t key_le, uint32_t len, uint32_t *leaf, uint32_t *slot) const {
-    if (len == 0 || len > 8) return -1;
-    key_le &= key_mask(len);
-    const Key k{order_key(key_le, len), len};
+uint64_t HostTable::load_rows(const uint8_t *keys, uint32_t key_stride, uint32_t key_size, const uint8_t *payloads,
+                              uint32_t payload_stride, uint64_t n, uint32_t commit_id, uint8_t *rc_out) {
+    images_.reserve(images_.size() + n);
+    arena_.reserve(arena_.size() + n * (uint64_t)(kpad_ + p_.payload_size));
+    uint64_t ok = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const int rc = insert(keys + i * (uint64_t)key_stride, key_size, payloads + i * (uint64_t)payload_stride, 0, 0,
+                              commit_id);
+        if (rc == STAGE_RC_OK) ++ok;
+        if (rc_out) rc_out[i] = (uint8_t)rc;
+    }
+    return ok;
+}
+
+int HostTable::find(const uint8_t *key, uint32_t len, uint32_t *leaf, uint32_t *slot) const {
+    if (!key_ok(len)) return -1;
+    const Key k = make_key(key, len, uns_);
     uint32_t lf = route(k, true);
     int64_t s = search(lf, k);
     if (s < 0) return -1;
@@ -295,10 +352,10 @@ int HostTable::find(uint64_t key_le, uint32_t len, uint32_t *leaf, uint32_t *slo
 
 // LeafNode::Update, b_tree.cpp:1061-1163 (is_for_update == false): the old image becomes the
 // overwrite copy (its image row is immutable), the record gets a new patched image.
-int HostTable::update(uint64_t key_le, uint32_t len, uint32_t payload_off, const uint8_t *delta, uint32_t delta_len,
-                      uint32_t writer_id) {
+int HostTable::update(const uint8_t *key, uint32_t len, uint32_t payload_off, const uint8_t *delta,
+                      uint32_t delta_len, uint32_t writer_id) {
     uint32_t leaf, slot;
-    if (find(key_le, len, &leaf, &slot) < 0) return STAGE_RC_NOT_FOUND;
+    if (find(key, len, &leaf, &slot) < 0) return STAGE_RC_NOT_FOUND;
     const size_t i = (size_t)leaf * cap_ + slot;
     const uint64_t m = meta_[i];
     if (meta_inserting(m)) return STAGE_RC_DIRTY;
@@ -318,15 +375,15 @@ int HostTable::update(uint64_t key_le, uint32_t len, uint32_t payload_off, const
     if (copies_.size() > kNextIndexMask) throw std::runtime_error("copy index overflow");
     next_[i] = kNextCopy | (uint32_t)(copies_.size() - 1);
     std::memcpy(pay.data() + payload_off, delta, delta_len);  // CopyPayload
-    image_[i] = new_image(images_[image_[i]].key_le, pay.data(), 0, 0);
+    image_[i] = new_image(key, len, pay.data(), 0, 0);
     touch(leaf, slot);
     return STAGE_RC_OK;
 }
 
 // CommitTransaction UPDATE entry (transaction_manager.cpp:610-676), single writer.
-int HostTable::commit_update(uint64_t key_le, uint32_t len, uint32_t commit_id, uint32_t sstamp) {
+int HostTable::commit_update(const uint8_t *key, uint32_t len, uint32_t commit_id, uint32_t sstamp) {
     uint32_t leaf, slot;
-    if (find(key_le, len, &leaf, &slot) < 0) return STAGE_RC_NOT_FOUND;
+    if (find(key, len, &leaf, &slot) < 0) return STAGE_RC_NOT_FOUND;
     const size_t i = (size_t)leaf * cap_ + slot;
     if (!meta_inserting(meta_[i]) || (next_[i] & kNextKindMask) != kNextCopy) return STAGE_RC_NOT_FOUND;
     const uint64_t ci = next_[i] & kNextIndexMask;
@@ -348,9 +405,9 @@ int HostTable::commit_update(uint64_t key_le, uint32_t len, uint32_t commit_id, 
 }
 
 // BTree::FinalizeUpdate (b_tree.cpp:2252-2268): cstamp := commit_id, next untouched.
-int HostTable::finalize_update(uint64_t key_le, uint32_t len, uint32_t commit_id) {
+int HostTable::finalize_update(const uint8_t *key, uint32_t len, uint32_t commit_id) {
     uint32_t leaf, slot;
-    if (find(key_le, len, &leaf, &slot) < 0) return STAGE_RC_NOT_FOUND;
+    if (find(key, len, &leaf, &slot) < 0) return STAGE_RC_NOT_FOUND;
     const size_t i = (size_t)leaf * cap_ + slot;
     meta_[i] = ((meta_[i] & ~kMetaTxn) | commit_id) & ~kMetaControl;
     touch(leaf, slot);
@@ -359,9 +416,9 @@ int HostTable::finalize_update(uint64_t key_le, uint32_t len, uint32_t commit_id
 
 // LeafNode::Delete (b_tree.cpp:1171-1251) + FinalizeDelete (b_tree.cpp:2275-2310).  Sibling
 // merges (BaseNode::CheckMerge) are not supported: such a delete reports RC_INVALID.
-int HostTable::remove(uint64_t key_le, uint32_t len, uint32_t commit_id) {
+int HostTable::remove(const uint8_t *key, uint32_t len, uint32_t commit_id) {
     uint32_t leaf, slot;
-    if (find(key_le, len, &leaf, &slot) < 0) return STAGE_RC_NOT_FOUND;
+    if (find(key, len, &leaf, &slot) < 0) return STAGE_RC_NOT_FOUND;
     const size_t i = (size_t)leaf * cap_ + slot;
     const uint64_t m = meta_[i];
     if (meta_inserting(m)) return STAGE_RC_DIRTY;
@@ -382,15 +439,16 @@ int HostTable::remove(uint64_t key_le, uint32_t len, uint32_t commit_id) {
     return STAGE_RC_OK;
 }
 
-uint64_t HostTable::update_batch(const uint64_t *keys, uint64_t n, uint32_t len, uint32_t payload_off,
-                                 const uint8_t *deltas, uint32_t delta_len, const uint32_t *writer_ids,
-                                 const uint32_t *commit_ids, const uint32_t *sstamps, uint8_t *rc_out) {
+uint64_t HostTable::update_batch(const uint8_t *keys, uint32_t key_stride, uint64_t n, uint32_t len,
+                                 uint32_t payload_off, const uint8_t *deltas, uint32_t delta_len,
+                                 const uint32_t *writer_ids, const uint32_t *commit_ids, const uint32_t *sstamps,
+                                 uint8_t *rc_out) {
     uint64_t ok = 0;
     for (uint64_t i = 0; i < n; ++i) {
-        int rc = update(keys[i], len, payload_off, deltas + i * (uint64_t)delta_len, delta_len, writer_ids[i]);
-        if (rc == STAGE_RC_OK && commit_ids && commit_ids[i]) {
-            rc = commit_update(keys[i], len, commit_ids[i], sstamps ? sstamps[i] : commit_ids[i]);
-        }
+        const uint8_t *k = keys + i * (uint64_t)key_stride;
+        int rc = update(k, len, payload_off, deltas + i * (uint64_t)delta_len, delta_len, writer_ids[i]);
+        if (rc == STAGE_RC_OK && commit_ids && commit_ids[i])
+            rc = commit_update(k, len, commit_ids[i], sstamps ? sstamps[i] : commit_ids[i]);
         if (rc == STAGE_RC_OK) ++ok;
         if (rc_out) rc_out[i] = (uint8_t)rc;
     }
@@ -421,6 +479,7 @@ void HostTable::stats(uint64_t *out) const {
     out[7] = versions_.size();
 }
 
+// keyw: the first 8 key bytes of each slot (the whole key for keys of <= 8 bytes)
 int64_t HostTable::export_leaves(uint32_t cap, uint64_t max_leaves, uint32_t *rc, uint32_t *sc, uint64_t *meta,
                                  uint64_t *keyw) const {
     std::vector<uint32_t> order;
@@ -433,8 +492,14 @@ int64_t HostTable::export_leaves(uint32_t cap, uint64_t max_leaves, uint32_t *rc
         for (uint32_t s = 0; s < cap; ++s) {
             uint64_t m = 0, kw = 0;
             if (s < L.count && s < cap_) {
-                m = meta_[(size_t)order[d] * cap_ + s];
-                if (m) kw = key_bytes_from_order(okey_[(size_t)order[d] * cap_ + s], meta_keylen(m));
+                const size_t i = (size_t)order[d] * cap_ + s;
+                m = meta_[i];
+                if (m) {
+                    uint8_t kb[kMaxKeyBytes] = {0};
+                    key_to_bytes(slot_key(i), kb, uns_);
+                    std::memcpy(&kw, kb, 8);
+                    if (meta_keylen(m) < 8) kw &= (1ull << (8 * meta_keylen(m))) - 1;
+                }
             }
             meta[d * cap + s] = m;
             keyw[d * cap + s] = kw;
@@ -450,7 +515,8 @@ int64_t HostTable::export_leaves(uint32_t cap, uint64_t max_leaves, uint32_t *rc
 // RecordMetadata{meta, next_ptr, loc_ptr} (record_meta.h:30-60) per slot, records
 // [key][pad to 8][payload] at meta.offset growing down from `size`.  Canonical form (the
 // oracle's orc_export_leaf_images uses the same): next_ptr / loc_ptr = 0, record bytes not
-// referenced by a non-zero meta word = 0.
+// referenced by a non-zero meta word = 0.  Separators: key_words() u64 words of key bytes
+// per leaf (little-endian), length 0xFFFF = +inf.
 static constexpr uint32_t kLeafHdr = 40, kOffIsLeaf = 8, kOffSize = 16, kOffSorted = 20, kOffStatus = 32;
 
 int64_t HostTable::export_leaf_images(uint64_t max_leaves, uint8_t *blocks, uint64_t *sep_key_le,
@@ -460,6 +526,7 @@ int64_t HostTable::export_leaf_images(uint64_t max_leaves, uint8_t *blocks, uint
     if (order.size() > max_leaves) return -(int64_t)order.size();
     const uint32_t B = p_.leaf_node_size;
     std::vector<uint8_t> pay(p_.payload_size);
+    uint8_t kb[kMaxKeyBytes];
     for (size_t d = 0; d < order.size(); ++d) {
         const Leaf &L = leaves_[order[d]];
         uint8_t *dst = blocks + d * (uint64_t)B;
@@ -475,13 +542,15 @@ int64_t HostTable::export_leaf_images(uint64_t max_leaves, uint8_t *blocks, uint
             std::memcpy(dst + kLeafHdr + 24 * s, &m, 8);
             if (!m) continue;
             const uint32_t off = meta_offset(m), kl = meta_keylen(m);
-            const uint64_t kw = key_bytes_from_order(okey_[b + s], kl);
-            std::memcpy(dst + off, &kw, kl);
+            key_to_bytes(slot_key(b + s), kb, uns_);
+            std::memcpy(dst + off, kb, kl);
             image_payload(image_[b + s], pay.data());
             std::memcpy(dst + off + pad8(kl), pay.data(), p_.payload_size);
         }
         if (sep_key_le) {
-            sep_key_le[d] = key_is_inf(L.sep) ? 0 : key_bytes_from_order(L.sep.okey, L.sep.len);
+            uint64_t *sw = sep_key_le + d * kw_;
+            for (uint32_t w = 0; w < kw_; ++w) sw[w] = 0;
+            if (!key_is_inf(L.sep)) key_to_bytes(L.sep, reinterpret_cast<uint8_t *>(sw), uns_);
             sep_len[d] = key_is_inf(L.sep) ? (uint16_t)kInfLen : (uint16_t)L.sep.len;
         }
     }
@@ -511,7 +580,7 @@ uint64_t HostTable::import_leaf_images(const uint8_t *blocks, uint64_t n, uint32
         if (size != block_size) bad("block " + std::to_string(i) + ": header size != block size");
         if ((status >> 60) & 1) bad("block " + std::to_string(i) + " is frozen (mid-split)");
         if (count > cap_ || count > max_records_ || sorted > count) bad("block " + std::to_string(i) + ": bad counts");
-        Key mx{0, 0}, mn{0, 0};
+        Key mx = key_zero(), mn = key_zero();
         bool any = false;
         for (uint32_t s = 0; s < count; ++s) {
             uint64_t m;
@@ -519,14 +588,11 @@ uint64_t HostTable::import_leaf_images(const uint8_t *blocks, uint64_t n, uint32
             if (!m) continue;
             if (m & kMetaControl) bad("block " + std::to_string(i) + ": in-flight record (control bit)");
             const uint32_t kl = meta_keylen(m), off = meta_offset(m);
-            if (kl == 0 || kl > 8) bad("block " + std::to_string(i) + ": key length outside 1..8");
-            if (p_.key_width && kl != p_.key_width) bad("block " + std::to_string(i) + ": key width");
+            if (!key_ok(kl)) bad("block " + std::to_string(i) + ": key length not valid for this table");
             if (off < kLeafHdr + 24 * count || (uint64_t)off + pad8(kl) + p_.payload_size > size)
                 bad("block " + std::to_string(i) + ": record offset out of range");
             if (!meta_visible(m)) continue;
-            uint64_t kw = 0;
-            std::memcpy(&kw, blk + off, kl);
-            const Key k{order_key(kw, kl), kl};
+            const Key k = make_key(blk + off, kl, uns_);
             if (!any || key_lt(mx, k)) mx = k;
             if (!any || key_lt(k, mn)) mn = k;
             any = true;
@@ -534,8 +600,8 @@ uint64_t HostTable::import_leaf_images(const uint8_t *blocks, uint64_t n, uint32
         }
         if (i + 1 < n) {
             if (sep_key_le) {
-                if (sep_len[i] == 0 || sep_len[i] > 8) bad("separator " + std::to_string(i) + ": length");
-                sep[i] = Key{order_key(sep_key_le[i], sep_len[i]), sep_len[i]};
+                if (!key_ok(sep_len[i])) bad("separator " + std::to_string(i) + ": length");
+                sep[i] = make_key(reinterpret_cast<const uint8_t *>(sep_key_le + i * kw_), sep_len[i], uns_);
             } else {
                 if (!any) bad("block " + std::to_string(i) + ": empty leaf needs an explicit separator");
                 sep[i] = mx;
@@ -570,24 +636,22 @@ uint64_t HostTable::import_leaf_images(const uint8_t *blocks, uint64_t n, uint32
             meta_[b + s] = m;
             next_[b + s] = 0;
             if (!m) {
-                okey_[b + s] = 0;
+                clear_slot_key(b + s);
                 image_[b + s] = 0;
                 continue;
             }
             const uint32_t kl = meta_keylen(m), off = meta_offset(m);
-            uint64_t kw = 0;
-            std::memcpy(&kw, blk + off, kl);
-            okey_[b + s] = order_key(kw, kl);
-            image_[b + s] = new_image(kw, blk + off + pad8(kl), 0, 0);
+            set_slot_key(b + s, make_key(blk + off, kl, uns_));
+            image_[b + s] = new_image(blk + off, kl, blk + off + pad8(kl), 0, 0);
         }
     }
     // router: every bucket lists, in key order, each leaf whose range (sep[i-1], sep[i]] meets it
     for (auto &v : buckets_) v.clear();
     for (uint64_t i = 0; i < n; ++i) {
         const uint32_t id = (uint32_t)(head_ + i);
-        const uint32_t b_lo = i == 0 ? 0 : bucket_of(sep[i - 1].okey);
-        const uint32_t b_hi = key_is_inf(sep[i]) ? (uint32_t)buckets_.size() - 1 : bucket_of(sep[i].okey);
-        for (uint32_t bk = b_lo; bk <= b_hi; ++bk) buckets_[bk].push_back(RouteEntry{sep[i].okey, id, sep[i].len});
+        const uint32_t b_lo = i == 0 ? 0 : bucket_of(sep[i - 1]);
+        const uint32_t b_hi = key_is_inf(sep[i]) ? (uint32_t)buckets_.size() - 1 : bucket_of(sep[i]);
+        for (uint32_t bk = b_lo; bk <= b_hi; ++bk) buckets_[bk].push_back(RouteEntry{sep[i], id});
     }
     layout_dirty_ = true;
     structure_dirty_ = true;

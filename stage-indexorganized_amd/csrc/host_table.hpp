@@ -6,6 +6,11 @@
 // payloads live in the device record heap and are produced there from their sources.
 // Inner-node traversal is replaced on the host by a bucketed separator router (same leaf for
 // every key as BTree::TraverseToLeaf) and on the device by an implicit separator tree.
+//
+// Keys: 1..8 bytes (fixed width or variable, YCSB / BTreeTest) or a fixed width of 9..32
+// bytes (TPC-C composite keys of int64 fields, tpcc_record.h).  A key is held as up to four
+// order words (stage_core.hpp order_key per 8-byte chunk) plus its length; the unsigned order
+// of (words, len) is the reference's KeyCompare order.
 #pragma once
 #include <cstdint>
 #include <string>
@@ -17,21 +22,39 @@
 namespace stage {
 
 struct Key {
-    uint64_t okey;
+    uint64_t w[kMaxKeyWords];
     uint32_t len;
 };
-inline bool key_lt(const Key &a, const Key &b) { return a.okey < b.okey || (a.okey == b.okey && a.len < b.len); }
-inline bool key_eq(const Key &a, const Key &b) { return a.okey == b.okey && a.len == b.len; }
+inline bool key_lt(const Key &a, const Key &b) {
+    for (int i = 0; i < kMaxKeyWords; ++i)
+        if (a.w[i] != b.w[i]) return a.w[i] < b.w[i];
+    return a.len < b.len;
+}
+inline bool key_eq(const Key &a, const Key &b) {
+    for (int i = 0; i < kMaxKeyWords; ++i)
+        if (a.w[i] != b.w[i]) return false;
+    return a.len == b.len;
+}
 inline bool key_le(const Key &a, const Key &b) { return !key_lt(b, a); }
 constexpr uint32_t kInfLen = 0xFFFF;
-inline Key key_inf() { return Key{~0ull, kInfLen}; }
+inline Key key_inf() {
+    Key k;
+    for (int i = 0; i < kMaxKeyWords; ++i) k.w[i] = ~0ull;
+    k.len = kInfLen;
+    return k;
+}
+inline Key key_zero() { return Key{{0, 0, 0, 0}, 0}; }
 inline bool key_is_inf(const Key &k) { return k.len == kInfLen; }
+// key bytes (len <= 32) -> order words; uns: unsigned byte order (tables of 16..32-byte keys)
+Key make_key(const uint8_t *bytes, uint32_t len, bool uns);
+// order words -> key bytes (len bytes written)
+void key_to_bytes(const Key &k, uint8_t *out, bool uns);
 
 // Source of one record-heap image: generated from a rowid, or explicit bytes in the arena.
 struct ImageDesc {
-    uint64_t key_le;  // key bytes (little-endian, zero above key_len)
+    uint64_t key_le;  // key bytes (little-endian, zero above key_len) -- keys of <= 8 bytes
     uint64_t arg;     // rowid (generated) or arena byte offset (explicit)
-    uint32_t kind;    // 0 = generated, 1 = arena
+    uint32_t kind;    // 0 = generated, 1 = arena payload (key in key_le), 2 = arena row [key pad][payload]
     uint32_t mode;    // payload generator mode (generated images)
 };
 
@@ -43,31 +66,68 @@ public:
     uint32_t cap() const { return cap_; }
     uint32_t stride() const { return stride_; }
     uint32_t hstride() const { return stride_; }
+    uint32_t key_words() const { return kw_; }      // order words stored per slot
+    uint32_t key_pad() const { return kpad_; }      // bytes of the key part of a row
+    bool key_unsigned() const { return uns_; }        // KeyCompare's memcmp branch (>= 16 bytes)
+    Key key_of(const uint8_t *bytes, uint32_t len) const { return make_key(bytes, len, uns_); }
 
-    // write path, reference ReturnCode values
-    int insert(uint64_t key_le, uint32_t len, const uint8_t *payload, uint64_t gen_rowid, int mode,
+    // write path, reference ReturnCode values; keys as bytes (len <= 32)
+    int insert(const uint8_t *key, uint32_t len, const uint8_t *payload, uint64_t gen_rowid, int mode,
                uint32_t commit_id);
+    int update(const uint8_t *key, uint32_t len, uint32_t payload_off, const uint8_t *delta, uint32_t delta_len,
+               uint32_t writer_id);
+    int commit_update(const uint8_t *key, uint32_t len, uint32_t commit_id, uint32_t sstamp);
+    int finalize_update(const uint8_t *key, uint32_t len, uint32_t commit_id);
+    int remove(const uint8_t *key, uint32_t len, uint32_t commit_id);
+    // the same for keys of <= 8 bytes passed little-endian in a u64
+    int insert(uint64_t key_le, uint32_t len, const uint8_t *payload, uint64_t gen_rowid, int mode,
+               uint32_t commit_id) {
+        return len > 8 ? STAGE_RC_INVALID : insert(le(key_le), len, payload, gen_rowid, mode, commit_id);
+    }
+    int update(uint64_t key_le, uint32_t len, uint32_t payload_off, const uint8_t *delta, uint32_t delta_len,
+               uint32_t writer_id) {
+        return len > 8 ? STAGE_RC_NOT_FOUND : update(le(key_le), len, payload_off, delta, delta_len, writer_id);
+    }
+    int commit_update(uint64_t key_le, uint32_t len, uint32_t commit_id, uint32_t sstamp) {
+        return len > 8 ? STAGE_RC_NOT_FOUND : commit_update(le(key_le), len, commit_id, sstamp);
+    }
+    int finalize_update(uint64_t key_le, uint32_t len, uint32_t commit_id) {
+        return len > 8 ? STAGE_RC_NOT_FOUND : finalize_update(le(key_le), len, commit_id);
+    }
+    int remove(uint64_t key_le, uint32_t len, uint32_t commit_id) {
+        return len > 8 ? STAGE_RC_NOT_FOUND : remove(le(key_le), len, commit_id);
+    }
+
     uint64_t load_ycsb(uint64_t begin, uint64_t end, uint32_t key_size, int mode);
     uint64_t load_keys(const uint64_t *keys, uint64_t n, uint32_t key_size, int mode);
-    int update(uint64_t key_le, uint32_t len, uint32_t payload_off, const uint8_t *delta, uint32_t delta_len,
-               uint32_t writer_id);
-    int commit_update(uint64_t key_le, uint32_t len, uint32_t commit_id, uint32_t sstamp);
-    int finalize_update(uint64_t key_le, uint32_t len, uint32_t commit_id);
-    int remove(uint64_t key_le, uint32_t len, uint32_t commit_id);
+    // explicit rows: key i = keys + i*key_stride (key_size bytes), payload i = payloads + i*payload_stride
+    uint64_t load_rows(const uint8_t *keys, uint32_t key_stride, uint32_t key_size, const uint8_t *payloads,
+                       uint32_t payload_stride, uint64_t n, uint32_t commit_id, uint8_t *rc_out);
 
     // host traversal (TraverseToLeaf equivalent) -> host leaf id
     uint32_t route(const Key &k, bool le_child) const;
+    // key -> (leaf, slot) of its first visible record; -1 if absent
+    int find(const uint8_t *key, uint32_t len, uint32_t *leaf, uint32_t *slot) const;
 
     void stats(uint64_t *out) const;
     // leaves in key order
     void key_order(std::vector<uint32_t> &order) const;
     int64_t export_leaves(uint32_t cap, uint64_t max_leaves, uint32_t *rc, uint32_t *sc, uint64_t *meta,
                           uint64_t *keyw) const;
-
     // leaf-level snapshot in the reference's 64 KiB block format (see host_table.cpp)
     int64_t export_leaf_images(uint64_t max_leaves, uint8_t *blocks, uint64_t *sep_key_le, uint16_t *sep_len) const;
     uint64_t import_leaf_images(const uint8_t *blocks, uint64_t n, uint32_t block_size, const uint64_t *sep_key_le,
                                 const uint16_t *sep_len);
+
+    // slot key (order words) of host slot index i = leaf*cap + slot
+    Key slot_key(size_t i) const {
+        Key k = key_zero();
+        for (uint32_t w = 0; w < kw_; ++w) k.w[w] = okey_[i * kw_ + w];
+        k.len = meta_keylen(meta_[i]);
+        return k;
+    }
+    // record-heap image payload bytes
+    void image_payload(uint32_t img, uint8_t *dst) const;
 
     // storage (read by the device-image builder)
     struct Leaf {
@@ -77,8 +137,8 @@ public:
         bool live = false;
     };
     std::vector<Leaf> leaves_;
-    std::vector<uint64_t> okey_;   // [leaf*cap + slot]
-    std::vector<uint64_t> meta_;
+    std::vector<uint64_t> okey_;   // [(leaf*cap + slot)*kw + word]
+    std::vector<uint64_t> meta_;   // [leaf*cap + slot]
     std::vector<uint32_t> next_;
     std::vector<uint32_t> image_;
     int32_t head_ = 0;
@@ -97,21 +157,20 @@ public:
     uint64_t copies_synced_ = 0, versions_synced_ = 0;  // headers already on the device
     uint64_t copies_dirty_from_ = ~0ull;                 // lowest synced copy header rewritten since
 
-    // batched write path (one call per YCSB-B epoch): update + optional commit per key
-    uint64_t update_batch(const uint64_t *keys, uint64_t n, uint32_t len, uint32_t payload_off, const uint8_t *deltas,
-                          uint32_t delta_len, const uint32_t *writer_ids, const uint32_t *commit_ids,
-                          const uint32_t *sstamps, uint8_t *rc_out);
+    // batched write path (one call per YCSB-B epoch): update + optional commit per key;
+    // keys: key_stride bytes apart (8 for u64 keys of <= 8 bytes)
+    uint64_t update_batch(const uint8_t *keys, uint32_t key_stride, uint64_t n, uint32_t len, uint32_t payload_off,
+                          const uint8_t *deltas, uint32_t delta_len, const uint32_t *writer_ids,
+                          const uint32_t *commit_ids, const uint32_t *sstamps, uint8_t *rc_out);
 
 private:
     struct RouteEntry {
-        uint64_t sep_okey;
+        Key sep;
         uint32_t leaf;
-        uint32_t sep_len;
     };
-    static uint32_t bucket_of(uint64_t okey) { return (uint32_t)(okey >> 48); }
-    static bool entry_lt_key(const RouteEntry &e, const Key &k) {
-        return e.sep_okey < k.okey || (e.sep_okey == k.okey && e.sep_len < k.len);
-    }
+    static uint32_t bucket_of(const Key &k) { return (uint32_t)(k.w[0] >> 48); }
+    static bool entry_lt_key(const RouteEntry &e, const Key &k) { return key_lt(e.sep, k); }
+    static const uint8_t *le(const uint64_t &key_le) { return reinterpret_cast<const uint8_t *>(&key_le); }
 
     void touch(uint32_t leaf, uint32_t slot) {
         layout_dirty_ = true;
@@ -122,12 +181,20 @@ private:
     uint32_t used_space(const Leaf &l) const { return 40u + l.block + l.count * 24u; }
     bool split(uint32_t leaf);
     void route_split(uint32_t p, uint32_t r, const Key &lo, const Key &s, const Key &hi);
-    uint32_t new_image(uint64_t key_le, const uint8_t *payload, uint64_t gen_rowid, int mode);
-    void image_payload(uint32_t img, uint8_t *dst) const;
-    int find(uint64_t key_le, uint32_t len, uint32_t *leaf, uint32_t *slot) const;
+    uint32_t new_image(const uint8_t *key, uint32_t len, const uint8_t *payload, uint64_t gen_rowid, int mode);
+    bool key_ok(uint32_t len) const;
+    void set_slot_key(size_t i, const Key &k) {
+        for (uint32_t w = 0; w < kw_; ++w) okey_[i * kw_ + w] = k.w[w];
+    }
+    void clear_slot_key(size_t i) {
+        for (uint32_t w = 0; w < kw_; ++w) okey_[i * kw_ + w] = 0;
+    }
 
     stage_params p_;
     uint32_t cap_ = 64;
+    uint32_t kw_ = 1;      // order words per slot
+    uint32_t kpad_ = 8;    // key bytes in a row (padded to 8)
+    bool uns_ = false;     // unsigned byte order
     uint32_t stride_ = 1008;
     uint32_t max_records_ = 63;
     std::vector<std::vector<RouteEntry>> buckets_;

@@ -41,11 +41,11 @@ hipError_t launch_scan(const DevTable &t, const uint64_t *keys, const uint16_t *
                        uint32_t *counts, uint8_t *recs, hipStream_t s, const ScanTuning &tune);
 hipError_t launch_murmur(const void *keys, uint32_t key_len, uint32_t key_stride, uint64_t seed, uint64_t n,
                          uint64_t *out, hipStream_t s);
-hipError_t launch_fill(uint8_t *heap, uint32_t stride, uint32_t payload_size, const ImageDescDev *descs,
-                       const uint8_t *arena, uint64_t first, uint64_t count, uint64_t ident_rowid0,
-                       uint32_t ident_key_width, int ident_mode, hipStream_t s);
-hipError_t launch_patch(uint8_t *head, uint64_t *okey, SlotInfo *slot, uint32_t head_bytes, const uint32_t *head_leaf,
-                        const void *head_src, uint64_t nhead, const uint64_t *slot_idx, const SlotInfo *slot_src,
-                        uint64_t nslot, hipStream_t s);
+hipError_t launch_fill(uint8_t *heap, uint32_t stride, uint32_t payload_size, uint32_t row_bytes,
+                       const ImageDescDev *descs, const uint8_t *arena, uint64_t first, uint64_t count,
+                       uint64_t ident_rowid0, uint32_t ident_key_width, int ident_mode, hipStream_t s);
+hipError_t launch_patch(uint8_t *head, uint64_t *okey, SlotInfo *slot, uint32_t head_bytes, uint32_t cap, uint32_t kw,
+                        const uint32_t *head_leaf, const void *head_src, uint64_t nhead, const uint64_t *slot_idx,
+                        const SlotInfo *slot_src, const uint64_t *words, uint64_t nslot, hipStream_t s);
 
 }  // namespace stage

@@ -43,35 +43,57 @@ __device__ __forceinline__ uint64_t head_vis(const DevTable &t, uint32_t leaf, i
     return *reinterpret_cast<const uint64_t *>(t.head + (uint64_t)leaf * t.head_bytes + t.cap + 8 * s);
 }
 
+// multi-word order keys (fixed-width keys of 9..32 bytes): lexicographic word order
+template <int KW>
+__device__ __forceinline__ bool kw_lt(const uint64_t *a, const uint64_t *b) {
+#pragma unroll
+    for (int j = 0; j < KW; ++j)
+        if (a[j] != b[j]) return a[j] < b[j];
+    return false;
+}
+
 // lower_bound over the separators: number of separators < x, i.e. the leaf whose range
 // (sep[i-1], sep[i]] holds x (le_child semantics).  Upper-bound callers pass succ(x).
-template <bool VARLEN>
-__device__ __forceinline__ uint32_t tree_lower_bound(const DevTable &t, uint64_t x, uint32_t xl) {
+// KW = 1: a node is 16 x 8 B = one 128-B line (8 x 16-B loads per lane); KW > 1: 16 entries
+// of KW words each, compared lexicographically.
+template <bool VARLEN, int KW>
+__device__ __forceinline__ uint32_t tree_lower_bound(const DevTable &t, const uint64_t *x, uint32_t xl) {
     static_assert(kTreeFanout == 16, "node = 8 x 16-B loads");
     uint32_t node = 0;
     for (int lvl = (int)t.levels - 1; lvl >= 0; --lvl) {
         const uint64_t off = t.level_off[lvl] + (uint64_t)node * kTreeFanout;
-        const u32x4 *e = reinterpret_cast<const u32x4 *>(t.tree + off);
-        u32x4 q[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) q[k] = e[k];
         uint32_t cnt = 0;
-        if (VARLEN) {
-            const uint64_t *lp = reinterpret_cast<const uint64_t *>(t.tree_len + off);
-            const uint64_t lw0 = lp[0], lw1 = lp[1];
+        if (KW > 1) {
+            const uint64_t *e = t.tree + off * KW;
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const uint64_t lw = k < 4 ? lw0 : lw1;
-                const int sh = 16 * (k & 3);
-                const uint64_t v0 = ((uint64_t)q[k].y << 32) | q[k].x, v1 = ((uint64_t)q[k].w << 32) | q[k].z;
-                cnt += kv_lt(v0, (uint32_t)((lw >> sh) & 0xFF), x, xl) ? 1u : 0u;
-                cnt += kv_lt(v1, (uint32_t)((lw >> (sh + 8)) & 0xFF), x, xl) ? 1u : 0u;
+            for (int k = 0; k < kTreeFanout; ++k) {
+                uint64_t w[KW];
+#pragma unroll
+                for (int j = 0; j < KW; ++j) w[j] = e[k * KW + j];
+                cnt += kw_lt<KW>(w, x) ? 1u : 0u;
             }
         } else {
+            const u32x4 *e = reinterpret_cast<const u32x4 *>(t.tree + off);
+            u32x4 q[8];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                cnt += ((((uint64_t)q[k].y << 32) | q[k].x) < x) ? 1u : 0u;
-                cnt += ((((uint64_t)q[k].w << 32) | q[k].z) < x) ? 1u : 0u;
+            for (int k = 0; k < 8; ++k) q[k] = e[k];
+            if (VARLEN) {
+                const uint64_t *lp = reinterpret_cast<const uint64_t *>(t.tree_len + off);
+                const uint64_t lw0 = lp[0], lw1 = lp[1];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const uint64_t lw = k < 4 ? lw0 : lw1;
+                    const int sh = 16 * (k & 3);
+                    const uint64_t v0 = ((uint64_t)q[k].y << 32) | q[k].x, v1 = ((uint64_t)q[k].w << 32) | q[k].z;
+                    cnt += kv_lt(v0, (uint32_t)((lw >> sh) & 0xFF), x[0], xl) ? 1u : 0u;
+                    cnt += kv_lt(v1, (uint32_t)((lw >> (sh + 8)) & 0xFF), x[0], xl) ? 1u : 0u;
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    cnt += ((((uint64_t)q[k].y << 32) | q[k].x) < x[0]) ? 1u : 0u;
+                    cnt += ((((uint64_t)q[k].w << 32) | q[k].z) < x[0]) ? 1u : 0u;
+                }
             }
         }
         node = node * kTreeFanout + cnt;
@@ -79,23 +101,43 @@ __device__ __forceinline__ uint32_t tree_lower_bound(const DevTable &t, uint64_t
     return node < t.nseps ? node : t.nseps;
 }
 
-template <bool VARLEN>
-__device__ __forceinline__ uint32_t resolve_leaf(const DevTable &t, uint64_t okey, uint32_t len, bool le_child) {
-    if (le_child) return tree_lower_bound<VARLEN>(t, okey, len);
-    if (VARLEN) return tree_lower_bound<VARLEN>(t, okey, len + 1);  // (okey, len+1) = succ
-    if (okey == ~0ull) return t.nseps;
-    return tree_lower_bound<VARLEN>(t, okey + 1, len);
+template <bool VARLEN, int KW>
+__device__ __forceinline__ uint32_t resolve_leaf(const DevTable &t, const uint64_t *okey, uint32_t len, bool le_child) {
+    if (le_child) return tree_lower_bound<VARLEN, KW>(t, okey, len);
+    if (VARLEN) return tree_lower_bound<VARLEN, KW>(t, okey, len + 1);  // (okey, len+1) = succ
+    // fixed width: succ = the key plus one in its last word, with carry
+    uint64_t s[KW];
+    bool carry = true;
+#pragma unroll
+    for (int j = KW - 1; j >= 0; --j) {
+        s[j] = okey[j] + (carry ? 1ull : 0ull);
+        carry = carry && okey[j] == ~0ull;
+    }
+    if (carry) return t.nseps;
+    return tree_lower_bound<VARLEN, KW>(t, s, len);
 }
 
+// order words of a key passed as KW little-endian u64 words (fixed width) or one word
+template <int KW>
+__device__ __forceinline__ void load_okey(const uint64_t *keys, uint64_t i, bool valid, uint32_t len, uint64_t *okw) {
+#pragma unroll
+    for (int j = 0; j < KW; ++j) {
+        const uint64_t le = valid ? keys[i * KW + j] : 0ull;
+        okw[j] = KW == 1 ? order_key(le, len) : order_word(le, len, (uint32_t)j, key_order_unsigned(len));
+    }
+}
+
+template <int KW>
 __global__ __launch_bounds__(256) void resolve_kernel(DevTable t, const uint64_t *__restrict__ keys,
                                                       const uint16_t *__restrict__ lens, uint64_t n, int le_child,
                                                       uint32_t *__restrict__ out) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint32_t len = t.key_width ? t.key_width : (lens ? lens[i] : 8u);
-    uint64_t ok = order_key(keys[i], len);
-    out[i] = t.key_width ? resolve_leaf<false>(t, ok, len, le_child != 0)
-                         : resolve_leaf<true>(t, ok, len, le_child != 0);
+    uint64_t ok[KW];
+    load_okey<KW>(keys, i, true, len, ok);
+    out[i] = t.key_width ? resolve_leaf<false, KW>(t, ok, len, le_child != 0)
+                         : resolve_leaf<true, 1>(t, ok, len, le_child != 0);
 }
 
 // ----------------------------------------------------------------------------------------
@@ -193,7 +235,7 @@ __device__ __forceinline__ void st16(T v, T *p) {
     else *p = v;
 }
 
-template <bool VARLEN, int SPL, int G, bool NT = true>
+template <bool VARLEN, int SPL, int G, bool NT = true, int KW = 1>
 __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *__restrict__ keys,
                                                     const uint16_t *__restrict__ lens,
                                                     const uint32_t *__restrict__ rids,
@@ -208,17 +250,17 @@ __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *
         const uint64_t i = base + lane;
         const bool valid = i < n;
         u32x4 my_a = u32x4{0, 0, 0, 0}, my_b = u32x4{0, 0, 0, 0};  // this lane's probe result
-        const uint64_t kle = valid ? keys[i] : 0;
         const uint32_t len = t.key_width ? t.key_width : (lens && valid ? (uint32_t)lens[i] : 8u);
         const uint32_t rid = rids ? (valid ? rids[i] : 0u) : 0xFFFFFFFEu;
-        const uint64_t ok = order_key(kle, len);
+        uint64_t ok[KW];
+        load_okey<KW>(keys, i, valid, len, ok);
         uint32_t leaf = 0;
-        if (valid) leaf = leaf_in ? leaf_in[i] : resolve_leaf<VARLEN>(t, ok, len, true);
+        if (valid) leaf = leaf_in ? leaf_in[i] : resolve_leaf<VARLEN, KW>(t, ok, len, true);
         if (leaf > t.nseps) leaf = t.nseps;  // host-supplied ids are clamped to the table
         const int cnt = (int)((n - base) < 64 ? (n - base) : 64);
         for (int j0 = 0; j0 < cnt; j0 += G) {
             uint32_t lf[G], rd[G], xl[G];
-            uint64_t x[G];
+            uint64_t x[G][KW];
             uint32_t fpb[G][SPL];
             uint64_t vm[G][SPL];
             // phase 1: leaf heads (fingerprints + visible masks) of G probes
@@ -227,7 +269,8 @@ __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *
                 const int j = j0 + g < cnt ? j0 + g : cnt - 1;
                 lf[g] = rl32(leaf, j);
                 rd[g] = rl32(rid, j);
-                x[g] = rl64(ok, j);
+#pragma unroll
+                for (int w = 0; w < KW; ++w) x[g][w] = rl64(ok[w], j);
                 xl[g] = VARLEN ? rl32(len, j) : t.key_width;
                 const uint8_t *h = t.head + (uint64_t)lf[g] * t.head_bytes;
 #pragma unroll
@@ -242,7 +285,7 @@ __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *
             bool cand[G][SPL];
 #pragma unroll
             for (int g = 0; g < G; ++g) {
-                const uint32_t fx = key_fp(x[g]);
+                const uint32_t fx = key_fp_words(x[g], KW);
 #pragma unroll
                 for (int s = 0; s < SPL; ++s) {
                     cand[g][s] = ((vm[g][s] >> lane) & 1) && fpb[g][s] == fx;
@@ -257,6 +300,13 @@ __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *
                         wmeta[g][s] = ((uint64_t)w0.w << 32) | w0.z;
                         wnext[g][s] = w1.x;
                         wimg[g][s] = w1.y;
+                        if (KW > 1 && wok[g][s] == x[g][0]) {  // confirm the other key words
+                            bool eq = true;
+#pragma unroll
+                            for (int w = 1; w < KW; ++w)
+                                eq = eq && t.okey[((uint64_t)lf[g] * KW + w) * t.cap + s * 64 + lane] == x[g][w];
+                            if (!eq) wok[g][s] = ~x[g][0];
+                        }
                     }
                 }
             }
@@ -269,7 +319,7 @@ __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *
                 uint32_t nx = 0, im = 0;
 #pragma unroll
                 for (int s = SPL - 1; s >= 0; --s) {
-                    const bool hitl = cand[g][s] && wok[g][s] == x[g] && (!VARLEN || meta_keylen(wmeta[g][s]) == xl[g]);
+                    const bool hitl = cand[g][s] && wok[g][s] == x[g][0] && (!VARLEN || meta_keylen(wmeta[g][s]) == xl[g]);
                     const uint64_t hit = ballot(hitl);
                     if (hit) {
                         const int b = __builtin_ctzll(hit);
@@ -355,18 +405,29 @@ __device__ __forceinline__ void copy_rows(const DevTable &t, const uint32_t *img
     }
 }
 
-template <bool VARLEN, int SPL, int R>
-__device__ void scan_one(const DevTable &t, uint64_t x, uint32_t xl, uint32_t leaf, uint32_t scan_size,
+template <bool VARLEN, int KW>
+__device__ __forceinline__ bool key_less(const uint64_t *a, uint32_t al, const uint64_t *b, uint32_t bl) {
+    if (KW == 1) return kv_lt(a[0], al, b[0], bl);
+    return kw_lt<KW>(a, b);  // fixed width: equal lengths
+}
+
+template <bool VARLEN, int SPL, int R, int KW>
+__device__ void scan_one(const DevTable &t, const uint64_t *x0, uint32_t xl, uint32_t leaf, uint32_t scan_size,
                          uint8_t *recs, uint32_t *count_out, uint32_t lane) {
     uint32_t remaining = scan_size, produced = 0;
     bool cont = false;
+    uint64_t x[KW];
+#pragma unroll
+    for (int w = 0; w < KW; ++w) x[w] = x0[w];
     for (uint32_t guard = 0; guard < scan_size + 2 && remaining > 0; ++guard) {
         const uint64_t base = (uint64_t)leaf * t.cap;
-        uint64_t col[SPL];
+        uint64_t col[SPL][KW];
         uint32_t kl[SPL];
         uint64_t q[SPL];
 #pragma unroll
-        for (int s = 0; s < SPL; ++s) col[s] = t.okey[base + s * 64 + lane];
+        for (int s = 0; s < SPL; ++s)
+#pragma unroll
+            for (int w = 0; w < KW; ++w) col[s][w] = t.okey[((uint64_t)leaf * KW + w) * t.cap + s * 64 + lane];
 #pragma unroll
         for (int s = 0; s < SPL; ++s) {
             const uint64_t vm = head_vis(t, leaf, s);
@@ -374,7 +435,7 @@ __device__ void scan_one(const DevTable &t, uint64_t x, uint32_t xl, uint32_t le
             kl[s] = t.key_width;
             if (VARLEN) kl[s] = vis ? meta_keylen(t.slot[base + s * 64 + lane].meta) : 0u;
             // RangeScanBySize keeps visible records with KeyCompare(start, key) <= 0
-            q[s] = ballot(vis && !kv_lt(col[s], kl[s], x, xl));
+            q[s] = ballot(vis && !key_less<VARLEN, KW>(col[s], kl[s], x, xl));
         }
         // slot-order truncation: records are collected until more than to_scan are held
         const uint32_t to_scan = remaining;
@@ -403,21 +464,28 @@ __device__ void scan_one(const DevTable &t, uint64_t x, uint32_t xl, uint32_t le
             while (mm) {
                 const int b = __builtin_ctzll(mm);
                 mm &= mm - 1;
-                const uint64_t ko = rl64(col[s2], b);
+                uint64_t ko[KW];
+#pragma unroll
+                for (int w = 0; w < KW; ++w) ko[w] = rl64(col[s2][w], b);
                 const uint32_t kll = rl32(kl[s2], b);
 #pragma unroll
-                for (int s = 0; s < SPL; ++s) kr[s] += kv_lt(ko, kll, col[s], kl[s]) ? 1u : 0u;
+                for (int s = 0; s < SPL; ++s) kr[s] += key_less<VARLEN, KW>(ko, kll, col[s], kl[s]) ? 1u : 0u;
             }
         }
         // continuation: if the new batch starts with the last key, the iterator stops
         if (cont) {
             bool dup = false;
 #pragma unroll
-            for (int s = 0; s < SPL; ++s) dup |= keep[s] && kr[s] == 0 && col[s] == x && kl[s] == xl;
+            for (int s = 0; s < SPL; ++s) {
+                bool eq = kl[s] == xl;
+#pragma unroll
+                for (int w = 0; w < KW; ++w) eq = eq && col[s][w] == x[w];
+                dup |= keep[s] && kr[s] == 0 && eq;
+            }
             if (ballot(dup)) break;
         }
         const uint32_t e = m < remaining ? m : remaining;
-        // emit the e smallest kept records at produced + rank, four rows in flight
+        // emit the e smallest kept records at produced + rank, R rows in flight
 #pragma unroll
         for (int s = 0; s < SPL; ++s) {
             const bool emit = keep[s] && kr[s] < e;
@@ -440,20 +508,19 @@ __device__ void scan_one(const DevTable &t, uint64_t x, uint32_t xl, uint32_t le
         remaining -= e;
         if (e < m) break;
         // last record popped: re-traverse from its key with le_child = false
-        uint64_t lastk = 0;
         uint32_t lastl = 0;
 #pragma unroll
         for (int s = 0; s < SPL; ++s) {
             const uint64_t lm = ballot(keep[s] && kr[s] == m - 1);
             if (lm) {
                 const int b = __builtin_ctzll(lm);
-                lastk = rl64(col[s], b);
+#pragma unroll
+                for (int w = 0; w < KW; ++w) x[w] = rl64(col[s][w], b);
                 lastl = rl32(kl[s], b);
             }
         }
-        x = lastk;
         xl = lastl;
-        leaf = uni32(resolve_leaf<VARLEN>(t, x, xl, false));
+        leaf = uni32(resolve_leaf<VARLEN, KW>(t, x, xl, false));
         cont = true;
     }
     if (lane == 0) *count_out = produced;
@@ -461,7 +528,7 @@ __device__ void scan_one(const DevTable &t, uint64_t x, uint32_t xl, uint32_t le
 
 // One wave per scan (grid-stride over scans): the start key's descent is wave-uniform, and a
 // wide grid keeps many scans -- and their R rows in flight each -- resident per CU.
-template <bool VARLEN, int SPL, int R>
+template <bool VARLEN, int SPL, int R, int KW = 1>
 __global__ __launch_bounds__(256) void scan_kernel(DevTable t, const uint64_t *__restrict__ keys,
                                                    const uint16_t *__restrict__ lens, uint64_t n, uint32_t scan_size,
                                                    uint32_t *__restrict__ counts, uint8_t *__restrict__ recs) {
@@ -470,10 +537,11 @@ __global__ __launch_bounds__(256) void scan_kernel(DevTable t, const uint64_t *_
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     for (uint64_t i = wave; i < n; i += nwaves) {
         const uint32_t len = t.key_width ? t.key_width : (lens ? (uint32_t)lens[i] : 8u);
-        const uint64_t ok = order_key(keys[i], len);
-        const uint32_t leaf = uni32(resolve_leaf<VARLEN>(t, ok, len, true));
-        scan_one<VARLEN, SPL, R>(t, ok, len, leaf, scan_size, recs + i * (uint64_t)scan_size * t.stride, counts + i,
-                                 lane);
+        uint64_t ok[KW];
+        load_okey<KW>(keys, i, true, len, ok);
+        const uint32_t leaf = uni32(resolve_leaf<VARLEN, KW>(t, ok, len, true));
+        scan_one<VARLEN, SPL, R, KW>(t, ok, len, leaf, scan_size, recs + i * (uint64_t)scan_size * t.stride,
+                                     counts + i, lane);
     }
 }
 
@@ -559,10 +627,20 @@ __device__ __forceinline__ uint64_t payload_word(const ImageDescDev &d, const ui
     return w;
 }
 
+// 8 bytes of an arena row (kind 2 images: [key padded][payload] copied whole), zero past `limit`
+__device__ __forceinline__ uint64_t arena_word(const uint8_t *arena, uint64_t base, uint32_t off, uint32_t limit) {
+    if (off >= limit) return 0;
+    const uint32_t nb = limit - off < 8 ? limit - off : 8;
+    uint64_t w = 0;
+    const uint8_t *s = arena + base + off;
+    for (uint32_t b = 0; b < nb; ++b) w |= (uint64_t)s[b] << (8 * b);
+    return w;
+}
+
 __global__ __launch_bounds__(256) void fill_kernel(uint8_t *__restrict__ heap, uint32_t stride, uint32_t payload_size,
-                                                   const ImageDescDev *__restrict__ descs, const uint8_t *__restrict__ arena,
-                                                   uint64_t first, uint64_t count, uint64_t ident_rowid0,
-                                                   uint32_t ident_key_width, int ident_mode) {
+                                                   uint32_t row_bytes, const ImageDescDev *__restrict__ descs,
+                                                   const uint8_t *__restrict__ arena, uint64_t first, uint64_t count,
+                                                   uint64_t ident_rowid0, uint32_t ident_key_width, int ident_mode) {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
@@ -578,6 +656,14 @@ __global__ __launch_bounds__(256) void fill_kernel(uint8_t *__restrict__ heap, u
             d.mode = (uint32_t)ident_mode;
         }
         u32x4 *row = reinterpret_cast<u32x4 *>(heap + (first + r) * stride);
+        if (d.kind == 2) {
+            for (uint32_t c = lane; c < chunks; c += 64) {
+                const uint64_t w0 = arena_word(arena, d.arg, 16 * c, row_bytes);
+                const uint64_t w1 = arena_word(arena, d.arg, 16 * c + 8, row_bytes);
+                row[c] = u32x4{(uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32)};
+            }
+            continue;
+        }
         for (uint32_t c = lane; c < chunks; c += 64) {
             uint64_t w0 = c == 0 ? d.key_le : payload_word(d, arena, 2 * c - 1, payload_size);
             uint64_t w1 = payload_word(d, arena, 2 * c, payload_size);
@@ -587,13 +673,14 @@ __global__ __launch_bounds__(256) void fill_kernel(uint8_t *__restrict__ heap, u
 }
 
 // Incremental publish: rewrite the heads of dirty leaves (16-B chunks) and the dirty slot
-// words + key-column entries in place.  One thread per chunk / slot, grid-stride.
+// words + key-plane entries in place.  One thread per chunk / slot, grid-stride.
 __global__ __launch_bounds__(256) void patch_kernel(uint8_t *__restrict__ head, uint64_t *__restrict__ okey,
-                                                    SlotInfo *__restrict__ slot, uint32_t head_bytes,
-                                                    const uint32_t *__restrict__ head_leaf,
+                                                    SlotInfo *__restrict__ slot, uint32_t head_bytes, uint32_t cap,
+                                                    uint32_t kw, const uint32_t *__restrict__ head_leaf,
                                                     const u32x4 *__restrict__ head_src, uint64_t nhead,
                                                     const uint64_t *__restrict__ slot_idx,
-                                                    const SlotInfo *__restrict__ slot_src, uint64_t nslot) {
+                                                    const SlotInfo *__restrict__ slot_src,
+                                                    const uint64_t *__restrict__ words, uint64_t nslot) {
     const uint32_t cpl = head_bytes >> 4;
     const uint64_t nchunk = nhead * cpl;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -603,9 +690,9 @@ __global__ __launch_bounds__(256) void patch_kernel(uint8_t *__restrict__ head, 
             reinterpret_cast<u32x4 *>(head + (uint64_t)head_leaf[l] * head_bytes)[c] = head_src[i];
         } else {
             const uint64_t k = i - nchunk, d = slot_idx[k];
-            const SlotInfo v = slot_src[k];
-            slot[d] = v;
-            okey[d] = v.okey;
+            slot[d] = slot_src[k];
+            const uint64_t leaf = d / cap, sl = d % cap;
+            for (uint32_t j = 0; j < kw; ++j) okey[(leaf * kw + j) * cap + sl] = words[k * kw + j];
         }
     }
 }
@@ -623,7 +710,10 @@ static int grid_for(uint64_t waves_needed, int waves_per_block, int max_blocks) 
 hipError_t launch_resolve(const DevTable &t, const uint64_t *keys, const uint16_t *lens, uint64_t n, int le_child,
                           uint32_t *out, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    resolve_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(t, keys, lens, n, le_child, out);
+    const unsigned b = (unsigned)((n + 255) / 256);
+    if (t.key_words == 4) resolve_kernel<4><<<b, 256, 0, s>>>(t, keys, lens, n, le_child, out);
+    else if (t.key_words == 2) resolve_kernel<2><<<b, 256, 0, s>>>(t, keys, lens, n, le_child, out);
+    else resolve_kernel<1><<<b, 256, 0, s>>>(t, keys, lens, n, le_child, out);
     return hipGetLastError();
 }
 
@@ -634,6 +724,26 @@ hipError_t launch_probe(const DevTable &t, const uint64_t *keys, const uint16_t 
     const uint64_t chunks = (n + 63) / 64;
     const int blocks = grid_for(chunks, 4, tune.max_blocks > 0 ? tune.max_blocks : 16384);
     const bool var = t.key_width == 0;
+    if (t.key_words > 1) {  // wide fixed-width keys: leaves of up to 1024 slots, one probe in flight
+#define STAGE_PROBE_W(S, KW) \
+    probe_kernel<false, S, 1, true, KW><<<blocks, 256, 0, s>>>(t, keys, lens, rids, leaf_in, n, out, recs)
+#define STAGE_PROBE_WK(KW)                      \
+    switch (t.cap / 64) {                       \
+        case 1: STAGE_PROBE_W(1, KW); break;    \
+        case 2: STAGE_PROBE_W(2, KW); break;    \
+        case 4: STAGE_PROBE_W(4, KW); break;    \
+        case 8: STAGE_PROBE_W(8, KW); break;    \
+        default: STAGE_PROBE_W(16, KW); break;  \
+    }
+        if (t.key_words == 2) {
+            STAGE_PROBE_WK(2)
+        } else {
+            STAGE_PROBE_WK(4)
+        }
+#undef STAGE_PROBE_WK
+#undef STAGE_PROBE_W
+        return hipGetLastError();
+    }
 #define STAGE_PROBE(V, S, G) probe_kernel<V, S, G><<<blocks, 256, 0, s>>>(t, keys, lens, rids, leaf_in, n, out, recs)
     if (t.cap == 64) {
         if (var) STAGE_PROBE(true, 1, 4);
@@ -651,10 +761,24 @@ hipError_t launch_probe(const DevTable &t, const uint64_t *keys, const uint16_t 
     return hipGetLastError();
 }
 
+template <int KW>
+static void launch_scan_w(const DevTable &t, const uint64_t *keys, uint64_t n, uint32_t scan_size, uint32_t *counts,
+                          uint8_t *recs, hipStream_t s, int blocks) {
+    switch (t.cap / 64) {
+        case 1: scan_kernel<false, 1, 4, KW><<<blocks, 256, 0, s>>>(t, keys, nullptr, n, scan_size, counts, recs); break;
+        case 2: scan_kernel<false, 2, 4, KW><<<blocks, 256, 0, s>>>(t, keys, nullptr, n, scan_size, counts, recs); break;
+        case 4: scan_kernel<false, 4, 4, KW><<<blocks, 256, 0, s>>>(t, keys, nullptr, n, scan_size, counts, recs); break;
+        case 8: scan_kernel<false, 8, 4, KW><<<blocks, 256, 0, s>>>(t, keys, nullptr, n, scan_size, counts, recs); break;
+        default: scan_kernel<false, 16, 4, KW><<<blocks, 256, 0, s>>>(t, keys, nullptr, n, scan_size, counts, recs);
+    }
+}
+
 template <int R>
 static void launch_scan_r(const DevTable &t, const uint64_t *keys, const uint16_t *lens, uint64_t n,
                           uint32_t scan_size, uint32_t *counts, uint8_t *recs, hipStream_t s, int blocks) {
     const bool var = t.key_width == 0;
+    if (t.key_words == 2) return launch_scan_w<2>(t, keys, n, scan_size, counts, recs, s, blocks);
+    if (t.key_words == 4) return launch_scan_w<4>(t, keys, n, scan_size, counts, recs, s, blocks);
     if (t.cap == 64) {
         if (var) scan_kernel<true, 1, R><<<blocks, 256, 0, s>>>(t, keys, lens, n, scan_size, counts, recs);
         else scan_kernel<false, 1, R><<<blocks, 256, 0, s>>>(t, keys, lens, n, scan_size, counts, recs);
@@ -681,25 +805,25 @@ hipError_t launch_murmur(const void *keys, uint32_t key_len, uint32_t key_stride
     return hipGetLastError();
 }
 
-hipError_t launch_fill(uint8_t *heap, uint32_t stride, uint32_t payload_size, const ImageDescDev *descs,
-                       const uint8_t *arena, uint64_t first, uint64_t count, uint64_t ident_rowid0,
-                       uint32_t ident_key_width, int ident_mode, hipStream_t s) {
+hipError_t launch_fill(uint8_t *heap, uint32_t stride, uint32_t payload_size, uint32_t row_bytes,
+                       const ImageDescDev *descs, const uint8_t *arena, uint64_t first, uint64_t count,
+                       uint64_t ident_rowid0, uint32_t ident_key_width, int ident_mode, hipStream_t s) {
     if (count == 0) return hipSuccess;
     const int blocks = grid_for(count, 4, 8192);
-    fill_kernel<<<blocks, 256, 0, s>>>(heap, stride, payload_size, descs, arena, first, count, ident_rowid0,
+    fill_kernel<<<blocks, 256, 0, s>>>(heap, stride, payload_size, row_bytes, descs, arena, first, count, ident_rowid0,
                                        ident_key_width, ident_mode);
     return hipGetLastError();
 }
 
-hipError_t launch_patch(uint8_t *head, uint64_t *okey, SlotInfo *slot, uint32_t head_bytes, const uint32_t *head_leaf,
-                        const void *head_src, uint64_t nhead, const uint64_t *slot_idx, const SlotInfo *slot_src,
-                        uint64_t nslot, hipStream_t s) {
+hipError_t launch_patch(uint8_t *head, uint64_t *okey, SlotInfo *slot, uint32_t head_bytes, uint32_t cap, uint32_t kw,
+                        const uint32_t *head_leaf, const void *head_src, uint64_t nhead, const uint64_t *slot_idx,
+                        const SlotInfo *slot_src, const uint64_t *words, uint64_t nslot, hipStream_t s) {
     const uint64_t work = nhead * (head_bytes >> 4) + nslot;
     if (work == 0) return hipSuccess;
     uint64_t blocks = (work + 255) / 256;
     if (blocks > 8192) blocks = 8192;
-    patch_kernel<<<(unsigned)blocks, 256, 0, s>>>(head, okey, slot, head_bytes, head_leaf, (const u32x4 *)head_src,
-                                                  nhead, slot_idx, slot_src, nslot);
+    patch_kernel<<<(unsigned)blocks, 256, 0, s>>>(head, okey, slot, head_bytes, cap, kw, head_leaf,
+                                                  (const u32x4 *)head_src, nhead, slot_idx, slot_src, words, nslot);
     return hipGetLastError();
 }
 

@@ -3,9 +3,10 @@
 // Device image of one index-organized table (DESIGN.md "Data layout in HBM"):
 //   head[L]         cap+cap/8 B rounded to 128: 1-byte key fingerprint per slot, then the
 //                   visible-slot masks -- the only per-leaf bytes a point probe reads
-//   okey[L*cap]     u64  order key column (range scans read it whole, 512 B/leaf)
-//   slot[L*cap]     32 B {okey, meta word, next handle, image id} (probe: candidates only)
-//   tree            u64  implicit 16-ary separator tree (128-B nodes), all levels
+//   okey[L*KW*cap]  u64  order key columns, one plane of cap words per key word (range scans
+//                   read them whole, 512 B/leaf for keys of <= 8 bytes)
+//   slot[L*cap]     32 B {okey word 0, meta word, next handle, image id} (probe: candidates)
+//   tree            u64  implicit 16-ary separator tree (KW words per entry), all levels
 //   heap[I*hstride] u8   record images [key padded to 8][payload] (current, copies,
 //                   versions); rows 128-B aligned when larger than 128 B
 //   chdr[C]         16 B overwrite-copy headers   (EphemeralPool::OverwriteVersionHeader)
@@ -65,6 +66,32 @@ STAGE_HD uint64_t key_bytes_from_order(uint64_t okey, uint32_t len) {
     return (bswap64(okey) ^ 0x8080808080808080ull) & mask;
 }
 
+// Keys longer than 8 bytes (fixed width 9..32, TPC-C): one order word per 8-byte chunk,
+// compared word by word, then by length.  KeyCompare (b_tree.h:114-134, and Sorter's copy at
+// b_tree.h:527-545) uses the signed-byte my_memcmp only when min(size1, size2) < 16 and libc
+// memcmp -- UNSIGNED bytes -- from 16 bytes up, so tables whose keys are 16..32 bytes order
+// by unsigned bytes (no 0x80 flip).
+constexpr int kMaxKeyWords = 4;
+constexpr uint32_t kMaxKeyBytes = 32;
+// order words per key of a table: 1 (<= 8 bytes), 2 (9..16), 4 (17..32; 24-byte keys carry a
+// zero fourth word, which every key of the table shares)
+STAGE_HD uint32_t table_key_words(uint32_t key_width) { return key_width <= 8 ? 1u : (key_width <= 16 ? 2u : 4u); }
+// order word j of a key of `len` bytes whose little-endian chunk j is `le_word`
+STAGE_HD bool key_order_unsigned(uint32_t key_width) { return key_width >= 16; }
+STAGE_HD uint64_t order_word(uint64_t le_word, uint32_t len, uint32_t j, bool uns) {
+    if (8u * j >= len) return 0;
+    const uint32_t rem = len - 8u * j;
+    const uint32_t nb = rem > 8u ? 8u : rem;
+    if (!uns) return order_key(le_word, nb);
+    const uint64_t mask = nb >= 8 ? ~0ull : ((1ull << (8u * nb)) - 1ull);
+    return bswap64(le_word & mask);
+}
+STAGE_HD uint32_t key_fp_words(const uint64_t *w, uint32_t kw) {
+    uint64_t h = w[0];
+    for (uint32_t j = 1; j < kw; ++j) h = (h ^ (h >> 29)) * 0xBF58476D1CE4E5B9ull + w[j];
+    return (uint32_t)((h * 0x9E3779B97F4A7C15ull) >> 56);
+}
+
 // per-slot word, read by the fingerprint candidates of a probe
 struct alignas(32) SlotInfo {
     uint64_t okey;  // order key (confirms a fingerprint match)
@@ -102,9 +129,9 @@ constexpr int kMaxTreeLevels = 16;
 // Everything a kernel needs to read one table (passed by value).
 struct DevTable {
     const uint8_t *head;        // [L * head_bytes]: fp[cap] then vis[cap/64]
-    const uint64_t *okey;
+    const uint64_t *okey;       // [(leaf*KW + word)*cap + slot]
     const SlotInfo *slot;
-    const uint64_t *tree;       // all levels, level 0 (leaf separators) first
+    const uint64_t *tree;       // all levels, level 0 (leaf separators) first; [entry*KW + word]
     const uint8_t *tree_len;    // variable-length tables only: key length per tree entry
     const uint8_t *heap;
     const CopyHdr *chdr;
@@ -119,6 +146,7 @@ struct DevTable {
     uint32_t head_bytes;        // bytes per leaf head
     uint32_t payload_size;
     uint32_t key_width;         // 0 = variable
+    uint32_t key_words;         // KW: order words per key (1 for keys of <= 8 bytes)
 };
 
 }  // namespace stage

@@ -43,8 +43,17 @@ SIGNATURES = {
                                            c_u8p]),
     "stage_finalize_update": (ctypes.c_int, [c_vp, ctypes.c_uint64, ctypes.c_uint16, ctypes.c_uint32, c_u8p]),
     "stage_delete": (ctypes.c_int, [c_vp, ctypes.c_uint64, ctypes.c_uint16, ctypes.c_uint32, c_u8p]),
-    "stage_update_batch": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64, ctypes.c_uint16, ctypes.c_uint32, c_vp,
-                                          ctypes.c_uint32, c_vp, c_vp, c_vp, c_vp, c_u64p]),
+    "stage_update_batch": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint16,
+                                          ctypes.c_uint32, c_vp, ctypes.c_uint32, c_vp, c_vp, c_vp, c_vp, c_u64p]),
+    "stage_insert_key": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint16, c_vp, ctypes.c_uint32, c_u8p]),
+    "stage_load_rows": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint32, ctypes.c_uint16, c_vp, ctypes.c_uint32,
+                                       ctypes.c_uint64, ctypes.c_uint32, c_vp, c_u64p]),
+    "stage_update_key": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint16, ctypes.c_uint32, c_vp, ctypes.c_uint32,
+                                        ctypes.c_uint32, c_u8p]),
+    "stage_commit_update_key": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint16, ctypes.c_uint32, ctypes.c_uint32,
+                                               c_u8p]),
+    "stage_delete_key": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint16, ctypes.c_uint32, c_u8p]),
+    "stage_key_words": (ctypes.c_uint32, [c_vp]),
     "stage_sync": (ctypes.c_int, [c_vp]),
     "stage_set_shard_chunks": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "stage_probe_sharded_loopback": (ctypes.c_int, [c_vp, ctypes.c_int, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_int,

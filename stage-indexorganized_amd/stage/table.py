@@ -192,7 +192,7 @@ class Table:
         sst = None if sstamps is None else np.ascontiguousarray(np.broadcast_to(np.asarray(sstamps, np.uint32), (n,)))
         rc = np.zeros(n, np.uint8)
         ok = ctypes.c_uint64()
-        check(lib().stage_update_batch(self.h, keys.ctypes.data, n, key_size or self.key_width, payload_off,
+        check(lib().stage_update_batch(self.h, keys.ctypes.data, 8, n, key_size or self.key_width, payload_off,
                                        deltas.ctypes.data, deltas.shape[1] if n else 0, wid.ctypes.data,
                                        cid.ctypes.data if cid is not None else None,
                                        sst.ctypes.data if sst is not None else None, rc.ctypes.data,
@@ -236,30 +236,92 @@ class Table:
     def export_leaf_images(self):
         """Reference-format leaf blocks in key order + upper separators (key_le, len; 0xFFFF = +inf)."""
         nl = self.stats()["leaves"]
+        kw = self.key_words
         blocks = np.zeros((nl, self.leaf_node_size), np.uint8)
-        sk = np.zeros(nl, np.uint64)
+        sk = np.zeros(nl * kw, np.uint64)
         sl = np.zeros(nl, np.uint16)
         got = lib().stage_export_leaf_images(self.h, nl, blocks.ctypes.data, sk.ctypes.data, sl.ctypes.data)
         if got < 0:
             check(int(got), "export_leaf_images")
-        return blocks[:got], sk[:got], sl[:got]
+        return blocks[:got], (sk[:got] if kw == 1 else sk.reshape(nl, kw)[:got]), sl[:got]
 
     def import_leaf_images(self, blocks, sep_keys=None, sep_lens=None):
         blocks = np.ascontiguousarray(blocks, np.uint8)
         n = ctypes.c_uint64()
-        sk = None if sep_keys is None else np.ascontiguousarray(sep_keys, np.uint64)
+        sk = None if sep_keys is None else np.ascontiguousarray(sep_keys, np.uint64).reshape(-1)
         sl = None if sep_lens is None else np.ascontiguousarray(sep_lens, np.uint16)
         check(lib().stage_import_leaf_images(self.h, blocks.ctypes.data, blocks.shape[0], blocks.shape[1], _ptr(sk),
                                              _ptr(sl), ctypes.byref(n)), "import_leaf_images")
         return n.value
 
+    @property
+    def key_words(self):
+        return int(lib().stage_key_words(self.h))
+
+    def key_buffer(self, keys):
+        """Keys -> (u64 words, count): 1-D integer keys (tables of <= 8-byte keys) or a 2-D uint8
+        array of key bytes (n, width), zero padded to stage_key_words() words per key."""
+        kw = self.key_words
+        a = np.asarray(keys)
+        if a.ndim == 2:
+            a = np.ascontiguousarray(a, np.uint8)
+            buf = np.zeros((a.shape[0], kw * 8), np.uint8)
+            buf[:, :a.shape[1]] = a
+            return buf.view(np.uint64).reshape(-1), a.shape[0]
+        assert kw == 1, "tables with keys above 8 bytes take (n, width) uint8 key arrays"
+        a = np.ascontiguousarray(a, np.uint64).reshape(-1)
+        return a, a.size
+
     def traverse(self, keys, lens=None, le_child=True):
-        keys = np.ascontiguousarray(keys, np.uint64)
+        words, n = self.key_buffer(keys)
         lens = None if lens is None else np.ascontiguousarray(lens, np.uint16)
-        out = np.zeros(keys.size, np.uint32)
-        check(lib().stage_traverse_batch(self.h, keys.ctypes.data, _ptr(lens), keys.size, int(le_child),
+        out = np.zeros(n, np.uint32)
+        check(lib().stage_traverse_batch(self.h, words.ctypes.data, _ptr(lens), n, int(le_child),
                                          out.ctypes.data), "traverse")
         return out
+
+    # ---------------------------------------------------------------- byte-key write path
+    def insert_key(self, key, payload, commit_id=0):
+        k = np.frombuffer(bytes(key), np.uint8)
+        p = np.frombuffer(bytes(payload), np.uint8)
+        assert p.size == self.payload_size
+        rc = ctypes.c_uint8()
+        check(lib().stage_insert_key(self.h, k.ctypes.data, k.size, p.ctypes.data, commit_id, ctypes.byref(rc)),
+              "insert_key")
+        return rc.value
+
+    def load_rows(self, keys, payloads, commit_id=0):
+        """keys (n, width) uint8, payloads (n, payload_size) uint8 -> (rc per row, inserted)."""
+        keys = np.ascontiguousarray(keys, np.uint8)
+        payloads = np.ascontiguousarray(payloads, np.uint8)
+        n = keys.shape[0]
+        assert payloads.shape == (n, self.payload_size)
+        rc = np.zeros(n, np.uint8)
+        ins = ctypes.c_uint64()
+        check(lib().stage_load_rows(self.h, keys.ctypes.data, keys.shape[1], keys.shape[1], payloads.ctypes.data,
+                                    payloads.shape[1], n, commit_id, rc.ctypes.data, ctypes.byref(ins)), "load_rows")
+        return rc, ins.value
+
+    def update_key(self, key, payload_off, delta, writer_id):
+        k = np.frombuffer(bytes(key), np.uint8)
+        d = np.frombuffer(bytes(delta), np.uint8)
+        rc = ctypes.c_uint8()
+        check(lib().stage_update_key(self.h, k.ctypes.data, k.size, payload_off, d.ctypes.data, d.size, writer_id,
+                                     ctypes.byref(rc)), "update_key")
+        return rc.value
+
+    def commit_update_key(self, key, commit_id, sstamp):
+        k = np.frombuffer(bytes(key), np.uint8)
+        rc = ctypes.c_uint8()
+        check(lib().stage_commit_update_key(self.h, k.ctypes.data, k.size, commit_id, sstamp, ctypes.byref(rc)),
+              "commit_update_key")
+        return rc.value
+
+    def delete_key(self, key, commit_id=0):
+        k = np.frombuffer(bytes(key), np.uint8)
+        rc = ctypes.c_uint8()
+        check(lib().stage_delete_key(self.h, k.ctypes.data, k.size, commit_id, ctypes.byref(rc)), "delete_key")
+        return rc.value
 
     # ---------------------------------------------------------------- device read path
     def probe_device(self, d_keys, n, d_out, d_records=None, d_read_ids=None, d_lens=None, d_leaf_ids=None,
@@ -269,9 +331,8 @@ class Table:
 
     def probe(self, keys, read_ids=None, lens=None, leaf_ids=None, records=True):
         """Batched BTree::Read + visibility.  Returns (out[n] PROBE_OUT_DTYPE, rows[n, stride] or None)."""
-        keys = np.ascontiguousarray(keys, np.uint64)
-        n = keys.size
-        bufs = [DeviceBuffer.from_numpy(keys)]
+        words, n = self.key_buffer(keys)
+        bufs = [DeviceBuffer.from_numpy(words) if n else DeviceBuffer(8)]
         d_rids = d_lens = d_leaf = None
         if read_ids is not None:
             bufs.append(DeviceBuffer.from_numpy(np.ascontiguousarray(read_ids, np.uint32)))
@@ -292,8 +353,7 @@ class Table:
 
     def probe_host(self, keys, read_ids=None, lens=None, records=True):
         """stage_probe_host: the same probe with host-memory inputs and outputs (pipelined)."""
-        keys = np.ascontiguousarray(keys, np.uint64)
-        n = keys.size
+        keys, n = self.key_buffer(keys)
         rids = None if read_ids is None else np.ascontiguousarray(read_ids, np.uint32)
         ln = None if lens is None else np.ascontiguousarray(lens, np.uint16)
         out = np.zeros(n, PROBE_OUT_DTYPE)
@@ -307,8 +367,7 @@ class Table:
 
     def range_scan(self, start_keys, scan_size, lens=None):
         """TableScanExecutor over RangeScanBySize/Iterator.  Returns (counts[n], rows[n, scan_size, stride])."""
-        keys = np.ascontiguousarray(start_keys, np.uint64)
-        n = keys.size
+        keys, n = self.key_buffer(start_keys)
         d_keys = DeviceBuffer.from_numpy(keys)
         d_lens = DeviceBuffer.from_numpy(np.ascontiguousarray(lens, np.uint16)) if lens is not None else None
         d_cnt = DeviceBuffer(n * 4)
@@ -322,14 +381,14 @@ class Table:
         return counts, rows
 
     def resolve(self, keys, lens=None, le_child=True):
-        keys = np.ascontiguousarray(keys, np.uint64)
+        keys, n = self.key_buffer(keys)
         d_keys = DeviceBuffer.from_numpy(keys)
         d_lens = DeviceBuffer.from_numpy(np.ascontiguousarray(lens, np.uint16)) if lens is not None else None
-        d_out = DeviceBuffer(keys.size * 4)
-        check(lib().stage_resolve_batch(self.h, d_keys.ptr, d_lens.ptr if d_lens else None, keys.size,
+        d_out = DeviceBuffer(n * 4)
+        check(lib().stage_resolve_batch(self.h, d_keys.ptr, d_lens.ptr if d_lens else None, n,
                                         int(le_child), d_out.ptr, None), "resolve")
         check(lib().stage_device_sync(), "sync")
-        return d_out.to_numpy(np.uint32, keys.size)
+        return d_out.to_numpy(np.uint32, n)
 
 
 class Reader:

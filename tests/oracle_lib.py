@@ -40,6 +40,10 @@ _SIG = {
     "orc_stats": (None, [vp, vp]),
     "orc_export_leaves": (ctypes.c_int64, [vp, u32, u64, vp, vp, vp, vp]),
     "orc_export_leaf_images": (ctypes.c_int64, [vp, u64, vp, vp, vp]),
+    "orc_export_leaf_images_k": (ctypes.c_int64, [vp, u64, vp, vp, u32, vp]),
+    "orc_tree_set_key_pad": (None, [vp, u32]),
+    "orc_read_batch_k": (ctypes.c_int, [vp, vp, u32, u32, vp, u64, vp, vp, ctypes.c_int]),
+    "orc_scan_batch_k": (u64, [vp, vp, u32, u32, u64, u32, vp, vp, ctypes.c_int]),
     "orc_key_compare": (ctypes.c_int, [vp, u32, vp, u32]),
     "orc_murmur64a": (u64, [vp, ctypes.c_int, u64]),
     "orc_murmur64a_batch": (None, [vp, u64, ctypes.c_int, u64, vp]),
@@ -74,12 +78,14 @@ def key_bytes(key, size):
 
 class OracleTree:
     def __init__(self, leaf_node_size=64 * 1024, split_threshold=16 * 1024, payload_size=1000,
-                 merge_threshold=32 * 1024):
+                 merge_threshold=32 * 1024, key_pad=8):
         self.t = lib().orc_tree_new(leaf_node_size, split_threshold, payload_size)
         lib().orc_tree_set_merge_threshold(self.t, merge_threshold)
+        lib().orc_tree_set_key_pad(self.t, key_pad)
         self.payload_size = payload_size
         self.leaf_node_size = leaf_node_size
-        self.row = 8 + payload_size
+        self.key_pad = key_pad
+        self.row = key_pad + payload_size
 
     def __del__(self):
         try:
@@ -117,6 +123,27 @@ class OracleTree:
                              outs.ctypes.data, recs.ctypes.data if recs is not None else None, nthreads)
         return outs, recs
 
+    def read_batch_k(self, keys, read_ids=None, records=True, nthreads=8):
+        """keys: (n, width) uint8 key bytes"""
+        keys = np.ascontiguousarray(keys, np.uint8)
+        n = keys.shape[0]
+        rids = None if read_ids is None else np.ascontiguousarray(read_ids, np.uint32)
+        outs = np.zeros(n, READ_OUT_DTYPE)
+        recs = np.zeros((n, self.row), np.uint8) if records else None
+        lib().orc_read_batch_k(self.t, keys.ctypes.data, keys.shape[1], keys.shape[1],
+                               rids.ctypes.data if rids is not None else None, n, outs.ctypes.data,
+                               recs.ctypes.data if recs is not None else None, nthreads)
+        return outs, recs
+
+    def scan_batch_k(self, keys, scan_size, nthreads=8):
+        keys = np.ascontiguousarray(keys, np.uint8)
+        n = keys.shape[0]
+        counts = np.zeros(n, np.uint32)
+        recs = np.zeros((n, scan_size, self.row), np.uint8)
+        lib().orc_scan_batch_k(self.t, keys.ctypes.data, keys.shape[1], keys.shape[1], n, scan_size,
+                               counts.ctypes.data, recs.ctypes.data, nthreads)
+        return counts, recs
+
     def scan(self, key, key_size, scan_size):
         kb = key_bytes(key, key_size)
         recs = np.zeros((max(scan_size, 1), self.row), np.uint8)
@@ -153,14 +180,14 @@ class OracleTree:
         keys = ["height", "inner", "leaves", "records", "sorted", "unsorted", "max_count", "versions"]
         return {k: int(v) for k, v in zip(keys, s)}
 
-    def export_leaf_images(self):
+    def export_leaf_images(self, kwords=1):
         nl = self.stats()["leaves"]
         blocks = np.zeros((nl, self.leaf_node_size), np.uint8)
-        sk = np.zeros(nl, np.uint64)
+        sk = np.zeros(nl * kwords, np.uint64)
         sl = np.zeros(nl, np.uint16)
-        got = lib().orc_export_leaf_images(self.t, nl, blocks.ctypes.data, sk.ctypes.data, sl.ctypes.data)
+        got = lib().orc_export_leaf_images_k(self.t, nl, blocks.ctypes.data, sk.ctypes.data, kwords, sl.ctypes.data)
         assert got == nl
-        return blocks, sk, sl
+        return blocks, (sk if kwords == 1 else sk.reshape(nl, kwords)), sl
 
     def export_leaves(self, cap):
         nl = self.stats()["leaves"]
