@@ -50,7 +50,10 @@ class DeviceBuffer:
         return out
 
     def memset(self, value=0, stream=None):
+        """Fill the buffer; completes before returning (the library's streams are non-blocking,
+        so an asynchronous fill on another stream could land after a later kernel's writes)."""
         check(lib().stage_dev_memset(self.ptr, value, self.nbytes, stream), "memset")
+        check(lib().stage_stream_sync(stream) if stream else lib().stage_device_sync(), "memset sync")
 
     def free(self):
         if self.ptr:
