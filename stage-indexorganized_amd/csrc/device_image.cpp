@@ -63,7 +63,7 @@ static void build_leaf(const HostTable &h, uint32_t hl, uint8_t *hd, uint64_t *o
     const uint64_t hbase = (uint64_t)hl * cap;
     const uint32_t count = h.leaves_[hl].count;
     std::memset(hd, 0, hb);
-    uint64_t vis[2] = {0, 0};
+    uint64_t vis[16] = {0};  // up to 1024 slots
     for (uint32_t s = 0; s < cap; ++s) {
         const bool live = s < count;
         const uint64_t m = live ? h.meta_[hbase + s] : 0;
