@@ -207,6 +207,15 @@ int stage_scan_batch(stage_table *t, const uint64_t *d_start_keys, const uint16_
                      void *stream);
 int stage_resolve_batch(stage_table *t, const uint64_t *d_keys, const uint16_t *d_lens, uint64_t n,
                         int le_child, uint32_t *d_leaf, void *stream);
+/* IndexScanExecutor::Execute range branch (executor.h:456-530): the scan of stage_scan_batch
+ * with per-record visibility for d_read_ids[i] (NULL -> 0xFFFFFFFE).  For iterator record j
+ * of scan i: d_row_status[i*scan_size + j] = STAGE_ST_LATEST (the leaf record, read_id >= its
+ * commit id), STAGE_ST_OLD (the TupleHeader version with begin <= read_id <= end) or
+ * STAGE_ST_NOT_FOUND (nothing produced; row zeroed); d_counts[i] = records consumed. */
+int stage_index_scan_batch(stage_table *t, const uint64_t *d_start_keys, const uint16_t *d_lens,
+                           const uint32_t *d_read_ids, uint64_t n, uint32_t scan_size,
+                           uint32_t *d_counts, uint8_t *d_records, uint8_t *d_row_status,
+                           void *stream);
 
 /* ---- host-buffer forms (keys and results in host memory) --------------------------------
  * stage_probe_host: stage_probe_batch for host buffers; the batch is cut into chunks that
@@ -241,6 +250,21 @@ int stage_set_probe_tuning(stage_table *t, int group, int max_blocks);
  * key_stride bytes apart; d_out[i] = hash.  Used as the multi-GPU shard router. */
 int stage_murmur64a_batch(const void *d_keys, uint32_t key_len, uint32_t key_stride, uint64_t seed,
                           uint64_t n, uint64_t *d_out, void *stream);
+
+/* ---- TPC-C stock-level through the path (tpcc_stock_level.cpp:37-180), batched -----------
+ * district: DistrictKey{int64 D_W_ID, int64 D_ID} (16 B) table whose payload starts with
+ * D_NEXT_O_ID (int32); order_line: OrderLineKey{W, D, O, NUMBER} (32 B), payload starts with
+ * OL_I_ID (int32); stock: StockKey{W, I} (16 B), payload starts with S_QUANTITY (int32)
+ * (tpcc_record.h GetData layouts).  Transaction i = (d_w_ids[i], d_d_ids[i],
+ * d_thresholds[i], read id d_read_ids[i] or 0xFFFFFFFE): DISTRICT point lookup; for the 20
+ * orders below D_NEXT_O_ID an ORDER_LINE range scan of 10 records from {w, d, o, 5} with
+ * IndexScanExecutor visibility, keeping OL_I_IDs of (w, d, o); a STOCK point lookup of each
+ * scan's first item; d_result[i] = number of distinct S_I_IDs with S_QUANTITY < threshold,
+ * or -1 when the transaction aborts (FAILURE / missing district).  All device-resident: three
+ * batched probe/scan launches and four small glue kernels, no host round trip. */
+int stage_tpcc_stock_level(stage_table *district, stage_table *order_line, stage_table *stock,
+                           const int64_t *d_w_ids, const int64_t *d_d_ids, const int32_t *d_thresholds,
+                           const uint32_t *d_read_ids, uint64_t n, int32_t *d_result, void *stream);
 
 /* ---- multi-GPU: hash-sharded probe front-end over RCCL (one process per GPU) ------------
  * stage_comm_unique_id fills 128 bytes on rank 0 (broadcast them out of band);

@@ -895,9 +895,48 @@ static void emit_scan_rec(orc_tree *t, uint8_t *dst, scanrec_t *r) {
     memcpy(dst + t->key_pad, r->leaf + m_offset(mm) + m_padded(mm), t->payload_size);
 }
 
-/* TableScanExecutor::Execute (executor.h:620-639) driving Iterator::GetNext (b_tree.h:899-941) */
+/* IndexScanExecutor::Execute range branch (executor.h:456-530), per iterator record: a
+ * reader with txn_id >= the record's commit id reads the leaf record (PerformRead; for an
+ * in-flight update that is the patched image); otherwise the TupleHeader chain from next_ptr
+ * gives the version with begin <= txn_id <= end, and nothing is produced when begin or end is
+ * INVALID_CID or the chain ends.  Deviations: the reference never leaves its chain loop after
+ * a match (executor.h:500-508 re-tests the same header forever) -- here the match ends the
+ * walk; a next_ptr that points at an overwrite copy (in-flight record) produces nothing.
+ * status: 1 = latest, 3 = old version, 0 = nothing produced. */
+static void emit_index_rec(orc_tree *t, uint8_t *dst, scanrec_t *r, uint32_t read_id, uint8_t *status) {
+    orc_rmeta *mp = l_meta(r->leaf, r->slot);
+    uint32_t rs = t->key_pad + t->payload_size;
+    if (read_id >= m_cstamp(mp->meta)) {
+        *status = ORC_ST_LATEST;
+        if (dst) emit_scan_rec(t, dst, r);
+        return;
+    }
+    *status = ORC_ST_NOT_FOUND;
+    if (dst) memset(dst, 0, rs);
+    uint64_t nx = mp->next;
+    while (nx != 0 && nx != ~0ull && NEXT_KIND(nx) == NEXT_TH) {
+        orc_th *th = NEXT_PTR(nx);
+        if (th->begin_id == INVALID_CID || th->comm_id == INVALID_CID) return;
+        if (read_id >= th->begin_id && read_id <= th->comm_id) {
+            *status = ORC_ST_OLD;
+            if (dst) emit_canonical(t, dst, th->slot, th->key_len, th->slot + th->key_len);
+            return;
+        }
+        nx = th->next;
+    }
+}
+
+/* TableScanExecutor::Execute (executor.h:620-639) driving Iterator::GetNext (b_tree.h:899-941);
+ * with `status` non-NULL the IndexScanExecutor range branch above decides each record. */
+static uint32_t scan_one_ex(orc_tree *t, const uint8_t *key, uint16_t ks, uint32_t scan_size, uint8_t *recs,
+                            scanrec_t *buf, uint32_t bufcap, uint32_t read_id, uint8_t *status);
 static uint32_t scan_one(orc_tree *t, const uint8_t *key, uint16_t ks, uint32_t scan_size, uint8_t *recs,
                          scanrec_t *buf, uint32_t bufcap) {
+    return scan_one_ex(t, key, ks, scan_size, recs, buf, bufcap, 0, NULL);
+}
+
+static uint32_t scan_one_ex(orc_tree *t, const uint8_t *key, uint16_t ks, uint32_t scan_size, uint8_t *recs,
+                            scanrec_t *buf, uint32_t bufcap, uint32_t read_id, uint8_t *status) {
     uint32_t rs = t->key_pad + t->payload_size, produced = 0;
     uint32_t remaining = scan_size;
     uint8_t lastkey[64];
@@ -910,14 +949,17 @@ static uint32_t scan_one(orc_tree *t, const uint8_t *key, uint16_t ks, uint32_t 
         if (head >= m || remaining == 0) continue; /* nullptr -> fail_num++ */
         remaining -= 1;
         if (m - head > 1) {
-            if (recs) emit_scan_rec(t, recs + (uint64_t)produced * rs, &buf[head]);
+            if (status) emit_index_rec(t, recs ? recs + (uint64_t)produced * rs : NULL, &buf[head], read_id,
+                                       status + produced);
+            else if (recs) emit_scan_rec(t, recs + (uint64_t)produced * rs, &buf[head]);
             produced++;
             head++;
             continue;
         }
         scanrec_t last = buf[head];
         head++;
-        if (recs) emit_scan_rec(t, recs + (uint64_t)produced * rs, &last);
+        if (status) emit_index_rec(t, recs ? recs + (uint64_t)produced * rs : NULL, &last, read_id, status + produced);
+        else if (recs) emit_scan_rec(t, recs + (uint64_t)produced * rs, &last);
         produced++;
         lastks = last.ks > 64 ? 64 : last.ks;
         memcpy(lastkey, last.k, lastks);
@@ -927,6 +969,15 @@ static uint32_t scan_one(orc_tree *t, const uint8_t *key, uint16_t ks, uint32_t 
         if (m > 0 && orc_key_compare(buf[0].k, buf[0].ks, lastkey, lastks) == 0) m = 0; /* item_vec.clear() */
     }
     return produced;
+}
+
+uint32_t orc_index_scan(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t scan_size, uint32_t read_id,
+                        uint8_t *recs, uint8_t *status) {
+    uint32_t cap = 4096;
+    scanrec_t *buf = xmalloc(sizeof(scanrec_t) * cap);
+    uint32_t r = scan_one_ex(t, key, (uint16_t)key_size, scan_size, recs, buf, cap, read_id, status);
+    free(buf);
+    return r;
 }
 
 uint32_t orc_scan(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t scan_size, uint8_t *recs) {

@@ -118,6 +118,11 @@ int64_t orc_export_leaf_images(orc_tree *t, uint64_t max_leaves, uint8_t *blocks
 /* the same with kwords u64 words of separator key bytes per leaf (keys above 8 bytes) */
 int64_t orc_export_leaf_images_k(orc_tree *t, uint64_t max_leaves, uint8_t *blocks, uint64_t *sep_key,
                                  uint32_t kwords, uint16_t *sep_len);
+/* IndexScanExecutor range branch (executor.h:456-530): the iterator records of a scan of
+ * scan_size with per-record visibility for read_id; status[j] = 1 latest, 3 old version,
+ * 0 nothing (row zeroed).  Returns the number of iterator records consumed. */
+uint32_t orc_index_scan(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t scan_size, uint32_t read_id,
+                        uint8_t *recs, uint8_t *status);
 /* canonical tuple rows [key padded to key_pad][payload]; default 8 (keys of <= 8 bytes) */
 void orc_tree_set_key_pad(orc_tree *t, uint32_t key_pad);
 /* batch forms over byte keys (key i at keys + i*key_stride) */

@@ -299,6 +299,20 @@ int stage_scan_batch(stage_table *t, const uint64_t *d_start_keys, const uint16_
     return hip_rc(e, "scan kernel");
 }
 
+int stage_index_scan_batch(stage_table *t, const uint64_t *d_start_keys, const uint16_t *d_lens,
+                           const uint32_t *d_read_ids, uint64_t n, uint32_t scan_size, uint32_t *d_counts,
+                           uint8_t *d_records, uint8_t *d_row_status, void *stream) {
+    int rc = need_synced(t);
+    if (rc) return rc;
+    if (n && (!d_start_keys || !d_counts || (scan_size && (!d_records || !d_row_status))))
+        return fail(STAGE_E_ARG, "null device buffer");
+    hipError_t e = hipSetDevice(t->dev.device);
+    if (e != hipSuccess) return hip_rc(e, "hipSetDevice");
+    e = stage::launch_scan(t->dev.view, d_start_keys, d_lens, n, scan_size, d_counts, d_records, pick(t, stream),
+                           t->scan_tune, d_read_ids, d_row_status);
+    return hip_rc(e, "index scan kernel");
+}
+
 int stage_resolve_batch(stage_table *t, const uint64_t *d_keys, const uint16_t *d_lens, uint64_t n, int le_child,
                         uint32_t *d_leaf, void *stream) {
     int rc = need_synced(t);

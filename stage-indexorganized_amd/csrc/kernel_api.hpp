@@ -37,8 +37,11 @@ struct ScanTuning {
     int max_blocks = 0;  // 0 = default grid cap (16384 blocks of 256 threads)
 };
 
+// row_status != nullptr: IndexScanExecutor range semantics (per-record visibility for
+// rids[i]); row_status[i*scan_size + j] = ST_LATEST / ST_OLD / ST_NOT_FOUND (row zeroed)
 hipError_t launch_scan(const DevTable &t, const uint64_t *keys, const uint16_t *lens, uint64_t n, uint32_t scan_size,
-                       uint32_t *counts, uint8_t *recs, hipStream_t s, const ScanTuning &tune);
+                       uint32_t *counts, uint8_t *recs, hipStream_t s, const ScanTuning &tune,
+                       const uint32_t *rids = nullptr, uint8_t *row_status = nullptr);
 hipError_t launch_murmur(const void *keys, uint32_t key_len, uint32_t key_stride, uint64_t seed, uint64_t n,
                          uint64_t *out, hipStream_t s);
 hipError_t launch_fill(uint8_t *heap, uint32_t stride, uint32_t payload_size, uint32_t row_bytes,

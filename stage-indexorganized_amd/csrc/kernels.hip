@@ -396,7 +396,8 @@ __device__ __forceinline__ void copy_rows(const DevTable &t, const uint32_t *img
 #pragma unroll
         for (int k = 0; k < R; ++k) {
             v[k] = u32x4{0, 0, 0, 0};
-            if (k < n && c < chunks) v[k] = reinterpret_cast<const u32x4 *>(t.heap + (uint64_t)img[k] * t.hstride)[c];
+            if (k < n && c < chunks && img[k] != 0xFFFFFFFFu)
+                v[k] = reinterpret_cast<const u32x4 *>(t.heap + (uint64_t)img[k] * t.hstride)[c];
         }
 #pragma unroll
         for (int k = 0; k < R; ++k)
@@ -411,9 +412,32 @@ __device__ __forceinline__ bool key_less(const uint64_t *a, uint32_t al, const u
     return kw_lt<KW>(a, b);  // fixed width: equal lengths
 }
 
-template <bool VARLEN, int SPL, int R, int KW>
+// IndexScanExecutor range branch (executor.h:456-530) for one iterator record: the leaf
+// image when rid >= its commit id, else the TupleHeader version with begin <= rid <= end
+// (nothing when begin/end is INVALID_CID, the chain ends, or next is an overwrite copy).
+__device__ __forceinline__ uint32_t scan_visible(const DevTable &t, const SlotInfo &si, uint32_t rid, uint8_t &st) {
+    if (rid >= meta_cstamp(si.meta)) {
+        st = ST_LATEST;
+        return si.image;
+    }
+    st = ST_NOT_FOUND;
+    uint32_t chain = si.next;
+    for (uint32_t guard = 0; guard < (1u << 24) && (chain & kNextKindMask) == kNextVersion; ++guard) {
+        const VersionHdr v = t.vhdr[chain & kNextIndexMask];
+        if (v.begin_id == kInvalidCid || v.comm_id == kInvalidCid) break;
+        if (rid >= v.begin_id && rid <= v.comm_id) {
+            st = ST_OLD;
+            return v.image;
+        }
+        chain = v.next;
+    }
+    return 0xFFFFFFFFu;
+}
+
+template <bool VARLEN, int SPL, int R, int KW, bool VIS = false>
 __device__ void scan_one(const DevTable &t, const uint64_t *x0, uint32_t xl, uint32_t leaf, uint32_t scan_size,
-                         uint8_t *recs, uint32_t *count_out, uint32_t lane) {
+                         uint8_t *recs, uint32_t *count_out, uint32_t lane, uint32_t rid = 0,
+                         uint8_t *row_status = nullptr) {
     uint32_t remaining = scan_size, produced = 0;
     bool cont = false;
     uint64_t x[KW];
@@ -490,7 +514,15 @@ __device__ void scan_one(const DevTable &t, const uint64_t *x0, uint32_t xl, uin
         for (int s = 0; s < SPL; ++s) {
             const bool emit = keep[s] && kr[s] < e;
             uint32_t img = 0;
-            if (emit) img = t.slot[base + s * 64 + lane].image;
+            if (emit) {
+                if (VIS) {
+                    uint8_t st;
+                    img = scan_visible(t, t.slot[base + s * 64 + lane], rid, st);
+                    row_status[produced + kr[s]] = st;
+                } else {
+                    img = t.slot[base + s * 64 + lane].image;
+                }
+            }
             uint64_t em = ballot(emit);
             while (em) {
                 uint32_t imr[R], dr[R];
@@ -528,10 +560,12 @@ __device__ void scan_one(const DevTable &t, const uint64_t *x0, uint32_t xl, uin
 
 // One wave per scan (grid-stride over scans): the start key's descent is wave-uniform, and a
 // wide grid keeps many scans -- and their R rows in flight each -- resident per CU.
-template <bool VARLEN, int SPL, int R, int KW = 1>
+template <bool VARLEN, int SPL, int R, int KW = 1, bool VIS = false>
 __global__ __launch_bounds__(256) void scan_kernel(DevTable t, const uint64_t *__restrict__ keys,
                                                    const uint16_t *__restrict__ lens, uint64_t n, uint32_t scan_size,
-                                                   uint32_t *__restrict__ counts, uint8_t *__restrict__ recs) {
+                                                   uint32_t *__restrict__ counts, uint8_t *__restrict__ recs,
+                                                   const uint32_t *__restrict__ rids = nullptr,
+                                                   uint8_t *__restrict__ row_status = nullptr) {
     const uint32_t lane = lane_id();
     const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
@@ -540,8 +574,9 @@ __global__ __launch_bounds__(256) void scan_kernel(DevTable t, const uint64_t *_
         uint64_t ok[KW];
         load_okey<KW>(keys, i, true, len, ok);
         const uint32_t leaf = uni32(resolve_leaf<VARLEN, KW>(t, ok, len, true));
-        scan_one<VARLEN, SPL, R, KW>(t, ok, len, leaf, scan_size, recs + i * (uint64_t)scan_size * t.stride,
-                                     counts + i, lane);
+        scan_one<VARLEN, SPL, R, KW, VIS>(t, ok, len, leaf, scan_size, recs + i * (uint64_t)scan_size * t.stride,
+                                          counts + i, lane, VIS ? (rids ? rids[i] : 0xFFFFFFFEu) : 0u,
+                                          VIS ? row_status + i * (uint64_t)scan_size : nullptr);
     }
 }
 
@@ -761,40 +796,54 @@ hipError_t launch_probe(const DevTable &t, const uint64_t *keys, const uint16_t 
     return hipGetLastError();
 }
 
-template <int KW>
+template <int KW, bool VIS>
 static void launch_scan_w(const DevTable &t, const uint64_t *keys, uint64_t n, uint32_t scan_size, uint32_t *counts,
-                          uint8_t *recs, hipStream_t s, int blocks) {
+                          uint8_t *recs, const uint32_t *rids, uint8_t *st, hipStream_t s, int blocks) {
+#define STAGE_SCAN_W(S) \
+    scan_kernel<false, S, 4, KW, VIS><<<blocks, 256, 0, s>>>(t, keys, nullptr, n, scan_size, counts, recs, rids, st)
     switch (t.cap / 64) {
-        case 1: scan_kernel<false, 1, 4, KW><<<blocks, 256, 0, s>>>(t, keys, nullptr, n, scan_size, counts, recs); break;
-        case 2: scan_kernel<false, 2, 4, KW><<<blocks, 256, 0, s>>>(t, keys, nullptr, n, scan_size, counts, recs); break;
-        case 4: scan_kernel<false, 4, 4, KW><<<blocks, 256, 0, s>>>(t, keys, nullptr, n, scan_size, counts, recs); break;
-        case 8: scan_kernel<false, 8, 4, KW><<<blocks, 256, 0, s>>>(t, keys, nullptr, n, scan_size, counts, recs); break;
-        default: scan_kernel<false, 16, 4, KW><<<blocks, 256, 0, s>>>(t, keys, nullptr, n, scan_size, counts, recs);
+        case 1: STAGE_SCAN_W(1); break;
+        case 2: STAGE_SCAN_W(2); break;
+        case 4: STAGE_SCAN_W(4); break;
+        case 8: STAGE_SCAN_W(8); break;
+        default: STAGE_SCAN_W(16);
     }
+#undef STAGE_SCAN_W
 }
 
-template <int R>
+template <int R, bool VIS>
 static void launch_scan_r(const DevTable &t, const uint64_t *keys, const uint16_t *lens, uint64_t n,
-                          uint32_t scan_size, uint32_t *counts, uint8_t *recs, hipStream_t s, int blocks) {
+                          uint32_t scan_size, uint32_t *counts, uint8_t *recs, const uint32_t *rids, uint8_t *st,
+                          hipStream_t s, int blocks) {
     const bool var = t.key_width == 0;
-    if (t.key_words == 2) return launch_scan_w<2>(t, keys, n, scan_size, counts, recs, s, blocks);
-    if (t.key_words == 4) return launch_scan_w<4>(t, keys, n, scan_size, counts, recs, s, blocks);
+    if (t.key_words == 2) return launch_scan_w<2, VIS>(t, keys, n, scan_size, counts, recs, rids, st, s, blocks);
+    if (t.key_words == 4) return launch_scan_w<4, VIS>(t, keys, n, scan_size, counts, recs, rids, st, s, blocks);
+#define STAGE_SCAN(V, S) \
+    scan_kernel<V, S, R, 1, VIS><<<blocks, 256, 0, s>>>(t, keys, lens, n, scan_size, counts, recs, rids, st)
     if (t.cap == 64) {
-        if (var) scan_kernel<true, 1, R><<<blocks, 256, 0, s>>>(t, keys, lens, n, scan_size, counts, recs);
-        else scan_kernel<false, 1, R><<<blocks, 256, 0, s>>>(t, keys, lens, n, scan_size, counts, recs);
+        if (var) STAGE_SCAN(true, 1);
+        else STAGE_SCAN(false, 1);
     } else {
-        if (var) scan_kernel<true, 2, R><<<blocks, 256, 0, s>>>(t, keys, lens, n, scan_size, counts, recs);
-        else scan_kernel<false, 2, R><<<blocks, 256, 0, s>>>(t, keys, lens, n, scan_size, counts, recs);
+        if (var) STAGE_SCAN(true, 2);
+        else STAGE_SCAN(false, 2);
     }
+#undef STAGE_SCAN
 }
 
 hipError_t launch_scan(const DevTable &t, const uint64_t *keys, const uint16_t *lens, uint64_t n, uint32_t scan_size,
-                       uint32_t *counts, uint8_t *recs, hipStream_t s, const ScanTuning &tune) {
+                       uint32_t *counts, uint8_t *recs, hipStream_t s, const ScanTuning &tune, const uint32_t *rids,
+                       uint8_t *row_status) {
     if (n == 0) return hipSuccess;
     const int blocks = grid_for(n, 4, tune.max_blocks > 0 ? tune.max_blocks : 16384);
-    if (tune.rows == 8) launch_scan_r<8>(t, keys, lens, n, scan_size, counts, recs, s, blocks);
-    else if (tune.rows == 2) launch_scan_r<2>(t, keys, lens, n, scan_size, counts, recs, s, blocks);
-    else launch_scan_r<4>(t, keys, lens, n, scan_size, counts, recs, s, blocks);
+    if (row_status) {  // IndexScanExecutor range branch: per-record visibility
+        launch_scan_r<4, true>(t, keys, lens, n, scan_size, counts, recs, rids, row_status, s, blocks);
+    } else if (tune.rows == 8) {
+        launch_scan_r<8, false>(t, keys, lens, n, scan_size, counts, recs, nullptr, nullptr, s, blocks);
+    } else if (tune.rows == 2) {
+        launch_scan_r<2, false>(t, keys, lens, n, scan_size, counts, recs, nullptr, nullptr, s, blocks);
+    } else {
+        launch_scan_r<4, false>(t, keys, lens, n, scan_size, counts, recs, nullptr, nullptr, s, blocks);
+    }
     return hipGetLastError();
 }
 

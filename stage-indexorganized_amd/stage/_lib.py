@@ -55,6 +55,9 @@ SIGNATURES = {
     "stage_delete_key": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint16, ctypes.c_uint32, c_u8p]),
     "stage_key_words": (ctypes.c_uint32, [c_vp]),
     "stage_sync": (ctypes.c_int, [c_vp]),
+    "stage_tpcc_stock_level": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_uint64, c_vp, c_vp]),
+    "stage_index_scan_batch": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, ctypes.c_uint64, ctypes.c_uint32, c_vp, c_vp,
+                                              c_vp, c_vp]),
     "stage_set_shard_chunks": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "stage_probe_sharded_loopback": (ctypes.c_int, [c_vp, ctypes.c_int, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_int,
                                                     c_vp]),

@@ -383,6 +383,26 @@ class Table:
         rows = d_rec.to_numpy(np.uint8, n * scan_size * self.stride).reshape(n, scan_size, self.stride)
         return counts, rows
 
+    def index_scan(self, start_keys, scan_size, read_ids=None, lens=None):
+        """IndexScanExecutor range branch: (counts[n], rows[n, scan_size, stride], status[n, scan_size])."""
+        keys, n = self.key_buffer(start_keys)
+        d_keys = DeviceBuffer.from_numpy(keys)
+        d_lens = DeviceBuffer.from_numpy(np.ascontiguousarray(lens, np.uint16)) if lens is not None else None
+        d_rid = DeviceBuffer.from_numpy(np.ascontiguousarray(read_ids, np.uint32)) if read_ids is not None else None
+        d_cnt = DeviceBuffer(n * 4)
+        d_rec = DeviceBuffer(max(1, n * scan_size * self.stride))
+        d_st = DeviceBuffer(max(1, n * scan_size))
+        d_rec.memset(0)
+        d_st.memset(0)
+        check(lib().stage_index_scan_batch(self.h, d_keys.ptr, d_lens.ptr if d_lens else None,
+                                           d_rid.ptr if d_rid else None, n, scan_size, d_cnt.ptr, d_rec.ptr,
+                                           d_st.ptr, None), "stage_index_scan_batch")
+        check(lib().stage_device_sync(), "sync")
+        counts = d_cnt.to_numpy(np.uint32, n)
+        rows = d_rec.to_numpy(np.uint8, n * scan_size * self.stride).reshape(n, scan_size, self.stride)
+        st = d_st.to_numpy(np.uint8, n * scan_size).reshape(n, scan_size)
+        return counts, rows, st
+
     def resolve(self, keys, lens=None, le_child=True):
         keys, n = self.key_buffer(keys)
         d_keys = DeviceBuffer.from_numpy(keys)

@@ -42,6 +42,7 @@ _SIG = {
     "orc_export_leaf_images": (ctypes.c_int64, [vp, u64, vp, vp, vp]),
     "orc_export_leaf_images_k": (ctypes.c_int64, [vp, u64, vp, vp, u32, vp]),
     "orc_tree_set_key_pad": (None, [vp, u32]),
+    "orc_index_scan": (u32, [vp, vp, u32, u32, u32, vp, vp]),
     "orc_read_batch_k": (ctypes.c_int, [vp, vp, u32, u32, vp, u64, vp, vp, ctypes.c_int]),
     "orc_scan_batch_k": (u64, [vp, vp, u32, u32, u64, u32, vp, vp, ctypes.c_int]),
     "orc_key_compare": (ctypes.c_int, [vp, u32, vp, u32]),
@@ -143,6 +144,14 @@ class OracleTree:
         lib().orc_scan_batch_k(self.t, keys.ctypes.data, keys.shape[1], keys.shape[1], n, scan_size,
                                counts.ctypes.data, recs.ctypes.data, nthreads)
         return counts, recs
+
+    def index_scan(self, key, key_size, scan_size, read_id):
+        """IndexScanExecutor range branch: (consumed, rows[consumed], status[consumed])"""
+        kb = key_bytes(key, key_size)
+        recs = np.zeros((max(scan_size, 1), self.row), np.uint8)
+        st = np.zeros(max(scan_size, 1), np.uint8)
+        c = lib().orc_index_scan(self.t, kb, key_size, scan_size, read_id, recs.ctypes.data, st.ctypes.data)
+        return c, recs[:c], st[:c]
 
     def scan(self, key, key_size, scan_size):
         kb = key_bytes(key, key_size)
