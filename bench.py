@@ -60,7 +60,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=None)
     p.add_argument("--warmup", type=int, default=None)
-    p.add_argument("--config", choices=["c2", "c3", "c4"], default="c2")
+    p.add_argument("--config", choices=["c2", "c3", "c4", "tpcc"], default="c2")
+    p.add_argument("--warehouses", type=int, default=16, help="tpcc: warehouses (10 districts, 3000 orders each)")
+    p.add_argument("--items", type=int, default=100_000, help="tpcc: items (stock rows per warehouse)")
     p.add_argument("--rows", type=int, default=100_000_000, help="rows per GPU")
     p.add_argument("--batch", type=int, default=None, help="lookups (c2/c3) or scans (c4) per GPU per step")
     p.add_argument("--theta", type=float, default=None)
@@ -77,7 +79,9 @@ def parse():
     a.steps = a.steps if a.steps is not None else (5 if a.config == "c3" else 20)
     a.warmup = a.warmup if a.warmup is not None else (1 if a.config == "c3" else 3)
     a.theta = a.theta if a.theta is not None else (0.99 if a.config == "c3" else 0.9)
-    a.batch = a.batch if a.batch is not None else ((1 << 18) if a.config == "c4" else (1 << 24))
+    a.batch = a.batch if a.batch is not None else ((1 << 18) if a.config in ("c4", "tpcc") else (1 << 24))
+    if a.config == "tpcc":
+        a.steps = a.steps if a.steps is not None else 10
     return a
 
 
@@ -197,8 +201,136 @@ class YcsbB:
         return reads, rids
 
 
+def tpcc_tables(args, seed=7):
+    """DISTRICT / ORDER_LINE / STOCK rows with the reference's key and payload layouts
+    (tpcc_record.h), generated vectorised: W warehouses x 10 districts x 3000 orders of 5..15
+    lines, `items` stock rows per warehouse.  First payload columns: D_NEXT_O_ID, OL_I_ID,
+    S_QUANTITY (int32)."""
+    rng = np.random.default_rng(seed)
+    W, I, D, O = args.warehouses, args.items, 10, 3000
+    out = {}
+    wi = np.stack(np.meshgrid(np.arange(1, W + 1), np.arange(1, I + 1), indexing="ij"), -1).reshape(-1, 2)
+    sk = np.ascontiguousarray(wi.astype(np.int64)).view(np.uint8).reshape(-1, 16)
+    sp = rng.integers(0, 256, (sk.shape[0], 400), dtype=np.uint8)
+    sp[:, :4] = rng.integers(10, 101, sk.shape[0]).astype(np.int32).view(np.uint8).reshape(-1, 4)
+    out["stock"] = (sk, sp)
+    wd = np.stack(np.meshgrid(np.arange(1, W + 1), np.arange(1, D + 1), indexing="ij"), -1).reshape(-1, 2)
+    dk = np.ascontiguousarray(wd.astype(np.int64)).view(np.uint8).reshape(-1, 16)
+    dp = rng.integers(0, 256, (dk.shape[0], 143), dtype=np.uint8)
+    dp[:, :4] = np.full(dk.shape[0], O + 1, np.int32).view(np.uint8).reshape(-1, 4)
+    out["district"] = (dk, dp)
+    wdo = np.stack(np.meshgrid(np.arange(1, W + 1), np.arange(1, D + 1), np.arange(1, O + 1), indexing="ij"),
+                   -1).reshape(-1, 3)
+    nl = rng.integers(5, 16, wdo.shape[0])
+    rep = np.repeat(wdo, nl, axis=0)
+    ln = np.arange(rep.shape[0]) - np.repeat(np.cumsum(nl) - nl, nl) + 1
+    ok = np.ascontiguousarray(np.concatenate([rep, ln[:, None]], 1).astype(np.int64)).view(np.uint8).reshape(-1, 32)
+    op = rng.integers(0, 256, (ok.shape[0], 60), dtype=np.uint8)
+    op[:, :4] = rng.integers(1, I + 1, ok.shape[0]).astype(np.int32).view(np.uint8).reshape(-1, 4)
+    out["order_line"] = (ok, op)
+    return out
+
+
+def run_tpcc(args):
+    """TPC-C stock-level through the path (stage_tpcc_stock_level), one GPU."""
+    L = stage.lib()
+    t0 = time.time()
+    data = tpcc_tables(args)
+    gen_s = time.time() - t0
+    widths = {"district": (16, 143), "order_line": (32, 60), "stock": (16, 400)}
+    tabs = {}
+    t0 = time.time()
+    for name, (k, p) in data.items():
+        t = stage.Table(payload_size=widths[name][1], key_width=widths[name][0])
+        _, ins = t.load_rows(k, p)
+        assert ins == k.shape[0]
+        tabs[name] = t
+    load_s = time.time() - t0
+    t0 = time.time()
+    for t in tabs.values():
+        t.sync()
+    sync_s = time.time() - t0
+    B = args.batch
+    rng = np.random.default_rng(args.seed)
+    w = rng.integers(1, args.warehouses + 1, B).astype(np.int64)
+    d = rng.integers(1, 11, B).astype(np.int64)
+    thr = rng.integers(10, 21, B).astype(np.int32)  # stock_min/max_threshold
+    dw, dd, dt = (stage.DeviceBuffer.from_numpy(x) for x in (w, d, thr))
+    dres = stage.DeviceBuffer(4 * B)
+    stream = stage.Stream()
+
+    def step():
+        check(L.stage_tpcc_stock_level(tabs["district"].h, tabs["order_line"].h, tabs["stock"].h, dw.ptr, dd.ptr,
+                                       dt.ptr, None, B, dres.ptr, stream.ptr), "stock level")
+
+    for _ in range(args.warmup):
+        step()
+    stream.sync()
+    t0 = time.perf_counter()
+    ev0, ev1 = stage.Event(), stage.Event()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    stream.sync()
+    elapsed = time.perf_counter() - t0
+    ms = ev0.elapsed_ms(ev1) / args.steps
+    res = dres.to_numpy(np.int32, B)
+    value = B * args.steps / elapsed
+    # algorithmic bytes per transaction: a point probe moves key + 64 (leaf head line) + 16
+    # (slot word) + row in + row out + status; a 10-record scan key + 2 x 64 (key planes) +
+    # 10 x (row in + row out + status)
+    probe = lambda kb, row: kb + 64 + 16 + 2 * row + 4
+    per_txn = probe(16, 16 + 143) + 20 * (32 + 128 + 10 * (2 * (32 + 60) + 1)) + 20 * probe(16, 16 + 400)
+    achieved = per_txn * B / (ms * 1e-3) / 1e9
+    cpu = None
+    if not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        import oracle_lib as O
+        t1 = time.time()
+        orcs = {}
+        for name, (k, p) in data.items():
+            o = O.OracleTree(payload_size=widths[name][1], key_pad=widths[name][0])
+            o.load_rows(k, p)
+            orcs[name] = o
+        build = time.time() - t1
+        threads = min(16, os.cpu_count() or 8)
+        n0 = 20_000
+        r0, sec = O.stock_level_batch(orcs["district"], orcs["order_line"], orcs["stock"], w[:n0], d[:n0], thr[:n0],
+                                      None, threads)
+        assert (r0 == res[:n0]).all(), "stock-level results differ from the oracle"
+        n1 = int(min(B, max(n0, n0 / max(sec, 1e-9) * args.cpu_seconds)))
+        r1, sec = O.stock_level_batch(orcs["district"], orcs["order_line"], orcs["stock"], w[:n1], d[:n1], thr[:n1],
+                                      None, threads)
+        cpu = {"value": round(n1 / sec, 1), "unit": "txns/s", "cores": threads, "kind": "port",
+               "sample": f"oracle orc_stock_level (DISTRICT read, 20 IndexScanExecutor range scans, STOCK reads), "
+                         f"{n1} txns, same tables (build {build:.1f}s), {threads} threads on {cpu_name()}, {sec:.1f}s"}
+        del orcs
+    result = {
+        "metric": "TPC-C stock-level txns/s through the index-organized path (supplementary to "
+                  + METRIC + ")",
+        "value": round(value, 1), "unit": "txns/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "int64 keys / bytes", "data": "synthetic TPC-C rows (tpcc_record.h layouts)",
+        "config": {"workload": "TPC-C stock-level (tpcc_stock_level.cpp), batched", "warehouses": args.warehouses,
+                   "items": args.items, "districts_per_wh": 10, "orders_per_district": 3000,
+                   "order_lines": int(data["order_line"][0].shape[0]), "txns_per_step": B,
+                   "aborted": int((res < 0).sum()), "mean_low_stock": round(float(res[res >= 0].mean()), 3)},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": "stock-level step (district probe + 20 index scans + 20 stock probes)",
+                     "algorithmic_bytes_per_unit": per_txn, "units_per_launch": B, "avg_launch_ms": round(ms, 4)},
+        "cpu_baseline": cpu, "self_check": bool((res >= -1).all()),
+        "setup_s": {"generate": round(gen_s, 1), "load": round(load_s, 1), "sync": round(sync_s, 1)},
+    }
+    print(json.dumps(result), flush=True)
+    return 0
+
+
 def main():
     args = parse()
+    if args.config == "tpcc":
+        return run_tpcc(args)
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))

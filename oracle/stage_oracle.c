@@ -631,6 +631,16 @@ uint64_t orc_load_keys(orc_tree *t, const uint64_t *keys, uint64_t n, uint32_t k
     return ok;
 }
 
+uint64_t orc_load_rows(orc_tree *t, const uint8_t *keys, uint32_t key_stride, uint32_t key_size,
+                       const uint8_t *payloads, uint32_t payload_stride, uint64_t n) {
+    uint64_t ok = 0;
+    for (uint64_t i = 0; i < n; i++)
+        if (orc_insert(t, keys + i * key_stride, key_size, payloads + i * (uint64_t)payload_stride, INVALID_CID) ==
+            ORC_RET_OK)
+            ok++;
+    return ok;
+}
+
 uint64_t orc_load_ycsb(orc_tree *t, uint64_t begin, uint64_t end, uint32_t key_size, int payload_mode) {
     uint8_t *payload = xmalloc(t->payload_size + 8);
     uint64_t ok = 0;
@@ -1340,4 +1350,87 @@ uint64_t orc_murmur64a(const void *key, int len, uint64_t seed) {
 
 void orc_murmur64a_batch(const uint64_t *keys, uint64_t n, int len, uint64_t seed, uint64_t *out) {
     for (uint64_t i = 0; i < n; i++) out[i] = orc_murmur64a(&keys[i], len, seed);
+}
+
+/* ---------------------------------------------------------------- TPC-C stock-level */
+/* tpcc_stock_level.cpp:37-180 over DISTRICT / ORDER_LINE / STOCK trees (keys of int64
+ * fields, payloads starting with D_NEXT_O_ID / OL_I_ID / S_QUANTITY as int32):
+ * returns the number of distinct S_I_IDs below the threshold, -1 if the transaction aborts. */
+static int32_t rd_i32(const uint8_t *p) { int32_t v; memcpy(&v, p, 4); return v; }
+static int64_t rd_i64(const uint8_t *p) { int64_t v; memcpy(&v, p, 8); return v; }
+
+int32_t orc_stock_level(orc_tree *dist, orc_tree *ol, orc_tree *stock, int64_t w, int64_t d, int32_t threshold,
+                        uint32_t read_id) {
+    orc_read_out o;
+    uint8_t drow[16 + 4096], srow[16 + 4096], olrows[10 * (32 + 4096)], st[10];
+    int64_t dk[2] = {w, d};
+    read_one(dist, (const uint8_t *)dk, 16, read_id, &o, drow);
+    if (o.status != ORC_ST_LATEST && o.status != ORC_ST_COPY && o.status != ORC_ST_OLD) return -1;
+    int32_t next = rd_i32(drow + dist->key_pad);
+    int32_t items[20];
+    int nitems = 0;
+    uint32_t ors = ol->key_pad + ol->payload_size;
+    scanrec_t *buf = xmalloc(sizeof(scanrec_t) * 4096);
+    for (int32_t oid = next - 20; oid < next; oid++) {
+        int64_t ok[4] = {w, d, oid, 5};
+        uint32_t c = scan_one_ex(ol, (const uint8_t *)ok, 32, 10, olrows, buf, 4096, read_id, st);
+        int found = 0;
+        int32_t item = 0;
+        for (uint32_t j = 0; j < c && !found; j++) {
+            if (st[j] != ORC_ST_LATEST && st[j] != ORC_ST_OLD) continue;
+            const uint8_t *r = olrows + (uint64_t)j * ors;
+            if (rd_i64(r + 16) == oid && rd_i64(r) == w && rd_i64(r + 8) == d) {
+                found = 1;
+                item = rd_i32(r + ol->key_pad);
+            }
+        }
+        if (!found) continue;
+        int64_t sk[2] = {w, item};
+        read_one(stock, (const uint8_t *)sk, 16, read_id, &o, srow);
+        if (o.status == ORC_ST_FAIL_INVALID_TS) { free(buf); return -1; }
+        if (o.status != ORC_ST_LATEST && o.status != ORC_ST_COPY && o.status != ORC_ST_OLD) continue;
+        if (rd_i32(srow + stock->key_pad) < threshold) {
+            int32_t sid = (int32_t)rd_i64(srow + 8), dup = 0;
+            for (int k = 0; k < nitems; k++) dup |= items[k] == sid;
+            if (!dup) items[nitems++] = sid;
+        }
+    }
+    free(buf);
+    return nitems;
+}
+
+typedef struct {
+    orc_tree *dist, *ol, *stock;
+    const int64_t *w, *d;
+    const int32_t *thr;
+    const uint32_t *rid;
+    int32_t *res;
+    uint64_t b, e;
+} sl_job_t;
+
+static void *sl_worker(void *arg) {
+    sl_job_t *j = arg;
+    for (uint64_t i = j->b; i < j->e; i++)
+        j->res[i] = orc_stock_level(j->dist, j->ol, j->stock, j->w[i], j->d[i], j->thr[i],
+                                    j->rid ? j->rid[i] : 0xFFFFFFFEu);
+    return NULL;
+}
+
+void orc_stock_level_batch(orc_tree *dist, orc_tree *ol, orc_tree *stock, const int64_t *w, const int64_t *d,
+                           const int32_t *thr, const uint32_t *rid, uint64_t n, int32_t *res, int nthreads,
+                           double *seconds) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    sl_job_t jobs[256];
+    struct timespec a, b;
+    clock_gettime(CLOCK_MONOTONIC, &a);
+    for (int i = 0; i < nthreads; i++) {
+        jobs[i] = (sl_job_t){dist, ol, stock, w, d, thr, rid, res, n * (uint64_t)i / nthreads,
+                             n * (uint64_t)(i + 1) / nthreads};
+        pthread_create(&th[i], NULL, sl_worker, &jobs[i]);
+    }
+    for (int i = 0; i < nthreads; i++) pthread_join(th[i], NULL);
+    clock_gettime(CLOCK_MONOTONIC, &b);
+    if (seconds) *seconds = (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
 }

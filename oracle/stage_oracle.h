@@ -123,6 +123,15 @@ int64_t orc_export_leaf_images_k(orc_tree *t, uint64_t max_leaves, uint8_t *bloc
  * 0 nothing (row zeroed).  Returns the number of iterator records consumed. */
 uint32_t orc_index_scan(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t scan_size, uint32_t read_id,
                         uint8_t *recs, uint8_t *status);
+/* bulk insert of explicit rows (key i at keys + i*key_stride, payload i at payloads + i*payload_stride) */
+uint64_t orc_load_rows(orc_tree *t, const uint8_t *keys, uint32_t key_stride, uint32_t key_size,
+                       const uint8_t *payloads, uint32_t payload_stride, uint64_t n);
+/* TPC-C stock-level (tpcc_stock_level.cpp:37-180): distinct items below threshold, -1 = abort */
+int32_t orc_stock_level(orc_tree *dist, orc_tree *ol, orc_tree *stock, int64_t w, int64_t d, int32_t threshold,
+                        uint32_t read_id);
+void orc_stock_level_batch(orc_tree *dist, orc_tree *ol, orc_tree *stock, const int64_t *w, const int64_t *d,
+                           const int32_t *thr, const uint32_t *rid, uint64_t n, int32_t *res, int nthreads,
+                           double *seconds);
 /* canonical tuple rows [key padded to key_pad][payload]; default 8 (keys of <= 8 bytes) */
 void orc_tree_set_key_pad(orc_tree *t, uint32_t key_pad);
 /* batch forms over byte keys (key i at keys + i*key_stride) */

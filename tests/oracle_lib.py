@@ -43,6 +43,10 @@ _SIG = {
     "orc_export_leaf_images_k": (ctypes.c_int64, [vp, u64, vp, vp, u32, vp]),
     "orc_tree_set_key_pad": (None, [vp, u32]),
     "orc_index_scan": (u32, [vp, vp, u32, u32, u32, vp, vp]),
+    "orc_load_rows": (u64, [vp, vp, u32, u32, vp, u32, u64]),
+    "orc_stock_level": (ctypes.c_int32, [vp, vp, vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, u32]),
+    "orc_stock_level_batch": (None, [vp, vp, vp, vp, vp, vp, vp, u64, vp, ctypes.c_int,
+                                     ctypes.POINTER(ctypes.c_double)]),
     "orc_read_batch_k": (ctypes.c_int, [vp, vp, u32, u32, vp, u64, vp, vp, ctypes.c_int]),
     "orc_scan_batch_k": (u64, [vp, vp, u32, u32, u64, u32, vp, vp, ctypes.c_int]),
     "orc_key_compare": (ctypes.c_int, [vp, u32, vp, u32]),
@@ -123,6 +127,12 @@ class OracleTree:
         lib().orc_read_batch(self.t, keys.ctypes.data, key_size, rids.ctypes.data if rids is not None else None, n,
                              outs.ctypes.data, recs.ctypes.data if recs is not None else None, nthreads)
         return outs, recs
+
+    def load_rows(self, keys, payloads):
+        keys = np.ascontiguousarray(keys, np.uint8)
+        payloads = np.ascontiguousarray(payloads, np.uint8)
+        return lib().orc_load_rows(self.t, keys.ctypes.data, keys.shape[1], keys.shape[1], payloads.ctypes.data,
+                                   payloads.shape[1], keys.shape[0])
 
     def read_batch_k(self, keys, read_ids=None, records=True, nthreads=8):
         """keys: (n, width) uint8 key bytes"""
@@ -208,6 +218,20 @@ class OracleTree:
                                       keyw.ctypes.data)
         assert got == nl
         return rc, sc, meta.reshape(nl, cap), keyw.reshape(nl, cap)
+
+
+def stock_level_batch(dist, ol, stock, w, d, thr, rids=None, nthreads=8):
+    """TPC-C stock-level over three oracle trees; returns (results, seconds)."""
+    w = np.ascontiguousarray(w, np.int64)
+    d = np.ascontiguousarray(d, np.int64)
+    thr = np.ascontiguousarray(thr, np.int32)
+    r = None if rids is None else np.ascontiguousarray(rids, np.uint32)
+    res = np.zeros(w.size, np.int32)
+    sec = ctypes.c_double()
+    lib().orc_stock_level_batch(dist.t, ol.t, stock.t, w.ctypes.data, d.ctypes.data, thr.ctypes.data,
+                                r.ctypes.data if r is not None else None, w.size, res.ctypes.data, nthreads,
+                                ctypes.byref(sec))
+    return res, sec.value
 
 
 def key_compare(k1, k2):
