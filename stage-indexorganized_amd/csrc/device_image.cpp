@@ -59,7 +59,7 @@ static void upload(DevBuf &b, const void *src, uint64_t bytes, hipStream_t s, co
 // order.  okey points at the leaf's KW planes of cap words.
 static void build_leaf(const HostTable &h, uint32_t hl, uint8_t *hd, uint64_t *okey, SlotInfo *slot) {
     const stage_params &p = h.params();
-    const uint32_t cap = h.cap(), spl = cap / 64, hb = leaf_head_bytes(cap), kw = h.key_words();
+    const uint32_t kw = h.key_words(), cap = h.cap(), spl = cap / 64, hb = leaf_head_bytes(cap, kw);
     const uint64_t hbase = (uint64_t)hl * cap;
     const uint32_t count = h.leaves_[hl].count;
     std::memset(hd, 0, hb);
@@ -82,6 +82,23 @@ static void build_leaf(const HostTable &h, uint32_t hl, uint8_t *hd, uint64_t *o
         }
     }
     std::memcpy(hd + cap, vis, 8 * spl);
+    // group max keys over live slots (lexicographic on the order words)
+    uint64_t *gm = reinterpret_cast<uint64_t *>(hd + head_gmax_offset(cap));
+    for (uint32_t g = 0; g < spl; ++g) {
+        uint64_t best[kMaxKeyWords] = {0, 0, 0, 0};
+        for (uint32_t s = g * 64; s < g * 64 + 64 && s < count; ++s) {
+            const uint64_t *w = h.okey_.data() + (hbase + s) * kw;
+            bool gt = false;
+            for (uint32_t j = 0; j < kw; ++j)
+                if (w[j] != best[j]) {
+                    gt = w[j] > best[j];
+                    break;
+                }
+            if (gt)
+                for (uint32_t j = 0; j < kw; ++j) best[j] = w[j];
+        }
+        for (uint32_t j = 0; j < kw; ++j) std::memcpy(gm + g * kw + j, &best[j], 8);
+    }
 }
 
 // Copy/version headers: append the new tail, re-send the rewritten range of copy headers.
@@ -117,7 +134,7 @@ static void sync_headers(HostTable &h, DeviceImage &d, hipStream_t s) {
 // Incremental publish (no split since the last publish): leaf order and separators are
 // unchanged, so only the written slots and their leaves' heads are patched in place.
 static void patch_device(HostTable &h, DeviceImage &d, hipStream_t s) {
-    const uint32_t cap = h.cap(), hb = leaf_head_bytes(cap);
+    const uint32_t cap = h.cap(), hb = leaf_head_bytes(cap, h.key_words());
     std::vector<uint64_t> &ds = h.dirty_slots_;
     std::sort(ds.begin(), ds.end());
     ds.erase(std::unique(ds.begin(), ds.end()), ds.end());
@@ -266,7 +283,7 @@ void sync_device(HostTable &h, DeviceImage &d) {
     d.host_to_dev.assign(h.leaves_.size(), 0xFFFFFFFFu);
     for (uint64_t i = 0; i < L; ++i) d.host_to_dev[order[i]] = (uint32_t)i;
 
-    const uint32_t hb = leaf_head_bytes(cap), kw = h.key_words();
+    const uint32_t kw = h.key_words(), hb = leaf_head_bytes(cap, kw);
     std::vector<uint64_t> okey(L * cap * kw);
     std::vector<uint8_t> head(L * hb, 0);
     std::vector<SlotInfo> slot(L * cap);

@@ -558,6 +558,152 @@ __device__ void scan_one(const DevTable &t, const uint64_t *x0, uint32_t xl, uin
     if (lane == 0) *count_out = produced;
 }
 
+// Range scan for leaves of many slot groups (wide-key tables, up to 1024 slots) and scans of
+// at most 63 records: RangeScanBySize's collection (first to_scan+1 qualifying records in slot
+// order) walks only the slot groups whose max key (leaf head) reaches the start key and stops
+// as soon as to_scan+1 records are held; the kept records (<= 64) go to a per-wave LDS list,
+// one lane per record ranks them (std::sort) and they are emitted as in scan_one.
+template <bool VARLEN, int SPL, int KW, bool VIS>
+__device__ void scan_one_compact(const DevTable &t, const uint64_t *x0, uint32_t xl, uint32_t leaf,
+                                 uint32_t scan_size, uint8_t *recs, uint32_t *count_out, uint32_t lane, uint32_t rid,
+                                 uint8_t *row_status, uint64_t *lk, uint32_t *ll, uint32_t *ls) {
+    uint32_t remaining = scan_size, produced = 0;
+    bool cont = false;
+    uint64_t x[KW];
+#pragma unroll
+    for (int w = 0; w < KW; ++w) x[w] = x0[w];
+    for (uint32_t guard = 0; guard < scan_size + 2 && remaining > 0; ++guard) {
+        const uint64_t base = (uint64_t)leaf * t.cap;
+        const uint8_t *hd = t.head + (uint64_t)leaf * t.head_bytes;
+        // slot groups that can hold a key >= x (lane g tests group g's max key)
+        bool act = false;
+        if (lane < (uint32_t)SPL) {
+            const uint64_t *gm = reinterpret_cast<const uint64_t *>(hd + head_gmax_offset(t.cap)) + lane * KW;
+            uint64_t g[KW];
+#pragma unroll
+            for (int w = 0; w < KW; ++w) g[w] = gm[w];
+            act = !kw_lt<KW>(g, x);
+        }
+        uint64_t active = ballot(act);
+        const uint32_t to_scan = remaining;
+        uint32_t kept = 0;
+        while (active) {
+            const int s = __builtin_ctzll(active);
+            active &= active - 1;
+            const uint64_t vm = head_vis(t, leaf, s);
+            if (!vm) continue;
+            const bool vis = (vm >> lane) & 1;
+            uint64_t col[KW];
+#pragma unroll
+            for (int w = 0; w < KW; ++w) col[w] = t.okey[((uint64_t)leaf * KW + w) * t.cap + s * 64 + lane];
+            uint32_t kl = t.key_width;
+            if (VARLEN) kl = vis ? meta_keylen(t.slot[base + s * 64 + lane].meta) : 0u;
+            const uint64_t q = ballot(vis && !key_less<VARLEN, KW>(col, kl, x, xl));
+            if (!q) continue;
+            const uint32_t rank = kept + count_below(q);
+            const bool take = ((q >> lane) & 1) && rank <= to_scan;
+            if (take) {
+#pragma unroll
+                for (int w = 0; w < KW; ++w) lk[rank * KW + w] = col[w];
+                ll[rank] = kl;
+                ls[rank] = (uint32_t)(s * 64) + lane;
+            }
+            kept += (uint32_t)__builtin_popcountll(ballot(take));
+            if (kept > to_scan) break;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t m = kept;
+        if (m == 0) break;
+        // lane k < m holds kept record k; its rank among the kept records = position after sort
+        const bool mine = lane < m;
+        uint64_t mk[KW];
+        uint32_t ml = 0, mslot = 0;
+#pragma unroll
+        for (int w = 0; w < KW; ++w) mk[w] = mine ? lk[lane * KW + w] : 0ull;
+        if (mine) {
+            ml = ll[lane];
+            mslot = ls[lane];
+        }
+        uint32_t kr = 0;
+        for (uint32_t j = 0; j < m; ++j) {
+            uint64_t kj[KW];
+#pragma unroll
+            for (int w = 0; w < KW; ++w) kj[w] = lk[j * KW + w];
+            kr += (mine && key_less<VARLEN, KW>(kj, ll[j], mk, ml)) ? 1u : 0u;
+        }
+        __builtin_amdgcn_wave_barrier();  // the LDS list is rewritten on the next leaf
+        if (cont) {
+            bool eq = ml == xl;
+#pragma unroll
+            for (int w = 0; w < KW; ++w) eq = eq && mk[w] == x[w];
+            if (ballot(mine && kr == 0 && eq)) break;
+        }
+        const uint32_t e = m < remaining ? m : remaining;
+        const bool emit = mine && kr < e;
+        uint32_t img = 0;
+        if (emit) {
+            if (VIS) {
+                uint8_t st;
+                img = scan_visible(t, t.slot[base + mslot], rid, st);
+                row_status[produced + kr] = st;
+            } else {
+                img = t.slot[base + mslot].image;
+            }
+        }
+        uint64_t em = ballot(emit);
+        while (em) {
+            uint32_t imr[4], dr[4];
+            int nk = 0;
+            for (; nk < 4 && em; ++nk) {
+                const int b = __builtin_ctzll(em);
+                em &= em - 1;
+                imr[nk] = rl32(img, b);
+                dr[nk] = produced + rl32(kr, b);
+            }
+            copy_rows<4>(t, imr, dr, nk, recs, lane);
+        }
+        produced += e;
+        remaining -= e;
+        if (e < m) break;
+        // last record popped: re-traverse from its key with le_child = false
+        const uint64_t lm = ballot(mine && kr == m - 1);
+        const int b = __builtin_ctzll(lm);
+#pragma unroll
+        for (int w = 0; w < KW; ++w) x[w] = rl64(mk[w], b);
+        xl = rl32(ml, b);
+        leaf = uni32(resolve_leaf<VARLEN, KW>(t, x, xl, false));
+        cont = true;
+    }
+    if (lane == 0) *count_out = produced;
+}
+
+template <bool VARLEN, int SPL, int KW, bool VIS>
+__global__ __launch_bounds__(256) void scan_kernel_compact(DevTable t, const uint64_t *__restrict__ keys,
+                                                           const uint16_t *__restrict__ lens, uint64_t n,
+                                                           uint32_t scan_size, uint32_t *__restrict__ counts,
+                                                           uint8_t *__restrict__ recs,
+                                                           const uint32_t *__restrict__ rids,
+                                                           uint8_t *__restrict__ row_status) {
+    __shared__ uint64_t s_keys[4][64 * KW];
+    __shared__ uint32_t s_len[4][64], s_slot[4][64];
+    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    for (uint64_t i = wave; i < n; i += nwaves) {
+        const uint32_t len = t.key_width ? t.key_width : (lens ? (uint32_t)lens[i] : 8u);
+        uint64_t ok[KW];
+        load_okey<KW>(keys, i, true, len, ok);
+        const uint32_t leaf = uni32(resolve_leaf<VARLEN, KW>(t, ok, len, true));
+        scan_one_compact<VARLEN, SPL, KW, VIS>(t, ok, len, leaf, scan_size,
+                                               recs + i * (uint64_t)scan_size * t.stride, counts + i, lane,
+                                               VIS ? (rids ? rids[i] : 0xFFFFFFFEu) : 0u,
+                                               VIS ? row_status + i * (uint64_t)scan_size : nullptr, s_keys[wv],
+                                               s_len[wv], s_slot[wv]);
+    }
+}
+
 // One wave per scan (grid-stride over scans): the start key's descent is wave-uniform, and a
 // wide grid keeps many scans -- and their R rows in flight each -- resident per CU.
 template <bool VARLEN, int SPL, int R, int KW = 1, bool VIS = false>
@@ -799,6 +945,20 @@ hipError_t launch_probe(const DevTable &t, const uint64_t *keys, const uint16_t 
 template <int KW, bool VIS>
 static void launch_scan_w(const DevTable &t, const uint64_t *keys, uint64_t n, uint32_t scan_size, uint32_t *counts,
                           uint8_t *recs, const uint32_t *rids, uint8_t *st, hipStream_t s, int blocks) {
+    if (scan_size <= 63) {  // at most 64 kept records per leaf visit: group-skipping LDS form
+#define STAGE_SCAN_C(S)                                                                                        \
+    scan_kernel_compact<false, S, KW, VIS><<<blocks, 256, 0, s>>>(t, keys, nullptr, n, scan_size, counts, recs, \
+                                                                  rids, st)
+        switch (t.cap / 64) {
+            case 1: STAGE_SCAN_C(1); break;
+            case 2: STAGE_SCAN_C(2); break;
+            case 4: STAGE_SCAN_C(4); break;
+            case 8: STAGE_SCAN_C(8); break;
+            default: STAGE_SCAN_C(16);
+        }
+#undef STAGE_SCAN_C
+        return;
+    }
 #define STAGE_SCAN_W(S) \
     scan_kernel<false, S, 4, KW, VIS><<<blocks, 256, 0, s>>>(t, keys, nullptr, n, scan_size, counts, recs, rids, st)
     switch (t.cap / 64) {

@@ -103,7 +103,13 @@ struct alignas(32) SlotInfo {
 
 // 1-byte key fingerprint stored per slot in the leaf head
 STAGE_HD uint32_t key_fp(uint64_t okey) { return (uint32_t)((okey * 0x9E3779B97F4A7C15ull) >> 56); }
-STAGE_HD uint32_t leaf_head_bytes(uint32_t cap) { return (cap + cap / 8 + 127u) & ~127u; }
+// leaf head: [fp: cap bytes][visible masks: cap/8 bytes][group max keys: cap/64 x KW words],
+// 128-B multiple.  A group's max key (over its live slots) lets a range scan skip slot groups
+// that hold nothing >= its start key.
+STAGE_HD uint32_t head_gmax_offset(uint32_t cap) { return cap + cap / 8; }
+STAGE_HD uint32_t leaf_head_bytes(uint32_t cap, uint32_t kw) {
+    return (head_gmax_offset(cap) + (cap / 64) * kw * 8u + 127u) & ~127u;
+}
 
 struct alignas(16) CopyHdr {  // EphemeralPool::OverwriteVersionHeader (ephemeral_pool.h:26-150)
     uint32_t rstamp;          // old cstamp (lower bound of the copy's visibility)
