@@ -117,6 +117,44 @@ __device__ __forceinline__ uint32_t resolve_leaf(const DevTable &t, const uint64
     return tree_lower_bound<VARLEN, KW>(t, s, len);
 }
 
+// Wave-cooperative descent for a wave-uniform key (range scans): per level, lane e < 16 loads
+// separator e of the node and one ballot counts the separators below the key -- one load
+// round per level instead of every lane reading the whole node.
+template <bool VARLEN, int KW>
+__device__ __forceinline__ uint32_t tree_lower_bound_uniform(const DevTable &t, const uint64_t *x, uint32_t xl,
+                                                             uint32_t lane) {
+    uint32_t node = 0;
+    for (int lvl = (int)t.levels - 1; lvl >= 0; --lvl) {
+        const uint64_t off = t.level_off[lvl] + (uint64_t)node * kTreeFanout;
+        bool lt = false;
+        if (lane < (uint32_t)kTreeFanout) {
+            uint64_t e[KW];
+#pragma unroll
+            for (int j = 0; j < KW; ++j) e[j] = t.tree[(off + lane) * KW + j];
+            if (KW == 1) lt = VARLEN ? kv_lt(e[0], t.tree_len[off + lane], x[0], xl) : e[0] < x[0];
+            else lt = kw_lt<KW>(e, x);
+        }
+        node = node * kTreeFanout + (uint32_t)__builtin_popcountll(ballot(lt));
+    }
+    return node < t.nseps ? node : t.nseps;
+}
+
+template <bool VARLEN, int KW>
+__device__ __forceinline__ uint32_t resolve_leaf_uniform(const DevTable &t, const uint64_t *okey, uint32_t len,
+                                                         bool le_child, uint32_t lane) {
+    if (le_child) return tree_lower_bound_uniform<VARLEN, KW>(t, okey, len, lane);
+    if (VARLEN) return tree_lower_bound_uniform<VARLEN, KW>(t, okey, len + 1, lane);
+    uint64_t s[KW];
+    bool carry = true;
+#pragma unroll
+    for (int j = KW - 1; j >= 0; --j) {
+        s[j] = okey[j] + (carry ? 1ull : 0ull);
+        carry = carry && okey[j] == ~0ull;
+    }
+    if (carry) return t.nseps;
+    return tree_lower_bound_uniform<VARLEN, KW>(t, s, len, lane);
+}
+
 // order words of a key passed as KW little-endian u64 words (fixed width) or one word
 template <int KW>
 __device__ __forceinline__ void load_okey(const uint64_t *keys, uint64_t i, bool valid, uint32_t len, uint64_t *okw) {
@@ -552,7 +590,7 @@ __device__ void scan_one(const DevTable &t, const uint64_t *x0, uint32_t xl, uin
             }
         }
         xl = lastl;
-        leaf = uni32(resolve_leaf<VARLEN, KW>(t, x, xl, false));
+        leaf = uni32(resolve_leaf_uniform<VARLEN, KW>(t, x, xl, false, lane));
         cont = true;
     }
     if (lane == 0) *count_out = produced;
@@ -673,7 +711,7 @@ __device__ void scan_one_compact(const DevTable &t, const uint64_t *x0, uint32_t
 #pragma unroll
         for (int w = 0; w < KW; ++w) x[w] = rl64(mk[w], b);
         xl = rl32(ml, b);
-        leaf = uni32(resolve_leaf<VARLEN, KW>(t, x, xl, false));
+        leaf = uni32(resolve_leaf_uniform<VARLEN, KW>(t, x, xl, false, lane));
         cont = true;
     }
     if (lane == 0) *count_out = produced;
@@ -695,7 +733,7 @@ __global__ __launch_bounds__(256) void scan_kernel_compact(DevTable t, const uin
         const uint32_t len = t.key_width ? t.key_width : (lens ? (uint32_t)lens[i] : 8u);
         uint64_t ok[KW];
         load_okey<KW>(keys, i, true, len, ok);
-        const uint32_t leaf = uni32(resolve_leaf<VARLEN, KW>(t, ok, len, true));
+        const uint32_t leaf = uni32(resolve_leaf_uniform<VARLEN, KW>(t, ok, len, true, lane));
         scan_one_compact<VARLEN, SPL, KW, VIS>(t, ok, len, leaf, scan_size,
                                                recs + i * (uint64_t)scan_size * t.stride, counts + i, lane,
                                                VIS ? (rids ? rids[i] : 0xFFFFFFFEu) : 0u,
@@ -719,7 +757,7 @@ __global__ __launch_bounds__(256) void scan_kernel(DevTable t, const uint64_t *_
         const uint32_t len = t.key_width ? t.key_width : (lens ? (uint32_t)lens[i] : 8u);
         uint64_t ok[KW];
         load_okey<KW>(keys, i, true, len, ok);
-        const uint32_t leaf = uni32(resolve_leaf<VARLEN, KW>(t, ok, len, true));
+        const uint32_t leaf = uni32(resolve_leaf_uniform<VARLEN, KW>(t, ok, len, true, lane));
         scan_one<VARLEN, SPL, R, KW, VIS>(t, ok, len, leaf, scan_size, recs + i * (uint64_t)scan_size * t.stride,
                                           counts + i, lane, VIS ? (rids ? rids[i] : 0xFFFFFFFEu) : 0u,
                                           VIS ? row_status + i * (uint64_t)scan_size : nullptr);
