@@ -96,10 +96,10 @@ def owned_keys(total_rows, world, rank):
     return np.concatenate(parts)
 
 
-def traffic_from_profile(batch, rows):
-    """Per-launch HBM bytes of probe_kernel from a committed rocprofv3 --pmc pass (see
+def traffic_from_profile(batch, rows, name="pmc_probe.json"):
+    """Per-launch HBM bytes of the dominant kernel from a committed rocprofv3 --pmc pass (see
     profiles/README.md), if one exists for this configuration."""
-    path = os.path.join(REPO, "profiles", "pmc_probe.json")
+    path = os.path.join(REPO, "profiles", name)
     if not os.path.exists(path):
         return None, None
     try:
@@ -507,10 +507,14 @@ def main():
             kernel = "probe_kernel" if not sharded else "sharded step (route + RCCL + probe_kernel)"
         units_per_launch = ops_done / args.steps
         achieved = per_unit * units_per_launch / (kern_ms * 1e-3) / 1e9
-        traffic, tsrc = (traffic_from_profile(B, args.rows) if args.config == "c2" and not sharded else (None, None))
+        traffic, tsrc = None, None
+        if not sharded and args.config in ("c2", "c4"):
+            traffic, tsrc = traffic_from_profile(B, args.rows, "pmc_probe.json" if args.config == "c2" else
+                                                 "pmc_scan.json")
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kernel,
                 "algorithmic_bytes_per_unit": per_unit, "units_per_launch": units_per_launch,
+                "algorithmic_bytes_per_launch": round(per_unit * units_per_launch),
                 "avg_launch_ms": round(kern_ms, 4)}
         if tsrc:
             roof["traffic_source"] = tsrc
