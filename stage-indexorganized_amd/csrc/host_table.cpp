@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <cstring>
 #include <stdexcept>
+#include <thread>
 
 namespace stage {
 
@@ -439,19 +440,194 @@ int HostTable::remove(const uint8_t *key, uint32_t len, uint32_t commit_id) {
     return STAGE_RC_OK;
 }
 
+// Batched epoch writes.  Small batches run the per-key path.  Large ones run in parallel:
+// (A) locate every key (read-only: updates never move records), (B) group the operations by
+// slot (an update of a key followed by another of the same key stays in batch order), (C)
+// process slot groups on worker threads, each appending its overwrite copies, versions and
+// images to thread-local buffers with references tagged "local", then (D) concatenate the
+// buffers in thread order and relocate the tagged references.  The result is the per-key
+// path's layout up to the order in which new copies / versions / images are numbered.
+namespace {
+constexpr uint32_t kLocalRef = 1u << 29;   // local copy / version index inside a tagged next handle
+constexpr uint32_t kLocalImg = 1u << 31;   // local image index
+struct LocalWrites {
+    std::vector<CopyHdr> copies;
+    std::vector<VersionHdr> versions;
+    std::vector<ImageDesc> images;
+    std::vector<uint8_t> arena;
+    std::vector<uint64_t> touched;  // host slot indices written
+    uint64_t copies_dirty_from = ~0ull;
+    uint64_t ok = 0;
+};
+uint32_t reloc_next(uint32_t nx, uint64_t cbase, uint64_t vbase) {
+    if (!(nx & kLocalRef) || (nx & kNextKindMask) == 0) return nx;
+    const uint32_t kind = nx & kNextKindMask, idx = nx & (kLocalRef - 1);
+    return kind | (uint32_t)(idx + (kind == kNextCopy ? cbase : vbase));
+}
+uint32_t reloc_img(uint32_t im, uint64_t ibase) { return (im & kLocalImg) ? (uint32_t)((im & ~kLocalImg) + ibase) : im; }
+}  // namespace
+
 uint64_t HostTable::update_batch(const uint8_t *keys, uint32_t key_stride, uint64_t n, uint32_t len,
                                  uint32_t payload_off, const uint8_t *deltas, uint32_t delta_len,
                                  const uint32_t *writer_ids, const uint32_t *commit_ids, const uint32_t *sstamps,
                                  uint8_t *rc_out) {
-    uint64_t ok = 0;
-    for (uint64_t i = 0; i < n; ++i) {
-        const uint8_t *k = keys + i * (uint64_t)key_stride;
-        int rc = update(k, len, payload_off, deltas + i * (uint64_t)delta_len, delta_len, writer_ids[i]);
-        if (rc == STAGE_RC_OK && commit_ids && commit_ids[i])
-            rc = commit_update(k, len, commit_ids[i], sstamps ? sstamps[i] : commit_ids[i]);
-        if (rc == STAGE_RC_OK) ++ok;
-        if (rc_out) rc_out[i] = (uint8_t)rc;
+    const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const bool small = n < 8192 || nt == 1 || copies_.size() + n >= kLocalRef || versions_.size() + n >= kLocalRef ||
+                       images_.size() + n >= (1ull << 30);
+    if (small) {
+        uint64_t ok = 0;
+        for (uint64_t i = 0; i < n; ++i) {
+            const uint8_t *k = keys + i * (uint64_t)key_stride;
+            int rc = update(k, len, payload_off, deltas + i * (uint64_t)delta_len, delta_len, writer_ids[i]);
+            if (rc == STAGE_RC_OK && commit_ids && commit_ids[i])
+                rc = commit_update(k, len, commit_ids[i], sstamps ? sstamps[i] : commit_ids[i]);
+            if (rc == STAGE_RC_OK) ++ok;
+            if (rc_out) rc_out[i] = (uint8_t)rc;
+        }
+        return ok;
     }
+    auto par = [&](uint64_t count, auto fn) {
+        std::vector<std::thread> th;
+        for (unsigned t = 0; t < nt; ++t)
+            th.emplace_back([&, t] { fn(t, count * t / nt, count * (t + 1) / nt); });
+        for (auto &x : th) x.join();
+    };
+    // (A) locate
+    std::vector<uint64_t> loc(n);
+    std::vector<uint8_t> rc(n, STAGE_RC_NOT_FOUND);
+    const bool bad_range = (uint64_t)payload_off + delta_len > p_.payload_size;
+    par(n, [&](unsigned, uint64_t b, uint64_t e) {
+        for (uint64_t i = b; i < e; ++i) {
+            uint32_t lf, sl;
+            loc[i] = find(keys + i * (uint64_t)key_stride, len, &lf, &sl) < 0 ? ~0ull : (uint64_t)lf * cap_ + sl;
+        }
+    });
+    // (B) group by slot, batch order inside a group
+    std::vector<uint32_t> ord;
+    ord.reserve(n);
+    for (uint64_t i = 0; i < n; ++i)
+        if (loc[i] != ~0ull) ord.push_back((uint32_t)i);
+    std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return loc[a] < loc[b] || (loc[a] == loc[b] && a < b); });
+    const uint64_t m = ord.size();
+    std::vector<uint64_t> cut(nt + 1, 0);
+    for (unsigned t = 1; t < nt; ++t) {
+        uint64_t c = m * t / nt;
+        while (c > 0 && c < m && loc[ord[c]] == loc[ord[c - 1]]) ++c;
+        cut[t] = std::max(c, cut[t - 1]);
+    }
+    cut[nt] = m;
+    for (unsigned t = 1; t <= nt; ++t) cut[t] = std::max(cut[t], cut[t - 1]);
+    // (C) per-thread processing with local appends
+    std::vector<LocalWrites> lw(nt);
+    par(nt, [&](unsigned, uint64_t tb, uint64_t te) {
+        for (uint64_t t = tb; t < te; ++t) {
+            LocalWrites &L = lw[t];
+            std::vector<uint8_t> pay(p_.payload_size);
+            auto payload_of = [&](uint32_t img, uint8_t *dst) {
+                if (img & kLocalImg) {
+                    const ImageDesc &d = L.images[img & ~kLocalImg];
+                    std::memcpy(dst, L.arena.data() + d.arg + (d.kind == 2 ? kpad_ : 0), p_.payload_size);
+                } else {
+                    image_payload(img, dst);
+                }
+            };
+            for (uint64_t q = cut[t]; q < cut[t + 1]; ++q) {
+                const uint32_t op = ord[q];
+                const uint64_t i = loc[op];
+                const uint8_t *key = keys + op * (uint64_t)key_stride;
+                const uint8_t *delta = deltas + op * (uint64_t)delta_len;
+                const uint64_t mw = meta_[i];
+                // LeafNode::Update (b_tree.cpp:1061-1163)
+                if (meta_inserting(mw)) { rc[op] = STAGE_RC_DIRTY; continue; }
+                if (bad_range) { rc[op] = STAGE_RC_INVALID; continue; }
+                payload_of(image_[i], pay.data());
+                if (std::memcmp(pay.data() + payload_off, delta, delta_len) == 0 || meta_cstamp(mw) > writer_ids[op]) {
+                    rc[op] = STAGE_RC_NOT_NEEDED_UPDATE;
+                    continue;
+                }
+                meta_[i] = mw | kMetaControl | kMetaVisible;
+                L.copies.push_back(CopyHdr{meta_cstamp(mw), kMaxCid, next_[i], image_[i]});
+                next_[i] = kNextCopy | kLocalRef | (uint32_t)(L.copies.size() - 1);
+                std::memcpy(pay.data() + payload_off, delta, delta_len);
+                ImageDesc d;
+                d.key_le = 0;
+                d.mode = 0;
+                d.arg = L.arena.size();
+                if (len > 8) {
+                    d.kind = 2;
+                    L.arena.resize(L.arena.size() + kpad_ + p_.payload_size, 0);
+                    std::memcpy(L.arena.data() + d.arg, key, len);
+                    std::memcpy(L.arena.data() + d.arg + kpad_, pay.data(), p_.payload_size);
+                } else {
+                    d.kind = 1;
+                    std::memcpy(&d.key_le, key, len);
+                    L.arena.insert(L.arena.end(), pay.begin(), pay.end());
+                }
+                L.images.push_back(d);
+                image_[i] = kLocalImg | (uint32_t)(L.images.size() - 1);
+                L.touched.push_back(i);
+                rc[op] = STAGE_RC_OK;
+                // CommitTransaction UPDATE entry (transaction_manager.cpp:610-676)
+                const uint32_t cid = commit_ids ? commit_ids[op] : 0;
+                if (cid) {
+                    CopyHdr &c = L.copies.back();
+                    c.sstamp = sstamps ? sstamps[op] : cid;
+                    L.versions.push_back(VersionHdr{c.rstamp, c.sstamp, c.next, c.image});
+                    meta_[i] = ((meta_[i] & ~kMetaTxn) | cid) & ~kMetaControl;
+                    next_[i] = kNextVersion | kLocalRef | (uint32_t)(L.versions.size() - 1);
+                }
+                ++L.ok;
+            }
+        }
+    });
+    // (D) concatenate in thread order, relocate the tagged references
+    std::vector<uint64_t> cb(nt), vb(nt), ib(nt), ab(nt);
+    uint64_t c0 = copies_.size(), v0 = versions_.size(), i0 = images_.size(), a0 = arena_.size(), ok = 0;
+    for (unsigned t = 0; t < nt; ++t) {
+        cb[t] = c0, vb[t] = v0, ib[t] = i0, ab[t] = a0;
+        c0 += lw[t].copies.size(), v0 += lw[t].versions.size(), i0 += lw[t].images.size();
+        a0 += lw[t].arena.size();
+        ok += lw[t].ok;
+    }
+    if (c0 > kNextIndexMask || v0 > kNextIndexMask || i0 > kNextIndexMask)
+        throw std::runtime_error("copy / version / image index overflow");
+    copies_.resize(c0);
+    copy_live_.resize(c0, 1);
+    versions_.resize(v0);
+    images_.resize(i0);
+    arena_.resize(a0);
+    par(nt, [&](unsigned, uint64_t tb, uint64_t te) {
+        for (uint64_t t = tb; t < te; ++t) {
+            const LocalWrites &L = lw[t];
+            for (size_t k = 0; k < L.copies.size(); ++k) {
+                CopyHdr c = L.copies[k];
+                c.next = reloc_next(c.next, cb[t], vb[t]);
+                c.image = reloc_img(c.image, ib[t]);
+                copies_[cb[t] + k] = c;
+            }
+            for (size_t k = 0; k < L.versions.size(); ++k) {
+                VersionHdr v = L.versions[k];
+                v.next = reloc_next(v.next, cb[t], vb[t]);
+                v.image = reloc_img(v.image, ib[t]);
+                versions_[vb[t] + k] = v;
+            }
+            for (size_t k = 0; k < L.images.size(); ++k) {
+                ImageDesc d = L.images[k];
+                d.arg += ab[t];
+                images_[ib[t] + k] = d;
+            }
+            if (!L.arena.empty()) std::memcpy(arena_.data() + ab[t], L.arena.data(), L.arena.size());
+            for (uint64_t i : L.touched) {
+                next_[i] = reloc_next(next_[i], cb[t], vb[t]);
+                image_[i] = reloc_img(image_[i], ib[t]);
+            }
+        }
+    });
+    for (unsigned t = 0; t < nt; ++t) {
+        for (uint64_t i : lw[t].touched) touch((uint32_t)(i / cap_), (uint32_t)(i % cap_));
+        copies_dirty_from_ = std::min(copies_dirty_from_, lw[t].copies_dirty_from);
+    }
+    if (rc_out) std::memcpy(rc_out, rc.data(), n);
     return ok;
 }
 

@@ -107,7 +107,8 @@ def test_updates_and_deletes_keep_layout():
     compare_layout(tab, orc)
 
 
-def test_update_batch_matches_per_key_oracle():
+@pytest.mark.parametrize("n", [4000, 20000])  # 20000: the parallel batched path
+def test_update_batch_matches_per_key_oracle(n):
     # one YCSB-B writer epoch through the batched entry point (stage_update_batch), with
     # duplicate keys, absent keys, no-op deltas and stale writer ids, against the oracle's
     # per-key LeafNode::Update + CommitTransaction calls
@@ -117,7 +118,6 @@ def test_update_batch_matches_per_key_oracle():
     orc.load_ycsb(0, 30000, 8, 1)
     rng = np.random.default_rng(21)
     for epoch in range(3):
-        n = 4000
         keys = np.concatenate([rng.integers(0, 30000, n - 50), rng.integers(30000, 40000, 50)]).astype(np.uint64)
         deltas = rng.integers(0, 256, (n, 16), dtype=np.uint8)
         deltas[::97] = 0  # payload mode 1 words are random: zero patches still change bytes
