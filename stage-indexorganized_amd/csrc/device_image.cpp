@@ -212,9 +212,10 @@ static void sync_heap(HostTable &h, DeviceImage &d, hipStream_t s) {
             if (d.arena.p) hip_check(hipFree(d.arena.p), "hipFree arena");
             d.arena = nb;
         }
-        hip_check(hipMemcpyAsync((uint8_t *)d.arena.p + h.arena_synced_, h.arena_.data() + h.arena_synced_,
-                                 h.arena_.size() - h.arena_synced_, hipMemcpyHostToDevice, s),
-                  "arena upload");
+        h.arena_.segments(h.arena_synced_, h.arena_.size(), [&](uint64_t off, const uint8_t *src, uint64_t bytes) {
+            hip_check(hipMemcpyAsync((uint8_t *)d.arena.p + off, src, bytes, hipMemcpyHostToDevice, s),
+                      "arena upload");
+        });
         h.arena_synced_ = h.arena_.size();
     }
     const uint64_t first = h.images_synced_, count = nimg - first;

@@ -16,6 +16,9 @@
 #include <cstring>
 #include <stdexcept>
 #include <thread>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 
 namespace stage {
 
@@ -156,16 +159,17 @@ uint32_t HostTable::new_image(const uint8_t *key, uint32_t len, const uint8_t *p
     if (len > 8) {  // wide key: the arena holds the whole row [key padded][payload]
         if (!payload) throw std::invalid_argument("keys above 8 bytes need an explicit payload");
         d.kind = 2;
-        d.arg = arena_.size();
-        arena_.resize(arena_.size() + kpad_ + p_.payload_size, 0);
-        std::memcpy(arena_.data() + d.arg, key, len);
-        std::memcpy(arena_.data() + d.arg + kpad_, payload, p_.payload_size);
+        d.arg = arena_.alloc(kpad_ + p_.payload_size);
+        uint8_t *row = arena_.at(d.arg);
+        std::memset(row, 0, kpad_);
+        std::memcpy(row, key, len);
+        std::memcpy(row + kpad_, payload, p_.payload_size);
     } else {
         std::memcpy(&d.key_le, key, len);
         if (payload) {
             d.kind = 1;
-            d.arg = arena_.size();
-            arena_.insert(arena_.end(), payload, payload + p_.payload_size);
+            d.arg = arena_.alloc(p_.payload_size);
+            std::memcpy(arena_.at(d.arg), payload, p_.payload_size);
         } else {
             d.kind = 0;
             d.arg = gen_rowid;
@@ -179,8 +183,8 @@ uint32_t HostTable::new_image(const uint8_t *key, uint32_t len, const uint8_t *p
 void HostTable::image_payload(uint32_t img, uint8_t *dst) const {
     const ImageDesc &d = images_[img];
     if (d.kind == 0) gen_payload(d.arg, (int)d.mode, dst, p_.payload_size);
-    else if (d.kind == 1) std::memcpy(dst, arena_.data() + d.arg, p_.payload_size);
-    else std::memcpy(dst, arena_.data() + d.arg + kpad_, p_.payload_size);
+    else if (d.kind == 1) std::memcpy(dst, arena_.at(d.arg), p_.payload_size);
+    else std::memcpy(dst, arena_.at(d.arg) + kpad_, p_.payload_size);
 }
 
 int HostTable::insert(const uint8_t *key, uint32_t len, const uint8_t *payload, uint64_t gen_rowid, int mode,
@@ -329,7 +333,6 @@ uint64_t HostTable::load_keys(const uint64_t *keys, uint64_t n, uint32_t key_siz
 uint64_t HostTable::load_rows(const uint8_t *keys, uint32_t key_stride, uint32_t key_size, const uint8_t *payloads,
                               uint32_t payload_stride, uint64_t n, uint32_t commit_id, uint8_t *rc_out) {
     images_.reserve(images_.size() + n);
-    arena_.reserve(arena_.size() + n * (uint64_t)(kpad_ + p_.payload_size));
     uint64_t ok = 0;
     for (uint64_t i = 0; i < n; ++i) {
         const int rc = insert(keys + i * (uint64_t)key_stride, key_size, payloads + i * (uint64_t)payload_stride, 0, 0,
@@ -486,6 +489,15 @@ uint64_t HostTable::update_batch(const uint8_t *keys, uint32_t key_stride, uint6
         }
         return ok;
     }
+    const bool timing = std::getenv("STAGE_TIMING") != nullptr;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto t_0 = now();
+    auto lap = [&](const char *what) {
+        if (!timing) return;
+        const auto t = now();
+        std::fprintf(stderr, "[update_batch] %s %.1f ms\n", what, std::chrono::duration<double, std::milli>(t - t_0).count());
+        t_0 = t;
+    };
     auto par = [&](uint64_t count, auto fn) {
         std::vector<std::thread> th;
         for (unsigned t = 0; t < nt; ++t)
@@ -502,26 +514,38 @@ uint64_t HostTable::update_batch(const uint8_t *keys, uint32_t key_stride, uint6
             loc[i] = find(keys + i * (uint64_t)key_stride, len, &lf, &sl) < 0 ? ~0ull : (uint64_t)lf * cap_ + sl;
         }
     });
-    // (B) group by slot, batch order inside a group
-    std::vector<uint32_t> ord;
-    ord.reserve(n);
+    lap("locate");
+    // (B) group by slot, batch order inside a group: bucket by leaf range (one bucket per
+    // worker, so a slot group never straddles two workers), then sort each bucket in parallel
+    const uint64_t span = (uint64_t)leaves_.size() * cap_;
+    std::vector<uint64_t> bcount(nt + 1, 0);
+    auto bucket = [&](uint64_t l) { return (unsigned)(l * nt / span); };
     for (uint64_t i = 0; i < n; ++i)
-        if (loc[i] != ~0ull) ord.push_back((uint32_t)i);
-    std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return loc[a] < loc[b] || (loc[a] == loc[b] && a < b); });
-    const uint64_t m = ord.size();
-    std::vector<uint64_t> cut(nt + 1, 0);
-    for (unsigned t = 1; t < nt; ++t) {
-        uint64_t c = m * t / nt;
-        while (c > 0 && c < m && loc[ord[c]] == loc[ord[c - 1]]) ++c;
-        cut[t] = std::max(c, cut[t - 1]);
+        if (loc[i] != ~0ull) bcount[bucket(loc[i]) + 1]++;
+    for (unsigned t = 0; t < nt; ++t) bcount[t + 1] += bcount[t];
+    const uint64_t m = bcount[nt];
+    std::vector<std::pair<uint64_t, uint32_t>> ord(m);
+    {
+        std::vector<uint64_t> pos(bcount.begin(), bcount.end() - 1);
+        for (uint64_t i = 0; i < n; ++i)
+            if (loc[i] != ~0ull) ord[pos[bucket(loc[i])]++] = {loc[i], (uint32_t)i};
     }
-    cut[nt] = m;
-    for (unsigned t = 1; t <= nt; ++t) cut[t] = std::max(cut[t], cut[t - 1]);
+    par(nt, [&](unsigned, uint64_t tb, uint64_t te) {
+        for (uint64_t t = tb; t < te; ++t) std::sort(ord.begin() + bcount[t], ord.begin() + bcount[t + 1]);
+    });
+    const std::vector<uint64_t> &cut = bcount;
+    lap("group");
     // (C) per-thread processing with local appends
     std::vector<LocalWrites> lw(nt);
     par(nt, [&](unsigned, uint64_t tb, uint64_t te) {
         for (uint64_t t = tb; t < te; ++t) {
             LocalWrites &L = lw[t];
+            const uint64_t nops = cut[t + 1] - cut[t];
+            L.copies.reserve(nops);
+            L.versions.reserve(commit_ids ? nops : 0);
+            L.images.reserve(nops);
+            L.touched.reserve(nops);
+            L.arena.reserve(nops * (uint64_t)(kpad_ + p_.payload_size));
             std::vector<uint8_t> pay(p_.payload_size);
             auto payload_of = [&](uint32_t img, uint8_t *dst) {
                 if (img & kLocalImg) {
@@ -532,8 +556,8 @@ uint64_t HostTable::update_batch(const uint8_t *keys, uint32_t key_stride, uint6
                 }
             };
             for (uint64_t q = cut[t]; q < cut[t + 1]; ++q) {
-                const uint32_t op = ord[q];
-                const uint64_t i = loc[op];
+                const uint32_t op = ord[q].second;
+                const uint64_t i = ord[q].first;
                 const uint8_t *key = keys + op * (uint64_t)key_stride;
                 const uint8_t *delta = deltas + op * (uint64_t)delta_len;
                 const uint64_t mw = meta_[i];
@@ -580,22 +604,29 @@ uint64_t HostTable::update_batch(const uint8_t *keys, uint32_t key_stride, uint6
             }
         }
     });
+    lap("process");
     // (D) concatenate in thread order, relocate the tagged references
-    std::vector<uint64_t> cb(nt), vb(nt), ib(nt), ab(nt);
-    uint64_t c0 = copies_.size(), v0 = versions_.size(), i0 = images_.size(), a0 = arena_.size(), ok = 0;
+    std::vector<uint64_t> cb(nt), vb(nt), ib(nt);
+    uint64_t c0 = copies_.size(), v0 = versions_.size(), i0 = images_.size(), ok = 0;
     for (unsigned t = 0; t < nt; ++t) {
-        cb[t] = c0, vb[t] = v0, ib[t] = i0, ab[t] = a0;
+        cb[t] = c0, vb[t] = v0, ib[t] = i0;
         c0 += lw[t].copies.size(), v0 += lw[t].versions.size(), i0 += lw[t].images.size();
-        a0 += lw[t].arena.size();
         ok += lw[t].ok;
     }
     if (c0 > kNextIndexMask || v0 > kNextIndexMask || i0 > kNextIndexMask)
         throw std::runtime_error("copy / version / image index overflow");
+    // arena rows keep their order; each gets a global offset that does not straddle a chunk
+    std::vector<std::vector<uint64_t>> row_at(nt);
+    for (unsigned t = 0; t < nt; ++t) {
+        row_at[t].resize(lw[t].images.size());
+        for (size_t k = 0; k < lw[t].images.size(); ++k)
+            row_at[t][k] = arena_.alloc(lw[t].images[k].kind == 2 ? kpad_ + p_.payload_size : p_.payload_size);
+    }
     copies_.resize(c0);
     copy_live_.resize(c0, 1);
     versions_.resize(v0);
     images_.resize(i0);
-    arena_.resize(a0);
+    lap("resize");
     par(nt, [&](unsigned, uint64_t tb, uint64_t te) {
         for (uint64_t t = tb; t < te; ++t) {
             const LocalWrites &L = lw[t];
@@ -613,21 +644,24 @@ uint64_t HostTable::update_batch(const uint8_t *keys, uint32_t key_stride, uint6
             }
             for (size_t k = 0; k < L.images.size(); ++k) {
                 ImageDesc d = L.images[k];
-                d.arg += ab[t];
+                const uint64_t bytes = d.kind == 2 ? kpad_ + p_.payload_size : p_.payload_size;
+                std::memcpy(arena_.at(row_at[t][k]), L.arena.data() + d.arg, bytes);
+                d.arg = row_at[t][k];
                 images_[ib[t] + k] = d;
             }
-            if (!L.arena.empty()) std::memcpy(arena_.data() + ab[t], L.arena.data(), L.arena.size());
             for (uint64_t i : L.touched) {
                 next_[i] = reloc_next(next_[i], cb[t], vb[t]);
                 image_[i] = reloc_img(image_[i], ib[t]);
             }
         }
     });
+    lap("concat");
     for (unsigned t = 0; t < nt; ++t) {
         for (uint64_t i : lw[t].touched) touch((uint32_t)(i / cap_), (uint32_t)(i % cap_));
         copies_dirty_from_ = std::min(copies_dirty_from_, lw[t].copies_dirty_from);
     }
     if (rc_out) std::memcpy(rc_out, rc.data(), n);
+    lap("touch");
     return ok;
 }
 

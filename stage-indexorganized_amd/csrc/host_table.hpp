@@ -16,6 +16,7 @@
 #include <string>
 #include <vector>
 
+#include "chunked.hpp"
 #include "stage_core.hpp"
 #include "../../include/stage_hip.h"
 
@@ -144,8 +145,8 @@ public:
     int32_t head_ = 0;
     uint32_t nleaves_live_ = 0;
 
-    std::vector<ImageDesc> images_;
-    std::vector<uint8_t> arena_;
+    ChunkedVector<ImageDesc, (1u << 20)> images_;
+    ChunkedArena arena_;
     std::vector<CopyHdr> copies_;
     std::vector<uint8_t> copy_live_;
     std::vector<VersionHdr> versions_;
