@@ -139,8 +139,13 @@ static void patch_device(HostTable &h, DeviceImage &d, hipStream_t s) {
     std::sort(ds.begin(), ds.end());
     ds.erase(std::unique(ds.begin(), ds.end()), ds.end());
     std::vector<uint32_t> leaves;
-    for (uint64_t x : ds)
-        if (leaves.empty() || leaves.back() != x / cap) leaves.push_back((uint32_t)(x / cap));
+    std::vector<uint64_t> first;  // first dirty slot of each leaf in ds
+    for (uint64_t k = 0; k < ds.size(); ++k)
+        if (leaves.empty() || leaves.back() != ds[k] / cap) {
+            leaves.push_back((uint32_t)(ds[k] / cap));
+            first.push_back(k);
+        }
+    first.push_back(ds.size());
     const uint64_t nl = leaves.size(), ns = ds.size();
     if (nl == 0) return;
     // staging: [dev leaf u32 ...][heads nl*hb][slot idx u64 ...][SlotInfo ...][key words ns*kw],
@@ -156,20 +161,21 @@ static void patch_device(HostTable &h, DeviceImage &d, hipStream_t s) {
     uint64_t *sidx = (uint64_t *)(st + o_idx);
     SlotInfo *ssrc = (SlotInfo *)(st + o_src);
     uint64_t *swords = (uint64_t *)(st + o_words);
-    std::vector<uint64_t> okey_tmp((uint64_t)cap * kw);
-    std::vector<SlotInfo> slot_tmp(cap);
-    uint64_t k = 0;
-    for (uint64_t li = 0; li < nl; ++li) {
+    parallel_for(nl, [&](uint64_t li) {
+        thread_local std::vector<uint64_t> okey_tmp;
+        thread_local std::vector<SlotInfo> slot_tmp;
+        okey_tmp.resize((uint64_t)cap * kw);
+        slot_tmp.resize(cap);
         const uint32_t hl = leaves[li], dl = d.host_to_dev[hl];
         dleaf[li] = dl;
         build_leaf(h, hl, st + o_head + li * hb, okey_tmp.data(), slot_tmp.data());
-        for (; k < ns && ds[k] / cap == hl; ++k) {
+        for (uint64_t k = first[li]; k < first[li + 1]; ++k) {
             const uint32_t sl = (uint32_t)(ds[k] % cap);
             sidx[k] = (uint64_t)dl * cap + sl;
             ssrc[k] = slot_tmp[sl];
             for (uint32_t j = 0; j < kw; ++j) swords[k * kw + j] = okey_tmp[(uint64_t)j * cap + sl];
         }
-    }
+    });
     upload(d.patch, st, bytes, s, "patch staging");
     uint8_t *dp = (uint8_t *)d.patch.p;
     hip_check(launch_patch((uint8_t *)d.head.p, (uint64_t *)d.okey.p, (SlotInfo *)d.slot.p, hb, cap, kw,
