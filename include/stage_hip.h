@@ -161,7 +161,8 @@ uint32_t stage_leaf_capacity(stage_table *t); /* slots per leaf on the device (6
 int stage_traverse_batch(stage_table *t, const uint64_t *keys, const uint16_t *lens, uint64_t n,
                          int le_child, uint32_t *leaf_out);
 /* export the leaf layout (key order) for layout parity against a reference tree:
- * rc/sc = record_count/sorted_count, meta words and key bytes per slot (cap slots) */
+ * rc/sc = record_count/sorted_count, meta words and the first 8 key bytes per slot (cap
+ * slots); returns the number of leaves, STAGE_E_ARG if max_leaves < stage_stats[2] */
 int64_t stage_export_leaves(stage_table *t, uint32_t cap, uint64_t max_leaves, uint32_t *rc,
                             uint32_t *sc, uint64_t *meta, uint64_t *keyw);
 

@@ -240,9 +240,13 @@ int stage_traverse_batch(stage_table *t, const uint64_t *keys, const uint16_t *l
 
 int64_t stage_export_leaves(stage_table *t, uint32_t cap, uint64_t max_leaves, uint32_t *rc, uint32_t *sc,
                             uint64_t *meta, uint64_t *keyw) {
-    if (!t || !rc || !sc || !meta || !keyw) return fail(STAGE_E_ARG, "null argument");
+    if (!t || !rc || !sc || !meta || !keyw || cap == 0) return fail(STAGE_E_ARG, "null argument");
     try {
-        return t->host->export_leaves(cap, max_leaves, rc, sc, meta, keyw);
+        const int64_t n = t->host->export_leaves(cap, max_leaves, rc, sc, meta, keyw);
+        if (n < 0) return fail(STAGE_E_ARG, "max_leaves is smaller than the leaf count (stage_stats[2])");
+        return n;
+    } catch (const std::bad_alloc &) {
+        return fail(STAGE_E_NOMEM, "host allocation failed");
     } catch (const std::exception &e) {
         return fail(STAGE_E_HIP, e.what());
     }
