@@ -269,3 +269,18 @@ def test_imported_snapshot_on_device(gpu):
     assert (counts == o_counts).all()
     for i in range(starts.size):
         assert (rows[i, :counts[i], :orc.row] == o_rows[i, :counts[i]]).all()
+
+
+def test_config1_ycsb_c_1000_rows(gpu):
+    # BASELINE configs[0] (YCSB-C -k 1000 -b 1 -o 10 -u 0 -z 0, the reference's CPU case) as
+    # a parity case: 1000 rows of 4-byte keys loaded as LoadYCSBRows does, uniform keys,
+    # 10 reads per transaction, 10^5 transactions
+    tab = stage.Table(key_width=4)
+    assert tab.load_ycsb(0, 1000, 4, mode=0) == 1000
+    tab.sync()
+    orc = O.OracleTree()
+    orc.load_ycsb(0, 1000, 4, 0)
+    keys = (stage.fastrandom(12345, 1_000_000) % np.uint64(1000)).astype(np.uint64)
+    out, rows = check_probe(tab, orc, keys, 4)
+    assert (out["status"] == stage.ST_LATEST).all()
+    assert (rows[:, 8:1008] == (keys & np.uint64(0xFF)).astype(np.uint8)[:, None]).all()
