@@ -280,11 +280,13 @@ def run_tpcc(args):
     ms = ev0.elapsed_ms(ev1) / args.steps
     res = dres.to_numpy(np.int32, B)
     value = B * args.steps / elapsed
-    # algorithmic bytes per transaction: a point probe moves key + 64 (leaf head line) + 16
-    # (slot word) + row in + row out + status; a 10-record scan key + 2 x 64 (key planes) +
-    # 10 x (row in + row out + status)
-    probe = lambda kb, row: kb + 64 + 16 + 2 * row + 4
-    per_txn = probe(16, 16 + 143) + 20 * (32 + 128 + 10 * (2 * (32 + 60) + 1)) + 20 * probe(16, 16 + 400)
+    # algorithmic bytes per transaction (what the fused transaction must touch; no tuple is
+    # materialised): a point probe reads key + 64 (fingerprint line) + 32 (slot word) + 64 (the
+    # sector holding the column it needs); a 10-record scan reads its 32-B start key, the key
+    # words + slot word of the <= 11 records RangeScanBySize collects, and one 64-B sector of the
+    # tuple it keeps; plus 4 B result
+    probe = lambda kb: kb + 64 + 32 + 64
+    per_txn = probe(16) + 20 * (32 + 11 * (32 + 32) + 64) + 20 * probe(16) + 4
     achieved = per_txn * B / (ms * 1e-3) / 1e9
     cpu = None
     if not args.no_cpu_baseline:

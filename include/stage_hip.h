@@ -121,6 +121,17 @@ int stage_update_batch(stage_table *t, const void *keys, uint32_t key_stride, ui
                        uint16_t key_size, uint32_t payload_off, const uint8_t *deltas,
                        uint32_t delta_len, const uint32_t *writer_ids, const uint32_t *commit_ids,
                        const uint32_t *sstamps, uint8_t *rc_out, uint64_t *n_ok);
+/* the same epoch applied by the device to the published image (in-place
+ * column update + overwrite copy + retire-at-commit, b_tree.cpp:1061-1163,
+ * transaction_manager.cpp:610-676), no re-publish: keys / lens as stage_probe_batch, deltas
+ * (n x delta_len), ids and d_rc (n ReturnCodes) in device memory; the table must be synced.
+ * Same return codes and resulting reads as stage_update_batch + stage_sync.  Returns after the
+ * host has adopted the epoch's bookkeeping (copy / version headers, slot words); the new
+ * payload bytes stay in HBM and are fetched only when a host path needs them. */
+int stage_update_batch_device(stage_table *t, const uint64_t *d_keys, const uint16_t *d_lens, uint64_t n,
+                              uint32_t payload_off, const uint8_t *d_deltas, uint32_t delta_len,
+                              const uint32_t *d_writer_ids, const uint32_t *d_commit_ids,
+                              const uint32_t *d_sstamps, uint8_t *d_rc, uint64_t *n_ok, void *stream);
 
 /* byte-key forms, for every key width a table takes: 1..8 bytes (key_width 1..8 or 0 =
  * variable) or a fixed width of 9..32 bytes (TPC-C composite keys, tpcc_record.h: int64

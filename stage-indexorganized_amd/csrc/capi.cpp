@@ -81,6 +81,7 @@ int stage_update(stage_table *t, uint64_t key, uint16_t key_size, uint32_t paylo
                  uint32_t delta_len, uint32_t writer_id, uint8_t *rc_out) {
     if (!t || (!delta && delta_len)) return fail(STAGE_E_ARG, "bad arguments");
     return guarded([&] {
+        ensure_host_rows(t);
         int rc = t->host->update(key, key_size, payload_off, delta, delta_len, writer_id);
         if (rc_out) *rc_out = (uint8_t)rc;
         return STAGE_OK;
@@ -103,6 +104,7 @@ int stage_update_batch(stage_table *t, const void *keys, uint32_t key_stride, ui
     if (!t || (n && (!keys || !writer_ids || (!deltas && delta_len))) || key_stride < key_size)
         return fail(STAGE_E_ARG, "bad arguments");
     return guarded([&] {
+        ensure_host_rows(t);
         uint64_t ok = t->host->update_batch((const uint8_t *)keys, key_stride, n, key_size, payload_off, deltas,
                                             delta_len, writer_ids, commit_ids, sstamps, rc_out);
         if (n_ok) *n_ok = ok;
@@ -155,6 +157,7 @@ int stage_update_key(stage_table *t, const uint8_t *key, uint16_t key_size, uint
                      const uint8_t *delta, uint32_t delta_len, uint32_t writer_id, uint8_t *rc_out) {
     if (!t || !key || (!delta && delta_len)) return fail(STAGE_E_ARG, "bad arguments");
     return guarded([&] {
+        ensure_host_rows(t);
         int rc = t->host->update(key, key_size, payload_off, delta, delta_len, writer_id);
         if (rc_out) *rc_out = (uint8_t)rc;
         return STAGE_OK;
@@ -256,6 +259,7 @@ int64_t stage_export_leaf_images(stage_table *t, uint64_t max_leaves, uint8_t *b
                                  uint16_t *sep_lens) {
     if (!t || !blocks || (!sep_keys != !sep_lens)) return fail(STAGE_E_ARG, "bad arguments");
     try {
+        ensure_host_rows(t);
         const int64_t n = t->host->export_leaf_images(max_leaves, blocks, sep_keys, sep_lens);
         if (n < 0) return fail(STAGE_E_ARG, "max_leaves is smaller than the leaf count (stage_stats[2])");
         return n;

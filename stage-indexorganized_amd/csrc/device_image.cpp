@@ -27,7 +27,7 @@ static void dev_ensure(DevBuf &b, uint64_t bytes, const char *what) {
 DeviceImage::~DeviceImage() { release(); }
 
 void DeviceImage::release() {
-    for (DevBuf *b : {&head, &okey, &slot, &tree, &tree_len, &heap, &chdr, &vhdr, &arena, &descs, &patch}) {
+    for (DevBuf *b : {&head, &okey, &slot, &tree, &tree_len, &heap, &chdr, &vhdr, &arena, &descs, &patch, &scratch}) {
         if (b->p) (void)hipFree(b->p);
         b->p = nullptr;
         b->cap = 0;
@@ -101,22 +101,68 @@ static void build_leaf(const HostTable &h, uint32_t hl, uint8_t *hd, uint64_t *o
     }
 }
 
+// grow a device buffer to `bytes`, keeping its first `keep` bytes
+static void grow_keep(DevBuf &b, uint64_t bytes, uint64_t keep, const char *what, hipStream_t s) {
+    if (b.cap >= bytes && b.p) return;
+    DevBuf nb;
+    const uint64_t want = std::max<uint64_t>(bytes + bytes / 4, 4096);
+    hip_check(hipMalloc(&nb.p, want), what);
+    nb.cap = want;
+    if (b.p && keep) hip_check(hipMemcpyAsync(nb.p, b.p, keep, hipMemcpyDeviceToDevice, s), what);
+    hip_check(hipStreamSynchronize(s), what);
+    if (b.p) hip_check(hipFree(b.p), "hipFree");
+    b = nb;
+}
+
+// record heap able to hold `rows` rows (the first images_synced_ rows are kept)
+static void grow_heap(HostTable &h, DeviceImage &d, uint64_t rows_needed, hipStream_t s) {
+    if (rows_needed <= d.heap_rows) return;
+    const uint32_t stride = h.hstride();
+    const uint64_t rows = rows_needed + std::max<uint64_t>(rows_needed / 16, 1024);
+    DevBuf nb;
+    hip_check(hipMalloc(&nb.p, rows * stride), "record heap");
+    nb.cap = rows * stride;
+    if (d.heap.p && h.images_synced_) {
+        hip_check(hipMemcpyAsync(nb.p, d.heap.p, h.images_synced_ * stride, hipMemcpyDeviceToDevice, s), "heap grow");
+        hip_check(hipStreamSynchronize(s), "heap grow sync");
+    }
+    if (d.heap.p) hip_check(hipFree(d.heap.p), "hipFree heap");
+    d.heap = nb;
+    d.heap_rows = rows;
+}
+
+uint8_t *scratch_bytes(DeviceImage &d, uint64_t bytes) {
+    if (d.scratch.cap < bytes) {
+        if (d.scratch.p) {
+            hip_check(hipDeviceSynchronize(), "scratch drain");
+            hip_check(hipFree(d.scratch.p), "hipFree scratch");
+        }
+        d.scratch.p = nullptr;
+        d.scratch.cap = 0;
+        const uint64_t want = bytes + bytes / 8 + 4096;
+        hip_check(hipMalloc(&d.scratch.p, want), "scratch");
+        d.scratch.cap = want;
+    }
+    return (uint8_t *)d.scratch.p;
+}
+
+void reserve_device_rows(HostTable &h, DeviceImage &d, uint64_t extra_images, uint64_t extra_copies,
+                         uint64_t extra_versions, hipStream_t s) {
+    grow_heap(h, d, h.images_.size() + extra_images, s);
+    grow_keep(d.chdr, (h.copies_.size() + extra_copies) * sizeof(CopyHdr), h.copies_synced_ * sizeof(CopyHdr), "chdr",
+              s);
+    grow_keep(d.vhdr, (h.versions_.size() + extra_versions) * sizeof(VersionHdr),
+              h.versions_synced_ * sizeof(VersionHdr), "vhdr", s);
+    d.view.heap = (const uint8_t *)d.heap.p;
+    d.view.chdr = (const CopyHdr *)d.chdr.p;
+    d.view.vhdr = (const VersionHdr *)d.vhdr.p;
+}
+
 // Copy/version headers: append the new tail, re-send the rewritten range of copy headers.
 static void sync_headers(HostTable &h, DeviceImage &d, hipStream_t s) {
     const uint64_t nc = h.copies_.size(), nv = h.versions_.size();
-    auto grow = [&](DevBuf &b, uint64_t bytes, uint64_t keep, const char *what) {
-        if (b.cap >= bytes && b.p) return;
-        DevBuf nb;
-        const uint64_t want = std::max<uint64_t>(bytes + bytes / 4, 4096);
-        hip_check(hipMalloc(&nb.p, want), what);
-        nb.cap = want;
-        if (b.p && keep) hip_check(hipMemcpyAsync(nb.p, b.p, keep, hipMemcpyDeviceToDevice, s), what);
-        hip_check(hipStreamSynchronize(s), what);
-        if (b.p) hip_check(hipFree(b.p), "hipFree hdr");
-        b = nb;
-    };
-    grow(d.chdr, nc * sizeof(CopyHdr), h.copies_synced_ * sizeof(CopyHdr), "chdr");
-    grow(d.vhdr, nv * sizeof(VersionHdr), h.versions_synced_ * sizeof(VersionHdr), "vhdr");
+    grow_keep(d.chdr, nc * sizeof(CopyHdr), h.copies_synced_ * sizeof(CopyHdr), "chdr", s);
+    grow_keep(d.vhdr, nv * sizeof(VersionHdr), h.versions_synced_ * sizeof(VersionHdr), "vhdr", s);
     const uint64_t c0 = std::min<uint64_t>(h.copies_synced_, h.copies_dirty_from_);
     if (nc > c0)
         hip_check(hipMemcpyAsync((CopyHdr *)d.chdr.p + c0, h.copies_.data() + c0, (nc - c0) * sizeof(CopyHdr),
@@ -191,20 +237,7 @@ static void sync_heap(HostTable &h, DeviceImage &d, hipStream_t s) {
     const stage_params &p = h.params();
     const uint32_t stride = h.hstride();
     const uint64_t nimg = h.images_.size();
-    if (nimg > d.heap_rows) {
-        const uint64_t rows = nimg + std::max<uint64_t>(nimg / 16, 1024);
-        DevBuf nb;
-        hip_check(hipMalloc(&nb.p, rows * stride), "record heap");
-        nb.cap = rows * stride;
-        if (d.heap.p && h.images_synced_) {
-            hip_check(hipMemcpyAsync(nb.p, d.heap.p, h.images_synced_ * stride, hipMemcpyDeviceToDevice, s),
-                      "heap grow");
-            hip_check(hipStreamSynchronize(s), "heap grow sync");
-        }
-        if (d.heap.p) hip_check(hipFree(d.heap.p), "hipFree heap");
-        d.heap = nb;
-        d.heap_rows = rows;
-    }
+    grow_heap(h, d, nimg, s);
     if (h.arena_.size() > h.arena_synced_) {
         // the device arena mirrors the host arena; grow keeps the already uploaded prefix
         if (d.arena.cap < h.arena_.size()) {
@@ -289,6 +322,7 @@ void sync_device(HostTable &h, DeviceImage &d) {
     const uint64_t L = order.size();
     d.host_to_dev.assign(h.leaves_.size(), 0xFFFFFFFFu);
     for (uint64_t i = 0; i < L; ++i) d.host_to_dev[order[i]] = (uint32_t)i;
+    d.dev_to_host = order;
 
     const uint32_t kw = h.key_words(), hb = leaf_head_bytes(cap, kw);
     std::vector<uint64_t> okey(L * cap * kw);

@@ -20,10 +20,12 @@ struct DeviceImage {
     int device = 0;
     hipStream_t stream = nullptr;
     DevBuf head, okey, slot, tree, tree_len, heap, chdr, vhdr, arena, descs, patch;
+    DevBuf scratch;  // per-call scratch of the device write path / stock-level (scratch_bytes)
     std::vector<uint8_t> staging;  // host staging of incremental patches
     uint64_t heap_rows = 0;  // rows the heap buffer can hold
     DevTable view{};
     std::vector<uint32_t> host_to_dev;  // host leaf id -> leaf index in key order
+    std::vector<uint32_t> dev_to_host;  // leaf index in key order -> host leaf id
     bool valid = false;
     double last_sync_seconds = 0;
     bool last_sync_incremental = false;
@@ -38,5 +40,15 @@ struct DeviceImage {
 void sync_device(HostTable &h, DeviceImage &d);
 
 void hip_check(hipError_t e, const char *what);
+
+// scratch of at least `bytes` (grown with hipMalloc after draining the device; reused by the
+// next call on the same table).  Stream-ordered pool memory (hipMallocAsync) is not used: on
+// gfx950 its reuse across calls showed stale reads on other XCDs between kernels of a stream.
+uint8_t *scratch_bytes(DeviceImage &d, uint64_t bytes);
+
+// grow the record heap and the copy / version header arrays so that `extra_*` more entries fit
+// after the host's current counts (device write path); refreshes the DevTable view
+void reserve_device_rows(HostTable &h, DeviceImage &d, uint64_t extra_images, uint64_t extra_copies,
+                         uint64_t extra_versions, hipStream_t s);
 
 }  // namespace stage

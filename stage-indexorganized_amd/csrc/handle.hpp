@@ -63,6 +63,10 @@ inline int need_synced(stage_table *t) {
     return STAGE_OK;
 }
 
+// device-written heap rows (stage_update_batch_device) are pulled into the host arena before a
+// host-side path reads payloads (write_path.hip)
+void ensure_host_rows(stage_table *t);
+
 inline hipStream_t pick(stage_table *t, void *stream) { return stream ? (hipStream_t)stream : t->dev.stream; }
 
 inline int hip_rc(hipError_t e, const char *what) {

@@ -184,7 +184,60 @@ void HostTable::image_payload(uint32_t img, uint8_t *dst) const {
     const ImageDesc &d = images_[img];
     if (d.kind == 0) gen_payload(d.arg, (int)d.mode, dst, p_.payload_size);
     else if (d.kind == 1) std::memcpy(dst, arena_.at(d.arg), p_.payload_size);
-    else std::memcpy(dst, arena_.at(d.arg) + kpad_, p_.payload_size);
+    else if (d.kind == 2) std::memcpy(dst, arena_.at(d.arg) + kpad_, p_.payload_size);
+    else throw std::logic_error("device-written heap row read before materialize_device_rows");
+}
+
+void HostTable::adopt_device_epoch(const CopyHdr *copies, uint64_t nc, const VersionHdr *versions, uint64_t nv,
+                                   uint64_t nimages, const SlotWords *slots, uint64_t nslots) {
+    if (copies_.size() + nc > kNextIndexMask || versions_.size() + nv > kNextIndexMask ||
+        images_.size() + nimages > kNextIndexMask)
+        throw std::runtime_error("copy / version / image index overflow");
+    copies_.insert(copies_.end(), copies, copies + nc);
+    copy_live_.resize(copies_.size(), 1);
+    versions_.insert(versions_.end(), versions, versions + nv);
+    if (nimages) {
+        device_rows_.emplace_back(images_.size(), nimages);
+        for (uint64_t k = 0; k < nimages; ++k) images_.push_back(ImageDesc{0, 0, 3, 0});
+    }
+    for (uint64_t k = 0; k < nslots; ++k) {
+        const SlotWords &w = slots[k];
+        meta_[w.idx] = w.meta;
+        next_[w.idx] = w.next;
+        image_[w.idx] = w.image;
+    }
+    // the device already holds all of it
+    copies_synced_ = copies_.size();
+    versions_synced_ = versions_.size();
+    images_synced_ = images_.size();
+}
+
+void HostTable::materialize_device_rows(const std::function<void(uint64_t, uint64_t, uint8_t *)> &fetch) {
+    const uint64_t row = kpad_ + p_.payload_size, chunk = 1u << 14;
+    std::vector<uint8_t> buf(chunk * stride_);
+    for (const auto &r : device_rows_) {
+        for (uint64_t b = 0; b < r.second; b += chunk) {
+            const uint64_t cnt = std::min(chunk, r.second - b);
+            fetch(r.first + b, cnt, buf.data());
+            for (uint64_t k = 0; k < cnt; ++k) {
+                const uint8_t *src = buf.data() + k * stride_;
+                ImageDesc &d = images_[r.first + b + k];
+                d.mode = 0;
+                if (kw_ > 1) {  // wide keys: the whole row
+                    d.kind = 2;
+                    d.key_le = 0;
+                    d.arg = arena_.alloc(row);
+                    std::memcpy(arena_.at(d.arg), src, row);
+                } else {        // key word + payload
+                    d.kind = 1;
+                    std::memcpy(&d.key_le, src, 8);
+                    d.arg = arena_.alloc(p_.payload_size);
+                    std::memcpy(arena_.at(d.arg), src + 8, p_.payload_size);
+                }
+            }
+        }
+    }
+    device_rows_.clear();
 }
 
 int HostTable::insert(const uint8_t *key, uint32_t len, const uint8_t *payload, uint64_t gen_rowid, int mode,

@@ -13,7 +13,9 @@
 // of (words, len) is the reference's KeyCompare order.
 #pragma once
 #include <cstdint>
+#include <functional>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "chunked.hpp"
@@ -55,7 +57,9 @@ void key_to_bytes(const Key &k, uint8_t *out, bool uns);
 struct ImageDesc {
     uint64_t key_le;  // key bytes (little-endian, zero above key_len) -- keys of <= 8 bytes
     uint64_t arg;     // rowid (generated) or arena byte offset (explicit)
-    uint32_t kind;    // 0 = generated, 1 = arena payload (key in key_le), 2 = arena row [key pad][payload]
+    uint32_t kind;    // 0 = generated, 1 = arena payload (key in key_le), 2 = arena row [key pad][payload],
+                      // 3 = written by the device write path, bytes only in the device heap until
+                      //     materialize_device_rows() pulls them into the arena
     uint32_t mode;    // payload generator mode (generated images)
 };
 
@@ -163,6 +167,22 @@ public:
     uint64_t update_batch(const uint8_t *keys, uint32_t key_stride, uint64_t n, uint32_t len, uint32_t payload_off,
                           const uint8_t *deltas, uint32_t delta_len, const uint32_t *writer_ids,
                           const uint32_t *commit_ids, const uint32_t *sstamps, uint8_t *rc_out);
+
+    // ---- device write path (write_path.hip): the device applied an update epoch in place;
+    // the host adopts its bookkeeping (new copy / version headers, the final slot words of the
+    // touched records, `nimages` new heap rows of kind 3) without touching payload bytes.
+    struct SlotWords {
+        uint64_t idx;   // host slot index leaf*cap + slot
+        uint64_t meta;
+        uint32_t next, image;
+    };
+    void adopt_device_epoch(const CopyHdr *copies, uint64_t nc, const VersionHdr *versions, uint64_t nv,
+                            uint64_t nimages, const SlotWords *slots, uint64_t nslots);
+    bool has_device_rows() const { return !device_rows_.empty(); }
+    // pull the bytes of device-written rows into the arena (host-side writes and the leaf-image
+    // export read payloads); fetch(first, count, dst) copies heap rows [first, first+count)
+    void materialize_device_rows(const std::function<void(uint64_t, uint64_t, uint8_t *)> &fetch);
+    std::vector<std::pair<uint64_t, uint64_t>> device_rows_;  // (first image, count) of kind 3
 
 private:
     struct RouteEntry {

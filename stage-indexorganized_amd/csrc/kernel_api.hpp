@@ -42,6 +42,12 @@ struct ScanTuning {
 hipError_t launch_scan(const DevTable &t, const uint64_t *keys, const uint16_t *lens, uint64_t n, uint32_t scan_size,
                        uint32_t *counts, uint8_t *recs, hipStream_t s, const ScanTuning &tune,
                        const uint32_t *rids = nullptr, uint8_t *row_status = nullptr);
+// IndexScanExecutor range scan (fixed-width tables) kept only up to its first produced tuple
+// whose key starts with the start key's first `words` order words: img_out[i] = its heap row
+// (0xFFFFFFFF if none), st_out[i] = ST_LATEST / ST_OLD / ST_NOT_FOUND
+hipError_t launch_scan_first(const DevTable &t, const uint64_t *keys, uint64_t n, uint32_t scan_size,
+                             const uint32_t *rids, uint32_t words, uint32_t *img_out, uint8_t *st_out, hipStream_t s,
+                             const ScanTuning &tune);
 hipError_t launch_murmur(const void *keys, uint32_t key_len, uint32_t key_stride, uint64_t seed, uint64_t n,
                          uint64_t *out, hipStream_t s);
 hipError_t launch_fill(uint8_t *heap, uint32_t stride, uint32_t payload_size, uint32_t row_bytes,

@@ -600,11 +600,92 @@ __device__ void scan_one(const DevTable &t, const uint64_t *x0, uint32_t xl, uin
 // at most 63 records: RangeScanBySize's collection (first to_scan+1 qualifying records in slot
 // order) walks only the slot groups whose max key (leaf head) reaches the start key and stops
 // as soon as to_scan+1 records are held; the kept records (<= 64) go to a per-wave LDS list,
-// one lane per record ranks them (std::sort) and they are emitted as in scan_one.
-template <bool VARLEN, int SPL, int KW, bool VIS>
-__device__ void scan_one_compact(const DevTable &t, const uint64_t *x0, uint32_t xl, uint32_t leaf,
-                                 uint32_t scan_size, uint8_t *recs, uint32_t *count_out, uint32_t lane, uint32_t rid,
-                                 uint8_t *row_status, uint64_t *lk, uint32_t *ll, uint32_t *ls) {
+// one lane per record ranks them (std::sort) and they are handed to the sink in key order.
+//
+// Sinks: emit() sees, per lane, whether the lane emits a record on this leaf visit (`on`), its
+// slot, its rank `kr` among this visit's records (`produced` records came before) and its key
+// words; it returns true to end the scan early.
+template <bool VIS>
+struct RowSink {  // rows (and, for VIS, per-record statuses) as scan_one writes them
+    uint8_t *recs;
+    uint8_t *row_status;
+    uint32_t rid;
+    template <int KW>
+    __device__ __forceinline__ bool emit(const DevTable &t, uint64_t base, bool on, uint32_t mslot, uint32_t kr,
+                                         uint32_t produced, const uint64_t *, uint32_t lane) {
+        uint32_t img = 0;
+        if (on) {
+            if (VIS) {
+                uint8_t st;
+                img = scan_visible(t, t.slot[base + mslot], rid, st);
+                row_status[produced + kr] = st;
+            } else {
+                img = t.slot[base + mslot].image;
+            }
+        }
+        uint64_t em = ballot(on);
+        while (em) {
+            uint32_t imr[4], dr[4];
+            int nk = 0;
+            for (; nk < 4 && em; ++nk) {
+                const int b = __builtin_ctzll(em);
+                em &= em - 1;
+                imr[nk] = rl32(img, b);
+                dr[nk] = produced + rl32(kr, b);
+            }
+            copy_rows<4>(t, imr, dr, nk, recs, lane);
+        }
+        return false;
+    }
+};
+
+// IndexScanExecutor range branch consumed up to its first produced tuple (LATEST or OLD) whose
+// key begins with the start key's first `words` order words -- a predicate over the scan that
+// keeps only that tuple (TPC-C stock-level, tpcc_stock_level.cpp:104-135, takes ol_i_ids[0]).
+// Result (wave-uniform): the tuple's heap row and status, or 0xFFFFFFFF / NOT_FOUND.
+template <int KW>
+struct FirstPrefixSink {
+    uint64_t pre[KW];
+    uint32_t words;
+    uint32_t rid;
+    uint32_t img;
+    uint32_t st;
+    template <int KW2>
+    __device__ __forceinline__ bool emit(const DevTable &t, uint64_t base, bool on, uint32_t mslot, uint32_t kr,
+                                         uint32_t, const uint64_t *mk, uint32_t) {
+        uint8_t s = ST_NOT_FOUND;
+        uint32_t im = 0xFFFFFFFFu;
+        bool pass = false;
+        if (on) {
+            im = scan_visible(t, t.slot[base + mslot], rid, s);
+            pass = s == ST_LATEST || s == ST_OLD;
+#pragma unroll
+            for (int w = 0; w < KW; ++w)
+                if ((uint32_t)w < words) pass = pass && mk[w] == pre[w];
+        }
+        uint64_t pm = ballot(pass);
+        if (!pm) return false;
+        uint32_t best = 0xFFFFFFFFu;
+        int bl = 0;
+        while (pm) {  // the passing record of lowest rank
+            const int b = __builtin_ctzll(pm);
+            pm &= pm - 1;
+            const uint32_t k = rl32(kr, b);
+            if (k < best) {
+                best = k;
+                bl = b;
+            }
+        }
+        img = rl32(im, bl);
+        st = rl32((uint32_t)s, bl);
+        return true;
+    }
+};
+
+template <bool VARLEN, int SPL, int KW, class Sink>
+__device__ uint32_t scan_one_compact(const DevTable &t, const uint64_t *x0, uint32_t xl, uint32_t leaf,
+                                     uint32_t scan_size, uint32_t lane, Sink &sink, uint64_t *lk, uint32_t *ll,
+                                     uint32_t *ls) {
     uint32_t remaining = scan_size, produced = 0;
     bool cont = false;
     uint64_t x[KW];
@@ -679,28 +760,9 @@ __device__ void scan_one_compact(const DevTable &t, const uint64_t *x0, uint32_t
             if (ballot(mine && kr == 0 && eq)) break;
         }
         const uint32_t e = m < remaining ? m : remaining;
-        const bool emit = mine && kr < e;
-        uint32_t img = 0;
-        if (emit) {
-            if (VIS) {
-                uint8_t st;
-                img = scan_visible(t, t.slot[base + mslot], rid, st);
-                row_status[produced + kr] = st;
-            } else {
-                img = t.slot[base + mslot].image;
-            }
-        }
-        uint64_t em = ballot(emit);
-        while (em) {
-            uint32_t imr[4], dr[4];
-            int nk = 0;
-            for (; nk < 4 && em; ++nk) {
-                const int b = __builtin_ctzll(em);
-                em &= em - 1;
-                imr[nk] = rl32(img, b);
-                dr[nk] = produced + rl32(kr, b);
-            }
-            copy_rows<4>(t, imr, dr, nk, recs, lane);
+        if (sink.template emit<KW>(t, base, mine && kr < e, mslot, kr, produced, mk, lane)) {
+            produced += e;
+            break;
         }
         produced += e;
         remaining -= e;
@@ -714,7 +776,7 @@ __device__ void scan_one_compact(const DevTable &t, const uint64_t *x0, uint32_t
         leaf = uni32(resolve_leaf_uniform<VARLEN, KW>(t, x, xl, false, lane));
         cont = true;
     }
-    if (lane == 0) *count_out = produced;
+    return produced;
 }
 
 template <bool VARLEN, int SPL, int KW, bool VIS>
@@ -734,11 +796,45 @@ __global__ __launch_bounds__(256) void scan_kernel_compact(DevTable t, const uin
         uint64_t ok[KW];
         load_okey<KW>(keys, i, true, len, ok);
         const uint32_t leaf = uni32(resolve_leaf_uniform<VARLEN, KW>(t, ok, len, true, lane));
-        scan_one_compact<VARLEN, SPL, KW, VIS>(t, ok, len, leaf, scan_size,
-                                               recs + i * (uint64_t)scan_size * t.stride, counts + i, lane,
-                                               VIS ? (rids ? rids[i] : 0xFFFFFFFEu) : 0u,
-                                               VIS ? row_status + i * (uint64_t)scan_size : nullptr, s_keys[wv],
-                                               s_len[wv], s_slot[wv]);
+        RowSink<VIS> sink{recs + i * (uint64_t)scan_size * t.stride,
+                          VIS ? row_status + i * (uint64_t)scan_size : nullptr,
+                          VIS ? (rids ? rids[i] : 0xFFFFFFFEu) : 0u};
+        const uint32_t produced = scan_one_compact<VARLEN, SPL, KW>(t, ok, len, leaf, scan_size, lane, sink,
+                                                                    s_keys[wv], s_len[wv], s_slot[wv]);
+        if (lane == 0) counts[i] = produced;
+    }
+}
+
+// One wave per scan: the IndexScanExecutor range scan of `scan_size` records from key i, kept
+// only up to its first produced tuple with the start key's first `words` order words
+// (FirstPrefixSink); img_out[i] / st_out[i] = that tuple's heap row and status.
+template <int SPL, int KW>
+__global__ __launch_bounds__(256) void scan_first_kernel(DevTable t, const uint64_t *__restrict__ keys, uint64_t n,
+                                                         uint32_t scan_size, const uint32_t *__restrict__ rids,
+                                                         uint32_t words, uint32_t *__restrict__ img_out,
+                                                         uint8_t *__restrict__ st_out) {
+    __shared__ uint64_t s_keys[4][64 * KW];
+    __shared__ uint32_t s_len[4][64], s_slot[4][64];
+    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    for (uint64_t i = wave; i < n; i += nwaves) {
+        const uint32_t len = t.key_width;
+        uint64_t ok[KW];
+        load_okey<KW>(keys, i, true, len, ok);
+        FirstPrefixSink<KW> sink;
+#pragma unroll
+        for (int w = 0; w < KW; ++w) sink.pre[w] = ok[w];
+        sink.words = words;
+        sink.rid = rids ? rids[i] : 0xFFFFFFFEu;
+        sink.img = 0xFFFFFFFFu;
+        sink.st = ST_NOT_FOUND;
+        const uint32_t leaf = uni32(resolve_leaf_uniform<false, KW>(t, ok, len, true, lane));
+        scan_one_compact<false, SPL, KW>(t, ok, len, leaf, scan_size, lane, sink, s_keys[wv], s_len[wv], s_slot[wv]);
+        if (lane == 0) {
+            img_out[i] = sink.img;
+            st_out[i] = (uint8_t)sink.st;
+        }
     }
 }
 
@@ -1042,6 +1138,34 @@ hipError_t launch_scan(const DevTable &t, const uint64_t *keys, const uint16_t *
     } else {
         launch_scan_r<4, false>(t, keys, lens, n, scan_size, counts, recs, nullptr, nullptr, s, blocks);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_scan_first(const DevTable &t, const uint64_t *keys, uint64_t n, uint32_t scan_size,
+                             const uint32_t *rids, uint32_t words, uint32_t *img_out, uint8_t *st_out, hipStream_t s,
+                             const ScanTuning &tune) {
+    if (n == 0) return hipSuccess;
+    if (t.key_width == 0 || scan_size == 0 || scan_size > 63) return hipErrorInvalidValue;
+    const int blocks = grid_for(n, 4, tune.max_blocks > 0 ? tune.max_blocks : 16384);
+#define STAGE_FIRST(S, KW) \
+    scan_first_kernel<S, KW><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words, img_out, st_out)
+#define STAGE_FIRST_K(KW)                      \
+    switch (t.cap / 64) {                      \
+        case 1: STAGE_FIRST(1, KW); break;     \
+        case 2: STAGE_FIRST(2, KW); break;     \
+        case 4: STAGE_FIRST(4, KW); break;     \
+        case 8: STAGE_FIRST(8, KW); break;     \
+        default: STAGE_FIRST(16, KW);          \
+    }
+    if (t.key_words == 4) {
+        STAGE_FIRST_K(4)
+    } else if (t.key_words == 2) {
+        STAGE_FIRST_K(2)
+    } else {
+        STAGE_FIRST_K(1)
+    }
+#undef STAGE_FIRST_K
+#undef STAGE_FIRST
     return hipGetLastError();
 }
 

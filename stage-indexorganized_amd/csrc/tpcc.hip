@@ -60,8 +60,8 @@ __global__ void sl_spread_rids(const uint32_t *__restrict__ rids, uint64_t ns, u
 
 // step 1 -> 2: abort flags and the 20 order-line start keys of each transaction
 __global__ void sl_order_keys(const int64_t *__restrict__ w, const int64_t *__restrict__ d, uint64_t n,
-                              const stage_probe_out_dev *__restrict__ dout, const uint8_t *__restrict__ drows,
-                              uint32_t dstride, uint32_t dkpad, int32_t *__restrict__ result,
+                              const stage_probe_out_dev *__restrict__ dout, const uint8_t *__restrict__ dheap,
+                              uint32_t dhstride, uint32_t dkpad, int32_t *__restrict__ result,
                               uint64_t *__restrict__ okeys) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
@@ -71,7 +71,7 @@ __global__ void sl_order_keys(const int64_t *__restrict__ w, const int64_t *__re
         result[t] = -1;  // FAILURE -> abort; no district -> districts.size() != 1 -> return false
     } else {
         result[t] = 0;
-        next = ld_i32(drows + t * (uint64_t)dstride + dkpad);  // D_NEXT_O_ID
+        next = ld_i32(dheap + (uint64_t)dout[t].w[6] * dhstride + dkpad);  // D_NEXT_O_ID of the tuple read
     }
     for (int k = 0; k < kOrdersPerTxn; ++k) {
         uint64_t *key = okeys + (t * kOrdersPerTxn + k) * 4;
@@ -82,30 +82,16 @@ __global__ void sl_order_keys(const int64_t *__restrict__ w, const int64_t *__re
     }
 }
 
-// step 2 -> 3: first OL_I_ID of each scan that passes the predicate -> stock key {w, i}
-__global__ void sl_stock_keys(const int64_t *__restrict__ w, const int64_t *__restrict__ d, uint64_t n,
-                              const int32_t *__restrict__ result, const uint64_t *__restrict__ okeys,
-                              const uint32_t *__restrict__ counts, const uint8_t *__restrict__ rows,
-                              const uint8_t *__restrict__ rst, uint32_t ostride, uint32_t okpad,
+// step 2 -> 3: OL_I_ID of each scan's first predicate-passing tuple -> stock key {w, i}
+__global__ void sl_stock_keys(const int64_t *__restrict__ w, uint64_t n, const int32_t *__restrict__ result,
+                              const uint32_t *__restrict__ oimg, const uint8_t *__restrict__ ost,
+                              const uint8_t *__restrict__ oheap, uint32_t ohstride, uint32_t okpad,
                               uint64_t *__restrict__ skeys, uint8_t *__restrict__ has_item) {
     const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n * kOrdersPerTxn) return;
     const uint64_t t = s / kOrdersPerTxn;
-    const int64_t o = (int64_t)okeys[s * 4 + 2];
-    bool found = false;
-    int32_t item = 0;
-    if (result[t] >= 0) {
-        const uint32_t c = counts[s] < (uint32_t)kLinesPerScan ? counts[s] : (uint32_t)kLinesPerScan;
-        for (uint32_t j = 0; j < c && !found; ++j) {
-            const uint64_t r = s * kLinesPerScan + j;
-            if (!produced_tuple(rst[r])) continue;
-            const uint8_t *row = rows + r * (uint64_t)ostride;
-            if (ld_i64(row + 16) == o && ld_i64(row) == w[t] && ld_i64(row + 8) == d[t]) {
-                found = true;
-                item = ld_i32(row + okpad);  // OL_I_ID
-            }
-        }
-    }
+    const bool found = result[t] >= 0 && produced_tuple(ost[s]);
+    const int32_t item = found ? ld_i32(oheap + (uint64_t)oimg[s] * ohstride + okpad) : 0;  // OL_I_ID
     has_item[s] = found ? 1 : 0;
     skeys[2 * s] = (uint64_t)w[t];
     skeys[2 * s + 1] = (uint64_t)(int64_t)item;
@@ -115,7 +101,7 @@ __global__ void sl_stock_keys(const int64_t *__restrict__ w, const int64_t *__re
 __global__ __launch_bounds__(64) void sl_count(uint64_t n, const int32_t *__restrict__ threshold,
                                                const uint8_t *__restrict__ has_item,
                                                const stage_probe_out_dev *__restrict__ sout,
-                                               const uint8_t *__restrict__ srows, uint32_t sstride, uint32_t skpad,
+                                               const uint8_t *__restrict__ sheap, uint32_t shstride, uint32_t skpad,
                                                int32_t *__restrict__ result) {
     const uint64_t t = blockIdx.x;
     const uint32_t lane = threadIdx.x;
@@ -130,7 +116,7 @@ __global__ __launch_bounds__(64) void sl_count(uint64_t n, const int32_t *__rest
             if (st == ST_FAIL_INVALID_TS) {
                 fail = true;
             } else if (produced_tuple(st)) {
-                const uint8_t *row = srows + s * (uint64_t)sstride;
+                const uint8_t *row = sheap + (uint64_t)sout[s].w[6] * shstride;  // the tuple read
                 below = ld_i32(row + skpad) < threshold[t];  // S_QUANTITY < threshold
                 sid = (int64_t)(int32_t)ld_i64(row + 8);     // distinct_items.insert(int(S_I_ID))
             }
@@ -175,46 +161,43 @@ extern "C" int stage_tpcc_stock_level(stage_table *district, stage_table *order_
         using namespace stage;
         hip_check(hipSetDevice(district->dev.device), "hipSetDevice");
         hipStream_t s = pick(district, stream);
-        const uint64_t ns = n * kOrdersPerTxn, nr = ns * kLinesPerScan;
+        const uint64_t ns = n * kOrdersPerTxn;
         const DevTable &dt = district->dev.view, &ot = order_line->dev.view, &st = stock->dev.view;
-        // scratch (stream-ordered)
-        uint8_t *buf = nullptr;
-        const uint64_t o_dkeys = 0, o_dout = o_dkeys + n * 16, o_drows = o_dout + n * 32,
-                       o_okeys = o_drows + n * (uint64_t)dt.stride, o_ocnt = o_okeys + ns * 32,
-                       o_orows = o_ocnt + ns * 4, o_ost = o_orows + nr * (uint64_t)ot.stride, o_skeys = o_ost + nr,
-                       o_has = o_skeys + ns * 16, o_sout = (o_has + ns + 15) & ~15ull, o_srows = o_sout + ns * 32,
-                       o_rids = o_srows + ns * (uint64_t)st.stride, total = o_rids + ns * 4;
-        hip_check(hipMallocAsync((void **)&buf, total, s), "stock-level scratch");
+        // scratch (the district table's; stream-ordered reuse); tuples are read from the record
+        // heaps in place
+        const uint64_t o_dkeys = 0, o_dout = o_dkeys + n * 16, o_okeys = o_dout + n * 32, o_oimg = o_okeys + ns * 32,
+                       o_ost = o_oimg + ns * 4, o_has = o_ost + ns, o_skeys = (o_has + ns + 15) & ~15ull,
+                       o_sout = o_skeys + ns * 16, o_rids = o_sout + ns * 32, total = o_rids + ns * 4;
+        uint8_t *buf = scratch_bytes(district->dev, total);
         auto *dkeys = (uint64_t *)(buf + o_dkeys);
         auto *dout = (stage_probe_out_dev *)(buf + o_dout);
         auto *okeys = (uint64_t *)(buf + o_okeys);
-        auto *ocnt = (uint32_t *)(buf + o_ocnt);
+        auto *oimg = (uint32_t *)(buf + o_oimg);
         auto *ost = buf + o_ost;
         auto *skeys = (uint64_t *)(buf + o_skeys);
         auto *has = buf + o_has;
         auto *sout = (stage_probe_out_dev *)(buf + o_sout);
         auto *orids = (uint32_t *)(buf + o_rids);
         const unsigned b256 = (unsigned)((n + 255) / 256), bs256 = (unsigned)((ns + 255) / 256);
-        // 1. DISTRICT point lookups
+        // 1. DISTRICT point lookups (status + heap row; no row copies)
         sl_district_keys<<<b256, 256, 0, s>>>(d_w_ids, d_d_ids, n, dkeys);
-        hip_check(launch_probe(dt, dkeys, nullptr, d_read_ids, nullptr, n, dout, buf + o_drows, s, district->tune),
+        hip_check(launch_probe(dt, dkeys, nullptr, d_read_ids, nullptr, n, dout, nullptr, s, district->tune),
                   "district probe");
-        // 2. ORDER_LINE range scans (IndexScanExecutor range branch), all transactions at once
-        sl_order_keys<<<b256, 256, 0, s>>>(d_w_ids, d_d_ids, n, dout, buf + o_drows, dt.stride,
+        // 2. ORDER_LINE range scans of 10 (IndexScanExecutor range branch), all transactions at
+        //    once, each kept up to its first produced tuple of order (w, d, o)
+        sl_order_keys<<<b256, 256, 0, s>>>(d_w_ids, d_d_ids, n, dout, dt.heap, dt.hstride,
                                            district->host->key_pad(), d_result, okeys);
         sl_spread_rids<<<bs256, 256, 0, s>>>(d_read_ids, ns, orids);
-        hip_check(launch_scan(ot, okeys, nullptr, ns, kLinesPerScan, ocnt, buf + o_orows, s, order_line->scan_tune,
-                              orids, ost),
+        hip_check(launch_scan_first(ot, okeys, ns, kLinesPerScan, orids, 3, oimg, ost, s, order_line->scan_tune),
                   "order-line scans");
         // 3. STOCK point lookups of each scan's first item, then the distinct count
-        sl_stock_keys<<<bs256, 256, 0, s>>>(d_w_ids, d_d_ids, n, d_result, okeys, ocnt, buf + o_orows, ost, ot.stride,
+        sl_stock_keys<<<bs256, 256, 0, s>>>(d_w_ids, n, d_result, oimg, ost, ot.heap, ot.hstride,
                                             order_line->host->key_pad(), skeys, has);
-        hip_check(launch_probe(st, skeys, nullptr, orids, nullptr, ns, sout, buf + o_srows, s, stock->tune),
+        hip_check(launch_probe(st, skeys, nullptr, orids, nullptr, ns, sout, nullptr, s, stock->tune),
                   "stock probe");
-        sl_count<<<(unsigned)n, 64, 0, s>>>(n, d_thresholds, has, sout, buf + o_srows, st.stride,
-                                            stock->host->key_pad(), d_result);
+        sl_count<<<(unsigned)n, 64, 0, s>>>(n, d_thresholds, has, sout, st.heap, st.hstride, stock->host->key_pad(),
+                                            d_result);
         hip_check(hipGetLastError(), "stock-level kernels");
-        hip_check(hipFreeAsync(buf, s), "free");
         return STAGE_OK;
     });
 }

@@ -1,0 +1,422 @@
+// write_path.hip -- the YCSB-B write path on the device.
+//
+// stage_update_batch_device applies an epoch of column updates, each optionally committed,
+// with the host path's semantics (HostTable::update / commit_update = LeafNode::Update,
+// b_tree.cpp:1061-1163, and the CommitTransaction UPDATE entry, transaction_manager.cpp:610-676),
+// directly on the HBM image:
+//   1. locate   probe_kernel without rows: each key's leaf and first visible slot
+//               (SearchRecordMeta);
+//   2. group    radix sort of (slot location, op index): a slot's ops stay in batch order;
+//   3. decide   every op's return code.  An op's outcome depends only on the slot state left
+//               by the previous successful op of its group (in-flight flag, cstamp, the
+//               patched column); failures leave the state unchanged.  Each op is first
+//               evaluated as if its predecessor succeeded, which is exact for the group's
+//               leading run of successes; a group with a failure is finished by one wave that
+//               evaluates the next 64 ops against the last success and jumps to the first that
+//               succeeds;
+//   4. number   exclusive scan of successes and commits: overwrite-copy, image and version
+//               indices in (slot, batch) order;
+//   5. write    per success (one wave) the overwrite-copy header, the retired-version header
+//               when committed, and the new heap row: the record's row at epoch start with the
+//               column window patched (all ops of a call patch the same window, so the k-th
+//               successive image is the epoch-start row with the k-th delta);
+//   6. publish  the last success of each group rewrites the slot word (meta, next, image).
+// The host then adopts the bookkeeping (HostTable::adopt_device_epoch): the new copy / version
+// headers and the touched slot words come back over PCIe; payload bytes stay in HBM until a
+// host-side path needs them (stage_capi::ensure_host_rows).
+#include <hip/hip_runtime.h>
+
+#include <hipcub/hipcub.hpp>
+
+#include <vector>
+
+#include "handle.hpp"
+
+using namespace stage_capi;
+
+namespace stage {
+namespace {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+struct WpArgs {
+    const uint64_t *loc;     // sorted slot locations (device leaf * cap + slot); `none` = key absent
+    const uint32_t *op;      // sorted op indices
+    const uint32_t *gs;      // sorted position -> its group's first position
+    const uint8_t *deltas;
+    const uint32_t *writer;
+    const uint32_t *cid;     // nullptr: no op commits
+    const uint32_t *sst;     // nullptr: sstamp = commit id
+    uint64_t n, none;
+    uint32_t delta_len, win_off;  // window = row bytes [win_off, win_off + delta_len)
+    uint32_t bad_range;
+};
+
+__device__ __forceinline__ uint32_t commit_of(const WpArgs &a, uint32_t o) { return a.cid ? a.cid[o] : 0u; }
+
+// reference ReturnCode of op at sorted position q given the slot state after sorted position
+// `last` (-1: the state at epoch start)
+__device__ uint8_t wp_eval(const WpArgs &a, const DevTable &t, uint64_t q, int64_t last, const SlotInfo &base) {
+    const uint32_t o = a.op[q];
+    bool inserting;
+    uint32_t cst;
+    const uint8_t *win;
+    if (last < 0) {
+        inserting = meta_inserting(base.meta);
+        cst = meta_cstamp(base.meta);
+        win = t.heap + (uint64_t)base.image * t.hstride + a.win_off;
+    } else {
+        const uint32_t lo = a.op[last];
+        cst = commit_of(a, lo);
+        inserting = cst == 0;  // an uncommitted update leaves the record in flight
+        win = a.deltas + (uint64_t)lo * a.delta_len;
+    }
+    if (inserting) return STAGE_RC_DIRTY;
+    if (a.bad_range) return STAGE_RC_INVALID;
+    const uint8_t *d = a.deltas + (uint64_t)o * a.delta_len;
+    bool same = true;
+    for (uint32_t b = 0; b < a.delta_len && same; ++b) same = d[b] == win[b];
+    if (same || cst > a.writer[o]) return STAGE_RC_NOT_NEEDED_UPDATE;
+    return STAGE_RC_OK;
+}
+
+__global__ void wp_keys(const stage_probe_out_dev *__restrict__ pout, uint64_t n, uint32_t cap, uint64_t none,
+                        uint64_t *__restrict__ loc, uint32_t *__restrict__ op) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t slot = pout[i].w[2] & 0xFFFF;
+    loc[i] = slot == 0xFFFF ? none : (uint64_t)pout[i].w[1] * cap + slot;
+    op[i] = (uint32_t)i;
+}
+
+__global__ void wp_heads(const uint64_t *__restrict__ loc, uint64_t n, uint32_t *__restrict__ head) {
+    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    head[q] = (q == 0 || loc[q] != loc[q - 1]) ? (uint32_t)q : 0u;
+}
+
+// step 3a: every op evaluated against its predecessor-as-success
+__global__ void wp_speculate(WpArgs a, DevTable t, uint8_t *__restrict__ rcs, uint8_t *__restrict__ succ,
+                             int32_t *__restrict__ prev, uint32_t *__restrict__ first_fail) {
+    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= a.n) return;
+    if (a.loc[q] == a.none) {
+        rcs[q] = STAGE_RC_NOT_FOUND;
+        succ[q] = 0;
+        prev[q] = -1;
+        return;
+    }
+    const uint32_t g = a.gs[q];
+    const int64_t last = q > g ? (int64_t)q - 1 : -1;
+    const SlotInfo base = t.slot[a.loc[q]];
+    const uint8_t r = wp_eval(a, t, q, last, base);
+    rcs[q] = r;
+    succ[q] = r == STAGE_RC_OK;
+    prev[q] = (int32_t)last;
+    if (r != STAGE_RC_OK) atomicMin(&first_fail[g], (uint32_t)q);
+}
+
+// step 3b: groups with a failure, one wave each, from the first failure on
+__global__ __launch_bounds__(256) void wp_finish_groups(WpArgs a, DevTable t, uint8_t *__restrict__ rcs,
+                                                        uint8_t *__restrict__ succ, int32_t *__restrict__ prev,
+                                                        const uint32_t *__restrict__ first_fail) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t base_q = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64;
+    const uint64_t mine = base_q + lane;
+    const bool start = mine < a.n && a.loc[mine] != a.none && a.gs[mine] == mine && first_fail[mine] != 0xFFFFFFFFu;
+    uint64_t groups = __builtin_amdgcn_ballot_w64(start);
+    while (groups) {
+        const uint64_t g = base_q + __builtin_ctzll(groups);
+        groups &= groups - 1;
+        const uint64_t l = a.loc[g];
+        const SlotInfo base = t.slot[l];
+        const uint64_t f = first_fail[g];
+        int64_t last = f > g ? (int64_t)f - 1 : -1;  // [g, f) all succeeded
+        uint64_t pos = f;
+        while (pos < a.n) {
+            const uint64_t q = pos + lane;
+            const bool in = q < a.n && a.loc[q] == l;
+            const uint8_t r = in ? wp_eval(a, t, q, last, base) : (uint8_t)0xFF;
+            const uint64_t okm = __builtin_amdgcn_ballot_w64(in && r == STAGE_RC_OK);
+            const uint64_t inm = __builtin_amdgcn_ballot_w64(in);
+            if (okm) {
+                const uint32_t first = (uint32_t)__builtin_ctzll(okm);
+                if (in && lane <= first) {
+                    rcs[q] = r;
+                    succ[q] = lane == first;
+                    prev[q] = (int32_t)last;
+                }
+                last = (int64_t)(pos + first);
+                pos = (uint64_t)last + 1;
+                continue;
+            }
+            if (in) {
+                rcs[q] = r;
+                succ[q] = 0;
+                prev[q] = (int32_t)last;
+            }
+            if (inm != ~0ull) break;  // the group ends inside this chunk
+            pos += 64;
+        }
+    }
+}
+
+// step 4 input: successes in the low word, committed successes in the high word
+__global__ void wp_flags(WpArgs a, const uint8_t *__restrict__ succ, uint64_t *__restrict__ flags) {
+    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= a.n) return;
+    const uint64_t s = succ[q] ? 1ull : 0ull;
+    flags[q] = s | ((s && commit_of(a, a.op[q]) != 0) ? (1ull << 32) : 0ull);
+}
+
+__global__ void wp_totals(const uint64_t *__restrict__ ranks, const uint64_t *__restrict__ flags, uint64_t n,
+                          uint64_t *__restrict__ tot) {
+    const uint64_t v = ranks[n - 1] + flags[n - 1];
+    tot[0] = v & 0xFFFFFFFFull;
+    tot[1] = v >> 32;
+}
+
+// step 5: one wave per sorted position; successes write their headers and their new row
+__global__ __launch_bounds__(256) void wp_write(WpArgs a, DevTable t, uint8_t *__restrict__ heap,
+                                                CopyHdr *__restrict__ chdr, VersionHdr *__restrict__ vhdr,
+                                                const uint8_t *__restrict__ succ, const int32_t *__restrict__ prev,
+                                                const uint64_t *__restrict__ ranks, uint32_t *__restrict__ last_succ,
+                                                uint64_t cbase, uint64_t vbase, uint64_t ibase) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    for (uint64_t q = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); q < a.n; q += nwaves) {
+        if (!succ[q]) continue;
+        const uint32_t o = a.op[q];
+        const SlotInfo base = t.slot[a.loc[q]];
+        const uint64_t rk = ranks[q];
+        const uint64_t irank = rk & 0xFFFFFFFFull, vrank = rk >> 32;
+        const uint32_t cid = commit_of(a, o);
+        const uint64_t img = ibase + irank;
+        if (lane == 0) {
+            const int32_t p = prev[q];
+            CopyHdr c;
+            if (p < 0) {  // first success of the group: the epoch-start record
+                c.rstamp = meta_cstamp(base.meta);
+                c.next = base.next;
+                c.image = base.image;
+            } else {      // the previous success, committed (an in-flight one makes this op DIRTY)
+                const uint64_t pr = ranks[p];
+                c.rstamp = commit_of(a, a.op[p]);
+                c.next = kNextVersion | (uint32_t)(vbase + (pr >> 32));
+                c.image = (uint32_t)(ibase + (pr & 0xFFFFFFFFull));
+            }
+            c.sstamp = cid ? (a.sst ? a.sst[o] : cid) : kMaxCid;
+            chdr[cbase + irank] = c;
+            if (cid) vhdr[vbase + vrank] = VersionHdr{c.rstamp, c.sstamp, c.next, c.image};
+            atomicMax(&last_succ[a.gs[q]], (uint32_t)q + 1u);
+        }
+        // new row: epoch-start row with the window patched (CopyPayload)
+        const uint8_t *src = t.heap + (uint64_t)base.image * t.hstride;
+        uint8_t *dst = heap + img * t.hstride;
+        const uint8_t *d = a.deltas + (uint64_t)o * a.delta_len;
+        const uint32_t w0 = a.win_off, w1 = a.win_off + a.delta_len;
+        for (uint32_t c = lane; c < t.hstride / 16; c += 64) {
+            u32x4 v = reinterpret_cast<const u32x4 *>(src)[c];
+            const uint32_t b0 = c * 16;
+            if (b0 + 16 > w0 && b0 < w1) {
+                union {
+                    u32x4 v;
+                    uint8_t b[16];
+                } u;
+                u.v = v;
+                for (uint32_t j = 0; j < 16; ++j)
+                    if (b0 + j >= w0 && b0 + j < w1) u.b[j] = d[b0 + j - w0];
+                v = u.v;
+            }
+            reinterpret_cast<u32x4 *>(dst)[c] = v;
+        }
+    }
+}
+
+struct FinRec {
+    uint64_t loc, meta;
+    uint32_t next, image;
+};
+
+// step 6: the last success of each group publishes the slot word; every op gets its code
+__global__ void wp_publish(WpArgs a, SlotInfo *__restrict__ slot, const uint8_t *__restrict__ rcs,
+                           const uint8_t *__restrict__ succ, const int32_t *__restrict__ prev,
+                           const uint64_t *__restrict__ ranks, const uint32_t *__restrict__ last_succ,
+                           uint64_t cbase, uint64_t vbase, uint64_t ibase, FinRec *__restrict__ fin,
+                           uint8_t *__restrict__ rc_out) {
+    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= a.n) return;
+    const uint32_t o = a.op[q];
+    rc_out[o] = rcs[q];
+    if (!succ[q] || last_succ[a.gs[q]] != q + 1) return;
+    const uint64_t l = a.loc[q];
+    const uint64_t m0 = slot[l].meta;
+    const uint32_t cid = commit_of(a, o);
+    const uint64_t rk = ranks[q];
+    auto committed_meta = [&](uint32_t c) { return ((m0 | kMetaVisible) & ~kMetaTxn & ~kMetaControl) | c; };
+    uint64_t meta;
+    uint32_t next;
+    if (cid) {  // PrepareForUpdate then FinalizeForUpdate(t_cstamp)
+        meta = committed_meta(cid);
+        next = kNextVersion | (uint32_t)(vbase + (rk >> 32));
+    } else {    // still in flight
+        const int32_t p = prev[q];
+        const uint64_t mb = p < 0 ? m0 : committed_meta(commit_of(a, a.op[p]));
+        meta = mb | kMetaControl | kMetaVisible;
+        next = kNextCopy | (uint32_t)(cbase + (rk & 0xFFFFFFFFull));
+    }
+    const uint32_t image = (uint32_t)(ibase + (rk & 0xFFFFFFFFull));
+    slot[l].meta = meta;
+    slot[l].next = next;
+    slot[l].image = image;
+    fin[a.gs[q]] = FinRec{l, meta, next, image};
+}
+
+unsigned blocks_for(uint64_t n, unsigned per) { return (unsigned)((n + per - 1) / per); }
+
+}  // namespace
+}  // namespace stage
+
+namespace stage_capi {
+void ensure_host_rows(stage_table *t) {
+    if (!t->host->has_device_rows()) return;
+    using namespace stage;
+    hip_check(hipSetDevice(t->dev.device), "hipSetDevice");
+    const uint64_t stride = t->host->hstride();
+    t->host->materialize_device_rows([&](uint64_t first, uint64_t count, uint8_t *dst) {
+        hip_check(hipMemcpy(dst, (const uint8_t *)t->dev.heap.p + first * stride, count * stride,
+                            hipMemcpyDeviceToHost),
+                  "device row fetch");
+    });
+}
+}  // namespace stage_capi
+
+extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys, const uint16_t *d_lens, uint64_t n,
+                                         uint32_t payload_off, const uint8_t *d_deltas, uint32_t delta_len,
+                                         const uint32_t *d_writer_ids, const uint32_t *d_commit_ids,
+                                         const uint32_t *d_sstamps, uint8_t *d_rc, uint64_t *n_ok, void *stream) {
+    int rc = need_synced(t);
+    if (rc) return rc;
+    if (n && (!d_keys || !d_writer_ids || !d_rc || (!d_deltas && delta_len)))
+        return fail(STAGE_E_ARG, "null device buffer");
+    if (n >= (1ull << 31)) return fail(STAGE_E_ARG, "batch too large");
+    if (n_ok) *n_ok = 0;
+    if (n == 0) return STAGE_OK;
+    return guarded([&] {
+        using namespace stage;
+        HostTable &h = *t->host;
+        DeviceImage &dv = t->dev;
+        hip_check(hipSetDevice(dv.device), "hipSetDevice");
+        hipStream_t s = pick(t, stream);
+        // room for one copy, image and version per op
+        reserve_device_rows(h, dv, n, n, n, s);
+        const DevTable &view = dv.view;
+        const uint64_t cbase = h.copies_.size(), vbase = h.versions_.size(), ibase = h.images_.size();
+        const uint64_t none = (uint64_t)view.nleaves * view.cap;
+        int end_bit = 1;
+        while (end_bit < 64 && (none >> end_bit)) ++end_bit;
+
+        // scratch
+        size_t cub_sort = 0, cub_scan = 0, cub_sum = 0;
+        hip_check(hipcub::DeviceRadixSort::SortPairs(nullptr, cub_sort, (uint64_t *)nullptr, (uint64_t *)nullptr,
+                                                     (uint32_t *)nullptr, (uint32_t *)nullptr, (int)n, 0, end_bit, s),
+                  "sort size");
+        hip_check(hipcub::DeviceScan::InclusiveScan(nullptr, cub_scan, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                                    hipcub::Max(), (int)n, s),
+                  "scan size");
+        hip_check(hipcub::DeviceScan::ExclusiveSum(nullptr, cub_sum, (uint64_t *)nullptr, (uint64_t *)nullptr, (int)n,
+                                                   s),
+                  "sum size");
+        const size_t cub_bytes = std::max(cub_sort, std::max(cub_scan, cub_sum));
+        auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
+        uint64_t off = 0;
+        auto take = [&](uint64_t bytes) {
+            const uint64_t o = off;
+            off += al(bytes);
+            return o;
+        };
+        const uint64_t o_pout = take(n * 32), o_loc0 = take(n * 8), o_loc = take(n * 8), o_op0 = take(n * 4),
+                       o_op = take(n * 4), o_head = take(n * 4), o_gs = take(n * 4), o_rcs = take(n), o_succ = take(n),
+                       o_prev = take(n * 4), o_ff = take(n * 4), o_ls = take(n * 4), o_flags = take(n * 8),
+                       o_ranks = take(n * 8), o_fin = take(n * sizeof(FinRec)), o_tot = take(16),
+                       o_cub = take(cub_bytes);
+        uint8_t *buf = scratch_bytes(dv, off);
+        auto *pout = (stage_probe_out_dev *)(buf + o_pout);
+        auto *loc0 = (uint64_t *)(buf + o_loc0);
+        auto *loc = (uint64_t *)(buf + o_loc);
+        auto *op0 = (uint32_t *)(buf + o_op0);
+        auto *op = (uint32_t *)(buf + o_op);
+        auto *head = (uint32_t *)(buf + o_head);
+        auto *gs = (uint32_t *)(buf + o_gs);
+        auto *rcs = buf + o_rcs;
+        auto *succ = buf + o_succ;
+        auto *prev = (int32_t *)(buf + o_prev);
+        auto *ff = (uint32_t *)(buf + o_ff);
+        auto *ls = (uint32_t *)(buf + o_ls);
+        auto *flags = (uint64_t *)(buf + o_flags);
+        auto *ranks = (uint64_t *)(buf + o_ranks);
+        auto *fin = (FinRec *)(buf + o_fin);
+        auto *tot = (uint64_t *)(buf + o_tot);
+        void *cub = buf + o_cub;
+        size_t cb = cub_bytes;
+
+        // 1. locate
+        hip_check(launch_probe(view, d_keys, d_lens, nullptr, nullptr, n, pout, nullptr, s, t->tune), "locate");
+        wp_keys<<<blocks_for(n, 256), 256, 0, s>>>(pout, n, view.cap, none, loc0, op0);
+        // 2. group
+        hip_check(hipcub::DeviceRadixSort::SortPairs(cub, cb, loc0, loc, op0, op, (int)n, 0, end_bit, s), "sort");
+        wp_heads<<<blocks_for(n, 256), 256, 0, s>>>(loc, n, head);
+        cb = cub_bytes;
+        hip_check(hipcub::DeviceScan::InclusiveScan(cub, cb, head, gs, hipcub::Max(), (int)n, s), "group starts");
+        // 3. decide
+        WpArgs a{loc, op, gs, d_deltas, d_writer_ids, d_commit_ids, d_sstamps, n, none, delta_len,
+                 h.key_pad() + payload_off, (uint64_t)payload_off + delta_len > h.params().payload_size ? 1u : 0u};
+        hip_check(hipMemsetAsync(ff, 0xFF, n * 4, s), "memset");
+        hip_check(hipMemsetAsync(ls, 0, n * 4, s), "memset");
+        hip_check(hipMemsetAsync(fin, 0xFF, n * sizeof(FinRec), s), "memset");
+        wp_speculate<<<blocks_for(n, 256), 256, 0, s>>>(a, view, rcs, succ, prev, ff);
+        wp_finish_groups<<<blocks_for(n, 256), 256, 0, s>>>(a, view, rcs, succ, prev, ff);
+        // 4. number
+        wp_flags<<<blocks_for(n, 256), 256, 0, s>>>(a, succ, flags);
+        cb = cub_bytes;
+        hip_check(hipcub::DeviceScan::ExclusiveSum(cub, cb, flags, ranks, (int)n, s), "ranks");
+        wp_totals<<<1, 1, 0, s>>>(ranks, flags, n, tot);
+        // 5. write, 6. publish
+        const int wblocks = (int)std::min<uint64_t>(blocks_for(n, 4), 16384);
+        wp_write<<<wblocks, 256, 0, s>>>(a, view, (uint8_t *)dv.heap.p, (CopyHdr *)dv.chdr.p, (VersionHdr *)dv.vhdr.p,
+                                         succ, prev, ranks, ls, cbase, vbase, ibase);
+        wp_publish<<<blocks_for(n, 256), 256, 0, s>>>(a, (SlotInfo *)dv.slot.p, rcs, succ, prev, ranks, ls, cbase,
+                                                      vbase, ibase, fin, d_rc);
+        hip_check(hipGetLastError(), "write-path kernels");
+
+        // the host adopts the epoch
+        uint64_t totals[2];
+        hip_check(hipMemcpyAsync(totals, tot, 16, hipMemcpyDeviceToHost, s), "totals");
+        hip_check(hipStreamSynchronize(s), "write path");
+        const uint64_t ns = totals[0], nv = totals[1];
+        std::vector<CopyHdr> copies(ns);
+        std::vector<VersionHdr> versions(nv);
+        std::vector<FinRec> fr(n);
+        if (ns)
+            hip_check(hipMemcpyAsync(copies.data(), (CopyHdr *)dv.chdr.p + cbase, ns * sizeof(CopyHdr),
+                                     hipMemcpyDeviceToHost, s),
+                      "copy headers");
+        if (nv)
+            hip_check(hipMemcpyAsync(versions.data(), (VersionHdr *)dv.vhdr.p + vbase, nv * sizeof(VersionHdr),
+                                     hipMemcpyDeviceToHost, s),
+                      "version headers");
+        hip_check(hipMemcpyAsync(fr.data(), fin, n * sizeof(FinRec), hipMemcpyDeviceToHost, s), "slot words");
+        hip_check(hipStreamSynchronize(s), "write path adopt");
+        std::vector<HostTable::SlotWords> sw;
+        sw.reserve(ns);
+        const uint32_t cap = view.cap;
+        for (const FinRec &f : fr) {
+            if (f.loc == ~0ull) continue;
+            const uint64_t hl = dv.dev_to_host[f.loc / cap];
+            sw.push_back(HostTable::SlotWords{hl * cap + f.loc % cap, f.meta, f.next, f.image});
+        }
+        h.adopt_device_epoch(copies.data(), ns, versions.data(), nv, ns, sw.data(), sw.size());
+        if (n_ok) *n_ok = ns;
+        return STAGE_OK;
+    });
+}

@@ -202,6 +202,30 @@ class Table:
                                        ctypes.byref(ok)), "update_batch")
         return rc, ok.value
 
+    def update_batch_device(self, keys, payload_off, deltas, writer_ids, commit_ids=None, sstamps=None, lens=None):
+        """stage_update_batch_device: the same epoch applied by the device to the published
+        image (keys as for probe: integers, or (n, width) uint8 key bytes); returns (rc, n_ok)."""
+        words, n = self.key_buffer(keys)
+        deltas = np.ascontiguousarray(deltas, np.uint8).reshape(n, -1) if n else np.zeros((0, 0), np.uint8)
+        wid = np.ascontiguousarray(np.broadcast_to(np.asarray(writer_ids, np.uint32), (n,)))
+        bufs = [DeviceBuffer.from_numpy(words) if n else DeviceBuffer(8),
+                DeviceBuffer.from_numpy(deltas.reshape(-1)) if deltas.size else DeviceBuffer(8),
+                DeviceBuffer.from_numpy(wid) if n else DeviceBuffer(8)]
+        opt = []
+        for a, dt in ((commit_ids, np.uint32), (sstamps, np.uint32), (lens, np.uint16)):
+            if a is None or not n:
+                opt.append(None)
+            else:
+                bufs.append(DeviceBuffer.from_numpy(np.ascontiguousarray(np.broadcast_to(np.asarray(a, dt), (n,)))))
+                opt.append(bufs[-1].ptr)
+        d_rc = DeviceBuffer(max(n, 1))
+        ok = ctypes.c_uint64()
+        check(lib().stage_update_batch_device(self.h, bufs[0].ptr, opt[2], n, payload_off, bufs[1].ptr,
+                                              deltas.shape[1] if n else 0, bufs[2].ptr, opt[0], opt[1], d_rc.ptr,
+                                              ctypes.byref(ok), None), "update_batch_device")
+        rc = d_rc.to_numpy(np.uint8, n) if n else np.zeros(0, np.uint8)
+        return rc, ok.value
+
     def finalize_update(self, key, commit_id, key_size=None):
         rc = ctypes.c_uint8()
         check(lib().stage_finalize_update(self.h, int(key), key_size or self.key_width, commit_id, ctypes.byref(rc)),

@@ -1,0 +1,191 @@
+"""GPU parity of the device write path (stage_update_batch_device).
+
+Each epoch is applied by the device to the published image; the reference semantics are the
+oracle's LeafNode::Update + CommitTransaction UPDATE entry applied op by op in batch order.
+After every epoch the device must return the oracle's return codes and answer every read
+(latest, in-flight copy, retired versions at old read ids, range scans) like the oracle, and
+host-side writes after a device epoch must still behave like the reference.
+"""
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import stage
+from test_gpu_incremental import check_all
+from test_gpu_parity import check_probe
+from test_leaf_images import assert_same_images
+
+pytestmark = pytest.mark.gpu
+
+
+def oracle_epoch(orc, keys, key_size, off, deltas, wid, cid):
+    rc = np.zeros(len(keys), np.uint8)
+    for i in range(len(keys)):
+        k = keys[i] if isinstance(keys[i], bytes) else int(keys[i])
+        r = orc.update(k, key_size, off, deltas[i].tobytes(), int(wid[i]))
+        if r == stage.RC_OK and cid[i]:
+            r = orc.commit_update(k, key_size, int(cid[i]), int(cid[i]))
+        rc[i] = r
+    return rc
+
+
+def epoch_ops(rng, base, hot, m, counter):
+    """keys: uniform, a hot set with repeats, absent keys; deltas: random, or one per hot key
+    (its repeats are NotNeededUpdate); ids from one counter; ~12 % left in flight."""
+    kind = rng.random(m)
+    keys = np.where(kind < 0.6, rng.choice(base, m), rng.choice(hot, m))
+    keys = np.where(kind > 0.93, rng.choice(base, m) + 1, keys).astype(np.uint64)  # absent
+    deltas = rng.integers(0, 256, (m, 24), dtype=np.uint8)
+    fixed = (kind >= 0.6) & (kind < 0.8)
+    deltas[fixed] = (keys[fixed] % 251).astype(np.uint8)[:, None]
+    wid = (counter + 2 * np.arange(m)).astype(np.uint32)
+    wid[rng.random(m) < 0.03] = 1  # older writer than the committed record -> NotNeededUpdate
+    cid = (wid + 1).astype(np.uint32)
+    cid[rng.random(m) < 0.12] = 0
+    return keys, deltas, wid, cid
+
+
+def test_device_epochs_match_oracle(gpu):
+    n = 120000
+    base = np.arange(n, dtype=np.uint64) * 4
+    tab = stage.Table(key_width=8)
+    orc = O.OracleTree()
+    tab.load_keys(base, 8, mode=1)
+    orc.load_keys(base, 8, 1)
+    tab.sync()
+    rng = np.random.default_rng(41)
+    hot = rng.choice(base, 40, replace=False)
+    counter = 10
+    seen = set()
+    for epoch in range(4):
+        m = 12000
+        keys, deltas, wid, cid = epoch_ops(rng, base, hot, m, counter)
+        counter += 2 * m + 2
+        off = 100 * epoch + 3
+        rc, ok = tab.update_batch_device(keys, off, deltas, wid, cid)
+        exp = oracle_epoch(orc, keys, 8, off, deltas, wid, cid)
+        bad = np.nonzero(rc != exp)[0]
+        assert bad.size == 0, (epoch, bad[:5], rc[bad[:5]], exp[bad[:5]], keys[bad[:5]])
+        assert ok == int(((exp == stage.RC_OK)).sum())
+        seen |= set(rc.tolist())
+        if epoch == 1:  # host writes after a device epoch (device rows materialised first)
+            for k in rng.choice(hot, 5, replace=False):
+                d = rng.integers(0, 256, 16, dtype=np.uint8)
+                assert tab.update(int(k), 7, d, counter) == orc.update(int(k), 8, 7, d.tobytes(), counter)
+            for k in rng.choice(base, 200, replace=False):
+                assert tab.delete(int(k), counter) == orc.delete(int(k), 8, counter)
+            tab.sync()
+            assert tab.sync_info()["incremental"]
+        if epoch == 2:  # the host batch path on top of device epochs
+            k2, d2, w2, c2 = epoch_ops(rng, base, hot, 3000, counter)
+            counter += 6002
+            rc2, _ = tab.update_batch(k2, 11, d2, w2, c2)
+            assert (rc2 == oracle_epoch(orc, k2, 8, 11, d2, w2, c2)).all()
+            tab.sync()
+        probe = np.concatenate([hot, rng.choice(keys, 3000), rng.choice(base, 2000)]).astype(np.uint64)
+        check_all(tab, orc, probe, rng, counter)
+    assert {stage.RC_OK, stage.RC_NOT_FOUND, stage.RC_NOT_NEEDED_UPDATE, stage.RC_DIRTY} <= seen
+    assert_same_images(tab, orc)
+
+
+def test_device_epoch_equals_host_epoch_zipf(gpu):
+    """YCSB-B shaped epoch (Zipf 0.99, one delta per key per epoch: a hot key's repeats are
+    NotNeededUpdate): codes and every read equal the host write path's."""
+    n = 400000
+    a, b = stage.Table(key_width=8), stage.Table(key_width=8)
+    for t in (a, b):
+        t.load_ycsb(0, n, 8, mode=0)
+        t.sync()
+    counter = 1
+    for epoch in range(3):
+        keys = stage.zipf_draws(n - 1, 0.99, 77 + epoch, 100000)
+        m = keys.size
+        wid = (counter + 2 * np.arange(m)).astype(np.uint32)
+        cid = (wid + 1).astype(np.uint32)
+        counter += 2 * m
+        cols = np.repeat(((keys + np.uint64(epoch + 1)) & np.uint64(0xFF)).astype(np.uint8)[:, None], 100, 1)
+        rc_a, ok_a = a.update_batch(keys, 0, cols, wid, cid)
+        a.sync()
+        rc_b, ok_b = b.update_batch_device(keys, 0, cols, wid, cid)
+        assert ok_a == ok_b and (rc_a == rc_b).all()
+        assert (rc_b == stage.RC_NOT_NEEDED_UPDATE).sum() > m // 4  # long groups were finished
+        probe = np.unique(keys)
+        for rid in (0, counter // 3, counter // 2, 0xFFFFFFFE):
+            rids = np.full(probe.size, rid, np.uint32)
+            oa, ra = a.probe(probe, read_ids=rids)
+            ob, rb = b.probe(probe, read_ids=rids)
+            for f in ("status", "flags", "hops", "leaf", "slot", "cstamp", "rec_cstamp", "copy_sstamp"):
+                assert (oa[f] == ob[f]).all(), (epoch, rid, f)
+            assert (ra == rb).all()
+
+
+def test_device_epoch_wide_keys(gpu):
+    """16-byte composite keys (TPC-C StockKey layout, unsigned memcmp order)."""
+    rng = np.random.default_rng(5)
+    wi = np.stack(np.meshgrid(np.arange(1, 5), np.arange(1, 6001), indexing="ij"), -1).reshape(-1, 2)
+    keys = np.ascontiguousarray(wi.astype(np.int64)).view(np.uint8).reshape(-1, 16)
+    pays = rng.integers(0, 256, (keys.shape[0], 400), dtype=np.uint8)
+    tab = stage.Table(payload_size=400, key_width=16)
+    tab.load_rows(keys, pays)
+    tab.sync()
+    orc = O.OracleTree(payload_size=400, key_pad=16)
+    orc.load_rows(keys, pays)
+    counter = 5
+    for epoch in range(3):
+        m = 3000
+        idx = rng.integers(0, keys.shape[0] + 200, m)  # some absent
+        uk = np.zeros((m, 16), np.uint8)
+        present = idx < keys.shape[0]
+        uk[present] = keys[idx[present]]
+        uk[~present] = np.ascontiguousarray(np.stack([np.full((~present).sum(), 9), idx[~present]], 1)
+                                            .astype(np.int64)).view(np.uint8).reshape(-1, 16)
+        deltas = rng.integers(0, 256, (m, 4), dtype=np.uint8)
+        deltas[::7] = 1
+        wid = (counter + 2 * np.arange(m)).astype(np.uint32)
+        cid = (wid + 1).astype(np.uint32)
+        cid[::9] = 0
+        counter += 2 * m
+        rc, _ = tab.update_batch_device(uk, 0, deltas, wid, cid)
+        exp = oracle_epoch(orc, [bytes(r) for r in uk], 16, 0, deltas, wid, cid)
+        assert (rc == exp).all()
+        for rid in (0, counter // 2, 0xFFFFFFFE):
+            out, rows = tab.probe(uk, read_ids=np.full(m, rid, np.uint32))
+            o_out, o_rec = orc.read_batch_k(uk, np.full(m, rid, np.uint32))
+            for f in ("status", "hops", "cstamp", "rec_cstamp", "copy_sstamp"):
+                assert (out[f] == o_out[f]).all(), (epoch, rid, f)
+            assert (rows[:, :orc.row] == o_rec).all()
+
+
+def test_device_epoch_edge_cases(gpu):
+    tab = stage.Table(key_width=8)
+    tab.load_ycsb(0, 5000, 8, mode=0)
+    tab.sync()
+    orc = O.OracleTree()
+    orc.load_ycsb(0, 5000, 8, 0)
+    # empty batch
+    rc, ok = tab.update_batch_device(np.zeros(0, np.uint64), 0, np.zeros((0, 8), np.uint8), [])
+    assert rc.size == 0 and ok == 0
+    # window past the payload: every op Invalid
+    k = np.array([1, 2, 2], np.uint64)
+    rc, ok = tab.update_batch_device(k, 995, np.ones((3, 8), np.uint8), 3, 4)
+    assert ok == 0 and (rc == oracle_epoch(orc, k, 8, 995, np.ones((3, 8), np.uint8), [3] * 3, [4] * 3)).all()
+    # one key many times, alternating deltas, no commits: first OK, then Dirty (in flight)
+    k = np.full(200, 7, np.uint64)
+    d = np.where(np.arange(200)[:, None] % 2 == 0, 1, 2).astype(np.uint8).repeat(8, 1)
+    w = np.arange(10, 210, dtype=np.uint32)
+    rc, ok = tab.update_batch_device(k, 0, d, w, None)
+    assert (rc == oracle_epoch(orc, k, 8, 0, d, w, np.zeros(200, np.uint32))).all() and ok == 1
+    # all commits, alternating deltas: every op succeeds (a 200-version chain)
+    k = np.full(200, 9, np.uint64)
+    w = np.arange(1000, 1400, 2, dtype=np.uint32)
+    rc, ok = tab.update_batch_device(k, 0, d, w, w + 1)
+    assert (rc == oracle_epoch(orc, k, 8, 0, d, w, w + 1)).all() and ok == 200
+    # a table that was written on the host but not published is refused
+    tab.update(11, 0, b"x" * 8, 5000)
+    with pytest.raises(stage.StageError):
+        tab.update_batch_device(np.array([12], np.uint64), 0, np.ones((1, 8), np.uint8), 6000)
+    orc.update(11, 8, 0, b"x" * 8, 5000)
+    tab.sync()
+    keys = np.array([1, 2, 7, 9, 11, 4999, 5000], np.uint64)
+    for rid in (0, 5, 1100, 1399, 0xFFFFFFFE):
+        check_probe(tab, orc, keys, 8, read_ids=np.full(keys.size, rid, np.uint32))
