@@ -10,9 +10,10 @@ Default (`--config c2`, BASELINE.json configs[1]): YCSB-C batched point lookup.
           with --gpus > 1 each key goes to shard MurmurHash64A(key, 8, 0) % world and is
           answered over RCCL (stage_probe_sharded) -- configs[4] at 8 GPUs
   value = lookups completed by all ranks / max-over-ranks wall time of the K timed steps.
-`--config c3` (configs[2]): YCSB-B epochs -- 5 % updates (zipf 0.99) applied on the host
-  write path between steps, the step probes the reads (25 % at older snapshots -> version
-  chains on the device).  `--config c4` (configs[3]): 100-key range scans.
+`--config c3` (configs[2]): YCSB-B epochs -- 5 % updates (zipf 0.99) applied between steps
+  by the device write path (stage_update_batch_device; `--write-path host` = host write path +
+  incremental publish), the step probes the reads (25 % at older snapshots -> version chains
+  on the device).  `--config c4` (configs[3]): 100-key range scans.
 
 The CPU baseline leg (rank 0, one GPU) times the test oracle -- the C restatement of the
 reference's BTree::Read + executor copy (or TableScanExecutor) -- on a bounded 2M-row sample
@@ -24,6 +25,7 @@ import json
 import math
 import os
 import platform
+import resource
 import sys
 import time
 
@@ -68,6 +70,9 @@ def parse():
     p.add_argument("--theta", type=float, default=None)
     p.add_argument("--scan-size", type=int, default=100)
     p.add_argument("--update-ratio", type=float, default=0.05)
+    p.add_argument("--write-path", choices=["device", "host"], default="device",
+                   help="c3: apply each epoch's updates on the device (stage_update_batch_device) or on the "
+                        "host write path + incremental publish (stage_update_batch + stage_sync)")
     p.add_argument("--seed", type=int, default=0x5EED)
     p.add_argument("--cpu-rows", type=int, default=2_000_000)
     p.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -188,13 +193,26 @@ class YcsbB:
         self.counter += 2 * m
         cols = np.repeat(((keys + np.uint64(self.epoch + 1)) & np.uint64(0xFF)).astype(np.uint8)[:, None], 100, 1)
         tu = time.time()
-        _, ok = self.tab.update_batch(keys, 0, cols, rid, cid)
-        self.update_s += time.time() - tu
+        if a.write_path == "device":
+            # keys / ids / column patches over PCIe, then the epoch runs on the published image
+            L = stage.lib()
+            bufs = [stage.DeviceBuffer.from_numpy(x) for x in (keys, cols.reshape(-1), rid, cid)] if m else None
+            d_rc = stage.DeviceBuffer(max(m, 1))
+            ok = ctypes.c_uint64()
+            if m:
+                check(L.stage_update_batch_device(self.tab.h, bufs[0].ptr, None, m, 0, bufs[1].ptr, 100, bufs[2].ptr,
+                                                  bufs[3].ptr, None, d_rc.ptr, ctypes.byref(ok), None),
+                      "update_batch_device")
+            ok = ok.value
+            self.update_s += time.time() - tu
+        else:
+            _, ok = self.tab.update_batch(keys, 0, cols, rid, cid)
+            self.update_s += time.time() - tu
+            t1 = time.time()
+            self.tab.sync()
+            self.sync_s += time.time() - t1
+            self.last_sync = self.tab.sync_info()
         self.updates += ok
-        t1 = time.time()
-        self.tab.sync()
-        self.sync_s += time.time() - t1
-        self.last_sync = self.tab.sync_info()
         self.host_s += time.time() - t0
         reads = draws[~is_upd]
         rids = np.full(reads.size, self.counter, np.uint32)
@@ -536,16 +554,18 @@ def main():
             config["theta"] = args.theta
         if ycsb_b is not None:
             config.update({"update_ratio": args.update_ratio, "updates_applied": ycsb_b.updates,
-                           "host_write_and_publish_s": round(ycsb_b.host_s, 2),
+                           "write_path": args.write_path,
+                           "write_and_publish_s": round(ycsb_b.host_s, 2),
                            "update_batch_s": round(ycsb_b.update_s, 3), "publish_s": round(ycsb_b.sync_s, 3),
                            "last_publish": ycsb_b.last_sync,
-                           "ops_per_s_incl_host_writes": round((ops_done + ycsb_b.updates) /
+                           "ops_per_s_incl_writes": round((ops_done + ycsb_b.updates) /
                                                                (elapsed + ycsb_b.host_s), 1),
                            "read_status_counts": {"latest": int(status_hist[1]), "copy": int(status_hist[2]),
                                                   "old": int(status_hist[3]), "fail": int(status_hist[4]),
                                                   "chain_miss": int(status_hist[5]),
                                                   "not_found": int(status_hist[0])},
-                           "timed": "device probe of the read share; host updates between steps excluded"})
+                           "timed": "device probe of the read share; the epoch's updates between steps excluded "
+                                    "(they are in ops_per_s_incl_writes)"})
         result = {
             "metric": METRIC, "value": round(value, 1), "unit": unit, "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
@@ -553,6 +573,7 @@ def main():
             "config": config, "roofline": roof, "cpu_baseline": cpu, "self_check": ok,
             **({"owner_reply": owner} if owner else {}),
             "setup_s": {"load": round(t_load, 1), "sync": round(t_sync, 1)},
+            "host_peak_rss_gib": round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20, 1),
         }
         print(json.dumps(result), flush=True)
     if dist:

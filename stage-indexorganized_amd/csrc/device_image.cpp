@@ -332,14 +332,15 @@ void sync_device(HostTable &h, DeviceImage &d) {
         build_leaf(h, order[di], head.data() + di * hb, okey.data() + di * cap * kw, slot.data() + di * cap);
     });
 
-    // ---- implicit 16-ary separator tree: level 0 = separators, level k+1 = max of each
-    // 16-entry node of level k, every level padded with +inf, top level one node.  An entry
-    // is kw order words (entry-major); lengths ride along for variable-length tables.
+    // ---- implicit separator tree: level 0 = separators in 8-entry nodes (a probe's bottom
+    // node is one 64-B sector for 8-B keys), level k+1 = max of each node of level k in
+    // 16-entry nodes (one 128-B line), every level padded with +inf, top level one node.  An
+    // entry is kw order words (entry-major); lengths ride along for variable-length tables.
     const uint64_t S = L ? L - 1 : 0;
     std::vector<std::vector<uint64_t>> lv;
     std::vector<std::vector<uint8_t>> lvlen;
     {
-        const uint64_t n0 = (S + 1 + kTreeFanout - 1) / kTreeFanout * kTreeFanout;
+        const uint64_t n0 = (S + 1 + kLeafFanout - 1) / kLeafFanout * kLeafFanout;
         std::vector<uint64_t> l0(n0 * kw, ~0ull);
         std::vector<uint8_t> l0len(n0, 0xFF);
         for (uint64_t i = 0; i < S; ++i) {
@@ -349,15 +350,16 @@ void sync_device(HostTable &h, DeviceImage &d) {
         }
         lv.push_back(std::move(l0));
         lvlen.push_back(std::move(l0len));
-        while (lvlen.back().size() > (uint64_t)kTreeFanout) {
+        while (lvlen.back().size() > (uint64_t)tree_fanout((int)lv.size() - 1)) {
+            const uint64_t f = (uint64_t)tree_fanout((int)lv.size() - 1);
             const auto &prev = lv.back();
             const auto &prevlen = lvlen.back();
-            const uint64_t nodes = prevlen.size() / kTreeFanout;
+            const uint64_t nodes = prevlen.size() / f;
             const uint64_t nn = (nodes + kTreeFanout - 1) / kTreeFanout * kTreeFanout;
             std::vector<uint64_t> nx(nn * kw, ~0ull);
             std::vector<uint8_t> nxlen(nn, 0xFF);
             for (uint64_t j = 0; j < nodes; ++j) {
-                const uint64_t last = j * kTreeFanout + kTreeFanout - 1;
+                const uint64_t last = j * f + f - 1;
                 for (uint32_t w = 0; w < kw; ++w) nx[j * kw + w] = prev[last * kw + w];
                 nxlen[j] = prevlen[last];
             }

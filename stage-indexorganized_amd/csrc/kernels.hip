@@ -1,11 +1,11 @@
 // kernels.hip -- gfx950 (CDNA4, wave64) kernels of the index-organized read path.
 //
 // Integer/pointer work only (no MFMA).  Mapping:
-//   * leaf resolve: lane-per-probe descent of the implicit 8-ary separator tree (one 64-B
-//     node per level = 4 x 16-B loads per lane), replaces InternalNode::GetChildIndex
+//   * leaf resolve: lane-per-probe descent of the implicit separator tree (16-entry 128-B
+//     inner nodes, 8-entry 64-B bottom nodes), replaces InternalNode::GetChildIndex
 //     (b_tree.cpp:664-702) / BTree::TraverseToLeaf (b_tree.cpp:1804-1846).
-//   * leaf probe: wave-per-probe.  64 lanes read the leaf head (1-byte key fingerprint per
-//     slot + visible mask, one 128-B line); ballot gives the fingerprint candidates, the
+//   * leaf probe: wave-per-probe.  64 lanes read the leaf head's fingerprints (1 byte per
+//     slot, 0 = empty/invisible: one 64-B sector); ballot gives the fingerprint candidates, the
 //     candidate lanes read their 32-B slot words and a second ballot confirms the order key:
 //     first visible slot holding the key in slot order == BaseNode::SearchRecordMeta
 //     (b_tree.cpp:18-122).
@@ -52,52 +52,62 @@ __device__ __forceinline__ bool kw_lt(const uint64_t *a, const uint64_t *b) {
     return false;
 }
 
+// separators of one node (F entries) below x.  KW = 1: the node is F x 8 B (F/2 16-B loads
+// per lane); KW > 1: F entries of KW words each, compared lexicographically.
+template <bool VARLEN, int KW, int F>
+__device__ __forceinline__ uint32_t node_count_below(const DevTable &t, uint64_t off, const uint64_t *x, uint32_t xl) {
+    uint32_t cnt = 0;
+    if (KW > 1) {
+        const uint64_t *e = t.tree + off * KW;
+#pragma unroll
+        for (int k = 0; k < F; ++k) {
+            uint64_t w[KW];
+#pragma unroll
+            for (int j = 0; j < KW; ++j) w[j] = e[k * KW + j];
+            cnt += kw_lt<KW>(w, x) ? 1u : 0u;
+        }
+        return cnt;
+    }
+    const u32x4 *e = reinterpret_cast<const u32x4 *>(t.tree + off);
+    u32x4 q[F / 2];
+#pragma unroll
+    for (int k = 0; k < F / 2; ++k) q[k] = e[k];
+    if (VARLEN) {
+        const uint64_t *lp = reinterpret_cast<const uint64_t *>(t.tree_len + off);
+        uint64_t lw[F / 8];
+#pragma unroll
+        for (int k = 0; k < F / 8; ++k) lw[k] = lp[k];
+#pragma unroll
+        for (int k = 0; k < F / 2; ++k) {
+            const uint64_t l = lw[k / 4];
+            const int sh = 16 * (k & 3);
+            const uint64_t v0 = ((uint64_t)q[k].y << 32) | q[k].x, v1 = ((uint64_t)q[k].w << 32) | q[k].z;
+            cnt += kv_lt(v0, (uint32_t)((l >> sh) & 0xFF), x[0], xl) ? 1u : 0u;
+            cnt += kv_lt(v1, (uint32_t)((l >> (sh + 8)) & 0xFF), x[0], xl) ? 1u : 0u;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < F / 2; ++k) {
+            cnt += ((((uint64_t)q[k].y << 32) | q[k].x) < x[0]) ? 1u : 0u;
+            cnt += ((((uint64_t)q[k].w << 32) | q[k].z) < x[0]) ? 1u : 0u;
+        }
+    }
+    return cnt;
+}
+
 // lower_bound over the separators: number of separators < x, i.e. the leaf whose range
 // (sep[i-1], sep[i]] holds x (le_child semantics).  Upper-bound callers pass succ(x).
-// KW = 1: a node is 16 x 8 B = one 128-B line (8 x 16-B loads per lane); KW > 1: 16 entries
-// of KW words each, compared lexicographically.
+// Inner levels are 16-entry nodes (one 128-B line for 8-B keys), the bottom level 8-entry
+// nodes (one 64-B sector): the bottom node is the one the probe usually fetches from beyond L2.
 template <bool VARLEN, int KW>
 __device__ __forceinline__ uint32_t tree_lower_bound(const DevTable &t, const uint64_t *x, uint32_t xl) {
-    static_assert(kTreeFanout == 16, "node = 8 x 16-B loads");
+    static_assert(kTreeFanout == 16 && kLeafFanout == 8, "node loads sized for 16 / 8 entries");
     uint32_t node = 0;
-    for (int lvl = (int)t.levels - 1; lvl >= 0; --lvl) {
-        const uint64_t off = t.level_off[lvl] + (uint64_t)node * kTreeFanout;
-        uint32_t cnt = 0;
-        if (KW > 1) {
-            const uint64_t *e = t.tree + off * KW;
-#pragma unroll
-            for (int k = 0; k < kTreeFanout; ++k) {
-                uint64_t w[KW];
-#pragma unroll
-                for (int j = 0; j < KW; ++j) w[j] = e[k * KW + j];
-                cnt += kw_lt<KW>(w, x) ? 1u : 0u;
-            }
-        } else {
-            const u32x4 *e = reinterpret_cast<const u32x4 *>(t.tree + off);
-            u32x4 q[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) q[k] = e[k];
-            if (VARLEN) {
-                const uint64_t *lp = reinterpret_cast<const uint64_t *>(t.tree_len + off);
-                const uint64_t lw0 = lp[0], lw1 = lp[1];
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const uint64_t lw = k < 4 ? lw0 : lw1;
-                    const int sh = 16 * (k & 3);
-                    const uint64_t v0 = ((uint64_t)q[k].y << 32) | q[k].x, v1 = ((uint64_t)q[k].w << 32) | q[k].z;
-                    cnt += kv_lt(v0, (uint32_t)((lw >> sh) & 0xFF), x[0], xl) ? 1u : 0u;
-                    cnt += kv_lt(v1, (uint32_t)((lw >> (sh + 8)) & 0xFF), x[0], xl) ? 1u : 0u;
-                }
-            } else {
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    cnt += ((((uint64_t)q[k].y << 32) | q[k].x) < x[0]) ? 1u : 0u;
-                    cnt += ((((uint64_t)q[k].w << 32) | q[k].z) < x[0]) ? 1u : 0u;
-                }
-            }
-        }
-        node = node * kTreeFanout + cnt;
-    }
+    for (int lvl = (int)t.levels - 1; lvl > 0; --lvl)
+        node = node * kTreeFanout +
+               node_count_below<VARLEN, KW, kTreeFanout>(t, t.level_off[lvl] + (uint64_t)node * kTreeFanout, x, xl);
+    node = node * kLeafFanout + node_count_below<VARLEN, KW, kLeafFanout>(t, t.level_off[0] + (uint64_t)node * kLeafFanout,
+                                                                          x, xl);
     return node < t.nseps ? node : t.nseps;
 }
 
@@ -117,7 +127,7 @@ __device__ __forceinline__ uint32_t resolve_leaf(const DevTable &t, const uint64
     return tree_lower_bound<VARLEN, KW>(t, s, len);
 }
 
-// Wave-cooperative descent for a wave-uniform key (range scans): per level, lane e < 16 loads
+// Wave-cooperative descent for a wave-uniform key (range scans): per level, lane e < fanout loads
 // separator e of the node and one ballot counts the separators below the key -- one load
 // round per level instead of every lane reading the whole node.
 template <bool VARLEN, int KW>
@@ -125,16 +135,17 @@ __device__ __forceinline__ uint32_t tree_lower_bound_uniform(const DevTable &t, 
                                                              uint32_t lane) {
     uint32_t node = 0;
     for (int lvl = (int)t.levels - 1; lvl >= 0; --lvl) {
-        const uint64_t off = t.level_off[lvl] + (uint64_t)node * kTreeFanout;
+        const uint32_t f = (uint32_t)tree_fanout(lvl);
+        const uint64_t off = t.level_off[lvl] + (uint64_t)node * f;
         bool lt = false;
-        if (lane < (uint32_t)kTreeFanout) {
+        if (lane < f) {
             uint64_t e[KW];
 #pragma unroll
             for (int j = 0; j < KW; ++j) e[j] = t.tree[(off + lane) * KW + j];
             if (KW == 1) lt = VARLEN ? kv_lt(e[0], t.tree_len[off + lane], x[0], xl) : e[0] < x[0];
             else lt = kw_lt<KW>(e, x);
         }
-        node = node * kTreeFanout + (uint32_t)__builtin_popcountll(ballot(lt));
+        node = node * f + (uint32_t)__builtin_popcountll(ballot(lt));
     }
     return node < t.nseps ? node : t.nseps;
 }
@@ -300,8 +311,9 @@ __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *
             uint32_t lf[G], rd[G], xl[G];
             uint64_t x[G][KW];
             uint32_t fpb[G][SPL];
-            uint64_t vm[G][SPL];
-            // phase 1: leaf heads (fingerprints + visible masks) of G probes
+            // phase 1: leaf heads of G probes -- the fingerprint bytes only: an empty or
+            // invisible slot holds fingerprint 0, which no key has (key_fp_words), so the
+            // visible masks behind them are not read
 #pragma unroll
             for (int g = 0; g < G; ++g) {
                 const int j = j0 + g < cnt ? j0 + g : cnt - 1;
@@ -312,10 +324,7 @@ __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *
                 xl[g] = VARLEN ? rl32(len, j) : t.key_width;
                 const uint8_t *h = t.head + (uint64_t)lf[g] * t.head_bytes;
 #pragma unroll
-                for (int s = 0; s < SPL; ++s) {
-                    fpb[g][s] = h[s * 64 + lane];
-                    vm[g][s] = head_vis(t, lf[g], s);
-                }
+                for (int s = 0; s < SPL; ++s) fpb[g][s] = h[s * 64 + lane];
             }
             // phase 2: fingerprint candidates read their slot words
             uint64_t wok[G][SPL], wmeta[G][SPL];
@@ -326,7 +335,7 @@ __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *
                 const uint32_t fx = key_fp_words(x[g], KW);
 #pragma unroll
                 for (int s = 0; s < SPL; ++s) {
-                    cand[g][s] = ((vm[g][s] >> lane) & 1) && fpb[g][s] == fx;
+                    cand[g][s] = fpb[g][s] == fx;
                     wok[g][s] = 0;
                     wmeta[g][s] = 0;
                     wnext[g][s] = 0;

@@ -89,7 +89,8 @@ STAGE_HD uint64_t order_word(uint64_t le_word, uint32_t len, uint32_t j, bool un
 STAGE_HD uint32_t key_fp_words(const uint64_t *w, uint32_t kw) {
     uint64_t h = w[0];
     for (uint32_t j = 1; j < kw; ++j) h = (h ^ (h >> 29)) * 0xBF58476D1CE4E5B9ull + w[j];
-    return (uint32_t)((h * 0x9E3779B97F4A7C15ull) >> 56);
+    const uint32_t fp = (uint32_t)((h * 0x9E3779B97F4A7C15ull) >> 56);
+    return fp ? fp : 1u;  // 0 marks a slot that is empty or invisible in the leaf head
 }
 
 // per-slot word, read by the fingerprint candidates of a probe
@@ -101,9 +102,7 @@ struct alignas(32) SlotInfo {
     uint64_t pad;
 };
 
-// 1-byte key fingerprint stored per slot in the leaf head
-STAGE_HD uint32_t key_fp(uint64_t okey) { return (uint32_t)((okey * 0x9E3779B97F4A7C15ull) >> 56); }
-// leaf head: [fp: cap bytes][visible masks: cap/8 bytes][group max keys: cap/64 x KW words],
+// leaf head: [fp: cap bytes, 0 = empty or invisible slot][visible masks: cap/8 bytes][group max keys: cap/64 x KW words],
 // 128-B multiple.  A group's max key (over its live slots) lets a range scan skip slot groups
 // that hold nothing >= its start key.
 STAGE_HD uint32_t head_gmax_offset(uint32_t cap) { return cap + cap / 8; }
@@ -129,7 +128,9 @@ struct alignas(16) VersionHdr { // TupleHeader (version_store.h:28-155)
 enum : uint8_t { ST_NOT_FOUND = 0, ST_LATEST = 1, ST_COPY = 2, ST_OLD = 3, ST_FAIL_INVALID_TS = 4,
                  ST_CHAIN_MISS = 5 };
 
-constexpr int kTreeFanout = 16;        // keys per separator-tree node (one 128-B line)
+constexpr int kTreeFanout = 16;        // keys per inner separator-tree node (one 128-B line)
+constexpr int kLeafFanout = 8;         // keys per bottom-level node (one 64-B sector for 8-B keys)
+STAGE_HD int tree_fanout(int level) { return level ? kTreeFanout : kLeafFanout; }
 constexpr int kMaxTreeLevels = 16;
 
 // Everything a kernel needs to read one table (passed by value).

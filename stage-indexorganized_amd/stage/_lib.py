@@ -7,7 +7,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libstage_hip.so")
+LIB_PATH = os.environ.get("STAGE_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "libstage_hip.so")
 
 c_u8p = ctypes.POINTER(ctypes.c_uint8)
 c_u16p = ctypes.POINTER(ctypes.c_uint16)
