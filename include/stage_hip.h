@@ -258,6 +258,15 @@ int stage_reader_destroy(stage_reader *r);
  * cap in 256-thread blocks (0 = default).  A tuning knob, not a semantic one. */
 int stage_set_probe_tuning(stage_table *t, int group, int max_blocks);
 
+/* cache policy of stage_probe_batch's output stores (rows + status records), 8-probe launch
+ * shape: STAGE_STORE_TEMPORAL, STAGE_STORE_NONTEMPORAL (default) or STAGE_STORE_WRITE_THROUGH
+ * (the output lines leave the GPU's L2 at once, which keeps hot rows and index lines cached).
+ * A tuning knob, not a semantic one; env STAGE_PROBE_STORE sets the initial value. */
+#define STAGE_STORE_TEMPORAL 0
+#define STAGE_STORE_NONTEMPORAL 1
+#define STAGE_STORE_WRITE_THROUGH 2
+int stage_set_probe_store(stage_table *t, int policy);
+
 /* MurmurHash64A (misc/murmur/MurmurHash2.cpp:99-147) over n keys of key_len bytes laid out
  * key_stride bytes apart; d_out[i] = hash.  Used as the multi-GPU shard router. */
 int stage_murmur64a_batch(const void *d_keys, uint32_t key_len, uint32_t key_stride, uint64_t seed,

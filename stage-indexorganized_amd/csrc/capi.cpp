@@ -27,6 +27,7 @@ int stage_table_create(const stage_params *params, stage_table **out) {
         t->dev.device = params->device;
         if (const char *g = std::getenv("STAGE_PROBE_GROUP")) t->tune.group = std::atoi(g);
         if (const char *g = std::getenv("STAGE_PROBE_MAX_BLOCKS")) t->tune.max_blocks = std::atoi(g);
+        if (const char *g = std::getenv("STAGE_PROBE_STORE")) t->tune.store = std::atoi(g);
         if (const char *g = std::getenv("STAGE_SCAN_ROWS")) t->scan_tune.rows = std::atoi(g);
         if (const char *g = std::getenv("STAGE_SCAN_MAX_BLOCKS")) t->scan_tune.max_blocks = std::atoi(g);
         if (const char *g = std::getenv("STAGE_OUT_STRIDE")) {
@@ -333,12 +334,17 @@ int stage_resolve_batch(stage_table *t, const uint64_t *d_keys, const uint16_t *
 }
 
 int stage_set_probe_tuning(stage_table *t, int group, int max_blocks) {
-    if (!t || (group != 1 && group != 2 && group != 4 && group != 8 && group != 104) || max_blocks < 0)
+    if (!t || (group != 1 && group != 2 && group != 4 && group != 8) || max_blocks < 0)
         return fail(STAGE_E_ARG, "bad tuning");
-    // group 104 = 4 in flight with ordinary (temporal) output stores (A/B knob)
-    t->tune.nt_store = group == 104 ? 0 : 1;  // (probe_kernel<.., 4, false>)
-    t->tune.group = group == 104 ? 4 : group;
+    t->tune.group = group;
     t->tune.max_blocks = max_blocks;
+    return STAGE_OK;
+}
+
+int stage_set_probe_store(stage_table *t, int policy) {
+    if (!t || policy < STAGE_STORE_TEMPORAL || policy > STAGE_STORE_WRITE_THROUGH)
+        return fail(STAGE_E_ARG, "bad store policy");
+    t->tune.store = policy;
     return STAGE_OK;
 }
 

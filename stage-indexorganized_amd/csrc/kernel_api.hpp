@@ -24,7 +24,7 @@ struct alignas(8) ImageDescDev {
 struct ProbeTuning {
     int group = 8;         // probes per wave in flight (swept: 8 > 4 > 2 > 1 at 100M rows)
     int max_blocks = 0;    // 0 = default grid cap (16384 blocks of 256 threads)
-    int nt_store = 1;      // nontemporal output stores
+    int store = 1;         // output stores: 0 temporal, 1 nontemporal, 2 write-through (sc1)
 };
 
 hipError_t launch_resolve(const DevTable &t, const uint64_t *keys, const uint16_t *lens, uint64_t n, int le_child,

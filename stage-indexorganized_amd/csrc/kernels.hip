@@ -166,6 +166,23 @@ __device__ __forceinline__ uint32_t resolve_leaf_uniform(const DevTable &t, cons
     return tree_lower_bound_uniform<VARLEN, KW>(t, s, len, lane);
 }
 
+// Iterator continuation (le_child = false from the last popped key x) when x came from
+// `leaf`: every key of a leaf lies in its separator range (sep[leaf-1], sep[leaf]], so the
+// separators <= x are those left of `leaf` plus sep[leaf] itself when it equals x -- the
+// upper-bound descent collapses to one load of sep[leaf] (+inf padding past the last leaf).
+template <bool VARLEN, int KW>
+__device__ __forceinline__ uint32_t next_leaf_after(const DevTable &t, uint32_t leaf, const uint64_t *x, uint32_t xl) {
+    if (leaf >= t.nseps) return t.nseps;
+    const uint64_t e = t.level_off[0] + leaf;
+    uint64_t sep[KW];
+#pragma unroll
+    for (int w = 0; w < KW; ++w) sep[w] = t.tree[e * KW + w];
+    bool x_lt_sep;
+    if (KW == 1) x_lt_sep = VARLEN ? kv_lt(x[0], xl, sep[0], t.tree_len[e]) : x[0] < sep[0];
+    else x_lt_sep = kw_lt<KW>(x, sep);
+    return x_lt_sep ? leaf : leaf + 1;
+}
+
 // order words of a key passed as KW little-endian u64 words (fixed width) or one word
 template <int KW>
 __device__ __forceinline__ void load_okey(const uint64_t *keys, uint64_t i, bool valid, uint32_t len, uint64_t *okw) {
@@ -278,13 +295,23 @@ __device__ __forceinline__ void pack_out(uint32_t leaf, const ProbeRes &r, u32x4
     b.w = 0;
 }
 
-template <bool NT, class T>
-__device__ __forceinline__ void st16(T v, T *p) {
-    if (NT) __builtin_nontemporal_store(v, p);
-    else *p = v;
+// 16-B output store at base + off (base wave-uniform).  POL 0: temporal; 1: nontemporal (the
+// line is still kept in the XCD's L2); 2: write-through (sc1 buffer store: the line leaves L2,
+// so the output stream does not evict cached rows, heads and separator nodes --
+// MI355X_MICROARCH.md, store flavours).
+template <int POL>
+__device__ __forceinline__ void st16(u32x4 v, uint8_t *base, uint32_t off) {
+    if (POL == 2) {
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7FFFFFFF, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)off, 0, 16);
+    } else if (POL == 1) {
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(base + off));
+    } else {
+        *reinterpret_cast<u32x4 *>(base + off) = v;
+    }
 }
 
-template <bool VARLEN, int SPL, int G, bool NT = true, int KW = 1>
+template <bool VARLEN, int SPL, int G, int POL = 1, int KW = 1>
 __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *__restrict__ keys,
                                                     const uint16_t *__restrict__ lens,
                                                     const uint32_t *__restrict__ rids,
@@ -407,7 +434,7 @@ __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *
                     for (int g = 0; g < G; ++g) {
                         const int j = j0 + g;
                         if (j < cnt && c < out_chunks)
-                            st16<NT>(v[g], reinterpret_cast<u32x4 *>(recs + (base + j) * (uint64_t)t.stride) + c);
+                            st16<POL>(v[g], recs + (base + j) * (uint64_t)t.stride, c * 16u);
                     }
                 }
             }
@@ -423,9 +450,9 @@ __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *
         }
         // one coalesced 2-KiB store of the chunk's 64 results
         if (valid) {
-            u32x4 *o = reinterpret_cast<u32x4 *>(out + i);
-            st16<NT>(my_a, o);
-            st16<NT>(my_b, o + 1);
+            uint8_t *ob = reinterpret_cast<uint8_t *>(out + base);
+            st16<POL>(my_a, ob, lane * 32u);
+            st16<POL>(my_b, ob, lane * 32u + 16u);
         }
     }
 }
@@ -586,7 +613,7 @@ __device__ void scan_one(const DevTable &t, const uint64_t *x0, uint32_t xl, uin
         produced += e;
         remaining -= e;
         if (e < m) break;
-        // last record popped: re-traverse from its key with le_child = false
+        // last record popped: continue from its key with le_child = false (next_leaf_after)
         uint32_t lastl = 0;
 #pragma unroll
         for (int s = 0; s < SPL; ++s) {
@@ -599,7 +626,7 @@ __device__ void scan_one(const DevTable &t, const uint64_t *x0, uint32_t xl, uin
             }
         }
         xl = lastl;
-        leaf = uni32(resolve_leaf_uniform<VARLEN, KW>(t, x, xl, false, lane));
+        leaf = uni32(next_leaf_after<VARLEN, KW>(t, leaf, x, xl));
         cont = true;
     }
     if (lane == 0) *count_out = produced;
@@ -776,13 +803,13 @@ __device__ uint32_t scan_one_compact(const DevTable &t, const uint64_t *x0, uint
         produced += e;
         remaining -= e;
         if (e < m) break;
-        // last record popped: re-traverse from its key with le_child = false
+        // last record popped: continue from its key with le_child = false (next_leaf_after)
         const uint64_t lm = ballot(mine && kr == m - 1);
         const int b = __builtin_ctzll(lm);
 #pragma unroll
         for (int w = 0; w < KW; ++w) x[w] = rl64(mk[w], b);
         xl = rl32(ml, b);
-        leaf = uni32(resolve_leaf_uniform<VARLEN, KW>(t, x, xl, false, lane));
+        leaf = uni32(next_leaf_after<VARLEN, KW>(t, leaf, x, xl));
         cont = true;
     }
     return produced;
@@ -814,9 +841,11 @@ __global__ __launch_bounds__(256) void scan_kernel_compact(DevTable t, const uin
     }
 }
 
-// One wave per scan: the IndexScanExecutor range scan of `scan_size` records from key i, kept
+// The IndexScanExecutor range scan of `scan_size` records from key i (a wave per scan, the
+// start-leaf descents of kFirstChunk scans done lane-parallel first), kept
 // only up to its first produced tuple with the start key's first `words` order words
 // (FirstPrefixSink); img_out[i] / st_out[i] = that tuple's heap row and status.
+constexpr int kFirstChunk = 16;
 template <int SPL, int KW>
 __global__ __launch_bounds__(256) void scan_first_kernel(DevTable t, const uint64_t *__restrict__ keys, uint64_t n,
                                                          uint32_t scan_size, const uint32_t *__restrict__ rids,
@@ -827,22 +856,37 @@ __global__ __launch_bounds__(256) void scan_first_kernel(DevTable t, const uint6
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
     const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wv;
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    for (uint64_t i = wave; i < n; i += nwaves) {
-        const uint32_t len = t.key_width;
+    const uint32_t len = t.key_width;
+    // chunks of kFirstChunk scans per wave: lane j descends the tree for scan j of the chunk
+    // (independent descents in flight together), then the wave runs the chunk's scans
+    for (uint64_t c0 = wave * kFirstChunk; c0 < n; c0 += nwaves * kFirstChunk) {
+        const uint64_t i = c0 + lane;
+        const bool valid = lane < (uint32_t)kFirstChunk && i < n;
         uint64_t ok[KW];
-        load_okey<KW>(keys, i, true, len, ok);
-        FirstPrefixSink<KW> sink;
+        load_okey<KW>(keys, i, valid, len, ok);
+        const uint32_t leafv = valid ? resolve_leaf<false, KW>(t, ok, len, true) : 0u;
+        const uint32_t ridv = valid && rids ? rids[i] : 0xFFFFFFFEu;
+        const int cnt = (int)((n - c0) < (uint64_t)kFirstChunk ? (n - c0) : (uint64_t)kFirstChunk);
+        uint32_t my_img = 0xFFFFFFFFu, my_st = ST_NOT_FOUND;
+        for (int j = 0; j < cnt; ++j) {
+            FirstPrefixSink<KW> sink;
+            uint64_t x[KW];
 #pragma unroll
-        for (int w = 0; w < KW; ++w) sink.pre[w] = ok[w];
-        sink.words = words;
-        sink.rid = rids ? rids[i] : 0xFFFFFFFEu;
-        sink.img = 0xFFFFFFFFu;
-        sink.st = ST_NOT_FOUND;
-        const uint32_t leaf = uni32(resolve_leaf_uniform<false, KW>(t, ok, len, true, lane));
-        scan_one_compact<false, SPL, KW>(t, ok, len, leaf, scan_size, lane, sink, s_keys[wv], s_len[wv], s_slot[wv]);
-        if (lane == 0) {
-            img_out[i] = sink.img;
-            st_out[i] = (uint8_t)sink.st;
+            for (int w = 0; w < KW; ++w) x[w] = sink.pre[w] = rl64(ok[w], j);
+            sink.words = words;
+            sink.rid = rl32(ridv, j);
+            sink.img = 0xFFFFFFFFu;
+            sink.st = ST_NOT_FOUND;
+            scan_one_compact<false, SPL, KW>(t, x, len, rl32(leafv, j), scan_size, lane, sink, s_keys[wv], s_len[wv],
+                                             s_slot[wv]);
+            if (lane == (uint32_t)j) {
+                my_img = sink.img;
+                my_st = sink.st;
+            }
+        }
+        if (valid) {
+            img_out[i] = my_img;
+            st_out[i] = (uint8_t)my_st;
         }
     }
 }
@@ -1050,7 +1094,7 @@ hipError_t launch_probe(const DevTable &t, const uint64_t *keys, const uint16_t 
     const bool var = t.key_width == 0;
     if (t.key_words > 1) {  // wide fixed-width keys: leaves of up to 1024 slots, one probe in flight
 #define STAGE_PROBE_W(S, KW) \
-    probe_kernel<false, S, 1, true, KW><<<blocks, 256, 0, s>>>(t, keys, lens, rids, leaf_in, n, out, recs)
+    probe_kernel<false, S, 1, 1, KW><<<blocks, 256, 0, s>>>(t, keys, lens, rids, leaf_in, n, out, recs)
 #define STAGE_PROBE_WK(KW)                      \
     switch (t.cap / 64) {                       \
         case 1: STAGE_PROBE_W(1, KW); break;    \
@@ -1073,9 +1117,11 @@ hipError_t launch_probe(const DevTable &t, const uint64_t *keys, const uint16_t 
         if (var) STAGE_PROBE(true, 1, 4);
         else if (tune.group == 1) STAGE_PROBE(false, 1, 1);
         else if (tune.group == 2) STAGE_PROBE(false, 1, 2);
-        else if (tune.group == 4 && !tune.nt_store)
-            probe_kernel<false, 1, 4, false><<<blocks, 256, 0, s>>>(t, keys, lens, rids, leaf_in, n, out, recs);
         else if (tune.group == 4) STAGE_PROBE(false, 1, 4);
+        else if (tune.store == 0)
+            probe_kernel<false, 1, 8, 0><<<blocks, 256, 0, s>>>(t, keys, lens, rids, leaf_in, n, out, recs);
+        else if (tune.store == 2)
+            probe_kernel<false, 1, 8, 2><<<blocks, 256, 0, s>>>(t, keys, lens, rids, leaf_in, n, out, recs);
         else STAGE_PROBE(false, 1, 8);
     } else {
         if (var) STAGE_PROBE(true, 2, 4);
@@ -1155,7 +1201,7 @@ hipError_t launch_scan_first(const DevTable &t, const uint64_t *keys, uint64_t n
                              const ScanTuning &tune) {
     if (n == 0) return hipSuccess;
     if (t.key_width == 0 || scan_size == 0 || scan_size > 63) return hipErrorInvalidValue;
-    const int blocks = grid_for(n, 4, tune.max_blocks > 0 ? tune.max_blocks : 16384);
+    const int blocks = grid_for((n + kFirstChunk - 1) / kFirstChunk, 4, tune.max_blocks > 0 ? tune.max_blocks : 16384);
 #define STAGE_FIRST(S, KW) \
     scan_first_kernel<S, KW><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words, img_out, st_out)
 #define STAGE_FIRST_K(KW)                      \

@@ -74,9 +74,17 @@ __device__ uint8_t wp_eval(const WpArgs &a, const DevTable &t, uint64_t q, int64
     if (inserting) return STAGE_RC_DIRTY;
     if (a.bad_range) return STAGE_RC_INVALID;
     const uint8_t *d = a.deltas + (uint64_t)o * a.delta_len;
-    bool same = true;
-    for (uint32_t b = 0; b < a.delta_len && same; ++b) same = d[b] == win[b];
-    if (same || cst > a.writer[o]) return STAGE_RC_NOT_NEEDED_UPDATE;
+    // no early exit: the loads of a whole window are independent and issue back to back
+    uint32_t diff = 0;
+    if ((((uintptr_t)d | (uintptr_t)win | a.delta_len) & 3u) == 0) {
+        const uint32_t *dw = reinterpret_cast<const uint32_t *>(d), *ww = reinterpret_cast<const uint32_t *>(win);
+#pragma unroll 8
+        for (uint32_t b = 0; b < a.delta_len / 4; ++b) diff |= dw[b] ^ ww[b];
+    } else {
+#pragma unroll 8
+        for (uint32_t b = 0; b < a.delta_len; ++b) diff |= (uint32_t)(d[b] ^ win[b]);
+    }
+    if (diff == 0 || cst > a.writer[o]) return STAGE_RC_NOT_NEEDED_UPDATE;
     return STAGE_RC_OK;
 }
 
@@ -116,7 +124,11 @@ __global__ void wp_speculate(WpArgs a, DevTable t, uint8_t *__restrict__ rcs, ui
     if (r != STAGE_RC_OK) atomicMin(&first_fail[g], (uint32_t)q);
 }
 
-// step 3b: groups with a failure, one wave each, from the first failure on
+// step 3b: groups with a failure, one wave each, from the first failure on.  A pass
+// evaluates the next kFinishChunks x 64 ops of the group against the last success (their
+// loads independent), takes the first success in batch order and restarts behind it: a hot
+// key's long run of NotNeededUpdate / DIRTY ops goes 512 ops per pass.
+constexpr int kFinishChunks = 8;
 __global__ __launch_bounds__(256) void wp_finish_groups(WpArgs a, DevTable t, uint8_t *__restrict__ rcs,
                                                         uint8_t *__restrict__ succ, int32_t *__restrict__ prev,
                                                         const uint32_t *__restrict__ first_fail) {
@@ -134,29 +146,43 @@ __global__ __launch_bounds__(256) void wp_finish_groups(WpArgs a, DevTable t, ui
         int64_t last = f > g ? (int64_t)f - 1 : -1;  // [g, f) all succeeded
         uint64_t pos = f;
         while (pos < a.n) {
-            const uint64_t q = pos + lane;
-            const bool in = q < a.n && a.loc[q] == l;
-            const uint8_t r = in ? wp_eval(a, t, q, last, base) : (uint8_t)0xFF;
-            const uint64_t okm = __builtin_amdgcn_ballot_w64(in && r == STAGE_RC_OK);
-            const uint64_t inm = __builtin_amdgcn_ballot_w64(in);
-            if (okm) {
-                const uint32_t first = (uint32_t)__builtin_ctzll(okm);
-                if (in && lane <= first) {
-                    rcs[q] = r;
-                    succ[q] = lane == first;
+            bool in[kFinishChunks];
+            uint8_t r[kFinishChunks];
+#pragma unroll
+            for (int k = 0; k < kFinishChunks; ++k) {
+                const uint64_t q = pos + 64 * k + lane;
+                in[k] = q < a.n && a.loc[q] == l;
+                r[k] = in[k] ? wp_eval(a, t, q, last, base) : (uint8_t)0xFF;
+            }
+            int kf = -1;
+            uint32_t first = 0;
+            bool whole = true;  // every chunk lies inside the group
+#pragma unroll
+            for (int k = 0; k < kFinishChunks; ++k) {
+                const uint64_t okm = __builtin_amdgcn_ballot_w64(in[k] && r[k] == STAGE_RC_OK);
+                if (kf < 0 && okm) {
+                    kf = k;
+                    first = (uint32_t)__builtin_ctzll(okm);
+                }
+                whole = whole && __builtin_amdgcn_ballot_w64(in[k]) == ~0ull;
+            }
+#pragma unroll
+            for (int k = 0; k < kFinishChunks; ++k) {
+                const uint64_t q = pos + 64 * k + lane;
+                const bool upto = kf < 0 || k < kf || (k == kf && lane <= first);
+                if (in[k] && upto) {
+                    rcs[q] = r[k];
+                    succ[q] = k == kf && lane == first;
                     prev[q] = (int32_t)last;
                 }
-                last = (int64_t)(pos + first);
+            }
+            if (kf >= 0) {
+                last = (int64_t)(pos + 64 * (uint64_t)kf + first);
                 pos = (uint64_t)last + 1;
                 continue;
             }
-            if (in) {
-                rcs[q] = r;
-                succ[q] = 0;
-                prev[q] = (int32_t)last;
-            }
-            if (inm != ~0ull) break;  // the group ends inside this chunk
-            pos += 64;
+            if (!whole) break;  // the group ends inside this pass
+            pos += 64 * kFinishChunks;
         }
     }
 }

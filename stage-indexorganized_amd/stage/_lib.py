@@ -84,6 +84,7 @@ SIGNATURES = {
     "stage_scan_batch": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_uint64, ctypes.c_uint32, c_vp, c_vp, c_vp]),
     "stage_resolve_batch": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_uint64, ctypes.c_int, c_vp, c_vp]),
     "stage_set_probe_tuning": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int]),
+    "stage_set_probe_store": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "stage_murmur64a_batch": (ctypes.c_int, [c_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64,
                                              ctypes.c_uint64, c_vp, c_vp]),
     "stage_comm_unique_id": (ctypes.c_int, [c_vp]),
