@@ -298,16 +298,20 @@ __device__ __forceinline__ void pack_out(uint32_t leaf, const ProbeRes &r, u32x4
 // 16-B output store at base + off (base wave-uniform).  POL 0: temporal; 1: nontemporal (the
 // line is still kept in the XCD's L2); 2: write-through (sc1 buffer store: the line leaves L2,
 // so the output stream does not evict cached rows, heads and separator nodes --
-// MI355X_MICROARCH.md, store flavours).
+// MI355X_MICROARCH.md, store flavours).  Measured (scripts/ab_store.py, 100M rows): 1 is
+// fastest (6.35 ms), 0 +1.7 %, 2 +2.6 %; nontemporal heap-row loads on top of 1 +5 %.
 template <int POL>
 __device__ __forceinline__ void st16(u32x4 v, uint8_t *base, uint32_t off) {
-    if (POL == 2) {
+    if constexpr (POL == 2) {
         const auto rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7FFFFFFF, 0x00020000);
         __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)off, 0, 16);
-    } else if (POL == 1) {
-        __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(base + off));
     } else {
-        *reinterpret_cast<u32x4 *>(base + off) = v;
+        // plain pointer arithmetic (u32x4 *) + chunk: the (base, off) form above, used for the
+        // flat stores too, raised probe_kernel<.., 8> from 95 to 154 VGPRs (3 waves/SIMD
+        // instead of 5) and cost 9 % of the launch time
+        u32x4 *p = reinterpret_cast<u32x4 *>(base) + (off >> 4);
+        if constexpr (POL == 1) __builtin_nontemporal_store(v, p);
+        else *p = v;
     }
 }
 
@@ -319,7 +323,9 @@ __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *
                                                     stage_probe_out_dev *__restrict__ out,
                                                     uint8_t *__restrict__ recs) {
     const uint32_t lane = lane_id();
-    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    // threadIdx.x / 64 made provably wave-uniform: the chunk base and the output row addresses
+    // live in SGPRs (probe_kernel<.., 8>: 78 VGPRs, 6 waves/SIMD, instead of 95 and 5)
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + uni32(threadIdx.x >> 6);
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     const uint32_t out_chunks = t.stride >> 4;
     for (uint64_t base = wave * 64; base < n; base += nwaves * 64) {
@@ -824,7 +830,7 @@ __global__ __launch_bounds__(256) void scan_kernel_compact(DevTable t, const uin
                                                            uint8_t *__restrict__ row_status) {
     __shared__ uint64_t s_keys[4][64 * KW];
     __shared__ uint32_t s_len[4][64], s_slot[4][64];
-    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+    const uint32_t lane = lane_id(), wv = uni32(threadIdx.x >> 6);
     const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wv;
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     for (uint64_t i = wave; i < n; i += nwaves) {
@@ -853,7 +859,7 @@ __global__ __launch_bounds__(256) void scan_first_kernel(DevTable t, const uint6
                                                          uint8_t *__restrict__ st_out) {
     __shared__ uint64_t s_keys[4][64 * KW];
     __shared__ uint32_t s_len[4][64], s_slot[4][64];
-    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+    const uint32_t lane = lane_id(), wv = uni32(threadIdx.x >> 6);
     const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wv;
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     const uint32_t len = t.key_width;
@@ -900,7 +906,7 @@ __global__ __launch_bounds__(256) void scan_kernel(DevTable t, const uint64_t *_
                                                    const uint32_t *__restrict__ rids = nullptr,
                                                    uint8_t *__restrict__ row_status = nullptr) {
     const uint32_t lane = lane_id();
-    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + uni32(threadIdx.x >> 6);
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     for (uint64_t i = wave; i < n; i += nwaves) {
         const uint32_t len = t.key_width ? t.key_width : (lens ? (uint32_t)lens[i] : 8u);
