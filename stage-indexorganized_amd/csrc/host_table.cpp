@@ -198,18 +198,35 @@ void HostTable::adopt_device_epoch(const CopyHdr *copies, uint64_t nc, const Ver
     versions_.insert(versions_.end(), versions, versions + nv);
     if (nimages) {
         device_rows_.emplace_back(images_.size(), nimages);
-        for (uint64_t k = 0; k < nimages; ++k) images_.push_back(ImageDesc{0, 0, 3, 0});
+        const uint64_t i0 = images_.size();
+        images_.resize(i0 + nimages);
+        for (uint64_t k = 0; k < nimages; ++k) images_[i0 + k] = ImageDesc{0, 0, 3, 0};
     }
-    for (uint64_t k = 0; k < nslots; ++k) {
-        const SlotWords &w = slots[k];
-        meta_[w.idx] = w.meta;
-        next_[w.idx] = w.next;
-        image_[w.idx] = w.image;
-    }
+    // one slot word per touched record (distinct indices): scattered writes in parallel
+    parallel_chunks(nslots, [&](uint64_t b, uint64_t e) {
+        for (uint64_t k = b; k < e; ++k) {
+            const SlotWords &w = slots[k];
+            if (w.idx == ~0ull) continue;
+            meta_[w.idx] = w.meta;
+            next_[w.idx] = w.next;
+            image_[w.idx] = w.image;
+        }
+    });
     // the device already holds all of it
     copies_synced_ = copies_.size();
     versions_synced_ = versions_.size();
     images_synced_ = images_.size();
+}
+
+void HostTable::parallel_chunks(uint64_t n, const std::function<void(uint64_t, uint64_t)> &fn) {
+    const unsigned nt = n < 65536 ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (nt == 1) {
+        if (n) fn(0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; ++t) th.emplace_back([&, t] { fn(n * t / nt, n * (t + 1) / nt); });
+    for (auto &x : th) x.join();
 }
 
 void HostTable::materialize_device_rows(const std::function<void(uint64_t, uint64_t, uint8_t *)> &fetch) {

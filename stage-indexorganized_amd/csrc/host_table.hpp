@@ -176,8 +176,11 @@ public:
         uint64_t meta;
         uint32_t next, image;
     };
+    // slots with idx == ~0 are skipped
     void adopt_device_epoch(const CopyHdr *copies, uint64_t nc, const VersionHdr *versions, uint64_t nv,
                             uint64_t nimages, const SlotWords *slots, uint64_t nslots);
+    // fn(begin, end) over [0, n) on up to 16 threads (one below 65536 items)
+    static void parallel_chunks(uint64_t n, const std::function<void(uint64_t, uint64_t)> &fn);
     bool has_device_rows() const { return !device_rows_.empty(); }
     // pull the bytes of device-written rows into the arena (host-side writes and the leaf-image
     // export read payloads); fetch(first, count, dst) copies heap rows [first, first+count)

@@ -28,6 +28,9 @@
 
 #include <hipcub/hipcub.hpp>
 
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "handle.hpp"
@@ -334,8 +337,14 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         DeviceImage &dv = t->dev;
         hip_check(hipSetDevice(dv.device), "hipSetDevice");
         hipStream_t s = pick(t, stream);
+        // STAGE_WP_TRACE=1: per-phase host wall times on stderr
+        static const bool trace = std::getenv("STAGE_WP_TRACE") != nullptr;
+        using clk = std::chrono::steady_clock;
+        const auto t0 = clk::now();
+        auto ms = [&](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
         // room for one copy, image and version per op
         reserve_device_rows(h, dv, n, n, n, s);
+        const double t_reserve = ms(t0);
         const DevTable &view = dv.view;
         const uint64_t cbase = h.copies_.size(), vbase = h.versions_.size(), ibase = h.images_.size();
         const uint64_t none = (uint64_t)view.nleaves * view.cap;
@@ -416,9 +425,11 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         hip_check(hipGetLastError(), "write-path kernels");
 
         // the host adopts the epoch
+        const double t_enqueue = ms(t0);
         uint64_t totals[2];
         hip_check(hipMemcpyAsync(totals, tot, 16, hipMemcpyDeviceToHost, s), "totals");
         hip_check(hipStreamSynchronize(s), "write path");
+        const double t_kernels = ms(t0);
         const uint64_t ns = totals[0], nv = totals[1];
         std::vector<CopyHdr> copies(ns);
         std::vector<VersionHdr> versions(nv);
@@ -433,15 +444,25 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
                       "version headers");
         hip_check(hipMemcpyAsync(fr.data(), fin, n * sizeof(FinRec), hipMemcpyDeviceToHost, s), "slot words");
         hip_check(hipStreamSynchronize(s), "write path adopt");
-        std::vector<HostTable::SlotWords> sw;
-        sw.reserve(ns);
+        const double t_d2h = ms(t0);
+        // device slot locations -> host slot indices, in place (FinRec and SlotWords share a
+        // layout; ops that published nothing keep ~0 and are skipped by the adoption)
+        static_assert(sizeof(FinRec) == sizeof(HostTable::SlotWords) &&
+                          offsetof(FinRec, meta) == offsetof(HostTable::SlotWords, meta) &&
+                          offsetof(FinRec, next) == offsetof(HostTable::SlotWords, next) &&
+                          offsetof(FinRec, image) == offsetof(HostTable::SlotWords, image),
+                      "FinRec / SlotWords layout");
         const uint32_t cap = view.cap;
-        for (const FinRec &f : fr) {
-            if (f.loc == ~0ull) continue;
-            const uint64_t hl = dv.dev_to_host[f.loc / cap];
-            sw.push_back(HostTable::SlotWords{hl * cap + f.loc % cap, f.meta, f.next, f.image});
-        }
-        h.adopt_device_epoch(copies.data(), ns, versions.data(), nv, ns, sw.data(), sw.size());
+        const std::vector<uint32_t> &d2h = dv.dev_to_host;
+        HostTable::parallel_chunks(n, [&](uint64_t b, uint64_t e) {
+            for (uint64_t k = b; k < e; ++k)
+                if (fr[k].loc != ~0ull) fr[k].loc = (uint64_t)d2h[fr[k].loc / cap] * cap + fr[k].loc % cap;
+        });
+        h.adopt_device_epoch(copies.data(), ns, versions.data(), nv, ns,
+                             reinterpret_cast<const HostTable::SlotWords *>(fr.data()), n);
+        if (trace)
+            std::fprintf(stderr, "[wp] n=%llu ok=%llu reserve %.2f enqueue %.2f kernels %.2f d2h %.2f adopt %.2f ms\n",
+                         (unsigned long long)n, (unsigned long long)ns, t_reserve, t_enqueue, t_kernels, t_d2h, ms(t0));
         if (n_ok) *n_ok = ns;
         return STAGE_OK;
     });
