@@ -91,3 +91,40 @@ def test_full_size_scans(full):
             assert counts[i] == want.size, (int(s), L, int(counts[i]), want.size)
             if want.size:
                 expect_rows(rows[i, :want.size], want)
+
+
+def test_full_size_device_epoch(full):
+    """BASELINE configs[2] at full size: one YCSB-B shaped epoch (Zipf 0.99 keys, 100-B column
+    patches, ids from one counter, some left in flight) on the device write path of the 100M-row
+    table.  A key's outcome depends only on its own record, so the oracle holding just the
+    touched keys (same rows: LoadYCSBRows payloads) is the reference: every return code and
+    every read of the touched keys at old, middle and current read ids must match it.
+    Runs last: it writes to the shared table."""
+    from test_gpu_parity import check_probe
+    from test_gpu_write_path import oracle_epoch
+    import oracle_lib as O
+
+    rng = np.random.default_rng(5)
+    m = 1 << 19
+    keys = np.concatenate([stage.zipf_draws(N - 1, 0.99, 0x5EED + 77, m - 16, nthreads=16),
+                           np.arange(N + 3, N + 19, dtype=np.uint64)])  # a few absent keys
+    deltas = np.repeat(((keys + np.uint64(1)) & np.uint64(0xFF)).astype(np.uint8)[:, None], 100, 1)
+    rand = rng.random(m) < 0.3  # a third with fresh bytes: hot keys take several versions
+    deltas[rand] = rng.integers(0, 256, (int(rand.sum()), 100), dtype=np.uint8)
+    wid = (10 + 2 * np.arange(m)).astype(np.uint32)
+    cid = (wid + 1).astype(np.uint32)
+    cid[rng.random(m) < 0.05] = 0  # left in flight: later ops on the key see DIRTY
+    rc, ok = full.update_batch_device(keys, 0, deltas, wid, cid)
+    touched = np.unique(keys[keys < N])
+    orc = O.OracleTree()
+    assert orc.load_keys(touched, 8, 0) == touched.size
+    exp = oracle_epoch(orc, keys, 8, 0, deltas, wid, cid)
+    bad = np.flatnonzero(rc != exp)
+    assert bad.size == 0, (bad[:5], rc[bad[:5]], exp[bad[:5]], keys[bad[:5]])
+    assert ok == int((exp == stage.RC_OK).sum()) and len(set(exp.tolist())) >= 3
+    hi = int(cid.max()) + 2
+    probe = np.concatenate([touched[rng.choice(touched.size, min(touched.size, 60000), replace=False)],
+                            keys[:2000]]).astype(np.uint64)
+    for r in (0, 1, hi // 3, hi, 0xFFFFFFFE):
+        check_probe(full, orc, probe, 8, read_ids=np.full(probe.size, r, np.uint32))
+    check_probe(full, orc, probe, 8, read_ids=rng.integers(0, hi, probe.size).astype(np.uint32))
