@@ -287,6 +287,31 @@ int stage_tpcc_stock_level(stage_table *district, stage_table *order_line, stage
                            const int64_t *d_w_ids, const int64_t *d_d_ids, const int32_t *d_thresholds,
                            const uint32_t *d_read_ids, uint64_t n, int32_t *d_result, void *stream);
 
+/* ---- CH-benCHmark Q2 -------------------------------------------------
+ * RunQuery2 (benchmark/tpcc/tpcc_new_order.cpp:608-982) at read id `read_id` over REGION /
+ * NATION / SUPPLIER / ITEM (8-byte keys; payloads R_NAME.., N_REGIONKEY.., SU_NATIONKEY..,
+ * I_IM_ID I_NAME I_PRICE I_DATA, tpcc_record.h:160-200, 773-880) and STOCK ({S_W_ID, S_I_ID},
+ * 16 bytes; payload S_QUANTITY S_YTD S_ORDER_CNT S_REMOTE_CNT .., :417-500).  The region named
+ * regions[target_region] (tpcc_record.h:931), its nations, their suppliers (every SUPPLIER
+ * record); per supplier the STOCK lookups of its supp_stock_map entries (tpcc_workload.cpp:
+ * 398-404, given as host CSR offsets map_off[10001] + device keys d_map_keys, two words {w, i}
+ * per entry in push order), the ITEM lookup of the last stock's S_I_ID, the I_DATA ('b') and
+ * S_QUANTITY < 10 tests.  out[k]: one record per visited supplier (nation order, then supplier
+ * key order; *n_out of them, at most max_out copied); *aborted = 1 where the reference aborts
+ * (a FAILURE read, or a STOCK / ITEM lookup without a tuple).  commit_id != 0 and not aborted:
+ * the marked updates (S_QUANTITY..S_REMOTE_CNT = q + 50, ytd, order_cnt, remote_cnt) are
+ * applied through stage_update_batch_device (writer read_id, commit commit_id), update_rc =
+ * their return codes. */
+typedef struct stage_q2_rec {
+    int64_t supp_key, s_w_id, s_i_id;  /* supplier; the stock its loop kept (the last one read) */
+    int32_t s_quantity, s_ytd, s_order_cnt, s_remote_cnt;
+    uint8_t item_has_b, update, update_rc, pad[5];
+} stage_q2_rec;
+int stage_ch_query2(stage_table *region, stage_table *nation, stage_table *supplier, stage_table *item,
+                    stage_table *stock, const uint32_t *map_off, const uint64_t *d_map_keys, int32_t target_region,
+                    uint32_t read_id, uint32_t commit_id, stage_q2_rec *out, uint64_t max_out, uint64_t *n_out,
+                    int32_t *aborted, void *stream);
+
 /* ---- multi-GPU: hash-sharded probe front-end over RCCL (one process per GPU) ------------
  * stage_comm_unique_id fills 128 bytes on rank 0 (broadcast them out of band);
  * stage_comm_init joins the communicator; stage_probe_sharded routes each key to rank

@@ -1434,3 +1434,162 @@ void orc_stock_level_batch(orc_tree *dist, orc_tree *ol, orc_tree *stock, const 
     clock_gettime(CLOCK_MONOTONIC, &b);
     if (seconds) *seconds = (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
 }
+
+/* ---------------------------------------------------------------- CH-benCHmark Q2 */
+/* RunQuery2 (benchmark/tpcc/tpcc_new_order.cpp:608-982) over REGION / NATION / SUPPLIER /
+ * ITEM / STOCK trees (tpcc_record.h:160-200, 417-500, 773-880: 8-byte keys, STOCK {w, i}
+ * 16 bytes; payloads R_NAME.. / N_REGIONKEY.. / SU_NATIONKEY.. / I_IM_ID, I_NAME, I_PRICE,
+ * I_DATA / S_QUANTITY, S_YTD, S_ORDER_CNT, S_REMOTE_CNT..), with the driver's pre-built
+ * supplier -> stocks map (tpcc_workload.cpp:398-404) as CSR: map_off[10001], (map_w, map_i)
+ * in push order.  One record per supplier the query visits, in visiting order; *aborted = 1
+ * where the reference aborts (a FAILURE read, or a STOCK / ITEM lookup that yields no tuple).
+ * Nothing is written: out[k].update marks the stock update the transaction would make
+ * (PointUpdateExecutor of S_QUANTITY..S_REMOTE_CNT = q + 50, ytd, order_cnt, remote_cnt). */
+static const char *const q2_regions[] = {"AFRICA", "AMERICA", "ASIA", "EUROPE", "MIDDLE EAST"}; /* tpcc_record.h:931 */
+
+typedef struct { int64_t supp, nation; } q2_supp_t;
+
+/* TableScanExecutor with scan_sz == -1 (executor.h:580-612): ScanLeafNode over every leaf,
+ * slots in slot order, raw records (no visibility).  Empty (meta == 0) slots are skipped. */
+static void q2_scan_leaves(void *node, q2_supp_t *out, uint64_t *n, uint64_t cap) {
+    if (is_leaf(node)) {
+        uint8_t *l = node;
+        uint32_t cnt = st_count(*l_status(l));
+        for (uint32_t i = 0; i < cnt && *n < cap; i++) {
+            uint64_t m = l_meta(l, i)->meta;
+            if (!m) continue;
+            const uint8_t *k = l + m_offset(m);
+            out[*n].supp = rd_i64(k);
+            out[*n].nation = rd_i64(k + pad_key(m_keylen(m)));
+            (*n)++;
+        }
+        return;
+    }
+    orc_inner *p = node;
+    for (uint32_t i = 0; i < p->count; i++) q2_scan_leaves(p->child[i], out, n, cap);
+}
+
+static int q2_produced(uint8_t st) { return st == ORC_ST_LATEST || st == ORC_ST_COPY || st == ORC_ST_OLD; }
+
+int64_t orc_ch_query2(orc_tree *region, orc_tree *nation, orc_tree *supplier, orc_tree *item, orc_tree *stock,
+                      const uint32_t *map_off, const int32_t *map_w, const int32_t *map_i, int target_region,
+                      uint32_t read_id, orc_q2_rec *out, uint64_t max_out, int *aborted) {
+    *aborted = 0;
+    uint64_t nout = 0;
+    uint32_t rrow = region->key_pad + region->payload_size, nrow = nation->key_pad + nation->payload_size;
+    uint8_t *regs = xmalloc((uint64_t)rrow * 6), *nats = xmalloc((uint64_t)nrow * 65);
+    scanrec_t *buf = xmalloc(sizeof(scanrec_t) * 4096);
+    uint64_t zero = 0;
+    uint32_t nreg = scan_one(region, (const uint8_t *)&zero, 8, 6, regs, buf, 4096);   /* :650-661 */
+    uint32_t nnat = scan_one(nation, (const uint8_t *)&zero, 8, 65, nats, buf, 4096);  /* :731-742 */
+    free(buf);
+    q2_supp_t *supps = xmalloc(sizeof(q2_supp_t) * 20000);
+    uint64_t nsupp = 0;
+    q2_scan_leaves(supplier->root, supps, &nsupp, 20000);                             /* :783-797 */
+    uint8_t irow[8 + 4096], srow[16 + 4096];
+    orc_read_out o;
+    for (uint32_t r = 0; r < nreg && !*aborted; r++) {
+        const uint8_t *rr = regs + (uint64_t)r * rrow;
+        char rname[56];
+        memcpy(rname, rr + region->key_pad, 55);
+        rname[55] = 0;
+        if (strcmp(rname, q2_regions[target_region]) != 0) continue;                     /* :772 */
+        int64_t rkey = rd_i64(rr);
+        for (uint32_t a = 0; a < nnat && !*aborted; a++) {
+            const uint8_t *nr = nats + (uint64_t)a * nrow;
+            if (rd_i64(nr + nation->key_pad) != rkey) continue;                           /* :778 */
+            int64_t nkey = rd_i64(nr);
+            for (uint64_t s = 0; s < nsupp && !*aborted; s++) {                           /* :801 */
+                if (supps[s].nation != nkey) continue;                                    /* :806 */
+                int64_t sk = supps[s].supp;
+                /* the "min" never moves (min_qty is not updated, :848): the last stock wins */
+                int64_t w0 = 0, i0 = 0;
+                int32_t q[4] = {0, 0, 0, 0};
+                if (sk >= 0 && sk < 10000)
+                    for (uint32_t e = map_off[sk]; e < map_off[sk + 1]; e++) {            /* :815 */
+                        int64_t key[2] = {map_w[e], map_i[e]};
+                        read_one(stock, (const uint8_t *)key, 16, read_id, &o, srow);
+                        if (!q2_produced(o.status)) { *aborted = 1; break; }               /* :840-851 */
+                        w0 = rd_i64(srow);
+                        i0 = rd_i64(srow + 8);
+                        for (int c = 0; c < 4; c++) q[c] = rd_i32(srow + stock->key_pad + 4 * c);
+                    }
+                if (*aborted) break;
+                uint64_t ik = (uint64_t)i0;                                                /* :863 */
+                read_one(item, (const uint8_t *)&ik, 8, read_id, &o, irow);
+                if (!q2_produced(o.status)) { *aborted = 1; break; }                       /* :879-887 */
+                /* std::string(I_DATA).find('b') (:890-892): I_DATA = payload bytes 44..107,
+                 * up to its first NUL */
+                const uint8_t *idata = irow + item->key_pad + 44;
+                uint8_t has_b = 0;
+                for (int c = 0; c < 64 && idata[c]; c++) has_b |= idata[c] == 'b';
+                if (nout < max_out) {
+                    orc_q2_rec *x = &out[nout];
+                    memset(x, 0, sizeof(*x));
+                    x->supp_key = sk;
+                    x->s_w_id = w0;
+                    x->s_i_id = i0;
+                    x->s_quantity = q[0];
+                    x->s_ytd = q[1];
+                    x->s_order_cnt = q[2];
+                    x->s_remote_cnt = q[3];
+                    x->item_has_b = has_b;
+                    x->update = !has_b && q[0] < 10;                                       /* :893-897 */
+                }
+                nout++;
+            }
+        }
+    }
+    free(regs);
+    free(nats);
+    free(supps);
+    return (int64_t)nout;
+}
+
+typedef struct {
+    orc_tree *r, *n, *s, *i, *k;
+    const uint32_t *off;
+    const int32_t *w, *it;
+    int target;
+    uint32_t rid;
+    uint64_t b, e, recs;
+    int aborts;
+} q2_job_t;
+
+static void *q2_worker(void *arg) {
+    q2_job_t *j = arg;
+    orc_q2_rec *tmp = xmalloc(sizeof(orc_q2_rec) * 16384);
+    for (uint64_t x = j->b; x < j->e; x++) {
+        int ab = 0;
+        j->recs += (uint64_t)orc_ch_query2(j->r, j->n, j->s, j->i, j->k, j->off, j->w, j->it, j->target, j->rid, tmp,
+                                           16384, &ab);
+        j->aborts += ab;
+    }
+    free(tmp);
+    return NULL;
+}
+
+/* count read-only Q2 transactions on nthreads threads (CPU baseline); returns records visited */
+uint64_t orc_ch_query2_timed(orc_tree *region, orc_tree *nation, orc_tree *supplier, orc_tree *item, orc_tree *stock,
+                             const uint32_t *map_off, const int32_t *map_w, const int32_t *map_i, int target_region,
+                             uint32_t read_id, uint64_t count, int nthreads, double *seconds) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    q2_job_t jobs[256];
+    struct timespec a, b;
+    clock_gettime(CLOCK_MONOTONIC, &a);
+    for (int t = 0; t < nthreads; t++) {
+        jobs[t] = (q2_job_t){region, nation, supplier, item, stock, map_off, map_w, map_i, target_region, read_id,
+                             count * (uint64_t)t / nthreads, count * (uint64_t)(t + 1) / nthreads, 0, 0};
+        pthread_create(&th[t], NULL, q2_worker, &jobs[t]);
+    }
+    uint64_t recs = 0;
+    for (int t = 0; t < nthreads; t++) {
+        pthread_join(th[t], NULL);
+        recs += jobs[t].recs;
+    }
+    clock_gettime(CLOCK_MONOTONIC, &b);
+    if (seconds) *seconds = (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
+    return recs;
+}

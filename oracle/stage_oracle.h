@@ -154,4 +154,17 @@ void orc_fill_payload(uint64_t rowid, int mode, uint8_t *dst, uint32_t payload_s
 #ifdef __cplusplus
 }
 #endif
+
+/* CH-benCHmark Q2 (RunQuery2, benchmark/tpcc/tpcc_new_order.cpp:608-982): see stage_oracle.c */
+typedef struct {
+    int64_t supp_key, s_w_id, s_i_id;
+    int32_t s_quantity, s_ytd, s_order_cnt, s_remote_cnt;
+    uint8_t item_has_b, update, pad[6];
+} orc_q2_rec;
+int64_t orc_ch_query2(orc_tree *region, orc_tree *nation, orc_tree *supplier, orc_tree *item, orc_tree *stock,
+                      const uint32_t *map_off, const int32_t *map_w, const int32_t *map_i, int target_region,
+                      uint32_t read_id, orc_q2_rec *out, uint64_t max_out, int *aborted);
+uint64_t orc_ch_query2_timed(orc_tree *region, orc_tree *nation, orc_tree *supplier, orc_tree *item, orc_tree *stock,
+                             const uint32_t *map_off, const int32_t *map_w, const int32_t *map_i, int target_region,
+                             uint32_t read_id, uint64_t count, int nthreads, double *seconds);
 #endif

@@ -1,0 +1,288 @@
+// chq2.hip -- CH-benCHmark Q2 (RunQuery2, benchmark/tpcc/tpcc_new_order.cpp:608-982) through the
+// index-organized read path.
+//
+// Reference transaction at one read id:
+//   1. REGION TableScan of 6 from key 0, NATION TableScan of 65 from key 0 (:650-761);
+//   2. for the region named regions[target] (tpcc_record.h:931) and each of its nations, the
+//      SUPPLIER table scan (scan_sz -1: every record, :779-797) filtered on SU_NATIONKEY;
+//   3. per supplier: the STOCK point lookups {w, i} of its supp_stock_map entries
+//      (tpcc_workload.cpp:398-404) -- a FAILURE read or a lookup with no tuple aborts; the
+//      "minimum" keeps the LAST stock read because min_qty is never updated (:812-859);
+//   4. the ITEM point lookup of that stock's S_I_ID (:862-887); I_DATA containing 'b' skips
+//      the supplier (:890-892); otherwise S_QUANTITY < 10 updates S_QUANTITY..S_REMOTE_CNT to
+//      (q + 50, ytd, order_cnt, remote_cnt) (:893-950), committed with the transaction.
+//
+// Here the three tiny scans run as device scans whose rows the host filters (a few hundred
+// KB); the hot part -- every visited supplier's stock lookups (W * I / 10^4 each, ~2600
+// suppliers for EUROPE) and the item lookups -- is one gather kernel, one probe_kernel launch
+// over all stock keys, one wave per supplier reducing its segment, one item probe launch and
+// one finishing kernel.  Updates go through the device write path when a commit id is given.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "handle.hpp"
+
+using namespace stage_capi;
+
+namespace stage {
+namespace {
+
+constexpr int kRegionScan = 6, kNationScan = 65;  // scan_sz of :653 and :734
+constexpr uint32_t kIDataOff = 4 + 32 + 8;         // I_DATA in Item's payload (I_IM_ID, I_NAME, I_PRICE)
+static const char *const kRegions[] = {"AFRICA", "AMERICA", "ASIA", "EUROPE", "MIDDLE EAST"};
+
+__device__ __forceinline__ bool produced(uint32_t st) { return st == ST_LATEST || st == ST_COPY || st == ST_OLD; }
+
+__device__ __forceinline__ int32_t ld_i32(const uint8_t *p) {
+    return (int32_t)((uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24));
+}
+
+__global__ void q2_fill_u32(uint32_t *p, uint64_t n, uint32_t v) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+
+// block s copies supplier s's map entries (2 words each) to its output segment
+__global__ void q2_gather(const uint64_t *__restrict__ map_keys, const uint64_t *__restrict__ src,
+                          const uint64_t *__restrict__ dst, const uint32_t *__restrict__ cnt,
+                          uint64_t *__restrict__ keys) {
+    const uint32_t s = blockIdx.x;
+    for (uint32_t e = threadIdx.x; e < cnt[s]; e += blockDim.x) {
+        keys[2 * (dst[s] + e)] = map_keys[2 * (src[s] + e)];
+        keys[2 * (dst[s] + e) + 1] = map_keys[2 * (src[s] + e) + 1];
+    }
+}
+
+// one wave per supplier: abort if any stock lookup of its segment produced no tuple; the last
+// entry's stock row gives (w, i, quantity, ytd, order_cnt, remote_cnt) and the item key
+__global__ __launch_bounds__(64) void q2_reduce(const stage_probe_out_dev *__restrict__ sout,
+                                                const uint64_t *__restrict__ skeys, const uint64_t *__restrict__ dst,
+                                                const uint32_t *__restrict__ cnt, const uint64_t *__restrict__ supp,
+                                                const uint8_t *__restrict__ sheap, uint32_t shstride,
+                                                uint32_t skpad, uint32_t n, stage_q2_rec *__restrict__ out,
+                                                uint64_t *__restrict__ ikeys, int32_t *__restrict__ abort_flag) {
+    const uint32_t s = blockIdx.x, lane = threadIdx.x;
+    if (s >= n) return;
+    const uint64_t b = dst[s];
+    const uint32_t c = cnt[s];
+    bool bad = false;
+    for (uint32_t e = lane; e < c; e += 64) bad |= !produced(sout[b + e].w[0] & 0xFF);
+    if (__builtin_amdgcn_ballot_w64(bad) && lane == 0) atomicOr(abort_flag, 1);
+    if (lane != 0) return;
+    stage_q2_rec r;
+    memset(&r, 0, sizeof(r));
+    r.supp_key = (int64_t)supp[s];
+    if (c) {  // stock_0 / stock_1 of the last lookup (a supplier without stocks keeps zeros)
+        const uint64_t last = b + c - 1;
+        r.s_w_id = (int64_t)skeys[2 * last];
+        r.s_i_id = (int64_t)skeys[2 * last + 1];
+        if (produced(sout[last].w[0] & 0xFF)) {
+            const uint8_t *row = sheap + (uint64_t)sout[last].w[6] * shstride + skpad;
+            r.s_quantity = ld_i32(row);
+            r.s_ytd = ld_i32(row + 4);
+            r.s_order_cnt = ld_i32(row + 8);
+            r.s_remote_cnt = ld_i32(row + 12);
+        }
+    }
+    out[s] = r;
+    ikeys[s] = (uint64_t)r.s_i_id;
+}
+
+// item outcome: no tuple aborts; I_DATA up to its first NUL containing 'b' skips; else a
+// quantity below 10 marks the update
+__global__ void q2_finish(const stage_probe_out_dev *__restrict__ iout, const uint8_t *__restrict__ iheap,
+                          uint32_t ihstride, uint32_t ikpad, uint32_t n, stage_q2_rec *__restrict__ out,
+                          int32_t *__restrict__ abort_flag) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n) return;
+    const uint32_t st = iout[s].w[0] & 0xFF;
+    if (!produced(st)) {
+        atomicOr(abort_flag, 1);
+        return;
+    }
+    const uint8_t *d = iheap + (uint64_t)iout[s].w[6] * ihstride + ikpad + kIDataOff;
+    uint8_t has_b = 0;
+    for (int c = 0; c < 64 && d[c]; ++c) has_b |= d[c] == 'b';
+    out[s].item_has_b = has_b;
+    out[s].update = !has_b && out[s].s_quantity < 10;
+}
+
+int64_t rd64(const uint8_t *p) {
+    int64_t v;
+    std::memcpy(&v, p, 8);
+    return v;
+}
+
+// TableScanExecutor rows of one scan from `start` (device scan, rows back to the host)
+std::vector<uint8_t> scan_rows(stage_table *t, uint64_t start, uint32_t scan_size, uint32_t &count, hipStream_t s) {
+    const DevTable &v = t->dev.view;
+    const uint64_t rows = (uint64_t)scan_size * v.stride;
+    uint8_t *buf = scratch_bytes(t->dev, 64 + rows);
+    auto *key = (uint64_t *)buf;
+    auto *cnt = (uint32_t *)(buf + 8);
+    hip_check(hipMemcpyAsync(key, &start, 8, hipMemcpyHostToDevice, s), "h2d");
+    hip_check(launch_scan(v, key, nullptr, 1, scan_size, cnt, buf + 64, s, t->scan_tune), "scan");
+    std::vector<uint8_t> h(rows);
+    hip_check(hipMemcpyAsync(&count, cnt, 4, hipMemcpyDeviceToHost, s), "d2h");
+    hip_check(hipMemcpyAsync(h.data(), buf + 64, rows, hipMemcpyDeviceToHost, s), "d2h");
+    hip_check(hipStreamSynchronize(s), "scan sync");
+    return h;
+}
+
+}  // namespace
+}  // namespace stage
+
+extern "C" int stage_ch_query2(stage_table *region, stage_table *nation, stage_table *supplier, stage_table *item,
+                               stage_table *stock, const uint32_t *map_off, const uint64_t *d_map_keys,
+                               int32_t target_region, uint32_t read_id, uint32_t commit_id, stage_q2_rec *out,
+                               uint64_t max_out, uint64_t *n_out, int32_t *aborted, void *stream) {
+    for (stage_table *t : {region, nation, supplier, item, stock}) {
+        int rc = need_synced(t);
+        if (rc) return rc;
+    }
+    if (!map_off || !d_map_keys || !n_out || !aborted || (max_out && !out))
+        return fail(STAGE_E_ARG, "null argument");
+    if (target_region < 0 || target_region > 4) return fail(STAGE_E_ARG, "target_region must be 0..4");
+    for (stage_table *t : {region, nation, supplier, item})
+        if (t->host->params().key_width != 8) return fail(STAGE_E_ARG, "REGION/NATION/SUPPLIER/ITEM keys are 8 bytes");
+    if (stock->host->params().key_width != 16) return fail(STAGE_E_ARG, "STOCK keys are {w, i}: 16 bytes");
+    if (region->host->params().payload_size < 55 || nation->host->params().payload_size < 8 ||
+        supplier->host->params().payload_size < 8 || item->host->params().payload_size < stage::kIDataOff + 64 ||
+        stock->host->params().payload_size < 16)
+        return fail(STAGE_E_ARG, "payloads too short for the Q2 columns");
+    for (stage_table *t : {region, nation, supplier, item})
+        if (t->dev.device != stock->dev.device) return fail(STAGE_E_ARG, "tables on different devices");
+    return guarded([&] {
+        using namespace stage;
+        hip_check(hipSetDevice(stock->dev.device), "hipSetDevice");
+        hipStream_t s = pick(stock, stream);
+        *n_out = 0;
+        *aborted = 0;
+        // 1. REGION / NATION scans, SUPPLIER scan of every record, filtered on the host
+        uint32_t nreg = 0, nnat = 0, nsup = 0;
+        const uint32_t rs = region->dev.view.stride, ns = nation->dev.view.stride, ss = supplier->dev.view.stride;
+        const std::vector<uint8_t> regs = scan_rows(region, 0, kRegionScan, nreg, s);
+        const std::vector<uint8_t> nats = scan_rows(nation, 0, kNationScan, nnat, s);
+        // scan_sz -1 walks every leaf (ScanLeafNode): a scan of all records from the smallest
+        // 8-byte key under KeyCompare (signed bytes: 0x80 in every byte), in key order
+        uint64_t st[8];
+        supplier->host->stats(st);
+        const std::vector<uint8_t> sups =
+            scan_rows(supplier, 0x8080808080808080ull, (uint32_t)std::max<uint64_t>(st[3], 1), nsup, s);
+        std::vector<uint64_t> sel;  // visited suppliers in visiting order
+        for (uint32_t r = 0; r < nreg; ++r) {
+            const uint8_t *rr = regs.data() + (uint64_t)r * rs;
+            char name[56];
+            std::memcpy(name, rr + 8, 55);
+            name[55] = 0;
+            if (std::string(name) != kRegions[target_region]) continue;
+            for (uint32_t a = 0; a < nnat; ++a) {
+                const uint8_t *nr = nats.data() + (uint64_t)a * ns;
+                if (rd64(nr + 8) != rd64(rr)) continue;
+                for (uint32_t k = 0; k < nsup; ++k) {
+                    const uint8_t *sr = sups.data() + (uint64_t)k * ss;
+                    if (rd64(sr + 8) == rd64(nr)) sel.push_back((uint64_t)rd64(sr));
+                }
+            }
+        }
+        const uint32_t n = (uint32_t)sel.size();
+        *n_out = n;
+        if (n == 0) return STAGE_OK;
+        // 2. stock keys of every visited supplier, one probe launch
+        std::vector<uint64_t> src(n), dst(n);
+        std::vector<uint32_t> cnt(n);
+        uint64_t m = 0;
+        for (uint32_t k = 0; k < n; ++k) {
+            const uint64_t sk = sel[k];
+            src[k] = sk < 10000 ? map_off[sk] : 0;
+            cnt[k] = sk < 10000 ? map_off[sk + 1] - map_off[sk] : 0;
+            dst[k] = m;
+            m += cnt[k];
+        }
+        auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
+        uint64_t off = 0;
+        auto take = [&](uint64_t bytes) {
+            const uint64_t o = off;
+            off += al(bytes);
+            return o;
+        };
+        const uint64_t o_src = take(n * 8), o_dst = take(n * 8), o_cnt = take(n * 4), o_sup = take(n * 8),
+                       o_keys = take(std::max<uint64_t>(m, 1) * 16), o_rids = take(std::max<uint64_t>(m, n) * 4),
+                       o_sout = take(std::max<uint64_t>(m, 1) * 32), o_rec = take(n * sizeof(stage_q2_rec)),
+                       o_ik = take(n * 8), o_iout = take(n * 32), o_ab = take(4);
+        uint8_t *buf = scratch_bytes(nation->dev, off);
+        auto *d_src = (uint64_t *)(buf + o_src), *d_dst = (uint64_t *)(buf + o_dst), *d_sup = (uint64_t *)(buf + o_sup);
+        auto *d_cnt = (uint32_t *)(buf + o_cnt), *d_rids = (uint32_t *)(buf + o_rids);
+        auto *d_keys = (uint64_t *)(buf + o_keys), *d_ik = (uint64_t *)(buf + o_ik);
+        auto *d_sout = (stage_probe_out_dev *)(buf + o_sout), *d_iout = (stage_probe_out_dev *)(buf + o_iout);
+        auto *d_rec = (stage_q2_rec *)(buf + o_rec);
+        auto *d_ab = (int32_t *)(buf + o_ab);
+        hip_check(hipMemcpyAsync(d_src, src.data(), n * 8, hipMemcpyHostToDevice, s), "h2d");
+        hip_check(hipMemcpyAsync(d_dst, dst.data(), n * 8, hipMemcpyHostToDevice, s), "h2d");
+        hip_check(hipMemcpyAsync(d_cnt, cnt.data(), n * 4, hipMemcpyHostToDevice, s), "h2d");
+        hip_check(hipMemcpyAsync(d_sup, sel.data(), n * 8, hipMemcpyHostToDevice, s), "h2d");
+        hip_check(hipMemsetAsync(d_ab, 0, 4, s), "memset");
+        const uint64_t nr = std::max<uint64_t>(m, n);
+        q2_fill_u32<<<(unsigned)((nr + 255) / 256), 256, 0, s>>>(d_rids, nr, read_id);
+        q2_gather<<<n, 256, 0, s>>>(d_map_keys, d_src, d_dst, d_cnt, d_keys);
+        const DevTable &sv = stock->dev.view, &iv = item->dev.view;
+        if (m)
+            hip_check(launch_probe(sv, d_keys, nullptr, d_rids, nullptr, m, d_sout, nullptr, s, stock->tune),
+                      "stock probe");
+        q2_reduce<<<n, 64, 0, s>>>(d_sout, d_keys, d_dst, d_cnt, d_sup, sv.heap, sv.hstride, stock->host->key_pad(),
+                                   n, d_rec, d_ik, d_ab);
+        // 3. item lookups of the last stocks, filter
+        hip_check(launch_probe(iv, d_ik, nullptr, d_rids, nullptr, n, d_iout, nullptr, s, item->tune), "item probe");
+        q2_finish<<<(n + 255) / 256, 256, 0, s>>>(d_iout, iv.heap, iv.hstride, item->host->key_pad(), n, d_rec, d_ab);
+        hip_check(hipGetLastError(), "q2 kernels");
+        std::vector<stage_q2_rec> recs(n);
+        hip_check(hipMemcpyAsync(recs.data(), d_rec, n * sizeof(stage_q2_rec), hipMemcpyDeviceToHost, s), "d2h");
+        hip_check(hipMemcpyAsync(aborted, d_ab, 4, hipMemcpyDeviceToHost, s), "d2h");
+        hip_check(hipStreamSynchronize(s), "q2 sync");
+        // 4. the transaction's stock updates, through the device write path
+        if (commit_id && !*aborted) {
+            std::vector<uint64_t> uk;
+            std::vector<int32_t> ud;
+            std::vector<uint32_t> ui;
+            for (uint32_t k = 0; k < n; ++k)
+                if (recs[k].update) {
+                    uk.push_back((uint64_t)recs[k].s_w_id);
+                    uk.push_back((uint64_t)recs[k].s_i_id);
+                    ud.insert(ud.end(), {recs[k].s_quantity + 50, recs[k].s_ytd, recs[k].s_order_cnt,
+                                         recs[k].s_remote_cnt});
+                    ui.push_back(k);
+                }
+            const uint64_t nu = ui.size();
+            if (nu) {
+                uint64_t o2 = 0;
+                auto take2 = [&](uint64_t bytes) {
+                    const uint64_t o = o2;
+                    o2 += al(bytes);
+                    return o;
+                };
+                const uint64_t u_k = take2(nu * 16), u_d = take2(nu * 16), u_w = take2(nu * 4), u_c = take2(nu * 4),
+                               u_rc = take2(nu);
+                uint8_t *ub = scratch_bytes(item->dev, o2);
+                std::vector<uint32_t> wid(nu, read_id), cid(nu, commit_id);
+                hip_check(hipMemcpyAsync(ub + u_k, uk.data(), nu * 16, hipMemcpyHostToDevice, s), "h2d");
+                hip_check(hipMemcpyAsync(ub + u_d, ud.data(), nu * 16, hipMemcpyHostToDevice, s), "h2d");
+                hip_check(hipMemcpyAsync(ub + u_w, wid.data(), nu * 4, hipMemcpyHostToDevice, s), "h2d");
+                hip_check(hipMemcpyAsync(ub + u_c, cid.data(), nu * 4, hipMemcpyHostToDevice, s), "h2d");
+                uint64_t ok = 0;
+                const int rc = stage_update_batch_device(stock, (const uint64_t *)(ub + u_k), nullptr, nu, 0,
+                                                         ub + u_d, 16, (const uint32_t *)(ub + u_w),
+                                                         (const uint32_t *)(ub + u_c), nullptr, ub + u_rc, &ok, s);
+                if (rc) return rc;
+                std::vector<uint8_t> rcs(nu);
+                hip_check(hipMemcpyAsync(rcs.data(), ub + u_rc, nu, hipMemcpyDeviceToHost, s), "d2h");
+                hip_check(hipStreamSynchronize(s), "update sync");
+                for (uint64_t j = 0; j < nu; ++j) recs[ui[j]].update_rc = rcs[j];
+            }
+        }
+        std::memcpy(out, recs.data(), std::min<uint64_t>(n, max_out) * sizeof(stage_q2_rec));
+        return STAGE_OK;
+    });
+}

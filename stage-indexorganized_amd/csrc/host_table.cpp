@@ -74,11 +74,11 @@ HostTable::HostTable(const stage_params &p) : p_(p) {
     const uint32_t room = p.leaf_node_size - 40;
     max_records_ = (room + (24 + rec) - 1) / (24 + rec) - 1;
     if (max_records_ < 3) throw std::invalid_argument("leaf holds fewer than 3 records");
-    // slots per device leaf: 64 * a power of two (the kernels' slot groups); keys of <= 8 bytes
-    // up to 128, wide keys (small TPC-C rows) up to 1024
+    // slots per device leaf: 64 * a power of two (the kernels' slot groups); variable-length
+    // keys up to 128, fixed-width keys (small TPC-C / CH rows) up to 1024
     cap_ = 64;
     while (cap_ < max_records_) cap_ *= 2;
-    if (cap_ > (kw_ == 1 ? 128u : 1024u))
+    if (cap_ > (p.key_width == 0 ? 128u : 1024u))
         throw std::invalid_argument("too many records per leaf for the device layout (payload too small)");
     // output/heap row: [key padded to 8][payload], 16-B multiple; rows above 128 B are
     // 128-B multiples so every row starts on an L2 line (a 1008-B tuple = 8 whole lines)

@@ -1098,7 +1098,9 @@ hipError_t launch_probe(const DevTable &t, const uint64_t *keys, const uint16_t 
     const uint64_t chunks = (n + 63) / 64;
     const int blocks = grid_for(chunks, 4, tune.max_blocks > 0 ? tune.max_blocks : 16384);
     const bool var = t.key_width == 0;
-    if (t.key_words > 1) {  // wide fixed-width keys: leaves of up to 1024 slots, one probe in flight
+    // wide fixed-width keys, and 8-byte keys in leaves above 128 slots (small rows): leaves of
+    // up to 1024 slots, one probe in flight
+    if (t.key_words > 1 || (!var && t.cap > 128)) {
 #define STAGE_PROBE_W(S, KW) \
     probe_kernel<false, S, 1, 1, KW><<<blocks, 256, 0, s>>>(t, keys, lens, rids, leaf_in, n, out, recs)
 #define STAGE_PROBE_WK(KW)                      \
@@ -1109,7 +1111,9 @@ hipError_t launch_probe(const DevTable &t, const uint64_t *keys, const uint16_t 
         case 8: STAGE_PROBE_W(8, KW); break;    \
         default: STAGE_PROBE_W(16, KW); break;  \
     }
-        if (t.key_words == 2) {
+        if (t.key_words == 1) {
+            STAGE_PROBE_WK(1)
+        } else if (t.key_words == 2) {
             STAGE_PROBE_WK(2)
         } else {
             STAGE_PROBE_WK(4)
@@ -1173,6 +1177,7 @@ static void launch_scan_r(const DevTable &t, const uint64_t *keys, const uint16_
     const bool var = t.key_width == 0;
     if (t.key_words == 2) return launch_scan_w<2, VIS>(t, keys, n, scan_size, counts, recs, rids, st, s, blocks);
     if (t.key_words == 4) return launch_scan_w<4, VIS>(t, keys, n, scan_size, counts, recs, rids, st, s, blocks);
+    if (!var && t.cap > 128) return launch_scan_w<1, VIS>(t, keys, n, scan_size, counts, recs, rids, st, s, blocks);
 #define STAGE_SCAN(V, S) \
     scan_kernel<V, S, R, 1, VIS><<<blocks, 256, 0, s>>>(t, keys, lens, n, scan_size, counts, recs, rids, st)
     if (t.cap == 64) {

@@ -18,6 +18,12 @@ PROBE_OUT_DTYPE = np.dtype([
 assert PROBE_OUT_DTYPE.itemsize == 32
 
 ST_NOT_FOUND, ST_LATEST, ST_COPY, ST_OLD, ST_FAIL_INVALID_TS, ST_CHAIN_MISS = range(6)
+Q2_REC_DTYPE = np.dtype([
+    ("supp_key", "i8"), ("s_w_id", "i8"), ("s_i_id", "i8"), ("s_quantity", "i4"), ("s_ytd", "i4"),
+    ("s_order_cnt", "i4"), ("s_remote_cnt", "i4"), ("item_has_b", "u1"), ("update", "u1"), ("update_rc", "u1"),
+    ("pad", "u1", (5,)),
+])
+assert Q2_REC_DTYPE.itemsize == 48
 RC_INVALID, RC_OK, RC_KEY_EXISTS, RC_NOT_FOUND = 0, 1, 2, 3
 RC_NOT_NEEDED_UPDATE, RC_DIRTY = 7, 9
 
@@ -551,3 +557,16 @@ def device_count():
     c = ctypes.c_int(0)
     rc = lib().stage_device_count(ctypes.byref(c))
     return c.value if rc == 0 else 0
+
+
+def ch_query2(region, nation, supplier, item, stock, map_off, d_map_keys, target_region=3, read_id=0xFFFFFFFE,
+              commit_id=0, max_out=1 << 16, stream=None):
+    """stage_ch_query2 (RunQuery2): returns (records Q2_REC_DTYPE[n], aborted)."""
+    map_off = np.ascontiguousarray(map_off, np.uint32)
+    out = np.zeros(max_out, Q2_REC_DTYPE)
+    n = ctypes.c_uint64()
+    ab = ctypes.c_int32()
+    check(lib().stage_ch_query2(region.h, nation.h, supplier.h, item.h, stock.h, map_off.ctypes.data, d_map_keys,
+                                int(target_region), int(read_id), int(commit_id), out.ctypes.data, max_out,
+                                ctypes.byref(n), ctypes.byref(ab), stream), "ch_query2")
+    return out[:min(n.value, max_out)], bool(ab.value)

@@ -47,6 +47,10 @@ _SIG = {
     "orc_stock_level": (ctypes.c_int32, [vp, vp, vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, u32]),
     "orc_stock_level_batch": (None, [vp, vp, vp, vp, vp, vp, vp, u64, vp, ctypes.c_int,
                                      ctypes.POINTER(ctypes.c_double)]),
+    "orc_ch_query2": (ctypes.c_int64, [vp, vp, vp, vp, vp, vp, vp, vp, ctypes.c_int, u32, vp, u64,
+                                       ctypes.POINTER(ctypes.c_int)]),
+    "orc_ch_query2_timed": (u64, [vp, vp, vp, vp, vp, vp, vp, vp, ctypes.c_int, u32, u64, ctypes.c_int,
+                                  ctypes.POINTER(ctypes.c_double)]),
     "orc_read_batch_k": (ctypes.c_int, [vp, vp, u32, u32, vp, u64, vp, vp, ctypes.c_int]),
     "orc_scan_batch_k": (u64, [vp, vp, u32, u32, u64, u32, vp, vp, ctypes.c_int]),
     "orc_key_compare": (ctypes.c_int, [vp, u32, vp, u32]),
