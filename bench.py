@@ -62,7 +62,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=None)
     p.add_argument("--warmup", type=int, default=None)
-    p.add_argument("--config", choices=["c2", "c3", "c4", "tpcc"], default="c2")
+    p.add_argument("--config", choices=["c2", "c3", "c4", "tpcc", "chq2"], default="c2")
     p.add_argument("--warehouses", type=int, default=16, help="tpcc: warehouses (10 districts, 3000 orders each)")
     p.add_argument("--items", type=int, default=100_000, help="tpcc: items (stock rows per warehouse)")
     p.add_argument("--rows", type=int, default=100_000_000, help="rows per GPU")
@@ -381,10 +381,80 @@ def run_tpcc(args):
     return 0
 
 
+def run_chq2(args):
+    """CH-benCHmark Q2 through the path (stage_ch_query2), one GPU: one read-only Q2 transaction
+    (target region EUROPE, the reference's fixed choice) per step over W warehouses' STOCK."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from ch_data import ChTables  # the CH table generator (data only; the oracle trees only for the CPU leg)
+    t0 = time.time()
+    ch = ChTables(W=args.warehouses, I=args.items, seed=args.seed & 0xFFFF, oracle=not args.no_cpu_baseline)
+    load_s = time.time() - t0
+    t0 = time.time()
+    ch.sync()
+    sync_s = time.time() - t0
+    for _ in range(args.warmup):
+        recs, ab = ch.query2(3)
+    check(stage.lib().stage_device_sync(), "sync")
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        recs, ab = ch.query2(3)
+    elapsed = time.perf_counter() - t0
+    ms = elapsed / args.steps * 1e3
+    nsupp = int(recs.size)
+    nstock = int(sum(int(ch.map_off[k + 1] - ch.map_off[k]) for k in recs["supp_key"]))
+    # algorithmic bytes per Q2: each STOCK / ITEM point lookup reads its key, the 64-B fingerprint
+    # sector and the 32-B slot word and writes its 32-B status record; the kept stock's and the
+    # item's column sectors (64 B each); the three scans read and write their rows
+    per_q2 = nstock * (16 + 64 + 32 + 32) + nsupp * (8 + 64 + 32 + 32 + 64 + 64) + \
+        10000 * (8 + 111 + 128) + 62 * (8 + 185 + 192) + 5 * (8 + 207 + 224)
+    achieved = per_q2 / (ms * 1e-3) / 1e9
+    cpu, ok = None, not ab
+    if not args.no_cpu_baseline:
+        import ctypes
+
+        import oracle_lib as O
+        orecs, oab = ch.query2_oracle(3)
+        a, b = np.sort(recs, order="supp_key"), np.sort(orecs, order="supp_key")
+        ok = ok and oab == ab and a.size == b.size and all((a[f] == b[f]).all() for f in
+                                                            ("supp_key", "s_w_id", "s_i_id", "s_quantity",
+                                                             "item_has_b", "update"))
+        threads = min(16, os.cpu_count() or 8)
+        o = ch.orc
+        sec = ctypes.c_double()
+        args_ = (o["region"].t, o["nation"].t, o["supplier"].t, o["item"].t, o["stock"].t, ch.map_off.ctypes.data,
+                 ch.map_w.ctypes.data, ch.map_i.ctypes.data, 3, 0xFFFFFFFE)
+        O.lib().orc_ch_query2_timed(*args_, threads, threads, ctypes.byref(sec))
+        count = int(max(threads, threads / max(sec.value, 1e-9) * args.cpu_seconds))
+        O.lib().orc_ch_query2_timed(*args_, count, threads, ctypes.byref(sec))
+        cpu = {"value": round(count / sec.value, 2), "unit": "q2/s", "cores": threads, "kind": "port",
+               "sample": f"oracle orc_ch_query2 (RunQuery2 restated), {count} read-only Q2s, same tables, "
+                         f"{threads} threads on {cpu_name()}, {sec.value:.1f}s"}
+    result = {
+        "metric": "CH-benCHmark Q2 txns/s through the index-organized path (supplementary to " + METRIC + ")",
+        "value": round(args.steps / elapsed, 2), "unit": "q2/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "int64 keys / bytes", "data": "synthetic CH rows (tpcc_record.h layouts, "
+                                                                      "tpcc_loader.cpp value rules)",
+        "config": {"workload": "CH-benCHmark Q2 (tpcc_new_order.cpp RunQuery2), region EUROPE",
+                   "warehouses": args.warehouses, "items": args.items, "suppliers_visited": nsupp,
+                   "stock_lookups": nstock, "aborted": bool(ab), "updates": int(recs["update"].sum())},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": "Q2 transaction (3 scans + batched STOCK / ITEM probes, host filtering of the scans)",
+                     "algorithmic_bytes_per_unit": per_q2, "units_per_launch": 1, "avg_launch_ms": round(ms, 4)},
+        "cpu_baseline": cpu, "self_check": bool(ok),
+        "setup_s": {"load": round(load_s, 1), "sync": round(sync_s, 1)},
+    }
+    print(json.dumps(result), flush=True)
+    return 0 if ok else 1
+
+
 def main():
     args = parse()
     if args.config == "tpcc":
         return run_tpcc(args)
+    if args.config == "chq2":
+        return run_chq2(args)
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))

@@ -12,8 +12,8 @@
 //      the supplier (:890-892); otherwise S_QUANTITY < 10 updates S_QUANTITY..S_REMOTE_CNT to
 //      (q + 50, ytd, order_cnt, remote_cnt) (:893-950), committed with the transaction.
 //
-// Here the three tiny scans run as device scans whose rows the host filters (a few hundred
-// KB); the hot part -- every visited supplier's stock lookups (W * I / 10^4 each, ~2600
+// Here REGION / NATION run as device scans and SUPPLIER as a one-lane-per-slot leaf dump; the
+// host filters their rows (a few hundred KB); the hot part -- every visited supplier's stock lookups (W * I / 10^4 each, ~2600
 // suppliers for EUROPE) and the item lookups -- is one gather kernel, one probe_kernel launch
 // over all stock keys, one wave per supplier reducing its segment, one item probe launch and
 // one finishing kernel.  Updates go through the device write path when a commit id is given.
@@ -110,6 +110,25 @@ __global__ void q2_finish(const stage_probe_out_dev *__restrict__ iout, const ui
     out[s].update = !has_b && out[s].s_quantity < 10;
 }
 
+// SUPPLIER scan with scan_sz -1 (TableScanExecutor::ScanLeafNode, executor.h:580-612): every
+// slot of every leaf in leaf order, slots in slot order, raw records without a visibility
+// test -- one lane per slot; pairs[i] = {SU_SUPPKEY, SU_NATIONKEY} of slot i, or ~0 for a slot
+// holding no record
+__global__ void q2_dump_leaves(DevTable t, uint32_t kpad, uint64_t *__restrict__ pairs) {
+    const uint64_t n = (uint64_t)t.nleaves * t.cap;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const SlotInfo si = t.slot[i];
+        uint64_t k = ~0ull, nat = ~0ull;
+        if (si.meta != 0) {
+            const uint8_t *row = t.heap + (uint64_t)si.image * t.hstride;
+            k = *reinterpret_cast<const uint64_t *>(row);
+            nat = *reinterpret_cast<const uint64_t *>(row + kpad);
+        }
+        pairs[2 * i] = k;
+        pairs[2 * i + 1] = nat;
+    }
+}
+
 int64_t rd64(const uint8_t *p) {
     int64_t v;
     std::memcpy(&v, p, 8);
@@ -162,16 +181,20 @@ extern "C" int stage_ch_query2(stage_table *region, stage_table *nation, stage_t
         *n_out = 0;
         *aborted = 0;
         // 1. REGION / NATION scans, SUPPLIER scan of every record, filtered on the host
-        uint32_t nreg = 0, nnat = 0, nsup = 0;
-        const uint32_t rs = region->dev.view.stride, ns = nation->dev.view.stride, ss = supplier->dev.view.stride;
+        uint32_t nreg = 0, nnat = 0;
+        const uint32_t rs = region->dev.view.stride, ns = nation->dev.view.stride;
         const std::vector<uint8_t> regs = scan_rows(region, 0, kRegionScan, nreg, s);
         const std::vector<uint8_t> nats = scan_rows(nation, 0, kNationScan, nnat, s);
-        // scan_sz -1 walks every leaf (ScanLeafNode): a scan of all records from the smallest
-        // 8-byte key under KeyCompare (signed bytes: 0x80 in every byte), in key order
-        uint64_t st[8];
-        supplier->host->stats(st);
-        const std::vector<uint8_t> sups =
-            scan_rows(supplier, 0x8080808080808080ull, (uint32_t)std::max<uint64_t>(st[3], 1), nsup, s);
+        // SUPPLIER: every record, ScanLeafNode order
+        const DevTable &pv = supplier->dev.view;
+        const uint64_t nslots = (uint64_t)pv.nleaves * pv.cap;
+        uint8_t *pbuf = scratch_bytes(supplier->dev, nslots * 16);
+        q2_dump_leaves<<<(unsigned)std::min<uint64_t>((nslots + 255) / 256, 4096), 256, 0, s>>>(
+            pv, supplier->host->key_pad(), (uint64_t *)pbuf);
+        hip_check(hipGetLastError(), "dump leaves");
+        std::vector<uint64_t> pairs(2 * nslots);
+        hip_check(hipMemcpyAsync(pairs.data(), pbuf, nslots * 16, hipMemcpyDeviceToHost, s), "d2h");
+        hip_check(hipStreamSynchronize(s), "dump sync");
         std::vector<uint64_t> sel;  // visited suppliers in visiting order
         for (uint32_t r = 0; r < nreg; ++r) {
             const uint8_t *rr = regs.data() + (uint64_t)r * rs;
@@ -182,10 +205,8 @@ extern "C" int stage_ch_query2(stage_table *region, stage_table *nation, stage_t
             for (uint32_t a = 0; a < nnat; ++a) {
                 const uint8_t *nr = nats.data() + (uint64_t)a * ns;
                 if (rd64(nr + 8) != rd64(rr)) continue;
-                for (uint32_t k = 0; k < nsup; ++k) {
-                    const uint8_t *sr = sups.data() + (uint64_t)k * ss;
-                    if (rd64(sr + 8) == rd64(nr)) sel.push_back((uint64_t)rd64(sr));
-                }
+                for (uint64_t k = 0; k < nslots; ++k)
+                    if (pairs[2 * k] != ~0ull && (int64_t)pairs[2 * k + 1] == rd64(nr)) sel.push_back(pairs[2 * k]);
             }
         }
         const uint32_t n = (uint32_t)sel.size();
