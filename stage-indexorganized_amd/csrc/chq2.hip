@@ -40,6 +40,8 @@ __device__ __forceinline__ int32_t ld_i32(const uint8_t *p) {
     return (int32_t)((uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24));
 }
 
+__global__ void q2_set_u64(uint64_t *p, uint64_t v) { *p = v; }
+
 __global__ void q2_fill_u32(uint32_t *p, uint64_t n, uint32_t v) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) p[i] = v;
@@ -135,19 +137,19 @@ int64_t rd64(const uint8_t *p) {
     return v;
 }
 
-// TableScanExecutor rows of one scan from `start` (device scan, rows back to the host)
+// TableScanExecutor rows of one scan from `start` (device scan, rows copied back to the host
+// asynchronously: the caller synchronises the stream before reading `count` or the rows)
 std::vector<uint8_t> scan_rows(stage_table *t, uint64_t start, uint32_t scan_size, uint32_t &count, hipStream_t s) {
     const DevTable &v = t->dev.view;
     const uint64_t rows = (uint64_t)scan_size * v.stride;
     uint8_t *buf = scratch_bytes(t->dev, 64 + rows);
     auto *key = (uint64_t *)buf;
     auto *cnt = (uint32_t *)(buf + 8);
-    hip_check(hipMemcpyAsync(key, &start, 8, hipMemcpyHostToDevice, s), "h2d");
+    q2_set_u64<<<1, 1, 0, s>>>(key, start);  // no host buffer outlives the call
     hip_check(launch_scan(v, key, nullptr, 1, scan_size, cnt, buf + 64, s, t->scan_tune), "scan");
     std::vector<uint8_t> h(rows);
     hip_check(hipMemcpyAsync(&count, cnt, 4, hipMemcpyDeviceToHost, s), "d2h");
     hip_check(hipMemcpyAsync(h.data(), buf + 64, rows, hipMemcpyDeviceToHost, s), "d2h");
-    hip_check(hipStreamSynchronize(s), "scan sync");
     return h;
 }
 
@@ -194,7 +196,7 @@ extern "C" int stage_ch_query2(stage_table *region, stage_table *nation, stage_t
         hip_check(hipGetLastError(), "dump leaves");
         std::vector<uint64_t> pairs(2 * nslots);
         hip_check(hipMemcpyAsync(pairs.data(), pbuf, nslots * 16, hipMemcpyDeviceToHost, s), "d2h");
-        hip_check(hipStreamSynchronize(s), "dump sync");
+        hip_check(hipStreamSynchronize(s), "scan sync");  // the three scans complete together
         std::vector<uint64_t> sel;  // visited suppliers in visiting order
         for (uint32_t r = 0; r < nreg; ++r) {
             const uint8_t *rr = regs.data() + (uint64_t)r * rs;

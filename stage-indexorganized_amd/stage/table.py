@@ -560,10 +560,13 @@ def device_count():
 
 
 def ch_query2(region, nation, supplier, item, stock, map_off, d_map_keys, target_region=3, read_id=0xFFFFFFFE,
-              commit_id=0, max_out=1 << 16, stream=None):
-    """stage_ch_query2 (RunQuery2): returns (records Q2_REC_DTYPE[n], aborted)."""
+              commit_id=0, max_out=1 << 14, stream=None, out=None):
+    """stage_ch_query2 (RunQuery2): returns (records Q2_REC_DTYPE[n], aborted); `out` (a
+    Q2_REC_DTYPE array) is reused when given."""
     map_off = np.ascontiguousarray(map_off, np.uint32)
-    out = np.zeros(max_out, Q2_REC_DTYPE)
+    if out is None:
+        out = np.zeros(max_out, Q2_REC_DTYPE)
+    max_out = out.size
     n = ctypes.c_uint64()
     ab = ctypes.c_int32()
     check(lib().stage_ch_query2(region.h, nation.h, supplier.h, item.h, stock.h, map_off.ctypes.data, d_map_keys,

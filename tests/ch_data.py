@@ -107,8 +107,12 @@ class ChTables:
 
     def query2(self, target=3, read_id=0xFFFFFFFE, commit_id=0):
         t = self.tables
-        return stage.ch_query2(t["region"], t["nation"], t["supplier"], t["item"], t["stock"], self.map_off,
-                               self.d_map.ptr, target, read_id, commit_id)
+        if getattr(self, "_out", None) is None:
+            self._out = np.zeros(1 << 14, stage.Q2_REC_DTYPE)
+            self._map_off = np.ascontiguousarray(self.map_off, np.uint32)
+        recs, ab = stage.ch_query2(t["region"], t["nation"], t["supplier"], t["item"], t["stock"], self._map_off,
+                                   self.d_map.ptr, target, read_id, commit_id, out=self._out)
+        return recs.copy(), ab
 
     def query2_oracle(self, target=3, read_id=0xFFFFFFFE):
         import ctypes
