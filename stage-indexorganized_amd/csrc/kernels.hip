@@ -315,7 +315,9 @@ __device__ __forceinline__ void st16(u32x4 v, uint8_t *base, uint32_t off) {
     }
 }
 
-template <bool VARLEN, int SPL, int G, int POL = 1, int KW = 1>
+// CH: probes per wave chunk (64; 16 for small batches of the one-probe-in-flight instances, so
+// that a wave's chunk is not a chain of 64 dependent probes while most of the chip idles)
+template <bool VARLEN, int SPL, int G, int POL = 1, int KW = 1, int CH = 64>
 __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *__restrict__ keys,
                                                     const uint16_t *__restrict__ lens,
                                                     const uint32_t *__restrict__ rids,
@@ -328,9 +330,9 @@ __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *
     const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + uni32(threadIdx.x >> 6);
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     const uint32_t out_chunks = t.stride >> 4;
-    for (uint64_t base = wave * 64; base < n; base += nwaves * 64) {
+    for (uint64_t base = wave * CH; base < n; base += nwaves * CH) {
         const uint64_t i = base + lane;
-        const bool valid = i < n;
+        const bool valid = lane < (uint32_t)CH && i < n;
         u32x4 my_a = u32x4{0, 0, 0, 0}, my_b = u32x4{0, 0, 0, 0};  // this lane's probe result
         const uint32_t len = t.key_width ? t.key_width : (lens && valid ? (uint32_t)lens[i] : 8u);
         const uint32_t rid = rids ? (valid ? rids[i] : 0u) : 0xFFFFFFFEu;
@@ -339,7 +341,7 @@ __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *
         uint32_t leaf = 0;
         if (valid) leaf = leaf_in ? leaf_in[i] : resolve_leaf<VARLEN, KW>(t, ok, len, true);
         if (leaf > t.nseps) leaf = t.nseps;  // host-supplied ids are clamped to the table
-        const int cnt = (int)((n - base) < 64 ? (n - base) : 64);
+        const int cnt = (int)((n - base) < CH ? (n - base) : CH);
         for (int j0 = 0; j0 < cnt; j0 += G) {
             uint32_t lf[G], rd[G], xl[G];
             uint64_t x[G][KW];
@@ -1101,8 +1103,13 @@ hipError_t launch_probe(const DevTable &t, const uint64_t *keys, const uint16_t 
     // wide fixed-width keys, and 8-byte keys in leaves above 128 slots (small rows): leaves of
     // up to 1024 slots, one probe in flight
     if (t.key_words > 1 || (!var && t.cap > 128)) {
-#define STAGE_PROBE_W(S, KW) \
-    probe_kernel<false, S, 1, 1, KW><<<blocks, 256, 0, s>>>(t, keys, lens, rids, leaf_in, n, out, recs)
+        const bool small = chunks < 16384;  // fewer 64-probe chunks than the chip holds waves
+        const int wblocks = small ? grid_for((n + 15) / 16, 4, tune.max_blocks > 0 ? tune.max_blocks : 16384) : blocks;
+#define STAGE_PROBE_W(S, KW)                                                                                  \
+    if (small)                                                                                                \
+        probe_kernel<false, S, 1, 1, KW, 16><<<wblocks, 256, 0, s>>>(t, keys, lens, rids, leaf_in, n, out, recs); \
+    else                                                                                                      \
+        probe_kernel<false, S, 1, 1, KW><<<blocks, 256, 0, s>>>(t, keys, lens, rids, leaf_in, n, out, recs)
 #define STAGE_PROBE_WK(KW)                      \
     switch (t.cap / 64) {                       \
         case 1: STAGE_PROBE_W(1, KW); break;    \
