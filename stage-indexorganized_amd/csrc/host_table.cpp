@@ -193,15 +193,32 @@ void HostTable::adopt_device_epoch(const CopyHdr *copies, uint64_t nc, const Ver
     if (copies_.size() + nc > kNextIndexMask || versions_.size() + nv > kNextIndexMask ||
         images_.size() + nimages > kNextIndexMask)
         throw std::runtime_error("copy / version / image index overflow");
+    const bool trace = std::getenv("STAGE_WP_TRACE") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    auto lap = [&](const char *what) {
+        if (trace)
+            std::fprintf(stderr, "[adopt] %s %.2f ms\n", what,
+                         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    };
+    // grow 4x (at least 4M entries) instead of doubling: each epoch appends ~n headers, and a
+    // reallocation copies (and page-faults in) every earlier one
+    auto room = [](auto &v, uint64_t add) {
+        if (v.capacity() < v.size() + add) v.reserve(std::max<uint64_t>(v.size() + add, 4 * v.capacity() + (1u << 22)));
+    };
+    room(copies_, nc);
+    room(copy_live_, nc);
+    room(versions_, nv);
     copies_.insert(copies_.end(), copies, copies + nc);
     copy_live_.resize(copies_.size(), 1);
     versions_.insert(versions_.end(), versions, versions + nv);
+    lap("headers");
     if (nimages) {
         device_rows_.emplace_back(images_.size(), nimages);
         const uint64_t i0 = images_.size();
         images_.resize(i0 + nimages);
         for (uint64_t k = 0; k < nimages; ++k) images_[i0 + k] = ImageDesc{0, 0, 3, 0};
     }
+    lap("images");
     // one slot word per touched record (distinct indices): scattered writes in parallel
     parallel_chunks(nslots, [&](uint64_t b, uint64_t e) {
         for (uint64_t k = b; k < e; ++k) {
@@ -212,6 +229,7 @@ void HostTable::adopt_device_epoch(const CopyHdr *copies, uint64_t nc, const Ver
             image_[w.idx] = w.image;
         }
     });
+    lap("slots");
     // the device already holds all of it
     copies_synced_ = copies_.size();
     versions_synced_ = versions_.size();

@@ -458,11 +458,13 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
             for (uint64_t k = b; k < e; ++k)
                 if (fr[k].loc != ~0ull) fr[k].loc = (uint64_t)d2h[fr[k].loc / cap] * cap + fr[k].loc % cap;
         });
+        const double t_conv = ms(t0);
         h.adopt_device_epoch(copies.data(), ns, versions.data(), nv, ns,
                              reinterpret_cast<const HostTable::SlotWords *>(fr.data()), n);
         if (trace)
-            std::fprintf(stderr, "[wp] n=%llu ok=%llu reserve %.2f enqueue %.2f kernels %.2f d2h %.2f adopt %.2f ms\n",
-                         (unsigned long long)n, (unsigned long long)ns, t_reserve, t_enqueue, t_kernels, t_d2h, ms(t0));
+            std::fprintf(stderr, "[wp] n=%llu ok=%llu reserve %.2f enqueue %.2f kernels %.2f d2h %.2f convert %.2f adopt %.2f ms\n",
+                         (unsigned long long)n, (unsigned long long)ns, t_reserve, t_enqueue, t_kernels, t_d2h, t_conv,
+                         ms(t0));
         if (n_ok) *n_ok = ns;
         return STAGE_OK;
     });
