@@ -46,6 +46,7 @@ WORKLOADS = {
 # algorithmic bytes
 BYTES_PER_LOOKUP = 2100  # 8 key + 64 key-column line + 16 slot word + 1000 payload + 1008 out + 4
 HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md: 8.0 TB/s HBM3E spec
+XGMI_LINK_GBS = 153.0    # per xGMI link of an MI355X (7 links per GPU, point to point)
 
 
 def scan_bytes(L, S=48.8):
@@ -124,6 +125,23 @@ def cpu_name():
     except OSError:
         pass
     return platform.processor() or "unknown"
+
+
+def xgmi_roofline(batch, world, stride, step_s, hbm_roof):
+    """Roofline of the multi-GPU step, bound by the xGMI exchange: per rank and step the remote
+    share of the batch ((W-1)/W of it, hash-uniform) sends its 16-B key record out and gets a
+    32-B status record + a stride-byte row back; peak = the W-1 links a rank uses."""
+    remote = batch * (world - 1) / world
+    unit = 16 + 32 + stride
+    achieved = remote * unit / step_s / 1e9
+    peak = XGMI_LINK_GBS * (world - 1)
+    return {"bound": "xgmi", "achieved": round(achieved, 1), "peak": peak, "unit": "GB/s",
+            "frac": round(achieved / peak, 4), "traffic": None,
+            "kernel": "sharded step (route + RCCL all-to-all-v + probe_kernel + un-permute)",
+            "algorithmic_bytes_per_unit": unit, "units_per_launch": round(remote),
+            "avg_launch_ms": round(step_s * 1e3, 4),
+            "peak_source": f"{XGMI_LINK_GBS:.0f} GB/s per xGMI link (7 per MI355X), {world - 1} links per rank",
+            "hbm": hbm_roof}
 
 
 def cpu_baseline(args, threads):
@@ -642,6 +660,8 @@ def main():
                 "avg_launch_ms": round(kern_ms, 4)}
         if tsrc:
             roof["traffic_source"] = tsrc
+        if sharded and world > 1:
+            roof = xgmi_roofline(B, world, tab.stride, elapsed / args.steps, roof)
         cpu = None
         if not sharded and not args.no_cpu_baseline:
             cpu = cpu_baseline(args, nthreads)
