@@ -312,6 +312,15 @@ int stage_ch_query2(stage_table *region, stage_table *nation, stage_table *suppl
                     uint32_t read_id, uint32_t commit_id, stage_q2_rec *out, uint64_t max_out, uint64_t *n_out,
                     int32_t *aborted, void *stream);
 
+/* nq read-only Q2 transactions at read_ids[0..nq) in one pass (the scans once, every
+ * query's STOCK / ITEM lookups in the same launches): out[q * max_per_query + k],
+ * aborted[q]; *n_out = records per query (the visited suppliers do not depend on the read
+ * id: the scans are TableScanExecutor ones, without visibility).  No updates are applied. */
+int stage_ch_query2_batch(stage_table *region, stage_table *nation, stage_table *supplier, stage_table *item,
+                          stage_table *stock, const uint32_t *map_off, const uint64_t *d_map_keys,
+                          int32_t target_region, const uint32_t *read_ids, uint32_t nq, stage_q2_rec *out,
+                          uint64_t max_per_query, uint64_t *n_out, int32_t *aborted, void *stream);
+
 /* ---- multi-GPU: hash-sharded probe front-end over RCCL (one process per GPU) ------------
  * stage_comm_unique_id fills 128 bytes on rank 0 (broadcast them out of band);
  * stage_comm_init joins the communicator; stage_probe_sharded routes each key to rank

@@ -42,19 +42,21 @@ __device__ __forceinline__ int32_t ld_i32(const uint8_t *p) {
 
 __global__ void q2_set_u64(uint64_t *p, uint64_t v) { *p = v; }
 
-__global__ void q2_fill_u32(uint32_t *p, uint64_t n, uint32_t v) {
+// read id of every lookup: copy q of a per-query segment of `per` lookups reads at rq[q]
+__global__ void q2_fill_rids(uint32_t *p, uint64_t per, uint32_t nq, const uint32_t *__restrict__ rq) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) p[i] = v;
+    if (i < per * nq) p[i] = rq[i / per];
 }
 
-// block s copies supplier s's map entries (2 words each) to its output segment
+// block (s, q) copies supplier s's map entries (2 words each) to its segment of query q's copy
 __global__ void q2_gather(const uint64_t *__restrict__ map_keys, const uint64_t *__restrict__ src,
-                          const uint64_t *__restrict__ dst, const uint32_t *__restrict__ cnt,
+                          const uint64_t *__restrict__ dst, const uint32_t *__restrict__ cnt, uint64_t m,
                           uint64_t *__restrict__ keys) {
     const uint32_t s = blockIdx.x;
+    uint64_t *kq = keys + 2 * m * blockIdx.y;
     for (uint32_t e = threadIdx.x; e < cnt[s]; e += blockDim.x) {
-        keys[2 * (dst[s] + e)] = map_keys[2 * (src[s] + e)];
-        keys[2 * (dst[s] + e) + 1] = map_keys[2 * (src[s] + e) + 1];
+        kq[2 * (dst[s] + e)] = map_keys[2 * (src[s] + e)];
+        kq[2 * (dst[s] + e) + 1] = map_keys[2 * (src[s] + e) + 1];
     }
 }
 
@@ -64,11 +66,14 @@ __global__ __launch_bounds__(64) void q2_reduce(const stage_probe_out_dev *__res
                                                 const uint64_t *__restrict__ skeys, const uint64_t *__restrict__ dst,
                                                 const uint32_t *__restrict__ cnt, const uint64_t *__restrict__ supp,
                                                 const uint8_t *__restrict__ sheap, uint32_t shstride,
-                                                uint32_t skpad, uint32_t n, stage_q2_rec *__restrict__ out,
+                                                uint32_t skpad, uint32_t n, uint64_t m, stage_q2_rec *__restrict__ out,
                                                 uint64_t *__restrict__ ikeys, int32_t *__restrict__ abort_flag) {
-    const uint32_t s = blockIdx.x, lane = threadIdx.x;
-    if (s >= n) return;
-    const uint64_t b = dst[s];
+    // block = (supplier s, query q): query q's lookups are the q-th copy of the m keys
+    const uint32_t s = blockIdx.x % n, q = blockIdx.x / n, lane = threadIdx.x;
+    abort_flag += q;
+    out += (uint64_t)q * n;
+    ikeys += (uint64_t)q * n;
+    const uint64_t b = (uint64_t)q * m + dst[s];
     const uint32_t c = cnt[s];
     bool bad = false;
     for (uint32_t e = lane; e < c; e += 64) bad |= !produced(sout[b + e].w[0] & 0xFF);
@@ -96,13 +101,13 @@ __global__ __launch_bounds__(64) void q2_reduce(const stage_probe_out_dev *__res
 // item outcome: no tuple aborts; I_DATA up to its first NUL containing 'b' skips; else a
 // quantity below 10 marks the update
 __global__ void q2_finish(const stage_probe_out_dev *__restrict__ iout, const uint8_t *__restrict__ iheap,
-                          uint32_t ihstride, uint32_t ikpad, uint32_t n, stage_q2_rec *__restrict__ out,
+                          uint32_t ihstride, uint32_t ikpad, uint32_t n, uint32_t nq, stage_q2_rec *__restrict__ out,
                           int32_t *__restrict__ abort_flag) {
-    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= n) return;
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;  // q * n + supplier
+    if (s >= n * nq) return;
     const uint32_t st = iout[s].w[0] & 0xFF;
     if (!produced(st)) {
-        atomicOr(abort_flag, 1);
+        atomicOr(abort_flag + s / n, 1);
         return;
     }
     const uint8_t *d = iheap + (uint64_t)iout[s].w[6] * ihstride + ikpad + kIDataOff;
@@ -156,10 +161,11 @@ std::vector<uint8_t> scan_rows(stage_table *t, uint64_t start, uint32_t scan_siz
 }  // namespace
 }  // namespace stage
 
-extern "C" int stage_ch_query2(stage_table *region, stage_table *nation, stage_table *supplier, stage_table *item,
-                               stage_table *stock, const uint32_t *map_off, const uint64_t *d_map_keys,
-                               int32_t target_region, uint32_t read_id, uint32_t commit_id, stage_q2_rec *out,
-                               uint64_t max_out, uint64_t *n_out, int32_t *aborted, void *stream) {
+// nq transactions at read ids rq[0..nq): out[q * max_out + k], aborted[q]; commit only for nq == 1
+static int q2_run(stage_table *region, stage_table *nation, stage_table *supplier, stage_table *item,
+                  stage_table *stock, const uint32_t *map_off, const uint64_t *d_map_keys, int32_t target_region,
+                  const uint32_t *rq, uint32_t nq, uint32_t commit_id, stage_q2_rec *out, uint64_t max_out,
+                  uint64_t *n_out, int32_t *aborted, void *stream) {
     for (stage_table *t : {region, nation, supplier, item, stock}) {
         int rc = need_synced(t);
         if (rc) return rc;
@@ -181,7 +187,7 @@ extern "C" int stage_ch_query2(stage_table *region, stage_table *nation, stage_t
         hip_check(hipSetDevice(stock->dev.device), "hipSetDevice");
         hipStream_t s = pick(stock, stream);
         *n_out = 0;
-        *aborted = 0;
+        for (uint32_t q = 0; q < nq; ++q) aborted[q] = 0;
         // 1. REGION / NATION scans, SUPPLIER scan of every record, filtered on the host
         uint32_t nreg = 0, nnat = 0;
         const uint32_t rs = region->dev.view.stride, ns = nation->dev.view.stride;
@@ -233,12 +239,15 @@ extern "C" int stage_ch_query2(stage_table *region, stage_table *nation, stage_t
             return o;
         };
         const uint64_t o_src = take(n * 8), o_dst = take(n * 8), o_cnt = take(n * 4), o_sup = take(n * 8),
-                       o_keys = take(std::max<uint64_t>(m, 1) * 16), o_rids = take(std::max<uint64_t>(m, n) * 4),
-                       o_sout = take(std::max<uint64_t>(m, 1) * 32), o_rec = take(n * sizeof(stage_q2_rec)),
-                       o_ik = take(n * 8), o_iout = take(n * 32), o_ab = take(4);
+                       o_keys = take(std::max<uint64_t>(m, 1) * 16 * nq),
+                       o_rids = take(std::max<uint64_t>(m, n) * 4 * nq), o_irids = take(n * 4 * nq),
+                       o_rq = take(nq * 4), o_sout = take(std::max<uint64_t>(m, 1) * 32 * nq),
+                       o_rec = take(n * sizeof(stage_q2_rec) * nq), o_ik = take(n * 8 * nq),
+                       o_iout = take(n * 32 * nq), o_ab = take(4 * nq);
         uint8_t *buf = scratch_bytes(nation->dev, off);
         auto *d_src = (uint64_t *)(buf + o_src), *d_dst = (uint64_t *)(buf + o_dst), *d_sup = (uint64_t *)(buf + o_sup);
         auto *d_cnt = (uint32_t *)(buf + o_cnt), *d_rids = (uint32_t *)(buf + o_rids);
+        auto *d_irids = (uint32_t *)(buf + o_irids), *d_rq = (uint32_t *)(buf + o_rq);
         auto *d_keys = (uint64_t *)(buf + o_keys), *d_ik = (uint64_t *)(buf + o_ik);
         auto *d_sout = (stage_probe_out_dev *)(buf + o_sout), *d_iout = (stage_probe_out_dev *)(buf + o_iout);
         auto *d_rec = (stage_q2_rec *)(buf + o_rec);
@@ -247,26 +256,31 @@ extern "C" int stage_ch_query2(stage_table *region, stage_table *nation, stage_t
         hip_check(hipMemcpyAsync(d_dst, dst.data(), n * 8, hipMemcpyHostToDevice, s), "h2d");
         hip_check(hipMemcpyAsync(d_cnt, cnt.data(), n * 4, hipMemcpyHostToDevice, s), "h2d");
         hip_check(hipMemcpyAsync(d_sup, sel.data(), n * 8, hipMemcpyHostToDevice, s), "h2d");
-        hip_check(hipMemsetAsync(d_ab, 0, 4, s), "memset");
-        const uint64_t nr = std::max<uint64_t>(m, n);
-        q2_fill_u32<<<(unsigned)((nr + 255) / 256), 256, 0, s>>>(d_rids, nr, read_id);
-        q2_gather<<<n, 256, 0, s>>>(d_map_keys, d_src, d_dst, d_cnt, d_keys);
+        hip_check(hipMemcpyAsync(d_rq, rq, nq * 4, hipMemcpyHostToDevice, s), "h2d");
+        hip_check(hipMemsetAsync(d_ab, 0, 4 * nq, s), "memset");
+        q2_fill_rids<<<(unsigned)((m * nq + 255) / 256) + 1, 256, 0, s>>>(d_rids, m, nq, d_rq);
+        q2_fill_rids<<<(unsigned)((n * nq + 255) / 256), 256, 0, s>>>(d_irids, n, nq, d_rq);
+        q2_gather<<<dim3(n, nq), 256, 0, s>>>(d_map_keys, d_src, d_dst, d_cnt, m, d_keys);
         const DevTable &sv = stock->dev.view, &iv = item->dev.view;
         if (m)
-            hip_check(launch_probe(sv, d_keys, nullptr, d_rids, nullptr, m, d_sout, nullptr, s, stock->tune),
+            hip_check(launch_probe(sv, d_keys, nullptr, d_rids, nullptr, m * nq, d_sout, nullptr, s, stock->tune),
                       "stock probe");
-        q2_reduce<<<n, 64, 0, s>>>(d_sout, d_keys, d_dst, d_cnt, d_sup, sv.heap, sv.hstride, stock->host->key_pad(),
-                                   n, d_rec, d_ik, d_ab);
+        q2_reduce<<<n * nq, 64, 0, s>>>(d_sout, d_keys, d_dst, d_cnt, d_sup, sv.heap, sv.hstride,
+                                        stock->host->key_pad(), n, m, d_rec, d_ik, d_ab);
         // 3. item lookups of the last stocks, filter
-        hip_check(launch_probe(iv, d_ik, nullptr, d_rids, nullptr, n, d_iout, nullptr, s, item->tune), "item probe");
-        q2_finish<<<(n + 255) / 256, 256, 0, s>>>(d_iout, iv.heap, iv.hstride, item->host->key_pad(), n, d_rec, d_ab);
+        hip_check(launch_probe(iv, d_ik, nullptr, d_irids, nullptr, (uint64_t)n * nq, d_iout, nullptr, s, item->tune),
+                  "item probe");
+        q2_finish<<<(n * nq + 255) / 256, 256, 0, s>>>(d_iout, iv.heap, iv.hstride, item->host->key_pad(), n, nq,
+                                                       d_rec, d_ab);
         hip_check(hipGetLastError(), "q2 kernels");
-        std::vector<stage_q2_rec> recs(n);
-        hip_check(hipMemcpyAsync(recs.data(), d_rec, n * sizeof(stage_q2_rec), hipMemcpyDeviceToHost, s), "d2h");
-        hip_check(hipMemcpyAsync(aborted, d_ab, 4, hipMemcpyDeviceToHost, s), "d2h");
+        std::vector<stage_q2_rec> recs((uint64_t)n * nq);
+        hip_check(hipMemcpyAsync(recs.data(), d_rec, recs.size() * sizeof(stage_q2_rec), hipMemcpyDeviceToHost, s),
+                  "d2h");
+        hip_check(hipMemcpyAsync(aborted, d_ab, 4 * nq, hipMemcpyDeviceToHost, s), "d2h");
         hip_check(hipStreamSynchronize(s), "q2 sync");
+        const uint32_t read_id = rq[0];
         // 4. the transaction's stock updates, through the device write path
-        if (commit_id && !*aborted) {
+        if (nq == 1 && commit_id && !*aborted) {
             std::vector<uint64_t> uk;
             std::vector<int32_t> ud;
             std::vector<uint32_t> ui;
@@ -305,7 +319,28 @@ extern "C" int stage_ch_query2(stage_table *region, stage_table *nation, stage_t
                 for (uint64_t j = 0; j < nu; ++j) recs[ui[j]].update_rc = rcs[j];
             }
         }
-        std::memcpy(out, recs.data(), std::min<uint64_t>(n, max_out) * sizeof(stage_q2_rec));
+        for (uint32_t q = 0; q < nq; ++q)
+            std::memcpy(out + (uint64_t)q * max_out, recs.data() + (uint64_t)q * n,
+                        std::min<uint64_t>(n, max_out) * sizeof(stage_q2_rec));
         return STAGE_OK;
     });
+}
+
+extern "C" int stage_ch_query2(stage_table *region, stage_table *nation, stage_table *supplier, stage_table *item,
+                               stage_table *stock, const uint32_t *map_off, const uint64_t *d_map_keys,
+                               int32_t target_region, uint32_t read_id, uint32_t commit_id, stage_q2_rec *out,
+                               uint64_t max_out, uint64_t *n_out, int32_t *aborted, void *stream) {
+    return q2_run(region, nation, supplier, item, stock, map_off, d_map_keys, target_region, &read_id, 1, commit_id,
+                  out, max_out, n_out, aborted, stream);
+}
+
+extern "C" int stage_ch_query2_batch(stage_table *region, stage_table *nation, stage_table *supplier,
+                                     stage_table *item, stage_table *stock, const uint32_t *map_off,
+                                     const uint64_t *d_map_keys, int32_t target_region, const uint32_t *read_ids,
+                                     uint32_t nq, stage_q2_rec *out, uint64_t max_per_query, uint64_t *n_out,
+                                     int32_t *aborted, void *stream) {
+    if (nq == 0) return STAGE_OK;
+    if (!read_ids || nq > 4096) return fail(STAGE_E_ARG, "read_ids: 1..4096 queries");
+    return q2_run(region, nation, supplier, item, stock, map_off, d_map_keys, target_region, read_ids, nq, 0, out,
+                  max_per_query, n_out, aborted, stream);
 }

@@ -58,6 +58,9 @@ SIGNATURES = {
     "stage_key_words": (ctypes.c_uint32, [c_vp]),
     "stage_sync": (ctypes.c_int, [c_vp]),
     "stage_tpcc_stock_level": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_uint64, c_vp, c_vp]),
+    "stage_ch_query2_batch": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_int32, c_vp,
+                                             ctypes.c_uint32, c_vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64),
+                                             c_vp, c_vp]),
     "stage_ch_query2": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_int32, ctypes.c_uint32,
                                        ctypes.c_uint32, c_vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64),
                                        ctypes.POINTER(ctypes.c_int32), c_vp]),

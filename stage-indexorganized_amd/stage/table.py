@@ -573,3 +573,18 @@ def ch_query2(region, nation, supplier, item, stock, map_off, d_map_keys, target
                                 int(target_region), int(read_id), int(commit_id), out.ctypes.data, max_out,
                                 ctypes.byref(n), ctypes.byref(ab), stream), "ch_query2")
     return out[:min(n.value, max_out)], bool(ab.value)
+
+
+def ch_query2_batch(region, nation, supplier, item, stock, map_off, d_map_keys, read_ids, target_region=3,
+                    max_per_query=1 << 14, stream=None):
+    """stage_ch_query2_batch: nq read-only Q2s in one pass -> (records [nq, n] Q2_REC_DTYPE, aborted[nq])."""
+    map_off = np.ascontiguousarray(map_off, np.uint32)
+    rids = np.ascontiguousarray(read_ids, np.uint32)
+    nq = rids.size
+    out = np.zeros((nq, max_per_query), Q2_REC_DTYPE)
+    ab = np.zeros(nq, np.int32)
+    n = ctypes.c_uint64()
+    check(lib().stage_ch_query2_batch(region.h, nation.h, supplier.h, item.h, stock.h, map_off.ctypes.data,
+                                      d_map_keys, int(target_region), rids.ctypes.data, nq, out.ctypes.data,
+                                      max_per_query, ctypes.byref(n), ab.ctypes.data, stream), "ch_query2_batch")
+    return out[:, :min(n.value, max_per_query)], ab.astype(bool)

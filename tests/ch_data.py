@@ -114,6 +114,11 @@ class ChTables:
                                    self.d_map.ptr, target, read_id, commit_id, out=self._out)
         return recs.copy(), ab
 
+    def query2_batch(self, read_ids, target=3):
+        t = self.tables
+        return stage.ch_query2_batch(t["region"], t["nation"], t["supplier"], t["item"], t["stock"], self.map_off,
+                                     self.d_map.ptr, read_ids, target)
+
     def query2_oracle(self, target=3, read_id=0xFFFFFFFE):
         import ctypes
 

@@ -39,6 +39,21 @@ def test_q2_matches_oracle_all_regions(ch):
     assert recs.size > 1000 and recs["update"].sum() > 0 and recs["item_has_b"].sum() > 0
 
 
+def test_q2_batch_equals_single_queries(ch):
+    rids = np.array([10, 0xFFFFFFFE, 3, 25, 0xFFFFFFFE, 7], np.uint32)
+    for target in (0, 3):
+        recs, ab = ch.query2_batch(rids, target)
+        assert recs.shape[0] == rids.size
+        for q, r in enumerate(rids):
+            one, ab1 = ch.query2(target, read_id=int(r))
+            assert ab[q] == ab1
+            if not ab1:
+                same(recs[q], one)
+                orecs, oab = ch.query2_oracle(target, int(r))
+                assert not oab
+                same(recs[q], orecs)
+
+
 def test_q2_visibility_and_commit(ch):
     ostock = ch.orc["stock"]
     stock = ch.tables["stock"]
@@ -54,12 +69,14 @@ def test_q2_visibility_and_commit(ch):
     k = np.array([r["s_w_id"], r["s_i_id"]], np.int64).tobytes()
     assert stock.update_key(k, 4, b"\x05\x00\x00\x00", 30) == ostock.update(k, 16, 4, b"\x05\x00\x00\x00", 30)
     stock.sync()
-    for rid in (10, 25, 40, 0xFFFFFFFE):  # rid 10: retired versions with begin 0 -> FAILURE -> abort
+    brecs, babort = ch.query2_batch(np.array([10, 25, 40, 0xFFFFFFFE], np.uint32), 3)
+    for q, rid in enumerate((10, 25, 40, 0xFFFFFFFE)):  # rid 10: retired versions with begin 0 -> FAILURE -> abort
         recs, ab = ch.query2(3, read_id=rid)
         orecs, oab = ch.query2_oracle(3, read_id=rid)
-        assert ab == oab, rid
+        assert ab == oab == babort[q], rid
         if not ab:
             same(recs, orecs)
+            same(brecs[q], orecs)
     assert ch.query2(3, read_id=10)[1]  # the abort case is exercised
     # commit path: the transaction's updates through the device write path, mirrored on the oracle
     rid, cid = 50, 51
