@@ -10,14 +10,20 @@ Default (`--config c2`, BASELINE.json configs[1]): YCSB-C batched point lookup.
           with --gpus > 1 each key goes to shard MurmurHash64A(key, 8, 0) % world and is
           answered over RCCL (stage_probe_sharded) -- configs[4] at 8 GPUs
   value = lookups completed by all ranks / max-over-ranks wall time of the K timed steps.
-`--config c3` (configs[2]): YCSB-B epochs -- 5 % updates (zipf 0.99) applied between steps
-  by the device write path (stage_update_batch_device; `--write-path host` = host write path +
-  incremental publish), the step probes the reads (25 % at older snapshots -> version chains
-  on the device).  `--config c4` (configs[3]): 100-key range scans.
+  After the headline the same 100M-row table runs configs[3] (C4, 100-key scans) and then
+  configs[2] (C3, YCSB-B epochs; last, since it mutates the table); their lines are nested
+  under "extras" and do not change value / metric / config.
+`--config c3` / `--config c4` make those the headline instead.
+
+`--gpus N` (N > 1) without a torch.distributed environment starts N ranks itself (a child
+`python -m torch.distributed.run`, before any GPU call) and forwards rank 0's JSON line; under
+torch.distributed the world size must equal --gpus.
 
 The CPU baseline leg (rank 0, one GPU) times the test oracle -- the C restatement of the
-reference's BTree::Read + executor copy (or TableScanExecutor) -- on a bounded 2M-row sample
-(the reference's own default pools cap a YCSB table at ~2-2.5M rows).
+reference's BTree::Read + executor copy ("lookup" mode) and of RunMixed's read-only
+transactions with the Index-SSN read side ("full-txn" mode) -- on the largest table the host
+RAM holds (up to the GPU's N; built in parallel with the same leaves as the single loader,
+while the GPU leg runs), with the threads this process may use (affinity and cgroup quota).
 """
 import argparse
 import ctypes
@@ -26,14 +32,17 @@ import math
 import os
 import platform
 import resource
+import socket
+import subprocess
 import sys
+import threading
 import time
 
 import numpy as np
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "stage-indexorganized_amd"))
-import stage  # noqa: E402  (load libstage_hip.so before anything else binds a HIP runtime)
+import stage  # noqa: E402  (libstage_hip.so is loaded lazily, on the first library call)
 from stage._lib import check  # noqa: E402
 
 METRIC = "YCSB ops/sec at 1/2/4/8 GPU + achieved HBM GB/s vs peak; CPU ref ops/sec"
@@ -45,8 +54,16 @@ WORKLOADS = {
 }
 # algorithmic bytes
 BYTES_PER_LOOKUP = 2100  # 8 key + 64 key-column line + 16 slot word + 1000 payload + 1008 out + 4
+HOP_BYTES = 64           # C3: one TupleHeader (version) line per chain hop taken
 HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md: 8.0 TB/s HBM3E spec
 XGMI_LINK_GBS = 153.0    # per xGMI link of an MI355X (7 links per GPU, point to point)
+ORACLE_BYTES_PER_ROW = 1800  # oracle tree host memory per YCSB row (64 KiB leaves, ~38-48 rows each, + inner)
+GPU_HOST_BYTES_PER_ROW = 130  # host side of a device table (host_peak_rss 11.8 GiB at 100M rows)
+# the reference itself, measured in the survey container and the oracle in
+# the same container type: calibration of the port
+REF_C1_OPS = 1533428.0       # YCSB-C -k 1000 -o 10, 1 thread
+REF_READ_NS_1M = 1786.0      # BTree::Read, 1M rows, 1 thread
+REF_TXN_OPS_1M = 428817.0    # YCSB-C 1M rows, 1 thread, full driver
 
 
 def scan_bytes(L, S=48.8):
@@ -58,9 +75,10 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=1,
+                   help="ranks (one per GPU); > 1 without torch.distributed env: launch them")
     p.add_argument("--steps", type=int, default=None)
     p.add_argument("--warmup", type=int, default=None)
     p.add_argument("--config", choices=["c2", "c3", "c4", "tpcc", "chq2"], default="c2")
@@ -71,25 +89,134 @@ def parse():
     p.add_argument("--batch", type=int, default=None, help="lookups (c2/c3) or scans (c4) per GPU per step")
     p.add_argument("--theta", type=float, default=None)
     p.add_argument("--scan-size", type=int, default=100)
+    p.add_argument("--scan-batch", type=int, default=1 << 18, help="scans per step of the C4 leg")
     p.add_argument("--update-ratio", type=float, default=0.05)
+    p.add_argument("--inflight-share", type=float, default=0.02,
+                   help="c3: share of the update ops left in flight (uncommitted; keys beyond the 10^4 hottest) "
+                        "so reads of them take the overwrite-copy (COPY) branch")
+    p.add_argument("--c3-epochs", type=int, default=3, help="timed YCSB-B epochs of the nested C3 leg")
     p.add_argument("--write-path", choices=["device", "host"], default="device",
                    help="c3: apply each epoch's updates on the device (stage_update_batch_device) or on the "
                         "host write path + incremental publish (stage_update_batch + stage_sync)")
     p.add_argument("--seed", type=int, default=0x5EED)
-    p.add_argument("--cpu-rows", type=int, default=2_000_000)
-    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--cpu-rows", type=int, default=0, help="oracle rows of the CPU leg (0 = the largest that fits)")
+    p.add_argument("--cpu-seconds", type=float, default=6.0, help="target CPU time of each timed CPU sample")
+    p.add_argument("--cpu-threads", type=int, default=0, help="0 = the CPUs this process may use")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-extras", action="store_true", help="c2: skip the nested C4 / C3 legs")
     p.add_argument("--host-traversal", action="store_true", help="leaf ids from the host router instead")
     p.add_argument("--force-sharded", action="store_true",
                    help="run the multi-GPU (RCCL) code path even with one rank -- a rehearsal, not a config")
-    a = p.parse_args()
-    a.steps = a.steps if a.steps is not None else (5 if a.config == "c3" else 20)
+    p.add_argument("--dry-run", action="store_true",
+                   help="control plane only (no GPU): ranks rendezvous over gloo, load their shard's host "
+                        "table, time a routing step; for CPU tests of the launcher")
+    a = p.parse_args(argv)
+    a.steps = a.steps if a.steps is not None else (5 if a.config == "c3" else (10 if a.config == "tpcc" else 20))
     a.warmup = a.warmup if a.warmup is not None else (1 if a.config == "c3" else 3)
     a.theta = a.theta if a.theta is not None else (0.99 if a.config == "c3" else 0.9)
     a.batch = a.batch if a.batch is not None else ((1 << 18) if a.config in ("c4", "tpcc") else (1 << 24))
-    if a.config == "tpcc":
-        a.steps = a.steps if a.steps is not None else 10
     return a
+
+
+# ------------------------------------------------------------------------ multi-rank launch
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args, argv):
+    """--gpus N > 1 outside torch.distributed: run N ranks as a child torch.distributed.run
+    (this process never touches the GPU and never execs), forward rank 0's JSON line, and
+    fail unless it reports n_gpus == N."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "8")
+    log(f"[launcher] {' '.join(cmd)}")
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, bufsize=1)
+    line = None
+    for raw in p.stdout:
+        s = raw.strip()
+        if s.startswith("{") and '"metric"' in s:
+            line = s
+        else:
+            log(raw.rstrip())
+    rc = p.wait()
+    if line is None:
+        log(f"[launcher] no result line from the ranks (exit {rc})")
+        return rc or 1
+    print(line, flush=True)
+    n = json.loads(line).get("n_gpus")
+    if n != args.gpus:
+        log(f"[launcher] ranks reported n_gpus={n}, expected {args.gpus}")
+        return 1
+    return rc
+
+
+def murmur64a_u64(keys, seed=0):
+    """MurmurHash64A of 8-byte little-endian keys (misc/murmur/MurmurHash2.cpp:99-147), numpy:
+    the router's hash for the host-only --dry-run (the GPU path uses murmur_kernel)."""
+    m, r = np.uint64(0xC6A4A7935BD1E995), np.uint64(47)
+    with np.errstate(over="ignore"):
+        h = np.full(keys.shape, np.uint64(seed) ^ (np.uint64(8) * m), np.uint64)
+        k = keys.astype(np.uint64) * m
+        k ^= k >> r
+        k *= m
+        h ^= k
+        h *= m
+        h ^= h >> r
+        h *= m
+        h ^= h >> r
+    return h
+
+
+def dry_run(args, rank, world, dist):
+    """Control-plane rehearsal without a GPU: the ranks of the launcher rendezvous, each loads
+    its shard (MurmurHash64A(key) % world) into a host table, routes a probe batch to its
+    owners with an all-to-all, and the step is timed with the bench's barrier / max-over-ranks
+    rule; rank 0 prints the result line."""
+    import torch
+    rows = min(args.rows, 200_000)
+    keys = np.arange(rows * world, dtype=np.uint64)
+    mine = keys[murmur64a_u64(keys) % np.uint64(world) == np.uint64(rank)]
+    tab = stage.Table(key_width=8)
+    loaded = tab.load_keys(mine, 8, 0)
+    probes = stage.zipf_draws(rows * world - 1, args.theta, args.seed + rank, 1 << 14, nthreads=2)
+    dest = (murmur64a_u64(probes) % np.uint64(world)).astype(np.int64)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        order = np.argsort(dest, kind="stable")
+        scount = torch.tensor(np.bincount(dest, minlength=world), dtype=torch.int64)
+        rcount = torch.zeros(world, dtype=torch.int64)
+        dist.all_to_all_single(rcount, scount)
+        recv = torch.zeros(int(rcount.sum()), dtype=torch.int64)
+        dist.all_to_all_single(recv, torch.from_numpy(probes[order].view(np.int64).copy()), rcount.tolist(),
+                               scount.tolist())
+    elapsed = time.perf_counter() - t0
+    got = recv.numpy().view(np.uint64)
+    ok = bool((murmur64a_u64(got) % np.uint64(world) == np.uint64(rank)).all())
+    tt = torch.tensor([elapsed], dtype=torch.float64)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    counts = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(counts, torch.tensor([rank, loaded], dtype=torch.int64))
+    oks = torch.tensor([int(ok)], dtype=torch.int64)
+    dist.all_reduce(oks, op=dist.ReduceOp.MIN)
+    if rank == 0:
+        total = float(tt.item())
+        print(json.dumps({"metric": METRIC, "value": round(probes.size * args.steps * world / total, 1),
+                          "unit": "routed keys/s (dry run, no GPU)", "n_gpus": world, "steps": args.steps,
+                          "warmup": 0, "ms_per_step": round(total / args.steps * 1e3, 4), "higher_is_better": True,
+                          "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+                          "dry_run": True, "ranks": [int(c[0]) for c in counts],
+                          "rows_per_rank": [int(c[1]) for c in counts], "self_check": bool(oks.item()),
+                          "config": {"workload": WORKLOADS["c5"] + " (control plane rehearsal)",
+                                     "parallelism": f"hash-shard x{world}"}}), flush=True)
+    return 0 if oks.item() else 1
 
 
 def owned_keys(total_rows, world, rank):
@@ -128,6 +255,45 @@ def cpu_name():
     return platform.processor() or "unknown"
 
 
+def _read(path):
+    try:
+        return open(path).read().strip()
+    except OSError:
+        return None
+
+
+def cpu_resources():
+    """What this process may use: affinity CPUs, the cgroup CPU quota (cpu.max), host memory
+    (MemTotal / MemAvailable) and the cgroup memory limit (memory.max)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    q = _read("/sys/fs/cgroup/cpu.max")
+    if q and not q.startswith("max"):
+        a, b = q.split()[:2]
+        quota = max(1, int(math.floor(int(a) / int(b))))
+    mem = {}
+    for line in (_read("/proc/meminfo") or "").splitlines():
+        k, v = line.split(":", 1)
+        mem[k] = int(v.split()[0]) * 1024
+    cg = _read("/sys/fs/cgroup/memory.max")
+    cg_mem = int(cg) if cg and cg.isdigit() else None
+    threads = min(aff, quota) if quota else aff
+    return {"nproc": os.cpu_count(), "affinity_cpus": aff, "cgroup_cpus": quota, "threads": threads,
+            "cpu_model": cpu_name(), "mem_total_gib": round(mem.get("MemTotal", 0) / 2**30, 1),
+            "mem_available_gib": round(mem.get("MemAvailable", 0) / 2**30, 1),
+            "cgroup_mem_gib": round(cg_mem / 2**30, 1) if cg_mem else None,
+            "_avail": min(x for x in (mem.get("MemAvailable", 0), cg_mem, 250 * 2**30) if x)}
+
+
+def cpu_rows_for(args, res, gpu_rows):
+    """Largest oracle table (rows) that fits beside the GPU leg's host memory, <= the GPU's N."""
+    if args.cpu_rows:
+        return args.cpu_rows
+    budget = res["_avail"] - 24 * 2**30 - gpu_rows * GPU_HOST_BYTES_PER_ROW
+    fit = int(budget // ORACLE_BYTES_PER_ROW) // 1_000_000 * 1_000_000
+    return max(1_000_000, min(gpu_rows, fit))
+
+
 def xgmi_roofline(batch, world, stride, step_s, hbm_roof):
     """Roofline of the multi-GPU step, bound by the xGMI exchange: per rank and step the remote
     share of the batch ((W-1)/W of it, hash-uniform) sends its 16-B key record out and gets a
@@ -145,40 +311,17 @@ def xgmi_roofline(batch, world, stride, step_s, hbm_roof):
             "hbm": hbm_roof}
 
 
-def cpu_baseline(args, threads):
-    sys.path.insert(0, os.path.join(REPO, "tests"))
-    import oracle_lib as O  # the checker, timed here as the reference CPU path
-    n = args.cpu_rows
-    t0 = time.time()
-    orc = O.OracleTree()
-    orc.load_ycsb(0, n, 8, 0)
-    build_s = time.time() - t0
-    secs = ctypes.c_double()
-    if args.config == "c4":
-        starts = (stage.fastrandom(args.seed, 20_000) % np.uint64(n)).astype(np.uint64)
-        O.lib().orc_scan_batch_timed(orc.t, starts.ctypes.data, 8, starts.size, args.scan_size, threads,
-                                     ctypes.byref(secs))
-        rate = starts.size / max(secs.value, 1e-9)
-        count = int(min(max(rate * args.cpu_seconds, 10_000), 5_000_000))
-        starts = (stage.fastrandom(args.seed + 1, count) % np.uint64(n)).astype(np.uint64)
-        O.lib().orc_scan_batch_timed(orc.t, starts.ctypes.data, 8, starts.size, args.scan_size, threads,
-                                     ctypes.byref(secs))
-        value = count / secs.value
-        what = f"oracle TableScanExecutor over Iterator, {count} scans of {args.scan_size}"
-        unit = "scans/s"
-    else:
-        keys = stage.zipf_draws(n - 1, args.theta, args.seed, 400_000, nthreads=threads)
-        O.lib().orc_read_batch_timed(orc.t, keys.ctypes.data, 8, None, keys.size, threads, ctypes.byref(secs))
-        rate = keys.size / max(secs.value, 1e-9)
-        count = int(min(max(rate * args.cpu_seconds, 100_000), 300_000_000))
-        keys = stage.zipf_draws(n - 1, args.theta, args.seed + 1, count, nthreads=threads)
-        O.lib().orc_read_batch_timed(orc.t, keys.ctypes.data, 8, None, keys.size, threads, ctypes.byref(secs))
-        value = count / secs.value
-        what = f"oracle BTree::Read+copy, {count} zipf-{args.theta} lookups"
-        unit = "ops/s"
-    return {"value": round(value, 1), "unit": unit, "cores": threads, "kind": "port",
-            "sample": f"{what}, {n} rows (8-B keys, 1000-B payload, build {build_s:.1f}s), {threads} threads "
-                      f"on {cpu_name()}, {secs.value:.1f}s"}
+def hbm_roofline(per_unit, units_per_launch, kern_ms, kernel, traffic=None, tsrc=None):
+    achieved = per_unit * units_per_launch / (kern_ms * 1e-3) / 1e9
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kernel,
+            "algorithmic_bytes_per_unit": round(per_unit, 2), "units_per_launch": units_per_launch,
+            "algorithmic_bytes_per_launch": round(per_unit * units_per_launch),
+            "avg_launch_ms": round(kern_ms, 4)}
+    if traffic:
+        roof["traffic_source"] = tsrc
+        roof["traffic_over_algorithmic"] = round(traffic / (per_unit * units_per_launch), 4)
+    return roof
 
 
 class PinnedArray:
@@ -202,12 +345,15 @@ class YcsbB:
     (LeafNode::Update + CommitTransaction UPDATE entry, read/commit ids from one counter as
     tid_counter does) -- on the device (stage_update_batch_device) or on the host
     (stage_update_batch + incremental publish) -- and returns the read share with read ids:
-    75 % current, 25 % drawn from the ids of this run so far (older snapshots).
+    75 % current, 25 % drawn from the ids of this run so far (older snapshots).  A share of
+    the update ops (--inflight-share, keys beyond the 10^4 hottest) stays in flight (commit id
+    0), so later reads of those keys take the overwrite-copy branch.
     Timed as the write path (`write_s`): the update share's transfer to the device and the call
-    (device) or the host update + publish (host); generating the synthetic epoch is not."""
+    (device) or the host update + publish (host); generating the synthetic epoch is not.
+    Every epoch is recorded (keys, column byte, ids) so the CPU leg can replay it on the oracle."""
 
-    def __init__(self, tab, args, nthreads):
-        self.tab, self.args, self.nthreads = tab, args, nthreads
+    def __init__(self, tab, args, nthreads, theta):
+        self.tab, self.args, self.nthreads, self.theta = tab, args, nthreads, theta
         self.counter = 1
         self.epoch = 0
         self.updates = 0
@@ -215,6 +361,7 @@ class YcsbB:
         self.write_s = 0.0
         self.sync_s = 0.0
         self.last_sync = None
+        self.record = []
         if args.write_path == "device":
             B = args.batch  # the update share of a batch never exceeds it
             self.h = {k: PinnedArray(B * w, dt) for k, (w, dt) in
@@ -223,11 +370,14 @@ class YcsbB:
             self.d = {k: stage.DeviceBuffer(v.nbytes) for k, v in self.h.items()}
             self.d_rc = stage.DeviceBuffer(B)
 
+    def reset_counters(self):
+        self.updates, self.write_s, self.sync_s = 0, 0.0, 0.0
+
     def next_batch(self):
         a = self.args
         n = a.rows
         t0 = time.time()
-        draws = stage.zipf_draws(n - 1, a.theta, a.seed + 1000 * self.epoch, a.batch, nthreads=self.nthreads)
+        draws = stage.zipf_draws(n - 1, self.theta, a.seed + 1000 * self.epoch, a.batch, nthreads=self.nthreads)
         rng = np.random.default_rng(a.seed + self.epoch)
         is_upd = rng.random(a.batch) < a.update_ratio
         keys = draws[is_upd]
@@ -235,10 +385,15 @@ class YcsbB:
         # read id / commit id pairs from one counter (tid_counter), one 100-B column patch each
         rid = (self.counter + 2 * np.arange(m, dtype=np.uint64)).astype(np.uint32)
         cid = rid + np.uint32(1)
+        cand = np.nonzero(keys > 10_000)[0]
+        k_in = min(cand.size, int(round(a.inflight_share * m)))
+        if k_in:
+            cid[rng.choice(cand, k_in, replace=False)] = 0  # left in flight
         self.counter += 2 * m
-        cols = np.repeat(((keys + np.uint64(self.epoch + 1)) & np.uint64(0xFF)).astype(np.uint8)[:, None], 100, 1)
+        colb = ((keys + np.uint64(self.epoch + 1)) & np.uint64(0xFF)).astype(np.uint8)
         if a.write_path == "device":
-            for k, x in (("keys", keys), ("cols", cols.reshape(-1)), ("rid", rid), ("cid", cid)):
+            self.h["cols"].a[:m * 100] = np.repeat(colb, 100)
+            for k, x in (("keys", keys), ("rid", rid), ("cid", cid)):
                 self.h[k].a[:x.size] = x
         self.prep_s += time.time() - t0
         tu = time.time()
@@ -255,6 +410,7 @@ class YcsbB:
                       "update_batch_device")
             ok = ok.value
         else:
+            cols = np.repeat(colb[:, None], 100, 1)
             _, ok = self.tab.update_batch(keys, 0, cols, rid, cid)
             t1 = time.time()
             self.tab.sync()
@@ -267,38 +423,160 @@ class YcsbB:
         rids = np.full(reads.size, self.counter, np.uint32)
         old = rng.random(reads.size) < 0.25
         rids[old] = rng.integers(1, max(2, self.counter), int(old.sum())).astype(np.uint32)
+        self.record.append({"keys": keys, "colb": colb, "rid": rid, "cid": cid, "ok": ok,
+                            "inflight": int(k_in)})
         self.epoch += 1
         self.prep_s += time.time() - t0
         return reads, rids
 
 
-def tpcc_tables(args, seed=7):
-    """DISTRICT / ORDER_LINE / STOCK rows with the reference's key and payload layouts
-    (tpcc_record.h), generated vectorised: W warehouses x 10 districts x 3000 orders of 5..15
-    lines, `items` stock rows per warehouse.  First payload columns: D_NEXT_O_ID, OL_I_ID,
-    S_QUANTITY (int32)."""
-    rng = np.random.default_rng(seed)
-    W, I, D, O = args.warehouses, args.items, 10, 3000
+class CpuOracle:
+    """The CPU leg's oracle table (test oracle = the reference path restated in C), built in a
+    background thread while the GPU leg runs: LoadYCSBRows of `rows` rows with the single
+    loader's leaves (orc_load_ycsb_parallel)."""
+
+    def __init__(self, rows, threads):
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        import oracle_lib as O  # the checker, timed here as the reference CPU path
+        self.O = O
+        self.rows, self.threads = rows, threads
+        self.tree = None
+        self.build_s = None
+        self.err = None
+        self.th = threading.Thread(target=self._build, daemon=True)
+        self.th.start()
+
+    def _build(self):
+        try:
+            t0 = time.time()
+            t = self.O.OracleTree()
+            t.load_ycsb_parallel(0, self.rows, 8, 0, self.threads)
+            self.tree = t
+            self.build_s = time.time() - t0
+        except Exception as e:  # reported in the result line
+            self.err = repr(e)
+
+    def wait(self):
+        self.th.join()
+        if self.err:
+            raise RuntimeError(f"oracle build failed: {self.err}")
+        return self.tree
+
+
+def cpu_sample_count(rate, seconds, lo, hi):
+    return int(min(max(rate * seconds, lo), hi))
+
+
+def cpu_calibration(O, threads):
+    """The port against the reference's own numbers: C1 (1000 rows, 4-byte
+    keys, 10 reads/txn, 1 thread, full-txn) and 1-thread BTree::Read + copy at 1M rows."""
+    t = O.OracleTree()
+    t.load_ycsb(0, 1000, 4, 0)
+    keys = np.random.default_rng(1).integers(0, 1000, 1_000_000).astype(np.uint64)
+    sec, com, ab, _ = t.ycsb_txn_timed(keys, 4, 10, 1)
+    c1 = keys.size / sec
+    del t
+    t = O.OracleTree()
+    t.load_ycsb_parallel(0, 1_000_000, 4, 0, threads)
+    keys = np.random.default_rng(2).integers(0, 1_000_000, 1_000_000).astype(np.uint64)
+    s = ctypes.c_double()
+    O.lib().orc_read_batch_timed(t.t, keys.ctypes.data, 4, None, keys.size, 1, ctypes.byref(s))
+    ns = s.value / keys.size * 1e9
+    sec, _, _, _ = t.ycsb_txn_timed(keys, 4, 10, 1)
+    txn_ops = keys.size / sec
+    del t
+    return {"c1_full_txn_ops_s": round(c1, 1), "c1_aborts": ab, "c1_vs_reference_1533428": round(c1 / REF_C1_OPS, 3),
+            "read_ns_1m_1thread": round(ns, 1), "read_vs_reference_1786ns": round(REF_READ_NS_1M / ns, 3),
+            "txn_ops_s_1m_1thread": round(txn_ops, 1), "txn_vs_reference_428817": round(txn_ops / REF_TXN_OPS_1M, 3),
+            "note": "reference numbers were measured on the survey container (8-core Xeon); ratios > 1 = the port "
+                    "is faster on this host; BASELINE.md §3 has the same-host ratios"}
+
+
+def cpu_legs(orc, args, res, threads, c2_check=None, c4_check=None, c3=None):
+    """Times the oracle on the GPU box's host cores: C2 lookup mode + full-txn mode, C4 scans,
+    C3 reads on the replayed epochs' snapshot with the GPU's read ids; checks GPU samples
+    against it (the oracle is the checker).  Returns {leg: cpu_baseline dict}."""
+    O = orc.O
+    tree = orc.wait()
+    n = orc.rows
+    L = O.lib()
+    secs = ctypes.c_double()
     out = {}
-    wi = np.stack(np.meshgrid(np.arange(1, W + 1), np.arange(1, I + 1), indexing="ij"), -1).reshape(-1, 2)
-    sk = np.ascontiguousarray(wi.astype(np.int64)).view(np.uint8).reshape(-1, 16)
-    sp = rng.integers(0, 256, (sk.shape[0], 400), dtype=np.uint8)
-    sp[:, :4] = rng.integers(10, 101, sk.shape[0]).astype(np.int32).view(np.uint8).reshape(-1, 4)
-    out["stock"] = (sk, sp)
-    wd = np.stack(np.meshgrid(np.arange(1, W + 1), np.arange(1, D + 1), indexing="ij"), -1).reshape(-1, 2)
-    dk = np.ascontiguousarray(wd.astype(np.int64)).view(np.uint8).reshape(-1, 16)
-    dp = rng.integers(0, 256, (dk.shape[0], 143), dtype=np.uint8)
-    dp[:, :4] = np.full(dk.shape[0], O + 1, np.int32).view(np.uint8).reshape(-1, 4)
-    out["district"] = (dk, dp)
-    wdo = np.stack(np.meshgrid(np.arange(1, W + 1), np.arange(1, D + 1), np.arange(1, O + 1), indexing="ij"),
-                   -1).reshape(-1, 3)
-    nl = rng.integers(5, 16, wdo.shape[0])
-    rep = np.repeat(wdo, nl, axis=0)
-    ln = np.arange(rep.shape[0]) - np.repeat(np.cumsum(nl) - nl, nl) + 1
-    ok = np.ascontiguousarray(np.concatenate([rep, ln[:, None]], 1).astype(np.int64)).view(np.uint8).reshape(-1, 32)
-    op = rng.integers(0, 256, (ok.shape[0], 60), dtype=np.uint8)
-    op[:, :4] = rng.integers(1, I + 1, ok.shape[0]).astype(np.int32).view(np.uint8).reshape(-1, 4)
-    out["order_line"] = (ok, op)
+    host = {k: v for k, v in res.items() if not k.startswith("_")}
+    common = {"cores": threads, "threads": threads, "kind": "port", "rows": n, "host": host,
+              "build_s": round(orc.build_s, 1)}
+    # C2, lookup mode
+    keys = stage.zipf_draws(n - 1, 0.9, args.seed, 400_000, nthreads=threads)
+    L.orc_read_batch_timed(tree.t, keys.ctypes.data, 8, None, keys.size, threads, ctypes.byref(secs))
+    count = cpu_sample_count(keys.size / max(secs.value, 1e-9), args.cpu_seconds, 100_000, 400_000_000)
+    keys = stage.zipf_draws(n - 1, 0.9, args.seed + 1, count, nthreads=threads)
+    L.orc_read_batch_timed(tree.t, keys.ctypes.data, 8, None, keys.size, threads, ctypes.byref(secs))
+    c2 = {"value": round(count / secs.value, 1), "unit": "ops/s", "mode": "lookup", **common,
+          "sample": f"oracle BTree::Read + executor copy, {count} zipf-0.9 lookups over {n} rows (8-B keys, "
+                    f"1000-B payload), {threads} threads on {res['cpu_model']}, {secs.value:.1f}s"}
+    # C2, full-txn mode (RunMixed read-only transactions of 10 reads, Index-SSN read side)
+    keys = stage.zipf_draws(n - 1, 0.9, args.seed + 2, 400_000, nthreads=threads)
+    sec, com, ab, _ = tree.ycsb_txn_timed(keys, 8, 10, threads)
+    count = cpu_sample_count(keys.size / max(sec, 1e-9), args.cpu_seconds * 0.6, 100_000, 200_000_000) // 10 * 10
+    keys = stage.zipf_draws(n - 1, 0.9, args.seed + 3, count, nthreads=threads)
+    sec, com, ab, _ = tree.ycsb_txn_timed(keys, 8, 10, threads)
+    c2["full_txn"] = {"value": round(count / sec, 1), "unit": "ops/s", "commits": com, "aborts": ab,
+                      "sample": f"{count // 10} read-only RunMixed txns x 10 reads (PerformRead rw-set, "
+                                f"CommitTransaction FindMinSstamp/FindMaxPstamp, active_tids), {sec:.1f}s"}
+    if c2_check is not None:
+        ck, st, rows = c2_check
+        sel = ck < n
+        o_out, o_rec = tree.read_batch(ck[sel], 8, nthreads=threads)
+        c2["gpu_check"] = {"compared": int(sel.sum()),
+                           "equal": bool((o_out["status"] == st[sel]).all() and
+                                         (rows[sel][:, :tree.row] == o_rec).all())}
+    out["c2"] = c2
+    # C4, scan mode (TableScanExecutor over RangeScanBySize/Iterator)
+    starts = (stage.fastrandom(args.seed, 20_000) % np.uint64(n)).astype(np.uint64)
+    L.orc_scan_batch_timed(tree.t, starts.ctypes.data, 8, starts.size, args.scan_size, threads, ctypes.byref(secs))
+    count = cpu_sample_count(starts.size / max(secs.value, 1e-9), args.cpu_seconds * 0.6, 10_000, 5_000_000)
+    starts = (stage.fastrandom(args.seed + 1, count) % np.uint64(n)).astype(np.uint64)
+    L.orc_scan_batch_timed(tree.t, starts.ctypes.data, 8, starts.size, args.scan_size, threads, ctypes.byref(secs))
+    c4 = {"value": round(count / secs.value, 1), "unit": "scans/s", "mode": "scan", **common,
+          "sample": f"oracle TableScanExecutor over Iterator, {count} scans of {args.scan_size} over {n} rows, "
+                    f"{threads} threads, {secs.value:.1f}s"}
+    if c4_check is not None:
+        ck, cnt, recs = c4_check
+        sel = np.nonzero(ck < n)[0][:256]
+        oc, orows = tree.scan_batch(ck[sel], 8, args.scan_size, nthreads=threads)
+        # scans near the top of a smaller CPU table stop earlier: compare the common prefix
+        eq = all((orows[i, :min(oc[i], cnt[j]), :tree.row] == recs[j, :min(oc[i], cnt[j]), :tree.row]).all()
+                 for i, j in enumerate(sel))
+        c4["gpu_check"] = {"compared": int(sel.size), "equal": bool(eq)}
+    out["c4"] = c4
+    # C3: replay the GPU's epochs on the oracle, then the last epoch's reads with its read ids
+    if c3 is not None:
+        t0 = time.time()
+        applied = 0
+        for ep in c3["record"]:
+            sel = ep["keys"] < n
+            deltas = np.repeat(ep["colb"][sel][:, None], 100, 1)
+            _, ok = tree.update_batch(ep["keys"][sel], 8, 0, deltas, ep["rid"][sel], ep["cid"][sel])
+            applied += ok
+        replay_s = time.time() - t0
+        reads, rids = c3["reads"], c3["rids"]
+        sel = reads < n
+        reads, rids = np.ascontiguousarray(reads[sel]), np.ascontiguousarray(rids[sel])
+        L.orc_read_batch_timed(tree.t, reads.ctypes.data, 8, rids.ctypes.data, reads.size, threads,
+                               ctypes.byref(secs))
+        c3o = {"value": round(reads.size / secs.value, 1), "unit": "ops/s", "mode": "lookup at read ids", **common,
+               "updates_replayed": applied, "replay_s_untimed": round(replay_s, 1),
+               "sample": f"oracle BTree::Read + visibility (latest / copy / TupleHeader chain) + copy, the GPU's "
+                         f"last-epoch reads and read ids ({reads.size}) on the same snapshot ({len(c3['record'])} "
+                         f"epochs replayed), {threads} threads, {secs.value:.1f}s"}
+        if c3.get("check") is not None:
+            ck_keys, ck_rids, st, rows = c3["check"]
+            s2 = ck_keys < n
+            o_out, o_rec = tree.read_batch(ck_keys[s2], 8, ck_rids[s2], nthreads=threads)
+            c3o["gpu_check"] = {"compared": int(s2.sum()), "snapshot_equal_rows": bool(n == args.rows),
+                                "equal": bool((o_out["status"] == st[s2]).all() and
+                                              (rows[s2][:, :tree.row] == o_rec).all())}
+        out["c3"] = c3o
     return out
 
 
@@ -367,7 +645,7 @@ def run_tpcc(args):
             o.load_rows(k, p)
             orcs[name] = o
         build = time.time() - t1
-        threads = min(16, os.cpu_count() or 8)
+        threads = args.cpu_threads or cpu_resources()["threads"]
         n0 = 20_000
         r0, sec = O.stock_level_batch(orcs["district"], orcs["order_line"], orcs["stock"], w[:n0], d[:n0], thr[:n0],
                                       None, threads)
@@ -414,10 +692,13 @@ def run_chq2(args):
     nq = args.q2_batch
     rids = (0xFFFFFFFE - np.arange(nq)).astype(np.uint32)  # nq transactions per step, one read id each
 
+    state = {}
+
     def step():
         if nq == 1:
             return ch.query2(3)
         recs_q, ab_q = ch.query2_batch(rids, 3)
+        state["all"] = (recs_q, ab_q)
         return recs_q[0], bool(ab_q.any())
 
     for _ in range(args.warmup):
@@ -428,6 +709,24 @@ def run_chq2(args):
         recs, ab = step()
     elapsed = time.perf_counter() - t0
     ms = elapsed / args.steps * 1e3
+    same = True
+    if nq > 1:  # every query of the batch must read what query 0 read (the visited suppliers and
+        # the kept stocks do not depend on the read id on an update-free table)
+        recs_q, ab_q = state["all"]
+        same = bool(all((recs_q[q] == recs_q[0]).all() for q in range(nq)) and (ab_q == ab_q[0]).all())
+    # the single-transaction commit path (stage_ch_query2 with a commit id: the marked STOCK
+    # updates go through stage_update_batch_device), after the read-only batch
+    commit = None
+    if nq > 1:
+        n1 = max(3, args.steps // 2)
+        t1 = time.perf_counter()
+        for i in range(n1):
+            rid = 0x7FFF0000 + 2 * i
+            r1, a1 = ch.query2(3, read_id=rid, commit_id=rid + 1)
+        dt = time.perf_counter() - t1
+        commit = {"value": round(n1 / dt, 2), "unit": "q2/s", "txns": n1, "ms_per_txn": round(dt / n1 * 1e3, 4),
+                  "updates_last": int(r1["update"].sum()), "aborted_last": bool(a1),
+                  "what": "one Q2 per call with its STOCK updates committed (RunQuery2 incl. the write)"}
     nsupp = int(recs.size)
     nstock = int(sum(int(ch.map_off[k + 1] - ch.map_off[k]) for k in recs["supp_key"]))
     # algorithmic bytes per Q2: each STOCK / ITEM point lookup reads its key, the 64-B fingerprint
@@ -436,17 +735,17 @@ def run_chq2(args):
     per_q2 = nstock * (16 + 64 + 32 + 32) + nsupp * (8 + 64 + 32 + 32 + 64 + 64) + \
         10000 * (8 + 111 + 128) + 62 * (8 + 185 + 192) + 5 * (8 + 207 + 224)
     achieved = per_q2 * nq / (ms * 1e-3) / 1e9
-    cpu, ok = None, not ab
+    cpu, ok = None, not ab and same
     if not args.no_cpu_baseline:
         import ctypes
 
         import oracle_lib as O
         orecs, oab = ch.query2_oracle(3)
         a, b = np.sort(recs, order="supp_key"), np.sort(orecs, order="supp_key")
-        ok = ok and oab == ab and a.size == b.size and all((a[f] == b[f]).all() for f in
+        ok = ok and same and oab == ab and a.size == b.size and all((a[f] == b[f]).all() for f in
                                                             ("supp_key", "s_w_id", "s_i_id", "s_quantity",
                                                              "item_has_b", "update"))
-        threads = min(16, os.cpu_count() or 8)
+        threads = args.cpu_threads or cpu_resources()["threads"]
         o = ch.orc
         sec = ctypes.c_double()
         args_ = (o["region"].t, o["nation"].t, o["supplier"].t, o["item"].t, o["stock"].t, ch.map_off.ctypes.data,
@@ -458,7 +757,9 @@ def run_chq2(args):
                "sample": f"oracle orc_ch_query2 (RunQuery2 restated), {count} read-only Q2s, same tables, "
                          f"{threads} threads on {cpu_name()}, {sec.value:.1f}s"}
     result = {
-        "metric": "CH-benCHmark Q2 txns/s through the index-organized path (supplementary to " + METRIC + ")",
+        "metric": ("CH-benCHmark Q2 txns/s, read-only batched (" + str(nq) + " Q2s per pass, no STOCK updates), "
+                   if nq > 1 else "CH-benCHmark Q2 txns/s (with its updates), ") +
+                  "through the index-organized path (supplementary to " + METRIC + ")",
         "value": round(args.steps * nq / elapsed, 2), "unit": "q2/s", "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "int64 keys / bytes", "data": "synthetic CH rows (tpcc_record.h layouts, "
@@ -466,7 +767,9 @@ def run_chq2(args):
         "config": {"workload": "CH-benCHmark Q2 (tpcc_new_order.cpp RunQuery2), region EUROPE",
                    "warehouses": args.warehouses, "items": args.items, "q2_per_step": nq,
                    "suppliers_visited": nsupp,
-                   "stock_lookups": nstock, "aborted": bool(ab), "updates": int(recs["update"].sum())},
+                   "stock_lookups": nstock, "aborted": bool(ab), "updates": int(recs["update"].sum()),
+                   "read_only_batch": nq > 1, "queries_equal_query0": same},
+        "single_q2_commit_path": commit,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                      "kernel": "Q2 step (3 scans + batched STOCK / ITEM probes of q2_per_step transactions)",
@@ -478,27 +781,145 @@ def run_chq2(args):
     return 0 if ok else 1
 
 
-def main():
-    args = parse()
+def c4_leg(tab, args, total_rows, rank, stream, steps, warmup):
+    """configs[3]: B uniform start keys, L-key range scans (stage_scan_batch); returns the leg's
+    measured dict and a sample for the oracle check."""
+    L = stage.lib()
+    B = args.scan_batch if args.config == "c2" else args.batch
+    starts = (stage.fastrandom(args.seed + rank, B) % np.uint64(total_rows)).astype(np.uint64)
+    d_keys = stage.DeviceBuffer.from_numpy(starts)
+    d_cnt = stage.DeviceBuffer(B * 4)
+    d_rec = stage.DeviceBuffer(B * args.scan_size * tab.stride)
+
+    def step():
+        check(L.stage_scan_batch(tab.h, d_keys.ptr, None, B, args.scan_size, d_cnt.ptr, d_rec.ptr, stream.ptr), "scan")
+
+    for _ in range(warmup):
+        step()
+    stream.sync()
+    evs = [stage.Event() for _ in range(2 * steps)]
+    t0 = time.perf_counter()
+    for i in range(steps):
+        evs[2 * i].record(stream)
+        step()
+        evs[2 * i + 1].record(stream)
+    stream.sync()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([evs[2 * i].elapsed_ms(evs[2 * i + 1]) for i in range(steps)]))
+    cnt = d_cnt.to_numpy(np.uint32, B)
+    ok = bool((cnt > 0).all() and (cnt == args.scan_size).mean() > 0.99)
+    ns = min(B, 256)
+    recs = d_rec.to_numpy(np.uint8, ns * args.scan_size * tab.stride).reshape(ns, args.scan_size, tab.stride)
+    traffic, tsrc = traffic_from_profile(B, args.rows, "pmc_scan.json")
+    d = {"value": round(B * steps / elapsed, 1), "unit": "scans/s", "steps": steps, "warmup": warmup,
+         "ms_per_step": round(elapsed / steps * 1e3, 4), "self_check": ok,
+         "config": {"workload": WORKLOADS["c4"], "scans_per_step": B, "scan_size": args.scan_size,
+                    "starts": "uniform over [0, N)"},
+         "roofline": hbm_roofline(scan_bytes(args.scan_size), B, kern_ms, "scan_kernel", traffic, tsrc)}
+    for b in (d_keys, d_cnt, d_rec):
+        b.free()
+    return d, (starts[:ns], cnt[:ns], recs)
+
+
+def c3_leg(tab, args, stream, nthreads, steps, warmup):
+    """configs[2]: YCSB-B epochs; each timed step applies one epoch's write share on the write
+    path (timed apart) and probes its read share at the epoch's read ids (timed)."""
+    L = stage.lib()
+    B = args.batch
+    theta = args.theta if args.config == "c3" else 0.99
+    ycsb_b = YcsbB(tab, args, nthreads, theta)
+    d_keys, d_rid = stage.DeviceBuffer(B * 8), stage.DeviceBuffer(B * 4)
+    d_out, d_rec = stage.DeviceBuffer(B * 32), stage.DeviceBuffer(B * tab.stride)
+    # the first `warmup` epochs are untimed (first-call allocations of the write path)
+    for _ in range(max(1, warmup)):
+        draws, rids = ycsb_b.next_batch()
+    ycsb_b.reset_counters()
+    evs = [stage.Event() for _ in range(2 * steps)]
+    elapsed, ops_done, hops = 0.0, 0, 0
+    hist = np.zeros(6, np.int64)
+    for i in range(steps):
+        draws, rids = ycsb_b.next_batch()
+        n_ops = draws.size
+        check(L.stage_memcpy_h2d(d_keys.ptr, draws.ctypes.data, draws.nbytes, None), "h2d")
+        check(L.stage_memcpy_h2d(d_rid.ptr, rids.ctypes.data, rids.nbytes, None), "h2d")
+        check(L.stage_device_sync(), "sync")
+        t0 = time.perf_counter()
+        evs[2 * i].record(stream)
+        tab.probe_device(d_keys.ptr, n_ops, d_out.ptr, d_rec.ptr, d_read_ids=d_rid.ptr, stream=stream.ptr)
+        evs[2 * i + 1].record(stream)
+        stream.sync()
+        elapsed += time.perf_counter() - t0
+        ops_done += n_ops
+        o = d_out.to_numpy(stage.PROBE_OUT_DTYPE, n_ops)
+        hist += np.bincount(o["status"], minlength=6)[:6]
+        hops += int(o["hops"].astype(np.int64).sum())
+    kern_ms = float(np.mean([evs[2 * i].elapsed_ms(evs[2 * i + 1]) for i in range(steps)]))
+    mean_hops = hops / max(ops_done, 1)
+    ns = min(draws.size, 4096)
+    rows = d_rec.to_numpy(np.uint8, ns * tab.stride).reshape(ns, tab.stride)
+    check_sample = (draws[:ns].copy(), rids[:ns].copy(), o["status"][:ns].copy(), rows)
+    ok = bool(hist[stage.ST_LATEST] > 0 and hist[stage.ST_OLD] > 0)
+    per_unit = BYTES_PER_LOOKUP + HOP_BYTES * mean_hops
+    d = {"value": round(ops_done / elapsed, 1), "unit": "ops/s", "steps": steps, "warmup": max(1, warmup),
+         "ms_per_step": round(elapsed / steps * 1e3, 4), "self_check": ok,
+         "ops_per_s_incl_writes": round((ops_done + ycsb_b.updates) / (elapsed + ycsb_b.write_s), 1),
+         "config": {"workload": WORKLOADS["c3"], "theta": theta, "update_ratio": args.update_ratio,
+                    "inflight_share": args.inflight_share, "updates_applied": ycsb_b.updates,
+                    "updates_in_flight": int(sum(e["inflight"] for e in ycsb_b.record)),
+                    "write_path": args.write_path, "write_s": round(ycsb_b.write_s, 3),
+                    "publish_s": round(ycsb_b.sync_s, 3), "epoch_prep_s_untimed": round(ycsb_b.prep_s, 2),
+                    "last_publish": ycsb_b.last_sync, "mean_chain_hops": round(mean_hops, 4),
+                    "read_status_counts": {"latest": int(hist[1]), "copy": int(hist[2]), "old": int(hist[3]),
+                                           "fail": int(hist[4]), "chain_miss": int(hist[5]),
+                                           "not_found": int(hist[0])},
+                    "timed": "device probe of the read share (value); ops_per_s_incl_writes adds the epoch's write "
+                             "path (update share over PCIe + stage_update_batch_device)"},
+         "roofline": hbm_roofline(per_unit, ops_done / steps, kern_ms, "probe_kernel (read ids, chain walks)")}
+    d["roofline"]["algorithmic_bytes"] = f"{BYTES_PER_LOOKUP} + {HOP_BYTES} x mean hops ({mean_hops:.4f})"
+    rec = {"record": ycsb_b.record, "reads": draws, "rids": rids, "check": check_sample}
+    for b in (d_keys, d_rid, d_out, d_rec):
+        b.free()
+    return d, rec
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    in_dist = "WORLD_SIZE" in os.environ
+    if args.gpus > 1 and not in_dist:
+        return launch_ranks(args, argv)
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    if in_dist and world != args.gpus:
+        log(f"[rank {rank}] WORLD_SIZE={world} but --gpus {args.gpus}: refusing to report a mislabelled point")
+        return 2
     if args.config == "tpcc":
         return run_tpcc(args)
     if args.config == "chq2":
         return run_chq2(args)
-    rank = int(os.environ.get("RANK", 0))
-    world = int(os.environ.get("WORLD_SIZE", 1))
-    local = int(os.environ.get("LOCAL_RANK", 0))
     dist = None
     sharded = world > 1 or args.force_sharded
-    if sharded:
+    if sharded or args.dry_run:
         import torch.distributed as tdist
         tdist.init_process_group("gloo")  # control plane only; the data path is RCCL in the library
         dist = tdist
         if args.config != "c2":
             raise SystemExit("multi-GPU runs use the point-lookup config (c2 -> configs[4])")
-    nthreads = min(16, os.cpu_count() or 8)
+    if args.dry_run:
+        try:
+            return dry_run(args, rank, world, dist)
+        finally:
+            dist.destroy_process_group()
+    res = cpu_resources()
+    nthreads = args.cpu_threads or res["threads"]
     check(stage.lib().stage_set_device(local), "set device")
 
     total_rows = args.rows * world
+    orc = None
+    cpu_leg = rank == 0 and not sharded and not args.no_cpu_baseline
+    if cpu_leg:  # the oracle table builds on the host while the GPU leg runs
+        orc = CpuOracle(cpu_rows_for(args, res, args.rows), nthreads)
     t0 = time.time()
     tab = stage.Table(key_width=8, device=local)
     if not sharded:
@@ -517,67 +938,46 @@ def main():
     B = args.batch
     L = stage.lib()
     stream = stage.Stream()
-    ycsb_b = None
+    extras, samples = {}, {}
     if args.config == "c4":
-        starts = (stage.fastrandom(args.seed + rank, B) % np.uint64(total_rows)).astype(np.uint64)
-        d_keys = stage.DeviceBuffer.from_numpy(starts)
-        d_cnt = stage.DeviceBuffer(B * 4)
-        d_rec = stage.DeviceBuffer(B * args.scan_size * tab.stride)
-        draws = starts
+        head, samples["c4"] = c4_leg(tab, args, total_rows, rank, stream, args.steps, args.warmup)
+    elif args.config == "c3":
+        head, samples["c3"] = c3_leg(tab, args, stream, nthreads, args.steps, args.warmup)
     else:
-        if args.config == "c3":
-            ycsb_b = YcsbB(tab, args, nthreads)
-            # epoch 0 is the warm-up (first-call allocations of the write path), untimed; every
-            # timed step applies one more epoch
-            draws, rids = ycsb_b.next_batch()
-            ycsb_b.updates, ycsb_b.write_s, ycsb_b.sync_s = 0, 0.0, 0.0
-            n_ops = draws.size
-        else:
-            draws = stage.zipf_draws(total_rows - 1, args.theta, args.seed + rank, B, nthreads=nthreads)
-            rids = None
-            n_ops = B
+        head = None
+    owner = None
+    if head is None:  # C2 (or C5 when sharded): the headline
+        draws = stage.zipf_draws(total_rows - 1, args.theta, args.seed + rank, B, nthreads=nthreads)
         d_keys = stage.DeviceBuffer(B * 8)
         check(L.stage_memcpy_h2d(d_keys.ptr, draws.ctypes.data, draws.nbytes, None), "h2d")
-        d_rid = None
-        if rids is not None:  # YCSB-B: the read share varies per epoch, buffers hold a whole batch
-            d_rid = stage.DeviceBuffer(B * 4)
-            check(L.stage_memcpy_h2d(d_rid.ptr, rids.ctypes.data, rids.nbytes, None), "h2d")
         d_out = stage.DeviceBuffer(B * 32)
         d_rec = stage.DeviceBuffer(B * tab.stride)
-    d_leaf = None
-    if args.host_traversal and world == 1 and args.config == "c2":
-        d_leaf = stage.DeviceBuffer.from_numpy(tab.traverse(draws))
+        d_leaf = None
+        if args.host_traversal and not sharded:
+            d_leaf = stage.DeviceBuffer.from_numpy(tab.traverse(draws))
+        if sharded:
+            uid = (ctypes.c_uint8 * 128)()
+            if rank == 0:
+                check(L.stage_comm_unique_id(uid), "unique id")
+            obj = [bytes(uid)]
+            dist.broadcast_object_list(obj, src=0)
+            uid = (ctypes.c_uint8 * 128).from_buffer_copy(obj[0])
+            check(L.stage_comm_init(tab.h, uid, rank, world), "comm init")
 
-    if sharded:
-        uid = (ctypes.c_uint8 * 128)()
-        if rank == 0:
-            check(L.stage_comm_unique_id(uid), "unique id")
-        obj = [bytes(uid)]
-        dist.broadcast_object_list(obj, src=0)
-        uid = (ctypes.c_uint8 * 128).from_buffer_copy(obj[0])
-        check(L.stage_comm_init(tab.h, uid, rank, world), "comm init")
+        def step():
+            if not sharded:
+                tab.probe_device(d_keys.ptr, B, d_out.ptr, d_rec.ptr,
+                                 d_leaf_ids=d_leaf.ptr if d_leaf else None, stream=stream.ptr)
+            else:
+                check(L.stage_probe_sharded(tab.h, d_keys.ptr, None, B, d_out.ptr, d_rec.ptr, stream.ptr), "sharded")
 
-    def step():
-        if args.config == "c4":
-            check(L.stage_scan_batch(tab.h, d_keys.ptr, None, B, args.scan_size, d_cnt.ptr, d_rec.ptr, stream.ptr),
-                  "scan")
-        elif not sharded:
-            tab.probe_device(d_keys.ptr, n_ops, d_out.ptr, d_rec.ptr, d_read_ids=d_rid.ptr if d_rid else None,
-                             d_leaf_ids=d_leaf.ptr if d_leaf else None, stream=stream.ptr)
-        else:
-            check(L.stage_probe_sharded(tab.h, d_keys.ptr, None, B, d_out.ptr, d_rec.ptr, stream.ptr), "sharded")
-
-    for _ in range(args.warmup):
-        step()
-    stream.sync()
-    if dist:
-        dist.barrier()
-    check(L.stage_device_sync(), "sync")
-    evs = [stage.Event() for _ in range(2 * args.steps)]
-    elapsed = 0.0
-    status_hist = np.zeros(6, np.int64)
-    ops_done = 0
-    if ycsb_b is None:
+        for _ in range(args.warmup):
+            step()
+        stream.sync()
+        if dist:
+            dist.barrier()
+        check(L.stage_device_sync(), "sync")
+        evs = [stage.Event() for _ in range(2 * args.steps)]
         t0 = time.perf_counter()
         for i in range(args.steps):
             evs[2 * i].record(stream)
@@ -586,135 +986,92 @@ def main():
         stream.sync()
         check(L.stage_device_sync(), "sync")
         elapsed = time.perf_counter() - t0
-        ops_done = B * args.steps
-    else:
-        # each step: one epoch's write share on the write path (timed apart, in write_s) ->
-        # timed device probe of its read share
-        for i in range(args.steps):
-            draws, rids = ycsb_b.next_batch()
-            n_ops = draws.size
-            check(L.stage_memcpy_h2d(d_keys.ptr, draws.ctypes.data, draws.nbytes, None), "h2d")
-            check(L.stage_memcpy_h2d(d_rid.ptr, rids.ctypes.data, rids.nbytes, None), "h2d")
-            check(L.stage_device_sync(), "sync")
-            t0 = time.perf_counter()
-            evs[2 * i].record(stream)
-            step()
-            evs[2 * i + 1].record(stream)
+        if dist:
+            dist.barrier()
+            import torch
+            tt = torch.tensor([elapsed], dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            elapsed = float(tt.item())
+            # the same steps with STAGE_REPLY_OWNER: rows stay in the owner's HBM, only the 32-B
+            # status records return -- the HBM-side scaling without the xGMI tuple return
+            for _ in range(max(1, args.warmup)):
+                check(L.stage_probe_sharded_ex(tab.h, d_keys.ptr, None, B, d_out.ptr, None, stage.REPLY_OWNER,
+                                               stream.ptr), "sharded owner")
             stream.sync()
-            elapsed += time.perf_counter() - t0
-            ops_done += n_ops
-            o = d_out.to_numpy(stage.PROBE_OUT_DTYPE, n_ops)
-            status_hist += np.bincount(o["status"], minlength=6)[:6]
-    owner = None
-    if dist:
-        dist.barrier()
-        import torch
-        tt = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-        # the same steps with STAGE_REPLY_OWNER: rows stay in the owner's HBM, only the 32-B
-        # status records return -- the HBM-side scaling without the xGMI tuple return
-        for _ in range(max(1, args.warmup)):
-            check(L.stage_probe_sharded_ex(tab.h, d_keys.ptr, None, B, d_out.ptr, None, stage.REPLY_OWNER, stream.ptr),
-                  "sharded owner")
-        stream.sync()
-        dist.barrier()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            check(L.stage_probe_sharded_ex(tab.h, d_keys.ptr, None, B, d_out.ptr, None, stage.REPLY_OWNER, stream.ptr),
-                  "sharded owner")
-        stream.sync()
-        t_own = time.perf_counter() - t0
-        tt = torch.tensor([t_own], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_own = float(tt.item())
-        owner = {"value": round(B * args.steps * world / t_own, 1), "ms_per_step": round(t_own / args.steps * 1e3, 4),
-                 "reply": "32-B status records to the caller, tuple rows materialised on the owner"}
-    step_ms = [evs[2 * i].elapsed_ms(evs[2 * i + 1]) for i in range(args.steps)]
-    kern_ms = float(np.mean(step_ms))
-
-    # self-check outside the timed region
-    ok = True
-    if args.config == "c4":
-        cnt = d_cnt.to_numpy(np.uint32, B)
-        ok = bool((cnt > 0).all() and (cnt == args.scan_size).mean() > 0.99)
-    elif args.config == "c2":
+            dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                check(L.stage_probe_sharded_ex(tab.h, d_keys.ptr, None, B, d_out.ptr, None, stage.REPLY_OWNER,
+                                               stream.ptr), "sharded owner")
+            stream.sync()
+            t_own = time.perf_counter() - t0
+            tt = torch.tensor([t_own], dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            t_own = float(tt.item())
+            owner = {"value": round(B * args.steps * world / t_own, 1),
+                     "ms_per_step": round(t_own / args.steps * 1e3, 4),
+                     "reply": "32-B status records to the caller, tuple rows materialised on the owner"}
+            # rerun the full-reply step once so the self-check reads full rows
+            step()
+            stream.sync()
+        kern_ms = float(np.mean([evs[2 * i].elapsed_ms(evs[2 * i + 1]) for i in range(args.steps)]))
         sample = min(B, 65536)
         outs = d_out.to_numpy(stage.PROBE_OUT_DTYPE, sample)
         rows = d_rec.to_numpy(np.uint8, sample * tab.stride).reshape(sample, tab.stride)
         ok = bool((outs["status"] == stage.ST_LATEST).all() and
                   (rows[:, :8].copy().view(np.uint64).ravel() == draws[:sample]).all() and
                   (rows[:, 8:1008] == (draws[:sample] & np.uint64(0xFF)).astype(np.uint8)[:, None]).all())
-    else:
-        ok = bool(status_hist[stage.ST_LATEST] > 0 and status_hist[stage.ST_OLD] > 0)
-    if not ok:
-        log(f"[rank {rank}] SELF-CHECK FAILED")
-
-    total = ops_done * world
-    value = total / elapsed
-    if rank == 0:
-        if args.config == "c4":
-            per_unit = scan_bytes(args.scan_size)
-            unit = "scans/s"
-            kernel = "scan_kernel"
-        else:
-            per_unit = BYTES_PER_LOOKUP
-            unit = "ops/s"
-            kernel = "probe_kernel" if not sharded else "sharded step (route + RCCL + probe_kernel)"
-        units_per_launch = ops_done / args.steps
-        achieved = per_unit * units_per_launch / (kern_ms * 1e-3) / 1e9
-        traffic, tsrc = None, None
-        if not sharded and args.config in ("c2", "c4"):
-            traffic, tsrc = traffic_from_profile(B, args.rows, "pmc_probe.json" if args.config == "c2" else
-                                                 "pmc_scan.json")
-        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kernel,
-                "algorithmic_bytes_per_unit": per_unit, "units_per_launch": units_per_launch,
-                "algorithmic_bytes_per_launch": round(per_unit * units_per_launch),
-                "avg_launch_ms": round(kern_ms, 4)}
-        if tsrc:
-            roof["traffic_source"] = tsrc
+        samples["c2"] = (draws[:4096].copy(), outs["status"][:4096].copy(), rows[:4096].copy())
+        traffic, tsrc = (None, None) if sharded else traffic_from_profile(B, args.rows, "pmc_probe.json")
+        roof = hbm_roofline(BYTES_PER_LOOKUP, B, kern_ms,
+                            "probe_kernel" if not sharded else "sharded step (route + RCCL + probe_kernel)",
+                            traffic, tsrc)
         if sharded and world > 1:
             roof = xgmi_roofline(B, world, tab.stride, elapsed / args.steps, roof)
+        head = {"value": round(B * args.steps * world / elapsed, 1), "unit": "ops/s",
+                "ms_per_step": round(elapsed / args.steps * 1e3, 4), "self_check": ok, "roofline": roof,
+                "config": {"workload": WORKLOADS["c2"] if not sharded else WORKLOADS["c5"], "theta": args.theta,
+                           "traversal": "host" if d_leaf else "device"}}
+        for b in (d_keys, d_out, d_rec) + ((d_leaf,) if d_leaf else ()):
+            b.free()
+        if not sharded and not args.no_extras:
+            # the other single-GPU configs on the same loaded table: C4, then C3 (mutates it)
+            extras["c4"], samples["c4"] = c4_leg(tab, args, total_rows, rank, stream, 5, 1)
+            extras["c3"], samples["c3"] = c3_leg(tab, args, stream, nthreads, args.c3_epochs, 1)
+    if not head["self_check"]:
+        log(f"[rank {rank}] SELF-CHECK FAILED")
+
+    if rank == 0:
         cpu = None
-        if not sharded and not args.no_cpu_baseline:
-            cpu = cpu_baseline(args, nthreads)
-        wl = WORKLOADS[args.config] if not sharded else WORKLOADS["c5"]
-        config = {"workload": wl, "rows_per_gpu": args.rows, "rows_total": total_rows, "batch_per_gpu": B,
-                  "key_bytes": 8, "payload_bytes": 1000, "leaf_bytes": 65536,
-                  "parallelism": f"hash-shard x{world}", "traversal": "host" if d_leaf else "device"}
-        if args.config == "c4":
-            config.update({"scan_size": args.scan_size, "starts": "uniform over [0, N)"})
-        else:
-            config["theta"] = args.theta
-        if ycsb_b is not None:
-            config.update({"update_ratio": args.update_ratio, "updates_applied": ycsb_b.updates,
-                           "write_path": args.write_path,
-                           "write_s": round(ycsb_b.write_s, 3), "publish_s": round(ycsb_b.sync_s, 3),
-                           "epoch_prep_s_untimed": round(ycsb_b.prep_s, 2),
-                           "last_publish": ycsb_b.last_sync,
-                           "ops_per_s_incl_writes": round((ops_done + ycsb_b.updates) /
-                                                               (elapsed + ycsb_b.write_s), 1),
-                           "read_status_counts": {"latest": int(status_hist[1]), "copy": int(status_hist[2]),
-                                                  "old": int(status_hist[3]), "fail": int(status_hist[4]),
-                                                  "chain_miss": int(status_hist[5]),
-                                                  "not_found": int(status_hist[0])},
-                           "timed": "device probe of the read share; the epoch's write path between steps excluded "
-                                    "(it is in ops_per_s_incl_writes: update share over PCIe + write path)"})
+        if cpu_leg:
+            legs = cpu_legs(orc, args, res, nthreads, c2_check=samples.get("c2"), c4_check=samples.get("c4"),
+                            c3=samples.get("c3"))
+            legs["c2"]["calibration"] = cpu_calibration(orc.O, nthreads)
+            key = args.config
+            cpu = legs[key]
+            for k, v in extras.items():
+                v["cpu_baseline"] = legs.get(k)
+        config = {**head["config"], "rows_per_gpu": args.rows, "rows_total": total_rows,
+                  "batch_per_gpu": B if args.config != "c4" else args.batch, "key_bytes": 8, "payload_bytes": 1000,
+                  "leaf_bytes": 65536, "parallelism": f"hash-shard x{world}"}
         result = {
-            "metric": METRIC, "value": round(value, 1), "unit": unit, "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "metric": METRIC, "value": head["value"], "unit": head["unit"], "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": head["ms_per_step"], "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic (LoadYCSBRows keys/payloads)",
-            "config": config, "roofline": roof, "cpu_baseline": cpu, "self_check": ok,
+            "config": config, "roofline": head["roofline"], "cpu_baseline": cpu, "self_check": head["self_check"],
+            **({"ops_per_s_incl_writes": head["ops_per_s_incl_writes"]} if "ops_per_s_incl_writes" in head else {}),
             **({"owner_reply": owner} if owner else {}),
+            **({"extras": extras} if extras else {}),
             "setup_s": {"load": round(t_load, 1), "sync": round(t_sync, 1)},
             "host_peak_rss_gib": round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20, 1),
         }
         print(json.dumps(result), flush=True)
     if dist:
         dist.barrier()
-        check(L.stage_comm_destroy(tab.h), "comm destroy")
+        if sharded:
+            check(L.stage_comm_destroy(tab.h), "comm destroy")
         dist.destroy_process_group()
+    ok = head["self_check"] and all(v["self_check"] for v in extras.values())
     return 0 if ok else 1
 
 

@@ -16,6 +16,7 @@
 #include "stage_oracle.h"
 
 #include <pthread.h>
+#include <sys/mman.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
@@ -81,6 +82,7 @@ typedef struct orc_copy { /* EphemeralPool::OverwriteVersionHeader, ephemeral_po
     uint16_t key_len;
     uint32_t payload_size;
     int live, waiting;
+    int wr_count; /* readers counted by IncreaseWRCount / DecreaseWRCount (ephemeral_pool.cpp:194-239) */
     uint8_t *image; /* [key(key_len)][payload] (b_tree.cpp:1143-1144) */
     struct orc_copy *reg_next;
 } orc_copy;
@@ -147,6 +149,7 @@ struct orc_tree {
     void **garbage; /* nodes replaced during the current Insert (released after install) */
     uint64_t ngarbage, capgarbage;
     uint64_t retired;
+    int bulk; /* orc_tree_set_bulk: a load of distinct keys, CheckUnique skipped */
 };
 
 typedef struct { orc_inner *node; uint32_t meta_index; } frame_t;
@@ -160,6 +163,66 @@ static void *xmalloc(size_t n) {
     void *p = malloc(n);
     if (!p) abort();
     return p;
+}
+
+/* leaf blocks come from a process-wide pool: leaves of one size carved from 1 GiB anonymous
+ * mappings, freed leaves kept on a free list and reused by the next split, a freed tree's
+ * leaves handed back to the kernel (MADV_DONTNEED).  malloc's heap fragments under the
+ * loader's split pattern (10M rows held 2x their live leaves); a 100M-row table would not fit
+ * the GPU box's per-command memory cap. */
+#define POOL_CHUNK (1ull << 30)
+typedef struct { uint32_t size; void *free_list; uint8_t *chunk; uint64_t left; } leaf_pool;
+static leaf_pool g_pools[4];
+static pthread_mutex_t g_pool_lock = PTHREAD_MUTEX_INITIALIZER;
+
+static leaf_pool *pool_of(uint32_t size) {
+    for (int i = 0; i < 4; i++) {
+        if (g_pools[i].size == size) return &g_pools[i];
+        if (g_pools[i].size == 0) {
+            g_pools[i].size = size;
+            return &g_pools[i];
+        }
+    }
+    return NULL;
+}
+
+static void *leaf_block_alloc(uint32_t size) {
+    pthread_mutex_lock(&g_pool_lock);
+    leaf_pool *p = pool_of(size);
+    void *b = NULL;
+    if (p && p->free_list) {
+        b = p->free_list;
+        p->free_list = *(void **)b;
+    } else if (p && size % 4096 == 0) {
+        if (p->left < size) {
+            void *c = mmap(NULL, POOL_CHUNK, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+            if (c == MAP_FAILED) abort();
+            p->chunk = c;
+            p->left = POOL_CHUNK;
+        }
+        b = p->chunk;
+        p->chunk += size;
+        p->left -= size;
+    }
+    pthread_mutex_unlock(&g_pool_lock);
+    if (!b) { /* sizes that are not page multiples: plain allocation */
+        b = aligned_alloc(64, size);
+        if (!b) abort();
+    }
+    return b;
+}
+
+static void leaf_block_free(uint32_t size, void *b, int release) {
+    if (size % 4096) {
+        free(b);
+        return;
+    }
+    if (release) madvise(b, size, MADV_DONTNEED);
+    pthread_mutex_lock(&g_pool_lock);
+    leaf_pool *p = pool_of(size);
+    *(void **)b = p->free_list;
+    p->free_list = b;
+    pthread_mutex_unlock(&g_pool_lock);
 }
 
 static void garbage_add(orc_tree *t, void *p) {
@@ -181,7 +244,7 @@ static void inner_free(orc_inner *n) {
 static void garbage_release(orc_tree *t) {
     for (uint64_t i = 0; i < t->ngarbage; i++) {
         void *p = t->garbage[i];
-        if (is_leaf(p)) free(p);
+        if (is_leaf(p)) leaf_block_free(t->leaf_node_size, p, 0);
         else inner_free((orc_inner *)p);
     }
     t->ngarbage = 0;
@@ -346,8 +409,7 @@ static orc_inner *inner_prepare_for_split(orc_tree *t, orc_inner *n, stack_t_ *s
 }
 
 static uint8_t *leaf_new(orc_tree *t) { /* LeafNode::New, b_tree.cpp:791-797 */
-    uint8_t *n = aligned_alloc(64, t->leaf_node_size);
-    if (!n) abort();
+    uint8_t *n = leaf_block_alloc(t->leaf_node_size);
     memset(n, 0, t->leaf_node_size);
     n[OFF_ISLEAF] = 1;
     *l_size(n) = t->leaf_node_size;
@@ -383,8 +445,9 @@ static int leaf_insert(orc_tree *t, uint8_t *n, const uint8_t *key, uint16_t ks,
                        uint32_t commit_id, orc_loc *loc, orc_rmeta **out) {
     uint64_t status = *l_status(n);
     if (st_frozen(status)) return ORC_RET_NODE_FROZEN;
-    /* CheckUnique, b_tree.cpp:1395-1417 */
-    int64_t hit = search_record_meta(n, key, ks, 1);
+    /* CheckUnique, b_tree.cpp:1395-1417 (a bulk load of distinct keys cannot hit:
+     * skipped, the resulting leaves are the same -- tests/test_oracle_golden.py) */
+    int64_t hit = t->bulk ? -1 : search_record_meta(n, key, ks, 1);
     if (hit >= 0) {
         uint64_t m = l_meta(n, (uint32_t)hit)->meta;
         if (m_inserting(m)) return ORC_RET_INVALID; /* ReCheck vs an in-flight update: unsupported */
@@ -468,8 +531,8 @@ static int leaf_prepare_for_split(orc_tree *t, uint8_t *n, stack_t_ *st, uint8_t
     qsort(v, nv, sizeof(sortrec_t), sortrec_cmp); /* Sorter::Sort (unique keys -> same order as std::sort) */
     if (total == 0) {
         free(v);
-        free(l);
-        free(r);
+        leaf_block_free(t->leaf_node_size, l, 0);
+        leaf_block_free(t->leaf_node_size, r, 0);
         return 0;
     }
     int32_t left_size = (int32_t)(total / 2);
@@ -556,20 +619,21 @@ orc_tree *orc_tree_new(uint32_t leaf_node_size, uint32_t split_threshold, uint32
 
 void orc_tree_set_merge_threshold(orc_tree *t, uint32_t merge_threshold) { t->merge_threshold = merge_threshold; }
 void orc_tree_set_key_pad(orc_tree *t, uint32_t key_pad) { t->key_pad = key_pad < 8 ? 8 : key_pad; }
+void orc_tree_set_bulk(orc_tree *t, int bulk) { t->bulk = bulk; }
 
-static void free_subtree(void *n) {
+static void free_subtree(orc_tree *t, void *n) {
     if (is_leaf(n)) {
-        free(n);
+        leaf_block_free(t->leaf_node_size, n, 1);
         return;
     }
     orc_inner *p = n;
-    for (uint32_t i = 0; i < p->count; i++) free_subtree(p->child[i]);
+    for (uint32_t i = 0; i < p->count; i++) free_subtree(t, p->child[i]);
     inner_free(p);
 }
 
 void orc_tree_free(orc_tree *t) {
     if (!t) return;
-    free_subtree(t->root);
+    free_subtree(t, t->root);
     for (orc_copy *c = t->copies; c;) {
         orc_copy *nx = c->reg_next;
         free(c->image);
@@ -650,6 +714,217 @@ uint64_t orc_load_ycsb(orc_tree *t, uint64_t begin, uint64_t end, uint32_t key_s
         if (orc_insert(t, (const uint8_t *)&k, key_size, payload, INVALID_CID) == ORC_RET_OK) ok++;
     }
     free(payload);
+    return ok;
+}
+
+/* ---------------------------------------------------------------- parallel load (CPU baseline)
+ * LoadYCSBRows of rows [begin, end) built by several threads with the same LEAVES as the
+ * single loader.  Leaves only ever split during inserts and a split depends only on the
+ * leaf's own records, so once a leaf boundary exists it stays: after the first rows are
+ * inserted sequentially, the leaves are cut into nthreads groups of consecutive leaves and
+ * each thread inserts, in row order, the remaining rows that route into its group (into a
+ * private tree holding just that group).  The inner levels are then rebuilt bottom-up over
+ * all leaves with the split-time separators and the reference's observed fanout (273
+ * children per inner node: 20,498 leaves under 75 bottom nodes at 1M rows):
+ * routing is identical, inner node shapes are not (tests/test_oracle_golden.py). */
+typedef struct { void **node; const uint8_t **sep; uint16_t *seplen; uint64_t n, cap; } node_list;
+
+static void nl_push(node_list *L, void *node, const uint8_t *sep, uint16_t seplen) {
+    if (L->n == L->cap) {
+        L->cap = L->cap ? 2 * L->cap : 1024;
+        L->node = realloc(L->node, L->cap * sizeof(void *));
+        L->sep = realloc((void *)L->sep, L->cap * sizeof(uint8_t *));
+        L->seplen = realloc(L->seplen, L->cap * sizeof(uint16_t));
+        if (!L->node || !L->sep || !L->seplen) abort();
+    }
+    L->node[L->n] = node;
+    L->sep[L->n] = sep;
+    L->seplen[L->n] = seplen;
+    L->n++;
+}
+
+/* leaves in key order, each with its lower separator (the inner key routing to it) */
+static void collect_leaves(void *node, node_list *L, const uint8_t *lo, uint16_t lo_len) {
+    if (is_leaf(node)) {
+        nl_push(L, node, lo, lo_len);
+        return;
+    }
+    orc_inner *p = node;
+    for (uint32_t i = 0; i < p->count; i++)
+        collect_leaves(p->child[i], L, i == 0 ? lo : p->key[i], i == 0 ? lo_len : p->klen[i]);
+}
+
+static void free_inner_only(void *node) {
+    if (is_leaf(node)) return;
+    orc_inner *p = node;
+    for (uint32_t i = 0; i < p->count; i++) free_inner_only(p->child[i]);
+    inner_free(p);
+}
+
+/* an inner node over entries [b, e) of L: slot 0 = dummy key, slot i = L->sep[b+i] */
+static orc_inner *inner_over(node_list *L, uint64_t b, uint64_t e) {
+    uint32_t nr = (uint32_t)(e - b), kbytes = 0, size = 48;
+    for (uint64_t i = b + 1; i < e; i++) kbytes += L->seplen[i];
+    orc_inner *n = inner_alloc(nr, kbytes);
+    kb_t kb = {0};
+    for (uint64_t i = b; i < e; i++) {
+        int first = i == b;
+        inner_set(n, &kb, (uint32_t)(i - b), first ? NULL : L->sep[i], first ? 0 : L->seplen[i], L->node[i]);
+        size += pad_key(first ? 0 : L->seplen[i]) + 8 + META_SZ;
+    }
+    n->size = size;
+    n->count = nr;
+    return n;
+}
+
+/* bottom-up inner levels over a list of children; the list is consumed */
+static void *build_levels(node_list *L, uint32_t fanout) {
+    while (L->n > 1) {
+        node_list up = {0};
+        for (uint64_t b = 0; b < L->n; b += fanout) {
+            uint64_t e = b + fanout < L->n ? b + fanout : L->n;
+            nl_push(&up, inner_over(L, b, e), L->sep[b], L->seplen[b]);
+        }
+        free(L->node);
+        free((void *)L->sep);
+        free(L->seplen);
+        *L = up;
+    }
+    void *root = L->node[0];
+    free(L->node);
+    free((void *)L->sep);
+    free(L->seplen);
+    return root;
+}
+
+typedef struct {
+    orc_tree *sub;
+    const uint8_t *part;
+    uint8_t g;
+    uint64_t begin, end;
+    uint32_t ks;
+    int mode;
+    uint64_t ok;
+} pload_t;
+
+static void *pload_worker(void *arg) {
+    pload_t *p = arg;
+    uint8_t *payload = xmalloc(p->sub->payload_size + 8);
+    for (uint64_t r = p->begin; r < p->end; r++) {
+        if (p->part[r - p->begin] != p->g) continue;
+        uint64_t k = r;
+        orc_fill_payload(r, p->mode, payload, p->sub->payload_size);
+        if (orc_insert(p->sub, (const uint8_t *)&k, p->ks, payload, INVALID_CID) == ORC_RET_OK) p->ok++;
+    }
+    free(payload);
+    return NULL;
+}
+
+typedef struct {
+    const uint8_t **bsep;
+    const uint16_t *blen;
+    uint32_t nb;
+    uint8_t *part;
+    uint64_t base, b, e;
+    uint32_t ks;
+} route_t;
+
+static void *route_worker(void *arg) {
+    route_t *r = arg;
+    for (uint64_t i = r->b; i < r->e; i++) {
+        uint64_t k = r->base + i;
+        uint32_t lo = 0, hi = r->nb; /* groups g > 0 start above separator bsep[g-1] */
+        while (lo < hi) {
+            uint32_t mid = (lo + hi) / 2;
+            if (orc_key_compare((const uint8_t *)&k, r->ks, r->bsep[mid], r->blen[mid]) > 0) lo = mid + 1;
+            else hi = mid;
+        }
+        r->part[i] = (uint8_t)lo;
+    }
+    return NULL;
+}
+
+uint64_t orc_load_ycsb_parallel(orc_tree *t, uint64_t begin, uint64_t end, uint32_t key_size, int payload_mode,
+                                int nthreads) {
+    if (nthreads > 64) nthreads = 64;
+    uint64_t seq_end = begin + 100000 < end ? begin + 100000 : end;
+    uint64_t ok = orc_load_ycsb(t, begin, seq_end, key_size, payload_mode);
+    node_list leaves = {0};
+    collect_leaves(t->root, &leaves, NULL, 0);
+    if (nthreads < 2 || seq_end == end || leaves.n < (uint64_t)nthreads) {
+        free(leaves.node);
+        free((void *)leaves.sep);
+        free(leaves.seplen);
+        return ok + orc_load_ycsb(t, seq_end, end, key_size, payload_mode);
+    }
+    int T = nthreads;
+    uint64_t m = leaves.n;
+    /* group g = leaves [m*g/T, m*(g+1)/T); boundary g-1 = lower separator of its first leaf */
+    const uint8_t *bsep[64];
+    uint16_t blen[64];
+    orc_tree *sub[64];
+    for (int g = 0; g < T; g++) {
+        uint64_t b = m * (uint64_t)g / T, e = m * (uint64_t)(g + 1) / T;
+        if (g > 0) {
+            bsep[g - 1] = leaves.sep[b];
+            blen[g - 1] = leaves.seplen[b];
+        }
+        sub[g] = orc_tree_new(t->leaf_node_size, t->split_threshold, t->payload_size);
+        leaf_block_free(t->leaf_node_size, sub[g]->root, 0);
+        sub[g]->merge_threshold = t->merge_threshold;
+        sub[g]->key_pad = t->key_pad;
+        sub[g]->bulk = t->bulk;
+        sub[g]->root = e - b == 1 ? leaves.node[b] : (void *)inner_over(&leaves, b, e);
+    }
+    uint64_t rest = end - seq_end;
+    uint8_t *part = xmalloc(rest ? rest : 1);
+    pthread_t th[64];
+    route_t rt[64];
+    for (int i = 0; i < T; i++) {
+        route_t r = {bsep, blen, (uint32_t)(T - 1), part, seq_end, rest * (uint64_t)i / T,
+                     rest * (uint64_t)(i + 1) / T, key_size};
+        rt[i] = r;
+        pthread_create(&th[i], NULL, route_worker, &rt[i]);
+    }
+    for (int i = 0; i < T; i++) pthread_join(th[i], NULL);
+    pload_t pl[64];
+    for (int g = 0; g < T; g++) {
+        pload_t p = {sub[g], part, (uint8_t)g, seq_end, end, key_size, payload_mode, 0};
+        pl[g] = p;
+        pthread_create(&th[g], NULL, pload_worker, &pl[g]);
+    }
+    for (int g = 0; g < T; g++) {
+        pthread_join(th[g], NULL);
+        ok += pl[g].ok;
+    }
+    free(part);
+    /* every leaf in key order with its lower separator, then the inner levels */
+    node_list all = {0};
+    for (int g = 0; g < T; g++) {
+        uint64_t first = all.n;
+        collect_leaves(sub[g]->root, &all, g ? bsep[g - 1] : NULL, g ? blen[g - 1] : 0);
+        (void)first;
+    }
+    void *old_root = t->root;
+    t->root = build_levels(&all, 273);
+    free_inner_only(old_root); /* the boundary separators lived here: copied by inner_set */
+    for (int g = 0; g < T; g++) {
+        orc_tree *s = sub[g];
+        free_inner_only(s->root);
+        for (uint64_t i = 0; i < s->nlocs; i++) {
+            if (t->nlocs == t->caplocs) {
+                t->caplocs = t->caplocs ? 2 * t->caplocs : 1024;
+                t->locs = realloc(t->locs, t->caplocs * sizeof(orc_loc *));
+            }
+            t->locs[t->nlocs++] = s->locs[i];
+        }
+        free(s->locs);
+        free(s->garbage);
+        free(s);
+    }
+    free(leaves.node);
+    free((void *)leaves.sep);
+    free(leaves.seplen);
     return ok;
 }
 
@@ -865,6 +1140,266 @@ uint64_t orc_read_batch_timed(orc_tree *t, const uint64_t *keys, uint32_t key_si
     clock_gettime(CLOCK_MONOTONIC, &b);
     if (seconds) *seconds = (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
     return j.sum;
+}
+
+/* ---------------------------------------------------------------- full transactions
+ * CPU baseline "full-txn" mode: RunMixed (benchmark/ycsb/ycsb_mixed.cpp:18-140) with every op
+ * a read, through IndexScanExecutor (executor.h:374-454) and the Index-SSN read side:
+ *   BeginTransaction     transaction_manager.cpp:280-309  read_id = tid_counter++, new context,
+ *                                                         active_tids.Insert(read_id)
+ *   PerformRead          transaction_manager.cpp:362-410  RecordRead (rw-set insert, hash on the
+ *                        meta word, equality on loc_ptr: txn_context.h:16-24), SetPredecessor,
+ *                        GetOversionHeader(next_ptr) -> IncreaseWRCount + SetSuccessor,
+ *                        CheckExclusion
+ *   CommitTransaction    transaction_manager.cpp:535-815  commit id = tid_counter++, FindMinSstamp
+ *                        (:113-221) and FindMaxPstamp (:29-102) over copies of the rw-set,
+ *                        post-commit READ entries (:749-764), active_tids.Insert(commit_id)
+ * The reference never erases active_tids nor deletes contexts (EndTransaction is empty,
+ * :311-322); here both are released after the timed region. */
+typedef struct rw_node { orc_rmeta *loc; uint64_t meta; int type; struct rw_node *next; } rw_node;
+typedef struct txn_ctx {
+    uint32_t read_id, commit_id, pred, succ;
+    int aborted, finished;
+    rw_node *bucket[16]; /* rw_set_ (ReadWriteSet, txn_context.h:28) */
+    uint32_t nrw;
+} txn_ctx;
+
+typedef struct tid_node { uint32_t tid; txn_ctx *ctx; struct tid_node *next; } tid_node;
+#define TID_STRIPES 64
+#define TID_BUCKETS (1u << 20)
+typedef struct { /* active_tids: concurrent map tid -> context (transaction_manager.h) */
+    pthread_mutex_t lock[TID_STRIPES];
+    tid_node **b;
+} tid_map;
+
+static void tid_insert(tid_map *m, uint32_t tid, txn_ctx *ctx) {
+    uint32_t h = (uint32_t)(((uint64_t)tid * 0x9ddfea08eb382d69ull) >> 44) & (TID_BUCKETS - 1);
+    tid_node *n = xmalloc(sizeof(tid_node));
+    n->tid = tid;
+    n->ctx = ctx;
+    pthread_mutex_t *l = &m->lock[h % TID_STRIPES];
+    pthread_mutex_lock(l);
+    n->next = m->b[h];
+    m->b[h] = n;
+    pthread_mutex_unlock(l);
+}
+
+static int tid_find(tid_map *m, uint32_t tid, txn_ctx **out) {
+    uint32_t h = (uint32_t)(((uint64_t)tid * 0x9ddfea08eb382d69ull) >> 44) & (TID_BUCKETS - 1);
+    pthread_mutex_t *l = &m->lock[h % TID_STRIPES];
+    int found = 0;
+    pthread_mutex_lock(l);
+    for (tid_node *n = m->b[h]; n; n = n->next)
+        if (n->tid == tid) {
+            *out = n->ctx;
+            found = 1;
+            break;
+        }
+    pthread_mutex_unlock(l);
+    return found;
+}
+
+static uint32_t rw_hash(uint64_t meta) { return (uint32_t)((meta * 0x9E3779B97F4A7C15ull) >> 60); }
+
+/* TransactionContext::RecordRead, transaction_context.cpp:88-99 */
+static int rw_record_read(txn_ctx *c, orc_rmeta *loc, uint64_t meta) {
+    uint32_t h = rw_hash(meta);
+    for (rw_node *n = c->bucket[h]; n; n = n->next)
+        if (n->loc == loc) return 0;
+    rw_node *n = xmalloc(sizeof(rw_node));
+    n->loc = loc;
+    n->meta = meta;
+    n->type = 0; /* RWType::READ */
+    n->next = c->bucket[h];
+    c->bucket[h] = n;
+    c->nrw++;
+    return 1;
+}
+
+/* `auto rw_set = current_txn->GetReadWriteSet()` copies the map (FindMinSstamp :111,
+ * FindMaxPstamp :30): flattened here into a per-call array */
+static uint32_t rw_copy(txn_ctx *c, rw_node *out) {
+    uint32_t k = 0;
+    for (int b = 0; b < 16; b++)
+        for (rw_node *n = c->bucket[b]; n; n = n->next) out[k++] = *n;
+    return k;
+}
+
+typedef struct {
+    orc_tree *t;
+    const uint64_t *keys;
+    uint32_t ks, ops;
+    uint64_t b, e; /* transactions [b, e) */
+    uint32_t *tid_counter;
+    tid_map *tids;
+    txn_ctx **ctxs;
+    uint64_t sum, commits, aborts;
+} txn_job_t;
+
+static void *txn_worker(void *arg) {
+    txn_job_t *j = arg;
+    orc_tree *t = j->t;
+    uint16_t ks = (uint16_t)j->ks;
+    uint64_t sum = 0, commits = 0, aborts = 0;
+    rw_node *copy = xmalloc(sizeof(rw_node) * (j->ops + 1));
+    for (uint64_t x = j->b; x < j->e; x++) {
+        txn_ctx *c = xmalloc(sizeof(txn_ctx));
+        memset(c, 0, sizeof(*c));
+        c->read_id = __atomic_fetch_add(j->tid_counter, 1, __ATOMIC_SEQ_CST);
+        c->succ = MAX_CID;
+        tid_insert(j->tids, c->read_id, c);
+        j->ctxs[x] = c;
+        int ok = 1;
+        for (uint32_t op = 0; op < j->ops && ok; op++) {
+            uint64_t k = j->keys[x * j->ops + op];
+            const uint8_t *key = (const uint8_t *)&k;
+            uint8_t *leaf = traverse_to_leaf(t, NULL, key, ks, 1);
+            int64_t slot = search_record_meta(leaf, key, ks, 1);
+            if (slot < 0) continue; /* Read -> nullptr: the executor returns true, no tuple */
+            orc_rmeta *mp = l_meta(leaf, (uint32_t)slot);
+            uint64_t m = mp->meta;
+            /* BTree::Read: heap Record (Record::New, b_tree.h:407-428) */
+            size_t rsz = 48 + 4 + m_padded(m) + t->payload_size;
+            uint8_t *r = xmalloc(rsz);
+            memcpy(r + 52, leaf + m_offset(m), m_padded(m) + t->payload_size);
+            uint32_t cstamp = m_inserting(m) ? 0 : c->read_id;
+            if (m_inserting(m)) {
+                orc_copy *cp = copy_of(mp->next);
+                if (cp) {
+                    memcpy(r + 52, cp->image, cp->key_len + t->payload_size);
+                    cstamp = cp->rstamp;
+                }
+            }
+            if (c->read_id >= m_cstamp(m)) {
+                /* PerformRead (transaction_manager.cpp:362-410) */
+                if (rw_record_read(c, mp, m)) {
+                    if (cstamp > c->pred) c->pred = cstamp;
+                    orc_copy *hdr = copy_of(mp->next);
+                    if (hdr) {
+                        __atomic_fetch_add(&hdr->wr_count, 1, __ATOMIC_SEQ_CST); /* IncreaseWRCount */
+                        if (hdr->sstamp != MAX_CID && hdr->sstamp < c->succ) c->succ = hdr->sstamp;
+                    }
+                    if (c->succ <= c->pred) { /* CheckExclusion */
+                        c->aborted = 1;
+                        ok = 0;
+                    }
+                }
+                /* the executor's `new T` + memcpy (executor.h:396-401), deleted by the driver */
+                uint8_t *tup = xmalloc(4 + t->payload_size);
+                memcpy(tup, r + 52, 4 + t->payload_size);
+                sum += tup[4 + (op % t->payload_size)];
+                free(tup);
+            } else {
+                orc_read_out o;
+                read_one(t, key, ks, c->read_id, &o, NULL);
+                sum += o.status;
+            }
+            free(r);
+        }
+        if (!ok) {
+            aborts++;
+            continue;
+        }
+        /* CommitTransaction (:535-815) */
+        c->commit_id = __atomic_fetch_add(j->tid_counter, 1, __ATOMIC_SEQ_CST);
+        /* FindMinSstamp: successor starts at t_cstamp; READ entries overwritten since */
+        if (c->commit_id < c->succ) c->succ = c->commit_id;
+        uint32_t nc = rw_copy(c, copy);
+        for (uint32_t i = 0; i < nc; i++) {
+            if (copy[i].type != 0) continue;
+            uint64_t cur = copy[i].loc->meta;
+            uint32_t cur_c = m_cstamp(cur), old_c = m_cstamp(copy[i].meta);
+            if (cur_c != old_c && cur_c < c->commit_id) {
+                txn_ctx *w;
+                if (cur_c != INVALID_CID && tid_find(j->tids, cur_c, &w) && !w->aborted && w->succ < c->succ)
+                    c->succ = w->succ;
+            } else {
+                orc_copy *hc = copy_of(copy[i].loc->next);
+                if (hc) {
+                    txn_ctx *w;
+                    if (tid_find(j->tids, hc->cstamp, &w) && w->finished && w->succ < c->succ) c->succ = w->succ;
+                }
+            }
+        }
+        /* FindMaxPstamp: UPDATE entries only (none in a read-only mix), over a second copy */
+        nc = rw_copy(c, copy);
+        for (uint32_t i = 0; i < nc; i++) sum += copy[i].type;
+        c->finished = 1;
+        /* post-commit, READ entries: v.pstamp = max(v.pstamp, t.cstamp), DecreaseWRCount */
+        for (int b = 0; b < 16; b++)
+            for (rw_node *n = c->bucket[b]; n; n = n->next) {
+                orc_copy *hc = copy_of(n->loc->next);
+                if (hc) {
+                    if (hc->pstamp < c->commit_id) hc->pstamp = c->commit_id;
+                    __atomic_fetch_sub(&hc->wr_count, 1, __ATOMIC_SEQ_CST);
+                }
+            }
+        tid_insert(j->tids, c->commit_id, c);
+        commits++;
+    }
+    free(copy);
+    j->sum = sum;
+    j->commits = commits;
+    j->aborts = aborts;
+    return NULL;
+}
+
+/* n_txns transactions of ops_per_txn reads each (keys[x*ops + op], u64 little-endian keys of
+ * key_size bytes); results[0] = commits, results[1] = aborts, results[2] = checksum. */
+void orc_ycsb_txn_timed(orc_tree *t, const uint64_t *keys, uint32_t key_size, uint32_t ops_per_txn, uint64_t n_txns,
+                        int nthreads, uint32_t first_tid, double *seconds, uint64_t *results) {
+    tid_map m;
+    for (int i = 0; i < TID_STRIPES; i++) pthread_mutex_init(&m.lock[i], NULL);
+    m.b = calloc(TID_BUCKETS, sizeof(tid_node *));
+    txn_ctx **ctxs = calloc(n_txns ? n_txns : 1, sizeof(txn_ctx *));
+    uint32_t counter = first_tid;
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    if ((uint64_t)nthreads > n_txns) nthreads = n_txns ? (int)n_txns : 1;
+    pthread_t th[256];
+    txn_job_t jobs[256];
+    struct timespec a, b;
+    clock_gettime(CLOCK_MONOTONIC, &a);
+    for (int i = 0; i < nthreads; i++) {
+        txn_job_t jj = {t, keys, key_size, ops_per_txn, n_txns * (uint64_t)i / nthreads,
+                        n_txns * (uint64_t)(i + 1) / nthreads, &counter, &m, ctxs, 0, 0, 0};
+        jobs[i] = jj;
+        pthread_create(&th[i], NULL, txn_worker, &jobs[i]);
+    }
+    uint64_t commits = 0, aborts = 0, sum = 0;
+    for (int i = 0; i < nthreads; i++) {
+        pthread_join(th[i], NULL);
+        commits += jobs[i].commits;
+        aborts += jobs[i].aborts;
+        sum += jobs[i].sum;
+    }
+    clock_gettime(CLOCK_MONOTONIC, &b);
+    if (seconds) *seconds = (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
+    if (results) {
+        results[0] = commits;
+        results[1] = aborts;
+        results[2] = sum;
+    }
+    for (uint64_t x = 0; x < n_txns; x++) {
+        txn_ctx *c = ctxs[x];
+        if (!c) continue;
+        for (int bb = 0; bb < 16; bb++)
+            for (rw_node *n = c->bucket[bb]; n;) {
+                rw_node *nx = n->next;
+                free(n);
+                n = nx;
+            }
+        free(c);
+    }
+    free(ctxs);
+    for (uint32_t i = 0; i < TID_BUCKETS; i++)
+        for (tid_node *n = m.b[i]; n;) {
+            tid_node *nx = n->next;
+            free(n);
+            n = nx;
+        }
+    free(m.b);
+    for (int i = 0; i < TID_STRIPES; i++) pthread_mutex_destroy(&m.lock[i]);
 }
 
 /* ---------------------------------------------------------------- scans */
@@ -1275,6 +1810,23 @@ int orc_commit_update(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32
     mp->meta = m;
     mp->next = (uint64_t)(uintptr_t)th | NEXT_TH;
     return ORC_RET_OK;
+}
+
+/* one transaction epoch of single-key writers, op by op in batch order (as tests/
+ * test_gpu_write_path.py::oracle_epoch): orc_update, then orc_commit_update(cid, cid) when it
+ * succeeded and cid[i] != 0 (cid 0 = left in flight); rc[i] = the last ReturnCode */
+uint64_t orc_update_batch(orc_tree *t, const uint64_t *keys, uint32_t key_size, uint64_t n, uint32_t payload_off,
+                          const uint8_t *deltas, uint32_t delta_len, const uint32_t *wid, const uint32_t *cid,
+                          uint8_t *rc) {
+    uint64_t ok = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        uint64_t k = keys[i];
+        int r = orc_update(t, (const uint8_t *)&k, key_size, payload_off, deltas + i * delta_len, delta_len, wid[i]);
+        if (r == ORC_RET_OK && cid[i]) r = orc_commit_update(t, (const uint8_t *)&k, key_size, cid[i], cid[i]);
+        if (rc) rc[i] = (uint8_t)r;
+        ok += r == ORC_RET_OK;
+    }
+    return ok;
 }
 
 /* BTree::FinalizeUpdate, b_tree.cpp:2252-2268: cstamp := commit_id, next_ptr untouched */

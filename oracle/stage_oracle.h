@@ -76,6 +76,19 @@ uint64_t orc_read_batch_timed(orc_tree *t, const uint64_t *keys, uint32_t key_si
                               const uint32_t *read_ids, uint64_t n, int nthreads,
                               double *seconds);
 
+/* CPU baseline full-txn mode: n_txns read-only RunMixed transactions of ops_per_txn reads
+ * (keys[x*ops_per_txn + op]) through the IndexScanExecutor point-lookup branch and the
+ * Index-SSN read side (PerformRead, CommitTransaction); tid_counter starts at first_tid.
+ * results[0] = commits, results[1] = aborts, results[2] = checksum. */
+void orc_ycsb_txn_timed(orc_tree *t, const uint64_t *keys, uint32_t key_size, uint32_t ops_per_txn, uint64_t n_txns,
+                        int nthreads, uint32_t first_tid, double *seconds, uint64_t *results);
+/* LoadYCSBRows built by nthreads threads: the same leaves as orc_load_ycsb, inner levels
+ * rebuilt bottom-up (same routing); for the CPU baseline's large tables */
+uint64_t orc_load_ycsb_parallel(orc_tree *t, uint64_t begin, uint64_t end, uint32_t key_size, int payload_mode,
+                                int nthreads);
+/* a load of distinct keys skips LeafNode::Insert's CheckUnique (same leaves, faster build) */
+void orc_tree_set_bulk(orc_tree *t, int bulk);
+
 /* TableScanExecutor (scan_sz >= 0) over RangeScanBySize/Iterator.  recs receives up to
  * scan_size rows of [key padded 8][payload]; returns the number of records produced. */
 uint32_t orc_scan(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t scan_size,
@@ -102,6 +115,9 @@ int orc_update(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t payl
                const uint8_t *delta, uint32_t delta_len, uint32_t writer_id);
 int orc_commit_update(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t commit_id,
                       uint32_t sstamp);
+uint64_t orc_update_batch(orc_tree *t, const uint64_t *keys, uint32_t key_size, uint64_t n, uint32_t payload_off,
+                          const uint8_t *deltas, uint32_t delta_len, const uint32_t *wid, const uint32_t *cid,
+                          uint8_t *rc);
 int orc_finalize_update(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t commit_id);
 int orc_delete(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t commit_id);
 

@@ -53,6 +53,10 @@ _SIG = {
                                   ctypes.POINTER(ctypes.c_double)]),
     "orc_read_batch_k": (ctypes.c_int, [vp, vp, u32, u32, vp, u64, vp, vp, ctypes.c_int]),
     "orc_scan_batch_k": (u64, [vp, vp, u32, u32, u64, u32, vp, vp, ctypes.c_int]),
+    "orc_ycsb_txn_timed": (None, [vp, vp, u32, u32, u64, ctypes.c_int, u32, ctypes.POINTER(ctypes.c_double), vp]),
+    "orc_update_batch": (u64, [vp, vp, u32, u64, u32, vp, u32, vp, vp, vp]),
+    "orc_tree_set_bulk": (None, [vp, ctypes.c_int]),
+    "orc_load_ycsb_parallel": (u64, [vp, u64, u64, u32, ctypes.c_int, ctypes.c_int]),
     "orc_key_compare": (ctypes.c_int, [vp, u32, vp, u32]),
     "orc_murmur64a": (u64, [vp, ctypes.c_int, u64]),
     "orc_murmur64a_batch": (None, [vp, u64, ctypes.c_int, u64, vp]),
@@ -110,6 +114,34 @@ class OracleTree:
 
     def load_ycsb(self, begin, end, key_size, mode=0):
         return lib().orc_load_ycsb(self.t, begin, end, key_size, mode)
+
+    def load_ycsb_bulk(self, begin, end, key_size, mode=0):
+        """LoadYCSBRows without CheckUnique (distinct keys): the same leaves, built faster"""
+        lib().orc_tree_set_bulk(self.t, 1)
+        try:
+            return lib().orc_load_ycsb(self.t, begin, end, key_size, mode)
+        finally:
+            lib().orc_tree_set_bulk(self.t, 0)
+
+    def load_ycsb_parallel(self, begin, end, key_size, mode=0, nthreads=8):
+        """LoadYCSBRows by nthreads threads: the single loader's leaves, inner levels rebuilt
+        bottom-up (same routing) -- the CPU baseline's large tables"""
+        lib().orc_tree_set_bulk(self.t, 1)
+        try:
+            return lib().orc_load_ycsb_parallel(self.t, begin, end, key_size, mode, nthreads)
+        finally:
+            lib().orc_tree_set_bulk(self.t, 0)
+
+    def ycsb_txn_timed(self, keys, key_size, ops_per_txn, nthreads=1, first_tid=1):
+        """full-txn CPU baseline: len(keys) // ops_per_txn read-only RunMixed transactions;
+        returns (seconds, commits, aborts, checksum)"""
+        keys = np.ascontiguousarray(keys, np.uint64)
+        n_txns = keys.size // ops_per_txn
+        sec = ctypes.c_double()
+        res = np.zeros(3, np.uint64)
+        lib().orc_ycsb_txn_timed(self.t, keys.ctypes.data, key_size, ops_per_txn, n_txns, nthreads, first_tid,
+                                 ctypes.byref(sec), res.ctypes.data)
+        return sec.value, int(res[0]), int(res[1]), int(res[2])
 
     def load_keys(self, keys, key_size, mode=0):
         keys = np.ascontiguousarray(keys, np.uint64)
@@ -187,6 +219,17 @@ class OracleTree:
     def update(self, key, key_size, payload_off, delta, writer_id):
         d = bytes(delta)
         return lib().orc_update(self.t, key_bytes(key, key_size), key_size, payload_off, d, len(d), writer_id)
+
+    def update_batch(self, keys, key_size, payload_off, deltas, wid, cid):
+        """orc_update_batch: returns (rc[n], n_ok)"""
+        keys = np.ascontiguousarray(keys, np.uint64)
+        deltas = np.ascontiguousarray(deltas, np.uint8).reshape(keys.size, -1)
+        wid = np.ascontiguousarray(wid, np.uint32)
+        cid = np.ascontiguousarray(cid, np.uint32)
+        rc = np.zeros(keys.size, np.uint8)
+        ok = lib().orc_update_batch(self.t, keys.ctypes.data, key_size, keys.size, payload_off, deltas.ctypes.data,
+                                    deltas.shape[1], wid.ctypes.data, cid.ctypes.data, rc.ctypes.data)
+        return rc, int(ok)
 
     def commit_update(self, key, key_size, commit_id, sstamp):
         return lib().orc_commit_update(self.t, key_bytes(key, key_size), key_size, commit_id, sstamp)

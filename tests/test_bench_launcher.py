@@ -1,0 +1,69 @@
+"""CPU: bench.py's multi-rank launcher and CPU-baseline plumbing (no GPU).
+
+`bench.py --gpus N` outside torch.distributed starts N ranks itself; the ranks' control plane
+(gloo rendezvous, barrier, max-over-ranks timing, rank 0's single JSON line) is exercised with
+--dry-run, which skips every device call.  Under torch.distributed a world size different
+from --gpus is refused instead of being reported as a scaling point.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+import bench
+import oracle_lib as O
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, env=None, timeout=300):
+    e = dict(os.environ)
+    e.update(env or {})
+    return subprocess.run([sys.executable, os.path.join(REPO, "bench.py")] + args, capture_output=True, text=True,
+                          timeout=timeout, env=e, cwd=REPO)
+
+
+def test_launcher_starts_two_ranks():
+    p = _run(["--gpus", "2", "--dry-run", "--steps", "2"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [s for s in p.stdout.splitlines() if s.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 2 and r["ranks"] == [0, 1] and r["dry_run"] and r["self_check"]
+    assert sum(r["rows_per_rank"]) == 2 * 200_000 and min(r["rows_per_rank"]) > 0
+    assert r["config"]["parallelism"] == "hash-shard x2"
+
+
+def test_world_size_mismatch_is_refused():
+    env = {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": "1"}
+    p = _run(["--gpus", "4", "--dry-run"], env=env, timeout=120)
+    assert p.returncode == 2
+    assert "refusing" in p.stderr
+    assert not [s for s in p.stdout.splitlines() if s.startswith("{")]
+
+
+def test_numpy_router_hash_matches_oracle_murmur():
+    keys = np.random.default_rng(3).integers(0, 2**63, 5000, dtype=np.uint64)
+    assert (bench.murmur64a_u64(keys) == O.murmur64a_keys(keys, 8, 0)).all()
+
+
+def test_cpu_resources_and_rows():
+    res = bench.cpu_resources()
+    assert res["threads"] >= 1 and res["threads"] <= res["affinity_cpus"] <= (res["nproc"] or 1 << 20)
+    assert res["mem_total_gib"] > 0
+    a = bench.parse([])
+    n = bench.cpu_rows_for(a, res, a.rows)
+    assert 1_000_000 <= n <= a.rows and n % 1_000_000 == 0
+    # a host that holds the whole table gets the whole table
+    big = dict(res, _avail=400 * 2**30)
+    assert bench.cpu_rows_for(a, big, a.rows) == a.rows
+    a2 = bench.parse(["--cpu-rows", "3000000"])
+    assert bench.cpu_rows_for(a2, res, a2.rows) == 3_000_000
+
+
+def test_default_args_carry_the_nested_legs():
+    a = bench.parse([])
+    assert not a.no_extras and a.c3_epochs >= 1 and a.scan_batch == 1 << 18 and a.inflight_share > 0
+    assert a.cpu_rows == 0 and a.cpu_threads == 0
