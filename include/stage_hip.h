@@ -152,6 +152,13 @@ int stage_commit_update_key(stage_table *t, const uint8_t *key, uint16_t key_siz
                             uint32_t commit_id, uint32_t sstamp, uint8_t *rc_out);
 int stage_delete_key(stage_table *t, const uint8_t *key, uint16_t key_size, uint32_t commit_id,
                      uint8_t *rc_out);
+/* AbortTransaction (transaction_manager.cpp:825-1045) for one key of the table:
+ * stage_abort_update_key = the UPDATE entry (:846-921): the old image back from the overwrite
+ *   copy, control bit cleared, next := the chain the update found, the copy released;
+ * stage_abort_insert_key = the INSERT entry (:949-979): FinalizeForDelete + FailForInsert on
+ *   the leaf's last slot (an insert not in its leaf's last slot: STAGE_RC_INVALID). */
+int stage_abort_update_key(stage_table *t, const uint8_t *key, uint16_t key_size, uint8_t *rc_out);
+int stage_abort_insert_key(stage_table *t, const uint8_t *key, uint16_t key_size, uint8_t *rc_out);
 uint32_t stage_key_words(stage_table *t);
 
 /* publish the host layout to HBM (leaf key columns, slot words, visibility masks, the

@@ -1812,6 +1812,45 @@ int orc_commit_update(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32
     return ORC_RET_OK;
 }
 
+/* AbortTransaction, UPDATE entry (transaction_manager.cpp:846-921): the old image is copied
+ * back from the overwrite copy into the record, FinalizeForUpdate() (control bit cleared, the
+ * cstamp untouched), next_ptr := the chain the update found (the TupleHeader it reserved is
+ * dropped -- this restatement reserves it only at commit), the copy header is released. */
+int orc_abort_update(orc_tree *t, const uint8_t *key, uint32_t key_size) {
+    uint16_t ks = (uint16_t)key_size;
+    uint8_t *leaf;
+    orc_rmeta *mp = find_meta(t, key, ks, &leaf);
+    if (!mp || !m_inserting(mp->meta)) return ORC_RET_NOT_FOUND;
+    orc_copy *c = copy_of(mp->next);
+    if (!c) return ORC_RET_NOT_FOUND;
+    uint8_t *rk = leaf + m_offset(mp->meta);
+    memcpy(rk, c->image, c->key_len);                                        /* key */
+    memcpy(rk + m_padded(mp->meta), c->image + c->key_len, t->payload_size); /* payload */
+    mp->meta = (mp->meta & ~M_CONTROL) | M_VISIBLE;
+    mp->next = c->next;
+    c->live = 0;
+    return ORC_RET_OK;
+}
+
+/* AbortTransaction, INSERT entry (transaction_manager.cpp:949-979): FinalizeForDelete (meta
+ * := 0, record_meta.h:167-172) and StatusWord::FailForInsert (record count - 1, block size -
+ * record size, version_store.h:214-217).  FailForInsert drops the leaf's LAST slot, so the
+ * aborted insert must be that slot (single writer); otherwise ORC_RET_INVALID. */
+int orc_abort_insert(orc_tree *t, const uint8_t *key, uint32_t key_size) {
+    uint16_t ks = (uint16_t)key_size;
+    uint8_t *leaf;
+    orc_rmeta *mp = find_meta(t, key, ks, &leaf);
+    if (!mp) return ORC_RET_NOT_FOUND;
+    uint64_t s = *l_status(leaf);
+    uint32_t slot = (uint32_t)(((uint8_t *)mp - (leaf + LEAF_HDR)) / META_SZ);
+    if (slot + 1 != st_count(s) || slot < *l_sorted(leaf)) return ORC_RET_INVALID;
+    uint32_t total = m_padded(mp->meta) + t->payload_size;
+    mp->meta = 0;
+    mp->next = 0;
+    *l_status(leaf) = s - ((1ull << 44) + ((uint64_t)total << 22));
+    return ORC_RET_OK;
+}
+
 /* one transaction epoch of single-key writers, op by op in batch order (as tests/
  * test_gpu_write_path.py::oracle_epoch): orc_update, then orc_commit_update(cid, cid) when it
  * succeeded and cid[i] != 0 (cid 0 = left in flight); rc[i] = the last ReturnCode */

@@ -118,6 +118,9 @@ int orc_commit_update(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32
 uint64_t orc_update_batch(orc_tree *t, const uint64_t *keys, uint32_t key_size, uint64_t n, uint32_t payload_off,
                           const uint8_t *deltas, uint32_t delta_len, const uint32_t *wid, const uint32_t *cid,
                           uint8_t *rc);
+/* AbortTransaction UPDATE / INSERT entries (transaction_manager.cpp:846-921, 949-979) */
+int orc_abort_update(orc_tree *t, const uint8_t *key, uint32_t key_size);
+int orc_abort_insert(orc_tree *t, const uint8_t *key, uint32_t key_size);
 int orc_finalize_update(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t commit_id);
 int orc_delete(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t commit_id);
 

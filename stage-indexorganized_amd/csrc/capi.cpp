@@ -184,6 +184,24 @@ int stage_delete_key(stage_table *t, const uint8_t *key, uint16_t key_size, uint
     });
 }
 
+int stage_abort_update_key(stage_table *t, const uint8_t *key, uint16_t key_size, uint8_t *rc_out) {
+    if (!t || !key) return fail(STAGE_E_ARG, "null argument");
+    return guarded([&] {
+        int rc = t->host->abort_update(key, key_size);
+        if (rc_out) *rc_out = (uint8_t)rc;
+        return STAGE_OK;
+    });
+}
+
+int stage_abort_insert_key(stage_table *t, const uint8_t *key, uint16_t key_size, uint8_t *rc_out) {
+    if (!t || !key) return fail(STAGE_E_ARG, "null argument");
+    return guarded([&] {
+        int rc = t->host->abort_insert(key, key_size);
+        if (rc_out) *rc_out = (uint8_t)rc;
+        return STAGE_OK;
+    });
+}
+
 uint32_t stage_key_words(stage_table *t) { return t ? t->host->key_words() : 0; }
 
 int stage_sync(stage_table *t) {

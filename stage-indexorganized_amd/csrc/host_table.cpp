@@ -496,6 +496,42 @@ int HostTable::commit_update(const uint8_t *key, uint32_t len, uint32_t commit_i
     return STAGE_RC_OK;
 }
 
+// AbortTransaction UPDATE entry (transaction_manager.cpp:846-921): the record gets its old
+// image back (the overwrite copy's immutable heap row), FinalizeForUpdate() clears the control
+// bit (cstamp untouched), next := the chain the update found; the copy is released.
+int HostTable::abort_update(const uint8_t *key, uint32_t len) {
+    uint32_t leaf, slot;
+    if (find(key, len, &leaf, &slot) < 0) return STAGE_RC_NOT_FOUND;
+    const size_t i = (size_t)leaf * cap_ + slot;
+    if (!meta_inserting(meta_[i]) || (next_[i] & kNextKindMask) != kNextCopy) return STAGE_RC_NOT_FOUND;
+    const uint64_t ci = next_[i] & kNextIndexMask;
+    image_[i] = copies_[ci].image;
+    next_[i] = copies_[ci].next;
+    meta_[i] = (meta_[i] & ~kMetaControl) | kMetaVisible;
+    copy_live_[ci] = 0;
+    touch(leaf, slot);
+    return STAGE_RC_OK;
+}
+
+// AbortTransaction INSERT entry (transaction_manager.cpp:949-979): FinalizeForDelete (meta 0)
+// and StatusWord::FailForInsert (count - 1, block - record size, version_store.h:214-217).
+// FailForInsert drops the leaf's last slot, so the aborted insert must be that slot.
+int HostTable::abort_insert(const uint8_t *key, uint32_t len) {
+    uint32_t leaf, slot;
+    if (find(key, len, &leaf, &slot) < 0) return STAGE_RC_NOT_FOUND;
+    Leaf &L = leaves_[leaf];
+    if (slot + 1 != L.count || slot < L.sorted) return STAGE_RC_INVALID;
+    const size_t i = (size_t)leaf * cap_ + slot;
+    L.block -= pad8(meta_keylen(meta_[i])) + p_.payload_size;
+    L.count -= 1;
+    meta_[i] = 0;
+    next_[i] = 0;
+    image_[i] = 0;
+    clear_slot_key(i);
+    touch(leaf, slot);
+    return STAGE_RC_OK;
+}
+
 // BTree::FinalizeUpdate (b_tree.cpp:2252-2268): cstamp := commit_id, next untouched.
 int HostTable::finalize_update(const uint8_t *key, uint32_t len, uint32_t commit_id) {
     uint32_t leaf, slot;

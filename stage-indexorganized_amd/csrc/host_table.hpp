@@ -84,6 +84,8 @@ public:
     int commit_update(const uint8_t *key, uint32_t len, uint32_t commit_id, uint32_t sstamp);
     int finalize_update(const uint8_t *key, uint32_t len, uint32_t commit_id);
     int remove(const uint8_t *key, uint32_t len, uint32_t commit_id);
+    int abort_update(const uint8_t *key, uint32_t len);
+    int abort_insert(const uint8_t *key, uint32_t len);
     // the same for keys of <= 8 bytes passed little-endian in a u64
     int insert(uint64_t key_le, uint32_t len, const uint8_t *payload, uint64_t gen_rowid, int mode,
                uint32_t commit_id) {

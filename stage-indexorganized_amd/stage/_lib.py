@@ -55,6 +55,8 @@ SIGNATURES = {
     "stage_commit_update_key": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint16, ctypes.c_uint32, ctypes.c_uint32,
                                                c_u8p]),
     "stage_delete_key": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint16, ctypes.c_uint32, c_u8p]),
+    "stage_abort_update_key": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint16, c_u8p]),
+    "stage_abort_insert_key": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint16, c_u8p]),
     "stage_key_words": (ctypes.c_uint32, [c_vp]),
     "stage_sync": (ctypes.c_int, [c_vp]),
     "stage_tpcc_stock_level": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_uint64, c_vp, c_vp]),

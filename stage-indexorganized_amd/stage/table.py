@@ -356,6 +356,20 @@ class Table:
         check(lib().stage_delete_key(self.h, k.ctypes.data, k.size, commit_id, ctypes.byref(rc)), "delete_key")
         return rc.value
 
+    def abort_update_key(self, key):
+        """AbortTransaction UPDATE entry (transaction_manager.cpp:846-921) for one key"""
+        k = np.frombuffer(bytes(key), np.uint8)
+        rc = ctypes.c_uint8()
+        check(lib().stage_abort_update_key(self.h, k.ctypes.data, k.size, ctypes.byref(rc)), "abort_update_key")
+        return rc.value
+
+    def abort_insert_key(self, key):
+        """AbortTransaction INSERT entry (transaction_manager.cpp:949-979) for one key"""
+        k = np.frombuffer(bytes(key), np.uint8)
+        rc = ctypes.c_uint8()
+        check(lib().stage_abort_insert_key(self.h, k.ctypes.data, k.size, ctypes.byref(rc)), "abort_insert_key")
+        return rc.value
+
     # ---------------------------------------------------------------- device read path
     def probe_device(self, d_keys, n, d_out, d_records=None, d_read_ids=None, d_lens=None, d_leaf_ids=None,
                      stream=None):

@@ -54,6 +54,8 @@ _SIG = {
     "orc_read_batch_k": (ctypes.c_int, [vp, vp, u32, u32, vp, u64, vp, vp, ctypes.c_int]),
     "orc_scan_batch_k": (u64, [vp, vp, u32, u32, u64, u32, vp, vp, ctypes.c_int]),
     "orc_ycsb_txn_timed": (None, [vp, vp, u32, u32, u64, ctypes.c_int, u32, ctypes.POINTER(ctypes.c_double), vp]),
+    "orc_abort_update": (ctypes.c_int, [vp, vp, u32]),
+    "orc_abort_insert": (ctypes.c_int, [vp, vp, u32]),
     "orc_update_batch": (u64, [vp, vp, u32, u64, u32, vp, u32, vp, vp, vp]),
     "orc_tree_set_bulk": (None, [vp, ctypes.c_int]),
     "orc_load_ycsb_parallel": (u64, [vp, u64, u64, u32, ctypes.c_int, ctypes.c_int]),
@@ -233,6 +235,12 @@ class OracleTree:
 
     def commit_update(self, key, key_size, commit_id, sstamp):
         return lib().orc_commit_update(self.t, key_bytes(key, key_size), key_size, commit_id, sstamp)
+
+    def abort_update(self, key, key_size):
+        return lib().orc_abort_update(self.t, key_bytes(key, key_size), key_size)
+
+    def abort_insert(self, key, key_size):
+        return lib().orc_abort_insert(self.t, key_bytes(key, key_size), key_size)
 
     def finalize_update(self, key, key_size, commit_id):
         return lib().orc_finalize_update(self.t, key_bytes(key, key_size), key_size, commit_id)

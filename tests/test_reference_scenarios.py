@@ -1,0 +1,47 @@
+"""CPU: the reference's transaction-level unit tests on the visibility path, restated as op
+sequences (tests/golden/reference_test_scenarios.json, made by tests/golden/make_scenarios.py
+from testing_execute.cpp BasicTransactionTest incl. Lookup-Old, AbortVersionChainTest,
+MVCCTest and testing_btree.cpp Update / Upsert):
+
+* the oracle meets every expected outcome the reference tests assert;
+* the product's host write path (insert / update / commit / abort / delete on the C-ABI)
+  leaves every leaf identical to the oracle's after each write (the device reads of the same
+  scenarios are tests/test_gpu_scenarios.py).
+
+Unpinned (no reference assertion reaches them through this path): a writer's own-write reads
+(is_for_update = true, MVCCTest results[4]) and re-updates of its own in-flight record.
+"""
+import pytest
+
+import scenarios as S
+import stage
+from test_host_layout import compare_layout
+
+SCEN = S.load()
+
+
+@pytest.mark.parametrize("sc", SCEN, ids=[s["name"] for s in SCEN])
+def test_oracle_meets_reference_assertions(sc):
+    assert S.run(sc, S.OracleBackend) == []
+
+
+@pytest.mark.parametrize("sc", SCEN, ids=[s["name"] for s in SCEN])
+def test_host_write_path_matches_oracle_layout(sc):
+    g = S.geometry(sc["table"])
+    o = S.OracleBackend(g)
+    h = S.DeviceBackend(g)  # host side only: no sync, no device call
+    for op in sc["ops"]:
+        if op["op"] in ("read", "scan"):
+            continue
+        assert h.write(op) == o.write(op), op
+        compare_layout(h.t, o.t)
+
+
+def test_fixture_covers_the_cited_assertions():
+    names = {s["name"] for s in SCEN}
+    assert {"ExecuteTest.BasicTransactionTest", "ExecuteTest.AbortVersionChainTest", "ExecuteTest.MVCCTest",
+            "BTreeTest.Update", "BTreeTest.Upsert"} <= names
+    srcs = " ".join(op["src"] for s in SCEN for op in s["ops"])
+    for cited in (":371-418 Lookup-Old", ":525-529", ":536-540", ":1414", ":557-565", ":569-575"):
+        assert cited in srcs
+    assert stage.RC_NOT_NEEDED_UPDATE == 7
