@@ -74,7 +74,10 @@ typedef struct stage_probe_out {
     uint32_t rec_cstamp;  /* meta.GetTxnCommitId() of the hit slot (executor.h:383)        */
     uint32_t copy_sstamp; /* overwrite header sstamp, 0xFFFFFFFF when none                 */
     uint32_t image;       /* record-heap row that supplied the tuple (0xFFFFFFFF if none)  */
-    uint32_t reserved;
+    uint32_t meta_hi;     /* upper half of the hit slot's RecordMetadata word (control, visible,
+                             key length, offset; record_meta.h:66-70): meta = meta_hi << 32 |
+                             rec_cstamp.  STAGE_REPLY_OWNER status records carry the owner-local
+                             row index here instead (stage_probe_sharded_ex)               */
 } stage_probe_out;
 
 const char *stage_last_error(void);
@@ -345,7 +348,7 @@ int stage_probe_sharded(stage_table *t, const uint64_t *d_keys, const uint32_t *
 /* reply modes: STAGE_REPLY_ROWS = status records and tuple rows come back to the caller (what
  * stage_probe_sharded does); STAGE_REPLY_OWNER = the owner materialises the tuple rows in its
  * own HBM result buffer and only the 32-B status records come back, each carrying the row's
- * owner-local index in `reserved` (owner rank = MurmurHash64A(key, 8, 0) % world); the owner
+ * owner-local index in `meta_hi` (owner rank = MurmurHash64A(key, 8, 0) % world); the owner
  * reads its buffer with stage_sharded_owner_rows (valid until its next sharded probe). */
 #define STAGE_REPLY_ROWS 0
 #define STAGE_REPLY_OWNER 1

@@ -150,7 +150,7 @@ __global__ void unpermute(const stage_probe_out_dev *__restrict__ bout, const ui
 }
 
 // reply mode "owner": the row stays in the owner's result buffer; the status record carries
-// its owner-local index in the reserved word
+// its owner-local index in the meta_hi word (stage_hip.h: STAGE_REPLY_OWNER)
 __global__ void tag_rows(stage_probe_out_dev *__restrict__ out, uint64_t m, uint32_t base) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < m) out[i].w[7] = base + (uint32_t)i;

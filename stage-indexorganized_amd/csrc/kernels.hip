@@ -210,7 +210,7 @@ __global__ __launch_bounds__(256) void resolve_kernel(DevTable t, const uint64_t
 // point probe
 
 struct ProbeRes {
-    uint32_t status, flags, hops, slot, key_len, cstamp, rec_cstamp, copy_sstamp, image;
+    uint32_t status, flags, hops, slot, meta_hi, cstamp, rec_cstamp, copy_sstamp, image;  // meta_hi: meta >> 32
 };
 
 // BTree::Read + IndexScanExecutor visibility for one wave-uniform probe whose slot word
@@ -223,7 +223,7 @@ __device__ __forceinline__ void visibility(const DevTable &t, int slot, uint64_t
     r.image = 0xFFFFFFFFu;
     r.cstamp = 0;
     r.rec_cstamp = 0;
-    r.key_len = 0;
+    r.meta_hi = 0;
     r.slot = 0xFFFF;
     if (slot < 0) {
         r.status = ST_NOT_FOUND;
@@ -231,7 +231,7 @@ __device__ __forceinline__ void visibility(const DevTable &t, int slot, uint64_t
     }
     r.slot = (uint32_t)slot;
     r.rec_cstamp = meta_cstamp(m);
-    r.key_len = meta_keylen(m);
+    r.meta_hi = (uint32_t)(m >> 32);
     CopyHdr c = {0, kMaxCid, 0, 0};
     const bool has_copy = (next & kNextKindMask) == kNextCopy;
     if (has_copy) {  // PerformRead: GetOversionHeader(meta.next_ptr) != nullptr
@@ -287,12 +287,12 @@ __device__ __forceinline__ void visibility(const DevTable &t, int slot, uint64_t
 __device__ __forceinline__ void pack_out(uint32_t leaf, const ProbeRes &r, u32x4 &a, u32x4 &b) {
     a.x = (r.status & 0xFF) | ((r.flags & 0xFF) << 8) | ((r.hops > 0xFFFF ? 0xFFFF : r.hops) << 16);
     a.y = leaf;
-    a.z = (r.slot & 0xFFFF) | (r.key_len << 16);
+    a.z = (r.slot & 0xFFFF) | (meta_keylen((uint64_t)r.meta_hi << 32) << 16);
     a.w = r.cstamp;
     b.x = r.rec_cstamp;
     b.y = r.copy_sstamp;
     b.z = r.image;
-    b.w = 0;
+    b.w = r.meta_hi;
 }
 
 // 16-B output store at base + off (base wave-uniform).  POL 0: temporal; 1: nontemporal (the
@@ -418,7 +418,7 @@ __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *
                     r[g].flags = 0;
                     r[g].hops = 0;
                     r[g].slot = (uint32_t)slot;
-                    r[g].key_len = meta_keylen(m);
+                    r[g].meta_hi = (uint32_t)(m >> 32);
                     r[g].cstamp = rd[g];
                     r[g].rec_cstamp = meta_cstamp(m);
                     r[g].copy_sstamp = kMaxCid;

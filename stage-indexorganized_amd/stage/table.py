@@ -13,7 +13,7 @@ from ._lib import StageParams, c_vp, check, lib
 
 PROBE_OUT_DTYPE = np.dtype([
     ("status", "u1"), ("flags", "u1"), ("hops", "u2"), ("leaf", "u4"), ("slot", "u2"), ("key_len", "u2"),
-    ("cstamp", "u4"), ("rec_cstamp", "u4"), ("copy_sstamp", "u4"), ("image", "u4"), ("reserved", "u4"),
+    ("cstamp", "u4"), ("rec_cstamp", "u4"), ("copy_sstamp", "u4"), ("image", "u4"), ("meta_hi", "u4"),
 ])
 assert PROBE_OUT_DTYPE.itemsize == 32
 

@@ -123,6 +123,6 @@ def test_owner_reply_mode_loopback(gpu):
         own = (O.murmur64a_keys(per_keys[r], 8, 0) % np.uint64(world)).astype(np.int64)
         for o in range(world):
             sel = np.nonzero(own == o)[0]
-            got = owner_bufs[o][out["reserved"][sel]]
+            got = owner_bufs[o][out["meta_hi"][sel]]
             hit = out["status"][sel] != stage.ST_NOT_FOUND
             assert (got[hit] == ref_rows[sel][hit]).all()

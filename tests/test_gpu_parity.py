@@ -34,6 +34,14 @@ def check_probe(tab, orc, keys, key_size, read_ids=None, lens=None, leaf_ids=Non
     bad = np.nonzero((rows[:, :orc.row] != o_rec).any(axis=1))[0]
     assert bad.size == 0, (bad[:5], keys[bad[:5]], out["status"][bad[:5]])
     assert (rows[:, orc.row:] == 0).all()
+    # the hit slot's whole RecordMetadata word (meta_hi << 32 | rec_cstamp) == the oracle leaf's
+    found = np.nonzero(out["status"] != 0)[0]
+    if found.size and orc.stats()["leaves"] < 400_000:
+        meta = orc.export_leaves(tab.leaf_capacity)[2]
+        m = meta[out["leaf"][found], out["slot"][found]]
+        dm = (out["meta_hi"][found].astype(np.uint64) << np.uint64(32)) | out["rec_cstamp"][found].astype(np.uint64)
+        bad = np.nonzero(m != dm)[0]
+        assert bad.size == 0, ("meta", bad[:5], m[bad[:5]], dm[bad[:5]])
     return out, rows
 
 
