@@ -324,65 +324,30 @@ def hbm_roofline(per_unit, units_per_launch, kern_ms, kernel, traffic=None, tsrc
     return roof
 
 
-class PinnedArray:
-    """numpy view of a pinned host buffer (stage_host_alloc): full-rate PCIe copies."""
-
-    def __init__(self, count, dtype):
-        self.nbytes = max(1, count * np.dtype(dtype).itemsize)
-        self.p = ctypes.c_void_p()
-        check(stage.lib().stage_host_alloc(self.nbytes, ctypes.byref(self.p)), "host alloc")
-        raw = (ctypes.c_uint8 * self.nbytes).from_address(self.p.value)
-        self.a = np.frombuffer(raw, np.uint8).view(dtype)[:count]
-
-    def free(self):
-        if self.p:
-            stage.lib().stage_host_free(self.p)
-            self.p = None
-
-
 class YcsbB:
-    """configs[2]: each epoch applies the update share of a YCSB-B batch on the write path
-    (LeafNode::Update + CommitTransaction UPDATE entry, read/commit ids from one counter as
-    tid_counter does) -- on the device (stage_update_batch_device) or on the host
-    (stage_update_batch + incremental publish) -- and returns the read share with read ids:
-    75 % current, 25 % drawn from the ids of this run so far (older snapshots).  A share of
-    the update ops (--inflight-share, keys beyond the 10^4 hottest) stays in flight (commit id
-    0), so later reads of those keys take the overwrite-copy branch.
-    Timed as the write path (`write_s`): the update share's transfer to the device and the call
-    (device) or the host update + publish (host); generating the synthetic epoch is not.
-    Every epoch is recorded (keys, column byte, ids) so the CPU leg can replay it on the oracle."""
+    """configs[2]: YCSB-B epochs.  Each epoch is the update share of a batch applied on the
+    write path (LeafNode::Update + CommitTransaction UPDATE entry, read / commit ids from one
+    counter as tid_counter does) -- on the device (stage_update_batch_device) or on the host
+    (stage_update_batch + incremental publish) -- and its read share with read ids: 75 %
+    current, 25 % drawn from the ids of this run so far (older snapshots).  A share of the
+    update ops (--inflight-share, keys beyond the 10^4 hottest) stays in flight (commit id 0),
+    so later reads of those keys take the overwrite-copy (COPY) branch.
+    Epochs are generated and their inputs uploaded to HBM before the timed loop (like the C2
+    keys); every epoch is recorded so the CPU leg can replay it on the oracle."""
 
     def __init__(self, tab, args, nthreads, theta):
         self.tab, self.args, self.nthreads, self.theta = tab, args, nthreads, theta
         self.counter = 1
         self.epoch = 0
-        self.updates = 0
-        self.prep_s = 0.0
-        self.write_s = 0.0
-        self.sync_s = 0.0
-        self.last_sync = None
         self.record = []
-        if args.write_path == "device":
-            B = args.batch  # the update share of a batch never exceeds it
-            self.h = {k: PinnedArray(B * w, dt) for k, (w, dt) in
-                      {"keys": (1, np.uint64), "cols": (100, np.uint8), "rid": (1, np.uint32),
-                       "cid": (1, np.uint32)}.items()}
-            self.d = {k: stage.DeviceBuffer(v.nbytes) for k, v in self.h.items()}
-            self.d_rc = stage.DeviceBuffer(B)
 
-    def reset_counters(self):
-        self.updates, self.write_s, self.sync_s = 0, 0.0, 0.0
-
-    def next_batch(self):
+    def make_epoch(self):
         a = self.args
-        n = a.rows
-        t0 = time.time()
-        draws = stage.zipf_draws(n - 1, self.theta, a.seed + 1000 * self.epoch, a.batch, nthreads=self.nthreads)
+        draws = stage.zipf_draws(a.rows - 1, self.theta, a.seed + 1000 * self.epoch, a.batch, nthreads=self.nthreads)
         rng = np.random.default_rng(a.seed + self.epoch)
         is_upd = rng.random(a.batch) < a.update_ratio
         keys = draws[is_upd]
         m = keys.size
-        # read id / commit id pairs from one counter (tid_counter), one 100-B column patch each
         rid = (self.counter + 2 * np.arange(m, dtype=np.uint64)).astype(np.uint32)
         cid = rid + np.uint32(1)
         cand = np.nonzero(keys > 10_000)[0]
@@ -391,43 +356,43 @@ class YcsbB:
             cid[rng.choice(cand, k_in, replace=False)] = 0  # left in flight
         self.counter += 2 * m
         colb = ((keys + np.uint64(self.epoch + 1)) & np.uint64(0xFF)).astype(np.uint8)
-        if a.write_path == "device":
-            self.h["cols"].a[:m * 100] = np.repeat(colb, 100)
-            for k, x in (("keys", keys), ("rid", rid), ("cid", cid)):
-                self.h[k].a[:x.size] = x
-        self.prep_s += time.time() - t0
-        tu = time.time()
-        if a.write_path == "device":
-            # keys / ids / column patches over PCIe, then the epoch runs on the published image
-            L = stage.lib()
-            ok = ctypes.c_uint64()
-            if m:
-                for k, w in (("keys", 8), ("cols", 100), ("rid", 4), ("cid", 4)):
-                    check(L.stage_memcpy_h2d(self.d[k].ptr, self.h[k].p, m * w, None), "h2d")
-                check(L.stage_update_batch_device(self.tab.h, self.d["keys"].ptr, None, m, 0, self.d["cols"].ptr, 100,
-                                                  self.d["rid"].ptr, self.d["cid"].ptr, None, self.d_rc.ptr,
-                                                  ctypes.byref(ok), None),
-                      "update_batch_device")
-            ok = ok.value
-        else:
-            cols = np.repeat(colb[:, None], 100, 1)
-            _, ok = self.tab.update_batch(keys, 0, cols, rid, cid)
-            t1 = time.time()
-            self.tab.sync()
-            self.sync_s += time.time() - t1
-            self.last_sync = self.tab.sync_info()
-        self.write_s += time.time() - tu
-        self.updates += ok
-        t0 = time.time()
-        reads = draws[~is_upd]
+        reads = np.ascontiguousarray(draws[~is_upd])
         rids = np.full(reads.size, self.counter, np.uint32)
         old = rng.random(reads.size) < 0.25
         rids[old] = rng.integers(1, max(2, self.counter), int(old.sum())).astype(np.uint32)
-        self.record.append({"keys": keys, "colb": colb, "rid": rid, "cid": cid, "ok": ok,
-                            "inflight": int(k_in)})
+        ep = {"keys": keys, "colb": colb, "rid": rid, "cid": cid, "inflight": int(k_in), "reads": reads, "rids": rids}
+        self.record.append(ep)
         self.epoch += 1
-        self.prep_s += time.time() - t0
-        return reads, rids
+        return ep
+
+    def upload(self, ep):
+        """the epoch's inputs into HBM: update keys, 100-B column patches, ids; read keys, ids"""
+        cols = np.repeat(ep["colb"], 100)
+        ep["d"] = {k: stage.DeviceBuffer.from_numpy(x) for k, x in
+                   (("keys", ep["keys"]), ("cols", cols), ("rid", ep["rid"]), ("cid", ep["cid"]),
+                    ("reads", ep["reads"]), ("rids", ep["rids"]))}
+        ep["d"]["rc"] = stage.DeviceBuffer(max(1, ep["keys"].size))
+        ep["d"]["out"] = stage.DeviceBuffer(32 * ep["reads"].size)
+
+    def apply(self, ep):
+        """the epoch's write share on the write path; returns the successful updates"""
+        m = ep["keys"].size
+        if self.args.write_path == "device":
+            ok = ctypes.c_uint64()
+            if m:
+                d = ep["d"]
+                check(stage.lib().stage_update_batch_device(self.tab.h, d["keys"].ptr, None, m, 0, d["cols"].ptr, 100,
+                                                            d["rid"].ptr, d["cid"].ptr, None, d["rc"].ptr,
+                                                            ctypes.byref(ok), None), "update_batch_device")
+            return ok.value
+        cols = np.repeat(ep["colb"][:, None], 100, 1)
+        _, ok = self.tab.update_batch(ep["keys"], 0, cols, ep["rid"], ep["cid"])
+        self.tab.sync()
+        return ok
+
+    def release(self, ep):
+        for b in ep.pop("d", {}).values():
+            b.free()
 
 
 class CpuOracle:
@@ -822,63 +787,89 @@ def c4_leg(tab, args, total_rows, rank, stream, steps, warmup):
 
 
 def c3_leg(tab, args, stream, nthreads, steps, warmup):
-    """configs[2]: YCSB-B epochs; each timed step applies one epoch's write share on the write
-    path (timed apart) and probes its read share at the epoch's read ids (timed)."""
+    """configs[2]: YCSB-B epochs.  Timed loop, per epoch: the write share on the write path,
+    then the device probe of the read share at the epoch's read ids.  value = reads / the
+    probes' wall time; ops_per_s_incl_writes = (reads + updates) / the whole loop's wall time
+    (the device write path returns after its kernels and the headers' D2H; the host table
+    adopts the epoch on a background thread while the next probe runs)."""
     L = stage.lib()
     B = args.batch
     theta = args.theta if args.config == "c3" else 0.99
     ycsb_b = YcsbB(tab, args, nthreads, theta)
-    d_keys, d_rid = stage.DeviceBuffer(B * 8), stage.DeviceBuffer(B * 4)
-    d_out, d_rec = stage.DeviceBuffer(B * 32), stage.DeviceBuffer(B * tab.stride)
-    # the first `warmup` epochs are untimed (first-call allocations of the write path)
-    for _ in range(max(1, warmup)):
-        draws, rids = ycsb_b.next_batch()
-    ycsb_b.reset_counters()
+    t0 = time.time()
+    warm = max(1, warmup)
+    epochs = [ycsb_b.make_epoch() for _ in range(warm + steps)]
+    if args.write_path == "device":
+        for ep in epochs:
+            ycsb_b.upload(ep)
+    else:
+        for ep in epochs:
+            ep["d"] = {"reads": stage.DeviceBuffer.from_numpy(ep["reads"]),
+                       "rids": stage.DeviceBuffer.from_numpy(ep["rids"]),
+                       "out": stage.DeviceBuffer(32 * ep["reads"].size)}
+    prep_s = time.time() - t0
+    d_rec = stage.DeviceBuffer(B * tab.stride)
+
+    def probe(ep):
+        d = ep["d"]
+        tab.probe_device(d["reads"].ptr, ep["reads"].size, d["out"].ptr, d_rec.ptr, d_read_ids=d["rids"].ptr,
+                         stream=stream.ptr)
+
+    for ep in epochs[:warm]:  # untimed: first-call allocations of the write path
+        ycsb_b.apply(ep)
+        probe(ep)
+    stream.sync()
+    check(L.stage_device_sync(), "sync")
     evs = [stage.Event() for _ in range(2 * steps)]
-    elapsed, ops_done, hops = 0.0, 0, 0
-    hist = np.zeros(6, np.int64)
-    for i in range(steps):
-        draws, rids = ycsb_b.next_batch()
-        n_ops = draws.size
-        check(L.stage_memcpy_h2d(d_keys.ptr, draws.ctypes.data, draws.nbytes, None), "h2d")
-        check(L.stage_memcpy_h2d(d_rid.ptr, rids.ctypes.data, rids.nbytes, None), "h2d")
-        check(L.stage_device_sync(), "sync")
-        t0 = time.perf_counter()
+    elapsed, write_s, updates, ops_done = 0.0, 0.0, 0, 0
+    t_loop = time.perf_counter()
+    for i, ep in enumerate(epochs[warm:]):
+        tw = time.perf_counter()
+        updates += ycsb_b.apply(ep)
+        write_s += time.perf_counter() - tw
+        tr = time.perf_counter()
         evs[2 * i].record(stream)
-        tab.probe_device(d_keys.ptr, n_ops, d_out.ptr, d_rec.ptr, d_read_ids=d_rid.ptr, stream=stream.ptr)
+        probe(ep)
         evs[2 * i + 1].record(stream)
         stream.sync()
-        elapsed += time.perf_counter() - t0
-        ops_done += n_ops
-        o = d_out.to_numpy(stage.PROBE_OUT_DTYPE, n_ops)
+        elapsed += time.perf_counter() - tr
+        ops_done += ep["reads"].size
+    loop_s = time.perf_counter() - t_loop
+    kern_ms = float(np.mean([evs[2 * i].elapsed_ms(evs[2 * i + 1]) for i in range(steps)]))
+    hist = np.zeros(6, np.int64)
+    hops = 0
+    for ep in epochs[warm:]:
+        o = ep["d"]["out"].to_numpy(stage.PROBE_OUT_DTYPE, ep["reads"].size)
         hist += np.bincount(o["status"], minlength=6)[:6]
         hops += int(o["hops"].astype(np.int64).sum())
-    kern_ms = float(np.mean([evs[2 * i].elapsed_ms(evs[2 * i + 1]) for i in range(steps)]))
     mean_hops = hops / max(ops_done, 1)
-    ns = min(draws.size, 4096)
+    last = epochs[-1]
+    ns = min(last["reads"].size, 4096)
     rows = d_rec.to_numpy(np.uint8, ns * tab.stride).reshape(ns, tab.stride)
-    check_sample = (draws[:ns].copy(), rids[:ns].copy(), o["status"][:ns].copy(), rows)
-    ok = bool(hist[stage.ST_LATEST] > 0 and hist[stage.ST_OLD] > 0)
+    st = last["d"]["out"].to_numpy(stage.PROBE_OUT_DTYPE, ns)["status"]
+    check_sample = (last["reads"][:ns].copy(), last["rids"][:ns].copy(), st, rows)
+    ok = bool(hist[stage.ST_LATEST] > 0 and hist[stage.ST_OLD] > 0 and hist[stage.ST_COPY] > 0)
     per_unit = BYTES_PER_LOOKUP + HOP_BYTES * mean_hops
-    d = {"value": round(ops_done / elapsed, 1), "unit": "ops/s", "steps": steps, "warmup": max(1, warmup),
+    d = {"value": round(ops_done / elapsed, 1), "unit": "ops/s", "steps": steps, "warmup": warm,
          "ms_per_step": round(elapsed / steps * 1e3, 4), "self_check": ok,
-         "ops_per_s_incl_writes": round((ops_done + ycsb_b.updates) / (elapsed + ycsb_b.write_s), 1),
+         "ops_per_s_incl_writes": round((ops_done + updates) / loop_s, 1),
          "config": {"workload": WORKLOADS["c3"], "theta": theta, "update_ratio": args.update_ratio,
-                    "inflight_share": args.inflight_share, "updates_applied": ycsb_b.updates,
-                    "updates_in_flight": int(sum(e["inflight"] for e in ycsb_b.record)),
-                    "write_path": args.write_path, "write_s": round(ycsb_b.write_s, 3),
-                    "publish_s": round(ycsb_b.sync_s, 3), "epoch_prep_s_untimed": round(ycsb_b.prep_s, 2),
-                    "last_publish": ycsb_b.last_sync, "mean_chain_hops": round(mean_hops, 4),
+                    "inflight_share": args.inflight_share, "updates_applied": updates,
+                    "update_ops": int(sum(ep["keys"].size for ep in epochs[warm:])),
+                    "updates_in_flight": int(sum(ep["inflight"] for ep in epochs[warm:])),
+                    "write_path": args.write_path, "write_s": round(write_s, 4), "loop_s": round(loop_s, 4),
+                    "epoch_prep_s_untimed": round(prep_s, 2), "mean_chain_hops": round(mean_hops, 4),
                     "read_status_counts": {"latest": int(hist[1]), "copy": int(hist[2]), "old": int(hist[3]),
                                            "fail": int(hist[4]), "chain_miss": int(hist[5]),
                                            "not_found": int(hist[0])},
-                    "timed": "device probe of the read share (value); ops_per_s_incl_writes adds the epoch's write "
-                             "path (update share over PCIe + stage_update_batch_device)"},
+                    "timed": "value: device probes of the read shares; ops_per_s_incl_writes: the whole loop "
+                             "(write path + probes), epoch inputs resident in HBM beforehand"},
          "roofline": hbm_roofline(per_unit, ops_done / steps, kern_ms, "probe_kernel (read ids, chain walks)")}
     d["roofline"]["algorithmic_bytes"] = f"{BYTES_PER_LOOKUP} + {HOP_BYTES} x mean hops ({mean_hops:.4f})"
-    rec = {"record": ycsb_b.record, "reads": draws, "rids": rids, "check": check_sample}
-    for b in (d_keys, d_rid, d_out, d_rec):
-        b.free()
+    rec = {"record": ycsb_b.record, "reads": last["reads"], "rids": last["rids"], "check": check_sample}
+    for ep in epochs:
+        ycsb_b.release(ep)
+    d_rec.free()
     return d, rec
 
 

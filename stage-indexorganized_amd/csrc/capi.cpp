@@ -52,7 +52,7 @@ int stage_insert(stage_table *t, uint64_t key, uint16_t key_size, const uint8_t 
                  int payload_mode, uint32_t commit_id, uint8_t *rc_out) {
     if (!t) return fail(STAGE_E_ARG, "null table");
     return guarded([&] {
-        int rc = t->host->insert(key, key_size, payload, gen_rowid, payload_mode, commit_id);
+        int rc = host(t).insert(key, key_size, payload, gen_rowid, payload_mode, commit_id);
         if (rc_out) *rc_out = (uint8_t)rc;
         return STAGE_OK;
     });
@@ -62,7 +62,7 @@ int stage_load_ycsb(stage_table *t, uint64_t begin_rowid, uint64_t end_rowid, ui
                     uint64_t *inserted) {
     if (!t || key_size == 0 || key_size > 8) return fail(STAGE_E_ARG, "bad arguments");
     return guarded([&] {
-        uint64_t n = t->host->load_ycsb(begin_rowid, end_rowid, key_size, payload_mode);
+        uint64_t n = host(t).load_ycsb(begin_rowid, end_rowid, key_size, payload_mode);
         if (inserted) *inserted = n;
         return STAGE_OK;
     });
@@ -72,7 +72,7 @@ int stage_load_keys(stage_table *t, const uint64_t *keys, uint64_t n, uint32_t k
                     uint64_t *inserted) {
     if (!t || (!keys && n) || key_size == 0 || key_size > 8) return fail(STAGE_E_ARG, "bad arguments");
     return guarded([&] {
-        uint64_t c = t->host->load_keys(keys, n, key_size, payload_mode);
+        uint64_t c = host(t).load_keys(keys, n, key_size, payload_mode);
         if (inserted) *inserted = c;
         return STAGE_OK;
     });
@@ -83,7 +83,7 @@ int stage_update(stage_table *t, uint64_t key, uint16_t key_size, uint32_t paylo
     if (!t || (!delta && delta_len)) return fail(STAGE_E_ARG, "bad arguments");
     return guarded([&] {
         ensure_host_rows(t);
-        int rc = t->host->update(key, key_size, payload_off, delta, delta_len, writer_id);
+        int rc = host(t).update(key, key_size, payload_off, delta, delta_len, writer_id);
         if (rc_out) *rc_out = (uint8_t)rc;
         return STAGE_OK;
     });
@@ -93,7 +93,7 @@ int stage_commit_update(stage_table *t, uint64_t key, uint16_t key_size, uint32_
                         uint8_t *rc_out) {
     if (!t) return fail(STAGE_E_ARG, "null table");
     return guarded([&] {
-        int rc = t->host->commit_update(key, key_size, commit_id, sstamp);
+        int rc = host(t).commit_update(key, key_size, commit_id, sstamp);
         if (rc_out) *rc_out = (uint8_t)rc;
         return STAGE_OK;
     });
@@ -106,7 +106,7 @@ int stage_update_batch(stage_table *t, const void *keys, uint32_t key_stride, ui
         return fail(STAGE_E_ARG, "bad arguments");
     return guarded([&] {
         ensure_host_rows(t);
-        uint64_t ok = t->host->update_batch((const uint8_t *)keys, key_stride, n, key_size, payload_off, deltas,
+        uint64_t ok = host(t).update_batch((const uint8_t *)keys, key_stride, n, key_size, payload_off, deltas,
                                             delta_len, writer_ids, commit_ids, sstamps, rc_out);
         if (n_ok) *n_ok = ok;
         return STAGE_OK;
@@ -116,7 +116,7 @@ int stage_update_batch(stage_table *t, const void *keys, uint32_t key_stride, ui
 int stage_finalize_update(stage_table *t, uint64_t key, uint16_t key_size, uint32_t commit_id, uint8_t *rc_out) {
     if (!t) return fail(STAGE_E_ARG, "null table");
     return guarded([&] {
-        int rc = t->host->finalize_update(key, key_size, commit_id);
+        int rc = host(t).finalize_update(key, key_size, commit_id);
         if (rc_out) *rc_out = (uint8_t)rc;
         return STAGE_OK;
     });
@@ -125,7 +125,7 @@ int stage_finalize_update(stage_table *t, uint64_t key, uint16_t key_size, uint3
 int stage_delete(stage_table *t, uint64_t key, uint16_t key_size, uint32_t commit_id, uint8_t *rc_out) {
     if (!t) return fail(STAGE_E_ARG, "null table");
     return guarded([&] {
-        int rc = t->host->remove(key, key_size, commit_id);
+        int rc = host(t).remove(key, key_size, commit_id);
         if (rc_out) *rc_out = (uint8_t)rc;
         return STAGE_OK;
     });
@@ -136,7 +136,7 @@ int stage_insert_key(stage_table *t, const uint8_t *key, uint16_t key_size, cons
                      uint8_t *rc_out) {
     if (!t || !key || !payload) return fail(STAGE_E_ARG, "null argument");
     return guarded([&] {
-        int rc = t->host->insert(key, key_size, payload, 0, 0, commit_id);
+        int rc = host(t).insert(key, key_size, payload, 0, 0, commit_id);
         if (rc_out) *rc_out = (uint8_t)rc;
         return STAGE_OK;
     });
@@ -146,9 +146,9 @@ int stage_load_rows(stage_table *t, const uint8_t *keys, uint32_t key_stride, ui
                     const uint8_t *payloads, uint32_t payload_stride, uint64_t n, uint32_t commit_id,
                     uint8_t *rc_out, uint64_t *inserted) {
     if (!t || (n && (!keys || !payloads)) || key_stride < key_size) return fail(STAGE_E_ARG, "bad arguments");
-    if (payload_stride < t->host->params().payload_size) return fail(STAGE_E_ARG, "payload stride < payload size");
+    if (payload_stride < host(t).params().payload_size) return fail(STAGE_E_ARG, "payload stride < payload size");
     return guarded([&] {
-        uint64_t c = t->host->load_rows(keys, key_stride, key_size, payloads, payload_stride, n, commit_id, rc_out);
+        uint64_t c = host(t).load_rows(keys, key_stride, key_size, payloads, payload_stride, n, commit_id, rc_out);
         if (inserted) *inserted = c;
         return STAGE_OK;
     });
@@ -159,7 +159,7 @@ int stage_update_key(stage_table *t, const uint8_t *key, uint16_t key_size, uint
     if (!t || !key || (!delta && delta_len)) return fail(STAGE_E_ARG, "bad arguments");
     return guarded([&] {
         ensure_host_rows(t);
-        int rc = t->host->update(key, key_size, payload_off, delta, delta_len, writer_id);
+        int rc = host(t).update(key, key_size, payload_off, delta, delta_len, writer_id);
         if (rc_out) *rc_out = (uint8_t)rc;
         return STAGE_OK;
     });
@@ -169,7 +169,7 @@ int stage_commit_update_key(stage_table *t, const uint8_t *key, uint16_t key_siz
                             uint32_t sstamp, uint8_t *rc_out) {
     if (!t || !key) return fail(STAGE_E_ARG, "null argument");
     return guarded([&] {
-        int rc = t->host->commit_update(key, key_size, commit_id, sstamp);
+        int rc = host(t).commit_update(key, key_size, commit_id, sstamp);
         if (rc_out) *rc_out = (uint8_t)rc;
         return STAGE_OK;
     });
@@ -178,7 +178,7 @@ int stage_commit_update_key(stage_table *t, const uint8_t *key, uint16_t key_siz
 int stage_delete_key(stage_table *t, const uint8_t *key, uint16_t key_size, uint32_t commit_id, uint8_t *rc_out) {
     if (!t || !key) return fail(STAGE_E_ARG, "null argument");
     return guarded([&] {
-        int rc = t->host->remove(key, key_size, commit_id);
+        int rc = host(t).remove(key, key_size, commit_id);
         if (rc_out) *rc_out = (uint8_t)rc;
         return STAGE_OK;
     });
@@ -187,7 +187,7 @@ int stage_delete_key(stage_table *t, const uint8_t *key, uint16_t key_size, uint
 int stage_abort_update_key(stage_table *t, const uint8_t *key, uint16_t key_size, uint8_t *rc_out) {
     if (!t || !key) return fail(STAGE_E_ARG, "null argument");
     return guarded([&] {
-        int rc = t->host->abort_update(key, key_size);
+        int rc = host(t).abort_update(key, key_size);
         if (rc_out) *rc_out = (uint8_t)rc;
         return STAGE_OK;
     });
@@ -196,18 +196,18 @@ int stage_abort_update_key(stage_table *t, const uint8_t *key, uint16_t key_size
 int stage_abort_insert_key(stage_table *t, const uint8_t *key, uint16_t key_size, uint8_t *rc_out) {
     if (!t || !key) return fail(STAGE_E_ARG, "null argument");
     return guarded([&] {
-        int rc = t->host->abort_insert(key, key_size);
+        int rc = host(t).abort_insert(key, key_size);
         if (rc_out) *rc_out = (uint8_t)rc;
         return STAGE_OK;
     });
 }
 
-uint32_t stage_key_words(stage_table *t) { return t ? t->host->key_words() : 0; }
+uint32_t stage_key_words(stage_table *t) { return t ? host(t).key_words() : 0; }
 
 int stage_sync(stage_table *t) {
     if (!t) return fail(STAGE_E_ARG, "null table");
     return guarded([&] {
-        stage::sync_device(*t->host, t->dev);
+        stage::sync_device(host(t), t->dev);
         return STAGE_OK;
     });
 }
@@ -226,13 +226,13 @@ int stage_sync_info(stage_table *t, double *seconds, uint64_t *info) {
 int stage_stats(stage_table *t, uint64_t *stats) {
     if (!t || !stats) return fail(STAGE_E_ARG, "null argument");
     return guarded([&] {
-        t->host->stats(stats);
+        host(t).stats(stats);
         return STAGE_OK;
     });
 }
 
-uint32_t stage_record_stride(stage_table *t) { return t ? (t->out_stride ? t->out_stride : t->host->stride()) : 0; }
-uint32_t stage_leaf_capacity(stage_table *t) { return t ? t->host->cap() : 0; }
+uint32_t stage_record_stride(stage_table *t) { return t ? (t->out_stride ? t->out_stride : host(t).stride()) : 0; }
+uint32_t stage_leaf_capacity(stage_table *t) { return t ? host(t).cap() : 0; }
 
 int stage_traverse_batch(stage_table *t, const uint64_t *keys, const uint16_t *lens, uint64_t n, int le_child,
                          uint32_t *leaf_out) {
@@ -243,18 +243,18 @@ int stage_traverse_batch(stage_table *t, const uint64_t *keys, const uint16_t *l
         // happened since (the traversal itself never needs the device)
         std::vector<uint32_t> local;
         const std::vector<uint32_t> *map = &t->dev.host_to_dev;
-        if (!t->dev.valid || t->host->layout_dirty_) {
+        if (!t->dev.valid || host(t).layout_dirty_) {
             std::vector<uint32_t> order;
-            t->host->key_order(order);
-            local.assign(t->host->leaves_.size(), 0xFFFFFFFFu);
+            host(t).key_order(order);
+            local.assign(host(t).leaves_.size(), 0xFFFFFFFFu);
             for (size_t i = 0; i < order.size(); ++i) local[order[i]] = (uint32_t)i;
             map = &local;
         }
-        const uint32_t width = t->host->params().key_width, kwords = t->host->key_words();
+        const uint32_t width = host(t).params().key_width, kwords = host(t).key_words();
         for (uint64_t i = 0; i < n; ++i) {
             const uint32_t len = width ? width : (lens ? lens[i] : 8u);
-            const stage::Key k = t->host->key_of(reinterpret_cast<const uint8_t *>(keys + i * kwords), len);
-            leaf_out[i] = (*map)[t->host->route(k, le_child != 0)];
+            const stage::Key k = host(t).key_of(reinterpret_cast<const uint8_t *>(keys + i * kwords), len);
+            leaf_out[i] = (*map)[host(t).route(k, le_child != 0)];
         }
         return STAGE_OK;
     });
@@ -264,7 +264,7 @@ int64_t stage_export_leaves(stage_table *t, uint32_t cap, uint64_t max_leaves, u
                             uint64_t *meta, uint64_t *keyw) {
     if (!t || !rc || !sc || !meta || !keyw || cap == 0) return fail(STAGE_E_ARG, "null argument");
     try {
-        const int64_t n = t->host->export_leaves(cap, max_leaves, rc, sc, meta, keyw);
+        const int64_t n = host(t).export_leaves(cap, max_leaves, rc, sc, meta, keyw);
         if (n < 0) return fail(STAGE_E_ARG, "max_leaves is smaller than the leaf count (stage_stats[2])");
         return n;
     } catch (const std::bad_alloc &) {
@@ -279,7 +279,7 @@ int64_t stage_export_leaf_images(stage_table *t, uint64_t max_leaves, uint8_t *b
     if (!t || !blocks || (!sep_keys != !sep_lens)) return fail(STAGE_E_ARG, "bad arguments");
     try {
         ensure_host_rows(t);
-        const int64_t n = t->host->export_leaf_images(max_leaves, blocks, sep_keys, sep_lens);
+        const int64_t n = host(t).export_leaf_images(max_leaves, blocks, sep_keys, sep_lens);
         if (n < 0) return fail(STAGE_E_ARG, "max_leaves is smaller than the leaf count (stage_stats[2])");
         return n;
     } catch (const std::bad_alloc &) {
@@ -293,7 +293,7 @@ int stage_import_leaf_images(stage_table *t, const uint8_t *blocks, uint64_t n_l
                              const uint64_t *sep_keys, const uint16_t *sep_lens, uint64_t *n_records) {
     if (!t || !blocks || (!sep_keys != !sep_lens)) return fail(STAGE_E_ARG, "bad arguments");
     return guarded([&] {
-        const uint64_t n = t->host->import_leaf_images(blocks, n_leaves, block_size, sep_keys, sep_lens);
+        const uint64_t n = host(t).import_leaf_images(blocks, n_leaves, block_size, sep_keys, sep_lens);
         if (n_records) *n_records = n;
         return STAGE_OK;
     });
@@ -416,7 +416,7 @@ int stage_comm_unique_id(uint8_t *id128) {
 
 int stage_comm_init(stage_table *t, const uint8_t *id128, int rank, int world) {
     if (!t || !id128 || world < 1 || rank < 0 || rank >= world) return fail(STAGE_E_ARG, "bad arguments");
-    if (t->host->key_words() != 1) return fail(STAGE_E_ARG, "the sharded front-end routes keys of <= 8 bytes");
+    if (host(t).key_words() != 1) return fail(STAGE_E_ARG, "the sharded front-end routes keys of <= 8 bytes");
     return guarded([&] {
         (void)hipSetDevice(t->dev.device);
         t->comm = std::make_unique<stage::ShardComm>();
@@ -482,7 +482,7 @@ int stage_probe_sharded_loopback(stage_table *const *shards, int world, const ui
     for (int r = 0; r < world; ++r) {
         int rc = need_synced(shards[r]);
         if (rc) return rc;
-        if (shards[r]->host->key_words() != 1) return fail(STAGE_E_ARG, "the sharded front-end routes keys of <= 8 bytes");
+        if (host(shards[r]).key_words() != 1) return fail(STAGE_E_ARG, "the sharded front-end routes keys of <= 8 bytes");
         if (shards[r]->dev.device != shards[0]->dev.device) return fail(STAGE_E_ARG, "shards on different devices");
         if ((d_records[r] == nullptr) != (d_records[0] == nullptr)) return fail(STAGE_E_ARG, "rows for all or none");
     }

@@ -32,6 +32,9 @@ void DeviceImage::release() {
         b->p = nullptr;
         b->cap = 0;
     }
+    if (pinned) (void)hipHostFree(pinned);
+    pinned = nullptr;
+    pinned_cap = 0;
     if (stream) (void)hipStreamDestroy(stream);
     stream = nullptr;
     valid = false;
@@ -144,6 +147,18 @@ uint8_t *scratch_bytes(DeviceImage &d, uint64_t bytes) {
         d.scratch.cap = want;
     }
     return (uint8_t *)d.scratch.p;
+}
+
+uint8_t *pinned_bytes(DeviceImage &d, uint64_t bytes) {
+    if (d.pinned_cap < bytes) {
+        if (d.pinned) hip_check(hipHostFree(d.pinned), "hipHostFree staging");
+        d.pinned = nullptr;
+        d.pinned_cap = 0;
+        const uint64_t want = bytes + bytes / 4 + 4096;
+        hip_check(hipHostMalloc(&d.pinned, want, hipHostMallocDefault), "pinned staging");
+        d.pinned_cap = want;
+    }
+    return (uint8_t *)d.pinned;
 }
 
 void reserve_device_rows(HostTable &h, DeviceImage &d, uint64_t extra_images, uint64_t extra_copies,

@@ -22,6 +22,8 @@ struct DeviceImage {
     DevBuf head, okey, slot, tree, tree_len, heap, chdr, vhdr, arena, descs, patch;
     DevBuf scratch;  // per-call scratch of the device write path / stock-level (scratch_bytes)
     std::vector<uint8_t> staging;  // host staging of incremental patches
+    void *pinned = nullptr;        // pinned host staging of the device write path's epoch results
+    uint64_t pinned_cap = 0;
     uint64_t heap_rows = 0;  // rows the heap buffer can hold
     DevTable view{};
     std::vector<uint32_t> host_to_dev;  // host leaf id -> leaf index in key order
@@ -45,6 +47,8 @@ void hip_check(hipError_t e, const char *what);
 // next call on the same table).  Stream-ordered pool memory (hipMallocAsync) is not used: on
 // gfx950 its reuse across calls showed stale reads on other XCDs between kernels of a stream.
 uint8_t *scratch_bytes(DeviceImage &d, uint64_t bytes);
+// pinned host buffer of at least `bytes` (grown with hipHostMalloc; reused by the next call)
+uint8_t *pinned_bytes(DeviceImage &d, uint64_t bytes);
 
 // grow the record heap and the copy / version header arrays so that `extra_*` more entries fit
 // after the host's current counts (device write path); refreshes the DevTable view

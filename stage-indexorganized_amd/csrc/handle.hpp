@@ -3,10 +3,12 @@
 #pragma once
 #include <hip/hip_runtime_api.h>
 
+#include <exception>
 #include <memory>
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 
 #include "../../include/stage_hip.h"
 #include "device_image.hpp"
@@ -33,6 +35,22 @@ struct stage_table {
     int shard_chunks = 0;                          // 0 = STAGE_SHARD_CHUNKS or the default
     std::mutex pipe_mu;  // serialises stage_probe_host calls on this table
     std::unique_ptr<stage::HostPipe, stage::HostPipeDeleter> pipe;
+    // the device write path hands its epoch's bookkeeping (new copy / version headers, slot
+    // words) to the host table on this thread while the device goes on (write_path.hip);
+    // every entry point that reads or writes the host table settles it first (host())
+    std::thread adopt;
+    std::exception_ptr adopt_err;
+    void settle() {
+        if (adopt.joinable()) adopt.join();
+        if (adopt_err) {
+            std::exception_ptr e = adopt_err;
+            adopt_err = nullptr;
+            std::rethrow_exception(e);
+        }
+    }
+    ~stage_table() {
+        if (adopt.joinable()) adopt.join();
+    }
 };
 
 namespace stage_capi {
@@ -56,6 +74,14 @@ int guarded(F fn) {
     }
 }
 
+// the host table, after any pending device-epoch adoption (stage_table::settle)
+inline stage::HostTable &host(stage_table *t) {
+    t->settle();
+    return *t->host;
+}
+
+// device entry points check the host's dirty flag without settling: a pending adoption never
+// touches layout_dirty_, and the device image is already current
 inline int need_synced(stage_table *t) {
     if (!t) return fail(STAGE_E_ARG, "null table");
     if (!t->dev.valid || t->host->layout_dirty_)

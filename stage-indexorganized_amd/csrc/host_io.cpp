@@ -62,7 +62,7 @@ void host_pipe_release(HostPipe *p) {
 
 static HostPipe *get_pipe(stage_table *t) {
     const uint64_t stride = t->out_stride ? t->out_stride : t->dev.view.stride;
-    const uint32_t kw = t->host->key_words();
+    const uint32_t kw = host(t).key_words();
     if (t->pipe && t->pipe->stride == stride && t->pipe->kw == kw && t->pipe->device == t->dev.device)
         return t->pipe.get();
     t->pipe.reset();
@@ -303,15 +303,15 @@ int stage_probe_host(stage_table *t, const uint64_t *keys, const uint16_t *lens,
 
 int stage_reader_create(stage_table *t, uint32_t max_batch, uint32_t max_wait_us, stage_reader **out) {
     if (!t || !out || max_batch == 0 || max_batch > (1u << 20)) return fail(STAGE_E_ARG, "bad reader arguments");
-    if (t->host->key_words() != 1) return fail(STAGE_E_ARG, "the single-key reader takes keys of <= 8 bytes");
+    if (host(t).key_words() != 1) return fail(STAGE_E_ARG, "the single-key reader takes keys of <= 8 bytes");
     *out = nullptr;
     return guarded([&] {
         std::unique_ptr<stage_reader> r(new stage_reader);
         r->t = t;
         r->max_batch = max_batch;
         r->max_wait_us = max_wait_us;
-        r->stride = t->host->stride();
-        r->row_bytes = 8 + t->host->params().payload_size;
+        r->stride = host(t).stride();
+        r->row_bytes = 8 + host(t).params().payload_size;
         const uint64_t mb = max_batch, bytes = mb * (8 + 2 + 4 + 32 + r->stride);
         stage::hip_check(hipSetDevice(t->dev.device), "hipSetDevice");
         for (auto &sl : r->slot) {

@@ -308,11 +308,11 @@ unsigned blocks_for(uint64_t n, unsigned per) { return (unsigned)((n + per - 1) 
 
 namespace stage_capi {
 void ensure_host_rows(stage_table *t) {
-    if (!t->host->has_device_rows()) return;
+    if (!host(t).has_device_rows()) return;
     using namespace stage;
     hip_check(hipSetDevice(t->dev.device), "hipSetDevice");
-    const uint64_t stride = t->host->hstride();
-    t->host->materialize_device_rows([&](uint64_t first, uint64_t count, uint8_t *dst) {
+    const uint64_t stride = host(t).hstride();
+    host(t).materialize_device_rows([&](uint64_t first, uint64_t count, uint8_t *dst) {
         hip_check(hipMemcpy(dst, (const uint8_t *)t->dev.heap.p + first * stride, count * stride,
                             hipMemcpyDeviceToHost),
                   "device row fetch");
@@ -333,7 +333,7 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
     if (n == 0) return STAGE_OK;
     return guarded([&] {
         using namespace stage;
-        HostTable &h = *t->host;
+        HostTable &h = host(t);
         DeviceImage &dv = t->dev;
         hip_check(hipSetDevice(dv.device), "hipSetDevice");
         hipStream_t s = pick(t, stream);
@@ -431,18 +431,19 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         hip_check(hipStreamSynchronize(s), "write path");
         const double t_kernels = ms(t0);
         const uint64_t ns = totals[0], nv = totals[1];
-        std::vector<CopyHdr> copies(ns);
-        std::vector<VersionHdr> versions(nv);
-        std::vector<FinRec> fr(n);
+        // headers and slot words into pinned staging (full PCIe rate); the background adoption
+        // reads them there, and the next call settles it before reusing the staging
+        const uint64_t bc = ns * sizeof(CopyHdr), bv = nv * sizeof(VersionHdr), bf = n * sizeof(FinRec);
+        uint8_t *pin = pinned_bytes(dv, bc + bv + bf + 64);
+        auto *copies = reinterpret_cast<CopyHdr *>(pin);
+        auto *versions = reinterpret_cast<VersionHdr *>(pin + bc);
+        auto *fr = reinterpret_cast<FinRec *>(pin + bc + bv);
         if (ns)
-            hip_check(hipMemcpyAsync(copies.data(), (CopyHdr *)dv.chdr.p + cbase, ns * sizeof(CopyHdr),
-                                     hipMemcpyDeviceToHost, s),
-                      "copy headers");
+            hip_check(hipMemcpyAsync(copies, (CopyHdr *)dv.chdr.p + cbase, bc, hipMemcpyDeviceToHost, s), "copy headers");
         if (nv)
-            hip_check(hipMemcpyAsync(versions.data(), (VersionHdr *)dv.vhdr.p + vbase, nv * sizeof(VersionHdr),
-                                     hipMemcpyDeviceToHost, s),
+            hip_check(hipMemcpyAsync(versions, (VersionHdr *)dv.vhdr.p + vbase, bv, hipMemcpyDeviceToHost, s),
                       "version headers");
-        hip_check(hipMemcpyAsync(fr.data(), fin, n * sizeof(FinRec), hipMemcpyDeviceToHost, s), "slot words");
+        hip_check(hipMemcpyAsync(fr, fin, bf, hipMemcpyDeviceToHost, s), "slot words");
         hip_check(hipStreamSynchronize(s), "write path adopt");
         const double t_d2h = ms(t0);
         // device slot locations -> host slot indices, in place (FinRec and SlotWords share a
@@ -452,19 +453,34 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
                           offsetof(FinRec, next) == offsetof(HostTable::SlotWords, next) &&
                           offsetof(FinRec, image) == offsetof(HostTable::SlotWords, image),
                       "FinRec / SlotWords layout");
-        const uint32_t cap = view.cap;
-        const std::vector<uint32_t> &d2h = dv.dev_to_host;
-        HostTable::parallel_chunks(n, [&](uint64_t b, uint64_t e) {
-            for (uint64_t k = b; k < e; ++k)
-                if (fr[k].loc != ~0ull) fr[k].loc = (uint64_t)d2h[fr[k].loc / cap] * cap + fr[k].loc % cap;
+        // the host adopts the epoch on a background thread (stage_table::adopt) while the device
+        // goes on; the next call that needs the host table waits for it (host() / settle).
+        // Device slot locations -> host slot indices first, in place (FinRec and SlotWords share
+        // a layout; ops that published nothing keep ~0 and are skipped by the adoption)
+        static_assert(sizeof(FinRec) == sizeof(HostTable::SlotWords) &&
+                          offsetof(FinRec, meta) == offsetof(HostTable::SlotWords, meta) &&
+                          offsetof(FinRec, next) == offsetof(HostTable::SlotWords, next) &&
+                          offsetof(FinRec, image) == offsetof(HostTable::SlotWords, image),
+                      "FinRec / SlotWords layout");
+        t->adopt = std::thread([t, &h, &dv, cap = view.cap, n, ns, nv, copies, versions, fr, t0, t_d2h, t_kernels,
+                                t_enqueue, t_reserve]() mutable {
+            try {
+                const std::vector<uint32_t> &d2h = dv.dev_to_host;
+                HostTable::parallel_chunks(n, [&](uint64_t b, uint64_t e) {
+                    for (uint64_t k = b; k < e; ++k)
+                        if (fr[k].loc != ~0ull) fr[k].loc = (uint64_t)d2h[fr[k].loc / cap] * cap + fr[k].loc % cap;
+                });
+                h.adopt_device_epoch(copies, ns, versions, nv, ns, reinterpret_cast<const HostTable::SlotWords *>(fr), n);
+                if (trace)
+                    std::fprintf(stderr,
+                                 "[wp] n=%llu ok=%llu reserve %.2f enqueue %.2f kernels %.2f d2h %.2f adopted %.2f ms "
+                                 "(background)\n",
+                                 (unsigned long long)n, (unsigned long long)ns, t_reserve, t_enqueue, t_kernels, t_d2h,
+                                 std::chrono::duration<double, std::milli>(clk::now() - t0).count());
+            } catch (...) {
+                t->adopt_err = std::current_exception();
+            }
         });
-        const double t_conv = ms(t0);
-        h.adopt_device_epoch(copies.data(), ns, versions.data(), nv, ns,
-                             reinterpret_cast<const HostTable::SlotWords *>(fr.data()), n);
-        if (trace)
-            std::fprintf(stderr, "[wp] n=%llu ok=%llu reserve %.2f enqueue %.2f kernels %.2f d2h %.2f convert %.2f adopt %.2f ms\n",
-                         (unsigned long long)n, (unsigned long long)ns, t_reserve, t_enqueue, t_kernels, t_d2h, t_conv,
-                         ms(t0));
         if (n_ok) *n_ok = ns;
         return STAGE_OK;
     });

@@ -79,8 +79,10 @@ int probe_mode(const char *path) {
     const std::vector<uint64_t> keys = {3, 3, 3, 3, 5, 5, 9042, 9042, 9042, 77, 123456, 4999};
     const std::vector<uint32_t> rids = {0xFFFFFFFEu, 4, 1, 0, 10, 3, 5, 11, 13, 100, 7, 1};
     std::vector<stage_probe_out> outs(keys.size());
-    std::vector<uint8_t> rows(keys.size() * kRow);
-    CK(stage_probe_host(t, keys.data(), nullptr, rids.data(), keys.size(), outs.data(), rows.data()));
+    const uint32_t stride = stage_record_stride(t);  // output row pitch (>= 8 + payload)
+    std::vector<uint8_t> wide(keys.size() * stride), rows(keys.size() * kRow);
+    CK(stage_probe_host(t, keys.data(), nullptr, rids.data(), keys.size(), outs.data(), wide.data()));
+    for (size_t i = 0; i < keys.size(); ++i) std::memcpy(&rows[i * kRow], &wide[i * stride], kRow);
     FILE *f = std::fopen(path, "wb");
     if (!f) return 1;
     frame_all(keys, rids, outs, rows, f);
