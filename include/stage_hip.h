@@ -192,8 +192,8 @@ int64_t stage_export_leaves(stage_table *t, uint32_t cap, uint64_t max_leaves, u
  * (b_tree.h:571-740: BaseNode{is_leaf, NodeHeader{size, sorted_count, next_record_slot,
  * StatusWord}} b_tree.h:109-113 / version_store.h:158-231, RecordMetadata{meta, next_ptr,
  * loc_ptr} record_meta.h:30-60 per slot, records [key][pad to 8][payload] growing down).
- * Canonical form: next_ptr and loc_ptr (process pointers: TupleHeader / copy buffer /
- * RecordLocation, record_location.h:13-42) are 0 and unreferenced record bytes are 0.
+ * Canonical form: next_ptr (a process pointer: TupleHeader / copy buffer) is 0, loc_ptr is the
+ * record's RecordLocation handle (see below; 0 = none), unreferenced record bytes are 0.
  * sep_keys[i]/sep_lens[i] = leaf i's upper bound, the inner-node key that routes to it
  * (GetChildIndex, b_tree.cpp:664-702), len 0xFFFF = +inf for the last leaf.
  * stage_export_leaf_images returns the number of leaves (STAGE_E_ARG if max_leaves is below
@@ -206,6 +206,20 @@ int64_t stage_export_leaf_images(stage_table *t, uint64_t max_leaves, uint8_t *b
 int stage_import_leaf_images(stage_table *t, const uint8_t *blocks, uint64_t n_leaves,
                              uint32_t block_size, const uint64_t *sep_keys,
                              const uint16_t *sep_lens, uint64_t *n_records);
+/* RecordLocation indirection (record_location.h:13-42): the stable name of a record across leaf
+ * splits.  The reference allocates one location per Insert attempt
+ * (BTree::RecordIndirectLocation, b_tree.cpp:1865-1866, 2034-2050) and LeafNode::CopyFrom
+ * repoints it at the record's new slot on every split (b_tree.cpp:1520-1527); handle = the
+ * location's allocation index + 1, exported as the RecordMetadata loc_ptr of the leaf images
+ * and kept by the import.  A record dropped by a split (deleted / invisible) or an aborted
+ * insert loses its location.  leaf = leaf index in key order (= stage_probe_out.leaf).
+ * stage_export_locations: every live location (handle order); returns the count (only the
+ *   first `max` written).
+ * stage_resolve_locations: where each handle's record is now; leaf 0xFFFFFFFF, slot 0xFFFF = none. */
+int64_t stage_export_locations(stage_table *t, uint64_t max, uint64_t *handles, uint32_t *leaf,
+                               uint16_t *slot);
+int stage_resolve_locations(stage_table *t, const uint64_t *handles, uint64_t n, uint32_t *leaf,
+                            uint16_t *slot);
 
 /* ---- device batch path (the replaced hot path) ------------------------------------------
  * stage_probe_batch  replaces LeafNode::Read/SearchRecordMeta (b_tree.cpp:1042-1051, 18-122),

@@ -73,7 +73,7 @@ static inline uint64_t m_finalize_insert(uint64_t off, uint64_t klen, uint64_t c
 #define NEXT_KIND(x) ((x) & 3ull)
 #define NEXT_PTR(x) ((void *)(uintptr_t)((x) & ~3ull))
 
-typedef struct orc_loc { uint8_t *leaf; uint32_t slot; } orc_loc; /* RecordLocation */
+typedef struct orc_loc { uint8_t *leaf; uint32_t slot; uint64_t id; } orc_loc; /* RecordLocation; id = allocation index */
 
 typedef struct orc_copy { /* EphemeralPool::OverwriteVersionHeader, ephemeral_pool.h:26-150 */
     uint32_t cstamp, pstamp, rstamp, sstamp;
@@ -535,6 +535,10 @@ static int leaf_prepare_for_split(orc_tree *t, uint8_t *n, stack_t_ *st, uint8_t
         leaf_block_free(t->leaf_node_size, r, 0);
         return 0;
     }
+    for (uint32_t i = 0; i < cnt; i++) { /* CopyFrom drops these records: their locations dangle */
+        orc_rmeta *mp = l_meta(n, i);
+        if (!(mp->meta != 0 && m_visible(mp->meta) && m_keylen(mp->meta) > 0) && mp->loc) mp->loc->leaf = NULL;
+    }
     int32_t left_size = (int32_t)(total / 2);
     uint32_t nleft = 0;
     for (uint32_t i = 0; i < nv; i++) {
@@ -564,6 +568,7 @@ static orc_loc *new_loc(orc_tree *t) { /* BTree::RecordIndirectLocation */
     orc_loc *l = xmalloc(sizeof(orc_loc));
     l->leaf = NULL;
     l->slot = 0;
+    l->id = t->nlocs;
     if (t->nlocs == t->caplocs) {
         t->caplocs = t->caplocs ? 2 * t->caplocs : 1024;
         t->locs = realloc(t->locs, t->caplocs * sizeof(orc_loc *));
@@ -916,6 +921,7 @@ uint64_t orc_load_ycsb_parallel(orc_tree *t, uint64_t begin, uint64_t end, uint3
                 t->caplocs = t->caplocs ? 2 * t->caplocs : 1024;
                 t->locs = realloc(t->locs, t->caplocs * sizeof(orc_loc *));
             }
+            s->locs[i]->id = t->nlocs; /* this build's allocation order differs from the single loader's */
             t->locs[t->nlocs++] = s->locs[i];
         }
         free(s->locs);
@@ -1681,7 +1687,9 @@ static void image_rec(void *node, image_export_t *e, const uint8_t *ub, uint16_t
             memset(dst + LEAF_HDR, 0, e->block - LEAF_HDR);
             for (uint32_t i = 0; i < cnt; i++) {
                 uint64_t m = l_meta(n, i)->meta;
+                uint64_t lp = l_meta(n, i)->loc ? l_meta(n, i)->loc->id + 1 : 0; /* location handle */
                 memcpy(dst + LEAF_HDR + META_SZ * i, &m, 8);
+                memcpy(dst + LEAF_HDR + META_SZ * i + 16, &lp, 8);
                 if (m) {
                     uint32_t off = m_offset(m), len = pad_key(m_keylen(m)) + e->payload;
                     memcpy(dst + off, n + off, len);
@@ -1847,6 +1855,8 @@ int orc_abort_insert(orc_tree *t, const uint8_t *key, uint32_t key_size) {
     uint32_t total = m_padded(mp->meta) + t->payload_size;
     mp->meta = 0;
     mp->next = 0;
+    if (mp->loc) mp->loc->leaf = NULL;
+    mp->loc = NULL;
     *l_status(leaf) = s - ((1ull << 44) + ((uint64_t)total << 22));
     return ORC_RET_OK;
 }
@@ -1903,6 +1913,50 @@ int orc_delete(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t comm
         return ORC_RET_INVALID;
     return ORC_RET_OK;
 }
+
+/* ---------------------------------------------------------------- record locations */
+/* RecordLocation (record_location.h:13-42) of handle h (= allocation index + 1) -> (leaf index
+ * in key order, slot); leaf 0xFFFFFFFF = the location dangles (dropped by a split, aborted). */
+static int ptr_cmp(const void *a, const void *b) {
+    uintptr_t x = *(const uintptr_t *)a, y = *(const uintptr_t *)b;
+    return (x > y) - (x < y);
+}
+
+static void leaves_in_order(void *node, uintptr_t *out, uint64_t *n) {
+    if (is_leaf(node)) {
+        out[(*n)++] = (uintptr_t)node;
+        return;
+    }
+    orc_inner *p = node;
+    for (uint32_t i = 0; i < p->count; i++) leaves_in_order(p->child[i], out, n);
+}
+
+void orc_resolve_locations(orc_tree *t, const uint64_t *handles, uint64_t n, uint32_t *leaf, uint16_t *slot) {
+    uint64_t stats[8];
+    orc_stats(t, stats);
+    uint64_t nl = 0;
+    uintptr_t *ord = xmalloc(sizeof(uintptr_t) * (stats[2] + 1));
+    leaves_in_order(t->root, ord, &nl);
+    /* (pointer, key-order index) pairs sorted by pointer */
+    uintptr_t *pairs = xmalloc(sizeof(uintptr_t) * 2 * (nl + 1));
+    for (uint64_t i = 0; i < nl; i++) {
+        pairs[2 * i] = ord[i];
+        pairs[2 * i + 1] = i;
+    }
+    qsort(pairs, nl, 2 * sizeof(uintptr_t), ptr_cmp);
+    for (uint64_t i = 0; i < n; i++) {
+        uint64_t h = handles[i];
+        orc_loc *l = (h == 0 || h > t->nlocs) ? NULL : t->locs[h - 1];
+        uintptr_t key = l ? (uintptr_t)l->leaf : 0;
+        uintptr_t *hit = key ? bsearch(&key, pairs, nl, 2 * sizeof(uintptr_t), ptr_cmp) : NULL;
+        leaf[i] = hit ? (uint32_t)hit[1] : 0xFFFFFFFFu;
+        slot[i] = hit ? (uint16_t)l->slot : 0xFFFF;
+    }
+    free(pairs);
+    free(ord);
+}
+
+uint64_t orc_location_count(orc_tree *t) { return t->nlocs; }
 
 /* ---------------------------------------------------------------- murmur */
 /* MurmurHash64A, misc/murmur/MurmurHash2.cpp:99-147 (little-endian, unaligned) */

@@ -161,6 +161,11 @@ uint64_t orc_scan_batch_k(orc_tree *t, const uint8_t *keys, uint32_t key_stride,
 int64_t orc_export_leaves(orc_tree *t, uint32_t cap, uint64_t max_leaves, uint32_t *rc,
                           uint32_t *sc, uint64_t *meta, uint64_t *keyw);
 
+/* RecordLocation handles (allocation index + 1) -> (leaf index in key order, slot);
+ * 0xFFFFFFFF / 0xFFFF = the location dangles */
+void orc_resolve_locations(orc_tree *t, const uint64_t *handles, uint64_t n, uint32_t *leaf, uint16_t *slot);
+uint64_t orc_location_count(orc_tree *t);
+
 /* KeyCompare (b_tree.h:116-134) */
 int orc_key_compare(const uint8_t *k1, uint32_t s1, const uint8_t *k2, uint32_t s2);
 /* MurmurHash64A (misc/murmur/MurmurHash2.cpp:99-147) */

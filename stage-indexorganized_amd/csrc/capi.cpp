@@ -289,6 +289,25 @@ int64_t stage_export_leaf_images(stage_table *t, uint64_t max_leaves, uint8_t *b
     }
 }
 
+int64_t stage_export_locations(stage_table *t, uint64_t max, uint64_t *handles, uint32_t *leaf, uint16_t *slot) {
+    if (!t || (max && (!handles || !leaf || !slot))) return fail(STAGE_E_ARG, "bad arguments");
+    try {
+        return (int64_t)host(t).export_locations(max, handles, leaf, slot);
+    } catch (const std::bad_alloc &) {
+        return fail(STAGE_E_NOMEM, "host allocation failed");
+    } catch (const std::exception &e) {
+        return fail(STAGE_E_HIP, e.what());
+    }
+}
+
+int stage_resolve_locations(stage_table *t, const uint64_t *handles, uint64_t n, uint32_t *leaf, uint16_t *slot) {
+    if (!t || (n && (!handles || !leaf || !slot))) return fail(STAGE_E_ARG, "bad arguments");
+    return guarded([&] {
+        host(t).resolve_locations(handles, n, leaf, slot);
+        return STAGE_OK;
+    });
+}
+
 int stage_import_leaf_images(stage_table *t, const uint8_t *blocks, uint64_t n_leaves, uint32_t block_size,
                              const uint64_t *sep_keys, const uint16_t *sep_lens, uint64_t *n_records) {
     if (!t || !blocks || (!sep_keys != !sep_lens)) return fail(STAGE_E_ARG, "bad arguments");

@@ -110,12 +110,14 @@ uint32_t HostTable::alloc_leaf() {
         meta_.resize(n, 0);
         next_.resize(n, 0);
         image_.resize(n, 0);
+        loc_.resize(n, 0);
     }
     size_t b = (size_t)id * cap_;
     std::fill(okey_.begin() + b * kw_, okey_.begin() + (b + cap_) * kw_, 0);
     std::fill(meta_.begin() + b, meta_.begin() + b + cap_, 0);
     std::fill(next_.begin() + b, next_.begin() + b + cap_, 0);
     std::fill(image_.begin() + b, image_.begin() + b + cap_, 0);
+    std::fill(loc_.begin() + b, loc_.begin() + b + cap_, 0);
     leaves_[id].live = true;
     nleaves_live_++;
     return id;
@@ -282,6 +284,9 @@ int HostTable::insert(const uint8_t *key, uint32_t len, const uint8_t *payload, 
     const uint32_t rec = (len > 8 ? pad8(len) : 8u) + p_.payload_size;
     for (int guard = 0; guard < 64; ++guard) {
         uint32_t leaf = route(k, true);
+        const uint64_t lid = locpos_.size();  // RecordIndirectLocation, every attempt (b_tree.cpp:1865-1866)
+        if (lid >= 0xFFFFFFFFull) throw std::runtime_error("location index overflow");
+        locpos_.push_back(kNoPos);
         int64_t hit = search(leaf, k);  // CheckUnique (b_tree.cpp:1395-1417)
         if (hit >= 0) {
             if (meta_inserting(meta_[(size_t)leaf * cap_ + hit])) return STAGE_RC_INVALID;  // ReCheck path
@@ -301,6 +306,8 @@ int HostTable::insert(const uint8_t *key, uint32_t len, const uint8_t *payload, 
         meta_[i] = ((uint64_t)len << 48) | kMetaVisible | (offset << 32) | commit_id;
         next_[i] = 0;
         image_[i] = new_image(key, len, payload, gen_rowid, mode);
+        loc_[i] = (uint32_t)(lid + 1);
+        locpos_[lid] = (uint64_t)leaf << 16 | slot;
         touch(leaf, slot);
         return STAGE_RC_OK;
     }
@@ -312,7 +319,7 @@ bool HostTable::split(uint32_t p) {
     struct Rec {
         Key key;
         uint64_t meta;
-        uint32_t next, image;
+        uint32_t next, image, loc;
     };
     const size_t pb = (size_t)p * cap_;
     std::vector<Rec> v;
@@ -320,13 +327,16 @@ bool HostTable::split(uint32_t p) {
     uint32_t total = 0;
     for (uint32_t s = 0; s < leaves_[p].count; ++s) {
         uint64_t m = meta_[pb + s];
-        if (m == 0) continue;
-        if (meta_visible(m) && meta_keylen(m) > 0) {
-            v.push_back(Rec{slot_key(pb + s), m, next_[pb + s], image_[pb + s]});
+        if (m != 0 && meta_visible(m) && meta_keylen(m) > 0) {
+            v.push_back(Rec{slot_key(pb + s), m, next_[pb + s], image_[pb + s], loc_[pb + s]});
             total += pad8(meta_keylen(m)) + p_.payload_size;
         }
     }
     if (total == 0) return false;
+    for (uint32_t s = 0; s < leaves_[p].count; ++s) {  // CopyFrom drops these: their locations dangle
+        const uint64_t m = meta_[pb + s];
+        if (!(m != 0 && meta_visible(m) && meta_keylen(m) > 0) && loc_[pb + s]) locpos_[loc_[pb + s] - 1] = kNoPos;
+    }
     std::sort(v.begin(), v.end(), [](const Rec &a, const Rec &b) { return key_lt(a.key, b.key); });
     int32_t left_size = (int32_t)(total / 2);
     uint32_t nleft = 0;
@@ -351,6 +361,8 @@ bool HostTable::split(uint32_t p) {
             meta_[b + n] = ((uint64_t)kl << 48) | kMetaVisible | ((uint64_t)offset << 32) | meta_cstamp(v[i].meta);
             next_[b + n] = v[i].next;
             image_[b + n] = v[i].image;
+            loc_[b + n] = v[i].loc;
+            if (v[i].loc) locpos_[v[i].loc - 1] = (uint64_t)leaf << 16 | n;  // loc->record_meta_ptr
             ++n;
         }
         for (uint32_t s = n; s < cap_; ++s) {
@@ -358,6 +370,7 @@ bool HostTable::split(uint32_t p) {
             meta_[b + s] = 0;
             next_[b + s] = 0;
             image_[b + s] = 0;
+            loc_[b + s] = 0;
         }
         L.count = L.sorted = n;
         L.block = p_.leaf_node_size - offset;
@@ -402,7 +415,10 @@ void HostTable::route_split(uint32_t p, uint32_t r, const Key &lo, const Key &s,
 
 uint64_t HostTable::load_ycsb(uint64_t begin, uint64_t end, uint32_t key_size, int mode) {
     if (key_size > 8) return 0;
-    if (end > begin) images_.reserve(images_.size() + (end - begin));
+    if (end > begin) {
+        images_.reserve(images_.size() + (end - begin));
+        locpos_.reserve(locpos_.size() + (end - begin) + (end - begin) / 32);
+    }
     uint64_t ok = 0;
     for (uint64_t rowid = begin; rowid < end; ++rowid)
         if (insert(rowid & key_mask(key_size), key_size, nullptr, rowid, mode, kInvalidCid) == STAGE_RC_OK) ++ok;
@@ -527,6 +543,8 @@ int HostTable::abort_insert(const uint8_t *key, uint32_t len) {
     meta_[i] = 0;
     next_[i] = 0;
     image_[i] = 0;
+    if (loc_[i]) locpos_[loc_[i] - 1] = kNoPos;
+    loc_[i] = 0;
     clear_slot_key(i);
     touch(leaf, slot);
     return STAGE_RC_OK;
@@ -842,14 +860,45 @@ int64_t HostTable::export_leaves(uint32_t cap, uint64_t max_leaves, uint32_t *rc
     return (int64_t)order.size();
 }
 
+// RecordLocation handles -> (leaf index in key order = the device leaf index, slot)
+uint64_t HostTable::export_locations(uint64_t max, uint64_t *handles, uint32_t *leaf, uint16_t *slot) const {
+    std::vector<uint32_t> order, rank(leaves_.size(), 0xFFFFFFFFu);
+    key_order(order);
+    for (size_t d = 0; d < order.size(); ++d) rank[order[d]] = (uint32_t)d;
+    uint64_t k = 0;
+    for (uint64_t id = 0; id < locpos_.size(); ++id) {
+        if (locpos_[id] == kNoPos) continue;
+        if (k < max) {
+            handles[k] = id + 1;
+            leaf[k] = rank[locpos_[id] >> 16];
+            slot[k] = (uint16_t)(locpos_[id] & 0xFFFF);
+        }
+        ++k;
+    }
+    return k;
+}
+
+void HostTable::resolve_locations(const uint64_t *handles, uint64_t n, uint32_t *leaf, uint16_t *slot) const {
+    std::vector<uint32_t> order, rank(leaves_.size(), 0xFFFFFFFFu);
+    key_order(order);
+    for (size_t d = 0; d < order.size(); ++d) rank[order[d]] = (uint32_t)d;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t h = handles[i];
+        const uint64_t pos = (h == 0 || h > locpos_.size()) ? kNoPos : locpos_[h - 1];
+        leaf[i] = pos == kNoPos ? 0xFFFFFFFFu : rank[pos >> 16];
+        slot[i] = pos == kNoPos ? 0xFFFF : (uint16_t)(pos & 0xFFFF);
+    }
+}
+
 // ---- leaf-level snapshot in the reference's block format --------------------------------
 // Block = LeafNode (b_tree.h:571-740): [vptr 8][is_leaf 1 + pad 7][NodeHeader: size u32,
 // sorted_count u32, next_record_slot u32 + pad 4, StatusWord u64 (version_store.h:158-231:
 // frozen bit 60, record count 44-59, block size 22-43, delete size 0-21)], then
 // RecordMetadata{meta, next_ptr, loc_ptr} (record_meta.h:30-60) per slot, records
 // [key][pad to 8][payload] at meta.offset growing down from `size`.  Canonical form (the
-// oracle's orc_export_leaf_images uses the same): next_ptr / loc_ptr = 0, record bytes not
-// referenced by a non-zero meta word = 0.  Separators: key_words() u64 words of key bytes
+// oracle's orc_export_leaf_images uses the same): next_ptr = 0, loc_ptr = the record's
+// RecordLocation handle (location id + 1, 0 = none), record bytes not referenced by a non-zero
+// meta word = 0.  Separators: key_words() u64 words of key bytes
 // per leaf (little-endian), length 0xFFFF = +inf.
 static constexpr uint32_t kLeafHdr = 40, kOffIsLeaf = 8, kOffSize = 16, kOffSorted = 20, kOffStatus = 32;
 
@@ -873,7 +922,9 @@ int64_t HostTable::export_leaf_images(uint64_t max_leaves, uint8_t *blocks, uint
         const size_t b = (size_t)order[d] * cap_;
         for (uint32_t s = 0; s < L.count; ++s) {
             const uint64_t m = meta_[b + s];
+            const uint64_t lp = loc_[b + s];  // loc_ptr: the record's location handle
             std::memcpy(dst + kLeafHdr + 24 * s, &m, 8);
+            std::memcpy(dst + kLeafHdr + 24 * s + 16, &lp, 8);
             if (!m) continue;
             const uint32_t off = meta_offset(m), kl = meta_keylen(m);
             key_to_bytes(slot_key(b + s), kb, uns_);
@@ -965,10 +1016,23 @@ uint64_t HostTable::import_leaf_images(const uint8_t *blocks, uint64_t n, uint32
         if (i > 0) leaves_[id - 1].next = (int32_t)id;
         const size_t b = (size_t)id * cap_;
         for (uint32_t s = 0; s < L.count; ++s) {
-            uint64_t m;
+            uint64_t m, lp;
             std::memcpy(&m, blk + kLeafHdr + 24 * s, 8);
+            std::memcpy(&lp, blk + kLeafHdr + 24 * s + 16, 8);
             meta_[b + s] = m;
             next_[b + s] = 0;
+            // the block's loc_ptr is kept as the record's location handle (0: a new one)
+            if (m || lp) {
+                if (lp == 0) {
+                    locpos_.push_back(kNoPos);
+                    lp = locpos_.size();
+                }
+                if (lp >= 0xFFFFFFFFull) bad("location handle out of range");
+                if (locpos_.size() < lp) locpos_.resize(lp, kNoPos);
+                if (locpos_[lp - 1] != kNoPos) bad("location handle " + std::to_string(lp) + " used twice");
+                locpos_[lp - 1] = (uint64_t)id << 16 | s;
+                loc_[b + s] = (uint32_t)lp;
+            }
             if (!m) {
                 clear_slot_key(b + s);
                 image_[b + s] = 0;

@@ -151,6 +151,16 @@ public:
     int32_t head_ = 0;
     uint32_t nleaves_live_ = 0;
 
+    // RecordLocation indirection (record_location.h:13-42; BTree::RecordIndirectLocation,
+    // b_tree.cpp:2034-2050): one location per Insert attempt, numbered in allocation order as
+    // the reference's indirection offsets are; a record's location follows it through splits
+    // (LeafNode::CopyFrom, b_tree.cpp:1520-1527).  Handle = location id + 1.
+    static constexpr uint64_t kNoPos = ~0ull;
+    std::vector<uint32_t> loc_;      // [leaf*cap + slot] -> handle (0 = none)
+    std::vector<uint64_t> locpos_;   // location id -> host leaf << 16 | slot, kNoPos = dropped
+    uint64_t export_locations(uint64_t max, uint64_t *handles, uint32_t *leaf, uint16_t *slot) const;
+    void resolve_locations(const uint64_t *handles, uint64_t n, uint32_t *leaf, uint16_t *slot) const;
+
     ChunkedVector<ImageDesc, (1u << 20)> images_;
     ChunkedArena arena_;
     std::vector<CopyHdr> copies_;

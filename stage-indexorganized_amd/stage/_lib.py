@@ -75,6 +75,8 @@ SIGNATURES = {
     "stage_sharded_owner_rows": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.POINTER(c_vp), c_u64p]),
     "stage_export_leaf_images": (ctypes.c_int64, [c_vp, ctypes.c_uint64, c_vp, c_vp, c_vp]),
     "stage_import_leaf_images": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64, ctypes.c_uint32, c_vp, c_vp, c_u64p]),
+    "stage_export_locations": (ctypes.c_int64, [c_vp, ctypes.c_uint64, c_vp, c_vp, c_vp]),
+    "stage_resolve_locations": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64, c_vp, c_vp]),
     "stage_host_alloc": (ctypes.c_int, [ctypes.c_uint64, ctypes.POINTER(c_vp)]),
     "stage_host_free": (ctypes.c_int, [c_vp]),
     "stage_probe_host": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, ctypes.c_uint64, c_vp, c_vp]),

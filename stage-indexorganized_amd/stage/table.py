@@ -287,6 +287,27 @@ class Table:
                                              _ptr(sl), ctypes.byref(n)), "import_leaf_images")
         return n.value
 
+    def export_locations(self):
+        """RecordLocation handles of every live record -> (handles, leaf in key order, slot)"""
+        n = lib().stage_export_locations(self.h, 0, None, None, None)
+        if n < 0:
+            raise RuntimeError("export_locations failed")
+        h = np.zeros(n, np.uint64)
+        lf = np.zeros(n, np.uint32)
+        sl = np.zeros(n, np.uint16)
+        if n:
+            lib().stage_export_locations(self.h, n, h.ctypes.data, lf.ctypes.data, sl.ctypes.data)
+        return h, lf, sl
+
+    def resolve_locations(self, handles):
+        """where each RecordLocation handle's record is now: (leaf, slot); 0xFFFFFFFF / 0xFFFF = gone"""
+        handles = np.ascontiguousarray(handles, np.uint64)
+        lf = np.zeros(handles.size, np.uint32)
+        sl = np.zeros(handles.size, np.uint16)
+        check(lib().stage_resolve_locations(self.h, handles.ctypes.data, handles.size, lf.ctypes.data, sl.ctypes.data),
+              "resolve_locations")
+        return lf, sl
+
     @property
     def key_words(self):
         return int(lib().stage_key_words(self.h))

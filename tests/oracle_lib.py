@@ -59,6 +59,8 @@ _SIG = {
     "orc_update_batch": (u64, [vp, vp, u32, u64, u32, vp, u32, vp, vp, vp]),
     "orc_tree_set_bulk": (None, [vp, ctypes.c_int]),
     "orc_load_ycsb_parallel": (u64, [vp, u64, u64, u32, ctypes.c_int, ctypes.c_int]),
+    "orc_resolve_locations": (None, [vp, vp, u64, vp, vp]),
+    "orc_location_count": (u64, [vp]),
     "orc_key_compare": (ctypes.c_int, [vp, u32, vp, u32]),
     "orc_murmur64a": (u64, [vp, ctypes.c_int, u64]),
     "orc_murmur64a_batch": (None, [vp, u64, ctypes.c_int, u64, vp]),
@@ -262,6 +264,16 @@ class OracleTree:
         got = lib().orc_export_leaf_images_k(self.t, nl, blocks.ctypes.data, sk.ctypes.data, kwords, sl.ctypes.data)
         assert got == nl
         return blocks, (sk if kwords == 1 else sk.reshape(nl, kwords)), sl
+
+    def resolve_locations(self, handles):
+        handles = np.ascontiguousarray(handles, np.uint64)
+        lf = np.zeros(handles.size, np.uint32)
+        sl = np.zeros(handles.size, np.uint16)
+        lib().orc_resolve_locations(self.t, handles.ctypes.data, handles.size, lf.ctypes.data, sl.ctypes.data)
+        return lf, sl
+
+    def location_count(self):
+        return int(lib().orc_location_count(self.t))
 
     def export_leaves(self, cap):
         nl = self.stats()["leaves"]
