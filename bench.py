@@ -545,6 +545,36 @@ def cpu_legs(orc, args, res, threads, c2_check=None, c4_check=None, c3=None):
     return out
 
 
+def tpcc_tables(args, seed=7):
+    """DISTRICT / ORDER_LINE / STOCK rows with the reference's key and payload layouts
+    (tpcc_record.h), generated vectorised: W warehouses x 10 districts x 3000 orders of 5..15
+    lines, `items` stock rows per warehouse.  First payload columns: D_NEXT_O_ID, OL_I_ID,
+    S_QUANTITY (int32)."""
+    rng = np.random.default_rng(seed)
+    W, I, D, O = args.warehouses, args.items, 10, 3000
+    out = {}
+    wi = np.stack(np.meshgrid(np.arange(1, W + 1), np.arange(1, I + 1), indexing="ij"), -1).reshape(-1, 2)
+    sk = np.ascontiguousarray(wi.astype(np.int64)).view(np.uint8).reshape(-1, 16)
+    sp = rng.integers(0, 256, (sk.shape[0], 400), dtype=np.uint8)
+    sp[:, :4] = rng.integers(10, 101, sk.shape[0]).astype(np.int32).view(np.uint8).reshape(-1, 4)
+    out["stock"] = (sk, sp)
+    wd = np.stack(np.meshgrid(np.arange(1, W + 1), np.arange(1, D + 1), indexing="ij"), -1).reshape(-1, 2)
+    dk = np.ascontiguousarray(wd.astype(np.int64)).view(np.uint8).reshape(-1, 16)
+    dp = rng.integers(0, 256, (dk.shape[0], 143), dtype=np.uint8)
+    dp[:, :4] = np.full(dk.shape[0], O + 1, np.int32).view(np.uint8).reshape(-1, 4)
+    out["district"] = (dk, dp)
+    wdo = np.stack(np.meshgrid(np.arange(1, W + 1), np.arange(1, D + 1), np.arange(1, O + 1), indexing="ij"),
+                   -1).reshape(-1, 3)
+    nl = rng.integers(5, 16, wdo.shape[0])
+    rep = np.repeat(wdo, nl, axis=0)
+    ln = np.arange(rep.shape[0]) - np.repeat(np.cumsum(nl) - nl, nl) + 1
+    ok = np.ascontiguousarray(np.concatenate([rep, ln[:, None]], 1).astype(np.int64)).view(np.uint8).reshape(-1, 32)
+    op = rng.integers(0, 256, (ok.shape[0], 60), dtype=np.uint8)
+    op[:, :4] = rng.integers(1, I + 1, ok.shape[0]).astype(np.int32).view(np.uint8).reshape(-1, 4)
+    out["order_line"] = (ok, op)
+    return out
+
+
 def run_tpcc(args):
     """TPC-C stock-level through the path (stage_tpcc_stock_level), one GPU."""
     L = stage.lib()

@@ -132,13 +132,16 @@ __global__ void wp_speculate(WpArgs a, DevTable t, uint8_t *__restrict__ rcs, ui
 // loads independent), takes the first success in batch order and restarts behind it: a hot
 // key's long run of NotNeededUpdate / DIRTY ops goes 512 ops per pass.
 constexpr int kFinishChunks = 8;
+constexpr uint32_t kBigGroup = 2048;  // ops from the first failure on: a workgroup finishes it (wp_finish_big)
 __global__ __launch_bounds__(256) void wp_finish_groups(WpArgs a, DevTable t, uint8_t *__restrict__ rcs,
                                                         uint8_t *__restrict__ succ, int32_t *__restrict__ prev,
-                                                        const uint32_t *__restrict__ first_fail) {
+                                                        const uint32_t *__restrict__ first_fail,
+                                                        const uint32_t *__restrict__ gend) {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t base_q = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64;
     const uint64_t mine = base_q + lane;
-    const bool start = mine < a.n && a.loc[mine] != a.none && a.gs[mine] == mine && first_fail[mine] != 0xFFFFFFFFu;
+    const bool start = mine < a.n && a.loc[mine] != a.none && a.gs[mine] == mine && first_fail[mine] != 0xFFFFFFFFu &&
+                       gend[mine] - first_fail[mine] < kBigGroup;
     uint64_t groups = __builtin_amdgcn_ballot_w64(start);
     while (groups) {
         const uint64_t g = base_q + __builtin_ctzll(groups);
@@ -186,6 +189,82 @@ __global__ __launch_bounds__(256) void wp_finish_groups(WpArgs a, DevTable t, ui
             }
             if (!whole) break;  // the group ends inside this pass
             pos += 64 * kFinishChunks;
+        }
+    }
+}
+
+// group extents: gend[g] = one past the last sorted position of the group starting at g
+__global__ void wp_group_ends(WpArgs a, uint32_t *__restrict__ gend) {
+    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= a.n) return;
+    if (q + 1 == a.n || a.loc[q + 1] != a.loc[q]) gend[a.gs[q]] = (uint32_t)(q + 1);
+}
+
+// failing groups with at least kBigGroup ops from their first failure on (a hot key's run of
+// NotNeededUpdate / DIRTY ops) -> list
+__global__ void wp_big_groups(WpArgs a, const uint32_t *__restrict__ first_fail, const uint32_t *__restrict__ gend,
+                              uint32_t *__restrict__ list, uint32_t *__restrict__ count) {
+    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= a.n || a.loc[q] == a.none || a.gs[q] != q || first_fail[q] == 0xFFFFFFFFu) return;
+    if (gend[q] - first_fail[q] >= kBigGroup) list[atomicAdd(count, 1u)] = (uint32_t)q;
+}
+
+// step 3b for big groups: one 1024-thread workgroup per group, 16 waves x kFinishChunks x 64 =
+// 8192 ops evaluated against the last success per pass, the first success in batch order
+// found across the waves through LDS
+__global__ __launch_bounds__(1024) void wp_finish_big(WpArgs a, DevTable t, uint8_t *__restrict__ rcs,
+                                                      uint8_t *__restrict__ succ, int32_t *__restrict__ prev,
+                                                      const uint32_t *__restrict__ first_fail,
+                                                      const uint32_t *__restrict__ gend,
+                                                      const uint32_t *__restrict__ list,
+                                                      const uint32_t *__restrict__ count) {
+    __shared__ uint64_t s_first[16];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    constexpr uint64_t kPass = 16ull * kFinishChunks * 64;
+    const uint32_t nbig = *count;
+    for (uint32_t i = blockIdx.x; i < nbig; i += gridDim.x) {
+        const uint64_t g = list[i];
+        const uint64_t l = a.loc[g], end = gend[g];
+        const SlotInfo base = t.slot[l];
+        const uint64_t f = first_fail[g];
+        int64_t last = f > g ? (int64_t)f - 1 : -1;  // [g, f) all succeeded
+        uint64_t pos = f;
+        while (pos < end) {
+            uint8_t r[kFinishChunks];
+            uint64_t mine_first = ~0ull;
+#pragma unroll
+            for (int k = 0; k < kFinishChunks; ++k) {
+                const uint64_t q = pos + (uint64_t)wv * (kFinishChunks * 64) + 64 * k + lane;
+                r[k] = q < end ? wp_eval(a, t, q, last, base) : (uint8_t)0xFF;
+                if (r[k] == STAGE_RC_OK && q < mine_first) mine_first = q;
+            }
+            // the wave's first success, then the block's
+            uint64_t wf = mine_first;
+            for (int o = 32; o > 0; o >>= 1) {
+                const uint64_t x = __shfl_xor(wf, o, 64);
+                wf = x < wf ? x : wf;
+            }
+            __syncthreads();  // the previous pass's readers of s_first are done
+            if (lane == 0) s_first[wv] = wf;
+            __syncthreads();
+            uint64_t bf = ~0ull;
+#pragma unroll
+            for (int w = 0; w < 16; ++w) bf = s_first[w] < bf ? s_first[w] : bf;
+#pragma unroll
+            for (int k = 0; k < kFinishChunks; ++k) {
+                const uint64_t q = pos + (uint64_t)wv * (kFinishChunks * 64) + 64 * k + lane;
+                if (q < end && q <= bf) {
+                    rcs[q] = r[k];
+                    succ[q] = q == bf;
+                    prev[q] = (int32_t)last;
+                }
+            }
+            if (bf != ~0ull) {
+                last = (int64_t)bf;
+                pos = bf + 1;
+            } else {
+                pos += kPass;
+            }
         }
     }
 }
@@ -372,7 +451,7 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         };
         const uint64_t o_pout = take(n * 32), o_loc0 = take(n * 8), o_loc = take(n * 8), o_op0 = take(n * 4),
                        o_op = take(n * 4), o_head = take(n * 4), o_gs = take(n * 4), o_rcs = take(n), o_succ = take(n),
-                       o_prev = take(n * 4), o_ff = take(n * 4), o_ls = take(n * 4), o_flags = take(n * 8),
+                       o_prev = take(n * 4), o_ff = take(n * 4), o_ls = take(n * 4), o_gend = take(n * 4), o_big = take(n * 4), o_flags = take(n * 8),
                        o_ranks = take(n * 8), o_fin = take(n * sizeof(FinRec)), o_tot = take(16),
                        o_cub = take(cub_bytes);
         uint8_t *buf = scratch_bytes(dv, off);
@@ -388,6 +467,8 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         auto *prev = (int32_t *)(buf + o_prev);
         auto *ff = (uint32_t *)(buf + o_ff);
         auto *ls = (uint32_t *)(buf + o_ls);
+        auto *gend = (uint32_t *)(buf + o_gend);
+        auto *big = (uint32_t *)(buf + o_big);
         auto *flags = (uint64_t *)(buf + o_flags);
         auto *ranks = (uint64_t *)(buf + o_ranks);
         auto *fin = (FinRec *)(buf + o_fin);
@@ -410,7 +491,11 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         hip_check(hipMemsetAsync(ls, 0, n * 4, s), "memset");
         hip_check(hipMemsetAsync(fin, 0xFF, n * sizeof(FinRec), s), "memset");
         wp_speculate<<<blocks_for(n, 256), 256, 0, s>>>(a, view, rcs, succ, prev, ff);
-        wp_finish_groups<<<blocks_for(n, 256), 256, 0, s>>>(a, view, rcs, succ, prev, ff);
+        wp_group_ends<<<blocks_for(n, 256), 256, 0, s>>>(a, gend);
+        hip_check(hipMemsetAsync(tot + 1, 0, 4, s), "memset");  // big-group count (tot is rewritten in step 4)
+        wp_big_groups<<<blocks_for(n, 256), 256, 0, s>>>(a, ff, gend, big, (uint32_t *)(tot + 1));
+        wp_finish_groups<<<blocks_for(n, 256), 256, 0, s>>>(a, view, rcs, succ, prev, ff, gend);
+        wp_finish_big<<<256, 1024, 0, s>>>(a, view, rcs, succ, prev, ff, gend, big, (uint32_t *)(tot + 1));
         // 4. number
         wp_flags<<<blocks_for(n, 256), 256, 0, s>>>(a, succ, flags);
         cb = cub_bytes;
