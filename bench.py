@@ -894,7 +894,8 @@ def c3_leg(tab, args, stream, nthreads, steps, warmup):
                                            "not_found": int(hist[0])},
                     "timed": "value: device probes of the read shares; ops_per_s_incl_writes: the whole loop "
                              "(write path + probes), epoch inputs resident in HBM beforehand"},
-         "roofline": hbm_roofline(per_unit, ops_done / steps, kern_ms, "probe_kernel (read ids, chain walks)")}
+         "roofline": hbm_roofline(per_unit, ops_done / steps, kern_ms, "probe_kernel (read ids, chain walks)",
+                                  *traffic_from_profile(args.batch, args.rows, "pmc_probe_c3.json"))}
     d["roofline"]["algorithmic_bytes"] = f"{BYTES_PER_LOOKUP} + {HOP_BYTES} x mean hops ({mean_hops:.4f})"
     rec = {"record": ycsb_b.record, "reads": last["reads"], "rids": last["rids"], "check": check_sample}
     for ep in epochs:

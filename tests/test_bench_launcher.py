@@ -67,3 +67,11 @@ def test_default_args_carry_the_nested_legs():
     a = bench.parse([])
     assert not a.no_extras and a.c3_epochs >= 1 and a.scan_batch == 1 << 18 and a.inflight_share > 0
     assert a.cpu_rows == 0 and a.cpu_threads == 0
+
+
+def test_tpcc_tables_small():
+    a = bench.parse(["--config", "tpcc", "--warehouses", "1", "--items", "200"])
+    d = bench.tpcc_tables(a)
+    assert d["stock"][0].shape == (200, 16) and d["district"][0].shape == (10, 16)
+    assert d["order_line"][0].shape[1] == 32 and d["order_line"][1].shape[1] == 60
+    assert callable(bench.run_tpcc) and callable(bench.run_chq2) and callable(bench.c3_leg) and callable(bench.c4_leg)
