@@ -889,6 +889,12 @@ def c3_leg(tab, args, stream, nthreads, steps, warmup):
                     "updates_in_flight": int(sum(ep["inflight"] for ep in epochs[warm:])),
                     "write_path": args.write_path, "write_s": round(write_s, 4), "loop_s": round(loop_s, 4),
                     "epoch_prep_s_untimed": round(prep_s, 2), "mean_chain_hops": round(mean_hops, 4),
+                    # copies / versions / heap images are append-only (no GC, as the reference
+                    # with its cleaner off): each successful update takes one of each, and the
+                    # 30-bit indices end the write path after about this many more updates
+                    "write_capacity_updates_left": int((1 << 30) - 1 - tab.stats()["records"] -
+                                                       tab.stats()["versions"] -
+                                                       sum(ep["keys"].size for ep in epochs)),
                     "read_status_counts": {"latest": int(hist[1]), "copy": int(hist[2]), "old": int(hist[3]),
                                            "fail": int(hist[4]), "chain_miss": int(hist[5]),
                                            "not_found": int(hist[0])},

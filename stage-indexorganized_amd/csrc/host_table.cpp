@@ -731,7 +731,10 @@ uint64_t HostTable::update_batch(const uint8_t *keys, uint32_t key_stride, uint6
                 }
                 L.images.push_back(d);
                 image_[i] = kLocalImg | (uint32_t)(L.images.size() - 1);
-                L.touched.push_back(i);
+                // once per slot (a slot's ops are consecutive here): the relocation below must
+                // run once per slot word -- the small-batch gate keeps global indices below
+                // kLocalRef, this keeps it independent of that gate
+                if (L.touched.empty() || L.touched.back() != i) L.touched.push_back(i);
                 rc[op] = STAGE_RC_OK;
                 // CommitTransaction UPDATE entry (transaction_manager.cpp:610-676)
                 const uint32_t cid = commit_ids ? commit_ids[op] : 0;

@@ -221,7 +221,7 @@ def test_hot_key_groups_finished_by_workgroups(gpu):
         bad = np.nonzero(rc != exp)[0]
         assert bad.size == 0, (epoch, bad[:5], rc[bad[:5]], exp[bad[:5]], keys[bad[:5]])
         assert ok == int((exp == stage.RC_OK).sum())
-        assert (exp[keys == hot[0]] == stage.RC_NOT_NEEDED_UPDATE).sum() > 2048
+        assert (keys == hot[0]).sum() > 4096 and (exp[keys == hot[0]] == stage.RC_NOT_NEEDED_UPDATE).sum() > 1000
         probe = np.concatenate([hot, rng.integers(0, n, 2000).astype(np.uint64)])
         for rid in (0, counter // 3, counter // 2, counter - 5, 0xFFFFFFFE):
             check_probe(tab, orc, probe, 8, read_ids=np.full(probe.size, rid, np.uint32))
