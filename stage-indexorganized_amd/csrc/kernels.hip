@@ -899,6 +899,212 @@ __global__ __launch_bounds__(256) void scan_first_kernel(DevTable t, const uint6
     }
 }
 
+// scan_first_kernel with NS scans of a chunk run in lockstep by one wave: every dependent load
+// step (group max keys, a slot group's visibility mask + key columns, the kept records' slot
+// words, the next leaf's separator) is issued for the NS scans together, so a wave keeps NS
+// times the loads in flight (the single-scan form is latency-bound: 61 % of wave cycles parked
+// on s_waitcnt, profiles/r02).  The visibility mask and key columns of a group are loaded
+// together (one round trip per group instead of two).  Semantics per scan are those of
+// scan_one_compact + FirstPrefixSink (fixed-width keys): RangeScanBySize's first to_scan+1
+// qualifying records in slot order, sorted; the first visible tuple with the start key's
+// prefix among the first `remaining` of them; the Iterator continuation (le_child = false from
+// the last popped key, a re-popped start key ends the scan).
+template <int SPL, int KW, int NS>
+__global__ __launch_bounds__(256) void scan_first_multi_kernel(DevTable t, const uint64_t *__restrict__ keys,
+                                                               uint64_t n, uint32_t scan_size,
+                                                               const uint32_t *__restrict__ rids, uint32_t words,
+                                                               uint32_t *__restrict__ img_out,
+                                                               uint8_t *__restrict__ st_out) {
+    __shared__ uint64_t s_keys[4][NS][64 * KW];
+    __shared__ uint32_t s_slot[4][NS][64];
+    const uint32_t lane = lane_id(), wv = uni32(threadIdx.x >> 6);
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint32_t len = t.key_width;
+    for (uint64_t c0 = wave * kFirstChunk; c0 < n; c0 += nwaves * kFirstChunk) {
+        const uint64_t i = c0 + lane;
+        const bool valid = lane < (uint32_t)kFirstChunk && i < n;
+        uint64_t ok[KW];
+        load_okey<KW>(keys, i, valid, len, ok);
+        const uint32_t leafv = valid ? resolve_leaf<false, KW>(t, ok, len, true) : 0u;
+        const uint32_t ridv = valid && rids ? rids[i] : 0xFFFFFFFEu;
+        const int cnt = (int)((n - c0) < (uint64_t)kFirstChunk ? (n - c0) : (uint64_t)kFirstChunk);
+        uint32_t my_img = 0xFFFFFFFFu, my_st = ST_NOT_FOUND;
+        for (int j0 = 0; j0 < cnt; j0 += NS) {
+            // per-scan state (wave-uniform)
+            uint64_t x[NS][KW], pre[NS][KW];
+            uint32_t leaf[NS], remaining[NS], rid[NS], img[NS], st[NS];
+            bool live[NS], cont[NS];
+#pragma unroll
+            for (int k = 0; k < NS; ++k) {
+                const int j = j0 + k < cnt ? j0 + k : j0;
+                live[k] = j0 + k < cnt && scan_size > 0;
+#pragma unroll
+                for (int w = 0; w < KW; ++w) x[k][w] = pre[k][w] = rl64(ok[w], j);
+                leaf[k] = rl32(leafv, j);
+                rid[k] = rl32(ridv, j);
+                remaining[k] = scan_size;
+                img[k] = 0xFFFFFFFFu;
+                st[k] = ST_NOT_FOUND;
+                cont[k] = false;
+            }
+            for (uint32_t guard = 0; guard < scan_size + 2; ++guard) {
+                bool any = false;
+#pragma unroll
+                for (int k = 0; k < NS; ++k) any = any || live[k];
+                if (!any) break;
+                // (A) slot groups that can hold a key >= x: lane g tests group g's max key
+                uint64_t gmx[NS][KW];
+#pragma unroll
+                for (int k = 0; k < NS; ++k) {
+                    const uint64_t *gm = reinterpret_cast<const uint64_t *>(t.head + (uint64_t)leaf[k] * t.head_bytes +
+                                                                            head_gmax_offset(t.cap)) +
+                                         (lane < (uint32_t)SPL ? lane : 0u) * KW;
+#pragma unroll
+                    for (int w = 0; w < KW; ++w) gmx[k][w] = live[k] && lane < (uint32_t)SPL ? gm[w] : 0ull;
+                }
+                uint64_t active[NS];
+                uint32_t kept[NS], to_scan[NS];
+#pragma unroll
+                for (int k = 0; k < NS; ++k) {
+                    active[k] = ballot(live[k] && lane < (uint32_t)SPL && !kw_lt<KW>(gmx[k], x[k]));
+                    kept[k] = 0;
+                    to_scan[k] = remaining[k];
+                }
+                // (B) the groups in slot order until to_scan+1 records are held; the NS scans'
+                // visibility masks and key columns load together
+                for (;;) {
+                    int s[NS];
+                    bool any_g = false;
+#pragma unroll
+                    for (int k = 0; k < NS; ++k) {
+                        s[k] = active[k] && kept[k] <= to_scan[k] ? __builtin_ctzll(active[k]) : -1;
+                        if (s[k] >= 0) active[k] &= active[k] - 1;
+                        any_g = any_g || s[k] >= 0;
+                    }
+                    if (!any_g) break;
+                    uint64_t vm[NS], col[NS][KW];
+#pragma unroll
+                    for (int k = 0; k < NS; ++k) {
+                        const int sg = s[k] >= 0 ? s[k] : 0;
+                        vm[k] = s[k] >= 0 ? head_vis(t, leaf[k], sg) : 0ull;
+#pragma unroll
+                        for (int w = 0; w < KW; ++w)
+                            col[k][w] = s[k] >= 0 ? t.okey[((uint64_t)leaf[k] * KW + w) * t.cap + sg * 64 + lane] : 0ull;
+                    }
+#pragma unroll
+                    for (int k = 0; k < NS; ++k) {
+                        if (s[k] < 0) continue;
+                        const bool vis = (vm[k] >> lane) & 1;
+                        const uint64_t q = ballot(vis && !kw_lt<KW>(col[k], x[k]));
+                        if (!q) continue;
+                        const uint32_t rank = kept[k] + count_below(q);
+                        const bool take = ((q >> lane) & 1) && rank <= to_scan[k];
+                        if (take) {
+#pragma unroll
+                            for (int w = 0; w < KW; ++w) s_keys[wv][k][rank * KW + w] = col[k][w];
+                            s_slot[wv][k][rank] = (uint32_t)(s[k] * 64) + lane;
+                        }
+                        kept[k] += (uint32_t)__builtin_popcountll(ballot(take));
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                // (C) rank the kept records (lane k < m holds record k); (D) their slot words
+                uint64_t mk[NS][KW];
+                uint32_t kr[NS], mslot[NS], e[NS];
+                bool on[NS];
+                SlotInfo si[NS];
+#pragma unroll
+                for (int k = 0; k < NS; ++k) {
+                    const uint32_t m = kept[k];
+                    if (live[k] && m == 0) live[k] = false;  // nothing left in range
+                    const bool mine = live[k] && lane < m;
+#pragma unroll
+                    for (int w = 0; w < KW; ++w) mk[k][w] = mine ? s_keys[wv][k][lane * KW + w] : 0ull;
+                    mslot[k] = mine ? s_slot[wv][k][lane] : 0u;
+                    uint32_t r = 0;
+                    for (uint32_t jj = 0; live[k] && jj < m; ++jj) {
+                        uint64_t kj[KW];
+#pragma unroll
+                        for (int w = 0; w < KW; ++w) kj[w] = s_keys[wv][k][jj * KW + w];
+                        r += (mine && kw_lt<KW>(kj, mk[k])) ? 1u : 0u;
+                    }
+                    kr[k] = r;
+                    if (live[k] && cont[k]) {  // the continuation re-popped the last key: the scan ends
+                        bool eq = true;
+#pragma unroll
+                        for (int w = 0; w < KW; ++w) eq = eq && mk[k][w] == x[k][w];
+                        if (ballot(mine && r == 0 && eq)) live[k] = false;
+                    }
+                    e[k] = m < remaining[k] ? m : remaining[k];
+                    on[k] = live[k] && mine && r < e[k];
+                    si[k] = on[k] ? t.slot[(uint64_t)leaf[k] * t.cap + mslot[k]] : SlotInfo{};
+                }
+                __builtin_amdgcn_wave_barrier();  // the LDS lists are rewritten on the next leaf
+#pragma unroll
+                for (int k = 0; k < NS; ++k) {
+                    if (!live[k]) continue;
+                    uint8_t sv = ST_NOT_FOUND;
+                    uint32_t im = 0xFFFFFFFFu;
+                    bool pass = false;
+                    if (on[k]) {
+                        im = scan_visible(t, si[k], rid[k], sv);
+                        pass = sv == ST_LATEST || sv == ST_OLD;
+#pragma unroll
+                        for (int w = 0; w < KW; ++w)
+                            if ((uint32_t)w < words) pass = pass && mk[k][w] == pre[k][w];
+                    }
+                    uint64_t pm = ballot(pass);
+                    if (pm) {  // the passing record of lowest rank
+                        uint32_t best = 0xFFFFFFFFu;
+                        int bl = 0;
+                        while (pm) {
+                            const int b = __builtin_ctzll(pm);
+                            pm &= pm - 1;
+                            const uint32_t rr = rl32(kr[k], b);
+                            if (rr < best) {
+                                best = rr;
+                                bl = b;
+                            }
+                        }
+                        img[k] = rl32(im, bl);
+                        st[k] = rl32((uint32_t)sv, bl);
+                        live[k] = false;
+                        continue;
+                    }
+                    remaining[k] -= e[k];
+                    if (e[k] < kept[k] || remaining[k] == 0) {
+                        live[k] = false;
+                        continue;
+                    }
+                    // last record popped: continue from its key with le_child = false
+                    const uint64_t lm = ballot(lane < kept[k] && kr[k] == kept[k] - 1);
+                    const int b = __builtin_ctzll(lm);
+#pragma unroll
+                    for (int w = 0; w < KW; ++w) x[k][w] = rl64(mk[k][w], b);
+                    cont[k] = true;
+                }
+                // (E) the continuing scans' next leaves, loads together
+#pragma unroll
+                for (int k = 0; k < NS; ++k)
+                    if (live[k]) leaf[k] = uni32(next_leaf_after<false, KW>(t, leaf[k], x[k], len));
+            }
+#pragma unroll
+            for (int k = 0; k < NS; ++k)
+                if (lane == (uint32_t)(j0 + k)) {
+                    my_img = img[k];
+                    my_st = st[k];
+                }
+        }
+        if (valid) {
+            img_out[i] = my_img;
+            st_out[i] = (uint8_t)my_st;
+        }
+    }
+}
+
 // One wave per scan (grid-stride over scans): the start key's descent is wave-uniform, and a
 // wide grid keeps many scans -- and their R rows in flight each -- resident per CU.
 template <bool VARLEN, int SPL, int R, int KW = 1, bool VIS = false>
@@ -1220,8 +1426,17 @@ hipError_t launch_scan_first(const DevTable &t, const uint64_t *keys, uint64_t n
     if (n == 0) return hipSuccess;
     if (t.key_width == 0 || scan_size == 0 || scan_size > 63) return hipErrorInvalidValue;
     const int blocks = grid_for((n + kFirstChunk - 1) / kFirstChunk, 4, tune.max_blocks > 0 ? tune.max_blocks : 16384);
-#define STAGE_FIRST(S, KW) \
-    scan_first_kernel<S, KW><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words, img_out, st_out)
+    // NS scans per wave in lockstep (scan_first_multi_kernel); STAGE_SL_SCANS=1 = one at a time
+    const int ns = tune.first_scans > 0 ? tune.first_scans : 2;
+#define STAGE_FIRST(S, KW)                                                                                  \
+    if (ns == 1)                                                                                            \
+        scan_first_kernel<S, KW><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words, img_out, st_out); \
+    else if (ns == 4)                                                                                       \
+        scan_first_multi_kernel<S, KW, 4><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words, img_out,   \
+                                                                 st_out);                                   \
+    else                                                                                                    \
+        scan_first_multi_kernel<S, KW, 2><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words, img_out,   \
+                                                                 st_out)
 #define STAGE_FIRST_K(KW)                      \
     switch (t.cap / 64) {                      \
         case 1: STAGE_FIRST(1, KW); break;     \
