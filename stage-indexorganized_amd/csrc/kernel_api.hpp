@@ -35,7 +35,7 @@ hipError_t launch_probe(const DevTable &t, const uint64_t *keys, const uint16_t 
 struct ScanTuning {
     int rows = 4;        // tuple rows in flight per wave (2, 4 or 8)
     int max_blocks = 0;  // 0 = default grid cap (16384 blocks of 256 threads)
-    int first_scans = 0; // scans per wave in lockstep of the first-tuple scans (1, 2, 4; 0 = 2)
+    int first_scans = 0; // scans per wave in lockstep of the first-tuple scans (1, 2, 4; 0 = 1)
 };
 
 // row_status != nullptr: IndexScanExecutor range semantics (per-record visibility for
