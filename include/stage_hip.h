@@ -401,10 +401,13 @@ int stage_event_record(void *ev, void *stream);
 int stage_event_elapsed(void *ev_start, void *ev_stop, float *ms);
 
 /* ---- YCSB harness generators (benchmark/benchmark_common.h:12-105) -----------------------
- * FastRandom(seed) stream and ZipfDistribution(n, theta).GetNextNumber() draws in [1, n]. */
+ * FastRandom(seed) stream and ZipfDistribution(n, theta).GetNextNumber() draws in [1, n], the
+ * generator seeded FastRandom(seed) (the reference seeds it with rand()); stage_zipf_zeta =
+ * ZipfDistribution::zeta (benchmark_common.h:80-84), bit-identical to its serial sum. */
 int stage_fastrandom_next(uint64_t seed, uint64_t count, uint64_t *out);
 int stage_zipf_draws(uint64_t n, double theta, uint64_t seed, uint64_t count, uint64_t *out,
                      int nthreads);
+int stage_zipf_zeta(uint64_t n, double theta, double *out);
 
 #ifdef __cplusplus
 }

@@ -1,8 +1,12 @@
 // ycsb_gen.cpp -- the YCSB driver's key generators (benchmark/benchmark_common.h:12-105),
 // restated for the harness with explicit seeds (the reference seeds with rand() after
 // srand(time(0)), ycsb_workload.cpp:520, so its streams are not reproducible).
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstring>
+#include <map>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -39,28 +43,55 @@ struct FastRandom {  // Java LCG, benchmark_common.h:12-64
     }
 };
 
-// ZipfDistribution::zeta (benchmark_common.h:80-84); sequential as the reference up to
-// 2^25 terms, fixed 64-way chunking above (deterministic, not bit-identical to a serial sum)
-double zeta(uint64_t n, double theta) {
-    if (n <= (1ull << 25)) {
+// ZipfDistribution::zeta (benchmark_common.h:80-84), bit-identical to the reference's serial
+// sum for every n: the pow() terms of a block are computed by worker threads, the block is then
+// added in the reference's order (i = 1, 2, ...) on this thread.  Cached per (n, theta): the
+// drivers draw many streams over one key range.
+double zeta_serial(uint64_t n, double theta) {
+    constexpr uint64_t kBlock = 1ull << 20;
+    if (n <= kBlock) {
         double sum = 0;
         for (uint64_t i = 1; i <= n; i++) sum += std::pow(1.0 / (double)i, theta);
         return sum;
     }
-    const int chunks = 64;
-    std::vector<double> part(chunks, 0.0);
-    std::vector<std::thread> th;
-    for (int c = 0; c < chunks; ++c)
-        th.emplace_back([&, c] {
-            uint64_t b = 1 + n * (uint64_t)c / chunks, e = n * (uint64_t)(c + 1) / chunks;
-            double s = 0;
-            for (uint64_t i = b; i <= e; i++) s += std::pow(1.0 / (double)i, theta);
-            part[c] = s;
-        });
-    for (auto &x : th) x.join();
+    const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<double> buf[2] = {std::vector<double>(kBlock), std::vector<double>(kBlock)};
+    auto fill = [&](std::vector<double> &dst, uint64_t b, uint64_t e) {  // terms b..e-1 (1-based)
+        std::vector<std::thread> th;
+        for (unsigned k = 0; k < nt; ++k)
+            th.emplace_back([&, k] {
+                const uint64_t lo = b + (e - b) * k / nt, hi = b + (e - b) * (k + 1) / nt;
+                for (uint64_t i = lo; i < hi; ++i) dst[i - b] = std::pow(1.0 / (double)i, theta);
+            });
+        for (auto &x : th) x.join();
+    };
     double sum = 0;
-    for (double v : part) sum += v;
+    uint64_t b = 1;
+    fill(buf[0], 1, std::min(n + 1, 1 + kBlock));
+    for (int cur = 0; b <= n; cur ^= 1) {
+        const uint64_t e = std::min(n + 1, b + kBlock);
+        const uint64_t nb = e, ne = std::min(n + 1, nb + kBlock);
+        std::thread next;  // the next block's terms while this block is summed
+        if (nb <= n) next = std::thread([&, nb, ne, cur] { fill(buf[cur ^ 1], nb, ne); });
+        const double *t = buf[cur].data();
+        for (uint64_t i = 0; i < e - b; ++i) sum += t[i];
+        if (next.joinable()) next.join();
+        b = e;
+    }
     return sum;
+}
+
+double zeta(uint64_t n, double theta) {
+    static std::mutex mu;
+    static std::map<std::pair<uint64_t, uint64_t>, double> cache;
+    uint64_t tb;
+    std::memcpy(&tb, &theta, 8);
+    std::lock_guard<std::mutex> g(mu);
+    auto it = cache.find({n, tb});
+    if (it != cache.end()) return it->second;
+    const double z = zeta_serial(n, theta);
+    cache.emplace(std::make_pair(n, tb), z);
+    return z;
 }
 
 }  // namespace
@@ -69,6 +100,12 @@ extern "C" int stage_fastrandom_next(uint64_t seed, uint64_t count, uint64_t *ou
     if (!out && count) return STAGE_E_ARG;
     FastRandom r(seed);
     for (uint64_t i = 0; i < count; ++i) out[i] = r.next64();
+    return STAGE_OK;
+}
+
+extern "C" int stage_zipf_zeta(uint64_t n, double theta, double *out) {
+    if (!out) return STAGE_E_ARG;
+    *out = zeta(n, theta);
     return STAGE_OK;
 }
 

@@ -119,6 +119,7 @@ SIGNATURES = {
     "stage_fastrandom_next": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint64, c_vp]),
     "stage_zipf_draws": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_double, ctypes.c_uint64, ctypes.c_uint64, c_vp,
                                         ctypes.c_int]),
+    "stage_zipf_zeta": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_double, c_vp]),
 }
 
 

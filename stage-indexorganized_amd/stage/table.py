@@ -582,6 +582,12 @@ def zipf_draws(n, theta, seed, count, nthreads=8):
     return out
 
 
+def zipf_zeta(n, theta):
+    out = np.zeros(1, np.float64)
+    check(lib().stage_zipf_zeta(n, theta, out.ctypes.data), "zeta")
+    return float(out[0])
+
+
 def fastrandom(seed, count):
     out = np.empty(count, np.uint64)
     check(lib().stage_fastrandom_next(seed, count, out.ctypes.data), "fastrandom")
