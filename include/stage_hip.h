@@ -265,7 +265,15 @@ int stage_index_scan_batch(stage_table *t, const uint64_t *d_start_keys, const u
  *   blocks until its own result (stage_probe_out + [key padded to 8][payload] in `record`,
  *   either may be NULL) is filled.  stats[0] = batches, [1] = reads, [2] = full batches.
  *   Writers must not stage_sync while readers are running (the host is the single writer and
- *   publishes between epochs, as for every other device entry point). */
+ *   publishes between epochs, as for every other device entry point).
+ * stage_reader_create_resident: the same adapter without a launch per batch: `waves` one-wave
+ *   workgroups stay resident on the device and poll a ring of `ring_slots` requests (a multiple
+ *   of 64 * waves; consecutive tickets go to different waves) in pinned host memory; a caller takes a ticket, writes its request into the slot,
+ *   publishes it and spins until the device publishes the results in the slot.  Each device
+ *   instance ends after `life_us` (a keeper thread queues the next one behind it, so no wave
+ *   outlives a bounded lifetime).  stage_reader_read / _stats / _destroy take either kind;
+ *   for the resident kind stats[0] = device instances launched, [1] = reads, [2] = 0.  Keys of
+ *   <= 8 bytes; a table that needs stage_sync ends the reader (reads fail with STAGE_E_STATE). */
 typedef struct stage_reader stage_reader;
 int stage_host_alloc(uint64_t bytes, void **ptr);
 int stage_host_free(void *ptr);
@@ -273,6 +281,8 @@ int stage_probe_host(stage_table *t, const uint64_t *keys, const uint16_t *lens,
                      const uint32_t *read_ids, uint64_t n, stage_probe_out *out, uint8_t *records);
 int stage_reader_create(stage_table *t, uint32_t max_batch, uint32_t max_wait_us,
                         stage_reader **out);
+int stage_reader_create_resident(stage_table *t, uint32_t ring_slots, uint32_t waves, uint32_t life_us,
+                                 stage_reader **out);
 int stage_reader_read(stage_reader *r, uint64_t key, uint16_t key_size, uint32_t read_id,
                       stage_probe_out *out, uint8_t *record);
 int stage_reader_stats(stage_reader *r, uint64_t *stats);

@@ -12,6 +12,9 @@
 //    waking it.  The batch is one probe launch reading keys from and writing results to
 //    pinned, device-mapped host memory (no separate copies).  While one batch is on the
 //    device the next one fills.
+//  * stage_reader_create_resident: the same adapter with the device side resident
+//    (resident_reader_kernel, kernels.hip) polling a request ring in pinned host memory -- a
+//    read costs no launch, no event and no thread hand-off, only PCIe round trips.
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
@@ -20,6 +23,7 @@
 #include <condition_variable>
 #include <climits>
 #include <cstring>
+#include <immintrin.h>
 #include <linux/futex.h>
 #include <sys/syscall.h>
 #include <unistd.h>
@@ -120,7 +124,66 @@ int64_t now_ns() {
 
 }  // namespace
 
+// the resident form: request ring + keeper thread (see stage_reader_create_resident)
+struct ResidentReader {
+    stage_table *t = nullptr;
+    uint32_t slots = 0, waves = 0, row_bytes = 0;
+    uint64_t stride = 0, life_ticks = 0;
+    uint8_t *h = nullptr, *hd = nullptr;  // ring block, host and device view
+    uint64_t *keys = nullptr;
+    uint16_t *lens = nullptr;
+    uint32_t *rids = nullptr, *posted = nullptr, *done = nullptr, *stop = nullptr;
+    stage_probe_out *out = nullptr;
+    uint8_t *rows = nullptr;
+    uint64_t *dpos = nullptr;             // device: next ticket per wave
+    stage::ReaderRing ring{};             // device pointers
+    std::unique_ptr<std::atomic<uint64_t>[]> freed;  // per slot: ticket + 1 of its last finished reader
+    std::atomic<uint64_t> tail{0};
+    std::atomic<int> dead{0};             // STAGE_E_STATE / STAGE_E_HIP once the device side ended
+    std::atomic<bool> closing{false}, quit{false};
+    std::atomic<uint64_t> n_inst{0}, n_reads{0};
+    hipStream_t s = nullptr;
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    std::thread keeper;
+    void run();
+};
+
+void ResidentReader::run() {
+    (void)hipSetDevice(t->dev.device);
+    int k = 0;
+    bool queued[2] = {false, false};
+    while (!quit.load(std::memory_order_acquire)) {
+        if (queued[k]) {  // two instances queued: wait for the older one before adding a third
+            if (hipEventSynchronize(ev[k]) != hipSuccess) {
+                dead.store(STAGE_E_HIP);
+                break;
+            }
+            queued[k] = false;
+            if (quit.load(std::memory_order_acquire)) break;
+        }
+        if (stage_capi::need_synced(t)) {
+            dead.store(STAGE_E_STATE);
+            break;
+        }
+        stage::DevTable view = t->dev.view;
+        view.stride = (uint32_t)stride;
+        hipError_t e = stage::launch_resident_reader(view, ring, s);
+        if (!e) e = hipEventRecord(ev[k], s);
+        if (e) {
+            dead.store(STAGE_E_HIP);
+            break;
+        }
+        queued[k] = true;
+        n_inst++;
+        k ^= 1;
+    }
+    __atomic_store_n(stop, 1u, __ATOMIC_RELEASE);  // running instances end at their next poll
+    (void)hipStreamSynchronize(s);
+    if (!dead.load()) dead.store(STAGE_E_STATE);
+}
+
 struct stage_reader {
+    std::unique_ptr<ResidentReader> res;  // set for the resident kind
     struct Req {
         uint64_t key;
         uint16_t len;
@@ -330,10 +393,130 @@ int stage_reader_create(stage_table *t, uint32_t max_batch, uint32_t max_wait_us
     });
 }
 
+static int resident_read(ResidentReader &R, uint64_t key, uint16_t key_size, uint32_t read_id, stage_probe_out *out,
+                         uint8_t *record) {
+    if (R.closing.load(std::memory_order_acquire) || R.dead.load(std::memory_order_acquire))
+        return fail(STAGE_E_STATE, "resident reader has ended");
+    const uint64_t q = R.tail.fetch_add(1, std::memory_order_acq_rel);
+    const uint32_t per = R.slots / R.waves;  // wave q % W, its (q / W)-th ticket
+    const uint32_t slot = (uint32_t)(q % R.waves) * per + (uint32_t)((q / R.waves) % per);
+    const uint64_t prev = q >= R.slots ? q - R.slots + 1 : 0;
+    auto wait = [&](auto ready) {  // spin (PCIe round trips are microseconds), then yield
+        for (uint64_t i = 0; !ready(); ++i) {
+            if (R.dead.load(std::memory_order_acquire)) return false;
+            if (i < 4096) _mm_pause();
+            else std::this_thread::yield();
+        }
+        return true;
+    };
+    if (!wait([&] { return R.freed[slot].load(std::memory_order_acquire) == prev; }))
+        return fail(R.dead.load(), "resident reader has ended");
+    R.keys[slot] = key;
+    R.lens[slot] = key_size;
+    R.rids[slot] = read_id;
+    __atomic_store_n(R.posted + slot, (uint32_t)(q + 1), __ATOMIC_RELEASE);
+    if (!wait([&] { return __atomic_load_n(R.done + slot, __ATOMIC_ACQUIRE) == (uint32_t)(q + 1); }))
+        return fail(R.dead.load(), R.dead.load() == STAGE_E_STATE ? "device image is stale: the resident reader ended"
+                                                                  : "resident reader failed on the device");
+    if (out) *out = R.out[slot];
+    if (record) std::memcpy(record, R.rows + (uint64_t)slot * R.stride, R.row_bytes);
+    R.freed[slot].store(q + 1, std::memory_order_release);
+    R.n_reads.fetch_add(1, std::memory_order_relaxed);
+    return STAGE_OK;
+}
+
+int stage_reader_create_resident(stage_table *t, uint32_t ring_slots, uint32_t waves, uint32_t life_us,
+                                 stage_reader **out) {
+    if (!t || !out || waves == 0 || waves > 1024 || ring_slots == 0 || ring_slots % (64 * waves) ||
+        ring_slots > (1u << 22) || life_us == 0 || life_us > 1000000)
+        return fail(STAGE_E_ARG, "bad resident reader arguments (ring_slots: a multiple of 64 * waves; waves "
+                                 "1..1024; life_us 1..1e6)");
+    if (host(t).key_words() != 1) return fail(STAGE_E_ARG, "the single-key reader takes keys of <= 8 bytes");
+    if (int rc = need_synced(t)) return rc;
+    const uint32_t cap = t->dev.view.cap;
+    if (t->dev.view.key_width == 0 ? cap > 128 : cap > 1024)
+        return fail(STAGE_E_ARG, "resident reader: leaf geometry not supported");
+    *out = nullptr;
+    return guarded([&] {
+        std::unique_ptr<stage_reader> r(new stage_reader);
+        r->t = t;
+        r->res.reset(new ResidentReader);
+        ResidentReader &R = *r->res;
+        R.t = t;
+        R.slots = ring_slots;
+        R.waves = waves;
+        R.stride = host(t).stride();
+        R.row_bytes = 8 + host(t).params().payload_size;
+        stage::hip_check(hipSetDevice(t->dev.device), "hipSetDevice");
+        int khz = 0;
+        stage::hip_check(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, t->dev.device), "clock rate");
+        R.life_ticks = (uint64_t)(khz > 0 ? khz : 100000) * life_us / 1000;
+        const uint64_t S = ring_slots;
+        // keys | rids | posted | done | lens | stop | out | rows (each array 64-B aligned)
+        auto al = [](uint64_t x) { return (x + 63) & ~63ull; };
+        const uint64_t o_rids = al(8 * S), o_posted = o_rids + al(4 * S), o_done = o_posted + al(4 * S),
+                       o_lens = o_done + al(4 * S), o_stop = o_lens + al(2 * S), o_out = o_stop + 64,
+                       o_rows = o_out + al(32 * S), bytes = o_rows + S * R.stride;
+        stage::hip_check(hipHostMalloc((void **)&R.h, bytes, hipHostMallocMapped | hipHostMallocCoherent |
+                                                                 hipHostMallocPortable),
+                         "resident ring");
+        std::memset(R.h, 0, bytes);
+        stage::hip_check(hipHostGetDevicePointer((void **)&R.hd, R.h, 0), "resident ring device pointer");
+        R.keys = (uint64_t *)R.h;
+        R.rids = (uint32_t *)(R.h + o_rids);
+        R.posted = (uint32_t *)(R.h + o_posted);
+        R.done = (uint32_t *)(R.h + o_done);
+        R.lens = (uint16_t *)(R.h + o_lens);
+        R.stop = (uint32_t *)(R.h + o_stop);
+        R.out = (stage_probe_out *)(R.h + o_out);
+        R.rows = R.h + o_rows;
+        R.freed.reset(new std::atomic<uint64_t>[S]);
+        for (uint64_t i = 0; i < S; ++i) R.freed[i].store(0);
+        std::vector<uint64_t> pos(waves, 0);
+        stage::hip_check(hipMalloc((void **)&R.dpos, 8ull * waves), "resident positions");
+        stage::hip_check(hipMemcpy(R.dpos, pos.data(), 8ull * waves, hipMemcpyHostToDevice), "resident positions");
+        stage::hip_check(hipStreamCreateWithFlags(&R.s, hipStreamNonBlocking), "resident stream");
+        for (auto &e : R.ev) stage::hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventBlockingSync),
+                                              "resident event");
+        R.ring = stage::ReaderRing{(const uint64_t *)R.hd, (const uint16_t *)(R.hd + o_lens),
+                                   (const uint32_t *)(R.hd + o_rids), (const uint32_t *)(R.hd + o_posted),
+                                   (uint32_t *)(R.hd + o_done), (stage::stage_probe_out_dev *)(R.hd + o_out),
+                                   R.hd + o_rows, (const uint32_t *)(R.hd + o_stop), R.dpos, ring_slots, waves,
+                                   R.life_ticks};
+        ResidentReader *raw = &R;
+        R.keeper = std::thread([raw] { raw->run(); });
+        *out = r.release();
+        return STAGE_OK;
+    });
+}
+
+static void resident_destroy(ResidentReader &R) {
+    R.closing.store(true, std::memory_order_release);
+    // the reads already holding a ticket finish (bounded: the keeper keeps instances queued
+    // until they are done or the device side has ended)
+    const uint64_t issued = R.tail.load(std::memory_order_acquire);
+    const auto t0 = std::chrono::steady_clock::now();
+    const uint32_t per = R.slots / R.waves;
+    for (uint64_t q = issued > R.slots ? issued - R.slots : 0; q < issued; ++q)
+        while (R.freed[(q % R.waves) * per + (q / R.waves) % per].load(std::memory_order_acquire) < q + 1 &&
+               !R.dead.load() &&
+               std::chrono::steady_clock::now() - t0 < std::chrono::seconds(2))
+            std::this_thread::yield();
+    R.quit.store(true, std::memory_order_release);
+    if (R.keeper.joinable()) R.keeper.join();
+    (void)hipSetDevice(R.t->dev.device);
+    if (R.s) (void)hipStreamSynchronize(R.s), (void)hipStreamDestroy(R.s);
+    for (auto &e : R.ev)
+        if (e) (void)hipEventDestroy(e);
+    if (R.dpos) (void)hipFree(R.dpos);
+    if (R.h) (void)hipHostFree(R.h);
+}
+
 int stage_reader_read(stage_reader *r, uint64_t key, uint16_t key_size, uint32_t read_id, stage_probe_out *out,
                       uint8_t *record) {
     if (!r) return fail(STAGE_E_ARG, "null reader");
     if (key_size == 0 || key_size > 8) return fail(STAGE_E_ARG, "key_size must be 1..8");
+    if (r->res) return resident_read(*r->res, key, key_size, read_id, out, record);
     int rc = STAGE_E_STATE;
     uint32_t seq;
     {
@@ -360,6 +543,12 @@ int stage_reader_read(stage_reader *r, uint64_t key, uint16_t key_size, uint32_t
 
 int stage_reader_stats(stage_reader *r, uint64_t *stats) {
     if (!r || !stats) return fail(STAGE_E_ARG, "null argument");
+    if (r->res) {
+        stats[0] = r->res->n_inst.load();
+        stats[1] = r->res->n_reads.load();
+        stats[2] = 0;
+        return STAGE_OK;
+    }
     stats[0] = r->n_batches.load();
     stats[1] = r->n_reads.load();
     stats[2] = r->n_full.load();
@@ -368,6 +557,11 @@ int stage_reader_stats(stage_reader *r, uint64_t *stats) {
 
 int stage_reader_destroy(stage_reader *r) {
     if (!r) return STAGE_OK;
+    if (r->res) {
+        resident_destroy(*r->res);
+        delete r;
+        return STAGE_OK;
+    }
     {
         std::lock_guard<std::mutex> lk(r->mu);
         r->stop = true;

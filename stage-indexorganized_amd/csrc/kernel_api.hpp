@@ -49,6 +49,23 @@ hipError_t launch_scan(const DevTable &t, const uint64_t *keys, const uint16_t *
 hipError_t launch_scan_first(const DevTable &t, const uint64_t *keys, uint64_t n, uint32_t scan_size,
                              const uint32_t *rids, uint32_t words, uint32_t *img_out, uint8_t *st_out, hipStream_t s,
                              const ScanTuning &tune);
+// request ring of the resident reader (all arrays in pinned, device-mapped host memory except
+// pos, which is device memory of `waves` words initialised to 0)
+struct ReaderRing {
+    const uint64_t *keys;      // [slots] little-endian key bytes
+    const uint16_t *lens;      // [slots] key lengths (variable-length tables)
+    const uint32_t *rids;      // [slots] read ids
+    const uint32_t *posted;    // [slots] ticket + 1 once the request is in place (host)
+    uint32_t *done;            // [slots] ticket + 1 once its results are in place (device)
+    stage_probe_out_dev *out;  // [slots]
+    uint8_t *rows;             // [slots * stride]
+    const uint32_t *stop;      // non-zero: instances end at their next poll
+    uint64_t *pos;             // [waves] next own ticket index k of each wave, kept across instances
+    uint32_t slots;            // multiple of 64 * waves
+    uint32_t waves;
+    uint64_t life_ticks;       // lifetime of one instance in real-time counter ticks
+};
+hipError_t launch_resident_reader(const DevTable &t, const ReaderRing &g, hipStream_t s);
 hipError_t launch_murmur(const void *keys, uint32_t key_len, uint32_t key_stride, uint64_t seed, uint64_t n,
                          uint64_t *out, hipStream_t s);
 hipError_t launch_fill(uint8_t *heap, uint32_t stride, uint32_t payload_size, uint32_t row_bytes,

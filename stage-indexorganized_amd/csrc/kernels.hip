@@ -466,6 +466,120 @@ __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *
 }
 
 // ----------------------------------------------------------------------------------------
+// resident single-key reader: one-wave workgroups poll a request ring in pinned host memory
+// (the stage_reader_* adapter of BTree::Read callers, b_tree.cpp:2066-2129, without a launch
+// per request).  Ticket q belongs to wave w = q % W as its k-th ticket, k = q / W, and lives in
+// slot w * P + k % P of the ring (P = slots / W, a multiple of 64): concurrent callers land on
+// different waves, and a wave's tickets are contiguous in the ring.  A caller fills its slot
+// and publishes posted[slot] = q + 1 (release); the wave takes the published prefix of its
+// current 64-ticket block, probes it (lane j = the block's j-th ticket throughout), writes the
+// status record and the row into the slot and publishes done[slot] = q + 1 (system-scope
+// release).  Every instance ends after life_ticks of the
+// 100 MHz real-time counter or when *stop is set, saving its position in pos[w] for the next
+// instance queued behind it on the same stream -- no wave outlives its instance's lifetime.
+
+// one wave-uniform probe (request j of the wave's lanes) with one probe in flight
+template <bool VARLEN, int SPL>
+__device__ __forceinline__ void ring_probe_one(const DevTable &t, uint32_t lane, int j, uint32_t leaf_l, uint64_t ok_l,
+                                               uint32_t len_l, uint32_t rid_l, uint8_t *row, uint32_t out_chunks,
+                                               u32x4 &a, u32x4 &b) {
+    const uint32_t lf = rl32(leaf_l, j);
+    const uint64_t x = rl64(ok_l, j);
+    const uint32_t xl = VARLEN ? rl32(len_l, j) : t.key_width;
+    const uint32_t rd = rl32(rid_l, j);
+    const uint8_t *h = t.head + (uint64_t)lf * t.head_bytes;
+    const uint32_t fx = key_fp_words(&x, 1);
+    int slot = -1;
+    uint64_t m = 0;
+    uint32_t nx = 0, im = 0;
+#pragma unroll
+    for (int s = SPL - 1; s >= 0; --s) {  // first hit in slot order (SearchRecordMeta)
+        const bool cand = h[s * 64 + lane] == fx;
+        uint64_t wok = 0, wmeta = 0;
+        uint32_t wnext = 0, wimg = 0;
+        if (cand) {
+            const u32x4 *w = reinterpret_cast<const u32x4 *>(t.slot + (uint64_t)lf * t.cap + s * 64 + lane);
+            const u32x4 w0 = w[0], w1 = w[1];
+            wok = ((uint64_t)w0.y << 32) | w0.x;
+            wmeta = ((uint64_t)w0.w << 32) | w0.z;
+            wnext = w1.x;
+            wimg = w1.y;
+        }
+        const uint64_t hit = ballot(cand && wok == x && (!VARLEN || meta_keylen(wmeta) == xl));
+        if (hit) {
+            const int bl = __builtin_ctzll(hit);
+            slot = s * 64 + bl;
+            m = rl64(wmeta, bl);
+            nx = rl32(wnext, bl);
+            im = rl32(wimg, bl);
+        }
+    }
+    ProbeRes r;
+    visibility(t, slot, m, nx, im, rd, r);
+    for (uint32_t c0 = 0; c0 < out_chunks; c0 += 64) {
+        const uint32_t c = c0 + lane;
+        if (c < out_chunks) {
+            u32x4 v = u32x4{0, 0, 0, 0};
+            if (r.image != 0xFFFFFFFFu) v = reinterpret_cast<const u32x4 *>(t.heap + (uint64_t)r.image * t.hstride)[c];
+            reinterpret_cast<u32x4 *>(row)[c] = v;
+        }
+    }
+    pack_out(lf, r, a, b);
+}
+
+template <bool VARLEN, int SPL>
+__global__ __launch_bounds__(64) void resident_reader_kernel(DevTable t, ReaderRing g) {
+    const uint32_t lane = lane_id();
+    const uint32_t w = blockIdx.x;
+    const uint32_t out_chunks = t.stride >> 4;
+    const uint32_t per = g.slots / g.waves;
+    uint64_t pos = g.pos[w];  // this wave's next k
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        if (__hip_atomic_load(g.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > g.life_ticks) break;
+        const uint64_t blk = pos & ~63ull;
+        const uint32_t d = (uint32_t)(pos & 63u);
+        const uint32_t s0 = w * per + (uint32_t)(blk % per);
+        const uint32_t want = (uint32_t)((blk + lane) * g.waves + w + 1u);
+        bool ready = false;
+        if (lane >= d)
+            ready = __hip_atomic_load(g.posted + s0 + lane, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == want;
+        const uint64_t m = ballot(ready) >> d;
+        const uint32_t k = ~m ? (uint32_t)__builtin_ctzll(~m) : 64u;  // published prefix from d
+        if (k == 0) {
+            __builtin_amdgcn_s_sleep(2);
+            continue;
+        }
+        const bool mine = lane >= d && lane < d + k;
+        const uint32_t len = t.key_width ? t.key_width : (mine ? (uint32_t)g.lens[s0 + lane] : 8u);
+        const uint32_t rid = mine ? g.rids[s0 + lane] : 0u;
+        uint64_t ok;
+        load_okey<1>(g.keys + s0, lane, mine, len, &ok);
+        uint32_t leaf = mine ? resolve_leaf<VARLEN, 1>(t, &ok, len, true) : 0u;
+        u32x4 my_a = u32x4{0, 0, 0, 0}, my_b = u32x4{0, 0, 0, 0};
+        for (uint32_t j = d; j < d + k; ++j) {
+            u32x4 a, b;
+            ring_probe_one<VARLEN, SPL>(t, lane, (int)j, leaf, ok, len, rid, g.rows + (uint64_t)(s0 + j) * t.stride,
+                                        out_chunks, a, b);
+            if (lane == j) {
+                my_a = a;
+                my_b = b;
+            }
+        }
+        if (mine) {
+            u32x4 *o = reinterpret_cast<u32x4 *>(g.out + s0 + lane);
+            o[0] = my_a;
+            o[1] = my_b;
+            // status record and row before the flag, system-wide
+            __hip_atomic_store(g.done + s0 + lane, want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        pos += k;
+    }
+    if (lane == 0) g.pos[w] = pos;
+}
+
+// ----------------------------------------------------------------------------------------
 // range scan (TableScanExecutor over Iterator), one wave per scan
 
 template <int R>
@@ -1351,6 +1465,26 @@ hipError_t launch_probe(const DevTable &t, const uint64_t *keys, const uint16_t 
         else STAGE_PROBE(false, 2, 4);
     }
 #undef STAGE_PROBE
+    return hipGetLastError();
+}
+
+hipError_t launch_resident_reader(const DevTable &t, const ReaderRing &g, hipStream_t s) {
+    if (t.key_words != 1 || g.waves == 0 || g.slots % (64 * g.waves)) return hipErrorInvalidValue;
+    const dim3 grid(g.waves), block(64);
+    if (t.key_width == 0) {
+        if (t.cap == 64) resident_reader_kernel<true, 1><<<grid, block, 0, s>>>(t, g);
+        else if (t.cap == 128) resident_reader_kernel<true, 2><<<grid, block, 0, s>>>(t, g);
+        else return hipErrorInvalidValue;
+    } else {
+        switch (t.cap / 64) {
+            case 1: resident_reader_kernel<false, 1><<<grid, block, 0, s>>>(t, g); break;
+            case 2: resident_reader_kernel<false, 2><<<grid, block, 0, s>>>(t, g); break;
+            case 4: resident_reader_kernel<false, 4><<<grid, block, 0, s>>>(t, g); break;
+            case 8: resident_reader_kernel<false, 8><<<grid, block, 0, s>>>(t, g); break;
+            case 16: resident_reader_kernel<false, 16><<<grid, block, 0, s>>>(t, g); break;
+            default: return hipErrorInvalidValue;
+        }
+    }
     return hipGetLastError();
 }
 

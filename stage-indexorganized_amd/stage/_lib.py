@@ -81,6 +81,8 @@ SIGNATURES = {
     "stage_host_free": (ctypes.c_int, [c_vp]),
     "stage_probe_host": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, ctypes.c_uint64, c_vp, c_vp]),
     "stage_reader_create": (ctypes.c_int, [c_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(c_vp)]),
+    "stage_reader_create_resident": (ctypes.c_int, [c_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                                    ctypes.POINTER(c_vp)]),
     "stage_reader_read": (ctypes.c_int, [c_vp, ctypes.c_uint64, ctypes.c_uint16, ctypes.c_uint32, c_vp, c_vp]),
     "stage_reader_stats": (ctypes.c_int, [c_vp, c_vp]),
     "stage_reader_destroy": (ctypes.c_int, [c_vp]),

@@ -430,8 +430,8 @@ class Table:
               "probe_host")
         return out, rows
 
-    def reader(self, max_batch=1024, max_wait_us=50):
-        return Reader(self, max_batch, max_wait_us)
+    def reader(self, max_batch=1024, max_wait_us=50, **resident):
+        return Reader(self, max_batch, max_wait_us, **resident)
 
     def range_scan(self, start_keys, scan_size, lens=None):
         """TableScanExecutor over RangeScanBySize/Iterator.  Returns (counts[n], rows[n, scan_size, stride])."""
@@ -482,12 +482,19 @@ class Table:
 class Reader:
     """stage_reader: thread-safe single-key BTree::Read adapter (calls are coalesced into
     device batches).  ``read`` releases the GIL inside the library, so Python threads
-    calling it concurrently are batched together."""
+    calling it concurrently are batched together.  ``resident=True``: the device side stays
+    resident and polls a request ring (stage_reader_create_resident)."""
 
-    def __init__(self, table, max_batch=1024, max_wait_us=50):
+    def __init__(self, table, max_batch=1024, max_wait_us=50, resident=False, ring_slots=4096, waves=16,
+                 life_us=5000):
         self.table = table
+        self.resident = resident
         h = ctypes.c_void_p()
-        check(lib().stage_reader_create(table.h, max_batch, max_wait_us, ctypes.byref(h)), "reader_create")
+        if resident:
+            check(lib().stage_reader_create_resident(table.h, ring_slots, waves, life_us, ctypes.byref(h)),
+                  "reader_create_resident")
+        else:
+            check(lib().stage_reader_create(table.h, max_batch, max_wait_us, ctypes.byref(h)), "reader_create")
         self.h = h
 
     def read(self, key, read_id=0xFFFFFFFE, key_size=None, record=True):

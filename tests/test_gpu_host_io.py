@@ -1,6 +1,7 @@
 """GPU parity of the host-buffer entry points: stage_probe_host (chunked, three streams) and the
-coalescing single-key reader (stage_reader_*, the BTree::Read adapter of SURVEY §8(b)), both
-against the oracle and against the device-buffer probe."""
+single-key readers (stage_reader_*, the BTree::Read adapter of SURVEY §8(b)) -- the coalescing
+one and the resident one (a device-resident polling loop over a request ring) -- against the
+oracle and against the device-buffer probe."""
 import threading
 
 import numpy as np
@@ -51,13 +52,16 @@ def test_probe_host_matches_device_and_oracle(chains):
     assert none is None and (out2 == out_h[:1000]).all()
 
 
-def test_reader_concurrent_threads_match_oracle(chains):
+@pytest.mark.parametrize("resident", [False, True])
+def test_reader_concurrent_threads_match_oracle(chains, resident):
     tab, orc, hot, n = chains
     rng = np.random.default_rng(43)
     keys = np.concatenate([rng.integers(0, n + 100, 6000), rng.choice(hot, 2000)]).astype(np.uint64)
     rids = rng.integers(0, 45, keys.size).astype(np.uint32)
     o_out, o_rec = orc.read_batch(keys, 8, rids)
-    r = tab.reader(max_batch=64, max_wait_us=200)
+    # resident: a 256-slot ring laps ~30 times; 4 waves
+    r = tab.reader(max_batch=64, max_wait_us=200, resident=True, ring_slots=256, waves=4) if resident else \
+        tab.reader(max_batch=64, max_wait_us=200)
     got_out = np.zeros(keys.size, stage.PROBE_OUT_DTYPE)
     got_rec = np.zeros((keys.size, orc.row), np.uint8)
     T = 16
@@ -82,7 +86,7 @@ def test_reader_concurrent_threads_match_oracle(chains):
     assert (got_rec == o_rec).all()
     st = r.stats()
     assert st["reads"] == keys.size
-    assert st["batches"] < keys.size  # requests were actually coalesced
+    assert st["batches"] < keys.size  # coalesced batches / resident instances
     r.close()
 
 
@@ -101,4 +105,48 @@ def test_reader_single_caller_and_stale_image(gpu):
     tab.sync()
     out, row = r.read(7, read_id=10)
     assert out["status"] == stage.ST_COPY and row[8] == 7
+    r.close()
+
+
+def test_resident_reader_single_caller_lifetimes_and_stale_image(gpu):
+    tab = stage.Table(key_width=4)
+    tab.load_ycsb(0, 1000, 4)
+    tab.sync()
+    orc = O.OracleTree()
+    orc.load_ycsb(0, 1000, 4, 0)
+    # 1-ms instances: reads cross many instance boundaries (positions carried over)
+    r = tab.reader(resident=True, ring_slots=128, waves=2, life_us=1000)
+    keys = np.array(list(range(0, 1200, 3)), np.uint64)
+    o_out, o_rec = orc.read_batch(keys, 4, np.full(keys.size, 0xFFFFFFFE, np.uint32))
+    for i, k in enumerate(keys):
+        out, row = r.read(int(k))
+        assert out["status"] == o_out["status"][i] and (row == o_rec[i]).all(), int(k)
+    assert r.stats()["reads"] == keys.size
+    assert tab.update(7, 0, b"\x01", 5) == stage.RC_OK
+    import time
+    time.sleep(0.05)  # the keeper sees the unpublished write at its next relaunch
+    with pytest.raises(RuntimeError):
+        r.read(7)
+    r.close()
+    tab.sync()
+    r = tab.reader(resident=True, ring_slots=64, waves=1)
+    out, row = r.read(7, read_id=10)
+    assert out["status"] == stage.ST_COPY and row[8] == 7
+    r.close()
+    with pytest.raises(RuntimeError):  # ring size must be a multiple of 64 * waves
+        tab.reader(resident=True, ring_slots=192, waves=2)
+
+
+def test_resident_reader_variable_length_keys(gpu):
+    tab = stage.Table(payload_size=8, leaf_node_size=4096, split_threshold=3072, merge_threshold=1024, key_width=0)
+    keys = [b"a", b"ab", b"abc", b"b", b"zz", b"k000", b"k001"]
+    for i, k in enumerate(keys):
+        assert tab.insert_key(k, bytes([i]) * 8, commit_id=1) == stage.RC_OK
+    tab.sync()
+    r = tab.reader(resident=True, ring_slots=64, waves=1)
+    for i, k in enumerate(keys):
+        out, row = r.read(int.from_bytes(k, "little"), key_size=len(k))
+        assert out["status"] == stage.ST_LATEST and row[8] == i, k
+    out, _ = r.read(int.from_bytes(b"abcd", "little"), key_size=4)
+    assert out["status"] == stage.ST_NOT_FOUND
     r.close()
