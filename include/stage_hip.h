@@ -80,6 +80,18 @@ typedef struct stage_probe_out {
                              row index here instead (stage_probe_sharded_ex)               */
 } stage_probe_out;
 
+/* lean probe result (16 B, opt-in for stage_probe_batch via stage_set_output_layout): what the
+ * IndexScanExecutor point branch and PerformRead consume -- the outcome, the PerformRead facts
+ * and the record cstamp; no leaf / slot / image / meta word. */
+typedef struct stage_probe_out16 {
+    uint8_t status;
+    uint8_t flags;
+    uint16_t hops;
+    uint32_t cstamp;
+    uint32_t copy_sstamp;
+    uint32_t rec_cstamp;
+} stage_probe_out16;
+
 const char *stage_last_error(void);
 const char *stage_version(void);
 
@@ -234,7 +246,14 @@ int stage_resolve_locations(stage_table *t, const uint64_t *handles, uint64_t n,
  * stage_scan_batch replaces BTree::RangeScanBySize + Iterator::GetNext + TableScanExecutor
  *   (b_tree.h:830-953, b_tree.cpp:1261-1315, executor.h:611-642): for each start key up to
  *   scan_size tuples in KeyCompare order into d_records[i*scan_size + j], count in d_counts.
- * stage_resolve_batch: device traversal only (le_child as TraverseToLeaf). */
+ * stage_resolve_batch: device traversal only (le_child as TraverseToLeaf).
+ * stage_set_output_layout: stage_probe_batch's output layout (default 0, 32): row_stride 0 =
+ *   stage_record_stride's default (the row rounded to 128 B above 128 B), else any multiple of
+ *   16 of at least key pad + payload (e.g. 1008 for YCSB rows: no pad bytes written);
+ *   status_bytes 32 = stage_probe_out, 16 = stage_probe_out16 records in d_out (fixed-width
+ *   keys of <= 8 bytes in 64-slot leaves).  The row stride also applies to stage_probe_host;
+ *   every other entry point keeps 32-B records. */
+int stage_set_output_layout(stage_table *t, uint32_t row_stride, uint32_t status_bytes);
 int stage_probe_batch(stage_table *t, const uint64_t *d_keys, const uint16_t *d_lens,
                       const uint32_t *d_read_ids, const uint32_t *d_leaf_ids, uint64_t n,
                       stage_probe_out *d_out, uint8_t *d_records, void *stream);

@@ -33,7 +33,8 @@ int stage_table_create(const stage_params *params, stage_table **out) {
         if (const char *g = std::getenv("STAGE_SCAN_MAX_BLOCKS")) t->scan_tune.max_blocks = std::atoi(g);
         if (const char *g = std::getenv("STAGE_OUT_STRIDE")) {
             uint32_t v = (uint32_t)std::atoi(g);
-            if (v >= t->host->stride() && v % 16 == 0) t->out_stride = v;
+            if (v >= ((t->host->key_pad() + t->host->params().payload_size + 15) & ~15u) && v % 16 == 0)
+                t->out_stride = v;
         }
         *out = t.release();
         return STAGE_OK;
@@ -329,9 +330,24 @@ int stage_probe_batch(stage_table *t, const uint64_t *d_keys, const uint16_t *d_
     if (e != hipSuccess) return hip_rc(e, "hipSetDevice");
     stage::DevTable view = t->dev.view;
     if (t->out_stride) view.stride = t->out_stride;
+    stage::ProbeTuning tune = t->tune;
+    tune.status_bytes = t->status_bytes;
     e = stage::launch_probe(view, d_keys, d_lens, d_read_ids, d_leaf_ids, n,
-                            reinterpret_cast<stage::stage_probe_out_dev *>(d_out), d_records, pick(t, stream), t->tune);
+                            reinterpret_cast<stage::stage_probe_out_dev *>(d_out), d_records, pick(t, stream), tune);
     return hip_rc(e, "probe kernel");
+}
+
+int stage_set_output_layout(stage_table *t, uint32_t row_stride, uint32_t status_bytes) {
+    if (!t) return fail(STAGE_E_ARG, "null table");
+    const uint32_t row = (host(t).key_pad() + host(t).params().payload_size + 15) & ~15u;
+    if (row_stride && (row_stride < row || row_stride % 16))
+        return fail(STAGE_E_ARG, "row_stride: 0 or a multiple of 16 of at least the row bytes (key pad + payload)");
+    if (status_bytes != 32 && status_bytes != 16) return fail(STAGE_E_ARG, "status_bytes: 32 or 16");
+    if (status_bytes == 16 && (host(t).params().key_width == 0 || host(t).key_words() != 1 || host(t).cap() != 64))
+        return fail(STAGE_E_ARG, "16-B status records: fixed-width keys of <= 8 bytes in 64-slot leaves");
+    t->out_stride = row_stride;
+    t->status_bytes = (int)status_bytes;
+    return STAGE_OK;
 }
 
 int stage_scan_batch(stage_table *t, const uint64_t *d_start_keys, const uint16_t *d_lens, uint64_t n,

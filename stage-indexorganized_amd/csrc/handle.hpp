@@ -29,7 +29,8 @@ struct stage_table {
     stage::DeviceImage dev;
     stage::ProbeTuning tune;
     stage::ScanTuning scan_tune;
-    uint32_t out_stride = 0;  // 0 = stride of the canonical row; STAGE_OUT_STRIDE overrides (A/B)
+    uint32_t out_stride = 0;  // 0 = stride of the canonical row (stage_set_output_layout / STAGE_OUT_STRIDE)
+    int status_bytes = 32;    // stage_probe_batch's status records: 32 or 16 (stage_set_output_layout)
     std::unique_ptr<stage::ShardComm> comm;
     std::unique_ptr<stage::ShardComm> loop_comm;  // stage_probe_sharded_loopback state
     int shard_chunks = 0;                          // 0 = STAGE_SHARD_CHUNKS or the default

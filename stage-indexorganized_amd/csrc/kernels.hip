@@ -316,8 +316,10 @@ __device__ __forceinline__ void st16(u32x4 v, uint8_t *base, uint32_t off) {
 }
 
 // CH: probes per wave chunk (64; 16 for small batches of the one-probe-in-flight instances, so
-// that a wave's chunk is not a chain of 64 dependent probes while most of the chip idles)
-template <bool VARLEN, int SPL, int G, int POL = 1, int KW = 1, int CH = 64>
+// that a wave's chunk is not a chain of 64 dependent probes while most of the chip idles).
+// ST: status record bytes -- 32 (stage_probe_out) or 16 (stage_probe_out16, opt-in: status |
+// flags | hops, cstamp, copy_sstamp, rec_cstamp -- what IndexScanExecutor and PerformRead use)
+template <bool VARLEN, int SPL, int G, int POL = 1, int KW = 1, int CH = 64, int ST = 32>
 __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *__restrict__ keys,
                                                     const uint16_t *__restrict__ lens,
                                                     const uint32_t *__restrict__ rids,
@@ -456,11 +458,17 @@ __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *
                 }
             }
         }
-        // one coalesced 2-KiB store of the chunk's 64 results
-        if (valid) {
-            uint8_t *ob = reinterpret_cast<uint8_t *>(out + base);
-            st16<POL>(my_a, ob, lane * 32u);
-            st16<POL>(my_b, ob, lane * 32u + 16u);
+        // one coalesced 2-KiB (1-KiB) store of the chunk's 64 results
+        if constexpr (ST == 16) {
+            if (valid)
+                st16<POL>(u32x4{my_a.x, my_a.w, my_b.y, my_b.x}, reinterpret_cast<uint8_t *>(out) + base * 16u,
+                          lane * 16u);
+        } else {
+            if (valid) {
+                uint8_t *ob = reinterpret_cast<uint8_t *>(out + base);
+                st16<POL>(my_a, ob, lane * 32u);
+                st16<POL>(my_b, ob, lane * 32u + 16u);
+            }
         }
     }
 }
@@ -1450,6 +1458,11 @@ hipError_t launch_probe(const DevTable &t, const uint64_t *keys, const uint16_t 
         return hipGetLastError();
     }
 #define STAGE_PROBE(V, S, G) probe_kernel<V, S, G><<<blocks, 256, 0, s>>>(t, keys, lens, rids, leaf_in, n, out, recs)
+    if (tune.status_bytes == 16) {  // opt-in lean status records: the YCSB geometry only
+        if (var || t.cap != 64 || tune.group != 8 || tune.store != 1) return hipErrorInvalidValue;
+        probe_kernel<false, 1, 8, 1, 1, 64, 16><<<blocks, 256, 0, s>>>(t, keys, lens, rids, leaf_in, n, out, recs);
+        return hipGetLastError();
+    }
     if (t.cap == 64) {
         if (var) STAGE_PROBE(true, 1, 4);
         else if (tune.group == 1) STAGE_PROBE(false, 1, 1);

@@ -93,6 +93,7 @@ SIGNATURES = {
     "stage_traverse_batch": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_uint64, ctypes.c_int, c_vp]),
     "stage_export_leaves": (ctypes.c_int64, [c_vp, ctypes.c_uint32, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp]),
     "stage_probe_batch": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_uint64, c_vp, c_vp, c_vp]),
+    "stage_set_output_layout": (ctypes.c_int, [c_vp, ctypes.c_uint32, ctypes.c_uint32]),
     "stage_scan_batch": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_uint64, ctypes.c_uint32, c_vp, c_vp, c_vp]),
     "stage_resolve_batch": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_uint64, ctypes.c_int, c_vp, c_vp]),
     "stage_set_probe_tuning": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.c_int]),

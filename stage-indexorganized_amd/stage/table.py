@@ -16,6 +16,9 @@ PROBE_OUT_DTYPE = np.dtype([
     ("cstamp", "u4"), ("rec_cstamp", "u4"), ("copy_sstamp", "u4"), ("image", "u4"), ("meta_hi", "u4"),
 ])
 assert PROBE_OUT_DTYPE.itemsize == 32
+PROBE_OUT16_DTYPE = np.dtype([("status", "u1"), ("flags", "u1"), ("hops", "u2"), ("cstamp", "u4"),
+                              ("copy_sstamp", "u4"), ("rec_cstamp", "u4")])
+assert PROBE_OUT16_DTYPE.itemsize == 16
 
 ST_NOT_FOUND, ST_LATEST, ST_COPY, ST_OLD, ST_FAIL_INVALID_TS, ST_CHAIN_MISS = range(6)
 Q2_REC_DTYPE = np.dtype([
@@ -411,13 +414,19 @@ class Table:
         if leaf_ids is not None:
             bufs.append(DeviceBuffer.from_numpy(np.ascontiguousarray(leaf_ids, np.uint32)))
             d_leaf = bufs[-1].ptr
-        d_out = DeviceBuffer(n * 32)
+        dt = PROBE_OUT16_DTYPE if getattr(self, "status_bytes", 32) == 16 else PROBE_OUT_DTYPE
+        d_out = DeviceBuffer(n * dt.itemsize)
         d_rec = DeviceBuffer(n * self.stride) if records else None
         self.probe_device(bufs[0].ptr, n, d_out.ptr, d_rec.ptr if d_rec else None, d_rids, d_lens, d_leaf)
         check(lib().stage_device_sync(), "sync")
-        out = d_out.to_numpy(PROBE_OUT_DTYPE, n)
+        out = d_out.to_numpy(dt, n)
         rows = d_rec.to_numpy(np.uint8, n * self.stride).reshape(n, self.stride) if d_rec else None
         return out, rows
+
+    def set_output_layout(self, row_stride=0, status_bytes=32):
+        """stage_set_output_layout: probe row stride (0 = default) and 32- or 16-B status records."""
+        check(lib().stage_set_output_layout(self.h, row_stride, status_bytes), "set_output_layout")
+        self.status_bytes = status_bytes
 
     def probe_host(self, keys, read_ids=None, lens=None, records=True):
         """stage_probe_host: the same probe with host-memory inputs and outputs (pipelined)."""
