@@ -24,6 +24,7 @@ run() {  # name limit cmd...
 }
 CAL=stage-indexorganized_amd/lib/fetch_calib
 SQ="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE"
+INSTS="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH"
 run calib_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/calib_fetch -o calib -- $CAL 32 2
 run calib_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/calib_write -o calib -- $CAL 32 2
 run c2_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/c2_trace -o c2 -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-extras
@@ -36,5 +37,6 @@ run c4_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/c4
 run tpcc_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/tpcc_trace -o tpcc -- python bench.py --config tpcc --steps 5 --warmup 1 --no-cpu-baseline
 run tpcc_sq 300 rocprofv3 --pmc $SQ --output-format csv -d $OUT/tpcc_sq -o tpcc -- python bench.py --config tpcc --steps 2 --warmup 1 --no-cpu-baseline
 run tpcc_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/tpcc_fetch -o tpcc -- python bench.py --config tpcc --steps 2 --warmup 1 --no-cpu-baseline
+run tpcc_insts 300 rocprofv3 --pmc $INSTS --output-format csv -d $OUT/tpcc_insts -o tpcc -- python bench.py --config tpcc --steps 2 --warmup 1 --no-cpu-baseline
 run c2_sq 300 rocprofv3 --pmc $SQ --output-format csv -d $OUT/c2_sq -o c2 -- python scripts/profile_probe.py
 find $OUT -name "*.csv" | sort
