@@ -110,7 +110,10 @@ int stage_table_destroy(stage_table *t);
  * stage_update      = BTree::Update / LeafNode::Update (b_tree.cpp:2132-2160, 1061-1163)
  * stage_commit_update = CommitTransaction UPDATE entry (transaction_manager.cpp:610-676)
  * stage_finalize_update = BTree::FinalizeUpdate (b_tree.cpp:2252-2268)
- * stage_delete      = BTree::Delete + FinalizeDelete (b_tree.cpp:2184-2237, 2275-2310)
+ * stage_delete      = BTree::Delete + FinalizeDelete (b_tree.cpp:2184-2237, 2275-2310); the
+ *                     record is deleted either way, and STAGE_RC_INVALID (instead of OK) says
+ *                     the leaf fell below merge_threshold, where the reference would merge it
+ *                     with a sibling (CheckMerge, not restated: the leaf stays as it is)
  * rc_out receives the reference ReturnCode (STAGE_RC_*). */
 int stage_insert(stage_table *t, uint64_t key, uint16_t key_size, const uint8_t *payload,
                  uint64_t gen_rowid, int payload_mode, uint32_t commit_id, uint8_t *rc_out);
