@@ -1,6 +1,11 @@
 // capi.cpp -- the extern "C" boundary (include/stage_hip.h).  No exception crosses it.
 #include <hip/hip_runtime_api.h>
 
+#include <execinfo.h>
+#include <unistd.h>
+
+#include <csignal>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <stdexcept>
@@ -17,6 +22,29 @@ using namespace stage_capi;
 extern "C" {
 
 const char *stage_last_error(void) { return g_err.c_str(); }
+
+// STAGE_SEGV_TRACE=1: a host-side SIGSEGV / SIGABRT prints the native backtrace of the faulting
+// thread to stderr before the default action (host-code debugging on the GPU box, where no
+// debugger is available)
+namespace {
+void segv_trace(int sig) {
+    void *frames[64];
+    const int n = backtrace(frames, 64);
+    const char msg[] = "stage: fatal signal, native backtrace:\n";
+    (void)!write(2, msg, sizeof(msg) - 1);
+    backtrace_symbols_fd(frames, n, 2);
+    std::signal(sig, SIG_DFL);
+    raise(sig);
+}
+struct SegvTraceInit {
+    SegvTraceInit() {
+        if (std::getenv("STAGE_SEGV_TRACE")) {
+            std::signal(SIGSEGV, segv_trace);
+            std::signal(SIGABRT, segv_trace);
+        }
+    }
+} segv_trace_init;
+}  // namespace
 const char *stage_version(void) { return "stage-hip 0.1 (gfx950)"; }
 
 int stage_table_create(const stage_params *params, stage_table **out) {

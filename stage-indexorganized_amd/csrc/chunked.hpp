@@ -9,7 +9,10 @@
 #include <cstdint>
 #include <memory>
 #include <stdexcept>
+#include <type_traits>
 #include <vector>
+
+#include "huge_alloc.hpp"
 
 namespace stage {
 
@@ -31,11 +34,23 @@ public:
     }
     void reserve(size_t n) { ensure(n); }
 
-private:
-    void ensure(size_t n) {
-        while (chunks_.size() * kChunk < n) chunks_.emplace_back(new T[kChunk]);
+    ChunkedVector() = default;
+    ChunkedVector(const ChunkedVector &) = delete;
+    ChunkedVector &operator=(const ChunkedVector &) = delete;
+    ~ChunkedVector() {
+        for (T *c : chunks_) HugeAlloc<T>().deallocate(c, kChunk);
     }
-    std::vector<std::unique_ptr<T[]>> chunks_;
+
+private:
+    // chunks on huge pages (a chunk of image descriptors is 24 MiB): an epoch's appends fault
+    // in a few 2-MiB pages instead of thousands of 4-KiB ones
+    void ensure(size_t n) {
+        while (chunks_.size() * kChunk < n) {
+            static_assert(std::is_trivially_copyable<T>::value, "chunk elements are raw storage");
+            chunks_.push_back(HugeAlloc<T>().allocate(kChunk));
+        }
+    }
+    std::vector<T *> chunks_;
     size_t size_ = 0;
 };
 

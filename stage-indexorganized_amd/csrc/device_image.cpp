@@ -27,7 +27,8 @@ static void dev_ensure(DevBuf &b, uint64_t bytes, const char *what) {
 DeviceImage::~DeviceImage() { release(); }
 
 void DeviceImage::release() {
-    for (DevBuf *b : {&head, &okey, &slot, &tree, &tree_len, &heap, &chdr, &vhdr, &arena, &descs, &patch, &scratch}) {
+    for (DevBuf *b :
+         {&head, &okey, &slot, &tree, &tree_len, &heap, &chdr, &vhdr, &arena, &descs, &patch, &scratch, &wp_out}) {
         if (b->p) (void)hipFree(b->p);
         b->p = nullptr;
         b->cap = 0;
@@ -37,6 +38,10 @@ void DeviceImage::release() {
     pinned_cap = 0;
     if (stream) (void)hipStreamDestroy(stream);
     stream = nullptr;
+    if (adopt_stream) (void)hipStreamDestroy(adopt_stream);
+    adopt_stream = nullptr;
+    if (adopt_ev) (void)hipEventDestroy(adopt_ev);
+    adopt_ev = nullptr;
     valid = false;
 }
 
@@ -108,7 +113,8 @@ static void build_leaf(const HostTable &h, uint32_t hl, uint8_t *hd, uint64_t *o
 static void grow_keep(DevBuf &b, uint64_t bytes, uint64_t keep, const char *what, hipStream_t s) {
     if (b.cap >= bytes && b.p) return;
     DevBuf nb;
-    const uint64_t want = std::max<uint64_t>(bytes + bytes / 4, 4096);
+    // doubling: the header arrays grow by one epoch at a time, and each growth synchronises
+    const uint64_t want = std::max<uint64_t>(2 * bytes, 4096);
     hip_check(hipMalloc(&nb.p, want), what);
     nb.cap = want;
     if (b.p && keep) hip_check(hipMemcpyAsync(nb.p, b.p, keep, hipMemcpyDeviceToDevice, s), what);
@@ -159,6 +165,21 @@ uint8_t *pinned_bytes(DeviceImage &d, uint64_t bytes) {
         d.pinned_cap = want;
     }
     return (uint8_t *)d.pinned;
+}
+
+uint8_t *wp_out_bytes(DeviceImage &d, uint64_t bytes) {
+    if (d.wp_out.cap < bytes) {
+        if (d.wp_out.p) {
+            hip_check(hipDeviceSynchronize(), "wp_out drain");
+            hip_check(hipFree(d.wp_out.p), "hipFree wp_out");
+        }
+        d.wp_out.p = nullptr;
+        d.wp_out.cap = 0;
+        const uint64_t want = bytes + bytes / 8 + 4096;
+        hip_check(hipMalloc(&d.wp_out.p, want), "wp_out");
+        d.wp_out.cap = want;
+    }
+    return (uint8_t *)d.wp_out.p;
 }
 
 void reserve_device_rows(HostTable &h, DeviceImage &d, uint64_t extra_images, uint64_t extra_copies,

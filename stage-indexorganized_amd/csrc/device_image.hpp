@@ -21,6 +21,9 @@ struct DeviceImage {
     hipStream_t stream = nullptr;
     DevBuf head, okey, slot, tree, tree_len, heap, chdr, vhdr, arena, descs, patch;
     DevBuf scratch;  // per-call scratch of the device write path / stock-level (scratch_bytes)
+    DevBuf wp_out;   // the write path's slot words + totals, read by its background adoption
+    hipStream_t adopt_stream = nullptr;  // the adoption's D2H copies (beside the caller's stream)
+    hipEvent_t adopt_ev = nullptr;       // end of an epoch's write-path kernels
     std::vector<uint8_t> staging;  // host staging of incremental patches
     void *pinned = nullptr;        // pinned host staging of the device write path's epoch results
     uint64_t pinned_cap = 0;
@@ -49,6 +52,9 @@ void hip_check(hipError_t e, const char *what);
 uint8_t *scratch_bytes(DeviceImage &d, uint64_t bytes);
 // pinned host buffer of at least `bytes` (grown with hipHostMalloc; reused by the next call)
 uint8_t *pinned_bytes(DeviceImage &d, uint64_t bytes);
+// the write path's own output buffer (not shared with scratch_bytes users: its background
+// adoption reads it after the call returned; the next write-path call settles first)
+uint8_t *wp_out_bytes(DeviceImage &d, uint64_t bytes);
 
 // grow the record heap and the copy / version header arrays so that `extra_*` more entries fit
 // after the host's current counts (device write path); refreshes the DevTable view

@@ -222,6 +222,9 @@ void HostTable::adopt_device_epoch(const CopyHdr *copies, uint64_t nc, const Ver
     }
     lap("images");
     // one slot word per touched record (distinct indices): scattered writes in parallel
+    for (uint64_t k = 0; k < nslots; ++k)
+        if (slots[k].idx != ~0ull && slots[k].idx >= meta_.size())
+            throw std::runtime_error("adopt_device_epoch: slot index outside the table");
     parallel_chunks(nslots, [&](uint64_t b, uint64_t e) {
         for (uint64_t k = b; k < e; ++k) {
             const SlotWords &w = slots[k];

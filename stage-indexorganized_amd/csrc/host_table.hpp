@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "chunked.hpp"
+#include "huge_alloc.hpp"
 #include "stage_core.hpp"
 #include "../../include/stage_hip.h"
 
@@ -144,10 +145,10 @@ public:
         bool live = false;
     };
     std::vector<Leaf> leaves_;
-    std::vector<uint64_t> okey_;   // [(leaf*cap + slot)*kw + word]
-    std::vector<uint64_t> meta_;   // [leaf*cap + slot]
-    std::vector<uint32_t> next_;
-    std::vector<uint32_t> image_;
+    std::vector<uint64_t, HugeAlloc<uint64_t>> okey_;   // [(leaf*cap + slot)*kw + word]
+    std::vector<uint64_t, HugeAlloc<uint64_t>> meta_;   // [leaf*cap + slot]
+    std::vector<uint32_t, HugeAlloc<uint32_t>> next_;
+    std::vector<uint32_t, HugeAlloc<uint32_t>> image_;
     int32_t head_ = 0;
     uint32_t nleaves_live_ = 0;
 
@@ -156,16 +157,16 @@ public:
     // the reference's indirection offsets are; a record's location follows it through splits
     // (LeafNode::CopyFrom, b_tree.cpp:1520-1527).  Handle = location id + 1.
     static constexpr uint64_t kNoPos = ~0ull;
-    std::vector<uint32_t> loc_;      // [leaf*cap + slot] -> handle (0 = none)
+    std::vector<uint32_t, HugeAlloc<uint32_t>> loc_;   // [leaf*cap + slot] -> handle (0 = none)
     std::vector<uint64_t> locpos_;   // location id -> host leaf << 16 | slot, kNoPos = dropped
     uint64_t export_locations(uint64_t max, uint64_t *handles, uint32_t *leaf, uint16_t *slot) const;
     void resolve_locations(const uint64_t *handles, uint64_t n, uint32_t *leaf, uint16_t *slot) const;
 
     ChunkedVector<ImageDesc, (1u << 20)> images_;
     ChunkedArena arena_;
-    std::vector<CopyHdr> copies_;
-    std::vector<uint8_t> copy_live_;
-    std::vector<VersionHdr> versions_;
+    std::vector<CopyHdr, HugeAlloc<CopyHdr>> copies_;
+    std::vector<uint8_t, HugeAlloc<uint8_t>> copy_live_;
+    std::vector<VersionHdr, HugeAlloc<VersionHdr>> versions_;
     uint64_t images_synced_ = 0;     // images already present on the device
     uint64_t arena_synced_ = 0;
     bool layout_dirty_ = true;       // any host write since the last publish

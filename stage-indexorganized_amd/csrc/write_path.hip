@@ -26,6 +26,9 @@
 // host-side path needs them (stage_capi::ensure_host_rows).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <string>
+
 #include <hipcub/hipcub.hpp>
 
 #include <chrono>
@@ -452,8 +455,7 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         const uint64_t o_pout = take(n * 32), o_loc0 = take(n * 8), o_loc = take(n * 8), o_op0 = take(n * 4),
                        o_op = take(n * 4), o_head = take(n * 4), o_gs = take(n * 4), o_rcs = take(n), o_succ = take(n),
                        o_prev = take(n * 4), o_ff = take(n * 4), o_ls = take(n * 4), o_gend = take(n * 4), o_big = take(n * 4), o_flags = take(n * 8),
-                       o_ranks = take(n * 8), o_fin = take(n * sizeof(FinRec)), o_tot = take(16),
-                       o_cub = take(cub_bytes);
+                       o_ranks = take(n * 8), o_cub = take(cub_bytes);
         uint8_t *buf = scratch_bytes(dv, off);
         auto *pout = (stage_probe_out_dev *)(buf + o_pout);
         auto *loc0 = (uint64_t *)(buf + o_loc0);
@@ -471,8 +473,10 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         auto *big = (uint32_t *)(buf + o_big);
         auto *flags = (uint64_t *)(buf + o_flags);
         auto *ranks = (uint64_t *)(buf + o_ranks);
-        auto *fin = (FinRec *)(buf + o_fin);
-        auto *tot = (uint64_t *)(buf + o_tot);
+        // slot words + totals: read back after this call returns (background adoption)
+        uint8_t *wo = wp_out_bytes(dv, al(n * sizeof(FinRec)) + 256);
+        auto *fin = (FinRec *)wo;
+        auto *tot = (uint64_t *)(wo + al(n * sizeof(FinRec)));
         void *cub = buf + o_cub;
         size_t cb = cub_bytes;
 
@@ -509,52 +513,74 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
                                                       vbase, ibase, fin, d_rc);
         hip_check(hipGetLastError(), "write-path kernels");
 
-        // the host adopts the epoch
+        // the host adopts the epoch.  The headers and slot words come back on a stream of their
+        // own into pinned staging (full PCIe rate) and the host adopts them on a background
+        // thread (stage_table::adopt) while the caller's stream goes on (the next probe overlaps
+        // the copies); the next call that needs the host table waits for it (host() / settle).
         const double t_enqueue = ms(t0);
-        uint64_t totals[2];
-        hip_check(hipMemcpyAsync(totals, tot, 16, hipMemcpyDeviceToHost, s), "totals");
-        hip_check(hipStreamSynchronize(s), "write path");
+        if (!dv.adopt_stream) hip_check(hipStreamCreateWithFlags(&dv.adopt_stream, hipStreamNonBlocking), "adopt stream");
+        if (!dv.adopt_ev) hip_check(hipEventCreateWithFlags(&dv.adopt_ev, hipEventDisableTiming), "adopt event");
+        hip_check(hipEventRecord(dv.adopt_ev, s), "adopt event");
+        // staging: [totals 64 B][copy headers][version headers][slot words], sized for the worst
+        // case (one copy and one version per op); every part starts on a 16-B boundary (the
+        // headers are 16-B aligned types: a misaligned source faults in the vectorised copy)
+        const uint64_t bf = n * sizeof(FinRec), bmax = 2 * n * sizeof(CopyHdr);
+        static_assert(sizeof(CopyHdr) == sizeof(VersionHdr) && sizeof(CopyHdr) % 16 == 0, "header sizes");
+        uint8_t *pin = pinned_bytes(dv, 64 + bmax + bf);
+        auto *totals = reinterpret_cast<uint64_t *>(pin);
+        auto *fr = reinterpret_cast<FinRec *>(pin + 64 + bmax);
+        uint64_t ns = 0;
+        if (n_ok) {  // the caller wants the count now: wait for the kernels
+            hip_check(hipMemcpyAsync(totals, tot, 16, hipMemcpyDeviceToHost, s), "totals");
+            hip_check(hipStreamSynchronize(s), "write path");
+            ns = totals[0];
+        }
         const double t_kernels = ms(t0);
-        const uint64_t ns = totals[0], nv = totals[1];
-        // headers and slot words into pinned staging (full PCIe rate); the background adoption
-        // reads them there, and the next call settles it before reusing the staging
-        const uint64_t bc = ns * sizeof(CopyHdr), bv = nv * sizeof(VersionHdr), bf = n * sizeof(FinRec);
-        uint8_t *pin = pinned_bytes(dv, bc + bv + bf + 64);
-        auto *copies = reinterpret_cast<CopyHdr *>(pin);
-        auto *versions = reinterpret_cast<VersionHdr *>(pin + bc);
-        auto *fr = reinterpret_cast<FinRec *>(pin + bc + bv);
-        if (ns)
-            hip_check(hipMemcpyAsync(copies, (CopyHdr *)dv.chdr.p + cbase, bc, hipMemcpyDeviceToHost, s), "copy headers");
-        if (nv)
-            hip_check(hipMemcpyAsync(versions, (VersionHdr *)dv.vhdr.p + vbase, bv, hipMemcpyDeviceToHost, s),
-                      "version headers");
-        hip_check(hipMemcpyAsync(fr, fin, bf, hipMemcpyDeviceToHost, s), "slot words");
-        hip_check(hipStreamSynchronize(s), "write path adopt");
-        const double t_d2h = ms(t0);
-        // device slot locations -> host slot indices, in place (FinRec and SlotWords share a
-        // layout; ops that published nothing keep ~0 and are skipped by the adoption)
+        // FinRec and HostTable::SlotWords share a layout: device slot locations become host slot
+        // indices in place (ops that published nothing keep ~0 and are skipped by the adoption)
         static_assert(sizeof(FinRec) == sizeof(HostTable::SlotWords) &&
                           offsetof(FinRec, meta) == offsetof(HostTable::SlotWords, meta) &&
                           offsetof(FinRec, next) == offsetof(HostTable::SlotWords, next) &&
                           offsetof(FinRec, image) == offsetof(HostTable::SlotWords, image),
                       "FinRec / SlotWords layout");
-        // the host adopts the epoch on a background thread (stage_table::adopt) while the device
-        // goes on; the next call that needs the host table waits for it (host() / settle).
-        // Device slot locations -> host slot indices first, in place (FinRec and SlotWords share
-        // a layout; ops that published nothing keep ~0 and are skipped by the adoption)
-        static_assert(sizeof(FinRec) == sizeof(HostTable::SlotWords) &&
-                          offsetof(FinRec, meta) == offsetof(HostTable::SlotWords, meta) &&
-                          offsetof(FinRec, next) == offsetof(HostTable::SlotWords, next) &&
-                          offsetof(FinRec, image) == offsetof(HostTable::SlotWords, image),
-                      "FinRec / SlotWords layout");
-        t->adopt = std::thread([t, &h, &dv, cap = view.cap, n, ns, nv, copies, versions, fr, t0, t_d2h, t_kernels,
-                                t_enqueue, t_reserve]() mutable {
+        t->adopt = std::thread([t, &h, &dv, cap = view.cap, n, cbase, vbase, pin, totals, fr, tot, fin, bf, t0,
+                                t_kernels, t_enqueue, t_reserve]() mutable {
             try {
+                hip_check(hipSetDevice(dv.device), "hipSetDevice");
+                hipStream_t a = dv.adopt_stream;
+                hip_check(hipStreamWaitEvent(a, dv.adopt_ev, 0), "adopt wait");
+                hip_check(hipMemcpyAsync(totals, tot, 16, hipMemcpyDeviceToHost, a), "totals");
+                hip_check(hipMemcpyAsync(fr, fin, bf, hipMemcpyDeviceToHost, a), "slot words");
+                hip_check(hipStreamSynchronize(a), "adopt totals");
+                const uint64_t ns = totals[0], nv = totals[1];
+                auto *copies = reinterpret_cast<CopyHdr *>(pin + 64);
+                auto *versions = reinterpret_cast<VersionHdr *>(pin + 64 + ns * sizeof(CopyHdr));
+                if (ns)
+                    hip_check(hipMemcpyAsync(copies, (CopyHdr *)dv.chdr.p + cbase, ns * sizeof(CopyHdr),
+                                             hipMemcpyDeviceToHost, a),
+                              "copy headers");
+                if (nv)
+                    hip_check(hipMemcpyAsync(versions, (VersionHdr *)dv.vhdr.p + vbase, nv * sizeof(VersionHdr),
+                                             hipMemcpyDeviceToHost, a),
+                              "version headers");
+                hip_check(hipStreamSynchronize(a), "adopt headers");
+                const double t_d2h = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
                 const std::vector<uint32_t> &d2h = dv.dev_to_host;
+                std::atomic<uint64_t> bad{0};
                 HostTable::parallel_chunks(n, [&](uint64_t b, uint64_t e) {
-                    for (uint64_t k = b; k < e; ++k)
-                        if (fr[k].loc != ~0ull) fr[k].loc = (uint64_t)d2h[fr[k].loc / cap] * cap + fr[k].loc % cap;
+                    for (uint64_t k = b; k < e; ++k) {
+                        if (fr[k].loc == ~0ull) continue;
+                        if (fr[k].loc / cap >= d2h.size()) {
+                            bad.fetch_add(1);
+                            fr[k].loc = ~0ull;
+                            continue;
+                        }
+                        fr[k].loc = (uint64_t)d2h[fr[k].loc / cap] * cap + fr[k].loc % cap;
+                    }
                 });
+                if (bad.load())
+                    throw std::runtime_error("write path: " + std::to_string(bad.load()) +
+                                             " slot words outside the table (ns " + std::to_string(ns) + ")");
                 h.adopt_device_epoch(copies, ns, versions, nv, ns, reinterpret_cast<const HostTable::SlotWords *>(fr), n);
                 if (trace)
                     std::fprintf(stderr,
