@@ -36,7 +36,7 @@ hipError_t launch_probe(const DevTable &t, const uint64_t *keys, const uint16_t 
 struct ScanTuning {
     int rows = 4;        // tuple rows in flight per wave (2, 4 or 8)
     int max_blocks = 0;  // 0 = default grid cap (16384 blocks of 256 threads)
-    int first_scans = 0; // scans per wave in lockstep of the first-tuple scans (1, 2, 4; 0 = 1)
+    int first_scans = 0; // first-tuple scans: 0 = scan_first_fast_kernel, 1 = general single-scan kernel, 2 / 4 = lockstep
 };
 
 // row_status != nullptr: IndexScanExecutor range semantics (per-record visibility for

@@ -1227,6 +1227,207 @@ __global__ __launch_bounds__(256) void scan_first_multi_kernel(DevTable t, const
     }
 }
 
+// Chunk-cooperative lower bound of kFirstChunk fixed-width start keys: lane L works for scan
+// L/4 and compares a quarter of each node (4 of the 16 inner entries, 2 of the 8 bottom ones);
+// two xor-shuffles sum the quarter counts.  Same result as tree_lower_bound (le_child = true),
+// one round trip per level for all 16 scans, a quarter of the per-lane loads and compares.
+template <int KW>
+__device__ __forceinline__ uint32_t chunk_lower_bound(const DevTable &t, const uint64_t *x, uint32_t part) {
+    static_assert(kTreeFanout == 16 && kLeafFanout == 8, "quarters sized for 16 / 8 entries");
+    uint32_t node = 0;
+    for (int lvl = (int)t.levels - 1; lvl >= 0; --lvl) {
+        const bool inner = lvl > 0;
+        const uint32_t f = inner ? (uint32_t)kTreeFanout : (uint32_t)kLeafFanout;
+        const uint32_t per = f / 4;
+        const uint64_t *e = t.tree + (t.level_off[lvl] + (uint64_t)node * f + part * per) * KW;
+        uint64_t w0[KW], w1[KW], w2[KW], w3[KW];
+#pragma unroll
+        for (int j = 0; j < KW; ++j) {
+            w0[j] = e[j];
+            w1[j] = e[KW + j];
+            w2[j] = inner ? e[2 * KW + j] : ~0ull;
+            w3[j] = inner ? e[3 * KW + j] : ~0ull;
+        }
+        int c = (kw_lt<KW>(w0, x) ? 1 : 0) + (kw_lt<KW>(w1, x) ? 1 : 0);
+        if (inner) c += (kw_lt<KW>(w2, x) ? 1 : 0) + (kw_lt<KW>(w3, x) ? 1 : 0);
+        c += __shfl_xor(c, 1);
+        c += __shfl_xor(c, 2);
+        node = node * f + (uint32_t)c;
+    }
+    return node < t.nseps ? node : t.nseps;
+}
+
+// scan_first_kernel's semantics (scan_one_compact + FirstPrefixSink, fixed-width keys) with
+// the per-scan instruction count cut (the single-scan kernel issues ~1070 instructions per scan
+// and is issue- as much as latency-bound: profiles/r02/prof/tpcc_insts):
+//  * the chunk's 16 start-leaf descents are chunk-cooperative (chunk_lower_bound);
+//  * a slot group's visibility mask and key columns load together (one round trip);
+//  * the kept records' ranks: when they are increasing in slot order (a start key in a leaf's
+//    sorted region -- the common case) rank = slot-order position, checked with one compare
+//    per record against its predecessor; otherwise the O(m) count of the general kernel;
+//  * visibility is resolved only for records carrying the start key's prefix (the sink keeps
+//    no other record), and the lowest-rank passing record is a ctz on the fast path.
+template <int SPL, int KW, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void scan_first_fast_kernel(DevTable t, const uint64_t *__restrict__ keys,
+                                                              uint64_t n, uint32_t scan_size,
+                                                              const uint32_t *__restrict__ rids, uint32_t words,
+                                                              uint32_t *__restrict__ img_out,
+                                                              uint8_t *__restrict__ st_out) {
+    __shared__ uint64_t s_keys[4][64 * KW];
+    __shared__ uint32_t s_slot[4][64];
+    const uint32_t lane = lane_id(), wv = uni32(threadIdx.x >> 6);
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint32_t len = t.key_width;
+    uint64_t *lk = s_keys[wv];
+    uint32_t *ls = s_slot[wv];
+    for (uint64_t c0 = wave * kFirstChunk; c0 < n; c0 += nwaves * kFirstChunk) {
+        const uint64_t i = c0 + (lane >> 2);  // the scan this lane descends for
+        const bool valid = i < n;
+        uint64_t ok[KW];
+        load_okey<KW>(keys, i, valid, len, ok);
+        const uint32_t leafv = chunk_lower_bound<KW>(t, ok, lane & 3);
+        const uint32_t ridv = valid && rids ? rids[i] : 0xFFFFFFFEu;
+        const int cnt = (int)((n - c0) < (uint64_t)kFirstChunk ? (n - c0) : (uint64_t)kFirstChunk);
+        uint32_t my_img = 0xFFFFFFFFu, my_st = ST_NOT_FOUND;
+        for (int j = 0; j < cnt; ++j) {
+            const int src = 4 * j;
+            uint64_t x[KW], pre[KW];
+#pragma unroll
+            for (int w = 0; w < KW; ++w) x[w] = pre[w] = rl64(ok[w], src);
+            uint32_t leaf = rl32(leafv, src);
+            const uint32_t rid = rl32(ridv, src);
+            uint32_t img = 0xFFFFFFFFu, st = ST_NOT_FOUND, remaining = scan_size;
+            bool cont = false;
+            for (uint32_t guard = 0; guard < scan_size + 2 && remaining > 0; ++guard) {
+                const uint64_t base = (uint64_t)leaf * t.cap;
+                // slot groups that can hold a key >= x (lane g tests group g's max key)
+                bool act = false;
+                if (lane < (uint32_t)SPL) {
+                    const uint64_t *gm =
+                        reinterpret_cast<const uint64_t *>(t.head + (uint64_t)leaf * t.head_bytes +
+                                                           head_gmax_offset(t.cap)) + lane * KW;
+                    uint64_t g[KW];
+#pragma unroll
+                    for (int w = 0; w < KW; ++w) g[w] = gm[w];
+                    act = !kw_lt<KW>(g, x);
+                }
+                uint64_t active = ballot(act);
+                const uint32_t to_scan = remaining;
+                uint32_t kept = 0;
+                while (active) {
+                    const int s = __builtin_ctzll(active);
+                    active &= active - 1;
+                    const uint64_t vm = head_vis(t, leaf, s);
+                    uint64_t col[KW];
+#pragma unroll
+                    for (int w = 0; w < KW; ++w) col[w] = t.okey[((uint64_t)leaf * KW + w) * t.cap + s * 64 + lane];
+                    const bool vis = (vm >> lane) & 1;
+                    const uint64_t q = ballot(vis && !kw_lt<KW>(col, x));
+                    if (!q) continue;
+                    const uint32_t rank = kept + count_below(q);
+                    const bool take = ((q >> lane) & 1) && rank <= to_scan;
+                    if (take) {
+#pragma unroll
+                        for (int w = 0; w < KW; ++w) lk[rank * KW + w] = col[w];
+                        ls[rank] = (uint32_t)(s * 64) + lane;
+                    }
+                    kept += (uint32_t)__builtin_popcountll(ballot(take));
+                    if (kept > to_scan) break;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const uint32_t m = kept;
+                if (m == 0) break;
+                const bool mine = lane < m;
+                uint64_t mk[KW];
+                uint32_t mslot = 0;
+#pragma unroll
+                for (int w = 0; w < KW; ++w) mk[w] = mine ? lk[lane * KW + w] : 0ull;
+                bool ord = true;
+                if (mine) {
+                    mslot = ls[lane];
+                    if (lane > 0) {
+                        uint64_t pk[KW];
+#pragma unroll
+                        for (int w = 0; w < KW; ++w) pk[w] = lk[(lane - 1) * KW + w];
+                        ord = kw_lt<KW>(pk, mk);
+                    }
+                }
+                const bool sorted = ballot(!ord) == 0;
+                uint32_t kr = lane;
+                if (!sorted) {
+                    kr = 0;
+                    for (uint32_t jj = 0; jj < m; ++jj) {
+                        uint64_t kj[KW];
+#pragma unroll
+                        for (int w = 0; w < KW; ++w) kj[w] = lk[jj * KW + w];
+                        kr += (mine && kw_lt<KW>(kj, mk)) ? 1u : 0u;
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();  // the LDS list is rewritten on the next leaf
+                if (cont) {  // the continuation re-popped the last key: the scan ends
+                    bool eq = true;
+#pragma unroll
+                    for (int w = 0; w < KW; ++w) eq = eq && mk[w] == x[w];
+                    if (ballot(mine && kr == 0 && eq)) break;
+                }
+                const uint32_t e = m < remaining ? m : remaining;
+                uint8_t sv = ST_NOT_FOUND;
+                uint32_t im = 0xFFFFFFFFu;
+                bool pass = false;
+                if (mine && kr < e) {
+                    bool pfx = true;
+#pragma unroll
+                    for (int w = 0; w < KW; ++w)
+                        if ((uint32_t)w < words) pfx = pfx && mk[w] == pre[w];
+                    if (pfx) {
+                        im = scan_visible(t, t.slot[base + mslot], rid, sv);
+                        pass = sv == ST_LATEST || sv == ST_OLD;
+                    }
+                }
+                uint64_t pm = ballot(pass);
+                if (pm) {  // the passing record of lowest rank
+                    int bl = __builtin_ctzll(pm);
+                    if (!sorted) {
+                        uint32_t best = 0xFFFFFFFFu;
+                        while (pm) {
+                            const int b = __builtin_ctzll(pm);
+                            pm &= pm - 1;
+                            const uint32_t rr = rl32(kr, b);
+                            if (rr < best) {
+                                best = rr;
+                                bl = b;
+                            }
+                        }
+                    }
+                    img = rl32(im, bl);
+                    st = rl32((uint32_t)sv, bl);
+                    break;
+                }
+                remaining -= e;
+                if (e < m) break;
+                // last record popped: continue from its key with le_child = false
+                const uint64_t lm = ballot(mine && kr == m - 1);
+                const int b = __builtin_ctzll(lm);
+#pragma unroll
+                for (int w = 0; w < KW; ++w) x[w] = rl64(mk[w], b);
+                leaf = uni32(next_leaf_after<false, KW>(t, leaf, x, len));
+                cont = true;
+            }
+            if (lane == (uint32_t)j) {
+                my_img = img;
+                my_st = st;
+            }
+        }
+        if (lane < (uint32_t)cnt) {
+            img_out[c0 + lane] = my_img;
+            st_out[c0 + lane] = (uint8_t)my_st;
+        }
+    }
+}
+
 // One wave per scan (grid-stride over scans): the start key's descent is wave-uniform, and a
 // wide grid keeps many scans -- and their R rows in flight each -- resident per CU.
 template <bool VARLEN, int SPL, int R, int KW = 1, bool VIS = false>
@@ -1573,11 +1774,18 @@ hipError_t launch_scan_first(const DevTable &t, const uint64_t *keys, uint64_t n
     if (n == 0) return hipSuccess;
     if (t.key_width == 0 || scan_size == 0 || scan_size > 63) return hipErrorInvalidValue;
     const int blocks = grid_for((n + kFirstChunk - 1) / kFirstChunk, 4, tune.max_blocks > 0 ? tune.max_blocks : 16384);
-    // NS scans per wave in lockstep (scan_first_multi_kernel, STAGE_SL_SCANS=2 or 4) or one at a
-    // time (default): measured equal at 2 (33.4 vs 33.6 M txns/s) and 19 % slower at 4
-    const int ns = tune.first_scans > 0 ? tune.first_scans : 1;
+    // default: scan_first_fast_kernel (STAGE_SL_SCANS unset or 0).  STAGE_SL_SCANS=1: the general
+    // single-scan kernel; 2 / 4: NS scans per wave in lockstep (scan_first_multi_kernel, measured
+    // equal to the single-scan kernel at 2 and 19 % slower at 4)
+    const int ns = tune.first_scans;
 #define STAGE_FIRST(S, KW)                                                                                  \
-    if (ns == 1)                                                                                            \
+    if (ns == 0)                                                                                            \
+        scan_first_fast_kernel<S, KW, 8><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words, img_out, \
+                                                                st_out);                                    \
+    else if (ns < 0)                                                                                        \
+        scan_first_fast_kernel<S, KW, 1><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words, img_out, \
+                                                                st_out);                                    \
+    else if (ns == 1)                                                                                       \
         scan_first_kernel<S, KW><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words, img_out, st_out); \
     else if (ns == 4)                                                                                       \
         scan_first_multi_kernel<S, KW, 4><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words, img_out,   \

@@ -10,8 +10,7 @@ from tpcc_data import TpccTables, key, stock_level_device
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def tpcc(gpu):
+def _tables():
     tt = TpccTables()
     rng = np.random.default_rng(8)
     # committed history: stock quantities and order-line delivery dates change at commit 11 / 21
@@ -26,6 +25,11 @@ def tpcc(gpu):
     tt.update("stock", key(2, 5), 0, np.int32(1).tobytes(), 30)
     tt.sync()
     return tt
+
+
+@pytest.fixture(scope="module")
+def tpcc(gpu):
+    return _tables()
 
 
 def test_index_scan_visibility_matches_oracle(tpcc):
@@ -63,3 +67,25 @@ def test_stock_level_matches_oracle(tpcc):
     got2 = stock_level_device(tt, w[5:50], d[5:50], thr[5:50])
     exp2 = np.array([tt.stock_level_oracle(int(a), int(b), int(c)) for a, b, c in zip(w[5:50], d[5:50], thr[5:50])])
     assert (got2 == exp2).all()
+
+
+@pytest.mark.parametrize("variant", ["0", "-1", "1", "2", "4"])
+def test_stock_level_scan_kernel_variants(gpu, monkeypatch, variant):
+    """Every first-tuple scan kernel (STAGE_SL_SCANS: 0 = scan_first_fast_kernel at 8 waves/SIMD,
+    -1 = the same without the occupancy cap, 1 = the general single-scan kernel, 2 / 4 = lockstep)
+    gives the oracle's stock-level results.  Order lines are inserted in numeric order, which is
+    not their memcmp key order, so leaves carry unsorted regions (the fast kernel's O(m) ranking)
+    and sorted ones (its slot-order ranking); starts of orders with fewer than 5 lines continue
+    across leaves."""
+    monkeypatch.setenv("STAGE_SL_SCANS", variant)
+    tt = _tables()
+    rng = np.random.default_rng(11)
+    n = 1000
+    w = rng.integers(1, 3, n)
+    d = rng.integers(1, 11, n)
+    thr = rng.integers(10, 31, n)
+    rids = rng.choice(np.array([0, 5, 11, 15, 21, 31, 0xFFFFFFFE], np.uint32), n)
+    got = stock_level_device(tt, w, d, thr, rids)
+    exp = np.array([tt.stock_level_oracle(int(a), int(b), int(c), int(r)) for a, b, c, r in zip(w, d, thr, rids)])
+    assert (got == exp).all(), np.nonzero(got != exp)[0][:10]
+    assert (got > 0).any()
