@@ -274,6 +274,15 @@ int stage_index_scan_batch(stage_table *t, const uint64_t *d_start_keys, const u
                            const uint32_t *d_read_ids, uint64_t n, uint32_t scan_size,
                            uint32_t *d_counts, uint8_t *d_records, uint8_t *d_row_status,
                            void *stream);
+/* The IndexScanExecutor range branch of stage_index_scan_batch consumed only up to its first
+ * produced tuple (LATEST or OLD) whose key begins with the start key's first `prefix_words`
+ * 8-byte fields (0..key_words) -- the predicate TPC-C stock-level puts on its ORDER_LINE scans
+ * (tpcc_stock_level.cpp:104-135 keeps ol_i_ids[0]).  Fixed-width keys of 9..32 bytes (or 8),
+ * scan_size 1..63.  d_image[i] = the tuple's record-heap row (0xFFFFFFFF if none),
+ * d_status[i] = STAGE_ST_LATEST / STAGE_ST_OLD / STAGE_ST_NOT_FOUND. */
+int stage_index_scan_first_batch(stage_table *t, const uint64_t *d_start_keys, const uint32_t *d_read_ids,
+                                 uint64_t n, uint32_t scan_size, uint32_t prefix_words, uint32_t *d_image,
+                                 uint8_t *d_status, void *stream);
 
 /* ---- host-buffer forms (keys and results in host memory) --------------------------------
  * stage_probe_host: stage_probe_batch for host buffers; the batch is cut into chunks that

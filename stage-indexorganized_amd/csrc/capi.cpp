@@ -404,6 +404,22 @@ int stage_index_scan_batch(stage_table *t, const uint64_t *d_start_keys, const u
     return hip_rc(e, "index scan kernel");
 }
 
+int stage_index_scan_first_batch(stage_table *t, const uint64_t *d_start_keys, const uint32_t *d_read_ids,
+                                 uint64_t n, uint32_t scan_size, uint32_t prefix_words, uint32_t *d_image,
+                                 uint8_t *d_status, void *stream) {
+    int rc = need_synced(t);
+    if (rc) return rc;
+    if (t->dev.view.key_width == 0) return fail(STAGE_E_ARG, "first-tuple scans need fixed-width keys");
+    if (scan_size == 0 || scan_size > 63) return fail(STAGE_E_ARG, "scan_size must be 1..63");
+    if (prefix_words > t->dev.view.key_words) return fail(STAGE_E_ARG, "prefix_words exceeds the key's words");
+    if (n && (!d_start_keys || !d_image || !d_status)) return fail(STAGE_E_ARG, "null device buffer");
+    hipError_t e = hipSetDevice(t->dev.device);
+    if (e != hipSuccess) return hip_rc(e, "hipSetDevice");
+    e = stage::launch_scan_first(t->dev.view, d_start_keys, n, scan_size, d_read_ids, prefix_words, d_image, d_status,
+                                 pick(t, stream), t->scan_tune);
+    return hip_rc(e, "first-tuple scan kernel");
+}
+
 int stage_resolve_batch(stage_table *t, const uint64_t *d_keys, const uint16_t *d_lens, uint64_t n, int le_child,
                         uint32_t *d_leaf, void *stream) {
     int rc = need_synced(t);

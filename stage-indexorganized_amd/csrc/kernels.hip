@@ -976,6 +976,7 @@ __global__ __launch_bounds__(256) void scan_kernel_compact(DevTable t, const uin
 // only up to its first produced tuple with the start key's first `words` order words
 // (FirstPrefixSink); img_out[i] / st_out[i] = that tuple's heap row and status.
 constexpr int kFirstChunk = 16;
+constexpr uint8_t kFirstUndecided = 0xFE;  // scan_first_split_kernel -> scan_first_rest_kernel
 template <int SPL, int KW>
 __global__ __launch_bounds__(256) void scan_first_kernel(DevTable t, const uint64_t *__restrict__ keys, uint64_t n,
                                                          uint32_t scan_size, const uint32_t *__restrict__ rids,
@@ -1267,7 +1268,7 @@ __device__ __forceinline__ uint32_t chunk_lower_bound(const DevTable &t, const u
 //    per record against its predecessor; otherwise the O(m) count of the general kernel;
 //  * visibility is resolved only for records carrying the start key's prefix (the sink keeps
 //    no other record), and the lowest-rank passing record is a ctz on the fast path.
-template <int SPL, int KW, int WPE>
+template <int SPL, int KW, int WPE, bool PF>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void scan_first_fast_kernel(DevTable t, const uint64_t *__restrict__ keys,
                                                               uint64_t n, uint32_t scan_size,
                                                               const uint32_t *__restrict__ rids, uint32_t words,
@@ -1289,21 +1290,63 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         const uint32_t leafv = chunk_lower_bound<KW>(t, ok, lane & 3);
         const uint32_t ridv = valid && rids ? rids[i] : 0xFFFFFFFEu;
         const int cnt = (int)((n - c0) < (uint64_t)kFirstChunk ? (n - c0) : (uint64_t)kFirstChunk);
+        // PF: the start leaves' active slot groups of all 16 scans in one round trip (lane L
+        // tests groups L%4, L%4+4, ... for scan L/4), and scan j+1's first active group (mask +
+        // key columns) in flight while scan j runs
+        uint32_t actv = 0;
+        uint64_t pf_vm = 0, pf_col[KW];
+        int pf_s = 0;
+        if (PF) {
+            const uint64_t *gm = reinterpret_cast<const uint64_t *>(t.head + (uint64_t)leafv * t.head_bytes +
+                                                                    head_gmax_offset(t.cap));
+#pragma unroll
+            for (int g = 0; g < SPL; g += 4) {
+                const uint32_t gg = (uint32_t)g + (lane & 3);
+                if (gg < (uint32_t)SPL) {
+                    uint64_t e[KW];
+#pragma unroll
+                    for (int w = 0; w < KW; ++w) e[w] = gm[gg * KW + w];
+                    actv |= kw_lt<KW>(e, ok) ? 0u : (1u << gg);
+                }
+            }
+            actv |= (uint32_t)__shfl_xor((int)actv, 1);
+            actv |= (uint32_t)__shfl_xor((int)actv, 2);
+            const uint32_t a0 = rl32(actv, 0), l0 = rl32(leafv, 0);
+            pf_s = a0 ? __builtin_ctz(a0) : 0;
+            pf_vm = head_vis(t, l0, pf_s);
+#pragma unroll
+            for (int w = 0; w < KW; ++w) pf_col[w] = t.okey[((uint64_t)l0 * KW + w) * t.cap + pf_s * 64 + lane];
+        }
         uint32_t my_img = 0xFFFFFFFFu, my_st = ST_NOT_FOUND;
         for (int j = 0; j < cnt; ++j) {
             const int src = 4 * j;
-            uint64_t x[KW], pre[KW];
+            uint64_t x[KW];
 #pragma unroll
-            for (int w = 0; w < KW; ++w) x[w] = pre[w] = rl64(ok[w], src);
+            for (int w = 0; w < KW; ++w) x[w] = rl64(ok[w], src);
             uint32_t leaf = rl32(leafv, src);
             const uint32_t rid = rl32(ridv, src);
             uint32_t img = 0xFFFFFFFFu, st = ST_NOT_FOUND, remaining = scan_size;
             bool cont = false;
+            // pf_* hold this scan's first group; once it is consumed the next scan's goes in flight
+            bool pf_pending = PF;
+            auto issue_next = [&]() {
+                pf_pending = false;
+                if (j + 1 < cnt) {
+                    const uint32_t an = rl32(actv, src + 4), ln = rl32(leafv, src + 4);
+                    pf_s = an ? __builtin_ctz(an) : 0;
+                    pf_vm = head_vis(t, ln, pf_s);
+#pragma unroll
+                    for (int w = 0; w < KW; ++w)
+                        pf_col[w] = t.okey[((uint64_t)ln * KW + w) * t.cap + pf_s * 64 + lane];
+                }
+            };
             for (uint32_t guard = 0; guard < scan_size + 2 && remaining > 0; ++guard) {
                 const uint64_t base = (uint64_t)leaf * t.cap;
                 // slot groups that can hold a key >= x (lane g tests group g's max key)
                 bool act = false;
-                if (lane < (uint32_t)SPL) {
+                if (PF && guard == 0) {
+                    act = lane < (uint32_t)SPL && ((rl32(actv, src) >> lane) & 1);
+                } else if (lane < (uint32_t)SPL) {
                     const uint64_t *gm =
                         reinterpret_cast<const uint64_t *>(t.head + (uint64_t)leaf * t.head_bytes +
                                                            head_gmax_offset(t.cap)) + lane * KW;
@@ -1318,13 +1361,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 while (active) {
                     const int s = __builtin_ctzll(active);
                     active &= active - 1;
-                    const uint64_t vm = head_vis(t, leaf, s);
-                    uint64_t col[KW];
+                    uint64_t vm, col[KW];
+                    const bool from_pf = PF && pf_pending && s == pf_s;
+                    if (from_pf) {  // the first visit's first group: prefetched
+                        vm = pf_vm;
 #pragma unroll
-                    for (int w = 0; w < KW; ++w) col[w] = t.okey[((uint64_t)leaf * KW + w) * t.cap + s * 64 + lane];
+                        for (int w = 0; w < KW; ++w) col[w] = pf_col[w];
+                    } else {
+                        vm = head_vis(t, leaf, s);
+#pragma unroll
+                        for (int w = 0; w < KW; ++w) col[w] = t.okey[((uint64_t)leaf * KW + w) * t.cap + s * 64 + lane];
+                    }
                     const bool vis = (vm >> lane) & 1;
                     const uint64_t q = ballot(vis && !kw_lt<KW>(col, x));
-                    if (!q) continue;
                     const uint32_t rank = kept + count_below(q);
                     const bool take = ((q >> lane) & 1) && rank <= to_scan;
                     if (take) {
@@ -1332,9 +1381,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                         for (int w = 0; w < KW; ++w) lk[rank * KW + w] = col[w];
                         ls[rank] = (uint32_t)(s * 64) + lane;
                     }
+                    if (from_pf) issue_next();
+                    if (!q) continue;
                     kept += (uint32_t)__builtin_popcountll(ballot(take));
                     if (kept > to_scan) break;
                 }
+                if (PF && pf_pending) issue_next();
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1381,7 +1433,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                     bool pfx = true;
 #pragma unroll
                     for (int w = 0; w < KW; ++w)
-                        if ((uint32_t)w < words) pfx = pfx && mk[w] == pre[w];
+                        if ((uint32_t)w < words) pfx = pfx && mk[w] == rl64(ok[w], src);  // start key prefix
                     if (pfx) {
                         im = scan_visible(t, t.slot[base + mslot], rid, sv);
                         pass = sv == ST_LATEST || sv == ST_OLD;
@@ -1424,6 +1476,241 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         if (lane < (uint32_t)cnt) {
             img_out[c0 + lane] = my_img;
             st_out[c0 + lane] = (uint8_t)my_st;
+        }
+    }
+}
+
+// The first-tuple scans split in two stages per chunk of 16 (same results as scan_first_kernel):
+//  A (wave per scan, in turn): the start leaf's first visit -- active groups (all 16 scans' in
+//    one round trip), the first group prefetched while the previous scan runs, the kept records
+//    ranked (slot order when increasing), and the first e = min(m, scan_size) of them in rank
+//    order written to LDS as candidates: the slot of a record carrying the start key's prefix,
+//    or a hole;
+//  B (lane per scan, all 16 together): the candidates' slot words and visibility in rank order,
+//    the first LATEST / OLD one is the result -- one round trip for the 16 scans instead of one
+//    per scan;
+//  a scan whose first visit decides nothing (no candidate passed, the visit held m <= e records
+//    and the scan has records left) is re-run by the general loop (scan_one_compact +
+//    FirstPrefixSink), which continues across leaves.
+template <int SPL, int KW, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void scan_first_split_kernel(
+    DevTable t, const uint64_t *__restrict__ keys, uint64_t n, uint32_t scan_size, const uint32_t *__restrict__ rids,
+    uint32_t words, uint32_t *__restrict__ img_out, uint8_t *__restrict__ st_out) {
+    __shared__ uint64_t s_keys[4][64 * KW];
+    __shared__ uint32_t s_slot[4][64];
+    __shared__ uint16_t s_cand[4][kFirstChunk][64];
+    const uint32_t lane = lane_id(), wv = uni32(threadIdx.x >> 6);
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint32_t len = t.key_width;
+    uint64_t *lk = s_keys[wv];
+    uint32_t *ls = s_slot[wv];
+    constexpr uint16_t kHole = 0xFFFF;
+    for (uint64_t c0 = wave * kFirstChunk; c0 < n; c0 += nwaves * kFirstChunk) {
+        const uint64_t i = c0 + (lane >> 2);  // the scan this lane descends for
+        const bool valid = i < n;
+        uint64_t ok[KW];
+        load_okey<KW>(keys, i, valid, len, ok);
+        const uint32_t leafv = chunk_lower_bound<KW>(t, ok, lane & 3);
+        const uint32_t ridv = valid && rids ? rids[i] : 0xFFFFFFFEu;
+        const int cnt = (int)((n - c0) < (uint64_t)kFirstChunk ? (n - c0) : (uint64_t)kFirstChunk);
+        // active slot groups of every start leaf (lane L tests groups L%4, L%4+4, ... of scan L/4)
+        uint32_t actv = 0;
+        {
+            const uint64_t *gm = reinterpret_cast<const uint64_t *>(t.head + (uint64_t)leafv * t.head_bytes +
+                                                                    head_gmax_offset(t.cap));
+#pragma unroll
+            for (int g = 0; g < SPL; g += 4) {
+                const uint32_t gg = (uint32_t)g + (lane & 3);
+                if (gg < (uint32_t)SPL) {
+                    uint64_t e[KW];
+#pragma unroll
+                    for (int w = 0; w < KW; ++w) e[w] = gm[gg * KW + w];
+                    actv |= kw_lt<KW>(e, ok) ? 0u : (1u << gg);
+                }
+            }
+            actv |= (uint32_t)__shfl_xor((int)actv, 1);
+            actv |= (uint32_t)__shfl_xor((int)actv, 2);
+        }
+        uint64_t pf_vm, pf_col[KW];
+        int pf_s;
+        auto prefetch = [&](int jn) {
+            const uint32_t an = rl32(actv, 4 * jn), ln = rl32(leafv, 4 * jn);
+            pf_s = an ? __builtin_ctz(an) : 0;
+            pf_vm = head_vis(t, ln, pf_s);
+#pragma unroll
+            for (int w = 0; w < KW; ++w) pf_col[w] = t.okey[((uint64_t)ln * KW + w) * t.cap + pf_s * 64 + lane];
+        };
+        prefetch(0);
+        uint32_t my_info = 0;  // lane j: scan j's candidate count e | 0x100 if an undecided visit continues
+        // ---- stage A
+        for (int j = 0; j < cnt; ++j) {
+            const int src = 4 * j;
+            uint64_t x[KW];
+#pragma unroll
+            for (int w = 0; w < KW; ++w) x[w] = rl64(ok[w], src);
+            const uint32_t leaf = rl32(leafv, src);
+            uint64_t active = ballot(lane < (uint32_t)SPL && ((rl32(actv, src) >> lane) & 1));
+            bool pending = true;
+            uint32_t kept = 0;
+            while (active) {
+                const int s = __builtin_ctzll(active);
+                active &= active - 1;
+                uint64_t vm, col[KW];
+                const bool from_pf = pending && s == pf_s;
+                if (from_pf) {
+                    vm = pf_vm;
+#pragma unroll
+                    for (int w = 0; w < KW; ++w) col[w] = pf_col[w];
+                } else {
+                    vm = head_vis(t, leaf, s);
+#pragma unroll
+                    for (int w = 0; w < KW; ++w) col[w] = t.okey[((uint64_t)leaf * KW + w) * t.cap + s * 64 + lane];
+                }
+                const bool vis = (vm >> lane) & 1;
+                const uint64_t q = ballot(vis && !kw_lt<KW>(col, x));
+                const uint32_t rank = kept + count_below(q);
+                const bool take = ((q >> lane) & 1) && rank <= scan_size;
+                if (take) {
+#pragma unroll
+                    for (int w = 0; w < KW; ++w) lk[rank * KW + w] = col[w];
+                    ls[rank] = (uint32_t)(s * 64) + lane;
+                }
+                if (from_pf) {
+                    pending = false;
+                    if (j + 1 < cnt) prefetch(j + 1);
+                }
+                kept += (uint32_t)__builtin_popcountll(ballot(take));
+                if (kept > scan_size) break;
+            }
+            if (pending && j + 1 < cnt) prefetch(j + 1);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const uint32_t m = kept;
+            uint32_t info = 0;
+            if (m > 0) {
+                const bool mine = lane < m;
+                uint64_t mk[KW];
+                uint32_t mslot = 0;
+#pragma unroll
+                for (int w = 0; w < KW; ++w) mk[w] = mine ? lk[lane * KW + w] : 0ull;
+                bool ord = true;
+                if (mine) {
+                    mslot = ls[lane];
+                    if (lane > 0) {
+                        uint64_t pk[KW];
+#pragma unroll
+                        for (int w = 0; w < KW; ++w) pk[w] = lk[(lane - 1) * KW + w];
+                        ord = kw_lt<KW>(pk, mk);
+                    }
+                }
+                uint32_t kr = lane;
+                bool dup = false;
+                if (ballot(!ord)) {
+                    kr = 0;
+                    for (uint32_t jj = 0; jj < m; ++jj) {
+                        uint64_t kj[KW];
+                        bool eq = jj != lane;
+#pragma unroll
+                        for (int w = 0; w < KW; ++w) {
+                            kj[w] = lk[jj * KW + w];
+                            eq = eq && kj[w] == mk[w];
+                        }
+                        kr += (mine && kw_lt<KW>(kj, mk)) ? 1u : 0u;
+                        dup = dup || (mine && eq);
+                    }
+                }
+                const uint32_t e = m < scan_size ? m : scan_size;
+                if (ballot(dup)) {
+                    info = 0x200u;  // equal keys share a rank: the general loop decides
+                } else {
+                    if (lane < e) s_cand[wv][j][lane] = kHole;
+                    if (mine && kr < e) {
+                        bool pfx = true;
+#pragma unroll
+                        for (int w = 0; w < KW; ++w)
+                            if ((uint32_t)w < words) pfx = pfx && mk[w] == x[w];
+                        if (pfx) s_cand[wv][j][kr] = (uint16_t)mslot;
+                    }
+                    info = e | (e == m && scan_size > e ? 0x100u : 0u);
+                }
+            }
+            __builtin_amdgcn_wave_barrier();  // the LDS list is rewritten by the next scan
+            if (lane == (uint32_t)j) my_info = info;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // ---- stage B: lane j resolves scan j's candidates in rank order
+        const uint32_t my_leaf = (uint32_t)__shfl((int)leafv, (int)(4 * (lane & 15)));
+        const uint32_t my_rid = (uint32_t)__shfl((int)ridv, (int)(4 * (lane & 15)));
+        uint32_t my_img = 0xFFFFFFFFu, my_st = ST_NOT_FOUND;
+        bool found = false;
+        if (lane < (uint32_t)cnt) {
+            const uint32_t e = my_info & 0xFF;
+            const uint64_t base = (uint64_t)my_leaf * t.cap;
+            for (uint32_t c = 0; c < e; ++c) {
+                const uint16_t sl = s_cand[wv][lane][c];
+                if (sl == kHole) continue;
+                uint8_t sv;
+                const uint32_t im = scan_visible(t, t.slot[base + sl], my_rid, sv);
+                if (sv == ST_LATEST || sv == ST_OLD) {
+                    my_img = im;
+                    my_st = sv;
+                    found = true;
+                    break;
+                }
+            }
+        }
+        // ---- undecided scans: marked for scan_first_rest_kernel
+        if (lane < (uint32_t)cnt && ((!found && (my_info & 0x100u)) || (my_info & 0x200u))) my_st = kFirstUndecided;
+        if (lane < (uint32_t)cnt) {
+            img_out[c0 + lane] = my_img;
+            st_out[c0 + lane] = (uint8_t)my_st;
+        }
+        __builtin_amdgcn_wave_barrier();  // s_cand is rewritten by the next chunk
+    }
+}
+
+// The scans scan_first_split_kernel left undecided (st_out == kFirstUndecided): the general loop
+// (scan_one_compact + FirstPrefixSink) from the start key, a wave per scan; 64 statuses are
+// read per wave and step, so a batch without undecided scans costs one pass over st_out.
+template <int SPL, int KW>
+__global__ __launch_bounds__(256) void scan_first_rest_kernel(DevTable t, const uint64_t *__restrict__ keys,
+                                                              uint64_t n, uint32_t scan_size,
+                                                              const uint32_t *__restrict__ rids, uint32_t words,
+                                                              uint32_t *__restrict__ img_out,
+                                                              uint8_t *__restrict__ st_out) {
+    __shared__ uint64_t s_keys[4][64 * KW];
+    __shared__ uint32_t s_len[4][64], s_slot[4][64];
+    const uint32_t lane = lane_id(), wv = uni32(threadIdx.x >> 6);
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint32_t len = t.key_width;
+    for (uint64_t c0 = wave * 64; c0 < n; c0 += nwaves * 64) {
+        const uint64_t i = c0 + lane;
+        uint64_t und = ballot(i < n && st_out[i] == kFirstUndecided);
+        while (und) {
+            const int b = __builtin_ctzll(und);
+            und &= und - 1;
+            const uint64_t k = c0 + (uint64_t)b;
+            uint64_t x[KW];
+            load_okey<KW>(keys, k, true, len, x);
+            FirstPrefixSink<KW> sink;
+#pragma unroll
+            for (int w = 0; w < KW; ++w) sink.pre[w] = x[w];
+            sink.words = words;
+            sink.rid = rids ? rids[k] : 0xFFFFFFFEu;
+            sink.img = 0xFFFFFFFFu;
+            sink.st = ST_NOT_FOUND;
+            const uint32_t leaf = uni32(resolve_leaf_uniform<false, KW>(t, x, len, true, lane));
+            scan_one_compact<false, SPL, KW>(t, x, len, leaf, scan_size, lane, sink, s_keys[wv], s_len[wv],
+                                             s_slot[wv]);
+            if (lane == 0) {
+                img_out[k] = sink.img;
+                st_out[k] = (uint8_t)sink.st;
+            }
         }
     }
 }
@@ -1779,12 +2066,28 @@ hipError_t launch_scan_first(const DevTable &t, const uint64_t *keys, uint64_t n
     // equal to the single-scan kernel at 2 and 19 % slower at 4)
     const int ns = tune.first_scans;
 #define STAGE_FIRST(S, KW)                                                                                  \
-    if (ns == 0)                                                                                            \
-        scan_first_fast_kernel<S, KW, 8><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words, img_out, \
-                                                                st_out);                                    \
+    if (ns == 0 || ns == -4) {                                                                              \
+        if (ns == 0)                                                                                        \
+            scan_first_split_kernel<S, KW, 8><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words,     \
+                                                                     img_out, st_out);                      \
+        else                                                                                                \
+            scan_first_split_kernel<S, KW, 7><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words,     \
+                                                                     img_out, st_out);                      \
+        scan_first_rest_kernel<S, KW><<<grid_for((n + 63) / 64, 4, 4096), 256, 0, s>>>(t, keys, n, scan_size,  \
+                                                                                    rids, words, img_out,   \
+                                                                                    st_out);                \
+    } else if (ns == -5)                                                                                    \
+        scan_first_fast_kernel<S, KW, 8, true><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words,    \
+                                                                      img_out, st_out);                     \
+    else if (ns == -1)                                                                                      \
+        scan_first_fast_kernel<S, KW, 1, true><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words,    \
+                                                                      img_out, st_out);                     \
+    else if (ns == -2)                                                                                      \
+        scan_first_fast_kernel<S, KW, 8, false><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words,   \
+                                                                       img_out, st_out);                    \
     else if (ns < 0)                                                                                        \
-        scan_first_fast_kernel<S, KW, 1><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words, img_out, \
-                                                                st_out);                                    \
+        scan_first_fast_kernel<S, KW, 7, true><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words,    \
+                                                                      img_out, st_out);                     \
     else if (ns == 1)                                                                                       \
         scan_first_kernel<S, KW><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words, img_out, st_out); \
     else if (ns == 4)                                                                                       \

@@ -68,6 +68,8 @@ SIGNATURES = {
                                        ctypes.POINTER(ctypes.c_int32), c_vp]),
     "stage_index_scan_batch": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, ctypes.c_uint64, ctypes.c_uint32, c_vp, c_vp,
                                               c_vp, c_vp]),
+    "stage_index_scan_first_batch": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_uint64, ctypes.c_uint32,
+                                                    ctypes.c_uint32, c_vp, c_vp, c_vp]),
     "stage_set_shard_chunks": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "stage_probe_sharded_loopback": (ctypes.c_int, [c_vp, ctypes.c_int, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_int,
                                                     c_vp]),

@@ -477,6 +477,20 @@ class Table:
         st = d_st.to_numpy(np.uint8, n * scan_size).reshape(n, scan_size)
         return counts, rows, st
 
+    def index_scan_first(self, start_keys, scan_size, prefix_words, read_ids=None):
+        """index_scan consumed up to its first LATEST / OLD tuple carrying the start key's first
+        prefix_words fields: (image[n] heap rows, status[n])."""
+        keys, n = self.key_buffer(start_keys)
+        d_keys = DeviceBuffer.from_numpy(keys)
+        d_rid = DeviceBuffer.from_numpy(np.ascontiguousarray(read_ids, np.uint32)) if read_ids is not None else None
+        d_img = DeviceBuffer(max(4, n * 4))
+        d_st = DeviceBuffer(max(1, n))
+        check(lib().stage_index_scan_first_batch(self.h, d_keys.ptr, d_rid.ptr if d_rid else None, n, scan_size,
+                                                 prefix_words, d_img.ptr, d_st.ptr, None),
+              "stage_index_scan_first_batch")
+        check(lib().stage_device_sync(), "sync")
+        return d_img.to_numpy(np.uint32, n), d_st.to_numpy(np.uint8, n)
+
     def resolve(self, keys, lens=None, le_child=True):
         keys, n = self.key_buffer(keys)
         d_keys = DeviceBuffer.from_numpy(keys)

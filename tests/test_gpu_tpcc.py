@@ -69,10 +69,11 @@ def test_stock_level_matches_oracle(tpcc):
     assert (got2 == exp2).all()
 
 
-@pytest.mark.parametrize("variant", ["0", "-1", "1", "2", "4"])
+@pytest.mark.parametrize("variant", ["0", "-1", "-2", "-3", "1", "2", "4"])
 def test_stock_level_scan_kernel_variants(gpu, monkeypatch, variant):
-    """Every first-tuple scan kernel (STAGE_SL_SCANS: 0 = scan_first_fast_kernel at 8 waves/SIMD,
-    -1 = the same without the occupancy cap, 1 = the general single-scan kernel, 2 / 4 = lockstep)
+    """Every first-tuple scan kernel (STAGE_SL_SCANS: 0 = scan_first_fast_kernel with the
+    prefetch pipeline at 8 waves/SIMD, -1 = the same without the occupancy cap, -2 = without the
+    pipeline, -3 = pipeline at 7 waves/SIMD, 1 = the general single-scan kernel, 2 / 4 = lockstep)
     gives the oracle's stock-level results.  Order lines are inserted in numeric order, which is
     not their memcmp key order, so leaves carry unsorted regions (the fast kernel's O(m) ranking)
     and sorted ones (its slot-order ranking); starts of orders with fewer than 5 lines continue
@@ -89,3 +90,44 @@ def test_stock_level_scan_kernel_variants(gpu, monkeypatch, variant):
     exp = np.array([tt.stock_level_oracle(int(a), int(b), int(c), int(r)) for a, b, c, r in zip(w, d, thr, rids)])
     assert (got == exp).all(), np.nonzero(got != exp)[0][:10]
     assert (got > 0).any()
+
+
+def test_first_tuple_scans_every_kernel(gpu, monkeypatch):
+    """stage_index_scan_first_batch (the stock-level ORDER_LINE scans, direct) against the oracle's
+    IndexScanExecutor range branch + the prefix predicate, for every scan kernel variant, over
+    starts that hit existing orders, missing orders (o > 40: the prefix never matches, so the
+    scan continues across leaves -- scan_first_split_kernel leaves such scans to
+    scan_first_rest_kernel), missing districts / warehouses and line numbers past the order."""
+    rng = np.random.default_rng(12)
+    n = 400
+    starts = np.stack([np.frombuffer(key(int(rng.integers(1, 4)), int(rng.integers(1, 12)),
+                                         int(rng.integers(1, 46)), int(rng.integers(1, 17))), np.uint8)
+                       for _ in range(n)])
+    rids = rng.choice(np.array([0, 5, 11, 15, 21, 25, 0xFFFFFFFE], np.uint32), n)
+    cases = [(10, 3), (3, 3), (1, 2), (10, 4), (63, 1)]
+    ref_tt = _tables()
+    expected = {}
+    for size, words in cases:
+        exp = np.zeros(n, np.uint8)
+        for i in range(n):
+            c, rows, st = ref_tt.ool.index_scan(starts[i].tobytes(), 32, size, int(rids[i]))
+            for j in range(c):
+                if st[j] in (1, 3) and bytes(rows[j][:8 * words]) == starts[i][:8 * words].tobytes():
+                    exp[i] = st[j]
+                    break
+        expected[(size, words)] = exp
+    images = {}
+    for variant in ["1", "0", "-4", "-5", "-1", "-2", "-3", "2", "4"]:
+        monkeypatch.setenv("STAGE_SL_SCANS", variant)
+        tt = _tables()
+        for size, words in cases:
+            img, st = tt.ol.index_scan_first(starts, size, words, read_ids=rids)
+            exp = expected[(size, words)]
+            assert (st == exp).all(), (variant, size, words, np.nonzero(st != exp)[0][:10])
+            assert ((img == 0xFFFFFFFF) == (st == 0)).all()
+            if (size, words) in images:
+                assert (img == images[(size, words)]).all(), (variant, size, words)
+            else:
+                images[(size, words)] = img
+    # starts past the last order of a district carry no prefix record
+    assert (expected[(10, 3)] == 0).any() and (expected[(10, 3)] != 0).any()
