@@ -374,8 +374,10 @@ class YcsbB:
         ep["d"]["rc"] = stage.DeviceBuffer(max(1, ep["keys"].size))
         ep["d"]["out"] = stage.DeviceBuffer(32 * ep["reads"].size)
 
-    def apply(self, ep):
-        """the epoch's write share on the write path; returns the successful updates"""
+    def apply(self, ep, stream=None):
+        """the epoch's write share on the write path; returns the successful updates.  With a
+        stream (device write path) the kernels are only enqueued on it -- no host wait; the
+        successes are counted afterwards from the per-op return codes (count_ok)."""
         m = ep["keys"].size
         if self.args.write_path == "device":
             ok = ctypes.c_uint64()
@@ -383,8 +385,16 @@ class YcsbB:
                 d = ep["d"]
                 check(stage.lib().stage_update_batch_device(self.tab.h, d["keys"].ptr, None, m, 0, d["cols"].ptr, 100,
                                                             d["rid"].ptr, d["cid"].ptr, None, d["rc"].ptr,
-                                                            ctypes.byref(ok), None), "update_batch_device")
+                                                            None if stream is not None else ctypes.byref(ok),
+                                                            stream.ptr if stream is not None else None),
+                      "update_batch_device")
             return ok.value
+
+    @staticmethod
+    def count_ok(ep):
+        """successful updates of an epoch applied on the device (return code RC_OK)"""
+        m = ep["keys"].size
+        return int((ep["d"]["rc"].to_numpy(np.uint8, m) == stage.RC_OK).sum()) if m else 0
         cols = np.repeat(ep["colb"][:, None], 100, 1)
         _, ok = self.tab.update_batch(ep["keys"], 0, cols, ep["rid"], ep["cid"])
         self.tab.sync()
@@ -819,9 +829,11 @@ def c4_leg(tab, args, total_rows, rank, stream, steps, warmup):
 def c3_leg(tab, args, stream, nthreads, steps, warmup):
     """configs[2]: YCSB-B epochs.  Timed loop, per epoch: the write share on the write path,
     then the device probe of the read share at the epoch's read ids.  value = reads / the
-    probes' wall time; ops_per_s_incl_writes = (reads + updates) / the whole loop's wall time
-    (the device write path returns after its kernels and the headers' D2H; the host table
-    adopts the epoch on a background thread while the next probe runs)."""
+    probes' time (device write path: the probes' stream time between events; host write path:
+    their wall time); ops_per_s_incl_writes = (reads + updates) / the whole loop's wall time
+    (device write path: each epoch's kernels are enqueued on the probe's stream without a host
+    wait, the host table adopts the epoch on a background thread while the probe runs, and the
+    next epoch's call waits for that adoption)."""
     L = stage.lib()
     B = args.batch
     theta = args.theta if args.config == "c3" else 0.99
@@ -851,21 +863,32 @@ def c3_leg(tab, args, stream, nthreads, steps, warmup):
     stream.sync()
     check(L.stage_device_sync(), "sync")
     evs = [stage.Event() for _ in range(2 * steps)]
+    device_wp = args.write_path == "device"
     elapsed, write_s, updates, ops_done = 0.0, 0.0, 0, 0
     t_loop = time.perf_counter()
     for i, ep in enumerate(epochs[warm:]):
         tw = time.perf_counter()
-        updates += ycsb_b.apply(ep)
+        # device write path: the epoch's kernels are enqueued on the probe's stream (the reads
+        # follow the epoch's writes in stream order; no host wait in between); host write path:
+        # applied and published before the probe
+        updates += ycsb_b.apply(ep, stream if device_wp else None)
         write_s += time.perf_counter() - tw
         tr = time.perf_counter()
         evs[2 * i].record(stream)
         probe(ep)
         evs[2 * i + 1].record(stream)
-        stream.sync()
-        elapsed += time.perf_counter() - tr
+        if not device_wp:
+            stream.sync()
+            elapsed += time.perf_counter() - tr
         ops_done += ep["reads"].size
+    stream.sync()
     loop_s = time.perf_counter() - t_loop
-    kern_ms = float(np.mean([evs[2 * i].elapsed_ms(evs[2 * i + 1]) for i in range(steps)]))
+    probe_ms = [evs[2 * i].elapsed_ms(evs[2 * i + 1]) for i in range(steps)]
+    if device_wp:  # the probes' device time (start event -> end event on the stream)
+        elapsed = sum(probe_ms) / 1e3
+        check(L.stage_device_sync(), "sync")
+        updates = sum(YcsbB.count_ok(ep) for ep in epochs[warm:])
+    kern_ms = float(np.mean(probe_ms))
     hist = np.zeros(6, np.int64)
     hops = 0
     for ep in epochs[warm:]:
@@ -887,7 +910,7 @@ def c3_leg(tab, args, stream, nthreads, steps, warmup):
                     "inflight_share": args.inflight_share, "updates_applied": updates,
                     "update_ops": int(sum(ep["keys"].size for ep in epochs[warm:])),
                     "updates_in_flight": int(sum(ep["inflight"] for ep in epochs[warm:])),
-                    "write_path": args.write_path, "write_s": round(write_s, 4), "loop_s": round(loop_s, 4),
+                    "write_path": args.write_path, "write_call_s": round(write_s, 4), "loop_s": round(loop_s, 4),
                     "epoch_prep_s_untimed": round(prep_s, 2), "mean_chain_hops": round(mean_hops, 4),
                     # copies / versions / heap images are append-only (no GC, as the reference
                     # with its cleaner off): each successful update takes one of each, and the
