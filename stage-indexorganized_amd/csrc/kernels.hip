@@ -43,6 +43,18 @@ __device__ __forceinline__ uint64_t head_vis(const DevTable &t, uint32_t leaf, i
     return *reinterpret_cast<const uint64_t *>(t.head + (uint64_t)leaf * t.head_bytes + t.cap + 8 * s);
 }
 
+// branch-free lexicographic a < b (for several compares in flight in one lane)
+template <int KW>
+__device__ __forceinline__ bool kw_lt_flat(const uint64_t *a, const uint64_t *b) {
+    bool lt = false, eq = true;
+#pragma unroll
+    for (int j = 0; j < KW; ++j) {
+        lt = lt | (eq & (a[j] < b[j]));
+        eq = eq & (a[j] == b[j]);
+    }
+    return lt;
+}
+
 // multi-word order keys (fixed-width keys of 9..32 bytes): lexicographic word order
 template <int KW>
 __device__ __forceinline__ bool kw_lt(const uint64_t *a, const uint64_t *b) {
@@ -1673,6 +1685,215 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     }
 }
 
+// inclusive prefix sum within each row of 16 lanes (DPP row shifts; lanes shifted in from
+// outside the row read 0)
+__device__ __forceinline__ uint32_t row16_incl_scan(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    return v;
+}
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+    return ((uint64_t)(uint32_t)__shfl((int)(v >> 32), src) << 32) | (uint32_t)__shfl((int)(uint32_t)v, src);
+}
+
+// scan_first_split_kernel with stage A run for SUB scans at once: lane segment r (64/SUB lanes)
+// works for scan SUB*p + r of pass p, each lane tests SUB consecutive slots of a slot group, a
+// segmented DPP prefix sum ranks the qualifying slots in slot order, and lane k of the segment
+// then holds kept record k (scan_size < 64/SUB).  The uniform per-scan control of the
+// wave-per-scan stage A (~420 instructions per scan) is shared by SUB scans.  Stage B and the
+// undecided scans as in scan_first_split_kernel.
+template <int SPL, int KW, int WPE, int SUB>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void scan_first_seg_kernel(
+    DevTable t, const uint64_t *__restrict__ keys, uint64_t n, uint32_t scan_size, const uint32_t *__restrict__ rids,
+    uint32_t words, uint32_t *__restrict__ img_out, uint8_t *__restrict__ st_out) {
+    static_assert(SUB == 2 || SUB == 4, "segments of 32 or 16 lanes");
+    constexpr uint32_t SEGW = 64 / SUB;
+    __shared__ uint64_t s_keys[4][SUB][SEGW * KW];
+    __shared__ uint32_t s_slot[4][SUB][SEGW];
+    __shared__ uint16_t s_cand[4][kFirstChunk][SEGW];
+    const uint32_t lane = lane_id(), wv = uni32(threadIdx.x >> 6);
+    const uint32_t seg = lane / SEGW, sl = lane % SEGW;
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint32_t len = t.key_width;
+    uint64_t *lk = s_keys[wv][seg];
+    uint32_t *ls = s_slot[wv][seg];
+    constexpr uint16_t kHole = 0xFFFF;
+    for (uint64_t c0 = wave * kFirstChunk; c0 < n; c0 += nwaves * kFirstChunk) {
+        const uint64_t i = c0 + (lane >> 2);  // the scan this lane descends for
+        const bool valid = i < n;
+        uint64_t ok[KW];
+        load_okey<KW>(keys, i, valid, len, ok);
+        const uint32_t leafv = chunk_lower_bound<KW>(t, ok, lane & 3);
+        const uint32_t ridv = valid && rids ? rids[i] : 0xFFFFFFFEu;
+        const int cnt = (int)((n - c0) < (uint64_t)kFirstChunk ? (n - c0) : (uint64_t)kFirstChunk);
+        uint32_t actv = 0;
+        {
+            const uint64_t *gm = reinterpret_cast<const uint64_t *>(t.head + (uint64_t)leafv * t.head_bytes +
+                                                                    head_gmax_offset(t.cap));
+#pragma unroll
+            for (int g = 0; g < SPL; g += 4) {
+                const uint32_t gg = (uint32_t)g + (lane & 3);
+                if (gg < (uint32_t)SPL) {
+                    uint64_t e[KW];
+#pragma unroll
+                    for (int w = 0; w < KW; ++w) e[w] = gm[gg * KW + w];
+                    actv |= kw_lt<KW>(e, ok) ? 0u : (1u << gg);
+                }
+            }
+            actv |= (uint32_t)__shfl_xor((int)actv, 1);
+            actv |= (uint32_t)__shfl_xor((int)actv, 2);
+        }
+        uint32_t my_info = 0;
+        // ---- stage A, SUB scans per pass
+#pragma unroll 1
+        for (int p = 0; p < (cnt + SUB - 1) / SUB; ++p) {
+            const int j = SUB * p + (int)seg;  // this segment's scan
+            const int src = 4 * (j < kFirstChunk ? j : 0);
+            uint64_t x[KW];
+#pragma unroll
+            for (int w = 0; w < KW; ++w) x[w] = shfl64(ok[w], src);
+            const uint32_t leaf = (uint32_t)__shfl((int)leafv, src);
+            uint32_t act = (uint32_t)__shfl((int)actv, src);
+            bool live = j < cnt && act != 0;
+            uint32_t kept = 0;
+#pragma unroll 1
+            while (ballot(live)) {
+                const int s = live ? __builtin_ctz(act) : 0;
+                if (live) act &= act - 1;
+                uint64_t vm = 0, col[SUB][KW];
+                const uint64_t gbase = (uint64_t)s * 64 + sl * SUB;
+                if (live) {
+                    vm = head_vis(t, leaf, s);
+#pragma unroll
+                    for (int w = 0; w < KW; ++w) {
+                        const uint64_t *cp = t.okey + ((uint64_t)leaf * KW + w) * t.cap + gbase;
+#pragma unroll
+                        for (int k = 0; k < SUB; ++k) col[k][w] = cp[k];
+                    }
+                }
+                uint32_t qb = 0;
+#pragma unroll
+                for (int k = 0; k < SUB; ++k)
+                    qb |= (live & (((vm >> (sl * SUB + k)) & 1) != 0) & !kw_lt_flat<KW>(col[k], x)) ? 1u << k : 0u;
+                const uint32_t c = (uint32_t)__builtin_popcount(qb);
+                uint32_t incl = row16_incl_scan(c);
+                if (SEGW == 32) {  // upper row of a 32-lane segment: + the lower row's total
+                    const uint32_t low = (uint32_t)__shfl((int)incl, (int)((lane & ~31u) | 15u));
+                    incl += (lane & 16) ? low : 0u;
+                }
+                const uint32_t total = (uint32_t)__shfl((int)incl, (int)(lane | (SEGW - 1)));
+                uint32_t r = kept + incl - c;
+#pragma unroll
+                for (int k = 0; k < SUB; ++k)
+                    if ((qb >> k) & 1) {
+                        if (r <= scan_size) {
+#pragma unroll
+                            for (int w = 0; w < KW; ++w) lk[r * KW + w] = col[k][w];
+                            ls[r] = (uint32_t)(gbase + k);
+                        }
+                        ++r;
+                    }
+                if (live) {
+                    kept += total;
+                    if (kept > scan_size || act == 0) live = false;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const uint32_t m = kept < scan_size + 1 ? kept : scan_size + 1;  // records held (<= SEGW)
+            const uint64_t segmask = (SEGW == 32 ? 0xFFFFFFFFull : 0xFFFFull) << (seg * SEGW);
+            const bool mine = j < cnt && sl < m;
+            uint64_t mk[KW];
+            uint32_t mslot = 0;
+            bool ord = true;
+#pragma unroll
+            for (int w = 0; w < KW; ++w) mk[w] = mine ? lk[sl * KW + w] : 0ull;
+            if (mine) {
+                mslot = ls[sl];
+                if (sl > 0) {
+                    uint64_t pk[KW];
+#pragma unroll
+                    for (int w = 0; w < KW; ++w) pk[w] = lk[(sl - 1) * KW + w];
+                    ord = kw_lt<KW>(pk, mk);
+                }
+            }
+            const bool seg_sorted = (ballot(!ord) & segmask) == 0;
+            uint32_t kr = sl;
+            bool dup = false;
+            if (!seg_sorted) {
+                kr = 0;
+                for (uint32_t jj = 0; jj < m; ++jj) {
+                    bool eq = jj != sl;
+                    uint64_t kj[KW];
+#pragma unroll
+                    for (int w = 0; w < KW; ++w) {
+                        kj[w] = lk[jj * KW + w];
+                        eq = eq && kj[w] == mk[w];
+                    }
+                    kr += (mine && kw_lt<KW>(kj, mk)) ? 1u : 0u;
+                    dup = dup || (mine && eq);
+                }
+            }
+            const bool seg_dup = (ballot(dup) & segmask) != 0;
+            const uint32_t e = m < scan_size ? m : scan_size;
+            uint32_t info = 0;
+            if (j < cnt && m > 0) {
+                if (seg_dup) {
+                    info = 0x200u;  // equal keys share a rank: the general loop decides
+                } else {
+                    info = e | (e == m && scan_size > e ? 0x100u : 0u);
+                    if (sl < e) s_cand[wv][j][sl] = kHole;
+                    if (mine && kr < e) {
+                        bool pfx = true;
+#pragma unroll
+                        for (int w = 0; w < KW; ++w)
+                            if ((uint32_t)w < words) pfx = pfx && mk[w] == x[w];
+                        if (pfx) s_cand[wv][j][kr] = (uint16_t)mslot;
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();  // the LDS lists are rewritten by the next pass
+            // lane q (< 16) keeps the info of scan q = SUB*p + r from segment r's lane 0
+            const uint32_t got = (uint32_t)__shfl((int)info, (int)((lane % SUB) * SEGW));
+            if (lane / SUB == (uint32_t)p && lane < 16) my_info = got;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // ---- stage B: lane j resolves scan j's candidates in rank order
+        const uint32_t my_leaf = (uint32_t)__shfl((int)leafv, (int)(4 * (lane & 15)));
+        const uint32_t my_rid = (uint32_t)__shfl((int)ridv, (int)(4 * (lane & 15)));
+        uint32_t my_img = 0xFFFFFFFFu, my_st = ST_NOT_FOUND;
+        bool found = false;
+        if (lane < (uint32_t)cnt) {
+            const uint32_t e = my_info & 0xFF;
+            const uint64_t base = (uint64_t)my_leaf * t.cap;
+            for (uint32_t c = 0; c < e; ++c) {
+                const uint16_t slo = s_cand[wv][lane][c];
+                if (slo == kHole) continue;
+                uint8_t sv;
+                const uint32_t im = scan_visible(t, t.slot[base + slo], my_rid, sv);
+                if (sv == ST_LATEST || sv == ST_OLD) {
+                    my_img = im;
+                    my_st = sv;
+                    found = true;
+                    break;
+                }
+            }
+        }
+        if (lane < (uint32_t)cnt && ((!found && (my_info & 0x100u)) || (my_info & 0x200u))) my_st = kFirstUndecided;
+        if (lane < (uint32_t)cnt) {
+            img_out[c0 + lane] = my_img;
+            st_out[c0 + lane] = (uint8_t)my_st;
+        }
+        __builtin_amdgcn_wave_barrier();  // s_cand is rewritten by the next chunk
+    }
+}
+
 // The scans scan_first_split_kernel left undecided (st_out == kFirstUndecided): the general loop
 // (scan_one_compact + FirstPrefixSink) from the start key, a wave per scan; 64 statuses are
 // read per wave and step, so a batch without undecided scans costs one pass over st_out.
@@ -2066,8 +2287,14 @@ hipError_t launch_scan_first(const DevTable &t, const uint64_t *keys, uint64_t n
     // equal to the single-scan kernel at 2 and 19 % slower at 4)
     const int ns = tune.first_scans;
 #define STAGE_FIRST(S, KW)                                                                                  \
-    if (ns == 0 || ns == -4) {                                                                              \
-        if (ns == 0)                                                                                        \
+    if (ns == 0 || ns == -4 || ns == -6 || ns == -7) {                                                      \
+        if (ns == -6 && scan_size <= 15)                                                                    \
+            scan_first_seg_kernel<S, KW, 4, 4><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words,    \
+                                                                      img_out, st_out);                     \
+        else if (ns == -7 && scan_size <= 31)                                                               \
+            scan_first_seg_kernel<S, KW, 1, 2><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words,    \
+                                                                      img_out, st_out);                     \
+        else if (ns != -4)                                                                                  \
             scan_first_split_kernel<S, KW, 8><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words,     \
                                                                      img_out, st_out);                      \
         else                                                                                                \

@@ -69,7 +69,7 @@ def test_stock_level_matches_oracle(tpcc):
     assert (got2 == exp2).all()
 
 
-@pytest.mark.parametrize("variant", ["0", "-1", "-2", "-3", "1", "2", "4"])
+@pytest.mark.parametrize("variant", ["0", "-1", "-2", "-3", "-4", "-5", "-6", "-7", "1", "2", "4"])
 def test_stock_level_scan_kernel_variants(gpu, monkeypatch, variant):
     """Every first-tuple scan kernel (STAGE_SL_SCANS: 0 = scan_first_fast_kernel with the
     prefetch pipeline at 8 waves/SIMD, -1 = the same without the occupancy cap, -2 = without the
@@ -104,7 +104,7 @@ def test_first_tuple_scans_every_kernel(gpu, monkeypatch):
                                          int(rng.integers(1, 46)), int(rng.integers(1, 17))), np.uint8)
                        for _ in range(n)])
     rids = rng.choice(np.array([0, 5, 11, 15, 21, 25, 0xFFFFFFFE], np.uint32), n)
-    cases = [(10, 3), (3, 3), (1, 2), (10, 4), (63, 1)]
+    cases = [(10, 3), (3, 3), (1, 2), (10, 4), (15, 3), (31, 2), (63, 1)]
     ref_tt = _tables()
     expected = {}
     for size, words in cases:
@@ -117,7 +117,7 @@ def test_first_tuple_scans_every_kernel(gpu, monkeypatch):
                     break
         expected[(size, words)] = exp
     images = {}
-    for variant in ["1", "0", "-4", "-5", "-1", "-2", "-3", "2", "4"]:
+    for variant in ["1", "0", "-4", "-5", "-6", "-7", "-1", "-2", "-3", "2", "4"]:
         monkeypatch.setenv("STAGE_SL_SCANS", variant)
         tt = _tables()
         for size, words in cases:
