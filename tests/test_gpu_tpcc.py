@@ -131,3 +131,30 @@ def test_first_tuple_scans_every_kernel(gpu, monkeypatch):
                 images[(size, words)] = img
     # starts past the last order of a district carry no prefix record
     assert (expected[(10, 3)] == 0).any() and (expected[(10, 3)] != 0).any()
+
+
+@pytest.mark.parametrize("variant", ["0", "-4", "-5", "-6", "-7", "1", "2"])
+def test_first_tuple_scans_16_byte_keys(gpu, monkeypatch, variant):
+    """stage_index_scan_first_batch on the STOCK table (16-byte keys, KW = 2 order words):
+    the first LATEST / OLD tuple of the same warehouse (prefix 1) or of the exact key (prefix
+    2) within scans of 4 / 12 records, against the oracle, including the history committed at
+    ids 11 / 21 and a row in flight (read ids before, between and after)."""
+    monkeypatch.setenv("STAGE_SL_SCANS", variant)
+    tt = _tables()
+    rng = np.random.default_rng(13)
+    n = 300
+    starts = np.stack([np.frombuffer(key(int(rng.integers(1, 4)), int(rng.integers(-2, tt.n_items + 4))), np.uint8)
+                       for _ in range(n)])
+    rids = rng.choice(np.array([0, 5, 11, 15, 21, 31, 0xFFFFFFFE], np.uint32), n)
+    for size, words in [(4, 1), (12, 1), (4, 2)]:
+        img, st = tt.stock.index_scan_first(starts, size, words, read_ids=rids)
+        exp = np.zeros(n, np.uint8)
+        for i in range(n):
+            c, rows, ost = tt.ostock.index_scan(starts[i].tobytes(), 16, size, int(rids[i]))
+            for j in range(c):
+                if ost[j] in (1, 3) and bytes(rows[j][:8 * words]) == starts[i][:8 * words].tobytes():
+                    exp[i] = ost[j]
+                    break
+        assert (st == exp).all(), (variant, size, words, np.nonzero(st != exp)[0][:10])
+        assert ((img == 0xFFFFFFFF) == (st == 0)).all()
+        assert (exp != 0).any() and (exp == 0).any()
