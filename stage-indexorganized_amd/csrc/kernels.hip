@@ -356,6 +356,16 @@ __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *
         if (valid) leaf = leaf_in ? leaf_in[i] : resolve_leaf<VARLEN, KW>(t, ok, len, true);
         if (leaf > t.nseps) leaf = t.nseps;  // host-supplied ids are clamped to the table
         const int cnt = (int)((n - base) < CH ? (n - base) : CH);
+        // one probe in flight (G = 1: the wide-key and large-leaf instances): the next probe's
+        // fingerprint bytes load while this one runs, so a probe exposes one dependent round
+        // trip (its candidates' slot words) instead of two
+        constexpr bool PFH = G == 1;
+        uint32_t nfp[SPL];
+        if (PFH) {
+            const uint8_t *h = t.head + (uint64_t)rl32(leaf, 0) * t.head_bytes;
+#pragma unroll
+            for (int s = 0; s < SPL; ++s) nfp[s] = h[s * 64 + lane];
+        }
         for (int j0 = 0; j0 < cnt; j0 += G) {
             uint32_t lf[G], rd[G], xl[G];
             uint64_t x[G][KW];
@@ -371,9 +381,19 @@ __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *
 #pragma unroll
                 for (int w = 0; w < KW; ++w) x[g][w] = rl64(ok[w], j);
                 xl[g] = VARLEN ? rl32(len, j) : t.key_width;
-                const uint8_t *h = t.head + (uint64_t)lf[g] * t.head_bytes;
+                if (PFH) {
 #pragma unroll
-                for (int s = 0; s < SPL; ++s) fpb[g][s] = h[s * 64 + lane];
+                    for (int s = 0; s < SPL; ++s) fpb[g][s] = nfp[s];
+                    if (j0 + 1 < cnt) {
+                        const uint8_t *h = t.head + (uint64_t)rl32(leaf, j0 + 1) * t.head_bytes;
+#pragma unroll
+                        for (int s = 0; s < SPL; ++s) nfp[s] = h[s * 64 + lane];
+                    }
+                } else {
+                    const uint8_t *h = t.head + (uint64_t)lf[g] * t.head_bytes;
+#pragma unroll
+                    for (int s = 0; s < SPL; ++s) fpb[g][s] = h[s * 64 + lane];
+                }
             }
             // phase 2: fingerprint candidates read their slot words
             uint64_t wok[G][SPL], wmeta[G][SPL];
@@ -392,6 +412,14 @@ __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *
                     if (cand[g][s]) {
                         const u32x4 *w = reinterpret_cast<const u32x4 *>(t.slot + (uint64_t)lf[g] * t.cap + s * 64 + lane);
                         const u32x4 w0 = w[0], w1 = w[1];
+                        // the other key words load with the slot word (one round trip) in leaves
+                        // of up to 4 slot groups; larger leaves load them after the order-key
+                        // match (fewer registers in flight)
+                        constexpr bool COK = SPL <= 4;
+                        uint64_t kw[KW > 1 ? KW : 1];
+#pragma unroll
+                        for (int w = 1; w < KW; ++w)
+                            kw[w] = COK ? t.okey[((uint64_t)lf[g] * KW + w) * t.cap + s * 64 + lane] : 0ull;
                         wok[g][s] = ((uint64_t)w0.y << 32) | w0.x;
                         wmeta[g][s] = ((uint64_t)w0.w << 32) | w0.z;
                         wnext[g][s] = w1.x;
@@ -400,7 +428,8 @@ __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *
                             bool eq = true;
 #pragma unroll
                             for (int w = 1; w < KW; ++w)
-                                eq = eq && t.okey[((uint64_t)lf[g] * KW + w) * t.cap + s * 64 + lane] == x[g][w];
+                                eq = eq && (COK ? kw[w] : t.okey[((uint64_t)lf[g] * KW + w) * t.cap + s * 64 + lane]) ==
+                                               x[g][w];
                             if (!eq) wok[g][s] = ~x[g][0];
                         }
                     }
