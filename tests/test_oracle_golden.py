@@ -184,3 +184,45 @@ def test_murmur_against_reference_build():
     for ln in range(0, 40):
         data = rng.integers(0, 256, ln, dtype=np.uint8).tobytes()
         assert ref.ref_murmur64a(data, ln, 7) == O.murmur64a(data, 7)
+
+
+def test_key_compare_wide_branch_is_libc_memcmp():
+    """KeyCompare's branch for keys of 16 bytes and more calls the C library's memcmp
+    (b_tree.h:126-128: `cmp = memcmp(key1, key2, min(size1, size2))`; shorter keys go through
+    the signed-char my_memcmp, :99-106).  The dependency is libc itself (glibc 2.35 in this image):
+    its published contract is an unsigned-byte lexicographic comparison.  The oracle's
+    restatement is pinned here against the real libc memcmp on random keys of 16-40 bytes
+    whose bytes straddle 0x80 (where signed and unsigned order disagree), equal prefixes of
+    different lengths included; and the < 16-byte branch against a signed-char restatement."""
+    import ctypes
+    libc = ctypes.CDLL(None)
+    libc.memcmp.restype = ctypes.c_int
+    libc.memcmp.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]
+    rng = np.random.default_rng(21)
+    checked_flip = 0
+    for _ in range(4000):
+        la, lb = (int(x) for x in rng.integers(16, 41, 2))
+        a = bytearray(rng.integers(0, 256, la, dtype=np.uint8).tobytes())
+        b = bytearray(rng.integers(0, 256, lb, dtype=np.uint8).tobytes())
+        cut = int(rng.integers(0, min(la, lb) + 1))  # shared prefix of random length
+        b[:cut] = a[:cut]
+        if cut < min(la, lb) and rng.random() < 0.5:  # first difference across the sign bit
+            a[cut], b[cut] = 0x7F, 0x80
+            checked_flip += 1
+        a, b = bytes(a), bytes(b)
+        c = libc.memcmp(a, b, min(la, lb))
+        exp = np.sign(c) if c != 0 else np.sign(la - lb)
+        assert np.sign(O.key_compare(a, b)) == exp, (a.hex(), b.hex())
+    assert checked_flip > 500
+    for _ in range(2000):  # the signed-char branch: min(size) < 16
+        la = int(rng.integers(1, 16))
+        lb = int(rng.integers(la, 24))
+        a = rng.integers(0, 256, la, dtype=np.uint8).tobytes()
+        b = a[:int(rng.integers(0, la + 1))] + rng.integers(0, 256, lb, dtype=np.uint8).tobytes()
+        b = b[:lb]
+        sa = np.frombuffer(a, np.int8).astype(int)
+        sb = np.frombuffer(b, np.int8).astype(int)
+        m = min(la, lb)
+        d = np.nonzero(sa[:m] != sb[:m])[0]
+        exp = np.sign(sa[d[0]] - sb[d[0]]) if d.size else np.sign(la - lb)
+        assert np.sign(O.key_compare(a, b)) == exp
