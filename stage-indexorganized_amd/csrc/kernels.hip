@@ -2311,9 +2311,10 @@ hipError_t launch_scan_first(const DevTable &t, const uint64_t *keys, uint64_t n
     if (n == 0) return hipSuccess;
     if (t.key_width == 0 || scan_size == 0 || scan_size > 63) return hipErrorInvalidValue;
     const int blocks = grid_for((n + kFirstChunk - 1) / kFirstChunk, 4, tune.max_blocks > 0 ? tune.max_blocks : 16384);
-    // default: scan_first_fast_kernel (STAGE_SL_SCANS unset or 0).  STAGE_SL_SCANS=1: the general
-    // single-scan kernel; 2 / 4: NS scans per wave in lockstep (scan_first_multi_kernel, measured
-    // equal to the single-scan kernel at 2 and 19 % slower at 4)
+    // default (STAGE_SL_SCANS unset or 0): scan_first_split_kernel + scan_first_rest_kernel.
+    // Variants: -4 split at 7 waves/SIMD; -5 / -3 / -1 scan_first_fast_kernel
+    // with the prefetch at 8 / 7 / 6 waves, -2 without it; -6 / -7 scan_first_seg_kernel (4 / 2
+    // scans per pass); 1 the general single-scan kernel; 2 / 4 NS scans per wave in lockstep
     const int ns = tune.first_scans;
 #define STAGE_FIRST(S, KW)                                                                                  \
     if (ns == 0 || ns == -4 || ns == -6 || ns == -7) {                                                      \
