@@ -1269,6 +1269,129 @@ __global__ __launch_bounds__(256) void scan_first_multi_kernel(DevTable t, const
     }
 }
 
+// Point probes of the one-probe-in-flight instances (fixed-width keys of 9..32 bytes, or
+// 8-byte keys in leaves above 128 slots) in two stages per chunk of CH probes -- the results of
+// probe_kernel<false, SPL, 1, .., KW, CH>:
+//  A (wave per probe, in turn): the leaf head's fingerprint bytes (the next probe's in flight
+//    while this one runs), one ballot per slot group, and the candidate slots in slot order
+//    written to LDS (at most kProbeCand; a probe with more is resolved by a lane-serial walk of
+//    its leaf head in stage B);
+//  B (lane per probe, all CH together): each candidate's slot word and remaining key words in
+//    slot order until the first confirmed one (SearchRecordMeta's first hit), then
+//    visibility() -- per lane, so the CH probes' dependent loads are in flight together instead
+//    of one probe's at a time.
+//  Rows (if requested) are then copied wave-wide, probe by probe, as probe_kernel's phase 4.
+constexpr int kProbeCand = 8;
+template <int SPL, int KW, int CH>
+__global__ __launch_bounds__(256) void probe_split_kernel(DevTable t, const uint64_t *__restrict__ keys,
+                                                          const uint32_t *__restrict__ rids,
+                                                          const uint32_t *__restrict__ leaf_in, uint64_t n,
+                                                          stage_probe_out_dev *__restrict__ out,
+                                                          uint8_t *__restrict__ recs) {
+    __shared__ uint16_t s_cand[4][64][kProbeCand];
+    const uint32_t lane = lane_id(), wv = uni32(threadIdx.x >> 6);
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint32_t out_chunks = t.stride >> 4;
+    const uint32_t len = t.key_width;
+    for (uint64_t base = wave * CH; base < n; base += nwaves * CH) {
+        const uint64_t i = base + lane;
+        const bool valid = lane < (uint32_t)CH && i < n;
+        const uint32_t rid = rids ? (valid ? rids[i] : 0u) : 0xFFFFFFFEu;
+        uint64_t ok[KW];
+        load_okey<KW>(keys, i, valid, len, ok);
+        uint32_t leaf = 0;
+        if (valid) leaf = leaf_in ? leaf_in[i] : resolve_leaf<false, KW>(t, ok, len, true);
+        if (leaf > t.nseps) leaf = t.nseps;  // host-supplied ids are clamped to the table
+        const uint32_t fx_mine = key_fp_words(ok, KW);
+        const int cnt = (int)((n - base) < CH ? (n - base) : CH);
+        // ---- stage A
+        uint32_t nfp[SPL];
+        {
+            const uint8_t *h = t.head + (uint64_t)rl32(leaf, 0) * t.head_bytes;
+#pragma unroll
+            for (int s = 0; s < SPL; ++s) nfp[s] = h[s * 64 + lane];
+        }
+        uint32_t my_nc = 0;
+        for (int j = 0; j < cnt; ++j) {
+            uint32_t fpb[SPL];
+#pragma unroll
+            for (int s = 0; s < SPL; ++s) fpb[s] = nfp[s];
+            if (j + 1 < cnt) {
+                const uint8_t *h = t.head + (uint64_t)rl32(leaf, j + 1) * t.head_bytes;
+#pragma unroll
+                for (int s = 0; s < SPL; ++s) nfp[s] = h[s * 64 + lane];
+            }
+            const uint32_t fx = rl32(fx_mine, j);
+            uint32_t nc = 0;
+#pragma unroll
+            for (int s = 0; s < SPL; ++s) {
+                const bool c = fpb[s] == fx;
+                const uint64_t cm = ballot(c);
+                const uint32_t r = nc + count_below(cm);
+                if (c && r < (uint32_t)kProbeCand) s_cand[wv][j][r] = (uint16_t)(s * 64 + lane);
+                nc += (uint32_t)__builtin_popcountll(cm);
+            }
+            if (lane == (uint32_t)j) my_nc = nc;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // ---- stage B: lane = probe
+        int slot = -1;
+        uint64_t m = 0;
+        uint32_t nx = 0, im = 0;
+        if (valid) {
+            const uint64_t lb = (uint64_t)leaf * t.cap;
+            auto confirm = [&](uint32_t sl) {
+                const u32x4 *w = reinterpret_cast<const u32x4 *>(t.slot + lb + sl);
+                const u32x4 w0 = w[0], w1 = w[1];
+                bool eq = (((uint64_t)w0.y << 32) | w0.x) == ok[0];
+#pragma unroll
+                for (int k = 1; k < KW; ++k) eq = eq && t.okey[((uint64_t)leaf * KW + k) * t.cap + sl] == ok[k];
+                if (eq) {
+                    slot = (int)sl;
+                    m = ((uint64_t)w0.w << 32) | w0.z;
+                    nx = w1.x;
+                    im = w1.y;
+                }
+                return eq;
+            };
+            if (my_nc <= (uint32_t)kProbeCand) {
+                for (uint32_t c = 0; c < my_nc; ++c)
+                    if (confirm(s_cand[wv][lane][c])) break;
+            } else {  // more candidates than the list holds: walk the head in slot order
+                const uint8_t *h = t.head + (uint64_t)leaf * t.head_bytes;
+                for (uint32_t sl = 0; sl < t.cap; ++sl)
+                    if (h[sl] == fx_mine && confirm(sl)) break;
+            }
+        }
+        ProbeRes r;
+        visibility(t, slot, m, nx, im, rid, r);
+        // rows: wave-wide, probe by probe
+        if (recs) {
+            for (int j = 0; j < cnt; ++j) {
+                const uint32_t img = rl32(r.image, j);
+                for (uint32_t c0 = 0; c0 < out_chunks; c0 += 64) {
+                    const uint32_t c = c0 + lane;
+                    if (c >= out_chunks) continue;
+                    u32x4 v = u32x4{0, 0, 0, 0};
+                    if (img != 0xFFFFFFFFu) v = reinterpret_cast<const u32x4 *>(t.heap + (uint64_t)img * t.hstride)[c];
+                    st16<1>(v, recs + (base + j) * (uint64_t)t.stride, c * 16u);
+                }
+            }
+        }
+        if (valid) {
+            u32x4 a, b;
+            pack_out(leaf, r, a, b);
+            uint8_t *ob = reinterpret_cast<uint8_t *>(out + base);
+            st16<1>(a, ob, lane * 32u);
+            st16<1>(b, ob, lane * 32u + 16u);
+        }
+        __builtin_amdgcn_wave_barrier();  // s_cand is rewritten by the next chunk
+    }
+}
+
 // Chunk-cooperative lower bound of kFirstChunk fixed-width start keys: lane L works for scan
 // L/4 and compares a quarter of each node (4 of the 16 inner entries, 2 of the 8 bottom ones);
 // two xor-shuffles sum the quarter counts.  Same result as tree_lower_bound (le_child = true),
@@ -2171,8 +2294,14 @@ hipError_t launch_probe(const DevTable &t, const uint64_t *keys, const uint16_t 
     if (t.key_words > 1 || (!var && t.cap > 128)) {
         const bool small = chunks < 16384;  // fewer 64-probe chunks than the chip holds waves
         const int wblocks = small ? grid_for((n + 15) / 16, 4, tune.max_blocks > 0 ? tune.max_blocks : 16384) : blocks;
+        // default: probe_split_kernel; STAGE_PROBE_WIDE=1: probe_kernel's one-probe-in-flight form
+        const bool split = tune.wide != 1 && tune.status_bytes != 16;
 #define STAGE_PROBE_W(S, KW)                                                                                  \
-    if (small)                                                                                                \
+    if (split && small)                                                                                       \
+        probe_split_kernel<S, KW, 16><<<wblocks, 256, 0, s>>>(t, keys, rids, leaf_in, n, out, recs);           \
+    else if (split)                                                                                           \
+        probe_split_kernel<S, KW, 64><<<blocks, 256, 0, s>>>(t, keys, rids, leaf_in, n, out, recs);            \
+    else if (small)                                                                                           \
         probe_kernel<false, S, 1, 1, KW, 16><<<wblocks, 256, 0, s>>>(t, keys, lens, rids, leaf_in, n, out, recs); \
     else                                                                                                      \
         probe_kernel<false, S, 1, 1, KW><<<blocks, 256, 0, s>>>(t, keys, lens, rids, leaf_in, n, out, recs)
