@@ -380,7 +380,7 @@ __global__ void wp_publish(WpArgs a, SlotInfo *__restrict__ slot, const uint8_t 
     slot[l].meta = meta;
     slot[l].next = next;
     slot[l].image = image;
-    fin[a.gs[q]] = FinRec{l, meta, next, image};
+    fin[rk & 0xFFFFFFFFull] = FinRec{l, meta, next, image};  // at the success rank: the first ns entries
 }
 
 unsigned blocks_for(uint64_t n, unsigned per) { return (unsigned)((n + per - 1) / per); }
@@ -543,16 +543,19 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
                           offsetof(FinRec, next) == offsetof(HostTable::SlotWords, next) &&
                           offsetof(FinRec, image) == offsetof(HostTable::SlotWords, image),
                       "FinRec / SlotWords layout");
-        t->adopt = std::thread([t, &h, &dv, cap = view.cap, n, cbase, vbase, pin, totals, fr, tot, fin, bf, t0,
+        t->adopt = std::thread([t, &h, &dv, cap = view.cap, n, cbase, vbase, pin, totals, fr, tot, fin, t0,
                                 t_kernels, t_enqueue, t_reserve]() mutable {
             try {
                 hip_check(hipSetDevice(dv.device), "hipSetDevice");
                 hipStream_t a = dv.adopt_stream;
                 hip_check(hipStreamWaitEvent(a, dv.adopt_ev, 0), "adopt wait");
                 hip_check(hipMemcpyAsync(totals, tot, 16, hipMemcpyDeviceToHost, a), "totals");
-                hip_check(hipMemcpyAsync(fr, fin, bf, hipMemcpyDeviceToHost, a), "slot words");
                 hip_check(hipStreamSynchronize(a), "adopt totals");
                 const uint64_t ns = totals[0], nv = totals[1];
+                if (ns > n) throw std::runtime_error("write path: more successes than ops");
+                // slot words sit at the success ranks (the last success of each key; the other
+                // entries stay ~0): ns records instead of n
+                if (ns) hip_check(hipMemcpyAsync(fr, fin, ns * sizeof(FinRec), hipMemcpyDeviceToHost, a), "slot words");
                 auto *copies = reinterpret_cast<CopyHdr *>(pin + 64);
                 auto *versions = reinterpret_cast<VersionHdr *>(pin + 64 + ns * sizeof(CopyHdr));
                 if (ns)
@@ -567,7 +570,7 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
                 const double t_d2h = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
                 const std::vector<uint32_t> &d2h = dv.dev_to_host;
                 std::atomic<uint64_t> bad{0};
-                HostTable::parallel_chunks(n, [&](uint64_t b, uint64_t e) {
+                HostTable::parallel_chunks(ns, [&](uint64_t b, uint64_t e) {
                     for (uint64_t k = b; k < e; ++k) {
                         if (fr[k].loc == ~0ull) continue;
                         if (fr[k].loc / cap >= d2h.size()) {
@@ -581,7 +584,7 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
                 if (bad.load())
                     throw std::runtime_error("write path: " + std::to_string(bad.load()) +
                                              " slot words outside the table (ns " + std::to_string(ns) + ")");
-                h.adopt_device_epoch(copies, ns, versions, nv, ns, reinterpret_cast<const HostTable::SlotWords *>(fr), n);
+                h.adopt_device_epoch(copies, ns, versions, nv, ns, reinterpret_cast<const HostTable::SlotWords *>(fr), ns);
                 if (trace)
                     std::fprintf(stderr,
                                  "[wp] n=%llu ok=%llu reserve %.2f enqueue %.2f kernels %.2f d2h %.2f adopted %.2f ms "
