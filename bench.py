@@ -294,17 +294,19 @@ def cpu_rows_for(args, res, gpu_rows):
     return max(1_000_000, min(gpu_rows, fit))
 
 
-def xgmi_roofline(batch, world, stride, step_s, hbm_roof):
-    """Roofline of the multi-GPU step, bound by the xGMI exchange: per rank and step the remote
-    share of the batch ((W-1)/W of it, hash-uniform) sends its 16-B key record out and gets a
-    32-B status record + a stride-byte row back; peak = the W-1 links a rank uses."""
-    remote = batch * (world - 1) / world
+def xgmi_roofline(batch, world, stride, step_s, hbm_roof, remote=None):
+    """Roofline of the multi-GPU step, bound by the xGMI exchange: per rank and step every
+    remote request sends its 16-B key record out and gets a 32-B status record + a stride-byte
+    row back; peak = the W-1 links a rank uses.  remote = the requests this rank routed to other
+    ranks (after coalescing, stage_sharded_stats); default the hash-uniform (W-1)/W of the batch."""
+    if remote is None:
+        remote = batch * (world - 1) / world
     unit = 16 + 32 + stride
     achieved = remote * unit / step_s / 1e9
     peak = XGMI_LINK_GBS * (world - 1)
     return {"bound": "xgmi", "achieved": round(achieved, 1), "peak": peak, "unit": "GB/s",
             "frac": round(achieved / peak, 4), "traffic": None,
-            "kernel": "sharded step (route + RCCL all-to-all-v + probe_kernel + un-permute)",
+            "kernel": "sharded step (coalesce + route + RCCL all-to-all-v + probe_kernel + expand)",
             "algorithmic_bytes_per_unit": unit, "units_per_launch": round(remote),
             "avg_launch_ms": round(step_s * 1e3, 4),
             "peak_source": f"{XGMI_LINK_GBS:.0f} GB/s per xGMI link (7 per MI355X), {world - 1} links per rank",
@@ -1066,21 +1068,35 @@ def main(argv=None):
             step()
             stream.sync()
         kern_ms = float(np.mean([evs[2 * i].elapsed_ms(evs[2 * i + 1]) for i in range(args.steps)]))
-        sample = min(B, 65536)
-        outs = d_out.to_numpy(stage.PROBE_OUT_DTYPE, sample)
-        rows = d_rec.to_numpy(np.uint8, sample * tab.stride).reshape(sample, tab.stride)
+        # self-check: 8 windows of 8192 lookups spread over the batch (every exchange chunk of
+        # the sharded path), each against its key's LoadYCSBRows row
+        sample = min(B, 8192)
+        outs_w, rows_w, keys_w = [], [], []
+        for w in range(8 if B > 8 * sample else 1):
+            o = (B - sample) * w // 7 if B > 8 * sample else 0
+            outs_w.append(d_out.to_numpy(stage.PROBE_OUT_DTYPE, sample, offset=o * 32))
+            rows_w.append(d_rec.to_numpy(np.uint8, sample * tab.stride, offset=o * tab.stride).reshape(sample, tab.stride))
+            keys_w.append(draws[o:o + sample])
+        outs, rows, kw = np.concatenate(outs_w), np.concatenate(rows_w), np.concatenate(keys_w)
         ok = bool((outs["status"] == stage.ST_LATEST).all() and
-                  (rows[:, :8].copy().view(np.uint64).ravel() == draws[:sample]).all() and
-                  (rows[:, 8:1008] == (draws[:sample] & np.uint64(0xFF)).astype(np.uint8)[:, None]).all())
-        samples["c2"] = (draws[:4096].copy(), outs["status"][:4096].copy(), rows[:4096].copy())
+                  (rows[:, :8].copy().view(np.uint64).ravel() == kw).all() and
+                  (rows[:, 8:1008] == (kw & np.uint64(0xFF)).astype(np.uint8)[:, None]).all())
+        samples["c2"] = (draws[:4096].copy(), outs_w[0]["status"][:4096].copy(), rows_w[0][:4096].copy())
         traffic, tsrc = (None, None) if sharded else traffic_from_profile(B, args.rows, "pmc_probe.json")
         roof = hbm_roofline(BYTES_PER_LOOKUP, B, kern_ms,
                             "probe_kernel" if not sharded else "sharded step (route + RCCL + probe_kernel)",
                             traffic, tsrc)
+        coalesce = None
+        if sharded:
+            nk, routed, remote = stage.sharded_stats(tab, loopback=False)
+            coalesce = {"keys": nk, "requests_routed": routed, "remote_requests": remote,
+                        "routed_share": round(routed / max(nk, 1), 4),
+                        "note": "equal keys of an exchange chunk travel and are probed once (stage_set_shard_dedupe)"}
         if sharded and world > 1:
-            roof = xgmi_roofline(B, world, tab.stride, elapsed / args.steps, roof)
+            roof = xgmi_roofline(B, world, tab.stride, elapsed / args.steps, roof, remote=coalesce["remote_requests"])
         head = {"value": round(B * args.steps * world / elapsed, 1), "unit": "ops/s",
                 "ms_per_step": round(elapsed / args.steps * 1e3, 4), "self_check": ok, "roofline": roof,
+                "coalescing": coalesce,
                 "config": {"workload": WORKLOADS["c2"] if not sharded else WORKLOADS["c5"], "theta": args.theta,
                            "traversal": "host" if d_leaf else "device"}}
         for b in (d_keys, d_out, d_rec) + ((d_leaf,) if d_leaf else ()):
@@ -1112,6 +1128,7 @@ def main(argv=None):
             "config": config, "roofline": head["roofline"], "cpu_baseline": cpu, "self_check": head["self_check"],
             **({"ops_per_s_incl_writes": head["ops_per_s_incl_writes"]} if "ops_per_s_incl_writes" in head else {}),
             **({"owner_reply": owner} if owner else {}),
+            **({"coalescing": head["coalescing"]} if head.get("coalescing") else {}),
             **({"extras": extras} if extras else {}),
             "setup_s": {"load": round(t_load, 1), "sync": round(t_sync, 1)},
             "host_peak_rss_gib": round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20, 1),

@@ -412,6 +412,15 @@ int stage_probe_sharded_ex(stage_table *t, const uint64_t *d_keys, const uint32_
                            void *stream);
 /* loopback != 0: the buffer of stage_probe_sharded_loopback's shard state */
 int stage_sharded_owner_rows(stage_table *t, int loopback, uint8_t **d_rows, uint64_t *n_rows);
+/* request coalescing (default on; STAGE_SHARD_DEDUPE=0 or on = 0 turns it off, -1 = the env
+ * default): within each exchange chunk, requests with equal (key, read id) are routed and probed
+ * once and the result is copied to every caller position -- results are identical, the key and
+ * tuple traffic over xGMI shrinks by the batch's duplicate share (about half of a Zipf-0.9
+ * batch).  Owner-reply rows are then one per distinct request. */
+int stage_set_shard_dedupe(stage_table *t, int on);
+/* the last sharded probe on this rank: caller keys, requests routed after coalescing, and of
+ * those the ones owned by other ranks (loopback != 0: the loopback shard state) */
+int stage_sharded_stats(stage_table *t, int loopback, uint64_t *n_keys, uint64_t *n_routed, uint64_t *n_remote);
 
 /* single-process rehearsal of stage_probe_sharded: `world` shard tables on ONE device play the
  * ranks; the routing, count exchange, offsets, local probes and un-permutation are the same

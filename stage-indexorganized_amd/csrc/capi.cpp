@@ -501,8 +501,29 @@ int stage_comm_init(stage_table *t, const uint8_t *id128, int rank, int world) {
     return guarded([&] {
         (void)hipSetDevice(t->dev.device);
         t->comm = std::make_unique<stage::ShardComm>();
-        return stage::shard_init(*t->comm, id128, rank, world, t->shard_chunks);
+        const int rc = stage::shard_init(*t->comm, id128, rank, world, t->shard_chunks);
+        if (t->shard_dedupe >= 0) t->comm->dedupe = t->shard_dedupe != 0;
+        return rc;
     });
+}
+
+int stage_set_shard_dedupe(stage_table *t, int on) {
+    if (!t || on < -1 || on > 1) return fail(STAGE_E_ARG, "dedupe must be -1, 0 or 1");
+    t->shard_dedupe = on;
+    const bool v = on < 0 ? stage::shard_default_dedupe() : on != 0;
+    if (t->comm) t->comm->dedupe = v;
+    if (t->loop_comm) t->loop_comm->dedupe = v;
+    return STAGE_OK;
+}
+
+int stage_sharded_stats(stage_table *t, int loopback, uint64_t *n_keys, uint64_t *n_routed, uint64_t *n_remote) {
+    if (!t || !n_keys || !n_routed || !n_remote) return fail(STAGE_E_ARG, "null argument");
+    stage::ShardComm *c = loopback ? t->loop_comm.get() : t->comm.get();
+    if (!c) return fail(STAGE_E_STATE, "no sharded probe has run");
+    *n_keys = c->last_n;
+    *n_routed = c->last_routed;
+    *n_remote = c->last_remote;
+    return STAGE_OK;
 }
 
 int stage_set_shard_chunks(stage_table *t, int chunks) {
@@ -584,6 +605,7 @@ int stage_probe_sharded_loopback(stage_table *const *shards, int world, const ui
                 t->loop_comm = std::make_unique<stage::ShardComm>();
                 stage::shard_init_loopback(*t->loop_comm, r, world, want);
             }
+            if (t->shard_dedupe >= 0) t->loop_comm->dedupe = t->shard_dedupe != 0;
             cs[r] = t->loop_comm.get();
             ts[r] = &t->dev.view;
             ks[r] = d_keys[r];

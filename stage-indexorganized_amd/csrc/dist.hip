@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <hipcub/hipcub.hpp>
+
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -104,7 +106,8 @@ __global__ __launch_bounds__(1024) void route_scan(const uint32_t *__restrict__ 
 __global__ __launch_bounds__(256) void route_scatter(const uint64_t *__restrict__ keys, const uint32_t *__restrict__ rids,
                                                      uint64_t n, int world, const uint8_t *__restrict__ dest,
                                                      const uint32_t *__restrict__ offs, SendRec *__restrict__ send,
-                                                     uint32_t *__restrict__ perm, uint32_t idx_base) {
+                                                     uint32_t *__restrict__ perm, uint32_t idx_base,
+                                                     uint32_t *__restrict__ upos) {
     __shared__ uint32_t cur[kMaxWorld];
     if (threadIdx.x < (unsigned)world) cur[threadIdx.x] = offs[threadIdx.x * gridDim.x + blockIdx.x];
     __syncthreads();
@@ -114,7 +117,44 @@ __global__ __launch_bounds__(256) void route_scatter(const uint64_t *__restrict_
         const uint32_t pos = atomicAdd(&cur[dest[i]], 1u);
         send[pos] = SendRec{keys[i], rids ? rids[i] : 0xFFFFFFFEu, 0};
         perm[pos] = idx_base + (uint32_t)i;
+        // coalesced requests: where request i was sent (send / perm start at the chunk base)
+        if (upos) upos[idx_base + i] = idx_base + pos;
     }
+}
+
+// ---- request coalescing of one chunk [b, b + len): the chunk's keys are radix-sorted with
+// their chunk positions; a sorted entry starts a request when its key or read id differs from
+// its predecessor's; requests are numbered by an inclusive scan and packed at [b, b + nu).
+__global__ void dd_iota_kernel(uint32_t *__restrict__ v, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) v[i] = (uint32_t)i;
+}
+
+__global__ void dd_heads(const uint64_t *__restrict__ skeys, const uint32_t *__restrict__ sidx,
+                         const uint32_t *__restrict__ rids, uint64_t n, uint32_t *__restrict__ flag) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    bool head = j == 0 || skeys[j] != skeys[j - 1];
+    if (!head && rids) head = rids[sidx[j]] != rids[sidx[j - 1]];
+    flag[j] = head ? 1u : 0u;
+}
+
+// uidx[b + p] = b + request number of the caller position p; the request's key / read id packed
+// at b + its number; nu[chunk] = the chunk's request count
+__global__ void dd_pack(const uint64_t *__restrict__ skeys, const uint32_t *__restrict__ sidx,
+                        const uint32_t *__restrict__ rids, const uint32_t *__restrict__ flag,
+                        const uint32_t *__restrict__ useq, uint64_t n, uint32_t b, uint32_t *__restrict__ uidx,
+                        uint64_t *__restrict__ ukeys, uint32_t *__restrict__ urids, uint32_t *__restrict__ nu,
+                        int chunk) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const uint32_t u = useq[j] - 1u, p = sidx[j];
+    uidx[b + p] = b + u;
+    if (flag[j]) {
+        ukeys[b + u] = skeys[j];
+        if (rids) urids[b + u] = rids[p];
+    }
+    if (j == n - 1) nu[chunk] = useq[j];
 }
 
 __global__ void unpack_keys(const SendRec *__restrict__ recv, uint64_t n, uint64_t *__restrict__ keys,
@@ -149,6 +189,29 @@ __global__ void unpermute(const stage_probe_out_dev *__restrict__ bout, const ui
     }
 }
 
+// coalesced requests back in the caller's order: caller position o takes the result of its
+// request, sent from position p = upos[uidx[o]] (own requests read in place, as unpermute)
+__global__ void expand(const stage_probe_out_dev *__restrict__ bout, const uint8_t *__restrict__ brec,
+                       const uint32_t *__restrict__ uidx, const uint32_t *__restrict__ upos, uint64_t o0, uint64_t o1,
+                       uint32_t stride, stage_probe_out_dev *__restrict__ out, uint8_t *__restrict__ recs, uint64_t q0,
+                       uint64_t q1, const stage_probe_out_dev *__restrict__ qout, const uint8_t *__restrict__ qrec) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    for (uint64_t o = o0 + w; o < o1; o += nw) {
+        const uint64_t p = upos[uidx[o]];
+        const bool own = p >= q0 && p < q1;
+        const stage_probe_out_dev *so = own ? qout + (p - q0) : bout + p;
+        if (lane < 2) reinterpret_cast<uint4 *>(out + o)[lane] = reinterpret_cast<const uint4 *>(so)[lane];
+        if (recs) {
+            const uint4 *sr = reinterpret_cast<const uint4 *>(own ? qrec + (p - q0) * (uint64_t)stride
+                                                                   : brec + p * (uint64_t)stride);
+            uint4 *d = reinterpret_cast<uint4 *>(recs + o * stride);
+            for (uint32_t c = lane; c < (stride >> 4); c += 64) d[c] = sr[c];
+        }
+    }
+}
+
 // reply mode "owner": the row stays in the owner's result buffer; the status record carries
 // its owner-local index in the meta_hi word (stage_hip.h: STAGE_REPLY_OWNER)
 __global__ void tag_rows(stage_probe_out_dev *__restrict__ out, uint64_t m, uint32_t base) {
@@ -169,8 +232,14 @@ ShardComm::~ShardComm() {
     if (us) (void)hipStreamSynchronize(us), (void)hipStreamDestroy(us);
     for (hipEvent_t e : evs) (void)hipEventDestroy(e);
     if (comm) ncclCommDestroy((ncclComm_t)comm);
-    for (void *p : {dest, cursor, perm, send, recv, rout, rrec, bout, brec, cnt, lkeys, lrids})
+    for (void *p : {dest, cursor, perm, send, recv, rout, rrec, bout, brec, cnt, lkeys, lrids, dd_skeys, dd_iota,
+                    dd_sidx, dd_flag, dd_useq, uidx, ukeys, urids, upos, dd_cub, dd_nu})
         if (p) (void)hipFree(p);
+}
+
+bool shard_default_dedupe() {
+    const char *e = std::getenv("STAGE_SHARD_DEDUPE");
+    return !(e && e[0] == '0');
 }
 
 int shard_unique_id(uint8_t *id128) {
@@ -187,6 +256,7 @@ static void init_common(ShardComm &c, int rank, int world, int chunks) {
     c.rank = rank;
     c.world = world;
     c.chunks = chunks;
+    c.dedupe = shard_default_dedupe();
     grow(c.cnt, 4ull * sizeof(uint32_t) * (uint64_t)world * chunks);
     grow(c.cursor, (2ull * world * kRouteBlocks + 16) * sizeof(uint32_t));
     chk(hipStreamCreateWithFlags(&c.cs, hipStreamNonBlocking), "comm stream");
@@ -228,6 +298,7 @@ struct Plan {
     std::vector<uint64_t> cb, rb;           // chunk bases (send side / receive side), C+1
     std::vector<uint32_t> sc, rc;           // [i*W + r] counts sent to / received from r
     std::vector<uint64_t> soff, roff;       // [i*(W+1) + r] absolute segment starts
+    bool dedupe = false;                    // chunk i routes its coalesced requests [cb_i, cb_i + nu_i)
     uint64_t m() const { return rb[C]; }
 };
 
@@ -251,17 +322,79 @@ static void plan_route(ShardComm &c, Plan &P, const uint64_t *d_keys, const uint
     P.C = C;
     P.cb.resize(C + 1);
     for (int i = 0; i <= C; ++i) P.cb[i] = n * (uint64_t)i / (uint64_t)C;
+    P.dedupe = c.dedupe && n > 0 && n < (1ull << 31);
+    // what is routed: the caller's keys, or each chunk's coalesced requests packed at its base
+    const uint64_t *rkeys = d_keys;
+    const uint32_t *rrids = d_rids;
+    std::vector<uint64_t> rlen(C);
+    for (int i = 0; i < C; ++i) rlen[i] = P.cb[i + 1] - P.cb[i];
+    if (P.dedupe) {
+        if (c.dd_cap < c.cap_local) {
+            const uint64_t cap = c.cap_local;
+            grow(c.dd_skeys, cap * 8);
+            grow(c.dd_iota, cap * 4);
+            grow(c.dd_sidx, cap * 4);
+            grow(c.dd_flag, cap * 4);
+            grow(c.dd_useq, cap * 4);
+            grow(c.uidx, cap * 4);
+            grow(c.ukeys, cap * 8);
+            grow(c.urids, cap * 4);
+            grow(c.upos, cap * 4);
+            grow(c.dd_nu, 64 * 4);
+            size_t sb = 0, cb = 0;
+            chk(hipcub::DeviceRadixSort::SortPairs(nullptr, sb, (uint64_t *)nullptr, (uint64_t *)nullptr,
+                                                   (uint32_t *)nullptr, (uint32_t *)nullptr, (int)cap, 0, 64, s),
+                "sort size");
+            chk(hipcub::DeviceScan::InclusiveSum(nullptr, cb, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)cap, s),
+                "scan size");
+            c.dd_cub_bytes = std::max(sb, cb);
+            grow(c.dd_cub, c.dd_cub_bytes);
+            c.dd_cap = cap;
+        }
+        uint32_t *nu = (uint32_t *)c.dd_nu;
+        chk(hipMemsetAsync(nu, 0, 64 * 4, s), "memset nu");
+        uint32_t *iota = (uint32_t *)c.dd_iota, *sidx = (uint32_t *)c.dd_sidx, *flag = (uint32_t *)c.dd_flag,
+                 *useq = (uint32_t *)c.dd_useq;
+        uint64_t *skeys = (uint64_t *)c.dd_skeys;
+        const uint64_t maxlen = *std::max_element(rlen.begin(), rlen.end());
+        dd_iota_kernel<<<(unsigned)((maxlen + 255) / 256), 256, 0, s>>>(iota, maxlen);
+        for (int i = 0; i < C; ++i) {
+            const uint64_t b = P.cb[i], len = rlen[i];
+            if (!len) continue;
+            const unsigned nb = (unsigned)((len + 255) / 256);
+            const uint32_t *cr = d_rids ? d_rids + b : nullptr;
+            size_t bytes = c.dd_cub_bytes;
+            chk(hipcub::DeviceRadixSort::SortPairs(c.dd_cub, bytes, d_keys + b, skeys, iota, sidx, (int)len, 0, 64, s),
+                "dedupe sort");
+            dd_heads<<<nb, 256, 0, s>>>(skeys, sidx, cr, len, flag);
+            bytes = c.dd_cub_bytes;
+            chk(hipcub::DeviceScan::InclusiveSum(c.dd_cub, bytes, flag, useq, (int)len, s), "dedupe scan");
+            dd_pack<<<nb, 256, 0, s>>>(skeys, sidx, cr, flag, useq, len, (uint32_t)b, (uint32_t *)c.uidx,
+                                       (uint64_t *)c.ukeys, (uint32_t *)c.urids, nu, i);
+        }
+        chk(hipGetLastError(), "dedupe");
+        std::vector<uint32_t> hn(C);
+        chk(hipMemcpyAsync(hn.data(), nu, C * 4, hipMemcpyDeviceToHost, s), "nu d2h");
+        chk(hipStreamSynchronize(s), "sync");
+        for (int i = 0; i < C; ++i) {
+            if (hn[i] > rlen[i]) throw std::runtime_error("dedupe: more requests than keys");
+            rlen[i] = hn[i];
+        }
+        rkeys = (const uint64_t *)c.ukeys;
+        rrids = d_rids ? (const uint32_t *)c.urids : nullptr;
+    }
     uint32_t *counts = (uint32_t *)c.cnt;  // [C][W] send counts
     uint32_t *blk = (uint32_t *)c.cursor, *offs = blk + (uint64_t)W * kRouteBlocks;
     chk(hipMemsetAsync(counts, 0, (uint64_t)C * W * sizeof(uint32_t), s), "memset counts");
     for (int i = 0; i < C; ++i) {
-        const uint64_t b = P.cb[i], len = P.cb[i + 1] - b;
+        const uint64_t b = P.cb[i], len = rlen[i];
         if (!len) continue;
-        route_hist<<<kRouteBlocks, 256, 0, s>>>(d_keys + b, len, W, (uint8_t *)c.dest + b, blk);
+        route_hist<<<kRouteBlocks, 256, 0, s>>>(rkeys + b, len, W, (uint8_t *)c.dest + b, blk);
         route_scan<<<1, 1024, 0, s>>>(blk, (uint32_t)(W * kRouteBlocks), W, kRouteBlocks, offs, counts + i * W);
-        route_scatter<<<kRouteBlocks, 256, 0, s>>>(d_keys + b, d_rids ? d_rids + b : nullptr, len, W,
+        route_scatter<<<kRouteBlocks, 256, 0, s>>>(rkeys + b, rrids ? rrids + b : nullptr, len, W,
                                                    (const uint8_t *)c.dest + b, offs, (SendRec *)c.send + b,
-                                                   (uint32_t *)c.perm + b, (uint32_t)b);
+                                                   (uint32_t *)c.perm + b, (uint32_t)b,
+                                                   P.dedupe ? (uint32_t *)c.upos : nullptr);
     }
     chk(hipGetLastError(), "route");
     P.sc.resize((size_t)C * W);
@@ -272,6 +405,13 @@ static void plan_route(ShardComm &c, Plan &P, const uint64_t *d_keys, const uint
         P.soff[i * (W + 1)] = P.cb[i];
         for (int r = 0; r < W; ++r) P.soff[i * (W + 1) + r + 1] = P.soff[i * (W + 1) + r] + P.sc[i * W + r];
     }
+    c.last_n = n;
+    c.last_routed = c.last_remote = 0;
+    for (int i = 0; i < C; ++i)
+        for (int r = 0; r < W; ++r) {
+            c.last_routed += P.sc[(size_t)i * W + r];
+            if (r != c.rank) c.last_remote += P.sc[(size_t)i * W + r];
+        }
 }
 
 // receive side of the plan from rc (filled by the transport's count exchange)
@@ -316,6 +456,15 @@ static void chunk_unpermute(ShardComm &c, const Plan &P, int i, uint32_t stride,
     const int W = P.W, me = c.rank;
     const uint64_t q0 = P.soff[(size_t)i * (W + 1) + me], q1 = P.soff[(size_t)i * (W + 1) + me + 1];
     const uint64_t ro = P.roff[(size_t)i * (W + 1) + me];  // where the local probe wrote them
+    if (P.dedupe) {
+        if (p1 > p0)
+            expand<<<(unsigned)std::min<uint64_t>((p1 - p0 + 3) / 4, 8192), 256, 0, s>>>(
+                (const stage_probe_out_dev *)c.bout, (const uint8_t *)c.brec, (const uint32_t *)c.uidx,
+                (const uint32_t *)c.upos, p0, p1, stride, d_out, d_recs, q0, q1, (const stage_probe_out_dev *)c.rout + ro,
+                (const uint8_t *)c.rrec + ro * stride);
+        chk(hipGetLastError(), "expand");
+        return;
+    }
     if (p1 > p0)
         unpermute<<<(unsigned)std::min<uint64_t>((p1 - p0 + 3) / 4, 8192), 256, 0, s>>>(
             (const stage_probe_out_dev *)c.bout, (const uint8_t *)c.brec, (const uint32_t *)c.perm, p0, p1, stride,

@@ -25,6 +25,14 @@ struct ShardComm {
     hipStream_t us = nullptr;        // un-permutation
     std::vector<hipEvent_t> evs;     // per-chunk keys / probe / results events + join
     uint64_t owner_rows = 0;         // rows left in rrec by the last owner-reply probe
+    // request coalescing: equal (key, read id) requests of a chunk are routed once and their
+    // result is expanded to every caller position (a Zipf batch is ~half duplicates)
+    bool dedupe = true;
+    void *dd_skeys = nullptr, *dd_iota = nullptr, *dd_sidx = nullptr, *dd_flag = nullptr, *dd_useq = nullptr;
+    void *uidx = nullptr, *ukeys = nullptr, *urids = nullptr, *upos = nullptr, *dd_cub = nullptr, *dd_nu = nullptr;
+    uint64_t dd_cap = 0, dd_cub_bytes = 0;
+    // the last sharded probe: caller keys, requests routed (after coalescing), of which remote
+    uint64_t last_n = 0, last_routed = 0, last_remote = 0;
     ~ShardComm();
 };
 
@@ -32,6 +40,7 @@ int shard_unique_id(uint8_t *id128);
 // chunks: overlapped exchange chunks, identical on every rank (<= 0: STAGE_SHARD_CHUNKS or 4)
 int shard_init(ShardComm &c, const uint8_t *id128, int rank, int world, int chunks);
 int shard_default_chunks();
+bool shard_default_dedupe();  // STAGE_SHARD_DEDUPE=0 turns request coalescing off
 int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const uint64_t *d_keys,
                 const uint32_t *d_rids, uint64_t n, stage_probe_out_dev *d_out, uint8_t *d_recs, int reply,
                 hipStream_t s);

@@ -34,6 +34,7 @@ struct stage_table {
     std::unique_ptr<stage::ShardComm> comm;
     std::unique_ptr<stage::ShardComm> loop_comm;  // stage_probe_sharded_loopback state
     int shard_chunks = 0;                          // 0 = STAGE_SHARD_CHUNKS or the default
+    int shard_dedupe = -1;                         // -1 = STAGE_SHARD_DEDUPE or on
     std::mutex pipe_mu;  // serialises stage_probe_host calls on this table
     std::unique_ptr<stage::HostPipe, stage::HostPipeDeleter> pipe;
     // the device write path hands its epoch's bookkeeping (new copy / version headers, slot

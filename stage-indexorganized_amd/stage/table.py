@@ -52,10 +52,11 @@ class DeviceBuffer:
             check(lib().stage_memcpy_h2d(b.ptr, arr.ctypes.data, arr.nbytes, stream), "h2d")
         return b
 
-    def to_numpy(self, dtype, count, stream=None):
+    def to_numpy(self, dtype, count, stream=None, offset=0):
+        """count elements from byte `offset` of the buffer."""
         out = np.empty(count, dtype=dtype)
         if out.nbytes:
-            check(lib().stage_memcpy_d2h(out.ctypes.data, self.ptr, out.nbytes, stream), "d2h")
+            check(lib().stage_memcpy_d2h(out.ctypes.data, self.ptr + offset, out.nbytes, stream), "d2h")
         return out
 
     def memset(self, value=0, stream=None):
@@ -553,6 +554,18 @@ def owner_rows(table, loopback=True):
     n = ctypes.c_uint64()
     check(lib().stage_sharded_owner_rows(table.h, int(loopback), ctypes.byref(p), ctypes.byref(n)), "owner_rows")
     return p.value, n.value
+
+
+def set_shard_dedupe(table, on):
+    """stage_set_shard_dedupe: request coalescing of the sharded front-end (-1 = env default)."""
+    check(lib().stage_set_shard_dedupe(table.h, int(on)), "set_shard_dedupe")
+
+
+def sharded_stats(table, loopback=True):
+    """stage_sharded_stats: (caller keys, routed requests, remote requests) of the last sharded probe."""
+    v = [ctypes.c_uint64() for _ in range(3)]
+    check(lib().stage_sharded_stats(table.h, int(loopback), *[ctypes.byref(x) for x in v]), "sharded_stats")
+    return tuple(x.value for x in v)
 
 
 def probe_sharded_loopback(tables, keys_per_rank, read_ids_per_rank=None, records=True, reply=REPLY_ROWS):

@@ -52,8 +52,8 @@ def shard_tables(keys, world, mode=1):
     return tabs, h
 
 
-@pytest.mark.parametrize("world,chunks", [(2, 1), (3, 4), (8, 7)])
-def test_sharded_data_path_loopback_equals_single_table(gpu, world, chunks):
+@pytest.mark.parametrize("world,chunks,dedupe", [(2, 1, 1), (3, 4, 1), (8, 7, 1), (3, 4, 0)])
+def test_sharded_data_path_loopback_equals_single_table(gpu, world, chunks, dedupe):
     # the multi-GPU data path (routing, count exchange, all-to-all-v offsets, local probes,
     # reverse exchange, un-permutation) with W shards on one device, against one table
     # holding every key; version chains on some keys so statuses and rows vary
@@ -73,6 +73,7 @@ def test_sharded_data_path_loopback_equals_single_table(gpu, world, chunks):
         t.sync()
     for t in tabs:
         check(stage.lib().stage_set_shard_chunks(t.h, chunks), "chunks")
+        stage.set_shard_dedupe(t, dedupe)
     sizes = [int(x) for x in rng.integers(1, 120_000, world)]
     sizes[-1] = 0  # a rank with nothing to probe still takes part in the exchange
     per_keys = [np.concatenate([rng.integers(0, n + 20_000, s), rng.choice(hot, min(s, 500))]).astype(np.uint64)
@@ -115,7 +116,9 @@ def test_owner_reply_mode_loopback(gpu):
         buf = np.zeros(cnt * t.stride, np.uint8)
         check(stage.lib().stage_memcpy_d2h(buf.ctypes.data, ptr, buf.nbytes, None), "d2h")
         owner_bufs.append(buf.reshape(cnt, t.stride))
-    assert sum(b.shape[0] for b in owner_bufs) == sum(k.size for k in per_keys)
+    # one owner row per routed request (equal keys of a chunk are coalesced)
+    routed = [stage.sharded_stats(t)[1] for t in tabs]
+    assert sum(b.shape[0] for b in owner_bufs) == sum(routed) <= sum(k.size for k in per_keys)
     for r in range(world):
         out, rows = res[r]
         ref_out, ref_rows = full.probe(per_keys[r])
@@ -126,3 +129,55 @@ def test_owner_reply_mode_loopback(gpu):
             got = owner_bufs[o][out["meta_hi"][sel]]
             hit = out["status"][sel] != stage.ST_NOT_FOUND
             assert (got[hit] == ref_rows[sel][hit]).all()
+
+
+@pytest.mark.parametrize("read_ids", [False, True])
+def test_request_coalescing_zipf_batch(gpu, read_ids):
+    # a Zipf batch is about half duplicates: equal (key, read id) requests of a chunk travel and
+    # are probed once, every caller position gets its request's result -- identical to the
+    # uncoalesced path and to one table holding every key
+    world, n = 4, 300_000
+    keys = np.arange(n, dtype=np.uint64)
+    tabs, h = shard_tables(keys, world)
+    full = stage.Table(key_width=8)
+    full.load_keys(keys, 8, mode=1)
+    rng = np.random.default_rng(5)
+    hot = rng.choice(n, 500, replace=False).astype(np.uint64)
+    for k in hot:  # version chains on some hot keys: results depend on the read id
+        owner = tabs[int(h[int(k)] % np.uint64(world))]
+        for t in (owner, full):
+            assert t.update(int(k), 16, b"\x17" * 24, 10) == stage.RC_OK
+            assert t.commit_update(int(k), 11, 11) == stage.RC_OK
+    for t in tabs + [full]:
+        t.sync()
+    per_keys = [np.concatenate([stage.zipf_draws(n + 999, 0.9, 40 + r, 60_000, nthreads=2), hot[:300]])
+                for r in range(world)]
+    per_rids = [rng.integers(9, 13, k.size).astype(np.uint32) for k in per_keys] if read_ids else None
+    got = {}
+    for dd in (1, 0):
+        for t in tabs:
+            stage.set_shard_dedupe(t, dd)
+        got[dd] = stage.probe_sharded_loopback(tabs, per_keys, per_rids)
+        stats = [stage.sharded_stats(t) for t in tabs]
+        for r in range(world):
+            nk, routed, remote = stats[r]
+            assert nk == per_keys[r].size and remote <= routed
+            pairs = per_keys[r] if per_rids is None else \
+                (per_keys[r] << np.uint64(8)) | per_rids[r].astype(np.uint64)
+            if dd:
+                # at least the distinct requests; equal keys with other read ids in between are
+                # separate requests, so only key-only batches must shrink a lot
+                assert np.unique(pairs).size <= routed <= nk
+                if per_rids is None:
+                    assert routed < 0.8 * nk
+            else:
+                assert routed == nk
+    for r in range(world):
+        ref_out, ref_rows = full.probe(per_keys[r], read_ids=None if per_rids is None else per_rids[r])
+        for dd in (1, 0):
+            out, rows = got[dd][r]
+            for f in ("status", "flags", "hops", "key_len", "cstamp", "rec_cstamp", "copy_sstamp"):
+                assert (out[f] == ref_out[f]).all(), (dd, r, f)
+            assert (rows == ref_rows).all(), (dd, r)
+    for t in tabs:
+        stage.set_shard_dedupe(t, -1)
