@@ -190,24 +190,47 @@ __global__ void unpermute(const stage_probe_out_dev *__restrict__ bout, const ui
 }
 
 // coalesced requests back in the caller's order: caller position o takes the result of its
-// request, sent from position p = upos[uidx[o]] (own requests read in place, as unpermute)
-__global__ void expand(const stage_probe_out_dev *__restrict__ bout, const uint8_t *__restrict__ brec,
+// request, sent from position p = upos[uidx[o]] (own requests read in place, as unpermute).
+// A wave copies R caller positions per pass with their R source rows in flight together.
+template <int R>
+__global__ __launch_bounds__(256) void expand(const stage_probe_out_dev *__restrict__ bout, const uint8_t *__restrict__ brec,
                        const uint32_t *__restrict__ uidx, const uint32_t *__restrict__ upos, uint64_t o0, uint64_t o1,
                        uint32_t stride, stage_probe_out_dev *__restrict__ out, uint8_t *__restrict__ recs, uint64_t q0,
                        uint64_t q1, const stage_probe_out_dev *__restrict__ qout, const uint8_t *__restrict__ qrec) {
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    for (uint64_t o = o0 + w; o < o1; o += nw) {
-        const uint64_t p = upos[uidx[o]];
-        const bool own = p >= q0 && p < q1;
-        const stage_probe_out_dev *so = own ? qout + (p - q0) : bout + p;
-        if (lane < 2) reinterpret_cast<uint4 *>(out + o)[lane] = reinterpret_cast<const uint4 *>(so)[lane];
+    const uint32_t chunks = stride >> 4;
+    for (uint64_t ob = o0 + w * R; ob < o1; ob += nw * R) {
+        const uint4 *sr[R];
+        const uint4 *so[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint64_t o = ob + r < o1 ? ob + r : o1 - 1;
+            const uint64_t p = upos[uidx[o]];
+            const bool own = p >= q0 && p < q1;
+            so[r] = reinterpret_cast<const uint4 *>(own ? qout + (p - q0) : bout + p);
+            sr[r] = reinterpret_cast<const uint4 *>(own ? qrec + (p - q0) * (uint64_t)stride : brec + p * (uint64_t)stride);
+        }
+        // status records: lanes 2r, 2r+1 copy position r's two halves
+        if (lane < 2 * R) {
+            const int r = lane >> 1;
+            const uint4 *src = so[0];
+#pragma unroll
+            for (int k = 1; k < R; ++k)
+                if (r == k) src = so[k];
+            if (ob + r < o1) reinterpret_cast<uint4 *>(out + ob + r)[lane & 1] = src[lane & 1];
+        }
         if (recs) {
-            const uint4 *sr = reinterpret_cast<const uint4 *>(own ? qrec + (p - q0) * (uint64_t)stride
-                                                                   : brec + p * (uint64_t)stride);
-            uint4 *d = reinterpret_cast<uint4 *>(recs + o * stride);
-            for (uint32_t c = lane; c < (stride >> 4); c += 64) d[c] = sr[c];
+            for (uint32_t c0 = 0; c0 < chunks; c0 += 64) {
+                const uint32_t c = c0 + lane;
+                uint4 v[R];
+#pragma unroll
+                for (int r = 0; r < R; ++r) v[r] = c < chunks ? sr[r][c] : uint4{0, 0, 0, 0};
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+                    if (c < chunks && ob + r < o1) reinterpret_cast<uint4 *>(recs + (ob + r) * stride)[c] = v[r];
+            }
         }
     }
 }
@@ -457,8 +480,9 @@ static void chunk_unpermute(ShardComm &c, const Plan &P, int i, uint32_t stride,
     const uint64_t q0 = P.soff[(size_t)i * (W + 1) + me], q1 = P.soff[(size_t)i * (W + 1) + me + 1];
     const uint64_t ro = P.roff[(size_t)i * (W + 1) + me];  // where the local probe wrote them
     if (P.dedupe) {
+        constexpr int R = 4;
         if (p1 > p0)
-            expand<<<(unsigned)std::min<uint64_t>((p1 - p0 + 3) / 4, 8192), 256, 0, s>>>(
+            expand<R><<<(unsigned)std::min<uint64_t>((p1 - p0 + 4 * R - 1) / (4 * R), 8192), 256, 0, s>>>(
                 (const stage_probe_out_dev *)c.bout, (const uint8_t *)c.brec, (const uint32_t *)c.uidx,
                 (const uint32_t *)c.upos, p0, p1, stride, d_out, d_recs, q0, q1, (const stage_probe_out_dev *)c.rout + ro,
                 (const uint8_t *)c.rrec + ro * stride);
