@@ -168,23 +168,47 @@ __global__ void unpack_keys(const SendRec *__restrict__ recv, uint64_t n, uint64
 // back in the caller's order: out[perm[p]] = bout[p] for p in [p0, p1), one wave per probe.
 // Positions [q0, q1) are this rank's own keys: they never left the device, so they are read
 // straight from the local probe's output (qout / qrec) instead of a received copy.
-__global__ void unpermute(const stage_probe_out_dev *__restrict__ bout, const uint8_t *__restrict__ brec,
+template <int R>
+__global__ __launch_bounds__(256) void unpermute(const stage_probe_out_dev *__restrict__ bout, const uint8_t *__restrict__ brec,
                           const uint32_t *__restrict__ perm, uint64_t p0, uint64_t p1, uint32_t stride,
                           stage_probe_out_dev *__restrict__ out, uint8_t *__restrict__ recs, uint64_t q0, uint64_t q1,
                           const stage_probe_out_dev *__restrict__ qout, const uint8_t *__restrict__ qrec) {
+    // R positions per wave pass, their rows in flight together (as expand)
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    for (uint64_t p = p0 + w; p < p1; p += nw) {
-        const uint32_t dst = perm[p];
-        const bool own = p >= q0 && p < q1;
-        const stage_probe_out_dev *so = own ? qout + (p - q0) : bout + p;
-        if (lane < 2) reinterpret_cast<uint4 *>(out + dst)[lane] = reinterpret_cast<const uint4 *>(so)[lane];
+    const uint32_t chunks = stride >> 4;
+    for (uint64_t pb = p0 + w * R; pb < p1; pb += nw * R) {
+        const uint4 *sr[R];
+        const uint4 *so[R];
+        uint64_t dst[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint64_t p = pb + r < p1 ? pb + r : p1 - 1;
+            dst[r] = perm[p];
+            const bool own = p >= q0 && p < q1;
+            so[r] = reinterpret_cast<const uint4 *>(own ? qout + (p - q0) : bout + p);
+            sr[r] = reinterpret_cast<const uint4 *>(own ? qrec + (p - q0) * (uint64_t)stride : brec + p * (uint64_t)stride);
+        }
+        if (lane < 2 * R) {
+            const int r = lane >> 1;
+            const uint4 *src = so[0];
+            uint64_t d = dst[0];
+#pragma unroll
+            for (int k = 1; k < R; ++k)
+                if (r == k) src = so[k], d = dst[k];
+            if (pb + r < p1) reinterpret_cast<uint4 *>(out + d)[lane & 1] = src[lane & 1];
+        }
         if (recs) {
-            const uint4 *sr = reinterpret_cast<const uint4 *>(own ? qrec + (p - q0) * (uint64_t)stride
-                                                                   : brec + p * (uint64_t)stride);
-            uint4 *d = reinterpret_cast<uint4 *>(recs + (uint64_t)dst * stride);
-            for (uint32_t c = lane; c < (stride >> 4); c += 64) d[c] = sr[c];
+            for (uint32_t c0 = 0; c0 < chunks; c0 += 64) {
+                const uint32_t c = c0 + lane;
+                uint4 v[R];
+#pragma unroll
+                for (int r = 0; r < R; ++r) v[r] = c < chunks ? sr[r][c] : uint4{0, 0, 0, 0};
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+                    if (c < chunks && pb + r < p1) reinterpret_cast<uint4 *>(recs + dst[r] * stride)[c] = v[r];
+            }
         }
     }
 }
@@ -489,8 +513,9 @@ static void chunk_unpermute(ShardComm &c, const Plan &P, int i, uint32_t stride,
         chk(hipGetLastError(), "expand");
         return;
     }
+    constexpr int R = 4;
     if (p1 > p0)
-        unpermute<<<(unsigned)std::min<uint64_t>((p1 - p0 + 3) / 4, 8192), 256, 0, s>>>(
+        unpermute<R><<<(unsigned)std::min<uint64_t>((p1 - p0 + 4 * R - 1) / (4 * R), 8192), 256, 0, s>>>(
             (const stage_probe_out_dev *)c.bout, (const uint8_t *)c.brec, (const uint32_t *)c.perm, p0, p1, stride,
             d_out, d_recs, q0, q1, (const stage_probe_out_dev *)c.rout + ro, (const uint8_t *)c.rrec + ro * stride);
     chk(hipGetLastError(), "unpermute");
