@@ -16,6 +16,10 @@ def test_xgmi_roofline_fields():
     assert r["units_per_launch"] == round(remote) and r["avg_launch_ms"] == 20.0
     r2 = bench.xgmi_roofline(1000, 2, 1024, 1.0, hbm)
     assert r2["peak"] == bench.XGMI_LINK_GBS and r2["units_per_launch"] == 500
+    # coalesced requests: the bytes of the remote requests actually routed
+    r3 = bench.xgmi_roofline(1 << 24, 8, 1024, 0.02, hbm, remote=7_900_000)
+    assert r3["units_per_launch"] == 7_900_000
+    assert abs(r3["achieved"] - 7_900_000 * (16 + 32 + 1024) / 0.02 / 1e9) < 0.1
 
 
 def test_default_args_are_the_c2_bench(monkeypatch):
