@@ -8,7 +8,7 @@ Default (`--config c2`, BASELINE.json configs[1]): YCSB-C batched point lookup.
           [1, N_total-1] (ZipfDistribution of benchmark_common.h, seed 0x5EED + rank):
           device traversal + leaf probe + visibility + 1008-B tuple copy (stage_probe_batch);
           with --gpus > 1 each key goes to shard MurmurHash64A(key, 8, 0) % world and is
-          answered over RCCL (stage_probe_sharded) -- configs[4] at 8 GPUs
+          answered over RCCL (stage_probe_sharded, run_sharded) -- configs[4] at 8 GPUs
   value = lookups completed by all ranks / max-over-ranks wall time of the K timed steps.
   After the headline the same 100M-row table runs configs[3] (C4, 100-key scans) and then
   configs[2] (C3, YCSB-B epochs; last, since it mutates the table); their lines are nested
@@ -19,7 +19,7 @@ Default (`--config c2`, BASELINE.json configs[1]): YCSB-C batched point lookup.
 `python -m torch.distributed.run`, before any GPU call) and forwards rank 0's JSON line; under
 torch.distributed the world size must equal --gpus.
 
-The CPU baseline leg (rank 0, one GPU) times the test oracle -- the C restatement of the
+The CPU baseline leg (rank 0; at N > 1 the per-shard C2 leg) times the test oracle -- the C restatement of the
 reference's BTree::Read + executor copy ("lookup" mode) and of RunMixed's read-only
 transactions with the Index-SSN read side ("full-txn" mode) -- on the largest table the host
 RAM holds (up to the GPU's N; built in parallel with the same leaves as the single loader,
@@ -175,16 +175,23 @@ def murmur64a_u64(keys, seed=0):
 
 
 def dry_run(args, rank, world, dist):
-    """Control-plane rehearsal without a GPU: the ranks of the launcher rendezvous, each loads
-    its shard (MurmurHash64A(key) % world) into a host table, routes a probe batch to its
+    """Control-plane rehearsal without a GPU: the ranks of the launcher rendezvous (gloo), each
+    loads its shard (MurmurHash64A(key) % world) into a host table, routes a probe batch to its
     owners with an all-to-all, and the step is timed with the bench's barrier / max-over-ranks
-    rule; rank 0 prints the result line."""
+    rule; rank 0 times the per-shard CPU leg (the oracle, as the sharded GPU run does) and
+    prints the result line with the same workload label and per-rank report as a GPU run."""
     import torch
+    res = cpu_resources()
+    threads = min(4, args.cpu_threads or res["threads"])
     rows = min(args.rows, 200_000)
     keys = np.arange(rows * world, dtype=np.uint64)
+    t0 = time.time()
     mine = keys[murmur64a_u64(keys) % np.uint64(world) == np.uint64(rank)]
+    t_owned = time.time() - t0
+    t0 = time.time()
     tab = stage.Table(key_width=8)
     loaded = tab.load_keys(mine, 8, 0)
+    t_load = time.time() - t0
     probes = stage.zipf_draws(rows * world - 1, args.theta, args.seed + rank, 1 << 14, nthreads=2)
     dest = (murmur64a_u64(probes) % np.uint64(world)).astype(np.int64)
     dist.barrier()
@@ -202,21 +209,61 @@ def dry_run(args, rank, world, dist):
     ok = bool((murmur64a_u64(got) % np.uint64(world) == np.uint64(rank)).all())
     tt = torch.tensor([elapsed], dtype=torch.float64)
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-    counts = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
-    dist.all_gather(counts, torch.tensor([rank, loaded], dtype=torch.int64))
-    oks = torch.tensor([int(ok)], dtype=torch.int64)
-    dist.all_reduce(oks, op=dist.ReduceOp.MIN)
+    mine_report = rank_report(rank, loaded, {"owned_keys": t_owned, "load": t_load}, ok)
+    reports = [torch.zeros(len(mine_report), dtype=torch.float64) for _ in range(world)]
+    dist.all_gather(reports, torch.tensor(mine_report, dtype=torch.float64))
+    dist.barrier()
     if rank == 0:
+        per_rank = per_rank_reports(np.stack([r.numpy() for r in reports]))
+        cpu = cpu_leg_sharded(args, res, world, threads, rows, rows, None)
         total = float(tt.item())
         print(json.dumps({"metric": METRIC, "value": round(probes.size * args.steps * world / total, 1),
                           "unit": "routed keys/s (dry run, no GPU)", "n_gpus": world, "steps": args.steps,
                           "warmup": 0, "ms_per_step": round(total / args.steps * 1e3, 4), "higher_is_better": True,
                           "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
-                          "dry_run": True, "ranks": [int(c[0]) for c in counts],
-                          "rows_per_rank": [int(c[1]) for c in counts], "self_check": bool(oks.item()),
-                          "config": {"workload": WORKLOADS["c5"] + " (control plane rehearsal)",
-                                     "parallelism": f"hash-shard x{world}"}}), flush=True)
-    return 0 if oks.item() else 1
+                          "dry_run": True, "ranks": [p["rank"] for p in per_rank],
+                          "rows_per_rank": [p["rows"] for p in per_rank], "per_rank": per_rank,
+                          "self_check": all(p["self_check"] for p in per_rank),
+                          "config": {"workload": sharded_workload(world, rows), "rows_per_gpu": rows,
+                                     "rows_total": rows * world, "parallelism": f"hash-shard x{world}",
+                                     "control_plane": "gloo (dry run)"},
+                          "cpu_baseline": cpu}), flush=True)
+    return 0
+
+
+RANK_REPORT = ("rank", "rows", "owned_keys_s", "load_s", "sync_s", "comm_init_s", "host_peak_rss_gib", "self_check")
+
+
+def rank_report(rank, rows, setup, ok):
+    """one rank's setup phases, peak host RSS and self-check as a float vector (gathered over ranks)"""
+    rss = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20
+    return [float(rank), float(rows), setup.get("owned_keys", 0.0), setup.get("load", 0.0), setup.get("sync", 0.0),
+            setup.get("comm_init", 0.0), rss, 1.0 if ok else 0.0]
+
+
+def per_rank_reports(mat):
+    out = []
+    for row in mat:
+        d = dict(zip(RANK_REPORT, (float(x) for x in row)))
+        out.append({"rank": int(d["rank"]), "rows": int(d["rows"]), "self_check": d["self_check"] > 0.5,
+                    "host_peak_rss_gib": round(d["host_peak_rss_gib"], 2),
+                    "setup_s": {k[:-2]: round(d[k], 2) for k in ("owned_keys_s", "load_s", "sync_s", "comm_init_s")}})
+    return out
+
+
+def cpu_leg_sharded(args, res, world, threads, cpu_rows, gpu_rows, c2_check):
+    """The CPU baseline of a sharded line (C2's per-shard CPU number): rank 0
+    builds the oracle table (LoadYCSBRows, the largest that fits beside the world's device tables
+    on this node, <= one shard's rows) after the GPU timing and times C2's lookup and full-txn
+    modes on it; GPU samples with keys inside the oracle's range are checked against it."""
+    if args.no_cpu_baseline:
+        return None
+    orc = CpuOracle(cpu_rows, threads)
+    legs = cpu_legs(orc, args, res, threads, c2_check=c2_check, legs=("c2",))
+    c2 = legs["c2"]
+    c2["scope"] = (f"per shard: one rank's share of the work on {cpu_rows} rows (a shard holds {gpu_rows}); "
+                   f"compare with the line's value / n_gpus")
+    return c2
 
 
 def owned_keys(total_rows, world, rank):
@@ -228,6 +275,206 @@ def owned_keys(total_rows, world, rank):
         h = stage.murmur64a_device(k, 8, 0)
         parts.append(k[(h % np.uint64(world)) == np.uint64(rank)])
     return np.concatenate(parts)
+
+
+class RcclControl:
+    """Control plane of the GPU ranks over their own RCCL communicator (no second collective
+    library in the process): the 128-byte unique id goes from rank 0 to the others through a
+    file on the node (the ranks of one torch.distributed.run share a parent and a /tmp), then
+    barrier / max-over-ranks / gather are small allreduces on the communicator."""
+
+    def __init__(self, tab, rank, world):
+        self.tab, self.rank, self.world = tab, rank, world
+        L = stage.lib()
+        tag = f"{os.environ.get('MASTER_ADDR', '127.0.0.1')}_{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}"
+        self.path = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"stage_rccl_uid_{tag}.bin")
+        uid = (ctypes.c_uint8 * 128)()
+        if rank == 0:
+            check(L.stage_comm_unique_id(uid), "unique id")
+            tmp = f"{self.path}.{os.getpid()}.tmp"
+            with open(tmp, "wb") as f:
+                f.write(bytes(uid))
+            os.replace(tmp, self.path)
+        else:
+            deadline = time.time() + 600
+            while True:
+                try:
+                    with open(self.path, "rb") as f:
+                        b = f.read()
+                    if len(b) == 128:
+                        break
+                except OSError:
+                    pass
+                if time.time() > deadline:
+                    raise RuntimeError(f"rank {rank}: no RCCL unique id from rank 0 at {self.path}")
+                time.sleep(0.05)
+            uid = (ctypes.c_uint8 * 128).from_buffer_copy(b)
+        check(L.stage_comm_init(tab.h, uid, rank, world), "comm init")
+
+    def barrier(self):
+        stage.comm_allreduce(self.tab, [1.0])
+
+    def max(self, x):
+        return float(stage.comm_allreduce(self.tab, [x], "max")[0])
+
+    def gather(self, vec):
+        return stage.comm_allgather(self.tab, vec, self.world)
+
+    def close(self):
+        if self.rank == 0:
+            try:
+                os.remove(self.path)
+            except OSError:
+                pass
+        check(stage.lib().stage_comm_destroy(self.tab.h), "comm destroy")
+
+
+def run_sharded(args, rank, world, local):
+    """configs[4] (C5) and its 1/2/4 smaller points: every rank holds the keys with
+    MurmurHash64A(key, 8, 0) % world == rank (rows_per_gpu each, weak scaling), originates its own
+    2^24 Zipf-0.9 lookups over all world x rows keys, and stage_probe_sharded answers them in its
+    order over RCCL.  This process loads no other HIP runtime or RCCL than libstage_hip's (no
+    torch: the control plane is the communicator itself, RcclControl)."""
+    res = cpu_resources()
+    nthreads = args.cpu_threads or res["threads"]
+    L = stage.lib()
+    rccl = stage.rccl_info()
+    check(L.stage_set_device(local), "set device")
+    total_rows = args.rows * world
+    # the CPU leg's table size is fixed before the ranks' host tables exist (MemAvailable then
+    # still holds them), for all `world` tables of this node
+    cpu_rows = cpu_rows_for(args, res, args.rows, world) if rank == 0 and not args.no_cpu_baseline else 0
+    setup = {}
+    t0 = time.time()
+    keys = owned_keys(total_rows, world, rank)
+    setup["owned_keys"] = time.time() - t0
+    t0 = time.time()
+    tab = stage.Table(key_width=8, device=local)
+    loaded = tab.load_keys(keys, 8, mode=0)
+    del keys
+    setup["load"] = time.time() - t0
+    t0 = time.time()
+    tab.sync()
+    setup["sync"] = time.time() - t0
+    log(f"[rank {rank}] loaded {loaded} rows: owned_keys {setup['owned_keys']:.1f}s load {setup['load']:.1f}s "
+        f"sync {setup['sync']:.1f}s; RCCL {rccl}")
+    t0 = time.time()
+    ctl = RcclControl(tab, rank, world)
+    setup["comm_init"] = time.time() - t0
+    # every key is < world x rows: the coalescing sorts read only those bits (same results)
+    stage.set_shard_key_bits(tab, max(1, int(total_rows - 1).bit_length()))
+
+    B = args.batch
+    stream = stage.Stream()
+    draws = stage.zipf_draws(total_rows - 1, args.theta, args.seed + rank, B, nthreads=nthreads)
+    d_keys = stage.DeviceBuffer(B * 8)
+    check(L.stage_memcpy_h2d(d_keys.ptr, draws.ctypes.data, draws.nbytes, None), "h2d")
+    d_out = stage.DeviceBuffer(B * 32)
+    d_rec = stage.DeviceBuffer(B * tab.stride)
+
+    def step(reply=stage.REPLY_ROWS):
+        check(L.stage_probe_sharded_ex(tab.h, d_keys.ptr, None, B, d_out.ptr,
+                                       d_rec.ptr if reply == stage.REPLY_ROWS else None, reply, stream.ptr), "sharded")
+
+    for _ in range(args.warmup):
+        step()
+    stream.sync()
+    check(L.stage_device_sync(), "sync")
+    ctl.barrier()
+    evs = [stage.Event() for _ in range(2 * args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        evs[2 * i].record(stream)
+        step()
+        evs[2 * i + 1].record(stream)
+    stream.sync()
+    check(L.stage_device_sync(), "sync")
+    elapsed = time.perf_counter() - t0
+    ctl.barrier()
+    elapsed = ctl.max(elapsed)
+    kern_ms = float(np.mean([evs[2 * i].elapsed_ms(evs[2 * i + 1]) for i in range(args.steps)]))
+    st = stage.sharded_stats_ex(tab)
+    # the same steps with STAGE_REPLY_OWNER: rows stay in the owner's HBM, only the 32-B status
+    # records return -- the HBM-side scaling without the xGMI tuple return
+    for _ in range(max(1, args.warmup)):
+        step(stage.REPLY_OWNER)
+    stream.sync()
+    ctl.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(stage.REPLY_OWNER)
+    stream.sync()
+    t_own = ctl.max(time.perf_counter() - t0)
+    owner = {"value": round(B * args.steps * world / t_own, 1), "ms_per_step": round(t_own / args.steps * 1e3, 4),
+             "reply": "32-B status records to the caller, tuple rows materialised on the owner"}
+    step()  # full reply again, so the self-check reads full rows
+    stream.sync()
+    # self-check: 8 windows of 8192 lookups spread over the batch (every exchange chunk), each
+    # against its key's LoadYCSBRows row
+    sample = min(B, 8192)
+    outs_w, rows_w, keys_w = [], [], []
+    for w in range(8 if B > 8 * sample else 1):
+        o = (B - sample) * w // 7 if B > 8 * sample else 0
+        outs_w.append(d_out.to_numpy(stage.PROBE_OUT_DTYPE, sample, offset=o * 32))
+        rows_w.append(d_rec.to_numpy(np.uint8, sample * tab.stride, offset=o * tab.stride).reshape(sample, tab.stride))
+        keys_w.append(draws[o:o + sample])
+    outs, rows, kw = np.concatenate(outs_w), np.concatenate(rows_w), np.concatenate(keys_w)
+    ok = bool((outs["status"] == stage.ST_LATEST).all() and
+              (rows[:, :8].copy().view(np.uint64).ravel() == kw).all() and
+              (rows[:, 8:1008] == (kw & np.uint64(0xFF)).astype(np.uint8)[:, None]).all())
+    c2_check = (draws[:4096].copy(), outs_w[0]["status"][:4096].copy(), rows_w[0][:4096].copy())
+    reports = ctl.gather(rank_report(rank, loaded, setup, ok) + [float(st[k]) for k in
+                                                                   ("keys", "routed", "remote", "received")])
+    for b in (d_keys, d_out, d_rec):
+        b.free()
+    ctl.barrier()
+    ctl.close()
+    if rank != 0:
+        return 0 if ok else 1
+    per_rank = per_rank_reports(reports[:, :len(RANK_REPORT)])
+    stats = [dict(zip(("keys", "routed", "remote", "received"), (int(x) for x in r[len(RANK_REPORT):])))
+             for r in reports]
+    for p, sx in zip(per_rank, stats):
+        p["requests"] = sx
+    step_s = elapsed / args.steps
+    # HBM roofline of the step: the bytes that move on each rank (owners' probes, caller rows,
+    # result copies), the busiest rank over the step time
+    hb = [sharded_hbm_bytes(sx, tab.stride) for sx in stats]
+    hmax = max(b for b, _ in hb)
+    hbm = {"bound": "hbm", "achieved": round(hmax / step_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(hmax / step_s / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+           "kernel": "sharded step: owners' probes (fan-out for own requests) + result returns + fan-out copies",
+           "algorithmic_bytes_per_launch": hmax, "bytes_by_part_rank0": hb[0][1],
+           "avg_launch_ms": round(step_s * 1e3, 4), "event_ms_per_step_rank0": round(kern_ms, 4),
+           "algorithmic_bytes": "bench.sharded_hbm_bytes (per rank, what moves)"}
+    if world > 1:
+        roof = xgmi_roofline(B, world, tab.stride, step_s, hbm, remote=max(sx["remote"] for sx in stats))
+    else:
+        roof = hbm
+    cpu = cpu_leg_sharded(args, res, world, nthreads, cpu_rows, args.rows, c2_check)
+    routed = sum(sx["routed"] for sx in stats)
+    result = {
+        "metric": METRIC, "value": round(B * args.steps * world / elapsed, 1), "unit": "ops/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic (LoadYCSBRows keys/payloads)",
+        "config": {"workload": sharded_workload(world, args.rows), "theta": args.theta, "traversal": "device",
+                   "rows_per_gpu": args.rows, "rows_total": total_rows, "batch_per_gpu": B, "key_bytes": 8,
+                   "payload_bytes": 1000, "leaf_bytes": 65536, "parallelism": f"hash-shard x{world}",
+                   "exchange_chunks": int(os.environ.get("STAGE_SHARD_CHUNKS", 4 if world > 1 else 1)),
+                   "control_plane": "the RCCL communicator (file rendezvous of the unique id)"},
+        "roofline": roof, "cpu_baseline": cpu, "self_check": all(p["self_check"] for p in per_rank),
+        "owner_reply": owner,
+        "coalescing": {"keys": sum(sx["keys"] for sx in stats), "requests_routed": routed,
+                       "remote_requests": sum(sx["remote"] for sx in stats),
+                       "routed_share": round(routed / max(1, sum(sx["keys"] for sx in stats)), 4),
+                       "note": "equal keys of an exchange chunk travel and are probed once; own requests are "
+                               "probed straight into their caller positions (fan-out probe)"},
+        "rccl": rccl, "per_rank": per_rank,
+        "setup_s": {k: round(max(p["setup_s"][k] for p in per_rank), 2) for k in per_rank[0]["setup_s"]},
+        "host_peak_rss_gib": max(p["host_peak_rss_gib"] for p in per_rank),
+    }
+    print(json.dumps(result), flush=True)
+    return 0 if result["self_check"] else 1
 
 
 def traffic_from_profile(batch, rows, name="pmc_probe.json"):
@@ -285,11 +532,12 @@ def cpu_resources():
             "_avail": min(x for x in (mem.get("MemAvailable", 0), cg_mem, 250 * 2**30) if x)}
 
 
-def cpu_rows_for(args, res, gpu_rows):
-    """Largest oracle table (rows) that fits beside the GPU leg's host memory, <= the GPU's N."""
+def cpu_rows_for(args, res, gpu_rows, world=1):
+    """Largest oracle table (rows) that fits beside the host memory of the `world` ranks' device
+    tables on this node, <= one GPU's N."""
     if args.cpu_rows:
         return args.cpu_rows
-    budget = res["_avail"] - 24 * 2**30 - gpu_rows * GPU_HOST_BYTES_PER_ROW
+    budget = res["_avail"] - 24 * 2**30 - world * gpu_rows * GPU_HOST_BYTES_PER_ROW
     fit = int(budget // ORACLE_BYTES_PER_ROW) // 1_000_000 * 1_000_000
     return max(1_000_000, min(gpu_rows, fit))
 
@@ -311,6 +559,44 @@ def xgmi_roofline(batch, world, stride, step_s, hbm_roof, remote=None):
             "avg_launch_ms": round(step_s * 1e3, 4),
             "peak_source": f"{XGMI_LINK_GBS:.0f} GB/s per xGMI link (7 per MI355X), {world - 1} links per rank",
             "hbm": hbm_roof}
+
+
+def fmt_rows(n):
+    """100000000 -> '100M' (the BASELINE.json spelling of row counts)"""
+    for div, suf in ((10**9, "B"), (10**6, "M"), (10**3, "K")):
+        if n % div == 0:
+            return f"{n // div}{suf}"
+    return str(n)
+
+
+def sharded_workload(world, rows_per_gpu):
+    """config.workload of a sharded run, naming its real world size and rows: at 8 ranks of
+    100M rows this is BASELINE.json configs[4] verbatim; any other world / size names itself."""
+    s = (f"YCSB-C {fmt_rows(world * rows_per_gpu)} rows sharded {world} way{'s' if world != 1 else ''}, "
+         f"RCCL all-to-all key routing over xGMI, {world}×MI355X")
+    if world == 1:
+        s += " (one-rank rehearsal of the multi-GPU path, --force-sharded)"
+    return s
+
+
+def sharded_hbm_bytes(st, stride, row_bytes=1008):
+    """Algorithmic HBM bytes of one sharded step on one rank, counting what actually moves
+    (stage_sharded_stats_ex after the step: n caller keys, `routed` requests after coalescing,
+    `remote` of them owned by other ranks, `received` requests this rank probed as owner):
+      owner probes      received x (8 key + 64 fingerprint line + 16 slot word + 1000 payload)
+      caller rows       n x (row_bytes + 4): every caller position's row + status (as C2)
+      remote results    (received - own) x 2 x (row_bytes + 4): written for the return, read by RCCL
+      returned results  remote x 2 x (row_bytes + 4): written by RCCL, read by the fan-out
+      key records       (remote + received - own) x 2 x 16: sent (read) and received (written)
+    The coalescing sorts and the routing's own scratch traffic are not counted (not algorithmic)."""
+    n, routed, remote, received = st["keys"], st["routed"], st["remote"], st["received"]
+    own = routed - remote
+    recv_remote = received - own
+    out = row_bytes + 4
+    parts = {"owner_probes": received * (8 + 64 + 16 + 1000), "caller_rows": n * out,
+             "remote_results": recv_remote * 2 * out, "returned_results": remote * 2 * out,
+             "key_records": (remote + recv_remote) * 32}
+    return sum(parts.values()), parts
 
 
 def hbm_roofline(per_unit, units_per_launch, kern_ms, kernel, traffic=None, tsrc=None):
@@ -391,16 +677,18 @@ class YcsbB:
                                                             stream.ptr if stream is not None else None),
                       "update_batch_device")
             return ok.value
+        # host write path: LeafNode::Update + commit on the host table, then the incremental
+        # publish of the touched leaves (stage_update_batch + stage_sync)
+        cols = np.repeat(ep["colb"][:, None], 100, 1)
+        _, ok = self.tab.update_batch(ep["keys"], 0, cols, ep["rid"], ep["cid"])
+        self.tab.sync()
+        return ok
 
     @staticmethod
     def count_ok(ep):
         """successful updates of an epoch applied on the device (return code RC_OK)"""
         m = ep["keys"].size
         return int((ep["d"]["rc"].to_numpy(np.uint8, m) == stage.RC_OK).sum()) if m else 0
-        cols = np.repeat(ep["colb"][:, None], 100, 1)
-        _, ok = self.tab.update_batch(ep["keys"], 0, cols, ep["rid"], ep["cid"])
-        self.tab.sync()
-        return ok
 
     def release(self, ep):
         for b in ep.pop("d", {}).values():
@@ -469,7 +757,7 @@ def cpu_calibration(O, threads):
                     "is faster on this host; BASELINE.md §3 has the same-host ratios"}
 
 
-def cpu_legs(orc, args, res, threads, c2_check=None, c4_check=None, c3=None):
+def cpu_legs(orc, args, res, threads, c2_check=None, c4_check=None, c3=None, legs=("c2", "c4", "c3")):
     """Times the oracle on the GPU box's host cores: C2 lookup mode + full-txn mode, C4 scans,
     C3 reads on the replayed epochs' snapshot with the GPU's read ids; checks GPU samples
     against it (the oracle is the checker).  Returns {leg: cpu_baseline dict}."""
@@ -508,12 +796,20 @@ def cpu_legs(orc, args, res, threads, c2_check=None, c4_check=None, c3=None):
                            "equal": bool((o_out["status"] == st[sel]).all() and
                                          (rows[sel][:, :tree.row] == o_rec).all())}
     out["c2"] = c2
+    if "c4" not in legs:
+        return out
     # C4, scan mode (TableScanExecutor over RangeScanBySize/Iterator)
-    starts = (stage.fastrandom(args.seed, 20_000) % np.uint64(n)).astype(np.uint64)
-    L.orc_scan_batch_timed(tree.t, starts.ctypes.data, 8, starts.size, args.scan_size, threads, ctypes.byref(secs))
-    count = cpu_sample_count(starts.size / max(secs.value, 1e-9), args.cpu_seconds * 0.6, 10_000, 5_000_000)
-    starts = (stage.fastrandom(args.seed + 1, count) % np.uint64(n)).astype(np.uint64)
-    L.orc_scan_batch_timed(tree.t, starts.ctypes.data, 8, starts.size, args.scan_size, threads, ctypes.byref(secs))
+    # the first short sample runs cold (its rate underestimates the steady one), so the sample
+    # is re-sized until it lasts at least 0.6 of its target time
+    target = args.cpu_seconds * 0.6
+    count = 20_000
+    for attempt in range(4):
+        starts = (stage.fastrandom(args.seed + attempt, count) % np.uint64(n)).astype(np.uint64)
+        L.orc_scan_batch_timed(tree.t, starts.ctypes.data, 8, starts.size, args.scan_size, threads, ctypes.byref(secs))
+        if attempt and (secs.value >= 0.6 * target or count >= 20_000_000):
+            break
+        count = cpu_sample_count(count / max(secs.value, 1e-9), target, 10_000, 20_000_000)
+    count = starts.size
     c4 = {"value": round(count / secs.value, 1), "unit": "scans/s", "mode": "scan", **common,
           "sample": f"oracle TableScanExecutor over Iterator, {count} scans of {args.scan_size} over {n} rows, "
                     f"{threads} threads, {secs.value:.1f}s"}
@@ -884,6 +1180,9 @@ def c3_leg(tab, args, stream, nthreads, steps, warmup):
             elapsed += time.perf_counter() - tr
         ops_done += ep["reads"].size
     stream.sync()
+    # the last epoch's host adoption (a background thread of the device write path) is part of
+    # the write work: settle it before the loop's clock stops
+    check(L.stage_settle(tab.h), "settle")
     loop_s = time.perf_counter() - t_loop
     probe_ms = [evs[2 * i].elapsed_ms(evs[2 * i + 1]) for i in range(steps)]
     if device_wp:  # the probes' device time (start event -> end event on the stream)
@@ -951,36 +1250,30 @@ def main(argv=None):
         return run_tpcc(args)
     if args.config == "chq2":
         return run_chq2(args)
-    dist = None
     sharded = world > 1 or args.force_sharded
-    if sharded or args.dry_run:
-        import torch.distributed as tdist
-        tdist.init_process_group("gloo")  # control plane only; the data path is RCCL in the library
-        dist = tdist
-        if args.config != "c2":
-            raise SystemExit("multi-GPU runs use the point-lookup config (c2 -> configs[4])")
+    if (sharded or args.dry_run) and args.config != "c2":
+        raise SystemExit("multi-GPU runs use the point-lookup config (c2 -> configs[4])")
     if args.dry_run:
+        import torch.distributed as tdist
+        tdist.init_process_group("gloo")  # CPU rehearsal of the control plane only
         try:
-            return dry_run(args, rank, world, dist)
+            return dry_run(args, rank, world, tdist)
         finally:
-            dist.destroy_process_group()
+            tdist.destroy_process_group()
+    if sharded:
+        return run_sharded(args, rank, world, local)
     res = cpu_resources()
     nthreads = args.cpu_threads or res["threads"]
     check(stage.lib().stage_set_device(local), "set device")
 
-    total_rows = args.rows * world
+    total_rows = args.rows
     orc = None
-    cpu_leg = rank == 0 and not sharded and not args.no_cpu_baseline
+    cpu_leg = not args.no_cpu_baseline
     if cpu_leg:  # the oracle table builds on the host while the GPU leg runs
         orc = CpuOracle(cpu_rows_for(args, res, args.rows), nthreads)
     t0 = time.time()
     tab = stage.Table(key_width=8, device=local)
-    if not sharded:
-        loaded = tab.load_ycsb(0, total_rows, 8, mode=0)
-    else:
-        keys = owned_keys(total_rows, world, rank)
-        loaded = tab.load_keys(keys, 8, mode=0)
-        del keys
+    loaded = tab.load_ycsb(0, total_rows, 8, mode=0)
     t_load = time.time() - t0
     t0 = time.time()
     tab.sync()
@@ -998,37 +1291,23 @@ def main(argv=None):
         head, samples["c3"] = c3_leg(tab, args, stream, nthreads, args.steps, args.warmup)
     else:
         head = None
-    owner = None
-    if head is None:  # C2 (or C5 when sharded): the headline
+    if head is None:  # C2: the headline
         draws = stage.zipf_draws(total_rows - 1, args.theta, args.seed + rank, B, nthreads=nthreads)
         d_keys = stage.DeviceBuffer(B * 8)
         check(L.stage_memcpy_h2d(d_keys.ptr, draws.ctypes.data, draws.nbytes, None), "h2d")
         d_out = stage.DeviceBuffer(B * 32)
         d_rec = stage.DeviceBuffer(B * tab.stride)
         d_leaf = None
-        if args.host_traversal and not sharded:
+        if args.host_traversal:
             d_leaf = stage.DeviceBuffer.from_numpy(tab.traverse(draws))
-        if sharded:
-            uid = (ctypes.c_uint8 * 128)()
-            if rank == 0:
-                check(L.stage_comm_unique_id(uid), "unique id")
-            obj = [bytes(uid)]
-            dist.broadcast_object_list(obj, src=0)
-            uid = (ctypes.c_uint8 * 128).from_buffer_copy(obj[0])
-            check(L.stage_comm_init(tab.h, uid, rank, world), "comm init")
 
         def step():
-            if not sharded:
-                tab.probe_device(d_keys.ptr, B, d_out.ptr, d_rec.ptr,
-                                 d_leaf_ids=d_leaf.ptr if d_leaf else None, stream=stream.ptr)
-            else:
-                check(L.stage_probe_sharded(tab.h, d_keys.ptr, None, B, d_out.ptr, d_rec.ptr, stream.ptr), "sharded")
+            tab.probe_device(d_keys.ptr, B, d_out.ptr, d_rec.ptr, d_leaf_ids=d_leaf.ptr if d_leaf else None,
+                             stream=stream.ptr)
 
         for _ in range(args.warmup):
             step()
         stream.sync()
-        if dist:
-            dist.barrier()
         check(L.stage_device_sync(), "sync")
         evs = [stage.Event() for _ in range(2 * args.steps)]
         t0 = time.perf_counter()
@@ -1039,37 +1318,9 @@ def main(argv=None):
         stream.sync()
         check(L.stage_device_sync(), "sync")
         elapsed = time.perf_counter() - t0
-        if dist:
-            dist.barrier()
-            import torch
-            tt = torch.tensor([elapsed], dtype=torch.float64)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            elapsed = float(tt.item())
-            # the same steps with STAGE_REPLY_OWNER: rows stay in the owner's HBM, only the 32-B
-            # status records return -- the HBM-side scaling without the xGMI tuple return
-            for _ in range(max(1, args.warmup)):
-                check(L.stage_probe_sharded_ex(tab.h, d_keys.ptr, None, B, d_out.ptr, None, stage.REPLY_OWNER,
-                                               stream.ptr), "sharded owner")
-            stream.sync()
-            dist.barrier()
-            t0 = time.perf_counter()
-            for _ in range(args.steps):
-                check(L.stage_probe_sharded_ex(tab.h, d_keys.ptr, None, B, d_out.ptr, None, stage.REPLY_OWNER,
-                                               stream.ptr), "sharded owner")
-            stream.sync()
-            t_own = time.perf_counter() - t0
-            tt = torch.tensor([t_own], dtype=torch.float64)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            t_own = float(tt.item())
-            owner = {"value": round(B * args.steps * world / t_own, 1),
-                     "ms_per_step": round(t_own / args.steps * 1e3, 4),
-                     "reply": "32-B status records to the caller, tuple rows materialised on the owner"}
-            # rerun the full-reply step once so the self-check reads full rows
-            step()
-            stream.sync()
         kern_ms = float(np.mean([evs[2 * i].elapsed_ms(evs[2 * i + 1]) for i in range(args.steps)]))
-        # self-check: 8 windows of 8192 lookups spread over the batch (every exchange chunk of
-        # the sharded path), each against its key's LoadYCSBRows row
+        # self-check: 8 windows of 8192 lookups spread over the batch, each against its key's
+        # LoadYCSBRows row
         sample = min(B, 8192)
         outs_w, rows_w, keys_w = [], [], []
         for w in range(8 if B > 8 * sample else 1):
@@ -1082,63 +1333,45 @@ def main(argv=None):
                   (rows[:, :8].copy().view(np.uint64).ravel() == kw).all() and
                   (rows[:, 8:1008] == (kw & np.uint64(0xFF)).astype(np.uint8)[:, None]).all())
         samples["c2"] = (draws[:4096].copy(), outs_w[0]["status"][:4096].copy(), rows_w[0][:4096].copy())
-        traffic, tsrc = (None, None) if sharded else traffic_from_profile(B, args.rows, "pmc_probe.json")
-        roof = hbm_roofline(BYTES_PER_LOOKUP, B, kern_ms,
-                            "probe_kernel" if not sharded else "sharded step (route + RCCL + probe_kernel)",
-                            traffic, tsrc)
-        coalesce = None
-        if sharded:
-            nk, routed, remote = stage.sharded_stats(tab, loopback=False)
-            coalesce = {"keys": nk, "requests_routed": routed, "remote_requests": remote,
-                        "routed_share": round(routed / max(nk, 1), 4),
-                        "note": "equal keys of an exchange chunk travel and are probed once (stage_set_shard_dedupe)"}
-        if sharded and world > 1:
-            roof = xgmi_roofline(B, world, tab.stride, elapsed / args.steps, roof, remote=coalesce["remote_requests"])
-        head = {"value": round(B * args.steps * world / elapsed, 1), "unit": "ops/s",
+        traffic, tsrc = traffic_from_profile(B, args.rows, "pmc_probe.json")
+        roof = hbm_roofline(BYTES_PER_LOOKUP, B, kern_ms, "probe_kernel", traffic, tsrc)
+        roof["timing_note"] = ("achieved uses this run's hipEvent time of the probe; traffic comes from a separate "
+                               "rocprofv3 --pmc pass (traffic_source), whose box and kernel time can differ by a few %")
+        head = {"value": round(B * args.steps / elapsed, 1), "unit": "ops/s",
                 "ms_per_step": round(elapsed / args.steps * 1e3, 4), "self_check": ok, "roofline": roof,
-                "coalescing": coalesce,
-                "config": {"workload": WORKLOADS["c2"] if not sharded else WORKLOADS["c5"], "theta": args.theta,
+                "config": {"workload": WORKLOADS["c2"], "theta": args.theta,
                            "traversal": "host" if d_leaf else "device"}}
         for b in (d_keys, d_out, d_rec) + ((d_leaf,) if d_leaf else ()):
             b.free()
-        if not sharded and not args.no_extras:
+        if not args.no_extras:
             # the other single-GPU configs on the same loaded table: C4, then C3 (mutates it)
             extras["c4"], samples["c4"] = c4_leg(tab, args, total_rows, rank, stream, 5, 1)
             extras["c3"], samples["c3"] = c3_leg(tab, args, stream, nthreads, args.c3_epochs, 1)
     if not head["self_check"]:
         log(f"[rank {rank}] SELF-CHECK FAILED")
 
-    if rank == 0:
-        cpu = None
-        if cpu_leg:
-            legs = cpu_legs(orc, args, res, nthreads, c2_check=samples.get("c2"), c4_check=samples.get("c4"),
-                            c3=samples.get("c3"))
-            legs["c2"]["calibration"] = cpu_calibration(orc.O, nthreads)
-            key = args.config
-            cpu = legs[key]
-            for k, v in extras.items():
-                v["cpu_baseline"] = legs.get(k)
-        config = {**head["config"], "rows_per_gpu": args.rows, "rows_total": total_rows,
-                  "batch_per_gpu": B if args.config != "c4" else args.batch, "key_bytes": 8, "payload_bytes": 1000,
-                  "leaf_bytes": 65536, "parallelism": f"hash-shard x{world}"}
-        result = {
-            "metric": METRIC, "value": head["value"], "unit": head["unit"], "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": head["ms_per_step"], "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic (LoadYCSBRows keys/payloads)",
-            "config": config, "roofline": head["roofline"], "cpu_baseline": cpu, "self_check": head["self_check"],
-            **({"ops_per_s_incl_writes": head["ops_per_s_incl_writes"]} if "ops_per_s_incl_writes" in head else {}),
-            **({"owner_reply": owner} if owner else {}),
-            **({"coalescing": head["coalescing"]} if head.get("coalescing") else {}),
-            **({"extras": extras} if extras else {}),
-            "setup_s": {"load": round(t_load, 1), "sync": round(t_sync, 1)},
-            "host_peak_rss_gib": round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20, 1),
-        }
-        print(json.dumps(result), flush=True)
-    if dist:
-        dist.barrier()
-        if sharded:
-            check(L.stage_comm_destroy(tab.h), "comm destroy")
-        dist.destroy_process_group()
+    cpu = None
+    if cpu_leg:
+        legs = cpu_legs(orc, args, res, nthreads, c2_check=samples.get("c2"), c4_check=samples.get("c4"),
+                        c3=samples.get("c3"))
+        legs["c2"]["calibration"] = cpu_calibration(orc.O, nthreads)
+        cpu = legs[args.config]
+        for k, v in extras.items():
+            v["cpu_baseline"] = legs.get(k)
+    config = {**head["config"], "rows_per_gpu": args.rows, "rows_total": total_rows,
+              "batch_per_gpu": B if args.config != "c4" else args.batch, "key_bytes": 8, "payload_bytes": 1000,
+              "leaf_bytes": 65536, "parallelism": "single GPU"}
+    result = {
+        "metric": METRIC, "value": head["value"], "unit": head["unit"], "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": head["ms_per_step"], "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic (LoadYCSBRows keys/payloads)",
+        "config": config, "roofline": head["roofline"], "cpu_baseline": cpu, "self_check": head["self_check"],
+        **({"ops_per_s_incl_writes": head["ops_per_s_incl_writes"]} if "ops_per_s_incl_writes" in head else {}),
+        **({"extras": extras} if extras else {}),
+        "setup_s": {"load": round(t_load, 1), "sync": round(t_sync, 1)},
+        "host_peak_rss_gib": round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20, 1),
+    }
+    print(json.dumps(result), flush=True)
     ok = head["self_check"] and all(v["self_check"] for v in extras.values())
     return 0 if ok else 1
 

@@ -150,6 +150,9 @@ int stage_update_batch_device(stage_table *t, const uint64_t *d_keys, const uint
                               uint32_t payload_off, const uint8_t *d_deltas, uint32_t delta_len,
                               const uint32_t *d_writer_ids, const uint32_t *d_commit_ids,
                               const uint32_t *d_sstamps, uint8_t *d_rc, uint64_t *n_ok, void *stream);
+/* waits for the host table's adoption of the last stage_update_batch_device epoch (it runs on a
+ * background thread; every host-table entry point waits for it anyway) and reports its error */
+int stage_settle(stage_table *t);
 
 /* byte-key forms, for every key width a table takes: 1..8 bytes (key_width 1..8 or 0 =
  * variable) or a fixed width of 9..32 bytes (TPC-C composite keys, tpcc_record.h: int64
@@ -393,7 +396,7 @@ int stage_ch_query2_batch(stage_table *region, stage_table *nation, stage_table 
  * caller's order (all-to-all-v out, local probe, all-to-all-v back). */
 int stage_comm_unique_id(uint8_t *id128);
 /* the sharded batch is exchanged in `chunks` pieces whose result transfers overlap the next
- * piece's probe (0 = STAGE_SHARD_CHUNKS env or 4); set before stage_comm_init, same value on
+ * piece's probe (0 = STAGE_SHARD_CHUNKS env, or 4 -- 1 at world 1); set before stage_comm_init, same value on
  * every rank */
 int stage_set_shard_chunks(stage_table *t, int chunks);
 int stage_comm_init(stage_table *t, const uint8_t *id128, int rank, int world);
@@ -418,9 +421,26 @@ int stage_sharded_owner_rows(stage_table *t, int loopback, uint8_t **d_rows, uin
  * tuple traffic over xGMI shrinks by the batch's duplicate share (about half of a Zipf-0.9
  * batch).  Owner-reply rows are then one per distinct request. */
 int stage_set_shard_dedupe(stage_table *t, int on);
+/* coalescing sorts the chunk's keys on their low `bits` bits (0 or 64 = all; default 64).  Any
+ * value gives the same results -- keys equal in those bits but different above them still form
+ * separate requests -- a caller whose keys are < 2^bits only saves radix passes. */
+int stage_set_shard_key_bits(stage_table *t, int bits);
+/* the RCCL the process runs: ncclGetVersion (e.g. 22707 = 2.27.7), the RCCL header version
+ * libstage_hip was built against, and the file that provided ncclGetVersion.  stage_comm_init
+ * fails (STAGE_E_HIP; stage_last_error names both versions and the file) when the runtime
+ * major.minor differs from the headers, unless STAGE_RCCL_ALLOW_MISMATCH=1. */
+int stage_rccl_info(int *runtime_version, int *header_version, char *path, uint64_t path_len);
 /* the last sharded probe on this rank: caller keys, requests routed after coalescing, and of
  * those the ones owned by other ranks (loopback != 0: the loopback shard state) */
 int stage_sharded_stats(stage_table *t, int loopback, uint64_t *n_keys, uint64_t *n_routed, uint64_t *n_remote);
+/* the same and more: v[0..nv) = {caller keys, requests routed, of those remote, requests this
+ * rank probed as owner (its own + the ones other ranks routed to it)} */
+int stage_sharded_stats_ex(stage_table *t, int loopback, uint64_t *v, int nv);
+/* control plane over the table's communicator, for callers without another one (the bench's
+ * barrier, max-over-ranks timing and per-rank reports): in-place allreduce of n doubles (op 0
+ * sum, 1 max, 2 min) and allgather (out[r * n + i] = rank r's in[i]); both wait for completion */
+int stage_comm_allreduce_f64(stage_table *t, double *values, uint64_t n, int op);
+int stage_comm_allgather_f64(stage_table *t, const double *in, uint64_t n, double *out);
 
 /* single-process rehearsal of stage_probe_sharded: `world` shard tables on ONE device play the
  * ranks; the routing, count exchange, offsets, local probes and un-permutation are the same

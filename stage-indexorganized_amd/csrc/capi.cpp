@@ -233,7 +233,15 @@ int stage_abort_insert_key(stage_table *t, const uint8_t *key, uint16_t key_size
     });
 }
 
-uint32_t stage_key_words(stage_table *t) { return t ? host(t).key_words() : 0; }
+int stage_settle(stage_table *t) {
+    if (!t) return fail(STAGE_E_ARG, "null table");
+    return guarded([&] {
+        t->settle();
+        return STAGE_OK;
+    });
+}
+
+uint32_t stage_key_words(stage_table *t) { return t ? facts(t).key_words() : 0; }
 
 int stage_sync(stage_table *t) {
     if (!t) return fail(STAGE_E_ARG, "null table");
@@ -262,8 +270,8 @@ int stage_stats(stage_table *t, uint64_t *stats) {
     });
 }
 
-uint32_t stage_record_stride(stage_table *t) { return t ? (t->out_stride ? t->out_stride : host(t).stride()) : 0; }
-uint32_t stage_leaf_capacity(stage_table *t) { return t ? host(t).cap() : 0; }
+uint32_t stage_record_stride(stage_table *t) { return t ? (t->out_stride ? t->out_stride : facts(t).stride()) : 0; }
+uint32_t stage_leaf_capacity(stage_table *t) { return t ? facts(t).cap() : 0; }
 
 int stage_traverse_batch(stage_table *t, const uint64_t *keys, const uint16_t *lens, uint64_t n, int le_child,
                          uint32_t *leaf_out) {
@@ -497,12 +505,13 @@ int stage_comm_unique_id(uint8_t *id128) {
 
 int stage_comm_init(stage_table *t, const uint8_t *id128, int rank, int world) {
     if (!t || !id128 || world < 1 || rank < 0 || rank >= world) return fail(STAGE_E_ARG, "bad arguments");
-    if (host(t).key_words() != 1) return fail(STAGE_E_ARG, "the sharded front-end routes keys of <= 8 bytes");
+    if (facts(t).key_words() != 1) return fail(STAGE_E_ARG, "the sharded front-end routes keys of <= 8 bytes");
     return guarded([&] {
         (void)hipSetDevice(t->dev.device);
         t->comm = std::make_unique<stage::ShardComm>();
         const int rc = stage::shard_init(*t->comm, id128, rank, world, t->shard_chunks);
         if (t->shard_dedupe >= 0) t->comm->dedupe = t->shard_dedupe != 0;
+        t->comm->key_bits = t->shard_key_bits;
         return rc;
     });
 }
@@ -516,6 +525,18 @@ int stage_set_shard_dedupe(stage_table *t, int on) {
     return STAGE_OK;
 }
 
+int stage_set_shard_key_bits(stage_table *t, int bits) {
+    if (!t || bits < 0 || bits > 64) return fail(STAGE_E_ARG, "bits must be 0..64");
+    t->shard_key_bits = bits ? bits : 64;
+    if (t->comm) t->comm->key_bits = t->shard_key_bits;
+    if (t->loop_comm) t->loop_comm->key_bits = t->shard_key_bits;
+    return STAGE_OK;
+}
+
+int stage_rccl_info(int *runtime_version, int *header_version, char *path, uint64_t path_len) {
+    return guarded([&] { return stage::shard_rccl_info(runtime_version, header_version, path, path_len); });
+}
+
 int stage_sharded_stats(stage_table *t, int loopback, uint64_t *n_keys, uint64_t *n_routed, uint64_t *n_remote) {
     if (!t || !n_keys || !n_routed || !n_remote) return fail(STAGE_E_ARG, "null argument");
     stage::ShardComm *c = loopback ? t->loop_comm.get() : t->comm.get();
@@ -524,6 +545,33 @@ int stage_sharded_stats(stage_table *t, int loopback, uint64_t *n_keys, uint64_t
     *n_routed = c->last_routed;
     *n_remote = c->last_remote;
     return STAGE_OK;
+}
+
+int stage_sharded_stats_ex(stage_table *t, int loopback, uint64_t *v, int nv) {
+    if (!t || !v || nv < 0) return fail(STAGE_E_ARG, "bad arguments");
+    stage::ShardComm *c = loopback ? t->loop_comm.get() : t->comm.get();
+    if (!c) return fail(STAGE_E_STATE, "no sharded probe has run");
+    const uint64_t all[4] = {c->last_n, c->last_routed, c->last_remote, c->last_received};
+    for (int i = 0; i < nv && i < 4; ++i) v[i] = all[i];
+    return STAGE_OK;
+}
+
+int stage_comm_allreduce_f64(stage_table *t, double *values, uint64_t n, int op) {
+    if (!t || (!values && n) || op < 0 || op > 2) return fail(STAGE_E_ARG, "bad arguments");
+    if (!t->comm) return fail(STAGE_E_STATE, "stage_comm_init first");
+    return guarded([&] {
+        (void)hipSetDevice(t->dev.device);
+        return stage::shard_allreduce_f64(*t->comm, values, n, op);
+    });
+}
+
+int stage_comm_allgather_f64(stage_table *t, const double *in, uint64_t n, double *out) {
+    if (!t || ((!in || !out) && n)) return fail(STAGE_E_ARG, "bad arguments");
+    if (!t->comm) return fail(STAGE_E_STATE, "stage_comm_init first");
+    return guarded([&] {
+        (void)hipSetDevice(t->dev.device);
+        return stage::shard_allgather_f64(*t->comm, in, n, out);
+    });
 }
 
 int stage_set_shard_chunks(stage_table *t, int chunks) {
@@ -584,7 +632,7 @@ int stage_probe_sharded_loopback(stage_table *const *shards, int world, const ui
     for (int r = 0; r < world; ++r) {
         int rc = need_synced(shards[r]);
         if (rc) return rc;
-        if (host(shards[r]).key_words() != 1) return fail(STAGE_E_ARG, "the sharded front-end routes keys of <= 8 bytes");
+        if (facts(shards[r]).key_words() != 1) return fail(STAGE_E_ARG, "the sharded front-end routes keys of <= 8 bytes");
         if (shards[r]->dev.device != shards[0]->dev.device) return fail(STAGE_E_ARG, "shards on different devices");
         if ((d_records[r] == nullptr) != (d_records[0] == nullptr)) return fail(STAGE_E_ARG, "rows for all or none");
     }
@@ -599,13 +647,14 @@ int stage_probe_sharded_loopback(stage_table *const *shards, int world, const ui
         std::vector<uint8_t *> recs(world);
         for (int r = 0; r < world; ++r) {
             stage_table *t = shards[r];
-            const int want = shards[0]->shard_chunks > 0 ? shards[0]->shard_chunks : stage::shard_default_chunks();
+            const int want = shards[0]->shard_chunks > 0 ? shards[0]->shard_chunks : stage::shard_default_chunks(world);
             if (!t->loop_comm || t->loop_comm->world != world || t->loop_comm->rank != r ||
                 t->loop_comm->chunks != want) {
                 t->loop_comm = std::make_unique<stage::ShardComm>();
                 stage::shard_init_loopback(*t->loop_comm, r, world, want);
             }
             if (t->shard_dedupe >= 0) t->loop_comm->dedupe = t->shard_dedupe != 0;
+            t->loop_comm->key_bits = t->shard_key_bits;
             cs[r] = t->loop_comm.get();
             ts[r] = &t->dev.view;
             ks[r] = d_keys[r];

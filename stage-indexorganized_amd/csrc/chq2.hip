@@ -174,11 +174,11 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         return fail(STAGE_E_ARG, "null argument");
     if (target_region < 0 || target_region > 4) return fail(STAGE_E_ARG, "target_region must be 0..4");
     for (stage_table *t : {region, nation, supplier, item})
-        if (host(t).params().key_width != 8) return fail(STAGE_E_ARG, "REGION/NATION/SUPPLIER/ITEM keys are 8 bytes");
-    if (host(stock).params().key_width != 16) return fail(STAGE_E_ARG, "STOCK keys are {w, i}: 16 bytes");
-    if (host(region).params().payload_size < 55 || host(nation).params().payload_size < 8 ||
-        host(supplier).params().payload_size < 8 || host(item).params().payload_size < stage::kIDataOff + 64 ||
-        host(stock).params().payload_size < 16)
+        if (facts(t).params().key_width != 8) return fail(STAGE_E_ARG, "REGION/NATION/SUPPLIER/ITEM keys are 8 bytes");
+    if (facts(stock).params().key_width != 16) return fail(STAGE_E_ARG, "STOCK keys are {w, i}: 16 bytes");
+    if (facts(region).params().payload_size < 55 || facts(nation).params().payload_size < 8 ||
+        facts(supplier).params().payload_size < 8 || facts(item).params().payload_size < stage::kIDataOff + 64 ||
+        facts(stock).params().payload_size < 16)
         return fail(STAGE_E_ARG, "payloads too short for the Q2 columns");
     for (stage_table *t : {region, nation, supplier, item})
         if (t->dev.device != stock->dev.device) return fail(STAGE_E_ARG, "tables on different devices");
@@ -198,7 +198,7 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         const uint64_t nslots = (uint64_t)pv.nleaves * pv.cap;
         uint8_t *pbuf = scratch_bytes(supplier->dev, nslots * 16);
         q2_dump_leaves<<<(unsigned)std::min<uint64_t>((nslots + 255) / 256, 4096), 256, 0, s>>>(
-            pv, host(supplier).key_pad(), (uint64_t *)pbuf);
+            pv, facts(supplier).key_pad(), (uint64_t *)pbuf);
         hip_check(hipGetLastError(), "dump leaves");
         std::vector<uint64_t> pairs(2 * nslots);
         hip_check(hipMemcpyAsync(pairs.data(), pbuf, nslots * 16, hipMemcpyDeviceToHost, s), "d2h");
@@ -266,11 +266,11 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
             hip_check(launch_probe(sv, d_keys, nullptr, d_rids, nullptr, m * nq, d_sout, nullptr, s, stock->tune),
                       "stock probe");
         q2_reduce<<<n * nq, 64, 0, s>>>(d_sout, d_keys, d_dst, d_cnt, d_sup, sv.heap, sv.hstride,
-                                        host(stock).key_pad(), n, m, d_rec, d_ik, d_ab);
+                                        facts(stock).key_pad(), n, m, d_rec, d_ik, d_ab);
         // 3. item lookups of the last stocks, filter
         hip_check(launch_probe(iv, d_ik, nullptr, d_irids, nullptr, (uint64_t)n * nq, d_iout, nullptr, s, item->tune),
                   "item probe");
-        q2_finish<<<(n * nq + 255) / 256, 256, 0, s>>>(d_iout, iv.heap, iv.hstride, host(item).key_pad(), n, nq,
+        q2_finish<<<(n * nq + 255) / 256, 256, 0, s>>>(d_iout, iv.heap, iv.hstride, facts(item).key_pad(), n, nq,
                                                        d_rec, d_ab);
         hip_check(hipGetLastError(), "q2 kernels");
         std::vector<stage_q2_rec> recs((uint64_t)n * nq);

@@ -1,15 +1,18 @@
 // dist.hip -- multi-GPU YCSB-C front-end: route every key to shard
 // MurmurHash64A(key, 8, 0) % world (misc/murmur/MurmurHash2.cpp:99-147 as the router),
 // exchange keys with one RCCL all-to-all-v (grouped ncclSend/ncclRecv over xGMI), probe the
-// local shard, return results with the reverse all-to-all-v and scatter them back into the
-// caller's order.  The reference has no distributed layer; this is the
-// build's own exchange step for the 8-GPU config.
+// local shard, return results with the reverse all-to-all-v and fan them out into the caller's
+// order.  The reference has no distributed layer; this is the build's own
+// exchange step for the 8-GPU config.  Result semantics per key are those of the single-table
+// probe (BTree::Read + IndexScanExecutor visibility, include/execute/executor.h:374-454).
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <climits>
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
@@ -29,6 +32,10 @@ void chk(hipError_t e, const char *what) {
 void nchk(ncclResult_t r, const char *what) {
     if (r != ncclSuccess) throw std::runtime_error(std::string(what) + ": " + ncclGetErrorString(r));
 }
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t rl32(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
 
 struct alignas(16) SendRec {
     uint64_t key;
@@ -52,16 +59,25 @@ __device__ __forceinline__ uint64_t mm64a_8(uint64_t k) {
 
 // Routing without global atomics: per-block LDS histograms (blk[d*NB + b]), one exclusive
 // scan over them (dest-major, so offsets come out grouped by destination rank), then a
-// scatter that claims positions with LDS atomics inside each block's range.
+// scatter that claims positions with LDS atomics inside each block's range.  The number of
+// keys routed is read on the device (n_dev: the chunk's coalesced request count), so the
+// host does not wait for the coalescing before it enqueues the routing.
 constexpr int kRouteBlocks = 1024;
 constexpr int kMaxWorld = 64;
 constexpr int kDefaultChunks = 4;  // sharded batches are exchanged in this many overlapped chunks
+// caller positions served by one coalesced request at most: a hot key's run is cut into
+// requests of <= 64 callers, so no single probe or fan-out copy stores more than 64 rows
+constexpr uint32_t kFanCap = 64;
 
-__global__ __launch_bounds__(256) void route_hist(const uint64_t *__restrict__ keys, uint64_t n, int world,
+__device__ __forceinline__ uint64_t dev_len(uint64_t n_max, const uint32_t *n_dev) { return n_dev ? *n_dev : n_max; }
+
+__global__ __launch_bounds__(256) void route_hist(const uint64_t *__restrict__ keys, uint64_t n_max,
+                                                  const uint32_t *__restrict__ n_dev, int world,
                                                   uint8_t *__restrict__ dest, uint32_t *__restrict__ blk) {
     __shared__ uint32_t h[kMaxWorld];
     if (threadIdx.x < (unsigned)world) h[threadIdx.x] = 0;
     __syncthreads();
+    const uint64_t n = dev_len(n_max, n_dev);
     const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
     const uint64_t b0 = (uint64_t)blockIdx.x * per, b1 = b0 + per < n ? b0 + per : n;
     for (uint64_t i = b0 + threadIdx.x; i < b1; i += blockDim.x) {
@@ -103,57 +119,80 @@ __global__ __launch_bounds__(1024) void route_scan(const uint32_t *__restrict__ 
     }
 }
 
+// send[pos] = request i's key record; perm[pos] = its index; fan[pos] = the caller positions
+// it serves: urange[base + i] (coalesced: a range of flist) or {base + i, base + i + 1} (one
+// caller, the request itself)
 __global__ __launch_bounds__(256) void route_scatter(const uint64_t *__restrict__ keys, const uint32_t *__restrict__ rids,
-                                                     uint64_t n, int world, const uint8_t *__restrict__ dest,
-                                                     const uint32_t *__restrict__ offs, SendRec *__restrict__ send,
-                                                     uint32_t *__restrict__ perm, uint32_t idx_base,
-                                                     uint32_t *__restrict__ upos) {
+                                                     uint64_t n_max, const uint32_t *__restrict__ n_dev, int world,
+                                                     const uint8_t *__restrict__ dest, const uint32_t *__restrict__ offs,
+                                                     SendRec *__restrict__ send, uint32_t *__restrict__ perm,
+                                                     uint32_t idx_base, uint32_t *__restrict__ upos,
+                                                     const FanRange *__restrict__ urange, FanRange *__restrict__ fan) {
     __shared__ uint32_t cur[kMaxWorld];
     if (threadIdx.x < (unsigned)world) cur[threadIdx.x] = offs[threadIdx.x * gridDim.x + blockIdx.x];
     __syncthreads();
+    const uint64_t n = dev_len(n_max, n_dev);
     const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
     const uint64_t b0 = (uint64_t)blockIdx.x * per, b1 = b0 + per < n ? b0 + per : n;
     for (uint64_t i = b0 + threadIdx.x; i < b1; i += blockDim.x) {
         const uint32_t pos = atomicAdd(&cur[dest[i]], 1u);
+        const uint32_t idx = idx_base + (uint32_t)i;
         send[pos] = SendRec{keys[i], rids ? rids[i] : 0xFFFFFFFEu, 0};
-        perm[pos] = idx_base + (uint32_t)i;
-        // coalesced requests: where request i was sent (send / perm start at the chunk base)
-        if (upos) upos[idx_base + i] = idx_base + pos;
+        perm[pos] = idx;
+        if (upos) upos[idx] = idx_base + pos;  // where request idx was sent (owner-reply expand)
+        fan[idx_base + pos] = urange ? urange[idx] : FanRange{idx, idx + 1};
     }
 }
 
+// [C][W] send counts -> [W][C] (peer-major: one all-to-all of C counts per peer)
+__global__ void transpose_counts(const uint32_t *__restrict__ cw, int C, int W, uint32_t *__restrict__ wc) {
+    for (int k = threadIdx.x; k < C * W; k += blockDim.x) wc[(k % W) * C + k / W] = cw[k];
+}
+
 // ---- request coalescing of one chunk [b, b + len): the chunk's keys are radix-sorted with
-// their chunk positions; a sorted entry starts a request when its key or read id differs from
-// its predecessor's; requests are numbered by an inclusive scan and packed at [b, b + nu).
+// their chunk positions (by (key, read id): read ids first, then a stable sort by key); a
+// sorted entry starts a request when its key or read id differs from its predecessor's, or at
+// every kFanCap-th sorted position; requests are numbered by an inclusive scan and packed at
+// [b, b + nu).
 __global__ void dd_iota_kernel(uint32_t *__restrict__ v, uint64_t n) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) v[i] = (uint32_t)i;
+}
+
+__global__ void dd_gather_keys(const uint64_t *__restrict__ keys, const uint32_t *__restrict__ idx, uint64_t n,
+                               uint64_t *__restrict__ out) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n) out[j] = keys[idx[j]];
 }
 
 __global__ void dd_heads(const uint64_t *__restrict__ skeys, const uint32_t *__restrict__ sidx,
                          const uint32_t *__restrict__ rids, uint64_t n, uint32_t *__restrict__ flag) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n) return;
-    bool head = j == 0 || skeys[j] != skeys[j - 1];
+    bool head = j % kFanCap == 0 || skeys[j] != skeys[j - 1];
     if (!head && rids) head = rids[sidx[j]] != rids[sidx[j - 1]];
     flag[j] = head ? 1u : 0u;
 }
 
-// uidx[b + p] = b + request number of the caller position p; the request's key / read id packed
-// at b + its number; nu[chunk] = the chunk's request count
+// uidx[b + p] = b + request number of the caller position p (owner reply; may be null); flist[b + j] = the caller position
+// of sorted entry j; urange[b + u] = request u's run [b + first, b + last + 1) of flist; the
+// request's key / read id packed at b + u; nu[chunk] = the chunk's request count
 __global__ void dd_pack(const uint64_t *__restrict__ skeys, const uint32_t *__restrict__ sidx,
                         const uint32_t *__restrict__ rids, const uint32_t *__restrict__ flag,
                         const uint32_t *__restrict__ useq, uint64_t n, uint32_t b, uint32_t *__restrict__ uidx,
-                        uint64_t *__restrict__ ukeys, uint32_t *__restrict__ urids, uint32_t *__restrict__ nu,
-                        int chunk) {
+                        uint32_t *__restrict__ flist, FanRange *__restrict__ urange, uint64_t *__restrict__ ukeys,
+                        uint32_t *__restrict__ urids, uint32_t *__restrict__ nu, int chunk) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n) return;
     const uint32_t u = useq[j] - 1u, p = sidx[j];
-    uidx[b + p] = b + u;
+    if (uidx) uidx[b + p] = b + u;  // owner-reply mode only
+    flist[b + j] = b + p;
     if (flag[j]) {
         ukeys[b + u] = skeys[j];
         if (rids) urids[b + u] = rids[p];
+        urange[b + u].lo = b + (uint32_t)j;
     }
+    if (j == n - 1 || flag[j + 1]) urange[b + u].hi = b + (uint32_t)j + 1u;
     if (j == n - 1) nu[chunk] = useq[j];
 }
 
@@ -165,98 +204,83 @@ __global__ void unpack_keys(const SendRec *__restrict__ recv, uint64_t n, uint64
     rids[i] = recv[i].rid;
 }
 
-// back in the caller's order: out[perm[p]] = bout[p] for p in [p0, p1), one wave per probe.
-// Positions [q0, q1) are this rank's own keys: they never left the device, so they are read
-// straight from the local probe's output (qout / qrec) instead of a received copy.
+__device__ __forceinline__ void st_nt(u32x4 v, uint8_t *p) { __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p)); }
+
+// Fan-out of results that arrived (or were probed) in request order: the result of request
+// position p in [p0, p1) -- status record sout[p - p0], row srec + (p - p0) * stride -- is
+// stored at each of its caller positions flist[k], k in fan[p] (flist null: k itself).  A wave
+// takes R request positions per pass with their R rows in flight together, then stores each
+// row once per caller (the rows are read once per request, not once per caller).
 template <int R>
-__global__ __launch_bounds__(256) void unpermute(const stage_probe_out_dev *__restrict__ bout, const uint8_t *__restrict__ brec,
-                          const uint32_t *__restrict__ perm, uint64_t p0, uint64_t p1, uint32_t stride,
-                          stage_probe_out_dev *__restrict__ out, uint8_t *__restrict__ recs, uint64_t q0, uint64_t q1,
-                          const stage_probe_out_dev *__restrict__ qout, const uint8_t *__restrict__ qrec) {
-    // R positions per wave pass, their rows in flight together (as expand)
+__global__ __launch_bounds__(256) void fan_copy(const stage_probe_out_dev *__restrict__ sout,
+                                                const uint8_t *__restrict__ srec, uint64_t p0, uint64_t p1,
+                                                const FanRange *__restrict__ fan, const uint32_t *__restrict__ flist,
+                                                uint32_t stride, stage_probe_out_dev *__restrict__ out,
+                                                uint8_t *__restrict__ recs) {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    const uint32_t chunks = stride >> 4;
+    const uint32_t chunks = recs ? stride >> 4 : 0u;
     for (uint64_t pb = p0 + w * R; pb < p1; pb += nw * R) {
-        const uint4 *sr[R];
-        const uint4 *so[R];
-        uint64_t dst[R];
+        FanRange fr[R];
+        u32x4 so[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            const uint64_t p = pb + r < p1 ? pb + r : p1 - 1;
-            dst[r] = perm[p];
-            const bool own = p >= q0 && p < q1;
-            so[r] = reinterpret_cast<const uint4 *>(own ? qout + (p - q0) : bout + p);
-            sr[r] = reinterpret_cast<const uint4 *>(own ? qrec + (p - q0) * (uint64_t)stride : brec + p * (uint64_t)stride);
+            const bool in = pb + r < p1;
+            const uint64_t q = (in ? pb + r : p1 - 1) - p0;
+            fr[r] = in ? fan[pb + r] : FanRange{0u, 0u};
+            so[r] = lane < 2 ? reinterpret_cast<const u32x4 *>(sout + q)[lane] : u32x4{0, 0, 0, 0};
         }
-        if (lane < 2 * R) {
-            const int r = lane >> 1;
-            const uint4 *src = so[0];
-            uint64_t d = dst[0];
+        for (uint32_t c0 = 0; c0 < (chunks ? chunks : 1u); c0 += 64) {
+            const uint32_t c = c0 + lane;
+            u32x4 v[R];
 #pragma unroll
-            for (int k = 1; k < R; ++k)
-                if (r == k) src = so[k], d = dst[k];
-            if (pb + r < p1) reinterpret_cast<uint4 *>(out + d)[lane & 1] = src[lane & 1];
-        }
-        if (recs) {
-            for (uint32_t c0 = 0; c0 < chunks; c0 += 64) {
-                const uint32_t c = c0 + lane;
-                uint4 v[R];
+            for (int r = 0; r < R; ++r) {
+                const uint64_t q = (pb + r < p1 ? pb + r : p1 - 1) - p0;
+                v[r] = c < chunks ? reinterpret_cast<const u32x4 *>(srec + q * stride)[c] : u32x4{0, 0, 0, 0};
+            }
 #pragma unroll
-                for (int r = 0; r < R; ++r) v[r] = c < chunks ? sr[r][c] : uint4{0, 0, 0, 0};
-#pragma unroll
-                for (int r = 0; r < R; ++r)
-                    if (c < chunks && pb + r < p1) reinterpret_cast<uint4 *>(recs + dst[r] * stride)[c] = v[r];
+            for (int r = 0; r < R; ++r) {
+                for (uint32_t k0 = fr[r].lo; k0 < fr[r].hi; k0 += 64) {
+                    const uint32_t kk = k0 + lane;
+                    const uint32_t mine = kk < fr[r].hi ? (flist ? flist[kk] : kk) : 0u;
+                    const uint32_t kn = fr[r].hi - k0 < 64u ? fr[r].hi - k0 : 64u;
+                    for (uint32_t k = 0; k < kn; ++k) {
+                        const uint64_t pos = rl32(mine, (int)k);
+                        if (c < chunks) st_nt(v[r], recs + pos * stride + c * 16u);
+                        if (c0 == 0 && lane < 2) st_nt(so[r], reinterpret_cast<uint8_t *>(out + pos) + lane * 16u);
+                    }
+                }
             }
         }
     }
 }
 
-// coalesced requests back in the caller's order: caller position o takes the result of its
-// request, sent from position p = upos[uidx[o]] (own requests read in place, as unpermute).
-// A wave copies R caller positions per pass with their R source rows in flight together.
-template <int R>
-__global__ __launch_bounds__(256) void expand(const stage_probe_out_dev *__restrict__ bout, const uint8_t *__restrict__ brec,
-                       const uint32_t *__restrict__ uidx, const uint32_t *__restrict__ upos, uint64_t o0, uint64_t o1,
-                       uint32_t stride, stage_probe_out_dev *__restrict__ out, uint8_t *__restrict__ recs, uint64_t q0,
-                       uint64_t q1, const stage_probe_out_dev *__restrict__ qout, const uint8_t *__restrict__ qrec) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    const uint32_t chunks = stride >> 4;
-    for (uint64_t ob = o0 + w * R; ob < o1; ob += nw * R) {
-        const uint4 *sr[R];
-        const uint4 *so[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const uint64_t o = ob + r < o1 ? ob + r : o1 - 1;
-            const uint64_t p = upos[uidx[o]];
-            const bool own = p >= q0 && p < q1;
-            so[r] = reinterpret_cast<const uint4 *>(own ? qout + (p - q0) : bout + p);
-            sr[r] = reinterpret_cast<const uint4 *>(own ? qrec + (p - q0) * (uint64_t)stride : brec + p * (uint64_t)stride);
-        }
-        // status records: lanes 2r, 2r+1 copy position r's two halves
-        if (lane < 2 * R) {
-            const int r = lane >> 1;
-            const uint4 *src = so[0];
-#pragma unroll
-            for (int k = 1; k < R; ++k)
-                if (r == k) src = so[k];
-            if (ob + r < o1) reinterpret_cast<uint4 *>(out + ob + r)[lane & 1] = src[lane & 1];
-        }
-        if (recs) {
-            for (uint32_t c0 = 0; c0 < chunks; c0 += 64) {
-                const uint32_t c = c0 + lane;
-                uint4 v[R];
-#pragma unroll
-                for (int r = 0; r < R; ++r) v[r] = c < chunks ? sr[r][c] : uint4{0, 0, 0, 0};
-#pragma unroll
-                for (int r = 0; r < R; ++r)
-                    if (c < chunks && ob + r < o1) reinterpret_cast<uint4 *>(recs + (ob + r) * stride)[c] = v[r];
-            }
-        }
-    }
+// owner-reply mode, back in the caller's order: out[perm[p]] = bout[p] for p in [p0, p1).
+// Positions [q0, q1) are this rank's own keys: they never left the device, so they are read
+// straight from the local probe's output (qout).  Status records only (rows stay on the owner).
+__global__ __launch_bounds__(256) void unpermute_status(const stage_probe_out_dev *__restrict__ bout,
+                                                        const uint32_t *__restrict__ perm, uint64_t p0, uint64_t p1,
+                                                        stage_probe_out_dev *__restrict__ out, uint64_t q0, uint64_t q1,
+                                                        const stage_probe_out_dev *__restrict__ qout) {
+    const uint64_t p = p0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= p1) return;
+    const bool own = p >= q0 && p < q1;
+    out[perm[p]] = own ? qout[p - q0] : bout[p];
+}
+
+// owner-reply mode with coalesced requests: caller position o takes the status record of its
+// request, sent from position p = upos[uidx[o]] (own requests read in place, as above)
+__global__ __launch_bounds__(256) void expand_status(const stage_probe_out_dev *__restrict__ bout,
+                                                     const uint32_t *__restrict__ uidx, const uint32_t *__restrict__ upos,
+                                                     uint64_t o0, uint64_t o1, stage_probe_out_dev *__restrict__ out,
+                                                     uint64_t q0, uint64_t q1,
+                                                     const stage_probe_out_dev *__restrict__ qout) {
+    const uint64_t o = o0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (o >= o1) return;
+    const uint64_t p = upos[uidx[o]];
+    const bool own = p >= q0 && p < q1;
+    out[o] = own ? qout[p - q0] : bout[p];
 }
 
 // reply mode "owner": the row stays in the owner's result buffer; the status record carries
@@ -272,6 +296,8 @@ void grow(void *&p, uint64_t bytes) {
     chk(hipMalloc(&p, bytes ? bytes : 16), "hipMalloc");
 }
 
+unsigned blocks_for(uint64_t n, unsigned per_block) { return (unsigned)std::max<uint64_t>(1, (n + per_block - 1) / per_block); }
+
 }  // namespace
 
 ShardComm::~ShardComm() {
@@ -279,8 +305,8 @@ ShardComm::~ShardComm() {
     if (us) (void)hipStreamSynchronize(us), (void)hipStreamDestroy(us);
     for (hipEvent_t e : evs) (void)hipEventDestroy(e);
     if (comm) ncclCommDestroy((ncclComm_t)comm);
-    for (void *p : {dest, cursor, perm, send, recv, rout, rrec, bout, brec, cnt, lkeys, lrids, dd_skeys, dd_iota,
-                    dd_sidx, dd_flag, dd_useq, uidx, ukeys, urids, upos, dd_cub, dd_nu})
+    for (void *p : {dest, cursor, perm, send, recv, rout, rrec, bout, brec, cnt, lkeys, lrids, fan, dd_skeys, dd_iota,
+                    dd_sidx, dd_flag, dd_useq, uidx, ukeys, urids, upos, urange, flist, dd_cub, dd_nu, ctl})
         if (p) (void)hipFree(p);
 }
 
@@ -297,6 +323,35 @@ int shard_unique_id(uint8_t *id128) {
     return STAGE_OK;
 }
 
+// The RCCL this process runs (ncclGetVersion through the library's own binding, and the file
+// that symbol resolved to) against the headers the library was compiled with.  Two RCCL builds
+// can coexist in one process (e.g. PyTorch's copy); the sharded front-end refuses to run on one
+// whose major.minor differs from its headers unless STAGE_RCCL_ALLOW_MISMATCH=1.
+int shard_rccl_info(int *runtime_code, int *header_code, char *path, uint64_t path_len) {
+    int v = 0;
+    nchk(ncclGetVersion(&v), "ncclGetVersion");
+    if (runtime_code) *runtime_code = v;
+    if (header_code) *header_code = NCCL_VERSION_CODE;
+    if (path && path_len) {
+        Dl_info info{};
+        const char *f = dladdr(reinterpret_cast<void *>(&ncclGetVersion), &info) && info.dli_fname ? info.dli_fname : "?";
+        std::strncpy(path, f, path_len - 1);
+        path[path_len - 1] = 0;
+    }
+    return STAGE_OK;
+}
+
+static void check_rccl_version() {
+    int rt = 0, hd = 0;
+    char path[512];
+    shard_rccl_info(&rt, &hd, path, sizeof path);
+    const char *e = std::getenv("STAGE_RCCL_ALLOW_MISMATCH");
+    if (rt / 100 != hd / 100 && !(e && e[0] == '1'))
+        throw std::runtime_error("RCCL " + std::to_string(rt) + " loaded from " + path + " but libstage_hip was built "
+                                 "against RCCL headers " + std::to_string(hd) +
+                                 " (load libstage_hip before another RCCL copy, or STAGE_RCCL_ALLOW_MISMATCH=1)");
+}
+
 static void init_common(ShardComm &c, int rank, int world, int chunks) {
     if (world < 1 || world > kMaxWorld || rank < 0 || rank >= world) throw std::invalid_argument("bad rank/world");
     if (chunks < 1 || chunks > 64) throw std::invalid_argument("chunks must be 1..64");
@@ -307,20 +362,24 @@ static void init_common(ShardComm &c, int rank, int world, int chunks) {
     grow(c.cnt, 4ull * sizeof(uint32_t) * (uint64_t)world * chunks);
     grow(c.cursor, (2ull * world * kRouteBlocks + 16) * sizeof(uint32_t));
     chk(hipStreamCreateWithFlags(&c.cs, hipStreamNonBlocking), "comm stream");
-    chk(hipStreamCreateWithFlags(&c.us, hipStreamNonBlocking), "unpermute stream");
+    chk(hipStreamCreateWithFlags(&c.us, hipStreamNonBlocking), "fan-out stream");
     c.evs.resize(3 * chunks + 2);
     for (auto &e : c.evs) chk(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
 }
 
-static int env_chunks() {
+// exchange chunks: STAGE_SHARD_CHUNKS, else 4 (the result return of chunk i overlaps the probe
+// of chunk i + 1), or 1 at world 1, where nothing crosses xGMI and one batch-wide coalescing
+// routes fewer requests (43.8 % of a Zipf-0.9 batch instead of 54 % in 4 chunks)
+static int env_chunks(int world) {
     const char *e = std::getenv("STAGE_SHARD_CHUNKS");
-    return e ? std::max(1, std::min(64, std::atoi(e))) : kDefaultChunks;
+    return e ? std::max(1, std::min(64, std::atoi(e))) : world == 1 ? 1 : kDefaultChunks;
 }
 
-int shard_default_chunks() { return env_chunks(); }
+int shard_default_chunks(int world) { return env_chunks(world); }
 
 int shard_init(ShardComm &c, const uint8_t *id128, int rank, int world, int chunks) {
-    init_common(c, rank, world, chunks > 0 ? chunks : env_chunks());
+    check_rccl_version();
+    init_common(c, rank, world, chunks > 0 ? chunks : env_chunks(world));
     ncclUniqueId id;
     std::memcpy(&id, id128, 128);
     ncclComm_t comm;
@@ -330,15 +389,48 @@ int shard_init(ShardComm &c, const uint8_t *id128, int rank, int world, int chun
 }
 
 int shard_init_loopback(ShardComm &c, int rank, int world, int chunks) {
-    init_common(c, rank, world, chunks > 0 ? chunks : env_chunks());
+    init_common(c, rank, world, chunks > 0 ? chunks : env_chunks(world));
     c.comm = nullptr;
+    return STAGE_OK;
+}
+
+// ---- control plane over the communicator (host values, e.g. the bench's barrier and its
+// max-over-ranks step time): small allreduce / allgather of doubles on the comm stream
+static double *ctl_buf(ShardComm &c, uint64_t doubles) {
+    if (doubles > c.ctl_cap) {
+        grow(c.ctl, doubles * sizeof(double));
+        c.ctl_cap = doubles;
+    }
+    return (double *)c.ctl;
+}
+
+int shard_allreduce_f64(ShardComm &c, double *v, uint64_t n, int op) {
+    if (!c.comm) throw std::invalid_argument("not an RCCL communicator");
+    if (n == 0) return STAGE_OK;
+    double *d = ctl_buf(c, n);
+    const ncclRedOp_t ro = op == 1 ? ncclMax : op == 2 ? ncclMin : ncclSum;
+    chk(hipMemcpyAsync(d, v, n * sizeof(double), hipMemcpyHostToDevice, c.cs), "ctl h2d");
+    nchk(ncclAllReduce(d, d, n, ncclFloat64, ro, (ncclComm_t)c.comm, c.cs), "ncclAllReduce");
+    chk(hipMemcpyAsync(v, d, n * sizeof(double), hipMemcpyDeviceToHost, c.cs), "ctl d2h");
+    chk(hipStreamSynchronize(c.cs), "ctl sync");
+    return STAGE_OK;
+}
+
+int shard_allgather_f64(ShardComm &c, const double *in, uint64_t n, double *out) {
+    if (!c.comm) throw std::invalid_argument("not an RCCL communicator");
+    if (n == 0) return STAGE_OK;
+    double *d = ctl_buf(c, n * (uint64_t)(c.world + 1));
+    chk(hipMemcpyAsync(d, in, n * sizeof(double), hipMemcpyHostToDevice, c.cs), "ctl h2d");
+    nchk(ncclAllGather(d, d + n, n, ncclFloat64, (ncclComm_t)c.comm, c.cs), "ncclAllGather");
+    chk(hipMemcpyAsync(out, d + n, n * (uint64_t)c.world * sizeof(double), hipMemcpyDeviceToHost, c.cs), "ctl d2h");
+    chk(hipStreamSynchronize(c.cs), "ctl sync");
     return STAGE_OK;
 }
 
 // ---- the plan of one sharded probe, shared by the RCCL path and the loopback rehearsal.
 // The caller's batch is cut into C chunks (C is the same on every rank, fixed at init, so the
-// ranks issue matching transfers).  Chunk i's keys are routed into send/perm positions
-// [cb_i, cb_{i+1}), grouped by destination; what arrives lands in recv positions
+// ranks issue matching transfers).  Chunk i's requests are routed into send/perm positions
+// [cb_i, cb_i + routed_i), grouped by destination; what arrives lands in recv positions
 // [rb_i, rb_{i+1}), grouped by source.  All offsets are absolute.
 struct Plan {
     int W = 1, C = 1;
@@ -349,9 +441,10 @@ struct Plan {
     uint64_t m() const { return rb[C]; }
 };
 
-// route every chunk (caller stream), return the send counts [C][W] (host, synchronised)
+// coalescing + routing of every chunk, enqueued on the caller stream s (no host wait); the
+// send counts [C][W] are left in c.cnt
 static void plan_route(ShardComm &c, Plan &P, const uint64_t *d_keys, const uint32_t *d_rids, uint64_t n,
-                       uint32_t stride, hipStream_t s) {
+                       uint32_t stride, bool owner, hipStream_t s) {
     const int W = c.world, C = c.chunks;
     if (n > 0xFFFFFFFFull) throw std::invalid_argument("batch too large");
     if (n > c.cap_local || stride != c.rec_stride) {
@@ -359,6 +452,7 @@ static void plan_route(ShardComm &c, Plan &P, const uint64_t *d_keys, const uint
         grow(c.dest, cap);
         grow(c.perm, cap * 4);
         grow(c.send, cap * sizeof(SendRec));
+        grow(c.fan, cap * sizeof(FanRange));
         grow(c.bout, cap * sizeof(stage_probe_out_dev));
         grow(c.brec, cap * stride);
         c.cap_local = cap;
@@ -375,6 +469,8 @@ static void plan_route(ShardComm &c, Plan &P, const uint64_t *d_keys, const uint
     const uint32_t *rrids = d_rids;
     std::vector<uint64_t> rlen(C);
     for (int i = 0; i < C; ++i) rlen[i] = P.cb[i + 1] - P.cb[i];
+    const uint64_t maxlen = *std::max_element(rlen.begin(), rlen.end());
+    const uint32_t *nu = nullptr;
     if (P.dedupe) {
         if (c.dd_cap < c.cap_local) {
             const uint64_t cap = c.cap_local;
@@ -387,48 +483,68 @@ static void plan_route(ShardComm &c, Plan &P, const uint64_t *d_keys, const uint
             grow(c.ukeys, cap * 8);
             grow(c.urids, cap * 4);
             grow(c.upos, cap * 4);
+            grow(c.urange, cap * sizeof(FanRange));
+            grow(c.flist, cap * 4);
             grow(c.dd_nu, 64 * 4);
-            size_t sb = 0, cb = 0;
-            chk(hipcub::DeviceRadixSort::SortPairs(nullptr, sb, (uint64_t *)nullptr, (uint64_t *)nullptr,
-                                                   (uint32_t *)nullptr, (uint32_t *)nullptr, (int)cap, 0, 64, s),
-                "sort size");
-            chk(hipcub::DeviceScan::InclusiveSum(nullptr, cb, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)cap, s),
-                "scan size");
-            c.dd_cub_bytes = std::max(sb, cb);
-            grow(c.dd_cub, c.dd_cub_bytes);
             c.dd_cap = cap;
+            c.dd_cub_items = 0;
         }
-        uint32_t *nu = (uint32_t *)c.dd_nu;
-        chk(hipMemsetAsync(nu, 0, 64 * 4, s), "memset nu");
+        // temporary storage of the sorts and the scan, sized for the longest chunk
+        if (maxlen > c.dd_cub_items) {
+            const int items = (int)std::min<uint64_t>(maxlen, INT_MAX);
+            size_t sb = 0, sr = 0, cb = 0;
+            chk(hipcub::DeviceRadixSort::SortPairs(nullptr, sb, (uint64_t *)nullptr, (uint64_t *)nullptr,
+                                                   (uint32_t *)nullptr, (uint32_t *)nullptr, items, 0, 64, s),
+                "sort size");
+            chk(hipcub::DeviceRadixSort::SortPairs(nullptr, sr, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                                   (uint32_t *)nullptr, (uint32_t *)nullptr, items, 0, 32, s),
+                "rid sort size");
+            chk(hipcub::DeviceScan::InclusiveSum(nullptr, cb, (uint32_t *)nullptr, (uint32_t *)nullptr, items, s),
+                "scan size");
+            c.dd_cub_bytes = std::max(std::max(sb, sr), cb);
+            grow(c.dd_cub, c.dd_cub_bytes);
+            c.dd_cub_items = maxlen;
+        }
+        uint32_t *nuw = (uint32_t *)c.dd_nu;
+        chk(hipMemsetAsync(nuw, 0, 64 * 4, s), "memset nu");
         uint32_t *iota = (uint32_t *)c.dd_iota, *sidx = (uint32_t *)c.dd_sidx, *flag = (uint32_t *)c.dd_flag,
                  *useq = (uint32_t *)c.dd_useq;
         uint64_t *skeys = (uint64_t *)c.dd_skeys;
-        const uint64_t maxlen = *std::max_element(rlen.begin(), rlen.end());
-        dd_iota_kernel<<<(unsigned)((maxlen + 255) / 256), 256, 0, s>>>(iota, maxlen);
+        const int bits = c.key_bits >= 1 && c.key_bits <= 64 ? c.key_bits : 64;
+        dd_iota_kernel<<<blocks_for(maxlen, 256), 256, 0, s>>>(iota, maxlen);
         for (int i = 0; i < C; ++i) {
             const uint64_t b = P.cb[i], len = rlen[i];
             if (!len) continue;
-            const unsigned nb = (unsigned)((len + 255) / 256);
+            const unsigned nb = blocks_for(len, 256);
             const uint32_t *cr = d_rids ? d_rids + b : nullptr;
             size_t bytes = c.dd_cub_bytes;
-            chk(hipcub::DeviceRadixSort::SortPairs(c.dd_cub, bytes, d_keys + b, skeys, iota, sidx, (int)len, 0, 64, s),
-                "dedupe sort");
+            if (cr) {
+                // (key, read id) order: sort by read id, then stably by key (LSD radix sorts are
+                // stable); flag / useq serve as scratch until the heads are computed
+                uint32_t *srid = flag, *sidx1 = useq;
+                uint64_t *gk = (uint64_t *)c.ukeys + b;  // chunk i's packed keys are written after this sort
+                chk(hipcub::DeviceRadixSort::SortPairs(c.dd_cub, bytes, cr, srid, iota, sidx1, (int)len, 0, 32, s),
+                    "dedupe rid sort");
+                dd_gather_keys<<<nb, 256, 0, s>>>(d_keys + b, sidx1, len, gk);
+                bytes = c.dd_cub_bytes;
+                chk(hipcub::DeviceRadixSort::SortPairs(c.dd_cub, bytes, gk, skeys, sidx1, sidx, (int)len, 0, bits, s),
+                    "dedupe key sort");
+            } else {
+                chk(hipcub::DeviceRadixSort::SortPairs(c.dd_cub, bytes, d_keys + b, skeys, iota, sidx, (int)len, 0, bits,
+                                                       s),
+                    "dedupe sort");
+            }
             dd_heads<<<nb, 256, 0, s>>>(skeys, sidx, cr, len, flag);
             bytes = c.dd_cub_bytes;
             chk(hipcub::DeviceScan::InclusiveSum(c.dd_cub, bytes, flag, useq, (int)len, s), "dedupe scan");
-            dd_pack<<<nb, 256, 0, s>>>(skeys, sidx, cr, flag, useq, len, (uint32_t)b, (uint32_t *)c.uidx,
-                                       (uint64_t *)c.ukeys, (uint32_t *)c.urids, nu, i);
+            dd_pack<<<nb, 256, 0, s>>>(skeys, sidx, cr, flag, useq, len, (uint32_t)b, owner ? (uint32_t *)c.uidx : nullptr,
+                                       (uint32_t *)c.flist, (FanRange *)c.urange, (uint64_t *)c.ukeys,
+                                       (uint32_t *)c.urids, nuw, i);
         }
         chk(hipGetLastError(), "dedupe");
-        std::vector<uint32_t> hn(C);
-        chk(hipMemcpyAsync(hn.data(), nu, C * 4, hipMemcpyDeviceToHost, s), "nu d2h");
-        chk(hipStreamSynchronize(s), "sync");
-        for (int i = 0; i < C; ++i) {
-            if (hn[i] > rlen[i]) throw std::runtime_error("dedupe: more requests than keys");
-            rlen[i] = hn[i];
-        }
         rkeys = (const uint64_t *)c.ukeys;
         rrids = d_rids ? (const uint32_t *)c.urids : nullptr;
+        nu = nuw;
     }
     uint32_t *counts = (uint32_t *)c.cnt;  // [C][W] send counts
     uint32_t *blk = (uint32_t *)c.cursor, *offs = blk + (uint64_t)W * kRouteBlocks;
@@ -436,24 +552,30 @@ static void plan_route(ShardComm &c, Plan &P, const uint64_t *d_keys, const uint
     for (int i = 0; i < C; ++i) {
         const uint64_t b = P.cb[i], len = rlen[i];
         if (!len) continue;
-        route_hist<<<kRouteBlocks, 256, 0, s>>>(rkeys + b, len, W, (uint8_t *)c.dest + b, blk);
+        const uint32_t *nd = nu ? nu + i : nullptr;
+        route_hist<<<kRouteBlocks, 256, 0, s>>>(rkeys + b, len, nd, W, (uint8_t *)c.dest + b, blk);
         route_scan<<<1, 1024, 0, s>>>(blk, (uint32_t)(W * kRouteBlocks), W, kRouteBlocks, offs, counts + i * W);
-        route_scatter<<<kRouteBlocks, 256, 0, s>>>(rkeys + b, rrids ? rrids + b : nullptr, len, W,
+        route_scatter<<<kRouteBlocks, 256, 0, s>>>(rkeys + b, rrids ? rrids + b : nullptr, len, nd, W,
                                                    (const uint8_t *)c.dest + b, offs, (SendRec *)c.send + b,
                                                    (uint32_t *)c.perm + b, (uint32_t)b,
-                                                   P.dedupe ? (uint32_t *)c.upos : nullptr);
+                                                   P.dedupe && owner ? (uint32_t *)c.upos : nullptr,
+                                                   P.dedupe ? (const FanRange *)c.urange : nullptr,
+                                                   (FanRange *)c.fan);
     }
     chk(hipGetLastError(), "route");
-    P.sc.resize((size_t)C * W);
-    chk(hipMemcpyAsync(P.sc.data(), counts, (uint64_t)C * W * 4, hipMemcpyDeviceToHost, s), "counts d2h");
-    chk(hipStreamSynchronize(s), "sync");
+}
+
+// the send side of the plan from P.sc (filled by the caller from the device counts)
+static void plan_send(ShardComm &c, Plan &P, uint64_t n) {
+    const int W = P.W, C = P.C;
     P.soff.assign((size_t)C * (W + 1), 0);
     for (int i = 0; i < C; ++i) {
         P.soff[i * (W + 1)] = P.cb[i];
         for (int r = 0; r < W; ++r) P.soff[i * (W + 1) + r + 1] = P.soff[i * (W + 1) + r] + P.sc[i * W + r];
+        if (P.soff[i * (W + 1) + W] > P.cb[i + 1]) throw std::runtime_error("routing: more requests than keys");
     }
     c.last_n = n;
-    c.last_routed = c.last_remote = 0;
+    c.last_routed = c.last_remote = c.last_received = 0;
     for (int i = 0; i < C; ++i)
         for (int r = 0; r < W; ++r) {
             c.last_routed += P.sc[(size_t)i * W + r];
@@ -472,6 +594,7 @@ static void plan_receive(ShardComm &c, Plan &P, uint32_t stride) {
         P.rb[i + 1] = P.roff[i * (W + 1) + W];
     }
     const uint64_t m = P.m();
+    c.last_received = m;
     if (m > c.cap_remote) {
         const uint64_t cap = m + m / 8 + 1024;
         grow(c.recv, cap * sizeof(SendRec));
@@ -483,48 +606,98 @@ static void plan_receive(ShardComm &c, Plan &P, uint32_t stride) {
     }
 }
 
-// probe what arrived in chunk i
-static void chunk_probe(ShardComm &c, const Plan &P, int i, const DevTable &t, const ProbeTuning &tune, bool rows,
-                        bool tag, hipStream_t s) {
-    const uint64_t b = P.rb[i], m = P.rb[i + 1] - b;
-    if (!m) return;
-    uint64_t *lk = (uint64_t *)c.lkeys + b;
-    uint32_t *lr = (uint32_t *)c.lrids + b;
-    unpack_keys<<<(unsigned)((m + 255) / 256), 256, 0, s>>>((const SendRec *)c.recv + b, m, lk, lr);
-    chk(launch_probe(t, lk, nullptr, lr, nullptr, m, (stage_probe_out_dev *)c.rout + b,
-                     rows ? (uint8_t *)c.rrec + b * (uint64_t)t.stride : nullptr, s, tune),
-        "probe");
-    if (tag) tag_rows<<<(unsigned)((m + 255) / 256), 256, 0, s>>>((stage_probe_out_dev *)c.rout + b, m, (uint32_t)b);
+static void fan_launch(const stage_probe_out_dev *sout, const uint8_t *srec, uint64_t p0, uint64_t p1, const ShardComm &c,
+                       const Plan &P, uint32_t stride, stage_probe_out_dev *d_out, uint8_t *d_recs, hipStream_t s) {
+    if (p1 <= p0) return;
+    constexpr int R = 4;
+    fan_copy<R><<<(unsigned)std::min<uint64_t>((p1 - p0 + 4 * R - 1) / (4 * R), 8192), 256, 0, s>>>(
+        sout, srec, p0, p1, (const FanRange *)c.fan, P.dedupe ? (const uint32_t *)c.flist : nullptr, stride, d_out,
+        d_recs);
+    chk(hipGetLastError(), "fan copy");
 }
 
-static void chunk_unpermute(ShardComm &c, const Plan &P, int i, uint32_t stride, stage_probe_out_dev *d_out,
-                            uint8_t *d_recs, hipStream_t s) {
-    const uint64_t p0 = P.cb[i], p1 = P.cb[i + 1];
+// Probe what chunk i holds for this rank.  The remote segments arrived in recv; this rank's own
+// requests never left the device (no self transfer): they are read from the send buffer.
+// Full reply: own requests are probed in fan-out form, straight to their caller positions in
+// d_out / d_recs (tables of other geometries: probed into rout / rrec, then fanned out); the
+// remote segments are probed into rout / rrec for the return transfer.  Owner reply: everything
+// into rout / rrec, rows tagged with their owner-local index.
+static void chunk_probe(ShardComm &c, const Plan &P, int i, const DevTable &t, const ProbeTuning &tune, bool owner,
+                        stage_probe_out_dev *d_out, uint8_t *d_recs, hipStream_t s) {
     const int W = P.W, me = c.rank;
-    const uint64_t q0 = P.soff[(size_t)i * (W + 1) + me], q1 = P.soff[(size_t)i * (W + 1) + me + 1];
-    const uint64_t ro = P.roff[(size_t)i * (W + 1) + me];  // where the local probe wrote them
-    if (P.dedupe) {
-        constexpr int R = 4;
-        if (p1 > p0)
-            expand<R><<<(unsigned)std::min<uint64_t>((p1 - p0 + 4 * R - 1) / (4 * R), 8192), 256, 0, s>>>(
-                (const stage_probe_out_dev *)c.bout, (const uint8_t *)c.brec, (const uint32_t *)c.uidx,
-                (const uint32_t *)c.upos, p0, p1, stride, d_out, d_recs, q0, q1, (const stage_probe_out_dev *)c.rout + ro,
-                (const uint8_t *)c.rrec + ro * stride);
-        chk(hipGetLastError(), "expand");
+    const uint64_t b = P.rb[i], e = P.rb[i + 1];
+    if (e == b) return;
+    const uint64_t r0 = P.roff[(size_t)i * (W + 1) + me], r1 = P.roff[(size_t)i * (W + 1) + me + 1];
+    const uint64_t q0 = P.soff[(size_t)i * (W + 1) + me];
+    uint64_t *lk = (uint64_t *)c.lkeys;
+    uint32_t *lr = (uint32_t *)c.lrids;
+    auto unpack = [&](const SendRec *src, uint64_t at, uint64_t m) {
+        if (m) unpack_keys<<<blocks_for(m, 256), 256, 0, s>>>(src, m, lk + at, lr + at);
+    };
+    unpack((const SendRec *)c.recv + b, b, r0 - b);
+    unpack((const SendRec *)c.send + q0, r0, r1 - r0);
+    unpack((const SendRec *)c.recv + r1, r1, e - r1);
+    stage_probe_out_dev *rout = (stage_probe_out_dev *)c.rout;
+    uint8_t *rrec = (uint8_t *)c.rrec;
+    const bool rows = owner || d_recs != nullptr;
+    auto probe = [&](uint64_t a, uint64_t z) {
+        if (z > a)
+            chk(launch_probe(t, lk + a, nullptr, lr + a, nullptr, z - a, rout + a, rows ? rrec + a * (uint64_t)t.stride : nullptr,
+                             s, tune),
+                "probe");
+    };
+    if (owner) {
+        probe(b, e);
+        tag_rows<<<blocks_for(e - b, 256), 256, 0, s>>>(rout + b, e - b, (uint32_t)b);
         return;
     }
-    constexpr int R = 4;
-    if (p1 > p0)
-        unpermute<R><<<(unsigned)std::min<uint64_t>((p1 - p0 + 4 * R - 1) / (4 * R), 8192), 256, 0, s>>>(
-            (const stage_probe_out_dev *)c.bout, (const uint8_t *)c.brec, (const uint32_t *)c.perm, p0, p1, stride,
-            d_out, d_recs, q0, q1, (const stage_probe_out_dev *)c.rout + ro, (const uint8_t *)c.rrec + ro * stride);
-    chk(hipGetLastError(), "unpermute");
+    probe(b, r0);
+    probe(r1, e);
+    if (r1 == r0) return;
+    if (d_recs && probe_fanout_supported(t)) {
+        chk(launch_probe_fanout(t, lk + r0, lr + r0, r1 - r0, (const FanRange *)c.fan + q0,
+                                P.dedupe ? (const uint32_t *)c.flist : nullptr, d_out, d_recs, s, tune),
+            "fan-out probe");
+    } else {
+        probe(r0, r1);
+        fan_launch(rout + r0, rrec + r0 * (uint64_t)t.stride, q0, q0 + (r1 - r0), c, P, t.stride, d_out, d_recs, s);
+    }
+}
+
+// chunk i's results that came back from other ranks (bout / brec, at their send positions) to
+// their caller positions; owner reply: status records of every position (own ones read in place)
+static void chunk_return(ShardComm &c, const Plan &P, int i, uint32_t stride, bool owner, stage_probe_out_dev *d_out,
+                         uint8_t *d_recs, hipStream_t s) {
+    const int W = P.W, me = c.rank;
+    const uint64_t p0 = P.cb[i], pz = P.soff[(size_t)i * (W + 1) + W];
+    const uint64_t q0 = P.soff[(size_t)i * (W + 1) + me], q1 = P.soff[(size_t)i * (W + 1) + me + 1];
+    const stage_probe_out_dev *bout = (const stage_probe_out_dev *)c.bout;
+    const uint8_t *brec = (const uint8_t *)c.brec;
+    if (!owner) {
+        fan_launch(bout + p0, brec + p0 * (uint64_t)stride, p0, q0, c, P, stride, d_out, d_recs, s);
+        fan_launch(bout + q1, brec + q1 * (uint64_t)stride, q1, pz, c, P, stride, d_out, d_recs, s);
+        return;
+    }
+    const uint64_t ro = P.roff[(size_t)i * (W + 1) + me];  // where the local probe wrote the own results
+    const stage_probe_out_dev *qout = (const stage_probe_out_dev *)c.rout + ro;
+    if (P.dedupe) {
+        const uint64_t o0 = P.cb[i], o1 = P.cb[i + 1];
+        if (o1 > o0)
+            expand_status<<<blocks_for(o1 - o0, 256), 256, 0, s>>>(bout, (const uint32_t *)c.uidx, (const uint32_t *)c.upos,
+                                                                   o0, o1, d_out, q0, q1, qout);
+    } else if (pz > p0) {
+        unpermute_status<<<blocks_for(pz - p0, 256), 256, 0, s>>>(bout, (const uint32_t *)c.perm, p0, pz, d_out, q0, q1,
+                                                                  qout);
+    }
+    chk(hipGetLastError(), "owner-reply return");
 }
 
 // RCCL path.  Streams: the caller's stream s routes and probes; c.cs carries the RCCL
-// transfers; c.us un-permutes.  Order: all key exchanges first (16 B/key), then for each
-// chunk the probe (s) and, as soon as it is done, its result exchange (cs) -- so the return
-// of chunk i over xGMI overlaps the probe of chunk i+1 in HBM -- and its un-permutation (us).
+// transfers; c.us fans the returned results out.  One host wait per call: the send counts are
+// transposed and exchanged on the device (ncclAllToAll), and the send and receive counts come
+// back together.  Then all key exchanges (16 B/request, own requests stay), and for each chunk
+// the probe (s) and, as soon as it is done, its result exchange (cs) -- so the return of chunk i
+// over xGMI overlaps the probe of chunk i+1 in HBM -- and its fan-out (us).
 int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const uint64_t *d_keys,
                 const uint32_t *d_rids, uint64_t n, stage_probe_out_dev *d_out, uint8_t *d_recs, int reply,
                 hipStream_t s) {
@@ -536,25 +709,26 @@ int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const 
     const uint32_t stride = t.stride;
     ncclComm_t comm = (ncclComm_t)c.comm;
     Plan P;
-    plan_route(c, P, d_keys, d_rids, n, stride, s);
-    // count exchange: peer-major [W][C] so one all-to-all of C counts per peer carries all chunks
+    plan_route(c, P, d_keys, d_rids, n, stride, owner, s);
     uint32_t *cnt = (uint32_t *)c.cnt, *sendT = cnt + (uint64_t)C * W, *recvT = sendT + (uint64_t)C * W;
-    std::vector<uint32_t> hT((size_t)C * W);
-    for (int i = 0; i < C; ++i)
-        for (int r = 0; r < W; ++r) hT[(size_t)r * C + i] = P.sc[(size_t)i * W + r];
-    chk(hipMemcpyAsync(sendT, hT.data(), hT.size() * 4, hipMemcpyHostToDevice, s), "counts h2d");
+    transpose_counts<<<1, 256, 0, s>>>(cnt, C, W, sendT);
     nchk(ncclAllToAll(sendT, recvT, (size_t)C, ncclUint32, comm, s), "ncclAllToAll counts");
-    chk(hipMemcpyAsync(hT.data(), recvT, hT.size() * 4, hipMemcpyDeviceToHost, s), "counts d2h");
+    std::vector<uint32_t> hc((size_t)2 * C * W);  // [C][W] send counts, then [W][C] receive counts
+    chk(hipMemcpyAsync(hc.data(), cnt, (size_t)C * W * 4, hipMemcpyDeviceToHost, s), "counts d2h");
+    chk(hipMemcpyAsync(hc.data() + (size_t)C * W, recvT, (size_t)C * W * 4, hipMemcpyDeviceToHost, s), "counts d2h");
     chk(hipStreamSynchronize(s), "sync");
+    P.sc.assign(hc.begin(), hc.begin() + (size_t)C * W);
+    plan_send(c, P, n);
     P.rc.resize((size_t)C * W);
     for (int i = 0; i < C; ++i)
-        for (int r = 0; r < W; ++r) P.rc[(size_t)i * W + r] = hT[(size_t)r * C + i];
+        for (int r = 0; r < W; ++r) P.rc[(size_t)i * W + r] = hc[(size_t)C * W + (size_t)r * C + i];
     plan_receive(c, P, stride);
     hipEvent_t *ev_keys = c.evs.data(), *ev_probe = ev_keys + C, *ev_res = ev_probe + C, ev_start = ev_res[C];
     // the comm stream starts after the routing (done: s was synchronised) -- keys of all chunks
     for (int i = 0; i < C; ++i) {
         nchk(ncclGroupStart(), "group");
         for (int r = 0; r < W; ++r) {
+            if (r == c.rank) continue;  // own requests are probed from the send buffer
             const uint32_t sn = P.sc[(size_t)i * W + r], rn = P.rc[(size_t)i * W + r];
             if (sn)
                 nchk(ncclSend((const SendRec *)c.send + P.soff[(size_t)i * (W + 1) + r], (uint64_t)sn * sizeof(SendRec),
@@ -571,12 +745,12 @@ int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const 
     const uint64_t ob = sizeof(stage_probe_out_dev);
     for (int i = 0; i < C; ++i) {
         chk(hipStreamWaitEvent(s, ev_keys[i], 0), "wait keys");
-        chunk_probe(c, P, i, t, tune, owner || d_recs != nullptr, owner, s);
+        chunk_probe(c, P, i, t, tune, owner, d_out, d_recs, s);
         chk(hipEventRecord(ev_probe[i], s), "event");
         chk(hipStreamWaitEvent(c.cs, ev_probe[i], 0), "wait probe");
         nchk(ncclGroupStart(), "group");
         for (int r = 0; r < W; ++r) {
-            if (r == c.rank) continue;  // own results are read in place by the un-permutation
+            if (r == c.rank) continue;  // own results are already in place
             const uint32_t sn = P.sc[(size_t)i * W + r], rn = P.rc[(size_t)i * W + r];
             const uint64_t so = P.soff[(size_t)i * (W + 1) + r], ro = P.roff[(size_t)i * (W + 1) + r];
             if (rn) {
@@ -595,9 +769,9 @@ int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const 
         nchk(ncclGroupEnd(), "group end");
         chk(hipEventRecord(ev_res[i], c.cs), "event");
         chk(hipStreamWaitEvent(c.us, ev_res[i], 0), "wait results");
-        chunk_unpermute(c, P, i, stride, d_out, d_recs, c.us);
+        chunk_return(c, P, i, stride, owner, d_out, d_recs, c.us);
     }
-    // the caller's stream completes after the last un-permutation
+    // the caller's stream completes after the last fan-out
     chk(hipEventRecord(ev_start, c.us), "event");
     chk(hipStreamWaitEvent(s, ev_start, 0), "join");
     if (owner) c.owner_rows = P.m();
@@ -622,7 +796,13 @@ int shard_probe_loopback(const std::vector<ShardComm *> &cs, const std::vector<c
     const int C = cs[0]->chunks;
     const bool rows = recs[0] != nullptr;
     std::vector<Plan> P(W);
-    for (int r = 0; r < W; ++r) plan_route(*cs[r], P[r], keys[r], rids[r], n[r], stride, s);
+    for (int r = 0; r < W; ++r) {
+        plan_route(*cs[r], P[r], keys[r], rids[r], n[r], stride, owner, s);
+        P[r].sc.resize((size_t)C * W);
+        chk(hipMemcpyAsync(P[r].sc.data(), cs[r]->cnt, (size_t)C * W * 4, hipMemcpyDeviceToHost, s), "counts d2h");
+    }
+    chk(hipStreamSynchronize(s), "sync");
+    for (int r = 0; r < W; ++r) plan_send(*cs[r], P[r], n[r]);
     for (int r = 0; r < W; ++r) {
         P[r].rc.resize((size_t)C * W);
         for (int i = 0; i < C; ++i)
@@ -634,16 +814,18 @@ int shard_probe_loopback(const std::vector<ShardComm *> &cs, const std::vector<c
     };
     for (int i = 0; i < C; ++i)  // keys: q's chunk-i segment for r -> r's chunk-i segment from q
         for (int r = 0; r < W; ++r)
-            for (int q = 0; q < W; ++q)
+            for (int q = 0; q < W; ++q) {
+                if (q == r) continue;  // as shard_probe: own requests are probed from the send buffer
                 copy((SendRec *)cs[r]->recv + P[r].roff[(size_t)i * (W + 1) + q],
                      (const SendRec *)cs[q]->send + P[q].soff[(size_t)i * (W + 1) + r],
                      (uint64_t)P[q].sc[(size_t)i * W + r] * sizeof(SendRec), "loopback keys");
+            }
     const uint64_t ob = sizeof(stage_probe_out_dev);
     for (int i = 0; i < C; ++i) {
-        for (int r = 0; r < W; ++r) chunk_probe(*cs[r], P[r], i, *ts[r], tune, rows || owner, owner, s);
+        for (int r = 0; r < W; ++r) chunk_probe(*cs[r], P[r], i, *ts[r], tune, owner, outs[r], recs[r], s);
         for (int q = 0; q < W; ++q)  // results: owner q's chunk-i segment for r -> r's chunk-i slots of q
             for (int r = 0; r < W; ++r) {
-                if (r == q) continue;  // as shard_probe: own results are read in place
+                if (r == q) continue;  // as shard_probe: own results are already in place
                 const uint64_t cnt = P[q].rc[(size_t)i * W + r];
                 const uint64_t ro = P[q].roff[(size_t)i * (W + 1) + r], so = P[r].soff[(size_t)i * (W + 1) + q];
                 copy((uint8_t *)cs[r]->bout + so * ob, (const uint8_t *)cs[q]->rout + ro * ob, cnt * ob, "loopback out");
@@ -651,7 +833,7 @@ int shard_probe_loopback(const std::vector<ShardComm *> &cs, const std::vector<c
                     copy((uint8_t *)cs[r]->brec + so * stride, (const uint8_t *)cs[q]->rrec + ro * stride,
                          cnt * stride, "loopback rows");
             }
-        for (int r = 0; r < W; ++r) chunk_unpermute(*cs[r], P[r], i, stride, outs[r], recs[r], s);
+        for (int r = 0; r < W; ++r) chunk_return(*cs[r], P[r], i, stride, owner, outs[r], recs[r], s);
     }
     for (int r = 0; r < W; ++r) cs[r]->owner_rows = owner ? P[r].m() : 0;
     return STAGE_OK;

@@ -18,6 +18,7 @@ struct ShardComm {
     void *dest = nullptr, *cursor = nullptr, *perm = nullptr, *send = nullptr, *recv = nullptr;
     void *rout = nullptr, *rrec = nullptr, *bout = nullptr, *brec = nullptr, *cnt = nullptr;
     void *lkeys = nullptr, *lrids = nullptr;
+    void *fan = nullptr;             // [send position] caller positions the request serves (FanRange)
     uint64_t cap_local = 0, cap_remote = 0;
     uint32_t rec_stride = 0;
     int chunks = 1;                  // overlapped exchange chunks (same on every rank)
@@ -30,17 +31,28 @@ struct ShardComm {
     bool dedupe = true;
     void *dd_skeys = nullptr, *dd_iota = nullptr, *dd_sidx = nullptr, *dd_flag = nullptr, *dd_useq = nullptr;
     void *uidx = nullptr, *ukeys = nullptr, *urids = nullptr, *upos = nullptr, *dd_cub = nullptr, *dd_nu = nullptr;
-    uint64_t dd_cap = 0, dd_cub_bytes = 0;
+    void *urange = nullptr, *flist = nullptr;  // request -> run of flist; flist = caller positions in key order
+    uint64_t dd_cap = 0, dd_cub_bytes = 0, dd_cub_items = 0;
+    int key_bits = 64;               // coalescing sorts on the low key_bits bits (any value is correct)
     // the last sharded probe: caller keys, requests routed (after coalescing), of which remote
     uint64_t last_n = 0, last_routed = 0, last_remote = 0;
+    uint64_t last_received = 0;      // requests this rank probed as owner (own + other ranks')
+    void *ctl = nullptr;             // control-plane scratch (doubles)
+    uint64_t ctl_cap = 0;
     ~ShardComm();
 };
 
 int shard_unique_id(uint8_t *id128);
-// chunks: overlapped exchange chunks, identical on every rank (<= 0: STAGE_SHARD_CHUNKS or 4)
+// RCCL version the process runs (ncclGetVersion), the version of the headers the library was
+// built against (NCCL_VERSION_CODE) and the file ncclGetVersion resolved to
+int shard_rccl_info(int *runtime_code, int *header_code, char *path, uint64_t path_len);
+// chunks: overlapped exchange chunks, identical on every rank (<= 0: STAGE_SHARD_CHUNKS, or 4; 1 at world 1)
 int shard_init(ShardComm &c, const uint8_t *id128, int rank, int world, int chunks);
-int shard_default_chunks();
+int shard_default_chunks(int world);
 bool shard_default_dedupe();  // STAGE_SHARD_DEDUPE=0 turns request coalescing off
+// control plane on the communicator: op 0 sum, 1 max, 2 min (in place); allgather: out[r*n + i]
+int shard_allreduce_f64(ShardComm &c, double *v, uint64_t n, int op);
+int shard_allgather_f64(ShardComm &c, const double *in, uint64_t n, double *out);
 int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const uint64_t *d_keys,
                 const uint32_t *d_rids, uint64_t n, stage_probe_out_dev *d_out, uint8_t *d_recs, int reply,
                 hipStream_t s);

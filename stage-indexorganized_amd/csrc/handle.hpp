@@ -35,22 +35,33 @@ struct stage_table {
     std::unique_ptr<stage::ShardComm> loop_comm;  // stage_probe_sharded_loopback state
     int shard_chunks = 0;                          // 0 = STAGE_SHARD_CHUNKS or the default
     int shard_dedupe = -1;                         // -1 = STAGE_SHARD_DEDUPE or on
+    int shard_key_bits = 64;                       // coalescing sort width (stage_set_shard_key_bits)
     std::mutex pipe_mu;  // serialises stage_probe_host calls on this table
     std::unique_ptr<stage::HostPipe, stage::HostPipeDeleter> pipe;
     // the device write path hands its epoch's bookkeeping (new copy / version headers, slot
     // words) to the host table on this thread while the device goes on (write_path.hip);
-    // every entry point that reads or writes the host table settles it first (host())
+    // every entry point that reads or writes the host table settles it first (host()).
+    // adopt_mu guards `adopt`: settle() may run on any caller thread while the writer (the
+    // thread calling stage_update_batch_device) starts the next adoption.  A failed adoption
+    // is sticky: the host table missed an epoch of the device, so every later host-table call
+    // (the writer's included) reports it.
+    std::mutex adopt_mu;
     std::thread adopt;
-    std::exception_ptr adopt_err;
+    std::exception_ptr adopt_err;  // written by the adoption thread before it ends, read after join
     void settle() {
+        std::lock_guard<std::mutex> g(adopt_mu);
         if (adopt.joinable()) adopt.join();
-        if (adopt_err) {
-            std::exception_ptr e = adopt_err;
-            adopt_err = nullptr;
-            std::rethrow_exception(e);
-        }
+        if (adopt_err) std::rethrow_exception(adopt_err);
+    }
+    // starts the adoption of an epoch (after settle(): no adoption is running)
+    template <class F>
+    void start_adoption(F &&fn) {
+        std::lock_guard<std::mutex> g(adopt_mu);
+        if (adopt.joinable()) adopt.join();
+        adopt = std::thread(std::forward<F>(fn));
     }
     ~stage_table() {
+        std::lock_guard<std::mutex> g(adopt_mu);
         if (adopt.joinable()) adopt.join();
     }
 };
@@ -81,6 +92,10 @@ inline stage::HostTable &host(stage_table *t) {
     t->settle();
     return *t->host;
 }
+
+// geometry facts fixed at stage_open (key width / words, payload size, stride, leaf capacity):
+// read without settling a pending adoption, so read-only paths never wait for the writer
+inline const stage::HostTable &facts(stage_table *t) { return *t->host; }
 
 // device entry points check the host's dirty flag without settling: a pending adoption never
 // touches layout_dirty_, and the device image is already current

@@ -66,7 +66,7 @@ void host_pipe_release(HostPipe *p) {
 
 static HostPipe *get_pipe(stage_table *t) {
     const uint64_t stride = t->out_stride ? t->out_stride : t->dev.view.stride;
-    const uint32_t kw = host(t).key_words();
+    const uint32_t kw = facts(t).key_words();
     if (t->pipe && t->pipe->stride == stride && t->pipe->kw == kw && t->pipe->device == t->dev.device)
         return t->pipe.get();
     t->pipe.reset();
@@ -366,15 +366,15 @@ int stage_probe_host(stage_table *t, const uint64_t *keys, const uint16_t *lens,
 
 int stage_reader_create(stage_table *t, uint32_t max_batch, uint32_t max_wait_us, stage_reader **out) {
     if (!t || !out || max_batch == 0 || max_batch > (1u << 20)) return fail(STAGE_E_ARG, "bad reader arguments");
-    if (host(t).key_words() != 1) return fail(STAGE_E_ARG, "the single-key reader takes keys of <= 8 bytes");
+    if (facts(t).key_words() != 1) return fail(STAGE_E_ARG, "the single-key reader takes keys of <= 8 bytes");
     *out = nullptr;
     return guarded([&] {
         std::unique_ptr<stage_reader> r(new stage_reader);
         r->t = t;
         r->max_batch = max_batch;
         r->max_wait_us = max_wait_us;
-        r->stride = host(t).stride();
-        r->row_bytes = 8 + host(t).params().payload_size;
+        r->stride = facts(t).stride();
+        r->row_bytes = 8 + facts(t).params().payload_size;
         const uint64_t mb = max_batch, bytes = mb * (8 + 2 + 4 + 32 + r->stride);
         stage::hip_check(hipSetDevice(t->dev.device), "hipSetDevice");
         for (auto &sl : r->slot) {
@@ -431,7 +431,7 @@ int stage_reader_create_resident(stage_table *t, uint32_t ring_slots, uint32_t w
         ring_slots > (1u << 22) || life_us == 0 || life_us > 1000000)
         return fail(STAGE_E_ARG, "bad resident reader arguments (ring_slots: a multiple of 64 * waves; waves "
                                  "1..1024; life_us 1..1e6)");
-    if (host(t).key_words() != 1) return fail(STAGE_E_ARG, "the single-key reader takes keys of <= 8 bytes");
+    if (facts(t).key_words() != 1) return fail(STAGE_E_ARG, "the single-key reader takes keys of <= 8 bytes");
     if (int rc = need_synced(t)) return rc;
     const uint32_t cap = t->dev.view.cap;
     if (t->dev.view.key_width == 0 ? cap > 128 : cap > 1024)
@@ -445,8 +445,8 @@ int stage_reader_create_resident(stage_table *t, uint32_t ring_slots, uint32_t w
         R.t = t;
         R.slots = ring_slots;
         R.waves = waves;
-        R.stride = host(t).stride();
-        R.row_bytes = 8 + host(t).params().payload_size;
+        R.stride = facts(t).stride();
+        R.row_bytes = 8 + facts(t).params().payload_size;
         stage::hip_check(hipSetDevice(t->dev.device), "hipSetDevice");
         int khz = 0;
         stage::hip_check(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, t->dev.device), "clock rate");

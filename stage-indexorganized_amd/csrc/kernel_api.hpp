@@ -34,6 +34,16 @@ hipError_t launch_resolve(const DevTable &t, const uint64_t *keys, const uint16_
 hipError_t launch_probe(const DevTable &t, const uint64_t *keys, const uint16_t *lens, const uint32_t *rids,
                         const uint32_t *leaf_in, uint64_t n, stage_probe_out_dev *out, uint8_t *recs, hipStream_t s,
                         const ProbeTuning &tune);
+// fan-out probe (sharded front-end, dist.hip): probe i's status record and row are stored at
+// every caller position flist[k], k in [fan[i].lo, fan[i].hi) (flist null: k itself).  Tables of
+// the YCSB geometry only (fixed-width 8-byte keys, 64-slot leaves, rows <= 1024 B).
+struct alignas(8) FanRange {
+    uint32_t lo, hi;
+};
+bool probe_fanout_supported(const DevTable &t);
+hipError_t launch_probe_fanout(const DevTable &t, const uint64_t *keys, const uint32_t *rids, uint64_t n,
+                               const FanRange *fan, const uint32_t *flist, stage_probe_out_dev *out, uint8_t *recs,
+                               hipStream_t s, const ProbeTuning &tune);
 struct ScanTuning {
     int rows = 4;        // tuple rows in flight per wave (2, 4 or 8)
     int max_blocks = 0;  // 0 = default grid cap (16384 blocks of 256 threads)

@@ -331,13 +331,18 @@ __device__ __forceinline__ void st16(u32x4 v, uint8_t *base, uint32_t off) {
 // that a wave's chunk is not a chain of 64 dependent probes while most of the chip idles).
 // ST: status record bytes -- 32 (stage_probe_out) or 16 (stage_probe_out16, opt-in: status |
 // flags | hops, cstamp, copy_sstamp, rec_cstamp -- what IndexScanExecutor and PerformRead use)
-template <bool VARLEN, int SPL, int G, int POL = 1, int KW = 1, int CH = 64, int ST = 32>
+// FAN: fan-out probes (the sharded front-end's coalesced requests, dist.hip): probe i's status
+// record and row go to every caller position flist[k], k in [fan[i].lo, fan[i].hi) (flist null:
+// the positions k themselves) instead of position i -- the row leaves registers once per
+// caller and no second pass copies it (rows of at most 1024 B, recs required).
+template <bool VARLEN, int SPL, int G, int POL = 1, int KW = 1, int CH = 64, int ST = 32, bool FAN = false>
 __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *__restrict__ keys,
                                                     const uint16_t *__restrict__ lens,
                                                     const uint32_t *__restrict__ rids,
                                                     const uint32_t *__restrict__ leaf_in, uint64_t n,
                                                     stage_probe_out_dev *__restrict__ out,
-                                                    uint8_t *__restrict__ recs) {
+                                                    uint8_t *__restrict__ recs, const FanRange *__restrict__ fan,
+                                                    const uint32_t *__restrict__ flist) {
     const uint32_t lane = lane_id();
     // threadIdx.x / 64 made provably wave-uniform: the chunk base and the output row addresses
     // live in SGPRs (probe_kernel<.., 8>: 78 VGPRs, 6 waves/SIMD, instead of 95 and 5)
@@ -350,6 +355,8 @@ __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *
         u32x4 my_a = u32x4{0, 0, 0, 0}, my_b = u32x4{0, 0, 0, 0};  // this lane's probe result
         const uint32_t len = t.key_width ? t.key_width : (lens && valid ? (uint32_t)lens[i] : 8u);
         const uint32_t rid = rids ? (valid ? rids[i] : 0u) : 0xFFFFFFFEu;
+        FanRange my_fan = FanRange{0u, 0u};
+        if (FAN && valid) my_fan = fan[i];
         uint64_t ok[KW];
         load_okey<KW>(keys, i, valid, len, ok);
         uint32_t leaf = 0;
@@ -470,6 +477,37 @@ __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *
                     visibility(t, slot, m, nx, im, rd[g], r[g]);
                 }
             }
+            // phase 4 (FAN): G rows in flight, each stored at its caller positions with its
+            // status record (lanes 0-1); up to 64 positions are loaded at once, one per lane
+            if constexpr (FAN) {
+                u32x4 v[G];
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    v[g] = u32x4{0, 0, 0, 0};
+                    if (lane < out_chunks && r[g].image != 0xFFFFFFFFu)
+                        v[g] = reinterpret_cast<const u32x4 *>(t.heap + (uint64_t)r[g].image * t.hstride)[lane];
+                }
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    const int j = j0 + g;
+                    if (j >= cnt) break;
+                    u32x4 a, b;
+                    pack_out(lf[g], r[g], a, b);
+                    const u32x4 half = lane == 0 ? a : b;
+                    const uint32_t lo = rl32(my_fan.lo, j), hi = rl32(my_fan.hi, j);
+                    for (uint32_t k0 = lo; k0 < hi; k0 += 64) {
+                        const uint32_t kk = k0 + lane;
+                        const uint32_t mine = kk < hi ? (flist ? flist[kk] : kk) : 0u;
+                        const uint32_t kn = hi - k0 < 64u ? hi - k0 : 64u;
+                        for (uint32_t k = 0; k < kn; ++k) {
+                            const uint64_t pos = rl32(mine, (int)k);
+                            if (lane < out_chunks) st16<POL>(v[g], recs + pos * (uint64_t)t.stride, lane * 16u);
+                            if (lane < 2) st16<POL>(half, reinterpret_cast<uint8_t *>(out + pos), lane * 16u);
+                        }
+                    }
+                }
+                continue;
+            }
             // phase 4: tuple rows (G rows in flight), then nontemporal stores
             if (recs) {
                 for (uint32_t c0 = 0; c0 < out_chunks; c0 += 64) {
@@ -500,7 +538,8 @@ __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *
             }
         }
         // one coalesced 2-KiB (1-KiB) store of the chunk's 64 results
-        if constexpr (ST == 16) {
+        if constexpr (FAN) {
+        } else if constexpr (ST == 16) {
             if (valid)
                 st16<POL>(u32x4{my_a.x, my_a.w, my_b.y, my_b.x}, reinterpret_cast<uint8_t *>(out) + base * 16u,
                           lane * 16u);
@@ -2302,9 +2341,11 @@ hipError_t launch_probe(const DevTable &t, const uint64_t *keys, const uint16_t 
     else if (split)                                                                                           \
         probe_split_kernel<S, KW, 64><<<blocks, 256, 0, s>>>(t, keys, rids, leaf_in, n, out, recs);            \
     else if (small)                                                                                           \
-        probe_kernel<false, S, 1, 1, KW, 16><<<wblocks, 256, 0, s>>>(t, keys, lens, rids, leaf_in, n, out, recs); \
+        probe_kernel<false, S, 1, 1, KW, 16><<<wblocks, 256, 0, s>>>(t, keys, lens, rids, leaf_in, n, out, recs, \
+                                                                     nullptr, nullptr);                        \
     else                                                                                                      \
-        probe_kernel<false, S, 1, 1, KW><<<blocks, 256, 0, s>>>(t, keys, lens, rids, leaf_in, n, out, recs)
+        probe_kernel<false, S, 1, 1, KW><<<blocks, 256, 0, s>>>(t, keys, lens, rids, leaf_in, n, out, recs,      \
+                                                                nullptr, nullptr)
 #define STAGE_PROBE_WK(KW)                      \
     switch (t.cap / 64) {                       \
         case 1: STAGE_PROBE_W(1, KW); break;    \
@@ -2324,10 +2365,12 @@ hipError_t launch_probe(const DevTable &t, const uint64_t *keys, const uint16_t 
 #undef STAGE_PROBE_W
         return hipGetLastError();
     }
-#define STAGE_PROBE(V, S, G) probe_kernel<V, S, G><<<blocks, 256, 0, s>>>(t, keys, lens, rids, leaf_in, n, out, recs)
+#define STAGE_PROBE(V, S, G) \
+    probe_kernel<V, S, G><<<blocks, 256, 0, s>>>(t, keys, lens, rids, leaf_in, n, out, recs, nullptr, nullptr)
     if (tune.status_bytes == 16) {  // opt-in lean status records: the YCSB geometry only
         if (var || t.cap != 64 || tune.group != 8 || tune.store != 1) return hipErrorInvalidValue;
-        probe_kernel<false, 1, 8, 1, 1, 64, 16><<<blocks, 256, 0, s>>>(t, keys, lens, rids, leaf_in, n, out, recs);
+        probe_kernel<false, 1, 8, 1, 1, 64, 16><<<blocks, 256, 0, s>>>(t, keys, lens, rids, leaf_in, n, out, recs,
+                                                                       nullptr, nullptr);
         return hipGetLastError();
     }
     if (t.cap == 64) {
@@ -2336,9 +2379,11 @@ hipError_t launch_probe(const DevTable &t, const uint64_t *keys, const uint16_t 
         else if (tune.group == 2) STAGE_PROBE(false, 1, 2);
         else if (tune.group == 4) STAGE_PROBE(false, 1, 4);
         else if (tune.store == 0)
-            probe_kernel<false, 1, 8, 0><<<blocks, 256, 0, s>>>(t, keys, lens, rids, leaf_in, n, out, recs);
+            probe_kernel<false, 1, 8, 0><<<blocks, 256, 0, s>>>(t, keys, lens, rids, leaf_in, n, out, recs, nullptr,
+                                                                 nullptr);
         else if (tune.store == 2)
-            probe_kernel<false, 1, 8, 2><<<blocks, 256, 0, s>>>(t, keys, lens, rids, leaf_in, n, out, recs);
+            probe_kernel<false, 1, 8, 2><<<blocks, 256, 0, s>>>(t, keys, lens, rids, leaf_in, n, out, recs, nullptr,
+                                                                 nullptr);
         else STAGE_PROBE(false, 1, 8);
     } else {
         if (var) STAGE_PROBE(true, 2, 4);
@@ -2346,6 +2391,22 @@ hipError_t launch_probe(const DevTable &t, const uint64_t *keys, const uint16_t 
     }
 #undef STAGE_PROBE
     return hipGetLastError();
+}
+
+hipError_t launch_probe_fanout(const DevTable &t, const uint64_t *keys, const uint32_t *rids, uint64_t n,
+                               const FanRange *fan, const uint32_t *flist, stage_probe_out_dev *out, uint8_t *recs,
+                               hipStream_t s, const ProbeTuning &tune) {
+    if (!probe_fanout_supported(t)) return hipErrorInvalidValue;
+    if (n == 0) return hipSuccess;
+    if (!recs || !fan) return hipErrorInvalidValue;
+    const int blocks = grid_for((n + 63) / 64, 4, tune.max_blocks > 0 ? tune.max_blocks : 16384);
+    probe_kernel<false, 1, 8, 1, 1, 64, 32, true><<<blocks, 256, 0, s>>>(t, keys, nullptr, rids, nullptr, n, out, recs,
+                                                                         fan, flist);
+    return hipGetLastError();
+}
+
+bool probe_fanout_supported(const DevTable &t) {
+    return t.key_width != 0 && t.key_words == 1 && t.cap == 64 && t.stride <= 1024;
 }
 
 hipError_t launch_resident_reader(const DevTable &t, const ReaderRing &g, hipStream_t s) {

@@ -147,11 +147,11 @@ extern "C" int stage_tpcc_stock_level(stage_table *district, stage_table *order_
         int rc = need_synced(t);
         if (rc) return rc;
     }
-    if (host(district).params().key_width != 16 || host(stock).params().key_width != 16 ||
-        host(order_line).params().key_width != 32)
+    if (facts(district).params().key_width != 16 || facts(stock).params().key_width != 16 ||
+        facts(order_line).params().key_width != 32)
         return fail(STAGE_E_ARG, "expected DistrictKey (16 B), OrderLineKey (32 B), StockKey (16 B) tables");
-    if (host(district).params().payload_size < 4 || host(order_line).params().payload_size < 4 ||
-        host(stock).params().payload_size < 4)
+    if (facts(district).params().payload_size < 4 || facts(order_line).params().payload_size < 4 ||
+        facts(stock).params().payload_size < 4)
         return fail(STAGE_E_ARG, "payloads must hold the 4-byte first column");
     if (district->dev.device != order_line->dev.device || district->dev.device != stock->dev.device)
         return fail(STAGE_E_ARG, "tables on different devices");
@@ -186,16 +186,16 @@ extern "C" int stage_tpcc_stock_level(stage_table *district, stage_table *order_
         // 2. ORDER_LINE range scans of 10 (IndexScanExecutor range branch), all transactions at
         //    once, each kept up to its first produced tuple of order (w, d, o)
         sl_order_keys<<<b256, 256, 0, s>>>(d_w_ids, d_d_ids, n, dout, dt.heap, dt.hstride,
-                                           host(district).key_pad(), d_result, okeys);
+                                           facts(district).key_pad(), d_result, okeys);
         sl_spread_rids<<<bs256, 256, 0, s>>>(d_read_ids, ns, orids);
         hip_check(launch_scan_first(ot, okeys, ns, kLinesPerScan, orids, 3, oimg, ost, s, order_line->scan_tune),
                   "order-line scans");
         // 3. STOCK point lookups of each scan's first item, then the distinct count
         sl_stock_keys<<<bs256, 256, 0, s>>>(d_w_ids, n, d_result, oimg, ost, ot.heap, ot.hstride,
-                                            host(order_line).key_pad(), skeys, has);
+                                            facts(order_line).key_pad(), skeys, has);
         hip_check(launch_probe(st, skeys, nullptr, orids, nullptr, ns, sout, nullptr, s, stock->tune),
                   "stock probe");
-        sl_count<<<(unsigned)n, 64, 0, s>>>(n, d_thresholds, has, sout, st.heap, st.hstride, host(stock).key_pad(),
+        sl_count<<<(unsigned)n, 64, 0, s>>>(n, d_thresholds, has, sout, st.heap, st.hstride, facts(stock).key_pad(),
                                             d_result);
         hip_check(hipGetLastError(), "stock-level kernels");
         return STAGE_OK;

@@ -543,8 +543,8 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
                           offsetof(FinRec, next) == offsetof(HostTable::SlotWords, next) &&
                           offsetof(FinRec, image) == offsetof(HostTable::SlotWords, image),
                       "FinRec / SlotWords layout");
-        t->adopt = std::thread([t, &h, &dv, cap = view.cap, n, cbase, vbase, pin, totals, fr, tot, fin, t0,
-                                t_kernels, t_enqueue, t_reserve]() mutable {
+        t->start_adoption([t, &h, &dv, cap = view.cap, n, cbase, vbase, pin, totals, fr, tot, fin, t0, t_kernels,
+                           t_enqueue, t_reserve]() mutable {
             try {
                 hip_check(hipSetDevice(dv.device), "hipSetDevice");
                 hipStream_t a = dv.adopt_stream;

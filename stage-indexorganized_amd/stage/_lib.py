@@ -76,7 +76,15 @@ SIGNATURES = {
     "stage_probe_sharded_ex": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_uint64, c_vp, c_vp, ctypes.c_int, c_vp]),
     "stage_sharded_owner_rows": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.POINTER(c_vp), c_u64p]),
     "stage_set_shard_dedupe": (ctypes.c_int, [c_vp, ctypes.c_int]),
+    "stage_set_shard_key_bits": (ctypes.c_int, [c_vp, ctypes.c_int]),
+    "stage_settle": (ctypes.c_int, [c_vp]),
+    "stage_rccl_info": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int), ctypes.c_char_p,
+                                       ctypes.c_uint64]),
     "stage_sharded_stats": (ctypes.c_int, [c_vp, ctypes.c_int, c_u64p, c_u64p, c_u64p]),
+    "stage_sharded_stats_ex": (ctypes.c_int, [c_vp, ctypes.c_int, c_u64p, ctypes.c_int]),
+    "stage_comm_allreduce_f64": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_double), ctypes.c_uint64, ctypes.c_int]),
+    "stage_comm_allgather_f64": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_double), ctypes.c_uint64,
+                                                ctypes.POINTER(ctypes.c_double)]),
     "stage_export_leaf_images": (ctypes.c_int64, [c_vp, ctypes.c_uint64, c_vp, c_vp, c_vp]),
     "stage_import_leaf_images": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64, ctypes.c_uint32, c_vp, c_vp, c_u64p]),
     "stage_export_locations": (ctypes.c_int64, [c_vp, ctypes.c_uint64, c_vp, c_vp, c_vp]),

@@ -561,6 +561,47 @@ def set_shard_dedupe(table, on):
     check(lib().stage_set_shard_dedupe(table.h, int(on)), "set_shard_dedupe")
 
 
+def set_shard_key_bits(table, bits):
+    """stage_set_shard_key_bits: the coalescing sort reads the low `bits` key bits (0 = 64);
+    same results for any value, fewer radix passes when every key is < 2^bits."""
+    check(lib().stage_set_shard_key_bits(table.h, int(bits)), "set_shard_key_bits")
+
+
+def rccl_info():
+    """stage_rccl_info: {"runtime": ncclGetVersion, "headers": the version libstage_hip was built
+    against, "path": the file that provided ncclGetVersion in this process}."""
+    rt, hd = ctypes.c_int(), ctypes.c_int()
+    buf = ctypes.create_string_buffer(512)
+    check(lib().stage_rccl_info(ctypes.byref(rt), ctypes.byref(hd), buf, 512), "rccl_info")
+    return {"runtime": rt.value, "headers": hd.value, "path": buf.value.decode()}
+
+
+def sharded_stats_ex(table, loopback=False):
+    """stage_sharded_stats_ex: {keys, routed, remote, received} of the last sharded probe --
+    caller keys, requests routed after coalescing, of those owned by other ranks, and the
+    requests this rank probed as owner."""
+    v = (ctypes.c_uint64 * 4)()
+    check(lib().stage_sharded_stats_ex(table.h, int(loopback), v, 4), "sharded_stats_ex")
+    return dict(zip(("keys", "routed", "remote", "received"), (int(x) for x in v)))
+
+
+def comm_allreduce(table, values, op="sum"):
+    """stage_comm_allreduce_f64 over the table's communicator (op: sum / max / min)."""
+    v = np.ascontiguousarray(values, np.float64).copy()
+    check(lib().stage_comm_allreduce_f64(table.h, v.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), v.size,
+                                         {"sum": 0, "max": 1, "min": 2}[op]), "comm_allreduce")
+    return v
+
+
+def comm_allgather(table, values, world):
+    """stage_comm_allgather_f64: [world, n] array of every rank's values."""
+    v = np.ascontiguousarray(values, np.float64)
+    out = np.zeros((world, v.size), np.float64)
+    check(lib().stage_comm_allgather_f64(table.h, v.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), v.size,
+                                         out.ctypes.data_as(ctypes.POINTER(ctypes.c_double))), "comm_allgather")
+    return out
+
+
 def sharded_stats(table, loopback=True):
     """stage_sharded_stats: (caller keys, routed requests, remote requests) of the last sharded probe."""
     v = [ctypes.c_uint64() for _ in range(3)]

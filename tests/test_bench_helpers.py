@@ -26,3 +26,28 @@ def test_default_args_are_the_c2_bench(monkeypatch):
     monkeypatch.setattr(sys, "argv", ["bench.py"])
     a = bench.parse()
     assert (a.config, a.gpus, a.rows, a.batch, a.steps, a.warmup, a.theta) == ("c2", 1, 100_000_000, 1 << 24, 20, 3, 0.9)
+
+
+def test_sharded_workload_names_world_and_rows():
+    import json
+    import os
+    base = json.load(open(os.path.join(os.path.dirname(bench.__file__), "BASELINE.json")))
+    assert bench.sharded_workload(8, 100_000_000) == base["configs"][4]
+    assert bench.sharded_workload(2, 100_000_000) == \
+        "YCSB-C 200M rows sharded 2 ways, RCCL all-to-all key routing over xGMI, 2×MI355X"
+    assert bench.sharded_workload(4, 100_000_000) != base["configs"][4]
+    assert "rehearsal" in bench.sharded_workload(1, 100_000_000)
+
+
+def test_sharded_hbm_bytes_counts_what_moves():
+    # world 1: everything is own -- owners' probes of the coalesced requests + every caller row
+    st = {"keys": 1000, "routed": 600, "remote": 0, "received": 600}
+    b, parts = bench.sharded_hbm_bytes(st, 1024)
+    assert parts["owner_probes"] == 600 * 1088 and parts["caller_rows"] == 1000 * 1012
+    assert parts["remote_results"] == parts["returned_results"] == parts["key_records"] == 0
+    assert b == 600 * 1088 + 1000 * 1012
+    # world > 1: 500 of 600 requests go out, 480 other-rank requests come in (+ 100 own)
+    st = {"keys": 1000, "routed": 600, "remote": 500, "received": 580}
+    b, parts = bench.sharded_hbm_bytes(st, 1024)
+    assert parts["remote_results"] == 480 * 2 * 1012 and parts["returned_results"] == 500 * 2 * 1012
+    assert parts["key_records"] == (500 + 480) * 32 and b == sum(parts.values())

@@ -25,15 +25,38 @@ def _run(args, env=None, timeout=300):
                           timeout=timeout, env=e, cwd=REPO)
 
 
-def test_launcher_starts_two_ranks():
-    p = _run(["--gpus", "2", "--dry-run", "--steps", "2"])
-    assert p.returncode == 0, p.stderr[-2000:]
+def _dry_line(world):
+    p = _run(["--gpus", str(world), "--dry-run", "--steps", "2", "--cpu-seconds", "0.2", "--cpu-threads", "2"],
+             timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
     lines = [s for s in p.stdout.splitlines() if s.startswith("{")]
     assert len(lines) == 1, p.stdout
-    r = json.loads(lines[0])
-    assert r["n_gpus"] == 2 and r["ranks"] == [0, 1] and r["dry_run"] and r["self_check"]
-    assert sum(r["rows_per_rank"]) == 2 * 200_000 and min(r["rows_per_rank"]) > 0
-    assert r["config"]["parallelism"] == "hash-shard x2"
+    return json.loads(lines[0])
+
+
+def _check_sharded_line(r, world):
+    rows = 200_000
+    assert r["n_gpus"] == world and r["ranks"] == list(range(world)) and r["dry_run"] and r["self_check"]
+    assert sum(r["rows_per_rank"]) == world * rows and min(r["rows_per_rank"]) > 0
+    assert r["config"]["parallelism"] == f"hash-shard x{world}"
+    # the workload names the real world and rows (configs[4]'s string only for 8 x 100M)
+    assert r["config"]["workload"] == bench.sharded_workload(world, rows)
+    assert r["config"]["workload"].startswith(f"YCSB-C {world * rows // 1000}K rows sharded {world} ways")
+    # every N > 1 line carries the per-shard CPU baseline (rank 0, the oracle)
+    cpu = r["cpu_baseline"]
+    assert cpu and cpu["kind"] == "port" and cpu["value"] > 0 and cpu["rows"] == rows and cpu["cores"] >= 1
+    assert "per shard" in cpu["scope"] and cpu["full_txn"]["value"] > 0
+    # per-rank setup phases and host memory, for diagnosing a timeout or OOM from the record
+    assert [p["rank"] for p in r["per_rank"]] == list(range(world))
+    assert all(p["host_peak_rss_gib"] > 0 and set(p["setup_s"]) >= {"owned_keys", "load"} for p in r["per_rank"])
+
+
+def test_launcher_starts_two_ranks():
+    _check_sharded_line(_dry_line(2), 2)
+
+
+def test_launcher_starts_eight_ranks():
+    _check_sharded_line(_dry_line(8), 8)
 
 
 def test_world_size_mismatch_is_refused():

@@ -6,14 +6,16 @@ keys routed to it by an all-to-all.  Checks: shards are disjoint and cover the k
 every routed key lands on the rank whose table holds it, and the per-shard leaf layout is
 what a single loader would build for that shard (against the oracle).  No GPU is touched.
 """
+import multiprocessing as mp
 import os
 import socket
 
 import numpy as np
 import pytest
-import torch
-import torch.distributed as dist
-import torch.multiprocessing as mp
+
+# torch is imported inside the (spawned) workers only, not at collection: a `pytest -m gpu` run
+# collects this module too, and a torch imported there would bring its own HIP runtime and RCCL
+# into the process before libstage_hip's (stage_rccl_info / stage_comm_init check the RCCL)
 
 
 def _free_port():
@@ -26,6 +28,9 @@ def _free_port():
 
 def _worker(rank, world, port, total, q):
     import sys
+
+    import torch
+    import torch.distributed as dist
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, os.path.join(repo, "stage-indexorganized_amd"))
     sys.path.insert(0, os.path.join(repo, "tests"))

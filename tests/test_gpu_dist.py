@@ -1,7 +1,9 @@
 """GPU: the sharded probe front-end.  stage_probe_sharded on a one-rank RCCL communicator
-returns exactly what the direct probe returns (routing, all-to-all-v to self, unpermute); the
-same data path with W = 2, 3, 8 shards on one device (stage_probe_sharded_loopback) returns
-what one table holding every key returns."""
+returns exactly what the direct probe returns (coalescing, routing, the fan-out probe of own
+requests); the same data path with W = 2, 3, 8 shards on one device
+(stage_probe_sharded_loopback) returns what one table holding every key returns -- with and
+without coalescing, hot keys beyond one request's 64 callers, read ids interleaved with keys,
+and tables outside the fan-out probe's geometry (probed, then fanned out by fan_copy)."""
 import ctypes
 
 import numpy as np
@@ -41,12 +43,12 @@ def test_sharded_world1_equals_direct(gpu):
         check(L.stage_comm_destroy(tab.h), "destroy")
 
 
-def shard_tables(keys, world, mode=1):
+def shard_tables(keys, world, mode=1, payload=1000):
     """Rank r's shard: the keys with MurmurHash64A(key, 8, 0) % world == r, in ascending order."""
     h = O.murmur64a_keys(keys, 8, 0)
     tabs = []
     for r in range(world):
-        t = stage.Table(key_width=8)
+        t = stage.Table(key_width=8, payload_size=payload)
         t.load_keys(keys[(h % np.uint64(world)) == np.uint64(r)], 8, mode=mode)
         tabs.append(t)
     return tabs, h
@@ -165,11 +167,10 @@ def test_request_coalescing_zipf_batch(gpu, read_ids):
             pairs = per_keys[r] if per_rids is None else \
                 (per_keys[r] << np.uint64(8)) | per_rids[r].astype(np.uint64)
             if dd:
-                # at least the distinct requests; equal keys with other read ids in between are
-                # separate requests, so only key-only batches must shrink a lot
-                assert np.unique(pairs).size <= routed <= nk
-                if per_rids is None:
-                    assert routed < 0.8 * nk
+                # the distinct (key, read id) requests of each chunk (the sort orders by key, then
+                # read id), plus the cuts of runs longer than 64 callers
+                assert np.unique(pairs).size <= routed <= min(nk, np.unique(pairs).size * 4 + nk // 64 + 4)
+                assert routed < 0.8 * nk
             else:
                 assert routed == nk
     for r in range(world):
@@ -179,5 +180,42 @@ def test_request_coalescing_zipf_batch(gpu, read_ids):
             for f in ("status", "flags", "hops", "key_len", "cstamp", "rec_cstamp", "copy_sstamp"):
                 assert (out[f] == ref_out[f]).all(), (dd, r, f)
             assert (rows == ref_rows).all(), (dd, r)
+    for t in tabs:
+        stage.set_shard_dedupe(t, -1)
+
+
+@pytest.mark.parametrize("world,chunks,payload", [(2, 1, 1000), (3, 3, 1000), (3, 2, 100)])
+def test_hot_keys_and_other_geometries_loopback(gpu, world, chunks, payload):
+    # one key asked 10,000 times in a batch (its run is cut into requests of <= 64 callers, each
+    # fanned out), a few keys a few hundred times, read ids interleaved; payload 100 = leaves of
+    # > 64 slots, outside the fan-out probe: own requests are probed, then fanned out (fan_copy)
+    n = 150_000
+    keys = np.arange(n, dtype=np.uint64)
+    tabs, h = shard_tables(keys, world, payload=payload)
+    full = stage.Table(key_width=8, payload_size=payload)
+    full.load_keys(keys, 8, mode=1)
+    for t in tabs + [full]:
+        t.sync()
+    for t in tabs:
+        check(stage.lib().stage_set_shard_chunks(t.h, chunks), "chunks")
+        stage.set_shard_dedupe(t, 1)
+    rng = np.random.default_rng(world * 10 + chunks)
+    per_keys, per_rids = [], []
+    for r in range(world):
+        k = np.concatenate([np.full(10_000, 4242 + r, np.uint64), np.repeat(rng.integers(0, n, 5), 300),
+                            rng.integers(0, n + 1000, 20_000)]).astype(np.uint64)
+        perm = rng.permutation(k.size)
+        per_keys.append(k[perm])
+        per_rids.append(rng.integers(1, 4, k.size).astype(np.uint32))
+    res = stage.probe_sharded_loopback(tabs, per_keys, per_rids)
+    for r in range(world):
+        out, rows = res[r]
+        ref_out, ref_rows = full.probe(per_keys[r], read_ids=per_rids[r])
+        for f in ("status", "flags", "hops", "key_len", "cstamp", "rec_cstamp", "copy_sstamp"):
+            assert (out[f] == ref_out[f]).all(), (r, f)
+        assert (rows == ref_rows).all(), r
+        nk, routed, remote = stage.sharded_stats(tabs[r])
+        # the 10,000 callers of one key (3 read ids) travel as ~160 requests of <= 64 callers
+        assert routed < 0.7 * nk
     for t in tabs:
         stage.set_shard_dedupe(t, -1)
