@@ -164,6 +164,15 @@ int stage_settle(stage_table *t);
  * little-endian, zero padded (1 word for keys of <= 8 bytes, 2 for 9..16, 4 for 17..32). */
 int stage_insert_key(stage_table *t, const uint8_t *key, uint16_t key_size, const uint8_t *payload,
                      uint32_t commit_id, uint8_t *rc_out);
+/* an uncommitted transaction's insert (InsertExecutor, executor.h:26-85 -> BTree::Insert, which
+ * leaves the record PrepareForInsert: control + visible, cstamp = writer_id, b_tree.cpp:860-864;
+ * other transactions' reads of it return nothing, b_tree.cpp:2087-2095), and the
+ * CommitTransaction INSERT entry that publishes it (FinalizeForInsert(t_cstamp),
+ * transaction_manager.cpp:677-695).  stage_abort_insert_key aborts it. */
+int stage_insert_key_inflight(stage_table *t, const uint8_t *key, uint16_t key_size, const uint8_t *payload,
+                              uint32_t writer_id, uint8_t *rc_out);
+int stage_commit_insert_key(stage_table *t, const uint8_t *key, uint16_t key_size, uint32_t commit_id,
+                            uint8_t *rc_out);
 int stage_load_rows(stage_table *t, const uint8_t *keys, uint32_t key_stride, uint16_t key_size,
                     const uint8_t *payloads, uint32_t payload_stride, uint64_t n, uint32_t commit_id,
                     uint8_t *rc_out, uint64_t *inserted);

@@ -1879,6 +1879,25 @@ uint64_t orc_update_batch(orc_tree *t, const uint64_t *keys, uint32_t key_size, 
 }
 
 /* BTree::FinalizeUpdate, b_tree.cpp:2252-2268: cstamp := commit_id, next_ptr untouched */
+/* InsertExecutor of a transaction that has not committed yet: BTree::Insert leaves the record
+ * PrepareForInsert (control + visible, cstamp = the writer's read id, b_tree.cpp:860-864; next
+ * pointer 0), so a reader's BTree::Read finds it inserting without an overwrite copy and returns
+ * nullptr (b_tree.cpp:2087-2095). */
+int orc_insert_inflight(orc_tree *t, const uint8_t *key, uint32_t key_size, const uint8_t *payload,
+                        uint32_t writer_id) {
+    orc_rmeta *mp = NULL;
+    return btree_insert(t, key, (uint16_t)key_size, payload, writer_id, &mp);
+}
+
+/* CommitTransaction INSERT entry (transaction_manager.cpp:677-695):
+ * FinalizeForInsert(offset, key_len, t_cstamp) -- visible, control cleared, cstamp = commit id */
+int orc_commit_insert(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t commit_id) {
+    orc_rmeta *mp = find_meta(t, key, (uint16_t)key_size, NULL);
+    if (!mp || !m_inserting(mp->meta)) return ORC_RET_NOT_FOUND;
+    mp->meta = m_finalize_insert(m_offset(mp->meta), m_keylen(mp->meta), commit_id);
+    return ORC_RET_OK;
+}
+
 int orc_finalize_update(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t commit_id) {
     orc_rmeta *mp = find_meta(t, key, (uint16_t)key_size, NULL);
     if (!mp) return ORC_RET_NOT_FOUND;

@@ -53,6 +53,10 @@ void orc_tree_free(orc_tree *t);
 /* BTree::Insert + BTree::FinalizeInsert (loader semantics, ycsb_loader.cpp:152-171) */
 int orc_insert(orc_tree *t, const uint8_t *key, uint32_t key_size, const uint8_t *payload,
                uint32_t commit_id);
+/* an uncommitted transaction's insert (PrepareForInsert, cstamp = writer id) and its commit */
+int orc_insert_inflight(orc_tree *t, const uint8_t *key, uint32_t key_size, const uint8_t *payload,
+                        uint32_t writer_id);
+int orc_commit_insert(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t commit_id);
 /* LoadYCSBRows (ycsb_loader.cpp:93-171) single loader, rows [begin,end), key = rowid as
  * key_size (4 or 8) little-endian bytes.  payload_mode 0 = reference memset(rowid),
  * 1 = "strong" per-word pattern (stage_payload_word).  Returns rows inserted. */

@@ -173,6 +173,26 @@ int stage_insert_key(stage_table *t, const uint8_t *key, uint16_t key_size, cons
     });
 }
 
+int stage_insert_key_inflight(stage_table *t, const uint8_t *key, uint16_t key_size, const uint8_t *payload,
+                              uint32_t writer_id, uint8_t *rc_out) {
+    if (!t || !key || !payload) return fail(STAGE_E_ARG, "null argument");
+    return guarded([&] {
+        int rc = host(t).insert(key, key_size, payload, 0, 0, writer_id, true);
+        if (rc_out) *rc_out = (uint8_t)rc;
+        return STAGE_OK;
+    });
+}
+
+int stage_commit_insert_key(stage_table *t, const uint8_t *key, uint16_t key_size, uint32_t commit_id,
+                            uint8_t *rc_out) {
+    if (!t || !key) return fail(STAGE_E_ARG, "null argument");
+    return guarded([&] {
+        int rc = host(t).commit_insert(key, key_size, commit_id);
+        if (rc_out) *rc_out = (uint8_t)rc;
+        return STAGE_OK;
+    });
+}
+
 int stage_load_rows(stage_table *t, const uint8_t *keys, uint32_t key_stride, uint16_t key_size,
                     const uint8_t *payloads, uint32_t payload_stride, uint64_t n, uint32_t commit_id,
                     uint8_t *rc_out, uint64_t *inserted) {

@@ -281,7 +281,7 @@ void HostTable::materialize_device_rows(const std::function<void(uint64_t, uint6
 }
 
 int HostTable::insert(const uint8_t *key, uint32_t len, const uint8_t *payload, uint64_t gen_rowid, int mode,
-                      uint32_t commit_id) {
+                      uint32_t commit_id, bool inflight) {
     if (!key_ok(len)) return STAGE_RC_INVALID;
     const Key k = make_key(key, len, uns_);
     const uint32_t rec = (len > 8 ? pad8(len) : 8u) + p_.payload_size;
@@ -305,8 +305,9 @@ int HostTable::insert(const uint8_t *key, uint32_t len, const uint8_t *payload, 
         const uint64_t offset = p_.leaf_node_size - L.block;
         const size_t i = (size_t)leaf * cap_ + slot;
         set_slot_key(i, k);
-        // PrepareForInsert then FinalizeInsert: control bit cleared, cstamp = commit_id
-        meta_[i] = ((uint64_t)len << 48) | kMetaVisible | (offset << 32) | commit_id;
+        // PrepareForInsert (b_tree.cpp:860-864), then -- unless the inserting transaction is
+        // still in flight -- FinalizeInsert: control bit cleared, cstamp = commit_id
+        meta_[i] = ((uint64_t)len << 48) | kMetaVisible | (offset << 32) | commit_id | (inflight ? kMetaControl : 0);
         next_[i] = 0;
         image_[i] = new_image(key, len, payload, gen_rowid, mode);
         loc_[i] = (uint32_t)(lid + 1);
@@ -549,6 +550,18 @@ int HostTable::abort_insert(const uint8_t *key, uint32_t len) {
     if (loc_[i]) locpos_[loc_[i] - 1] = kNoPos;
     loc_[i] = 0;
     clear_slot_key(i);
+    touch(leaf, slot);
+    return STAGE_RC_OK;
+}
+
+// CommitTransaction INSERT entry (transaction_manager.cpp:677-695): FinalizeForInsert(offset,
+// key_len, t_cstamp) on a record an in-flight insert left PrepareForInsert.
+int HostTable::commit_insert(const uint8_t *key, uint32_t len, uint32_t commit_id) {
+    uint32_t leaf, slot;
+    if (find(key, len, &leaf, &slot) < 0) return STAGE_RC_NOT_FOUND;
+    const size_t i = (size_t)leaf * cap_ + slot;
+    if (!meta_inserting(meta_[i]) || next_[i] != 0) return STAGE_RC_NOT_FOUND;
+    meta_[i] = ((meta_[i] & ~kMetaTxn) | commit_id | kMetaVisible) & ~kMetaControl;
     touch(leaf, slot);
     return STAGE_RC_OK;
 }

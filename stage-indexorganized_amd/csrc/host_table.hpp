@@ -78,8 +78,11 @@ public:
     Key key_of(const uint8_t *bytes, uint32_t len) const { return make_key(bytes, len, uns_); }
 
     // write path, reference ReturnCode values; keys as bytes (len <= 32)
+    // inflight: an uncommitted transaction's insert -- the record stays PrepareForInsert
+    // (control + visible, cstamp = commit_id = the writer's read id) until commit_insert
     int insert(const uint8_t *key, uint32_t len, const uint8_t *payload, uint64_t gen_rowid, int mode,
-               uint32_t commit_id);
+               uint32_t commit_id, bool inflight = false);
+    int commit_insert(const uint8_t *key, uint32_t len, uint32_t commit_id);
     int update(const uint8_t *key, uint32_t len, uint32_t payload_off, const uint8_t *delta, uint32_t delta_len,
                uint32_t writer_id);
     int commit_update(const uint8_t *key, uint32_t len, uint32_t commit_id, uint32_t sstamp);

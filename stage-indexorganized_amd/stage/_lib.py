@@ -48,6 +48,8 @@ SIGNATURES = {
     "stage_update_batch_device": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_uint64, ctypes.c_uint32, c_vp,
                                                  ctypes.c_uint32, c_vp, c_vp, c_vp, c_vp, c_u64p, c_vp]),
     "stage_insert_key": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint16, c_vp, ctypes.c_uint32, c_u8p]),
+    "stage_insert_key_inflight": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint16, c_vp, ctypes.c_uint32, c_u8p]),
+    "stage_commit_insert_key": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint16, ctypes.c_uint32, c_u8p]),
     "stage_load_rows": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint32, ctypes.c_uint16, c_vp, ctypes.c_uint32,
                                        ctypes.c_uint64, ctypes.c_uint32, c_vp, c_u64p]),
     "stage_update_key": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint16, ctypes.c_uint32, c_vp, ctypes.c_uint32,

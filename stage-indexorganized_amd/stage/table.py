@@ -348,6 +348,24 @@ class Table:
               "insert_key")
         return rc.value
 
+    def insert_key_inflight(self, key, payload, writer_id):
+        """stage_insert_key_inflight: an uncommitted transaction's insert (PrepareForInsert)"""
+        k = np.frombuffer(bytes(key), np.uint8)
+        p = np.frombuffer(bytes(payload), np.uint8)
+        assert p.size == self.payload_size
+        rc = ctypes.c_uint8()
+        check(lib().stage_insert_key_inflight(self.h, k.ctypes.data, k.size, p.ctypes.data, writer_id,
+                                              ctypes.byref(rc)), "insert_key_inflight")
+        return rc.value
+
+    def commit_insert_key(self, key, commit_id):
+        """stage_commit_insert_key: CommitTransaction INSERT entry (FinalizeForInsert(t_cstamp))"""
+        k = np.frombuffer(bytes(key), np.uint8)
+        rc = ctypes.c_uint8()
+        check(lib().stage_commit_insert_key(self.h, k.ctypes.data, k.size, commit_id, ctypes.byref(rc)),
+              "commit_insert_key")
+        return rc.value
+
     def load_rows(self, keys, payloads, commit_id=0):
         """keys (n, width) uint8, payloads (n, payload_size) uint8 -> (rc per row, inserted)."""
         keys = np.ascontiguousarray(keys, np.uint8)

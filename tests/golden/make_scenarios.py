@@ -8,11 +8,20 @@ the intended semantics, which the fixture pins).  Ids follow the reference's tid
 (transaction_manager.cpp:14, :287 BeginTransaction read_id = counter++, :552 commit id =
 counter++, aborts take no commit id); the counter starts at TID0 = 1 here (the reference's
 process-wide counter starts at INVALID_CID = 0 and keeps counting across tests).
+TransactionScheduler tests (testing_transaction_util.h:203-309) run their ops one at a time in
+the written order; a txn begins (read id = counter++) at its first op; an explicit Abort() op
+takes a counter value (GetNextCurrentTidCounter, :275); a txn whose op failed (e.g. an update
+of a record another txn is updating: Dirty) is aborted on the spot without one, and its later
+ops are skipped (:221-224, :302-308).  Reads with is_for_update = true (the writer's own-write
+reads) are not restated: that path stays on the host.
 
 Op vocabulary (keys: "key" = u64 little-endian of key_size bytes, "key_str" = ASCII bytes):
   insert        key, payload_u64 (payload = those u64 words), cid: Insert + FinalizeInsert
                 (InsertExecutor + CommitTransaction INSERT: FinalizeForInsert(t_cstamp))
   insert_abort  key, payload_u64, wid: Insert by an aborting txn + AbortTransaction INSERT
+  insert_inflight key, payload_u64, wid: Insert by a txn that has not committed (the record
+                stays PrepareForInsert, b_tree.cpp:860-864)
+  commit_insert key, cid: CommitTransaction INSERT entry (FinalizeForInsert(t_cstamp), :677-695)
   update        key, off, payload_u64, wid: LeafNode::Update (PointUpdateExecutor), expect_rc
   commit_update key, cid: CommitTransaction UPDATE entry (sstamp = cid, single writer)
   abort_update  key: AbortTransaction UPDATE entry
@@ -135,12 +144,14 @@ def abort_version_chain_test():
     r0 = tid.next()  # Txn(0).Update(1, 100) ; Txn(0).Abort()
     ops.append({"op": "update", "key": 1, "off": 0, "payload_u64": [100], "wid": r0, "expect_rc": 1, "src": ":523"})
     ops.append({"op": "abort_update", "key": 1, "expect_rc": 1, "src": ":524"})
+    tid.next()  # the explicit Abort() takes a counter value
     r1 = tid.next()  # Txn(1).Read(1) -> 0
     ops.append({"op": "read", "key": 1, "rid": r1, "expect": {"found": True, "payload_u64": [0]},
                 "src": ":525-529 (assert results[0] == 0)"})
     tid.next()
     r0 = tid.next()  # Txn(0).Insert(100, 0) ; Abort
     ops.append({"op": "insert_abort", "key": 100, "payload_u64": [0], "wid": r0, "src": ":534-535"})
+    tid.next()  # Abort()
     r1 = tid.next()  # Txn(1).Read(100) -> -1
     ops.append({"op": "read", "key": 100, "rid": r1, "expect": {"found": False},
                 "src": ":536-540 (assert results[0] == -1)"})
@@ -175,6 +186,211 @@ def mvcc_test():
     tid.next()
     return {"name": "ExecuteTest.MVCCTest", "source": "test/testing_execute.cpp:1397-1424", "table": CT_TABLE,
             "ops": ops}
+
+
+def read(key, rid, value, src):
+    """a point lookup of another transaction; value None = no tuple (-1)"""
+    exp = {"found": False} if value is None else {"found": True, "payload_u64": [value]}
+    return {"op": "read", "key": key, "rid": rid, "expect": exp, "src": src}
+
+
+def upd(key, value, wid, src, rc=1):
+    """TestingTransactionUtil::ExecuteUpdate: column 1 (the value) := value (testing_transaction_util.cpp:139-160)"""
+    return {"op": "update", "key": key, "off": 0, "payload_u64": [value], "wid": wid, "expect_rc": rc, "src": src}
+
+
+def concurrent_transaction_tests():
+    """TEST_F(ExecuteTest, ConcurrentTransactionTest), test/testing_execute.cpp:808-871, two
+    schedules on fresh tables.  Not restated: Txn 0's own-write reads (Read(.., true))."""
+    out = []
+    # :819-836 Txn0 inserts key 100; Txn1 reads it in flight and after Txn0's commit: both -1
+    tid = Counter()
+    ops = create_table(tid)
+    r0 = tid.next()
+    ops.append({"op": "insert_inflight", "key": 100, "payload_u64": [1], "wid": r0, "src": ":819 Insert(100, 1)"})
+    r1 = tid.next()
+    ops.append(read(100, r1, None, ":820 (assert :832 schedules[1].results[0] == -1): an uncommitted insert"))
+    c0 = tid.next()
+    ops.append({"op": "commit_insert", "key": 100, "cid": c0, "src": ":822 Txn(0).Commit()"})
+    ops.append(read(100, r1, None, ":823 (assert :836 results[1] == -1): committed after Txn1 began (no version)"))
+    tid.next()  # Txn1 commit
+    ops.append(read(100, tid.next(), 1, "derived: a txn that begins after the commit reads it (latest)"))
+    out.append({"name": "ExecuteTest.ConcurrentTransactionTest/insert", "source": "test/testing_execute.cpp:810-839",
+                "table": CT_TABLE, "ops": ops})
+    # :849-866 Txn0 updates key 0 to 1; Txn1 reads it in flight and after the commit: both 0
+    tid = Counter()
+    ops = create_table(tid)
+    r0 = tid.next()
+    ops.append(upd(0, 1, r0, ":849 Update(0, 1)"))
+    r1 = tid.next()
+    ops.append(read(0, r1, 0, ":850 (assert :865 results[0] == 0): the overwrite copy"))
+    c0 = tid.next()
+    ops.append({"op": "commit_update", "key": 0, "cid": c0, "src": ":852"})
+    ops.append(read(0, r1, 0, ":853 (assert :866 results[1] == 0): the retired version"))
+    tid.next()
+    out.append({"name": "ExecuteTest.ConcurrentTransactionTest/update", "source": "test/testing_execute.cpp:841-869",
+                "table": CT_TABLE, "ops": ops})
+    return out
+
+
+def multi_transaction_test():
+    """TEST_F(ExecuteTest, MultiTransactionTest), test/testing_execute.cpp:873-1004: five
+    schedules on one table.  Scan(-1) passes the 4-byte int -1 as an 8-byte key
+    (testing_transaction_util.cpp:182, the upper 4 bytes are whatever follows it): its first
+    byte 0xFF is -1 under KeyCompare's signed bytes, below every key, so the 20-record scan
+    returns all 10 rows -- results.size() == 10.  The upper bytes are taken as 0 here."""
+    tid = Counter()
+    ops = create_table(tid)
+    start = 0xFFFFFFFF
+    keys = list(range(10))
+    scan = lambda src: {"op": "scan", "key": start, "size": 20, "expect_keys": keys, "src": src}
+    # :889-905
+    tid.next()
+    ops.append(scan(":890 Txn(0).Scan(-1, true) (assert :905 results.size() == 10)"))
+    tid.next()
+    ops.append(scan(":891 Txn(1).Scan(-1)"))
+    tid.next()  # Txn1 commit
+    tid.next()
+    ops.append(scan(":893 Txn(2).Scan(-1, true)"))
+    tid.next()
+    tid.next()
+    # :913-925
+    tid.next()
+    ops.append(scan(":914 Txn(0).Scan(-1, true)"))
+    tid.next()  # Abort()
+    tid.next()
+    ops.append(scan(":916 Txn(1).Scan(-1, true) (assert :925 results.size() == 10)"))
+    tid.next()
+    # :933-943
+    r0 = tid.next()
+    ops.append(read(0, r0, 0, ":934 Txn(0).Read(0)"))
+    tid.next()  # Abort()
+    r1 = tid.next()
+    ops.append(read(0, r1, 0, ":936 (assert :943 results.size() == 1; key 0 holds 0)"))
+    tid.next()
+    # :949-971
+    r0 = tid.next()
+    for k, line in enumerate((950, 951, 952, 953)):
+        ops.append(read(0, r0, 0, f":{line} (assert :{965 + k} results[{k}] == 0)"))
+    ops.append(upd(0, 1, r0, ":954 Update(0, 1)"))
+    ops.append(read(100, r0, None, ":956 Read(100, true) of a missing key (assert :970 results[5] == -1)"))
+    c0 = tid.next()
+    ops.append({"op": "commit_update", "key": 0, "cid": c0, "src": ":957"})
+    r1 = tid.next()
+    ops.append(read(0, r1, 1, ":958 (assert :971 schedules[1].results[0] == 1)"))
+    tid.next()
+    # :977-998 commit / abort with part of the read tuples updated
+    r0 = tid.next()
+    ops.append(read(3, r0, 0, ":978"))
+    ops.append(read(4, r0, 0, ":979"))
+    ops.append(upd(3, 1, r0, ":980 Update(3, 1)"))
+    ops.append({"op": "abort_update", "key": 3, "expect_rc": 1, "src": ":981 Abort()"})
+    tid.next()
+    r1 = tid.next()
+    ops.append(read(3, r1, 0, ":982 (assert :995 results[0] == 0)"))
+    ops.append(read(4, r1, 0, ":983 (assert :996 results[1] == 0)"))
+    ops.append(upd(3, 2, r1, ":984 Update(3, 2)"))
+    c1 = tid.next()
+    ops.append({"op": "commit_update", "key": 3, "cid": c1, "src": ":985"})
+    r2 = tid.next()
+    ops.append(read(3, r2, 2, ":986 (assert :997 schedules[2].results[0] == 2)"))
+    ops.append(read(4, r2, 0, ":987 (assert :998 results[1] == 0)"))
+    tid.next()
+    return {"name": "ExecuteTest.MultiTransactionTest", "source": "test/testing_execute.cpp:873-1004",
+            "table": CT_TABLE, "ops": ops}
+
+
+def dirty_write_tests():
+    """TEST_F(ExecuteTest, DirtyWriteTest), test/testing_execute.cpp:1007-1225: Txn0 and Txn1
+    update key 0 one after the other; Txn1's update meets Txn0's in-flight record (Dirty), so
+    Txn1 is aborted on the spot (asserted ABORTED in every schedule) and its Commit / Abort op is
+    skipped; the observer Txn2 reads what Txn0's end left."""
+    out = []
+    cases = [("T0 commit, T1 commit", "commit", 1, ":1018-1038"), ("T1 commit, T0 commit", "commit", 1, ":1053-1072"),
+             ("T0 abort, T1 commit", "abort", 0, ":1086-1107"), ("T1 commit, T0 abort", "abort", 0, ":1126-1142"),
+             ("T0 abort, T1 abort", "abort", 0, ":1157-1178"), ("T1 abort, T0 abort", "abort", 0, ":1194-1215")]
+    for name, t0_end, value, src in cases:
+        tid = Counter()
+        ops = create_table(tid)
+        r0 = tid.next()
+        ops.append(upd(0, 1, r0, "Txn(0).Update(0, 1)"))
+        r1 = tid.next()
+        ops.append(upd(0, 2, r1, "Txn(1).Update(0, 2): Dirty, Txn1 aborted", rc=9))
+        if t0_end == "commit":
+            ops.append({"op": "commit_update", "key": 0, "cid": tid.next(), "src": "Txn(0).Commit()"})
+        else:
+            ops.append({"op": "abort_update", "key": 0, "expect_rc": 1, "src": "Txn(0).Abort()"})
+            tid.next()
+        r2 = tid.next()
+        last = src.split("-")[1]
+        ops.append(read(0, r2, value, f"observer Txn(2).Read(0) (assert :{last} results[0] == {value})"))
+        tid.next()
+        out.append({"name": f"ExecuteTest.DirtyWriteTest/{name}", "source": f"test/testing_execute.cpp{src}",
+                    "table": CT_TABLE, "ops": ops})
+    return out
+
+
+def dirty_read_tests():
+    """TEST_F(ExecuteTest, DirtyReadTest), test/testing_execute.cpp:1227-1304: Txn1 reads key 0
+    while Txn0's update is in flight -- the overwrite copy (old value) -- then Txn0 commits or
+    aborts and the observer reads the outcome."""
+    out = []
+    for name, t0_end, value, src, a1, a2 in (("commit", "commit", 1, ":1229-1264", 1258, 1259),
+                                            ("abort", "abort", 0, ":1266-1301", 1295, 1296)):
+        tid = Counter()
+        ops = create_table(tid)
+        r0 = tid.next()
+        ops.append(upd(0, 1, r0, "Txn(0).Update(0, 1)"))
+        r1 = tid.next()
+        ops.append(read(0, r1, 0, f"Txn(1).Read(0) during the update (assert :{a1} results[0] == 0)"))
+        if t0_end == "commit":
+            ops.append({"op": "commit_update", "key": 0, "cid": tid.next(), "src": "Txn(0).Commit()"})
+        else:
+            ops.append({"op": "abort_update", "key": 0, "expect_rc": 1, "src": "Txn(0).Abort()"})
+            tid.next()
+        tid.next()  # Txn1 commit
+        r2 = tid.next()
+        ops.append(read(0, r2, value, f"observer (assert :{a2} results[0] == {value})"))
+        tid.next()
+        out.append({"name": f"ExecuteTest.DirtyReadTest/{name}", "source": f"test/testing_execute.cpp{src}",
+                    "table": CT_TABLE, "ops": ops})
+    return out
+
+
+def fuzzy_read_tests():
+    """TEST_F(ExecuteTest, FuzzyReadTest), test/testing_execute.cpp:1306-1395: a reader that
+    began before a concurrent update commits keeps reading the old version (TupleHeader chain)."""
+    out = []
+    # :1315-1341: T0 begins first
+    tid = Counter()
+    ops = create_table(tid)
+    r0 = tid.next()
+    ops.append(read(0, r0, 0, ":1322 (assert :1338 results[0] == 0)"))
+    r1 = tid.next()
+    ops.append(upd(0, 1, r1, ":1323 Txn(1).Update(0, 1)"))
+    ops.append({"op": "commit_update", "key": 0, "cid": tid.next(), "src": ":1324"})
+    ops.append(read(0, r0, 0, ":1325 should read the old version (assert :1339 results[1] == 0)"))
+    tid.next()
+    ops.append(read(0, tid.next(), 1, "observer (assert :1341 results[0] == 1)"))
+    tid.next()
+    out.append({"name": "ExecuteTest.FuzzyReadTest/reader-first", "source": "test/testing_execute.cpp:1308-1346",
+                "table": CT_TABLE, "ops": ops})
+    # :1355-1387: T1 begins first, reads, T0 reads, T1 updates + commits, T0 reads again
+    tid = Counter()
+    ops = create_table(tid)
+    r1 = tid.next()
+    ops.append(read(0, r1, 0, ":1363 (assert :1384 schedules[1].results[0] == 0)"))
+    r0 = tid.next()
+    ops.append(read(0, r0, 0, ":1364 (assert :1382 results[0] == 0)"))
+    ops.append(upd(0, 1, r1, ":1365 Txn(1).Update(0, 1)"))
+    ops.append({"op": "commit_update", "key": 0, "cid": tid.next(), "src": ":1366"})
+    ops.append(read(0, r0, 0, ":1367 (assert :1383 results[1] == 0)"))
+    tid.next()
+    ops.append(read(0, tid.next(), 1, "observer (assert :1387 results[0] == 1)"))
+    tid.next()
+    out.append({"name": "ExecuteTest.FuzzyReadTest/writer-first", "source": "test/testing_execute.cpp:1348-1392",
+                "table": CT_TABLE, "ops": ops})
+    return out
 
 
 BT_TABLE = {"key_size": 0, "payload_size": 8, "split_threshold": 3072, "merge_threshold": 1024,
@@ -226,7 +442,8 @@ def btree_upsert_test():
 
 def main():
     scen = [basic_transaction_test(), abort_version_chain_test(), mvcc_test(), btree_update_test(),
-            btree_upsert_test()]
+            btree_upsert_test()] + concurrent_transaction_tests() + [multi_transaction_test()] + \
+        dirty_write_tests() + dirty_read_tests() + fuzzy_read_tests()
     doc = {"generator": "tests/golden/make_scenarios.py", "tid0": TID0, "scenarios": scen}
     with open(OUT, "w") as f:
         json.dump(doc, f, indent=1)

@@ -24,6 +24,8 @@ _SIG = {
     "orc_tree_set_merge_threshold": (None, [vp, u32]),
     "orc_tree_free": (None, [vp]),
     "orc_insert": (ctypes.c_int, [vp, vp, u32, vp, u32]),
+    "orc_insert_inflight": (ctypes.c_int, [vp, vp, u32, vp, u32]),
+    "orc_commit_insert": (ctypes.c_int, [vp, vp, u32, u32]),
     "orc_load_ycsb": (u64, [vp, u64, u64, u32, ctypes.c_int]),
     "orc_load_keys": (u64, [vp, vp, u64, u32, ctypes.c_int]),
     "orc_read": (ctypes.c_int, [vp, vp, u32, u32, vp, vp]),
@@ -115,6 +117,16 @@ class OracleTree:
         pb = bytes(payload)
         assert len(pb) == self.payload_size
         return lib().orc_insert(self.t, kb, key_size, pb, commit_id)
+
+    def insert_inflight(self, key, key_size, payload, writer_id):
+        """an uncommitted transaction's insert (PrepareForInsert, cstamp = writer id)"""
+        pb = bytes(payload)
+        assert len(pb) == self.payload_size
+        return lib().orc_insert_inflight(self.t, key_bytes(key, key_size), key_size, pb, writer_id)
+
+    def commit_insert(self, key, key_size, commit_id):
+        """CommitTransaction INSERT entry (FinalizeForInsert(t_cstamp))"""
+        return lib().orc_commit_insert(self.t, key_bytes(key, key_size), key_size, commit_id)
 
     def load_ycsb(self, begin, end, key_size, mode=0):
         return lib().orc_load_ycsb(self.t, begin, end, key_size, mode)

@@ -63,6 +63,10 @@ class OracleBackend:
             rc = self.t.insert(k, ks, payload(op, self.ps).tobytes(), op["wid"])
             assert rc == 1, rc
             return self.t.abort_insert(k, ks)
+        if o == "insert_inflight":
+            return self.t.insert_inflight(k, ks, payload(op, self.ps).tobytes(), op["wid"])
+        if o == "commit_insert":
+            return self.t.commit_insert(k, ks, op["cid"])
         if o == "update":
             d = np.array(op["payload_u64"], np.uint64).view(np.uint8).tobytes()
             return self.t.update(k, ks, op["off"], d, op["wid"])
@@ -110,6 +114,10 @@ class DeviceBackend:
             rc = t.insert_key(k, payload(op, self.ps).tobytes(), op["wid"])
             assert rc == 1, rc
             return t.abort_insert_key(k)
+        if o == "insert_inflight":
+            return t.insert_key_inflight(k, payload(op, self.ps).tobytes(), op["wid"])
+        if o == "commit_insert":
+            return t.commit_insert_key(k, op["cid"])
         if o == "update":
             d = np.array(op["payload_u64"], np.uint64).view(np.uint8).tobytes()
             return t.update_key(k, op["off"], d, op["wid"])

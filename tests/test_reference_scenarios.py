@@ -1,7 +1,8 @@
 """CPU: the reference's transaction-level unit tests on the visibility path, restated as op
 sequences (tests/golden/reference_test_scenarios.json, made by tests/golden/make_scenarios.py
 from testing_execute.cpp BasicTransactionTest incl. Lookup-Old, AbortVersionChainTest,
-MVCCTest and testing_btree.cpp Update / Upsert):
+ConcurrentTransactionTest, MultiTransactionTest, DirtyWriteTest (observer reads), DirtyReadTest,
+FuzzyReadTest, MVCCTest and testing_btree.cpp Update / Upsert):
 
 * the oracle meets every expected outcome the reference tests assert;
 * the product's host write path (insert / update / commit / abort / delete on the C-ABI)
@@ -44,4 +45,13 @@ def test_fixture_covers_the_cited_assertions():
     srcs = " ".join(op["src"] for s in SCEN for op in s["ops"])
     for cited in (":371-418 Lookup-Old", ":525-529", ":536-540", ":1414", ":557-565", ":569-575"):
         assert cited in srcs
+    # round 3: the other-transaction read path of the scheduler tests
+    assert {"ExecuteTest.ConcurrentTransactionTest/insert", "ExecuteTest.ConcurrentTransactionTest/update",
+            "ExecuteTest.MultiTransactionTest", "ExecuteTest.DirtyReadTest/commit", "ExecuteTest.DirtyReadTest/abort",
+            "ExecuteTest.FuzzyReadTest/reader-first", "ExecuteTest.FuzzyReadTest/writer-first"} <= names
+    assert sum(n.startswith("ExecuteTest.DirtyWriteTest/") for n in names) == 6
+    for cited in (":832", ":836", ":865", ":866", ":905", ":925", ":943", ":965", ":970", ":971", ":995", ":998",
+                  ":1038", ":1072", ":1107", ":1142", ":1178", ":1215", ":1258", ":1259", ":1295", ":1296",
+                  ":1338", ":1339", ":1341", ":1382", ":1383", ":1384", ":1387"):
+        assert f"assert {cited}" in srcs, cited
     assert stage.RC_NOT_NEEDED_UPDATE == 7
