@@ -107,6 +107,21 @@ static void build_leaf(const HostTable &h, uint32_t hl, uint8_t *hd, uint64_t *o
         }
         for (uint32_t j = 0; j < kw; ++j) std::memcpy(gm + g * kw + j, &best[j], 8);
     }
+    // info word: count | mp << 16, mp = the longest slot prefix with strictly increasing keys
+    uint32_t mp = count ? 1u : 0u;
+    while (mp < count) {
+        const uint64_t *a = h.okey_.data() + (hbase + mp - 1) * kw, *b = a + kw;
+        bool lt = false;
+        for (uint32_t j = 0; j < kw; ++j)
+            if (a[j] != b[j]) {
+                lt = a[j] < b[j];
+                break;
+            }
+        if (!lt) break;
+        ++mp;
+    }
+    const uint32_t info = count | (mp << 16);
+    std::memcpy(hd + head_info_offset(cap, kw), &info, 4);
 }
 
 // grow a device buffer to `bytes`, keeping its first `keep` bytes

@@ -1876,6 +1876,203 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     }
 }
 
+// The first-tuple scans without the wave-serial stage of scan_first_split_kernel, for the
+// leaves' monotone prefix: the head info word carries the leaf's record count and the length mp
+// of its longest slot prefix whose keys increase (>= the sorted region, RangeScanBySize's
+// reference layout after a split; the whole leaf for a table loaded in key order).
+// RangeScanBySize keeps the first to_scan + 1 visible records with key >= x in slot order
+// (b_tree.cpp:1276-1302): when the monotone prefix alone holds that many from p =
+// lower_bound(x) on, they are its visible slots from p on, already in key order, so the first
+// candidates in rank order are the first visible slots >= p.  Per chunk of 16 scans, 4 lanes per
+// scan (lane L: scan L/4, part L%4), every step one round trip for all 16:
+//   1. the start leaf (chunk_lower_bound);
+//   2. the info word, group maxima and visible masks (a quarter per lane);
+//   3. p: the first full monotone group whose max key is >= x (or the partial one), then a 5-ary
+//      search in it, the 4 lanes comparing 4 pivots (64 -> 12 -> 2 -> 0 slots);
+//   4. the first 4 visible slots >= p, one per lane: key prefix and slot word, visibility
+//      (scan_visible); the lowest passing one in slot order is the scan's tuple.
+// Scans this does not decide -- fewer than to_scan + 1 visible records in [p, mp) while records
+// follow mp, or no pass among the first 4 candidates while more candidates or an Iterator
+// continuation remain -- are left to scan_first_rest_kernel (kFirstUndecided).
+template <int SPL, int KW, int WPE = 8>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void scan_first_mono_kernel(
+    DevTable t, const uint64_t *__restrict__ keys,
+                                                              uint64_t n, uint32_t scan_size,
+                                                              const uint32_t *__restrict__ rids, uint32_t words,
+                                                              uint32_t *__restrict__ img_out,
+                                                              uint8_t *__restrict__ st_out) {
+    static_assert(SPL <= 16, "visible masks: up to 4 words per lane");
+    const uint32_t lane = lane_id(), part = lane & 3, quad = lane & ~3u;
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + uni32(threadIdx.x >> 6);
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint32_t len = t.key_width;
+    constexpr int VPL = SPL >= 4 ? SPL / 4 : 1;  // visible-mask words per lane
+    for (uint64_t c0 = wave * kFirstChunk; c0 < n; c0 += nwaves * kFirstChunk) {
+        const uint64_t i = c0 + (lane >> 2);
+        const bool valid = i < n;
+        uint64_t x[KW];
+        load_okey<KW>(keys, i, valid, len, x);
+        const uint32_t leaf = chunk_lower_bound<KW>(t, x, part);
+        const uint32_t rid = valid && rids ? rids[i] : 0xFFFFFFFEu;
+        // 2. info word, group maxima (groups part, part + 4, ...), visible masks (words part * VPL ..)
+        const uint8_t *hd = t.head + (uint64_t)leaf * t.head_bytes;
+        const uint32_t info = *reinterpret_cast<const uint32_t *>(hd + head_info_offset(t.cap, KW));
+        const uint64_t *gm = reinterpret_cast<const uint64_t *>(hd + head_gmax_offset(t.cap));
+        uint32_t actv = 0;
+#pragma unroll
+        for (int g = 0; g < SPL; g += 4) {
+            const uint32_t gg = (uint32_t)g + part;
+            if (gg < (uint32_t)SPL) {
+                uint64_t e[KW];
+#pragma unroll
+                for (int w = 0; w < KW; ++w) e[w] = gm[gg * KW + w];
+                actv |= kw_lt<KW>(e, x) ? 0u : (1u << gg);
+            }
+        }
+        uint64_t vis[VPL];
+#pragma unroll
+        for (int k = 0; k < VPL; ++k) {
+            const uint32_t wi = part * VPL + (uint32_t)k;
+            vis[k] = wi < (uint32_t)SPL ? head_vis(t, leaf, (int)wi) : 0ull;
+        }
+        actv |= (uint32_t)__shfl_xor((int)actv, 1);
+        actv |= (uint32_t)__shfl_xor((int)actv, 2);
+        const uint32_t count = info & 0xFFFFu, mp = info >> 16;
+        // 3. p = lower_bound(x) over the monotone prefix [0, mp).  Full groups inside it have
+        //    their last key as maximum: the first one >= x holds p; else p is in the partial group.
+        const uint32_t nfull = mp / 64u;
+        const uint32_t act_full = actv & (nfull >= 32u ? ~0u : ((1u << nfull) - 1u));
+        uint32_t lo = act_full ? 64u * (uint32_t)__builtin_ctz(act_full) : 64u * nfull;
+        uint32_t hi = act_full ? lo + 64u : mp;
+        const uint64_t *plane = t.okey + (uint64_t)leaf * KW * t.cap;
+        for (int step = 0; step < 4; ++step) {
+            const uint32_t span = hi > lo ? hi - lo : 0u;
+            // the 4 lanes of a scan share lo / hi (same inputs, same steps): quads go together
+            if (span == 0) continue;
+            const uint32_t piv = lo + ((part + 1u) * span) / 5u;
+            uint64_t k[KW];
+#pragma unroll
+            for (int w = 0; w < KW; ++w) k[w] = plane[(uint64_t)w * t.cap + piv];
+            int c = kw_lt<KW>(k, x) ? 1 : 0;
+            c += __shfl_xor(c, 1);
+            c += __shfl_xor(c, 2);
+            // pivots increase with the part and keys with the slot: parts [0, c) hold keys < x,
+            // so p lies in (piv[c-1], piv[c]]
+            const uint32_t plo = c > 0 ? (uint32_t)__shfl((int)piv, (int)(quad + (uint32_t)c - 1u)) + 1u : lo;
+            const uint32_t phi = c < 4 ? (uint32_t)__shfl((int)piv, (int)(quad + (uint32_t)c)) : hi;
+            lo = plo;
+            hi = phi;
+        }
+        const uint32_t p = lo;
+        // 4. visible slots in [p, mp): this lane's words masked and counted
+        uint32_t nv = 0;
+#pragma unroll
+        for (int k = 0; k < VPL; ++k) {
+            const uint32_t s0 = (part * VPL + (uint32_t)k) * 64u;
+            uint64_t v = vis[k];
+            if (s0 + 64u <= p || s0 >= mp) v = 0;
+            else {
+                if (s0 < p) v &= ~0ull << (p - s0);
+                if (mp < s0 + 64u) v &= (1ull << (mp - s0)) - 1ull;
+            }
+            vis[k] = v;
+            nv += (uint32_t)__builtin_popcountll(v);
+        }
+        const uint32_t n0 = (uint32_t)__shfl((int)nv, (int)quad), n1 = (uint32_t)__shfl((int)nv, (int)(quad + 1u)),
+                       n2 = (uint32_t)__shfl((int)nv, (int)(quad + 2u));
+        const uint32_t before = part == 0 ? 0u : part == 1 ? n0 : part == 2 ? n0 + n1 : n0 + n1 + n2;
+        uint32_t vs = nv;
+        vs += (uint32_t)__shfl_xor((int)vs, 1);
+        vs += (uint32_t)__shfl_xor((int)vs, 2);
+        // part r's candidate: the (r + 1)-th visible slot >= p, found by whichever lane's words
+        // hold it (each lane walks its own set bits), then OR-gathered over the scan's lanes
+        uint32_t cand[4] = {0u, 0u, 0u, 0u};  // slot + 1, 0 = none
+        {
+            uint32_t r = before;
+#pragma unroll
+            for (int k = 0; k < VPL; ++k) {
+                uint64_t v = vis[k];
+                while (v && r < 4u) {
+                    const uint32_t s = (part * VPL + (uint32_t)k) * 64u + (uint32_t)__builtin_ctzll(v);
+                    v &= v - 1;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        if (r == (uint32_t)q) cand[q] = s + 1u;
+                    ++r;
+                }
+            }
+        }
+        uint32_t my_cand = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            uint32_t v = cand[q];
+            v |= (uint32_t)__shfl_xor((int)v, 1);
+            v |= (uint32_t)__shfl_xor((int)v, 2);
+            if (part == (uint32_t)q) my_cand = v;
+        }
+        // the visit's kept records m and candidates e -- decided when the prefix alone supplies
+        // to_scan + 1 records, or when nothing follows it (then m is all it has)
+        const bool whole = mp >= count;
+        const bool decided = vs >= scan_size + 1u || whole;
+        const uint32_t m = vs < scan_size + 1u ? vs : scan_size + 1u;
+        const uint32_t e = m < scan_size ? m : scan_size;
+        // per candidate: 1 = has the prefix and resolves (LATEST / OLD), 2 = no prefix (a hole:
+        // its key, and every later candidate's, is past the prefix range, so the scan has no
+        // tuple), 3 = prefix but nothing visible for the read id, 0 = no candidate
+        uint32_t res = 0;
+        uint32_t img = 0xFFFFFFFFu;
+        uint8_t sv = ST_NOT_FOUND;
+        if (valid && decided && my_cand && part < e) {
+            const uint32_t sl = my_cand - 1u;
+            bool pfx = true;
+#pragma unroll
+            for (int w = 0; w < KW; ++w)
+                if ((uint32_t)w < words) pfx = pfx && plane[(uint64_t)w * t.cap + sl] == x[w];
+            const SlotInfo si = t.slot[(uint64_t)leaf * t.cap + sl];
+            if (pfx) {
+                img = scan_visible(t, si, rid, sv);
+                res = sv == ST_LATEST || sv == ST_OLD ? 1u : 3u;
+            } else {
+                res = 2u;
+            }
+        }
+        // the scan's outcome from its candidates in rank order (parts 0..3): the first that
+        // resolves or is a hole decides; candidates past the 4th are left to the general loop
+        uint32_t code = 0;  // 4 x 2 bits, part r at bits 2r
+#pragma unroll
+        for (int q = 0; q < 4; ++q) code |= (uint32_t)__shfl((int)res, (int)(quad + (uint32_t)q)) << (2 * q);
+        int first = -1;  // first part that resolves (1) or is a hole (2)
+        int stop = 4;    // first part without a candidate
+#pragma unroll
+        for (int q = 3; q >= 0; --q) {
+            const uint32_t c = (code >> (2 * q)) & 3u;
+            if (c == 1u || c == 2u) first = q;
+            if (c == 0u) stop = q;
+        }
+        const uint32_t wimg = (uint32_t)__shfl((int)img, (int)(quad + (uint32_t)(first < 0 ? 0 : first)));
+        const uint32_t wst = (uint32_t)__shfl((int)sv, (int)(quad + (uint32_t)(first < 0 ? 0 : first)));
+        if (valid && part == 0) {
+            uint8_t st = ST_NOT_FOUND;
+            uint32_t im = 0xFFFFFFFFu;
+            const bool reached = first >= 0 && first < stop;  // decided before the candidates ran out
+            if (!decided) {
+                st = kFirstUndecided;
+            } else if (reached && ((code >> (2 * first)) & 3u) == 1u) {
+                st = (uint8_t)wst;
+                im = wimg;
+            } else if (reached) {
+                st = ST_NOT_FOUND;  // a hole: no candidate from it on has the prefix
+            } else if (m == 0) {
+                st = ST_NOT_FOUND;  // the visit kept nothing: the Iterator ends
+            } else if (e > 4u || (e == m && scan_size > e)) {
+                st = kFirstUndecided;  // candidates past the 4th, or an Iterator continuation
+            }
+            img_out[i] = im;
+            st_out[i] = st;
+        }
+    }
+}
+
 // inclusive prefix sum within each row of 16 lanes (DPP row shifts; lanes shifted in from
 // outside the row read 0)
 __device__ __forceinline__ uint32_t row16_incl_scan(uint32_t v) {
@@ -2501,14 +2698,24 @@ hipError_t launch_scan_first(const DevTable &t, const uint64_t *keys, uint64_t n
     if (n == 0) return hipSuccess;
     if (t.key_width == 0 || scan_size == 0 || scan_size > 63) return hipErrorInvalidValue;
     const int blocks = grid_for((n + kFirstChunk - 1) / kFirstChunk, 4, tune.max_blocks > 0 ? tune.max_blocks : 16384);
-    // default (STAGE_SL_SCANS unset or 0): scan_first_split_kernel + scan_first_rest_kernel.
-    // Variants: -4 split at 7 waves/SIMD; -5 / -3 / -1 scan_first_fast_kernel
-    // with the prefetch at 8 / 7 / 6 waves, -2 without it; -6 / -7 scan_first_seg_kernel (4 / 2
-    // scans per pass); 1 the general single-scan kernel; 2 / 4 NS scans per wave in lockstep
+    // default (STAGE_SL_SCANS unset or 0): scan_first_mono_kernel + scan_first_rest_kernel.
+    // Variants: -8 scan_first_split_kernel (the round-2 default), -4 split at 7
+    // waves/SIMD; -5 / -3 / -1 scan_first_fast_kernel with the prefetch at 8 / 7 / 6 waves, -2
+    // without it; -6 / -7 scan_first_seg_kernel (4 / 2 scans per pass); 1 the general
+    // single-scan kernel; 2 / 4 NS scans per wave in lockstep
     const int ns = tune.first_scans;
 #define STAGE_FIRST(S, KW)                                                                                  \
-    if (ns == 0 || ns == -4 || ns == -6 || ns == -7) {                                                      \
-        if (ns == -6 && scan_size <= 15)                                                                    \
+    if (ns == 0 || ns == -4 || ns == -6 || ns == -7 || ns == -8 || ns == -9 || ns == -10) {                 \
+        if (ns == 0)                                                                                        \
+            scan_first_mono_kernel<S, KW, 8><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words, img_out, \
+                                                                    st_out);                                \
+        else if (ns == -9)                                                                                  \
+            scan_first_mono_kernel<S, KW, 10><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words,     \
+                                                                     img_out, st_out);                      \
+        else if (ns == -10)                                                                                 \
+            scan_first_mono_kernel<S, KW, 1><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words,      \
+                                                                    img_out, st_out);                       \
+        else if (ns == -6 && scan_size <= 15)                                                               \
             scan_first_seg_kernel<S, KW, 4, 4><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words,    \
                                                                       img_out, st_out);                     \
         else if (ns == -7 && scan_size <= 31)                                                               \

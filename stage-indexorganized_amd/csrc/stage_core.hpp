@@ -106,8 +106,11 @@ struct alignas(32) SlotInfo {
 // 128-B multiple.  A group's max key (over its live slots) lets a range scan skip slot groups
 // that hold nothing >= its start key.
 STAGE_HD uint32_t head_gmax_offset(uint32_t cap) { return cap + cap / 8; }
+// leaf info word after the group maxima: record count (bits 0-15) | mp (bits 16-31), the length
+// of the longest slot prefix whose keys increase strictly (>= the sorted region)
+STAGE_HD uint32_t head_info_offset(uint32_t cap, uint32_t kw) { return head_gmax_offset(cap) + (cap / 64) * kw * 8u; }
 STAGE_HD uint32_t leaf_head_bytes(uint32_t cap, uint32_t kw) {
-    return (head_gmax_offset(cap) + (cap / 64) * kw * 8u + 127u) & ~127u;
+    return (head_info_offset(cap, kw) + 8u + 127u) & ~127u;
 }
 
 struct alignas(16) CopyHdr {  // EphemeralPool::OverwriteVersionHeader (ephemeral_pool.h:26-150)

@@ -10,8 +10,8 @@ from tpcc_data import TpccTables, key, stock_level_device
 pytestmark = pytest.mark.gpu
 
 
-def _tables():
-    tt = TpccTables()
+def _tables(key_order=False):
+    tt = TpccTables(key_order=key_order)
     rng = np.random.default_rng(8)
     # committed history: stock quantities and order-line delivery dates change at commit 11 / 21
     for cid in (10, 20):
@@ -69,17 +69,20 @@ def test_stock_level_matches_oracle(tpcc):
     assert (got2 == exp2).all()
 
 
-@pytest.mark.parametrize("variant", ["0", "-1", "-2", "-3", "-4", "-5", "-6", "-7", "1", "2", "4"])
-def test_stock_level_scan_kernel_variants(gpu, monkeypatch, variant):
-    """Every first-tuple scan kernel (STAGE_SL_SCANS: 0 = scan_first_fast_kernel with the
-    prefetch pipeline at 8 waves/SIMD, -1 = the same without the occupancy cap, -2 = without the
-    pipeline, -3 = pipeline at 7 waves/SIMD, 1 = the general single-scan kernel, 2 / 4 = lockstep)
-    gives the oracle's stock-level results.  Order lines are inserted in numeric order, which is
-    not their memcmp key order, so leaves carry unsorted regions (the fast kernel's O(m) ranking)
-    and sorted ones (its slot-order ranking); starts of orders with fewer than 5 lines continue
-    across leaves."""
+@pytest.mark.parametrize("variant,key_order", [(v, False) for v in ("0", "-1", "-2", "-3", "-4", "-5", "-6", "-7",
+                                                                   "-8", "1", "2", "4")] +
+                         [("0", True), ("-8", True)])
+def test_stock_level_scan_kernel_variants(gpu, monkeypatch, variant, key_order):
+    """Every first-tuple scan kernel (STAGE_SL_SCANS: 0 = scan_first_mono_kernel, the default,
+    -8 = scan_first_split_kernel, -5 / -3 / -1 / -2 = scan_first_fast_kernel variants, -4 split at
+    7 waves/SIMD, -6 / -7 = scan_first_seg_kernel, 1 = the general single-scan kernel, 2 / 4 =
+    lockstep) gives the oracle's stock-level results.  Order lines are inserted in numeric order,
+    which is not their memcmp key order, so leaves carry unsorted regions (the fast kernel's O(m)
+    ranking, the mono kernel's fallback beyond the monotone prefix) and sorted ones (its
+    slot-order ranking); starts of orders with fewer than 5 lines continue across leaves.
+    key_order: the same rows loaded in key order -- whole leaves monotone."""
     monkeypatch.setenv("STAGE_SL_SCANS", variant)
-    tt = _tables()
+    tt = _tables(key_order)
     rng = np.random.default_rng(11)
     n = 1000
     w = rng.integers(1, 3, n)
@@ -92,7 +95,8 @@ def test_stock_level_scan_kernel_variants(gpu, monkeypatch, variant):
     assert (got > 0).any()
 
 
-def test_first_tuple_scans_every_kernel(gpu, monkeypatch):
+@pytest.mark.parametrize("key_order", [False, True])
+def test_first_tuple_scans_every_kernel(gpu, monkeypatch, key_order):
     """stage_index_scan_first_batch (the stock-level ORDER_LINE scans, direct) against the oracle's
     IndexScanExecutor range branch + the prefix predicate, for every scan kernel variant, over
     starts that hit existing orders, missing orders (o > 40: the prefix never matches, so the
@@ -105,7 +109,7 @@ def test_first_tuple_scans_every_kernel(gpu, monkeypatch):
                        for _ in range(n)])
     rids = rng.choice(np.array([0, 5, 11, 15, 21, 25, 0xFFFFFFFE], np.uint32), n)
     cases = [(10, 3), (3, 3), (1, 2), (10, 4), (15, 3), (31, 2), (63, 1)]
-    ref_tt = _tables()
+    ref_tt = _tables(key_order)
     expected = {}
     for size, words in cases:
         exp = np.zeros(n, np.uint8)
@@ -117,9 +121,9 @@ def test_first_tuple_scans_every_kernel(gpu, monkeypatch):
                     break
         expected[(size, words)] = exp
     images = {}
-    for variant in ["1", "0", "-4", "-5", "-6", "-7", "-1", "-2", "-3", "2", "4"]:
+    for variant in ["1", "0", "-8", "-4", "-5", "-6", "-7", "-1", "-2", "-3", "2", "4"]:
         monkeypatch.setenv("STAGE_SL_SCANS", variant)
-        tt = _tables()
+        tt = _tables(key_order)
         for size, words in cases:
             img, st = tt.ol.index_scan_first(starts, size, words, read_ids=rids)
             exp = expected[(size, words)]
@@ -133,7 +137,7 @@ def test_first_tuple_scans_every_kernel(gpu, monkeypatch):
     assert (expected[(10, 3)] == 0).any() and (expected[(10, 3)] != 0).any()
 
 
-@pytest.mark.parametrize("variant", ["0", "-4", "-5", "-6", "-7", "1", "2"])
+@pytest.mark.parametrize("variant", ["0", "-8", "-4", "-5", "-6", "-7", "1", "2"])
 def test_first_tuple_scans_16_byte_keys(gpu, monkeypatch, variant):
     """stage_index_scan_first_batch on the STOCK table (16-byte keys, KW = 2 order words):
     the first LATEST / OLD tuple of the same warehouse (prefix 1) or of the exact key (prefix

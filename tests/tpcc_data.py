@@ -25,8 +25,12 @@ def i64(b):
 
 
 class TpccTables:
-    def __init__(self, n_w=2, n_d=10, n_o=40, n_items=1000, seed=7):
+    """key_order: load each batch sorted by its key bytes (the tables' memcmp order) instead of
+    the loader's numeric order -- every leaf's keys then increase in slot order."""
+
+    def __init__(self, n_w=2, n_d=10, n_o=40, n_items=1000, seed=7, key_order=False):
         rng = np.random.default_rng(seed)
+        self.key_order = key_order
         self.n_w, self.n_d, self.n_o, self.n_items = n_w, n_d, n_o, n_items
         self.dist = stage.Table(payload_size=D_PAYLOAD, key_width=16)
         self.ol = stage.Table(payload_size=OL_PAYLOAD, key_width=32)
@@ -59,10 +63,12 @@ class TpccTables:
                         pays.append(p)
             self._load(self.ol, self.ool, 32, keys, pays)
 
-    @staticmethod
-    def _load(tab, orc, width, keys, pays):
+    def _load(self, tab, orc, width, keys, pays):
         keys = np.stack(keys)
         pays = np.stack(pays)
+        if self.key_order:
+            order = np.lexsort(keys.T[::-1])
+            keys, pays = keys[order], pays[order]
         rc, ins = tab.load_rows(keys, pays)
         assert ins == keys.shape[0]
         assert orc.load_rows(keys, pays) == keys.shape[0]
