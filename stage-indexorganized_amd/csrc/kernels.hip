@@ -2698,21 +2698,19 @@ hipError_t launch_scan_first(const DevTable &t, const uint64_t *keys, uint64_t n
     if (n == 0) return hipSuccess;
     if (t.key_width == 0 || scan_size == 0 || scan_size > 63) return hipErrorInvalidValue;
     const int blocks = grid_for((n + kFirstChunk - 1) / kFirstChunk, 4, tune.max_blocks > 0 ? tune.max_blocks : 16384);
-    // default (STAGE_SL_SCANS unset or 0): scan_first_mono_kernel + scan_first_rest_kernel.
-    // Variants: -8 scan_first_split_kernel (the round-2 default), -4 split at 7
-    // waves/SIMD; -5 / -3 / -1 scan_first_fast_kernel with the prefetch at 8 / 7 / 6 waves, -2
-    // without it; -6 / -7 scan_first_seg_kernel (4 / 2 scans per pass); 1 the general
-    // single-scan kernel; 2 / 4 NS scans per wave in lockstep
+    // default (STAGE_SL_SCANS unset or 0): scan_first_split_kernel + scan_first_rest_kernel.
+    // Variants: -8 / -9 scan_first_mono_kernel at 8 waves/SIMD / uncapped
+    // (round 3: a third of the instructions and of the HBM bytes, but per-lane scattered key
+    // loads -- no faster); -4 split at 7 waves/SIMD; -5 / -3 / -1 scan_first_fast_kernel with the
+    // prefetch at 8 / 7 / 6 waves, -2 without it; -6 / -7 scan_first_seg_kernel (4 / 2 scans per
+    // pass); 1 the general single-scan kernel; 2 / 4 NS scans per wave in lockstep
     const int ns = tune.first_scans;
 #define STAGE_FIRST(S, KW)                                                                                  \
-    if (ns == 0 || ns == -4 || ns == -6 || ns == -7 || ns == -8 || ns == -9 || ns == -10) {                 \
-        if (ns == 0)                                                                                        \
+    if (ns == 0 || ns == -4 || ns == -6 || ns == -7 || ns == -8 || ns == -9) {                              \
+        if (ns == -8)                                                                                       \
             scan_first_mono_kernel<S, KW, 8><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words, img_out, \
                                                                     st_out);                                \
         else if (ns == -9)                                                                                  \
-            scan_first_mono_kernel<S, KW, 10><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words,     \
-                                                                     img_out, st_out);                      \
-        else if (ns == -10)                                                                                 \
             scan_first_mono_kernel<S, KW, 1><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words,      \
                                                                     img_out, st_out);                       \
         else if (ns == -6 && scan_size <= 15)                                                               \

@@ -70,12 +70,12 @@ def test_stock_level_matches_oracle(tpcc):
 
 
 @pytest.mark.parametrize("variant,key_order", [(v, False) for v in ("0", "-1", "-2", "-3", "-4", "-5", "-6", "-7",
-                                                                   "-8", "1", "2", "4")] +
+                                                                   "-8", "-9", "1", "2", "4")] +
                          [("0", True), ("-8", True)])
 def test_stock_level_scan_kernel_variants(gpu, monkeypatch, variant, key_order):
-    """Every first-tuple scan kernel (STAGE_SL_SCANS: 0 = scan_first_mono_kernel, the default,
-    -8 = scan_first_split_kernel, -5 / -3 / -1 / -2 = scan_first_fast_kernel variants, -4 split at
-    7 waves/SIMD, -6 / -7 = scan_first_seg_kernel, 1 = the general single-scan kernel, 2 / 4 =
+    """Every first-tuple scan kernel (STAGE_SL_SCANS: 0 = scan_first_split_kernel, the default,
+    -8 / -9 = scan_first_mono_kernel, -5 / -3 / -1 / -2 = scan_first_fast_kernel variants, -4 split
+    at 7 waves/SIMD, -6 / -7 = scan_first_seg_kernel, 1 = the general single-scan kernel, 2 / 4 =
     lockstep) gives the oracle's stock-level results.  Order lines are inserted in numeric order,
     which is not their memcmp key order, so leaves carry unsorted regions (the fast kernel's O(m)
     ranking, the mono kernel's fallback beyond the monotone prefix) and sorted ones (its
@@ -121,7 +121,7 @@ def test_first_tuple_scans_every_kernel(gpu, monkeypatch, key_order):
                     break
         expected[(size, words)] = exp
     images = {}
-    for variant in ["1", "0", "-8", "-4", "-5", "-6", "-7", "-1", "-2", "-3", "2", "4"]:
+    for variant in ["1", "0", "-8", "-9", "-4", "-5", "-6", "-7", "-1", "-2", "-3", "2", "4"]:
         monkeypatch.setenv("STAGE_SL_SCANS", variant)
         tt = _tables(key_order)
         for size, words in cases:
