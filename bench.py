@@ -467,7 +467,7 @@ def run_sharded(args, rank, world, local):
         "coalescing": {"keys": sum(sx["keys"] for sx in stats), "requests_routed": routed,
                        "remote_requests": sum(sx["remote"] for sx in stats),
                        "routed_share": round(routed / max(1, sum(sx["keys"] for sx in stats)), 4),
-                       "note": "equal keys of an exchange chunk travel and are probed once; own requests are "
+                       "note": "equal (key, read id) requests of the batch travel and are probed once, whatever exchange chunk they fall in; own requests are "
                                "probed straight into their caller positions (fan-out probe)"},
         "rccl": rccl, "per_rank": per_rank,
         "setup_s": {k: round(max(p["setup_s"][k] for p in per_rank), 2) for k in per_rank[0]["setup_s"]},

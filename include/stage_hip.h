@@ -404,9 +404,9 @@ int stage_ch_query2_batch(stage_table *region, stage_table *nation, stage_table 
  * MurmurHash64A(key, key_width, 0) % world, probes it there and returns the results in the
  * caller's order (all-to-all-v out, local probe, all-to-all-v back). */
 int stage_comm_unique_id(uint8_t *id128);
-/* the sharded batch is exchanged in `chunks` pieces whose result transfers overlap the next
- * piece's probe (0 = STAGE_SHARD_CHUNKS env, or 4 -- 1 at world 1); set before stage_comm_init, same value on
- * every rank */
+/* the sharded batch's requests are exchanged in `chunks` pieces whose result transfers overlap
+ * the next piece's probe (0 = STAGE_SHARD_CHUNKS env, or 4 -- 1 at world 1); set before
+ * stage_comm_init, same value on every rank */
 int stage_set_shard_chunks(stage_table *t, int chunks);
 int stage_comm_init(stage_table *t, const uint8_t *id128, int rank, int world);
 int stage_comm_destroy(stage_table *t);
@@ -425,12 +425,13 @@ int stage_probe_sharded_ex(stage_table *t, const uint64_t *d_keys, const uint32_
 /* loopback != 0: the buffer of stage_probe_sharded_loopback's shard state */
 int stage_sharded_owner_rows(stage_table *t, int loopback, uint8_t **d_rows, uint64_t *n_rows);
 /* request coalescing (default on; STAGE_SHARD_DEDUPE=0 or on = 0 turns it off, -1 = the env
- * default): within each exchange chunk, requests with equal (key, read id) are routed and probed
- * once and the result is copied to every caller position -- results are identical, the key and
- * tuple traffic over xGMI shrinks by the batch's duplicate share (about half of a Zipf-0.9
- * batch).  Owner-reply rows are then one per distinct request. */
+ * default): requests with equal (key, read id) anywhere in the batch are routed and probed once
+ * (runs of more than 64 callers are cut into requests of at most 64) and the result is copied to
+ * every caller position -- results are identical, the key and tuple traffic over xGMI shrinks by
+ * the batch's duplicate share (55 % of a 16M-key Zipf-0.9 batch over 100M rows).  Owner-reply
+ * rows are then one per request. */
 int stage_set_shard_dedupe(stage_table *t, int on);
-/* coalescing sorts the chunk's keys on their low `bits` bits (0 or 64 = all; default 64).  Any
+/* coalescing sorts the batch's keys on their low `bits` bits (0 or 64 = all; default 64).  Any
  * value gives the same results -- keys equal in those bits but different above them still form
  * separate requests -- a caller whose keys are < 2^bits only saves radix passes. */
 int stage_set_shard_key_bits(stage_table *t, int bits);

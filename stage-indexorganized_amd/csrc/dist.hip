@@ -64,23 +64,33 @@ __device__ __forceinline__ uint64_t mm64a_8(uint64_t k) {
 // host does not wait for the coalescing before it enqueues the routing.
 constexpr int kRouteBlocks = 1024;
 constexpr int kMaxWorld = 64;
+constexpr int kMaxChunks = 64;
 constexpr int kDefaultChunks = 4;  // sharded batches are exchanged in this many overlapped chunks
 // caller positions served by one coalesced request at most: a hot key's run is cut into
 // requests of <= 64 callers, so no single probe or fan-out copy stores more than 64 rows
 constexpr uint32_t kFanCap = 64;
 
-__device__ __forceinline__ uint64_t dev_len(uint64_t n_max, const uint32_t *n_dev) { return n_dev ? *n_dev : n_max; }
+// chunk i of C over the routed items [0, total): [total*i/C, total*(i+1)/C); total is the batch
+// size, or the coalesced request count read on the device (total_dev)
+struct ChunkSpan {
+    uint64_t lo, hi;
+};
+__device__ __forceinline__ ChunkSpan chunk_span(uint64_t total_max, const uint32_t *total_dev, int i, int C) {
+    const uint64_t total = total_dev ? *total_dev : total_max;
+    return ChunkSpan{total * (uint64_t)i / (uint64_t)C, total * (uint64_t)(i + 1) / (uint64_t)C};
+}
 
-__global__ __launch_bounds__(256) void route_hist(const uint64_t *__restrict__ keys, uint64_t n_max,
-                                                  const uint32_t *__restrict__ n_dev, int world,
-                                                  uint8_t *__restrict__ dest, uint32_t *__restrict__ blk) {
+__global__ __launch_bounds__(256) void route_hist(const uint64_t *__restrict__ keys, uint64_t total_max,
+                                                  const uint32_t *__restrict__ total_dev, int chunk, int nchunks,
+                                                  int world, uint8_t *__restrict__ dest, uint32_t *__restrict__ blk) {
     __shared__ uint32_t h[kMaxWorld];
     if (threadIdx.x < (unsigned)world) h[threadIdx.x] = 0;
     __syncthreads();
-    const uint64_t n = dev_len(n_max, n_dev);
+    const ChunkSpan cs = chunk_span(total_max, total_dev, chunk, nchunks);
+    const uint64_t n = cs.hi - cs.lo;
     const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
     const uint64_t b0 = (uint64_t)blockIdx.x * per, b1 = b0 + per < n ? b0 + per : n;
-    for (uint64_t i = b0 + threadIdx.x; i < b1; i += blockDim.x) {
+    for (uint64_t i = cs.lo + b0 + threadIdx.x; i < cs.lo + b1; i += blockDim.x) {
         const uint32_t d = (uint32_t)(mm64a_8(keys[i]) % (uint64_t)world);
         dest[i] = (uint8_t)d;
         atomicAdd(&h[d], 1u);
@@ -119,28 +129,30 @@ __global__ __launch_bounds__(1024) void route_scan(const uint32_t *__restrict__ 
     }
 }
 
-// send[pos] = request i's key record; perm[pos] = its index; fan[pos] = the caller positions
-// it serves: urange[base + i] (coalesced: a range of flist) or {base + i, base + i + 1} (one
-// caller, the request itself)
+// send[lo + pos] = item i's key record (i in the chunk [lo, hi), pos its place in the chunk,
+// grouped by destination); perm[lo + pos] = i; fan[lo + pos] = the caller positions it serves:
+// urange[i] (coalesced: a run of flist) or {i, i + 1} (one caller, the item itself)
 __global__ __launch_bounds__(256) void route_scatter(const uint64_t *__restrict__ keys, const uint32_t *__restrict__ rids,
-                                                     uint64_t n_max, const uint32_t *__restrict__ n_dev, int world,
+                                                     uint64_t total_max, const uint32_t *__restrict__ total_dev,
+                                                     int chunk, int nchunks, int world,
                                                      const uint8_t *__restrict__ dest, const uint32_t *__restrict__ offs,
                                                      SendRec *__restrict__ send, uint32_t *__restrict__ perm,
-                                                     uint32_t idx_base, uint32_t *__restrict__ upos,
-                                                     const FanRange *__restrict__ urange, FanRange *__restrict__ fan) {
+                                                     uint32_t *__restrict__ upos, const FanRange *__restrict__ urange,
+                                                     FanRange *__restrict__ fan) {
     __shared__ uint32_t cur[kMaxWorld];
     if (threadIdx.x < (unsigned)world) cur[threadIdx.x] = offs[threadIdx.x * gridDim.x + blockIdx.x];
     __syncthreads();
-    const uint64_t n = dev_len(n_max, n_dev);
+    const ChunkSpan cs = chunk_span(total_max, total_dev, chunk, nchunks);
+    const uint64_t n = cs.hi - cs.lo;
     const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
     const uint64_t b0 = (uint64_t)blockIdx.x * per, b1 = b0 + per < n ? b0 + per : n;
-    for (uint64_t i = b0 + threadIdx.x; i < b1; i += blockDim.x) {
-        const uint32_t pos = atomicAdd(&cur[dest[i]], 1u);
-        const uint32_t idx = idx_base + (uint32_t)i;
+    for (uint64_t i = cs.lo + b0 + threadIdx.x; i < cs.lo + b1; i += blockDim.x) {
+        const uint32_t pos = (uint32_t)cs.lo + atomicAdd(&cur[dest[i]], 1u);
+        const uint32_t idx = (uint32_t)i;
         send[pos] = SendRec{keys[i], rids ? rids[i] : 0xFFFFFFFEu, 0};
         perm[pos] = idx;
-        if (upos) upos[idx] = idx_base + pos;  // where request idx was sent (owner-reply expand)
-        fan[idx_base + pos] = urange ? urange[idx] : FanRange{idx, idx + 1};
+        if (upos) upos[idx] = pos;  // where request idx was sent (owner-reply expand)
+        fan[pos] = urange ? urange[idx] : FanRange{idx, idx + 1};
     }
 }
 
@@ -149,11 +161,11 @@ __global__ void transpose_counts(const uint32_t *__restrict__ cw, int C, int W, 
     for (int k = threadIdx.x; k < C * W; k += blockDim.x) wc[(k % W) * C + k / W] = cw[k];
 }
 
-// ---- request coalescing of one chunk [b, b + len): the chunk's keys are radix-sorted with
-// their chunk positions (by (key, read id): read ids first, then a stable sort by key); a
-// sorted entry starts a request when its key or read id differs from its predecessor's, or at
-// every kFanCap-th sorted position; requests are numbered by an inclusive scan and packed at
-// [b, b + nu).
+// ---- request coalescing of the whole batch: its keys are radix-sorted with their positions (by
+// (key, read id): read ids first, then a stable sort by key); a sorted entry starts a request
+// when its key or read id differs from its predecessor's, or at every kFanCap-th sorted
+// position; requests are numbered by an inclusive scan and packed at [0, nu).  The exchange
+// chunks then cut the requests, not the callers: a key asked in two chunks travels once.
 __global__ void dd_iota_kernel(uint32_t *__restrict__ v, uint64_t n) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) v[i] = (uint32_t)i;
@@ -176,7 +188,8 @@ __global__ void dd_heads(const uint64_t *__restrict__ skeys, const uint32_t *__r
 
 // uidx[b + p] = b + request number of the caller position p (owner reply; may be null); flist[b + j] = the caller position
 // of sorted entry j; urange[b + u] = request u's run [b + first, b + last + 1) of flist; the
-// request's key / read id packed at b + u; nu[chunk] = the chunk's request count
+// request's key / read id packed at b + u; nu[chunk] = the request count (the sharded probe
+// coalesces its whole batch at once: b = 0, chunk 0)
 __global__ void dd_pack(const uint64_t *__restrict__ skeys, const uint32_t *__restrict__ sidx,
                         const uint32_t *__restrict__ rids, const uint32_t *__restrict__ flag,
                         const uint32_t *__restrict__ useq, uint64_t n, uint32_t b, uint32_t *__restrict__ uidx,
@@ -269,18 +282,25 @@ __global__ __launch_bounds__(256) void unpermute_status(const stage_probe_out_de
     out[perm[p]] = own ? qout[p - q0] : bout[p];
 }
 
-// owner-reply mode with coalesced requests: caller position o takes the status record of its
-// request, sent from position p = upos[uidx[o]] (own requests read in place, as above)
+// owner-reply mode with coalesced requests, once every chunk is back: caller position o takes
+// the status record of its request, sent from position p = upos[uidx[o]].  p's chunk i is the
+// last whose base cb[i] <= p; own requests of chunk i, [q0[i], q1[i]), are read in place from
+// the local probe's output (rout + ro[i]).
+struct OwnSegs {
+    uint32_t cb[kMaxChunks], q0[kMaxChunks], q1[kMaxChunks], ro[kMaxChunks];
+    int C;
+};
 __global__ __launch_bounds__(256) void expand_status(const stage_probe_out_dev *__restrict__ bout,
                                                      const uint32_t *__restrict__ uidx, const uint32_t *__restrict__ upos,
-                                                     uint64_t o0, uint64_t o1, stage_probe_out_dev *__restrict__ out,
-                                                     uint64_t q0, uint64_t q1,
-                                                     const stage_probe_out_dev *__restrict__ qout) {
-    const uint64_t o = o0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (o >= o1) return;
-    const uint64_t p = upos[uidx[o]];
-    const bool own = p >= q0 && p < q1;
-    out[o] = own ? qout[p - q0] : bout[p];
+                                                     uint64_t n, stage_probe_out_dev *__restrict__ out, OwnSegs own,
+                                                     const stage_probe_out_dev *__restrict__ rout) {
+    const uint64_t o = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (o >= n) return;
+    const uint32_t p = upos[uidx[o]];
+    int i = 0;
+    while (i + 1 < own.C && own.cb[i + 1] <= p) ++i;
+    const bool mine = p >= own.q0[i] && p < own.q1[i];
+    out[o] = mine ? rout[own.ro[i] + (p - own.q0[i])] : bout[p];
 }
 
 // reply mode "owner": the row stays in the owner's result buffer; the status record carries
@@ -354,7 +374,7 @@ static void check_rccl_version() {
 
 static void init_common(ShardComm &c, int rank, int world, int chunks) {
     if (world < 1 || world > kMaxWorld || rank < 0 || rank >= world) throw std::invalid_argument("bad rank/world");
-    if (chunks < 1 || chunks > 64) throw std::invalid_argument("chunks must be 1..64");
+    if (chunks < 1 || chunks > kMaxChunks) throw std::invalid_argument("chunks must be 1..64");
     c.rank = rank;
     c.world = world;
     c.chunks = chunks;
@@ -368,11 +388,10 @@ static void init_common(ShardComm &c, int rank, int world, int chunks) {
 }
 
 // exchange chunks: STAGE_SHARD_CHUNKS, else 4 (the result return of chunk i overlaps the probe
-// of chunk i + 1), or 1 at world 1, where nothing crosses xGMI and one batch-wide coalescing
-// routes fewer requests (43.8 % of a Zipf-0.9 batch instead of 54 % in 4 chunks)
+// of chunk i + 1), or 1 at world 1, where nothing crosses xGMI to overlap
 static int env_chunks(int world) {
     const char *e = std::getenv("STAGE_SHARD_CHUNKS");
-    return e ? std::max(1, std::min(64, std::atoi(e))) : world == 1 ? 1 : kDefaultChunks;
+    return e ? std::max(1, std::min(kMaxChunks, std::atoi(e))) : world == 1 ? 1 : kDefaultChunks;
 }
 
 int shard_default_chunks(int world) { return env_chunks(world); }
@@ -428,21 +447,25 @@ int shard_allgather_f64(ShardComm &c, const double *in, uint64_t n, double *out)
 }
 
 // ---- the plan of one sharded probe, shared by the RCCL path and the loopback rehearsal.
-// The caller's batch is cut into C chunks (C is the same on every rank, fixed at init, so the
-// ranks issue matching transfers).  Chunk i's requests are routed into send/perm positions
-// [cb_i, cb_i + routed_i), grouped by destination; what arrives lands in recv positions
-// [rb_i, rb_{i+1}), grouped by source.  All offsets are absolute.
+// What is routed is the caller's batch, or -- coalesced -- its distinct requests (one pass over
+// the whole batch, so a key asked in two chunks travels once).  The routed items [0, total) are
+// cut into C chunks (C is the same on every rank, fixed at init, so the ranks issue matching
+// transfers); chunk i's items [cb_i, cb_{i+1}) take send/perm positions [cb_i, cb_{i+1}),
+// grouped by destination; what arrives lands in recv positions [rb_i, rb_{i+1}), grouped by
+// source.  All offsets are absolute.  total is known to the host only after the count
+// exchange (the coalesced count is read back with the counts).
 struct Plan {
     int W = 1, C = 1;
+    uint64_t n = 0, total = 0;              // caller positions, routed items
     std::vector<uint64_t> cb, rb;           // chunk bases (send side / receive side), C+1
     std::vector<uint32_t> sc, rc;           // [i*W + r] counts sent to / received from r
     std::vector<uint64_t> soff, roff;       // [i*(W+1) + r] absolute segment starts
-    bool dedupe = false;                    // chunk i routes its coalesced requests [cb_i, cb_i + nu_i)
+    bool dedupe = false;                    // routed items are coalesced requests (c.dd_nu[0] of them)
     uint64_t m() const { return rb[C]; }
 };
 
 // coalescing + routing of every chunk, enqueued on the caller stream s (no host wait); the
-// send counts [C][W] are left in c.cnt
+// send counts [C][W] are left in c.cnt, the coalesced request count in c.dd_nu[0]
 static void plan_route(ShardComm &c, Plan &P, const uint64_t *d_keys, const uint32_t *d_rids, uint64_t n,
                        uint32_t stride, bool owner, hipStream_t s) {
     const int W = c.world, C = c.chunks;
@@ -461,16 +484,14 @@ static void plan_route(ShardComm &c, Plan &P, const uint64_t *d_keys, const uint
     }
     P.W = W;
     P.C = C;
-    P.cb.resize(C + 1);
-    for (int i = 0; i <= C; ++i) P.cb[i] = n * (uint64_t)i / (uint64_t)C;
+    P.n = n;
+    P.total = n;
     P.dedupe = c.dedupe && n > 0 && n < (1ull << 31);
-    // what is routed: the caller's keys, or each chunk's coalesced requests packed at its base
+    // what is routed: the caller's keys, or the coalesced requests packed at [0, nu)
     const uint64_t *rkeys = d_keys;
     const uint32_t *rrids = d_rids;
-    std::vector<uint64_t> rlen(C);
-    for (int i = 0; i < C; ++i) rlen[i] = P.cb[i + 1] - P.cb[i];
-    const uint64_t maxlen = *std::max_element(rlen.begin(), rlen.end());
     const uint32_t *nu = nullptr;
+    if (!c.dd_nu) grow(c.dd_nu, 64 * 4);
     if (P.dedupe) {
         if (c.dd_cap < c.cap_local) {
             const uint64_t cap = c.cap_local;
@@ -485,13 +506,12 @@ static void plan_route(ShardComm &c, Plan &P, const uint64_t *d_keys, const uint
             grow(c.upos, cap * 4);
             grow(c.urange, cap * sizeof(FanRange));
             grow(c.flist, cap * 4);
-            grow(c.dd_nu, 64 * 4);
             c.dd_cap = cap;
             c.dd_cub_items = 0;
         }
-        // temporary storage of the sorts and the scan, sized for the longest chunk
-        if (maxlen > c.dd_cub_items) {
-            const int items = (int)std::min<uint64_t>(maxlen, INT_MAX);
+        // temporary storage of the sorts and the scan
+        if (n > c.dd_cub_items) {
+            const int items = (int)n;
             size_t sb = 0, sr = 0, cb = 0;
             chk(hipcub::DeviceRadixSort::SortPairs(nullptr, sb, (uint64_t *)nullptr, (uint64_t *)nullptr,
                                                    (uint32_t *)nullptr, (uint32_t *)nullptr, items, 0, 64, s),
@@ -503,78 +523,73 @@ static void plan_route(ShardComm &c, Plan &P, const uint64_t *d_keys, const uint
                 "scan size");
             c.dd_cub_bytes = std::max(std::max(sb, sr), cb);
             grow(c.dd_cub, c.dd_cub_bytes);
-            c.dd_cub_items = maxlen;
+            c.dd_cub_items = n;
         }
         uint32_t *nuw = (uint32_t *)c.dd_nu;
-        chk(hipMemsetAsync(nuw, 0, 64 * 4, s), "memset nu");
         uint32_t *iota = (uint32_t *)c.dd_iota, *sidx = (uint32_t *)c.dd_sidx, *flag = (uint32_t *)c.dd_flag,
                  *useq = (uint32_t *)c.dd_useq;
         uint64_t *skeys = (uint64_t *)c.dd_skeys;
         const int bits = c.key_bits >= 1 && c.key_bits <= 64 ? c.key_bits : 64;
-        dd_iota_kernel<<<blocks_for(maxlen, 256), 256, 0, s>>>(iota, maxlen);
-        for (int i = 0; i < C; ++i) {
-            const uint64_t b = P.cb[i], len = rlen[i];
-            if (!len) continue;
-            const unsigned nb = blocks_for(len, 256);
-            const uint32_t *cr = d_rids ? d_rids + b : nullptr;
-            size_t bytes = c.dd_cub_bytes;
-            if (cr) {
-                // (key, read id) order: sort by read id, then stably by key (LSD radix sorts are
-                // stable); flag / useq serve as scratch until the heads are computed
-                uint32_t *srid = flag, *sidx1 = useq;
-                uint64_t *gk = (uint64_t *)c.ukeys + b;  // chunk i's packed keys are written after this sort
-                chk(hipcub::DeviceRadixSort::SortPairs(c.dd_cub, bytes, cr, srid, iota, sidx1, (int)len, 0, 32, s),
-                    "dedupe rid sort");
-                dd_gather_keys<<<nb, 256, 0, s>>>(d_keys + b, sidx1, len, gk);
-                bytes = c.dd_cub_bytes;
-                chk(hipcub::DeviceRadixSort::SortPairs(c.dd_cub, bytes, gk, skeys, sidx1, sidx, (int)len, 0, bits, s),
-                    "dedupe key sort");
-            } else {
-                chk(hipcub::DeviceRadixSort::SortPairs(c.dd_cub, bytes, d_keys + b, skeys, iota, sidx, (int)len, 0, bits,
-                                                       s),
-                    "dedupe sort");
-            }
-            dd_heads<<<nb, 256, 0, s>>>(skeys, sidx, cr, len, flag);
+        const unsigned nb = blocks_for(n, 256);
+        dd_iota_kernel<<<nb, 256, 0, s>>>(iota, n);
+        size_t bytes = c.dd_cub_bytes;
+        if (d_rids) {
+            // (key, read id) order: sort by read id, then stably by key (LSD radix sorts are
+            // stable); flag / useq serve as scratch until the heads are computed
+            uint32_t *srid = flag, *sidx1 = useq;
+            uint64_t *gk = (uint64_t *)c.ukeys;  // the packed keys are written after this sort
+            chk(hipcub::DeviceRadixSort::SortPairs(c.dd_cub, bytes, d_rids, srid, iota, sidx1, (int)n, 0, 32, s),
+                "dedupe rid sort");
+            dd_gather_keys<<<nb, 256, 0, s>>>(d_keys, sidx1, n, gk);
             bytes = c.dd_cub_bytes;
-            chk(hipcub::DeviceScan::InclusiveSum(c.dd_cub, bytes, flag, useq, (int)len, s), "dedupe scan");
-            dd_pack<<<nb, 256, 0, s>>>(skeys, sidx, cr, flag, useq, len, (uint32_t)b, owner ? (uint32_t *)c.uidx : nullptr,
-                                       (uint32_t *)c.flist, (FanRange *)c.urange, (uint64_t *)c.ukeys,
-                                       (uint32_t *)c.urids, nuw, i);
+            chk(hipcub::DeviceRadixSort::SortPairs(c.dd_cub, bytes, gk, skeys, sidx1, sidx, (int)n, 0, bits, s),
+                "dedupe key sort");
+        } else {
+            chk(hipcub::DeviceRadixSort::SortPairs(c.dd_cub, bytes, d_keys, skeys, iota, sidx, (int)n, 0, bits, s),
+                "dedupe sort");
         }
+        dd_heads<<<nb, 256, 0, s>>>(skeys, sidx, d_rids, n, flag);
+        bytes = c.dd_cub_bytes;
+        chk(hipcub::DeviceScan::InclusiveSum(c.dd_cub, bytes, flag, useq, (int)n, s), "dedupe scan");
+        dd_pack<<<nb, 256, 0, s>>>(skeys, sidx, d_rids, flag, useq, n, 0u, owner ? (uint32_t *)c.uidx : nullptr,
+                                   (uint32_t *)c.flist, (FanRange *)c.urange, (uint64_t *)c.ukeys, (uint32_t *)c.urids,
+                                   nuw, 0);
         chk(hipGetLastError(), "dedupe");
         rkeys = (const uint64_t *)c.ukeys;
         rrids = d_rids ? (const uint32_t *)c.urids : nullptr;
         nu = nuw;
+    } else {
+        chk(hipMemsetAsync(c.dd_nu, 0, 4, s), "memset nu");  // read back with the counts: unused
     }
     uint32_t *counts = (uint32_t *)c.cnt;  // [C][W] send counts
     uint32_t *blk = (uint32_t *)c.cursor, *offs = blk + (uint64_t)W * kRouteBlocks;
     chk(hipMemsetAsync(counts, 0, (uint64_t)C * W * sizeof(uint32_t), s), "memset counts");
+    if (n == 0) return;
     for (int i = 0; i < C; ++i) {
-        const uint64_t b = P.cb[i], len = rlen[i];
-        if (!len) continue;
-        const uint32_t *nd = nu ? nu + i : nullptr;
-        route_hist<<<kRouteBlocks, 256, 0, s>>>(rkeys + b, len, nd, W, (uint8_t *)c.dest + b, blk);
+        route_hist<<<kRouteBlocks, 256, 0, s>>>(rkeys, n, nu, i, C, W, (uint8_t *)c.dest, blk);
         route_scan<<<1, 1024, 0, s>>>(blk, (uint32_t)(W * kRouteBlocks), W, kRouteBlocks, offs, counts + i * W);
-        route_scatter<<<kRouteBlocks, 256, 0, s>>>(rkeys + b, rrids ? rrids + b : nullptr, len, nd, W,
-                                                   (const uint8_t *)c.dest + b, offs, (SendRec *)c.send + b,
-                                                   (uint32_t *)c.perm + b, (uint32_t)b,
+        route_scatter<<<kRouteBlocks, 256, 0, s>>>(rkeys, rrids, n, nu, i, C, W, (const uint8_t *)c.dest, offs,
+                                                   (SendRec *)c.send, (uint32_t *)c.perm,
                                                    P.dedupe && owner ? (uint32_t *)c.upos : nullptr,
-                                                   P.dedupe ? (const FanRange *)c.urange : nullptr,
-                                                   (FanRange *)c.fan);
+                                                   P.dedupe ? (const FanRange *)c.urange : nullptr, (FanRange *)c.fan);
     }
     chk(hipGetLastError(), "route");
 }
 
-// the send side of the plan from P.sc (filled by the caller from the device counts)
-static void plan_send(ShardComm &c, Plan &P, uint64_t n) {
+// the send side of the plan from P.sc and P.total (filled by the caller from the device counts)
+static void plan_send(ShardComm &c, Plan &P) {
     const int W = P.W, C = P.C;
+    if (!P.dedupe) P.total = P.n;
+    if (P.total > P.n) throw std::runtime_error("routing: more requests than keys");
+    P.cb.resize(C + 1);
+    for (int i = 0; i <= C; ++i) P.cb[i] = P.total * (uint64_t)i / (uint64_t)C;
     P.soff.assign((size_t)C * (W + 1), 0);
     for (int i = 0; i < C; ++i) {
         P.soff[i * (W + 1)] = P.cb[i];
         for (int r = 0; r < W; ++r) P.soff[i * (W + 1) + r + 1] = P.soff[i * (W + 1) + r] + P.sc[i * W + r];
-        if (P.soff[i * (W + 1) + W] > P.cb[i + 1]) throw std::runtime_error("routing: more requests than keys");
+        if (P.soff[i * (W + 1) + W] != P.cb[i + 1]) throw std::runtime_error("routing: counts disagree with the chunk");
     }
-    c.last_n = n;
+    c.last_n = P.n;
     c.last_routed = c.last_remote = c.last_received = 0;
     for (int i = 0; i < C; ++i)
         for (int r = 0; r < W; ++r) {
@@ -666,6 +681,7 @@ static void chunk_probe(ShardComm &c, const Plan &P, int i, const DevTable &t, c
 
 // chunk i's results that came back from other ranks (bout / brec, at their send positions) to
 // their caller positions; owner reply: status records of every position (own ones read in place)
+// -- coalesced, once all chunks are back (owner_expand: a caller's request may sit in any chunk)
 static void chunk_return(ShardComm &c, const Plan &P, int i, uint32_t stride, bool owner, stage_probe_out_dev *d_out,
                          uint8_t *d_recs, hipStream_t s) {
     const int W = P.W, me = c.rank;
@@ -678,18 +694,31 @@ static void chunk_return(ShardComm &c, const Plan &P, int i, uint32_t stride, bo
         fan_launch(bout + q1, brec + q1 * (uint64_t)stride, q1, pz, c, P, stride, d_out, d_recs, s);
         return;
     }
+    if (P.dedupe) return;
     const uint64_t ro = P.roff[(size_t)i * (W + 1) + me];  // where the local probe wrote the own results
     const stage_probe_out_dev *qout = (const stage_probe_out_dev *)c.rout + ro;
-    if (P.dedupe) {
-        const uint64_t o0 = P.cb[i], o1 = P.cb[i + 1];
-        if (o1 > o0)
-            expand_status<<<blocks_for(o1 - o0, 256), 256, 0, s>>>(bout, (const uint32_t *)c.uidx, (const uint32_t *)c.upos,
-                                                                   o0, o1, d_out, q0, q1, qout);
-    } else if (pz > p0) {
+    if (pz > p0) {
         unpermute_status<<<blocks_for(pz - p0, 256), 256, 0, s>>>(bout, (const uint32_t *)c.perm, p0, pz, d_out, q0, q1,
                                                                   qout);
     }
     chk(hipGetLastError(), "owner-reply return");
+}
+
+static void owner_expand(ShardComm &c, const Plan &P, stage_probe_out_dev *d_out, hipStream_t s) {
+    if (!P.dedupe || P.n == 0) return;
+    const int W = P.W, me = c.rank;
+    OwnSegs own{};
+    own.C = P.C;
+    for (int i = 0; i < P.C; ++i) {
+        own.cb[i] = (uint32_t)P.cb[i];
+        own.q0[i] = (uint32_t)P.soff[(size_t)i * (W + 1) + me];
+        own.q1[i] = (uint32_t)P.soff[(size_t)i * (W + 1) + me + 1];
+        own.ro[i] = (uint32_t)P.roff[(size_t)i * (W + 1) + me];
+    }
+    expand_status<<<blocks_for(P.n, 256), 256, 0, s>>>((const stage_probe_out_dev *)c.bout, (const uint32_t *)c.uidx,
+                                                        (const uint32_t *)c.upos, P.n, d_out, own,
+                                                        (const stage_probe_out_dev *)c.rout);
+    chk(hipGetLastError(), "owner-reply expand");
 }
 
 // RCCL path.  Streams: the caller's stream s routes and probes; c.cs carries the RCCL
@@ -713,12 +742,15 @@ int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const 
     uint32_t *cnt = (uint32_t *)c.cnt, *sendT = cnt + (uint64_t)C * W, *recvT = sendT + (uint64_t)C * W;
     transpose_counts<<<1, 256, 0, s>>>(cnt, C, W, sendT);
     nchk(ncclAllToAll(sendT, recvT, (size_t)C, ncclUint32, comm, s), "ncclAllToAll counts");
-    std::vector<uint32_t> hc((size_t)2 * C * W);  // [C][W] send counts, then [W][C] receive counts
+    // [C][W] send counts, then [W][C] receive counts, then the coalesced request count
+    std::vector<uint32_t> hc((size_t)2 * C * W + 1);
     chk(hipMemcpyAsync(hc.data(), cnt, (size_t)C * W * 4, hipMemcpyDeviceToHost, s), "counts d2h");
     chk(hipMemcpyAsync(hc.data() + (size_t)C * W, recvT, (size_t)C * W * 4, hipMemcpyDeviceToHost, s), "counts d2h");
+    chk(hipMemcpyAsync(hc.data() + (size_t)2 * C * W, c.dd_nu, 4, hipMemcpyDeviceToHost, s), "nu d2h");
     chk(hipStreamSynchronize(s), "sync");
     P.sc.assign(hc.begin(), hc.begin() + (size_t)C * W);
-    plan_send(c, P, n);
+    P.total = hc[(size_t)2 * C * W];
+    plan_send(c, P);
     P.rc.resize((size_t)C * W);
     for (int i = 0; i < C; ++i)
         for (int r = 0; r < W; ++r) P.rc[(size_t)i * W + r] = hc[(size_t)C * W + (size_t)r * C + i];
@@ -771,6 +803,7 @@ int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const 
         chk(hipStreamWaitEvent(c.us, ev_res[i], 0), "wait results");
         chunk_return(c, P, i, stride, owner, d_out, d_recs, c.us);
     }
+    if (owner) owner_expand(c, P, d_out, c.us);
     // the caller's stream completes after the last fan-out
     chk(hipEventRecord(ev_start, c.us), "event");
     chk(hipStreamWaitEvent(s, ev_start, 0), "join");
@@ -796,13 +829,18 @@ int shard_probe_loopback(const std::vector<ShardComm *> &cs, const std::vector<c
     const int C = cs[0]->chunks;
     const bool rows = recs[0] != nullptr;
     std::vector<Plan> P(W);
+    std::vector<uint32_t> tot(W);
     for (int r = 0; r < W; ++r) {
         plan_route(*cs[r], P[r], keys[r], rids[r], n[r], stride, owner, s);
         P[r].sc.resize((size_t)C * W);
         chk(hipMemcpyAsync(P[r].sc.data(), cs[r]->cnt, (size_t)C * W * 4, hipMemcpyDeviceToHost, s), "counts d2h");
+        chk(hipMemcpyAsync(&tot[r], cs[r]->dd_nu, 4, hipMemcpyDeviceToHost, s), "nu d2h");
     }
     chk(hipStreamSynchronize(s), "sync");
-    for (int r = 0; r < W; ++r) plan_send(*cs[r], P[r], n[r]);
+    for (int r = 0; r < W; ++r) {
+        P[r].total = tot[r];
+        plan_send(*cs[r], P[r]);
+    }
     for (int r = 0; r < W; ++r) {
         P[r].rc.resize((size_t)C * W);
         for (int i = 0; i < C; ++i)
@@ -835,6 +873,8 @@ int shard_probe_loopback(const std::vector<ShardComm *> &cs, const std::vector<c
             }
         for (int r = 0; r < W; ++r) chunk_return(*cs[r], P[r], i, stride, owner, outs[r], recs[r], s);
     }
+    if (owner)
+        for (int r = 0; r < W; ++r) owner_expand(*cs[r], P[r], outs[r], s);
     for (int r = 0; r < W; ++r) cs[r]->owner_rows = owner ? P[r].m() : 0;
     return STAGE_OK;
 }

@@ -99,9 +99,11 @@ def test_sharded_data_path_loopback_equals_single_table(gpu, world, chunks, dedu
             assert (res2[r][0]["status"] == ref_out["status"]).all()
 
 
-def test_owner_reply_mode_loopback(gpu):
+@pytest.mark.parametrize("dedupe", [1, 0])
+def test_owner_reply_mode_loopback(gpu, dedupe):
     # STAGE_REPLY_OWNER: only status records travel back; each row stays in its owner's result
-    # buffer at the index the record carries
+    # buffer at the index the record carries.  Repeated keys: coalesced, a caller's request may
+    # sit in any exchange chunk (the status records are expanded once every chunk is back)
     world, n = 4, 200_000
     keys = np.arange(n, dtype=np.uint64)
     tabs, h = shard_tables(keys, world)
@@ -110,7 +112,12 @@ def test_owner_reply_mode_loopback(gpu):
     for t in tabs + [full]:
         t.sync()
     rng = np.random.default_rng(77)
-    per_keys = [rng.integers(0, n + 5000, 30_000 + 1000 * r).astype(np.uint64) for r in range(world)]
+    for t in tabs:
+        stage.set_shard_dedupe(t, dedupe)
+    per_keys = []
+    for r in range(world):
+        k = np.concatenate([rng.integers(0, n + 5000, 30_000 + 1000 * r), np.repeat(rng.integers(0, n, 20), 150)])
+        per_keys.append(k[rng.permutation(k.size)].astype(np.uint64))
     res = stage.probe_sharded_loopback(tabs, per_keys, None, records=True, reply=stage.REPLY_OWNER)
     owner_bufs = []
     for t in tabs:
@@ -118,9 +125,10 @@ def test_owner_reply_mode_loopback(gpu):
         buf = np.zeros(cnt * t.stride, np.uint8)
         check(stage.lib().stage_memcpy_d2h(buf.ctypes.data, ptr, buf.nbytes, None), "d2h")
         owner_bufs.append(buf.reshape(cnt, t.stride))
-    # one owner row per routed request (equal keys of a chunk are coalesced)
+    # one owner row per routed request (equal keys of the batch are coalesced)
     routed = [stage.sharded_stats(t)[1] for t in tabs]
     assert sum(b.shape[0] for b in owner_bufs) == sum(routed) <= sum(k.size for k in per_keys)
+    assert (sum(routed) < sum(k.size for k in per_keys)) == bool(dedupe)
     for r in range(world):
         out, rows = res[r]
         ref_out, ref_rows = full.probe(per_keys[r])
@@ -131,12 +139,14 @@ def test_owner_reply_mode_loopback(gpu):
             got = owner_bufs[o][out["meta_hi"][sel]]
             hit = out["status"][sel] != stage.ST_NOT_FOUND
             assert (got[hit] == ref_rows[sel][hit]).all()
+    for t in tabs:
+        stage.set_shard_dedupe(t, -1)
 
 
 @pytest.mark.parametrize("read_ids", [False, True])
 def test_request_coalescing_zipf_batch(gpu, read_ids):
-    # a Zipf batch is about half duplicates: equal (key, read id) requests of a chunk travel and
-    # are probed once, every caller position gets its request's result -- identical to the
+    # a Zipf batch is about half duplicates: equal (key, read id) requests of the batch travel
+    # and are probed once (whatever exchange chunk they fall in), every caller position gets its request's result -- identical to the
     # uncoalesced path and to one table holding every key
     world, n = 4, 300_000
     keys = np.arange(n, dtype=np.uint64)
@@ -167,9 +177,9 @@ def test_request_coalescing_zipf_batch(gpu, read_ids):
             pairs = per_keys[r] if per_rids is None else \
                 (per_keys[r] << np.uint64(8)) | per_rids[r].astype(np.uint64)
             if dd:
-                # the distinct (key, read id) requests of each chunk (the sort orders by key, then
-                # read id), plus the cuts of runs longer than 64 callers
-                assert np.unique(pairs).size <= routed <= min(nk, np.unique(pairs).size * 4 + nk // 64 + 4)
+                # the distinct (key, read id) requests of the batch, plus the cuts of the sorted
+                # batch every 64 positions (a run of > 64 callers travels as several requests)
+                assert np.unique(pairs).size <= routed <= min(nk, np.unique(pairs).size + nk // 64 + 1)
                 assert routed < 0.8 * nk
             else:
                 assert routed == nk
