@@ -94,7 +94,7 @@ def parse(argv=None):
     p.add_argument("--inflight-share", type=float, default=0.02,
                    help="c3: share of the update ops left in flight (uncommitted; keys beyond the 10^4 hottest) "
                         "so reads of them take the overwrite-copy (COPY) branch")
-    p.add_argument("--c3-epochs", type=int, default=3, help="timed YCSB-B epochs of the nested C3 leg")
+    p.add_argument("--c3-epochs", type=int, default=8, help="timed YCSB-B epochs of the nested C3 leg")
     p.add_argument("--write-path", choices=["device", "host"], default="device",
                    help="c3: apply each epoch's updates on the device (stage_update_batch_device) or on the "
                         "host write path + incremental publish (stage_update_batch + stage_sync)")
@@ -111,7 +111,7 @@ def parse(argv=None):
                    help="control plane only (no GPU): ranks rendezvous over gloo, load their shard's host "
                         "table, time a routing step; for CPU tests of the launcher")
     a = p.parse_args(argv)
-    a.steps = a.steps if a.steps is not None else (5 if a.config == "c3" else (10 if a.config == "tpcc" else 20))
+    a.steps = a.steps if a.steps is not None else (10 if a.config in ("c3", "tpcc") else 20)
     a.warmup = a.warmup if a.warmup is not None else (1 if a.config == "c3" else 3)
     a.theta = a.theta if a.theta is not None else (0.99 if a.config == "c3" else 0.9)
     a.batch = a.batch if a.batch is not None else ((1 << 18) if a.config in ("c4", "tpcc") else (1 << 24))
@@ -680,9 +680,22 @@ class YcsbB:
         # host write path: LeafNode::Update + commit on the host table, then the incremental
         # publish of the touched leaves (stage_update_batch + stage_sync)
         cols = np.repeat(ep["colb"][:, None], 100, 1)
-        _, ok = self.tab.update_batch(ep["keys"], 0, cols, ep["rid"], ep["cid"])
+        ep["rc_host"], ok = self.tab.update_batch(ep["keys"], 0, cols, ep["rid"], ep["cid"])
         self.tab.sync()
         return ok
+
+    RC_NAMES = {stage.RC_OK: "ok", stage.RC_NOT_NEEDED_UPDATE: "not_needed_update", stage.RC_DIRTY: "dirty",
+                stage.RC_NOT_FOUND: "not_found", stage.RC_INVALID: "invalid"}
+
+    @staticmethod
+    def rc_counts(ep):
+        """the epoch's update return codes by name (LeafNode::Update's ReturnCode)"""
+        m = ep["keys"].size
+        if not m:
+            return {}
+        rc = ep["rc_host"] if "rc_host" in ep else ep["d"]["rc"].to_numpy(np.uint8, m)
+        v, c = np.unique(rc, return_counts=True)
+        return {YcsbB.RC_NAMES.get(int(x), f"rc{int(x)}"): int(k) for x, k in zip(v, c)}
 
     @staticmethod
     def count_ok(ep):
@@ -1191,6 +1204,10 @@ def c3_leg(tab, args, stream, nthreads, steps, warmup):
         check(L.stage_device_sync(), "sync")
         updates = sum(YcsbB.count_ok(ep) for ep in epochs[warm:])
     kern_ms = float(np.mean(probe_ms))
+    rc_hist = {}
+    for ep in epochs[warm:]:
+        for k, v in YcsbB.rc_counts(ep).items():
+            rc_hist[k] = rc_hist.get(k, 0) + v
     hist = np.zeros(6, np.int64)
     hops = 0
     for ep in epochs[warm:]:
@@ -1212,6 +1229,11 @@ def c3_leg(tab, args, stream, nthreads, steps, warmup):
                     "inflight_share": args.inflight_share, "updates_applied": updates,
                     "update_ops": int(sum(ep["keys"].size for ep in epochs[warm:])),
                     "updates_in_flight": int(sum(ep["inflight"] for ep in epochs[warm:])),
+                    # why update ops fail: not_needed_update = the column already holds the value
+                    # (YCSB-B's patch byte is a function of key and epoch, so a hot key's repeats in
+                    # an epoch find their own value) or a newer committed writer; dirty = the
+                    # record is in flight (an uncommitted update earlier in the epoch)
+                    "update_rc_counts": rc_hist,
                     "write_path": args.write_path, "write_call_s": round(write_s, 4), "loop_s": round(loop_s, 4),
                     "epoch_prep_s_untimed": round(prep_s, 2), "mean_chain_hops": round(mean_hops, 4),
                     # copies / versions / heap images are append-only (no GC, as the reference

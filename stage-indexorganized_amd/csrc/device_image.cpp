@@ -28,20 +28,25 @@ DeviceImage::~DeviceImage() { release(); }
 
 void DeviceImage::release() {
     for (DevBuf *b :
-         {&head, &okey, &slot, &tree, &tree_len, &heap, &chdr, &vhdr, &arena, &descs, &patch, &scratch, &wp_out}) {
+         {&head, &okey, &slot, &tree, &tree_len, &heap, &chdr, &vhdr, &arena, &descs, &patch, &scratch, &wp_out[0],
+          &wp_out[1], &wp_bases}) {
         if (b->p) (void)hipFree(b->p);
         b->p = nullptr;
         b->cap = 0;
     }
-    if (pinned) (void)hipHostFree(pinned);
-    pinned = nullptr;
-    pinned_cap = 0;
+    for (int k = 0; k < 2; ++k) {
+        if (pinned[k]) (void)hipHostFree(pinned[k]);
+        pinned[k] = nullptr;
+        pinned_cap[k] = 0;
+        if (adopt_ev[k]) (void)hipEventDestroy(adopt_ev[k]);
+        adopt_ev[k] = nullptr;
+        if (export_ev[k]) (void)hipEventDestroy(export_ev[k]);
+        export_ev[k] = nullptr;
+    }
     if (stream) (void)hipStreamDestroy(stream);
     stream = nullptr;
     if (adopt_stream) (void)hipStreamDestroy(adopt_stream);
     adopt_stream = nullptr;
-    if (adopt_ev) (void)hipEventDestroy(adopt_ev);
-    adopt_ev = nullptr;
     valid = false;
 }
 
@@ -170,31 +175,32 @@ uint8_t *scratch_bytes(DeviceImage &d, uint64_t bytes) {
     return (uint8_t *)d.scratch.p;
 }
 
-uint8_t *pinned_bytes(DeviceImage &d, uint64_t bytes) {
-    if (d.pinned_cap < bytes) {
-        if (d.pinned) hip_check(hipHostFree(d.pinned), "hipHostFree staging");
-        d.pinned = nullptr;
-        d.pinned_cap = 0;
+uint8_t *pinned_bytes(DeviceImage &d, uint64_t bytes, int k) {
+    if (d.pinned_cap[k] < bytes) {
+        if (d.pinned[k]) hip_check(hipHostFree(d.pinned[k]), "hipHostFree staging");
+        d.pinned[k] = nullptr;
+        d.pinned_cap[k] = 0;
         const uint64_t want = bytes + bytes / 4 + 4096;
-        hip_check(hipHostMalloc(&d.pinned, want, hipHostMallocDefault), "pinned staging");
-        d.pinned_cap = want;
+        hip_check(hipHostMalloc(&d.pinned[k], want, hipHostMallocDefault), "pinned staging");
+        d.pinned_cap[k] = want;
     }
-    return (uint8_t *)d.pinned;
+    return (uint8_t *)d.pinned[k];
 }
 
-uint8_t *wp_out_bytes(DeviceImage &d, uint64_t bytes) {
-    if (d.wp_out.cap < bytes) {
-        if (d.wp_out.p) {
+uint8_t *wp_out_bytes(DeviceImage &d, uint64_t bytes, int k) {
+    DevBuf &b = d.wp_out[k];
+    if (b.cap < bytes) {
+        if (b.p) {
             hip_check(hipDeviceSynchronize(), "wp_out drain");
-            hip_check(hipFree(d.wp_out.p), "hipFree wp_out");
+            hip_check(hipFree(b.p), "hipFree wp_out");
         }
-        d.wp_out.p = nullptr;
-        d.wp_out.cap = 0;
+        b.p = nullptr;
+        b.cap = 0;
         const uint64_t want = bytes + bytes / 8 + 4096;
-        hip_check(hipMalloc(&d.wp_out.p, want), "wp_out");
-        d.wp_out.cap = want;
+        hip_check(hipMalloc(&b.p, want), "wp_out");
+        b.cap = want;
     }
-    return (uint8_t *)d.wp_out.p;
+    return (uint8_t *)b.p;
 }
 
 void reserve_device_rows(HostTable &h, DeviceImage &d, uint64_t extra_images, uint64_t extra_copies,

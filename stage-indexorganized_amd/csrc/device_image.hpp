@@ -21,12 +21,17 @@ struct DeviceImage {
     hipStream_t stream = nullptr;
     DevBuf head, okey, slot, tree, tree_len, heap, chdr, vhdr, arena, descs, patch;
     DevBuf scratch;  // per-call scratch of the device write path / stock-level (scratch_bytes)
-    DevBuf wp_out;   // the write path's slot words + totals, read by its background adoption
+    // the device write path's per-epoch outputs, double-buffered by epoch parity: epoch e's
+    // background adoption reads wp_out[e % 2] / pinned[e % 2] while epoch e + 1 runs
+    DevBuf wp_out[2];  // slot words + totals
+    DevBuf wp_bases;   // the next epoch's copy / version / image indices (device-side append counters)
+    uint64_t wp_ub[3] = {0, 0, 0};       // upper bounds of those counters (copies, versions, images)
     hipStream_t adopt_stream = nullptr;  // the adoption's D2H copies (beside the caller's stream)
-    hipEvent_t adopt_ev = nullptr;       // end of an epoch's write-path kernels
+    hipEvent_t adopt_ev[2] = {nullptr, nullptr};  // end of an epoch's write-path kernels
+    hipEvent_t export_ev[2] = {nullptr, nullptr}; // end of its export into pinned host memory
     std::vector<uint8_t> staging;  // host staging of incremental patches
-    void *pinned = nullptr;        // pinned host staging of the device write path's epoch results
-    uint64_t pinned_cap = 0;
+    void *pinned[2] = {nullptr, nullptr};  // pinned host staging of the epoch results
+    uint64_t pinned_cap[2] = {0, 0};
     uint64_t heap_rows = 0;  // rows the heap buffer can hold
     DevTable view{};
     std::vector<uint32_t> host_to_dev;  // host leaf id -> leaf index in key order
@@ -50,11 +55,11 @@ void hip_check(hipError_t e, const char *what);
 // next call on the same table).  Stream-ordered pool memory (hipMallocAsync) is not used: on
 // gfx950 its reuse across calls showed stale reads on other XCDs between kernels of a stream.
 uint8_t *scratch_bytes(DeviceImage &d, uint64_t bytes);
-// pinned host buffer of at least `bytes` (grown with hipHostMalloc; reused by the next call)
-uint8_t *pinned_bytes(DeviceImage &d, uint64_t bytes);
-// the write path's own output buffer (not shared with scratch_bytes users: its background
-// adoption reads it after the call returned; the next write-path call settles first)
-uint8_t *wp_out_bytes(DeviceImage &d, uint64_t bytes);
+// pinned host buffer `k` (0/1) of at least `bytes` (grown with hipHostMalloc; reused by later calls)
+uint8_t *pinned_bytes(DeviceImage &d, uint64_t bytes, int k = 0);
+// the write path's own output buffer `k` (0/1; not shared with scratch_bytes users: its
+// background adoption reads it after the call returned)
+uint8_t *wp_out_bytes(DeviceImage &d, uint64_t bytes, int k = 0);
 
 // grow the record heap and the copy / version header arrays so that `extra_*` more entries fit
 // after the host's current counts (device write path); refreshes the DevTable view

@@ -8,6 +8,8 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <atomic>
+#include <chrono>
 #include <thread>
 
 #include "../../include/stage_hip.h"
@@ -39,26 +41,48 @@ struct stage_table {
     std::mutex pipe_mu;  // serialises stage_probe_host calls on this table
     std::unique_ptr<stage::HostPipe, stage::HostPipeDeleter> pipe;
     // the device write path hands its epoch's bookkeeping (new copy / version headers, slot
-    // words) to the host table on this thread while the device goes on (write_path.hip);
+    // words) to the host table on a thread of its own while the device goes on (write_path.hip);
     // every entry point that reads or writes the host table settles it first (host()).
-    // adopt_mu guards `adopt`: settle() may run on any caller thread while the writer (the
-    // thread calling stage_update_batch_device) starts the next adoption.  A failed adoption
-    // is sticky: the host table missed an epoch of the device, so every later host-table call
-    // (the writer's included) reports it.
+    // Adoptions are pipelined: epoch e + 1's kernels are enqueued while epoch e is still being
+    // adopted (the device keeps its own append counters); epoch e + 1's adoption thread joins
+    // epoch e's before it touches the host table, so epochs are adopted in order.  adopt_mu
+    // guards `adopt` (the newest thread): settle() may run on any caller thread while the writer
+    // starts the next adoption.  A failed adoption is sticky: the host table missed an epoch of
+    // the device, so every later host-table call (the writer's included) reports it.
     std::mutex adopt_mu;
     std::thread adopt;
-    std::exception_ptr adopt_err;  // written by the adoption thread before it ends, read after join
+    std::exception_ptr adopt_err;        // written by an adoption thread, read after its join
+    uint64_t wp_started = 0;             // device epochs enqueued (the writer's count)
+    std::atomic<uint64_t> wp_adopted{0}; // device epochs adopted (or failed) -- in order
+    std::atomic<bool> adopt_failed{false};
+    std::atomic<uint64_t> adopted_sz[3] = {{0}, {0}, {0}};  // host copies / versions / images after the last adoption
+    uint64_t wp_epoch_n[2] = {0, 0};                          // ops of the writer's last two epochs (by parity)
     void settle() {
         std::lock_guard<std::mutex> g(adopt_mu);
         if (adopt.joinable()) adopt.join();
         if (adopt_err) std::rethrow_exception(adopt_err);
     }
-    // starts the adoption of an epoch (after settle(): no adoption is running)
+    // starts the adoption of epoch `epoch`: a thread that first joins the previous adoption
     template <class F>
-    void start_adoption(F &&fn) {
+    void start_adoption(uint64_t epoch, F &&fn) {
         std::lock_guard<std::mutex> g(adopt_mu);
-        if (adopt.joinable()) adopt.join();
-        adopt = std::thread(std::forward<F>(fn));
+        std::thread prev = std::move(adopt);
+        adopt = std::thread([this, epoch, prev = std::move(prev), fn = std::forward<F>(fn)]() mutable {
+            if (prev.joinable()) prev.join();
+            if (!adopt_err) {
+                try {
+                    fn();
+                } catch (...) {
+                    adopt_err = std::current_exception();
+                    adopt_failed.store(true, std::memory_order_release);
+                }
+            }
+            wp_adopted.store(epoch, std::memory_order_release);
+        });
+    }
+    // the writer waits until epoch `epoch` is adopted (its double-buffered outputs are free)
+    void wait_adopted(uint64_t epoch) {
+        while (wp_adopted.load(std::memory_order_acquire) < epoch) std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
     ~stage_table() {
         std::lock_guard<std::mutex> g(adopt_mu);

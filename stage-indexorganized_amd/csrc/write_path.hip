@@ -9,16 +9,22 @@
 //   2. group    radix sort of (slot location, op index): a slot's ops stay in batch order;
 //   3. decide   every op's return code.  An op's outcome depends only on the slot state left
 //               by the previous successful op of its group (in-flight flag, cstamp, the
-//               patched column); failures leave the state unchanged.  Each op is first
+//               patched column); failures leave the state unchanged.  The column comparison
+//               (new value == current value: NotNeededUpdate) is prepared once per op by
+//               wp_classify: runs of equal deltas in sorted order share a class number, and
+//               every delta (and each group's epoch-start window) has a 64-bit content
+//               fingerprint -- same class: equal; different fingerprints: different; only a
+//               fingerprint match across classes compares the bytes.  Each op is first
 //               evaluated as if its predecessor succeeded, which is exact for the group's
 //               leading run of successes; a group with a failure is finished by one wave that
 //               evaluates the next 64 ops against the last success and jumps to the first that
 //               succeeds;
 //   4. number   exclusive scan of successes and commits: overwrite-copy, image and version
 //               indices in (slot, batch) order;
-//   5. write    per success (one wave) the overwrite-copy header, the retired-version header
-//               when committed, and the new heap row: the record's row at epoch start with the
-//               column window patched (all ops of a call patch the same window, so the k-th
+//   5. write    per success the overwrite-copy header and the retired-version header when
+//               committed (one thread per op, wp_headers), then the new heap row (a 16-lane
+//               team per success, wp_write): the record's row at epoch start with the column
+//               window patched (all ops of a call patch the same window, so the k-th
 //               successive image is the epoch-start row with the k-th delta);
 //   6. publish  the last success of each group rewrites the slot word (meta, next, image).
 // The host then adopts the bookkeeping (HostTable::adopt_device_epoch): the new copy / version
@@ -60,38 +66,142 @@ struct WpArgs {
 
 __device__ __forceinline__ uint32_t commit_of(const WpArgs &a, uint32_t o) { return a.cid ? a.cid[o] : 0u; }
 
-// reference ReturnCode of op at sorted position q given the slot state after sorted position
-// `last` (-1: the state at epoch start)
-__device__ uint8_t wp_eval(const WpArgs &a, const DevTable &t, uint64_t q, int64_t last, const SlotInfo &base) {
+// per sorted position q (wp_classify): cls = number of breaks up to q, where a break is a group
+// head or a delta unequal to its predecessor's (so cls[q] == cls[p], p < q in one group, means
+// equal deltas); fp = the delta's content fingerprint; for group heads, eqw = the delta equals
+// the epoch-start window, wfp = the window's fingerprint
+struct WpCls {
+    const uint32_t *cls;
+    const uint64_t *fp, *wfp;
+    const uint8_t *eqw;
+};
+
+__device__ __forceinline__ bool bytes_equal(const uint8_t *d, const uint8_t *w, uint32_t len) {
+    uint32_t diff = 0;
+    if ((((uintptr_t)d | (uintptr_t)w | len) & 3u) == 0) {
+        const uint32_t *dw = reinterpret_cast<const uint32_t *>(d), *ww = reinterpret_cast<const uint32_t *>(w);
+#pragma unroll 8
+        for (uint32_t b = 0; b < len / 4; ++b) diff |= dw[b] ^ ww[b];
+    } else {
+#pragma unroll 8
+        for (uint32_t b = 0; b < len; ++b) diff |= (uint32_t)(d[b] ^ w[b]);
+    }
+    return diff == 0;
+}
+
+// reference ReturnCode of op at sorted position q (group head g) given the slot state after
+// sorted position `last` (-1: the state at epoch start, base)
+__device__ uint8_t wp_eval(const WpArgs &a, const WpCls &k, const DevTable &t, uint64_t q, uint64_t g, int64_t last,
+                           const SlotInfo &base) {
     const uint32_t o = a.op[q];
     bool inserting;
     uint32_t cst;
-    const uint8_t *win;
     if (last < 0) {
         inserting = meta_inserting(base.meta);
         cst = meta_cstamp(base.meta);
-        win = t.heap + (uint64_t)base.image * t.hstride + a.win_off;
     } else {
-        const uint32_t lo = a.op[last];
-        cst = commit_of(a, lo);
+        cst = commit_of(a, a.op[last]);
         inserting = cst == 0;  // an uncommitted update leaves the record in flight
-        win = a.deltas + (uint64_t)lo * a.delta_len;
     }
     if (inserting) return STAGE_RC_DIRTY;
     if (a.bad_range) return STAGE_RC_INVALID;
     const uint8_t *d = a.deltas + (uint64_t)o * a.delta_len;
-    // no early exit: the loads of a whole window are independent and issue back to back
-    uint32_t diff = 0;
-    if ((((uintptr_t)d | (uintptr_t)win | a.delta_len) & 3u) == 0) {
-        const uint32_t *dw = reinterpret_cast<const uint32_t *>(d), *ww = reinterpret_cast<const uint32_t *>(win);
-#pragma unroll 8
-        for (uint32_t b = 0; b < a.delta_len / 4; ++b) diff |= dw[b] ^ ww[b];
+    bool eq;
+    if (last >= 0) {
+        if (k.cls[q] == k.cls[last]) eq = true;
+        else if (k.fp[q] != k.fp[last]) eq = false;
+        else eq = bytes_equal(d, a.deltas + (uint64_t)a.op[last] * a.delta_len, a.delta_len);
     } else {
-#pragma unroll 8
-        for (uint32_t b = 0; b < a.delta_len; ++b) diff |= (uint32_t)(d[b] ^ win[b]);
+        if (k.cls[q] == k.cls[g]) eq = k.eqw[g] != 0;
+        else if (k.fp[q] != k.wfp[g]) eq = false;
+        else eq = bytes_equal(d, t.heap + (uint64_t)base.image * t.hstride + a.win_off, a.delta_len);
     }
-    if (diff == 0 || cst > a.writer[o]) return STAGE_RC_NOT_NEEDED_UPDATE;
+    if (eq || cst > a.writer[o]) return STAGE_RC_NOT_NEEDED_UPDATE;
     return STAGE_RC_OK;
+}
+
+// bytes [4k, 4k + 4) of p (those below len; the rest read as 0)
+__device__ __forceinline__ uint32_t ld_word(const uint8_t *p, uint32_t k, uint32_t len, bool aligned) {
+    if (aligned && 4 * k + 4 <= len) return reinterpret_cast<const uint32_t *>(p)[k];
+    uint32_t v = 0;
+    for (uint32_t j = 0; j < 4; ++j)
+        if (4 * k + j < len) v |= (uint32_t)p[4 * k + j] << (8 * j);
+    return v;
+}
+
+__device__ __forceinline__ uint64_t fmix64(uint64_t h) {
+    h ^= h >> 33;
+    h *= 0xff51afd7ed558ccdull;
+    h ^= h >> 33;
+    h *= 0xc4ceb9fe1a85ec53ull;
+    h ^= h >> 33;
+    return h;
+}
+__device__ __forceinline__ uint64_t word_fp(uint32_t w, uint32_t k) {
+    return fmix64(((uint64_t)k << 32 | w) ^ 0x9e3779b97f4a7c15ull);
+}
+
+// step 3 preparation: a team of kTeam lanes per sorted position reads its delta (and its
+// predecessor's, or at a group head the epoch-start window) with word loads, 4 per lane in
+// flight together
+constexpr uint32_t kTeam = 8;
+__global__ __launch_bounds__(256) void wp_classify(WpArgs a, DevTable t, uint32_t *__restrict__ brk,
+                                                   uint64_t *__restrict__ fp, uint64_t *__restrict__ wfp,
+                                                   uint8_t *__restrict__ eqw) {
+    const uint32_t lane = threadIdx.x & 63, tl = lane & (kTeam - 1);
+    const uint64_t q = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / kTeam;
+    const bool live = q < a.n && a.loc[q] != a.none;
+    const bool head = live && a.gs[q] == q;
+    const uint8_t *d = nullptr, *p = nullptr;
+    if (live) {
+        d = a.deltas + (uint64_t)a.op[q] * a.delta_len;
+        p = head ? t.heap + (uint64_t)t.slot[a.loc[q]].image * t.hstride + a.win_off
+                 : a.deltas + (uint64_t)a.op[q - 1] * a.delta_len;
+    }
+    const bool al = live && ((((uintptr_t)d | (uintptr_t)p) & 3u) == 0);
+    uint64_t h = 0, hw = 0;
+    bool ne = false;
+    const uint32_t words = live ? (a.delta_len + 3) / 4 : 0u;
+    for (uint32_t k0 = 0; k0 < words; k0 += 4 * kTeam) {
+        uint32_t x[4], y[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t k = k0 + u * kTeam + tl;
+            x[u] = k < words ? ld_word(d, k, a.delta_len, al) : 0u;
+            y[u] = k < words ? ld_word(p, k, a.delta_len, al) : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t k = k0 + u * kTeam + tl;
+            if (k < words) {
+                h ^= word_fp(x[u], k);
+                hw ^= word_fp(y[u], k);
+                ne |= x[u] != y[u];
+            }
+        }
+    }
+    const uint64_t nem = __builtin_amdgcn_ballot_w64(ne);
+    const bool team_ne = ((nem >> (lane & ~(kTeam - 1))) & ((1ull << kTeam) - 1)) != 0;
+#pragma unroll
+    for (int o = kTeam / 2; o > 0; o >>= 1) {
+        h ^= __shfl_xor(h, o, 64);
+        hw ^= __shfl_xor(hw, o, 64);
+    }
+    if (tl == 0 && q < a.n) {
+        brk[q] = !live || head || team_ne ? 1u : 0u;
+        fp[q] = h;
+        if (head) {
+            wfp[q] = hw;
+            eqw[q] = team_ne ? 0 : 1;
+        }
+    }
+}
+
+// lanes [from, lane) of a wave
+__device__ __forceinline__ uint64_t lanes_between(uint32_t from, uint32_t lane) {
+    const uint64_t below = lane ? ~0ull >> (64 - lane) : 0ull;
+    const uint64_t skip = from ? ~0ull >> (64 - from) : 0ull;
+    return below & ~skip;
 }
 
 __global__ void wp_keys(const stage_probe_out_dev *__restrict__ pout, uint64_t n, uint32_t cap, uint64_t none,
@@ -110,24 +220,30 @@ __global__ void wp_heads(const uint64_t *__restrict__ loc, uint64_t n, uint32_t 
 }
 
 // step 3a: every op evaluated against its predecessor-as-success
-__global__ void wp_speculate(WpArgs a, DevTable t, uint8_t *__restrict__ rcs, uint8_t *__restrict__ succ,
+__global__ void wp_speculate(WpArgs a, WpCls k, DevTable t, uint8_t *__restrict__ rcs, uint8_t *__restrict__ succ,
                              int32_t *__restrict__ prev, uint32_t *__restrict__ first_fail) {
-    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // blockDim: a multiple of 64
     if (q >= a.n) return;
-    if (a.loc[q] == a.none) {
-        rcs[q] = STAGE_RC_NOT_FOUND;
-        succ[q] = 0;
-        prev[q] = -1;
-        return;
-    }
+    const uint32_t lane = threadIdx.x & 63;
+    const bool found = a.loc[q] != a.none;
     const uint32_t g = a.gs[q];
     const int64_t last = q > g ? (int64_t)q - 1 : -1;
-    const SlotInfo base = t.slot[a.loc[q]];
-    const uint8_t r = wp_eval(a, t, q, last, base);
+    uint8_t r = STAGE_RC_NOT_FOUND;
+    if (found) {
+        SlotInfo base{};
+        if (last < 0) base = t.slot[a.loc[q]];  // the epoch-start state matters to the head only
+        r = wp_eval(a, k, t, q, g, last, base);
+    }
     rcs[q] = r;
     succ[q] = r == STAGE_RC_OK;
-    prev[q] = (int32_t)last;
-    if (r != STAGE_RC_OK) atomicMin(&first_fail[g], (uint32_t)q);
+    prev[q] = found ? (int32_t)last : -1;
+    // a group's first failure: only the first failing lane of the group in this wave competes
+    // (a hot key's run of failures would otherwise serialise on one address)
+    const bool fail = found && r != STAGE_RC_OK;
+    const uint64_t fm = __builtin_amdgcn_ballot_w64(fail);
+    const uint64_t wbase = q - lane;
+    const uint32_t glane = g > wbase ? (uint32_t)(g - wbase) : 0u;
+    if (fail && !(fm & lanes_between(glane, lane))) atomicMin(&first_fail[g], (uint32_t)q);
 }
 
 // step 3b: groups with a failure, one wave each, from the first failure on.  A pass
@@ -136,7 +252,7 @@ __global__ void wp_speculate(WpArgs a, DevTable t, uint8_t *__restrict__ rcs, ui
 // key's long run of NotNeededUpdate / DIRTY ops goes 512 ops per pass.
 constexpr int kFinishChunks = 8;
 constexpr uint32_t kBigGroup = 2048;  // ops from the first failure on: a workgroup finishes it (wp_finish_big)
-__global__ __launch_bounds__(256) void wp_finish_groups(WpArgs a, DevTable t, uint8_t *__restrict__ rcs,
+__global__ __launch_bounds__(256) void wp_finish_groups(WpArgs a, WpCls kc, DevTable t, uint8_t *__restrict__ rcs,
                                                         uint8_t *__restrict__ succ, int32_t *__restrict__ prev,
                                                         const uint32_t *__restrict__ first_fail,
                                                         const uint32_t *__restrict__ gend) {
@@ -161,7 +277,7 @@ __global__ __launch_bounds__(256) void wp_finish_groups(WpArgs a, DevTable t, ui
             for (int k = 0; k < kFinishChunks; ++k) {
                 const uint64_t q = pos + 64 * k + lane;
                 in[k] = q < a.n && a.loc[q] == l;
-                r[k] = in[k] ? wp_eval(a, t, q, last, base) : (uint8_t)0xFF;
+                r[k] = in[k] ? wp_eval(a, kc, t, q, g, last, base) : (uint8_t)0xFF;
             }
             int kf = -1;
             uint32_t first = 0;
@@ -215,7 +331,7 @@ __global__ void wp_big_groups(WpArgs a, const uint32_t *__restrict__ first_fail,
 // step 3b for big groups: one 1024-thread workgroup per group, 16 waves x kFinishChunks x 64 =
 // 8192 ops evaluated against the last success per pass, the first success in batch order
 // found across the waves through LDS
-__global__ __launch_bounds__(1024) void wp_finish_big(WpArgs a, DevTable t, uint8_t *__restrict__ rcs,
+__global__ __launch_bounds__(1024) void wp_finish_big(WpArgs a, WpCls kc, DevTable t, uint8_t *__restrict__ rcs,
                                                       uint8_t *__restrict__ succ, int32_t *__restrict__ prev,
                                                       const uint32_t *__restrict__ first_fail,
                                                       const uint32_t *__restrict__ gend,
@@ -238,7 +354,7 @@ __global__ __launch_bounds__(1024) void wp_finish_big(WpArgs a, DevTable t, uint
 #pragma unroll
             for (int k = 0; k < kFinishChunks; ++k) {
                 const uint64_t q = pos + (uint64_t)wv * (kFinishChunks * 64) + 64 * k + lane;
-                r[k] = q < end ? wp_eval(a, t, q, last, base) : (uint8_t)0xFF;
+                r[k] = q < end ? wp_eval(a, kc, t, q, g, last, base) : (uint8_t)0xFF;
                 if (r[k] == STAGE_RC_OK && q < mine_first) mine_first = q;
             }
             // the wave's first success, then the block's
@@ -280,66 +396,121 @@ __global__ void wp_flags(WpArgs a, const uint8_t *__restrict__ succ, uint64_t *_
     flags[q] = s | ((s && commit_of(a, a.op[q]) != 0) ? (1ull << 32) : 0ull);
 }
 
+// tot = {successes, committed successes, this epoch's copy / version / image bases}; the
+// device's append counters (bases) move past this epoch's entries
 __global__ void wp_totals(const uint64_t *__restrict__ ranks, const uint64_t *__restrict__ flags, uint64_t n,
-                          uint64_t *__restrict__ tot) {
+                          uint64_t *__restrict__ tot, uint64_t *__restrict__ bases) {
     const uint64_t v = ranks[n - 1] + flags[n - 1];
-    tot[0] = v & 0xFFFFFFFFull;
-    tot[1] = v >> 32;
+    const uint64_t ns = v & 0xFFFFFFFFull, nv = v >> 32;
+    tot[0] = ns;
+    tot[1] = nv;
+    tot[2] = bases[0];
+    tot[3] = bases[1];
+    tot[4] = bases[2];
+    bases[0] += ns;
+    bases[1] += nv;
+    bases[2] += ns;
 }
 
-// step 5: one wave per sorted position; successes write their headers and their new row
-__global__ __launch_bounds__(256) void wp_write(WpArgs a, DevTable t, uint8_t *__restrict__ heap,
-                                                CopyHdr *__restrict__ chdr, VersionHdr *__restrict__ vhdr,
-                                                const uint8_t *__restrict__ succ, const int32_t *__restrict__ prev,
-                                                const uint64_t *__restrict__ ranks, uint32_t *__restrict__ last_succ,
-                                                uint64_t cbase, uint64_t vbase, uint64_t ibase) {
+__global__ void wp_set_bases(uint64_t *__restrict__ bases, uint64_t c, uint64_t v, uint64_t i) {
+    bases[0] = c;
+    bases[1] = v;
+    bases[2] = i;
+}
+
+// what wp_write needs per success, at its success rank: the epoch-start image to copy and the op
+struct WRec {
+    uint32_t image, op;
+};
+
+// step 5a, one thread per sorted position: a success writes its overwrite-copy header, the
+// retired-version header when committed, and its WRec; the last success of each group is
+// marked (last_succ; one atomic per group per wave)
+__global__ void wp_headers(WpArgs a, DevTable t, const uint8_t *__restrict__ succ, const int32_t *__restrict__ prev,
+                           const uint64_t *__restrict__ ranks, CopyHdr *__restrict__ chdr, VersionHdr *__restrict__ vhdr,
+                           uint32_t *__restrict__ last_succ, WRec *__restrict__ wrec, const uint64_t *__restrict__ tot) {
+    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // blockDim: a multiple of 64
+    if (q >= a.n) return;
+    const uint64_t cbase = tot[2], vbase = tot[3], ibase = tot[4];
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    for (uint64_t q = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); q < a.n; q += nwaves) {
-        if (!succ[q]) continue;
+    const bool ok = succ[q] != 0;
+    const uint32_t g = a.gs[q];
+    if (ok) {
         const uint32_t o = a.op[q];
         const SlotInfo base = t.slot[a.loc[q]];
         const uint64_t rk = ranks[q];
         const uint64_t irank = rk & 0xFFFFFFFFull, vrank = rk >> 32;
         const uint32_t cid = commit_of(a, o);
-        const uint64_t img = ibase + irank;
-        if (lane == 0) {
-            const int32_t p = prev[q];
-            CopyHdr c;
-            if (p < 0) {  // first success of the group: the epoch-start record
-                c.rstamp = meta_cstamp(base.meta);
-                c.next = base.next;
-                c.image = base.image;
-            } else {      // the previous success, committed (an in-flight one makes this op DIRTY)
-                const uint64_t pr = ranks[p];
-                c.rstamp = commit_of(a, a.op[p]);
-                c.next = kNextVersion | (uint32_t)(vbase + (pr >> 32));
-                c.image = (uint32_t)(ibase + (pr & 0xFFFFFFFFull));
-            }
-            c.sstamp = cid ? (a.sst ? a.sst[o] : cid) : kMaxCid;
-            chdr[cbase + irank] = c;
-            if (cid) vhdr[vbase + vrank] = VersionHdr{c.rstamp, c.sstamp, c.next, c.image};
-            atomicMax(&last_succ[a.gs[q]], (uint32_t)q + 1u);
+        const int32_t p = prev[q];
+        CopyHdr c;
+        if (p < 0) {  // first success of the group: the epoch-start record
+            c.rstamp = meta_cstamp(base.meta);
+            c.next = base.next;
+            c.image = base.image;
+        } else {      // the previous success, committed (an in-flight one makes this op DIRTY)
+            const uint64_t pr = ranks[p];
+            c.rstamp = commit_of(a, a.op[p]);
+            c.next = kNextVersion | (uint32_t)(vbase + (pr >> 32));
+            c.image = (uint32_t)(ibase + (pr & 0xFFFFFFFFull));
         }
-        // new row: epoch-start row with the window patched (CopyPayload)
-        const uint8_t *src = t.heap + (uint64_t)base.image * t.hstride;
-        uint8_t *dst = heap + img * t.hstride;
-        const uint8_t *d = a.deltas + (uint64_t)o * a.delta_len;
-        const uint32_t w0 = a.win_off, w1 = a.win_off + a.delta_len;
-        for (uint32_t c = lane; c < t.hstride / 16; c += 64) {
-            u32x4 v = reinterpret_cast<const u32x4 *>(src)[c];
-            const uint32_t b0 = c * 16;
-            if (b0 + 16 > w0 && b0 < w1) {
-                union {
-                    u32x4 v;
-                    uint8_t b[16];
-                } u;
-                u.v = v;
-                for (uint32_t j = 0; j < 16; ++j)
-                    if (b0 + j >= w0 && b0 + j < w1) u.b[j] = d[b0 + j - w0];
-                v = u.v;
+        c.sstamp = cid ? (a.sst ? a.sst[o] : cid) : kMaxCid;
+        chdr[cbase + irank] = c;
+        if (cid) vhdr[vbase + vrank] = VersionHdr{c.rstamp, c.sstamp, c.next, c.image};
+        wrec[irank] = WRec{base.image, o};
+    }
+    // the group's last success in this wave (no later lane of the group -- the lanes up to the
+    // next group head -- succeeded) competes for last_succ
+    const uint64_t sm = __builtin_amdgcn_ballot_w64(ok);
+    const uint64_t hm = __builtin_amdgcn_ballot_w64(g == q);
+    const uint64_t after = lane == 63 ? 0ull : ~0ull << (lane + 1);
+    const uint64_t nh = hm & after;
+    const uint64_t mine_after = after & (nh ? (nh & (~nh + 1)) - 1 : ~0ull);
+    if (ok && !(sm & mine_after)) atomicMax(&last_succ[g], (uint32_t)q + 1u);
+}
+
+// step 5b: the new rows, a team of 16 lanes per success (4 per wave, 4 chunks of 16 B per lane
+// in flight): the epoch-start row with the column window patched (CopyPayload)
+constexpr uint32_t kRowTeam = 16;
+__global__ __launch_bounds__(256) void wp_write(WpArgs a, DevTable t, uint8_t *__restrict__ heap,
+                                                const WRec *__restrict__ wrec, const uint64_t *__restrict__ tot) {
+    const uint64_t ibase = tot[4];
+    const uint32_t tl = threadIdx.x & (kRowTeam - 1);
+    const uint64_t nteams = (uint64_t)gridDim.x * (blockDim.x / kRowTeam);
+    const uint64_t ns = tot[0];
+    const uint32_t chunks = t.hstride / 16;
+    const uint32_t w0 = a.win_off, w1 = a.win_off + a.delta_len;
+    for (uint64_t si = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / kRowTeam; si < ns; si += nteams) {
+        const WRec w = wrec[si];
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(t.heap + (uint64_t)w.image * t.hstride);
+        u32x4 *dst = reinterpret_cast<u32x4 *>(heap + (ibase + si) * t.hstride);
+        const uint8_t *d = a.deltas + (uint64_t)w.op * a.delta_len;
+        for (uint32_t c0 = 0; c0 < chunks; c0 += 4 * kRowTeam) {
+            u32x4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t c = c0 + u * kRowTeam + tl;
+                v[u] = c < chunks ? src[c] : u32x4{0, 0, 0, 0};
             }
-            reinterpret_cast<u32x4 *>(dst)[c] = v;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t c = c0 + u * kRowTeam + tl;
+                if (c >= chunks) continue;
+                const uint32_t b0 = c * 16;
+                if (b0 + 16 > w0 && b0 < w1) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        uint32_t x = v[u][k];
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const uint32_t pos = b0 + 4 * k + j;
+                            if (pos >= w0 && pos < w1)
+                                x = (x & ~(0xFFu << (8 * j))) | ((uint32_t)d[pos - w0] << (8 * j));
+                        }
+                        v[u][k] = x;
+                    }
+                }
+                dst[c] = v[u];
+            }
         }
     }
 }
@@ -353,10 +524,10 @@ struct FinRec {
 __global__ void wp_publish(WpArgs a, SlotInfo *__restrict__ slot, const uint8_t *__restrict__ rcs,
                            const uint8_t *__restrict__ succ, const int32_t *__restrict__ prev,
                            const uint64_t *__restrict__ ranks, const uint32_t *__restrict__ last_succ,
-                           uint64_t cbase, uint64_t vbase, uint64_t ibase, FinRec *__restrict__ fin,
-                           uint8_t *__restrict__ rc_out) {
+                           const uint64_t *__restrict__ tot, FinRec *__restrict__ fin, uint8_t *__restrict__ rc_out) {
     const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= a.n) return;
+    const uint64_t cbase = tot[2], vbase = tot[3], ibase = tot[4];
     const uint32_t o = a.op[q];
     rc_out[o] = rcs[q];
     if (!succ[q] || last_succ[a.gs[q]] != q + 1) return;
@@ -381,6 +552,29 @@ __global__ void wp_publish(WpArgs a, SlotInfo *__restrict__ slot, const uint8_t 
     slot[l].next = next;
     slot[l].image = image;
     fin[rk & 0xFFFFFFFFull] = FinRec{l, meta, next, image};  // at the success rank: the first ns entries
+}
+
+// the epoch's results for the host, written by the GPU straight into pinned host memory as soon
+// as the write path is done (on the adoption stream, beside the next probe): totals, the new
+// copy and version headers, the slot words -- the staging layout of stage_update_batch_device
+__global__ __launch_bounds__(256) void wp_export(const uint64_t *__restrict__ tot, const FinRec *__restrict__ fin,
+                                                 const CopyHdr *__restrict__ chdr, const VersionHdr *__restrict__ vhdr,
+                                                 uint8_t *__restrict__ pin, uint64_t fin_off) {
+    const uint64_t ns = tot[0], nv = tot[1];
+    const uint64_t *c = reinterpret_cast<const uint64_t *>(chdr + tot[2]);
+    const uint64_t *v = reinterpret_cast<const uint64_t *>(vhdr + tot[3]);
+    const uint64_t *f = reinterpret_cast<const uint64_t *>(fin);
+    uint64_t *oc = reinterpret_cast<uint64_t *>(pin + 64), *ov = oc + ns * 2;
+    uint64_t *of = reinterpret_cast<uint64_t *>(pin + fin_off);
+    static_assert(sizeof(CopyHdr) == 16 && sizeof(VersionHdr) == 16 && sizeof(FinRec) == 24, "export words");
+    const uint64_t w1 = ns * 2, w2 = w1 + nv * 2, total = w2 + ns * 3;
+    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = gid; i < total; i += stride) {
+        if (i < w1) oc[i] = c[i];
+        else if (i < w2) ov[i - w1] = v[i - w1];
+        else of[i - w2] = f[i - w2];
+    }
+    if (gid < 5) reinterpret_cast<uint64_t *>(pin)[gid] = tot[gid];
 }
 
 unsigned blocks_for(uint64_t n, unsigned per) { return (unsigned)((n + per - 1) / per); }
@@ -415,7 +609,10 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
     if (n == 0) return STAGE_OK;
     return guarded([&] {
         using namespace stage;
-        HostTable &h = host(t);
+        // the host table is NOT settled here: the previous epoch may still be adopted in the
+        // background (stage_table::start_adoption) -- this call reads only the table's fixed
+        // geometry and the device image
+        HostTable &h = *t->host;
         DeviceImage &dv = t->dev;
         hip_check(hipSetDevice(dv.device), "hipSetDevice");
         hipStream_t s = pick(t, stream);
@@ -423,12 +620,58 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         static const bool trace = std::getenv("STAGE_WP_TRACE") != nullptr;
         using clk = std::chrono::steady_clock;
         const auto t0 = clk::now();
+        static const auto g0 = t0;  // trace: the first call's start
         auto ms = [&](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
-        // room for one copy, image and version per op
-        reserve_device_rows(h, dv, n, n, n, s);
+        // epoch e uses output buffers e % 2: epoch e - 2's adoption must be done with them
+        const uint64_t epoch = ++t->wp_started;
+        const int par = (int)(epoch & 1);
+        // an epoch that fails before its adoption starts still counts as adopted -- with a
+        // sticky error (the device may hold part of it): later calls neither hang nor go on
+        struct EpochGuard {
+            stage_table *t;
+            uint64_t epoch;
+            bool started = false;
+            ~EpochGuard() {
+                if (!started)
+                    t->start_adoption(epoch, [] { throw std::runtime_error("a device write-path epoch failed"); });
+            }
+        } guard{t, epoch};
+        // STAGE_WP_PIPELINE=0: every epoch waits for the previous one's adoption (A/B of the pipeline)
+        static const bool pipeline = !(std::getenv("STAGE_WP_PIPELINE") && std::getenv("STAGE_WP_PIPELINE")[0] == '0');
+        if (!pipeline) t->settle();
+        if (epoch > 2) t->wait_adopted(epoch - 2);
+        if (t->adopt_failed.load(std::memory_order_acquire)) t->settle();  // rethrows the adoption's error
+        // pending: epoch e - 1 is still being adopted, so the device's append counters are ahead
+        // of the host table; otherwise (no epoch in flight) they are set from the host's counts
+        bool pending = t->wp_adopted.load(std::memory_order_acquire) + 1 < epoch;
+        if (!dv.wp_bases.p) {
+            hip_check(hipMalloc(&dv.wp_bases.p, 64), "wp bases");
+            dv.wp_bases.cap = 64;
+        }
+        // room for one copy, image and version per op beyond the device's counters -- at most the
+        // host's counts after the last adopted epoch plus the ops of the one still pending.
+        // Growing moves the header arrays, which a pending adoption may be reading: settle
+        // first then, and leave room for the next pipelined epoch too
+        uint64_t *ub = dv.wp_ub;
+        if (!pending) {  // no adoption running: the host's counts are the device's
+            ub[0] = h.copies_.size(), ub[1] = h.versions_.size(), ub[2] = h.images_.size();
+            for (int k = 0; k < 3; ++k) t->adopted_sz[k].store(ub[k], std::memory_order_relaxed);
+        } else {
+            for (int k = 0; k < 3; ++k) ub[k] = t->adopted_sz[k].load(std::memory_order_acquire) + t->wp_epoch_n[par ^ 1];
+        }
+        const bool fits = dv.heap_rows >= ub[2] + n && dv.chdr.cap >= (ub[0] + n) * sizeof(CopyHdr) &&
+                          dv.vhdr.cap >= (ub[1] + n) * sizeof(VersionHdr) && dv.chdr.p && dv.vhdr.p && dv.heap.p;
+        if (!fits) {  // room for the next 8 epochs of this size: a growth drains the pipeline
+            t->settle();
+            pending = false;
+            reserve_device_rows(h, dv, 8 * n, 8 * n, 8 * n, s);
+        }
+        if (!pending)
+            wp_set_bases<<<1, 1, 0, s>>>((uint64_t *)dv.wp_bases.p, h.copies_.size(), h.versions_.size(),
+                                         h.images_.size());
+        t->wp_epoch_n[par] = n;
         const double t_reserve = ms(t0);
         const DevTable &view = dv.view;
-        const uint64_t cbase = h.copies_.size(), vbase = h.versions_.size(), ibase = h.images_.size();
         const uint64_t none = (uint64_t)view.nleaves * view.cap;
         int end_bit = 1;
         while (end_bit < 64 && (none >> end_bit)) ++end_bit;
@@ -444,7 +687,10 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         hip_check(hipcub::DeviceScan::ExclusiveSum(nullptr, cub_sum, (uint64_t *)nullptr, (uint64_t *)nullptr, (int)n,
                                                    s),
                   "sum size");
-        const size_t cub_bytes = std::max(cub_sort, std::max(cub_scan, cub_sum));
+        size_t cub_cls = 0;
+        hip_check(hipcub::DeviceScan::InclusiveSum(nullptr, cub_cls, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)n, s),
+                  "class scan size");
+        const size_t cub_bytes = std::max(std::max(cub_sort, cub_cls), std::max(cub_scan, cub_sum));
         auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
         uint64_t off = 0;
         auto take = [&](uint64_t bytes) {
@@ -455,7 +701,8 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         const uint64_t o_pout = take(n * 32), o_loc0 = take(n * 8), o_loc = take(n * 8), o_op0 = take(n * 4),
                        o_op = take(n * 4), o_head = take(n * 4), o_gs = take(n * 4), o_rcs = take(n), o_succ = take(n),
                        o_prev = take(n * 4), o_ff = take(n * 4), o_ls = take(n * 4), o_gend = take(n * 4), o_big = take(n * 4), o_flags = take(n * 8),
-                       o_ranks = take(n * 8), o_cub = take(cub_bytes);
+                       o_ranks = take(n * 8), o_brk = take(n * 4), o_cls = take(n * 4),
+                       o_fp = take(n * 8), o_wfp = take(n * 8), o_eqw = take(n), o_wrec = take(n * sizeof(WRec)), o_cub = take(cub_bytes);
         uint8_t *buf = scratch_bytes(dv, off);
         auto *pout = (stage_probe_out_dev *)(buf + o_pout);
         auto *loc0 = (uint64_t *)(buf + o_loc0);
@@ -473,8 +720,18 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         auto *big = (uint32_t *)(buf + o_big);
         auto *flags = (uint64_t *)(buf + o_flags);
         auto *ranks = (uint64_t *)(buf + o_ranks);
+        auto *brk = (uint32_t *)(buf + o_brk);
+        auto *cls = (uint32_t *)(buf + o_cls);
+        auto *fpd = (uint64_t *)(buf + o_fp);
+        auto *wfp = (uint64_t *)(buf + o_wfp);
+        auto *eqw = buf + o_eqw;
+        auto *wrec = (WRec *)(buf + o_wrec);
         // slot words + totals: read back after this call returns (background adoption)
-        uint8_t *wo = wp_out_bytes(dv, al(n * sizeof(FinRec)) + 256);
+        // both parities are sized together when no adoption is reading the other one: a first
+        // use inside a run of epochs would allocate (and drain the device) in the middle of it
+        const uint64_t wo_bytes = al(n * sizeof(FinRec)) + 256;
+        uint8_t *wo = wp_out_bytes(dv, wo_bytes, par);
+        if (!pending) wp_out_bytes(dv, wo_bytes, par ^ 1);
         auto *fin = (FinRec *)wo;
         auto *tot = (uint64_t *)(wo + al(n * sizeof(FinRec)));
         void *cub = buf + o_cub;
@@ -490,50 +747,74 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         hip_check(hipcub::DeviceScan::InclusiveScan(cub, cb, head, gs, hipcub::Max(), (int)n, s), "group starts");
         // 3. decide
         WpArgs a{loc, op, gs, d_deltas, d_writer_ids, d_commit_ids, d_sstamps, n, none, delta_len,
-                 h.key_pad() + payload_off, (uint64_t)payload_off + delta_len > h.params().payload_size ? 1u : 0u};
+                 facts(t).key_pad() + payload_off,
+                 (uint64_t)payload_off + delta_len > facts(t).params().payload_size ? 1u : 0u};
         hip_check(hipMemsetAsync(ff, 0xFF, n * 4, s), "memset");
         hip_check(hipMemsetAsync(ls, 0, n * 4, s), "memset");
         hip_check(hipMemsetAsync(fin, 0xFF, n * sizeof(FinRec), s), "memset");
-        wp_speculate<<<blocks_for(n, 256), 256, 0, s>>>(a, view, rcs, succ, prev, ff);
+        wp_classify<<<blocks_for(n * kTeam, 256), 256, 0, s>>>(a, view, brk, fpd, wfp, eqw);
+        cb = cub_bytes;
+        hip_check(hipcub::DeviceScan::InclusiveSum(cub, cb, brk, cls, (int)n, s), "delta classes");
+        const WpCls kc{cls, fpd, wfp, eqw};
+        wp_speculate<<<blocks_for(n, 256), 256, 0, s>>>(a, kc, view, rcs, succ, prev, ff);
         wp_group_ends<<<blocks_for(n, 256), 256, 0, s>>>(a, gend);
         hip_check(hipMemsetAsync(tot + 1, 0, 4, s), "memset");  // big-group count (tot is rewritten in step 4)
         wp_big_groups<<<blocks_for(n, 256), 256, 0, s>>>(a, ff, gend, big, (uint32_t *)(tot + 1));
-        wp_finish_groups<<<blocks_for(n, 256), 256, 0, s>>>(a, view, rcs, succ, prev, ff, gend);
-        wp_finish_big<<<256, 1024, 0, s>>>(a, view, rcs, succ, prev, ff, gend, big, (uint32_t *)(tot + 1));
+        wp_finish_groups<<<blocks_for(n, 256), 256, 0, s>>>(a, kc, view, rcs, succ, prev, ff, gend);
+        wp_finish_big<<<256, 1024, 0, s>>>(a, kc, view, rcs, succ, prev, ff, gend, big, (uint32_t *)(tot + 1));
         // 4. number
         wp_flags<<<blocks_for(n, 256), 256, 0, s>>>(a, succ, flags);
         cb = cub_bytes;
         hip_check(hipcub::DeviceScan::ExclusiveSum(cub, cb, flags, ranks, (int)n, s), "ranks");
-        wp_totals<<<1, 1, 0, s>>>(ranks, flags, n, tot);
+        wp_totals<<<1, 1, 0, s>>>(ranks, flags, n, tot, (uint64_t *)dv.wp_bases.p);
+        wp_headers<<<blocks_for(n, 256), 256, 0, s>>>(a, view, succ, prev, ranks, (CopyHdr *)dv.chdr.p,
+                                                      (VersionHdr *)dv.vhdr.p, ls, wrec, tot);
         // 5. write, 6. publish
-        const int wblocks = (int)std::min<uint64_t>(blocks_for(n, 4), 16384);
-        wp_write<<<wblocks, 256, 0, s>>>(a, view, (uint8_t *)dv.heap.p, (CopyHdr *)dv.chdr.p, (VersionHdr *)dv.vhdr.p,
-                                         succ, prev, ranks, ls, cbase, vbase, ibase);
-        wp_publish<<<blocks_for(n, 256), 256, 0, s>>>(a, (SlotInfo *)dv.slot.p, rcs, succ, prev, ranks, ls, cbase,
-                                                      vbase, ibase, fin, d_rc);
+        const int wblocks = (int)std::min<uint64_t>(blocks_for(n, 256 / kRowTeam), 32768);
+        wp_write<<<wblocks, 256, 0, s>>>(a, view, (uint8_t *)dv.heap.p, wrec, tot);
+        wp_publish<<<blocks_for(n, 256), 256, 0, s>>>(a, (SlotInfo *)dv.slot.p, rcs, succ, prev, ranks, ls, tot, fin,
+                                                      d_rc);
         hip_check(hipGetLastError(), "write-path kernels");
 
         // the host adopts the epoch.  The headers and slot words come back on a stream of their
         // own into pinned staging (full PCIe rate) and the host adopts them on a background
-        // thread (stage_table::adopt) while the caller's stream goes on (the next probe overlaps
-        // the copies); the next call that needs the host table waits for it (host() / settle).
+        // thread (stage_table::start_adoption) while the caller's stream goes on (the next probe
+        // -- and the next epoch's write path -- overlap the copies); the next call that needs the
+        // host table waits for it (host() / settle).
         const double t_enqueue = ms(t0);
-        if (!dv.adopt_stream) hip_check(hipStreamCreateWithFlags(&dv.adopt_stream, hipStreamNonBlocking), "adopt stream");
-        if (!dv.adopt_ev) hip_check(hipEventCreateWithFlags(&dv.adopt_ev, hipEventDisableTiming), "adopt event");
-        hip_check(hipEventRecord(dv.adopt_ev, s), "adopt event");
+        if (!dv.adopt_stream) {  // high priority: the export gets its CUs beside the next probe
+            int lo = 0, hi = 0;
+            hip_check(hipDeviceGetStreamPriorityRange(&lo, &hi), "stream priorities");
+            hip_check(hipStreamCreateWithPriority(&dv.adopt_stream, hipStreamNonBlocking, hi), "adopt stream");
+        }
+        for (hipEvent_t *e : {&dv.adopt_ev[0], &dv.adopt_ev[1], &dv.export_ev[0], &dv.export_ev[1]})
+            if (!*e) hip_check(hipEventCreateWithFlags(e, hipEventDisableTiming), "adopt event");
+        const double t_events = ms(t0);
+        hip_check(hipEventRecord(dv.adopt_ev[par], s), "adopt event");
         // staging: [totals 64 B][copy headers][version headers][slot words], sized for the worst
         // case (one copy and one version per op); every part starts on a 16-B boundary (the
         // headers are 16-B aligned types: a misaligned source faults in the vectorised copy)
         const uint64_t bf = n * sizeof(FinRec), bmax = 2 * n * sizeof(CopyHdr);
         static_assert(sizeof(CopyHdr) == sizeof(VersionHdr) && sizeof(CopyHdr) % 16 == 0, "header sizes");
-        uint8_t *pin = pinned_bytes(dv, 64 + bmax + bf);
+        uint8_t *pin = pinned_bytes(dv, 64 + bmax + bf, par);
+        if (!pending) pinned_bytes(dv, 64 + bmax + bf, par ^ 1);
         auto *totals = reinterpret_cast<uint64_t *>(pin);
         auto *fr = reinterpret_cast<FinRec *>(pin + 64 + bmax);
+        const double t_pinned = ms(t0);
+        void *pin_dev = nullptr;
+        hip_check(hipHostGetDevicePointer(&pin_dev, pin, 0), "pinned device pointer");
+        hip_check(hipStreamWaitEvent(dv.adopt_stream, dv.adopt_ev[par], 0), "export wait");
+        static const int export_blocks = std::getenv("STAGE_WP_EXPORT_BLOCKS") ? std::atoi(std::getenv("STAGE_WP_EXPORT_BLOCKS")) : 32;
+        wp_export<<<export_blocks, 256, 0, dv.adopt_stream>>>(tot, fin, (const CopyHdr *)dv.chdr.p, (const VersionHdr *)dv.vhdr.p,
+                                                    (uint8_t *)pin_dev, 64 + bmax);
+        hip_check(hipGetLastError(), "export");
+        hip_check(hipEventRecord(dv.export_ev[par], dv.adopt_stream), "export event");
         uint64_t ns = 0;
         if (n_ok) {  // the caller wants the count now: wait for the kernels
-            hip_check(hipMemcpyAsync(totals, tot, 16, hipMemcpyDeviceToHost, s), "totals");
+            uint64_t tv[2] = {0, 0};
+            hip_check(hipMemcpyAsync(tv, tot, 16, hipMemcpyDeviceToHost, s), "totals");
             hip_check(hipStreamSynchronize(s), "write path");
-            ns = totals[0];
+            ns = tv[0];
         }
         const double t_kernels = ms(t0);
         // FinRec and HostTable::SlotWords share a layout: device slot locations become host slot
@@ -543,58 +824,49 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
                           offsetof(FinRec, next) == offsetof(HostTable::SlotWords, next) &&
                           offsetof(FinRec, image) == offsetof(HostTable::SlotWords, image),
                       "FinRec / SlotWords layout");
-        t->start_adoption([t, &h, &dv, cap = view.cap, n, cbase, vbase, pin, totals, fr, tot, fin, t0, t_kernels,
-                           t_enqueue, t_reserve]() mutable {
-            try {
-                hip_check(hipSetDevice(dv.device), "hipSetDevice");
-                hipStream_t a = dv.adopt_stream;
-                hip_check(hipStreamWaitEvent(a, dv.adopt_ev, 0), "adopt wait");
-                hip_check(hipMemcpyAsync(totals, tot, 16, hipMemcpyDeviceToHost, a), "totals");
-                hip_check(hipStreamSynchronize(a), "adopt totals");
-                const uint64_t ns = totals[0], nv = totals[1];
-                if (ns > n) throw std::runtime_error("write path: more successes than ops");
-                // slot words sit at the success ranks (the last success of each key; the other
-                // entries stay ~0): ns records instead of n
-                if (ns) hip_check(hipMemcpyAsync(fr, fin, ns * sizeof(FinRec), hipMemcpyDeviceToHost, a), "slot words");
-                auto *copies = reinterpret_cast<CopyHdr *>(pin + 64);
-                auto *versions = reinterpret_cast<VersionHdr *>(pin + 64 + ns * sizeof(CopyHdr));
-                if (ns)
-                    hip_check(hipMemcpyAsync(copies, (CopyHdr *)dv.chdr.p + cbase, ns * sizeof(CopyHdr),
-                                             hipMemcpyDeviceToHost, a),
-                              "copy headers");
-                if (nv)
-                    hip_check(hipMemcpyAsync(versions, (VersionHdr *)dv.vhdr.p + vbase, nv * sizeof(VersionHdr),
-                                             hipMemcpyDeviceToHost, a),
-                              "version headers");
-                hip_check(hipStreamSynchronize(a), "adopt headers");
-                const double t_d2h = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
-                const std::vector<uint32_t> &d2h = dv.dev_to_host;
-                std::atomic<uint64_t> bad{0};
-                HostTable::parallel_chunks(ns, [&](uint64_t b, uint64_t e) {
-                    for (uint64_t k = b; k < e; ++k) {
-                        if (fr[k].loc == ~0ull) continue;
-                        if (fr[k].loc / cap >= d2h.size()) {
-                            bad.fetch_add(1);
-                            fr[k].loc = ~0ull;
-                            continue;
-                        }
-                        fr[k].loc = (uint64_t)d2h[fr[k].loc / cap] * cap + fr[k].loc % cap;
+        t->start_adoption(epoch, [t, &h, &dv, par, epoch, cap = view.cap, n, pin, totals, fr, t0, t_kernels, t_enqueue,
+                           t_reserve, t_events, t_pinned]() {
+            const double t_join = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+            hip_check(hipSetDevice(dv.device), "hipSetDevice");
+            hip_check(hipEventSynchronize(dv.export_ev[par]), "adopt export");
+            const uint64_t ns = totals[0], nv = totals[1], cbase = totals[2], vbase = totals[3];
+            if (ns > n) throw std::runtime_error("write path: more successes than ops");
+            // the epochs are adopted in order: the host's counts are this epoch's bases
+            if (h.copies_.size() != cbase || h.versions_.size() != vbase || h.images_.size() != totals[4])
+                throw std::runtime_error("write path: device append counters disagree with the host table");
+            auto *copies = reinterpret_cast<CopyHdr *>(pin + 64);
+            auto *versions = reinterpret_cast<VersionHdr *>(pin + 64 + ns * sizeof(CopyHdr));
+            const double t_d2h = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+            const std::vector<uint32_t> &d2h = dv.dev_to_host;
+            std::atomic<uint64_t> bad{0};
+            HostTable::parallel_chunks(ns, [&](uint64_t b, uint64_t e) {
+                for (uint64_t k = b; k < e; ++k) {
+                    if (fr[k].loc == ~0ull) continue;
+                    if (fr[k].loc / cap >= d2h.size()) {
+                        bad.fetch_add(1);
+                        fr[k].loc = ~0ull;
+                        continue;
                     }
-                });
-                if (bad.load())
-                    throw std::runtime_error("write path: " + std::to_string(bad.load()) +
-                                             " slot words outside the table (ns " + std::to_string(ns) + ")");
-                h.adopt_device_epoch(copies, ns, versions, nv, ns, reinterpret_cast<const HostTable::SlotWords *>(fr), ns);
-                if (trace)
-                    std::fprintf(stderr,
-                                 "[wp] n=%llu ok=%llu reserve %.2f enqueue %.2f kernels %.2f d2h %.2f adopted %.2f ms "
-                                 "(background)\n",
-                                 (unsigned long long)n, (unsigned long long)ns, t_reserve, t_enqueue, t_kernels, t_d2h,
-                                 std::chrono::duration<double, std::milli>(clk::now() - t0).count());
-            } catch (...) {
-                t->adopt_err = std::current_exception();
-            }
+                    fr[k].loc = (uint64_t)d2h[fr[k].loc / cap] * cap + fr[k].loc % cap;
+                }
+            });
+            if (bad.load())
+                throw std::runtime_error("write path: " + std::to_string(bad.load()) +
+                                         " slot words outside the table (ns " + std::to_string(ns) + ")");
+            h.adopt_device_epoch(copies, ns, versions, nv, ns, reinterpret_cast<const HostTable::SlotWords *>(fr), ns);
+            t->adopted_sz[0].store(h.copies_.size(), std::memory_order_release);
+            t->adopted_sz[1].store(h.versions_.size(), std::memory_order_release);
+            t->adopted_sz[2].store(h.images_.size(), std::memory_order_release);
+            if (trace)
+                std::fprintf(stderr,
+                             "[wp] epoch %llu at %.2f ms: n=%llu ok=%llu reserve %.2f enqueue %.2f events %.2f pinned %.2f kernels %.2f "
+                             "previous adopted %.2f exported %.2f adopted %.2f ms (background)\n",
+                             (unsigned long long)epoch,
+                             std::chrono::duration<double, std::milli>(t0 - g0).count(), (unsigned long long)n,
+                             (unsigned long long)ns, t_reserve, t_enqueue, t_events, t_pinned, t_kernels, t_join, t_d2h,
+                             std::chrono::duration<double, std::milli>(clk::now() - t0).count());
         });
+        guard.started = true;
         if (n_ok) *n_ok = ns;
         return STAGE_OK;
     });

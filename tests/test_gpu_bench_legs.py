@@ -25,6 +25,9 @@ def test_c3_leg_write_paths(gpu, write_path):
     cfg = d["config"]
     assert d["self_check"] and d["value"] > 0 and d["ops_per_s_incl_writes"] > 0
     assert cfg["write_path"] == write_path and 0 < cfg["updates_applied"] <= cfg["update_ops"]
+    rcs = cfg["update_rc_counts"]
+    assert sum(rcs.values()) == cfg["update_ops"] and rcs["ok"] == cfg["updates_applied"]
+    assert rcs.get("not_needed_update", 0) > 0  # a hot key's repeats within an epoch
     # the oracle replays every epoch and answers the last epoch's sampled reads at their read ids
     orc = O.OracleTree()
     orc.load_ycsb(0, rows, 8, 0)

@@ -11,6 +11,7 @@ import pytest
 
 import oracle_lib as O
 import stage
+from stage._lib import check
 from test_gpu_incremental import check_all
 from test_gpu_parity import check_probe
 from test_leaf_images import assert_same_images
@@ -225,3 +226,76 @@ def test_hot_key_groups_finished_by_workgroups(gpu):
         probe = np.concatenate([hot, rng.integers(0, n, 2000).astype(np.uint64)])
         for rid in (0, counter // 3, counter // 2, counter - 5, 0xFFFFFFFE):
             check_probe(tab, orc, probe, 8, read_ids=np.full(probe.size, rid, np.uint32))
+
+
+@pytest.mark.parametrize("dlen,off", [(150, 5), (133, 0), (3, 1)])
+def test_long_and_ragged_windows(gpu, dlen, off):
+    """Windows longer than one 32-lane team pass (wp_classify loops), lengths that are not a
+    word multiple and unaligned offsets; an A-B-A delta pattern per key (equal contents in
+    different runs: the byte comparison behind a fingerprint match)."""
+    n = 3000
+    tab = stage.Table(key_width=8)
+    tab.load_ycsb(0, n, 8, mode=1)
+    tab.sync()
+    orc = O.OracleTree()
+    orc.load_ycsb(0, n, 8, 1)
+    rng = np.random.default_rng(dlen)
+    counter = 10
+    for epoch in range(2):
+        m = 5000
+        keys = np.where(rng.random(m) < 0.5, rng.integers(0, 8, m), rng.integers(0, n + 20, m)).astype(np.uint64)
+        deltas = rng.integers(0, 3, (m, 1), dtype=np.uint8).repeat(dlen, 1)
+        deltas[:, -1] ^= rng.integers(0, 2, m, dtype=np.uint8)  # a difference in the last (ragged) byte only
+        wid = (counter + 2 * np.arange(m)).astype(np.uint32)
+        cid = (wid + 1).astype(np.uint32)
+        counter += 2 * m + 2
+        rc, ok = tab.update_batch_device(keys, off, deltas, wid, cid)
+        exp = oracle_epoch(orc, keys, 8, off, deltas, wid, cid)
+        bad = np.nonzero(rc != exp)[0]
+        assert bad.size == 0, (epoch, bad[:5], rc[bad[:5]], exp[bad[:5]], keys[bad[:5]])
+        assert (exp == stage.RC_NOT_NEEDED_UPDATE).sum() > 100 and ok > 100
+        probe = np.arange(0, 40, dtype=np.uint64)
+        for rid in (0, counter // 2, 0xFFFFFFFE):
+            check_probe(tab, orc, probe, 8, read_ids=np.full(probe.size, rid, np.uint32))
+
+
+def test_pipelined_epochs_without_waits(gpu):
+    """Epochs enqueued back to back on one stream with no host wait: each epoch's adoption runs
+    in the background while the next epoch's kernels are enqueued (device-side append counters,
+    double-buffered outputs); a large epoch in the middle grows the header arrays and the heap
+    (settling first).  Codes, reads and the host table after settling equal the oracle's."""
+    n = 30000
+    tab = stage.Table(key_width=8)
+    tab.load_ycsb(0, n, 8, mode=1)
+    tab.sync()
+    orc = O.OracleTree()
+    orc.load_ycsb(0, n, 8, 1)
+    rng = np.random.default_rng(8)
+    s = stage.Stream()
+    counter, epochs = 10, []
+    for m in (2000, 500, 9000, 120000, 700, 3000, 1):
+        keys = np.where(rng.random(m) < 0.3, rng.integers(0, 50, m), rng.integers(0, n + 100, m)).astype(np.uint64)
+        deltas = rng.integers(0, 4, (m, 1), dtype=np.uint8).repeat(12, 1)
+        wid = (counter + 2 * np.arange(m)).astype(np.uint32)
+        cid = np.where(rng.random(m) < 0.05, 0, wid + 1).astype(np.uint32)
+        counter += 2 * m + 2
+        d = [stage.DeviceBuffer.from_numpy(x) for x in (keys, deltas.reshape(-1), wid, cid)]
+        rcb = stage.DeviceBuffer(m)
+        check(stage.lib().stage_update_batch_device(tab.h, d[0].ptr, None, m, 16, d[1].ptr, 12, d[2].ptr, d[3].ptr,
+                                                    None, rcb.ptr, None, s.ptr), "update_batch_device")
+        epochs.append((keys, deltas, wid, cid, rcb, d))
+    s.sync()
+    for keys, deltas, wid, cid, rcb, _ in epochs:
+        rc = rcb.to_numpy(np.uint8, keys.size)
+        exp = oracle_epoch(orc, keys, 8, 16, deltas, wid, cid)
+        bad = np.nonzero(rc != exp)[0]
+        assert bad.size == 0, (keys.size, bad[:5], rc[bad[:5]], exp[bad[:5]])
+    probe = np.concatenate([np.arange(60), rng.integers(0, n, 3000)]).astype(np.uint64)
+    check_all(tab, orc, probe, rng, counter)
+    # the host table (settled) agrees too: host-side writes on top, then a publish
+    for k in range(0, 50, 7):
+        dd = rng.integers(0, 256, 8, dtype=np.uint8)
+        assert tab.update(k, 3, dd, counter) == orc.update(k, 8, 3, dd.tobytes(), counter)
+    tab.sync()
+    check_all(tab, orc, probe, rng, counter + 1)
+    assert_same_images(tab, orc)
