@@ -486,7 +486,11 @@ def traffic_from_profile(batch, rows, name="pmc_probe.json"):
     try:
         d = json.load(open(path))
         if d.get("batch") == batch and d.get("rows") == rows:
-            return d["hbm_bytes_per_launch"], os.path.relpath(path, REPO)
+            src = os.path.relpath(path, REPO)
+            prof = d.get("profiled")
+            if prof:  # where the counter pass ran: another box / tree than this run's
+                src += f" (profiled on {prof.get('host')} {prof.get('date')}, tree {prof.get('tree')})"
+            return d["hbm_bytes_per_launch"], src
     except Exception:
         pass
     return None, None
