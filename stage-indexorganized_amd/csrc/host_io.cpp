@@ -130,9 +130,8 @@ struct ResidentReader {
     uint32_t slots = 0, waves = 0, row_bytes = 0;
     uint64_t stride = 0, life_ticks = 0;
     uint8_t *h = nullptr, *hd = nullptr;  // ring block, host and device view
-    uint64_t *keys = nullptr;
-    uint16_t *lens = nullptr;
-    uint32_t *rids = nullptr, *posted = nullptr, *done = nullptr, *stop = nullptr;
+    stage::ReaderReq *req = nullptr;
+    uint32_t *done = nullptr, *stop = nullptr;
     stage_probe_out *out = nullptr;
     uint8_t *rows = nullptr;
     uint64_t *dpos = nullptr;             // device: next ticket per wave
@@ -401,20 +400,22 @@ static int resident_read(ResidentReader &R, uint64_t key, uint16_t key_size, uin
     const uint32_t per = R.slots / R.waves;  // wave q % W, its (q / W)-th ticket
     const uint32_t slot = (uint32_t)(q % R.waves) * per + (uint32_t)((q / R.waves) % per);
     const uint64_t prev = q >= R.slots ? q - R.slots + 1 : 0;
-    auto wait = [&](auto ready) {  // spin (PCIe round trips are microseconds), then yield
+    // spin about the length of a read (a few microseconds), then yield: more callers than
+    // CPUs must not hold the CPUs the finished ones need
+    auto wait = [&](auto ready) {
         for (uint64_t i = 0; !ready(); ++i) {
             if (R.dead.load(std::memory_order_acquire)) return false;
-            if (i < 4096) _mm_pause();
+            if (i < 256) _mm_pause();
             else std::this_thread::yield();
         }
         return true;
     };
     if (!wait([&] { return R.freed[slot].load(std::memory_order_acquire) == prev; }))
         return fail(R.dead.load(), "resident reader has ended");
-    R.keys[slot] = key;
-    R.lens[slot] = key_size;
-    R.rids[slot] = read_id;
-    __atomic_store_n(R.posted + slot, (uint32_t)(q + 1), __ATOMIC_RELEASE);
+    stage::ReaderReq &rq = R.req[slot];
+    rq.key = key;
+    rq.rid = read_id;
+    __atomic_store_n(&rq.tag, (uint32_t)(((q + 1) << 4) | (key_size & 15u)), __ATOMIC_RELEASE);
     if (!wait([&] { return __atomic_load_n(R.done + slot, __ATOMIC_ACQUIRE) == (uint32_t)(q + 1); }))
         return fail(R.dead.load(), R.dead.load() == STAGE_E_STATE ? "device image is stale: the resident reader ended"
                                                                   : "resident reader failed on the device");
@@ -452,21 +453,17 @@ int stage_reader_create_resident(stage_table *t, uint32_t ring_slots, uint32_t w
         stage::hip_check(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, t->dev.device), "clock rate");
         R.life_ticks = (uint64_t)(khz > 0 ? khz : 100000) * life_us / 1000;
         const uint64_t S = ring_slots;
-        // keys | rids | posted | done | lens | stop | out | rows (each array 64-B aligned)
+        // requests | done | stop | out | rows (each array 64-B aligned)
         auto al = [](uint64_t x) { return (x + 63) & ~63ull; };
-        const uint64_t o_rids = al(8 * S), o_posted = o_rids + al(4 * S), o_done = o_posted + al(4 * S),
-                       o_lens = o_done + al(4 * S), o_stop = o_lens + al(2 * S), o_out = o_stop + 64,
+        const uint64_t o_done = al(sizeof(stage::ReaderReq) * S), o_stop = o_done + al(4 * S), o_out = o_stop + 64,
                        o_rows = o_out + al(32 * S), bytes = o_rows + S * R.stride;
         stage::hip_check(hipHostMalloc((void **)&R.h, bytes, hipHostMallocMapped | hipHostMallocCoherent |
                                                                  hipHostMallocPortable),
                          "resident ring");
         std::memset(R.h, 0, bytes);
         stage::hip_check(hipHostGetDevicePointer((void **)&R.hd, R.h, 0), "resident ring device pointer");
-        R.keys = (uint64_t *)R.h;
-        R.rids = (uint32_t *)(R.h + o_rids);
-        R.posted = (uint32_t *)(R.h + o_posted);
+        R.req = (stage::ReaderReq *)R.h;
         R.done = (uint32_t *)(R.h + o_done);
-        R.lens = (uint16_t *)(R.h + o_lens);
         R.stop = (uint32_t *)(R.h + o_stop);
         R.out = (stage_probe_out *)(R.h + o_out);
         R.rows = R.h + o_rows;
@@ -478,9 +475,7 @@ int stage_reader_create_resident(stage_table *t, uint32_t ring_slots, uint32_t w
         stage::hip_check(hipStreamCreateWithFlags(&R.s, hipStreamNonBlocking), "resident stream");
         for (auto &e : R.ev) stage::hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventBlockingSync),
                                               "resident event");
-        R.ring = stage::ReaderRing{(const uint64_t *)R.hd, (const uint16_t *)(R.hd + o_lens),
-                                   (const uint32_t *)(R.hd + o_rids), (const uint32_t *)(R.hd + o_posted),
-                                   (uint32_t *)(R.hd + o_done), (stage::stage_probe_out_dev *)(R.hd + o_out),
+        R.ring = stage::ReaderRing{(const stage::ReaderReq *)R.hd, (uint32_t *)(R.hd + o_done), (stage::stage_probe_out_dev *)(R.hd + o_out),
                                    R.hd + o_rows, (const uint32_t *)(R.hd + o_stop), R.dpos, ring_slots, waves,
                                    R.life_ticks};
         ResidentReader *raw = &R;

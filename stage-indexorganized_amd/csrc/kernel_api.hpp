@@ -63,11 +63,15 @@ hipError_t launch_scan_first(const DevTable &t, const uint64_t *keys, uint64_t n
                              const ScanTuning &tune);
 // request ring of the resident reader (all arrays in pinned, device-mapped host memory except
 // pos, which is device memory of `waves` words initialised to 0)
+// one request: {key bytes (LE), read id, tag}, tag = (ticket + 1) << 4 | key length, written by
+// the caller last (release); 16-B aligned, so one device load sees the tag with its key
+struct alignas(16) ReaderReq {
+    uint64_t key;
+    uint32_t rid;
+    uint32_t tag;
+};
 struct ReaderRing {
-    const uint64_t *keys;      // [slots] little-endian key bytes
-    const uint16_t *lens;      // [slots] key lengths (variable-length tables)
-    const uint32_t *rids;      // [slots] read ids
-    const uint32_t *posted;    // [slots] ticket + 1 once the request is in place (host)
+    const ReaderReq *req;      // [slots]
     uint32_t *done;            // [slots] ticket + 1 once its results are in place (device)
     stage_probe_out_dev *out;  // [slots]
     uint8_t *rows;             // [slots * stride]

@@ -558,8 +558,10 @@ __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *
 // (the stage_reader_* adapter of BTree::Read callers, b_tree.cpp:2066-2129, without a launch
 // per request).  Ticket q belongs to wave w = q % W as its k-th ticket, k = q / W, and lives in
 // slot w * P + k % P of the ring (P = slots / W, a multiple of 64): concurrent callers land on
-// different waves, and a wave's tickets are contiguous in the ring.  A caller fills its slot
-// and publishes posted[slot] = q + 1 (release); the wave takes the published prefix of its
+// different waves, and a wave's tickets are contiguous in the ring.  A caller writes its 16-B
+// request record -- key, read id, then the tag (q + 1) << 4 | key length with release -- so a
+// wave's poll is one 16-B load per lane over PCIe that brings the key along with the tag; the
+// wave takes the published prefix of its
 // current 64-ticket block, probes it (lane j = the block's j-th ticket throughout), writes the
 // status record and the row into the slot and publishes done[slot] = q + 1 (system-scope
 // release).  Every instance ends after life_ticks of the
@@ -630,9 +632,11 @@ __global__ __launch_bounds__(64) void resident_reader_kernel(DevTable t, ReaderR
         const uint32_t d = (uint32_t)(pos & 63u);
         const uint32_t s0 = w * per + (uint32_t)(blk % per);
         const uint32_t want = (uint32_t)((blk + lane) * g.waves + w + 1u);
-        bool ready = false;
-        if (lane >= d)
-            ready = __hip_atomic_load(g.posted + s0 + lane, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == want;
+        u32x4 rq = u32x4{0, 0, 0, 0};
+        // the whole record in one load (volatile: system-coherent, past the caches); the tag is
+        // written after the key and read id, in the same 16-B line, so seeing it brings them
+        if (lane >= d) rq = *reinterpret_cast<const volatile u32x4 *>(g.req + s0 + lane);
+        const bool ready = lane >= d && (rq.w >> 4) == (want & 0x0FFFFFFFu);
         const uint64_t m = ballot(ready) >> d;
         const uint32_t k = ~m ? (uint32_t)__builtin_ctzll(~m) : 64u;  // published prefix from d
         if (k == 0) {
@@ -640,10 +644,9 @@ __global__ __launch_bounds__(64) void resident_reader_kernel(DevTable t, ReaderR
             continue;
         }
         const bool mine = lane >= d && lane < d + k;
-        const uint32_t len = t.key_width ? t.key_width : (mine ? (uint32_t)g.lens[s0 + lane] : 8u);
-        const uint32_t rid = mine ? g.rids[s0 + lane] : 0u;
-        uint64_t ok;
-        load_okey<1>(g.keys + s0, lane, mine, len, &ok);
+        const uint32_t len = t.key_width ? t.key_width : (mine ? (rq.w & 15u) : 8u);
+        const uint32_t rid = mine ? rq.z : 0u;
+        const uint64_t ok = order_key(mine ? ((uint64_t)rq.y << 32 | rq.x) : 0ull, len);
         uint32_t leaf = mine ? resolve_leaf<VARLEN, 1>(t, &ok, len, true) : 0u;
         u32x4 my_a = u32x4{0, 0, 0, 0}, my_b = u32x4{0, 0, 0, 0};
         for (uint32_t j = d; j < d + k; ++j) {
