@@ -19,5 +19,5 @@ run() {  # name args...
 W=${WAVES:-16}
 for T in ${THREADS:-1 16 64}; do
   [ -n "$SKIP_COALESCING" ] || run coalescing_t$T 20000000 3 $T 1024 100 1048576 0.9 0
-  run resident_w${W}_t$T 20000000 3 $T 1024 100 1048576 0.9 $W
+  run resident_w${W}_t$T${TAG} 20000000 3 $T 1024 100 1048576 0.9 $W
 done
