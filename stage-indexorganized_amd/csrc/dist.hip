@@ -323,6 +323,9 @@ unsigned blocks_for(uint64_t n, unsigned per_block) { return (unsigned)std::max<
 ShardComm::~ShardComm() {
     if (cs) (void)hipStreamSynchronize(cs), (void)hipStreamDestroy(cs);
     if (us) (void)hipStreamSynchronize(us), (void)hipStreamDestroy(us);
+    if (ps) (void)hipStreamSynchronize(ps), (void)hipStreamDestroy(ps);
+    for (hipEvent_t e : {ev_fork, ev_own})
+        if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : evs) (void)hipEventDestroy(e);
     if (comm) ncclCommDestroy((ncclComm_t)comm);
     for (void *p : {dest, cursor, perm, send, recv, rout, rrec, bout, brec, cnt, lkeys, lrids, fan, dd_skeys, dd_iota,
@@ -383,6 +386,9 @@ static void init_common(ShardComm &c, int rank, int world, int chunks) {
     grow(c.cursor, (2ull * world * kRouteBlocks + 16) * sizeof(uint32_t));
     chk(hipStreamCreateWithFlags(&c.cs, hipStreamNonBlocking), "comm stream");
     chk(hipStreamCreateWithFlags(&c.us, hipStreamNonBlocking), "fan-out stream");
+    chk(hipStreamCreateWithFlags(&c.ps, hipStreamNonBlocking), "own-probe stream");
+    chk(hipEventCreateWithFlags(&c.ev_fork, hipEventDisableTiming), "event");
+    chk(hipEventCreateWithFlags(&c.ev_own, hipEventDisableTiming), "event");
     c.evs.resize(3 * chunks + 2);
     for (auto &e : c.evs) chk(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
 }
@@ -634,9 +640,11 @@ static void fan_launch(const stage_probe_out_dev *sout, const uint8_t *srec, uin
 // Probe what chunk i holds for this rank.  The remote segments arrived in recv; this rank's own
 // requests never left the device (no self transfer): they are read from the send buffer.
 // Full reply: own requests are probed in fan-out form, straight to their caller positions in
-// d_out / d_recs (tables of other geometries: probed into rout / rrec, then fanned out); the
-// remote segments are probed into rout / rrec for the return transfer.  Owner reply: everything
-// into rout / rrec, rows tagged with their owner-local index.
+// d_out / d_recs, on their own stream c.ps beside the remote probes (a chunk's own share is a
+// small launch whose latency the remote probes hide; joined by own_join); tables of other
+// geometries: probed into rout / rrec, then fanned out.  The remote segments are probed into
+// rout / rrec for the return transfer.  Owner reply: everything into rout / rrec, rows tagged
+// with their owner-local index.
 static void chunk_probe(ShardComm &c, const Plan &P, int i, const DevTable &t, const ProbeTuning &tune, bool owner,
                         stage_probe_out_dev *d_out, uint8_t *d_recs, hipStream_t s) {
     const int W = P.W, me = c.rank;
@@ -670,13 +678,25 @@ static void chunk_probe(ShardComm &c, const Plan &P, int i, const DevTable &t, c
     probe(r1, e);
     if (r1 == r0) return;
     if (d_recs && probe_fanout_supported(t)) {
+        // STAGE_SHARD_OWN_STREAM=0: on the caller's stream after the remote probes (A/B)
+        static const bool own_stream = !(std::getenv("STAGE_SHARD_OWN_STREAM") &&
+                                         std::getenv("STAGE_SHARD_OWN_STREAM")[0] == '0');
+        hipStream_t os = own_stream ? c.ps : s;
+        chk(hipEventRecord(c.ev_fork, s), "fork");  // the unpacked keys
+        chk(hipStreamWaitEvent(os, c.ev_fork, 0), "fork");
         chk(launch_probe_fanout(t, lk + r0, lr + r0, r1 - r0, (const FanRange *)c.fan + q0,
-                                P.dedupe ? (const uint32_t *)c.flist : nullptr, d_out, d_recs, s, tune),
+                                P.dedupe ? (const uint32_t *)c.flist : nullptr, d_out, d_recs, os, tune),
             "fan-out probe");
     } else {
         probe(r0, r1);
         fan_launch(rout + r0, rrec + r0 * (uint64_t)t.stride, q0, q0 + (r1 - r0), c, P, t.stride, d_out, d_recs, s);
     }
+}
+
+// the caller's stream waits for the own-request probes of every chunk
+static void own_join(ShardComm &c, hipStream_t s) {
+    chk(hipEventRecord(c.ev_own, c.ps), "own join");
+    chk(hipStreamWaitEvent(s, c.ev_own, 0), "own join");
 }
 
 // chunk i's results that came back from other ranks (bout / brec, at their send positions) to
@@ -804,9 +824,10 @@ int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const 
         chunk_return(c, P, i, stride, owner, d_out, d_recs, c.us);
     }
     if (owner) owner_expand(c, P, d_out, c.us);
-    // the caller's stream completes after the last fan-out
+    // the caller's stream completes after the last fan-out and the own-request probes
     chk(hipEventRecord(ev_start, c.us), "event");
     chk(hipStreamWaitEvent(s, ev_start, 0), "join");
+    own_join(c, s);
     if (owner) c.owner_rows = P.m();
     return STAGE_OK;
 }
@@ -875,6 +896,7 @@ int shard_probe_loopback(const std::vector<ShardComm *> &cs, const std::vector<c
     }
     if (owner)
         for (int r = 0; r < W; ++r) owner_expand(*cs[r], P[r], outs[r], s);
+    for (int r = 0; r < W; ++r) own_join(*cs[r], s);
     for (int r = 0; r < W; ++r) cs[r]->owner_rows = owner ? P[r].m() : 0;
     return STAGE_OK;
 }

@@ -23,7 +23,9 @@ struct ShardComm {
     uint32_t rec_stride = 0;
     int chunks = 1;                  // overlapped exchange chunks (same on every rank)
     hipStream_t cs = nullptr;        // RCCL transfers
-    hipStream_t us = nullptr;        // un-permutation
+    hipStream_t us = nullptr;        // fan-out of returned results / owner-reply expand
+    hipStream_t ps = nullptr;        // fan-out probes of own requests (beside the remote probes)
+    hipEvent_t ev_fork = nullptr, ev_own = nullptr;
     std::vector<hipEvent_t> evs;     // per-chunk keys / probe / results events + join
     uint64_t owner_rows = 0;         // rows left in rrec by the last owner-reply probe
     // request coalescing: equal (key, read id) requests of a chunk are routed once and their
