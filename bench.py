@@ -558,7 +558,7 @@ def xgmi_roofline(batch, world, stride, step_s, hbm_roof, remote=None):
     peak = XGMI_LINK_GBS * (world - 1)
     return {"bound": "xgmi", "achieved": round(achieved, 1), "peak": peak, "unit": "GB/s",
             "frac": round(achieved / peak, 4), "traffic": None,
-            "kernel": "sharded step (coalesce + route + RCCL all-to-all-v + probe_kernel + expand)",
+            "kernel": "sharded step (coalesce + route + RCCL all-to-all-v + probe_kernel + fan-out)",
             "algorithmic_bytes_per_unit": unit, "units_per_launch": round(remote),
             "avg_launch_ms": round(step_s * 1e3, 4),
             "peak_source": f"{XGMI_LINK_GBS:.0f} GB/s per xGMI link (7 per MI355X), {world - 1} links per rank",
