@@ -1314,8 +1314,9 @@ __global__ __launch_bounds__(256) void scan_first_multi_kernel(DevTable t, const
 // Point probes of the one-probe-in-flight instances (fixed-width keys of 9..32 bytes, or
 // 8-byte keys in leaves above 128 slots) in two stages per chunk of CH probes -- the results of
 // probe_kernel<false, SPL, 1, .., KW, CH>:
-//  A (wave per probe, in turn): the leaf head's fingerprint bytes (the next probe's in flight
-//    while this one runs), one ballot per slot group, and the candidate slots in slot order
+//  A (wave per probe, in turn): the leaf head's fingerprint bytes (the next 4 probes' in flight
+//    while this one runs -- the next one only for leaves above 256 slots, whose larger heads
+//    would cost occupancy), one ballot per slot group, and the candidate slots in slot order
 //    written to LDS (at most kProbeCand; a probe with more is resolved by a lane-serial walk of
 //    its leaf head in stage B);
 //  B (lane per probe, all CH together): each candidate's slot word and remaining key words in
@@ -1347,34 +1348,44 @@ __global__ __launch_bounds__(256) void probe_split_kernel(DevTable t, const uint
         if (leaf > t.nseps) leaf = t.nseps;  // host-supplied ids are clamped to the table
         const uint32_t fx_mine = key_fp_words(ok, KW);
         const int cnt = (int)((n - base) < CH ? (n - base) : CH);
-        // ---- stage A
-        uint32_t nfp[SPL];
-        {
-            const uint8_t *h = t.head + (uint64_t)rl32(leaf, 0) * t.head_bytes;
+        // ---- stage A: the heads of the next PD probes in flight while one is examined (a ring of
+        // PD register sets, indexed statically by unrolling PD probes per pass)
+        constexpr int PD = SPL <= 4 ? 4 : 1;
+        uint32_t pf[PD][SPL];
 #pragma unroll
-            for (int s = 0; s < SPL; ++s) nfp[s] = h[s * 64 + lane];
+        for (int d = 0; d < PD; ++d) {
+            if (d < cnt) {
+                const uint8_t *h = t.head + (uint64_t)rl32(leaf, d) * t.head_bytes;
+#pragma unroll
+                for (int s = 0; s < SPL; ++s) pf[d][s] = h[s * 64 + lane];
+            }
         }
         uint32_t my_nc = 0;
-        for (int j = 0; j < cnt; ++j) {
-            uint32_t fpb[SPL];
+        for (int j0 = 0; j0 < cnt; j0 += PD) {
 #pragma unroll
-            for (int s = 0; s < SPL; ++s) fpb[s] = nfp[s];
-            if (j + 1 < cnt) {
-                const uint8_t *h = t.head + (uint64_t)rl32(leaf, j + 1) * t.head_bytes;
+            for (int u = 0; u < PD; ++u) {
+                const int j = j0 + u;
+                if (j >= cnt) break;
+                uint32_t fpb[SPL];
 #pragma unroll
-                for (int s = 0; s < SPL; ++s) nfp[s] = h[s * 64 + lane];
+                for (int s = 0; s < SPL; ++s) fpb[s] = pf[u][s];
+                if (j + PD < cnt) {
+                    const uint8_t *h = t.head + (uint64_t)rl32(leaf, j + PD) * t.head_bytes;
+#pragma unroll
+                    for (int s = 0; s < SPL; ++s) pf[u][s] = h[s * 64 + lane];
+                }
+                const uint32_t fx = rl32(fx_mine, j);
+                uint32_t nc = 0;
+#pragma unroll
+                for (int s = 0; s < SPL; ++s) {
+                    const bool c = fpb[s] == fx;
+                    const uint64_t cm = ballot(c);
+                    const uint32_t r = nc + count_below(cm);
+                    if (c && r < (uint32_t)kProbeCand) s_cand[wv][j][r] = (uint16_t)(s * 64 + lane);
+                    nc += (uint32_t)__builtin_popcountll(cm);
+                }
+                if (lane == (uint32_t)j) my_nc = nc;
             }
-            const uint32_t fx = rl32(fx_mine, j);
-            uint32_t nc = 0;
-#pragma unroll
-            for (int s = 0; s < SPL; ++s) {
-                const bool c = fpb[s] == fx;
-                const uint64_t cm = ballot(c);
-                const uint32_t r = nc + count_below(cm);
-                if (c && r < (uint32_t)kProbeCand) s_cand[wv][j][r] = (uint16_t)(s * 64 + lane);
-                nc += (uint32_t)__builtin_popcountll(cm);
-            }
-            if (lane == (uint32_t)j) my_nc = nc;
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
