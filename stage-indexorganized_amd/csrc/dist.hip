@@ -244,6 +244,13 @@ __global__ __launch_bounds__(256) void fan_copy(const stage_probe_out_dev *__res
             fr[r] = in ? fan[pb + r] : FanRange{0u, 0u};
             so[r] = lane < 2 ? reinterpret_cast<const u32x4 *>(sout + q)[lane] : u32x4{0, 0, 0, 0};
         }
+        // the first 64 caller positions of each request, in flight with the rows below
+        uint32_t mine0[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t kk = fr[r].lo + lane;
+            mine0[r] = kk < fr[r].hi ? (flist ? flist[kk] : kk) : 0u;
+        }
         for (uint32_t c0 = 0; c0 < (chunks ? chunks : 1u); c0 += 64) {
             const uint32_t c = c0 + lane;
             u32x4 v[R];
@@ -256,7 +263,7 @@ __global__ __launch_bounds__(256) void fan_copy(const stage_probe_out_dev *__res
             for (int r = 0; r < R; ++r) {
                 for (uint32_t k0 = fr[r].lo; k0 < fr[r].hi; k0 += 64) {
                     const uint32_t kk = k0 + lane;
-                    const uint32_t mine = kk < fr[r].hi ? (flist ? flist[kk] : kk) : 0u;
+                    const uint32_t mine = k0 == fr[r].lo ? mine0[r] : kk < fr[r].hi ? (flist ? flist[kk] : kk) : 0u;
                     const uint32_t kn = fr[r].hi - k0 < 64u ? fr[r].hi - k0 : 64u;
                     for (uint32_t k = 0; k < kn; ++k) {
                         const uint64_t pos = rl32(mine, (int)k);

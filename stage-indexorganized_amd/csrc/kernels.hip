@@ -480,12 +480,19 @@ __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *
             // phase 4 (FAN): G rows in flight, each stored at its caller positions with its
             // status record (lanes 0-1); up to 64 positions are loaded at once, one per lane
             if constexpr (FAN) {
+                // the G rows and the first 64 caller positions of each request, all in flight
+                // together (a request has at most kFanCap = 64 callers; longer runs loop)
                 u32x4 v[G];
+                uint32_t mine0[G];
 #pragma unroll
                 for (int g = 0; g < G; ++g) {
                     v[g] = u32x4{0, 0, 0, 0};
                     if (lane < out_chunks && r[g].image != 0xFFFFFFFFu)
                         v[g] = reinterpret_cast<const u32x4 *>(t.heap + (uint64_t)r[g].image * t.hstride)[lane];
+                    const int j = j0 + g;
+                    const uint32_t lo = rl32(my_fan.lo, j & 63), hi = rl32(my_fan.hi, j & 63);
+                    const uint32_t kk = lo + lane;
+                    mine0[g] = j < cnt && kk < hi ? (flist ? flist[kk] : kk) : 0u;
                 }
 #pragma unroll
                 for (int g = 0; g < G; ++g) {
@@ -497,7 +504,7 @@ __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *
                     const uint32_t lo = rl32(my_fan.lo, j), hi = rl32(my_fan.hi, j);
                     for (uint32_t k0 = lo; k0 < hi; k0 += 64) {
                         const uint32_t kk = k0 + lane;
-                        const uint32_t mine = kk < hi ? (flist ? flist[kk] : kk) : 0u;
+                        const uint32_t mine = k0 == lo ? mine0[g] : kk < hi ? (flist ? flist[kk] : kk) : 0u;
                         const uint32_t kn = hi - k0 < 64u ? hi - k0 : 64u;
                         for (uint32_t k = 0; k < kn; ++k) {
                             const uint64_t pos = rl32(mine, (int)k);
