@@ -329,12 +329,35 @@ class RcclControl:
         check(stage.lib().stage_comm_destroy(self.tab.h), "comm destroy")
 
 
+SHARE_GPU_ENV = "STAGE_RANKS_SHARE_GPU"
+
+
+def share_gpu_rehearsal(rank, world):
+    """STAGE_RANKS_SHARE_GPU=1 with world > 1: every rank runs on device 0 of a one-GPU box and
+    RCCL is told the ranks live on different hosts (a per-rank NCCL_HOSTID; RCCL refuses two
+    ranks of one host on one device), so the exchange runs over its socket transport on the
+    loopback interface.  That executes the real multi-rank RCCL calls of the sharded step (the
+    counts all-to-all, grouped send/recv with peers, the control plane) on hardware this pool
+    hands out; xGMI bandwidth is not what it measures, and the line says so.  Must run before
+    the first RCCL call of the process."""
+    if world <= 1 or os.environ.get(SHARE_GPU_ENV) != "1":
+        return False
+    os.environ["NCCL_HOSTID"] = f"stage-rehearsal-{os.getppid()}-rank{rank}"
+    os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+    os.environ.setdefault("NCCL_NET", "Socket")
+    os.environ.setdefault("NCCL_IB_DISABLE", "1")
+    return True
+
+
 def run_sharded(args, rank, world, local):
     """configs[4] (C5) and its 1/2/4 smaller points: every rank holds the keys with
     MurmurHash64A(key, 8, 0) % world == rank (rows_per_gpu each, weak scaling), originates its own
     2^24 Zipf-0.9 lookups over all world x rows keys, and stage_probe_sharded answers them in its
     order over RCCL.  This process loads no other HIP runtime or RCCL than libstage_hip's (no
     torch: the control plane is the communicator itself, RcclControl)."""
+    shared = share_gpu_rehearsal(rank, world)
+    if shared:
+        local = 0
     res = cpu_resources()
     nthreads = args.cpu_threads or res["threads"]
     L = stage.lib()
@@ -447,7 +470,10 @@ def run_sharded(args, rank, world, local):
            "algorithmic_bytes_per_launch": hmax, "bytes_by_part_rank0": hb[0][1],
            "avg_launch_ms": round(step_s * 1e3, 4), "event_ms_per_step_rank0": round(kern_ms, 4),
            "algorithmic_bytes": "bench.sharded_hbm_bytes (per rank, what moves)"}
-    if world > 1:
+    if shared:  # the exchange ran over host sockets: no xGMI figure to price it against
+        roof = dict(hbm, note="ranks share one GPU (rehearsal): HBM bytes of the busiest rank, all ranks' "
+                              "kernels contend for the same HBM")
+    elif world > 1:
         roof = xgmi_roofline(B, world, tab.stride, step_s, hbm, remote=max(sx["remote"] for sx in stats))
     else:
         roof = hbm
@@ -457,7 +483,7 @@ def run_sharded(args, rank, world, local):
         "metric": METRIC, "value": round(B * args.steps * world / elapsed, 1), "unit": "ops/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic (LoadYCSBRows keys/payloads)",
-        "config": {"workload": sharded_workload(world, args.rows), "theta": args.theta, "traversal": "device",
+        "config": {"workload": sharded_workload(world, args.rows, shared), "theta": args.theta, "traversal": "device",
                    "rows_per_gpu": args.rows, "rows_total": total_rows, "batch_per_gpu": B, "key_bytes": 8,
                    "payload_bytes": 1000, "leaf_bytes": 65536, "parallelism": f"hash-shard x{world}",
                    "exchange_chunks": int(os.environ.get("STAGE_SHARD_CHUNKS", 4 if world > 1 else 1)),
@@ -573,9 +599,13 @@ def fmt_rows(n):
     return str(n)
 
 
-def sharded_workload(world, rows_per_gpu):
+def sharded_workload(world, rows_per_gpu, shared=False):
     """config.workload of a sharded run, naming its real world size and rows: at 8 ranks of
     100M rows this is BASELINE.json configs[4] verbatim; any other world / size names itself."""
+    if shared:
+        return (f"YCSB-C {fmt_rows(world * rows_per_gpu)} rows sharded {world} ways, RCCL all-to-all key routing "
+                f"over its socket transport, {world} ranks sharing 1×MI355X (multi-rank rehearsal, "
+                f"{SHARE_GPU_ENV}=1; not an xGMI or scaling point)")
     s = (f"YCSB-C {fmt_rows(world * rows_per_gpu)} rows sharded {world} way{'s' if world != 1 else ''}, "
          f"RCCL all-to-all key routing over xGMI, {world}×MI355X")
     if world == 1:
