@@ -105,6 +105,8 @@ def parse(argv=None):
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extras", action="store_true", help="c2: skip the nested C4 / C3 legs")
     p.add_argument("--host-traversal", action="store_true", help="leaf ids from the host router instead")
+    p.add_argument("--out-stride", type=int, default=0,
+                   help="caller row stride in bytes (stage_set_output_layout; 0 = the 1008-B canonical row)")
     p.add_argument("--force-sharded", action="store_true",
                    help="run the multi-GPU (RCCL) code path even with one rank -- a rehearsal, not a config")
     p.add_argument("--dry-run", action="store_true",
@@ -381,6 +383,8 @@ def run_sharded(args, rank, world, local):
     setup["sync"] = time.time() - t0
     log(f"[rank {rank}] loaded {loaded} rows: owned_keys {setup['owned_keys']:.1f}s load {setup['load']:.1f}s "
         f"sync {setup['sync']:.1f}s; RCCL {rccl}")
+    if args.out_stride:
+        tab.set_output_layout(args.out_stride)
     t0 = time.time()
     ctl = RcclControl(tab, rank, world)
     setup["comm_init"] = time.time() - t0
@@ -1335,6 +1339,8 @@ def main(argv=None):
     t0 = time.time()
     tab.sync()
     t_sync = time.time() - t0
+    if args.out_stride:
+        tab.set_output_layout(args.out_stride)
     st = tab.stats()
     log(f"[rank {rank}] loaded {loaded} rows in {t_load:.1f}s, sync {t_sync:.1f}s, leaves {st['leaves']}")
 

@@ -615,7 +615,11 @@ int stage_probe_sharded(stage_table *t, const uint64_t *d_keys, const uint32_t *
     if (!t->comm) return fail(STAGE_E_STATE, "stage_comm_init first");
     return guarded([&] {
         (void)hipSetDevice(t->dev.device);
-        return stage::shard_probe(*t->comm, t->dev.view, t->tune, d_keys, d_read_ids, n,
+        // the caller's row stride (stage_set_output_layout) is also the stride the rows travel
+        // at: one row layout from the owner's probe to the caller's position
+        stage::DevTable view = t->dev.view;
+        if (t->out_stride) view.stride = t->out_stride;
+        return stage::shard_probe(*t->comm, view, t->tune, d_keys, d_read_ids, n,
                                   reinterpret_cast<stage::stage_probe_out_dev *>(d_out), d_records, STAGE_REPLY_ROWS,
                                   pick(t, stream));
     });
@@ -629,7 +633,11 @@ int stage_probe_sharded_ex(stage_table *t, const uint64_t *d_keys, const uint32_
     if (reply_mode != STAGE_REPLY_ROWS && reply_mode != STAGE_REPLY_OWNER) return fail(STAGE_E_ARG, "bad reply mode");
     return guarded([&] {
         (void)hipSetDevice(t->dev.device);
-        return stage::shard_probe(*t->comm, t->dev.view, t->tune, d_keys, d_read_ids, n,
+        // the caller's row stride (stage_set_output_layout) is also the stride the rows travel
+        // at: one row layout from the owner's probe to the caller's position
+        stage::DevTable view = t->dev.view;
+        if (t->out_stride) view.stride = t->out_stride;
+        return stage::shard_probe(*t->comm, view, t->tune, d_keys, d_read_ids, n,
                                   reinterpret_cast<stage::stage_probe_out_dev *>(d_out), d_records, reply_mode,
                                   pick(t, stream));
     });
@@ -660,6 +668,7 @@ int stage_probe_sharded_loopback(stage_table *const *shards, int world, const ui
         (void)hipSetDevice(shards[0]->dev.device);
         std::vector<stage::ShardComm *> cs(world);
         std::vector<const stage::DevTable *> ts(world);
+        std::vector<stage::DevTable> views(world);
         std::vector<const uint64_t *> ks(world);
         std::vector<const uint32_t *> rs(world);
         std::vector<uint64_t> ns(world);
@@ -676,7 +685,9 @@ int stage_probe_sharded_loopback(stage_table *const *shards, int world, const ui
             if (t->shard_dedupe >= 0) t->loop_comm->dedupe = t->shard_dedupe != 0;
             t->loop_comm->key_bits = t->shard_key_bits;
             cs[r] = t->loop_comm.get();
-            ts[r] = &t->dev.view;
+            views[r] = t->dev.view;
+            if (shards[0]->out_stride) views[r].stride = shards[0]->out_stride;  // as stage_probe_sharded_ex
+            ts[r] = &views[r];
             ks[r] = d_keys[r];
             rs[r] = d_read_ids ? d_read_ids[r] : nullptr;
             ns[r] = n[r];

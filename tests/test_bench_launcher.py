@@ -98,3 +98,21 @@ def test_tpcc_tables_small():
     assert d["stock"][0].shape == (200, 16) and d["district"][0].shape == (10, 16)
     assert d["order_line"][0].shape[1] == 32 and d["order_line"][1].shape[1] == 60
     assert callable(bench.run_tpcc) and callable(bench.run_chq2) and callable(bench.c3_leg) and callable(bench.c4_leg)
+
+
+def test_share_gpu_rehearsal_labels_and_env(monkeypatch):
+    # STAGE_RANKS_SHARE_GPU=1: ranks get distinct NCCL host ids (RCCL's socket transport between
+    # ranks on one device) and the line names the rehearsal instead of an xGMI / scaling point
+    for k in ("NCCL_HOSTID", "NCCL_SOCKET_IFNAME", "NCCL_NET", "NCCL_IB_DISABLE", bench.SHARE_GPU_ENV):
+        monkeypatch.delenv(k, raising=False)
+    assert not bench.share_gpu_rehearsal(0, 2)  # off unless asked for
+    monkeypatch.setenv(bench.SHARE_GPU_ENV, "1")
+    assert not bench.share_gpu_rehearsal(0, 1)  # nothing to share at world 1
+    ids = set()
+    for r in range(3):
+        assert bench.share_gpu_rehearsal(r, 3)
+        ids.add(os.environ["NCCL_HOSTID"])
+    assert len(ids) == 3 and os.environ["NCCL_NET"] == "Socket" and os.environ["NCCL_SOCKET_IFNAME"] == "lo"
+    w = bench.sharded_workload(2, 2_000_000, shared=True)
+    assert "4M rows sharded 2 ways" in w and "sharing 1×MI355X" in w and "not an xGMI or scaling point" in w
+    assert bench.sharded_workload(8, 100_000_000) == bench.WORKLOADS["c5"]
