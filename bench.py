@@ -58,7 +58,7 @@ HOP_BYTES = 64           # C3: one TupleHeader (version) line per chain hop take
 HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md: 8.0 TB/s HBM3E spec
 XGMI_LINK_GBS = 153.0    # per xGMI link of an MI355X (7 links per GPU, point to point)
 ORACLE_BYTES_PER_ROW = 1800  # oracle tree host memory per YCSB row (64 KiB leaves, ~38-48 rows each, + inner)
-GPU_HOST_BYTES_PER_ROW = 130  # host side of a device table (host_peak_rss 11.8 GiB at 100M rows)
+GPU_HOST_BYTES_PER_ROW = 210  # host peak of a rank per row (19.5 GiB at 100M rows, sharded world 1, round 3)
 # the reference itself, measured in the survey container and the oracle in
 # the same container type: calibration of the port
 REF_C1_OPS = 1533428.0       # YCSB-C -k 1000 -o 10, 1 thread
