@@ -1756,11 +1756,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             actv |= (uint32_t)__shfl_xor((int)actv, 1);
             actv |= (uint32_t)__shfl_xor((int)actv, 2);
         }
+        // the start leaf's monotone prefix length mp (info word, beside the group maxima): slots
+        // [0, mp) hold strictly increasing keys
+        const uint32_t mpv = *reinterpret_cast<const uint32_t *>(t.head + (uint64_t)leafv * t.head_bytes +
+                                                                 head_info_offset(t.cap, KW)) >> 16;
         uint64_t pf_vm, pf_col[KW];
-        int pf_s;
+        int pf_s = -1;
+        uint32_t pf_leaf = 0xFFFFFFFFu;
+        // the next scan's first active group; the scans of a chunk are mostly one transaction's
+        // consecutive orders in one leaf, so that group is often the one already held in the
+        // pf registers (data of a kernel's lifetime never changes): then nothing is loaded and
+        // the scan starts without a round trip
         auto prefetch = [&](int jn) {
             const uint32_t an = rl32(actv, 4 * jn), ln = rl32(leafv, 4 * jn);
-            pf_s = an ? __builtin_ctz(an) : 0;
+            const int s = an ? __builtin_ctz(an) : 0;
+            if (ln == pf_leaf && s == pf_s) return;
+            pf_s = s;
+            pf_leaf = ln;
             pf_vm = head_vis(t, ln, pf_s);
 #pragma unroll
             for (int w = 0; w < KW; ++w) pf_col[w] = t.okey[((uint64_t)ln * KW + w) * t.cap + pf_s * 64 + lane];
@@ -1774,15 +1786,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
             for (int w = 0; w < KW; ++w) x[w] = rl64(ok[w], src);
             const uint32_t leaf = rl32(leafv, src);
+            const uint32_t mp = rl32(mpv, src);
             uint64_t active = ballot(lane < (uint32_t)SPL && ((rl32(actv, src) >> lane) & 1));
-            bool pending = true;
+            bool pending = true, mono = false;
             uint32_t kept = 0;
             while (active) {
                 const int s = __builtin_ctzll(active);
                 active &= active - 1;
                 uint64_t vm, col[KW];
                 const bool from_pf = pending && s == pf_s;
-                if (from_pf) {
+                // a later group may be the one just prefetched for the next scan (in flight
+                // since this scan's first group was consumed)
+                if (from_pf || (leaf == pf_leaf && s == pf_s)) {
                     vm = pf_vm;
 #pragma unroll
                     for (int w = 0; w < KW; ++w) col[w] = pf_col[w];
@@ -1794,6 +1809,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                 const bool vis = (vm >> lane) & 1;
                 const uint64_t q = ballot(vis && !kw_lt<KW>(col, x));
                 const uint32_t rank = kept + count_below(q);
+                // fast path: nothing kept yet, the group lies in the monotone prefix and holds
+                // more than scan_size qualifying records -- the kept scan_size + 1 records are
+                // its first ones, already in key order (unique keys), so their ranks are their
+                // slot order and the first e = scan_size are the candidates; no LDS list
+                if (kept == 0 && (uint32_t)s * 64u + 64u <= mp && (uint32_t)__builtin_popcountll(q) > scan_size) {
+                    if (((q >> lane) & 1) && rank < scan_size) {
+                        bool pfx = true;
+#pragma unroll
+                        for (int w = 0; w < KW; ++w)
+                            if ((uint32_t)w < words) pfx = pfx && col[w] == x[w];
+                        s_cand[wv][j][rank] = pfx ? (uint16_t)(s * 64 + (int)lane) : kHole;
+                    }
+                    if (from_pf) {
+                        pending = false;
+                        if (j + 1 < cnt) prefetch(j + 1);
+                    }
+                    mono = true;
+                    break;
+                }
                 const bool take = ((q >> lane) & 1) && rank <= scan_size;
                 if (take) {
 #pragma unroll
@@ -1813,7 +1847,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             const uint32_t m = kept;
             uint32_t info = 0;
-            if (m > 0) {
+            if (mono) {
+                info = scan_size;
+            } else if (m > 0) {
                 const bool mine = lane < m;
                 uint64_t mk[KW];
                 uint32_t mslot = 0;
