@@ -105,6 +105,9 @@ def parse(argv=None):
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extras", action="store_true", help="c2: skip the nested C4 / C3 legs")
     p.add_argument("--host-traversal", action="store_true", help="leaf ids from the host router instead")
+    p.add_argument("--write-overlap", type=int, choices=[0, 1], default=1,
+                   help="device write path: an epoch's kernels up to its publish run beside the previous "
+                        "epoch's read probe (stage_set_write_overlap; the epoch inputs are resident beforehand)")
     p.add_argument("--out-stride", type=int, default=0,
                    help="caller row stride in bytes (stage_set_output_layout; 0 = the 1008-B canonical row)")
     p.add_argument("--force-sharded", action="store_true",
@@ -1200,6 +1203,8 @@ def c3_leg(tab, args, stream, nthreads, steps, warmup):
                        "out": stage.DeviceBuffer(32 * ep["reads"].size)}
     prep_s = time.time() - t0
     d_rec = stage.DeviceBuffer(B * tab.stride)
+    if args.write_path == "device":
+        tab.set_write_overlap(args.write_overlap)
 
     def probe(ep):
         d = ep["d"]
@@ -1272,7 +1277,8 @@ def c3_leg(tab, args, stream, nthreads, steps, warmup):
                     # an epoch find their own value) or a newer committed writer; dirty = the
                     # record is in flight (an uncommitted update earlier in the epoch)
                     "update_rc_counts": rc_hist,
-                    "write_path": args.write_path, "write_call_s": round(write_s, 4), "loop_s": round(loop_s, 4),
+                    "write_path": args.write_path,
+                    "write_overlap": bool(args.write_overlap) and args.write_path == "device", "write_call_s": round(write_s, 4), "loop_s": round(loop_s, 4),
                     "epoch_prep_s_untimed": round(prep_s, 2), "mean_chain_hops": round(mean_hops, 4),
                     # copies / versions / heap images are append-only (no GC, as the reference
                     # with its cleaner off): each successful update takes one of each, and the

@@ -153,6 +153,13 @@ int stage_update_batch_device(stage_table *t, const uint64_t *d_keys, const uint
 /* waits for the host table's adoption of the last stage_update_batch_device epoch (it runs on a
  * background thread; every host-table entry point waits for it anyway) and reports its error */
 int stage_settle(stage_table *t);
+/* write-overlap mode of stage_update_batch_device (default 0): an epoch's kernels up to the
+ * publish of its slot words run on the table's own stream as soon as the previous epoch has
+ * published, beside whatever the caller enqueued on `stream` after that (e.g. the previous
+ * epoch's read probes); only the publish waits for `stream`.  Results are the same.  Contract:
+ * the epoch's inputs (keys, deltas, ids) are complete when the call is made -- not produced by
+ * work still pending on `stream`. */
+int stage_set_write_overlap(stage_table *t, int on);
 
 /* byte-key forms, for every key width a table takes: 1..8 bytes (key_width 1..8 or 0 =
  * variable) or a fixed width of 9..32 bytes (TPC-C composite keys, tpcc_record.h: int64

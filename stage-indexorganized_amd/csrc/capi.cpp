@@ -545,6 +545,12 @@ int stage_set_shard_dedupe(stage_table *t, int on) {
     return STAGE_OK;
 }
 
+int stage_set_write_overlap(stage_table *t, int on) {
+    if (!t) return fail(STAGE_E_ARG, "null table");
+    t->wp_overlap = on ? 1 : 0;
+    return STAGE_OK;
+}
+
 int stage_set_shard_key_bits(stage_table *t, int bits) {
     if (!t || bits < 0 || bits > 64) return fail(STAGE_E_ARG, "bits must be 0..64");
     t->shard_key_bits = bits ? bits : 64;

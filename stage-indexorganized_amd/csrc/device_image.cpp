@@ -47,6 +47,12 @@ void DeviceImage::release() {
     stream = nullptr;
     if (adopt_stream) (void)hipStreamDestroy(adopt_stream);
     adopt_stream = nullptr;
+    if (wp_pub_ev) (void)hipEventDestroy(wp_pub_ev);
+    if (wp_pre_ev) (void)hipEventDestroy(wp_pre_ev);
+    wp_pub_ev = wp_pre_ev = nullptr;
+    wp_pub_valid = false;
+    if (wp_stream) (void)hipStreamDestroy(wp_stream);
+    wp_stream = nullptr;
     valid = false;
 }
 
@@ -205,6 +211,7 @@ uint8_t *wp_out_bytes(DeviceImage &d, uint64_t bytes, int k) {
 
 void reserve_device_rows(HostTable &h, DeviceImage &d, uint64_t extra_images, uint64_t extra_copies,
                          uint64_t extra_versions, hipStream_t s) {
+    d.wp_pub_valid = false;  // the grown arrays are filled on s: an overlapped epoch waits for s
     grow_heap(h, d, h.images_.size() + extra_images, s);
     grow_keep(d.chdr, (h.copies_.size() + extra_copies) * sizeof(CopyHdr), h.copies_synced_ * sizeof(CopyHdr), "chdr",
               s);
@@ -353,6 +360,7 @@ static void sync_heap(HostTable &h, DeviceImage &d, hipStream_t s) {
 
 void sync_device(HostTable &h, DeviceImage &d) {
     auto t0 = std::chrono::steady_clock::now();
+    d.wp_pub_valid = false;  // the next overlapped write-path epoch waits for this publish
     hip_check(hipSetDevice(d.device), "hipSetDevice");
     if (!d.stream) hip_check(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking), "hipStreamCreate");
     hipStream_t s = d.stream;

@@ -29,6 +29,13 @@ struct DeviceImage {
     hipStream_t adopt_stream = nullptr;  // the adoption's D2H copies (beside the caller's stream)
     hipEvent_t adopt_ev[2] = {nullptr, nullptr};  // end of an epoch's write-path kernels
     hipEvent_t export_ev[2] = {nullptr, nullptr}; // end of its export into pinned host memory
+    // write-overlap mode (stage_set_write_overlap): an epoch's kernels up to the publish run on
+    // wp_stream after the previous epoch's publish (wp_pub_ev), beside the caller's later work;
+    // the publish joins the caller's stream (wp_pre_ev).  wp_pub_valid: wp_pub_ev marks the
+    // last change of the device image (cleared by sync_device and every other republish)
+    hipStream_t wp_stream = nullptr;
+    hipEvent_t wp_pub_ev = nullptr, wp_pre_ev = nullptr;
+    bool wp_pub_valid = false;
     std::vector<uint8_t> staging;  // host staging of incremental patches
     void *pinned[2] = {nullptr, nullptr};  // pinned host staging of the epoch results
     uint64_t pinned_cap[2] = {0, 0};

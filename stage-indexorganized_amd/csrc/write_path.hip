@@ -666,9 +666,26 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
             pending = false;
             reserve_device_rows(h, dv, 8 * n, 8 * n, 8 * n, s);
         }
+        // write-overlap mode: the kernels up to the publish go on the table's write stream ks,
+        // which waits for the previous epoch's publish only (or, when the device image changed
+        // otherwise since, for all of s) -- not for the caller's work enqueued after it, such as
+        // the previous epoch's read probes.  They read the slot words that publish left and
+        // write only scratch, this epoch's output parity and the appended header / row ranges
+        // no published slot word reaches yet; the publish joins s behind them.
+        hipStream_t ks = s;
+        if (t->wp_overlap) {
+            if (!dv.wp_stream) hip_check(hipStreamCreateWithFlags(&dv.wp_stream, hipStreamNonBlocking), "write stream");
+            for (hipEvent_t *e : {&dv.wp_pub_ev, &dv.wp_pre_ev})
+                if (!*e) hip_check(hipEventCreateWithFlags(e, hipEventDisableTiming), "write event");
+            if (!dv.wp_pub_valid) hip_check(hipEventRecord(dv.wp_pub_ev, s), "write event");
+            hip_check(hipStreamWaitEvent(dv.wp_stream, dv.wp_pub_ev, 0), "write wait");
+            ks = dv.wp_stream;
+        } else {
+            dv.wp_pub_valid = false;  // this epoch publishes without recording wp_pub_ev
+        }
         if (!pending)
-            wp_set_bases<<<1, 1, 0, s>>>((uint64_t *)dv.wp_bases.p, h.copies_.size(), h.versions_.size(),
-                                         h.images_.size());
+            wp_set_bases<<<1, 1, 0, ks>>>((uint64_t *)dv.wp_bases.p, h.copies_.size(), h.versions_.size(),
+                                          h.images_.size());
         t->wp_epoch_n[par] = n;
         const double t_reserve = ms(t0);
         const DevTable &view = dv.view;
@@ -738,43 +755,51 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         size_t cb = cub_bytes;
 
         // 1. locate
-        hip_check(launch_probe(view, d_keys, d_lens, nullptr, nullptr, n, pout, nullptr, s, t->tune), "locate");
-        wp_keys<<<blocks_for(n, 256), 256, 0, s>>>(pout, n, view.cap, none, loc0, op0);
+        hip_check(launch_probe(view, d_keys, d_lens, nullptr, nullptr, n, pout, nullptr, ks, t->tune), "locate");
+        wp_keys<<<blocks_for(n, 256), 256, 0, ks>>>(pout, n, view.cap, none, loc0, op0);
         // 2. group
-        hip_check(hipcub::DeviceRadixSort::SortPairs(cub, cb, loc0, loc, op0, op, (int)n, 0, end_bit, s), "sort");
-        wp_heads<<<blocks_for(n, 256), 256, 0, s>>>(loc, n, head);
+        hip_check(hipcub::DeviceRadixSort::SortPairs(cub, cb, loc0, loc, op0, op, (int)n, 0, end_bit, ks), "sort");
+        wp_heads<<<blocks_for(n, 256), 256, 0, ks>>>(loc, n, head);
         cb = cub_bytes;
-        hip_check(hipcub::DeviceScan::InclusiveScan(cub, cb, head, gs, hipcub::Max(), (int)n, s), "group starts");
+        hip_check(hipcub::DeviceScan::InclusiveScan(cub, cb, head, gs, hipcub::Max(), (int)n, ks), "group starts");
         // 3. decide
         WpArgs a{loc, op, gs, d_deltas, d_writer_ids, d_commit_ids, d_sstamps, n, none, delta_len,
                  facts(t).key_pad() + payload_off,
                  (uint64_t)payload_off + delta_len > facts(t).params().payload_size ? 1u : 0u};
-        hip_check(hipMemsetAsync(ff, 0xFF, n * 4, s), "memset");
-        hip_check(hipMemsetAsync(ls, 0, n * 4, s), "memset");
-        hip_check(hipMemsetAsync(fin, 0xFF, n * sizeof(FinRec), s), "memset");
-        wp_classify<<<blocks_for(n * kTeam, 256), 256, 0, s>>>(a, view, brk, fpd, wfp, eqw);
+        hip_check(hipMemsetAsync(ff, 0xFF, n * 4, ks), "memset");
+        hip_check(hipMemsetAsync(ls, 0, n * 4, ks), "memset");
+        hip_check(hipMemsetAsync(fin, 0xFF, n * sizeof(FinRec), ks), "memset");
+        wp_classify<<<blocks_for(n * kTeam, 256), 256, 0, ks>>>(a, view, brk, fpd, wfp, eqw);
         cb = cub_bytes;
-        hip_check(hipcub::DeviceScan::InclusiveSum(cub, cb, brk, cls, (int)n, s), "delta classes");
+        hip_check(hipcub::DeviceScan::InclusiveSum(cub, cb, brk, cls, (int)n, ks), "delta classes");
         const WpCls kc{cls, fpd, wfp, eqw};
-        wp_speculate<<<blocks_for(n, 256), 256, 0, s>>>(a, kc, view, rcs, succ, prev, ff);
-        wp_group_ends<<<blocks_for(n, 256), 256, 0, s>>>(a, gend);
-        hip_check(hipMemsetAsync(tot + 1, 0, 4, s), "memset");  // big-group count (tot is rewritten in step 4)
-        wp_big_groups<<<blocks_for(n, 256), 256, 0, s>>>(a, ff, gend, big, (uint32_t *)(tot + 1));
-        wp_finish_groups<<<blocks_for(n, 256), 256, 0, s>>>(a, kc, view, rcs, succ, prev, ff, gend);
-        wp_finish_big<<<256, 1024, 0, s>>>(a, kc, view, rcs, succ, prev, ff, gend, big, (uint32_t *)(tot + 1));
+        wp_speculate<<<blocks_for(n, 256), 256, 0, ks>>>(a, kc, view, rcs, succ, prev, ff);
+        wp_group_ends<<<blocks_for(n, 256), 256, 0, ks>>>(a, gend);
+        hip_check(hipMemsetAsync(tot + 1, 0, 4, ks), "memset");  // big-group count (tot is rewritten in step 4)
+        wp_big_groups<<<blocks_for(n, 256), 256, 0, ks>>>(a, ff, gend, big, (uint32_t *)(tot + 1));
+        wp_finish_groups<<<blocks_for(n, 256), 256, 0, ks>>>(a, kc, view, rcs, succ, prev, ff, gend);
+        wp_finish_big<<<256, 1024, 0, ks>>>(a, kc, view, rcs, succ, prev, ff, gend, big, (uint32_t *)(tot + 1));
         // 4. number
-        wp_flags<<<blocks_for(n, 256), 256, 0, s>>>(a, succ, flags);
+        wp_flags<<<blocks_for(n, 256), 256, 0, ks>>>(a, succ, flags);
         cb = cub_bytes;
-        hip_check(hipcub::DeviceScan::ExclusiveSum(cub, cb, flags, ranks, (int)n, s), "ranks");
-        wp_totals<<<1, 1, 0, s>>>(ranks, flags, n, tot, (uint64_t *)dv.wp_bases.p);
-        wp_headers<<<blocks_for(n, 256), 256, 0, s>>>(a, view, succ, prev, ranks, (CopyHdr *)dv.chdr.p,
+        hip_check(hipcub::DeviceScan::ExclusiveSum(cub, cb, flags, ranks, (int)n, ks), "ranks");
+        wp_totals<<<1, 1, 0, ks>>>(ranks, flags, n, tot, (uint64_t *)dv.wp_bases.p);
+        wp_headers<<<blocks_for(n, 256), 256, 0, ks>>>(a, view, succ, prev, ranks, (CopyHdr *)dv.chdr.p,
                                                       (VersionHdr *)dv.vhdr.p, ls, wrec, tot);
         // 5. write, 6. publish
         const int wblocks = (int)std::min<uint64_t>(blocks_for(n, 256 / kRowTeam), 32768);
-        wp_write<<<wblocks, 256, 0, s>>>(a, view, (uint8_t *)dv.heap.p, wrec, tot);
+        wp_write<<<wblocks, 256, 0, ks>>>(a, view, (uint8_t *)dv.heap.p, wrec, tot);
+        if (ks != s) {
+            hip_check(hipEventRecord(dv.wp_pre_ev, ks), "write event");
+            hip_check(hipStreamWaitEvent(s, dv.wp_pre_ev, 0), "publish wait");
+        }
         wp_publish<<<blocks_for(n, 256), 256, 0, s>>>(a, (SlotInfo *)dv.slot.p, rcs, succ, prev, ranks, ls, tot, fin,
                                                       d_rc);
         hip_check(hipGetLastError(), "write-path kernels");
+        if (t->wp_overlap) {  // the next overlapped epoch starts after this publish
+            hip_check(hipEventRecord(dv.wp_pub_ev, s), "write event");
+            dv.wp_pub_valid = true;
+        }
 
         // the host adopts the epoch.  The headers and slot words come back on a stream of their
         // own into pinned staging (full PCIe rate) and the host adopts them on a background

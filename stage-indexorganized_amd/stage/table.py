@@ -442,6 +442,11 @@ class Table:
         rows = d_rec.to_numpy(np.uint8, n * self.stride).reshape(n, self.stride) if d_rec else None
         return out, rows
 
+    def set_write_overlap(self, on):
+        """stage_set_write_overlap: a device write-path epoch's kernels up to its publish run beside
+        the caller's later work (inputs must be complete when update_batch_device is called)."""
+        check(lib().stage_set_write_overlap(self.h, int(on)), "set_write_overlap")
+
     def set_output_layout(self, row_stride=0, status_bytes=32):
         """stage_set_output_layout: probe row stride (0 = default) and 32- or 16-B status records."""
         check(lib().stage_set_output_layout(self.h, row_stride, status_bytes), "set_output_layout")

@@ -299,3 +299,65 @@ def test_pipelined_epochs_without_waits(gpu):
     tab.sync()
     check_all(tab, orc, probe, rng, counter + 1)
     assert_same_images(tab, orc)
+
+
+def test_write_overlap_epochs_with_probes_between(gpu):
+    """stage_set_write_overlap: epoch e + 1's kernels up to its publish run beside epoch e's read
+    probe (same caller stream, no host waits).  Each epoch's probe -- enqueued right after that
+    epoch's call, at old and current read ids over hot and cold keys -- must read exactly the
+    oracle's state after that epoch (not the next one's, not the previous one's); codes equal the
+    oracle's; a growth in the middle and a host write + publish between overlapped epochs are
+    ordered too."""
+    n = 30000
+    tab = stage.Table(key_width=8)
+    tab.load_ycsb(0, n, 8, mode=1)
+    tab.sync()
+    tab.set_write_overlap(1)
+    orc = O.OracleTree()
+    orc.load_ycsb(0, n, 8, 1)
+    rng = np.random.default_rng(31)
+    s = stage.Stream()
+    base, hot = np.arange(0, n, 2, dtype=np.uint64), np.arange(0, 40, dtype=np.uint64)
+    counter, epochs = 10, []
+    probe_keys = np.concatenate([hot, rng.integers(0, n + 50, 6000)]).astype(np.uint64)
+    for e, m in enumerate((3000, 800, 9000, 90000, 1500, 4000, 2)):
+        keys, deltas, wid, cid = epoch_ops(rng, base, hot, m, counter)
+        counter += 2 * m + 2
+        if e == 5:  # a host-side write + publish between two overlapped epochs
+            s.sync()
+            check(stage.lib().stage_settle(tab.h), "settle")
+            k0 = int(hot[3])
+            dd = rng.integers(0, 256, 8, dtype=np.uint8)
+            ep_host = (k0, dd, counter, tab.update(k0, 3, dd, counter))
+            counter += 2
+            tab.sync()
+        else:
+            ep_host = None
+        d = [stage.DeviceBuffer.from_numpy(x) for x in (keys, deltas.reshape(-1), wid, cid)]
+        rcb = stage.DeviceBuffer(m)
+        check(stage.lib().stage_update_batch_device(tab.h, d[0].ptr, None, m, 16, d[1].ptr, 24, d[2].ptr, d[3].ptr,
+                                                    None, rcb.ptr, None, s.ptr), "update_batch_device")
+        rids = np.where(rng.random(probe_keys.size) < 0.5, rng.integers(0, counter, probe_keys.size),
+                        0xFFFFFFFE).astype(np.uint32)
+        pk, pr = stage.DeviceBuffer.from_numpy(probe_keys), stage.DeviceBuffer.from_numpy(rids)
+        pout, prow = stage.DeviceBuffer(probe_keys.size * 32), stage.DeviceBuffer(probe_keys.size * tab.stride)
+        tab.probe_device(pk.ptr, probe_keys.size, pout.ptr, prow.ptr, d_read_ids=pr.ptr, stream=s.ptr)
+        epochs.append((keys, deltas, wid, cid, rcb, d, rids, pk, pr, pout, prow, ep_host))
+    s.sync()
+    for keys, deltas, wid, cid, rcb, _, rids, _, _, pout, prow, ep_host in epochs:
+        if ep_host is not None:
+            k0, dd, c0, rc0 = ep_host
+            assert orc.update(k0, 8, 3, dd.tobytes(), c0) == rc0
+        exp = oracle_epoch(orc, keys, 8, 16, deltas, wid, cid)
+        rc = rcb.to_numpy(np.uint8, keys.size)
+        bad = np.nonzero(rc != exp)[0]
+        assert bad.size == 0, (keys.size, bad[:5], rc[bad[:5]], exp[bad[:5]])
+        out = pout.to_numpy(stage.PROBE_OUT_DTYPE, probe_keys.size)
+        rows = prow.to_numpy(np.uint8, probe_keys.size * tab.stride).reshape(probe_keys.size, tab.stride)
+        o_out, o_rec = orc.read_batch(probe_keys, 8, rids)
+        for f in ("status", "hops", "cstamp", "rec_cstamp", "copy_sstamp"):
+            badf = np.nonzero(out[f] != o_out[f])[0]
+            assert badf.size == 0, (keys.size, f, badf[:5], out[f][badf[:5]], o_out[f][badf[:5]])
+        assert not (rows[:, :orc.row] != o_rec).any(axis=1).any(), keys.size
+    check_all(tab, orc, probe_keys, rng, counter)
+    assert_same_images(tab, orc)
