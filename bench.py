@@ -354,6 +354,19 @@ def share_gpu_rehearsal(rank, world):
     return True
 
 
+def rank_device(local):
+    """The device of local rank `local`: device `local` when every GPU of the node is visible;
+    device 0 when a launcher left each rank exactly one visible GPU (HIP_VISIBLE_DEVICES /
+    ROCR_VISIBLE_DEVICES per rank)."""
+    ndev = stage.device_count()
+    if local < ndev:
+        return local
+    if ndev == 1:
+        log(f"[local rank {local}] one visible GPU: using device 0")
+        return 0
+    raise SystemExit(f"local rank {local} but only {ndev} visible GPUs")
+
+
 def run_sharded(args, rank, world, local):
     """configs[4] (C5) and its 1/2/4 smaller points: every rank holds the keys with
     MurmurHash64A(key, 8, 0) % world == rank (rows_per_gpu each, weak scaling), originates its own
@@ -363,6 +376,8 @@ def run_sharded(args, rank, world, local):
     shared = share_gpu_rehearsal(rank, world)
     if shared:
         local = 0
+    else:
+        local = rank_device(local)
     res = cpu_resources()
     nthreads = args.cpu_threads or res["threads"]
     L = stage.lib()
