@@ -1305,7 +1305,9 @@ def c3_leg(tab, args, stream, nthreads, steps, warmup):
                                            "fail": int(hist[4]), "chain_miss": int(hist[5]),
                                            "not_found": int(hist[0])},
                     "timed": "value: device probes of the read shares; ops_per_s_incl_writes: the whole loop "
-                             "(write path + probes), epoch inputs resident in HBM beforehand"},
+                             "(write path + probes), epoch inputs resident in HBM beforehand" +
+                             ("; write overlap: each probe runs beside the next epoch's write-path kernels "
+                              "(its time includes that contention)" if device_wp and args.write_overlap else "")},
          "roofline": hbm_roofline(per_unit, ops_done / steps, kern_ms, "probe_kernel (read ids, chain walks)",
                                   *traffic_from_profile(args.batch, args.rows, "pmc_probe_c3.json"))}
     d["roofline"]["algorithmic_bytes"] = f"{BYTES_PER_LOOKUP} + {HOP_BYTES} x mean hops ({mean_hops:.4f})"
