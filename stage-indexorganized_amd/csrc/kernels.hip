@@ -55,13 +55,16 @@ __device__ __forceinline__ bool kw_lt_flat(const uint64_t *a, const uint64_t *b)
     return lt;
 }
 
-// multi-word order keys (fixed-width keys of 9..32 bytes): lexicographic word order
+// multi-word order keys (fixed-width keys of 9..32 bytes): lexicographic word order.  Written
+// as selects from the last word to the first rather than early returns: per-lane early exits
+// become exec-mask branches and lane-mask logic on the CU's one scalar pipe, which the
+// first-tuple scans saturate; selects stay on the SIMD's vector pipe
 template <int KW>
 __device__ __forceinline__ bool kw_lt(const uint64_t *a, const uint64_t *b) {
+    uint32_t r = 0;
 #pragma unroll
-    for (int j = 0; j < KW; ++j)
-        if (a[j] != b[j]) return a[j] < b[j];
-    return false;
+    for (int j = KW - 1; j >= 0; --j) r = a[j] < b[j] ? 1u : (a[j] != b[j] ? 0u : r);
+    return r != 0;
 }
 
 // separators of one node (F entries) below x.  KW = 1: the node is F x 8 B (F/2 16-B loads
