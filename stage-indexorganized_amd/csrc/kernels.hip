@@ -1336,7 +1336,7 @@ __global__ __launch_bounds__(256) void scan_first_multi_kernel(DevTable t, const
 //  Rows (if requested) are then copied wave-wide, probe by probe, as probe_kernel's phase 4.
 constexpr int kProbeCand = 8;
 template <int SPL, int KW, int CH>
-__global__ __launch_bounds__(256) void probe_split_kernel(DevTable t, const uint64_t *__restrict__ keys,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void probe_split_kernel(DevTable t, const uint64_t *__restrict__ keys,
                                                           const uint32_t *__restrict__ rids,
                                                           const uint32_t *__restrict__ leaf_in, uint64_t n,
                                                           stage_probe_out_dev *__restrict__ out,
