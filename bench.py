@@ -689,7 +689,9 @@ class YcsbB:
         a = self.args
         draws = stage.zipf_draws(a.rows - 1, self.theta, a.seed + 1000 * self.epoch, a.batch, nthreads=self.nthreads)
         rng = np.random.default_rng(a.seed + self.epoch)
-        is_upd = rng.random(a.batch) < a.update_ratio
+        # RunMixed's op stream (ycsb_mixed.cpp:26-44): NextUniform() < update_ratio makes an
+        # update whose 100-B delta is memset to the next_char() drawn right after it
+        is_upd, chr_ = stage.ycsb_ops(a.seed * 1_000_003 + self.epoch, a.batch, a.update_ratio)
         keys = draws[is_upd]
         m = keys.size
         rid = (self.counter + 2 * np.arange(m, dtype=np.uint64)).astype(np.uint32)
@@ -699,7 +701,7 @@ class YcsbB:
         if k_in:
             cid[rng.choice(cand, k_in, replace=False)] = 0  # left in flight
         self.counter += 2 * m
-        colb = ((keys + np.uint64(self.epoch + 1)) & np.uint64(0xFF)).astype(np.uint8)
+        colb = np.ascontiguousarray(chr_[is_upd])
         reads = np.ascontiguousarray(draws[~is_upd])
         rids = np.full(reads.size, self.counter, np.uint32)
         old = rng.random(reads.size) < 0.25
@@ -1284,13 +1286,15 @@ def c3_leg(tab, args, stream, nthreads, steps, warmup):
          "ms_per_step": round(elapsed / steps * 1e3, 4), "self_check": ok,
          "ops_per_s_incl_writes": round((ops_done + updates) / loop_s, 1),
          "config": {"workload": WORKLOADS["c3"], "theta": theta, "update_ratio": args.update_ratio,
+                    "update_stream": "RunMixed: FastRandom NextUniform() < update_ratio, delta = 100 x next_char() "
+                                     "(ycsb_mixed.cpp:26-44)",
                     "inflight_share": args.inflight_share, "updates_applied": updates,
                     "update_ops": int(sum(ep["keys"].size for ep in epochs[warm:])),
                     "updates_in_flight": int(sum(ep["inflight"] for ep in epochs[warm:])),
                     # why update ops fail: not_needed_update = the column already holds the value
-                    # (YCSB-B's patch byte is a function of key and epoch, so a hot key's repeats in
-                    # an epoch find their own value) or a newer committed writer; dirty = the
-                    # record is in flight (an uncommitted update earlier in the epoch)
+                    # (RunMixed's delta byte is a fresh next_char() per update: a 1/256 chance) or a
+                    # newer committed writer; dirty = the record is in flight (an uncommitted
+                    # update earlier in the epoch)
                     "update_rc_counts": rc_hist,
                     "write_path": args.write_path,
                     "write_overlap": bool(args.write_overlap) and args.write_path == "device", "write_call_s": round(write_s, 4), "loop_s": round(loop_s, 4),

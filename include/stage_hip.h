@@ -495,6 +495,11 @@ int stage_fastrandom_next(uint64_t seed, uint64_t count, uint64_t *out);
 int stage_zipf_draws(uint64_t n, double theta, uint64_t seed, uint64_t count, uint64_t *out,
                      int nthreads);
 int stage_zipf_zeta(uint64_t n, double theta, double *out);
+/* RunMixed's operation stream (benchmark/ycsb/ycsb_mixed.cpp:26-44) from FastRandom(seed): op i
+ * is an update when NextUniform() < update_ratio (is_update[i] = 1) and then draws its delta
+ * byte chr[i] = next_char() (the 100-B column patch memset to it); a read draws nothing more
+ * (chr[i] = 0). */
+int stage_ycsb_ops(uint64_t seed, uint64_t count, double update_ratio, uint8_t *is_update, uint8_t *chr);
 
 #ifdef __cplusplus
 }

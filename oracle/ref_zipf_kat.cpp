@@ -6,6 +6,8 @@
 // generator by FastRandom(seed) after construction, so the draws are reproducible.
 //   ref_zipf_kat fast SEED COUNT          -> FastRandom(SEED).next() x COUNT
 //   ref_zipf_kat zipf N THETA SEED COUNT  -> zeta values (hex bits) + GetNextNumber() x COUNT
+//   ref_zipf_kat ops SEED COUNT RATIO     -> RunMixed's per-op draws (ycsb_mixed.cpp:26, 37, 43):
+//                                            NextUniform() < RATIO, then next_char() for an update
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -44,6 +46,23 @@ int main(int argc, char **argv) {
         std::printf("]}\n");
         return 0;
     }
-    std::fprintf(stderr, "usage: ref_zipf_kat fast SEED COUNT | zipf N THETA SEED COUNT\n");
+    if (argc >= 5 && !std::strcmp(argv[1], "ops")) {
+        FastRandom rng(std::strtoull(argv[2], nullptr, 0));
+        const unsigned long long count = std::strtoull(argv[3], nullptr, 0);
+        const double ratio = std::strtod(argv[4], nullptr);
+        std::printf("{\"ops\": [");
+        for (unsigned long long i = 0; i < count; ++i) {
+            auto rng_val = rng.NextUniform();
+            int v = -1;  // read
+            if (rng_val < ratio) {
+                char chr = rng.next_char();
+                v = (unsigned char)chr;
+            }
+            std::printf("%s%d", i ? ", " : "", v);
+        }
+        std::printf("]}\n");
+        return 0;
+    }
+    std::fprintf(stderr, "usage: ref_zipf_kat fast SEED COUNT | zipf N THETA SEED COUNT | ops SEED COUNT RATIO\n");
     return 2;
 }

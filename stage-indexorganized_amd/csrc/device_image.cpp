@@ -28,7 +28,7 @@ DeviceImage::~DeviceImage() { release(); }
 
 void DeviceImage::release() {
     for (DevBuf *b :
-         {&head, &okey, &slot, &tree, &tree_len, &heap, &chdr, &vhdr, &arena, &descs, &patch, &scratch, &wp_out[0],
+         {&head, &okey, &slot, &tree, &tree_len, &heap, &chdr, &vhdr, &arena, &descs, &patch, &scratch, &wp_scratch, &wp_out[0],
           &wp_out[1], &wp_bases}) {
         if (b->p) (void)hipFree(b->p);
         b->p = nullptr;
@@ -166,20 +166,24 @@ static void grow_heap(HostTable &h, DeviceImage &d, uint64_t rows_needed, hipStr
     d.heap_rows = rows;
 }
 
-uint8_t *scratch_bytes(DeviceImage &d, uint64_t bytes) {
-    if (d.scratch.cap < bytes) {
-        if (d.scratch.p) {
-            hip_check(hipDeviceSynchronize(), "scratch drain");
-            hip_check(hipFree(d.scratch.p), "hipFree scratch");
+static uint8_t *grow_scratch(DevBuf &b, uint64_t bytes, const char *what) {
+    if (b.cap < bytes) {
+        if (b.p) {
+            hip_check(hipDeviceSynchronize(), what);
+            hip_check(hipFree(b.p), what);
         }
-        d.scratch.p = nullptr;
-        d.scratch.cap = 0;
+        b.p = nullptr;
+        b.cap = 0;
         const uint64_t want = bytes + bytes / 8 + 4096;
-        hip_check(hipMalloc(&d.scratch.p, want), "scratch");
-        d.scratch.cap = want;
+        hip_check(hipMalloc(&b.p, want), what);
+        b.cap = want;
     }
-    return (uint8_t *)d.scratch.p;
+    return (uint8_t *)b.p;
 }
+
+uint8_t *scratch_bytes(DeviceImage &d, uint64_t bytes) { return grow_scratch(d.scratch, bytes, "scratch"); }
+
+uint8_t *wp_scratch_bytes(DeviceImage &d, uint64_t bytes) { return grow_scratch(d.wp_scratch, bytes, "write-path scratch"); }
 
 uint8_t *pinned_bytes(DeviceImage &d, uint64_t bytes, int k) {
     if (d.pinned_cap[k] < bytes) {

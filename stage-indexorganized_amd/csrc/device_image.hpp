@@ -20,7 +20,9 @@ struct DeviceImage {
     int device = 0;
     hipStream_t stream = nullptr;
     DevBuf head, okey, slot, tree, tree_len, heap, chdr, vhdr, arena, descs, patch;
-    DevBuf scratch;  // per-call scratch of the device write path / stock-level (scratch_bytes)
+    DevBuf scratch;     // per-call scratch of stock-level / CH-Q2 / scans (scratch_bytes)
+    DevBuf wp_scratch;  // the device write path's own scratch (wp_scratch_bytes): an overlapped
+                        // epoch runs beside the caller's later work on the shared scratch
     // the device write path's per-epoch outputs, double-buffered by epoch parity: epoch e's
     // background adoption reads wp_out[e % 2] / pinned[e % 2] while epoch e + 1 runs
     DevBuf wp_out[2];  // slot words + totals
@@ -62,6 +64,8 @@ void hip_check(hipError_t e, const char *what);
 // next call on the same table).  Stream-ordered pool memory (hipMallocAsync) is not used: on
 // gfx950 its reuse across calls showed stale reads on other XCDs between kernels of a stream.
 uint8_t *scratch_bytes(DeviceImage &d, uint64_t bytes);
+// the same for the device write path alone (write_path.hip)
+uint8_t *wp_scratch_bytes(DeviceImage &d, uint64_t bytes);
 // pinned host buffer `k` (0/1) of at least `bytes` (grown with hipHostMalloc; reused by later calls)
 uint8_t *pinned_bytes(DeviceImage &d, uint64_t bytes, int k = 0);
 // the write path's own output buffer `k` (0/1; not shared with scratch_bytes users: its

@@ -627,13 +627,19 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         const int par = (int)(epoch & 1);
         // an epoch that fails before its adoption starts still counts as adopted -- with a
         // sticky error (the device may hold part of it): later calls neither hang nor go on
+        // -- unless nothing of it reached the device yet (an allocation or stream / event creation
+        // failed): then the epoch is rolled back and the table stays usable
         struct EpochGuard {
             stage_table *t;
             uint64_t epoch;
-            bool started = false;
+            bool enqueued = false, started = false;
             ~EpochGuard() {
-                if (!started)
-                    t->start_adoption(epoch, [] { throw std::runtime_error("a device write-path epoch failed"); });
+                if (started) return;
+                if (!enqueued) {
+                    --t->wp_started;
+                    return;
+                }
+                t->start_adoption(epoch, [] { throw std::runtime_error("a device write-path epoch failed"); });
             }
         } guard{t, epoch};
         // STAGE_WP_PIPELINE=0: every epoch waits for the previous one's adoption (A/B of the pipeline)
@@ -666,28 +672,18 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
             pending = false;
             reserve_device_rows(h, dv, 8 * n, 8 * n, 8 * n, s);
         }
-        // write-overlap mode: the kernels up to the publish go on the table's write stream ks,
-        // which waits for the previous epoch's publish only (or, when the device image changed
-        // otherwise since, for all of s) -- not for the caller's work enqueued after it, such as
-        // the previous epoch's read probes.  They read the slot words that publish left and
-        // write only scratch, this epoch's output parity and the appended header / row ranges
-        // no published slot word reaches yet; the publish joins s behind them.
-        hipStream_t ks = s;
-        if (t->wp_overlap) {
-            if (!dv.wp_stream) hip_check(hipStreamCreateWithFlags(&dv.wp_stream, hipStreamNonBlocking), "write stream");
-            for (hipEvent_t *e : {&dv.wp_pub_ev, &dv.wp_pre_ev})
-                if (!*e) hip_check(hipEventCreateWithFlags(e, hipEventDisableTiming), "write event");
-            if (!dv.wp_pub_valid) hip_check(hipEventRecord(dv.wp_pub_ev, s), "write event");
-            hip_check(hipStreamWaitEvent(dv.wp_stream, dv.wp_pub_ev, 0), "write wait");
-            ks = dv.wp_stream;
-        } else {
-            dv.wp_pub_valid = false;  // this epoch publishes without recording wp_pub_ev
-        }
-        if (!pending)
-            wp_set_bases<<<1, 1, 0, ks>>>((uint64_t *)dv.wp_bases.p, h.copies_.size(), h.versions_.size(),
-                                          h.images_.size());
-        t->wp_epoch_n[par] = n;
         const double t_reserve = ms(t0);
+        if (t->wp_overlap && !dv.wp_stream)
+            hip_check(hipStreamCreateWithFlags(&dv.wp_stream, hipStreamNonBlocking), "write stream");
+        for (hipEvent_t *e : {&dv.wp_pub_ev, &dv.wp_pre_ev})
+            if (!*e) hip_check(hipEventCreateWithFlags(e, hipEventDisableTiming), "write event");
+        if (!dv.adopt_stream) {  // high priority: the export gets its CUs beside the next probe
+            int lo = 0, hi = 0;
+            hip_check(hipDeviceGetStreamPriorityRange(&lo, &hi), "stream priorities");
+            hip_check(hipStreamCreateWithPriority(&dv.adopt_stream, hipStreamNonBlocking, hi), "adopt stream");
+        }
+        for (hipEvent_t *e : {&dv.adopt_ev[0], &dv.adopt_ev[1], &dv.export_ev[0], &dv.export_ev[1]})
+            if (!*e) hip_check(hipEventCreateWithFlags(e, hipEventDisableTiming), "adopt event");
         const DevTable &view = dv.view;
         const uint64_t none = (uint64_t)view.nleaves * view.cap;
         int end_bit = 1;
@@ -720,7 +716,9 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
                        o_prev = take(n * 4), o_ff = take(n * 4), o_ls = take(n * 4), o_gend = take(n * 4), o_big = take(n * 4), o_flags = take(n * 8),
                        o_ranks = take(n * 8), o_brk = take(n * 4), o_cls = take(n * 4),
                        o_fp = take(n * 8), o_wfp = take(n * 8), o_eqw = take(n), o_wrec = take(n * sizeof(WRec)), o_cub = take(cub_bytes);
-        uint8_t *buf = scratch_bytes(dv, off);
+        // the write path's own scratch: an overlapped epoch runs beside the caller's later work,
+        // which may use the table's shared scratch (stock-level, CH-Q2, scans)
+        uint8_t *buf = wp_scratch_bytes(dv, off);
         auto *pout = (stage_probe_out_dev *)(buf + o_pout);
         auto *loc0 = (uint64_t *)(buf + o_loc0);
         auto *loc = (uint64_t *)(buf + o_loc);
@@ -753,6 +751,37 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         auto *tot = (uint64_t *)(wo + al(n * sizeof(FinRec)));
         void *cub = buf + o_cub;
         size_t cb = cub_bytes;
+        // pinned staging of the adoption: [totals 64 B][copy headers][version headers][slot
+        // words], sized for the worst case (one copy and one version per op); every part starts
+        // on a 16-B boundary (the headers are 16-B aligned types: a misaligned source faults in
+        // the vectorised copy)
+        const uint64_t bf = n * sizeof(FinRec), bmax = 2 * n * sizeof(CopyHdr);
+        static_assert(sizeof(CopyHdr) == sizeof(VersionHdr) && sizeof(CopyHdr) % 16 == 0, "header sizes");
+        uint8_t *pin = pinned_bytes(dv, 64 + bmax + bf, par);
+        if (!pending) pinned_bytes(dv, 64 + bmax + bf, par ^ 1);
+        // write-overlap mode: the kernels up to the publish go on the table's write stream ks,
+        // which waits for the previous epoch's publish only (or, when the device image changed
+        // otherwise since, for all of s) -- not for the caller's work enqueued after it, such as
+        // the previous epoch's read probes.  They read the slot words that publish left and
+        // write only scratch, this epoch's output parity and the appended header / row ranges
+        // no published slot word reaches yet; the publish joins s behind them.
+        // Either mode: the epoch starts after the previous epoch's publish (wp_pub_ev, recorded
+        // after every publish), so a caller that alternates streams between epochs stays ordered
+        // on the device append counters and slot words the previous epoch left.
+        hipStream_t ks = s;
+        if (t->wp_overlap) {
+            if (!dv.wp_pub_valid) hip_check(hipEventRecord(dv.wp_pub_ev, s), "write event");
+            hip_check(hipStreamWaitEvent(dv.wp_stream, dv.wp_pub_ev, 0), "write wait");
+            ks = dv.wp_stream;
+        } else if (dv.wp_pub_valid) {
+            hip_check(hipStreamWaitEvent(s, dv.wp_pub_ev, 0), "previous publish");
+        }
+        // from here on the epoch reaches the device: a failure is sticky (see EpochGuard)
+        guard.enqueued = true;
+        if (!pending)
+            wp_set_bases<<<1, 1, 0, ks>>>((uint64_t *)dv.wp_bases.p, h.copies_.size(), h.versions_.size(),
+                                          h.images_.size());
+        t->wp_epoch_n[par] = n;
 
         // 1. locate
         hip_check(launch_probe(view, d_keys, d_lens, nullptr, nullptr, n, pout, nullptr, ks, t->tune), "locate");
@@ -796,10 +825,8 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         wp_publish<<<blocks_for(n, 256), 256, 0, s>>>(a, (SlotInfo *)dv.slot.p, rcs, succ, prev, ranks, ls, tot, fin,
                                                       d_rc);
         hip_check(hipGetLastError(), "write-path kernels");
-        if (t->wp_overlap) {  // the next overlapped epoch starts after this publish
-            hip_check(hipEventRecord(dv.wp_pub_ev, s), "write event");
-            dv.wp_pub_valid = true;
-        }
+        hip_check(hipEventRecord(dv.wp_pub_ev, s), "write event");  // the next epoch starts after it
+        dv.wp_pub_valid = true;
 
         // the host adopts the epoch.  The headers and slot words come back on a stream of their
         // own into pinned staging (full PCIe rate) and the host adopts them on a background
@@ -807,22 +834,8 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         // -- and the next epoch's write path -- overlap the copies); the next call that needs the
         // host table waits for it (host() / settle).
         const double t_enqueue = ms(t0);
-        if (!dv.adopt_stream) {  // high priority: the export gets its CUs beside the next probe
-            int lo = 0, hi = 0;
-            hip_check(hipDeviceGetStreamPriorityRange(&lo, &hi), "stream priorities");
-            hip_check(hipStreamCreateWithPriority(&dv.adopt_stream, hipStreamNonBlocking, hi), "adopt stream");
-        }
-        for (hipEvent_t *e : {&dv.adopt_ev[0], &dv.adopt_ev[1], &dv.export_ev[0], &dv.export_ev[1]})
-            if (!*e) hip_check(hipEventCreateWithFlags(e, hipEventDisableTiming), "adopt event");
         const double t_events = ms(t0);
         hip_check(hipEventRecord(dv.adopt_ev[par], s), "adopt event");
-        // staging: [totals 64 B][copy headers][version headers][slot words], sized for the worst
-        // case (one copy and one version per op); every part starts on a 16-B boundary (the
-        // headers are 16-B aligned types: a misaligned source faults in the vectorised copy)
-        const uint64_t bf = n * sizeof(FinRec), bmax = 2 * n * sizeof(CopyHdr);
-        static_assert(sizeof(CopyHdr) == sizeof(VersionHdr) && sizeof(CopyHdr) % 16 == 0, "header sizes");
-        uint8_t *pin = pinned_bytes(dv, 64 + bmax + bf, par);
-        if (!pending) pinned_bytes(dv, 64 + bmax + bf, par ^ 1);
         auto *totals = reinterpret_cast<uint64_t *>(pin);
         auto *fr = reinterpret_cast<FinRec *>(pin + 64 + bmax);
         const double t_pinned = ms(t0);

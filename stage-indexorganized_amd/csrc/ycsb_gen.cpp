@@ -103,6 +103,21 @@ extern "C" int stage_fastrandom_next(uint64_t seed, uint64_t count, uint64_t *ou
     return STAGE_OK;
 }
 
+// RunMixed's per-op draws from its FastRandom (ycsb_mixed.cpp:26, 37, 43): rng.NextUniform() <
+// update_ratio makes op i an update, whose 100-B delta is memset to rng.next_char() (next(8) %
+// 256, benchmark_common.h:29) drawn right after; a read consumes only the uniform.
+extern "C" int stage_ycsb_ops(uint64_t seed, uint64_t count, double update_ratio, uint8_t *is_update,
+                              uint8_t *chr) {
+    if (count && (!is_update || !chr)) return STAGE_E_ARG;
+    FastRandom r(seed);
+    for (uint64_t i = 0; i < count; ++i) {
+        const bool upd = r.uniform() < update_ratio;
+        is_update[i] = upd;
+        chr[i] = upd ? (uint8_t)(r.next(8) % 256) : 0;
+    }
+    return STAGE_OK;
+}
+
 extern "C" int stage_zipf_zeta(uint64_t n, double theta, double *out) {
     if (!out) return STAGE_E_ARG;
     *out = zeta(n, theta);

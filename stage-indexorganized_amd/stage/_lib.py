@@ -138,6 +138,7 @@ SIGNATURES = {
     "stage_zipf_draws": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_double, ctypes.c_uint64, ctypes.c_uint64, c_vp,
                                         ctypes.c_int]),
     "stage_zipf_zeta": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_double, c_vp]),
+    "stage_ycsb_ops": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_double, c_vp, c_vp]),
 }
 
 

@@ -701,6 +701,14 @@ def fastrandom(seed, count):
     return out
 
 
+def ycsb_ops(seed, count, update_ratio):
+    """RunMixed's per-op stream (ycsb_mixed.cpp:26-44): (is_update bool[count], delta byte u8[count])"""
+    upd = np.empty(count, np.uint8)
+    chr_ = np.empty(count, np.uint8)
+    check(lib().stage_ycsb_ops(seed, count, update_ratio, upd.ctypes.data, chr_.ctypes.data), "ycsb_ops")
+    return upd.astype(bool), chr_
+
+
 def device_count():
     c = ctypes.c_int(0)
     rc = lib().stage_device_count(ctypes.byref(c))

@@ -19,6 +19,8 @@ BIN = os.path.join(REPO, "oracle", "_ref", "ref_zipf_kat")
 FAST = [(0, 64), (1, 64), (0x5EED, 64), ((1 << 47) + 3, 64)]
 ZIPF = [(999, 0.9, 1, 512), (999, 0.99, 7, 512), (999_999, 0.9, 0x5EED, 512), (999_999, 0.99, 0x5EED + 1, 512),
         (99_999_999, 0.9, 0x5EED, 512), (99_999_999, 0.99, 0x5EED + 1000, 512)]
+# RunMixed op streams (ycsb_mixed.cpp:26-44): (seed, count, update_ratio); -1 = read, else the delta byte
+OPS = [(1, 2048, 0.05), (0x5EED + 77, 2048, 0.05), (3, 1024, 0.5), (9, 256, 1.0)]
 
 
 def run(*args):
@@ -36,6 +38,8 @@ def main():
         r = run("zipf", n, repr(theta), seed, count)
         out["zipf"].append(dict(n=n, theta=theta, seed=seed, **r))
         print(n, theta, r["zeta_n_bits"])
+    out["ops"] = [dict(seed=seed, count=count, update_ratio=ratio, ops=run("ops", seed, count, repr(ratio))["ops"])
+                  for seed, count, ratio in OPS]
     with open(os.path.join(HERE, "zipf_kat.json"), "w") as f:
         json.dump(out, f, indent=0)
 

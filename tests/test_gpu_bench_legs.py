@@ -27,7 +27,9 @@ def test_c3_leg_write_paths(gpu, write_path):
     assert cfg["write_path"] == write_path and 0 < cfg["updates_applied"] <= cfg["update_ops"]
     rcs = cfg["update_rc_counts"]
     assert sum(rcs.values()) == cfg["update_ops"] and rcs["ok"] == cfg["updates_applied"]
-    assert rcs.get("not_needed_update", 0) > 0  # a hot key's repeats within an epoch
+    # RunMixed's stream: each update's byte is a fresh next_char(), so an update finds its own
+    # value already there only by chance (1/256 per update), not on every repeat of a hot key
+    assert rcs.get("not_needed_update", 0) < 0.05 * cfg["update_ops"]
     # the oracle replays every epoch and answers the last epoch's sampled reads at their read ids
     orc = O.OracleTree()
     orc.load_ycsb(0, rows, 8, 0)

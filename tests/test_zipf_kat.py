@@ -46,3 +46,14 @@ def test_zipf_draws(case, nthreads):
     if nthreads > 1:  # the other threads' jumped streams continue the same sequence
         assert (got == stage.zipf_draws(case["n"], case["theta"], case["seed"], count, nthreads=1)).all()
     assert got.min() >= 1 and got.max() <= case["n"]
+
+
+@pytest.mark.parametrize("case", KAT["ops"], ids=lambda c: "seed%d_u%g" % (c["seed"], c["update_ratio"]))
+def test_ycsb_op_stream(case):
+    """RunMixed's op stream (ycsb_mixed.cpp:26-44): which ops update, and each update's
+    next_char() delta byte, equal the reference's FastRandom draws."""
+    want = np.array(case["ops"])
+    upd, chr_ = stage.ycsb_ops(case["seed"], case["count"], case["update_ratio"])
+    assert (upd == (want >= 0)).all()
+    assert (chr_[upd] == want[want >= 0]).all()
+    assert (chr_[~upd] == 0).all()
