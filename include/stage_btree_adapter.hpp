@@ -15,14 +15,30 @@
 //                         [key 4][pad 4][payload 0..995]; retired = memcpy from the TupleHeader
 //                         slot = [key 4][payload 0..999] (executor.h:396-401, 424)
 //
-// Pointers the reference keeps in these objects (RecordMetadata::next_ptr / loc_ptr,
-// RecordMeta::next_tuple_ptr) are process-local addresses there; here they are stable opaque
-// handles: loc_ptr = record_handle() (the rw-set identity, RecordMeta::operator== compares
-// loc_ptr only, record_meta.h:248-251), next_ptr = a non-zero copy handle exactly when an
-// overwrite header exists (what PerformRead's GetOversionHeader(next_ptr) tests), else 0.
+// and what the kept SSNTransactionManager dereferences through such a Record
+// (transaction_manager.cpp:29-221, 362-410, 535-1046):
+//
+//   LocationTable         RecordMetadata::loc_ptr -> RecordLocation -> record_meta_ptr: one
+//                         RecordLocation per location handle (record_location.h:13-42) whose
+//                         record_meta_ptr is the library's live cell (stage_location_cell), so
+//                         `*reinterpret_cast<RecordMetadata *>(loc->record_meta_ptr)` is the
+//                         record's current RecordMetadata wherever splits moved it (tm.cpp:37,
+//                         123, 605)
+//   OverwritePool         the EphemeralPool methods the manager calls on a next_ptr
+//                         (GetOversionHeader, IncreaseWRCount, DecreaseWRCount, UpdatePs) and
+//                         the AddReader BTree::Read does (b_tree.cpp:2104-2105), over stage_copy_*
+//   read_via_copy()       whether BTree::Read served the read from the overwrite copy (then it
+//                         registers the reader: b_tree.cpp:2087-2105)
+//
+// next_ptr is the library's next handle (stage_hip.h STAGE_NEXT_*: the overwrite copy while an
+// update is in flight -- the EphemeralPool key --, the newest TupleHeader after a commit);
+// loc_ptr is whatever the facade uses for RecordLocation * (LocationTable::get(handle)).
 #pragma once
 #include <cstdint>
 #include <cstring>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
 #include <vector>
 
 #include "stage_hip.h"
@@ -55,8 +71,107 @@ constexpr uint64_t kVisible = 1ull << 62;
 inline uint64_t meta_word(const stage_probe_out &o) { return ((uint64_t)o.meta_hi << 32) | o.rec_cstamp; }
 inline uint32_t key_length(uint64_t meta) { return (uint32_t)((meta >> 48) & 0x2FFF); }
 inline uint32_t padded_key_length(uint64_t meta) { return (key_length(meta) + 7u) / 8u * 8u; }
-// stable identity of the hit record (leaf, slot) -- never 0
-inline uint64_t record_handle(const stage_probe_out &o) { return ((uint64_t)o.leaf << 16 | o.slot) + 1; }
+inline bool is_inserting(uint64_t meta) { return (meta & kVisible) && (meta & kControl); }
+inline bool is_copy_handle(uint64_t next_ptr) {
+    return next_ptr != 0 && (next_ptr & STAGE_NEXT_KIND_MASK) == STAGE_NEXT_COPY && next_ptr <= 0xFFFFFFFFull;
+}
+inline uint32_t copy_id(uint64_t next_ptr) { return (uint32_t)(next_ptr & STAGE_NEXT_INDEX_MASK); }
+
+// BTree::Read served the read from the overwrite copy (record in flight, copy header found,
+// not for update): Record::Neww + AddReader(commit_id) (b_tree.cpp:2087-2105)
+inline bool read_via_copy(const stage_probe_out &o, const stage_probe_ident &id) {
+    return o.status != STAGE_ST_NOT_FOUND && is_inserting(meta_word(o)) && is_copy_handle(id.next);
+}
+
+// RecordLocation (record_location.h:13-42)
+struct RecordLocation {
+    uint64_t node_header_ptr;
+    uint64_t record_meta_ptr;
+};
+
+// One RecordLocation per location handle at a stable address; record_meta_ptr = the library's
+// cell for the handle (stage_location_cells must be on).  The facade puts get(handle) into
+// RecordMetadata::loc_ptr; handle_of() maps it back.  Thread-safe.
+class LocationTable {
+public:
+    explicit LocationTable(stage_table *t) : t_(t) {}
+    RecordLocation *get(uint64_t handle) {
+        if (handle == 0) return nullptr;
+        std::lock_guard<std::mutex> g(mu_);
+        const uint64_t c = (handle - 1) >> kBits, i = (handle - 1) & ((1u << kBits) - 1);
+        if (chunks_.size() <= c) chunks_.resize(c + 1);
+        if (!chunks_[c]) chunks_[c].reset(new RecordLocation[1u << kBits]());
+        RecordLocation &l = chunks_[c][i];
+        if (!l.record_meta_ptr) {
+            const void *cell = nullptr;
+            if (stage_location_cell(t_, handle, &cell) != STAGE_OK) throw std::runtime_error(stage_last_error());
+            l.record_meta_ptr = reinterpret_cast<uint64_t>(cell);
+        }
+        return &l;
+    }
+    // the RecordMetadata the location points at now (the manager's `meta_location` deref)
+    static const RecordMetadata *record_meta(const RecordLocation *l) {
+        return reinterpret_cast<const RecordMetadata *>(l->record_meta_ptr);
+    }
+    static uint64_t handle_of(const RecordLocation *l) { return l ? record_meta(l)->loc_ptr : 0; }
+
+private:
+    static constexpr uint32_t kBits = 16;
+    stage_table *t_;
+    std::mutex mu_;
+    std::vector<std::unique_ptr<RecordLocation[]>> chunks_;
+};
+
+// EphemeralPool::OverwriteVersionHeader as the manager reads it (ephemeral_pool.h:26-150)
+struct OverwriteHeader {
+    uint32_t cstamp, pstamp, rstamp, sstamp;
+    uint16_t count;
+    bool waiting;
+    std::vector<uint32_t> readers;
+    int GetReadersNum() const { return (int)readers.size(); }
+    uint32_t GetReaders(int i) const { return i < (int)readers.size() ? readers[i] : 0u; }
+};
+
+// The EphemeralPool calls of the kept manager, keyed by next_ptr as the reference keys them by
+// copy location (ephemeral_pool.cpp:69-205); a next_ptr that is not a copy handle has no header.
+class OverwritePool {
+public:
+    explicit OverwritePool(stage_table *t) : t_(t) {}
+    bool GetOversionHeader(uint64_t next_ptr, OverwriteHeader &h) const {
+        if (!is_copy_handle(next_ptr)) return false;
+        const uint32_t id = copy_id(next_ptr);
+        stage_copy_state s;
+        if (stage_copy_get(t_, &id, 1, &s) != STAGE_OK) return false;
+        h.cstamp = s.cstamp, h.pstamp = s.pstamp, h.rstamp = s.rstamp, h.sstamp = s.sstamp;
+        h.count = s.count, h.waiting = s.waiting != 0;
+        h.readers.resize(s.readers);
+        uint32_t k = 0;
+        if (s.readers && stage_copy_readers(t_, id, h.readers.data(), s.readers, &k) != STAGE_OK) return false;
+        h.readers.resize(k < s.readers ? k : s.readers);
+        return true;
+    }
+    void AddReader(uint64_t next_ptr, uint32_t read_id) {  // OverwriteVersionHeader::AddReader
+        if (is_copy_handle(next_ptr)) check(stage_copy_add_reader(t_, copy_id(next_ptr), read_id));
+    }
+    bool IncreaseWRCount(uint64_t next_ptr) {
+        int ok = 0;
+        if (!is_copy_handle(next_ptr) || stage_copy_wr_count(t_, copy_id(next_ptr), +1, &ok) != STAGE_OK) return false;
+        return ok != 0;
+    }
+    void DecreaseWRCount(uint64_t next_ptr) {
+        int ok = 0;
+        if (is_copy_handle(next_ptr)) check(stage_copy_wr_count(t_, copy_id(next_ptr), -1, &ok));
+    }
+    bool UpdatePs(uint64_t next_ptr, uint32_t pstamp) {
+        return is_copy_handle(next_ptr) && stage_copy_update_ps(t_, copy_id(next_ptr), pstamp) == STAGE_OK;
+    }
+
+private:
+    static void check(int rc) {
+        if (rc != STAGE_OK) throw std::runtime_error(stage_last_error());
+    }
+    stage_table *t_;
+};
 
 // LeafNode::Read -> SearchRecordMeta hit or RecordMetadata{0}
 inline int read_return_code(const stage_probe_out &o) {
@@ -70,21 +185,31 @@ inline bool has_record(const stage_probe_out &o) {
     return o.status == STAGE_ST_LATEST || o.status == STAGE_ST_COPY;
 }
 
+// The RecordMeta BTree::Read builds (RecordMeta(*meta), b_tree.cpp:2083): the hit slot's
+// RecordMetadata -- meta word, next_ptr = its next handle, loc_ptr = the facade's RecordLocation
+// for its location handle (LocationTable::get(id.loc), or any stable value the facade maps back)
+inline RecordMeta record_meta(const stage_probe_out &o, const stage_probe_ident &id, uint64_t loc_ptr,
+                              uint32_t payload_size) {
+    RecordMeta rm{};
+    rm.meta_data.meta = meta_word(o);
+    rm.meta_data.next_ptr = id.next;
+    rm.meta_data.loc_ptr = loc_ptr;
+    rm.total_size = padded_key_length(rm.meta_data.meta) + payload_size;  // SetTotalSize, b_tree.cpp:2084
+    rm.next_tuple_ptr = 0;  // TupleHeader / copy-next handles stay device-side
+    rm.cstamp = o.cstamp;   // latest: reader id; copy: the copy's rstamp
+    return rm;
+}
+
 // The Record bytes (b_tree.h:400-448): RecordMeta, then tuple_data_ = [cstamp][key][payload].
 // `row` = the probe's tuple row [key padded to 8][payload] (canonical: the pad bytes, which
 // Record::Neww leaves uninitialised, are zero).  Empty when has_record() is false.
-inline std::vector<uint8_t> make_record(const stage_probe_out &o, const uint8_t *row, uint32_t payload_size) {
+inline std::vector<uint8_t> make_record(const stage_probe_out &o, const stage_probe_ident &id, uint64_t loc_ptr,
+                                        const uint8_t *row, uint32_t payload_size) {
     std::vector<uint8_t> out;
     if (!has_record(o)) return out;
     const uint64_t meta = meta_word(o);
     const uint32_t kp = padded_key_length(meta);
-    RecordMeta rm{};
-    rm.meta_data.meta = meta;
-    rm.meta_data.next_ptr = (o.flags & STAGE_FLAG_COPY_PRESENT) ? (record_handle(o) | (1ull << 63)) : 0;
-    rm.meta_data.loc_ptr = record_handle(o);
-    rm.total_size = kp + payload_size;  // SetTotalSize(padded key + payload), b_tree.cpp:2079
-    rm.next_tuple_ptr = 0;              // TupleHeader / copy-next handles stay device-side
-    rm.cstamp = o.cstamp;               // latest: reader id; copy: the copy's rstamp
+    RecordMeta rm = record_meta(o, id, loc_ptr, payload_size);
     out.resize(sizeof(RecordMeta) + 4 + kp + payload_size);
     std::memcpy(out.data(), &rm, sizeof rm);
     std::memcpy(out.data() + sizeof rm, &o.cstamp, 4);  // Record::SetCstamp

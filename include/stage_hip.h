@@ -255,6 +255,66 @@ int64_t stage_export_locations(stage_table *t, uint64_t max, uint64_t *handles, 
 int stage_resolve_locations(stage_table *t, const uint64_t *handles, uint64_t n, uint32_t *leaf,
                             uint16_t *slot);
 
+/* ---- what the kept transaction manager reads through a Record -----------------------------
+ * The reference's Record carries RecordMetadata{meta, next_ptr, loc_ptr} (record_meta.h:30-60)
+ * and SSNTransactionManager dereferences two of them (transaction_manager.cpp:29-221, 362-410,
+ * 535-815): loc_ptr -> RecordLocation -> record_meta_ptr, the record's CURRENT RecordMetadata
+ * wherever splits moved it (FindMaxPstamp :37, FindMinSstamp :123, commit :605), and next_ptr ->
+ * EphemeralPool::GetOversionHeader, the in-flight update's overwrite-copy header with its
+ * readers (PerformRead :379-399, FindMinSstamp :148-215, FindMaxPstamp :41-97, post-commit
+ * READ :753-762).  Here both are stable handles:
+ *   location handle  = the RecordLocation's allocation index + 1 (stage_export_locations);
+ *   next handle      = 0, STAGE_NEXT_COPY | copy id (the overwrite copy, EphemeralPool's
+ *                      location) or STAGE_NEXT_VERSION | version id (the newest TupleHeader).
+ * stage_probe_identify: for probe results d_out[0..n) (32-B records of stage_probe_batch on the same
+ *   published image, same stream), the hit record's {location handle, next handle} -- the
+ *   loc_ptr / next_ptr of the RecordMetadata BTree::Read put in the Record (0/0 for NOT_FOUND).
+ *   stage_reader_read_ident is stage_reader_read with the same two handles.
+ * stage_location_cells turns on the cells: from then on every host write keeps, per location,
+ *   the RecordMetadata it points at as 24 B {meta, next_ptr = next handle, loc_ptr = handle} at a
+ *   stable address -- what RecordLocation::record_meta_ptr points at, readable without a call or
+ *   a lock from any thread (a dropped location reads meta 0).  stage_location_cell gives the cell
+ *   of one handle (valid for the table's lifetime).
+ * stage_copy_*: the transaction side of overwrite copy `copy_id` (EphemeralPool::
+ *   OverwriteVersionHeader, ephemeral_pool.h:26-150): its stamps, AddReader (BTree::Read for a
+ *   read served from the copy, b_tree.cpp:2104-2105), the reader list FindMaxPstamp walks,
+ *   IncreaseWRCount (+1, refused -- *ok = 0 -- once the header is waiting) / DecreaseWRCount (-1)
+ *   (ephemeral_pool.cpp:69-103) and UpdatePs (:194-205).  The writer's commit (stage_commit_update*)
+ *   sets sstamp and waiting (tm.cpp:618-619), its abort waiting with sstamp MAX (:872-875); the
+ *   pool never frees a header (no GC).  Thread-safe among themselves and against the writer. */
+#define STAGE_NEXT_KIND_MASK 0xC0000000u
+#define STAGE_NEXT_COPY 0x40000000u
+#define STAGE_NEXT_VERSION 0x80000000u
+#define STAGE_NEXT_INDEX_MASK 0x3FFFFFFFu
+typedef struct stage_probe_ident {
+    uint32_t loc;   /* RecordLocation handle of the hit record (0 = none)                     */
+    uint32_t next;  /* the hit slot's next handle (STAGE_NEXT_*), as BTree::Read saw it        */
+} stage_probe_ident;
+typedef struct stage_copy_state {
+    uint32_t cstamp;   /* the writer's id (OverwriteVersionHeader::cstamp)                      */
+    uint32_t pstamp;   /* version access stamp: the writer's id until UpdatePs                  */
+    uint32_t rstamp;   /* the overwritten version's cstamp                                      */
+    uint32_t sstamp;   /* 0xFFFFFFFF until the writer commits                                   */
+    uint32_t readers;  /* GetReadersNum                                                         */
+    uint16_t count;    /* read dependency count (IncreaseWRCount - DecreaseWRCount)              */
+    uint8_t waiting;   /* the writer committed or aborted                                       */
+    uint8_t pad;
+} stage_copy_state;
+int stage_probe_identify(stage_table *t, const stage_probe_out *d_out, uint64_t n, stage_probe_ident *d_ident,
+                      void *stream);
+/* the host layout's RecordMetadata of the key's record now (SearchRecordMeta on the host leaf):
+ * what BTree::Update hands back in meta_upt_ for PerformUpdate (b_tree.cpp:2144-2155) -- meta word
+ * and {location handle, next handle}; *rc_out = STAGE_RC_NOT_FOUND when the key has no record */
+int stage_record_meta_key(stage_table *t, const uint8_t *key, uint16_t key_size, uint64_t *meta,
+                          stage_probe_ident *ident, uint8_t *rc_out);
+int stage_location_cells(stage_table *t);
+int stage_location_cell(stage_table *t, uint64_t handle, const void **cell);
+int stage_copy_get(stage_table *t, const uint32_t *copy_ids, uint64_t n, stage_copy_state *out);
+int stage_copy_readers(stage_table *t, uint32_t copy_id, uint32_t *read_ids, uint32_t max, uint32_t *count);
+int stage_copy_add_reader(stage_table *t, uint32_t copy_id, uint32_t read_id);
+int stage_copy_wr_count(stage_table *t, uint32_t copy_id, int delta, int *ok);
+int stage_copy_update_ps(stage_table *t, uint32_t copy_id, uint32_t pstamp);
+
 /* ---- device batch path (the replaced hot path) ------------------------------------------
  * stage_probe_batch  replaces LeafNode::Read/SearchRecordMeta (b_tree.cpp:1042-1051, 18-122),
  *   Record::New/Neww (b_tree.h:407-448), BTree::Read (b_tree.cpp:2066-2129) and the
@@ -335,6 +395,8 @@ int stage_reader_create_resident(stage_table *t, uint32_t ring_slots, uint32_t w
                                  stage_reader **out);
 int stage_reader_read(stage_reader *r, uint64_t key, uint16_t key_size, uint32_t read_id,
                       stage_probe_out *out, uint8_t *record);
+int stage_reader_read_ident(stage_reader *r, uint64_t key, uint16_t key_size, uint32_t read_id,
+                            stage_probe_out *out, uint8_t *record, stage_probe_ident *ident);
 int stage_reader_stats(stage_reader *r, uint64_t *stats);
 int stage_reader_destroy(stage_reader *r);
 

@@ -85,6 +85,9 @@ typedef struct orc_copy { /* EphemeralPool::OverwriteVersionHeader, ephemeral_po
     int wr_count; /* readers counted by IncreaseWRCount / DecreaseWRCount (ephemeral_pool.cpp:194-239) */
     uint8_t *image; /* [key(key_len)][payload] (b_tree.cpp:1143-1144) */
     struct orc_copy *reg_next;
+    uint32_t id;                /* allocation order (the copy id of a next handle) */
+    uint32_t *readers;          /* AddReader (ephemeral_pool.h:61-65) */
+    uint32_t nreaders, capreaders;
 } orc_copy;
 
 typedef struct orc_th { /* TupleHeader, version_store.h:28-155 */
@@ -93,6 +96,7 @@ typedef struct orc_th { /* TupleHeader, version_store.h:28-155 */
     uint8_t *slot; /* [key(key_len)][payload] (transaction_manager.cpp:639-640) */
     uint16_t key_len;
     struct orc_th *reg_next;
+    uint32_t id; /* allocation order (the version id of a next handle) */
 } orc_th;
 
 /* ---------------------------------------------------------------- leaf image */
@@ -150,6 +154,8 @@ struct orc_tree {
     uint64_t ngarbage, capgarbage;
     uint64_t retired;
     int bulk; /* orc_tree_set_bulk: a load of distinct keys, CheckUnique skipped */
+    orc_copy **copy_by_id; /* copy id -> copy (ids in allocation order) */
+    uint32_t ncopies, capcopies, nths;
 };
 
 typedef struct { orc_inner *node; uint32_t meta_index; } frame_t;
@@ -642,6 +648,7 @@ void orc_tree_free(orc_tree *t) {
     for (orc_copy *c = t->copies; c;) {
         orc_copy *nx = c->reg_next;
         free(c->image);
+        free(c->readers);
         free(c);
         c = nx;
     }
@@ -654,6 +661,7 @@ void orc_tree_free(orc_tree *t) {
     for (uint64_t i = 0; i < t->nlocs; i++) free(t->locs[i]);
     free(t->locs);
     free(t->garbage);
+    free(t->copy_by_id);
     free(t);
 }
 
@@ -1764,6 +1772,13 @@ static orc_copy *copy_alloc(orc_tree *t, const uint8_t *src_key, uint16_t klen, 
     memcpy(c->image + klen, src_key + pad_key(klen), t->payload_size); /* b_tree.cpp:1144 */
     c->reg_next = t->copies;
     t->copies = c;
+    if (t->ncopies == t->capcopies) {
+        t->capcopies = t->capcopies ? 2 * t->capcopies : 1024;
+        t->copy_by_id = realloc(t->copy_by_id, sizeof(orc_copy *) * t->capcopies);
+        if (!t->copy_by_id) abort();
+    }
+    c->id = t->ncopies;
+    t->copy_by_id[t->ncopies++] = c;
     return c;
 }
 
@@ -1810,6 +1825,7 @@ int orc_commit_update(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32
     memcpy(th->slot, c->image, c->key_len + t->payload_size);
     th->reg_next = t->ths;
     t->ths = th;
+    th->id = t->nths++;
     t->retired++;
     c->pre = (uint64_t)(uintptr_t)th;
     uint64_t m = mp->meta;
@@ -1836,7 +1852,9 @@ int orc_abort_update(orc_tree *t, const uint8_t *key, uint32_t key_size) {
     memcpy(rk + m_padded(mp->meta), c->image + c->key_len, t->payload_size); /* payload */
     mp->meta = (mp->meta & ~M_CONTROL) | M_VISIBLE;
     mp->next = c->next;
-    c->live = 0;
+    c->live = 0;        /* no record reaches it any more */
+    c->sstamp = MAX_CID; /* UpdateSs(MAX_CID), SetWaiting(true): the header stays in the pool */
+    c->waiting = 1;
     return ORC_RET_OK;
 }
 
@@ -1976,6 +1994,123 @@ void orc_resolve_locations(orc_tree *t, const uint64_t *handles, uint64_t n, uin
 }
 
 uint64_t orc_location_count(orc_tree *t) { return t->nlocs; }
+
+/* ---------------------------------------------------------------- transaction-manager facts
+ * What the kept SSNTransactionManager reads through a Record and its pool (the checker side of
+ * stage_hip.h's stage_probe_ident / stage_location_cell / stage_copy_*):
+ *   next handle   RecordMetadata::next_ptr named canonically: 0, ORC_NEXT_COPY | copy id (the
+ *                 EphemeralPool location of an in-flight update), ORC_NEXT_TH | version id
+ *   loc handle    RecordMetadata::loc_ptr = the RecordLocation's allocation index + 1
+ *   location meta *GetLocationPtr()->record_meta_ptr now (tm.cpp:37, 123, 605)
+ *   copy state    OverwriteVersionHeader cstamp / pstamp / rstamp / sstamp / readers / count /
+ *                 waiting (ephemeral_pool.h:26-150) and AddReader (b_tree.cpp:2105),
+ *                 IncreaseWRCount / DecreaseWRCount (ephemeral_pool.cpp:69-103), UpdatePs (:194-205) */
+#define ORC_NEXT_COPY 0x40000000u
+#define ORC_NEXT_TH 0x80000000u
+
+static uint32_t next_handle(uint64_t next) {
+    if (next == 0) return 0;
+    if (NEXT_KIND(next) == NEXT_COPY) return ORC_NEXT_COPY | ((orc_copy *)NEXT_PTR(next))->id;
+    if (NEXT_KIND(next) == NEXT_TH) return ORC_NEXT_TH | ((orc_th *)NEXT_PTR(next))->id;
+    return 0;
+}
+
+int orc_read_ident(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t read_id, orc_read_out *out,
+                   uint8_t *rec, uint64_t *meta, uint32_t *loc, uint32_t *next) {
+    read_one(t, key, (uint16_t)key_size, read_id, out, rec);
+    *meta = 0;
+    *loc = 0;
+    *next = 0;
+    if (out->status == ORC_ST_NOT_FOUND) return 0;
+    uint8_t *leaf = traverse_to_leaf(t, NULL, key, (uint16_t)key_size, 1);
+    int64_t slot = search_record_meta(leaf, key, (uint16_t)key_size, 1);
+    if (slot < 0) return -1;
+    orc_rmeta *mp = l_meta(leaf, (uint32_t)slot);
+    *meta = mp->meta;
+    *loc = mp->loc ? (uint32_t)(mp->loc->id + 1) : 0;
+    *next = next_handle(mp->next);
+    return 0;
+}
+
+/* the key's record now (BTree::Update's meta_upt_, b_tree.cpp:2144-2155): 0 = found, -1 = none */
+int orc_record_meta(orc_tree *t, const uint8_t *key, uint32_t key_size, uint64_t *meta, uint32_t *loc, uint32_t *next) {
+    *meta = 0;
+    *loc = 0;
+    *next = 0;
+    orc_rmeta *mp = find_meta(t, key, (uint16_t)key_size, NULL);
+    if (!mp) return -1;
+    *meta = mp->meta;
+    *loc = mp->loc ? (uint32_t)(mp->loc->id + 1) : 0;
+    *next = next_handle(mp->next);
+    return 0;
+}
+
+int orc_location_meta(orc_tree *t, uint64_t handle, uint64_t *meta, uint32_t *next) {
+    *meta = 0;
+    *next = 0;
+    if (handle == 0 || handle > t->nlocs) return -1;
+    orc_loc *l = t->locs[handle - 1];
+    if (!l || !l->leaf) return 0; /* dangling: dropped by a split or an aborted insert */
+    orc_rmeta *mp = l_meta(l->leaf, l->slot);
+    *meta = mp->meta;
+    *next = next_handle(mp->next);
+    return 0;
+}
+
+static orc_copy *copy_by(orc_tree *t, uint32_t id) { return id < t->ncopies ? t->copy_by_id[id] : NULL; }
+
+int orc_copy_state(orc_tree *t, uint32_t copy_id, uint32_t *st /* cstamp pstamp rstamp sstamp nreaders count waiting */) {
+    orc_copy *c = copy_by(t, copy_id);
+    if (!c) return -1;
+    st[0] = c->cstamp;
+    st[1] = c->pstamp;
+    st[2] = c->rstamp;
+    st[3] = c->sstamp;
+    st[4] = c->nreaders;
+    st[5] = (uint32_t)(uint16_t)c->wr_count;
+    st[6] = (uint32_t)c->waiting;
+    return 0;
+}
+
+uint32_t orc_copy_readers(orc_tree *t, uint32_t copy_id, uint32_t *out, uint32_t max) {
+    orc_copy *c = copy_by(t, copy_id);
+    if (!c) return 0;
+    for (uint32_t i = 0; i < c->nreaders && i < max; i++) out[i] = c->readers[i];
+    return c->nreaders;
+}
+
+int orc_copy_add_reader(orc_tree *t, uint32_t copy_id, uint32_t read_id) {
+    orc_copy *c = copy_by(t, copy_id);
+    if (!c) return -1;
+    if (c->nreaders == c->capreaders) {
+        c->capreaders = c->capreaders ? 2 * c->capreaders : 8;
+        c->readers = realloc(c->readers, sizeof(uint32_t) * c->capreaders);
+        if (!c->readers) abort();
+    }
+    c->readers[c->nreaders++] = read_id;
+    return 0;
+}
+
+/* delta +1: IncreaseWRCount -> AddCount, refused (0) once the header is waiting; -1:
+ * DecreaseWRCount -> SubCount (a uint16_t count) */
+int orc_copy_wr_count(orc_tree *t, uint32_t copy_id, int delta) {
+    orc_copy *c = copy_by(t, copy_id);
+    if (!c) return -1;
+    if (delta > 0) {
+        if (c->waiting) return 0;
+        c->wr_count = (uint16_t)(c->wr_count + 1);
+        return 1;
+    }
+    c->wr_count = (uint16_t)(c->wr_count - 1);
+    return 1;
+}
+
+int orc_copy_update_ps(orc_tree *t, uint32_t copy_id, uint32_t pstamp) {
+    orc_copy *c = copy_by(t, copy_id);
+    if (!c) return -1;
+    c->pstamp = pstamp;
+    return 0;
+}
 
 /* ---------------------------------------------------------------- murmur */
 /* MurmurHash64A, misc/murmur/MurmurHash2.cpp:99-147 (little-endian, unaligned) */

@@ -170,6 +170,21 @@ int64_t orc_export_leaves(orc_tree *t, uint32_t cap, uint64_t max_leaves, uint32
 void orc_resolve_locations(orc_tree *t, const uint64_t *handles, uint64_t n, uint32_t *leaf, uint16_t *slot);
 uint64_t orc_location_count(orc_tree *t);
 
+/* transaction-manager facts (see stage_oracle.c "transaction-manager facts"): the hit slot's meta
+ * word, RecordLocation handle and next handle (0 / 0x40000000 | copy id / 0x80000000 | version
+ * id); a location's current meta word + next handle; overwrite-copy state st[7] = {cstamp,
+ * pstamp, rstamp, sstamp, readers, count, waiting}, its readers, AddReader, WR count (+1 / -1;
+ * returns 0 when IncreaseWRCount is refused), UpdatePs */
+int orc_read_ident(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t read_id, orc_read_out *out,
+                   uint8_t *rec, uint64_t *meta, uint32_t *loc, uint32_t *next);
+int orc_location_meta(orc_tree *t, uint64_t handle, uint64_t *meta, uint32_t *next);
+int orc_record_meta(orc_tree *t, const uint8_t *key, uint32_t key_size, uint64_t *meta, uint32_t *loc, uint32_t *next);
+int orc_copy_state(orc_tree *t, uint32_t copy_id, uint32_t *st);
+uint32_t orc_copy_readers(orc_tree *t, uint32_t copy_id, uint32_t *out, uint32_t max);
+int orc_copy_add_reader(orc_tree *t, uint32_t copy_id, uint32_t read_id);
+int orc_copy_wr_count(orc_tree *t, uint32_t copy_id, int delta);
+int orc_copy_update_ps(orc_tree *t, uint32_t copy_id, uint32_t pstamp);
+
 /* KeyCompare (b_tree.h:116-134) */
 int orc_key_compare(const uint8_t *k1, uint32_t s1, const uint8_t *k2, uint32_t s2);
 /* MurmurHash64A (misc/murmur/MurmurHash2.cpp:99-147) */

@@ -367,6 +367,147 @@ int stage_resolve_locations(stage_table *t, const uint64_t *handles, uint64_t n,
     });
 }
 
+// ---- what the kept transaction manager reads through a Record (stage_hip.h) ----------------
+
+}  // extern "C"
+
+// the SSN state of copy `id` under its mutex; a copy the device wrote in an epoch the host has
+// not adopted yet is waited for (stage_table::settle) once
+template <class F>
+static int with_copy(stage_table *t, uint32_t id, F fn) {
+    stage::CopySsnTable &s = t->host->ssn_;
+    {
+        std::unique_lock<std::mutex> g(s.mu);
+        if (id < s.e.size()) return fn(s, s.e[id]);
+    }
+    int rc = guarded([&] {
+        t->settle();
+        return STAGE_OK;
+    });
+    if (rc) return rc;
+    std::unique_lock<std::mutex> g(s.mu);
+    if (id >= s.e.size()) return fail(STAGE_E_ARG, "no such overwrite copy");
+    return fn(s, s.e[id]);
+}
+
+extern "C" {
+
+int stage_probe_identify(stage_table *t, const stage_probe_out *d_out, uint64_t n, stage_probe_ident *d_ident,
+                      void *stream) {
+    int rc = need_synced(t);
+    if (rc) return rc;
+    if (n && (!d_out || !d_ident)) return fail(STAGE_E_ARG, "null device buffer");
+    if (t->status_bytes != 32) return fail(STAGE_E_STATE, "stage_probe_identify reads 32-B status records (leaf, slot)");
+    hipError_t e = hipSetDevice(t->dev.device);
+    if (e != hipSuccess) return hip_rc(e, "hipSetDevice");
+    e = stage::launch_ident(t->dev.view, reinterpret_cast<const stage::stage_probe_out_dev *>(d_out), n,
+                            reinterpret_cast<uint32_t *>(d_ident), pick(t, stream));
+    return hip_rc(e, "ident kernel");
+}
+
+int stage_record_meta_key(stage_table *t, const uint8_t *key, uint16_t key_size, uint64_t *meta,
+                          stage_probe_ident *ident, uint8_t *rc_out) {
+    if (!t || !key || !meta || !ident) return fail(STAGE_E_ARG, "null argument");
+    return guarded([&] {
+        stage::HostTable &h = host(t);
+        uint32_t leaf, slot;
+        *meta = 0;
+        *ident = stage_probe_ident{0, 0};
+        if (h.find(key, key_size, &leaf, &slot) < 0) {
+            if (rc_out) *rc_out = STAGE_RC_NOT_FOUND;
+            return STAGE_OK;
+        }
+        const size_t i = (size_t)leaf * h.cap() + slot;
+        *meta = h.meta_[i];
+        *ident = stage_probe_ident{h.loc_[i], h.next_[i]};
+        if (rc_out) *rc_out = STAGE_RC_OK;
+        return STAGE_OK;
+    });
+}
+
+int stage_location_cells(stage_table *t) {
+    if (!t) return fail(STAGE_E_ARG, "null table");
+    return guarded([&] {
+        host(t).enable_cells();
+        return STAGE_OK;
+    });
+}
+
+int stage_location_cell(stage_table *t, uint64_t handle, const void **cell) {
+    if (!t || !cell) return fail(STAGE_E_ARG, "null argument");
+    stage::HostTable &h = *t->host;  // no settle: a cell is read while the writer goes on
+    if (!h.cells_.on()) return fail(STAGE_E_STATE, "location cells are off: call stage_location_cells first");
+    if (handle == 0 || (handle >> stage::LocCells::kChunkBits) >= stage::LocCells::kDir)
+        return fail(STAGE_E_ARG, "location handle out of range");
+    return guarded([&] {
+        h.cells_.ensure(handle);
+        *cell = h.cells_.find(handle);
+        return STAGE_OK;
+    });
+}
+
+int stage_copy_get(stage_table *t, const uint32_t *copy_ids, uint64_t n, stage_copy_state *out) {
+    if (!t || (n && (!copy_ids || !out))) return fail(STAGE_E_ARG, "bad arguments");
+    for (uint64_t i = 0; i < n; ++i) {
+        const int rc = with_copy(t, copy_ids[i], [&](stage::CopySsnTable &s, stage::CopySsn &c) {
+            auto it = s.readers.find(copy_ids[i]);
+            out[i] = stage_copy_state{c.cstamp, c.pstamp, c.rstamp, c.sstamp,
+                                      it == s.readers.end() ? 0u : (uint32_t)it->second.size(), c.count, c.waiting, 0};
+            return STAGE_OK;
+        });
+        if (rc) return rc;
+    }
+    return STAGE_OK;
+}
+
+int stage_copy_readers(stage_table *t, uint32_t copy_id, uint32_t *read_ids, uint32_t max, uint32_t *count) {
+    if (!t || !count || (max && !read_ids)) return fail(STAGE_E_ARG, "bad arguments");
+    return with_copy(t, copy_id, [&](stage::CopySsnTable &s, stage::CopySsn &) {
+        auto it = s.readers.find(copy_id);
+        const uint32_t k = it == s.readers.end() ? 0u : (uint32_t)it->second.size();
+        for (uint32_t i = 0; i < k && i < max; ++i) read_ids[i] = it->second[i];
+        *count = k;
+        return STAGE_OK;
+    });
+}
+
+// EphemeralPool::OverwriteVersionHeader::AddReader (ephemeral_pool.h:61-65), called by BTree::Read
+// for a read served from the copy (b_tree.cpp:2104-2105)
+int stage_copy_add_reader(stage_table *t, uint32_t copy_id, uint32_t read_id) {
+    if (!t) return fail(STAGE_E_ARG, "null table");
+    return with_copy(t, copy_id, [&](stage::CopySsnTable &s, stage::CopySsn &) {
+        return guarded([&] {
+            s.readers[copy_id].push_back(read_id);
+            return STAGE_OK;
+        });
+    });
+}
+
+// IncreaseWRCount (+1: AddCount, refused once the header is waiting) / DecreaseWRCount (-1:
+// SubCount), ephemeral_pool.cpp:69-103
+int stage_copy_wr_count(stage_table *t, uint32_t copy_id, int delta, int *ok) {
+    if (!t || !ok || (delta != 1 && delta != -1)) return fail(STAGE_E_ARG, "bad arguments");
+    return with_copy(t, copy_id, [&](stage::CopySsnTable &, stage::CopySsn &c) {
+        if (delta > 0) {
+            *ok = c.waiting ? 0 : 1;
+            if (*ok) ++c.count;
+        } else {
+            --c.count;
+            *ok = 1;
+        }
+        return STAGE_OK;
+    });
+}
+
+// UpdatePs (ephemeral_pool.cpp:194-205)
+int stage_copy_update_ps(stage_table *t, uint32_t copy_id, uint32_t pstamp) {
+    if (!t) return fail(STAGE_E_ARG, "null table");
+    return with_copy(t, copy_id, [&](stage::CopySsnTable &, stage::CopySsn &c) {
+        c.pstamp = pstamp;
+        return STAGE_OK;
+    });
+}
+
 int stage_import_leaf_images(stage_table *t, const uint8_t *blocks, uint64_t n_leaves, uint32_t block_size,
                              const uint64_t *sep_keys, const uint16_t *sep_lens, uint64_t *n_records) {
     if (!t || !blocks || (!sep_keys != !sep_lens)) return fail(STAGE_E_ARG, "bad arguments");

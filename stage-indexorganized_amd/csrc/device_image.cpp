@@ -94,6 +94,7 @@ static void build_leaf(const HostTable &h, uint32_t hl, uint8_t *hd, uint64_t *o
         slot[s].meta = m;
         slot[s].next = live ? h.next_[hbase + s] : 0;
         slot[s].image = live ? h.image_[hbase + s] : 0;
+        slot[s].loc = live ? h.loc_[hbase + s] : 0;
         slot[s].pad = 0;
         if (meta_visible(m) && (p.key_width == 0 || meta_keylen(m) == p.key_width)) {
             vis[s / 64] |= 1ull << (s % 64);

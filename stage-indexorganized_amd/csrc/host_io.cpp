@@ -134,6 +134,7 @@ struct ResidentReader {
     uint32_t *done = nullptr, *stop = nullptr;
     stage_probe_out *out = nullptr;
     uint8_t *rows = nullptr;
+    stage_probe_ident *ident = nullptr;   // per slot: the read's location / next handles
     uint64_t *dpos = nullptr;             // device: next ticket per wave
     stage::ReaderRing ring{};             // device pointers
     std::unique_ptr<std::atomic<uint64_t>[]> freed;  // per slot: ticket + 1 of its last finished reader
@@ -189,14 +190,15 @@ struct stage_reader {
         uint32_t rid;
         stage_probe_out *out;
         uint8_t *rec;
+        stage_probe_ident *ident;
         int *rc;
     };
     // one batch buffer: a pinned, device-mapped block the probe kernel reads the keys from and
-    // writes the results to directly over PCIe (zero-copy: one launch, no copies)
+    // writes the results to directly over PCIe (zero-copy: one launch + the ident pass, no copies)
     struct Slot {
         hipStream_t s = nullptr;
         hipEvent_t ev = nullptr;
-        uint8_t *h = nullptr;   // keys | lens | read ids | out | rows
+        uint8_t *h = nullptr;   // keys | lens | read ids | out | rows | ident
         uint8_t *hd = nullptr;  // the same block as the device sees it
         std::vector<Req> reqs;
         uint32_t seq = 0;
@@ -246,6 +248,9 @@ void stage_reader::launch(Slot &sl) {
         e = stage::launch_probe(view, (const uint64_t *)sl.hd, (const uint16_t *)(sl.hd + 8 * mb),
                                 (const uint32_t *)(sl.hd + 10 * mb), nullptr, n,
                                 (stage::stage_probe_out_dev *)(sl.hd + 14 * mb), sl.hd + 46 * mb, sl.s, t->tune);
+    if (!e)
+        e = stage::launch_ident(view, (const stage::stage_probe_out_dev *)(sl.hd + 14 * mb), n,
+                                (uint32_t *)(sl.hd + (46 + stride) * mb), sl.s);
     if (!e) e = hipEventRecord(sl.ev, sl.s);
     if (e) {  // fail the batch now; complete() only delivers
         for (auto &r : sl.reqs) *r.rc = stale ? STAGE_E_STATE : STAGE_E_HIP;
@@ -258,6 +263,7 @@ void stage_reader::complete(Slot &sl) {
     const uint64_t n = sl.reqs.size(), mb = max_batch;
     const stage_probe_out *out = (const stage_probe_out *)(sl.h + 14 * mb);
     const uint8_t *rows = sl.h + 46 * mb;
+    const stage_probe_ident *ident = (const stage_probe_ident *)(sl.h + (46 + stride) * mb);
     if (n && hipEventSynchronize(sl.ev) != hipSuccess) {
         for (auto &r : sl.reqs) *r.rc = STAGE_E_HIP;
     } else {
@@ -265,6 +271,7 @@ void stage_reader::complete(Slot &sl) {
             const Req &r = sl.reqs[i];
             if (r.out) *r.out = out[i];
             if (r.rec) std::memcpy(r.rec, rows + i * stride, row_bytes);
+            if (r.ident) *r.ident = ident[i];
             *r.rc = STAGE_OK;
         }
     }
@@ -374,7 +381,7 @@ int stage_reader_create(stage_table *t, uint32_t max_batch, uint32_t max_wait_us
         r->max_wait_us = max_wait_us;
         r->stride = facts(t).stride();
         r->row_bytes = 8 + facts(t).params().payload_size;
-        const uint64_t mb = max_batch, bytes = mb * (8 + 2 + 4 + 32 + r->stride);
+        const uint64_t mb = max_batch, bytes = mb * (8 + 2 + 4 + 32 + r->stride + 8);
         stage::hip_check(hipSetDevice(t->dev.device), "hipSetDevice");
         for (auto &sl : r->slot) {
             stage::hip_check(hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking), "reader stream");
@@ -393,7 +400,7 @@ int stage_reader_create(stage_table *t, uint32_t max_batch, uint32_t max_wait_us
 }
 
 static int resident_read(ResidentReader &R, uint64_t key, uint16_t key_size, uint32_t read_id, stage_probe_out *out,
-                         uint8_t *record) {
+                         uint8_t *record, stage_probe_ident *ident) {
     if (R.closing.load(std::memory_order_acquire) || R.dead.load(std::memory_order_acquire))
         return fail(STAGE_E_STATE, "resident reader has ended");
     const uint64_t q = R.tail.fetch_add(1, std::memory_order_acq_rel);
@@ -421,6 +428,7 @@ static int resident_read(ResidentReader &R, uint64_t key, uint16_t key_size, uin
                                                                   : "resident reader failed on the device");
     if (out) *out = R.out[slot];
     if (record) std::memcpy(record, R.rows + (uint64_t)slot * R.stride, R.row_bytes);
+    if (ident) *ident = R.ident[slot];
     R.freed[slot].store(q + 1, std::memory_order_release);
     R.n_reads.fetch_add(1, std::memory_order_relaxed);
     return STAGE_OK;
@@ -453,10 +461,10 @@ int stage_reader_create_resident(stage_table *t, uint32_t ring_slots, uint32_t w
         stage::hip_check(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, t->dev.device), "clock rate");
         R.life_ticks = (uint64_t)(khz > 0 ? khz : 100000) * life_us / 1000;
         const uint64_t S = ring_slots;
-        // requests | done | stop | out | rows (each array 64-B aligned)
+        // requests | done | stop | out | ident | rows (each array 64-B aligned)
         auto al = [](uint64_t x) { return (x + 63) & ~63ull; };
         const uint64_t o_done = al(sizeof(stage::ReaderReq) * S), o_stop = o_done + al(4 * S), o_out = o_stop + 64,
-                       o_rows = o_out + al(32 * S), bytes = o_rows + S * R.stride;
+                       o_ident = o_out + al(32 * S), o_rows = o_ident + al(8 * S), bytes = o_rows + S * R.stride;
         stage::hip_check(hipHostMalloc((void **)&R.h, bytes, hipHostMallocMapped | hipHostMallocCoherent |
                                                                  hipHostMallocPortable),
                          "resident ring");
@@ -467,6 +475,7 @@ int stage_reader_create_resident(stage_table *t, uint32_t ring_slots, uint32_t w
         R.stop = (uint32_t *)(R.h + o_stop);
         R.out = (stage_probe_out *)(R.h + o_out);
         R.rows = R.h + o_rows;
+        R.ident = (stage_probe_ident *)(R.h + o_ident);
         R.freed.reset(new std::atomic<uint64_t>[S]);
         for (uint64_t i = 0; i < S; ++i) R.freed[i].store(0);
         std::vector<uint64_t> pos(waves, 0);
@@ -477,7 +486,7 @@ int stage_reader_create_resident(stage_table *t, uint32_t ring_slots, uint32_t w
                                               "resident event");
         R.ring = stage::ReaderRing{(const stage::ReaderReq *)R.hd, (uint32_t *)(R.hd + o_done), (stage::stage_probe_out_dev *)(R.hd + o_out),
                                    R.hd + o_rows, (const uint32_t *)(R.hd + o_stop), R.dpos, ring_slots, waves,
-                                   R.life_ticks};
+                                   R.life_ticks, (uint32_t *)(R.hd + o_ident)};
         ResidentReader *raw = &R;
         R.keeper = std::thread([raw] { raw->run(); });
         *out = r.release();
@@ -509,16 +518,21 @@ static void resident_destroy(ResidentReader &R) {
 
 int stage_reader_read(stage_reader *r, uint64_t key, uint16_t key_size, uint32_t read_id, stage_probe_out *out,
                       uint8_t *record) {
+    return stage_reader_read_ident(r, key, key_size, read_id, out, record, nullptr);
+}
+
+int stage_reader_read_ident(stage_reader *r, uint64_t key, uint16_t key_size, uint32_t read_id, stage_probe_out *out,
+                            uint8_t *record, stage_probe_ident *ident) {
     if (!r) return fail(STAGE_E_ARG, "null reader");
     if (key_size == 0 || key_size > 8) return fail(STAGE_E_ARG, "key_size must be 1..8");
-    if (r->res) return resident_read(*r->res, key, key_size, read_id, out, record);
+    if (r->res) return resident_read(*r->res, key, key_size, read_id, out, record, ident);
     int rc = STAGE_E_STATE;
     uint32_t seq;
     {
         std::unique_lock<std::mutex> lk(r->mu);
         r->cv_space.wait(lk, [&] { return r->stop || r->open.size() < r->max_batch; });
         if (r->stop) return fail(STAGE_E_STATE, "reader is closing");
-        r->open.push_back({key, key_size, read_id, out, record, &rc});
+        r->open.push_back({key, key_size, read_id, out, record, ident, &rc});
         const int64_t now = now_ns();
         if (r->open.size() == 1) r->first_arrival_ns.store(now, std::memory_order_release);
         r->last_arrival_ns.store(now, std::memory_order_release);

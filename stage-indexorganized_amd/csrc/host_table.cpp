@@ -190,8 +190,9 @@ void HostTable::image_payload(uint32_t img, uint8_t *dst) const {
     else throw std::logic_error("device-written heap row read before materialize_device_rows");
 }
 
-void HostTable::adopt_device_epoch(const CopyHdr *copies, uint64_t nc, const VersionHdr *versions, uint64_t nv,
-                                   uint64_t nimages, const SlotWords *slots, uint64_t nslots) {
+void HostTable::adopt_device_epoch(const CopyHdr *copies, const uint32_t *writers, uint64_t nc,
+                                   const VersionHdr *versions, uint64_t nv, uint64_t nimages, const SlotWords *slots,
+                                   uint64_t nslots) {
     if (copies_.size() + nc > kNextIndexMask || versions_.size() + nv > kNextIndexMask ||
         images_.size() + nimages > kNextIndexMask)
         throw std::runtime_error("copy / version / image index overflow");
@@ -210,9 +211,19 @@ void HostTable::adopt_device_epoch(const CopyHdr *copies, uint64_t nc, const Ver
     room(copies_, nc);
     room(copy_live_, nc);
     room(versions_, nv);
+    const uint64_t c0 = copies_.size();
     copies_.insert(copies_.end(), copies, copies + nc);
     copy_live_.resize(copies_.size(), 1);
     versions_.insert(versions_.end(), versions, versions + nv);
+    {
+        std::lock_guard<std::mutex> g(ssn_.mu);
+        ssn_.e.reserve(c0 + nc);
+        for (uint64_t k = 0; k < nc; ++k) {
+            const uint32_t w = writers ? writers[k] : 0;
+            ssn_.e.push_back(CopySsn{w, w, copies[k].rstamp, copies[k].sstamp, 0,
+                                     (uint8_t)(copies[k].sstamp != kMaxCid), 0});
+        }
+    }
     lap("headers");
     if (nimages) {
         device_rows_.emplace_back(images_.size(), nimages);
@@ -232,6 +243,7 @@ void HostTable::adopt_device_epoch(const CopyHdr *copies, uint64_t nc, const Ver
             meta_[w.idx] = w.meta;
             next_[w.idx] = w.next;
             image_[w.idx] = w.image;
+            cell(w.idx);
         }
     });
     lap("slots");
@@ -239,6 +251,52 @@ void HostTable::adopt_device_epoch(const CopyHdr *copies, uint64_t nc, const Ver
     copies_synced_ = copies_.size();
     versions_synced_ = versions_.size();
     images_synced_ = images_.size();
+}
+
+LocCells::~LocCells() {
+    for (auto &d : dir_) delete[] d.load();
+}
+
+void LocCells::ensure(uint64_t handle) {
+    const uint64_t k = handle >> kChunkBits;
+    if (k >= kDir) throw std::runtime_error("location cell directory exhausted");
+    if (dir_[k].load(std::memory_order_acquire)) return;
+    Cell *c = new Cell[1u << kChunkBits];
+    for (uint32_t i = 0; i < (1u << kChunkBits); ++i) {
+        c[i].meta.store(0, std::memory_order_relaxed);
+        c[i].next.store(0, std::memory_order_relaxed);
+        c[i].loc.store(((uint64_t)k << kChunkBits) + i, std::memory_order_relaxed);
+    }
+    Cell *expect = nullptr;
+    if (!dir_[k].compare_exchange_strong(expect, c, std::memory_order_acq_rel)) delete[] c;  // another thread won
+}
+
+void CopySsnTable::created(uint64_t id, uint32_t writer, uint32_t rstamp) {
+    std::lock_guard<std::mutex> g(mu);
+    if (e.size() <= id) e.resize(id + 1, CopySsn{0, 0, 0, kMaxCid, 0, 0, 0});
+    e[id] = CopySsn{writer, writer, rstamp, kMaxCid, 0, 0, 0};
+}
+
+void CopySsnTable::committed(uint64_t id, uint32_t sstamp) {
+    std::lock_guard<std::mutex> g(mu);
+    if (id < e.size()) e[id].sstamp = sstamp, e[id].waiting = 1;
+}
+
+void CopySsnTable::aborted(uint64_t id) {
+    std::lock_guard<std::mutex> g(mu);
+    if (id < e.size()) e[id].sstamp = kMaxCid, e[id].waiting = 1;
+}
+
+// builds every cell from the current layout; afterwards each write keeps them current
+void HostTable::enable_cells() {
+    if (cells_.on()) return;
+    if (!locpos_.empty()) cells_.ensure(locpos_.size());
+    for (uint64_t h = 1; h <= locpos_.size(); h += 1u << LocCells::kChunkBits) cells_.ensure(h);
+    cells_.enable();
+    for (uint32_t l = 0; l < leaves_.size(); ++l) {
+        if (!leaves_[l].live) continue;
+        for (uint32_t s = 0; s < leaves_[l].count; ++s) cell((size_t)l * cap_ + s);
+    }
 }
 
 void HostTable::parallel_chunks(uint64_t n, const std::function<void(uint64_t, uint64_t)> &fn) {
@@ -312,6 +370,10 @@ int HostTable::insert(const uint8_t *key, uint32_t len, const uint8_t *payload, 
         image_[i] = new_image(key, len, payload, gen_rowid, mode);
         loc_[i] = (uint32_t)(lid + 1);
         locpos_[lid] = (uint64_t)leaf << 16 | slot;
+        if (cells_.on()) {
+            cells_.ensure(lid + 1);
+            cell(i);
+        }
         touch(leaf, slot);
         return STAGE_RC_OK;
     }
@@ -339,7 +401,10 @@ bool HostTable::split(uint32_t p) {
     if (total == 0) return false;
     for (uint32_t s = 0; s < leaves_[p].count; ++s) {  // CopyFrom drops these: their locations dangle
         const uint64_t m = meta_[pb + s];
-        if (!(m != 0 && meta_visible(m) && meta_keylen(m) > 0) && loc_[pb + s]) locpos_[loc_[pb + s] - 1] = kNoPos;
+        if (!(m != 0 && meta_visible(m) && meta_keylen(m) > 0) && loc_[pb + s]) {
+            locpos_[loc_[pb + s] - 1] = kNoPos;
+            cell_drop(loc_[pb + s]);
+        }
     }
     std::sort(v.begin(), v.end(), [](const Rec &a, const Rec &b) { return key_lt(a.key, b.key); });
     int32_t left_size = (int32_t)(total / 2);
@@ -367,6 +432,7 @@ bool HostTable::split(uint32_t p) {
             image_[b + n] = v[i].image;
             loc_[b + n] = v[i].loc;
             if (v[i].loc) locpos_[v[i].loc - 1] = (uint64_t)leaf << 16 | n;  // loc->record_meta_ptr
+            cell(b + n);
             ++n;
         }
         for (uint32_t s = n; s < cap_; ++s) {
@@ -486,8 +552,10 @@ int HostTable::update(const uint8_t *key, uint32_t len, uint32_t payload_off, co
     copy_live_.push_back(1);
     if (copies_.size() > kNextIndexMask) throw std::runtime_error("copy index overflow");
     next_[i] = kNextCopy | (uint32_t)(copies_.size() - 1);
+    ssn_.created(copies_.size() - 1, writer_id, c.rstamp);
     std::memcpy(pay.data() + payload_off, delta, delta_len);  // CopyPayload
     image_[i] = new_image(key, len, pay.data(), 0, 0);
+    cell(i);
     touch(leaf, slot);
     return STAGE_RC_OK;
 }
@@ -512,6 +580,8 @@ int HostTable::commit_update(const uint8_t *key, uint32_t len, uint32_t commit_i
     uint64_t m = (meta_[i] & ~kMetaTxn) | commit_id;  // FinalizeForUpdate(t_cstamp)
     meta_[i] = m & ~kMetaControl;
     next_[i] = kNextVersion | (uint32_t)(versions_.size() - 1);
+    ssn_.committed(ci, sstamp);
+    cell(i);
     touch(leaf, slot);
     return STAGE_RC_OK;
 }
@@ -529,6 +599,8 @@ int HostTable::abort_update(const uint8_t *key, uint32_t len) {
     next_[i] = copies_[ci].next;
     meta_[i] = (meta_[i] & ~kMetaControl) | kMetaVisible;
     copy_live_[ci] = 0;
+    ssn_.aborted(ci);
+    cell(i);
     touch(leaf, slot);
     return STAGE_RC_OK;
 }
@@ -548,6 +620,7 @@ int HostTable::abort_insert(const uint8_t *key, uint32_t len) {
     next_[i] = 0;
     image_[i] = 0;
     if (loc_[i]) locpos_[loc_[i] - 1] = kNoPos;
+    cell_drop(loc_[i]);
     loc_[i] = 0;
     clear_slot_key(i);
     touch(leaf, slot);
@@ -562,6 +635,7 @@ int HostTable::commit_insert(const uint8_t *key, uint32_t len, uint32_t commit_i
     const size_t i = (size_t)leaf * cap_ + slot;
     if (!meta_inserting(meta_[i]) || next_[i] != 0) return STAGE_RC_NOT_FOUND;
     meta_[i] = ((meta_[i] & ~kMetaTxn) | commit_id | kMetaVisible) & ~kMetaControl;
+    cell(i);
     touch(leaf, slot);
     return STAGE_RC_OK;
 }
@@ -572,6 +646,7 @@ int HostTable::finalize_update(const uint8_t *key, uint32_t len, uint32_t commit
     if (find(key, len, &leaf, &slot) < 0) return STAGE_RC_NOT_FOUND;
     const size_t i = (size_t)leaf * cap_ + slot;
     meta_[i] = ((meta_[i] & ~kMetaTxn) | commit_id) & ~kMetaControl;
+    cell(i);
     touch(leaf, slot);
     return STAGE_RC_OK;
 }
@@ -592,7 +667,9 @@ int HostTable::remove(const uint8_t *key, uint32_t len, uint32_t commit_id) {
     copies_.push_back(c);
     copy_live_.push_back(1);
     next_[i] = kNextCopy | (uint32_t)(copies_.size() - 1);
+    ssn_.created(copies_.size() - 1, commit_id, c.rstamp);
     meta_[i] = 0;
+    cell(i);
     Leaf &L = leaves_[leaf];
     L.deleted += pad8(meta_keylen(m)) + p_.payload_size;
     touch(leaf, slot);
@@ -613,6 +690,7 @@ constexpr uint32_t kLocalRef = 1u << 29;   // local copy / version index inside 
 constexpr uint32_t kLocalImg = 1u << 31;   // local image index
 struct LocalWrites {
     std::vector<CopyHdr> copies;
+    std::vector<uint32_t> writers;  // writer id per copy
     std::vector<VersionHdr> versions;
     std::vector<ImageDesc> images;
     std::vector<uint8_t> arena;
@@ -729,6 +807,7 @@ uint64_t HostTable::update_batch(const uint8_t *keys, uint32_t key_stride, uint6
                 }
                 meta_[i] = mw | kMetaControl | kMetaVisible;
                 L.copies.push_back(CopyHdr{meta_cstamp(mw), kMaxCid, next_[i], image_[i]});
+                L.writers.push_back(writer_ids[op]);
                 next_[i] = kNextCopy | kLocalRef | (uint32_t)(L.copies.size() - 1);
                 std::memcpy(pay.data() + payload_off, delta, delta_len);
                 ImageDesc d;
@@ -817,8 +896,21 @@ uint64_t HostTable::update_batch(const uint8_t *keys, uint32_t key_stride, uint6
         }
     });
     lap("concat");
+    {
+        std::lock_guard<std::mutex> g(ssn_.mu);
+        ssn_.e.reserve(c0);
+        for (unsigned t = 0; t < nt; ++t)
+            for (size_t k = 0; k < lw[t].copies.size(); ++k) {
+                const CopyHdr &c = lw[t].copies[k];
+                ssn_.e.push_back(CopySsn{lw[t].writers[k], lw[t].writers[k], c.rstamp, c.sstamp, 0,
+                                         (uint8_t)(c.sstamp != kMaxCid), 0});
+            }
+    }
     for (unsigned t = 0; t < nt; ++t) {
-        for (uint64_t i : lw[t].touched) touch((uint32_t)(i / cap_), (uint32_t)(i % cap_));
+        for (uint64_t i : lw[t].touched) {
+            touch((uint32_t)(i / cap_), (uint32_t)(i % cap_));
+            cell(i);
+        }
         copies_dirty_from_ = std::min(copies_dirty_from_, lw[t].copies_dirty_from);
     }
     if (rc_out) std::memcpy(rc_out, rc.data(), n);
@@ -1069,6 +1161,13 @@ uint64_t HostTable::import_leaf_images(const uint8_t *blocks, uint64_t n, uint32
         const uint32_t b_lo = i == 0 ? 0 : bucket_of(sep[i - 1]);
         const uint32_t b_hi = key_is_inf(sep[i]) ? (uint32_t)buckets_.size() - 1 : bucket_of(sep[i]);
         for (uint32_t bk = b_lo; bk <= b_hi; ++bk) buckets_[bk].push_back(RouteEntry{sep[i], id});
+    }
+    if (cells_.on()) {  // rebuild every cell from the imported layout
+        for (uint64_t h = 1; h <= locpos_.size(); h += 1u << LocCells::kChunkBits) cells_.ensure(h);
+        if (!locpos_.empty()) cells_.ensure(locpos_.size());
+        for (uint32_t l = 0; l < leaves_.size(); ++l)
+            if (leaves_[l].live)
+                for (uint32_t s = 0; s < leaves_[l].count; ++s) cell((size_t)l * cap_ + s);
     }
     layout_dirty_ = true;
     structure_dirty_ = true;

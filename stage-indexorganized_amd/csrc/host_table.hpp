@@ -12,9 +12,13 @@
 // order words (stage_core.hpp order_key per 8-byte chunk) plus its length; the unsigned order
 // of (words, len) is the reference's KeyCompare order.
 #pragma once
+#include <atomic>
 #include <cstdint>
 #include <functional>
+#include <memory>
+#include <mutex>
 #include <string>
+#include <unordered_map>
 #include <utility>
 #include <vector>
 
@@ -62,6 +66,68 @@ struct ImageDesc {
                       // 3 = written by the device write path, bytes only in the device heap until
                       //     materialize_device_rows() pulls them into the arena
     uint32_t mode;    // payload generator mode (generated images)
+};
+
+// The RecordMetadata each RecordLocation points at (record_location.h:13-42: record_meta_ptr),
+// kept current by the host write path: 24-B cells {meta, next_ptr, loc_ptr} in the reference's
+// RecordMetadata layout (record_meta.h:30-60) at stable addresses, so a transaction manager can
+// dereference a location at commit without a call or a lock (tm.cpp:37, 123, 605), as the
+// reference reads the live slot.  next_ptr = the slot's next handle (stage_hip.h STAGE_NEXT_*),
+// loc_ptr = the handle; a dropped location reads meta 0.  Cells live in 2^20-entry chunks
+// behind a fixed directory: chunks are allocated by the writer before any handle in them is
+// published, readers only load.
+class LocCells {
+public:
+    static constexpr uint32_t kChunkBits = 20, kDir = 4096;  // 2^32 handles
+    struct Cell {
+        std::atomic<uint64_t> meta, next, loc;
+    };
+    static_assert(sizeof(Cell) == 24, "a cell is a RecordMetadata");
+    bool on() const { return on_; }
+    void enable() { on_ = true; }
+    void ensure(uint64_t handle);  // the chunk holding `handle` exists (writer)
+    void set(uint64_t handle, uint64_t meta, uint32_t next) {
+        Cell &c = at(handle);
+        c.next.store(next, std::memory_order_relaxed);
+        c.loc.store(handle, std::memory_order_relaxed);
+        c.meta.store(meta, std::memory_order_release);
+    }
+    const Cell *find(uint64_t handle) const {
+        if (handle == 0 || (handle >> kChunkBits) >= kDir) return nullptr;
+        const Cell *c = dir_[handle >> kChunkBits].load(std::memory_order_acquire);
+        return c ? c + (handle & ((1u << kChunkBits) - 1)) : nullptr;
+    }
+    ~LocCells();
+
+private:
+    Cell &at(uint64_t handle) { return dir_[handle >> kChunkBits].load(std::memory_order_relaxed)[handle & ((1u << kChunkBits) - 1)]; }
+    bool on_ = false;
+    std::atomic<Cell *> dir_[kDir] = {};
+};
+
+// The transaction side of an overwrite copy: EphemeralPool::OverwriteVersionHeader's cstamp
+// (writer id), pstamp, rstamp, sstamp, readers, dependency count and waiting flag
+// (ephemeral_pool.h:26-150).  The device keeps {rstamp, sstamp, next, image} per copy for reads
+// (CopyHdr); this is what the kept SSNTransactionManager reads and updates (AddReader,
+// b_tree.cpp:2105; IncreaseWRCount / DecreaseWRCount / UpdatePs, ephemeral_pool.cpp:69-205).
+// The pool never frees a header (no GC, as the reference with its cleaner off): an aborted
+// update's header stays, waiting.  Reader threads and the writer reach it concurrently: one mutex.
+struct CopySsn {
+    uint32_t cstamp, pstamp, rstamp, sstamp;
+    uint16_t count;
+    uint8_t waiting, pad;
+};
+class CopySsnTable {
+public:
+    std::mutex mu;
+    std::vector<CopySsn> e;                                      // by copy id
+    std::unordered_map<uint32_t, std::vector<uint32_t>> readers;  // copy id -> AddReader ids
+    // EphemeralPool::Allocate (ephemeral_pool.cpp:17-44): cstamp = pstamp = writer, sstamp MAX
+    void created(uint64_t id, uint32_t writer, uint32_t rstamp);
+    // CommitTransaction UPDATE entry: SetSstamp(t_sstamp), SetWaiting(true) (tm.cpp:618-619)
+    void committed(uint64_t id, uint32_t sstamp);
+    // AbortTransaction UPDATE entry: UpdateSs(MAX_CID), SetWaiting(true) (tm.cpp:872-875)
+    void aborted(uint64_t id);
 };
 
 class HostTable {
@@ -165,6 +231,12 @@ public:
     uint64_t export_locations(uint64_t max, uint64_t *handles, uint32_t *leaf, uint16_t *slot) const;
     void resolve_locations(const uint64_t *handles, uint64_t n, uint32_t *leaf, uint16_t *slot) const;
 
+    // location cells (stage_location_cell): off until enable_cells(); then every write keeps them
+    LocCells cells_;
+    void enable_cells();
+    // the transaction side of the overwrite copies (stage_copy_*)
+    CopySsnTable ssn_;
+
     ChunkedVector<ImageDesc, (1u << 20)> images_;
     ChunkedArena arena_;
     std::vector<CopyHdr, HugeAlloc<CopyHdr>> copies_;
@@ -193,8 +265,9 @@ public:
         uint32_t next, image;
     };
     // slots with idx == ~0 are skipped
-    void adopt_device_epoch(const CopyHdr *copies, uint64_t nc, const VersionHdr *versions, uint64_t nv,
-                            uint64_t nimages, const SlotWords *slots, uint64_t nslots);
+    // writers[k] = the writer id of copy k (its OverwriteVersionHeader cstamp)
+    void adopt_device_epoch(const CopyHdr *copies, const uint32_t *writers, uint64_t nc, const VersionHdr *versions,
+                            uint64_t nv, uint64_t nimages, const SlotWords *slots, uint64_t nslots);
     // fn(begin, end) over [0, n) on up to 16 threads (one below 65536 items)
     static void parallel_chunks(uint64_t n, const std::function<void(uint64_t, uint64_t)> &fn);
     bool has_device_rows() const { return !device_rows_.empty(); }
@@ -212,6 +285,13 @@ private:
     static bool entry_lt_key(const RouteEntry &e, const Key &k) { return key_lt(e.sep, k); }
     static const uint8_t *le(const uint64_t &key_le) { return reinterpret_cast<const uint8_t *>(&key_le); }
 
+    // slot i's words changed: its location's cell follows
+    void cell(size_t i) {
+        if (cells_.on() && loc_[i]) cells_.set(loc_[i], meta_[i], next_[i]);
+    }
+    void cell_drop(uint32_t handle) {
+        if (cells_.on() && handle) cells_.set(handle, 0, 0);
+    }
     void touch(uint32_t leaf, uint32_t slot) {
         layout_dirty_ = true;
         if (!structure_dirty_) dirty_slots_.push_back((uint64_t)leaf * cap_ + slot);

@@ -80,8 +80,11 @@ struct ReaderRing {
     uint32_t slots;            // multiple of 64 * waves
     uint32_t waves;
     uint64_t life_ticks;       // lifetime of one instance in real-time counter ticks
+    uint32_t *ident;           // [slots * 2] {location handle, next handle} of each read (stage_probe_ident)
 };
 hipError_t launch_resident_reader(const DevTable &t, const ReaderRing &g, hipStream_t s);
+// stage_probe_ident: {location handle, next handle} of each probe's hit slot (two u32 per probe)
+hipError_t launch_ident(const DevTable &t, const stage_probe_out_dev *out, uint64_t n, uint32_t *ident, hipStream_t s);
 hipError_t launch_murmur(const void *keys, uint32_t key_len, uint32_t key_stride, uint64_t seed, uint64_t n,
                          uint64_t *out, hipStream_t s);
 hipError_t launch_fill(uint8_t *heap, uint32_t stride, uint32_t payload_size, uint32_t row_bytes,

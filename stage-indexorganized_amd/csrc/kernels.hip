@@ -582,7 +582,7 @@ __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *
 template <bool VARLEN, int SPL>
 __device__ __forceinline__ void ring_probe_one(const DevTable &t, uint32_t lane, int j, uint32_t leaf_l, uint64_t ok_l,
                                                uint32_t len_l, uint32_t rid_l, uint8_t *row, uint32_t out_chunks,
-                                               u32x4 &a, u32x4 &b) {
+                                               u32x4 &a, u32x4 &b, uint32_t &id_loc, uint32_t &id_next) {
     const uint32_t lf = rl32(leaf_l, j);
     const uint64_t x = rl64(ok_l, j);
     const uint32_t xl = VARLEN ? rl32(len_l, j) : t.key_width;
@@ -591,12 +591,12 @@ __device__ __forceinline__ void ring_probe_one(const DevTable &t, uint32_t lane,
     const uint32_t fx = key_fp_words(&x, 1);
     int slot = -1;
     uint64_t m = 0;
-    uint32_t nx = 0, im = 0;
+    uint32_t nx = 0, im = 0, lc = 0;
 #pragma unroll
     for (int s = SPL - 1; s >= 0; --s) {  // first hit in slot order (SearchRecordMeta)
         const bool cand = h[s * 64 + lane] == fx;
         uint64_t wok = 0, wmeta = 0;
-        uint32_t wnext = 0, wimg = 0;
+        uint32_t wnext = 0, wimg = 0, wloc = 0;
         if (cand) {
             const u32x4 *w = reinterpret_cast<const u32x4 *>(t.slot + (uint64_t)lf * t.cap + s * 64 + lane);
             const u32x4 w0 = w[0], w1 = w[1];
@@ -604,6 +604,7 @@ __device__ __forceinline__ void ring_probe_one(const DevTable &t, uint32_t lane,
             wmeta = ((uint64_t)w0.w << 32) | w0.z;
             wnext = w1.x;
             wimg = w1.y;
+            wloc = w1.z;
         }
         const uint64_t hit = ballot(cand && wok == x && (!VARLEN || meta_keylen(wmeta) == xl));
         if (hit) {
@@ -612,10 +613,13 @@ __device__ __forceinline__ void ring_probe_one(const DevTable &t, uint32_t lane,
             m = rl64(wmeta, bl);
             nx = rl32(wnext, bl);
             im = rl32(wimg, bl);
+            lc = rl32(wloc, bl);
         }
     }
     ProbeRes r;
     visibility(t, slot, m, nx, im, rd, r);
+    id_loc = r.status == ST_NOT_FOUND ? 0u : lc;
+    id_next = r.status == ST_NOT_FOUND ? 0u : nx;
     for (uint32_t c0 = 0; c0 < out_chunks; c0 += 64) {
         const uint32_t c = c0 + lane;
         if (c < out_chunks) {
@@ -659,19 +663,25 @@ __global__ __launch_bounds__(64) void resident_reader_kernel(DevTable t, ReaderR
         const uint64_t ok = order_key(mine ? ((uint64_t)rq.y << 32 | rq.x) : 0ull, len);
         uint32_t leaf = mine ? resolve_leaf<VARLEN, 1>(t, &ok, len, true) : 0u;
         u32x4 my_a = u32x4{0, 0, 0, 0}, my_b = u32x4{0, 0, 0, 0};
+        uint32_t my_loc = 0, my_next = 0;
         for (uint32_t j = d; j < d + k; ++j) {
             u32x4 a, b;
+            uint32_t il, in;
             ring_probe_one<VARLEN, SPL>(t, lane, (int)j, leaf, ok, len, rid, g.rows + (uint64_t)(s0 + j) * t.stride,
-                                        out_chunks, a, b);
+                                        out_chunks, a, b, il, in);
             if (lane == j) {
                 my_a = a;
                 my_b = b;
+                my_loc = il;
+                my_next = in;
             }
         }
         if (mine) {
             u32x4 *o = reinterpret_cast<u32x4 *>(g.out + s0 + lane);
             o[0] = my_a;
             o[1] = my_b;
+            g.ident[2 * (uint64_t)(s0 + lane)] = my_loc;
+            g.ident[2 * (uint64_t)(s0 + lane) + 1] = my_next;
             // status record and row before the flag, system-wide
             __hip_atomic_store(g.done + s0 + lane, want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
@@ -2664,6 +2674,29 @@ hipError_t launch_probe_fanout(const DevTable &t, const uint64_t *keys, const ui
 
 bool probe_fanout_supported(const DevTable &t) {
     return t.key_width != 0 && t.key_words == 1 && t.cap == 64 && t.stride <= 1024;
+}
+
+// stage_probe_ident: a probe's hit slot (leaf, slot in its status record) -> the slot word's
+// location handle and next handle, from the same published image.  A thread per probe.
+__global__ __launch_bounds__(256) void ident_kernel(DevTable t, const stage_probe_out_dev *__restrict__ out, uint64_t n,
+                                                    uint32_t *__restrict__ ident) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const u32x4 a = reinterpret_cast<const u32x4 *>(out + i)[0];
+    const uint32_t status = a.x & 0xFF, leaf = a.y, slot = a.z & 0xFFFF;
+    uint32_t loc = 0, next = 0;
+    if (status != ST_NOT_FOUND && slot < t.cap && leaf < t.nleaves) {
+        const u32x4 w1 = reinterpret_cast<const u32x4 *>(t.slot + (uint64_t)leaf * t.cap + slot)[1];
+        next = w1.x;
+        loc = w1.z;
+    }
+    reinterpret_cast<uint2 *>(ident)[i] = make_uint2(loc, next);
+}
+
+hipError_t launch_ident(const DevTable &t, const stage_probe_out_dev *out, uint64_t n, uint32_t *ident, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    ident_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(t, out, n, ident);
+    return hipGetLastError();
 }
 
 hipError_t launch_resident_reader(const DevTable &t, const ReaderRing &g, hipStream_t s) {

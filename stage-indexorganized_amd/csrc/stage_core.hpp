@@ -5,7 +5,8 @@
 //                   visible-slot masks -- the only per-leaf bytes a point probe reads
 //   okey[L*KW*cap]  u64  order key columns, one plane of cap words per key word (range scans
 //                   read them whole, 512 B/leaf for keys of <= 8 bytes)
-//   slot[L*cap]     32 B {okey word 0, meta word, next handle, image id} (probe: candidates)
+//   slot[L*cap]     32 B {okey word 0, meta word, next handle, image id, location handle}
+//                   (probe: candidates)
 //   tree            u64  implicit 16-ary separator tree (KW words per entry), all levels
 //   heap[I*hstride] u8   record images [key padded to 8][payload] (current, copies,
 //                   versions); rows 128-B aligned when larger than 128 B
@@ -99,7 +100,8 @@ struct alignas(32) SlotInfo {
     uint64_t meta;  // reference RecordMetadata.meta
     uint32_t next;  // tagged next handle
     uint32_t image; // record-heap row of the current image
-    uint64_t pad;
+    uint32_t loc;   // RecordLocation handle of the record (host loc_; read only by stage_probe_ident)
+    uint32_t pad;
 };
 
 // leaf head: [fp: cap bytes, 0 = empty or invisible slot][visible masks: cap/8 bytes][group max keys: cap/64 x KW words],

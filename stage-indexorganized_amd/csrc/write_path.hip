@@ -428,7 +428,8 @@ struct WRec {
 // marked (last_succ; one atomic per group per wave)
 __global__ void wp_headers(WpArgs a, DevTable t, const uint8_t *__restrict__ succ, const int32_t *__restrict__ prev,
                            const uint64_t *__restrict__ ranks, CopyHdr *__restrict__ chdr, VersionHdr *__restrict__ vhdr,
-                           uint32_t *__restrict__ last_succ, WRec *__restrict__ wrec, const uint64_t *__restrict__ tot) {
+                           uint32_t *__restrict__ last_succ, WRec *__restrict__ wrec, const uint64_t *__restrict__ tot,
+                           uint32_t *__restrict__ cwriter) {
     const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // blockDim: a multiple of 64
     if (q >= a.n) return;
     const uint64_t cbase = tot[2], vbase = tot[3], ibase = tot[4];
@@ -457,6 +458,7 @@ __global__ void wp_headers(WpArgs a, DevTable t, const uint8_t *__restrict__ suc
         chdr[cbase + irank] = c;
         if (cid) vhdr[vbase + vrank] = VersionHdr{c.rstamp, c.sstamp, c.next, c.image};
         wrec[irank] = WRec{base.image, o};
+        cwriter[irank] = a.writer[o];  // the copy's OverwriteVersionHeader cstamp (the host's SSN state)
     }
     // the group's last success in this wave (no later lane of the group -- the lanes up to the
     // next group head -- succeeded) competes for last_succ
@@ -559,7 +561,8 @@ __global__ void wp_publish(WpArgs a, SlotInfo *__restrict__ slot, const uint8_t 
 // copy and version headers, the slot words -- the staging layout of stage_update_batch_device
 __global__ __launch_bounds__(256) void wp_export(const uint64_t *__restrict__ tot, const FinRec *__restrict__ fin,
                                                  const CopyHdr *__restrict__ chdr, const VersionHdr *__restrict__ vhdr,
-                                                 uint8_t *__restrict__ pin, uint64_t fin_off) {
+                                                 const uint32_t *__restrict__ cwriter, uint8_t *__restrict__ pin,
+                                                 uint64_t fin_off, uint64_t wr_off) {
     const uint64_t ns = tot[0], nv = tot[1];
     const uint64_t *c = reinterpret_cast<const uint64_t *>(chdr + tot[2]);
     const uint64_t *v = reinterpret_cast<const uint64_t *>(vhdr + tot[3]);
@@ -574,6 +577,8 @@ __global__ __launch_bounds__(256) void wp_export(const uint64_t *__restrict__ to
         else if (i < w2) ov[i - w1] = v[i - w1];
         else of[i - w2] = f[i - w2];
     }
+    uint32_t *ow = reinterpret_cast<uint32_t *>(pin + wr_off);
+    for (uint64_t i = gid; i < ns; i += stride) ow[i] = cwriter[i];
     if (gid < 5) reinterpret_cast<uint64_t *>(pin)[gid] = tot[gid];
 }
 
@@ -744,21 +749,23 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         // slot words + totals: read back after this call returns (background adoption)
         // both parities are sized together when no adoption is reading the other one: a first
         // use inside a run of epochs would allocate (and drain the device) in the middle of it
-        const uint64_t wo_bytes = al(n * sizeof(FinRec)) + 256;
+        const uint64_t wo_bytes = al(n * sizeof(FinRec)) + 256 + al(n * 4);
         uint8_t *wo = wp_out_bytes(dv, wo_bytes, par);
         if (!pending) wp_out_bytes(dv, wo_bytes, par ^ 1);
         auto *fin = (FinRec *)wo;
         auto *tot = (uint64_t *)(wo + al(n * sizeof(FinRec)));
+        auto *cwriter = (uint32_t *)(wo + al(n * sizeof(FinRec)) + 256);  // writer id per new copy
         void *cub = buf + o_cub;
         size_t cb = cub_bytes;
         // pinned staging of the adoption: [totals 64 B][copy headers][version headers][slot
         // words], sized for the worst case (one copy and one version per op); every part starts
         // on a 16-B boundary (the headers are 16-B aligned types: a misaligned source faults in
         // the vectorised copy)
-        const uint64_t bf = n * sizeof(FinRec), bmax = 2 * n * sizeof(CopyHdr);
+        // [.. slot words][writer id per copy]
+        const uint64_t bf = n * sizeof(FinRec), bmax = 2 * n * sizeof(CopyHdr), bw = n * 4;
         static_assert(sizeof(CopyHdr) == sizeof(VersionHdr) && sizeof(CopyHdr) % 16 == 0, "header sizes");
-        uint8_t *pin = pinned_bytes(dv, 64 + bmax + bf, par);
-        if (!pending) pinned_bytes(dv, 64 + bmax + bf, par ^ 1);
+        uint8_t *pin = pinned_bytes(dv, 64 + bmax + bf + bw, par);
+        if (!pending) pinned_bytes(dv, 64 + bmax + bf + bw, par ^ 1);
         // write-overlap mode: the kernels up to the publish go on the table's write stream ks,
         // which waits for the previous epoch's publish only (or, when the device image changed
         // otherwise since, for all of s) -- not for the caller's work enqueued after it, such as
@@ -814,7 +821,7 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         hip_check(hipcub::DeviceScan::ExclusiveSum(cub, cb, flags, ranks, (int)n, ks), "ranks");
         wp_totals<<<1, 1, 0, ks>>>(ranks, flags, n, tot, (uint64_t *)dv.wp_bases.p);
         wp_headers<<<blocks_for(n, 256), 256, 0, ks>>>(a, view, succ, prev, ranks, (CopyHdr *)dv.chdr.p,
-                                                      (VersionHdr *)dv.vhdr.p, ls, wrec, tot);
+                                                      (VersionHdr *)dv.vhdr.p, ls, wrec, tot, cwriter);
         // 5. write, 6. publish
         const int wblocks = (int)std::min<uint64_t>(blocks_for(n, 256 / kRowTeam), 32768);
         wp_write<<<wblocks, 256, 0, ks>>>(a, view, (uint8_t *)dv.heap.p, wrec, tot);
@@ -838,13 +845,14 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         hip_check(hipEventRecord(dv.adopt_ev[par], s), "adopt event");
         auto *totals = reinterpret_cast<uint64_t *>(pin);
         auto *fr = reinterpret_cast<FinRec *>(pin + 64 + bmax);
+        auto *writers = reinterpret_cast<const uint32_t *>(pin + 64 + bmax + bf);
         const double t_pinned = ms(t0);
         void *pin_dev = nullptr;
         hip_check(hipHostGetDevicePointer(&pin_dev, pin, 0), "pinned device pointer");
         hip_check(hipStreamWaitEvent(dv.adopt_stream, dv.adopt_ev[par], 0), "export wait");
         static const int export_blocks = std::getenv("STAGE_WP_EXPORT_BLOCKS") ? std::atoi(std::getenv("STAGE_WP_EXPORT_BLOCKS")) : 32;
         wp_export<<<export_blocks, 256, 0, dv.adopt_stream>>>(tot, fin, (const CopyHdr *)dv.chdr.p, (const VersionHdr *)dv.vhdr.p,
-                                                    (uint8_t *)pin_dev, 64 + bmax);
+                                                    cwriter, (uint8_t *)pin_dev, 64 + bmax, 64 + bmax + bf);
         hip_check(hipGetLastError(), "export");
         hip_check(hipEventRecord(dv.export_ev[par], dv.adopt_stream), "export event");
         uint64_t ns = 0;
@@ -862,7 +870,7 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
                           offsetof(FinRec, next) == offsetof(HostTable::SlotWords, next) &&
                           offsetof(FinRec, image) == offsetof(HostTable::SlotWords, image),
                       "FinRec / SlotWords layout");
-        t->start_adoption(epoch, [t, &h, &dv, par, epoch, cap = view.cap, n, pin, totals, fr, t0, t_kernels, t_enqueue,
+        t->start_adoption(epoch, [t, &h, &dv, par, epoch, cap = view.cap, n, pin, totals, fr, writers, t0, t_kernels, t_enqueue,
                            t_reserve, t_events, t_pinned]() {
             const double t_join = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
             hip_check(hipSetDevice(dv.device), "hipSetDevice");
@@ -891,7 +899,7 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
             if (bad.load())
                 throw std::runtime_error("write path: " + std::to_string(bad.load()) +
                                          " slot words outside the table (ns " + std::to_string(ns) + ")");
-            h.adopt_device_epoch(copies, ns, versions, nv, ns, reinterpret_cast<const HostTable::SlotWords *>(fr), ns);
+            h.adopt_device_epoch(copies, writers, ns, versions, nv, ns, reinterpret_cast<const HostTable::SlotWords *>(fr), ns);
             t->adopted_sz[0].store(h.copies_.size(), std::memory_order_release);
             t->adopted_sz[1].store(h.versions_.size(), std::memory_order_release);
             t->adopted_sz[2].store(h.images_.size(), std::memory_order_release);

@@ -139,6 +139,17 @@ SIGNATURES = {
                                         ctypes.c_int]),
     "stage_zipf_zeta": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_double, c_vp]),
     "stage_ycsb_ops": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_double, c_vp, c_vp]),
+    "stage_probe_identify": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64, c_vp, c_vp]),
+    "stage_reader_read_ident": (ctypes.c_int, [c_vp, ctypes.c_uint64, ctypes.c_uint16, ctypes.c_uint32, c_vp, c_vp,
+                                               c_vp]),
+    "stage_record_meta_key": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint16, c_u64p, c_vp, c_u8p]),
+    "stage_location_cells": (ctypes.c_int, [c_vp]),
+    "stage_location_cell": (ctypes.c_int, [c_vp, ctypes.c_uint64, ctypes.POINTER(c_vp)]),
+    "stage_copy_get": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint64, c_vp]),
+    "stage_copy_readers": (ctypes.c_int, [c_vp, ctypes.c_uint32, c_vp, ctypes.c_uint32, c_u32p]),
+    "stage_copy_add_reader": (ctypes.c_int, [c_vp, ctypes.c_uint32, ctypes.c_uint32]),
+    "stage_copy_wr_count": (ctypes.c_int, [c_vp, ctypes.c_uint32, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
+    "stage_copy_update_ps": (ctypes.c_int, [c_vp, ctypes.c_uint32, ctypes.c_uint32]),
 }
 
 

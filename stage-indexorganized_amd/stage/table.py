@@ -19,6 +19,12 @@ assert PROBE_OUT_DTYPE.itemsize == 32
 PROBE_OUT16_DTYPE = np.dtype([("status", "u1"), ("flags", "u1"), ("hops", "u2"), ("cstamp", "u4"),
                               ("copy_sstamp", "u4"), ("rec_cstamp", "u4")])
 assert PROBE_OUT16_DTYPE.itemsize == 16
+# stage_probe_ident: the hit record's RecordLocation handle and next handle
+IDENT_DTYPE = np.dtype([("loc", "u4"), ("next", "u4")])
+NEXT_COPY, NEXT_VERSION, NEXT_KIND_MASK, NEXT_INDEX_MASK = 0x40000000, 0x80000000, 0xC0000000, 0x3FFFFFFF
+# stage_copy_state
+COPY_STATE_DTYPE = np.dtype([("cstamp", "u4"), ("pstamp", "u4"), ("rstamp", "u4"), ("sstamp", "u4"),
+                             ("readers", "u4"), ("count", "u2"), ("waiting", "u1"), ("pad", "u1")])
 
 ST_NOT_FOUND, ST_LATEST, ST_COPY, ST_OLD, ST_FAIL_INVALID_TS, ST_CHAIN_MISS = range(6)
 Q2_REC_DTYPE = np.dtype([
@@ -442,6 +448,53 @@ class Table:
         rows = d_rec.to_numpy(np.uint8, n * self.stride).reshape(n, self.stride) if d_rec else None
         return out, rows
 
+    def identify(self, keys, read_ids=None):
+        """stage_probe_batch + stage_probe_identify: (out[n], ident[n] IDENT_DTYPE) -- each hit's
+        RecordLocation handle and next handle (the Record's loc_ptr / next_ptr)"""
+        words, n = self.key_buffer(keys)
+        bufs = [DeviceBuffer.from_numpy(words) if n else DeviceBuffer(8)]
+        d_rids = None
+        if read_ids is not None:
+            bufs.append(DeviceBuffer.from_numpy(np.ascontiguousarray(read_ids, np.uint32)))
+            d_rids = bufs[-1].ptr
+        d_out = DeviceBuffer(max(1, n) * 32)
+        d_id = DeviceBuffer(max(1, n) * 8)
+        self.probe_device(bufs[0].ptr, n, d_out.ptr, None, d_rids)
+        check(lib().stage_probe_identify(self.h, d_out.ptr, n, d_id.ptr, None), "stage_probe_identify")
+        check(lib().stage_device_sync(), "sync")
+        return d_out.to_numpy(PROBE_OUT_DTYPE, n), d_id.to_numpy(IDENT_DTYPE, n)
+
+    def record_meta(self, key, key_size=None):
+        """stage_record_meta_key: (meta word, location handle, next handle) or None"""
+        kb = np.array([int(key)], np.uint64).tobytes()[:key_size or self.key_width]
+        meta = ctypes.c_uint64()
+        ident = np.zeros(1, IDENT_DTYPE)
+        rc = ctypes.c_uint8()
+        check(lib().stage_record_meta_key(self.h, kb, len(kb), ctypes.byref(meta), ident.ctypes.data, ctypes.byref(rc)),
+              "record_meta_key")
+        return None if rc.value != RC_OK else (meta.value, int(ident[0]["loc"]), int(ident[0]["next"]))
+
+    def enable_location_cells(self):
+        check(lib().stage_location_cells(self.h), "location_cells")
+
+    def location_cell(self, handle):
+        """the 24-B RecordMetadata {meta, next_ptr, loc_ptr} location `handle` points at now"""
+        p = ctypes.c_void_p()
+        check(lib().stage_location_cell(self.h, handle, ctypes.byref(p)), "location_cell")
+        return tuple(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint64))[i] for i in range(3))
+
+    def copy_state(self, copy_id):
+        """stage_copy_get + stage_copy_readers: dict of the overwrite copy's transaction state"""
+        st = np.zeros(1, COPY_STATE_DTYPE)
+        ids = np.array([copy_id], np.uint32)
+        check(lib().stage_copy_get(self.h, ids.ctypes.data, 1, st.ctypes.data), "copy_get")
+        d = {k: int(st[0][k]) for k in COPY_STATE_DTYPE.names if k != "pad"}
+        buf = np.zeros(max(1, d["readers"]), np.uint32)
+        cnt = ctypes.c_uint32()
+        check(lib().stage_copy_readers(self.h, copy_id, buf.ctypes.data, buf.size, ctypes.byref(cnt)), "copy_readers")
+        d["reader_ids"] = buf[:cnt.value].tolist()
+        return d
+
     def set_write_overlap(self, on):
         """stage_set_write_overlap: a device write-path epoch's kernels up to its publish run beside
         the caller's later work (inputs must be complete when update_batch_device is called)."""
@@ -550,6 +603,15 @@ class Reader:
         check(lib().stage_reader_read(self.h, int(key), key_size or self.table.key_width, read_id, out.ctypes.data,
                                       _ptr(row)), "reader_read")
         return out[0], row
+
+    def read_ident(self, key, read_id=0xFFFFFFFE, key_size=None):
+        """stage_reader_read_ident: (out, row, ident)"""
+        out = np.zeros(1, PROBE_OUT_DTYPE)
+        row = np.zeros(8 + self.table.payload_size, np.uint8)
+        ident = np.zeros(1, IDENT_DTYPE)
+        check(lib().stage_reader_read_ident(self.h, int(key), key_size or self.table.key_width, read_id,
+                                            out.ctypes.data, row.ctypes.data, ident.ctypes.data), "reader_read_ident")
+        return out[0], row, ident[0]
 
     def stats(self):
         s = np.zeros(3, np.uint64)

@@ -25,6 +25,7 @@ PAYLOAD, ROW = 1000, 1008
 PROBE_OUT = np.dtype([("status", "u1"), ("flags", "u1"), ("hops", "u2"), ("leaf", "u4"), ("slot", "u2"),
                       ("key_len", "u2"), ("cstamp", "u4"), ("rec_cstamp", "u4"), ("copy_sstamp", "u4"),
                       ("image", "u4"), ("meta_hi", "u4")])
+IDENT = np.dtype([("loc", "u4"), ("next", "u4")])  # stage_probe_ident
 
 # the scenario `adapter_drive probe` writes (tools/adapter_drive.cpp)
 QUERIES = [(3, 0xFFFFFFFE), (3, 4), (3, 1), (3, 0), (5, 10), (5, 3), (9042, 5), (9042, 11), (9042, 13), (77, 100),
@@ -56,12 +57,15 @@ def hit_slot(t, key, ks, cache):
 
 
 def oracle_probe_out(t, queries, ks=4):
-    """stage_probe_out records + rows the C-ABI would return, from the oracle"""
+    """stage_probe_out records + stage_probe_ident records + rows the C-ABI would return, from the
+    oracle"""
     cache = {}
     outs = np.zeros(len(queries), PROBE_OUT)
+    idents = np.zeros(len(queries), IDENT)
     rows = np.zeros((len(queries), ROW), np.uint8)
     for i, (k, rid) in enumerate(queries):
-        o, rec = t.read(k, ks, rid)
+        o, rec, _, loc, nxt = t.read_ident(k, ks, rid)
+        idents[i]["loc"], idents[i]["next"] = loc, nxt
         outs[i]["status"] = o["status"]
         outs[i]["flags"] = o["copy_present"]
         outs[i]["hops"] = o["hops"]
@@ -75,30 +79,35 @@ def oracle_probe_out(t, queries, ks=4):
             outs[i]["meta_hi"] = h[2] >> 32
             outs[i]["key_len"] = (h[2] >> 48) & 0x2FFF
         rows[i, :t.row] = rec
-    return outs, rows
+    return outs, idents, rows
 
 
-def expected(out, row):
-    """(ReturnCode, ResultType, perform_read, tuple, retired, record bytes, 1004 tuple bytes)"""
+def expected(out, row, ident):
+    """(ReturnCode, ResultType, perform_read, tuple, retired, via_copy, record bytes, 1004 tuple
+    bytes).  The Record's RecordMetadata carries next_ptr = the next handle and loc_ptr = the
+    location handle (the frame tool maps handles to themselves)."""
     st = int(out["status"])
     rc = 3 if st == 0 else 1
     result = 2 if st == 4 else 1
     perform = st in (1, 2)
     tup = st in (1, 2, 3)
     retired = st == 3
+    meta_w = (int(out["meta_hi"]) << 32) | int(out["rec_cstamp"])
+    inserting = (meta_w >> 62) & 1 and (meta_w >> 63) & 1
+    via_copy = bool(st != 0 and inserting and (int(ident["next"]) & 0xC0000000) == 0x40000000)
     rec = b""
     if st in (1, 2):
         meta = (int(out["meta_hi"]) << 32) | int(out["rec_cstamp"])
         kl = (meta >> 48) & 0x2FFF
         kp = (kl + 7) // 8 * 8
-        handle = ((int(out["leaf"]) << 16) | int(out["slot"])) + 1
-        nxt = (handle | (1 << 63)) if int(out["flags"]) & 1 else 0
+        handle = int(ident["loc"])
+        nxt = int(ident["next"])
         rec = struct.pack("<QQQIIQII", meta, nxt, handle, kp + PAYLOAD, 0, 0, int(out["cstamp"]), 0)
         rec += struct.pack("<I", int(out["cstamp"])) + bytes(row[:kp]) + bytes(row[max(kp, 8):max(kp, 8) + PAYLOAD])
     t = np.zeros(1004, np.uint8)
     if tup:
         t[:] = row[:1004] if not retired else np.concatenate([row[:4], row[8:1008]])
-    return rc, result, perform, tup, retired, rec, bytes(t)
+    return rc, result, perform, tup, retired, via_copy, rec, bytes(t)
 
 
 def parse(path):
@@ -108,15 +117,15 @@ def parse(path):
     for _ in range(n):
         key, rid = struct.unpack_from("<QI", b, off)
         off += 12
-        st, rc, result, perform, tup, retired = b[off:off + 6]
-        off += 6
+        st, rc, result, perform, tup, retired, via_copy = b[off:off + 7]
+        off += 7
         ln = struct.unpack_from("<H", b, off)[0]
         off += 2
         rec = b[off:off + ln]
         off += ln
         tb = b[off:off + 1004]
         off += 1004
-        res.append((key, rid, st, rc, result, bool(perform), bool(tup), bool(retired), rec, tb))
+        res.append((key, rid, st, rc, result, bool(perform), bool(tup), bool(retired), bool(via_copy), rec, tb))
     assert off == len(b)
     return res
 

@@ -68,6 +68,14 @@ _SIG = {
     "orc_murmur64a_batch": (None, [vp, u64, ctypes.c_int, u64, vp]),
     "orc_payload_word": (u64, [u64, u32]),
     "orc_fill_payload": (None, [u64, ctypes.c_int, vp, u32]),
+    "orc_read_ident": (ctypes.c_int, [vp, vp, u32, u32, vp, vp, vp, vp, vp]),
+    "orc_location_meta": (ctypes.c_int, [vp, u64, vp, vp]),
+    "orc_record_meta": (ctypes.c_int, [vp, vp, u32, vp, vp, vp]),
+    "orc_copy_state": (ctypes.c_int, [vp, u32, vp]),
+    "orc_copy_readers": (u32, [vp, u32, vp, u32]),
+    "orc_copy_add_reader": (ctypes.c_int, [vp, u32, u32]),
+    "orc_copy_wr_count": (ctypes.c_int, [vp, u32, ctypes.c_int]),
+    "orc_copy_update_ps": (ctypes.c_int, [vp, u32, u32]),
 }
 
 _lib = None
@@ -169,6 +177,33 @@ class OracleTree:
         rec = np.zeros(self.row, np.uint8)
         lib().orc_read(self.t, kb, key_size, read_id, out.ctypes.data, rec.ctypes.data)
         return out[0], rec
+
+    def read_ident(self, key, key_size, read_id=0xFFFFFFFE):
+        """orc_read + the hit slot's meta word, location handle and next handle"""
+        kb = key_bytes(key, key_size)
+        out = np.zeros(1, READ_OUT_DTYPE)
+        rec = np.zeros(self.row, np.uint8)
+        meta, loc, nxt = ctypes.c_uint64(), ctypes.c_uint32(), ctypes.c_uint32()
+        lib().orc_read_ident(self.t, kb, key_size, read_id, out.ctypes.data, rec.ctypes.data, ctypes.byref(meta),
+                             ctypes.byref(loc), ctypes.byref(nxt))
+        return out[0], rec, meta.value, loc.value, nxt.value
+
+    def location_meta(self, handle):
+        meta, nxt = ctypes.c_uint64(), ctypes.c_uint32()
+        lib().orc_location_meta(self.t, handle, ctypes.byref(meta), ctypes.byref(nxt))
+        return meta.value, nxt.value
+
+    def copy_state(self, copy_id):
+        """(cstamp, pstamp, rstamp, sstamp, readers, count, waiting) or None"""
+        st = np.zeros(7, np.uint32)
+        if lib().orc_copy_state(self.t, copy_id, st.ctypes.data) != 0:
+            return None
+        return tuple(int(x) for x in st)
+
+    def copy_readers(self, copy_id):
+        buf = np.zeros(4096, np.uint32)
+        n = lib().orc_copy_readers(self.t, copy_id, buf.ctypes.data, buf.size)
+        return buf[:min(n, buf.size)].tolist()
 
     def read_batch(self, keys, key_size, read_ids=None, records=True, nthreads=8):
         keys = np.ascontiguousarray(keys, np.uint64)

@@ -1,0 +1,61 @@
+"""The boundary's transaction facts (VERDICT r03 "What's missing" #1): the kept
+SSNTransactionManager dereferences every Record's loc_ptr (the record's CURRENT RecordMetadata,
+wherever splits moved it: FindMaxPstamp tm.cpp:37, FindMinSstamp :123, commit :605) and next_ptr
+(the in-flight update's overwrite-copy header and its readers: PerformRead :379-399, FindMinSstamp
+:148-215, FindMaxPstamp :41-97, post-commit READ :753-762), and BTree::Read registers a copy's
+readers (b_tree.cpp:2104-2105).
+
+oracle/txn_parity (built by oracle/Makefile) runs a restatement of that manager
+(oracle/ssn_txn.hpp) over one seeded schedule of concurrent YCSB-style transactions twice: over
+device probe results framed by include/stage_btree_adapter.hpp (stage_probe_identify's location /
+next handles, LocationTable -> stage_location_cell, OverwritePool -> stage_copy_*), and over the
+oracle.  Every step (read facts, PerformRead / PerformUpdate outcome, commit / abort), every
+transaction's final stamps, every overwrite-copy header (stamps, readers, dependency count) and
+every RecordLocation cell must be equal.  The schedule splits the leaves of hot records between
+reads and commits (bursts of committed inserts), reads in-flight records through their copies,
+and commits writers over copies whose readers committed first.
+
+CPU: the oracle run is deterministic and covers those cases.  GPU: the device run equals it."""
+import json
+import os
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TOOL = os.path.join(REPO, "oracle", "_build", "txn_parity")
+SEEDS = [1, 2, 3]
+
+
+def run(mode, seed, rows=3000, txns=300):
+    p = subprocess.run([TOOL, mode, str(seed), str(rows), str(txns)], capture_output=True, text=True, timeout=600)
+    return p.returncode, p.stdout, p.stderr
+
+
+def coverage(summary):
+    assert summary["reads_via_copy"] > 0          # BTree::Read served from the overwrite copy (AddReader)
+    assert summary["copy_reader_commits"] > 0     # a writer committed over a copy with registered readers
+    assert summary["max_pstamp_readers"] > 0      # FindMaxPstamp took a finished reader's predecessor
+    assert summary["max_pstamp_headers"] > 0
+    assert summary["min_sstamp_writers"] > 0      # FindMinSstamp through a committed overwriter
+    assert summary["moved_between_read_and_commit"] > 0  # a split moved a read record before its commit
+    assert summary["commits"] > 0 and summary["aborts"] > 0
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_oracle_schedule_is_deterministic_and_covers_the_manager(seed):
+    assert os.access(TOOL, os.X_OK), "oracle/_build/txn_parity not built (make -C oracle)"
+    rc1, out1, err1 = run("oracle", seed)
+    rc2, out2, _ = run("oracle", seed)
+    assert rc1 == 0 and rc2 == 0, err1
+    assert out1 == out2
+    coverage(json.loads(out1.strip().splitlines()[-1]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", SEEDS)
+def test_device_results_drive_the_manager_like_the_oracle(gpu, seed):
+    rc, out, err = run("both", seed)
+    lines = out.strip().splitlines()
+    assert rc == 0 and lines[0] == "MATCH", (out[-3000:], err[-2000:])
+    coverage(json.loads(lines[-1]))
