@@ -1142,7 +1142,10 @@ def run_chq2(args):
                    "warehouses": args.warehouses, "items": args.items, "q2_per_step": nq,
                    "suppliers_visited": nsupp,
                    "stock_lookups": nstock, "aborted": bool(ab), "updates": int(recs["update"].sum()),
-                   "read_only_batch": nq > 1, "queries_equal_query0": same},
+                   "read_only_batch": nq > 1, "queries_equal_query0": same,
+                   "batch_lookups": "the batch's queries look up the same STOCK / ITEM keys (the visited suppliers do "
+                                    "not depend on the read id): each key is probed once and its hit slot's "
+                                    "visibility evaluated at every query's read id" if nq > 1 else None},
         "single_q2_commit_path": commit,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,

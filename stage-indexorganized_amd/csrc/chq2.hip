@@ -48,15 +48,14 @@ __global__ void q2_fill_rids(uint32_t *p, uint64_t per, uint32_t nq, const uint3
     if (i < per * nq) p[i] = rq[i / per];
 }
 
-// block (s, q) copies supplier s's map entries (2 words each) to its segment of query q's copy
+// block s copies supplier s's map entries (2 words each) to its segment
 __global__ void q2_gather(const uint64_t *__restrict__ map_keys, const uint64_t *__restrict__ src,
-                          const uint64_t *__restrict__ dst, const uint32_t *__restrict__ cnt, uint64_t m,
+                          const uint64_t *__restrict__ dst, const uint32_t *__restrict__ cnt,
                           uint64_t *__restrict__ keys) {
     const uint32_t s = blockIdx.x;
-    uint64_t *kq = keys + 2 * m * blockIdx.y;
     for (uint32_t e = threadIdx.x; e < cnt[s]; e += blockDim.x) {
-        kq[2 * (dst[s] + e)] = map_keys[2 * (src[s] + e)];
-        kq[2 * (dst[s] + e) + 1] = map_keys[2 * (src[s] + e) + 1];
+        keys[2 * (dst[s] + e)] = map_keys[2 * (src[s] + e)];
+        keys[2 * (dst[s] + e) + 1] = map_keys[2 * (src[s] + e) + 1];
     }
 }
 
@@ -68,12 +67,13 @@ __global__ __launch_bounds__(64) void q2_reduce(const stage_probe_out_dev *__res
                                                 const uint8_t *__restrict__ sheap, uint32_t shstride,
                                                 uint32_t skpad, uint32_t n, uint64_t m, stage_q2_rec *__restrict__ out,
                                                 uint64_t *__restrict__ ikeys, int32_t *__restrict__ abort_flag) {
-    // block = (supplier s, query q): query q's lookups are the q-th copy of the m keys
+    // block = (supplier s, query q): query q's lookup results are the q-th segment of m records
+    // (the m keys are the same for every query)
     const uint32_t s = blockIdx.x % n, q = blockIdx.x / n, lane = threadIdx.x;
     abort_flag += q;
     out += (uint64_t)q * n;
     ikeys += (uint64_t)q * n;
-    const uint64_t b = (uint64_t)q * m + dst[s];
+    const uint64_t b = (uint64_t)q * m + dst[s], kb = dst[s];
     const uint32_t c = cnt[s];
     bool bad = false;
     for (uint32_t e = lane; e < c; e += 64) bad |= !produced(sout[b + e].w[0] & 0xFF);
@@ -83,9 +83,9 @@ __global__ __launch_bounds__(64) void q2_reduce(const stage_probe_out_dev *__res
     memset(&r, 0, sizeof(r));
     r.supp_key = (int64_t)supp[s];
     if (c) {  // stock_0 / stock_1 of the last lookup (a supplier without stocks keeps zeros)
-        const uint64_t last = b + c - 1;
-        r.s_w_id = (int64_t)skeys[2 * last];
-        r.s_i_id = (int64_t)skeys[2 * last + 1];
+        const uint64_t last = b + c - 1, klast = kb + c - 1;
+        r.s_w_id = (int64_t)skeys[2 * klast];
+        r.s_i_id = (int64_t)skeys[2 * klast + 1];
         if (produced(sout[last].w[0] & 0xFF)) {
             const uint8_t *row = sheap + (uint64_t)sout[last].w[6] * shstride + skpad;
             r.s_quantity = ld_i32(row);
@@ -239,17 +239,19 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
             return o;
         };
         const uint64_t o_src = take(n * 8), o_dst = take(n * 8), o_cnt = take(n * 4), o_sup = take(n * 8),
-                       o_keys = take(std::max<uint64_t>(m, 1) * 16 * nq),
-                       o_rids = take(std::max<uint64_t>(m, n) * 4 * nq), o_irids = take(n * 4 * nq),
-                       o_rq = take(nq * 4), o_sout = take(std::max<uint64_t>(m, 1) * 32 * nq),
+                       o_keys = take(std::max<uint64_t>(m, 1) * 16), o_rids = take(std::max<uint64_t>(m, 1) * 4),
+                       o_irids = take(n * 4 * nq), o_rq = take(nq * 4),
+                       o_sbase = take(nq > 1 ? std::max<uint64_t>(m, 1) * 32 : 0),
+                       o_sout = take(std::max<uint64_t>(m, 1) * 32 * nq),
                        o_rec = take(n * sizeof(stage_q2_rec) * nq), o_ik = take(n * 8 * nq),
-                       o_iout = take(n * 32 * nq), o_ab = take(4 * nq);
+                       o_iout = take(n * 32 * nq), o_ibase = take(nq > 1 ? n * 32 : 0), o_ab = take(4 * nq);
         uint8_t *buf = scratch_bytes(nation->dev, off);
         auto *d_src = (uint64_t *)(buf + o_src), *d_dst = (uint64_t *)(buf + o_dst), *d_sup = (uint64_t *)(buf + o_sup);
         auto *d_cnt = (uint32_t *)(buf + o_cnt), *d_rids = (uint32_t *)(buf + o_rids);
         auto *d_irids = (uint32_t *)(buf + o_irids), *d_rq = (uint32_t *)(buf + o_rq);
         auto *d_keys = (uint64_t *)(buf + o_keys), *d_ik = (uint64_t *)(buf + o_ik);
         auto *d_sout = (stage_probe_out_dev *)(buf + o_sout), *d_iout = (stage_probe_out_dev *)(buf + o_iout);
+        auto *d_sbase = (stage_probe_out_dev *)(buf + o_sbase), *d_ibase = (stage_probe_out_dev *)(buf + o_ibase);
         auto *d_rec = (stage_q2_rec *)(buf + o_rec);
         auto *d_ab = (int32_t *)(buf + o_ab);
         hip_check(hipMemcpyAsync(d_src, src.data(), n * 8, hipMemcpyHostToDevice, s), "h2d");
@@ -258,18 +260,26 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         hip_check(hipMemcpyAsync(d_sup, sel.data(), n * 8, hipMemcpyHostToDevice, s), "h2d");
         hip_check(hipMemcpyAsync(d_rq, rq, nq * 4, hipMemcpyHostToDevice, s), "h2d");
         hip_check(hipMemsetAsync(d_ab, 0, 4 * nq, s), "memset");
-        q2_fill_rids<<<(unsigned)((m * nq + 255) / 256) + 1, 256, 0, s>>>(d_rids, m, nq, d_rq);
+        q2_fill_rids<<<(unsigned)((m + 255) / 256) + 1, 256, 0, s>>>(d_rids, m, 1, d_rq);
         q2_fill_rids<<<(unsigned)((n * nq + 255) / 256), 256, 0, s>>>(d_irids, n, nq, d_rq);
-        q2_gather<<<dim3(n, nq), 256, 0, s>>>(d_map_keys, d_src, d_dst, d_cnt, m, d_keys);
+        q2_gather<<<n, 256, 0, s>>>(d_map_keys, d_src, d_dst, d_cnt, d_keys);
         const DevTable &sv = stock->dev.view, &iv = item->dev.view;
-        if (m)
-            hip_check(launch_probe(sv, d_keys, nullptr, d_rids, nullptr, m * nq, d_sout, nullptr, s, stock->tune),
+        // every query of the batch looks up the same STOCK keys (the visited suppliers and their
+        // supp_stock_map do not depend on the read id): each key is probed once and its hit slot's
+        // visibility evaluated at every query's read id (launch_revisit)
+        if (m) {
+            hip_check(launch_probe(sv, d_keys, nullptr, d_rids, nullptr, m, nq > 1 ? d_sbase : d_sout, nullptr, s,
+                                   stock->tune),
                       "stock probe");
+            if (nq > 1) hip_check(launch_revisit(sv, d_sbase, m, d_rq, nq, d_sout, s), "stock read ids");
+        }
         q2_reduce<<<n * nq, 64, 0, s>>>(d_sout, d_keys, d_dst, d_cnt, d_sup, sv.heap, sv.hstride,
                                         facts(stock).key_pad(), n, m, d_rec, d_ik, d_ab);
-        // 3. item lookups of the last stocks, filter
-        hip_check(launch_probe(iv, d_ik, nullptr, d_irids, nullptr, (uint64_t)n * nq, d_iout, nullptr, s, item->tune),
+        // 3. item lookups of the last stocks (the same keys in every query: probed once, as above),
+        // filter
+        hip_check(launch_probe(iv, d_ik, nullptr, d_irids, nullptr, n, nq > 1 ? d_ibase : d_iout, nullptr, s, item->tune),
                   "item probe");
+        if (nq > 1) hip_check(launch_revisit(iv, d_ibase, n, d_rq, nq, d_iout, s), "item read ids");
         q2_finish<<<(n * nq + 255) / 256, 256, 0, s>>>(d_iout, iv.heap, iv.hstride, facts(item).key_pad(), n, nq,
                                                        d_rec, d_ab);
         hip_check(hipGetLastError(), "q2 kernels");

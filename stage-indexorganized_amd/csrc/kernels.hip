@@ -2676,6 +2676,35 @@ bool probe_fanout_supported(const DevTable &t) {
     return t.key_width != 0 && t.key_words == 1 && t.cap == 64 && t.stride <= 1024;
 }
 
+// launch_revisit: thread per (key i, read id q); a NOT_FOUND result (no visible slot, or an
+// in-flight insert without a copy) holds for every read id and is copied as it is
+__global__ __launch_bounds__(256) void revisit_kernel(DevTable t, const stage_probe_out_dev *__restrict__ base,
+                                                      uint64_t n, const uint32_t *__restrict__ rids, uint32_t nq,
+                                                      stage_probe_out_dev *__restrict__ out) {
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n * nq) return;
+    const uint64_t i = g % n, q = g / n;
+    const u32x4 *bp = reinterpret_cast<const u32x4 *>(base + i);
+    u32x4 a = bp[0], b = bp[1];
+    const uint32_t slot = a.z & 0xFFFF, leaf = a.y;
+    if ((a.x & 0xFF) != ST_NOT_FOUND && slot < t.cap && leaf < t.nleaves) {
+        const SlotInfo si = t.slot[(uint64_t)leaf * t.cap + slot];
+        ProbeRes r;
+        visibility(t, (int)slot, si.meta, si.next, si.image, rids[q], r);
+        pack_out(leaf, r, a, b);
+    }
+    u32x4 *op = reinterpret_cast<u32x4 *>(out + q * n + i);
+    op[0] = a;
+    op[1] = b;
+}
+
+hipError_t launch_revisit(const DevTable &t, const stage_probe_out_dev *base, uint64_t n, const uint32_t *rids,
+                          uint32_t nq, stage_probe_out_dev *out, hipStream_t s) {
+    if (n == 0 || nq == 0) return hipSuccess;
+    revisit_kernel<<<(unsigned)((n * nq + 255) / 256), 256, 0, s>>>(t, base, n, rids, nq, out);
+    return hipGetLastError();
+}
+
 // stage_probe_ident: a probe's hit slot (leaf, slot in its status record) -> the slot word's
 // location handle and next handle, from the same published image.  A thread per probe.
 __global__ __launch_bounds__(256) void ident_kernel(DevTable t, const stage_probe_out_dev *__restrict__ out, uint64_t n,
