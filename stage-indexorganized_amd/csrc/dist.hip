@@ -177,11 +177,42 @@ __global__ void dd_gather_keys(const uint64_t *__restrict__ keys, const uint32_t
     if (j < n) out[j] = keys[idx[j]];
 }
 
-__global__ void dd_heads(const uint64_t *__restrict__ skeys, const uint32_t *__restrict__ sidx,
+// Narrow sort keys (requests without read ids, coalescing width <= 32 bits): the batch's low
+// 32 key bits and the positions; hi[0] |= any key's upper half, so the sorted low words stand
+// for the keys themselves only when every key fits 32 bits (else the keys are gathered back
+// by position -- a sort on fewer bits than the keys hold only coalesces less, see key_bits).
+__global__ __launch_bounds__(256) void dd_narrow_iota(const uint64_t *__restrict__ keys, uint64_t n,
+                                                      uint32_t *__restrict__ k32, uint32_t *__restrict__ iota,
+                                                      uint32_t *__restrict__ hi) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t k = 0;
+    if (i < n) {
+        k = keys[i];
+        k32[i] = (uint32_t)k;
+        iota[i] = (uint32_t)i;
+    }
+    if (__builtin_amdgcn_ballot_w64((k >> 32) != 0) != 0 && (threadIdx.x & 63) == 0) atomicOr(hi, 1u);
+}
+
+// the key of sorted entry j: the sorted 64-bit key, or the narrow one (widened, or gathered
+// by position when some key exceeds 32 bits)
+struct SortedKeys {
+    const uint64_t *k64;   // 64-bit sort: the sorted keys
+    const uint32_t *k32;   // 32-bit sort: the sorted low words
+    const uint64_t *keys;  // 32-bit sort: the caller's keys (gathered when *hi)
+    const uint32_t *hi;
+    __device__ __forceinline__ uint64_t at(uint64_t j, const uint32_t *sidx, bool wide) const {
+        if (k64) return k64[j];
+        return wide ? keys[sidx[j]] : (uint64_t)k32[j];
+    }
+};
+
+__global__ void dd_heads(SortedKeys sk, const uint32_t *__restrict__ sidx,
                          const uint32_t *__restrict__ rids, uint64_t n, uint32_t *__restrict__ flag) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n) return;
-    bool head = j % kFanCap == 0 || skeys[j] != skeys[j - 1];
+    const bool wide = !sk.k64 && *sk.hi != 0;
+    bool head = j % kFanCap == 0 || sk.at(j, sidx, wide) != sk.at(j - 1, sidx, wide);
     if (!head && rids) head = rids[sidx[j]] != rids[sidx[j - 1]];
     flag[j] = head ? 1u : 0u;
 }
@@ -190,7 +221,7 @@ __global__ void dd_heads(const uint64_t *__restrict__ skeys, const uint32_t *__r
 // of sorted entry j; urange[b + u] = request u's run [b + first, b + last + 1) of flist; the
 // request's key / read id packed at b + u; nu[chunk] = the request count (the sharded probe
 // coalesces its whole batch at once: b = 0, chunk 0)
-__global__ void dd_pack(const uint64_t *__restrict__ skeys, const uint32_t *__restrict__ sidx,
+__global__ void dd_pack(SortedKeys sk, const uint32_t *__restrict__ sidx,
                         const uint32_t *__restrict__ rids, const uint32_t *__restrict__ flag,
                         const uint32_t *__restrict__ useq, uint64_t n, uint32_t b, uint32_t *__restrict__ uidx,
                         uint32_t *__restrict__ flist, FanRange *__restrict__ urange, uint64_t *__restrict__ ukeys,
@@ -201,7 +232,7 @@ __global__ void dd_pack(const uint64_t *__restrict__ skeys, const uint32_t *__re
     if (uidx) uidx[b + p] = b + u;  // owner-reply mode only
     flist[b + j] = b + p;
     if (flag[j]) {
-        ukeys[b + u] = skeys[j];
+        ukeys[b + u] = sk.k64 ? sk.k64[j] : *sk.hi ? sk.keys[p] : (uint64_t)sk.k32[j];
         if (rids) urids[b + u] = rids[p];
         urange[b + u].lo = b + (uint32_t)j;
     }
@@ -324,6 +355,36 @@ void grow(void *&p, uint64_t bytes) {
 }
 
 unsigned blocks_for(uint64_t n, unsigned per_block) { return (unsigned)std::max<uint64_t>(1, (n + per_block - 1) / per_block); }
+
+// The 32-bit coalescing sort (u32 keys, u32 positions): hipcub's onesweep (8 bits a pass), or
+// rocprim's onesweep at RB bits a pass -- 3 passes instead of 4 over 25-30 key bits
+// (STAGE_DD_RADIX_BITS = 10 / 11).  temp == nullptr: storage size query.
+template <unsigned RB>
+using Onesweep32 = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<512, 8>, rocprim::kernel_config<512, 8>, RB,
+                                        rocprim::block_radix_rank_algorithm::match>>;
+
+int dd_radix_bits() {
+    static const int rb = [] {
+        const char *e = std::getenv("STAGE_DD_RADIX_BITS");
+        const int v = e ? std::atoi(e) : 8;
+        return v == 10 || v == 11 ? v : 8;
+    }();
+    return rb;
+}
+
+hipError_t sort32(void *temp, size_t &bytes, const uint32_t *kin, uint32_t *kout, const uint32_t *vin,
+                  uint32_t *vout, int n, int bits, hipStream_t s) {
+    switch (dd_radix_bits()) {
+        case 10:
+            return rocprim::radix_sort_pairs<Onesweep32<10>>(temp, bytes, kin, kout, vin, vout, n, 0u, (unsigned)bits, s);
+        case 11:
+            return rocprim::radix_sort_pairs<Onesweep32<11>>(temp, bytes, kin, kout, vin, vout, n, 0u, (unsigned)bits, s);
+        default:
+            return hipcub::DeviceRadixSort::SortPairs(temp, bytes, kin, kout, vin, vout, n, 0, bits, s);
+    }
+}
 
 }  // namespace
 
@@ -525,16 +586,17 @@ static void plan_route(ShardComm &c, Plan &P, const uint64_t *d_keys, const uint
         // temporary storage of the sorts and the scan
         if (n > c.dd_cub_items) {
             const int items = (int)n;
-            size_t sb = 0, sr = 0, cb = 0;
+            size_t sb = 0, sr = 0, cb = 0, s32 = 0;
             chk(hipcub::DeviceRadixSort::SortPairs(nullptr, sb, (uint64_t *)nullptr, (uint64_t *)nullptr,
                                                    (uint32_t *)nullptr, (uint32_t *)nullptr, items, 0, 64, s),
                 "sort size");
             chk(hipcub::DeviceRadixSort::SortPairs(nullptr, sr, (uint32_t *)nullptr, (uint32_t *)nullptr,
                                                    (uint32_t *)nullptr, (uint32_t *)nullptr, items, 0, 32, s),
                 "rid sort size");
+            chk(sort32(nullptr, s32, nullptr, nullptr, nullptr, nullptr, items, 32, s), "narrow sort size");
             chk(hipcub::DeviceScan::InclusiveSum(nullptr, cb, (uint32_t *)nullptr, (uint32_t *)nullptr, items, s),
                 "scan size");
-            c.dd_cub_bytes = std::max(std::max(sb, sr), cb);
+            c.dd_cub_bytes = std::max(std::max(std::max(sb, sr), cb), s32);
             grow(c.dd_cub, c.dd_cub_bytes);
             c.dd_cub_items = n;
         }
@@ -544,9 +606,18 @@ static void plan_route(ShardComm &c, Plan &P, const uint64_t *d_keys, const uint
         uint64_t *skeys = (uint64_t *)c.dd_skeys;
         const int bits = c.key_bits >= 1 && c.key_bits <= 64 ? c.key_bits : 64;
         const unsigned nb = blocks_for(n, 256);
-        dd_iota_kernel<<<nb, 256, 0, s>>>(iota, n);
         size_t bytes = c.dd_cub_bytes;
-        if (d_rids) {
+        SortedKeys sk{skeys, nullptr, nullptr, nullptr};
+        if (!d_rids && bits <= 32) {
+            // narrow sort: low words (in flag until the heads overwrite it) + positions; the
+            // sorted low words land in skeys' storage
+            uint32_t *k32 = flag, *sk32 = reinterpret_cast<uint32_t *>(skeys), *hi = nuw + 32;
+            chk(hipMemsetAsync(hi, 0, 4, s), "memset hi");
+            dd_narrow_iota<<<nb, 256, 0, s>>>(d_keys, n, k32, iota, hi);
+            chk(sort32(c.dd_cub, bytes, k32, sk32, iota, sidx, (int)n, bits, s), "dedupe narrow sort");
+            sk = SortedKeys{nullptr, sk32, d_keys, hi};
+        } else if (d_rids) {
+            dd_iota_kernel<<<nb, 256, 0, s>>>(iota, n);
             // (key, read id) order: sort by read id, then stably by key (LSD radix sorts are
             // stable); flag / useq serve as scratch until the heads are computed
             uint32_t *srid = flag, *sidx1 = useq;
@@ -558,13 +629,14 @@ static void plan_route(ShardComm &c, Plan &P, const uint64_t *d_keys, const uint
             chk(hipcub::DeviceRadixSort::SortPairs(c.dd_cub, bytes, gk, skeys, sidx1, sidx, (int)n, 0, bits, s),
                 "dedupe key sort");
         } else {
+            dd_iota_kernel<<<nb, 256, 0, s>>>(iota, n);
             chk(hipcub::DeviceRadixSort::SortPairs(c.dd_cub, bytes, d_keys, skeys, iota, sidx, (int)n, 0, bits, s),
                 "dedupe sort");
         }
-        dd_heads<<<nb, 256, 0, s>>>(skeys, sidx, d_rids, n, flag);
+        dd_heads<<<nb, 256, 0, s>>>(sk, sidx, d_rids, n, flag);
         bytes = c.dd_cub_bytes;
         chk(hipcub::DeviceScan::InclusiveSum(c.dd_cub, bytes, flag, useq, (int)n, s), "dedupe scan");
-        dd_pack<<<nb, 256, 0, s>>>(skeys, sidx, d_rids, flag, useq, n, 0u, owner ? (uint32_t *)c.uidx : nullptr,
+        dd_pack<<<nb, 256, 0, s>>>(sk, sidx, d_rids, flag, useq, n, 0u, owner ? (uint32_t *)c.uidx : nullptr,
                                    (uint32_t *)c.flist, (FanRange *)c.urange, (uint64_t *)c.ukeys, (uint32_t *)c.urids,
                                    nuw, 0);
         chk(hipGetLastError(), "dedupe");

@@ -229,3 +229,51 @@ def test_hot_keys_and_other_geometries_loopback(gpu, world, chunks, payload):
         assert routed < 0.7 * nk
     for t in tabs:
         stage.set_shard_dedupe(t, -1)
+
+
+@pytest.mark.parametrize("bits,wide", [(18, False), (12, False), (18, True)])
+def test_narrow_coalescing_sort(gpu, bits, wide):
+    # a coalescing width of <= 32 bits sorts the keys' low words (stage_set_shard_key_bits, as
+    # the bench sets it from the row count): exact grouping when every key fits 32 bits; a
+    # width below the keys' (12 of 18 bits) or keys above 2^32 in the batch (gathered back by
+    # position) only coalesce less -- every caller still gets the one-table result
+    world, n = 3, 200_000
+    keys = np.arange(n, dtype=np.uint64)
+    tabs, _ = shard_tables(keys, world)
+    full = stage.Table(key_width=8)
+    full.load_keys(keys, 8, mode=1)
+    for t in tabs + [full]:
+        t.sync()
+    rng = np.random.default_rng(bits + wide)
+    per_keys = []
+    for r in range(world):
+        k = np.concatenate([stage.zipf_draws(n + 99, 0.9, 70 + r, 50_000, nthreads=2),
+                            np.full(3000, 77 + r, np.uint64)])
+        if wide:  # absent keys above 2^32, some sharing low words with present keys
+            k = np.concatenate([k, (np.uint64(1) << np.uint64(32 + r)) + rng.integers(0, n, 2000).astype(np.uint64)])
+        per_keys.append(k[rng.permutation(k.size)].astype(np.uint64))
+    for t in tabs:
+        stage.set_shard_dedupe(t, 1)
+        stage.set_shard_key_bits(t, bits)
+    try:
+        res = stage.probe_sharded_loopback(tabs, per_keys, None)
+        for r in range(world):
+            out, rows = res[r]
+            ref_out, ref_rows = full.probe(per_keys[r])
+            for f in ("status", "flags", "hops", "key_len", "cstamp", "rec_cstamp", "copy_sstamp"):
+                assert (out[f] == ref_out[f]).all(), (r, f)
+            assert (rows == ref_rows).all(), r
+            nk, routed, _ = stage.sharded_stats(tabs[r])
+            u = np.unique(per_keys[r]).size
+            assert u <= routed <= nk
+            if bits == 18 and not wide:  # exact grouping: distinct keys + the 64-caller cuts
+                assert routed <= u + nk // 64 + 1
+        own = stage.probe_sharded_loopback(tabs, per_keys, None, records=True, reply=stage.REPLY_OWNER)
+        for r in range(world):
+            ref_out, _ = full.probe(per_keys[r])
+            for f in ("status", "cstamp", "rec_cstamp"):
+                assert (own[r][0][f] == ref_out[f]).all(), (r, f)
+    finally:
+        for t in tabs:
+            stage.set_shard_dedupe(t, -1)
+            stage.set_shard_key_bits(t, 0)
