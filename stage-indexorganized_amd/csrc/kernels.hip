@@ -2352,6 +2352,128 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     }
 }
 
+// First-tuple scans decided as point probes of their start key.  RangeScanBySize keeps the
+// first to_scan + 1 visible records with key >= x in slot order and ranks them by key
+// (b_tree.cpp:1276-1302); the scan's result is the first LATEST / OLD record in rank order that
+// carries the start key's prefix (executor.h:459-490 with the predicate).  When a visible record
+// holds exactly x at slot p inside the leaf's monotone slot prefix (p < mp, the head's info
+// word), every visible slot before p holds a key below x, so p is the first record kept and --
+// x being the least key >= x -- rank 0, unless another visible record also holds x (only
+// possible beyond mp, where the key order is not known: such a candidate is confirmed).  Rank 0
+// carries every prefix of x, so if its visibility at the read id is LATEST / OLD it is the
+// result.  Everything else -- no exact record, p >= mp, an equal key beyond mp, more than
+// kProbeCand fingerprint candidates, rank 0 invisible to the reader -- is marked kFirstUndecided
+// for scan_first_rest_kernel's general loop.  A TPC-C stock-level scan starts at {w, d, o, 5},
+// the fifth line of an order of 5..15 lines, so the exact record is the usual case, and the scan
+// costs what a point probe costs: the probe_split_kernel structure (a lane-per-scan descent,
+// the fingerprint heads wave-serial with 4 in flight, the candidates' slot words lane-parallel)
+// instead of a slot group's key columns per scan.
+template <int SPL, int KW, int CH>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void scan_first_probe_kernel(
+    DevTable t, const uint64_t *__restrict__ keys, uint64_t n, const uint32_t *__restrict__ rids,
+    uint32_t *__restrict__ img_out, uint8_t *__restrict__ st_out) {
+    __shared__ uint16_t s_cand[4][64][kProbeCand];
+    const uint32_t lane = lane_id(), wv = uni32(threadIdx.x >> 6);
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint32_t len = t.key_width;
+    for (uint64_t base = wave * CH; base < n; base += nwaves * CH) {
+        const uint64_t i = base + lane;
+        const bool valid = lane < (uint32_t)CH && i < n;
+        const uint32_t rid = rids ? (valid ? rids[i] : 0u) : 0xFFFFFFFEu;
+        uint64_t ok[KW];
+        load_okey<KW>(keys, i, valid, len, ok);
+        uint32_t leaf = 0;
+        if (valid) leaf = resolve_leaf<false, KW>(t, ok, len, true);
+        // the leaf's monotone prefix length, in flight through stage A
+        const uint32_t mp = valid ? *reinterpret_cast<const uint32_t *>(t.head + (uint64_t)leaf * t.head_bytes +
+                                                                       head_info_offset(t.cap, KW)) >> 16
+                                  : 0u;
+        const uint32_t fx_mine = key_fp_words(ok, KW);
+        const int cnt = (int)((n - base) < CH ? (n - base) : CH);
+        // ---- stage A (probe_split_kernel's): fingerprint candidates in slot order to LDS
+        constexpr int PD = SPL <= 4 ? 4 : 1;
+        uint32_t pf[PD][SPL];
+#pragma unroll
+        for (int d = 0; d < PD; ++d) {
+            if (d < cnt) {
+                const uint8_t *h = t.head + (uint64_t)rl32(leaf, d) * t.head_bytes;
+#pragma unroll
+                for (int s = 0; s < SPL; ++s) pf[d][s] = h[s * 64 + lane];
+            }
+        }
+        uint32_t my_nc = 0;
+        for (int j0 = 0; j0 < cnt; j0 += PD) {
+#pragma unroll
+            for (int u = 0; u < PD; ++u) {
+                const int j = j0 + u;
+                if (j >= cnt) break;
+                uint32_t fpb[SPL];
+#pragma unroll
+                for (int s = 0; s < SPL; ++s) fpb[s] = pf[u][s];
+                if (j + PD < cnt) {
+                    const uint8_t *h = t.head + (uint64_t)rl32(leaf, j + PD) * t.head_bytes;
+#pragma unroll
+                    for (int s = 0; s < SPL; ++s) pf[u][s] = h[s * 64 + lane];
+                }
+                const uint32_t fx = rl32(fx_mine, j);
+                uint32_t nc = 0;
+#pragma unroll
+                for (int s = 0; s < SPL; ++s) {
+                    const bool c = fpb[s] == fx;
+                    const uint64_t cm = ballot(c);
+                    const uint32_t r = nc + count_below(cm);
+                    if (c && r < (uint32_t)kProbeCand) s_cand[wv][j][r] = (uint16_t)(s * 64 + lane);
+                    nc += (uint32_t)__builtin_popcountll(cm);
+                }
+                if (lane == (uint32_t)j) my_nc = nc;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // ---- stage B: lane = scan
+        if (valid) {
+            const uint64_t lb = (uint64_t)leaf * t.cap;
+            int p = -1;
+            bool undecided = my_nc > (uint32_t)kProbeCand;
+            SlotInfo si{};
+            for (uint32_t c = 0; c < my_nc && !undecided; ++c) {
+                const uint32_t sl = s_cand[wv][lane][c];
+                if (p >= 0 && sl < mp) continue;  // after p inside the monotone prefix: key > x
+                const u32x4 *w = reinterpret_cast<const u32x4 *>(t.slot + lb + sl);
+                const u32x4 w0 = w[0], w1 = w[1];
+                bool eq = (((uint64_t)w0.y << 32) | w0.x) == ok[0];
+#pragma unroll
+                for (int k = 1; k < KW; ++k) eq = eq && t.okey[((uint64_t)leaf * KW + k) * t.cap + sl] == ok[k];
+                if (!eq) continue;
+                if (p >= 0 || sl >= mp) {
+                    undecided = true;  // a second record holding x, or x beyond the monotone prefix
+                } else {
+                    p = (int)sl;
+                    si.okey = ((uint64_t)w0.y << 32) | w0.x;
+                    si.meta = ((uint64_t)w0.w << 32) | w0.z;
+                    si.next = w1.x;
+                    si.image = w1.y;
+                }
+            }
+            uint32_t img = 0xFFFFFFFFu;
+            uint8_t st = kFirstUndecided;
+            if (!undecided && p >= 0) {
+                uint8_t sv;
+                const uint32_t im = scan_visible(t, si, rid, sv);
+                if (sv == ST_LATEST || sv == ST_OLD) {
+                    img = im;
+                    st = sv;
+                }
+            }
+            img_out[i] = img;
+            st_out[i] = st;
+        }
+        __builtin_amdgcn_wave_barrier();  // s_cand is rewritten by the next chunk
+    }
+}
+
 // The scans scan_first_split_kernel left undecided (st_out == kFirstUndecided): the general loop
 // (scan_one_compact + FirstPrefixSink) from the start key, a wave per scan; 64 statuses are
 // read per wave and step, so a batch without undecided scans costs one pass over st_out.
@@ -2823,12 +2945,24 @@ hipError_t launch_scan_first(const DevTable &t, const uint64_t *keys, uint64_t n
     // default (STAGE_SL_SCANS unset or 0): scan_first_split_kernel + scan_first_rest_kernel.
     // Variants: -8 / -9 scan_first_mono_kernel at 8 waves/SIMD / uncapped
     // (round 3: a third of the instructions and of the HBM bytes, but per-lane scattered key
-    // loads -- no faster); -4 split at 7 waves/SIMD; -5 / -3 / -1 scan_first_fast_kernel with the
+    // loads -- no faster); -4 / -10 split at 7 / 6 waves/SIMD; -5 / -3 / -1 scan_first_fast_kernel with the
     // prefetch at 8 / 7 / 6 waves, -2 without it; -6 / -7 scan_first_seg_kernel (4 / 2 scans per
     // pass); 1 the general single-scan kernel; 2 / 4 NS scans per wave in lockstep
     const int ns = tune.first_scans;
+    const uint64_t pchunks = (n + 63) / 64;
+    const bool psmall = pchunks < 16384;  // as launch_probe: 16-scan chunks when 64-scan ones cannot fill the chip
+    const int pblocks = psmall ? grid_for((n + 15) / 16, 4, tune.max_blocks > 0 ? tune.max_blocks : 16384)
+                               : grid_for(pchunks, 4, tune.max_blocks > 0 ? tune.max_blocks : 16384);
 #define STAGE_FIRST(S, KW)                                                                                  \
-    if (ns == 0 || ns == -4 || ns == -6 || ns == -7 || ns == -8 || ns == -9) {                              \
+    if (ns == -11) {                                                                                        \
+        if (psmall)                                                                                         \
+            scan_first_probe_kernel<S, KW, 16><<<pblocks, 256, 0, s>>>(t, keys, n, rids, img_out, st_out);   \
+        else                                                                                                \
+            scan_first_probe_kernel<S, KW, 64><<<pblocks, 256, 0, s>>>(t, keys, n, rids, img_out, st_out);   \
+        scan_first_rest_kernel<S, KW><<<grid_for((n + 63) / 64, 4, 4096), 256, 0, s>>>(t, keys, n, scan_size,  \
+                                                                                    rids, words, img_out,   \
+                                                                                    st_out);                \
+    } else if (ns == 0 || ns == -4 || ns == -6 || ns == -7 || ns == -8 || ns == -9 || ns == -10) {                 \
         if (ns == -8)                                                                                       \
             scan_first_mono_kernel<S, KW, 8><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words, img_out, \
                                                                     st_out);                                \
@@ -2841,6 +2975,9 @@ hipError_t launch_scan_first(const DevTable &t, const uint64_t *keys, uint64_t n
         else if (ns == -7 && scan_size <= 31)                                                               \
             scan_first_seg_kernel<S, KW, 1, 2><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words,    \
                                                                       img_out, st_out);                     \
+        else if (ns == -10)                                                                                 \
+            scan_first_split_kernel<S, KW, 6><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words,     \
+                                                                     img_out, st_out);                      \
         else if (ns != -4)                                                                                  \
             scan_first_split_kernel<S, KW, 8><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words,     \
                                                                      img_out, st_out);                      \

@@ -69,13 +69,13 @@ def test_stock_level_matches_oracle(tpcc):
     assert (got2 == exp2).all()
 
 
-@pytest.mark.parametrize("variant,key_order", [(v, False) for v in ("0", "-1", "-2", "-3", "-4", "-5", "-6", "-7",
+@pytest.mark.parametrize("variant,key_order", [(v, False) for v in ("0", "-1", "-2", "-3", "-4", "-5", "-6", "-7", "-10", "-11",
                                                                    "-8", "-9", "1", "2", "4")] +
-                         [("0", True), ("-8", True)])
+                         [("0", True), ("-8", True), ("-11", True)])
 def test_stock_level_scan_kernel_variants(gpu, monkeypatch, variant, key_order):
     """Every first-tuple scan kernel (STAGE_SL_SCANS: 0 = scan_first_split_kernel, the default,
-    -8 / -9 = scan_first_mono_kernel, -5 / -3 / -1 / -2 = scan_first_fast_kernel variants, -4 split
-    at 7 waves/SIMD, -6 / -7 = scan_first_seg_kernel, 1 = the general single-scan kernel, 2 / 4 =
+    -8 / -9 = scan_first_mono_kernel, -5 / -3 / -1 / -2 = scan_first_fast_kernel variants, -4 / -10 split
+    at 7 / 6 waves/SIMD, -6 / -7 = scan_first_seg_kernel, 1 = the general single-scan kernel, 2 / 4 =
     lockstep) gives the oracle's stock-level results.  Order lines are inserted in numeric order,
     which is not their memcmp key order, so leaves carry unsorted regions (the fast kernel's O(m)
     ranking, the mono kernel's fallback beyond the monotone prefix) and sorted ones (its
@@ -121,7 +121,7 @@ def test_first_tuple_scans_every_kernel(gpu, monkeypatch, key_order):
                     break
         expected[(size, words)] = exp
     images = {}
-    for variant in ["1", "0", "-8", "-9", "-4", "-5", "-6", "-7", "-1", "-2", "-3", "2", "4"]:
+    for variant in ["1", "0", "-8", "-9", "-4", "-5", "-6", "-7", "-1", "-2", "-3", "2", "4", "-10", "-11"]:
         monkeypatch.setenv("STAGE_SL_SCANS", variant)
         tt = _tables(key_order)
         for size, words in cases:
@@ -137,7 +137,7 @@ def test_first_tuple_scans_every_kernel(gpu, monkeypatch, key_order):
     assert (expected[(10, 3)] == 0).any() and (expected[(10, 3)] != 0).any()
 
 
-@pytest.mark.parametrize("variant", ["0", "-8", "-4", "-5", "-6", "-7", "1", "2"])
+@pytest.mark.parametrize("variant", ["0", "-8", "-4", "-5", "-6", "-7", "1", "2", "-11"])
 def test_first_tuple_scans_16_byte_keys(gpu, monkeypatch, variant):
     """stage_index_scan_first_batch on the STOCK table (16-byte keys, KW = 2 order words):
     the first LATEST / OLD tuple of the same warehouse (prefix 1) or of the exact key (prefix
