@@ -452,6 +452,16 @@ def run_sharded(args, rank, world, local):
     t_own = ctl.max(time.perf_counter() - t0)
     owner = {"value": round(B * args.steps * world / t_own, 1), "ms_per_step": round(t_own / args.steps * 1e3, 4),
              "reply": "32-B status records to the caller, tuple rows materialised on the owner"}
+    direct = None
+    if world == 1:  # the one-rank rehearsal against the direct probe of the same batch on the same table
+        for _ in range(max(1, args.warmup)):
+            tab.probe_device(d_keys.ptr, B, d_out.ptr, d_rec.ptr, stream=stream.ptr)
+        stream.sync()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            tab.probe_device(d_keys.ptr, B, d_out.ptr, d_rec.ptr, stream=stream.ptr)
+        stream.sync()
+        direct = round((time.perf_counter() - t0) / args.steps * 1e3, 4)
     step()  # full reply again, so the self-check reads full rows
     stream.sync()
     # self-check: 8 windows of 8192 lookups spread over the batch (every exchange chunk), each
@@ -512,6 +522,10 @@ def run_sharded(args, rank, world, local):
                    "control_plane": "the RCCL communicator (file rendezvous of the unique id)"},
         "roofline": roof, "cpu_baseline": cpu, "self_check": all(p["self_check"] for p in per_rank),
         "owner_reply": owner,
+        **({"world1_vs_direct": {"sharded_ms_per_step": round(step_s * 1e3, 4), "owner_reply_ms_per_step":
+                                 owner["ms_per_step"], "direct_probe_ms_per_step": direct,
+                                 "note": "same table and batch: stage_probe_sharded_ex at world 1 (coalescing, "
+                                         "routing, fan-out probe) vs stage_probe_batch"}} if direct else {}),
         "coalescing": {"keys": sum(sx["keys"] for sx in stats), "requests_routed": routed,
                        "remote_requests": sum(sx["remote"] for sx in stats),
                        "routed_share": round(routed / max(1, sum(sx["keys"] for sx in stats)), 4),

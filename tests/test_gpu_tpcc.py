@@ -162,3 +162,53 @@ def test_first_tuple_scans_16_byte_keys(gpu, monkeypatch, variant):
         assert (st == exp).all(), (variant, size, words, np.nonzero(st != exp)[0][:10])
         assert ((img == 0xFFFFFFFF) == (st == 0)).all()
         assert (exp != 0).any() and (exp == 0).any()
+
+
+def test_stock_level_between_overlapped_district_epochs(gpu):
+    """Stock-level steps enqueued between device write-path epochs of the DISTRICT table in
+    write-overlap mode, all on one stream with no host wait (the write path's
+    kernels run beside the caller's stream and must not share its scratch): each step reads
+    D_NEXT_O_ID as of the epoch just before it -- the oracle's stock-level after that epoch."""
+    from stage._lib import check
+    tt = _tables()
+    tt.dist.set_write_overlap(1)
+    s = stage.Stream()
+    rng = np.random.default_rng(14)
+    n = 700
+    w = rng.integers(1, 3, n).astype(np.int64)
+    d = rng.integers(1, 11, n).astype(np.int64)
+    thr = rng.integers(10, 31, n).astype(np.int32)
+    tx = [stage.DeviceBuffer.from_numpy(x) for x in (w, d, thr)]
+    dkeys = np.stack([np.frombuffer(key(a, b), np.uint8) for a in (1, 2) for b in range(1, 11)])
+    kept, steps = [], []
+    for e in range(4):
+        nxt = rng.integers(21, 42, dkeys.shape[0]).astype(np.int32)  # D_NEXT_O_ID: 20 orders back stay loaded
+        wid = np.full(dkeys.shape[0], 100 + 10 * e, np.uint32)
+        cid = wid + 1
+        if e == 0:  # district (2, 3) is in flight since _tables(): leave it out of the epochs
+            keep = np.ones(dkeys.shape[0], bool)
+            keep[10 + 2] = False
+        dk, nx, wi, ci = dkeys[keep], nxt[keep], wid[keep], cid[keep]
+        words, m = tt.dist.key_buffer(dk)
+        bufs = [stage.DeviceBuffer.from_numpy(words), stage.DeviceBuffer.from_numpy(nx.view(np.uint8)),
+                stage.DeviceBuffer.from_numpy(wi), stage.DeviceBuffer.from_numpy(ci)]
+        rcb = stage.DeviceBuffer(m)
+        check(stage.lib().stage_update_batch_device(tt.dist.h, bufs[0].ptr, None, m, 0, bufs[1].ptr, 4, bufs[2].ptr,
+                                                    bufs[3].ptr, None, rcb.ptr, None, s.ptr), "update_batch_device")
+        res = stage.DeviceBuffer(4 * n)
+        check(stage.lib().stage_tpcc_stock_level(tt.dist.h, tt.ol.h, tt.stock.h, tx[0].ptr, tx[1].ptr, tx[2].ptr,
+                                                 None, n, res.ptr, s.ptr), "stock level")
+        kept.append((bufs, rcb))
+        steps.append((dk, nx, wi, ci, rcb, res))
+    s.sync()
+    check(stage.lib().stage_settle(tt.dist.h), "settle")
+    for dk, nx, wi, ci, rcb, res in steps:
+        rc = rcb.to_numpy(np.uint8, dk.shape[0])
+        for i in range(dk.shape[0]):
+            a = tt.odist.update(dk[i].tobytes(), 16, 0, nx[i].tobytes(), int(wi[i]))
+            if a == stage.RC_OK:
+                assert tt.odist.commit_update(dk[i].tobytes(), 16, int(ci[i]), int(ci[i])) == stage.RC_OK
+            assert rc[i] == a, (i, rc[i], a)
+        got = res.to_numpy(np.int32, n)
+        exp = np.array([tt.stock_level_oracle(int(a), int(b), int(c)) for a, b, c in zip(w, d, thr)])
+        assert (got == exp).all(), np.nonzero(got != exp)[0][:10]
