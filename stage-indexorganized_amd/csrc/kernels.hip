@@ -1729,7 +1729,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 //  a scan whose first visit decides nothing (no candidate passed, the visit held m <= e records
 //    and the scan has records left) is re-run by the general loop (scan_one_compact +
 //    FirstPrefixSink), which continues across leaves.
-template <int SPL, int KW, int WPE>
+// SKIP: a second pass behind scan_first_probe_kernel -- a chunk whose 16 scans that kernel
+// all decided is skipped (recomputing a decided scan would store the same result).
+template <int SPL, int KW, int WPE, bool SKIP = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void scan_first_split_kernel(
     DevTable t, const uint64_t *__restrict__ keys, uint64_t n, uint32_t scan_size, const uint32_t *__restrict__ rids,
     uint32_t words, uint32_t *__restrict__ img_out, uint8_t *__restrict__ st_out) {
@@ -1744,6 +1746,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     uint32_t *ls = s_slot[wv];
     constexpr uint16_t kHole = 0xFFFF;
     for (uint64_t c0 = wave * kFirstChunk; c0 < n; c0 += nwaves * kFirstChunk) {
+        if constexpr (SKIP) {
+            const uint64_t q = c0 + lane;
+            if (!ballot(lane < (uint32_t)kFirstChunk && q < n && st_out[q] == kFirstUndecided)) continue;
+        }
         const uint64_t i = c0 + (lane >> 2);  // the scan this lane descends for
         const bool valid = i < n;
         uint64_t ok[KW];
@@ -2947,7 +2953,9 @@ hipError_t launch_scan_first(const DevTable &t, const uint64_t *keys, uint64_t n
     // (round 3: a third of the instructions and of the HBM bytes, but per-lane scattered key
     // loads -- no faster); -4 / -10 split at 7 / 6 waves/SIMD; -5 / -3 / -1 scan_first_fast_kernel with the
     // prefetch at 8 / 7 / 6 waves, -2 without it; -6 / -7 scan_first_seg_kernel (4 / 2 scans per
-    // pass); 1 the general single-scan kernel; 2 / 4 NS scans per wave in lockstep
+    // pass); 1 the general single-scan kernel; 2 / 4 NS scans per wave in lockstep; -11
+    // scan_first_probe_kernel (the start key's exact record as a point probe), then the split
+    // kernel on the chunks it left undecided, then the rest kernel
     const int ns = tune.first_scans;
     const uint64_t pchunks = (n + 63) / 64;
     const bool psmall = pchunks < 16384;  // as launch_probe: 16-scan chunks when 64-scan ones cannot fill the chip
@@ -2959,6 +2967,8 @@ hipError_t launch_scan_first(const DevTable &t, const uint64_t *keys, uint64_t n
             scan_first_probe_kernel<S, KW, 16><<<pblocks, 256, 0, s>>>(t, keys, n, rids, img_out, st_out);   \
         else                                                                                                \
             scan_first_probe_kernel<S, KW, 64><<<pblocks, 256, 0, s>>>(t, keys, n, rids, img_out, st_out);   \
+        scan_first_split_kernel<S, KW, 8, true><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words,   \
+                                                                       img_out, st_out);                    \
         scan_first_rest_kernel<S, KW><<<grid_for((n + 63) / 64, 4, 4096), 256, 0, s>>>(t, keys, n, scan_size,  \
                                                                                     rids, words, img_out,   \
                                                                                     st_out);                \
