@@ -137,6 +137,7 @@ struct DeviceStore {
         CK(stage_probe_batch(t, (const uint64_t *)dk, nullptr, (const uint32_t *)dr, nullptr, 1, (stage_probe_out *)dout,
                              (uint8_t *)drow, nullptr));
         CK(stage_probe_identify(t, (const stage_probe_out *)dout, 1, (stage_probe_ident *)did, nullptr));
+        CK(stage_device_sync());  // the probe ran on the table's stream, the copies use the null stream
         stage_probe_out o;
         stage_probe_ident id;
         CK(stage_memcpy_d2h(&o, dout, 32, nullptr));

@@ -101,6 +101,7 @@ int probe_mode(const char *path) {
     CK(stage_probe_batch(t, (const uint64_t *)dk, nullptr, (const uint32_t *)dr, nullptr, n, (stage_probe_out *)dout,
                          (uint8_t *)drow, nullptr));
     CK(stage_probe_identify(t, (const stage_probe_out *)dout, n, (stage_probe_ident *)did, nullptr));
+    CK(stage_device_sync());  // the probe ran on the table's stream, the copies use the null stream
     CK(stage_memcpy_d2h(outs.data(), dout, 32 * n, nullptr));
     CK(stage_memcpy_d2h(ids.data(), did, 8 * n, nullptr));
     CK(stage_memcpy_d2h(wide.data(), drow, (uint64_t)stride * n, nullptr));

@@ -29,7 +29,7 @@ def scenario(tab, orc):
         upd = (lambda k, b, w: t.update(k, 0, bytes([b]) * 100, w)) if t else \
               (lambda k, b, w: o.update(k, 8, 0, bytes([b]) * 100, w))
         com = (lambda k, c: t.commit_update(k, c, c)) if t else (lambda k, c: o.commit_update(k, 8, c, c))
-        abt = (lambda k: t.abort_update(k)) if t else (lambda k: o.abort_update(k, 8))
+        abt = (lambda k: t.abort_update_key(int(k).to_bytes(8, "little"))) if t else (lambda k: o.abort_update(k, 8))
         assert upd(3, 7, 1) == 1 and com(3, 2) == 1
         assert upd(5, 55, 8) == 1
         assert upd(7, 77, 10) == 1 and abt(7) == 1
