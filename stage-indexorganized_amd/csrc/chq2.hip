@@ -19,9 +19,12 @@
 // one finishing kernel.  Updates go through the device write path when a commit id is given.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
+
+#include <hipcub/hipcub.hpp>
 
 #include "handle.hpp"
 
@@ -57,6 +60,21 @@ __global__ void q2_gather(const uint64_t *__restrict__ map_keys, const uint64_t 
         keys[2 * (dst[s] + e)] = map_keys[2 * (src[s] + e)];
         keys[2 * (dst[s] + e) + 1] = map_keys[2 * (src[s] + e) + 1];
     }
+}
+
+__global__ void q2_iota(uint32_t *__restrict__ v, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) v[i] = (uint32_t)i;
+}
+
+// the stock keys in leaf order: out[j] = keys[perm[j]] (2 words each)
+__global__ void q2_permute_keys(const uint64_t *__restrict__ keys, const uint32_t *__restrict__ perm, uint64_t m,
+                                uint64_t *__restrict__ out) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= m) return;
+    const uint64_t p = perm[j];
+    out[2 * j] = keys[2 * p];
+    out[2 * j + 1] = keys[2 * p + 1];
 }
 
 // one wave per supplier: abort if any stock lookup of its segment produced no tuple; the last
@@ -231,6 +249,19 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
             dst[k] = m;
             m += cnt[k];
         }
+        // STAGE_Q2_SORT=1: the STOCK keys probed in leaf order (their descents first, a radix sort of
+        // (leaf, position), the probe from the known leaves, results written back in place by the
+        // per-read-id revisit) -- neighbouring probes share leaf heads and bottom nodes in L2
+        const char *qs = std::getenv("STAGE_Q2_SORT");
+        const bool sorted = m > 1 && qs && qs[0] == '1';
+        const DevTable &sv0 = stock->dev.view;
+        int lbits = 1;
+        while (lbits < 32 && (1ull << lbits) <= sv0.nleaves) ++lbits;
+        size_t cub_bytes = 0;
+        if (sorted)
+            hip_check(hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                                         (uint32_t *)nullptr, (uint32_t *)nullptr, (int)m, 0, lbits, s),
+                      "sort size");
         auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
         uint64_t off = 0;
         auto take = [&](uint64_t bytes) {
@@ -241,7 +272,10 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         const uint64_t o_src = take(n * 8), o_dst = take(n * 8), o_cnt = take(n * 4), o_sup = take(n * 8),
                        o_keys = take(std::max<uint64_t>(m, 1) * 16), o_rids = take(std::max<uint64_t>(m, 1) * 4),
                        o_irids = take(n * 4 * nq), o_rq = take(nq * 4),
-                       o_sbase = take(nq > 1 ? std::max<uint64_t>(m, 1) * 32 : 0),
+                       o_sbase = take(nq > 1 || sorted ? std::max<uint64_t>(m, 1) * 32 : 0),
+                       o_leaf = take(sorted ? m * 4 : 0), o_sleaf = take(sorted ? m * 4 : 0),
+                       o_iota = take(sorted ? m * 4 : 0), o_perm = take(sorted ? m * 4 : 0),
+                       o_skeys = take(sorted ? m * 16 : 0), o_cub = take(sorted ? cub_bytes : 0),
                        o_sout = take(std::max<uint64_t>(m, 1) * 32 * nq),
                        o_rec = take(n * sizeof(stage_q2_rec) * nq), o_ik = take(n * 8 * nq),
                        o_iout = take(n * 32 * nq), o_ibase = take(nq > 1 ? n * 32 : 0), o_ab = take(4 * nq);
@@ -267,11 +301,26 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         // every query of the batch looks up the same STOCK keys (the visited suppliers and their
         // supp_stock_map do not depend on the read id): each key is probed once and its hit slot's
         // visibility evaluated at every query's read id (launch_revisit)
-        if (m) {
+        if (sorted) {
+            auto *d_leaf = (uint32_t *)(buf + o_leaf), *d_sleaf = (uint32_t *)(buf + o_sleaf);
+            auto *d_iota = (uint32_t *)(buf + o_iota), *d_perm = (uint32_t *)(buf + o_perm);
+            auto *d_skeys = (uint64_t *)(buf + o_skeys);
+            const unsigned mb = (unsigned)((m + 255) / 256);
+            hip_check(launch_resolve(sv, d_keys, nullptr, m, 1, d_leaf, s), "stock descents");
+            q2_iota<<<mb, 256, 0, s>>>(d_iota, m);
+            size_t cb = cub_bytes;
+            hip_check(hipcub::DeviceRadixSort::SortPairs(buf + o_cub, cb, d_leaf, d_sleaf, d_iota, d_perm, (int)m, 0,
+                                                         lbits, s),
+                      "stock leaf sort");
+            q2_permute_keys<<<mb, 256, 0, s>>>(d_keys, d_perm, m, d_skeys);
+            hip_check(launch_probe(sv, d_skeys, nullptr, d_rids, d_sleaf, m, d_sbase, nullptr, s, stock->tune),
+                      "stock probe");
+            hip_check(launch_revisit(sv, d_sbase, m, d_rq, nq, d_perm, d_sout, s), "stock read ids");
+        } else if (m) {
             hip_check(launch_probe(sv, d_keys, nullptr, d_rids, nullptr, m, nq > 1 ? d_sbase : d_sout, nullptr, s,
                                    stock->tune),
                       "stock probe");
-            if (nq > 1) hip_check(launch_revisit(sv, d_sbase, m, d_rq, nq, d_sout, s), "stock read ids");
+            if (nq > 1) hip_check(launch_revisit(sv, d_sbase, m, d_rq, nq, nullptr, d_sout, s), "stock read ids");
         }
         q2_reduce<<<n * nq, 64, 0, s>>>(d_sout, d_keys, d_dst, d_cnt, d_sup, sv.heap, sv.hstride,
                                         facts(stock).key_pad(), n, m, d_rec, d_ik, d_ab);
@@ -279,7 +328,7 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         // filter
         hip_check(launch_probe(iv, d_ik, nullptr, d_irids, nullptr, n, nq > 1 ? d_ibase : d_iout, nullptr, s, item->tune),
                   "item probe");
-        if (nq > 1) hip_check(launch_revisit(iv, d_ibase, n, d_rq, nq, d_iout, s), "item read ids");
+        if (nq > 1) hip_check(launch_revisit(iv, d_ibase, n, d_rq, nq, nullptr, d_iout, s), "item read ids");
         q2_finish<<<(n * nq + 255) / 256, 256, 0, s>>>(d_iout, iv.heap, iv.hstride, facts(item).key_pad(), n, nq,
                                                        d_rec, d_ab);
         hip_check(hipGetLastError(), "q2 kernels");

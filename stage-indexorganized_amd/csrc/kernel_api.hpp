@@ -85,9 +85,10 @@ struct ReaderRing {
 hipError_t launch_resident_reader(const DevTable &t, const ReaderRing &g, hipStream_t s);
 // the probes of one key set at several read ids: base[0..n) holds probe results (any read id) of
 // n keys; out[q * n + i] = the result of key i at rids[q], q < nq -- the hit slot is the same for
-// every read id (SearchRecordMeta does not depend on it), only the visibility walk is redone
+// every read id (SearchRecordMeta does not depend on it), only the visibility walk is redone;
+// perm (may be null): base[i] is key perm[i]'s result, written to out[q * n + perm[i]]
 hipError_t launch_revisit(const DevTable &t, const stage_probe_out_dev *base, uint64_t n, const uint32_t *rids,
-                          uint32_t nq, stage_probe_out_dev *out, hipStream_t s);
+                          uint32_t nq, const uint32_t *perm, stage_probe_out_dev *out, hipStream_t s);
 // stage_probe_ident: {location handle, next handle} of each probe's hit slot (two u32 per probe)
 hipError_t launch_ident(const DevTable &t, const stage_probe_out_dev *out, uint64_t n, uint32_t *ident, hipStream_t s);
 hipError_t launch_murmur(const void *keys, uint32_t key_len, uint32_t key_stride, uint64_t seed, uint64_t n,

@@ -2808,6 +2808,7 @@ bool probe_fanout_supported(const DevTable &t) {
 // in-flight insert without a copy) holds for every read id and is copied as it is
 __global__ __launch_bounds__(256) void revisit_kernel(DevTable t, const stage_probe_out_dev *__restrict__ base,
                                                       uint64_t n, const uint32_t *__restrict__ rids, uint32_t nq,
+                                                      const uint32_t *__restrict__ perm,
                                                       stage_probe_out_dev *__restrict__ out) {
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= n * nq) return;
@@ -2821,15 +2822,15 @@ __global__ __launch_bounds__(256) void revisit_kernel(DevTable t, const stage_pr
         visibility(t, (int)slot, si.meta, si.next, si.image, rids[q], r);
         pack_out(leaf, r, a, b);
     }
-    u32x4 *op = reinterpret_cast<u32x4 *>(out + q * n + i);
+    u32x4 *op = reinterpret_cast<u32x4 *>(out + q * n + (perm ? perm[i] : i));
     op[0] = a;
     op[1] = b;
 }
 
 hipError_t launch_revisit(const DevTable &t, const stage_probe_out_dev *base, uint64_t n, const uint32_t *rids,
-                          uint32_t nq, stage_probe_out_dev *out, hipStream_t s) {
+                          uint32_t nq, const uint32_t *perm, stage_probe_out_dev *out, hipStream_t s) {
     if (n == 0 || nq == 0) return hipSuccess;
-    revisit_kernel<<<(unsigned)((n * nq + 255) / 256), 256, 0, s>>>(t, base, n, rids, nq, out);
+    revisit_kernel<<<(unsigned)((n * nq + 255) / 256), 256, 0, s>>>(t, base, n, rids, nq, perm, out);
     return hipGetLastError();
 }
 

@@ -30,7 +30,9 @@ def ch(gpu):
     return c
 
 
-def test_q2_matches_oracle_all_regions(ch):
+@pytest.mark.parametrize("q2_sort", ["0", "1"])
+def test_q2_matches_oracle_all_regions(ch, monkeypatch, q2_sort):
+    monkeypatch.setenv("STAGE_Q2_SORT", q2_sort)  # 1: the STOCK keys probed in leaf order
     for target in range(5):
         recs, ab = ch.query2(target)
         orecs, oab = ch.query2_oracle(target)
@@ -39,7 +41,9 @@ def test_q2_matches_oracle_all_regions(ch):
     assert recs.size > 1000 and recs["update"].sum() > 0 and recs["item_has_b"].sum() > 0
 
 
-def test_q2_batch_equals_single_queries(ch):
+@pytest.mark.parametrize("q2_sort", ["0", "1"])
+def test_q2_batch_equals_single_queries(ch, monkeypatch, q2_sort):
+    monkeypatch.setenv("STAGE_Q2_SORT", q2_sort)
     rids = np.array([10, 0xFFFFFFFE, 3, 25, 0xFFFFFFFE, 7], np.uint32)
     for target in (0, 3):
         recs, ab = ch.query2_batch(rids, target)
@@ -54,7 +58,7 @@ def test_q2_batch_equals_single_queries(ch):
                 same(recs[q], orecs)
 
 
-def test_q2_visibility_and_commit(ch):
+def test_q2_visibility_and_commit(ch, monkeypatch):
     ostock = ch.orc["stock"]
     stock = ch.tables["stock"]
     recs, _ = ch.query2(3, read_id=10)
@@ -78,6 +82,13 @@ def test_q2_visibility_and_commit(ch):
             same(recs, orecs)
             same(brecs[q], orecs)
     assert ch.query2(3, read_id=10)[1]  # the abort case is exercised
+    monkeypatch.setenv("STAGE_Q2_SORT", "1")  # leaf-ordered STOCK probes: the same outcomes
+    srecs, sabort = ch.query2_batch(np.array([10, 25, 40, 0xFFFFFFFE], np.uint32), 3)
+    assert (sabort == babort).all()
+    for q in range(4):
+        if not babort[q]:
+            same(srecs[q], brecs[q])
+    monkeypatch.delenv("STAGE_Q2_SORT")
     # commit path: the transaction's updates through the device write path, mirrored on the oracle
     rid, cid = 50, 51
     recs, ab = ch.query2(3, read_id=rid, commit_id=cid)
