@@ -91,6 +91,9 @@ def parse(argv=None):
     p.add_argument("--scan-size", type=int, default=100)
     p.add_argument("--scan-batch", type=int, default=1 << 18, help="scans per step of the C4 leg")
     p.add_argument("--update-ratio", type=float, default=0.05)
+    p.add_argument("--reader-window", type=int, default=1280,
+                   help="c3: older-snapshot readers trail the newest id by up to this many ids (RunMixed: "
+                        "64 threads x 10 ops x 2 ids)")
     p.add_argument("--inflight-share", type=float, default=0.02,
                    help="c3: share of the update ops left in flight (uncommitted; keys beyond the 10^4 hottest) "
                         "so reads of them take the overwrite-copy (COPY) branch")
@@ -687,7 +690,8 @@ class YcsbB:
     write path (LeafNode::Update + CommitTransaction UPDATE entry, read / commit ids from one
     counter as tid_counter does) -- on the device (stage_update_batch_device) or on the host
     (stage_update_batch + incremental publish) -- and its read share with read ids: 75 %
-    current, 25 % drawn from the ids of this run so far (older snapshots).  A share of the
+    current, 25 % drawn from the last --reader-window ids (readers concurrent with the newest
+    writers: older snapshots a few commits back).  A share of the
     update ops (--inflight-share, keys beyond the 10^4 hottest) stays in flight (commit id 0),
     so later reads of those keys take the overwrite-copy (COPY) branch.
     Epochs are generated and their inputs uploaded to HBM before the timed loop (like the C2
@@ -719,7 +723,12 @@ class YcsbB:
         reads = np.ascontiguousarray(draws[~is_upd])
         rids = np.full(reads.size, self.counter, np.uint32)
         old = rng.random(reads.size) < 0.25
-        rids[old] = rng.integers(1, max(2, self.counter), int(old.sum())).astype(np.uint32)
+        # an older snapshot is a reader running beside the writers (RunMixed's threads): its id
+        # trails the newest commit by at most the ids its concurrent transactions take, not by
+        # the whole run -- with RunMixed's update stream every update adds a version, so a hot
+        # key's chain grows by ~10^4 per epoch and a reader at a random historical id would walk it
+        win = max(2, min(self.counter, a.reader_window))
+        rids[old] = (self.counter - rng.integers(1, win, int(old.sum()))).astype(np.uint32)
         ep = {"keys": keys, "colb": colb, "rid": rid, "cid": cid, "inflight": int(k_in), "reads": reads, "rids": rids}
         self.record.append(ep)
         self.epoch += 1
@@ -1310,6 +1319,7 @@ def c3_leg(tab, args, stream, nthreads, steps, warmup):
                     "update_stream": "RunMixed: FastRandom NextUniform() < update_ratio, delta = 100 x next_char() "
                                      "(ycsb_mixed.cpp:26-44)",
                     "inflight_share": args.inflight_share, "updates_applied": updates,
+                    "read_ids": f"75 % the newest id, 25 % up to {args.reader_window} ids older (concurrent readers)",
                     "update_ops": int(sum(ep["keys"].size for ep in epochs[warm:])),
                     "updates_in_flight": int(sum(ep["inflight"] for ep in epochs[warm:])),
                     # why update ops fail: not_needed_update = the column already holds the value
@@ -1456,13 +1466,17 @@ def main(argv=None):
             b.free()
         if not args.no_extras:
             # the other single-GPU configs on the same loaded table: C4, then C3 (mutates it)
+            log(f"[rank {rank}] C2: {head['value'] / 1e9:.3f} G lookups/s; C4 leg")
             extras["c4"], samples["c4"] = c4_leg(tab, args, total_rows, rank, stream, 5, 1)
+            log(f"[rank {rank}] C4: {extras['c4']['value'] / 1e6:.1f} M scans/s; C3 leg")
             extras["c3"], samples["c3"] = c3_leg(tab, args, stream, nthreads, args.c3_epochs, 1)
+            log(f"[rank {rank}] C3: {extras['c3']['value'] / 1e9:.3f} G reads/s")
     if not head["self_check"]:
         log(f"[rank {rank}] SELF-CHECK FAILED")
 
     cpu = None
     if cpu_leg:
+        log(f"[rank {rank}] CPU legs ({nthreads} threads)")
         legs = cpu_legs(orc, args, res, nthreads, c2_check=samples.get("c2"), c4_check=samples.get("c4"),
                         c3=samples.get("c3"))
         legs["c2"]["calibration"] = cpu_calibration(orc.O, nthreads)

@@ -10,6 +10,8 @@
   waiting) follows AddReader / IncreaseWRCount / DecreaseWRCount / UpdatePs and the writer's
   commit / abort -- also for copies the device write path created (their writer ids come back
   with the epoch's adoption)."""
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -116,12 +118,12 @@ def test_copy_state_follows_the_pool_calls(tables):
     assert (s["cstamp"], s["pstamp"], s["rstamp"], s["sstamp"], s["waiting"]) == (8, 8, 0, 0xFFFFFFFF, 0)
     assert s["reader_ids"] == [] and s["count"] == 0
     L = stage.lib()
-    ok = np.zeros(1, np.int32)
+    ok = ctypes.c_int(0)
     for rid in (21, 22):
         stage.table.check(L.stage_copy_add_reader(tab.h, cid, rid), "add_reader")
-        stage.table.check(L.stage_copy_wr_count(tab.h, cid, 1, ok.ctypes.data), "wr+")
-        assert ok[0] == 1
-    stage.table.check(L.stage_copy_wr_count(tab.h, cid, -1, ok.ctypes.data), "wr-")
+        stage.table.check(L.stage_copy_wr_count(tab.h, cid, 1, ctypes.byref(ok)), "wr+")
+        assert ok.value == 1
+    stage.table.check(L.stage_copy_wr_count(tab.h, cid, -1, ctypes.byref(ok)), "wr-")
     stage.table.check(L.stage_copy_update_ps(tab.h, cid, 30), "ps")
     s = tab.copy_state(cid)
     assert s["reader_ids"] == [21, 22] and s["readers"] == 2 and s["count"] == 1 and s["pstamp"] == 30
