@@ -217,7 +217,7 @@ void HostTable::adopt_device_epoch(const CopyHdr *copies, const uint32_t *writer
     versions_.insert(versions_.end(), versions, versions + nv);
     {
         std::lock_guard<std::mutex> g(ssn_.mu);
-        ssn_.e.reserve(c0 + nc);
+        room(ssn_.e, nc);  // not reserve(c0 + nc): an exact reserve reallocates every epoch
         for (uint64_t k = 0; k < nc; ++k) {
             const uint32_t w = writers ? writers[k] : 0;
             ssn_.e.push_back(CopySsn{w, w, copies[k].rstamp, copies[k].sstamp, 0,
@@ -898,7 +898,7 @@ uint64_t HostTable::update_batch(const uint8_t *keys, uint32_t key_stride, uint6
     lap("concat");
     {
         std::lock_guard<std::mutex> g(ssn_.mu);
-        ssn_.e.reserve(c0);
+        if (ssn_.e.capacity() < c0) ssn_.e.reserve(std::max<size_t>(c0, 2 * ssn_.e.capacity()));
         for (unsigned t = 0; t < nt; ++t)
             for (size_t k = 0; k < lw[t].copies.size(); ++k) {
                 const CopyHdr &c = lw[t].copies[k];
