@@ -302,8 +302,26 @@ __global__ __launch_bounds__(256) void wp_finish_groups(WpArgs a, WpCls kc, DevT
                 }
             }
             if (kf >= 0) {
-                last = (int64_t)(pos + 64 * (uint64_t)kf + first);
-                pos = (uint64_t)last + 1;
+                // ops after a success hold their speculative outcome (evaluated against their
+                // predecessor as a success: exact now) up to the next speculative failure,
+                // which is exact too; re-evaluation resumes behind it
+                const uint64_t bq = pos + 64 * (uint64_t)kf + first;
+                uint64_t nf = ~0ull;
+                for (uint64_t s0 = bq + 1; s0 < a.n && nf == ~0ull; s0 += 64 * kFinishChunks) {
+                    bool more = true;
+#pragma unroll
+                    for (int k = 0; k < kFinishChunks; ++k) {
+                        const uint64_t q = s0 + 64 * k + lane;
+                        const bool ing = q < a.n && a.loc[q] == l;
+                        const uint64_t fm = __builtin_amdgcn_ballot_w64(ing && !succ[q]);
+                        if (nf == ~0ull && fm) nf = s0 + 64 * k + (uint64_t)__builtin_ctzll(fm);
+                        more = more && __builtin_amdgcn_ballot_w64(ing) == ~0ull;
+                    }
+                    if (!more) break;  // the group ends inside this stretch
+                }
+                if (nf == ~0ull) break;  // no failure left: the rest of the group stands
+                last = (int64_t)nf - 1;
+                pos = nf + 1;
                 continue;
             }
             if (!whole) break;  // the group ends inside this pass
@@ -379,8 +397,29 @@ __global__ __launch_bounds__(1024) void wp_finish_big(WpArgs a, WpCls kc, DevTab
                 }
             }
             if (bf != ~0ull) {
-                last = (int64_t)bf;
-                pos = bf + 1;
+                // as wp_finish_groups: the speculative outcomes behind a success stand up to
+                // and including the next speculative failure
+                uint64_t nf = ~0ull;
+                for (uint64_t s0 = bf + 1; s0 < end && nf == ~0ull; s0 += kPass) {
+                    uint64_t mf = ~0ull;
+#pragma unroll
+                    for (int k = 0; k < kFinishChunks; ++k) {
+                        const uint64_t q = s0 + (uint64_t)wv * (kFinishChunks * 64) + 64 * k + lane;
+                        if (q < end && !succ[q] && q < mf) mf = q;
+                    }
+                    for (int o = 32; o > 0; o >>= 1) {
+                        const uint64_t x = __shfl_xor(mf, o, 64);
+                        mf = x < mf ? x : mf;
+                    }
+                    __syncthreads();
+                    if (lane == 0) s_first[wv] = mf;
+                    __syncthreads();
+#pragma unroll
+                    for (int w = 0; w < 16; ++w) nf = s_first[w] < nf ? s_first[w] : nf;
+                }
+                if (nf == ~0ull) break;
+                last = (int64_t)nf - 1;
+                pos = nf + 1;
             } else {
                 pos += kPass;
             }

@@ -192,12 +192,14 @@ def test_device_epoch_edge_cases(gpu):
         check_probe(tab, orc, keys, 8, read_ids=np.full(keys.size, rid, np.uint32))
 
 
-def test_hot_key_groups_finished_by_workgroups(gpu):
+@pytest.mark.parametrize("alphabet", [3, 256])
+def test_hot_key_groups_finished_by_workgroups(gpu, alphabet):
     """Groups longer than the workgroup finisher's threshold (wp_finish_big, 2048 ops from the
     first failure): three hot keys hammered ~6000 times each in one epoch with a 3-letter delta
-    alphabet (NotNeededUpdate and successes interleave), some writers older than the record
-    (NotNeededUpdate by cstamp) and a few left in flight (the rest of that group DIRTY) --
-    return codes, versions and reads equal to the oracle applied op by op."""
+    alphabet (NotNeededUpdate and successes interleave) or RunMixed's 256 (successes with sparse
+    failures: the speculative outcomes behind each re-evaluated success stand), some writers
+    older than the record (NotNeededUpdate by cstamp) and a few left in flight (the rest of that
+    group DIRTY) -- return codes, versions and reads equal to the oracle applied op by op."""
     n = 20000
     tab = stage.Table(key_width=8)
     tab.load_ycsb(0, n, 8, mode=1)
@@ -210,7 +212,7 @@ def test_hot_key_groups_finished_by_workgroups(gpu):
         m = 24000
         hot = np.array([3, 1000, 19999], np.uint64)
         keys = np.where(rng.random(m) < 0.75, rng.choice(hot, m), rng.integers(0, n + 50, m)).astype(np.uint64)
-        deltas = rng.integers(0, 3, (m, 1), dtype=np.uint8).repeat(16, 1)
+        deltas = rng.integers(0, alphabet, (m, 1), dtype=np.uint8).repeat(16, 1)
         wid = (counter + 2 * np.arange(m)).astype(np.uint32)
         wid[rng.random(m) < 0.02] = 1
         cid = (wid + 1).astype(np.uint32)
@@ -222,7 +224,11 @@ def test_hot_key_groups_finished_by_workgroups(gpu):
         bad = np.nonzero(rc != exp)[0]
         assert bad.size == 0, (epoch, bad[:5], rc[bad[:5]], exp[bad[:5]], keys[bad[:5]])
         assert ok == int((exp == stage.RC_OK).sum())
-        assert (keys == hot[0]).sum() > 4096 and (exp[keys == hot[0]] == stage.RC_NOT_NEEDED_UPDATE).sum() > 1000
+        assert (keys == hot[0]).sum() > 4096
+        if alphabet == 3:
+            assert (exp[keys == hot[0]] == stage.RC_NOT_NEEDED_UPDATE).sum() > 1000
+        else:
+            assert (exp[keys == hot[0]] == stage.RC_OK).sum() > 4000 and (exp[keys == hot[0]] != stage.RC_OK).sum() > 50
         probe = np.concatenate([hot, rng.integers(0, n, 2000).astype(np.uint64)])
         for rid in (0, counter // 3, counter // 2, counter - 5, 0xFFFFFFFE):
             check_probe(tab, orc, probe, 8, read_ids=np.full(probe.size, rid, np.uint32))
