@@ -33,6 +33,9 @@ run fs_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/fs
 run q2_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/q2_trace -o q2 -- $B --config chq2 --steps 3 --warmup 1
 run q2_sq 300 rocprofv3 --pmc $SQ --output-format csv -d $OUT/q2_sq -o q2 -- $B --config chq2 --steps 3 --warmup 1
 run q2_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/q2_fetch -o q2 -- $B --config chq2 --steps 3 --warmup 1
+export STAGE_Q2_SORT=1
+run q2s_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/q2s_trace -o q2s -- $B --config chq2 --steps 3 --warmup 1
+unset STAGE_Q2_SORT
 run sl_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/sl_trace -o sl -- $B --config tpcc --steps 5 --warmup 1
 run sl_sq 300 rocprofv3 --pmc $SQ --output-format csv -d $OUT/sl_sq -o sl -- $B --config tpcc --steps 3 --warmup 1
 run sl_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/sl_fetch -o sl -- $B --config tpcc --steps 3 --warmup 1
