@@ -218,11 +218,15 @@ void HostTable::adopt_device_epoch(const CopyHdr *copies, const uint32_t *writer
     {
         std::lock_guard<std::mutex> g(ssn_.mu);
         room(ssn_.e, nc);  // not reserve(c0 + nc): an exact reserve reallocates every epoch
-        for (uint64_t k = 0; k < nc; ++k) {
-            const uint32_t w = writers ? writers[k] : 0;
-            ssn_.e.push_back(CopySsn{w, w, copies[k].rstamp, copies[k].sstamp, 0,
-                                     (uint8_t)(copies[k].sstamp != kMaxCid), 0});
-        }
+        const uint64_t e0 = ssn_.e.size();
+        ssn_.e.resize(e0 + nc);
+        CopySsn *dst = ssn_.e.data() + e0;
+        parallel_chunks(nc, [&](uint64_t b, uint64_t e) {
+            for (uint64_t k = b; k < e; ++k) {
+                const uint32_t w = writers ? writers[k] : 0;
+                dst[k] = CopySsn{w, w, copies[k].rstamp, copies[k].sstamp, 0, (uint8_t)(copies[k].sstamp != kMaxCid), 0};
+            }
+        });
     }
     lap("headers");
     if (nimages) {

@@ -120,7 +120,7 @@ struct CopySsn {
 class CopySsnTable {
 public:
     std::mutex mu;
-    std::vector<CopySsn> e;                                      // by copy id
+    std::vector<CopySsn, HugeAlloc<CopySsn>> e;                  // by copy id (an epoch appends ~10^6)
     std::unordered_map<uint32_t, std::vector<uint32_t>> readers;  // copy id -> AddReader ids
     // EphemeralPool::Allocate (ephemeral_pool.cpp:17-44): cstamp = pstamp = writer, sstamp MAX
     void created(uint64_t id, uint32_t writer, uint32_t rstamp);

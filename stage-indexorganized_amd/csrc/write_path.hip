@@ -367,34 +367,29 @@ __global__ __launch_bounds__(1024) void wp_finish_big(WpArgs a, WpCls kc, DevTab
         int64_t last = f > g ? (int64_t)f - 1 : -1;  // [g, f) all succeeded
         uint64_t pos = f;
         while (pos < end) {
-            uint8_t r[kFinishChunks];
-            uint64_t mine_first = ~0ull;
+            // a pass: up to kFinishChunks slices of 1024 ops (one 64-op chunk per wave), evaluated
+            // against the last success slice by slice until one holds a success -- behind a
+            // single failure the next op usually succeeds, so most passes take one slice
+            uint64_t bf = ~0ull, done = pos;
+            for (int k = 0; k < kFinishChunks && bf == ~0ull && done < end; ++k) {
+                const uint64_t q = done + (uint64_t)wv * 64 + lane;
+                const uint8_t r = q < end ? wp_eval(a, kc, t, q, g, last, base) : (uint8_t)0xFF;
+                uint64_t wf = r == STAGE_RC_OK ? q : ~0ull;  // the wave's first success, then the block's
+                for (int o = 32; o > 0; o >>= 1) {
+                    const uint64_t x = __shfl_xor(wf, o, 64);
+                    wf = x < wf ? x : wf;
+                }
+                __syncthreads();  // the previous slice's readers of s_first are done
+                if (lane == 0) s_first[wv] = wf;
+                __syncthreads();
 #pragma unroll
-            for (int k = 0; k < kFinishChunks; ++k) {
-                const uint64_t q = pos + (uint64_t)wv * (kFinishChunks * 64) + 64 * k + lane;
-                r[k] = q < end ? wp_eval(a, kc, t, q, g, last, base) : (uint8_t)0xFF;
-                if (r[k] == STAGE_RC_OK && q < mine_first) mine_first = q;
-            }
-            // the wave's first success, then the block's
-            uint64_t wf = mine_first;
-            for (int o = 32; o > 0; o >>= 1) {
-                const uint64_t x = __shfl_xor(wf, o, 64);
-                wf = x < wf ? x : wf;
-            }
-            __syncthreads();  // the previous pass's readers of s_first are done
-            if (lane == 0) s_first[wv] = wf;
-            __syncthreads();
-            uint64_t bf = ~0ull;
-#pragma unroll
-            for (int w = 0; w < 16; ++w) bf = s_first[w] < bf ? s_first[w] : bf;
-#pragma unroll
-            for (int k = 0; k < kFinishChunks; ++k) {
-                const uint64_t q = pos + (uint64_t)wv * (kFinishChunks * 64) + 64 * k + lane;
+                for (int w = 0; w < 16; ++w) bf = s_first[w] < bf ? s_first[w] : bf;
                 if (q < end && q <= bf) {
-                    rcs[q] = r[k];
+                    rcs[q] = r;
                     succ[q] = q == bf;
                     prev[q] = (int32_t)last;
                 }
+                done += 1024;
             }
             if (bf != ~0ull) {
                 // as wp_finish_groups: the speculative outcomes behind a success stand up to
@@ -421,7 +416,7 @@ __global__ __launch_bounds__(1024) void wp_finish_big(WpArgs a, WpCls kc, DevTab
                 last = (int64_t)nf - 1;
                 pos = nf + 1;
             } else {
-                pos += kPass;
+                pos = done;
             }
         }
     }
