@@ -9,6 +9,9 @@ rows left at the owner), coalescing on.  The direct probe's results are taken fi
 100M-row table is released before the shards are built (both at once would not leave room for
 the exchange buffers in 288 GB).  Reference semantics: executor.h:374-454 (IndexScanExecutor
 point lookup) through BTree::Read (b_tree.cpp:2066-2129) on every shard."""
+import sys
+import time
+
 import numpy as np
 import pytest
 
@@ -23,7 +26,12 @@ PER_RANK = 1 << 21  # 2^24 keys in all
 
 
 @pytest.mark.timeout(900)
+def _say(t0, what):  # progress on stderr: each phase takes tens of seconds at this size
+    print(f"[c5 at size] {time.time() - t0:6.1f}s {what}", file=sys.stderr, flush=True)
+
+
 def test_c5_loopback_at_size_equals_one_table(gpu):
+    t0 = time.time()
     rng = np.random.default_rng(0xC5)
     per_keys = []
     for r in range(W):
@@ -32,10 +40,13 @@ def test_c5_loopback_at_size_equals_one_table(gpu):
         k = np.concatenate([k, absent])
         per_keys.append(k[rng.permutation(k.size)].astype(np.uint64))
     # 1. the direct probe of one 100M-row table (LoadYCSBRows rows)
+    _say(t0, "batches drawn")
     full = stage.Table(key_width=8)
     assert full.load_ycsb(0, N, 8, 0) == N
     full.sync()
+    _say(t0, "100M-row table loaded")
     ref = [full.probe(k) for k in per_keys]
+    _say(t0, "direct probes done")
     full.close()
     del full
     # 2. the shards: rank r holds the keys with MurmurHash64A(key, 8, 0) % 8 == r, ascending
@@ -48,12 +59,14 @@ def test_c5_loopback_at_size_equals_one_table(gpu):
         assert t.load_keys(mine, 8, mode=0) == mine.size
         t.sync()
         tabs.append(t)
+        _say(t0, f"shard {r} loaded ({mine.size} rows)")
     del keys, own
     for t in tabs:
         stage.set_shard_dedupe(t, 1)
     fields = ("status", "flags", "hops", "key_len", "cstamp", "rec_cstamp", "copy_sstamp")
     # 3. rows back to the caller
     res = stage.probe_sharded_loopback(tabs, per_keys, None)
+    _say(t0, "sharded probe, rows mode")
     routed = 0
     for r in range(W):
         out, rows = res[r]
@@ -68,6 +81,7 @@ def test_c5_loopback_at_size_equals_one_table(gpu):
     del res
     # 4. rows left at their owners, status records back (each carries the owner-local row index)
     res = stage.probe_sharded_loopback(tabs, per_keys, None, records=True, reply=stage.REPLY_OWNER)
+    _say(t0, "sharded probe, owner mode")
     owner_rows = []
     for t in tabs:
         ptr, cnt = stage.owner_rows(t, loopback=True)
