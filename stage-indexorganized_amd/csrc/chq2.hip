@@ -27,6 +27,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "handle.hpp"
+#include "radix_sort.hpp"
 
 using namespace stage_capi;
 
@@ -259,8 +260,8 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         while (lbits < 32 && (1ull << lbits) <= sv0.nleaves) ++lbits;
         size_t cub_bytes = 0;
         if (sorted)
-            hip_check(hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, (uint32_t *)nullptr, (uint32_t *)nullptr,
-                                                         (uint32_t *)nullptr, (uint32_t *)nullptr, (int)m, 0, lbits, s),
+            hip_check(sort_pairs(nullptr, cub_bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                 (const uint32_t *)nullptr, (uint32_t *)nullptr, m, 0, lbits, s),
                       "sort size");
         auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
         uint64_t off = 0;
@@ -309,8 +310,8 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
             hip_check(launch_resolve(sv, d_keys, nullptr, m, 1, d_leaf, s), "stock descents");
             q2_iota<<<mb, 256, 0, s>>>(d_iota, m);
             size_t cb = cub_bytes;
-            hip_check(hipcub::DeviceRadixSort::SortPairs(buf + o_cub, cb, d_leaf, d_sleaf, d_iota, d_perm, (int)m, 0,
-                                                         lbits, s),
+            hip_check(sort_pairs(buf + o_cub, cb, (const uint32_t *)d_leaf, d_sleaf, (const uint32_t *)d_iota, d_perm, m, 0,
+                                 lbits, s),
                       "stock leaf sort");
             q2_permute_keys<<<mb, 256, 0, s>>>(d_keys, d_perm, m, d_skeys);
             hip_check(launch_probe(sv, d_skeys, nullptr, d_rids, d_sleaf, m, d_sbase, nullptr, s, stock->tune),

@@ -43,6 +43,7 @@
 #include <vector>
 
 #include "handle.hpp"
+#include "radix_sort.hpp"
 
 using namespace stage_capi;
 
@@ -730,8 +731,8 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
 
         // scratch
         size_t cub_sort = 0, cub_scan = 0, cub_sum = 0;
-        hip_check(hipcub::DeviceRadixSort::SortPairs(nullptr, cub_sort, (uint64_t *)nullptr, (uint64_t *)nullptr,
-                                                     (uint32_t *)nullptr, (uint32_t *)nullptr, (int)n, 0, end_bit, s),
+        hip_check(sort_pairs(nullptr, cub_sort, (const uint64_t *)nullptr, (uint64_t *)nullptr, (const uint32_t *)nullptr,
+                             (uint32_t *)nullptr, n, 0, end_bit, s),
                   "sort size");
         hip_check(hipcub::DeviceScan::InclusiveScan(nullptr, cub_scan, (uint32_t *)nullptr, (uint32_t *)nullptr,
                                                     hipcub::Max(), (int)n, s),
@@ -828,7 +829,7 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         hip_check(launch_probe(view, d_keys, d_lens, nullptr, nullptr, n, pout, nullptr, ks, t->tune), "locate");
         wp_keys<<<blocks_for(n, 256), 256, 0, ks>>>(pout, n, view.cap, none, loc0, op0);
         // 2. group
-        hip_check(hipcub::DeviceRadixSort::SortPairs(cub, cb, loc0, loc, op0, op, (int)n, 0, end_bit, ks), "sort");
+        hip_check(sort_pairs(cub, cb, (const uint64_t *)loc0, loc, (const uint32_t *)op0, op, n, 0, end_bit, ks), "sort");
         wp_heads<<<blocks_for(n, 256), 256, 0, ks>>>(loc, n, head);
         cb = cub_bytes;
         hip_check(hipcub::DeviceScan::InclusiveScan(cub, cb, head, gs, hipcub::Max(), (int)n, ks), "group starts");
