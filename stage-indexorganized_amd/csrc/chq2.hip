@@ -19,6 +19,8 @@
 // one finishing kernel.  Updates go through the device write path when a commit id is given.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -205,6 +207,14 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         using namespace stage;
         hip_check(hipSetDevice(stock->dev.device), "hipSetDevice");
         hipStream_t s = pick(stock, stream);
+        // STAGE_Q2_TRACE=1: host wall time of each phase on stderr
+        static const bool trace = std::getenv("STAGE_Q2_TRACE") != nullptr;
+        const auto t0 = std::chrono::steady_clock::now();
+        auto lap = [&](const char *what) {
+            if (trace)
+                std::fprintf(stderr, "[q2] %s %.1f us\n", what,
+                             std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+        };
         *n_out = 0;
         for (uint32_t q = 0; q < nq; ++q) aborted[q] = 0;
         // 1. REGION / NATION scans, SUPPLIER scan of every record, filtered on the host
@@ -221,7 +231,9 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         hip_check(hipGetLastError(), "dump leaves");
         std::vector<uint64_t> pairs(2 * nslots);
         hip_check(hipMemcpyAsync(pairs.data(), pbuf, nslots * 16, hipMemcpyDeviceToHost, s), "d2h");
+        lap("scans enqueued");
         hip_check(hipStreamSynchronize(s), "scan sync");  // the three scans complete together
+        lap("scans done");
         std::vector<uint64_t> sel;  // visited suppliers in visiting order
         for (uint32_t r = 0; r < nreg; ++r) {
             const uint8_t *rr = regs.data() + (uint64_t)r * rs;
@@ -237,6 +249,7 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
             }
         }
         const uint32_t n = (uint32_t)sel.size();
+        lap("suppliers selected");
         *n_out = n;
         if (n == 0) return STAGE_OK;
         // 2. stock keys of every visited supplier, one probe launch
@@ -337,7 +350,9 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         hip_check(hipMemcpyAsync(recs.data(), d_rec, recs.size() * sizeof(stage_q2_rec), hipMemcpyDeviceToHost, s),
                   "d2h");
         hip_check(hipMemcpyAsync(aborted, d_ab, 4 * nq, hipMemcpyDeviceToHost, s), "d2h");
+        lap("probes enqueued");
         hip_check(hipStreamSynchronize(s), "q2 sync");
+        lap("results back");
         const uint32_t read_id = rq[0];
         // 4. the transaction's stock updates, through the device write path
         if (nq == 1 && commit_id && !*aborted) {
@@ -382,6 +397,7 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         for (uint32_t q = 0; q < nq; ++q)
             std::memcpy(out + (uint64_t)q * max_out, recs.data() + (uint64_t)q * n,
                         std::min<uint64_t>(n, max_out) * sizeof(stage_q2_rec));
+        lap("out copied");
         return STAGE_OK;
     });
 }

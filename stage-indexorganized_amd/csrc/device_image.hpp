@@ -42,6 +42,13 @@ struct DeviceImage {
     void *pinned[2] = {nullptr, nullptr};  // pinned host staging of the epoch results
     uint64_t pinned_cap[2] = {0, 0};
     uint64_t heap_rows = 0;  // rows the heap buffer can hold
+    // the record heap in a reserved virtual range (HIP virtual memory management): a growth maps
+    // physical chunks behind the rows already there -- no copy of the heap, no second heap while
+    // it grows.  heap_vm_va == nullptr: a plain hipMalloc'd heap (STAGE_HEAP_VMM=0, or no VMM)
+    void *heap_vm_va = nullptr;
+    uint64_t heap_vm_reserved = 0, heap_vm_mapped = 0;
+    std::vector<uint64_t> heap_vm_handles;  // hipMemGenericAllocationHandle_t per mapped chunk
+    std::vector<uint64_t> heap_vm_sizes;
     DevTable view{};
     std::vector<uint32_t> host_to_dev;  // host leaf id -> leaf index in key order
     std::vector<uint32_t> dev_to_host;  // leaf index in key order -> host leaf id
