@@ -163,9 +163,9 @@ int64_t rd64(const uint8_t *p) {
     return v;
 }
 
-// TableScanExecutor rows of one scan from `start` (device scan, rows copied back to the host
-// asynchronously: the caller synchronises the stream before reading `count` or the rows)
-std::vector<uint8_t> scan_rows(stage_table *t, uint64_t start, uint32_t scan_size, uint32_t &count, hipStream_t s) {
+// TableScanExecutor rows of one scan from `start` (device scan; count and rows copied to the
+// pinned host destinations asynchronously: the caller synchronises the stream before reading)
+void scan_rows(stage_table *t, uint64_t start, uint32_t scan_size, uint32_t *count, uint8_t *rows_out, hipStream_t s) {
     const DevTable &v = t->dev.view;
     const uint64_t rows = (uint64_t)scan_size * v.stride;
     uint8_t *buf = scratch_bytes(t->dev, 64 + rows);
@@ -173,10 +173,8 @@ std::vector<uint8_t> scan_rows(stage_table *t, uint64_t start, uint32_t scan_siz
     auto *cnt = (uint32_t *)(buf + 8);
     q2_set_u64<<<1, 1, 0, s>>>(key, start);  // no host buffer outlives the call
     hip_check(launch_scan(v, key, nullptr, 1, scan_size, cnt, buf + 64, s, t->scan_tune), "scan");
-    std::vector<uint8_t> h(rows);
-    hip_check(hipMemcpyAsync(&count, cnt, 4, hipMemcpyDeviceToHost, s), "d2h");
-    hip_check(hipMemcpyAsync(h.data(), buf + 64, rows, hipMemcpyDeviceToHost, s), "d2h");
-    return h;
+    hip_check(hipMemcpyAsync(count, cnt, 4, hipMemcpyDeviceToHost, s), "d2h");
+    hip_check(hipMemcpyAsync(rows_out, buf + 64, rows, hipMemcpyDeviceToHost, s), "d2h");
 }
 
 }  // namespace
@@ -218,31 +216,40 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         *n_out = 0;
         for (uint32_t q = 0; q < nq; ++q) aborted[q] = 0;
         // 1. REGION / NATION scans, SUPPLIER scan of every record, filtered on the host
-        uint32_t nreg = 0, nnat = 0;
         const uint32_t rs = region->dev.view.stride, ns = nation->dev.view.stride;
-        const std::vector<uint8_t> regs = scan_rows(region, 0, kRegionScan, nreg, s);
-        const std::vector<uint8_t> nats = scan_rows(nation, 0, kNationScan, nnat, s);
         // SUPPLIER: every record, ScanLeafNode order
         const DevTable &pv = supplier->dev.view;
         const uint64_t nslots = (uint64_t)pv.nleaves * pv.cap;
+        // the host copies go through the stock table's pinned call staging (pageable copies
+        // are staged by the runtime and wait for each other): [counts][REGION rows][NATION
+        // rows][SUPPLIER (key, nation) pairs]
+        auto alp = [](uint64_t x) { return (x + 255) & ~255ull; };
+        const uint64_t p_regs = 256, p_nats = p_regs + alp((uint64_t)kRegionScan * rs),
+                       p_pairs = p_nats + alp((uint64_t)kNationScan * ns), p_end = p_pairs + nslots * 16;
+        uint8_t *pin = pinned_bytes(stock->dev, p_end, 2);
+        uint32_t *counts = (uint32_t *)pin;
+        scan_rows(region, 0, kRegionScan, counts, pin + p_regs, s);
+        scan_rows(nation, 0, kNationScan, counts + 1, pin + p_nats, s);
         uint8_t *pbuf = scratch_bytes(supplier->dev, nslots * 16);
         q2_dump_leaves<<<(unsigned)std::min<uint64_t>((nslots + 255) / 256, 4096), 256, 0, s>>>(
             pv, facts(supplier).key_pad(), (uint64_t *)pbuf);
         hip_check(hipGetLastError(), "dump leaves");
-        std::vector<uint64_t> pairs(2 * nslots);
-        hip_check(hipMemcpyAsync(pairs.data(), pbuf, nslots * 16, hipMemcpyDeviceToHost, s), "d2h");
+        hip_check(hipMemcpyAsync(pin + p_pairs, pbuf, nslots * 16, hipMemcpyDeviceToHost, s), "d2h");
+        const uint8_t *regs_p = pin + p_regs, *nats_p = pin + p_nats;
+        const uint64_t *pairs = (const uint64_t *)(pin + p_pairs);
         lap("scans enqueued");
         hip_check(hipStreamSynchronize(s), "scan sync");  // the three scans complete together
         lap("scans done");
+        const uint32_t nreg = counts[0], nnat = counts[1];
         std::vector<uint64_t> sel;  // visited suppliers in visiting order
         for (uint32_t r = 0; r < nreg; ++r) {
-            const uint8_t *rr = regs.data() + (uint64_t)r * rs;
+            const uint8_t *rr = regs_p + (uint64_t)r * rs;
             char name[56];
             std::memcpy(name, rr + 8, 55);
             name[55] = 0;
             if (std::string(name) != kRegions[target_region]) continue;
             for (uint32_t a = 0; a < nnat; ++a) {
-                const uint8_t *nr = nats.data() + (uint64_t)a * ns;
+                const uint8_t *nr = nats_p + (uint64_t)a * ns;
                 if (rd64(nr + 8) != rd64(rr)) continue;
                 for (uint64_t k = 0; k < nslots; ++k)
                     if (pairs[2 * k] != ~0ull && (int64_t)pairs[2 * k + 1] == rd64(nr)) sel.push_back(pairs[2 * k]);
@@ -252,9 +259,17 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         lap("suppliers selected");
         *n_out = n;
         if (n == 0) return STAGE_OK;
-        // 2. stock keys of every visited supplier, one probe launch
-        std::vector<uint64_t> src(n), dst(n);
-        std::vector<uint32_t> cnt(n);
+        // 2. stock keys of every visited supplier, one probe launch.  Pinned call staging again
+        // (the scans' contents are no longer needed: a growth may move it): [src][dst][cnt][sel]
+        // [read ids] going down, [records][aborted] coming back
+        const uint64_t q_src = 0, q_dst = q_src + alp(n * 8ull), q_cnt = q_dst + alp(n * 8ull),
+                       q_sel = q_cnt + alp(n * 4ull), q_rq = q_sel + alp(n * 8ull), q_rec = q_rq + alp(nq * 4ull),
+                       q_ab = q_rec + alp((uint64_t)n * nq * sizeof(stage_q2_rec)), q_end = q_ab + alp(nq * 4ull);
+        uint8_t *pq = pinned_bytes(stock->dev, q_end, 2);
+        uint64_t *src = (uint64_t *)(pq + q_src), *dst = (uint64_t *)(pq + q_dst);
+        uint32_t *cnt = (uint32_t *)(pq + q_cnt);
+        std::memcpy(pq + q_sel, sel.data(), n * 8ull);
+        std::memcpy(pq + q_rq, rq, nq * 4ull);
         uint64_t m = 0;
         for (uint32_t k = 0; k < n; ++k) {
             const uint64_t sk = sel[k];
@@ -302,11 +317,11 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         auto *d_sbase = (stage_probe_out_dev *)(buf + o_sbase), *d_ibase = (stage_probe_out_dev *)(buf + o_ibase);
         auto *d_rec = (stage_q2_rec *)(buf + o_rec);
         auto *d_ab = (int32_t *)(buf + o_ab);
-        hip_check(hipMemcpyAsync(d_src, src.data(), n * 8, hipMemcpyHostToDevice, s), "h2d");
-        hip_check(hipMemcpyAsync(d_dst, dst.data(), n * 8, hipMemcpyHostToDevice, s), "h2d");
-        hip_check(hipMemcpyAsync(d_cnt, cnt.data(), n * 4, hipMemcpyHostToDevice, s), "h2d");
-        hip_check(hipMemcpyAsync(d_sup, sel.data(), n * 8, hipMemcpyHostToDevice, s), "h2d");
-        hip_check(hipMemcpyAsync(d_rq, rq, nq * 4, hipMemcpyHostToDevice, s), "h2d");
+        hip_check(hipMemcpyAsync(d_src, src, n * 8, hipMemcpyHostToDevice, s), "h2d");
+        hip_check(hipMemcpyAsync(d_dst, dst, n * 8, hipMemcpyHostToDevice, s), "h2d");
+        hip_check(hipMemcpyAsync(d_cnt, cnt, n * 4, hipMemcpyHostToDevice, s), "h2d");
+        hip_check(hipMemcpyAsync(d_sup, pq + q_sel, n * 8, hipMemcpyHostToDevice, s), "h2d");
+        hip_check(hipMemcpyAsync(d_rq, pq + q_rq, nq * 4, hipMemcpyHostToDevice, s), "h2d");
         hip_check(hipMemsetAsync(d_ab, 0, 4 * nq, s), "memset");
         q2_fill_rids<<<(unsigned)((m + 255) / 256) + 1, 256, 0, s>>>(d_rids, m, 1, d_rq);
         q2_fill_rids<<<(unsigned)((n * nq + 255) / 256), 256, 0, s>>>(d_irids, n, nq, d_rq);
@@ -346,13 +361,14 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         q2_finish<<<(n * nq + 255) / 256, 256, 0, s>>>(d_iout, iv.heap, iv.hstride, facts(item).key_pad(), n, nq,
                                                        d_rec, d_ab);
         hip_check(hipGetLastError(), "q2 kernels");
-        std::vector<stage_q2_rec> recs((uint64_t)n * nq);
-        hip_check(hipMemcpyAsync(recs.data(), d_rec, recs.size() * sizeof(stage_q2_rec), hipMemcpyDeviceToHost, s),
+        stage_q2_rec *recs = (stage_q2_rec *)(pq + q_rec);
+        hip_check(hipMemcpyAsync(recs, d_rec, (uint64_t)n * nq * sizeof(stage_q2_rec), hipMemcpyDeviceToHost, s),
                   "d2h");
-        hip_check(hipMemcpyAsync(aborted, d_ab, 4 * nq, hipMemcpyDeviceToHost, s), "d2h");
+        hip_check(hipMemcpyAsync(pq + q_ab, d_ab, 4 * nq, hipMemcpyDeviceToHost, s), "d2h");
         lap("probes enqueued");
         hip_check(hipStreamSynchronize(s), "q2 sync");
         lap("results back");
+        std::memcpy(aborted, pq + q_ab, 4ull * nq);
         const uint32_t read_id = rq[0];
         // 4. the transaction's stock updates, through the device write path
         if (nq == 1 && commit_id && !*aborted) {
@@ -395,7 +411,7 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
             }
         }
         for (uint32_t q = 0; q < nq; ++q)
-            std::memcpy(out + (uint64_t)q * max_out, recs.data() + (uint64_t)q * n,
+            std::memcpy(out + (uint64_t)q * max_out, recs + (uint64_t)q * n,
                         std::min<uint64_t>(n, max_out) * sizeof(stage_q2_rec));
         lap("out copied");
         return STAGE_OK;

@@ -3,7 +3,6 @@
 
 #include <algorithm>
 #include <chrono>
-#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -27,26 +26,7 @@ static void dev_ensure(DevBuf &b, uint64_t bytes, const char *what) {
 
 DeviceImage::~DeviceImage() { release(); }
 
-static void release_vm_heap(DeviceImage &d) {
-    if (!d.heap_vm_va) return;
-    uint64_t off = 0;
-    for (size_t k = 0; k < d.heap_vm_handles.size(); ++k) {
-        (void)hipMemUnmap((char *)d.heap_vm_va + off, d.heap_vm_sizes[k]);
-        (void)hipMemRelease((hipMemGenericAllocationHandle_t)d.heap_vm_handles[k]);
-        off += d.heap_vm_sizes[k];
-    }
-    (void)hipMemAddressFree(d.heap_vm_va, d.heap_vm_reserved);
-    d.heap_vm_va = nullptr;
-    d.heap_vm_reserved = d.heap_vm_mapped = 0;
-    d.heap_vm_handles.clear();
-    d.heap_vm_sizes.clear();
-    d.heap.p = nullptr;
-    d.heap.cap = 0;
-    d.heap_rows = 0;
-}
-
 void DeviceImage::release() {
-    release_vm_heap(*this);
     for (DevBuf *b :
          {&head, &okey, &slot, &tree, &tree_len, &heap, &chdr, &vhdr, &arena, &descs, &patch, &scratch, &wp_scratch, &wp_out[0],
           &wp_out[1], &wp_bases}) {
@@ -54,10 +34,12 @@ void DeviceImage::release() {
         b->p = nullptr;
         b->cap = 0;
     }
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < 3; ++k) {
         if (pinned[k]) (void)hipHostFree(pinned[k]);
         pinned[k] = nullptr;
         pinned_cap[k] = 0;
+    }
+    for (int k = 0; k < 2; ++k) {
         if (adopt_ev[k]) (void)hipEventDestroy(adopt_ev[k]);
         adopt_ev[k] = nullptr;
         if (export_ev[k]) (void)hipEventDestroy(export_ev[k]);
@@ -170,74 +152,15 @@ static void grow_keep(DevBuf &b, uint64_t bytes, uint64_t keep, const char *what
     b = nb;
 }
 
-// VMM heap: the range reserved once (the device's memory, so any heap fits), chunks mapped on
-// growth; false when the device or the runtime refuses (then the copying heap below)
-static bool grow_vm_heap(DeviceImage &d, uint64_t bytes) {
-    static const bool off = std::getenv("STAGE_HEAP_VMM") && std::getenv("STAGE_HEAP_VMM")[0] == '0';
-    if (off) return false;
-    hipMemAllocationProp prop{};
-    prop.type = hipMemAllocationTypePinned;
-    prop.location.type = hipMemLocationTypeDevice;
-    prop.location.id = d.device;
-    size_t gran = 0;
-    if (!d.heap_vm_va) {
-        if (d.heap.p) return false;  // a plain heap already holds rows: keep growing it that way
-        int vmm = 0;
-        if (hipDeviceGetAttribute(&vmm, hipDeviceAttributeVirtualMemoryManagementSupported, d.device) != hipSuccess ||
-            !vmm)
-            return false;
-        if (hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended) != hipSuccess || !gran)
-            return false;
-        size_t free_b = 0, total_b = 0;
-        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return false;
-        const uint64_t reserve = (std::max<uint64_t>(total_b, bytes) + gran - 1) / gran * gran;
-        void *va = nullptr;
-        if (hipMemAddressReserve(&va, reserve, gran, nullptr, 0) != hipSuccess) {
-            (void)hipGetLastError();
-            return false;
-        }
-        d.heap_vm_va = va;
-        d.heap_vm_reserved = reserve;
-    } else {
-        hip_check(hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended), "granularity");
-    }
-    if (bytes <= d.heap_vm_mapped) return true;
-    const uint64_t add = (bytes - d.heap_vm_mapped + gran - 1) / gran * gran;
-    if (d.heap_vm_mapped + add > d.heap_vm_reserved) throw std::runtime_error("record heap: beyond the reserved range");
-    hipMemGenericAllocationHandle_t hd;
-    hip_check(hipMemCreate(&hd, add, &prop, 0), "record heap chunk");
-    char *at = (char *)d.heap_vm_va + d.heap_vm_mapped;
-    hipError_t e = hipMemMap(at, add, 0, hd, 0);
-    if (e != hipSuccess) {
-        (void)hipMemRelease(hd);
-        hip_check(e, "record heap map");
-    }
-    hipMemAccessDesc acc{};
-    acc.location = prop.location;
-    acc.flags = hipMemAccessFlagsProtReadWrite;
-    e = hipMemSetAccess(at, add, &acc, 1);
-    if (e != hipSuccess) {
-        (void)hipMemUnmap(at, add);
-        (void)hipMemRelease(hd);
-        hip_check(e, "record heap access");
-    }
-    d.heap_vm_handles.push_back((uint64_t)hd);
-    d.heap_vm_sizes.push_back(add);
-    d.heap_vm_mapped += add;
-    d.heap.p = d.heap_vm_va;
-    d.heap.cap = d.heap_vm_mapped;
-    return true;
-}
-
 // record heap able to hold `rows` rows (the first images_synced_ rows are kept)
 static void grow_heap(HostTable &h, DeviceImage &d, uint64_t rows_needed, hipStream_t s) {
     if (rows_needed <= d.heap_rows) return;
     const uint32_t stride = h.hstride();
-    const uint64_t rows = rows_needed + std::max<uint64_t>(rows_needed / 16, 1024);
-    if (grow_vm_heap(d, rows * stride)) {
-        d.heap_rows = d.heap_vm_mapped / stride;
-        return;
-    }
+    // first allocation: 1/16 spare rows; a heap that had to grow is being written (e.g. a device
+    // write-path epoch appends one image per successful update): 1/8, so that the copy of the
+    // whole heap a growth costs comes half as often (the old and the new heap coexist during
+    // the copy: 2.1x the rows at the peak)
+    const uint64_t rows = rows_needed + std::max<uint64_t>(rows_needed / (d.heap.p ? 8 : 16), 1024);
     DevBuf nb;
     hip_check(hipMalloc(&nb.p, rows * stride), "record heap");
     nb.cap = rows * stride;

@@ -39,16 +39,11 @@ struct DeviceImage {
     hipEvent_t wp_pub_ev = nullptr, wp_pre_ev = nullptr;
     bool wp_pub_valid = false;
     std::vector<uint8_t> staging;  // host staging of incremental patches
-    void *pinned[2] = {nullptr, nullptr};  // pinned host staging of the epoch results
-    uint64_t pinned_cap[2] = {0, 0};
+    // pinned host staging: [0], [1] the write path's epoch results (by epoch parity); [2] the
+    // host copies of one synchronous call (CH-Q2's scan rows, supplier list, records)
+    void *pinned[3] = {nullptr, nullptr, nullptr};
+    uint64_t pinned_cap[3] = {0, 0, 0};
     uint64_t heap_rows = 0;  // rows the heap buffer can hold
-    // the record heap in a reserved virtual range (HIP virtual memory management): a growth maps
-    // physical chunks behind the rows already there -- no copy of the heap, no second heap while
-    // it grows.  heap_vm_va == nullptr: a plain hipMalloc'd heap (STAGE_HEAP_VMM=0, or no VMM)
-    void *heap_vm_va = nullptr;
-    uint64_t heap_vm_reserved = 0, heap_vm_mapped = 0;
-    std::vector<uint64_t> heap_vm_handles;  // hipMemGenericAllocationHandle_t per mapped chunk
-    std::vector<uint64_t> heap_vm_sizes;
     DevTable view{};
     std::vector<uint32_t> host_to_dev;  // host leaf id -> leaf index in key order
     std::vector<uint32_t> dev_to_host;  // leaf index in key order -> host leaf id
