@@ -1090,11 +1090,14 @@ def run_chq2(args):
     rids = (0xFFFFFFFE - np.arange(nq)).astype(np.uint32)  # nq transactions per step, one read id each
 
     state = {}
+    # the records land in one reused array (only the last step's are read): a fresh 12-MiB
+    # array per step costs the step its page faults
+    out_buf = np.zeros((nq, 1 << 14), stage.Q2_REC_DTYPE)
 
     def step():
         if nq == 1:
             return ch.query2(3)
-        recs_q, ab_q = ch.query2_batch(rids, 3)
+        recs_q, ab_q = ch.query2_batch(rids, 3, out=out_buf)
         state["all"] = (recs_q, ab_q)
         return recs_q[0], bool(ab_q.any())
 

@@ -241,7 +241,10 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         hip_check(hipStreamSynchronize(s), "scan sync");  // the three scans complete together
         lap("scans done");
         const uint32_t nreg = counts[0], nnat = counts[1];
-        std::vector<uint64_t> sel;  // visited suppliers in visiting order
+        // the visiting order of :770-797: for each region named regions[target] (scan order),
+        // for each of its nations (scan order), every SUPPLIER slot of that nation in
+        // ScanLeafNode order -- one pass over the slots into per-visit buckets
+        std::vector<int64_t> visit;  // nation key of each (region, nation) visit, in order
         for (uint32_t r = 0; r < nreg; ++r) {
             const uint8_t *rr = regs_p + (uint64_t)r * rs;
             char name[56];
@@ -250,11 +253,18 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
             if (std::string(name) != kRegions[target_region]) continue;
             for (uint32_t a = 0; a < nnat; ++a) {
                 const uint8_t *nr = nats_p + (uint64_t)a * ns;
-                if (rd64(nr + 8) != rd64(rr)) continue;
-                for (uint64_t k = 0; k < nslots; ++k)
-                    if (pairs[2 * k] != ~0ull && (int64_t)pairs[2 * k + 1] == rd64(nr)) sel.push_back(pairs[2 * k]);
+                if (rd64(nr + 8) == rd64(rr)) visit.push_back(rd64(nr));
             }
         }
+        std::vector<std::vector<uint64_t>> bucket(visit.size());
+        for (uint64_t k = 0; k < nslots; ++k) {
+            if (pairs[2 * k] == ~0ull) continue;
+            const int64_t nat = (int64_t)pairs[2 * k + 1];
+            for (size_t j = 0; j < visit.size(); ++j)
+                if (visit[j] == nat) bucket[j].push_back(pairs[2 * k]);
+        }
+        std::vector<uint64_t> sel;  // visited suppliers in visiting order
+        for (const auto &b : bucket) sel.insert(sel.end(), b.begin(), b.end());
         const uint32_t n = (uint32_t)sel.size();
         lap("suppliers selected");
         *n_out = n;

@@ -794,12 +794,17 @@ def ch_query2(region, nation, supplier, item, stock, map_off, d_map_keys, target
 
 
 def ch_query2_batch(region, nation, supplier, item, stock, map_off, d_map_keys, read_ids, target_region=3,
-                    max_per_query=1 << 14, stream=None):
-    """stage_ch_query2_batch: nq read-only Q2s in one pass -> (records [nq, n] Q2_REC_DTYPE, aborted[nq])."""
+                    max_per_query=1 << 14, stream=None, out=None):
+    """stage_ch_query2_batch: nq read-only Q2s in one pass -> (records [nq, n] Q2_REC_DTYPE, aborted[nq]).
+    out: a caller-owned [nq, max_per_query] Q2_REC_DTYPE array to fill (the result is a view of it)."""
     map_off = np.ascontiguousarray(map_off, np.uint32)
     rids = np.ascontiguousarray(read_ids, np.uint32)
     nq = rids.size
-    out = np.zeros((nq, max_per_query), Q2_REC_DTYPE)
+    if out is None:
+        out = np.zeros((nq, max_per_query), Q2_REC_DTYPE)
+    else:
+        assert out.dtype == Q2_REC_DTYPE and out.flags.c_contiguous and out.shape[0] == nq
+        max_per_query = out.shape[1]
     ab = np.zeros(nq, np.int32)
     n = ctypes.c_uint64()
     check(lib().stage_ch_query2_batch(region.h, nation.h, supplier.h, item.h, stock.h, map_off.ctypes.data,

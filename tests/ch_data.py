@@ -114,10 +114,10 @@ class ChTables:
                                    self.d_map.ptr, target, read_id, commit_id, out=self._out)
         return recs.copy(), ab
 
-    def query2_batch(self, read_ids, target=3):
+    def query2_batch(self, read_ids, target=3, out=None):
         t = self.tables
         return stage.ch_query2_batch(t["region"], t["nation"], t["supplier"], t["item"], t["stock"], self.map_off,
-                                     self.d_map.ptr, read_ids, target)
+                                     self.d_map.ptr, read_ids, target, out=out)
 
     def query2_oracle(self, target=3, read_id=0xFFFFFFFE):
         import ctypes
