@@ -228,13 +228,26 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
                        p_pairs = p_nats + alp((uint64_t)kNationScan * ns), p_end = p_pairs + nslots * 16;
         uint8_t *pin = pinned_bytes(stock->dev, p_end, 2);
         uint32_t *counts = (uint32_t *)pin;
-        scan_rows(region, 0, kRegionScan, counts, pin + p_regs, s);
-        scan_rows(nation, 0, kNationScan, counts + 1, pin + p_nats, s);
+        // the REGION and NATION scans on their tables' own streams beside the SUPPLIER dump on
+        // s (forked from and joined back into s): three short dependent chains side by side
+        hipEvent_t *ev = stock->dev.call_ev;
+        for (int k = 0; k < 3; ++k)
+            if (!ev[k]) hip_check(hipEventCreateWithFlags(&ev[k], hipEventDisableTiming), "call event");
+        hipStream_t rs_s = region->dev.stream ? region->dev.stream : s, ns_s = nation->dev.stream ? nation->dev.stream : s;
+        hip_check(hipEventRecord(ev[0], s), "fork");
+        hip_check(hipStreamWaitEvent(rs_s, ev[0], 0), "fork");
+        hip_check(hipStreamWaitEvent(ns_s, ev[0], 0), "fork");
+        scan_rows(region, 0, kRegionScan, counts, pin + p_regs, rs_s);
+        scan_rows(nation, 0, kNationScan, counts + 1, pin + p_nats, ns_s);
+        hip_check(hipEventRecord(ev[1], rs_s), "join");
+        hip_check(hipEventRecord(ev[2], ns_s), "join");
         uint8_t *pbuf = scratch_bytes(supplier->dev, nslots * 16);
         q2_dump_leaves<<<(unsigned)std::min<uint64_t>((nslots + 255) / 256, 4096), 256, 0, s>>>(
             pv, facts(supplier).key_pad(), (uint64_t *)pbuf);
         hip_check(hipGetLastError(), "dump leaves");
         hip_check(hipMemcpyAsync(pin + p_pairs, pbuf, nslots * 16, hipMemcpyDeviceToHost, s), "d2h");
+        hip_check(hipStreamWaitEvent(s, ev[1], 0), "join");
+        hip_check(hipStreamWaitEvent(s, ev[2], 0), "join");
         const uint8_t *regs_p = pin + p_regs, *nats_p = pin + p_nats;
         const uint64_t *pairs = (const uint64_t *)(pin + p_pairs);
         lap("scans enqueued");
