@@ -211,10 +211,14 @@ void HostTable::adopt_device_epoch(const CopyHdr *copies, const uint32_t *writer
     room(copies_, nc);
     room(copy_live_, nc);
     room(versions_, nv);
-    const uint64_t c0 = copies_.size();
-    copies_.insert(copies_.end(), copies, copies + nc);
+    const uint64_t c0 = copies_.size(), v0 = versions_.size();
+    copies_.resize(c0 + nc);  // uninitialised (HugeAllocNoInit): filled below, in parallel
+    versions_.resize(v0 + nv);
     copy_live_.resize(copies_.size(), 1);
-    versions_.insert(versions_.end(), versions, versions + nv);
+    parallel_chunks(std::max(nc, nv), [&](uint64_t b, uint64_t e) {
+        if (b < nc) std::memcpy(copies_.data() + c0 + b, copies + b, (std::min(e, nc) - b) * sizeof(CopyHdr));
+        if (b < nv) std::memcpy(versions_.data() + v0 + b, versions + b, (std::min(e, nv) - b) * sizeof(VersionHdr));
+    });
     {
         std::lock_guard<std::mutex> g(ssn_.mu);
         room(ssn_.e, nc);  // not reserve(c0 + nc): an exact reserve reallocates every epoch
@@ -233,7 +237,9 @@ void HostTable::adopt_device_epoch(const CopyHdr *copies, const uint32_t *writer
         device_rows_.emplace_back(images_.size(), nimages);
         const uint64_t i0 = images_.size();
         images_.resize(i0 + nimages);
-        for (uint64_t k = 0; k < nimages; ++k) images_[i0 + k] = ImageDesc{0, 0, 3, 0};
+        parallel_chunks(nimages, [&](uint64_t b, uint64_t e) {
+            for (uint64_t k = b; k < e; ++k) images_[i0 + k] = ImageDesc{0, 0, 3, 0};
+        });
     }
     lap("images");
     // one slot word per touched record (distinct indices): scattered writes in parallel

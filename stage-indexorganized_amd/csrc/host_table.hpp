@@ -120,7 +120,7 @@ struct CopySsn {
 class CopySsnTable {
 public:
     std::mutex mu;
-    std::vector<CopySsn, HugeAlloc<CopySsn>> e;                  // by copy id (an epoch appends ~10^6)
+    std::vector<CopySsn, HugeAllocNoInit<CopySsn>> e;                  // by copy id (an epoch appends ~10^6)
     std::unordered_map<uint32_t, std::vector<uint32_t>> readers;  // copy id -> AddReader ids
     // EphemeralPool::Allocate (ephemeral_pool.cpp:17-44): cstamp = pstamp = writer, sstamp MAX
     void created(uint64_t id, uint32_t writer, uint32_t rstamp);
@@ -239,9 +239,9 @@ public:
 
     ChunkedVector<ImageDesc, (1u << 20)> images_;
     ChunkedArena arena_;
-    std::vector<CopyHdr, HugeAlloc<CopyHdr>> copies_;
+    std::vector<CopyHdr, HugeAllocNoInit<CopyHdr>> copies_;
     std::vector<uint8_t, HugeAlloc<uint8_t>> copy_live_;
-    std::vector<VersionHdr, HugeAlloc<VersionHdr>> versions_;
+    std::vector<VersionHdr, HugeAllocNoInit<VersionHdr>> versions_;
     uint64_t images_synced_ = 0;     // images already present on the device
     uint64_t arena_synced_ = 0;
     bool layout_dirty_ = true;       // any host write since the last publish

@@ -9,6 +9,7 @@
 #include <cstddef>
 #include <cstdlib>
 #include <new>
+#include <utility>
 
 namespace stage {
 
@@ -36,6 +37,29 @@ struct HugeAlloc {
     bool operator==(const HugeAlloc<U> &) const { return true; }
     template <class U>
     bool operator!=(const HugeAlloc<U> &) const { return false; }
+};
+
+// HugeAlloc whose resize() leaves new trivially constructible elements uninitialised: for the
+// header arrays an epoch's adoption appends ~10^6 entries to, every one of them then written
+// (in parallel, so the first touch of the new pages is spread over the threads too)
+template <class T>
+struct HugeAllocNoInit : HugeAlloc<T> {
+    using value_type = T;
+    template <class U>
+    struct rebind {
+        using other = HugeAllocNoInit<U>;
+    };
+    HugeAllocNoInit() = default;
+    template <class U>
+    HugeAllocNoInit(const HugeAllocNoInit<U> &) {}
+    template <class U, class... A>
+    void construct(U *p, A &&...a) {
+        ::new ((void *)p) U(std::forward<A>(a)...);
+    }
+    template <class U>
+    void construct(U *p) noexcept {
+        ::new ((void *)p) U;  // default-initialisation: no zero fill
+    }
 };
 
 }  // namespace stage
