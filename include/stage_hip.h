@@ -502,7 +502,10 @@ int stage_sharded_owner_rows(stage_table *t, int loopback, uint8_t **d_rows, uin
 int stage_set_shard_dedupe(stage_table *t, int on);
 /* coalescing sorts the batch's keys on their low `bits` bits (0 or 64 = all; default 64).  Any
  * value gives the same results -- keys equal in those bits but different above them still form
- * separate requests -- a caller whose keys are < 2^bits only saves radix passes. */
+ * separate requests -- a caller whose keys are < 2^bits only saves radix passes.  bits <= 32
+ * (batches without read ids): the sort moves 32-bit key words and positions instead of 64-bit
+ * keys; a batch holding a key above 2^32 is still answered exactly (its keys are gathered back
+ * by position). */
 int stage_set_shard_key_bits(stage_table *t, int bits);
 /* the RCCL the process runs: ncclGetVersion (e.g. 22707 = 2.27.7), the RCCL header version
  * libstage_hip was built against, and the file that provided ncclGetVersion.  stage_comm_init
