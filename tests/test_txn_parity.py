@@ -59,3 +59,12 @@ def test_device_results_drive_the_manager_like_the_oracle(gpu, seed):
     lines = out.strip().splitlines()
     assert rc == 0 and lines[0] == "MATCH", (out[-3000:], err[-2000:])
     coverage(json.loads(lines[-1]))
+
+
+@pytest.mark.gpu
+def test_device_results_drive_the_manager_like_the_oracle_longer(gpu):
+    # a longer schedule over a larger table: more splits between reads and commits, more copies
+    rc, out, err = run("both", 7, rows=20000, txns=2000)
+    lines = out.strip().splitlines()
+    assert rc == 0 and lines[0] == "MATCH", (out[-3000:], err[-2000:])
+    coverage(json.loads(lines[-1]))
