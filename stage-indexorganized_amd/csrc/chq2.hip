@@ -15,8 +15,9 @@
 // Here REGION / NATION run as device scans and SUPPLIER as a one-lane-per-slot leaf dump; the
 // host filters their rows (a few hundred KB); the hot part -- every visited supplier's stock lookups (W * I / 10^4 each, ~2600
 // suppliers for EUROPE) and the item lookups -- is one gather kernel, one probe_kernel launch
-// over all stock keys, one wave per supplier reducing its segment, one item probe launch and
-// one finishing kernel.  Updates go through the device write path when a commit id is given.
+// over all stock keys, their visibility folded at every read id of the batch (aborts and each
+// supplier's last stock), one item probe launch and one finishing kernel.  Updates go through the device write path when
+// a commit id is given.
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -48,12 +49,6 @@ __device__ __forceinline__ int32_t ld_i32(const uint8_t *p) {
 
 __global__ void q2_set_u64(uint64_t *p, uint64_t v) { *p = v; }
 
-// read id of every lookup: copy q of a per-query segment of `per` lookups reads at rq[q]
-__global__ void q2_fill_rids(uint32_t *p, uint64_t per, uint32_t nq, const uint32_t *__restrict__ rq) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < per * nq) p[i] = rq[i / per];
-}
-
 // block s copies supplier s's map entries (2 words each) to its segment
 __global__ void q2_gather(const uint64_t *__restrict__ map_keys, const uint64_t *__restrict__ src,
                           const uint64_t *__restrict__ dst, const uint32_t *__restrict__ cnt,
@@ -80,43 +75,43 @@ __global__ void q2_permute_keys(const uint64_t *__restrict__ keys, const uint32_
     out[2 * j + 1] = keys[2 * p + 1];
 }
 
-// one wave per supplier: abort if any stock lookup of its segment produced no tuple; the last
-// entry's stock row gives (w, i, quantity, ytd, order_cnt, remote_cnt) and the item key
-__global__ __launch_bounds__(64) void q2_reduce(const stage_probe_out_dev *__restrict__ sout,
-                                                const uint64_t *__restrict__ skeys, const uint64_t *__restrict__ dst,
-                                                const uint32_t *__restrict__ cnt, const uint64_t *__restrict__ supp,
-                                                const uint8_t *__restrict__ sheap, uint32_t shstride,
-                                                uint32_t skpad, uint32_t n, uint64_t m, stage_q2_rec *__restrict__ out,
-                                                uint64_t *__restrict__ ikeys, int32_t *__restrict__ abort_flag) {
-    // block = (supplier s, query q): query q's lookup results are the q-th segment of m records
-    // (the m keys are the same for every query)
-    const uint32_t s = blockIdx.x % n, q = blockIdx.x / n, lane = threadIdx.x;
-    abort_flag += q;
-    out += (uint64_t)q * n;
-    ikeys += (uint64_t)q * n;
-    const uint64_t b = (uint64_t)q * m + dst[s], kb = dst[s];
+// the leaf-ordered probe results back in key order: out[perm[j]] = in[j]
+__global__ void q2_unpermute(const stage_probe_out_dev *__restrict__ in, const uint32_t *__restrict__ perm, uint64_t m,
+                             stage_probe_out_dev *__restrict__ out) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < m) out[perm[j]] = in[j];
+}
+
+// thread per (query q, supplier s): the abort for a stock lookup that produced no tuple is already
+// in abort_flag (launch_revisit_segments); the last entry's stock row, at q's read id, gives
+// (w, i, quantity, ytd, order_cnt, remote_cnt) and the item key
+__global__ void q2_reduce(const stage_probe_out_dev *__restrict__ slast, const uint64_t *__restrict__ skeys,
+                          const uint64_t *__restrict__ dst, const uint32_t *__restrict__ cnt,
+                          const uint64_t *__restrict__ supp, const uint8_t *__restrict__ sheap, uint32_t shstride,
+                          uint32_t skpad, uint32_t n, uint32_t nq, stage_q2_rec *__restrict__ out,
+                          uint64_t *__restrict__ ikeys) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;  // q * n + s
+    if (g >= n * nq) return;
+    const uint32_t s = g % n;
+    const uint64_t kb = dst[s];
     const uint32_t c = cnt[s];
-    bool bad = false;
-    for (uint32_t e = lane; e < c; e += 64) bad |= !produced(sout[b + e].w[0] & 0xFF);
-    if (__builtin_amdgcn_ballot_w64(bad) && lane == 0) atomicOr(abort_flag, 1);
-    if (lane != 0) return;
     stage_q2_rec r;
     memset(&r, 0, sizeof(r));
     r.supp_key = (int64_t)supp[s];
     if (c) {  // stock_0 / stock_1 of the last lookup (a supplier without stocks keeps zeros)
-        const uint64_t last = b + c - 1, klast = kb + c - 1;
+        const uint64_t klast = kb + c - 1;
         r.s_w_id = (int64_t)skeys[2 * klast];
         r.s_i_id = (int64_t)skeys[2 * klast + 1];
-        if (produced(sout[last].w[0] & 0xFF)) {
-            const uint8_t *row = sheap + (uint64_t)sout[last].w[6] * shstride + skpad;
+        if (produced(slast[g].w[0] & 0xFF)) {
+            const uint8_t *row = sheap + (uint64_t)slast[g].w[6] * shstride + skpad;
             r.s_quantity = ld_i32(row);
             r.s_ytd = ld_i32(row + 4);
             r.s_order_cnt = ld_i32(row + 8);
             r.s_remote_cnt = ld_i32(row + 12);
         }
     }
-    out[s] = r;
-    ikeys[s] = (uint64_t)r.s_i_id;
+    out[g] = r;
+    ikeys[g] = (uint64_t)r.s_i_id;
 }
 
 // item outcome: no tuple aborts; I_DATA up to its first NUL containing 'b' skips; else a
@@ -163,18 +158,22 @@ int64_t rd64(const uint8_t *p) {
     return v;
 }
 
-// TableScanExecutor rows of one scan from `start` (device scan; count and rows copied to the
-// pinned host destinations asynchronously: the caller synchronises the stream before reading)
-void scan_rows(stage_table *t, uint64_t start, uint32_t scan_size, uint32_t *count, uint8_t *rows_out, hipStream_t s) {
+// TableScanExecutor rows of one scan from `start` (device scan): area[0..4) = the row count and
+// area + 8 the rows, one asynchronous copy to the pinned host area (the caller synchronises the
+// stream before reading)
+void scan_rows(stage_table *t, uint64_t start, uint32_t scan_size, uint8_t *area, hipStream_t s) {
     const DevTable &v = t->dev.view;
     const uint64_t rows = (uint64_t)scan_size * v.stride;
     uint8_t *buf = scratch_bytes(t->dev, 64 + rows);
     auto *key = (uint64_t *)buf;
-    auto *cnt = (uint32_t *)(buf + 8);
+    auto *cnt = (uint32_t *)(buf + 56);  // 8 bytes before the rows
     q2_set_u64<<<1, 1, 0, s>>>(key, start);  // no host buffer outlives the call
-    hip_check(launch_scan(v, key, nullptr, 1, scan_size, cnt, buf + 64, s, t->scan_tune), "scan");
-    hip_check(hipMemcpyAsync(count, cnt, 4, hipMemcpyDeviceToHost, s), "d2h");
-    hip_check(hipMemcpyAsync(rows_out, buf + 64, rows, hipMemcpyDeviceToHost, s), "d2h");
+    // one scan on one wave: the row copies are its chain of round trips, so 8 rows in flight per
+    // round unless STAGE_SCAN_ROWS chose otherwise
+    ScanTuning tn = t->scan_tune;
+    if (!std::getenv("STAGE_SCAN_ROWS")) tn.rows = 8;
+    hip_check(launch_scan(v, key, nullptr, 1, scan_size, cnt, buf + 64, s, tn), "scan");
+    hip_check(hipMemcpyAsync(area, cnt, 8 + rows, hipMemcpyDeviceToHost, s), "d2h");
 }
 
 }  // namespace
@@ -221,13 +220,12 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         const DevTable &pv = supplier->dev.view;
         const uint64_t nslots = (uint64_t)pv.nleaves * pv.cap;
         // the host copies go through the stock table's pinned call staging (pageable copies
-        // are staged by the runtime and wait for each other): [counts][REGION rows][NATION
-        // rows][SUPPLIER (key, nation) pairs]
+        // are staged by the runtime and wait for each other): [REGION count, rows][NATION
+        // count, rows][SUPPLIER (key, nation) pairs]
         auto alp = [](uint64_t x) { return (x + 255) & ~255ull; };
-        const uint64_t p_regs = 256, p_nats = p_regs + alp((uint64_t)kRegionScan * rs),
-                       p_pairs = p_nats + alp((uint64_t)kNationScan * ns), p_end = p_pairs + nslots * 16;
+        const uint64_t p_regs = 0, p_nats = p_regs + alp(8 + (uint64_t)kRegionScan * rs),
+                       p_pairs = p_nats + alp(8 + (uint64_t)kNationScan * ns), p_end = p_pairs + nslots * 16;
         uint8_t *pin = pinned_bytes(stock->dev, p_end, 2);
-        uint32_t *counts = (uint32_t *)pin;
         // the REGION and NATION scans on their tables' own streams beside the SUPPLIER dump on
         // s (forked from and joined back into s): three short dependent chains side by side
         hipEvent_t *ev = stock->dev.call_ev;
@@ -237,8 +235,8 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         hip_check(hipEventRecord(ev[0], s), "fork");
         hip_check(hipStreamWaitEvent(rs_s, ev[0], 0), "fork");
         hip_check(hipStreamWaitEvent(ns_s, ev[0], 0), "fork");
-        scan_rows(region, 0, kRegionScan, counts, pin + p_regs, rs_s);
-        scan_rows(nation, 0, kNationScan, counts + 1, pin + p_nats, ns_s);
+        scan_rows(region, 0, kRegionScan, pin + p_regs, rs_s);
+        scan_rows(nation, 0, kNationScan, pin + p_nats, ns_s);
         hip_check(hipEventRecord(ev[1], rs_s), "join");
         hip_check(hipEventRecord(ev[2], ns_s), "join");
         uint8_t *pbuf = scratch_bytes(supplier->dev, nslots * 16);
@@ -248,12 +246,14 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         hip_check(hipMemcpyAsync(pin + p_pairs, pbuf, nslots * 16, hipMemcpyDeviceToHost, s), "d2h");
         hip_check(hipStreamWaitEvent(s, ev[1], 0), "join");
         hip_check(hipStreamWaitEvent(s, ev[2], 0), "join");
-        const uint8_t *regs_p = pin + p_regs, *nats_p = pin + p_nats;
+        const uint8_t *regs_p = pin + p_regs + 8, *nats_p = pin + p_nats + 8;
         const uint64_t *pairs = (const uint64_t *)(pin + p_pairs);
         lap("scans enqueued");
         hip_check(hipStreamSynchronize(s), "scan sync");  // the three scans complete together
         lap("scans done");
-        const uint32_t nreg = counts[0], nnat = counts[1];
+        uint32_t nreg, nnat;
+        std::memcpy(&nreg, pin + p_regs, 4);
+        std::memcpy(&nnat, pin + p_nats, 4);
         // the visiting order of :770-797: for each region named regions[target] (scan order),
         // for each of its nations (scan order), every SUPPLIER slot of that nation in
         // ScanLeafNode order -- one pass over the slots into per-visit buckets
@@ -269,30 +269,56 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
                 if (rd64(nr + 8) == rd64(rr)) visit.push_back(rd64(nr));
             }
         }
-        std::vector<std::vector<uint64_t>> bucket(visit.size());
-        for (uint64_t k = 0; k < nslots; ++k) {
-            if (pairs[2 * k] == ~0ull) continue;
-            const int64_t nat = (int64_t)pairs[2 * k + 1];
-            for (size_t j = 0; j < visit.size(); ++j)
-                if (visit[j] == nat) bucket[j].push_back(pairs[2 * k]);
+        // visit index of each nation key: a direct table when the visited keys are small and
+        // distinct (always, for the loader's nations 0..61), else the per-slot search over visits
+        constexpr int64_t kDirect = 4096;
+        std::vector<int32_t> vidx(kDirect, -1);
+        bool direct = true;
+        for (size_t j = 0; j < visit.size() && direct; ++j) {
+            if (visit[j] < 0 || visit[j] >= kDirect || vidx[visit[j]] >= 0) direct = false;
+            else vidx[visit[j]] = (int32_t)j;
         }
         std::vector<uint64_t> sel;  // visited suppliers in visiting order
-        for (const auto &b : bucket) sel.insert(sel.end(), b.begin(), b.end());
+        if (direct) {  // counting pass, then each slot placed at its visit's next position
+            std::vector<uint32_t> pos(visit.size() + 1, 0);
+            for (uint64_t k = 0; k < nslots; ++k) {
+                const int64_t nat = (int64_t)pairs[2 * k + 1];
+                if (pairs[2 * k] != ~0ull && nat >= 0 && nat < kDirect && vidx[nat] >= 0) ++pos[vidx[nat] + 1];
+            }
+            for (size_t j = 0; j < visit.size(); ++j) pos[j + 1] += pos[j];
+            sel.resize(pos[visit.size()]);
+            for (uint64_t k = 0; k < nslots; ++k) {
+                const int64_t nat = (int64_t)pairs[2 * k + 1];
+                if (pairs[2 * k] != ~0ull && nat >= 0 && nat < kDirect && vidx[nat] >= 0)
+                    sel[pos[vidx[nat]]++] = pairs[2 * k];
+            }
+        } else {
+            std::vector<std::vector<uint64_t>> bucket(visit.size());
+            for (uint64_t k = 0; k < nslots; ++k) {
+                if (pairs[2 * k] == ~0ull) continue;
+                const int64_t nat = (int64_t)pairs[2 * k + 1];
+                for (size_t j = 0; j < visit.size(); ++j)
+                    if (visit[j] == nat) bucket[j].push_back(pairs[2 * k]);
+            }
+            for (const auto &b : bucket) sel.insert(sel.end(), b.begin(), b.end());
+        }
         const uint32_t n = (uint32_t)sel.size();
         lap("suppliers selected");
         *n_out = n;
         if (n == 0) return STAGE_OK;
         // 2. stock keys of every visited supplier, one probe launch.  Pinned call staging again
-        // (the scans' contents are no longer needed: a growth may move it): [src][dst][cnt][sel]
-        // [read ids] going down, [records][aborted] coming back
+        // (the scans' contents are no longer needed: a growth may move it), mirrored by the head
+        // of the device scratch so that one copy goes down and one comes back:
+        // [src][dst][cnt][sel][read ids] down, [aborted] (zeroed) down and up, [records] up
         const uint64_t q_src = 0, q_dst = q_src + alp(n * 8ull), q_cnt = q_dst + alp(n * 8ull),
-                       q_sel = q_cnt + alp(n * 4ull), q_rq = q_sel + alp(n * 8ull), q_rec = q_rq + alp(nq * 4ull),
-                       q_ab = q_rec + alp((uint64_t)n * nq * sizeof(stage_q2_rec)), q_end = q_ab + alp(nq * 4ull);
+                       q_sel = q_cnt + alp(n * 4ull), q_rq = q_sel + alp(n * 8ull), q_ab = q_rq + alp(nq * 4ull),
+                       q_rec = q_ab + alp(nq * 4ull), q_end = q_rec + alp((uint64_t)n * nq * sizeof(stage_q2_rec));
         uint8_t *pq = pinned_bytes(stock->dev, q_end, 2);
         uint64_t *src = (uint64_t *)(pq + q_src), *dst = (uint64_t *)(pq + q_dst);
         uint32_t *cnt = (uint32_t *)(pq + q_cnt);
         std::memcpy(pq + q_sel, sel.data(), n * 8ull);
         std::memcpy(pq + q_rq, rq, nq * 4ull);
+        std::memset(pq + q_ab, 0, nq * 4ull);
         uint64_t m = 0;
         for (uint32_t k = 0; k < n; ++k) {
             const uint64_t sk = sel[k];
@@ -321,38 +347,31 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
             off += al(bytes);
             return o;
         };
-        const uint64_t o_src = take(n * 8), o_dst = take(n * 8), o_cnt = take(n * 4), o_sup = take(n * 8),
-                       o_keys = take(std::max<uint64_t>(m, 1) * 16), o_rids = take(std::max<uint64_t>(m, 1) * 4),
-                       o_irids = take(n * 4 * nq), o_rq = take(nq * 4),
-                       o_sbase = take(nq > 1 || sorted ? std::max<uint64_t>(m, 1) * 32 : 0),
+        const uint64_t o_mir = take(q_end), o_keys = take(std::max<uint64_t>(m, 1) * 16),
+                       o_sbase = take(std::max<uint64_t>(m, 1) * 32),
                        o_leaf = take(sorted ? m * 4 : 0), o_sleaf = take(sorted ? m * 4 : 0),
                        o_iota = take(sorted ? m * 4 : 0), o_perm = take(sorted ? m * 4 : 0),
                        o_skeys = take(sorted ? m * 16 : 0), o_cub = take(sorted ? cub_bytes : 0),
-                       o_sout = take(std::max<uint64_t>(m, 1) * 32 * nq),
-                       o_rec = take(n * sizeof(stage_q2_rec) * nq), o_ik = take(n * 8 * nq),
-                       o_iout = take(n * 32 * nq), o_ibase = take(nq > 1 ? n * 32 : 0), o_ab = take(4 * nq);
-        uint8_t *buf = scratch_bytes(nation->dev, off);
-        auto *d_src = (uint64_t *)(buf + o_src), *d_dst = (uint64_t *)(buf + o_dst), *d_sup = (uint64_t *)(buf + o_sup);
-        auto *d_cnt = (uint32_t *)(buf + o_cnt), *d_rids = (uint32_t *)(buf + o_rids);
-        auto *d_irids = (uint32_t *)(buf + o_irids), *d_rq = (uint32_t *)(buf + o_rq);
+                       o_sout = take(sorted ? m * 32 : 0), o_slast = take(n * 32ull * nq),
+                       o_ik = take(n * 8 * nq), o_iout = take(n * 32 * nq), o_ibase = take(n * 32);
+        uint8_t *buf = scratch_bytes(nation->dev, off), *mir = buf + o_mir;
+        auto *d_src = (uint64_t *)(mir + q_src), *d_dst = (uint64_t *)(mir + q_dst), *d_sup = (uint64_t *)(mir + q_sel);
+        auto *d_cnt = (uint32_t *)(mir + q_cnt), *d_rq = (uint32_t *)(mir + q_rq);
         auto *d_keys = (uint64_t *)(buf + o_keys), *d_ik = (uint64_t *)(buf + o_ik);
         auto *d_sout = (stage_probe_out_dev *)(buf + o_sout), *d_iout = (stage_probe_out_dev *)(buf + o_iout);
+        auto *d_slast = (stage_probe_out_dev *)(buf + o_slast);
         auto *d_sbase = (stage_probe_out_dev *)(buf + o_sbase), *d_ibase = (stage_probe_out_dev *)(buf + o_ibase);
-        auto *d_rec = (stage_q2_rec *)(buf + o_rec);
-        auto *d_ab = (int32_t *)(buf + o_ab);
-        hip_check(hipMemcpyAsync(d_src, src, n * 8, hipMemcpyHostToDevice, s), "h2d");
-        hip_check(hipMemcpyAsync(d_dst, dst, n * 8, hipMemcpyHostToDevice, s), "h2d");
-        hip_check(hipMemcpyAsync(d_cnt, cnt, n * 4, hipMemcpyHostToDevice, s), "h2d");
-        hip_check(hipMemcpyAsync(d_sup, pq + q_sel, n * 8, hipMemcpyHostToDevice, s), "h2d");
-        hip_check(hipMemcpyAsync(d_rq, pq + q_rq, nq * 4, hipMemcpyHostToDevice, s), "h2d");
-        hip_check(hipMemsetAsync(d_ab, 0, 4 * nq, s), "memset");
-        q2_fill_rids<<<(unsigned)((m + 255) / 256) + 1, 256, 0, s>>>(d_rids, m, 1, d_rq);
-        q2_fill_rids<<<(unsigned)((n * nq + 255) / 256), 256, 0, s>>>(d_irids, n, nq, d_rq);
+        auto *d_rec = (stage_q2_rec *)(mir + q_rec);
+        auto *d_ab = (int32_t *)(mir + q_ab);
+        hip_check(hipMemcpyAsync(mir, pq, q_rec, hipMemcpyHostToDevice, s), "h2d");
         q2_gather<<<n, 256, 0, s>>>(d_map_keys, d_src, d_dst, d_cnt, d_keys);
         const DevTable &sv = stock->dev.view, &iv = item->dev.view;
         // every query of the batch looks up the same STOCK keys (the visited suppliers and their
-        // supp_stock_map do not depend on the read id): each key is probed once and its hit slot's
-        // visibility evaluated at every query's read id (launch_revisit)
+        // supp_stock_map do not depend on the read id): each key is probed once, with no read id
+        // (the hit slot does not depend on it), and its visibility evaluated at every query's read
+        // id inside the per-supplier fold (launch_revisit_segments: the aborts and each
+        // supplier's last stock, per query)
+        const stage_probe_out_dev *d_stock = d_sbase;
         if (sorted) {
             auto *d_leaf = (uint32_t *)(buf + o_leaf), *d_sleaf = (uint32_t *)(buf + o_sleaf);
             auto *d_iota = (uint32_t *)(buf + o_iota), *d_perm = (uint32_t *)(buf + o_perm);
@@ -365,29 +384,30 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
                                  lbits, s),
                       "stock leaf sort");
             q2_permute_keys<<<mb, 256, 0, s>>>(d_keys, d_perm, m, d_skeys);
-            hip_check(launch_probe(sv, d_skeys, nullptr, d_rids, d_sleaf, m, d_sbase, nullptr, s, stock->tune),
+            hip_check(launch_probe(sv, d_skeys, nullptr, nullptr, d_sleaf, m, d_sbase, nullptr, s, stock->tune),
                       "stock probe");
-            hip_check(launch_revisit(sv, d_sbase, m, d_rq, nq, d_perm, d_sout, s), "stock read ids");
+            q2_unpermute<<<mb, 256, 0, s>>>(d_sbase, d_perm, m, d_sout);
+            d_stock = d_sout;
         } else if (m) {
-            hip_check(launch_probe(sv, d_keys, nullptr, d_rids, nullptr, m, nq > 1 ? d_sbase : d_sout, nullptr, s,
-                                   stock->tune),
+            hip_check(launch_probe(sv, d_keys, nullptr, nullptr, nullptr, m, d_sbase, nullptr, s, stock->tune),
                       "stock probe");
-            if (nq > 1) hip_check(launch_revisit(sv, d_sbase, m, d_rq, nq, nullptr, d_sout, s), "stock read ids");
         }
-        q2_reduce<<<n * nq, 64, 0, s>>>(d_sout, d_keys, d_dst, d_cnt, d_sup, sv.heap, sv.hstride,
-                                        facts(stock).key_pad(), n, m, d_rec, d_ik, d_ab);
+        if (m)
+            hip_check(launch_revisit_segments(sv, d_stock, m, d_dst, d_cnt, n, d_rq, nq, d_slast, d_ab, s),
+                      "stock read ids");
+        q2_reduce<<<(n * nq + 255) / 256, 256, 0, s>>>(d_slast, d_keys, d_dst, d_cnt, d_sup, sv.heap, sv.hstride,
+                                                       facts(stock).key_pad(), n, nq, d_rec, d_ik);
         // 3. item lookups of the last stocks (the same keys in every query: probed once, as above),
         // filter
-        hip_check(launch_probe(iv, d_ik, nullptr, d_irids, nullptr, n, nq > 1 ? d_ibase : d_iout, nullptr, s, item->tune),
-                  "item probe");
-        if (nq > 1) hip_check(launch_revisit(iv, d_ibase, n, d_rq, nq, nullptr, d_iout, s), "item read ids");
+        hip_check(launch_probe(iv, d_ik, nullptr, nullptr, nullptr, n, d_ibase, nullptr, s, item->tune), "item probe");
+        hip_check(launch_revisit(iv, d_ibase, n, d_rq, nq, nullptr, d_iout, s), "item read ids");
         q2_finish<<<(n * nq + 255) / 256, 256, 0, s>>>(d_iout, iv.heap, iv.hstride, facts(item).key_pad(), n, nq,
                                                        d_rec, d_ab);
         hip_check(hipGetLastError(), "q2 kernels");
         stage_q2_rec *recs = (stage_q2_rec *)(pq + q_rec);
-        hip_check(hipMemcpyAsync(recs, d_rec, (uint64_t)n * nq * sizeof(stage_q2_rec), hipMemcpyDeviceToHost, s),
-                  "d2h");
-        hip_check(hipMemcpyAsync(pq + q_ab, d_ab, 4 * nq, hipMemcpyDeviceToHost, s), "d2h");
+        hip_check(hipMemcpyAsync(pq + q_ab, d_ab, (q_rec - q_ab) + (uint64_t)n * nq * sizeof(stage_q2_rec),
+                                 hipMemcpyDeviceToHost, s),
+                  "d2h");  // [aborted][records]
         lap("probes enqueued");
         hip_check(hipStreamSynchronize(s), "q2 sync");
         lap("results back");

@@ -89,6 +89,14 @@ hipError_t launch_resident_reader(const DevTable &t, const ReaderRing &g, hipStr
 // perm (may be null): base[i] is key perm[i]'s result, written to out[q * n + perm[i]]
 hipError_t launch_revisit(const DevTable &t, const stage_probe_out_dev *base, uint64_t n, const uint32_t *rids,
                           uint32_t nq, const uint32_t *perm, stage_probe_out_dev *out, hipStream_t s);
+// launch_revisit folded, for n probes cut into segments (segment k = base[seg_off[k], + seg_cnt[k])):
+// missed[q] |= 1 when any probe yields no record (LATEST / COPY / OLD) at rids[q], and
+// last[q * nseg + k] = segment k's last probe at rids[q] (left as it is for an empty segment) --
+// the n * nq results themselves are never stored
+hipError_t launch_revisit_segments(const DevTable &t, const stage_probe_out_dev *base, uint64_t n,
+                                   const uint64_t *seg_off, const uint32_t *seg_cnt, uint32_t nseg,
+                                   const uint32_t *rids, uint32_t nq, stage_probe_out_dev *last, int32_t *missed,
+                                   hipStream_t s);
 // stage_probe_ident: {location handle, next handle} of each probe's hit slot (two u32 per probe)
 hipError_t launch_ident(const DevTable &t, const stage_probe_out_dev *out, uint64_t n, uint32_t *ident, hipStream_t s);
 hipError_t launch_murmur(const void *keys, uint32_t key_len, uint32_t key_stride, uint64_t seed, uint64_t n,

@@ -2806,6 +2806,16 @@ bool probe_fanout_supported(const DevTable &t) {
 
 // launch_revisit: thread per (key i, read id q); a NOT_FOUND result (no visible slot, or an
 // in-flight insert without a copy) holds for every read id and is copied as it is
+__device__ __forceinline__ void revisit_one(const DevTable &t, uint32_t rid, u32x4 &a, u32x4 &b) {
+    const uint32_t slot = a.z & 0xFFFF, leaf = a.y;
+    if ((a.x & 0xFF) != ST_NOT_FOUND && slot < t.cap && leaf < t.nleaves) {
+        const SlotInfo si = t.slot[(uint64_t)leaf * t.cap + slot];
+        ProbeRes r;
+        visibility(t, (int)slot, si.meta, si.next, si.image, rid, r);
+        pack_out(leaf, r, a, b);
+    }
+}
+
 __global__ __launch_bounds__(256) void revisit_kernel(DevTable t, const stage_probe_out_dev *__restrict__ base,
                                                       uint64_t n, const uint32_t *__restrict__ rids, uint32_t nq,
                                                       const uint32_t *__restrict__ perm,
@@ -2815,16 +2825,68 @@ __global__ __launch_bounds__(256) void revisit_kernel(DevTable t, const stage_pr
     const uint64_t i = g % n, q = g / n;
     const u32x4 *bp = reinterpret_cast<const u32x4 *>(base + i);
     u32x4 a = bp[0], b = bp[1];
-    const uint32_t slot = a.z & 0xFFFF, leaf = a.y;
-    if ((a.x & 0xFF) != ST_NOT_FOUND && slot < t.cap && leaf < t.nleaves) {
-        const SlotInfo si = t.slot[(uint64_t)leaf * t.cap + slot];
-        ProbeRes r;
-        visibility(t, (int)slot, si.meta, si.next, si.image, rids[q], r);
-        pack_out(leaf, r, a, b);
-    }
+    revisit_one(t, rids[q], a, b);
     u32x4 *op = reinterpret_cast<u32x4 *>(out + q * n + (perm ? perm[i] : i));
     op[0] = a;
     op[1] = b;
+}
+
+// launch_revisit_segments, the misses: thread per (probe i, kRevisitQ read ids) -- the probe's
+// status record and slot word are loaded once and the visibility walk redone per read id; nothing
+// is stored but a miss (rare: the transaction aborts)
+constexpr uint32_t kRevisitQ = 16;
+__global__ __launch_bounds__(256) void revisit_missed_kernel(DevTable t, const stage_probe_out_dev *__restrict__ base,
+                                                             uint64_t n, const uint32_t *__restrict__ rids, uint32_t nq,
+                                                             int32_t *__restrict__ missed) {
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n * ((nq + kRevisitQ - 1) / kRevisitQ)) return;
+    const uint64_t i = g % n;
+    const uint32_t q0 = (uint32_t)(g / n) * kRevisitQ, q1 = q0 + kRevisitQ < nq ? q0 + kRevisitQ : nq;
+    const u32x4 *bp = reinterpret_cast<const u32x4 *>(base + i);
+    const u32x4 a0 = bp[0];
+    const uint32_t slot = a0.z & 0xFFFF, leaf = a0.y;
+    const bool redo = (a0.x & 0xFF) != ST_NOT_FOUND && slot < t.cap && leaf < t.nleaves;
+    SlotInfo si = {};
+    if (redo) si = t.slot[(uint64_t)leaf * t.cap + slot];
+    for (uint32_t q = q0; q < q1; ++q) {
+        uint32_t st = a0.x & 0xFF;
+        if (redo) {
+            ProbeRes r;
+            visibility(t, (int)slot, si.meta, si.next, si.image, rids[q], r);
+            st = r.status;
+        }
+        if (st != ST_LATEST && st != ST_COPY && st != ST_OLD) atomicOr(missed + q, 1);
+    }
+}
+
+// launch_revisit_segments, the last probes: thread per (read id q, segment k)
+__global__ __launch_bounds__(256) void revisit_last_kernel(DevTable t, const stage_probe_out_dev *__restrict__ base,
+                                                           const uint64_t *__restrict__ seg_off,
+                                                           const uint32_t *__restrict__ seg_cnt, uint32_t nseg,
+                                                           const uint32_t *__restrict__ rids, uint32_t nq,
+                                                           stage_probe_out_dev *__restrict__ last) {
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= (uint64_t)nseg * nq) return;
+    const uint32_t k = (uint32_t)(g % nseg), q = (uint32_t)(g / nseg);
+    const uint32_t c = seg_cnt[k];
+    if (c == 0) return;
+    const u32x4 *bp = reinterpret_cast<const u32x4 *>(base + seg_off[k] + c - 1);
+    u32x4 a = bp[0], b = bp[1];
+    revisit_one(t, rids[q], a, b);
+    u32x4 *op = reinterpret_cast<u32x4 *>(last + g);
+    op[0] = a;
+    op[1] = b;
+}
+
+hipError_t launch_revisit_segments(const DevTable &t, const stage_probe_out_dev *base, uint64_t n,
+                                   const uint64_t *seg_off, const uint32_t *seg_cnt, uint32_t nseg,
+                                   const uint32_t *rids, uint32_t nq, stage_probe_out_dev *last, int32_t *missed,
+                                   hipStream_t s) {
+    if (nq == 0) return hipSuccess;
+    const uint64_t tm = n * ((nq + kRevisitQ - 1) / kRevisitQ), tl = (uint64_t)nseg * nq;
+    if (tm) revisit_missed_kernel<<<(unsigned)((tm + 255) / 256), 256, 0, s>>>(t, base, n, rids, nq, missed);
+    if (tl) revisit_last_kernel<<<(unsigned)((tl + 255) / 256), 256, 0, s>>>(t, base, seg_off, seg_cnt, nseg, rids, nq, last);
+    return hipGetLastError();
 }
 
 hipError_t launch_revisit(const DevTable &t, const stage_probe_out_dev *base, uint64_t n, const uint32_t *rids,
@@ -2877,7 +2939,7 @@ hipError_t launch_resident_reader(const DevTable &t, const ReaderRing &g, hipStr
     return hipGetLastError();
 }
 
-template <int KW, bool VIS>
+template <int KW, bool VIS, int R = 4>
 static void launch_scan_w(const DevTable &t, const uint64_t *keys, uint64_t n, uint32_t scan_size, uint32_t *counts,
                           uint8_t *recs, const uint32_t *rids, uint8_t *st, hipStream_t s, int blocks) {
     if (scan_size <= 63) {  // at most 64 kept records per leaf visit: group-skipping LDS form
@@ -2895,7 +2957,7 @@ static void launch_scan_w(const DevTable &t, const uint64_t *keys, uint64_t n, u
         return;
     }
 #define STAGE_SCAN_W(S) \
-    scan_kernel<false, S, 4, KW, VIS><<<blocks, 256, 0, s>>>(t, keys, nullptr, n, scan_size, counts, recs, rids, st)
+    scan_kernel<false, S, R, KW, VIS><<<blocks, 256, 0, s>>>(t, keys, nullptr, n, scan_size, counts, recs, rids, st)
     switch (t.cap / 64) {
         case 1: STAGE_SCAN_W(1); break;
         case 2: STAGE_SCAN_W(2); break;
@@ -2913,7 +2975,7 @@ static void launch_scan_r(const DevTable &t, const uint64_t *keys, const uint16_
     const bool var = t.key_width == 0;
     if (t.key_words == 2) return launch_scan_w<2, VIS>(t, keys, n, scan_size, counts, recs, rids, st, s, blocks);
     if (t.key_words == 4) return launch_scan_w<4, VIS>(t, keys, n, scan_size, counts, recs, rids, st, s, blocks);
-    if (!var && t.cap > 128) return launch_scan_w<1, VIS>(t, keys, n, scan_size, counts, recs, rids, st, s, blocks);
+    if (!var && t.cap > 128) return launch_scan_w<1, VIS, R>(t, keys, n, scan_size, counts, recs, rids, st, s, blocks);
 #define STAGE_SCAN(V, S) \
     scan_kernel<V, S, R, 1, VIS><<<blocks, 256, 0, s>>>(t, keys, lens, n, scan_size, counts, recs, rids, st)
     if (t.cap == 64) {
