@@ -1090,9 +1090,10 @@ def run_chq2(args):
     rids = (0xFFFFFFFE - np.arange(nq)).astype(np.uint32)  # nq transactions per step, one read id each
 
     state = {}
-    # the records land in one reused array (only the last step's are read): a fresh 12-MiB
-    # array per step costs the step its page faults
-    out_buf = np.zeros((nq, 1 << 14), stage.Q2_REC_DTYPE)
+    # the records land in one reused page-locked array (only the last step's are read): the
+    # library copies them there straight from the device (a fresh 12-MiB pageable array per step
+    # would cost the step its page faults and a staging copy)
+    out_buf = stage.pinned_empty((nq, 1 << 14), stage.Q2_REC_DTYPE)
 
     def step():
         if nq == 1:

@@ -19,7 +19,7 @@ ch = ChTables(W=args.warehouses, I=args.items, seed=args.seed & 0xFFFF, oracle=F
 ch.sync()
 nq = args.q2_batch
 rids = (0xFFFFFFFE - np.arange(nq)).astype(np.uint32)
-out = np.zeros((nq, 1 << 14), stage.Q2_REC_DTYPE)
+out = (stage.pinned_empty if os.environ.get("Q2_PINNED", "1") == "1" else np.zeros)((nq, 1 << 14), stage.Q2_REC_DTYPE)
 for _ in range(5):
     ch.query2_batch(rids, 3, out=out)
 t = ch.tables

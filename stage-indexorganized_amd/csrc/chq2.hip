@@ -168,11 +168,7 @@ void scan_rows(stage_table *t, uint64_t start, uint32_t scan_size, uint8_t *area
     auto *key = (uint64_t *)buf;
     auto *cnt = (uint32_t *)(buf + 56);  // 8 bytes before the rows
     q2_set_u64<<<1, 1, 0, s>>>(key, start);  // no host buffer outlives the call
-    // one scan on one wave: the row copies are its chain of round trips, so 8 rows in flight per
-    // round unless STAGE_SCAN_ROWS chose otherwise
-    ScanTuning tn = t->scan_tune;
-    if (!std::getenv("STAGE_SCAN_ROWS")) tn.rows = 8;
-    hip_check(launch_scan(v, key, nullptr, 1, scan_size, cnt, buf + 64, s, tn), "scan");
+    hip_check(launch_scan(v, key, nullptr, 1, scan_size, cnt, buf + 64, s, t->scan_tune), "scan");
     hip_check(hipMemcpyAsync(area, cnt, 8 + rows, hipMemcpyDeviceToHost, s), "d2h");
 }
 
@@ -404,10 +400,26 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         q2_finish<<<(n * nq + 255) / 256, 256, 0, s>>>(d_iout, iv.heap, iv.hstride, facts(item).key_pad(), n, nq,
                                                        d_rec, d_ab);
         hip_check(hipGetLastError(), "q2 kernels");
-        stage_q2_rec *recs = (stage_q2_rec *)(pq + q_rec);
-        hip_check(hipMemcpyAsync(pq + q_ab, d_ab, (q_rec - q_ab) + (uint64_t)n * nq * sizeof(stage_q2_rec),
-                                 hipMemcpyDeviceToHost, s),
-                  "d2h");  // [aborted][records]
+        // `out` in page-locked memory (stage_host_alloc, stage.pinned_empty) with room for every
+        // record: the records go straight there (one 2-D copy) instead of through the call
+        // staging and a host memcpy
+        bool to_out = false;
+        if (out && n <= max_out) {
+            hipPointerAttribute_t pa;
+            to_out = hipPointerGetAttributes(&pa, out) == hipSuccess && pa.type == hipMemoryTypeHost;
+            (void)hipGetLastError();  // a pageable pointer is not an error here
+        }
+        stage_q2_rec *recs = to_out ? out : (stage_q2_rec *)(pq + q_rec);
+        if (to_out) {
+            hip_check(hipMemcpyAsync(pq + q_ab, d_ab, 4ull * nq, hipMemcpyDeviceToHost, s), "d2h");
+            hip_check(hipMemcpy2DAsync(out, max_out * sizeof(stage_q2_rec), d_rec, n * sizeof(stage_q2_rec),
+                                       n * sizeof(stage_q2_rec), nq, hipMemcpyDeviceToHost, s),
+                      "d2h");
+        } else {
+            hip_check(hipMemcpyAsync(pq + q_ab, d_ab, (q_rec - q_ab) + (uint64_t)n * nq * sizeof(stage_q2_rec),
+                                     hipMemcpyDeviceToHost, s),
+                      "d2h");  // [aborted][records]
+        }
         lap("probes enqueued");
         hip_check(hipStreamSynchronize(s), "q2 sync");
         lap("results back");
@@ -453,9 +465,10 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
                 for (uint64_t j = 0; j < nu; ++j) recs[ui[j]].update_rc = rcs[j];
             }
         }
-        for (uint32_t q = 0; q < nq; ++q)
-            std::memcpy(out + (uint64_t)q * max_out, recs + (uint64_t)q * n,
-                        std::min<uint64_t>(n, max_out) * sizeof(stage_q2_rec));
+        if (!to_out)
+            for (uint32_t q = 0; q < nq; ++q)
+                std::memcpy(out + (uint64_t)q * max_out, recs + (uint64_t)q * n,
+                            std::min<uint64_t>(n, max_out) * sizeof(stage_q2_rec));
         lap("out copied");
         return STAGE_OK;
     });

@@ -83,6 +83,33 @@ class DeviceBuffer:
             pass
 
 
+class _PinnedBlock:
+    """stage_host_alloc memory kept alive by the numpy arrays viewing it."""
+
+    def __init__(self, nbytes):
+        p = c_vp()
+        check(lib().stage_host_alloc(max(int(nbytes), 16), ctypes.byref(p)), "stage_host_alloc")
+        self.ptr = p.value
+
+    def __del__(self):
+        try:
+            if self.ptr:
+                lib().stage_host_free(self.ptr)
+        except Exception:
+            pass
+
+
+def pinned_empty(shape, dtype):
+    """A numpy array in page-locked host memory (stage_host_alloc): result arrays the library
+    can copy into straight from the device (e.g. ch_query2_batch's `out`)."""
+    dtype = np.dtype(dtype)
+    count = int(np.prod(shape)) if np.ndim(shape) else int(shape)
+    blk = _PinnedBlock(count * dtype.itemsize)
+    buf = (ctypes.c_uint8 * max(count * dtype.itemsize, 1)).from_address(blk.ptr)
+    buf._stage_block = blk  # the block lives as long as an array viewing it
+    return np.frombuffer(buf, dtype=dtype, count=count).reshape(shape)
+
+
 class Stream:
     def __init__(self):
         p = c_vp()

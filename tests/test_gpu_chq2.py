@@ -41,13 +41,19 @@ def test_q2_matches_oracle_all_regions(ch, monkeypatch, q2_sort):
     assert recs.size > 1000 and recs["update"].sum() > 0 and recs["item_has_b"].sum() > 0
 
 
-@pytest.mark.parametrize("q2_sort", ["0", "1"])
-def test_q2_batch_equals_single_queries(ch, monkeypatch, q2_sort):
+@pytest.mark.parametrize("q2_sort,pinned", [("0", False), ("1", False), ("0", True)])
+def test_q2_batch_equals_single_queries(ch, monkeypatch, q2_sort, pinned):
     monkeypatch.setenv("STAGE_Q2_SORT", q2_sort)
     rids = np.array([10, 0xFFFFFFFE, 3, 25, 0xFFFFFFFE, 7], np.uint32)
+    # pinned: a page-locked `out` the records are copied into straight from the device
+    out = stage.pinned_empty((rids.size, 1 << 14), stage.Q2_REC_DTYPE) if pinned else None
     for target in (0, 3):
-        recs, ab = ch.query2_batch(rids, target)
+        if out is not None:
+            out[...] = np.zeros(1, stage.Q2_REC_DTYPE)[0]
+        recs, ab = ch.query2_batch(rids, target, out=out)
         assert recs.shape[0] == rids.size
+        if out is not None:
+            assert recs.base is not None and np.shares_memory(recs, out)
         for q, r in enumerate(rids):
             one, ab1 = ch.query2(target, read_id=int(r))
             assert ab[q] == ab1
@@ -74,6 +80,12 @@ def test_q2_visibility_and_commit(ch, monkeypatch):
     assert stock.update_key(k, 4, b"\x05\x00\x00\x00", 30) == ostock.update(k, 16, 4, b"\x05\x00\x00\x00", 30)
     stock.sync()
     brecs, babort = ch.query2_batch(np.array([10, 25, 40, 0xFFFFFFFE], np.uint32), 3)
+    pout = stage.pinned_empty((4, 1 << 14), stage.Q2_REC_DTYPE)
+    precs, pabort = ch.query2_batch(np.array([10, 25, 40, 0xFFFFFFFE], np.uint32), 3, out=pout)
+    assert (pabort == babort).all() and precs.shape == brecs.shape
+    for q in range(4):
+        if not babort[q]:
+            assert (precs[q] == brecs[q]).all()
     for q, rid in enumerate((10, 25, 40, 0xFFFFFFFE)):  # rid 10: retired versions with begin 0 -> FAILURE -> abort
         recs, ab = ch.query2(3, read_id=rid)
         orecs, oab = ch.query2_oracle(3, read_id=rid)
