@@ -461,7 +461,10 @@ int stage_ch_query2(stage_table *region, stage_table *nation, stage_table *suppl
 /* nq read-only Q2 transactions at read_ids[0..nq) in one pass (the scans once, every
  * query's STOCK / ITEM lookups in the same launches): out[q * max_per_query + k],
  * aborted[q]; *n_out = records per query (the visited suppliers do not depend on the read
- * id: the scans are TableScanExecutor ones, without visibility).  No updates are applied. */
+ * id: the scans are TableScanExecutor ones, without visibility).  No updates are applied.
+ * Each STOCK / ITEM key is probed once and its hit slot's visibility evaluated at every read
+ * id.  `out` in page-locked memory (stage_host_alloc) with max_per_query >= *n_out: the
+ * records are copied into it straight from the device (both entry points). */
 int stage_ch_query2_batch(stage_table *region, stage_table *nation, stage_table *supplier, stage_table *item,
                           stage_table *stock, const uint32_t *map_off, const uint64_t *d_map_keys,
                           int32_t target_region, const uint32_t *read_ids, uint32_t nq, stage_q2_rec *out,
