@@ -57,6 +57,7 @@ int stage_table_create(const stage_params *params, stage_table **out) {
         if (const char *g = std::getenv("STAGE_PROBE_MAX_BLOCKS")) t->tune.max_blocks = std::atoi(g);
         if (const char *g = std::getenv("STAGE_PROBE_STORE")) t->tune.store = std::atoi(g);
         if (const char *g = std::getenv("STAGE_PROBE_WIDE")) t->tune.wide = std::atoi(g);
+        if (const char *g = std::getenv("STAGE_PROBE_SMALL_BELOW")) t->tune.small_below = std::atoi(g);
         if (const char *g = std::getenv("STAGE_SCAN_ROWS")) t->scan_tune.rows = std::atoi(g);
         if (const char *g = std::getenv("STAGE_SL_SCANS")) t->scan_tune.first_scans = std::atoi(g);
         if (const char *g = std::getenv("STAGE_SCAN_MAX_BLOCKS")) t->scan_tune.max_blocks = std::atoi(g);

@@ -27,6 +27,7 @@ struct ProbeTuning {
     int store = 1;         // output stores: 0 temporal, 1 nontemporal, 2 write-through (sc1)
     int status_bytes = 32; // status record: 32 (stage_probe_out) or 16 (stage_probe_out16)
     int wide = 0;          // wide-key / large-leaf probes: 0 = probe_split_kernel, 1 = probe_kernel<.., G = 1>
+    int small_below = 16384;  // wide-key probes: 16-probe wave chunks below this many 64-probe chunks
 };
 
 hipError_t launch_resolve(const DevTable &t, const uint64_t *keys, const uint16_t *lens, uint64_t n, int le_child,

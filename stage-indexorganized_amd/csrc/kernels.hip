@@ -2726,7 +2726,7 @@ hipError_t launch_probe(const DevTable &t, const uint64_t *keys, const uint16_t 
     // wide fixed-width keys, and 8-byte keys in leaves above 128 slots (small rows): leaves of
     // up to 1024 slots, one probe in flight
     if (t.key_words > 1 || (!var && t.cap > 128)) {
-        const bool small = chunks < 16384;  // fewer 64-probe chunks than the chip holds waves
+        const bool small = chunks < (uint64_t)tune.small_below;  // fewer 64-probe chunks than the chip holds waves
         const int wblocks = small ? grid_for((n + 15) / 16, 4, tune.max_blocks > 0 ? tune.max_blocks : 16384) : blocks;
         // default: probe_split_kernel; STAGE_PROBE_WIDE=1: probe_kernel's one-probe-in-flight form
         const bool split = tune.wide != 1 && tune.status_bytes != 16;

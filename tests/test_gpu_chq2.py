@@ -126,3 +126,20 @@ def test_q2_visibility_and_commit(ch, monkeypatch):
     assert ab2 == oab2
     if not ab2:
         same(recs2, orecs2)
+
+
+def test_q2_batch_many_read_ids(ch):
+    """40 queries: the folded revisit evaluates read ids 16 at a time per probe (three groups, the
+    last partial); every query's records and abort flag equal its single-query run's."""
+    rng = np.random.default_rng(5)
+    rids = rng.choice(np.array([3, 10, 25, 40, 60, 0xFFFFFFFE], np.uint32), 40)
+    out = stage.pinned_empty((rids.size, 1 << 14), stage.Q2_REC_DTYPE)
+    recs, ab = ch.query2_batch(rids, 3, out=out)
+    seen = {}
+    for q, r in enumerate(rids):
+        if int(r) not in seen:
+            seen[int(r)] = ch.query2(3, read_id=int(r))
+        one, ab1 = seen[int(r)]
+        assert ab[q] == ab1, (q, r)
+        if not ab1:
+            same(recs[q], one)
