@@ -713,6 +713,57 @@ __device__ __forceinline__ void copy_rows(const DevTable &t, const uint32_t *img
     }
 }
 
+// position of the k-th (from 0) set bit of m (m has more than k bits set), per lane
+__device__ __forceinline__ uint32_t kth_set_bit(uint64_t m, uint32_t k) {
+    uint32_t pos = 0;
+#pragma unroll
+    for (int w = 32; w >= 1; w >>= 1) {
+        const uint32_t c = (uint32_t)__builtin_popcountll(m & ((1ull << w) - 1));
+        if (k >= c) {
+            k -= c;
+            m >>= w;
+            pos += (uint32_t)w;
+        }
+    }
+    return pos;
+}
+
+// Rows of at most 32 16-B chunks (512 B): the emitting lanes' rows (lane b of em: heap row
+// img, output position dst) copied with the whole wave spread over (row, chunk) pairs -- U
+// loads in flight per lane cover 64 * U / chunks rows per round trip (16 rows of 256 B), where
+// copy_rows moves R rows per round trip whatever their size.  Same bytes as copy_rows.
+template <int U>
+__device__ __forceinline__ void copy_rows_flat(const DevTable &t, uint64_t em, uint32_t img, uint32_t dst,
+                                               uint8_t *recs, uint32_t lane) {
+    const uint32_t chunks = t.stride >> 4;
+    const uint32_t rpr = (uint32_t)(U * 64) / chunks, nrows = (uint32_t)__builtin_popcountll(em);
+    uint32_t rk[U], ck[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint32_t f = (uint32_t)u * 64u + lane;
+        rk[u] = f / chunks;
+        ck[u] = f - rk[u] * chunks;
+    }
+    for (uint32_t r0 = 0; r0 < nrows; r0 += rpr) {
+        u32x4 v[U];
+        uint32_t d[U];
+        bool ok[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t k = r0 + rk[u];
+            ok[u] = rk[u] < rpr && k < nrows;
+            const int src = ok[u] ? (int)kth_set_bit(em, k) : 0;
+            const uint32_t im = (uint32_t)__shfl((int)img, src);
+            d[u] = (uint32_t)__shfl((int)dst, src);
+            v[u] = u32x4{0, 0, 0, 0};
+            if (ok[u] && im != 0xFFFFFFFFu) v[u] = reinterpret_cast<const u32x4 *>(t.heap + (uint64_t)im * t.hstride)[ck[u]];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (ok[u]) __builtin_nontemporal_store(v[u], reinterpret_cast<u32x4 *>(recs + (uint64_t)d[u] * t.stride) + ck[u]);
+    }
+}
+
 template <bool VARLEN, int KW>
 __device__ __forceinline__ bool key_less(const uint64_t *a, uint32_t al, const uint64_t *b, uint32_t bl) {
     if (KW == 1) return kv_lt(a[0], al, b[0], bl);
@@ -831,6 +882,10 @@ __device__ void scan_one(const DevTable &t, const uint64_t *x0, uint32_t xl, uin
                 }
             }
             uint64_t em = ballot(emit);
+            if (em && t.stride <= 512) {  // small rows: several per load instruction
+                copy_rows_flat<4>(t, em, img, produced + kr[s], recs, lane);
+                em = 0;
+            }
             while (em) {
                 uint32_t imr[R], dr[R];
                 int nk = 0;
@@ -893,6 +948,10 @@ struct RowSink {  // rows (and, for VIS, per-record statuses) as scan_one writes
             }
         }
         uint64_t em = ballot(on);
+        if (em && t.stride <= 512) {  // small rows: several per load instruction
+            copy_rows_flat<4>(t, em, img, produced + kr, recs, lane);
+            em = 0;
+        }
         while (em) {
             uint32_t imr[4], dr[4];
             int nk = 0;
