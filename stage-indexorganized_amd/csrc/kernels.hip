@@ -803,6 +803,9 @@ __device__ void scan_one(const DevTable &t, const uint64_t *x0, uint32_t xl, uin
     for (int w = 0; w < KW; ++w) x[w] = x0[w];
     for (uint32_t guard = 0; guard < scan_size + 2 && remaining > 0; ++guard) {
         const uint64_t base = (uint64_t)leaf * t.cap;
+        // the leaf's monotone slot prefix (info word), loaded beside the key columns
+        const uint32_t mp =
+            *reinterpret_cast<const uint32_t *>(t.head + (uint64_t)leaf * t.head_bytes + head_info_offset(t.cap, KW)) >> 16;
         uint64_t col[SPL][KW];
         uint32_t kl[SPL];
         uint64_t q[SPL];
@@ -836,13 +839,26 @@ __device__ void scan_one(const DevTable &t, const uint64_t *x0, uint32_t xl, uin
             m += (uint32_t)__builtin_popcountll(km[s]);
         }
         if (m == 0) break;
-        // key rank among the kept records (std::sort by KeyCompare; keys are unique)
+        // key rank among the kept records (std::sort by KeyCompare; keys are unique).  When
+        // every kept record lies in the leaf's monotone slot prefix [0, mp) (info word), keys
+        // increase with the slot, so a record's rank is its slot-order position: no compare loop
         uint32_t kr[SPL];
+        uint32_t top = 0;  // one past the highest kept slot
 #pragma unroll
-        for (int s = 0; s < SPL; ++s) kr[s] = 0;
+        for (int s = 0; s < SPL; ++s)
+            if (km[s]) top = (uint32_t)s * 64u + 64u - (uint32_t)__builtin_clzll(km[s]);
+        const bool mono = top <= mp;
+        {
+            uint32_t pre = 0;
+#pragma unroll
+            for (int s = 0; s < SPL; ++s) {
+                kr[s] = mono ? pre + count_below(km[s]) : 0u;
+                pre += (uint32_t)__builtin_popcountll(km[s]);
+            }
+        }
 #pragma unroll
         for (int s2 = 0; s2 < SPL; ++s2) {
-            uint64_t mm = km[s2];
+            uint64_t mm = mono ? 0ull : km[s2];
             while (mm) {
                 const int b = __builtin_ctzll(mm);
                 mm &= mm - 1;
@@ -1022,6 +1038,7 @@ __device__ uint32_t scan_one_compact(const DevTable &t, const uint64_t *x0, uint
     for (uint32_t guard = 0; guard < scan_size + 2 && remaining > 0; ++guard) {
         const uint64_t base = (uint64_t)leaf * t.cap;
         const uint8_t *hd = t.head + (uint64_t)leaf * t.head_bytes;
+        const uint32_t mp = *reinterpret_cast<const uint32_t *>(hd + head_info_offset(t.cap, KW)) >> 16;  // info word
         // slot groups that can hold a key >= x (lane g tests group g's max key)
         bool act = false;
         if (lane < (uint32_t)SPL) {
@@ -1073,8 +1090,11 @@ __device__ uint32_t scan_one_compact(const DevTable &t, const uint64_t *x0, uint
             ml = ll[lane];
             mslot = ls[lane];
         }
-        uint32_t kr = 0;
-        for (uint32_t j = 0; j < m; ++j) {
+        // the list is in slot order; when its last (highest) slot lies in the leaf's monotone slot
+        // prefix [0, mp) (info word), keys increase with the slot and the list order is the rank
+        const bool mono = ls[m - 1] < mp;
+        uint32_t kr = mono ? lane : 0u;
+        for (uint32_t j = 0; j < (mono ? 0u : m); ++j) {
             uint64_t kj[KW];
 #pragma unroll
             for (int w = 0; w < KW; ++w) kj[w] = lk[j * KW + w];
