@@ -77,10 +77,14 @@ inline bool is_copy_handle(uint64_t next_ptr) {
 }
 inline uint32_t copy_id(uint64_t next_ptr) { return (uint32_t)(next_ptr & STAGE_NEXT_INDEX_MASK); }
 
+// the probe was answered as BTree::Read(..., is_for_update = true) (stage_probe_batch_ex,
+// stage_reader_read_ex)
+inline bool for_update(const stage_probe_out &o) { return (o.flags & STAGE_FLAG_FOR_UPDATE) != 0; }
+
 // BTree::Read served the read from the overwrite copy (record in flight, copy header found,
 // not for update): Record::Neww + AddReader(commit_id) (b_tree.cpp:2087-2105)
 inline bool read_via_copy(const stage_probe_out &o, const stage_probe_ident &id) {
-    return o.status != STAGE_ST_NOT_FOUND && is_inserting(meta_word(o)) && is_copy_handle(id.next);
+    return !for_update(o) && o.status != STAGE_ST_NOT_FOUND && is_inserting(meta_word(o)) && is_copy_handle(id.next);
 }
 
 // RecordLocation (record_location.h:13-42)
@@ -221,7 +225,7 @@ inline std::vector<uint8_t> make_record(const stage_probe_out &o, const stage_pr
 
 struct PointLookup {
     ResultType result;     // what Execute() leaves in the transaction (FAILURE => returns false)
-    bool perform_read;     // PerformRead(txn, record->meta, cstamp) is called (not for_update)
+    bool perform_read;     // PerformRead(txn, record->meta, cstamp) is called (not for update)
     bool tuple;            // ycsb_tuple is produced
     bool retired;          // ... from a TupleHeader slot (retired framing)
     uint32_t cstamp;       // PerformRead facts (transaction_manager.cpp:362-410)
@@ -229,13 +233,14 @@ struct PointLookup {
     uint32_t copy_sstamp;
 };
 
-// IndexScanExecutor point lookup (executor.h:374-454) for a reader that is not for_update
+// IndexScanExecutor point lookup (executor.h:374-454); a for-update probe (STAGE_FLAG_FOR_UPDATE)
+// is the executor built with is_for_update: no PerformRead on the latest branch (:388)
 inline PointLookup point_lookup(const stage_probe_out &o) {
     PointLookup p{ResultType::SUCCESS, false, false, false, o.cstamp,
                   (o.flags & STAGE_FLAG_COPY_PRESENT) != 0, o.copy_sstamp};
     switch (o.status) {
         case STAGE_ST_LATEST:
-        case STAGE_ST_COPY: p.perform_read = true; p.tuple = true; break;  // txn_id >= cstamp
+        case STAGE_ST_COPY: p.perform_read = !for_update(o); p.tuple = true; break;  // txn_id >= cstamp
         case STAGE_ST_OLD: p.tuple = true; p.retired = true; break;       // begin <= txn_id <= end
         case STAGE_ST_FAIL_INVALID_TS: p.result = ResultType::FAILURE; break;  // begin/end INVALID
         default: break;  // NOT_FOUND: Read -> nullptr; CHAIN_MISS: walked off the chain

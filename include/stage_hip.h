@@ -48,6 +48,9 @@ extern "C" {
 #define STAGE_ST_CHAIN_MISS 5     /* no version visible to txn_id (tuple stays null)       */
 
 #define STAGE_FLAG_COPY_PRESENT 1u /* PerformRead would find an overwrite header (tm.cpp:379-399) */
+#define STAGE_FLAG_FOR_UPDATE 2u   /* answered as BTree::Read(..., is_for_update = true): the
+                                      executor skips PerformRead (executor.h:388) and Read did not
+                                      AddReader (b_tree.cpp:2087, 2114-2120)                  */
 
 typedef struct stage_table stage_table; /* one index-organized table: BTree + device image */
 
@@ -195,6 +198,16 @@ int stage_delete_key(stage_table *t, const uint8_t *key, uint16_t key_size, uint
  * stage_abort_insert_key = the INSERT entry (:949-979): FinalizeForDelete + FailForInsert on
  *   the leaf's last slot (an insert not in its leaf's last slot: STAGE_RC_INVALID). */
 int stage_abort_update_key(stage_table *t, const uint8_t *key, uint16_t key_size, uint8_t *rc_out);
+/* the writer's own record, is_for_update = true (PointUpdateExecutor / PointDeleteExecutor built
+ * with is_for_update, executor.h:194-340, 101-193; TestingTransactionUtil's Update(.., true) /
+ * Delete(.., true)): stage_update_key_owned = LeafNode::Update's in-place branch (b_tree.cpp:
+ * 1101-1104: no Dirty refusal of an in-flight record, no overwrite copy, no version; NotFound /
+ * NotNeededUpdate as stage_update_key); stage_delete_key_owned = LeafNode::Delete's is_for_update
+ * branch (:1210-1220: the meta word cleared, nothing for a commit to finalize; STAGE_RC_INVALID
+ * where stage_delete_key's merge rule applies).  Publish with stage_sync as any host write. */
+int stage_update_key_owned(stage_table *t, const uint8_t *key, uint16_t key_size, uint32_t payload_off,
+                           const uint8_t *delta, uint32_t delta_len, uint32_t writer_id, uint8_t *rc_out);
+int stage_delete_key_owned(stage_table *t, const uint8_t *key, uint16_t key_size, uint8_t *rc_out);
 int stage_abort_insert_key(stage_table *t, const uint8_t *key, uint16_t key_size, uint8_t *rc_out);
 uint32_t stage_key_words(stage_table *t);
 
@@ -339,6 +352,20 @@ int stage_set_output_layout(stage_table *t, uint32_t row_stride, uint32_t status
 int stage_probe_batch(stage_table *t, const uint64_t *d_keys, const uint16_t *d_lens,
                       const uint32_t *d_read_ids, const uint32_t *d_leaf_ids, uint64_t n,
                       stage_probe_out *d_out, uint8_t *d_records, void *stream);
+/* stage_probe_batch with BTree::Read's is_for_update per probe (b_tree.h:812-813; the
+ *   IndexScanExecutor point lookup of a transaction reading its own record, executor.h:376-388;
+ *   e.g. the TPC-C drivers' executors built with is_for_update, tpcc_delivery.cpp:104).
+ *   d_for_update[i] != 0: the record is read from the leaf even while an update is in flight
+ *   (b_tree.cpp:2087 takes the overwrite copy only when !is_for_update; :2114-2120 Record::New,
+ *   cstamp = the reader's id, no AddReader), i.e. the writer sees its own patched image; the
+ *   executor rule is then the same (read id >= the record's cstamp -> LATEST, else the chain)
+ *   with PerformRead skipped, which STAGE_FLAG_FOR_UPDATE in the status record says.  An
+ *   uncommitted insert is found by its own writer (the ordinary rule returns nothing for it).
+ *   d_for_update NULL = stage_probe_batch.  32-B status records only (STAGE_E_UNSUPPORTED with
+ *   stage_set_output_layout(.., 16)). */
+int stage_probe_batch_ex(stage_table *t, const uint64_t *d_keys, const uint16_t *d_lens,
+                         const uint32_t *d_read_ids, const uint32_t *d_leaf_ids, const uint8_t *d_for_update,
+                         uint64_t n, stage_probe_out *d_out, uint8_t *d_records, void *stream);
 int stage_scan_batch(stage_table *t, const uint64_t *d_start_keys, const uint16_t *d_lens,
                      uint64_t n, uint32_t scan_size, uint32_t *d_counts, uint8_t *d_records,
                      void *stream);
@@ -397,6 +424,10 @@ int stage_reader_read(stage_reader *r, uint64_t key, uint16_t key_size, uint32_t
                       stage_probe_out *out, uint8_t *record);
 int stage_reader_read_ident(stage_reader *r, uint64_t key, uint16_t key_size, uint32_t read_id,
                             stage_probe_out *out, uint8_t *record, stage_probe_ident *ident);
+/* stage_reader_read_ident with BTree::Read's is_for_update (see stage_probe_batch_ex); either
+ * reader kind */
+int stage_reader_read_ex(stage_reader *r, uint64_t key, uint16_t key_size, uint32_t read_id, int is_for_update,
+                         stage_probe_out *out, uint8_t *record, stage_probe_ident *ident);
 int stage_reader_stats(stage_reader *r, uint64_t *stats);
 int stage_reader_destroy(stage_reader *r);
 

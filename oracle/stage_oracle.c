@@ -959,8 +959,19 @@ static void emit_canonical(orc_tree *t, uint8_t *rec, const uint8_t *key, uint16
 }
 
 /* BTree::Read (b_tree.cpp:2066-2129) followed by the point-lookup branch of
- * IndexScanExecutor::Execute (executor.h:374-454), canonical output. */
+ * IndexScanExecutor::Execute (executor.h:374-454), canonical output.
+ * for_update: Read(..., is_for_update = true) -- the copy branch is taken only when
+ * `meta->IsInserting() && !is_for_update` (:2087), so the writer reads its own in-flight record
+ * from the leaf like any other (:2114-2120, cstamp = the reader's id, no AddReader); the
+ * executor's rule is unchanged apart from skipping PerformRead (executor.h:388), which the
+ * oracle's outputs do not model (the caller knows it asked for update). */
+static int read_one_fu(orc_tree *t, const uint8_t *key, uint16_t ks, uint32_t read_id, int for_update,
+                       orc_read_out *o, uint8_t *rec);
 static int read_one(orc_tree *t, const uint8_t *key, uint16_t ks, uint32_t read_id, orc_read_out *o, uint8_t *rec) {
+    return read_one_fu(t, key, ks, read_id, 0, o, rec);
+}
+static int read_one_fu(orc_tree *t, const uint8_t *key, uint16_t ks, uint32_t read_id, int for_update,
+                       orc_read_out *o, uint8_t *rec) {
     memset(o, 0, sizeof(*o));
     o->copy_sstamp = MAX_CID;
     uint32_t rs = t->key_pad + t->payload_size;
@@ -982,7 +993,7 @@ static int read_one(orc_tree *t, const uint8_t *key, uint16_t ks, uint32_t read_
     const uint8_t *rkey, *rpay;
     uint64_t next_tuple;
     int from_copy = 0;
-    if (m_inserting(m)) {
+    if (m_inserting(m) && !for_update) {
         orc_copy *c = pc;
         if (!c) { /* copy location 0 / header gone: Read returns nullptr */
             o->status = ORC_ST_NOT_FOUND;
@@ -1033,6 +1044,11 @@ static int read_one(orc_tree *t, const uint8_t *key, uint16_t ks, uint32_t read_
 
 int orc_read(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t read_id, orc_read_out *out, uint8_t *rec) {
     return read_one(t, key, (uint16_t)key_size, read_id, out, rec);
+}
+
+int orc_read_fu(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t read_id, int for_update,
+                orc_read_out *out, uint8_t *rec) {
+    return read_one_fu(t, key, (uint16_t)key_size, read_id, for_update, out, rec);
 }
 
 typedef struct {
@@ -1806,6 +1822,23 @@ int orc_update(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t payl
     return ORC_RET_OK;
 }
 
+/* LeafNode::Update, b_tree.cpp:1061-1163 with is_for_update == true: no WriteDirty refusal of an
+ * inserting record (:1077), ComparePayload and the newer-writer check as above (:1086-1100),
+ * then CopyPayload in place (:1101-1104) -- no copy, no PrepareForUpdate. */
+int orc_update_owned(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t payload_off, const uint8_t *delta,
+                     uint32_t delta_len, uint32_t writer_id) {
+    uint16_t ks = (uint16_t)key_size;
+    uint8_t *leaf;
+    orc_rmeta *mp = find_meta(t, key, ks, &leaf);
+    if (!mp) return ORC_RET_NOT_FOUND;
+    uint8_t *col = leaf + m_offset(mp->meta) + m_padded(mp->meta) + payload_off;
+    if (payload_off + delta_len > t->payload_size) return ORC_RET_INVALID;
+    if (memcmp(col, delta, delta_len) == 0) return ORC_RET_NOT_NEEDED_UPDATE; /* ComparePayload */
+    if (m_cstamp(mp->meta) > writer_id) return ORC_RET_NOT_NEEDED_UPDATE;
+    memcpy(col, delta, delta_len); /* CopyPayload */
+    return ORC_RET_OK;
+}
+
 /* CommitTransaction, UPDATE entry (transaction_manager.cpp:610-676) for a single writer
  * whose t_sstamp is `sstamp` (FindMinSstamp starts it at t_cstamp, :113-121). */
 int orc_commit_update(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t commit_id, uint32_t sstamp) {
@@ -1948,6 +1981,21 @@ int orc_delete(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t comm
     uint32_t valid = used_space(s) - st_deleted(s);
     if (leaf != t->root && valid <= t->merge_threshold)
         return ORC_RET_INVALID;
+    return ORC_RET_OK;
+}
+
+/* LeafNode::Delete with is_for_update == true (b_tree.cpp:1210-1220): meta := 0 (the copy the
+ * reference allocates at :1195-1203 is reachable from nothing and is not restated); no
+ * PerformDelete, hence no FinalizeDelete and no deleted-size change; the merge gate as orc_delete. */
+int orc_delete_owned(orc_tree *t, const uint8_t *key, uint32_t key_size) {
+    uint16_t ks = (uint16_t)key_size;
+    uint8_t *leaf;
+    orc_rmeta *mp = find_meta(t, key, ks, &leaf);
+    if (!mp) return ORC_RET_NOT_FOUND;
+    mp->meta = 0;
+    uint64_t s = *l_status(leaf);
+    uint32_t valid = used_space(s) - st_deleted(s);
+    if (leaf != t->root && valid <= t->merge_threshold) return ORC_RET_INVALID;
     return ORC_RET_OK;
 }
 

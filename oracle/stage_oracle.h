@@ -70,6 +70,15 @@ uint64_t orc_load_keys(orc_tree *t, const uint64_t *keys, uint64_t n, uint32_t k
  * when no tuple is produced. */
 int orc_read(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t read_id,
              orc_read_out *out, uint8_t *rec);
+/* orc_read with BTree::Read's is_for_update (b_tree.cpp:2087, 2114-2120): an in-flight record is
+ * read from the leaf (the writer's own image), never from its overwrite copy */
+int orc_read_fu(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t read_id, int for_update,
+                orc_read_out *out, uint8_t *rec);
+/* the writer's own record (is_for_update = true): LeafNode::Update's in-place branch
+ * (b_tree.cpp:1101-1104) and LeafNode::Delete's meta := 0 branch (:1210-1220) */
+int orc_update_owned(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t payload_off, const uint8_t *delta,
+                     uint32_t delta_len, uint32_t writer_id);
+int orc_delete_owned(orc_tree *t, const uint8_t *key, uint32_t key_size);
 /* batch of little-endian u64 keys of key_size bytes; rec may be NULL (only outs). */
 int orc_read_batch(orc_tree *t, const uint64_t *keys, uint32_t key_size, const uint32_t *read_ids,
                    uint64_t n, orc_read_out *outs, uint8_t *recs, int nthreads);

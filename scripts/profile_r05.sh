@@ -1,0 +1,53 @@
+#!/bin/bash
+# Round-5 profile passes on one box, from one tree; each pass its own run, PMC never combined
+# with trace domains.  Output: gpurun_out/prof_r05/<pass>/...
+#   c4_trace / c4_fetch / c4_write -> pmc_scan.json (scan_kernel, calibrated as pmc_probe.json)
+#   c3_trace                       -> the C3 write-path kernels on this tree
+#   q2_trace                       -> CH-Q2 step kernels
+# Usage: TREE=<git head> scripts/profile_r05.sh [pass ...]   (no pass names: all of them)
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out/prof_r05
+mkdir -p $OUT
+PASSES="$*"
+want() { [ -z "$PASSES" ] && return 0; for p in $PASSES; do [ "$p" = "$1" ] && return 0; done; return 1; }
+run() {  # name limit cmd...
+  local name=$1 lim=$2; shift 2
+  want "$name" || return 0
+  echo "=== $name"
+  timeout -k 10 $lim "$@" > $OUT/$name.log 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"
+  tail -n 3 $OUT/$name.log
+  if [ $rc -ne 0 ]; then exit $rc; fi
+}
+B="python3 -u bench.py --no-cpu-baseline"
+run c4_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/c4_trace -o c4 -- $B --config c4 --steps 5 --warmup 1
+run c4_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/c4_fetch -o c4 -- python3 scripts/profile_scan.py
+run c4_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/c4_write -o c4 -- python3 scripts/profile_scan.py
+run c3_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/c3_trace -o c3 -- $B --config c3 --steps 5 --warmup 1
+run q2_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/q2_trace -o q2 -- $B --config chq2 --steps 3 --warmup 1
+stamp() {  # file trace: add where / what the counters came from
+  python3 - "$1" "${TREE:-unknown}" "$2" <<'PY'
+import json, socket, subprocess, sys, time
+path, tree, trace = sys.argv[1:4]
+p = json.load(open(path))
+try:
+    gpu = subprocess.run(["rocm-smi", "--showproductname"], capture_output=True, text=True, timeout=30).stdout
+    gpu = [l.split(":", 2)[-1].strip() for l in gpu.splitlines() if "Card Series" in l or "Card SKU" in l][:2]
+except Exception:
+    gpu = []
+p["profiled"] = {"host": socket.gethostname(), "gpu": gpu, "date": time.strftime("%Y-%m-%d"), "tree": tree,
+                 "kernel_trace": trace}
+json.dump(p, open(path, "w"), indent=1)
+print(json.dumps(p["profiled"]))
+PY
+}
+# wide bytes per scan (whole 128-B lines): 100 heap rows of 1024 B + the key columns (512 B) of
+# about 3 leaves visited; the rest of FETCH_SIZE (heads, separator nodes) is counted 1x
+if [ -f $OUT/c4_fetch/c4_counter_collection.csv ] && [ -f $OUT/c4_write/c4_counter_collection.csv ]; then
+  python3 scripts/pmc_summary.py $OUT/c4_fetch/c4_counter_collection.csv $OUT/c4_write/c4_counter_collection.csv \
+    scan_kernel 262144 100000000 $OUT/pmc_scan.json 0 103936 > $OUT/pmc_summary.log 2>&1 &&
+    stamp $OUT/pmc_scan.json "prof_r05/c4_trace (same call)"
+fi
+find $OUT -name "*.csv" | sort

@@ -227,6 +227,26 @@ int stage_commit_update_key(stage_table *t, const uint8_t *key, uint16_t key_siz
     });
 }
 
+int stage_update_key_owned(stage_table *t, const uint8_t *key, uint16_t key_size, uint32_t payload_off,
+                           const uint8_t *delta, uint32_t delta_len, uint32_t writer_id, uint8_t *rc_out) {
+    if (!t || !key || (!delta && delta_len)) return fail(STAGE_E_ARG, "bad arguments");
+    return guarded([&] {
+        ensure_host_rows(t);
+        int rc = host(t).update_owned(key, key_size, payload_off, delta, delta_len, writer_id);
+        if (rc_out) *rc_out = (uint8_t)rc;
+        return STAGE_OK;
+    });
+}
+
+int stage_delete_key_owned(stage_table *t, const uint8_t *key, uint16_t key_size, uint8_t *rc_out) {
+    if (!t || !key) return fail(STAGE_E_ARG, "null argument");
+    return guarded([&] {
+        int rc = host(t).remove_owned(key, key_size);
+        if (rc_out) *rc_out = (uint8_t)rc;
+        return STAGE_OK;
+    });
+}
+
 int stage_delete_key(stage_table *t, const uint8_t *key, uint16_t key_size, uint32_t commit_id, uint8_t *rc_out) {
     if (!t || !key) return fail(STAGE_E_ARG, "null argument");
     return guarded([&] {
@@ -534,6 +554,23 @@ int stage_probe_batch(stage_table *t, const uint64_t *d_keys, const uint16_t *d_
     e = stage::launch_probe(view, d_keys, d_lens, d_read_ids, d_leaf_ids, n,
                             reinterpret_cast<stage::stage_probe_out_dev *>(d_out), d_records, pick(t, stream), tune);
     return hip_rc(e, "probe kernel");
+}
+
+int stage_probe_batch_ex(stage_table *t, const uint64_t *d_keys, const uint16_t *d_lens, const uint32_t *d_read_ids,
+                         const uint32_t *d_leaf_ids, const uint8_t *d_for_update, uint64_t n, stage_probe_out *d_out,
+                         uint8_t *d_records, void *stream) {
+    if (!d_for_update) return stage_probe_batch(t, d_keys, d_lens, d_read_ids, d_leaf_ids, n, d_out, d_records, stream);
+    if (!t) return fail(STAGE_E_ARG, "null table");
+    if (t->status_bytes != 32)
+        return fail(STAGE_E_UNSUPPORTED, "is_for_update probes need the 32-B status records (stage_set_output_layout)");
+    int rc = stage_probe_batch(t, d_keys, d_lens, d_read_ids, d_leaf_ids, n, d_out, d_records, stream);
+    if (rc) return rc;
+    stage::DevTable view = t->dev.view;
+    if (t->out_stride) view.stride = t->out_stride;
+    return hip_rc(stage::launch_for_update(view, d_for_update, d_read_ids, n,
+                                           reinterpret_cast<stage::stage_probe_out_dev *>(d_out), d_records,
+                                           pick(t, stream)),
+                  "for-update kernel");
 }
 
 int stage_set_output_layout(stage_table *t, uint32_t row_stride, uint32_t status_bytes) {

@@ -188,6 +188,7 @@ struct stage_reader {
         uint64_t key;
         uint16_t len;
         uint32_t rid;
+        bool for_update;
         stage_probe_out *out;
         uint8_t *rec;
         stage_probe_ident *ident;
@@ -205,6 +206,12 @@ struct stage_reader {
         bool busy = false;
     };
     static constexpr int kSlots = 2;
+    // byte offsets of a slot block's arrays, each 16-B aligned (the kernels store 16-B records
+    // and 8-B ident pairs there whatever max_batch is)
+    struct Layout {
+        uint64_t lens, rids, fu, out, rows, ident, bytes;
+    };
+    Layout lay{};
 
     stage_table *t = nullptr;
     uint32_t max_batch = 0;
@@ -231,26 +238,31 @@ struct stage_reader {
 };
 
 void stage_reader::launch(Slot &sl) {
-    const uint64_t n = sl.reqs.size(), mb = max_batch;
+    const uint64_t n = sl.reqs.size();
     uint64_t *keys = (uint64_t *)sl.h;
-    uint16_t *lens = (uint16_t *)(sl.h + 8 * mb);
-    uint32_t *rids = (uint32_t *)(sl.h + 10 * mb);
+    uint16_t *lens = (uint16_t *)(sl.h + lay.lens);
+    uint32_t *rids = (uint32_t *)(sl.h + lay.rids);
+    uint8_t *fu = sl.h + lay.fu;
+    bool any_fu = false;
     for (uint64_t i = 0; i < n; ++i) {
         keys[i] = sl.reqs[i].key;
         lens[i] = sl.reqs[i].len;
         rids[i] = sl.reqs[i].rid;
+        fu[i] = sl.reqs[i].for_update ? 1 : 0;
+        any_fu = any_fu || sl.reqs[i].for_update;
     }
     stage::DevTable view = t->dev.view;
     view.stride = (uint32_t)stride;
     hipError_t e = stage_capi::need_synced(t) ? hipErrorInvalidValue : hipSuccess;
     const int stale = e != hipSuccess;
+    auto *dout = (stage::stage_probe_out_dev *)(sl.hd + lay.out);
     if (!e)
-        e = stage::launch_probe(view, (const uint64_t *)sl.hd, (const uint16_t *)(sl.hd + 8 * mb),
-                                (const uint32_t *)(sl.hd + 10 * mb), nullptr, n,
-                                (stage::stage_probe_out_dev *)(sl.hd + 14 * mb), sl.hd + 46 * mb, sl.s, t->tune);
-    if (!e)
-        e = stage::launch_ident(view, (const stage::stage_probe_out_dev *)(sl.hd + 14 * mb), n,
-                                (uint32_t *)(sl.hd + (46 + stride) * mb), sl.s);
+        e = stage::launch_probe(view, (const uint64_t *)sl.hd, (const uint16_t *)(sl.hd + lay.lens),
+                                (const uint32_t *)(sl.hd + lay.rids), nullptr, n, dout, sl.hd + lay.rows, sl.s, t->tune);
+    if (!e && any_fu)  // the batch's is_for_update reads (BTree::Read(..., true)) re-answered
+        e = stage::launch_for_update(view, sl.hd + lay.fu, (const uint32_t *)(sl.hd + lay.rids), n, dout,
+                                     sl.hd + lay.rows, sl.s);
+    if (!e) e = stage::launch_ident(view, dout, n, (uint32_t *)(sl.hd + lay.ident), sl.s);
     if (!e) e = hipEventRecord(sl.ev, sl.s);
     if (e) {  // fail the batch now; complete() only delivers
         for (auto &r : sl.reqs) *r.rc = stale ? STAGE_E_STATE : STAGE_E_HIP;
@@ -260,10 +272,10 @@ void stage_reader::launch(Slot &sl) {
 }
 
 void stage_reader::complete(Slot &sl) {
-    const uint64_t n = sl.reqs.size(), mb = max_batch;
-    const stage_probe_out *out = (const stage_probe_out *)(sl.h + 14 * mb);
-    const uint8_t *rows = sl.h + 46 * mb;
-    const stage_probe_ident *ident = (const stage_probe_ident *)(sl.h + (46 + stride) * mb);
+    const uint64_t n = sl.reqs.size();
+    const stage_probe_out *out = (const stage_probe_out *)(sl.h + lay.out);
+    const uint8_t *rows = sl.h + lay.rows;
+    const stage_probe_ident *ident = (const stage_probe_ident *)(sl.h + lay.ident);
     if (n && hipEventSynchronize(sl.ev) != hipSuccess) {
         for (auto &r : sl.reqs) *r.rc = STAGE_E_HIP;
     } else {
@@ -381,7 +393,17 @@ int stage_reader_create(stage_table *t, uint32_t max_batch, uint32_t max_wait_us
         r->max_wait_us = max_wait_us;
         r->stride = facts(t).stride();
         r->row_bytes = 8 + facts(t).params().payload_size;
-        const uint64_t mb = max_batch, bytes = mb * (8 + 2 + 4 + 32 + r->stride + 8);
+        const uint64_t mb = max_batch;
+        auto al = [](uint64_t x) { return (x + 15) & ~15ull; };
+        auto &L = r->lay;
+        L.lens = al(8 * mb);
+        L.rids = L.lens + al(2 * mb);
+        L.fu = L.rids + al(4 * mb);
+        L.out = L.fu + al(mb);
+        L.rows = L.out + al(32 * mb);
+        L.ident = L.rows + al(r->stride * mb);
+        L.bytes = L.ident + al(8 * mb);
+        const uint64_t bytes = L.bytes;
         stage::hip_check(hipSetDevice(t->dev.device), "hipSetDevice");
         for (auto &sl : r->slot) {
             stage::hip_check(hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking), "reader stream");
@@ -399,8 +421,8 @@ int stage_reader_create(stage_table *t, uint32_t max_batch, uint32_t max_wait_us
     });
 }
 
-static int resident_read(ResidentReader &R, uint64_t key, uint16_t key_size, uint32_t read_id, stage_probe_out *out,
-                         uint8_t *record, stage_probe_ident *ident) {
+static int resident_read(ResidentReader &R, uint64_t key, uint16_t key_size, uint32_t read_id, bool for_update,
+                         stage_probe_out *out, uint8_t *record, stage_probe_ident *ident) {
     if (R.closing.load(std::memory_order_acquire) || R.dead.load(std::memory_order_acquire))
         return fail(STAGE_E_STATE, "resident reader has ended");
     const uint64_t q = R.tail.fetch_add(1, std::memory_order_acq_rel);
@@ -422,7 +444,9 @@ static int resident_read(ResidentReader &R, uint64_t key, uint16_t key_size, uin
     stage::ReaderReq &rq = R.req[slot];
     rq.key = key;
     rq.rid = read_id;
-    __atomic_store_n(&rq.tag, (uint32_t)(((q + 1) << 4) | (key_size & 15u)), __ATOMIC_RELEASE);
+    // tag: ticket + 1 above 4 bits of key length - 1 (1..8 bytes) and is_for_update
+    const uint32_t low = ((uint32_t)(key_size - 1) & 7u) | (for_update ? 8u : 0u);
+    __atomic_store_n(&rq.tag, (uint32_t)(((q + 1) << 4) | low), __ATOMIC_RELEASE);
     if (!wait([&] { return __atomic_load_n(R.done + slot, __ATOMIC_ACQUIRE) == (uint32_t)(q + 1); }))
         return fail(R.dead.load(), R.dead.load() == STAGE_E_STATE ? "device image is stale: the resident reader ended"
                                                                   : "resident reader failed on the device");
@@ -518,21 +542,27 @@ static void resident_destroy(ResidentReader &R) {
 
 int stage_reader_read(stage_reader *r, uint64_t key, uint16_t key_size, uint32_t read_id, stage_probe_out *out,
                       uint8_t *record) {
-    return stage_reader_read_ident(r, key, key_size, read_id, out, record, nullptr);
+    return stage_reader_read_ex(r, key, key_size, read_id, 0, out, record, nullptr);
 }
 
 int stage_reader_read_ident(stage_reader *r, uint64_t key, uint16_t key_size, uint32_t read_id, stage_probe_out *out,
                             uint8_t *record, stage_probe_ident *ident) {
+    return stage_reader_read_ex(r, key, key_size, read_id, 0, out, record, ident);
+}
+
+int stage_reader_read_ex(stage_reader *r, uint64_t key, uint16_t key_size, uint32_t read_id, int is_for_update,
+                         stage_probe_out *out, uint8_t *record, stage_probe_ident *ident) {
     if (!r) return fail(STAGE_E_ARG, "null reader");
     if (key_size == 0 || key_size > 8) return fail(STAGE_E_ARG, "key_size must be 1..8");
-    if (r->res) return resident_read(*r->res, key, key_size, read_id, out, record, ident);
+    const bool fu = is_for_update != 0;
+    if (r->res) return resident_read(*r->res, key, key_size, read_id, fu, out, record, ident);
     int rc = STAGE_E_STATE;
     uint32_t seq;
     {
         std::unique_lock<std::mutex> lk(r->mu);
         r->cv_space.wait(lk, [&] { return r->stop || r->open.size() < r->max_batch; });
         if (r->stop) return fail(STAGE_E_STATE, "reader is closing");
-        r->open.push_back({key, key_size, read_id, out, record, ident, &rc});
+        r->open.push_back({key, key_size, read_id, fu, out, record, ident, &rc});
         const int64_t now = now_ns();
         if (r->open.size() == 1) r->first_arrival_ns.store(now, std::memory_order_release);
         r->last_arrival_ns.store(now, std::memory_order_release);

@@ -570,6 +570,44 @@ int HostTable::update(const uint8_t *key, uint32_t len, uint32_t payload_off, co
     return STAGE_RC_OK;
 }
 
+// LeafNode::Update with is_for_update = true (b_tree.cpp:1061-1163): the transaction updates a
+// record it owns (its own in-flight update or insert, or a record it locked for update): no Dirty
+// check (:1077), the same ComparePayload / newer-writer NotNeededUpdate checks (:1086-1100), and
+// CopyPayload in place -- no overwrite copy, no PrepareForUpdate (:1101-1104).  The record gets
+// a new image row (rows are immutable); its meta word, next handle and any copy stay.
+int HostTable::update_owned(const uint8_t *key, uint32_t len, uint32_t payload_off, const uint8_t *delta,
+                            uint32_t delta_len, uint32_t writer_id) {
+    uint32_t leaf, slot;
+    if (find(key, len, &leaf, &slot) < 0) return STAGE_RC_NOT_FOUND;
+    const size_t i = (size_t)leaf * cap_ + slot;
+    const uint64_t m = meta_[i];
+    if ((uint64_t)payload_off + delta_len > p_.payload_size) return STAGE_RC_INVALID;
+    std::vector<uint8_t> pay(p_.payload_size);
+    image_payload(image_[i], pay.data());
+    if (std::memcmp(pay.data() + payload_off, delta, delta_len) == 0) return STAGE_RC_NOT_NEEDED_UPDATE;
+    if (meta_cstamp(m) > writer_id) return STAGE_RC_NOT_NEEDED_UPDATE;
+    std::memcpy(pay.data() + payload_off, delta, delta_len);  // CopyPayload
+    image_[i] = new_image(key, len, pay.data(), 0, 0);
+    touch(leaf, slot);
+    return STAGE_RC_OK;
+}
+
+// LeafNode::Delete with is_for_update = true (b_tree.cpp:1171-1251): the record's meta word is
+// cleared (vacant; the reference's copy allocation at :1195-1203 is reachable from nothing), no
+// deleted-size accounting (PointDeleteExecutor skips PerformDelete, so no FinalizeDelete runs).
+// BTree::Delete's merge check then sees the leaf's unchanged live size (RC_INVALID as remove()).
+int HostTable::remove_owned(const uint8_t *key, uint32_t len) {
+    uint32_t leaf, slot;
+    if (find(key, len, &leaf, &slot) < 0) return STAGE_RC_NOT_FOUND;
+    const size_t i = (size_t)leaf * cap_ + slot;
+    meta_[i] = 0;
+    cell(i);
+    Leaf &L = leaves_[leaf];
+    touch(leaf, slot);
+    if (nleaves_live_ > 1 && used_space(L) - L.deleted <= p_.merge_threshold) return STAGE_RC_INVALID;
+    return STAGE_RC_OK;
+}
+
 // CommitTransaction UPDATE entry (transaction_manager.cpp:610-676), single writer.
 int HostTable::commit_update(const uint8_t *key, uint32_t len, uint32_t commit_id, uint32_t sstamp) {
     uint32_t leaf, slot;

@@ -154,6 +154,12 @@ public:
     int commit_update(const uint8_t *key, uint32_t len, uint32_t commit_id, uint32_t sstamp);
     int finalize_update(const uint8_t *key, uint32_t len, uint32_t commit_id);
     int remove(const uint8_t *key, uint32_t len, uint32_t commit_id);
+    // the writer's own record (is_for_update = true): LeafNode::Update patches in place, no copy
+    // (b_tree.cpp:1101-1104); LeafNode::Delete clears the meta word, no copy reachable
+    // (:1210-1220)
+    int update_owned(const uint8_t *key, uint32_t len, uint32_t payload_off, const uint8_t *delta, uint32_t delta_len,
+                     uint32_t writer_id);
+    int remove_owned(const uint8_t *key, uint32_t len);
     int abort_update(const uint8_t *key, uint32_t len);
     int abort_insert(const uint8_t *key, uint32_t len);
     // the same for keys of <= 8 bytes passed little-endian in a u64

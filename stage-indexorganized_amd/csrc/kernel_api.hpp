@@ -98,6 +98,10 @@ hipError_t launch_revisit_segments(const DevTable &t, const stage_probe_out_dev 
                                    const uint64_t *seg_off, const uint32_t *seg_cnt, uint32_t nseg,
                                    const uint32_t *rids, uint32_t nq, stage_probe_out_dev *last, int32_t *missed,
                                    hipStream_t s);
+// stage_probe_batch_ex: after launch_probe of the same batch, re-answer the probes with fu[i] != 0
+// as BTree::Read(..., is_for_update = true) (status record and, if recs, the row); 32-B records
+hipError_t launch_for_update(const DevTable &t, const uint8_t *fu, const uint32_t *rids, uint64_t n,
+                             stage_probe_out_dev *out, uint8_t *recs, hipStream_t s);
 // stage_probe_ident: {location handle, next handle} of each probe's hit slot (two u32 per probe)
 hipError_t launch_ident(const DevTable &t, const stage_probe_out_dev *out, uint64_t n, uint32_t *ident, hipStream_t s);
 hipError_t launch_murmur(const void *keys, uint32_t key_len, uint32_t key_stride, uint64_t seed, uint64_t n,

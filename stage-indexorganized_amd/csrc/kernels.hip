@@ -229,10 +229,15 @@ struct ProbeRes {
 };
 
 // BTree::Read + IndexScanExecutor visibility for one wave-uniform probe whose slot word
-// (meta, next, image) is already known.
+// (meta, next, image) is already known.  FU: BTree::Read(..., is_for_update = true), the
+// writer's read of its own record: an in-flight record is read from the leaf, not from the
+// overwrite copy (b_tree.cpp:2087 takes the copy branch only when !is_for_update; the else
+// branch :2114-2120 is Record::New of the leaf image with cstamp = the reader's id and no
+// AddReader), and the executor skips PerformRead (executor.h:388) -- flag bit 2 says so.
+template <bool FU = false>
 __device__ __forceinline__ void visibility(const DevTable &t, int slot, uint64_t m, uint32_t next, uint32_t image,
                                            uint32_t rid, ProbeRes &r) {
-    r.flags = 0;
+    r.flags = FU ? 2u : 0u;
     r.hops = 0;
     r.copy_sstamp = kMaxCid;
     r.image = 0xFFFFFFFFu;
@@ -256,7 +261,7 @@ __device__ __forceinline__ void visibility(const DevTable &t, int slot, uint64_t
     }
     uint32_t img, chain;
     bool from_copy = false;
-    if (meta_inserting(m)) {
+    if (!FU && meta_inserting(m)) {
         if (!has_copy) {  // copy location 0 / header gone: Read returns nullptr
             r.status = ST_NOT_FOUND;
             return;
@@ -579,7 +584,7 @@ __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *
 // instance queued behind it on the same stream -- no wave outlives its instance's lifetime.
 
 // one wave-uniform probe (request j of the wave's lanes) with one probe in flight
-template <bool VARLEN, int SPL>
+template <bool VARLEN, int SPL, bool FU = false>
 __device__ __forceinline__ void ring_probe_one(const DevTable &t, uint32_t lane, int j, uint32_t leaf_l, uint64_t ok_l,
                                                uint32_t len_l, uint32_t rid_l, uint8_t *row, uint32_t out_chunks,
                                                u32x4 &a, u32x4 &b, uint32_t &id_loc, uint32_t &id_next) {
@@ -617,7 +622,7 @@ __device__ __forceinline__ void ring_probe_one(const DevTable &t, uint32_t lane,
         }
     }
     ProbeRes r;
-    visibility(t, slot, m, nx, im, rd, r);
+    visibility<FU>(t, slot, m, nx, im, rd, r);
     id_loc = r.status == ST_NOT_FOUND ? 0u : lc;
     id_next = r.status == ST_NOT_FOUND ? 0u : nx;
     for (uint32_t c0 = 0; c0 < out_chunks; c0 += 64) {
@@ -658,8 +663,10 @@ __global__ __launch_bounds__(64) void resident_reader_kernel(DevTable t, ReaderR
             continue;
         }
         const bool mine = lane >= d && lane < d + k;
-        const uint32_t len = t.key_width ? t.key_width : (mine ? (rq.w & 15u) : 8u);
+        // tag low nibble: key length - 1 (bits 0-2), is_for_update (bit 3)
+        const uint32_t len = t.key_width ? t.key_width : (mine ? (rq.w & 7u) + 1u : 8u);
         const uint32_t rid = mine ? rq.z : 0u;
+        const bool fu = mine && (rq.w & 8u) != 0;
         const uint64_t ok = order_key(mine ? ((uint64_t)rq.y << 32 | rq.x) : 0ull, len);
         uint32_t leaf = mine ? resolve_leaf<VARLEN, 1>(t, &ok, len, true) : 0u;
         u32x4 my_a = u32x4{0, 0, 0, 0}, my_b = u32x4{0, 0, 0, 0};
@@ -667,8 +674,12 @@ __global__ __launch_bounds__(64) void resident_reader_kernel(DevTable t, ReaderR
         for (uint32_t j = d; j < d + k; ++j) {
             u32x4 a, b;
             uint32_t il, in;
-            ring_probe_one<VARLEN, SPL>(t, lane, (int)j, leaf, ok, len, rid, g.rows + (uint64_t)(s0 + j) * t.stride,
-                                        out_chunks, a, b, il, in);
+            if (rl32(fu ? 1u : 0u, (int)j))
+                ring_probe_one<VARLEN, SPL, true>(t, lane, (int)j, leaf, ok, len, rid,
+                                                  g.rows + (uint64_t)(s0 + j) * t.stride, out_chunks, a, b, il, in);
+            else
+                ring_probe_one<VARLEN, SPL>(t, lane, (int)j, leaf, ok, len, rid, g.rows + (uint64_t)(s0 + j) * t.stride,
+                                            out_chunks, a, b, il, in);
             if (lane == j) {
                 my_a = a;
                 my_b = b;
@@ -2990,6 +3001,57 @@ __global__ __launch_bounds__(256) void ident_kernel(DevTable t, const stage_prob
         loc = w1.z;
     }
     reinterpret_cast<uint2 *>(ident)[i] = make_uint2(loc, next);
+}
+
+// stage_probe_batch_ex's is_for_update probes: a second pass over the flagged probes of a batch
+// the ordinary probe has answered (so the probe kernels stay as they are).  The hit slot is in
+// each status record -- also for an in-flight record the ordinary rule left NOT_FOUND (an
+// uncommitted insert without a copy) -- and its slot word gives the for-update outcome
+// (visibility<true>); the status record is rewritten and the row re-copied from the leaf image.
+// A wave takes 64 probes and walks its flagged ones wave-uniformly (lanes 0-1 store the record,
+// every lane a 16-B chunk of the row).
+__global__ __launch_bounds__(256) void for_update_kernel(DevTable t, const uint8_t *__restrict__ fu,
+                                                         const uint32_t *__restrict__ rids, uint64_t n,
+                                                         stage_probe_out_dev *__restrict__ out, uint8_t *__restrict__ recs) {
+    const uint32_t lane = lane_id();
+    const uint64_t base = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + uni32(threadIdx.x >> 6)) * 64;
+    const uint64_t i = base + lane;
+    uint64_t todo = ballot(i < n && fu[i] != 0);
+    const uint32_t chunks = t.stride >> 4;
+    while (todo) {
+        const int j = __builtin_ctzll(todo);
+        todo &= todo - 1;
+        const uint64_t p = base + (uint64_t)j;
+        const u32x4 *op = reinterpret_cast<const u32x4 *>(out + p);
+        u32x4 a = op[0], b = op[1];
+        const uint32_t rid = rids ? rids[p] : 0xFFFFFFFEu;
+        const uint32_t slot = a.z & 0xFFFF, leaf = a.y;
+        uint32_t image = 0xFFFFFFFFu;
+        if (slot < t.cap && leaf < t.nleaves) {
+            const SlotInfo si = t.slot[(uint64_t)leaf * t.cap + slot];
+            ProbeRes r;
+            visibility<true>(t, (int)slot, si.meta, si.next, si.image, rid, r);
+            pack_out(leaf, r, a, b);
+            image = r.image;
+        } else {
+            a.x |= 2u << 8;  // no record: NOT_FOUND stays, flagged for update
+        }
+        if (lane < 2) reinterpret_cast<u32x4 *>(out + p)[lane] = lane == 0 ? a : b;
+        if (recs) {
+            for (uint32_t c = lane; c < chunks; c += 64) {
+                u32x4 v = u32x4{0, 0, 0, 0};
+                if (image != 0xFFFFFFFFu) v = reinterpret_cast<const u32x4 *>(t.heap + (uint64_t)image * t.hstride)[c];
+                reinterpret_cast<u32x4 *>(recs + p * (uint64_t)t.stride)[c] = v;
+            }
+        }
+    }
+}
+
+hipError_t launch_for_update(const DevTable &t, const uint8_t *fu, const uint32_t *rids, uint64_t n,
+                             stage_probe_out_dev *out, uint8_t *recs, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    for_update_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(t, fu, rids, n, out, recs);
+    return hipGetLastError();
 }
 
 hipError_t launch_ident(const DevTable &t, const stage_probe_out_dev *out, uint64_t n, uint32_t *ident, hipStream_t s) {

@@ -108,6 +108,12 @@ SIGNATURES = {
     "stage_traverse_batch": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_uint64, ctypes.c_int, c_vp]),
     "stage_export_leaves": (ctypes.c_int64, [c_vp, ctypes.c_uint32, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp]),
     "stage_probe_batch": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_uint64, c_vp, c_vp, c_vp]),
+    "stage_probe_batch_ex": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_uint64, c_vp, c_vp, c_vp]),
+    "stage_reader_read_ex": (ctypes.c_int, [c_vp, ctypes.c_uint64, ctypes.c_uint16, ctypes.c_uint32, ctypes.c_int,
+                                            c_vp, c_vp, c_vp]),
+    "stage_update_key_owned": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint16, ctypes.c_uint32, c_vp, ctypes.c_uint32,
+                                              ctypes.c_uint32, c_u8p]),
+    "stage_delete_key_owned": (ctypes.c_int, [c_vp, c_vp, ctypes.c_uint16, c_u8p]),
     "stage_set_output_layout": (ctypes.c_int, [c_vp, ctypes.c_uint32, ctypes.c_uint32]),
     "stage_scan_batch": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_uint64, ctypes.c_uint32, c_vp, c_vp, c_vp]),
     "stage_resolve_batch": (ctypes.c_int, [c_vp, c_vp, c_vp, ctypes.c_uint64, ctypes.c_int, c_vp, c_vp]),

@@ -419,6 +419,22 @@ class Table:
                                      ctypes.byref(rc)), "update_key")
         return rc.value
 
+    def update_key_owned(self, key, payload_off, delta, writer_id):
+        """LeafNode::Update with is_for_update = true: in place, no copy (b_tree.cpp:1101-1104)"""
+        k = np.frombuffer(bytes(key), np.uint8)
+        d = np.frombuffer(bytes(delta), np.uint8)
+        rc = ctypes.c_uint8()
+        check(lib().stage_update_key_owned(self.h, k.ctypes.data, k.size, payload_off, d.ctypes.data, d.size,
+                                           writer_id, ctypes.byref(rc)), "update_key_owned")
+        return rc.value
+
+    def delete_key_owned(self, key):
+        """LeafNode::Delete with is_for_update = true: meta := 0 (b_tree.cpp:1210-1220)"""
+        k = np.frombuffer(bytes(key), np.uint8)
+        rc = ctypes.c_uint8()
+        check(lib().stage_delete_key_owned(self.h, k.ctypes.data, k.size, ctypes.byref(rc)), "delete_key_owned")
+        return rc.value
+
     def commit_update_key(self, key, commit_id, sstamp):
         k = np.frombuffer(bytes(key), np.uint8)
         rc = ctypes.c_uint8()
@@ -452,11 +468,16 @@ class Table:
         check(lib().stage_probe_batch(self.h, d_keys, d_lens, d_read_ids, d_leaf_ids, n, d_out, d_records,
                                       stream), "stage_probe_batch")
 
-    def probe(self, keys, read_ids=None, lens=None, leaf_ids=None, records=True):
-        """Batched BTree::Read + visibility.  Returns (out[n] PROBE_OUT_DTYPE, rows[n, stride] or None)."""
+    def probe(self, keys, read_ids=None, lens=None, leaf_ids=None, records=True, for_update=None):
+        """Batched BTree::Read + visibility.  Returns (out[n] PROBE_OUT_DTYPE, rows[n, stride] or None).
+        for_update: per-probe is_for_update flags (stage_probe_batch_ex)."""
         words, n = self.key_buffer(keys)
         bufs = [DeviceBuffer.from_numpy(words) if n else DeviceBuffer(8)]
         d_rids = d_lens = d_leaf = None
+        d_fu = None
+        if for_update is not None:
+            bufs.append(DeviceBuffer.from_numpy(np.ascontiguousarray(for_update, np.uint8)) if n else DeviceBuffer(8))
+            d_fu = bufs[-1].ptr
         if read_ids is not None:
             bufs.append(DeviceBuffer.from_numpy(np.ascontiguousarray(read_ids, np.uint32)))
             d_rids = bufs[-1].ptr
@@ -469,7 +490,11 @@ class Table:
         dt = PROBE_OUT16_DTYPE if getattr(self, "status_bytes", 32) == 16 else PROBE_OUT_DTYPE
         d_out = DeviceBuffer(n * dt.itemsize)
         d_rec = DeviceBuffer(n * self.stride) if records else None
-        self.probe_device(bufs[0].ptr, n, d_out.ptr, d_rec.ptr if d_rec else None, d_rids, d_lens, d_leaf)
+        if d_fu is None:
+            self.probe_device(bufs[0].ptr, n, d_out.ptr, d_rec.ptr if d_rec else None, d_rids, d_lens, d_leaf)
+        else:
+            check(lib().stage_probe_batch_ex(self.h, bufs[0].ptr, d_lens, d_rids, d_leaf, d_fu, n, d_out.ptr,
+                                             d_rec.ptr if d_rec else None, None), "stage_probe_batch_ex")
         check(lib().stage_device_sync(), "sync")
         out = d_out.to_numpy(dt, n)
         rows = d_rec.to_numpy(np.uint8, n * self.stride).reshape(n, self.stride) if d_rec else None
@@ -630,6 +655,16 @@ class Reader:
         check(lib().stage_reader_read(self.h, int(key), key_size or self.table.key_width, read_id, out.ctypes.data,
                                       _ptr(row)), "reader_read")
         return out[0], row
+
+    def read_ex(self, key, read_id=0xFFFFFFFE, for_update=False, key_size=None):
+        """stage_reader_read_ex: (out, row, ident) of BTree::Read(.., is_for_update)"""
+        out = np.zeros(1, PROBE_OUT_DTYPE)
+        row = np.zeros(8 + self.table.payload_size, np.uint8)
+        ident = np.zeros(1, IDENT_DTYPE)
+        check(lib().stage_reader_read_ex(self.h, int(key), key_size or self.table.key_width, read_id,
+                                         1 if for_update else 0, out.ctypes.data, row.ctypes.data,
+                                         ident.ctypes.data), "reader_read_ex")
+        return out[0], row, ident[0]
 
     def read_ident(self, key, read_id=0xFFFFFFFE, key_size=None):
         """stage_reader_read_ident: (out, row, ident)"""

@@ -12,8 +12,8 @@ TransactionScheduler tests (testing_transaction_util.h:203-309) run their ops on
 the written order; a txn begins (read id = counter++) at its first op; an explicit Abort() op
 takes a counter value (GetNextCurrentTidCounter, :275); a txn whose op failed (e.g. an update
 of a record another txn is updating: Dirty) is aborted on the spot without one, and its later
-ops are skipped (:221-224, :302-308).  Reads with is_for_update = true (the writer's own-write
-reads) are not restated: that path stays on the host.
+ops are skipped (:221-224, :302-308).  Since round 5 the ops with is_for_update = true (the
+writer's reads, updates and deletes of its own record, MVCCTest) are restated too.
 
 Op vocabulary (keys: "key" = u64 little-endian of key_size bytes, "key_str" = ASCII bytes):
   insert        key, payload_u64 (payload = those u64 words), cid: Insert + FinalizeInsert
@@ -27,8 +27,11 @@ Op vocabulary (keys: "key" = u64 little-endian of key_size bytes, "key_str" = AS
   abort_update  key: AbortTransaction UPDATE entry
   finalize_update key, cid: BTree::FinalizeUpdate (BTreeTest style)
   delete        key, cid: PointDeleteExecutor + CommitTransaction DELETE
+  update_owned  key, off, payload_u64, wid: LeafNode::Update with is_for_update = true (in place)
+  delete_owned  key: LeafNode::Delete with is_for_update = true (meta := 0)
   read          key, rid, expect: {"found": false} | {"found": true, "payload_u64": [...]}
-                (IndexScanExecutor point lookup at read id rid; canonical payload)
+                (IndexScanExecutor point lookup at read id rid; canonical payload);
+                for_update: true = BTree::Read(.., is_for_update = true), PerformRead skipped
   scan          key, size, expect_keys (TableScanExecutor over RangeScanBySize/Iterator)
 Run `python tests/golden/make_scenarios.py` to regenerate.
 """
@@ -161,30 +164,77 @@ def abort_version_chain_test():
 
 
 def mvcc_test():
-    """TEST_F(ExecuteTest, MVCCTest) first schedule, test/testing_execute.cpp:1397-1424: Txn0
-    reads key 0 four times, updates it to 1, reads key 100, commits; then Txn1 reads key 0.
-    Not restated: Txn0's own-write read of key 0 (is_for_update = true, results[4] == 1) and
-    the later schedules of own-write re-updates / insert-delete within one txn -- the writer's
-    own path, kept on the host (north star)."""
+    """TEST_F(ExecuteTest, MVCCTest), test/testing_execute.cpp:1397-1470, all three schedules.
+    Schedule 1 (:1405-1428): Txn0 reads key 0 four times, updates it to 1, reads it back for
+    update (its own in-flight update: BTree::Read(.., is_for_update = true) reads the leaf, not the
+    copy -- b_tree.cpp:2087, 2114-2120 -- and the executor skips PerformRead, executor.h:388), reads
+    key 100 for update, commits; then Txn1 reads key 0.  Schedule 2 (:1430-1441): one txn updates
+    key 0 to 1 (already 1: NotNeededUpdate), then to 2, 3, 4 with is_for_update = true (LeafNode::
+    Update's in-place branch, b_tree.cpp:1101-1104) and reads 4 back for update.  Schedule 3
+    (:1443-1470): one txn inserts key 1000, deletes it for update (meta := 0, b_tree.cpp:1210-1220),
+    reads nothing, again, then inserts it, reads 2, updates it in place to 3 and reads 3."""
     tid = Counter()
     ops = create_table(tid)
+    # schedule 1
     r0 = tid.next()
     for k in range(4):
         ops.append({"op": "read", "key": 0, "rid": r0, "expect": {"found": True, "payload_u64": [0]},
-                    "src": f":1406 (assert results[{k}] == 0)"})
-    ops.append({"op": "update", "key": 0, "off": 0, "payload_u64": [1], "wid": r0, "expect_rc": 1, "src": ":1410"})
-    ops.append({"op": "read", "key": 100, "rid": r0, "expect": {"found": False},
-                "src": ":1412 (assert results[5] == -1)"})
+                    "src": f":{1409 + k} (assert results[{k}] == 0, :{1421 + k})"})
+    ops.append({"op": "update", "key": 0, "off": 0, "payload_u64": [1], "wid": r0, "expect_rc": 1, "src": ":1413"})
+    ops.append({"op": "read", "key": 0, "rid": r0, "for_update": True, "expect": {"found": True, "payload_u64": [1]},
+                "src": ":1414 Read(0, true) (assert results[4] == 1, :1425)"})
+    ops.append({"op": "read", "key": 100, "rid": r0, "for_update": True, "expect": {"found": False},
+                "src": ":1415 Read(100, true) (assert results[5] == -1, :1426)"})
     c0 = tid.next()
-    ops.append({"op": "commit_update", "key": 0, "cid": c0, "src": ":1413"})
+    ops.append({"op": "commit_update", "key": 0, "cid": c0, "src": ":1416"})
     r1 = tid.next()
     ops.append({"op": "read", "key": 0, "rid": r1, "expect": {"found": True, "payload_u64": [1]},
-                "src": ":1414 (assert schedules[1].results[0] == 1)"})
+                "src": ":1417 (assert schedules[1].results[0] == 1, :1427)"})
     # a reader that began before Txn0 committed still reads the old version
     ops.append({"op": "read", "key": 0, "rid": r0, "expect": {"found": True, "payload_u64": [0]},
                 "src": "derived: read id r0 < commit id, inclusive [begin, end] (executor.h:407-449)"})
     tid.next()
-    return {"name": "ExecuteTest.MVCCTest", "source": "test/testing_execute.cpp:1397-1424", "table": CT_TABLE,
+    # schedule 2
+    r2 = tid.next()
+    ops.append({"op": "update", "key": 0, "off": 0, "payload_u64": [1], "wid": r2, "expect_rc": 7,
+                "src": ":1433 Update(0, 1, false): the value is already 1 (ComparePayload -> NotNeededUpdate)"})
+    for v, line in ((2, 1434), (3, 1435), (4, 1436)):
+        ops.append({"op": "update_owned", "key": 0, "off": 0, "payload_u64": [v], "wid": r2, "expect_rc": 1,
+                    "src": f":{line} Update(0, {v}, true) (LeafNode::Update in place, b_tree.cpp:1101-1104)"})
+    ops.append({"op": "read", "key": 0, "rid": r2, "for_update": True, "expect": {"found": True, "payload_u64": [4]},
+                "src": ":1437 Read(0, true) (assert results[0] == 4, :1440)"})
+    tid.next()  # Commit(): nothing in the rw-set (the updates were for update, the first NotNeeded)
+    r = tid.next()
+    ops.append({"op": "read", "key": 0, "rid": r, "expect": {"found": True, "payload_u64": [4]},
+                "src": "derived: an in-place update keeps the record's cstamp; a later reader sees 4"})
+    tid.next()
+    # schedule 3
+    r3 = tid.next()
+    for n, v in enumerate((0, 1)):
+        ops.append({"op": "insert_inflight", "key": 1000, "payload_u64": [v], "wid": r3,
+                    "src": f":{1448 + 4 * n} Insert(1000, {v}) (InsertExecutor: BTree::Insert at the read id)"})
+        ops.append({"op": "delete_owned", "key": 1000, "expect_rc": 1,
+                    "src": f":{1449 + 4 * n} Delete(1000, true) (LeafNode::Delete: meta := 0, b_tree.cpp:1210-1220)"})
+        ops.append({"op": "read", "key": 1000, "rid": r3, "for_update": True, "expect": {"found": False},
+                    "src": f":{1450 + 4 * n} Read(1000, true) (assert results[{n}] == -1, :{1466 + n})"})
+    ops.append({"op": "insert_inflight", "key": 1000, "payload_u64": [2], "wid": r3, "src": ":1456 Insert(1000, 2)"})
+    ops.append({"op": "read", "key": 1000, "rid": r3, "for_update": True, "expect": {"found": True, "payload_u64": [2]},
+                "src": ":1457 Read(1000, true) (assert results[2] == 2, :1468)"})
+    ops.append({"op": "update_owned", "key": 1000, "off": 0, "payload_u64": [3], "wid": r3, "expect_rc": 1,
+                "src": ":1459 Update(1000, 3, true)"})
+    ops.append({"op": "read", "key": 1000, "rid": r3, "for_update": True, "expect": {"found": True, "payload_u64": [3]},
+                "src": ":1460 Read(1000, true) (assert results[3] == 3, :1469)"})
+    # an other transaction's read of the uncommitted insert returns nothing (b_tree.cpp:2087-2095)
+    ops.append({"op": "read", "key": 1000, "rid": r3, "expect": {"found": False},
+                "src": "derived: not for update, the in-flight insert has no copy -> nullptr"})
+    c3 = tid.next()
+    ops.append({"op": "commit_insert", "key": 1000, "cid": c3,
+                "src": ":1462 Commit() (CommitTransaction INSERT: FinalizeForInsert(t_cstamp) on the live record)"})
+    r = tid.next()
+    ops.append({"op": "read", "key": 1000, "rid": r, "expect": {"found": True, "payload_u64": [3]},
+                "src": "derived: after the commit another reader sees 3"})
+    tid.next()
+    return {"name": "ExecuteTest.MVCCTest", "source": "test/testing_execute.cpp:1397-1470", "table": CT_TABLE,
             "ops": ops}
 
 

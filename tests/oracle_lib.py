@@ -29,6 +29,9 @@ _SIG = {
     "orc_load_ycsb": (u64, [vp, u64, u64, u32, ctypes.c_int]),
     "orc_load_keys": (u64, [vp, vp, u64, u32, ctypes.c_int]),
     "orc_read": (ctypes.c_int, [vp, vp, u32, u32, vp, vp]),
+    "orc_read_fu": (ctypes.c_int, [vp, vp, u32, u32, ctypes.c_int, vp, vp]),
+    "orc_update_owned": (ctypes.c_int, [vp, vp, u32, u32, vp, u32, u32]),
+    "orc_delete_owned": (ctypes.c_int, [vp, vp, u32]),
     "orc_read_batch": (ctypes.c_int, [vp, vp, u32, vp, u64, vp, vp, ctypes.c_int]),
     "orc_read_batch_timed": (u64, [vp, vp, u32, vp, u64, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]),
     "orc_scan": (u32, [vp, vp, u32, u32, vp]),
@@ -171,11 +174,11 @@ class OracleTree:
         keys = np.ascontiguousarray(keys, np.uint64)
         return lib().orc_load_keys(self.t, keys.ctypes.data, keys.size, key_size, mode)
 
-    def read(self, key, key_size, read_id=0xFFFFFFFE):
+    def read(self, key, key_size, read_id=0xFFFFFFFE, for_update=False):
         kb = key_bytes(key, key_size)
         out = np.zeros(1, READ_OUT_DTYPE)
         rec = np.zeros(self.row, np.uint8)
-        lib().orc_read(self.t, kb, key_size, read_id, out.ctypes.data, rec.ctypes.data)
+        lib().orc_read_fu(self.t, kb, key_size, read_id, 1 if for_update else 0, out.ctypes.data, rec.ctypes.data)
         return out[0], rec
 
     def read_ident(self, key, key_size, read_id=0xFFFFFFFE):
@@ -270,6 +273,13 @@ class OracleTree:
     def update(self, key, key_size, payload_off, delta, writer_id):
         d = bytes(delta)
         return lib().orc_update(self.t, key_bytes(key, key_size), key_size, payload_off, d, len(d), writer_id)
+
+    def update_owned(self, key, key_size, payload_off, delta, writer_id):
+        d = bytes(delta)
+        return lib().orc_update_owned(self.t, key_bytes(key, key_size), key_size, payload_off, d, len(d), writer_id)
+
+    def delete_owned(self, key, key_size):
+        return lib().orc_delete_owned(self.t, key_bytes(key, key_size), key_size)
 
     def update_batch(self, keys, key_size, payload_off, deltas, wid, cid):
         """orc_update_batch: returns (rc[n], n_ok)"""

@@ -78,11 +78,16 @@ class OracleBackend:
             return self.t.finalize_update(k, ks, op["cid"])
         if o == "delete":
             return self.t.delete(k, ks, op["cid"])
+        if o == "update_owned":
+            d = np.array(op["payload_u64"], np.uint64).view(np.uint8).tobytes()
+            return self.t.update_owned(k, ks, op["off"], d, op["wid"])
+        if o == "delete_owned":
+            return self.t.delete_owned(k, ks)
         raise ValueError(o)
 
     def read(self, op):
         k, ks = key_of(op, self.ks)
-        out, rec = self.t.read(k, ks, op["rid"])
+        out, rec = self.t.read(k, ks, op["rid"], for_update=op.get("for_update", False))
         return int(out["status"]), rec[8:8 + self.ps]
 
     def scan(self, op):
@@ -129,6 +134,11 @@ class DeviceBackend:
             return t.finalize_update(int.from_bytes(k, "little"), op["cid"], key_size=ks)
         if o == "delete":
             return t.delete_key(k, op["cid"])
+        if o == "update_owned":
+            d = np.array(op["payload_u64"], np.uint64).view(np.uint8).tobytes()
+            return t.update_key_owned(k, op["off"], d, op["wid"])
+        if o == "delete_owned":
+            return t.delete_key_owned(k)
         raise ValueError(o)
 
     def _key(self, op):
@@ -136,10 +146,17 @@ class DeviceBackend:
         return np.array([int.from_bytes(k, "little")], np.uint64), np.array([ks], np.uint16)
 
     def read(self, op):
+        """A read for update goes through stage_probe_batch_ex, whose status record must carry
+        STAGE_FLAG_FOR_UPDATE (the executor skips PerformRead, executor.h:388); -1 = flag missing."""
         self.t.sync()
         keys, lens = self._key(op)
+        fu = op.get("for_update", False)
         out, rows = self.t.probe(keys, read_ids=np.array([op["rid"]], np.uint32),
-                                 lens=lens if self.ks == 0 else None)
+                                 lens=lens if self.ks == 0 else None,
+                                 for_update=np.array([1], np.uint8) if fu else None)
+        flag = (int(out["flags"][0]) & 2) != 0
+        if flag != fu:
+            return -1, rows[0, 8:8 + self.ps]
         return int(out["status"][0]), rows[0, 8:8 + self.ps]
 
     def scan(self, op):

@@ -9,8 +9,9 @@ FuzzyReadTest, MVCCTest and testing_btree.cpp Update / Upsert):
   leaves every leaf identical to the oracle's after each write (the device reads of the same
   scenarios are tests/test_gpu_scenarios.py).
 
-Unpinned (no reference assertion reaches them through this path): a writer's own-write reads
-(is_for_update = true, MVCCTest results[4]) and re-updates of its own in-flight record.
+Round 5: MVCCTest is restated in full (its three schedules), including the writer's own-record
+operations with is_for_update = true -- reads (results[4] == 1, :1425; 4, :1440; -1 / -1 / 2 / 3,
+:1466-1469), in-place updates and deletes (stage_update_key_owned / stage_delete_key_owned).
 """
 import pytest
 
@@ -54,4 +55,9 @@ def test_fixture_covers_the_cited_assertions():
                   ":1038", ":1072", ":1107", ":1142", ":1178", ":1215", ":1258", ":1259", ":1295", ":1296",
                   ":1338", ":1339", ":1341", ":1382", ":1383", ":1384", ":1387"):
         assert f"assert {cited}" in srcs, cited
+    # round 5: MVCCTest's is_for_update operations (testing_execute.cpp:1414-1469)
+    for cited in (":1425", ":1426", ":1427", ":1440", ":1466", ":1467", ":1468", ":1469"):
+        assert f"{cited})" in srcs, cited
+    fu = [op for s in SCEN for op in s["ops"] if op.get("for_update")]
+    assert len(fu) == 7 and {op["op"] for s in SCEN for op in s["ops"]} >= {"update_owned", "delete_owned"}
     assert stage.RC_NOT_NEEDED_UPDATE == 7
