@@ -100,8 +100,9 @@ def test_probe_batch_for_update_matches_oracle(states):
     out, _ = tab.probe(keys, read_ids=rids, for_update=fu)
     plain, _ = tab.probe(keys, read_ids=rids)
     copy_to_latest = np.count_nonzero((plain["status"] == stage.ST_COPY) & (out["status"] == stage.ST_LATEST))
-    own_insert = np.count_nonzero((plain["status"] == stage.ST_NOT_FOUND) & (out["status"] == stage.ST_LATEST))
-    assert copy_to_latest >= 1000 and own_insert == 1000, (copy_to_latest, own_insert)
+    assert copy_to_latest >= 1500, copy_to_latest  # every in-flight update (keys may repeat)
+    ins = slice(4000, 5000)  # the uncommitted inserts: nothing for others, the record for its writer
+    assert (plain["status"][ins] == stage.ST_NOT_FOUND).all() and (out["status"][ins] == stage.ST_LATEST).all()
 
 
 def test_probe_batch_for_update_all_off_equals_plain(states):
@@ -125,7 +126,7 @@ def test_probe_batch_for_update_ragged_and_empty(states):
 
 
 def test_for_update_needs_32_byte_records(gpu):
-    tab = stage.Table(key_width=8, payload_size=100)
+    tab = stage.Table(key_width=8)  # the YCSB geometry (16-B records need 64-slot leaves)
     tab.load_ycsb(0, 1000, 8)
     tab.sync()
     tab.set_output_layout(0, 16)
