@@ -190,6 +190,17 @@ void HostTable::image_payload(uint32_t img, uint8_t *dst) const {
     else throw std::logic_error("device-written heap row read before materialize_device_rows");
 }
 
+void HostTable::reserve_adoption(uint64_t add) {
+    auto room = [](auto &v, uint64_t k) {
+        if (v.capacity() < v.size() + k) v.reserve(std::max<uint64_t>(v.size() + k, 2 * v.capacity()));
+    };
+    room(copies_, add);
+    room(copy_live_, add);
+    room(versions_, add);
+    std::lock_guard<std::mutex> g(ssn_.mu);
+    room(ssn_.e, add);
+}
+
 void HostTable::adopt_device_epoch(const CopyHdr *copies, const uint32_t *writers, uint64_t nc,
                                    const VersionHdr *versions, uint64_t nv, uint64_t nimages, const SlotWords *slots,
                                    uint64_t nslots) {
@@ -222,9 +233,10 @@ void HostTable::adopt_device_epoch(const CopyHdr *copies, const uint32_t *writer
     {
         std::lock_guard<std::mutex> g(ssn_.mu);
         room(ssn_.e, nc);  // not reserve(c0 + nc): an exact reserve reallocates every epoch
-        const uint64_t e0 = ssn_.e.size();
-        ssn_.e.resize(e0 + nc);
-        CopySsn *dst = ssn_.e.data() + e0;
+        // the epoch's copies are c0 .. c0 + nc - 1: their SSN state goes at the same ids
+        if (ssn_.e.size() > c0) throw std::runtime_error("adopt_device_epoch: SSN state ahead of the copies");
+        ssn_.e.resize(c0 + nc, CopySsn{0, 0, 0, kMaxCid, 0, 0, 0});
+        CopySsn *dst = ssn_.e.data() + c0;
         parallel_chunks(nc, [&](uint64_t b, uint64_t e) {
             for (uint64_t k = b; k < e; ++k) {
                 const uint32_t w = writers ? writers[k] : 0;
@@ -945,13 +957,18 @@ uint64_t HostTable::update_batch(const uint8_t *keys, uint32_t key_stride, uint6
     });
     lap("concat");
     {
+        // each copy's SSN state at its copy id (cb[t] + k), not appended: the two arrays must
+        // never drift apart (a copy id indexes both)
         std::lock_guard<std::mutex> g(ssn_.mu);
-        if (ssn_.e.capacity() < c0) ssn_.e.reserve(std::max<size_t>(c0, 2 * ssn_.e.capacity()));
+        if (nt && ssn_.e.size() > cb[0]) throw std::runtime_error("update_batch: SSN state ahead of the copies");
+        if (ssn_.e.capacity() < copies_.size())
+            ssn_.e.reserve(std::max<size_t>(copies_.size(), 2 * ssn_.e.capacity()));
+        ssn_.e.resize(copies_.size(), CopySsn{0, 0, 0, kMaxCid, 0, 0, 0});
         for (unsigned t = 0; t < nt; ++t)
             for (size_t k = 0; k < lw[t].copies.size(); ++k) {
                 const CopyHdr &c = lw[t].copies[k];
-                ssn_.e.push_back(CopySsn{lw[t].writers[k], lw[t].writers[k], c.rstamp, c.sstamp, 0,
-                                         (uint8_t)(c.sstamp != kMaxCid), 0});
+                ssn_.e[cb[t] + k] = CopySsn{lw[t].writers[k], lw[t].writers[k], c.rstamp, c.sstamp, 0,
+                                            (uint8_t)(c.sstamp != kMaxCid), 0};
             }
     }
     for (unsigned t = 0; t < nt; ++t) {

@@ -83,8 +83,9 @@ public:
         std::atomic<uint64_t> meta, next, loc;
     };
     static_assert(sizeof(Cell) == 24, "a cell is a RecordMetadata");
-    bool on() const { return on_; }
-    void enable() { on_ = true; }
+    // read by stage_location_cell and the adoption thread beside the writer that enables it
+    bool on() const { return on_.load(std::memory_order_acquire); }
+    void enable() { on_.store(true, std::memory_order_release); }
     void ensure(uint64_t handle);  // the chunk holding `handle` exists (writer)
     void set(uint64_t handle, uint64_t meta, uint32_t next) {
         Cell &c = at(handle);
@@ -101,7 +102,7 @@ public:
 
 private:
     Cell &at(uint64_t handle) { return dir_[handle >> kChunkBits].load(std::memory_order_relaxed)[handle & ((1u << kChunkBits) - 1)]; }
-    bool on_ = false;
+    std::atomic<bool> on_{false};
     std::atomic<Cell *> dir_[kDir] = {};
 };
 
@@ -274,6 +275,10 @@ public:
     // writers[k] = the writer id of copy k (its OverwriteVersionHeader cstamp)
     void adopt_device_epoch(const CopyHdr *copies, const uint32_t *writers, uint64_t nc, const VersionHdr *versions,
                             uint64_t nv, uint64_t nimages, const SlotWords *slots, uint64_t nslots);
+    // room for `add` more copy / version headers with no reallocation inside adopt_device_epoch
+    // (a reallocation there moves every earlier header -- ~30 ms at 4M -- on the adoption thread,
+    // which the next epochs' calls wait for); called while no adoption is running
+    void reserve_adoption(uint64_t add);
     // fn(begin, end) over [0, n) on up to 16 threads (one below 65536 items)
     static void parallel_chunks(uint64_t n, const std::function<void(uint64_t, uint64_t)> &fn);
     bool has_device_rows() const { return !device_rows_.empty(); }

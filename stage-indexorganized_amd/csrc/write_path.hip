@@ -253,15 +253,16 @@ __global__ void wp_speculate(WpArgs a, WpCls k, DevTable t, uint8_t *__restrict_
 // key's long run of NotNeededUpdate / DIRTY ops goes 512 ops per pass.
 constexpr int kFinishChunks = 8;
 constexpr uint32_t kBigGroup = 2048;  // ops from the first failure on: a workgroup finishes it (wp_finish_big)
+constexpr uint32_t kJumpFrom = 256;   // ... by pointer jumping (wp_finish_jump)
 __global__ __launch_bounds__(256) void wp_finish_groups(WpArgs a, WpCls kc, DevTable t, uint8_t *__restrict__ rcs,
                                                         uint8_t *__restrict__ succ, int32_t *__restrict__ prev,
                                                         const uint32_t *__restrict__ first_fail,
-                                                        const uint32_t *__restrict__ gend) {
+                                                        const uint32_t *__restrict__ gend, uint32_t big_from) {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t base_q = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64;
     const uint64_t mine = base_q + lane;
     const bool start = mine < a.n && a.loc[mine] != a.none && a.gs[mine] == mine && first_fail[mine] != 0xFFFFFFFFu &&
-                       gend[mine] - first_fail[mine] < kBigGroup;
+                       gend[mine] - first_fail[mine] < big_from;
     uint64_t groups = __builtin_amdgcn_ballot_w64(start);
     while (groups) {
         const uint64_t g = base_q + __builtin_ctzll(groups);
@@ -341,15 +342,228 @@ __global__ void wp_group_ends(WpArgs a, uint32_t *__restrict__ gend) {
 // failing groups with at least kBigGroup ops from their first failure on (a hot key's run of
 // NotNeededUpdate / DIRTY ops) -> list
 __global__ void wp_big_groups(WpArgs a, const uint32_t *__restrict__ first_fail, const uint32_t *__restrict__ gend,
-                              uint32_t *__restrict__ list, uint32_t *__restrict__ count) {
+                              uint32_t *__restrict__ list, uint32_t *__restrict__ count, uint32_t big_from) {
     const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= a.n || a.loc[q] == a.none || a.gs[q] != q || first_fail[q] == 0xFFFFFFFFu) return;
-    if (gend[q] - first_fail[q] >= kBigGroup) list[atomicAdd(count, 1u)] = (uint32_t)q;
+    if (gend[q] - first_fail[q] >= big_from) list[atomicAdd(count, 1u)] = (uint32_t)q;
 }
 
-// step 3b for big groups: one 1024-thread workgroup per group, 16 waves x kFinishChunks x 64 =
-// 8192 ops evaluated against the last success per pass, the first success in batch order
-// found across the waves through LDS
+// step 3b for big groups, the walk (round 4; now the fallback of wp_finish_jump): one
+// 1024-thread workgroup per group, 16 waves x kFinishChunks x 64 = 8192 ops evaluated against
+// the last success per pass, the first success in batch order found across the waves through
+// LDS.  Serial in the group's failures: ~700 passes for a Zipf-0.99 hot key on RunMixed's stream.
+__device__ void finish_big_walk(const WpArgs &a, const WpCls &kc, const DevTable &t, uint8_t *__restrict__ rcs,
+                                uint8_t *__restrict__ succ, int32_t *__restrict__ prev, uint64_t g, uint64_t end,
+                                uint64_t f, const SlotInfo &base, uint64_t *s_first) {
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    constexpr uint64_t kPass = 16ull * kFinishChunks * 64;
+    int64_t last = f > g ? (int64_t)f - 1 : -1;  // [g, f) all succeeded
+    uint64_t pos = f;
+    while (pos < end) {
+        // a pass: up to kFinishChunks slices of 1024 ops (one 64-op chunk per wave), evaluated
+        // against the last success slice by slice until one holds a success -- behind a
+        // single failure the next op usually succeeds, so most passes take one slice
+        uint64_t bf = ~0ull, done = pos;
+        for (int k = 0; k < kFinishChunks && bf == ~0ull && done < end; ++k) {
+            const uint64_t q = done + (uint64_t)wv * 64 + lane;
+            const uint8_t r = q < end ? wp_eval(a, kc, t, q, g, last, base) : (uint8_t)0xFF;
+            uint64_t wf = r == STAGE_RC_OK ? q : ~0ull;  // the wave's first success, then the block's
+            for (int o = 32; o > 0; o >>= 1) {
+                const uint64_t x = __shfl_xor(wf, o, 64);
+                wf = x < wf ? x : wf;
+            }
+            __syncthreads();  // the previous slice's readers of s_first are done
+            if (lane == 0) s_first[wv] = wf;
+            __syncthreads();
+#pragma unroll
+            for (int w = 0; w < 16; ++w) bf = s_first[w] < bf ? s_first[w] : bf;
+            if (q < end && q <= bf) {
+                rcs[q] = r;
+                succ[q] = q == bf;
+                prev[q] = (int32_t)last;
+            }
+            done += 1024;
+        }
+        if (bf != ~0ull) {
+            // as wp_finish_groups: the speculative outcomes behind a success stand up to
+            // and including the next speculative failure
+            uint64_t nf = ~0ull;
+            for (uint64_t s0 = bf + 1; s0 < end && nf == ~0ull; s0 += kPass) {
+                uint64_t mf = ~0ull;
+#pragma unroll
+                for (int k = 0; k < kFinishChunks; ++k) {
+                    const uint64_t q = s0 + (uint64_t)wv * (kFinishChunks * 64) + 64 * k + lane;
+                    if (q < end && !succ[q] && q < mf) mf = q;
+                }
+                for (int o = 32; o > 0; o >>= 1) {
+                    const uint64_t x = __shfl_xor(mf, o, 64);
+                    mf = x < mf ? x : mf;
+                }
+                __syncthreads();
+                if (lane == 0) s_first[wv] = mf;
+                __syncthreads();
+#pragma unroll
+                for (int w = 0; w < 16; ++w) nf = s_first[w] < nf ? s_first[w] : nf;
+            }
+            if (nf == ~0ull) break;
+            last = (int64_t)nf - 1;
+            pos = nf + 1;
+        } else {
+            pos = done;
+        }
+    }
+}
+
+// step 3b for big groups by pointer jumping (round 5).  An op's outcome depends only on the
+// last success before it (wp_eval), so the group's successes are the chain s0, nxt(s0),
+// nxt(nxt(s0)), ... where nxt(p) = the first later op of the group that succeeds if p is the
+// last success: none after an uncommitted success (the record stays in flight: DIRTY), else
+// the first op whose delta differs from p's -- the start of the next run of equal deltas
+// (wp_classify's class numbers; cfirst[c] = the first position of class c) when p+1 repeats
+// p's delta, else p+1 -- provided its writer is not older than p's commit id.  When that
+// writer is older (NotNeededUpdate by cstamp) the candidate fails and the chain is not known
+// locally: the group is finished by finish_big_walk instead (never on RunMixed's stream, whose
+// writer ids grow with the batch).  One 1024-thread workgroup per group:
+//   A. per 64-op chunk (a wave), nxt of every op, then exit(p) (the first chain node at or past
+//      the chunk's end) and mask(p) (the chain's nodes inside the chunk) by 6 doubling steps
+//      over the wave's lanes (shuffles, no memory);
+//   B. one wave follows the chain chunk to chunk: entry(c) = the chain's first node in chunk c,
+//      carry(c) = the last success before it -- one dependent load per chunk that holds a success;
+//   C. per chunk, successes = mask(entry); every op's return code against the last success
+//      before it (wp_eval) and its prev.
+// Scratch (position-indexed, disjoint between groups): jx (exit), jm (mask), ci (entry | carry).
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+__global__ __launch_bounds__(1024) void wp_finish_jump(WpArgs a, WpCls kc, DevTable t, uint8_t *__restrict__ rcs,
+                                                       uint8_t *__restrict__ succ, int32_t *__restrict__ prev,
+                                                       const uint32_t *__restrict__ first_fail,
+                                                       const uint32_t *__restrict__ gend,
+                                                       const uint32_t *__restrict__ list,
+                                                       const uint32_t *__restrict__ count,
+                                                       const uint32_t *__restrict__ cfirst, uint32_t *__restrict__ jx,
+                                                       uint64_t *__restrict__ jm, uint64_t *__restrict__ ci) {
+    __shared__ uint64_t s_first[16];
+    __shared__ uint32_t s_unres;
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t nbig = *count;
+    for (uint32_t i = blockIdx.x; i < nbig; i += gridDim.x) {
+        const uint64_t g = list[i];
+        const uint64_t l = a.loc[g], end = gend[g];
+        const SlotInfo base = t.slot[l];
+        const uint64_t f = first_fail[g];
+        // the chain's first node: f - 1 (a success of the leading run), or when the group's head
+        // already failed the first op that succeeds against the epoch-start state
+        uint64_t start;
+        if (f > g) {
+            start = f - 1;
+        } else {
+            start = ~0ull;
+            for (uint64_t done = g; done < end && start == ~0ull; done += 1024) {
+                const uint64_t q = done + (uint64_t)wv * 64 + lane;
+                const uint8_t r = q < end ? wp_eval(a, kc, t, q, g, -1, base) : (uint8_t)0xFF;
+                uint64_t wf = r == STAGE_RC_OK ? q : ~0ull;
+                for (int o = 32; o > 0; o >>= 1) {
+                    const uint64_t x = __shfl_xor(wf, o, 64);
+                    wf = x < wf ? x : wf;
+                }
+                __syncthreads();
+                if (lane == 0) s_first[wv] = wf;
+                __syncthreads();
+                uint64_t bf = ~0ull;
+#pragma unroll
+                for (int w = 0; w < 16; ++w) bf = s_first[w] < bf ? s_first[w] : bf;
+                if (q < end && q <= bf) {  // up to the first success: evaluated against the start state
+                    rcs[q] = r;
+                    succ[q] = q == bf;
+                    prev[q] = -1;
+                }
+                start = bf;
+            }
+            if (start == ~0ull) continue;  // nothing succeeds: every op was evaluated above
+        }
+        // A. nxt, exit and mask of every op from `start` on
+        if (threadIdx.x == 0) s_unres = 0;
+        __syncthreads();
+        const uint64_t nch = (end - start + 63) / 64;
+        for (uint64_t c = wv; c < nch; c += 16) {
+            const uint64_t cb = start + 64 * c;
+            const uint64_t p = cb + lane;
+            uint32_t J = kNone;
+            uint64_t M = 0;
+            if (p < end) {
+                M = 1ull << lane;
+                const uint32_t cp = commit_of(a, a.op[p]);
+                if (cp != 0) {  // an uncommitted success leaves every later op DIRTY
+                    const uint32_t cl = kc.cls[p];
+                    const uint64_t cand = (p + 1 < end && kc.cls[p + 1] == cl) ? cfirst[cl + 1] : p + 1;
+                    if (cand < end) {
+                        if (a.writer[a.op[cand]] >= cp) J = (uint32_t)cand;
+                        else s_unres = 1;  // (benign race: every writer stores 1)
+                    }
+                }
+            }
+            const uint32_t cend = (uint32_t)(cb + 64);
+#pragma unroll
+            for (int r = 0; r < 6; ++r) {  // doubling inside the chunk: J = f^(2^r)(p), M = its path
+                const bool in = J < cend;
+                const int src = in ? (int)(J - (uint32_t)cb) : (int)lane;
+                const uint32_t Jn = (uint32_t)__shfl((int)J, src, 64);
+                const uint64_t Mn = __shfl(M, src, 64);
+                if (in) {
+                    J = Jn;
+                    M |= Mn;
+                }
+            }
+            if (p < end) {
+                jx[p] = J;
+                jm[p] = M;
+            }
+        }
+        __syncthreads();
+        if (s_unres) {  // a candidate's writer is older than the commit: walk the group instead
+            finish_big_walk(a, kc, t, rcs, succ, prev, g, end, f, base, s_first);
+            __syncthreads();
+            continue;
+        }
+        // B. the chain, chunk to chunk (wave 0; the loop is wave-uniform)
+        if (wv == 0) {
+            uint64_t e = start;
+            int64_t carry = f > g ? (start > g ? (int64_t)start - 1 : -1) : -1;
+            for (uint64_t c = 0; c < nch; ++c) {
+                const uint64_t cb = start + 64 * c;
+                uint64_t entry = kNone;
+                int64_t next_carry = carry;
+                if (e != kNone && e < cb + 64) {
+                    entry = e;
+                    const uint64_t m = jm[e];
+                    next_carry = (int64_t)(cb + 63 - __builtin_clzll(m));
+                    e = jx[e];
+                }
+                if (lane == 0) ci[cb] = entry | ((uint64_t)(uint32_t)(int32_t)carry << 32);
+                carry = next_carry;
+            }
+        }
+        __syncthreads();
+        // C. return codes
+        for (uint64_t c = wv; c < nch; c += 16) {
+            const uint64_t cb = start + 64 * c;
+            const uint64_t q = cb + lane;
+            const uint64_t info = ci[cb];
+            const uint32_t entry = (uint32_t)info;
+            const int32_t carry = (int32_t)(uint32_t)(info >> 32);
+            const uint64_t M = entry != kNone ? jm[entry] : 0ull;
+            if (q < end) {
+                const bool s = (M >> lane) & 1ull;
+                const uint64_t below = M & (lane ? ~0ull >> (64 - lane) : 0ull);
+                const int64_t ps = below ? (int64_t)(cb + 63 - __builtin_clzll(below)) : (int64_t)carry;
+                succ[q] = s;
+                prev[q] = (int32_t)ps;
+                rcs[q] = s ? (uint8_t)STAGE_RC_OK : wp_eval(a, kc, t, q, g, ps, base);
+            }
+        }
+        __syncthreads();
+    }
+}
+
 __global__ __launch_bounds__(1024) void wp_finish_big(WpArgs a, WpCls kc, DevTable t, uint8_t *__restrict__ rcs,
                                                       uint8_t *__restrict__ succ, int32_t *__restrict__ prev,
                                                       const uint32_t *__restrict__ first_fail,
@@ -357,70 +571,22 @@ __global__ __launch_bounds__(1024) void wp_finish_big(WpArgs a, WpCls kc, DevTab
                                                       const uint32_t *__restrict__ list,
                                                       const uint32_t *__restrict__ count) {
     __shared__ uint64_t s_first[16];
-    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    constexpr uint64_t kPass = 16ull * kFinishChunks * 64;
     const uint32_t nbig = *count;
     for (uint32_t i = blockIdx.x; i < nbig; i += gridDim.x) {
         const uint64_t g = list[i];
-        const uint64_t l = a.loc[g], end = gend[g];
-        const SlotInfo base = t.slot[l];
-        const uint64_t f = first_fail[g];
-        int64_t last = f > g ? (int64_t)f - 1 : -1;  // [g, f) all succeeded
-        uint64_t pos = f;
-        while (pos < end) {
-            // a pass: up to kFinishChunks slices of 1024 ops (one 64-op chunk per wave), evaluated
-            // against the last success slice by slice until one holds a success -- behind a
-            // single failure the next op usually succeeds, so most passes take one slice
-            uint64_t bf = ~0ull, done = pos;
-            for (int k = 0; k < kFinishChunks && bf == ~0ull && done < end; ++k) {
-                const uint64_t q = done + (uint64_t)wv * 64 + lane;
-                const uint8_t r = q < end ? wp_eval(a, kc, t, q, g, last, base) : (uint8_t)0xFF;
-                uint64_t wf = r == STAGE_RC_OK ? q : ~0ull;  // the wave's first success, then the block's
-                for (int o = 32; o > 0; o >>= 1) {
-                    const uint64_t x = __shfl_xor(wf, o, 64);
-                    wf = x < wf ? x : wf;
-                }
-                __syncthreads();  // the previous slice's readers of s_first are done
-                if (lane == 0) s_first[wv] = wf;
-                __syncthreads();
-#pragma unroll
-                for (int w = 0; w < 16; ++w) bf = s_first[w] < bf ? s_first[w] : bf;
-                if (q < end && q <= bf) {
-                    rcs[q] = r;
-                    succ[q] = q == bf;
-                    prev[q] = (int32_t)last;
-                }
-                done += 1024;
-            }
-            if (bf != ~0ull) {
-                // as wp_finish_groups: the speculative outcomes behind a success stand up to
-                // and including the next speculative failure
-                uint64_t nf = ~0ull;
-                for (uint64_t s0 = bf + 1; s0 < end && nf == ~0ull; s0 += kPass) {
-                    uint64_t mf = ~0ull;
-#pragma unroll
-                    for (int k = 0; k < kFinishChunks; ++k) {
-                        const uint64_t q = s0 + (uint64_t)wv * (kFinishChunks * 64) + 64 * k + lane;
-                        if (q < end && !succ[q] && q < mf) mf = q;
-                    }
-                    for (int o = 32; o > 0; o >>= 1) {
-                        const uint64_t x = __shfl_xor(mf, o, 64);
-                        mf = x < mf ? x : mf;
-                    }
-                    __syncthreads();
-                    if (lane == 0) s_first[wv] = mf;
-                    __syncthreads();
-#pragma unroll
-                    for (int w = 0; w < 16; ++w) nf = s_first[w] < nf ? s_first[w] : nf;
-                }
-                if (nf == ~0ull) break;
-                last = (int64_t)nf - 1;
-                pos = nf + 1;
-            } else {
-                pos = done;
-            }
-        }
+        finish_big_walk(a, kc, t, rcs, succ, prev, g, gend[g], first_fail[g], t.slot[a.loc[g]], s_first);
+        __syncthreads();
     }
+}
+
+// first position of every delta class (cls = inclusive sum of wp_classify's breaks); cfirst[last
+// class + 1] = n, so the run after a group's last run starts at or past the group's end
+__global__ void wp_class_first(const uint32_t *__restrict__ brk, const uint32_t *__restrict__ cls, uint64_t n,
+                               uint32_t *__restrict__ cfirst) {
+    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    if (brk[q]) cfirst[cls[q]] = (uint32_t)q;
+    if (q + 1 == n) cfirst[cls[q] + 1] = (uint32_t)n;
 }
 
 // step 4 input: successes in the low word, committed successes in the high word
@@ -700,6 +866,7 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         // first then, and leave room for the next pipelined epoch too
         uint64_t *ub = dv.wp_ub;
         if (!pending) {  // no adoption running: the host's counts are the device's
+            h.reserve_adoption(16 * n);  // the next 16 epochs of this size adopt without reallocating
             ub[0] = h.copies_.size(), ub[1] = h.versions_.size(), ub[2] = h.images_.size();
             for (int k = 0; k < 3; ++k) t->adopted_sz[k].store(ub[k], std::memory_order_relaxed);
         } else {
@@ -755,7 +922,9 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
                        o_op = take(n * 4), o_head = take(n * 4), o_gs = take(n * 4), o_rcs = take(n), o_succ = take(n),
                        o_prev = take(n * 4), o_ff = take(n * 4), o_ls = take(n * 4), o_gend = take(n * 4), o_big = take(n * 4), o_flags = take(n * 8),
                        o_ranks = take(n * 8), o_brk = take(n * 4), o_cls = take(n * 4),
-                       o_fp = take(n * 8), o_wfp = take(n * 8), o_eqw = take(n), o_wrec = take(n * sizeof(WRec)), o_cub = take(cub_bytes);
+                       o_fp = take(n * 8), o_wfp = take(n * 8), o_eqw = take(n), o_wrec = take(n * sizeof(WRec)),
+                       o_cfirst = take((n + 2) * 4), o_jx = take(n * 4), o_jm = take(n * 8), o_ci = take(n * 8),
+                       o_cub = take(cub_bytes);
         // the write path's own scratch: an overlapped epoch runs beside the caller's later work,
         // which may use the table's shared scratch (stock-level, CH-Q2, scans)
         uint8_t *buf = wp_scratch_bytes(dv, off);
@@ -781,6 +950,10 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         auto *wfp = (uint64_t *)(buf + o_wfp);
         auto *eqw = buf + o_eqw;
         auto *wrec = (WRec *)(buf + o_wrec);
+        auto *cfirst = (uint32_t *)(buf + o_cfirst);
+        auto *jx = (uint32_t *)(buf + o_jx);
+        auto *jm = (uint64_t *)(buf + o_jm);
+        auto *ci = (uint64_t *)(buf + o_ci);
         // slot words + totals: read back after this call returns (background adoption)
         // both parities are sized together when no adoption is reading the other one: a first
         // use inside a run of epochs would allocate (and drain the device) in the middle of it
@@ -847,9 +1020,22 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         wp_speculate<<<blocks_for(n, 256), 256, 0, ks>>>(a, kc, view, rcs, succ, prev, ff);
         wp_group_ends<<<blocks_for(n, 256), 256, 0, ks>>>(a, gend);
         hip_check(hipMemsetAsync(tot + 1, 0, 4, ks), "memset");  // big-group count (tot is rewritten in step 4)
-        wp_big_groups<<<blocks_for(n, 256), 256, 0, ks>>>(a, ff, gend, big, (uint32_t *)(tot + 1));
-        wp_finish_groups<<<blocks_for(n, 256), 256, 0, ks>>>(a, kc, view, rcs, succ, prev, ff, gend);
-        wp_finish_big<<<256, 1024, 0, ks>>>(a, kc, view, rcs, succ, prev, ff, gend, big, (uint32_t *)(tot + 1));
+        // big failing groups: pointer jumping (STAGE_WP_FINISH=walk: the round-4 walk, for A/B);
+        // groups with at least big_from ops from their first failure on (STAGE_WP_BIG) take it,
+        // smaller ones a wave each (wp_finish_groups)
+        static const bool walk = std::getenv("STAGE_WP_FINISH") && std::string(std::getenv("STAGE_WP_FINISH")) == "walk";
+        static const uint32_t big_from = walk ? kBigGroup
+                                              : (std::getenv("STAGE_WP_BIG") ? (uint32_t)std::atoi(std::getenv("STAGE_WP_BIG"))
+                                                                              : kJumpFrom);
+        wp_big_groups<<<blocks_for(n, 256), 256, 0, ks>>>(a, ff, gend, big, (uint32_t *)(tot + 1), big_from);
+        wp_finish_groups<<<blocks_for(n, 256), 256, 0, ks>>>(a, kc, view, rcs, succ, prev, ff, gend, big_from);
+        if (walk) {
+            wp_finish_big<<<256, 1024, 0, ks>>>(a, kc, view, rcs, succ, prev, ff, gend, big, (uint32_t *)(tot + 1));
+        } else {
+            wp_class_first<<<blocks_for(n, 256), 256, 0, ks>>>(brk, cls, n, cfirst);
+            wp_finish_jump<<<256, 1024, 0, ks>>>(a, kc, view, rcs, succ, prev, ff, gend, big, (uint32_t *)(tot + 1),
+                                                 cfirst, jx, jm, ci);
+        }
         // 4. number
         wp_flags<<<blocks_for(n, 256), 256, 0, ks>>>(a, succ, flags);
         cb = cub_bytes;

@@ -23,7 +23,7 @@ def test_c3_leg_write_paths(gpu, write_path):
     stream = stage.Stream()
     d, rec = bench.c3_leg(tab, args, stream, 4, args.steps, args.warmup)
     cfg = d["config"]
-    assert d["self_check"] and d["value"] > 0 and d["ops_per_s_incl_writes"] > 0
+    assert d["self_check"] and d["value"] > 0 and d["ops_per_s_incl_writes"] == d["value"] and d["reads_per_s"] > 0
     assert cfg["write_path"] == write_path and 0 < cfg["updates_applied"] <= cfg["update_ops"]
     rcs = cfg["update_rc_counts"]
     assert sum(rcs.values()) == cfg["update_ops"] and rcs["ok"] == cfg["updates_applied"]
