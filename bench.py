@@ -1513,7 +1513,8 @@ def main(argv=None):
         "warmup": args.warmup, "ms_per_step": head["ms_per_step"], "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic (LoadYCSBRows keys/payloads)",
         "config": config, "roofline": head["roofline"], "cpu_baseline": cpu, "self_check": head["self_check"],
-        **({"ops_per_s_incl_writes": head["ops_per_s_incl_writes"]} if "ops_per_s_incl_writes" in head else {}),
+        **({k: head[k] for k in ("value_is", "reads_per_s", "read_probe_ms_per_step", "ops_per_s_incl_writes")
+            if k in head}),
         **({"extras": extras} if extras else {}),
         "setup_s": {"load": round(t_load, 1), "sync": round(t_sync, 1)},
         "host_peak_rss_gib": round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20, 1),
