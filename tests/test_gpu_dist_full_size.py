@@ -17,6 +17,7 @@ import pytest
 
 import oracle_lib as O
 import stage
+from progress import say
 
 pytestmark = pytest.mark.gpu
 
@@ -25,11 +26,11 @@ W = 8
 PER_RANK = 1 << 21  # 2^24 keys in all
 
 
+def _say(t0, what):  # progress (stderr + gpurun_out/progress.log): each phase takes tens of seconds
+    say(f"[c5 at size] {what}", t0)
+
+
 @pytest.mark.timeout(900)
-def _say(t0, what):  # progress on stderr: each phase takes tens of seconds at this size
-    print(f"[c5 at size] {time.time() - t0:6.1f}s {what}", file=sys.stderr, flush=True)
-
-
 def test_c5_loopback_at_size_equals_one_table(gpu):
     t0 = time.time()
     rng = np.random.default_rng(0xC5)

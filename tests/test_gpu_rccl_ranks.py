@@ -54,11 +54,11 @@ def rank_env(rank, world, **extra):
     return env
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_sharded_probe_over_rccl_ranks(gpu, world):
     with tempfile.TemporaryDirectory() as d:
         envs = [rank_env(r, world, OUTDIR=d) for r in range(world)]
-        rcs, outs = run_group([[sys.executable, "-u", WORKER]] * world, envs, timeout=240)
+        rcs, outs = run_group([[sys.executable, "-u", WORKER]] * world, envs, timeout=300)
         reports = []
         for r in range(world):
             path = os.path.join(d, f"rank{r}.json")
