@@ -20,13 +20,14 @@ import time
 import traceback
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-rank = int(os.environ["RANK"])
-world = int(os.environ["WORLD_SIZE"])
-outdir = os.environ["OUTDIR"]
-os.environ["NCCL_HOSTID"] = f"stage-c5-{os.getppid()}-rank{rank}"
-os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
-os.environ.setdefault("NCCL_NET", "Socket")
-os.environ.setdefault("NCCL_IB_DISABLE", "1")
+if __name__ == "__main__":  # a rank (the test module imports digest() only)
+    rank = int(os.environ["RANK"])
+    world = int(os.environ["WORLD_SIZE"])
+    outdir = os.environ["OUTDIR"]
+    os.environ["NCCL_HOSTID"] = f"stage-c5-{os.getppid()}-rank{rank}"
+    os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+    os.environ.setdefault("NCCL_NET", "Socket")
+    os.environ.setdefault("NCCL_IB_DISABLE", "1")
 sys.path.insert(0, os.path.join(REPO, "stage-indexorganized_amd"))
 sys.path.insert(0, os.path.join(REPO, "tests"))
 
