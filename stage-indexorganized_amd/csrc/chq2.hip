@@ -12,12 +12,17 @@
 //      the supplier (:890-892); otherwise S_QUANTITY < 10 updates S_QUANTITY..S_REMOTE_CNT to
 //      (q + 50, ytd, order_cnt, remote_cnt) (:893-950), committed with the transaction.
 //
-// Here REGION / NATION run as device scans and SUPPLIER as a one-lane-per-slot leaf dump; the
-// host filters their rows (a few hundred KB); the hot part -- every visited supplier's stock lookups (W * I / 10^4 each, ~2600
-// suppliers for EUROPE) and the item lookups -- is one gather kernel, one probe_kernel launch
-// over all stock keys, their visibility folded at every read id of the batch (aborts and each
-// supplier's last stock), one item probe launch and one finishing kernel.  Updates go through the device write path when
-// a commit id is given.
+// Here REGION / NATION run as device scans and SUPPLIER as a one-lane-per-slot leaf dump; one
+// workgroup (q2_select) filters them -- the region named regions[target], its nations, their
+// suppliers in visiting order -- and lays out each visited supplier's supp_stock_map segment; the
+// hot part -- every visited supplier's stock lookups (W * I / 10^4 each, ~2600 suppliers for
+// EUROPE) and the item lookups -- is one gather kernel, one probe launch over all stock keys,
+// their visibility folded at every read id of the batch (aborts and each supplier's last
+// stock), one item probe launch and one finishing kernel that writes the records straight into
+// the caller's page-locked `out`.  The counts stay on the device (the kernels read them there),
+// so a batch has ONE host synchronisation, at its end (round 5; before, the host filtered the
+// scans between two synchronisations).  Updates go through the device write path when a commit
+// id is given.
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -30,7 +35,6 @@
 #include <hipcub/hipcub.hpp>
 
 #include "handle.hpp"
-#include "radix_sort.hpp"
 
 using namespace stage_capi;
 
@@ -41,6 +45,8 @@ constexpr int kRegionScan = 6, kNationScan = 65;  // scan_sz of :653 and :734
 constexpr uint32_t kIDataOff = 4 + 32 + 8;         // I_DATA in Item's payload (I_IM_ID, I_NAME, I_PRICE)
 static const char *const kRegions[] = {"AFRICA", "AMERICA", "ASIA", "EUROPE", "MIDDLE EAST"};
 
+__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+__device__ __forceinline__ uint32_t rl32(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
 __device__ __forceinline__ bool produced(uint32_t st) { return st == ST_LATEST || st == ST_COPY || st == ST_OLD; }
 
 __device__ __forceinline__ int32_t ld_i32(const uint8_t *p) {
@@ -49,37 +55,176 @@ __device__ __forceinline__ int32_t ld_i32(const uint8_t *p) {
 
 __global__ void q2_set_u64(uint64_t *p, uint64_t v) { *p = v; }
 
-// block s copies supplier s's map entries (2 words each) to its segment
+// blocks copy the visited suppliers' map entries (2 words each) to their segments; counts[0] =
+// the number of visited suppliers (q2_select)
 __global__ void q2_gather(const uint64_t *__restrict__ map_keys, const uint64_t *__restrict__ src,
                           const uint64_t *__restrict__ dst, const uint32_t *__restrict__ cnt,
-                          uint64_t *__restrict__ keys) {
-    const uint32_t s = blockIdx.x;
-    for (uint32_t e = threadIdx.x; e < cnt[s]; e += blockDim.x) {
-        keys[2 * (dst[s] + e)] = map_keys[2 * (src[s] + e)];
-        keys[2 * (dst[s] + e) + 1] = map_keys[2 * (src[s] + e) + 1];
+                          const uint64_t *__restrict__ counts, uint64_t *__restrict__ keys) {
+    const uint64_t n = counts[0];
+    for (uint64_t s = blockIdx.x; s < n; s += gridDim.x)
+        for (uint32_t e = threadIdx.x; e < cnt[s]; e += blockDim.x) {
+            keys[2 * (dst[s] + e)] = map_keys[2 * (src[s] + e)];
+            keys[2 * (dst[s] + e) + 1] = map_keys[2 * (src[s] + e) + 1];
+        }
+}
+
+// RunQuery2's selection (tpcc_new_order.cpp:650-797) in one workgroup, from the REGION / NATION
+// scan rows and the SUPPLIER slot dump:
+//   visits   = for each REGION row named the target (scan order), each NATION row of that region
+//              (scan order); a nation is visited at most once (it has one region key, region
+//              keys are unique), so at most kNationScan visits, found through an LDS hash;
+//   sel      = every SUPPLIER record of each visited nation, visit by visit, in ScanLeafNode
+//              (slot dump) order: a stable counting sort by visit -- each wave counts its
+//              contiguous share of the slots per visit (one ballot per distinct visit of a
+//              64-slot chunk), one prefix over (visit, wave), then each wave places its records;
+//   segments = src / cnt of each selected supplier's supp_stock_map entries (map_off, keys
+//              below 10000), dst = their exclusive prefix sum;
+//   counts   = {suppliers, stock keys}.
+constexpr int kVisits = kNationScan, kVisitHash = 256;
+__global__ __launch_bounds__(1024) void q2_select(const uint8_t *__restrict__ regs, uint32_t rs,
+                                                  const uint8_t *__restrict__ nats, uint32_t ns, uint64_t name0,
+                                                  uint64_t name1, const uint64_t *__restrict__ pairs, uint64_t nslots,
+                                                  const uint32_t *__restrict__ map_off, uint64_t *__restrict__ sel,
+                                                  uint64_t *__restrict__ src, uint32_t *__restrict__ cnt,
+                                                  uint64_t *__restrict__ dst, uint64_t *__restrict__ counts) {
+    __shared__ uint8_t s_rmatch[kRegionScan];
+    __shared__ uint8_t s_flag[kRegionScan * kNationScan];
+    __shared__ int64_t s_visit[kVisits];
+    __shared__ uint32_t s_nvisit;
+    __shared__ int64_t s_hkey[kVisitHash];
+    __shared__ int32_t s_hval[kVisitHash];
+    __shared__ uint32_t s_cnt[16][kVisits];
+    __shared__ uint64_t s_wsum[16];
+    __shared__ uint64_t s_n;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint32_t nreg = *reinterpret_cast<const uint32_t *>(regs - 8);
+    const uint32_t nnat = *reinterpret_cast<const uint32_t *>(nats - 8);
+    // 1. the visits
+    if (tid < kRegionScan && tid < nreg) {  // R_NAME (55 bytes, NUL-terminated) == regions[target]
+        const uint8_t *name = regs + (uint64_t)tid * rs + 8;
+        bool eq = true;
+        for (int i = 0; i < 55; ++i) {
+            const uint8_t c = name[i];
+            const uint8_t want = i < 8 ? (uint8_t)(name0 >> (8 * i)) : i < 16 ? (uint8_t)(name1 >> (8 * (i - 8))) : 0;
+            if (c != want) {
+                eq = false;
+                break;
+            }
+            if (c == 0) break;
+        }
+        s_rmatch[tid] = eq;
     }
-}
-
-__global__ void q2_iota(uint32_t *__restrict__ v, uint64_t n) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) v[i] = (uint32_t)i;
-}
-
-// the stock keys in leaf order: out[j] = keys[perm[j]] (2 words each)
-__global__ void q2_permute_keys(const uint64_t *__restrict__ keys, const uint32_t *__restrict__ perm, uint64_t m,
-                                uint64_t *__restrict__ out) {
-    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= m) return;
-    const uint64_t p = perm[j];
-    out[2 * j] = keys[2 * p];
-    out[2 * j + 1] = keys[2 * p + 1];
-}
-
-// the leaf-ordered probe results back in key order: out[perm[j]] = in[j]
-__global__ void q2_unpermute(const stage_probe_out_dev *__restrict__ in, const uint32_t *__restrict__ perm, uint64_t m,
-                             stage_probe_out_dev *__restrict__ out) {
-    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j < m) out[perm[j]] = in[j];
+    for (uint32_t i = tid; i < kVisitHash; i += blockDim.x) s_hkey[i] = INT64_MIN, s_hval[i] = -1;
+    for (uint32_t w = 0; w < kVisits; ++w)
+        if (tid < 16) s_cnt[tid][w] = 0;
+    __syncthreads();
+    if (tid < nreg * nnat && tid < kRegionScan * kNationScan) {
+        const uint32_t r = tid / nnat, a = tid % nnat;
+        const uint8_t *rr = regs + (uint64_t)r * rs, *nr = nats + (uint64_t)a * ns;
+        s_flag[tid] = s_rmatch[r] && *reinterpret_cast<const int64_t *>(nr + 8) == *reinterpret_cast<const int64_t *>(rr);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t nv = 0;
+        for (uint32_t f = 0; f < nreg * nnat && f < kRegionScan * kNationScan; ++f)
+            if (s_flag[f] && nv < (uint32_t)kVisits) {
+                const int64_t nk = *reinterpret_cast<const int64_t *>(nats + (uint64_t)(f % nnat) * ns);
+                uint32_t h = (uint32_t)(((uint64_t)nk * 0x9E3779B97F4A7C15ull) >> 56);
+                while (s_hkey[h] != INT64_MIN && s_hkey[h] != nk) h = (h + 1) & (kVisitHash - 1);
+                if (s_hkey[h] == nk) continue;  // (cannot happen: one region per nation)
+                s_hkey[h] = nk;
+                s_hval[h] = (int32_t)nv;
+                s_visit[nv++] = nk;
+            }
+        s_nvisit = nv;
+    }
+    __syncthreads();
+    const uint32_t nv = s_nvisit;
+    auto visit_of = [&](uint64_t key, uint64_t nat) -> int {
+        if (key == ~0ull || nv == 0) return -1;
+        uint32_t h = (uint32_t)((nat * 0x9E3779B97F4A7C15ull) >> 56);
+        while (s_hkey[h] != INT64_MIN) {
+            if (s_hkey[h] == (int64_t)nat) return s_hval[h];
+            h = (h + 1) & (kVisitHash - 1);
+        }
+        return -1;
+    };
+    // 2. counting pass: wave w owns slots [w * per, (w + 1) * per)
+    const uint64_t per = ((nslots + 16 * 64 - 1) / (16 * 64)) * 64;
+    const uint64_t lo = wv * per, hi = lo + per < nslots ? lo + per : nslots;
+    for (uint64_t c0 = lo; c0 < hi; c0 += 64) {
+        const uint64_t i = c0 + lane;
+        const int v = i < hi ? visit_of(pairs[2 * i], pairs[2 * i + 1]) : -1;
+        uint64_t todo = ballot(v >= 0);
+        while (todo) {
+            const int vl = (int)rl32((uint32_t)v, (int)__builtin_ctzll(todo));
+            const uint64_t mm = ballot(v == vl);
+            if (lane == 0) s_cnt[wv][vl] += (uint32_t)__builtin_popcountll(mm);
+            todo &= ~mm;
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {  // placement starts: visit-major, then wave (slot order)
+        uint32_t pos = 0;
+        for (uint32_t v = 0; v < nv; ++v)
+            for (uint32_t w = 0; w < 16; ++w) {
+                const uint32_t c = s_cnt[w][v];
+                s_cnt[w][v] = pos;
+                pos += c;
+            }
+        counts[0] = pos;
+        s_n = pos;
+    }
+    __syncthreads();
+    // 3. placement pass
+    for (uint64_t c0 = lo; c0 < hi; c0 += 64) {
+        const uint64_t i = c0 + lane;
+        const uint64_t key = i < hi ? pairs[2 * i] : ~0ull;
+        const int v = i < hi ? visit_of(key, pairs[2 * i + 1]) : -1;
+        uint64_t todo = ballot(v >= 0);
+        while (todo) {
+            const int vl = (int)rl32((uint32_t)v, (int)__builtin_ctzll(todo));
+            const uint64_t mm = ballot(v == vl);
+            const uint32_t base = s_cnt[wv][vl];
+            if (v == vl) sel[base + (uint32_t)__builtin_popcountll(mm & ((1ull << lane) - 1))] = key;
+            if (lane == 0) s_cnt[wv][vl] = base + (uint32_t)__builtin_popcountll(mm);
+            todo &= ~mm;
+        }
+    }
+    __syncthreads();
+    // 4. map segments: src / cnt per selected supplier, dst = exclusive prefix of cnt
+    const uint64_t n = s_n;
+    uint64_t carry = 0;
+    for (uint64_t b = 0; b < n; b += blockDim.x) {
+        const uint64_t i = b + tid;
+        uint64_t c = 0;
+        if (i < n) {
+            const uint64_t sk = sel[i];
+            uint64_t s0 = 0;
+            if (sk < 10000) {
+                s0 = map_off[sk];
+                c = map_off[sk + 1] > map_off[sk] ? map_off[sk + 1] - map_off[sk] : 0;
+            }
+            src[i] = s0;
+            cnt[i] = (uint32_t)c;
+        }
+        uint64_t x = c;  // inclusive scan in the wave, then across the 16 waves
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint64_t y = __shfl_up(x, o, 64);
+            if (lane >= (uint32_t)o) x += y;
+        }
+        if (lane == 63) s_wsum[wv] = x;
+        __syncthreads();
+        uint64_t before = carry;
+        for (uint32_t w = 0; w < wv; ++w) before += s_wsum[w];
+        if (i < n) dst[i] = before + x - c;
+        uint64_t total = 0;
+        for (uint32_t w = 0; w < 16; ++w) total += s_wsum[w];
+        carry += total;
+        __syncthreads();
+    }
+    if (tid == 0) counts[1] = carry;
 }
 
 // thread per (query q, supplier s): the abort for a stock lookup that produced no tuple is already
@@ -88,8 +233,9 @@ __global__ void q2_unpermute(const stage_probe_out_dev *__restrict__ in, const u
 __global__ void q2_reduce(const stage_probe_out_dev *__restrict__ slast, const uint64_t *__restrict__ skeys,
                           const uint64_t *__restrict__ dst, const uint32_t *__restrict__ cnt,
                           const uint64_t *__restrict__ supp, const uint8_t *__restrict__ sheap, uint32_t shstride,
-                          uint32_t skpad, uint32_t n, uint32_t nq, stage_q2_rec *__restrict__ out,
-                          uint64_t *__restrict__ ikeys) {
+                          uint32_t skpad, const uint64_t *__restrict__ counts, uint32_t nq,
+                          stage_q2_rec *__restrict__ out, uint64_t *__restrict__ ikeys) {
+    const uint32_t n = (uint32_t)counts[0];
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;  // q * n + s
     if (g >= n * nq) return;
     const uint32_t s = g % n;
@@ -116,21 +262,28 @@ __global__ void q2_reduce(const stage_probe_out_dev *__restrict__ slast, const u
 
 // item outcome: no tuple aborts; I_DATA up to its first NUL containing 'b' skips; else a
 // quantity below 10 marks the update
+// ... and each record straight into the caller's page-locked records (host_out, row pitch
+// max_out; null: the records stay in `out` on the device)
 __global__ void q2_finish(const stage_probe_out_dev *__restrict__ iout, const uint8_t *__restrict__ iheap,
-                          uint32_t ihstride, uint32_t ikpad, uint32_t n, uint32_t nq, stage_q2_rec *__restrict__ out,
-                          int32_t *__restrict__ abort_flag) {
+                          uint32_t ihstride, uint32_t ikpad, const uint64_t *__restrict__ counts, uint32_t nq,
+                          stage_q2_rec *__restrict__ out, int32_t *__restrict__ abort_flag,
+                          stage_q2_rec *__restrict__ host_out, uint64_t max_out) {
+    const uint32_t n = (uint32_t)counts[0];
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;  // q * n + supplier
     if (s >= n * nq) return;
     const uint32_t st = iout[s].w[0] & 0xFF;
+    stage_q2_rec r = out[s];
     if (!produced(st)) {
         atomicOr(abort_flag + s / n, 1);
-        return;
+    } else {
+        const uint8_t *d = iheap + (uint64_t)iout[s].w[6] * ihstride + ikpad + kIDataOff;
+        uint8_t has_b = 0;
+        for (int c = 0; c < 64 && d[c]; ++c) has_b |= d[c] == 'b';
+        r.item_has_b = has_b;
+        r.update = !has_b && r.s_quantity < 10;
+        out[s] = r;
     }
-    const uint8_t *d = iheap + (uint64_t)iout[s].w[6] * ihstride + ikpad + kIDataOff;
-    uint8_t has_b = 0;
-    for (int c = 0; c < 64 && d[c]; ++c) has_b |= d[c] == 'b';
-    out[s].item_has_b = has_b;
-    out[s].update = !has_b && out[s].s_quantity < 10;
+    if (host_out && s % n < max_out) host_out[(uint64_t)(s / n) * max_out + s % n] = r;
 }
 
 // SUPPLIER scan with scan_sz -1 (TableScanExecutor::ScanLeafNode, executor.h:580-612): every
@@ -152,16 +305,9 @@ __global__ void q2_dump_leaves(DevTable t, uint32_t kpad, uint64_t *__restrict__
     }
 }
 
-int64_t rd64(const uint8_t *p) {
-    int64_t v;
-    std::memcpy(&v, p, 8);
-    return v;
-}
-
-// TableScanExecutor rows of one scan from `start` (device scan): area[0..4) = the row count and
-// area + 8 the rows, one asynchronous copy to the pinned host area (the caller synchronises the
-// stream before reading)
-void scan_rows(stage_table *t, uint64_t start, uint32_t scan_size, uint8_t *area, hipStream_t s) {
+// TableScanExecutor rows of one scan from `start` (device scan) into the table's scratch: the
+// returned pointer is the first row, the row count (u32) 8 bytes before it
+const uint8_t *scan_rows(stage_table *t, uint64_t start, uint32_t scan_size, hipStream_t s) {
     const DevTable &v = t->dev.view;
     const uint64_t rows = (uint64_t)scan_size * v.stride;
     uint8_t *buf = scratch_bytes(t->dev, 64 + rows);
@@ -169,7 +315,7 @@ void scan_rows(stage_table *t, uint64_t start, uint32_t scan_size, uint8_t *area
     auto *cnt = (uint32_t *)(buf + 56);  // 8 bytes before the rows
     q2_set_u64<<<1, 1, 0, s>>>(key, start);  // no host buffer outlives the call
     hip_check(launch_scan(v, key, nullptr, 1, scan_size, cnt, buf + 64, s, t->scan_tune), "scan");
-    hip_check(hipMemcpyAsync(area, cnt, 8 + rows, hipMemcpyDeviceToHost, s), "d2h");
+    return buf + 64;
 }
 
 }  // namespace
@@ -210,20 +356,51 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         };
         *n_out = 0;
         for (uint32_t q = 0; q < nq; ++q) aborted[q] = 0;
-        // 1. REGION / NATION scans, SUPPLIER scan of every record, filtered on the host
-        const uint32_t rs = region->dev.view.stride, ns = nation->dev.view.stride;
-        // SUPPLIER: every record, ScanLeafNode order
-        const DevTable &pv = supplier->dev.view;
+        const DevTable &pv = supplier->dev.view, &sv = stock->dev.view, &iv = item->dev.view;
         const uint64_t nslots = (uint64_t)pv.nleaves * pv.cap;
-        // the host copies go through the stock table's pinned call staging (pageable copies
-        // are staged by the runtime and wait for each other): [REGION count, rows][NATION
-        // count, rows][SUPPLIER (key, nation) pairs]
-        auto alp = [](uint64_t x) { return (x + 255) & ~255ull; };
-        const uint64_t p_regs = 0, p_nats = p_regs + alp(8 + (uint64_t)kRegionScan * rs),
-                       p_pairs = p_nats + alp(8 + (uint64_t)kNationScan * ns), p_end = p_pairs + nslots * 16;
-        uint8_t *pin = pinned_bytes(stock->dev, p_end, 2);
-        // the REGION and NATION scans on their tables' own streams beside the SUPPLIER dump on
-        // s (forked from and joined back into s): three short dependent chains side by side
+        // upper bounds (buffer sizes, grids): every SUPPLIER slot visited, every map entry looked up
+        constexpr uint32_t kMapKeys = 10000;
+        uint64_t m_max = 0;
+        for (uint32_t k = 0; k < kMapKeys; ++k) m_max += map_off[k + 1] > map_off[k] ? map_off[k + 1] - map_off[k] : 0;
+        const uint64_t n_max = std::max<uint64_t>(nslots, 1);
+        // launch shapes from the previous call's counts (the visited set depends on the data only)
+        const uint64_t n_hint = stock->q2_hint[0] ? std::min(stock->q2_hint[0], n_max) : n_max;
+        const uint64_t m_hint = stock->q2_hint[1] ? std::min(stock->q2_hint[1], std::max<uint64_t>(m_max, 1)) : m_max;
+        // pinned call staging mirrored at the head of the device scratch: [map_off][read ids]
+        // [aborted] go down in one copy; [counts][aborted] come back in one copy
+        auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
+        const uint64_t q_map = 0, q_rq = q_map + al((kMapKeys + 1) * 4ull), q_cn = q_rq + al(nq * 4ull),
+                       q_ab = q_cn + 16, q_end = q_ab + al(nq * 4ull);
+        uint8_t *pq = pinned_bytes(stock->dev, q_end, 2);
+        std::memcpy(pq + q_map, map_off, (kMapKeys + 1) * 4ull);
+        std::memcpy(pq + q_rq, rq, nq * 4ull);
+        std::memset(pq + q_cn, 0, 16 + nq * 4ull);
+        uint64_t off = 0;
+        auto take = [&](uint64_t bytes) {
+            const uint64_t o = off;
+            off += al(bytes);
+            return o;
+        };
+        const uint64_t o_mir = take(q_end), o_pairs = take(n_max * 16), o_sel = take(n_max * 8),
+                       o_src = take(n_max * 8), o_cnt = take(n_max * 4), o_dst = take(n_max * 8),
+                       o_keys = take(std::max<uint64_t>(m_max, 1) * 16), o_sbase = take(std::max<uint64_t>(m_max, 1) * 32),
+                       o_slast = take(n_max * 32 * nq), o_ik = take(n_max * 8 * nq), o_iout = take(n_max * 32 * nq),
+                       o_ibase = take(n_max * 32), o_rec = take(n_max * nq * sizeof(stage_q2_rec));
+        uint8_t *buf = scratch_bytes(nation->dev, off), *mir = buf + o_mir;
+        auto *d_map = (const uint32_t *)(mir + q_map);
+        auto *d_rq = (const uint32_t *)(mir + q_rq);
+        auto *d_counts = (uint64_t *)(mir + q_cn);
+        auto *d_ab = (int32_t *)(mir + q_ab);
+        auto *d_pairs = (uint64_t *)(buf + o_pairs), *d_sel = (uint64_t *)(buf + o_sel);
+        auto *d_src = (uint64_t *)(buf + o_src), *d_dst = (uint64_t *)(buf + o_dst);
+        auto *d_cnt = (uint32_t *)(buf + o_cnt);
+        auto *d_keys = (uint64_t *)(buf + o_keys), *d_ik = (uint64_t *)(buf + o_ik);
+        auto *d_iout = (stage_probe_out_dev *)(buf + o_iout), *d_slast = (stage_probe_out_dev *)(buf + o_slast);
+        auto *d_sbase = (stage_probe_out_dev *)(buf + o_sbase), *d_ibase = (stage_probe_out_dev *)(buf + o_ibase);
+        auto *d_rec = (stage_q2_rec *)(buf + o_rec);
+        hip_check(hipMemcpyAsync(mir, pq, q_end, hipMemcpyHostToDevice, s), "h2d");
+        // 1. REGION / NATION scans on their tables' own streams beside the SUPPLIER dump on s
+        // (forked from and joined back into s): three short dependent chains side by side
         hipEvent_t *ev = stock->dev.call_ev;
         for (int k = 0; k < 3; ++k)
             if (!ev[k]) hip_check(hipEventCreateWithFlags(&ev[k], hipEventDisableTiming), "call event");
@@ -231,211 +408,102 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         hip_check(hipEventRecord(ev[0], s), "fork");
         hip_check(hipStreamWaitEvent(rs_s, ev[0], 0), "fork");
         hip_check(hipStreamWaitEvent(ns_s, ev[0], 0), "fork");
-        scan_rows(region, 0, kRegionScan, pin + p_regs, rs_s);
-        scan_rows(nation, 0, kNationScan, pin + p_nats, ns_s);
+        const uint8_t *regs = scan_rows(region, 0, kRegionScan, rs_s);
+        const uint8_t *nats = scan_rows(nation, 0, kNationScan, ns_s);
         hip_check(hipEventRecord(ev[1], rs_s), "join");
         hip_check(hipEventRecord(ev[2], ns_s), "join");
-        uint8_t *pbuf = scratch_bytes(supplier->dev, nslots * 16);
         q2_dump_leaves<<<(unsigned)std::min<uint64_t>((nslots + 255) / 256, 4096), 256, 0, s>>>(
-            pv, facts(supplier).key_pad(), (uint64_t *)pbuf);
+            pv, facts(supplier).key_pad(), d_pairs);
         hip_check(hipGetLastError(), "dump leaves");
-        hip_check(hipMemcpyAsync(pin + p_pairs, pbuf, nslots * 16, hipMemcpyDeviceToHost, s), "d2h");
         hip_check(hipStreamWaitEvent(s, ev[1], 0), "join");
         hip_check(hipStreamWaitEvent(s, ev[2], 0), "join");
-        const uint8_t *regs_p = pin + p_regs + 8, *nats_p = pin + p_nats + 8;
-        const uint64_t *pairs = (const uint64_t *)(pin + p_pairs);
-        lap("scans enqueued");
-        hip_check(hipStreamSynchronize(s), "scan sync");  // the three scans complete together
-        lap("scans done");
-        uint32_t nreg, nnat;
-        std::memcpy(&nreg, pin + p_regs, 4);
-        std::memcpy(&nnat, pin + p_nats, 4);
-        // the visiting order of :770-797: for each region named regions[target] (scan order),
-        // for each of its nations (scan order), every SUPPLIER slot of that nation in
-        // ScanLeafNode order -- one pass over the slots into per-visit buckets
-        std::vector<int64_t> visit;  // nation key of each (region, nation) visit, in order
-        for (uint32_t r = 0; r < nreg; ++r) {
-            const uint8_t *rr = regs_p + (uint64_t)r * rs;
-            char name[56];
-            std::memcpy(name, rr + 8, 55);
-            name[55] = 0;
-            if (std::string(name) != kRegions[target_region]) continue;
-            for (uint32_t a = 0; a < nnat; ++a) {
-                const uint8_t *nr = nats_p + (uint64_t)a * ns;
-                if (rd64(nr + 8) == rd64(rr)) visit.push_back(rd64(nr));
-            }
-        }
-        // visit index of each nation key: a direct table when the visited keys are small and
-        // distinct (always, for the loader's nations 0..61), else the per-slot search over visits
-        constexpr int64_t kDirect = 4096;
-        std::vector<int32_t> vidx(kDirect, -1);
-        bool direct = true;
-        for (size_t j = 0; j < visit.size() && direct; ++j) {
-            if (visit[j] < 0 || visit[j] >= kDirect || vidx[visit[j]] >= 0) direct = false;
-            else vidx[visit[j]] = (int32_t)j;
-        }
-        std::vector<uint64_t> sel;  // visited suppliers in visiting order
-        if (direct) {  // counting pass, then each slot placed at its visit's next position
-            std::vector<uint32_t> pos(visit.size() + 1, 0);
-            for (uint64_t k = 0; k < nslots; ++k) {
-                const int64_t nat = (int64_t)pairs[2 * k + 1];
-                if (pairs[2 * k] != ~0ull && nat >= 0 && nat < kDirect && vidx[nat] >= 0) ++pos[vidx[nat] + 1];
-            }
-            for (size_t j = 0; j < visit.size(); ++j) pos[j + 1] += pos[j];
-            sel.resize(pos[visit.size()]);
-            for (uint64_t k = 0; k < nslots; ++k) {
-                const int64_t nat = (int64_t)pairs[2 * k + 1];
-                if (pairs[2 * k] != ~0ull && nat >= 0 && nat < kDirect && vidx[nat] >= 0)
-                    sel[pos[vidx[nat]]++] = pairs[2 * k];
-            }
-        } else {
-            std::vector<std::vector<uint64_t>> bucket(visit.size());
-            for (uint64_t k = 0; k < nslots; ++k) {
-                if (pairs[2 * k] == ~0ull) continue;
-                const int64_t nat = (int64_t)pairs[2 * k + 1];
-                for (size_t j = 0; j < visit.size(); ++j)
-                    if (visit[j] == nat) bucket[j].push_back(pairs[2 * k]);
-            }
-            for (const auto &b : bucket) sel.insert(sel.end(), b.begin(), b.end());
-        }
-        const uint32_t n = (uint32_t)sel.size();
-        lap("suppliers selected");
-        *n_out = n;
-        if (n == 0) return STAGE_OK;
-        // 2. stock keys of every visited supplier, one probe launch.  Pinned call staging again
-        // (the scans' contents are no longer needed: a growth may move it), mirrored by the head
-        // of the device scratch so that one copy goes down and one comes back:
-        // [src][dst][cnt][sel][read ids] down, [aborted] (zeroed) down and up, [records] up
-        const uint64_t q_src = 0, q_dst = q_src + alp(n * 8ull), q_cnt = q_dst + alp(n * 8ull),
-                       q_sel = q_cnt + alp(n * 4ull), q_rq = q_sel + alp(n * 8ull), q_ab = q_rq + alp(nq * 4ull),
-                       q_rec = q_ab + alp(nq * 4ull), q_end = q_rec + alp((uint64_t)n * nq * sizeof(stage_q2_rec));
-        uint8_t *pq = pinned_bytes(stock->dev, q_end, 2);
-        uint64_t *src = (uint64_t *)(pq + q_src), *dst = (uint64_t *)(pq + q_dst);
-        uint32_t *cnt = (uint32_t *)(pq + q_cnt);
-        std::memcpy(pq + q_sel, sel.data(), n * 8ull);
-        std::memcpy(pq + q_rq, rq, nq * 4ull);
-        std::memset(pq + q_ab, 0, nq * 4ull);
-        uint64_t m = 0;
-        for (uint32_t k = 0; k < n; ++k) {
-            const uint64_t sk = sel[k];
-            src[k] = sk < 10000 ? map_off[sk] : 0;
-            cnt[k] = sk < 10000 ? map_off[sk + 1] - map_off[sk] : 0;
-            dst[k] = m;
-            m += cnt[k];
-        }
-        // STAGE_Q2_SORT=1: the STOCK keys probed in leaf order (their descents first, a radix sort of
-        // (leaf, position), the probe from the known leaves, results written back in place by the
-        // per-read-id revisit) -- neighbouring probes share leaf heads and bottom nodes in L2
-        const char *qs = std::getenv("STAGE_Q2_SORT");
-        const bool sorted = m > 1 && qs && qs[0] == '1';
-        const DevTable &sv0 = stock->dev.view;
-        int lbits = 1;
-        while (lbits < 32 && (1ull << lbits) <= sv0.nleaves) ++lbits;
-        size_t cub_bytes = 0;
-        if (sorted)
-            hip_check(sort_pairs(nullptr, cub_bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-                                 (const uint32_t *)nullptr, (uint32_t *)nullptr, m, 0, lbits, s),
-                      "sort size");
-        auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
-        uint64_t off = 0;
-        auto take = [&](uint64_t bytes) {
-            const uint64_t o = off;
-            off += al(bytes);
-            return o;
-        };
-        const uint64_t o_mir = take(q_end), o_keys = take(std::max<uint64_t>(m, 1) * 16),
-                       o_sbase = take(std::max<uint64_t>(m, 1) * 32),
-                       o_leaf = take(sorted ? m * 4 : 0), o_sleaf = take(sorted ? m * 4 : 0),
-                       o_iota = take(sorted ? m * 4 : 0), o_perm = take(sorted ? m * 4 : 0),
-                       o_skeys = take(sorted ? m * 16 : 0), o_cub = take(sorted ? cub_bytes : 0),
-                       o_sout = take(sorted ? m * 32 : 0), o_slast = take(n * 32ull * nq),
-                       o_ik = take(n * 8 * nq), o_iout = take(n * 32 * nq), o_ibase = take(n * 32);
-        uint8_t *buf = scratch_bytes(nation->dev, off), *mir = buf + o_mir;
-        auto *d_src = (uint64_t *)(mir + q_src), *d_dst = (uint64_t *)(mir + q_dst), *d_sup = (uint64_t *)(mir + q_sel);
-        auto *d_cnt = (uint32_t *)(mir + q_cnt), *d_rq = (uint32_t *)(mir + q_rq);
-        auto *d_keys = (uint64_t *)(buf + o_keys), *d_ik = (uint64_t *)(buf + o_ik);
-        auto *d_sout = (stage_probe_out_dev *)(buf + o_sout), *d_iout = (stage_probe_out_dev *)(buf + o_iout);
-        auto *d_slast = (stage_probe_out_dev *)(buf + o_slast);
-        auto *d_sbase = (stage_probe_out_dev *)(buf + o_sbase), *d_ibase = (stage_probe_out_dev *)(buf + o_ibase);
-        auto *d_rec = (stage_q2_rec *)(mir + q_rec);
-        auto *d_ab = (int32_t *)(mir + q_ab);
-        hip_check(hipMemcpyAsync(mir, pq, q_rec, hipMemcpyHostToDevice, s), "h2d");
-        q2_gather<<<n, 256, 0, s>>>(d_map_keys, d_src, d_dst, d_cnt, d_keys);
-        const DevTable &sv = stock->dev.view, &iv = item->dev.view;
+        // 2. the selection and the map segments, on the device
+        char tname[16] = {0};
+        std::strncpy(tname, kRegions[target_region], 15);
+        uint64_t name0, name1;
+        std::memcpy(&name0, tname, 8);
+        std::memcpy(&name1, tname + 8, 8);
+        q2_select<<<1, 1024, 0, s>>>(regs, region->dev.view.stride, nats, nation->dev.view.stride, name0, name1, d_pairs,
+                                     nslots, d_map, d_sel, d_src, d_cnt, d_dst, d_counts);
+        hip_check(hipGetLastError(), "select");
+        lap("selection enqueued");
+        // 3. every visited supplier's STOCK keys, one probe of them all (the counts on the device)
+        q2_gather<<<(unsigned)std::max<uint64_t>(std::min<uint64_t>(n_hint, 4096), 1), 256, 0, s>>>(
+            d_map_keys, d_src, d_dst, d_cnt, d_counts, d_keys);
         // every query of the batch looks up the same STOCK keys (the visited suppliers and their
         // supp_stock_map do not depend on the read id): each key is probed once, with no read id
         // (the hit slot does not depend on it), and its visibility evaluated at every query's read
         // id inside the per-supplier fold (launch_revisit_segments: the aborts and each
         // supplier's last stock, per query)
-        const stage_probe_out_dev *d_stock = d_sbase;
-        if (sorted) {
-            auto *d_leaf = (uint32_t *)(buf + o_leaf), *d_sleaf = (uint32_t *)(buf + o_sleaf);
-            auto *d_iota = (uint32_t *)(buf + o_iota), *d_perm = (uint32_t *)(buf + o_perm);
-            auto *d_skeys = (uint64_t *)(buf + o_skeys);
-            const unsigned mb = (unsigned)((m + 255) / 256);
-            hip_check(launch_resolve(sv, d_keys, nullptr, m, 1, d_leaf, s), "stock descents");
-            q2_iota<<<mb, 256, 0, s>>>(d_iota, m);
-            size_t cb = cub_bytes;
-            hip_check(sort_pairs(buf + o_cub, cb, (const uint32_t *)d_leaf, d_sleaf, (const uint32_t *)d_iota, d_perm, m, 0,
-                                 lbits, s),
-                      "stock leaf sort");
-            q2_permute_keys<<<mb, 256, 0, s>>>(d_keys, d_perm, m, d_skeys);
-            hip_check(launch_probe(sv, d_skeys, nullptr, nullptr, d_sleaf, m, d_sbase, nullptr, s, stock->tune),
+        if (m_max)
+            hip_check(launch_probe(sv, d_keys, nullptr, nullptr, nullptr, m_max, d_sbase, nullptr, s, stock->tune,
+                                   d_counts + 1, m_hint),
                       "stock probe");
-            q2_unpermute<<<mb, 256, 0, s>>>(d_sbase, d_perm, m, d_sout);
-            d_stock = d_sout;
-        } else if (m) {
-            hip_check(launch_probe(sv, d_keys, nullptr, nullptr, nullptr, m, d_sbase, nullptr, s, stock->tune),
-                      "stock probe");
-        }
-        if (m)
-            hip_check(launch_revisit_segments(sv, d_stock, m, d_dst, d_cnt, n, d_rq, nq, d_slast, d_ab, s),
+        if (m_max)
+            hip_check(launch_revisit_segments(sv, d_sbase, m_max, d_dst, d_cnt, (uint32_t)n_max, d_rq, nq, d_slast, d_ab, s,
+                                              d_counts + 1, d_counts),
                       "stock read ids");
-        q2_reduce<<<(n * nq + 255) / 256, 256, 0, s>>>(d_slast, d_keys, d_dst, d_cnt, d_sup, sv.heap, sv.hstride,
-                                                       facts(stock).key_pad(), n, nq, d_rec, d_ik);
-        // 3. item lookups of the last stocks (the same keys in every query: probed once, as above),
-        // filter
-        hip_check(launch_probe(iv, d_ik, nullptr, nullptr, nullptr, n, d_ibase, nullptr, s, item->tune), "item probe");
-        hip_check(launch_revisit(iv, d_ibase, n, d_rq, nq, nullptr, d_iout, s), "item read ids");
-        q2_finish<<<(n * nq + 255) / 256, 256, 0, s>>>(d_iout, iv.heap, iv.hstride, facts(item).key_pad(), n, nq,
-                                                       d_rec, d_ab);
-        hip_check(hipGetLastError(), "q2 kernels");
-        // `out` in page-locked memory (stage_host_alloc, stage.pinned_empty) with room for every
-        // record: the records go straight there (one 2-D copy) instead of through the call
-        // staging and a host memcpy
-        bool to_out = false;
-        if (out && n <= max_out) {
+        q2_reduce<<<(unsigned)((n_max * nq + 255) / 256), 256, 0, s>>>(d_slast, d_keys, d_dst, d_cnt, d_sel, sv.heap,
+                                                                       sv.hstride, facts(stock).key_pad(), d_counts,
+                                                                       nq, d_rec, d_ik);
+        // 4. item lookups of the last stocks (the same keys in every query: probed once, as above),
+        // the I_DATA filter, the records into `out`
+        hip_check(launch_probe(iv, d_ik, nullptr, nullptr, nullptr, n_max, d_ibase, nullptr, s, item->tune, d_counts,
+                               n_hint),
+                  "item probe");
+        hip_check(launch_revisit(iv, d_ibase, n_max, d_rq, nq, nullptr, d_iout, s, d_counts), "item read ids");
+        // `out` in page-locked memory (stage_host_alloc, stage.pinned_empty): the finishing kernel
+        // writes the records into it directly; otherwise they are copied once the count is known
+        stage_q2_rec *host_out = nullptr;
+        if (out && max_out) {
             hipPointerAttribute_t pa;
-            to_out = hipPointerGetAttributes(&pa, out) == hipSuccess && pa.type == hipMemoryTypeHost;
+            void *dp = nullptr;
+            if (hipPointerGetAttributes(&pa, out) == hipSuccess && pa.type == hipMemoryTypeHost &&
+                hipHostGetDevicePointer(&dp, out, 0) == hipSuccess)
+                host_out = (stage_q2_rec *)dp;
             (void)hipGetLastError();  // a pageable pointer is not an error here
         }
-        stage_q2_rec *recs = to_out ? out : (stage_q2_rec *)(pq + q_rec);
-        if (to_out) {
-            hip_check(hipMemcpyAsync(pq + q_ab, d_ab, 4ull * nq, hipMemcpyDeviceToHost, s), "d2h");
-            hip_check(hipMemcpy2DAsync(out, max_out * sizeof(stage_q2_rec), d_rec, n * sizeof(stage_q2_rec),
-                                       n * sizeof(stage_q2_rec), nq, hipMemcpyDeviceToHost, s),
-                      "d2h");
-        } else {
-            hip_check(hipMemcpyAsync(pq + q_ab, d_ab, (q_rec - q_ab) + (uint64_t)n * nq * sizeof(stage_q2_rec),
-                                     hipMemcpyDeviceToHost, s),
-                      "d2h");  // [aborted][records]
-        }
-        lap("probes enqueued");
-        hip_check(hipStreamSynchronize(s), "q2 sync");
+        q2_finish<<<(unsigned)((n_max * nq + 255) / 256), 256, 0, s>>>(d_iout, iv.heap, iv.hstride, facts(item).key_pad(),
+                                                                       d_counts, nq, d_rec, d_ab, host_out, max_out);
+        hip_check(hipGetLastError(), "q2 kernels");
+        hip_check(hipMemcpyAsync(pq + q_cn, d_counts, 16 + nq * 4ull, hipMemcpyDeviceToHost, s), "d2h");
+        lap("enqueued");
+        hip_check(hipStreamSynchronize(s), "q2 sync");  // the batch's one synchronisation
         lap("results back");
+        uint64_t cn[2];
+        std::memcpy(cn, pq + q_cn, 16);
         std::memcpy(aborted, pq + q_ab, 4ull * nq);
+        const uint64_t n = cn[0];
+        if (n > n_max || cn[1] > m_max) throw std::runtime_error("q2: device counts out of range");
+        stock->q2_hint[0] = n;
+        stock->q2_hint[1] = cn[1];
+        *n_out = n;
+        if (n == 0) {
+            for (uint32_t q = 0; q < nq; ++q) aborted[q] = 0;
+            return STAGE_OK;
+        }
+        std::vector<stage_q2_rec> recs_buf;
+        const stage_q2_rec *recs = host_out ? out : nullptr;
+        if (!host_out) {  // a pageable (or no) `out`: the records come back now
+            recs_buf.resize(n * nq);
+            hip_check(hipMemcpy(recs_buf.data(), d_rec, n * nq * sizeof(stage_q2_rec), hipMemcpyDeviceToHost), "d2h");
+            recs = recs_buf.data();
+        }
+        auto rec = [&](uint32_t q, uint64_t k) -> stage_q2_rec & {
+            return host_out ? out[(uint64_t)q * max_out + k] : recs_buf[(uint64_t)q * n + k];
+        };
         const uint32_t read_id = rq[0];
-        // 4. the transaction's stock updates, through the device write path
+        // 5. the transaction's stock updates, through the device write path
         if (nq == 1 && commit_id && !*aborted) {
             std::vector<uint64_t> uk;
             std::vector<int32_t> ud;
             std::vector<uint32_t> ui;
-            for (uint32_t k = 0; k < n; ++k)
-                if (recs[k].update) {
-                    uk.push_back((uint64_t)recs[k].s_w_id);
-                    uk.push_back((uint64_t)recs[k].s_i_id);
-                    ud.insert(ud.end(), {recs[k].s_quantity + 50, recs[k].s_ytd, recs[k].s_order_cnt,
-                                         recs[k].s_remote_cnt});
+            for (uint32_t k = 0; k < n && (!host_out || k < max_out); ++k)
+                if (rec(0, k).update) {
+                    uk.push_back((uint64_t)rec(0, k).s_w_id);
+                    uk.push_back((uint64_t)rec(0, k).s_i_id);
+                    ud.insert(ud.end(), {rec(0, k).s_quantity + 50, rec(0, k).s_ytd, rec(0, k).s_order_cnt,
+                                         rec(0, k).s_remote_cnt});
                     ui.push_back(k);
                 }
             const uint64_t nu = ui.size();
@@ -462,10 +530,10 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
                 std::vector<uint8_t> rcs(nu);
                 hip_check(hipMemcpyAsync(rcs.data(), ub + u_rc, nu, hipMemcpyDeviceToHost, s), "d2h");
                 hip_check(hipStreamSynchronize(s), "update sync");
-                for (uint64_t j = 0; j < nu; ++j) recs[ui[j]].update_rc = rcs[j];
+                for (uint64_t j = 0; j < nu; ++j) rec(0, ui[j]).update_rc = rcs[j];
             }
         }
-        if (!to_out)
+        if (!host_out && out)
             for (uint32_t q = 0; q < nq; ++q)
                 std::memcpy(out + (uint64_t)q * max_out, recs + (uint64_t)q * n,
                             std::min<uint64_t>(n, max_out) * sizeof(stage_q2_rec));

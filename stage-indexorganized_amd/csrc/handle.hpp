@@ -39,6 +39,7 @@ struct stage_table {
     int shard_dedupe = -1;                         // -1 = STAGE_SHARD_DEDUPE or on
     int shard_key_bits = 64;                       // coalescing sort width (stage_set_shard_key_bits)
     int wp_overlap = 0;                            // stage_set_write_overlap
+    uint64_t q2_hint[2] = {0, 0};                  // CH-Q2's last visited suppliers / STOCK keys (launch shapes)
     std::mutex pipe_mu;  // serialises stage_probe_host calls on this table
     std::unique_ptr<stage::HostPipe, stage::HostPipeDeleter> pipe;
     // the device write path hands its epoch's bookkeeping (new copy / version headers, slot

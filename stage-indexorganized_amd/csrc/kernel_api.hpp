@@ -32,9 +32,12 @@ struct ProbeTuning {
 
 hipError_t launch_resolve(const DevTable &t, const uint64_t *keys, const uint16_t *lens, uint64_t n, int le_child,
                           uint32_t *out, hipStream_t s);
+// d_n (optional, the split-probe tables only -- wide keys or leaves above 128 slots): the batch's
+// size lives on the device (written by an earlier kernel of the stream); n is its upper bound and
+// sizes the grid, shape_n (0 = n) the expected size that picks the launch shape
 hipError_t launch_probe(const DevTable &t, const uint64_t *keys, const uint16_t *lens, const uint32_t *rids,
                         const uint32_t *leaf_in, uint64_t n, stage_probe_out_dev *out, uint8_t *recs, hipStream_t s,
-                        const ProbeTuning &tune);
+                        const ProbeTuning &tune, const uint64_t *d_n = nullptr, uint64_t shape_n = 0);
 // fan-out probe (sharded front-end, dist.hip): probe i's status record and row are stored at
 // every caller position flist[k], k in [fan[i].lo, fan[i].hi) (flist null: k itself).  Tables of
 // the YCSB geometry only (fixed-width 8-byte keys, 64-slot leaves, rows <= 1024 B).
@@ -88,8 +91,10 @@ hipError_t launch_resident_reader(const DevTable &t, const ReaderRing &g, hipStr
 // n keys; out[q * n + i] = the result of key i at rids[q], q < nq -- the hit slot is the same for
 // every read id (SearchRecordMeta does not depend on it), only the visibility walk is redone;
 // perm (may be null): base[i] is key perm[i]'s result, written to out[q * n + perm[i]]
+// d_n (optional): the key count on the device (n its upper bound); out is then [nq][*d_n]
 hipError_t launch_revisit(const DevTable &t, const stage_probe_out_dev *base, uint64_t n, const uint32_t *rids,
-                          uint32_t nq, const uint32_t *perm, stage_probe_out_dev *out, hipStream_t s);
+                          uint32_t nq, const uint32_t *perm, stage_probe_out_dev *out, hipStream_t s,
+                          const uint64_t *d_n = nullptr);
 // launch_revisit folded, for n probes cut into segments (segment k = base[seg_off[k], + seg_cnt[k])):
 // missed[q] |= 1 when any probe yields no record (LATEST / COPY / OLD) at rids[q], and
 // last[q * nseg + k] = segment k's last probe at rids[q] (left as it is for an empty segment) --
@@ -97,7 +102,7 @@ hipError_t launch_revisit(const DevTable &t, const stage_probe_out_dev *base, ui
 hipError_t launch_revisit_segments(const DevTable &t, const stage_probe_out_dev *base, uint64_t n,
                                    const uint64_t *seg_off, const uint32_t *seg_cnt, uint32_t nseg,
                                    const uint32_t *rids, uint32_t nq, stage_probe_out_dev *last, int32_t *missed,
-                                   hipStream_t s);
+                                   hipStream_t s, const uint64_t *d_n = nullptr, const uint64_t *d_nseg = nullptr);
 // stage_probe_batch_ex: after launch_probe of the same batch, re-answer the probes with fu[i] != 0
 // as BTree::Read(..., is_for_update = true) (status record and, if recs, the row); 32-B records
 hipError_t launch_for_update(const DevTable &t, const uint8_t *fu, const uint32_t *rids, uint64_t n,

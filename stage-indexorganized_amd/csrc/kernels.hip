@@ -1440,8 +1440,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void p
                                                           const uint32_t *__restrict__ rids,
                                                           const uint32_t *__restrict__ leaf_in, uint64_t n,
                                                           stage_probe_out_dev *__restrict__ out,
-                                                          uint8_t *__restrict__ recs) {
+                                                          uint8_t *__restrict__ recs,
+                                                          const uint64_t *__restrict__ dn) {
     __shared__ uint16_t s_cand[4][64][kProbeCand];
+    if (dn) n = *dn < n ? *dn : n;  // the batch's size as a previous kernel left it (launched for n at most)
     const uint32_t lane = lane_id(), wv = uni32(threadIdx.x >> 6);
     const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wv;
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
@@ -2808,23 +2810,30 @@ hipError_t launch_resolve(const DevTable &t, const uint64_t *keys, const uint16_
 
 hipError_t launch_probe(const DevTable &t, const uint64_t *keys, const uint16_t *lens, const uint32_t *rids,
                         const uint32_t *leaf_in, uint64_t n, stage_probe_out_dev *out, uint8_t *recs, hipStream_t s,
-                        const ProbeTuning &tune) {
+                        const ProbeTuning &tune, const uint64_t *d_n, uint64_t shape_n) {
     if (n == 0) return hipSuccess;
+    if (d_n) {  // device-sized batches: the split kernel only (wide keys / large leaves)
+        const bool split_path = (t.key_words > 1 || (t.key_width != 0 && t.cap > 128)) && tune.wide != 1 &&
+                                tune.status_bytes != 16;
+        if (!split_path) return hipErrorInvalidValue;
+    }
     const uint64_t chunks = (n + 63) / 64;
     const int blocks = grid_for(chunks, 4, tune.max_blocks > 0 ? tune.max_blocks : 16384);
     const bool var = t.key_width == 0;
     // wide fixed-width keys, and 8-byte keys in leaves above 128 slots (small rows): leaves of
     // up to 1024 slots, one probe in flight
     if (t.key_words > 1 || (!var && t.cap > 128)) {
-        const bool small = chunks < (uint64_t)tune.small_below;  // fewer 64-probe chunks than the chip holds waves
-        const int wblocks = small ? grid_for((n + 15) / 16, 4, tune.max_blocks > 0 ? tune.max_blocks : 16384) : blocks;
+        // launch shape from the expected size (a device-sized batch's hint), the grid from n
+        const uint64_t sn = d_n && shape_n ? std::min(shape_n, n) : n;
+        const bool small = (sn + 63) / 64 < (uint64_t)tune.small_below;  // fewer 64-probe chunks than the chip holds waves
+        const int wblocks = small ? grid_for((sn + 15) / 16, 4, tune.max_blocks > 0 ? tune.max_blocks : 16384) : blocks;
         // default: probe_split_kernel; STAGE_PROBE_WIDE=1: probe_kernel's one-probe-in-flight form
         const bool split = tune.wide != 1 && tune.status_bytes != 16;
 #define STAGE_PROBE_W(S, KW)                                                                                  \
     if (split && small)                                                                                       \
-        probe_split_kernel<S, KW, 16><<<wblocks, 256, 0, s>>>(t, keys, rids, leaf_in, n, out, recs);           \
+        probe_split_kernel<S, KW, 16><<<wblocks, 256, 0, s>>>(t, keys, rids, leaf_in, n, out, recs, d_n);      \
     else if (split)                                                                                           \
-        probe_split_kernel<S, KW, 64><<<blocks, 256, 0, s>>>(t, keys, rids, leaf_in, n, out, recs);            \
+        probe_split_kernel<S, KW, 64><<<blocks, 256, 0, s>>>(t, keys, rids, leaf_in, n, out, recs, d_n);       \
     else if (small)                                                                                           \
         probe_kernel<false, S, 1, 1, KW, 16><<<wblocks, 256, 0, s>>>(t, keys, lens, rids, leaf_in, n, out, recs, \
                                                                      nullptr, nullptr);                        \
@@ -2909,7 +2918,9 @@ __device__ __forceinline__ void revisit_one(const DevTable &t, uint32_t rid, u32
 __global__ __launch_bounds__(256) void revisit_kernel(DevTable t, const stage_probe_out_dev *__restrict__ base,
                                                       uint64_t n, const uint32_t *__restrict__ rids, uint32_t nq,
                                                       const uint32_t *__restrict__ perm,
-                                                      stage_probe_out_dev *__restrict__ out) {
+                                                      stage_probe_out_dev *__restrict__ out,
+                                                      const uint64_t *__restrict__ dn) {
+    if (dn) n = *dn < n ? *dn : n;  // out[q * n + i] with the device count n
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= n * nq) return;
     const uint64_t i = g % n, q = g / n;
@@ -2927,7 +2938,8 @@ __global__ __launch_bounds__(256) void revisit_kernel(DevTable t, const stage_pr
 constexpr uint32_t kRevisitQ = 16;
 __global__ __launch_bounds__(256) void revisit_missed_kernel(DevTable t, const stage_probe_out_dev *__restrict__ base,
                                                              uint64_t n, const uint32_t *__restrict__ rids, uint32_t nq,
-                                                             int32_t *__restrict__ missed) {
+                                                             int32_t *__restrict__ missed, const uint64_t *__restrict__ dn) {
+    if (dn) n = *dn < n ? *dn : n;
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= n * ((nq + kRevisitQ - 1) / kRevisitQ)) return;
     const uint64_t i = g % n;
@@ -2954,7 +2966,9 @@ __global__ __launch_bounds__(256) void revisit_last_kernel(DevTable t, const sta
                                                            const uint64_t *__restrict__ seg_off,
                                                            const uint32_t *__restrict__ seg_cnt, uint32_t nseg,
                                                            const uint32_t *__restrict__ rids, uint32_t nq,
-                                                           stage_probe_out_dev *__restrict__ last) {
+                                                           stage_probe_out_dev *__restrict__ last,
+                                                           const uint64_t *__restrict__ dseg) {
+    if (dseg) nseg = *dseg < nseg ? (uint32_t)*dseg : nseg;
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= (uint64_t)nseg * nq) return;
     const uint32_t k = (uint32_t)(g % nseg), q = (uint32_t)(g / nseg);
@@ -2971,18 +2985,21 @@ __global__ __launch_bounds__(256) void revisit_last_kernel(DevTable t, const sta
 hipError_t launch_revisit_segments(const DevTable &t, const stage_probe_out_dev *base, uint64_t n,
                                    const uint64_t *seg_off, const uint32_t *seg_cnt, uint32_t nseg,
                                    const uint32_t *rids, uint32_t nq, stage_probe_out_dev *last, int32_t *missed,
-                                   hipStream_t s) {
+                                   hipStream_t s, const uint64_t *d_n, const uint64_t *d_nseg) {
     if (nq == 0) return hipSuccess;
     const uint64_t tm = n * ((nq + kRevisitQ - 1) / kRevisitQ), tl = (uint64_t)nseg * nq;
-    if (tm) revisit_missed_kernel<<<(unsigned)((tm + 255) / 256), 256, 0, s>>>(t, base, n, rids, nq, missed);
-    if (tl) revisit_last_kernel<<<(unsigned)((tl + 255) / 256), 256, 0, s>>>(t, base, seg_off, seg_cnt, nseg, rids, nq, last);
+    if (tm) revisit_missed_kernel<<<(unsigned)((tm + 255) / 256), 256, 0, s>>>(t, base, n, rids, nq, missed, d_n);
+    if (tl)
+        revisit_last_kernel<<<(unsigned)((tl + 255) / 256), 256, 0, s>>>(t, base, seg_off, seg_cnt, nseg, rids, nq, last,
+                                                                         d_nseg);
     return hipGetLastError();
 }
 
 hipError_t launch_revisit(const DevTable &t, const stage_probe_out_dev *base, uint64_t n, const uint32_t *rids,
-                          uint32_t nq, const uint32_t *perm, stage_probe_out_dev *out, hipStream_t s) {
+                          uint32_t nq, const uint32_t *perm, stage_probe_out_dev *out, hipStream_t s,
+                          const uint64_t *d_n) {
     if (n == 0 || nq == 0) return hipSuccess;
-    revisit_kernel<<<(unsigned)((n * nq + 255) / 256), 256, 0, s>>>(t, base, n, rids, nq, perm, out);
+    revisit_kernel<<<(unsigned)((n * nq + 255) / 256), 256, 0, s>>>(t, base, n, rids, nq, perm, out, d_n);
     return hipGetLastError();
 }
 

@@ -2,7 +2,9 @@
 the path: stage_ch_query2 against the oracle's restatement (orc_ch_query2) on identically
 loaded REGION / NATION / SUPPLIER / ITEM / STOCK tables -- visited suppliers, the stock each
 one keeps, the I_DATA and quantity tests, aborts under version-chain visibility, and the
-committed stock updates read back through both."""
+committed stock updates read back through both.  Since round 5 the selection (regions, nations,
+suppliers, map segments) runs on the device and a batch synchronises once; the records land in
+a page-locked `out` from the finishing kernel, or are copied once the count is known."""
 import numpy as np
 import pytest
 
@@ -30,9 +32,7 @@ def ch(gpu):
     return c
 
 
-@pytest.mark.parametrize("q2_sort", ["0", "1"])
-def test_q2_matches_oracle_all_regions(ch, monkeypatch, q2_sort):
-    monkeypatch.setenv("STAGE_Q2_SORT", q2_sort)  # 1: the STOCK keys probed in leaf order
+def test_q2_matches_oracle_all_regions(ch):
     for target in range(5):
         recs, ab = ch.query2(target)
         orecs, oab = ch.query2_oracle(target)
@@ -41,9 +41,8 @@ def test_q2_matches_oracle_all_regions(ch, monkeypatch, q2_sort):
     assert recs.size > 1000 and recs["update"].sum() > 0 and recs["item_has_b"].sum() > 0
 
 
-@pytest.mark.parametrize("q2_sort,pinned", [("0", False), ("1", False), ("0", True)])
-def test_q2_batch_equals_single_queries(ch, monkeypatch, q2_sort, pinned):
-    monkeypatch.setenv("STAGE_Q2_SORT", q2_sort)
+@pytest.mark.parametrize("pinned", [False, True])
+def test_q2_batch_equals_single_queries(ch, pinned):
     rids = np.array([10, 0xFFFFFFFE, 3, 25, 0xFFFFFFFE, 7], np.uint32)
     # pinned: a page-locked `out` the records are copied into straight from the device
     out = stage.pinned_empty((rids.size, 1 << 14), stage.Q2_REC_DTYPE) if pinned else None
@@ -64,7 +63,7 @@ def test_q2_batch_equals_single_queries(ch, monkeypatch, q2_sort, pinned):
                 same(recs[q], orecs)
 
 
-def test_q2_visibility_and_commit(ch, monkeypatch):
+def test_q2_visibility_and_commit(ch):
     ostock = ch.orc["stock"]
     stock = ch.tables["stock"]
     recs, _ = ch.query2(3, read_id=10)
@@ -94,13 +93,6 @@ def test_q2_visibility_and_commit(ch, monkeypatch):
             same(recs, orecs)
             same(brecs[q], orecs)
     assert ch.query2(3, read_id=10)[1]  # the abort case is exercised
-    monkeypatch.setenv("STAGE_Q2_SORT", "1")  # leaf-ordered STOCK probes: the same outcomes
-    srecs, sabort = ch.query2_batch(np.array([10, 25, 40, 0xFFFFFFFE], np.uint32), 3)
-    assert (sabort == babort).all()
-    for q in range(4):
-        if not babort[q]:
-            same(srecs[q], brecs[q])
-    monkeypatch.delenv("STAGE_Q2_SORT")
     # commit path: the transaction's updates through the device write path, mirrored on the oracle
     rid, cid = 50, 51
     recs, ab = ch.query2(3, read_id=rid, commit_id=cid)
