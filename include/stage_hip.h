@@ -522,6 +522,15 @@ int stage_probe_sharded(stage_table *t, const uint64_t *d_keys, const uint32_t *
  * reads its buffer with stage_sharded_owner_rows (valid until its next sharded probe). */
 #define STAGE_REPLY_ROWS 0
 #define STAGE_REPLY_OWNER 1
+/* STAGE_REPLY_PEER: what STAGE_REPLY_ROWS returns (status records and rows at the caller's
+ * positions), but only the 32-B status records travel over RCCL: each owner keeps the rows of the
+ * remote requests it probed in one of two row buffers of its own (by call parity) and the caller's
+ * fan-out reads each row there -- over xGMI, through the owner's buffers opened by IPC handle
+ * (hipIpcGetMemHandle / hipIpcOpenMemHandle, handles exchanged over the communicator when a buffer
+ * grows).  No RCCL receive buffer is written and read back for the rows.  Every rank knows every
+ * rank's send counts (an allgather instead of the count all-to-all), hence where each owner put
+ * each row.  d_records required; at world 1 the same as STAGE_REPLY_ROWS. */
+#define STAGE_REPLY_PEER 2
 int stage_probe_sharded_ex(stage_table *t, const uint64_t *d_keys, const uint32_t *d_read_ids,
                            uint64_t n, stage_probe_out *d_out, uint8_t *d_records, int reply_mode,
                            void *stream);

@@ -389,6 +389,9 @@ hipError_t sort32(void *temp, size_t &bytes, const uint32_t *kin, uint32_t *kout
 }  // namespace
 
 ShardComm::~ShardComm() {
+    for (void *p : opened) (void)hipIpcCloseMemHandle(p);
+    for (void *p : {prow[0], prow[1], hbuf})
+        if (p) (void)hipFree(p);
     if (cs) (void)hipStreamSynchronize(cs), (void)hipStreamDestroy(cs);
     if (us) (void)hipStreamSynchronize(us), (void)hipStreamDestroy(us);
     if (ps) (void)hipStreamSynchronize(ps), (void)hipStreamDestroy(ps);
@@ -725,7 +728,7 @@ static void fan_launch(const stage_probe_out_dev *sout, const uint8_t *srec, uin
 // rout / rrec for the return transfer.  Owner reply: everything into rout / rrec, rows tagged
 // with their owner-local index.
 static void chunk_probe(ShardComm &c, const Plan &P, int i, const DevTable &t, const ProbeTuning &tune, bool owner,
-                        stage_probe_out_dev *d_out, uint8_t *d_recs, hipStream_t s) {
+                        stage_probe_out_dev *d_out, uint8_t *d_recs, hipStream_t s, uint8_t *rows_buf = nullptr) {
     const int W = P.W, me = c.rank;
     const uint64_t b = P.rb[i], e = P.rb[i + 1];
     if (e == b) return;
@@ -740,7 +743,7 @@ static void chunk_probe(ShardComm &c, const Plan &P, int i, const DevTable &t, c
     unpack((const SendRec *)c.send + q0, r0, r1 - r0);
     unpack((const SendRec *)c.recv + r1, r1, e - r1);
     stage_probe_out_dev *rout = (stage_probe_out_dev *)c.rout;
-    uint8_t *rrec = (uint8_t *)c.rrec;
+    uint8_t *rrec = rows_buf ? rows_buf : (uint8_t *)c.rrec;  // peer reply: this call's exported row buffer
     const bool rows = owner || d_recs != nullptr;
     auto probe = [&](uint64_t a, uint64_t z) {
         if (z > a)
@@ -803,6 +806,107 @@ static void chunk_return(ShardComm &c, const Plan &P, int i, uint32_t stride, bo
     chk(hipGetLastError(), "owner-reply return");
 }
 
+// ---- STAGE_REPLY_PEER.  Every rank knows every rank's send counts S[q][i][r] (an allgather in
+// place of the count all-to-all), hence where owner q put the rows of the requests rank r sent it
+// in chunk i: q's receive layout is chunk-major, then by source rank (plan_receive), so
+//   peer_row_off(q, i, r) = sum_{i' < i} sum_{r'} S[r'][i'][q] + sum_{r' < r} S[r'][i][q].
+// Each rank's two row buffers hold m_q = sum_{i, r} S[r][i][q] rows; every rank applies the same
+// growth rule to every rank's size, so all of them know when the buffers moved and re-exchange
+// the IPC handles together (an allgather of 2 handles per rank).
+struct PeerCounts {
+    int W, C;
+    std::vector<uint32_t> S;  // [q][i][r]: q sends r in chunk i
+    uint32_t at(int q, int i, int r) const { return S[((size_t)q * C + i) * W + r]; }
+    uint64_t row_off(int q, int i, int r) const {
+        uint64_t o = 0;
+        for (int i2 = 0; i2 < i; ++i2)
+            for (int r2 = 0; r2 < W; ++r2) o += at(r2, i2, q);
+        for (int r2 = 0; r2 < r; ++r2) o += at(r2, i, q);
+        return o;
+    }
+    uint64_t received(int q) const {
+        uint64_t m = 0;
+        for (int i = 0; i < C; ++i)
+            for (int r = 0; r < W; ++r) m += at(r, i, q);
+        return m;
+    }
+};
+
+// the growth rule every rank applies to every rank's row buffers; true when one of them grows
+static bool peer_grow_plan(ShardComm &c, const PeerCounts &pc) {
+    if ((int)c.peer_cap.size() != pc.W) c.peer_cap.assign(pc.W, 0);
+    bool grew = false;
+    for (int q = 0; q < pc.W; ++q) {
+        const uint64_t m = pc.received(q);
+        if (m > c.peer_cap[q]) {
+            c.peer_cap[q] = m + m / 8 + 1024;
+            grew = true;
+        }
+    }
+    return grew;
+}
+
+// this rank's row buffers at the size the plan says (the old ones are freed: their readers are
+// done -- every rank's fan-out of the previous call ended before this call's count exchange)
+static void peer_alloc_own(ShardComm &c, uint32_t stride) {
+    const uint64_t cap = c.peer_cap[c.rank];
+    if (cap == c.prow_cap && c.prow[0]) return;
+    for (int k = 0; k < 2; ++k) grow(c.prow[k], cap * stride);
+    c.prow_cap = cap;
+}
+
+static void *hbuf(ShardComm &c, uint64_t bytes) {
+    if (bytes > c.hbuf_cap) {
+        grow(c.hbuf, bytes);
+        c.hbuf_cap = bytes;
+    }
+    return c.hbuf;
+}
+
+// the IPC handles of every rank's two row buffers, exchanged over the communicator; the peers'
+// buffers opened here (own buffers used in place)
+static void peer_exchange(ShardComm &c, hipStream_t s) {
+    const int W = c.world;
+    static_assert(sizeof(hipIpcMemHandle_t) == 64, "IPC handle size");
+    std::vector<hipIpcMemHandle_t> mine(2), all((size_t)2 * W);
+    for (int k = 0; k < 2; ++k) chk(hipIpcGetMemHandle(&mine[k], c.prow[k]), "hipIpcGetMemHandle (peer rows)");
+    uint8_t *d = (uint8_t *)hbuf(c, (uint64_t)(W + 1) * 128);
+    chk(hipMemcpyAsync(d, mine.data(), 128, hipMemcpyHostToDevice, s), "handles h2d");
+    nchk(ncclAllGather(d, d + 128, 128, ncclUint8, (ncclComm_t)c.comm, s), "ncclAllGather handles");
+    chk(hipMemcpyAsync(all.data(), d + 128, (size_t)128 * W, hipMemcpyDeviceToHost, s), "handles d2h");
+    chk(hipStreamSynchronize(s), "handles sync");
+    for (void *p : c.opened) (void)hipIpcCloseMemHandle(p);
+    c.opened.clear();
+    for (int k = 0; k < 2; ++k) c.peer_row[k].assign(W, nullptr);
+    for (int q = 0; q < W; ++q)
+        for (int k = 0; k < 2; ++k) {
+            if (q == c.rank) {
+                c.peer_row[k][q] = c.prow[k];
+                continue;
+            }
+            void *p = nullptr;
+            chk(hipIpcOpenMemHandle(&p, all[(size_t)2 * q + k], hipIpcMemLazyEnablePeerAccess),
+                "hipIpcOpenMemHandle (peer rows)");
+            c.opened.push_back(p);
+            c.peer_row[k][q] = p;
+        }
+}
+
+// peer reply, chunk i: the status records that came back from every other rank, with each row read
+// where its owner left it (peer_row) and stored at the caller positions
+static void chunk_return_peer(ShardComm &c, const Plan &P, const PeerCounts &pc, int i, uint32_t stride,
+                              stage_probe_out_dev *d_out, uint8_t *d_recs, hipStream_t s) {
+    const int W = P.W, me = c.rank;
+    const stage_probe_out_dev *bout = (const stage_probe_out_dev *)c.bout;
+    for (int q = 0; q < W; ++q) {
+        if (q == me) continue;  // own requests: probed straight to their caller positions
+        const uint64_t p0 = P.soff[(size_t)i * (W + 1) + q], sn = P.sc[(size_t)i * W + q];
+        if (!sn) continue;
+        const uint8_t *rows = (const uint8_t *)c.peer_row[c.parity][q] + pc.row_off(q, i, me) * (uint64_t)stride;
+        fan_launch(bout + p0, rows, p0, p0 + sn, c, P, stride, d_out, d_recs, s);
+    }
+}
+
 static void owner_expand(ShardComm &c, const Plan &P, stage_probe_out_dev *d_out, hipStream_t s) {
     if (!P.dedupe || P.n == 0) return;
     const int W = P.W, me = c.rank;
@@ -831,6 +935,7 @@ int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const 
                 hipStream_t s) {
     if (!c.comm) throw std::invalid_argument("not an RCCL communicator");
     const bool owner = reply == STAGE_REPLY_OWNER;
+    const bool peer = reply == STAGE_REPLY_PEER && c.world > 1 && d_recs != nullptr;
     if (owner) d_recs = nullptr;  // rows stay on the owner
     c.owner_rows = 0;
     const int W = c.world, C = c.chunks;
@@ -839,20 +944,43 @@ int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const 
     Plan P;
     plan_route(c, P, d_keys, d_rids, n, stride, owner, s);
     uint32_t *cnt = (uint32_t *)c.cnt, *sendT = cnt + (uint64_t)C * W, *recvT = sendT + (uint64_t)C * W;
-    transpose_counts<<<1, 256, 0, s>>>(cnt, C, W, sendT);
-    nchk(ncclAllToAll(sendT, recvT, (size_t)C, ncclUint32, comm, s), "ncclAllToAll counts");
-    // [C][W] send counts, then [W][C] receive counts, then the coalesced request count
-    std::vector<uint32_t> hc((size_t)2 * C * W + 1);
-    chk(hipMemcpyAsync(hc.data(), cnt, (size_t)C * W * 4, hipMemcpyDeviceToHost, s), "counts d2h");
-    chk(hipMemcpyAsync(hc.data() + (size_t)C * W, recvT, (size_t)C * W * 4, hipMemcpyDeviceToHost, s), "counts d2h");
-    chk(hipMemcpyAsync(hc.data() + (size_t)2 * C * W, c.dd_nu, 4, hipMemcpyDeviceToHost, s), "nu d2h");
-    chk(hipStreamSynchronize(s), "sync");
-    P.sc.assign(hc.begin(), hc.begin() + (size_t)C * W);
-    P.total = hc[(size_t)2 * C * W];
+    PeerCounts pc{W, C, {}};
+    if (peer) {
+        // every rank's [C][W] send counts (the peer fan-out needs the owners' receive layouts),
+        // then the coalesced request count
+        uint32_t *all = (uint32_t *)hbuf(c, ((uint64_t)W * C * W + 1) * 4);
+        nchk(ncclAllGather(cnt, all, (size_t)C * W, ncclUint32, comm, s), "ncclAllGather counts");
+        std::vector<uint32_t> hc((size_t)W * C * W + 1);
+        chk(hipMemcpyAsync(hc.data(), all, (size_t)W * C * W * 4, hipMemcpyDeviceToHost, s), "counts d2h");
+        chk(hipMemcpyAsync(hc.data() + (size_t)W * C * W, c.dd_nu, 4, hipMemcpyDeviceToHost, s), "nu d2h");
+        chk(hipStreamSynchronize(s), "sync");
+        pc.S.assign(hc.begin(), hc.begin() + (size_t)W * C * W);
+        P.sc.assign(pc.S.begin() + (size_t)c.rank * C * W, pc.S.begin() + (size_t)(c.rank + 1) * C * W);
+        P.total = hc[(size_t)W * C * W];
+        P.rc.resize((size_t)C * W);
+        for (int i = 0; i < C; ++i)
+            for (int r = 0; r < W; ++r) P.rc[(size_t)i * W + r] = pc.at(r, i, c.rank);
+        if (peer_grow_plan(c, pc)) {  // the same decision on every rank
+            peer_alloc_own(c, stride);
+            peer_exchange(c, s);
+        }
+        c.parity ^= 1;
+    } else {
+        transpose_counts<<<1, 256, 0, s>>>(cnt, C, W, sendT);
+        nchk(ncclAllToAll(sendT, recvT, (size_t)C, ncclUint32, comm, s), "ncclAllToAll counts");
+        // [C][W] send counts, then [W][C] receive counts, then the coalesced request count
+        std::vector<uint32_t> hc((size_t)2 * C * W + 1);
+        chk(hipMemcpyAsync(hc.data(), cnt, (size_t)C * W * 4, hipMemcpyDeviceToHost, s), "counts d2h");
+        chk(hipMemcpyAsync(hc.data() + (size_t)C * W, recvT, (size_t)C * W * 4, hipMemcpyDeviceToHost, s), "counts d2h");
+        chk(hipMemcpyAsync(hc.data() + (size_t)2 * C * W, c.dd_nu, 4, hipMemcpyDeviceToHost, s), "nu d2h");
+        chk(hipStreamSynchronize(s), "sync");
+        P.sc.assign(hc.begin(), hc.begin() + (size_t)C * W);
+        P.total = hc[(size_t)2 * C * W];
+        P.rc.resize((size_t)C * W);
+        for (int i = 0; i < C; ++i)
+            for (int r = 0; r < W; ++r) P.rc[(size_t)i * W + r] = hc[(size_t)C * W + (size_t)r * C + i];
+    }
     plan_send(c, P);
-    P.rc.resize((size_t)C * W);
-    for (int i = 0; i < C; ++i)
-        for (int r = 0; r < W; ++r) P.rc[(size_t)i * W + r] = hc[(size_t)C * W + (size_t)r * C + i];
     plan_receive(c, P, stride);
     hipEvent_t *ev_keys = c.evs.data(), *ev_probe = ev_keys + C, *ev_res = ev_probe + C, ev_start = ev_res[C];
     // the comm stream starts after the routing (done: s was synchronised) -- keys of all chunks
@@ -876,7 +1004,7 @@ int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const 
     const uint64_t ob = sizeof(stage_probe_out_dev);
     for (int i = 0; i < C; ++i) {
         chk(hipStreamWaitEvent(s, ev_keys[i], 0), "wait keys");
-        chunk_probe(c, P, i, t, tune, owner, d_out, d_recs, s);
+        chunk_probe(c, P, i, t, tune, owner, d_out, d_recs, s, peer ? (uint8_t *)c.prow[c.parity] : nullptr);
         chk(hipEventRecord(ev_probe[i], s), "event");
         chk(hipStreamWaitEvent(c.cs, ev_probe[i], 0), "wait probe");
         nchk(ncclGroupStart(), "group");
@@ -884,15 +1012,16 @@ int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const 
             if (r == c.rank) continue;  // own results are already in place
             const uint32_t sn = P.sc[(size_t)i * W + r], rn = P.rc[(size_t)i * W + r];
             const uint64_t so = P.soff[(size_t)i * (W + 1) + r], ro = P.roff[(size_t)i * (W + 1) + r];
+            const bool send_rows = d_recs && !peer;  // peer reply: the rows stay here, read in place
             if (rn) {
                 nchk(ncclSend((const uint8_t *)c.rout + ro * ob, (uint64_t)rn * ob, ncclUint8, r, comm, c.cs), "send out");
-                if (d_recs)
+                if (send_rows)
                     nchk(ncclSend((const uint8_t *)c.rrec + ro * stride, (uint64_t)rn * stride, ncclUint8, r, comm, c.cs),
                          "send rows");
             }
             if (sn) {
                 nchk(ncclRecv((uint8_t *)c.bout + so * ob, (uint64_t)sn * ob, ncclUint8, r, comm, c.cs), "recv out");
-                if (d_recs)
+                if (send_rows)
                     nchk(ncclRecv((uint8_t *)c.brec + so * stride, (uint64_t)sn * stride, ncclUint8, r, comm, c.cs),
                          "recv rows");
             }
@@ -900,7 +1029,8 @@ int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const 
         nchk(ncclGroupEnd(), "group end");
         chk(hipEventRecord(ev_res[i], c.cs), "event");
         chk(hipStreamWaitEvent(c.us, ev_res[i], 0), "wait results");
-        chunk_return(c, P, i, stride, owner, d_out, d_recs, c.us);
+        if (peer) chunk_return_peer(c, P, pc, i, stride, d_out, d_recs, c.us);
+        else chunk_return(c, P, i, stride, owner, d_out, d_recs, c.us);
     }
     if (owner) owner_expand(c, P, d_out, c.us);
     // the caller's stream completes after the last fan-out and the own-request probes
@@ -921,6 +1051,7 @@ int shard_probe_loopback(const std::vector<ShardComm *> &cs, const std::vector<c
     const int W = (int)cs.size();
     const uint32_t stride = ts[0]->stride;
     const bool owner = reply == STAGE_REPLY_OWNER;
+    const bool peer = reply == STAGE_REPLY_PEER && W > 1 && recs[0] != nullptr;
     if (owner)
         for (auto &r : recs) r = nullptr;
     for (int r = 0; r < W; ++r)
@@ -947,6 +1078,22 @@ int shard_probe_loopback(const std::vector<ShardComm *> &cs, const std::vector<c
             for (int q = 0; q < W; ++q) P[r].rc[(size_t)i * W + q] = P[q].sc[(size_t)i * W + r];
         plan_receive(*cs[r], P[r], stride);
     }
+    // peer reply: every shard's counts (what the allgather gives each rank), the same growth rule,
+    // and the other shards' row buffers used in place (one process: no IPC)
+    PeerCounts pc{W, C, {}};
+    if (peer) {
+        pc.S.resize((size_t)W * C * W);
+        for (int q = 0; q < W; ++q) std::copy(P[q].sc.begin(), P[q].sc.end(), pc.S.begin() + (size_t)q * C * W);
+        for (int r = 0; r < W; ++r)
+            if (peer_grow_plan(*cs[r], pc)) peer_alloc_own(*cs[r], stride);
+        for (int r = 0; r < W; ++r) {
+            for (int k = 0; k < 2; ++k) {
+                cs[r]->peer_row[k].resize(W);
+                for (int q = 0; q < W; ++q) cs[r]->peer_row[k][q] = cs[q]->prow[k];
+            }
+            cs[r]->parity ^= 1;
+        }
+    }
     auto copy = [&](void *dst, const void *src, uint64_t bytes, const char *what) {
         if (bytes) chk(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s), what);
     };
@@ -960,18 +1107,23 @@ int shard_probe_loopback(const std::vector<ShardComm *> &cs, const std::vector<c
             }
     const uint64_t ob = sizeof(stage_probe_out_dev);
     for (int i = 0; i < C; ++i) {
-        for (int r = 0; r < W; ++r) chunk_probe(*cs[r], P[r], i, *ts[r], tune, owner, outs[r], recs[r], s);
+        for (int r = 0; r < W; ++r)
+            chunk_probe(*cs[r], P[r], i, *ts[r], tune, owner, outs[r], recs[r], s,
+                        peer ? (uint8_t *)cs[r]->prow[cs[r]->parity] : nullptr);
         for (int q = 0; q < W; ++q)  // results: owner q's chunk-i segment for r -> r's chunk-i slots of q
             for (int r = 0; r < W; ++r) {
                 if (r == q) continue;  // as shard_probe: own results are already in place
                 const uint64_t cnt = P[q].rc[(size_t)i * W + r];
                 const uint64_t ro = P[q].roff[(size_t)i * (W + 1) + r], so = P[r].soff[(size_t)i * (W + 1) + q];
                 copy((uint8_t *)cs[r]->bout + so * ob, (const uint8_t *)cs[q]->rout + ro * ob, cnt * ob, "loopback out");
-                if (rows)
+                if (rows && !peer)
                     copy((uint8_t *)cs[r]->brec + so * stride, (const uint8_t *)cs[q]->rrec + ro * stride,
                          cnt * stride, "loopback rows");
             }
-        for (int r = 0; r < W; ++r) chunk_return(*cs[r], P[r], i, stride, owner, outs[r], recs[r], s);
+        for (int r = 0; r < W; ++r) {
+            if (peer) chunk_return_peer(*cs[r], P[r], pc, i, stride, outs[r], recs[r], s);
+            else chunk_return(*cs[r], P[r], i, stride, owner, outs[r], recs[r], s);
+        }
     }
     if (owner)
         for (int r = 0; r < W; ++r) owner_expand(*cs[r], P[r], outs[r], s);

@@ -41,6 +41,17 @@ struct ShardComm {
     uint64_t last_received = 0;      // requests this rank probed as owner (own + other ranks')
     void *ctl = nullptr;             // control-plane scratch (doubles)
     uint64_t ctl_cap = 0;
+    // STAGE_REPLY_PEER: the owner keeps the rows of the remote requests it probed in one of its
+    // two row buffers (by call parity), and each caller's fan-out reads them there -- over xGMI,
+    // through the owner's buffers opened by IPC handle (loopback: the other shard's pointers)
+    void *prow[2] = {nullptr, nullptr};  // this rank's row buffers
+    uint64_t prow_cap = 0;               // rows each of them holds
+    std::vector<uint64_t> peer_cap;      // every rank's prow_cap, as every rank computes it
+    std::vector<void *> peer_row[2];     // [parity][rank]: where rank's row buffers are here
+    std::vector<void *> opened;          // IPC mappings to close
+    void *hbuf = nullptr;                // handle / count exchange scratch
+    uint64_t hbuf_cap = 0;
+    int parity = 0;
     ~ShardComm();
 };
 

@@ -692,7 +692,7 @@ class Reader:
             pass
 
 
-REPLY_ROWS, REPLY_OWNER = 0, 1
+REPLY_ROWS, REPLY_OWNER, REPLY_PEER = 0, 1, 2  # stage_hip.h STAGE_REPLY_*
 
 
 def owner_rows(table, loopback=True):

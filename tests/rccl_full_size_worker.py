@@ -89,14 +89,14 @@ def main():
     d_out = stage.DeviceBuffer(nk * 32)
     d_rec = stage.DeviceBuffer(nk * shard.stride)
     ok = True
-    for reply in (stage.REPLY_ROWS, stage.REPLY_OWNER):
-        name = "rows" if reply == stage.REPLY_ROWS else "owner"
+    for reply in (stage.REPLY_ROWS, stage.REPLY_OWNER, stage.REPLY_PEER):
+        name = {stage.REPLY_OWNER: "owner", stage.REPLY_PEER: "peer"}.get(reply, "rows")
         times = []
         for it in range(3):  # the first call grows the exchange buffers; all three are checked alike
             stage.comm_allreduce(shard, [1.0])  # barrier
             ts = time.perf_counter()
             check(L.stage_probe_sharded_ex(shard.h, d_keys.ptr, None, nk, d_out.ptr,
-                                           d_rec.ptr if reply == stage.REPLY_ROWS else None, reply, None), "sharded")
+                                           d_rec.ptr if reply != stage.REPLY_OWNER else None, reply, None), "sharded")
             check(L.stage_device_sync(), "sync")
             times.append(time.perf_counter() - ts)
         st = stage.sharded_stats_ex(shard)
@@ -104,11 +104,11 @@ def main():
         case = {"reply": name, "keys": int(nk), "step_s": [round(x, 4) for x in times],
                 "stats": {kk: int(v) for kk, v in st.items()}}
         good = True
-        for f in (FIELDS if reply == stage.REPLY_ROWS else ("status", "cstamp", "rec_cstamp")):
+        for f in (FIELDS if reply != stage.REPLY_OWNER else ("status", "cstamp", "rec_cstamp")):
             if not (out[f] == ref_out[f]).all():
                 good = False
                 case.setdefault("mismatch", []).append(f)
-        if reply == stage.REPLY_ROWS:
+        if reply != stage.REPLY_OWNER:
             rows = d_rec.to_numpy(np.uint8, nk * shard.stride).reshape(nk, shard.stride)
             if not (digest(rows) == ref_dig).all():
                 good = False

@@ -90,9 +90,12 @@ def main():
     ok = True
     # (chunks, dedupe, read ids, reply, batch size): rank world-1 probes nothing in one case (it
     # still takes part in every exchange)
+    # STAGE_REPLY_PEER: rows read through the owners' IPC-mapped row buffers (two parities: the
+    # case runs its probe twice, as every case does)
     cases = [(1, 1, True, stage.REPLY_ROWS, 60_000), (4, 1, True, stage.REPLY_ROWS, 90_000),
              (3, 0, False, stage.REPLY_ROWS, 40_000), (4, 1, False, stage.REPLY_OWNER, 50_000),
-             (2, 1, True, stage.REPLY_ROWS, 0 if rank == world - 1 else 30_000)]
+             (2, 1, True, stage.REPLY_ROWS, 0 if rank == world - 1 else 30_000),
+             (4, 1, True, stage.REPLY_PEER, 80_000), (2, 0, False, stage.REPLY_PEER, 0 if rank == 0 else 35_000)]
     for ci, (chunks, dedupe, use_rids, reply, size) in enumerate(cases):
         check(L.stage_set_shard_chunks(shard.h, chunks), "chunks")
         stage.set_shard_dedupe(shard, dedupe)
@@ -107,24 +110,24 @@ def main():
         d_keys = stage.DeviceBuffer.from_numpy(k) if nk else None
         d_rids = stage.DeviceBuffer.from_numpy(rids) if (use_rids and nk) else None
         d_out = stage.DeviceBuffer(max(nk, 1) * 32)
-        d_rec = stage.DeviceBuffer(max(nk, 1) * shard.stride) if reply == stage.REPLY_ROWS else None
+        d_rec = stage.DeviceBuffer(max(nk, 1) * shard.stride) if reply != stage.REPLY_OWNER else None
         for _ in range(2):  # the second call reuses grown scratch buffers
             check(L.stage_probe_sharded_ex(shard.h, d_keys.ptr if d_keys else None, d_rids.ptr if d_rids else None,
                                            nk, d_out.ptr, d_rec.ptr if d_rec else None, reply, None), "sharded")
             check(L.stage_device_sync(), "sync")
         st = stage.sharded_stats_ex(shard)
         case = {"case": ci, "chunks": chunks, "dedupe": dedupe, "read_ids": use_rids,
-                "reply": "owner" if reply == stage.REPLY_OWNER else "rows", "keys": nk,
+                "reply": {stage.REPLY_OWNER: "owner", stage.REPLY_PEER: "peer"}.get(reply, "rows"), "keys": nk,
                 "stats": {kk: int(v) for kk, v in st.items()} if isinstance(st, dict) else str(st)}
         good = True
         if nk:
             out = d_out.to_numpy(stage.PROBE_OUT_DTYPE, nk)
             ref_out, ref_rows = full.probe(k, read_ids=rids)
-            for f in FIELDS if reply == stage.REPLY_ROWS else ("status", "cstamp"):
+            for f in FIELDS if reply != stage.REPLY_OWNER else ("status", "cstamp"):
                 if not (out[f] == ref_out[f]).all():
                     good = False
                     case.setdefault("mismatch", []).append(f)
-            if reply == stage.REPLY_ROWS:
+            if reply != stage.REPLY_OWNER:
                 rows = d_rec.to_numpy(np.uint8, nk * shard.stride).reshape(nk, shard.stride)
                 if not (rows == ref_rows).all():
                     good = False
