@@ -55,6 +55,7 @@ struct ReadFacts {
     uint32_t cstamp;
     uint64_t meta;
     uint32_t loc, next;
+    uint64_t value = 0;  // the tuple's first payload word (TestTuple::value, testing_transaction_util.h:82-92)
 };
 
 // EphemeralPool::OverwriteVersionHeader (ephemeral_pool.h:26-150)
@@ -92,14 +93,15 @@ struct Txn {
 };
 
 // Store (duck-typed):
-//   ReadFacts read(uint64_t key, uint32_t read_id)             -- no side effects on the pool
+//   ReadFacts read(uint64_t key, uint32_t read_id, bool for_update)
+//                                                                -- no side effects on the pool
 //   bool header(uint32_t copy_id, Hdr &out)                     -- GetOversionHeader by copy id
 //   void add_reader(uint32_t copy_id, uint32_t read_id)          -- AddReader
 //   int  wr_count(uint32_t copy_id, int delta)                   -- 1 ok, 0 refused (waiting)
 //   void update_ps(uint32_t copy_id, uint32_t pstamp)            -- UpdatePs
 //   void location(uint32_t loc, uint64_t &meta, uint32_t &next)  -- *record_meta_ptr now
-//   int  update(uint64_t key, uint8_t byte, uint32_t writer, RecordMeta &meta_upt)
-//                                                                -- BTree::Update (ReturnCode)
+//   int  update(uint64_t key, const std::vector<uint8_t> &delta, bool for_update, uint32_t writer,
+//               RecordMeta &meta_upt)                            -- BTree::Update (ReturnCode)
 //   int  commit_update(uint64_t key, uint32_t cid, uint32_t sstamp), abort_update(uint64_t key)
 // what the run exercised (for coverage assertions; equal between stores when the traces are)
 struct Stats {
@@ -130,50 +132,73 @@ public:
     }
 
     // IndexScanExecutor point lookup (executor.h:374-454) through BTree::Read; false = the
-    // executor failed (the caller aborts the transaction)
-    bool read(Txn *t, uint64_t key) {
-        const ReadFacts f = st_.read(key, t->read_id);
+    // executor failed (the caller aborts the transaction).  *value: the tuple's value, -1 when
+    // the executor produced none (ExecuteRead, testing_transaction_util.cpp:111-119).
+    // is_for_update: BTree::Read's own-record branch (b_tree.cpp:2087 -- no copy, no AddReader)
+    // and no PerformRead (executor.h:388)
+    bool read(Txn *t, uint64_t key, bool for_update = false, int64_t *value = nullptr) {
+        const ReadFacts f = st_.read(key, t->read_id, for_update);
         // BTree::Read served from the overwrite copy tracks the reader (b_tree.cpp:2087-2105)
-        const bool via_copy = inserting(f.meta) && (f.next & kKindMask) == kCopy && f.status != ST_NOT_FOUND;
+        const bool via_copy =
+            !for_update && inserting(f.meta) && (f.next & kKindMask) == kCopy && f.status != ST_NOT_FOUND;
         if (via_copy) st_.add_reader(f.next & kIndexMask, t->read_id);
         bool ok = true;
         int pr = -1;
         if (f.status == ST_LATEST || f.status == ST_COPY) {  // txn_id >= the record's cstamp
-            pr = perform_read(t, RecordMeta{f.meta, f.next, f.loc}, f.cstamp) ? 1 : 0;
-            ok = pr == 1;
+            if (!for_update) {
+                pr = perform_read(t, RecordMeta{f.meta, f.next, f.loc}, f.cstamp) ? 1 : 0;
+                ok = pr == 1;
+            }
         } else if (f.status == ST_FAIL) {
             ok = false;
         }
+        const bool tuple = f.status == ST_LATEST || f.status == ST_COPY || f.status == ST_OLD;
+        if (value) *value = tuple ? (int64_t)f.value : -1;
         if (!ok) t->result = Result::FAILURE;
         stats.reads++;
         stats.reads_via_copy += via_copy;
         stats.perform_read_fail += pr == 0;
-        emit("read T%u key=%llu st=%u cstamp=%u meta=%016llx loc=%u next=%08x via_copy=%d perform_read=%d ok=%d", t->id,
-             (unsigned long long)key, f.status, f.cstamp, (unsigned long long)f.meta, f.loc, f.next, (int)via_copy, pr,
-             (int)ok);
+        emit("read T%u key=%llu fu=%d st=%u cstamp=%u meta=%016llx loc=%u next=%08x value=%llu via_copy=%d "
+             "perform_read=%d ok=%d",
+             t->id, (unsigned long long)key, (int)for_update, f.status, f.cstamp, (unsigned long long)f.meta, f.loc,
+             f.next, (unsigned long long)(tuple ? f.value : 0), (int)via_copy, pr, (int)ok);
         return ok;
     }
 
     // PointUpdateExecutor (executor.h:206-322): BTree::Update, then PerformUpdate; a failure is
     // retried until retry_count > 5 -- the retries meet the transaction's own in-flight update
-    // (Dirty), so a failed PerformUpdate ends the executor with FAILURE all the same
-    bool update(Txn *t, uint64_t key, uint8_t byte) {
+    // (Dirty), so a failed PerformUpdate ends the executor with FAILURE all the same.
+    // is_for_update: the writer's own record, patched in place, no PerformUpdate (:246-256)
+    bool update(Txn *t, uint64_t key, const std::vector<uint8_t> &delta, bool for_update = false) {
         RecordMeta upt{0, 0, 0};  // BTree::Update's meta_upt_ (b_tree.cpp:2153)
-        const int rc = st_.update(key, byte, t->read_id, upt);
+        const int rc = st_.update(key, delta, for_update, t->read_id, upt);
         bool ok = true;
         int pu = -1;
-        if (rc == 1) {                                // Ok
-            pu = perform_update(t, upt, key) ? 1 : 0;
-            ok = pu == 1;
-        } else if (rc != 7 && rc != 3) {              // not NotNeededUpdate / NotFound
+        if (rc == 1) {  // Ok
+            if (!for_update) {
+                pu = perform_update(t, upt, key) ? 1 : 0;
+                ok = pu == 1;
+            }
+        } else if (rc != 7 && rc != 3) {  // not NotNeededUpdate / NotFound
             ok = false;
         }
         t->result = ok ? Result::SUCCESS : Result::FAILURE;
         (rc == 1 && ok ? stats.updates_ok : stats.updates_failed) += (rc == 1 || !ok);
-        emit("update T%u key=%llu byte=%u rc=%d perform_update=%d ok=%d", t->id, (unsigned long long)key, byte, rc, pu,
-             (int)ok);
+        emit("update T%u key=%llu byte=%u len=%u fu=%d rc=%d perform_update=%d ok=%d", t->id, (unsigned long long)key,
+             delta.empty() ? 0u : delta[0], (unsigned)delta.size(), (int)for_update, rc, pu, (int)ok);
         return ok;
     }
+
+    // TXN_OP_ABORT (testing_transaction_util.h:271-279): the aborting transaction takes a counter
+    // value as its commit id (GetNextCurrentTidCounter) before AbortTransaction
+    void abort_explicit(Txn *t) {
+        t->commit_id = counter_++;
+        emit("abort_id T%u cid=%u", t->id, t->commit_id);
+        abort(t);
+    }
+
+    // transactions outside the schedule that took counter values (begin / commit ids)
+    void tick(uint32_t n) { counter_ += n; }
 
     void begin_commit(Txn *t) {  // CommitTransaction up to SetCommitting (:550-564)
         t->commit_id = counter_++;

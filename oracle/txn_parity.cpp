@@ -11,8 +11,20 @@
 //   txn_parity oracle|device|both SEED [ROWS] [TXNS]
 //       oracle / device: one run, its trace on stdout; both: the two runs compared -- prints
 //       "MATCH" and the coverage summary (exit 0) or the first differing line (exit 1)
+//   txn_parity sched oracle|device|both < SCHEDULES
+//       the reference's TransactionScheduler tests (testing_transaction_util.h:142-440) whose ops
+//       are point reads, point updates, commits and aborts, run through the same manager: one
+//       "txn" line per transaction (txn_result and the read results) per schedule, for the test
+//       to hold against the reference's own assertions (tests/golden/make_scenarios.py); both =
+//       the two stores' traces must also be equal.  Input, one directive a line:
+//         schedule NAME | table new N | table same | tick N
+//         op TXN read KEY FU | op TXN update KEY VALUE FU | op TXN commit | op TXN abort | end
 #include <algorithm>
 #include <cstdio>
+#include <iostream>
+#include <map>
+#include <memory>
+#include <stdexcept>
 #include <cstdlib>
 #include <cstring>
 #include <random>
@@ -30,6 +42,19 @@ namespace {
 
 constexpr uint32_t kPayload = 1000, kDelta = 100, kKey = 8;
 
+// ParameterSet (b_tree.h:23-40): YCSB's (ycsb.cpp:72) and CreateTable's (testing_transaction_util.cpp:31)
+struct Geometry {
+    uint32_t split, merge, leaf, payload;
+};
+constexpr Geometry kYcsb{16 * 1024, 0, 64 * 1024, kPayload};
+constexpr Geometry kTestTable{64 * 1024, 32 * 1024, 64 * 1024, 8};
+
+inline uint64_t word_at(const uint8_t *p) {
+    uint64_t v;
+    std::memcpy(&v, p, 8);
+    return v;
+}
+
 #define CK(x)                                                                             \
     do {                                                                                  \
         int rc_ = (x);                                                                    \
@@ -42,17 +67,28 @@ constexpr uint32_t kPayload = 1000, kDelta = 100, kKey = 8;
 // ---- the oracle as the manager's store
 struct OracleStore {
     orc_tree *t = nullptr;
-    explicit OracleStore(uint64_t rows) {
-        t = orc_tree_new(64 * 1024, 16 * 1024, kPayload);
-        orc_load_ycsb(t, 0, rows, kKey, 0);
+    std::vector<uint8_t> rec;
+    explicit OracleStore(uint64_t rows) : OracleStore(kYcsb) { orc_load_ycsb(t, 0, rows, kKey, 0); }
+    explicit OracleStore(const Geometry &g) : rec(8 + g.payload) {
+        t = orc_tree_new(g.leaf, g.split, g.payload);
+        if (g.merge) orc_tree_set_merge_threshold(t, g.merge);
+    }
+    // TestingTransactionUtil::CreateTable: keys 0..n-1, value 0, one committed transaction
+    void create_table(uint32_t n, uint32_t cid) {
+        std::vector<uint8_t> pay(rec.size() - 8, 0);
+        for (uint64_t k = 0; k < n; ++k) orc_insert(t, (const uint8_t *)&k, kKey, pay.data(), cid);
     }
     ~OracleStore() { orc_tree_free(t); }
-    ssn::ReadFacts read(uint64_t key, uint32_t rid) {
+    ssn::ReadFacts read(uint64_t key, uint32_t rid, bool fu) {
         orc_read_out o;
+        if (fu) {  // the manager takes no record facts from a for-update read
+            orc_read_fu(t, (const uint8_t *)&key, kKey, rid, 1, &o, rec.data());
+            return ssn::ReadFacts{o.status, o.cstamp, 0, 0, 0, word_at(rec.data() + 8)};
+        }
         uint64_t m;
         uint32_t loc, nx;
-        orc_read_ident(t, (const uint8_t *)&key, kKey, rid, &o, nullptr, &m, &loc, &nx);
-        return ssn::ReadFacts{o.status, o.cstamp, m, loc, nx};
+        orc_read_ident(t, (const uint8_t *)&key, kKey, rid, &o, rec.data(), &m, &loc, &nx);
+        return ssn::ReadFacts{o.status, o.cstamp, m, loc, nx, word_at(rec.data() + 8)};
     }
     bool header(uint32_t id, ssn::Hdr &h) {
         uint32_t st[7];
@@ -67,9 +103,9 @@ struct OracleStore {
     int wr_count(uint32_t id, int d) { return orc_copy_wr_count(t, id, d) > 0 ? 1 : 0; }
     void update_ps(uint32_t id, uint32_t ps) { orc_copy_update_ps(t, id, ps); }
     void location(uint32_t loc, uint64_t &meta, uint32_t &next) { orc_location_meta(t, loc, &meta, &next); }
-    int update(uint64_t key, uint8_t byte, uint32_t writer, ssn::RecordMeta &upt) {
-        std::vector<uint8_t> d(kDelta, byte);
-        const int rc = orc_update(t, (const uint8_t *)&key, kKey, 0, d.data(), kDelta, writer);
+    int update(uint64_t key, const std::vector<uint8_t> &d, bool fu, uint32_t writer, ssn::RecordMeta &upt) {
+        if (fu) return orc_update_owned(t, (const uint8_t *)&key, kKey, 0, d.data(), (uint32_t)d.size(), writer);
+        const int rc = orc_update(t, (const uint8_t *)&key, kKey, 0, d.data(), (uint32_t)d.size(), writer);
         if (rc == 1) {
             uint32_t loc, nx;
             orc_record_meta(t, (const uint8_t *)&key, kKey, &upt.meta, &loc, &nx);
@@ -105,14 +141,27 @@ struct DeviceStore {
     stage_table *t = nullptr;
     stage_adapter::LocationTable *locs = nullptr;
     stage_adapter::OverwritePool *pool = nullptr;
-    void *dk = nullptr, *dr = nullptr, *dout = nullptr, *did = nullptr, *drow = nullptr;
+    void *dk = nullptr, *dr = nullptr, *dout = nullptr, *did = nullptr, *drow = nullptr, *dfu = nullptr;
     uint32_t stride = 0;
     std::vector<uint8_t> row;
-    explicit DeviceStore(uint64_t rows) {
-        stage_params p{16 * 1024, 32 * 1024, 64 * 1024, kPayload, kKey, 0};
-        CK(stage_table_create(&p, &t));
+    explicit DeviceStore(uint64_t rows) : DeviceStore(kYcsb) {
         uint64_t n = 0;
         CK(stage_load_ycsb(t, 0, rows, kKey, 0, &n));
+        ready();
+    }
+    explicit DeviceStore(const Geometry &g) {
+        stage_params p{g.split, g.merge ? g.merge : 32 * 1024, g.leaf, g.payload, kKey, 0};
+        CK(stage_table_create(&p, &t));
+    }
+    void create_table(uint32_t n, uint32_t cid) {
+        std::vector<uint8_t> pay(stage_record_stride(t), 0);
+        for (uint64_t k = 0; k < n; ++k) {
+            uint8_t rc;
+            CK(stage_insert(t, k, kKey, pay.data(), 0, 0, cid, &rc));
+        }
+        ready();
+    }
+    void ready() {  // after the load: location cells, the first publish, the adapter's views
         CK(stage_location_cells(t));
         CK(stage_sync(t));
         locs = new stage_adapter::LocationTable(t);
@@ -124,27 +173,33 @@ struct DeviceStore {
         CK(stage_dev_alloc(32, &dout));
         CK(stage_dev_alloc(8, &did));
         CK(stage_dev_alloc(stride, &drow));
+        CK(stage_dev_alloc(1, &dfu));
     }
     ~DeviceStore() {
-        for (void *p : {dk, dr, dout, did, drow}) stage_dev_free(p);
+        for (void *p : {dk, dr, dout, did, drow, dfu})
+            if (p) stage_dev_free(p);
         delete pool;
         delete locs;
         stage_table_destroy(t);
     }
-    ssn::ReadFacts read(uint64_t key, uint32_t rid) {
+    ssn::ReadFacts read(uint64_t key, uint32_t rid, bool fu) {
+        const uint8_t f = fu ? 1 : 0;
         CK(stage_memcpy_h2d(dk, &key, 8, nullptr));
         CK(stage_memcpy_h2d(dr, &rid, 4, nullptr));
-        CK(stage_probe_batch(t, (const uint64_t *)dk, nullptr, (const uint32_t *)dr, nullptr, 1, (stage_probe_out *)dout,
-                             (uint8_t *)drow, nullptr));
-        CK(stage_probe_identify(t, (const stage_probe_out *)dout, 1, (stage_probe_ident *)did, nullptr));
+        CK(stage_memcpy_h2d(dfu, &f, 1, nullptr));
+        CK(stage_probe_batch_ex(t, (const uint64_t *)dk, nullptr, (const uint32_t *)dr, nullptr, (const uint8_t *)dfu, 1,
+                                (stage_probe_out *)dout, (uint8_t *)drow, nullptr));
+        if (!fu) CK(stage_probe_identify(t, (const stage_probe_out *)dout, 1, (stage_probe_ident *)did, nullptr));
         CK(stage_device_sync());  // the probe ran on the table's stream, the copies use the null stream
         stage_probe_out o;
         stage_probe_ident id;
         CK(stage_memcpy_d2h(&o, dout, 32, nullptr));
-        CK(stage_memcpy_d2h(&id, did, 8, nullptr));
         CK(stage_memcpy_d2h(row.data(), drow, stride, nullptr));
         last = o;
-        if (o.status == STAGE_ST_NOT_FOUND) return ssn::ReadFacts{o.status, o.cstamp, 0, 0, 0};
+        const uint64_t value = word_at(row.data() + 8);
+        if (fu) return ssn::ReadFacts{o.status, o.cstamp, 0, 0, 0, value};
+        CK(stage_memcpy_d2h(&id, did, 8, nullptr));
+        if (o.status == STAGE_ST_NOT_FOUND) return ssn::ReadFacts{o.status, o.cstamp, 0, 0, 0, value};
         // the RecordMeta BTree::Read hands the executor, framed by the adapter; its loc_ptr is
         // the facade's RecordLocation, mapped back to the handle for the manager's rw-set key
         stage_adapter::RecordLocation *rl = locs->get(id.loc);
@@ -152,7 +207,7 @@ struct DeviceStore {
             stage_adapter::record_meta(o, id, reinterpret_cast<uint64_t>(rl), kPayload);
         const uint32_t loc = (uint32_t)stage_adapter::LocationTable::handle_of(
             reinterpret_cast<const stage_adapter::RecordLocation *>(rm.meta_data.loc_ptr));
-        return ssn::ReadFacts{o.status, rm.cstamp, rm.meta_data.meta, loc, (uint32_t)rm.meta_data.next_ptr};
+        return ssn::ReadFacts{o.status, rm.cstamp, rm.meta_data.meta, loc, (uint32_t)rm.meta_data.next_ptr, value};
     }
     bool header(uint32_t id, ssn::Hdr &h) {
         stage_adapter::OverwriteHeader oh;
@@ -175,10 +230,14 @@ struct DeviceStore {
         meta = m->meta;
         next = (uint32_t)m->next_ptr;
     }
-    int update(uint64_t key, uint8_t byte, uint32_t writer, ssn::RecordMeta &upt) {
-        std::vector<uint8_t> d(kDelta, byte);
+    int update(uint64_t key, const std::vector<uint8_t> &d, bool fu, uint32_t writer, ssn::RecordMeta &upt) {
         uint8_t rc = 0;
-        CK(stage_update_key(t, (const uint8_t *)&key, kKey, 0, d.data(), kDelta, writer, &rc));
+        if (fu) {
+            CK(stage_update_key_owned(t, (const uint8_t *)&key, kKey, 0, d.data(), (uint32_t)d.size(), writer, &rc));
+            CK(stage_sync(t));
+            return rc;
+        }
+        CK(stage_update_key(t, (const uint8_t *)&key, kKey, 0, d.data(), (uint32_t)d.size(), writer, &rc));
         if (rc == STAGE_RC_OK) {
             stage_probe_ident id;
             uint8_t r2;
@@ -299,9 +358,9 @@ Run run(Store &st, uint32_t seed, uint64_t rows, uint32_t ntx) {
             const uint64_t key = chance(0.75) ? uni(hot) : uni(rows + rows / 16);
             bool ok;
             if (chance(0.35)) {
-                ok = m.update(L.t, key, (uint8_t)uni(256));
+                ok = m.update(L.t, key, std::vector<uint8_t>(kDelta, (uint8_t)uni(256)));
             } else {
-                ok = m.read(L.t, key);
+                ok = m.read(L.t, key, false);
                 if (ok && !L.t->rw.empty()) {
                     const uint32_t loc = L.t->rw.back().rm.loc_ptr;
                     if (loc) L.reads.emplace_back(loc, st.where(loc));
@@ -365,9 +424,180 @@ void summary(const Run &r) {
         (unsigned long long)std::count(r.trace.begin(), r.trace.end(), '\n'));
 }
 
+// ---- the reference's TransactionScheduler tests (testing_transaction_util.h:142-440)
+struct SOp {
+    int txn;         // -1: a directive
+    std::string op;  // read / update / commit / abort; table-new / table-same / tick
+    uint64_t key = 0, value = 0;
+    bool fu = false;
+};
+struct Sched {
+    std::string name;
+    std::vector<SOp> ops;
+};
+
+std::vector<Sched> parse_schedules(std::istream &in) {
+    std::vector<Sched> out;
+    std::string line;
+    while (std::getline(in, line)) {
+        std::istringstream ls(line);
+        std::string w;
+        if (!(ls >> w) || w[0] == '#') continue;
+        if (w == "schedule") {
+            out.emplace_back();
+            ls >> out.back().name;
+            continue;
+        }
+        if (out.empty()) throw std::runtime_error("directive before 'schedule': " + line);
+        SOp o;
+        o.txn = -1;
+        if (w == "table") {
+            std::string kind;
+            ls >> kind;
+            o.op = "table-" + kind;
+            if (kind == "new") ls >> o.key;
+        } else if (w == "tick") {
+            o.op = "tick";
+            ls >> o.key;
+        } else if (w == "op") {
+            int fu = 0;
+            ls >> o.txn >> o.op;
+            if (o.op == "read") ls >> o.key >> fu;
+            else if (o.op == "update") ls >> o.key >> o.value >> fu;
+            else if (o.op != "commit" && o.op != "abort") throw std::runtime_error("unknown op: " + line);
+            o.fu = fu != 0;
+        } else if (w == "end") {
+            continue;
+        } else {
+            throw std::runtime_error("unknown directive: " + line);
+        }
+        out.back().ops.push_back(o);
+    }
+    return out;
+}
+
+// Runs every schedule in order; "table same" keeps the previous schedule's table and manager
+// (the reference's tests that run several TransactionSchedulers over one table and one
+// SSNTransactionManager).  The reference's driver runs one op at a time and waits for it; a
+// commit that would spin in FindMinSstamp / FindMaxPstamp on a transaction of the same schedule
+// is parked here and finished as soon as the state it waits for is reached (after the op that
+// reaches it), which is the outcome the tests' assertions describe.
+template <class Store>
+std::string run_schedules(const std::vector<Sched> &ss, std::string &trace) {
+    std::unique_ptr<Store> st;
+    std::unique_ptr<ssn::Manager<Store>> m;
+    std::ostringstream out;
+    std::string all;  // every manager's trace
+    for (const Sched &s : ss) {
+        struct TS {
+            ssn::Txn *t = nullptr;
+            const char *result = "FAILURE";  // TransactionSchedule's initial txn_result (:150)
+            std::vector<int64_t> results;
+            bool parked = false;
+        };
+        std::map<int, TS> ts;
+        std::vector<int> parked;
+        auto finish = [&](int i) {
+            ts[i].result = m->finish_commit(ts[i].t) == ssn::Result::SUCCESS ? "SUCCESS" : "FAILURE";
+            ts[i].parked = false;
+        };
+        auto resume = [&] {
+            for (bool moved = true; moved;) {
+                moved = false;
+                for (size_t k = 0; k < parked.size(); ++k)
+                    if (!m->would_block(ts[parked[k]].t)) {
+                        finish(parked[k]);
+                        parked.erase(parked.begin() + (long)k);
+                        moved = true;
+                        break;
+                    }
+            }
+        };
+        for (const SOp &o : s.ops) {
+            if (o.txn < 0) {
+                if (o.op == "table-new") {
+                    if (m) all += m->log;
+                    m.reset();
+                    st.reset(new Store(kTestTable));
+                    st->create_table((uint32_t)o.key, 2);  // CreateTable's transaction: read id 1, commit id 2
+                    m.reset(new ssn::Manager<Store>(*st, 3));
+                } else if (o.op == "table-same") {
+                    if (!m) throw std::runtime_error("table same without a table");
+                } else if (o.op == "tick") {
+                    m->tick((uint32_t)o.key);
+                }
+                continue;
+            }
+            TS &x = ts[o.txn];
+            if (!x.t) x.t = m->begin();                         // cur_seq == 0 (:213-219)
+            if (std::strcmp(x.result, "ABORTED") == 0) continue;  // (:221-224)
+            if (o.op == "read") {
+                int64_t v = -1;
+                const bool ok = m->read(x.t, o.key, o.fu, &v);
+                x.results.push_back(ok ? v : -2);  // -2: the executor failed (result unset)
+            } else if (o.op == "update") {
+                std::vector<uint8_t> d(8);
+                std::memcpy(d.data(), &o.value, 8);
+                m->update(x.t, o.key, d, o.fu);
+            } else if (o.op == "abort") {
+                m->abort_explicit(x.t);
+                x.result = "ABORTED";
+            } else {  // commit
+                m->begin_commit(x.t);
+                if (m->would_block(x.t)) {
+                    x.parked = true;
+                    parked.push_back(o.txn);
+                    m->log += "parked T" + std::to_string(x.t->id) + "\n";
+                } else {
+                    finish(o.txn);
+                }
+            }
+            // a failed executor: AbortTransaction, txn_result ABORTED (:302-308)
+            if ((o.op == "read" || o.op == "update") && x.t->result == ssn::Result::FAILURE) {
+                m->abort(x.t);
+                x.result = "ABORTED";
+            }
+            resume();
+        }
+        if (m) m->log += "end of " + s.name + "\n";
+        out << "schedule " << s.name << "\n";
+        for (auto &kv : ts) {
+            out << "txn " << kv.first << " result=" << (kv.second.parked ? "BLOCKED" : kv.second.result) << " results=";
+            for (size_t i = 0; i < kv.second.results.size(); ++i) out << (i ? "," : "") << kv.second.results[i];
+            out << "\n";
+        }
+    }
+    trace = all + (m ? m->log : std::string());
+    return out.str();
+}
+
+int sched_main(const std::string &mode) {
+    const std::vector<Sched> ss = parse_schedules(std::cin);
+    std::string ta, tb;
+    const std::string a = run_schedules<OracleStore>(ss, ta);
+    if (mode == "oracle" || mode == "oracle-trace") {
+        std::fputs(a.c_str(), stdout);
+        if (mode == "oracle-trace") std::fputs(ta.c_str(), stdout);
+        return 0;
+    }
+    const std::string b = run_schedules<DeviceStore>(ss, tb);
+    if (mode == "device") {
+        std::fputs(b.c_str(), stdout);
+        return 0;
+    }
+    if (a == b && ta == tb) {
+        std::printf("MATCH\n");
+        std::fputs(a.c_str(), stdout);
+        return 0;
+    }
+    std::printf("MISMATCH\n--- oracle\n%s%s--- device\n%s%s", a.c_str(), ta.c_str(), b.c_str(), tb.c_str());
+    return 1;
+}
+
 }  // namespace
 
 int main(int argc, char **argv) {
+    if (argc >= 3 && std::string(argv[1]) == "sched") return sched_main(argv[2]);
     if (argc < 3) {
         std::fprintf(stderr, "usage: %s oracle|device|both SEED [ROWS] [TXNS]\n", argv[0]);
         return 2;
