@@ -864,13 +864,19 @@ static void *hbuf(ShardComm &c, uint64_t bytes) {
 }
 
 // the IPC handles of every rank's two row buffers, exchanged over the communicator; the peers'
-// buffers opened here (own buffers used in place)
+// buffers opened here (own buffers used in place).  The ranks agree on the outcome (an allreduce
+// of an ok flag) before any of them goes on, so a runtime that refuses the mapping on one rank
+// makes the call fail on every rank, with nothing left mapped -- not a rank hanging in the
+// exchange that follows; the next peer call tries again.
 static void peer_exchange(ShardComm &c, hipStream_t s) {
     const int W = c.world;
     static_assert(sizeof(hipIpcMemHandle_t) == 64, "IPC handle size");
     std::vector<hipIpcMemHandle_t> mine(2), all((size_t)2 * W);
-    for (int k = 0; k < 2; ++k) chk(hipIpcGetMemHandle(&mine[k], c.prow[k]), "hipIpcGetMemHandle (peer rows)");
-    uint8_t *d = (uint8_t *)hbuf(c, (uint64_t)(W + 1) * 128);
+    std::memset(mine.data(), 0, 128);
+    hipError_t e = hipSuccess;
+    const char *what = "hipIpcGetMemHandle";
+    for (int k = 0; k < 2 && !e; ++k) e = hipIpcGetMemHandle(&mine[k], c.prow[k]);
+    uint8_t *d = (uint8_t *)hbuf(c, (uint64_t)(W + 1) * 128 + 8);
     chk(hipMemcpyAsync(d, mine.data(), 128, hipMemcpyHostToDevice, s), "handles h2d");
     nchk(ncclAllGather(d, d + 128, 128, ncclUint8, (ncclComm_t)c.comm, s), "ncclAllGather handles");
     chk(hipMemcpyAsync(all.data(), d + 128, (size_t)128 * W, hipMemcpyDeviceToHost, s), "handles d2h");
@@ -878,18 +884,35 @@ static void peer_exchange(ShardComm &c, hipStream_t s) {
     for (void *p : c.opened) (void)hipIpcCloseMemHandle(p);
     c.opened.clear();
     for (int k = 0; k < 2; ++k) c.peer_row[k].assign(W, nullptr);
-    for (int q = 0; q < W; ++q)
-        for (int k = 0; k < 2; ++k) {
+    if (!e) what = "hipIpcOpenMemHandle";
+    for (int q = 0; q < W && !e; ++q)
+        for (int k = 0; k < 2 && !e; ++k) {
             if (q == c.rank) {
                 c.peer_row[k][q] = c.prow[k];
                 continue;
             }
             void *p = nullptr;
-            chk(hipIpcOpenMemHandle(&p, all[(size_t)2 * q + k], hipIpcMemLazyEnablePeerAccess),
-                "hipIpcOpenMemHandle (peer rows)");
-            c.opened.push_back(p);
-            c.peer_row[k][q] = p;
+            e = hipIpcOpenMemHandle(&p, all[(size_t)2 * q + k], hipIpcMemLazyEnablePeerAccess);
+            if (!e) {
+                c.opened.push_back(p);
+                c.peer_row[k][q] = p;
+            }
         }
+    if (e) (void)hipGetLastError();  // the refusal is reported below, not by a later call
+    int32_t ok = e ? 0 : 1, all_ok = 0;
+    int32_t *dok = (int32_t *)(d + (uint64_t)(W + 1) * 128);
+    chk(hipMemcpyAsync(dok, &ok, 4, hipMemcpyHostToDevice, s), "ok h2d");
+    nchk(ncclAllReduce(dok, dok, 1, ncclInt32, ncclMin, (ncclComm_t)c.comm, s), "ncclAllReduce ok");
+    chk(hipMemcpyAsync(&all_ok, dok, 4, hipMemcpyDeviceToHost, s), "ok d2h");
+    chk(hipStreamSynchronize(s), "ok sync");
+    if (all_ok) return;
+    for (void *p : c.opened) (void)hipIpcCloseMemHandle(p);
+    c.opened.clear();
+    for (int k = 0; k < 2; ++k) c.peer_row[k].assign(W, nullptr);
+    c.peer_cap.clear();  // every rank: the next peer call plans and exchanges afresh
+    throw std::runtime_error(std::string("peer reply unavailable: ") +
+                             (e ? std::string(what) + " failed on this rank: " + hipGetErrorString(e)
+                                : std::string("another rank could not map the row buffers")));
 }
 
 // peer reply, chunk i: the status records that came back from every other rank, with each row read
