@@ -115,6 +115,10 @@ def parse(argv=None):
                         "epoch's read probe (stage_set_write_overlap; the epoch inputs are resident beforehand)")
     p.add_argument("--out-stride", type=int, default=0,
                    help="caller row stride in bytes (stage_set_output_layout; 0 = the 1008-B canonical row)")
+    p.add_argument("--reply", choices=["auto", "rows", "peer"], default="auto",
+                   help="N > 1: how remote rows reach the caller -- rows: back over RCCL; peer: read by the caller's "
+                        "fan-out from the owners' IPC-mapped row buffers (STAGE_REPLY_PEER); auto: peer, falling back "
+                        "to rows when the runtime refuses the mapping (same results either way)")
     p.add_argument("--force-sharded", action="store_true",
                    help="run the multi-GPU (RCCL) code path even with one rank -- a rehearsal, not a config")
     p.add_argument("--dry-run", action="store_true",
@@ -422,9 +426,29 @@ def run_sharded(args, rank, world, local):
     d_out = stage.DeviceBuffer(B * 32)
     d_rec = stage.DeviceBuffer(B * tab.stride)
 
-    def step(reply=stage.REPLY_ROWS):
-        check(L.stage_probe_sharded_ex(tab.h, d_keys.ptr, None, B, d_out.ptr,
-                                       d_rec.ptr if reply == stage.REPLY_ROWS else None, reply, stream.ptr), "sharded")
+    def call(reply):
+        return L.stage_probe_sharded_ex(tab.h, d_keys.ptr, None, B, d_out.ptr,
+                                        None if reply == stage.REPLY_OWNER else d_rec.ptr, reply, stream.ptr)
+
+    # the reply mode of the headline: peer (rows read in place from the owners' exported buffers)
+    # unless refused; the library makes every rank agree on a refusal, so all ranks fall back
+    # together at the same call
+    reply_mode = {"rows": stage.REPLY_ROWS, "peer": stage.REPLY_PEER}.get(
+        args.reply, stage.REPLY_PEER if world > 1 else stage.REPLY_ROWS)
+    reply_note = None
+    if reply_mode == stage.REPLY_PEER:
+        rc = call(reply_mode)
+        if rc != 0:
+            err = L.stage_last_error().decode(errors="replace")
+            if args.reply == "peer":
+                raise SystemExit(f"[rank {rank}] peer reply: {err}")
+            reply_note = f"peer reply refused, rows over RCCL instead: {err}"
+            log(f"[rank {rank}] {reply_note}")
+            reply_mode = stage.REPLY_ROWS
+        stream.sync()
+
+    def step(reply=None):
+        check(call(reply_mode if reply is None else reply), "sharded")
 
     for _ in range(args.warmup):
         step()
@@ -457,6 +481,20 @@ def run_sharded(args, rank, world, local):
     t_own = ctl.max(time.perf_counter() - t0)
     owner = {"value": round(B * args.steps * world / t_own, 1), "ms_per_step": round(t_own / args.steps * 1e3, 4),
              "reply": "32-B status records to the caller, tuple rows materialised on the owner"}
+    rows_mode = None
+    if reply_mode == stage.REPLY_PEER:  # the same steps with the rows back over RCCL, for comparison
+        for _ in range(max(1, args.warmup)):
+            step(stage.REPLY_ROWS)
+        stream.sync()
+        ctl.barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step(stage.REPLY_ROWS)
+        stream.sync()
+        t_rows = ctl.max(time.perf_counter() - t0)
+        rows_mode = {"value": round(B * args.steps * world / t_rows, 1),
+                     "ms_per_step": round(t_rows / args.steps * 1e3, 4),
+                     "reply": "status records and rows back over RCCL, fanned out from the receive buffer"}
     direct = None
     if world == 1:  # the one-rank rehearsal against the direct probe of the same batch on the same table
         for _ in range(max(1, args.warmup)):
@@ -499,7 +537,7 @@ def run_sharded(args, rank, world, local):
     step_s = elapsed / args.steps
     # HBM roofline of the step: the bytes that move on each rank (owners' probes, caller rows,
     # result copies), the busiest rank over the step time
-    hb = [sharded_hbm_bytes(sx, tab.stride) for sx in stats]
+    hb = [sharded_hbm_bytes(sx, tab.stride, peer=reply_mode == stage.REPLY_PEER) for sx in stats]
     hmax = max(b for b, _ in hb)
     hbm = {"bound": "hbm", "achieved": round(hmax / step_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(hmax / step_s / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
@@ -526,6 +564,9 @@ def run_sharded(args, rank, world, local):
                    "exchange_chunks": int(os.environ.get("STAGE_SHARD_CHUNKS", 4 if world > 1 else 1)),
                    "control_plane": "the RCCL communicator (file rendezvous of the unique id)"},
         "roofline": roof, "cpu_baseline": cpu, "self_check": all(p["self_check"] for p in per_rank),
+        "reply": {stage.REPLY_PEER: "peer", stage.REPLY_ROWS: "rows"}[reply_mode],
+        **({"reply_note": reply_note} if reply_note else {}),
+        **({"rows_reply": rows_mode} if rows_mode else {}),
         "owner_reply": owner,
         **({"world1_vs_direct": {"sharded_ms_per_step": round(step_s * 1e3, 4), "owner_reply_ms_per_step":
                                  owner["ms_per_step"], "direct_probe_ms_per_step": direct,
@@ -654,7 +695,7 @@ def sharded_workload(world, rows_per_gpu, shared=False):
     return s
 
 
-def sharded_hbm_bytes(st, stride, row_bytes=1008):
+def sharded_hbm_bytes(st, stride, row_bytes=1008, peer=False):
     """Algorithmic HBM bytes of one sharded step on one rank, counting what actually moves
     (stage_sharded_stats_ex after the step: n caller keys, `routed` requests after coalescing,
     `remote` of them owned by other ranks, `received` requests this rank probed as owner):
@@ -663,13 +704,17 @@ def sharded_hbm_bytes(st, stride, row_bytes=1008):
       remote results    (received - own) x 2 x (row_bytes + 4): written for the return, read by RCCL
       returned results  remote x 2 x (row_bytes + 4): written by RCCL, read by the fan-out
       key records       (remote + received - own) x 2 x 16: sent (read) and received (written)
+    Peer reply (STAGE_REPLY_PEER): the remote results are written once into this rank's exported
+    row buffer and read once by the requesting rank's fan-out (from this rank's HBM, over the
+    fabric) -- the same 2 x per row here; the returned results are only status records
+    (remote x 2 x 32), their rows are read from the owners' HBM.
     The coalescing sorts and the routing's own scratch traffic are not counted (not algorithmic)."""
     n, routed, remote, received = st["keys"], st["routed"], st["remote"], st["received"]
     own = routed - remote
     recv_remote = received - own
     out = row_bytes + 4
     parts = {"owner_probes": received * (8 + 64 + 16 + 1000), "caller_rows": n * out,
-             "remote_results": recv_remote * 2 * out, "returned_results": remote * 2 * out,
+             "remote_results": recv_remote * 2 * out, "returned_results": remote * 2 * (32 if peer else out),
              "key_records": (remote + recv_remote) * 32}
     return sum(parts.values()), parts
 
