@@ -4,8 +4,8 @@ count exchange, chunked key / result exchange, the owners' fan-out probes, the f
 returned rows) run by stage_probe_sharded_loopback over W = 8 shard tables of 12.5M rows each
 (100M rows in all, the keys each rank of C5 owns), fed a 2^24-key Zipf-0.9 batch (2^21 keys per
 rank, drawn over all 100M keys as C5's ranks draw them), must return byte for byte what ONE
-100M-row table returns for the same keys -- in both reply modes (rows back to the caller /
-rows left at the owner), coalescing on.  The direct probe's results are taken first and the
+100M-row table returns for the same keys -- in the three reply modes (rows back to the caller,
+rows read by the caller from the owners' row buffers, rows left at the owner), coalescing on.  The direct probe's results are taken first and the
 100M-row table is released before the shards are built (both at once would not leave room for
 the exchange buffers in 288 GB).  Reference semantics: executor.h:374-454 (IndexScanExecutor
 point lookup) through BTree::Read (b_tree.cpp:2066-2129) on every shard."""
@@ -79,6 +79,16 @@ def test_c5_loopback_at_size_equals_one_table(gpu):
         assert nk == per_keys[r].size and remote < rt < 0.8 * nk  # Zipf duplicates coalesced
         routed += rt
     assert (np.concatenate([o["status"] for o, _ in res]) == stage.ST_LATEST).sum() == W * (PER_RANK - 64)
+    del res
+    # 3b. peer reply: status records back, rows read from the owners' row buffers (STAGE_REPLY_PEER)
+    res = stage.probe_sharded_loopback(tabs, per_keys, None, reply=stage.REPLY_PEER)
+    _say(t0, "sharded probe, peer mode")
+    for r in range(W):
+        out, rows = res[r]
+        ref_out, ref_rows = ref[r]
+        for f in fields:
+            assert (out[f] == ref_out[f]).all(), (r, f)
+        assert (rows == ref_rows).all(), r
     del res
     # 4. rows left at their owners, status records back (each carries the owner-local row index)
     res = stage.probe_sharded_loopback(tabs, per_keys, None, records=True, reply=stage.REPLY_OWNER)
