@@ -67,6 +67,8 @@ def test_sharded_data_path_loopback_equals_single_table(gpu, world, chunks, dedu
     tabs, h = shard_tables(keys, world)
     full = stage.Table(key_width=8)
     full.load_keys(keys, 8, mode=1)
+    orc = O.OracleTree(payload_size=1000)  # the same table in the oracle: a direct pin
+    orc.load_ycsb_bulk(0, n, 8, 1)
     rng = np.random.default_rng(world)
     hot = rng.choice(n, 3000, replace=False).astype(np.uint64)
     for k in hot:
@@ -74,6 +76,8 @@ def test_sharded_data_path_loopback_equals_single_table(gpu, world, chunks, dedu
         for t in (owner, full):
             assert t.update(int(k), 16, b"\x42" * 32, 10) == stage.RC_OK
             assert t.commit_update(int(k), 11, 11) == stage.RC_OK
+        assert orc.update(int(k), 8, 16, b"\x42" * 32, 10) == stage.RC_OK
+        assert orc.commit_update(int(k), 8, 11, 11) == stage.RC_OK
     for t in tabs + [full]:
         t.sync()
     for t in tabs:
@@ -96,6 +100,10 @@ def test_sharded_data_path_loopback_equals_single_table(gpu, world, chunks, dedu
         for f in ("status", "flags", "hops", "key_len", "cstamp", "rec_cstamp", "copy_sstamp"):
             assert (out[f] == ref_out[f]).all(), (world, r, f)
         assert (rows == ref_rows).all(), (world, r)
+        for i in rng.choice(per_keys[r].size, min(400, per_keys[r].size), replace=False):  # and the oracle's
+            o, rec = orc.read(int(per_keys[r][i]), 8, int(per_rids[r][i]))
+            assert (out["status"][i], out["cstamp"][i]) == (o["status"], o["cstamp"]), (world, r, i)
+            assert (rows[i, :orc.row] == rec).all(), (world, r, i)
     # and a second round reuses the grown scratch buffers, without rows
     res2 = stage.probe_sharded_loopback(tabs, per_keys, None, records=False)
     for r in range(world):
