@@ -56,13 +56,14 @@ __device__ __forceinline__ int32_t ld_i32(const uint8_t *p) {
 __global__ void q2_set_u64(uint64_t *p, uint64_t v) { *p = v; }
 
 // blocks copy the visited suppliers' map entries (2 words each) to their segments; counts[0] =
-// the number of visited suppliers (q2_select)
+// the number of visited suppliers (q2_select); nothing is written past m_cap keys (the host
+// rejects counts above it after the batch)
 __global__ void q2_gather(const uint64_t *__restrict__ map_keys, const uint64_t *__restrict__ src,
                           const uint64_t *__restrict__ dst, const uint32_t *__restrict__ cnt,
-                          const uint64_t *__restrict__ counts, uint64_t *__restrict__ keys) {
+                          const uint64_t *__restrict__ counts, uint64_t m_cap, uint64_t *__restrict__ keys) {
     const uint64_t n = counts[0];
     for (uint64_t s = blockIdx.x; s < n; s += gridDim.x)
-        for (uint32_t e = threadIdx.x; e < cnt[s]; e += blockDim.x) {
+        for (uint32_t e = threadIdx.x; e < cnt[s] && dst[s] + e < m_cap; e += blockDim.x) {
             keys[2 * (dst[s] + e)] = map_keys[2 * (src[s] + e)];
             keys[2 * (dst[s] + e) + 1] = map_keys[2 * (src[s] + e) + 1];
         }
@@ -386,7 +387,8 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
                        o_keys = take(std::max<uint64_t>(m_max, 1) * 16), o_sbase = take(std::max<uint64_t>(m_max, 1) * 32),
                        o_slast = take(n_max * 32 * nq), o_ik = take(n_max * 8 * nq), o_iout = take(n_max * 32 * nq),
                        o_ibase = take(n_max * 32), o_rec = take(n_max * nq * sizeof(stage_q2_rec));
-        uint8_t *buf = scratch_bytes(nation->dev, off), *mir = buf + o_mir;
+        // the SUPPLIER table's scratch: REGION's and NATION's hold their scan rows (scan_rows)
+        uint8_t *buf = scratch_bytes(supplier->dev, off), *mir = buf + o_mir;
         auto *d_map = (const uint32_t *)(mir + q_map);
         auto *d_rq = (const uint32_t *)(mir + q_rq);
         auto *d_counts = (uint64_t *)(mir + q_cn);
@@ -429,7 +431,7 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         lap("selection enqueued");
         // 3. every visited supplier's STOCK keys, one probe of them all (the counts on the device)
         q2_gather<<<(unsigned)std::max<uint64_t>(std::min<uint64_t>(n_hint, 4096), 1), 256, 0, s>>>(
-            d_map_keys, d_src, d_dst, d_cnt, d_counts, d_keys);
+            d_map_keys, d_src, d_dst, d_cnt, d_counts, m_max, d_keys);
         // every query of the batch looks up the same STOCK keys (the visited suppliers and their
         // supp_stock_map do not depend on the read id): each key is probed once, with no read id
         // (the hit slot does not depend on it), and its visibility evaluated at every query's read
