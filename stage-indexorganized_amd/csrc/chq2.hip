@@ -457,14 +457,12 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         // `out` in page-locked memory (stage_host_alloc, stage.pinned_empty): the finishing kernel
         // writes the records into it directly; otherwise they are copied once the count is known
         stage_q2_rec *host_out = nullptr;
-        if (out && max_out) {
-            hipPointerAttribute_t pa;
+        if (out && max_out) {  // page-locked memory has a device view; pageable memory has none
             void *dp = nullptr;
-            if (hipPointerGetAttributes(&pa, out) == hipSuccess && pa.type == hipMemoryTypeHost &&
-                hipHostGetDevicePointer(&dp, out, 0) == hipSuccess)
-                host_out = (stage_q2_rec *)dp;
+            if (hipHostGetDevicePointer(&dp, out, 0) == hipSuccess && dp) host_out = (stage_q2_rec *)dp;
             (void)hipGetLastError();  // a pageable pointer is not an error here
         }
+        if (trace) std::fprintf(stderr, "[q2] out %s\n", host_out ? "page-locked: written by q2_finish" : "pageable: copied");
         q2_finish<<<(unsigned)((n_max * nq + 255) / 256), 256, 0, s>>>(d_iout, iv.heap, iv.hstride, facts(item).key_pad(),
                                                                        d_counts, nq, d_rec, d_ab, host_out, max_out);
         hip_check(hipGetLastError(), "q2 kernels");
