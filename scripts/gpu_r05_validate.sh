@@ -14,3 +14,5 @@ timeout -k 10 120 python -u bench.py --config chq2 --steps 300 > $out/bench_chq2
 STAGE_Q2_TRACE=1 timeout -k 10 120 python -u bench.py --config chq2 --steps 50 > $out/trace.log 2>&1
 STAGE_RANKS_SHARE_GPU=1 timeout -k 10 300 python -u bench.py --gpus 2 --rows 20000000 --steps 5 --warmup 2 \
     --no-cpu-baseline > $out/bench_g2.log 2>&1
+STAGE_Q2_TRACE=1 timeout -k 10 120 python -u bench.py --config chq2 --steps 20 > $out/trace2.log 2>&1
+bash scripts/profile_r05.sh q2_trace > $out/prof_q2.log 2>&1

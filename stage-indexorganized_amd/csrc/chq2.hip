@@ -75,31 +75,39 @@ __global__ void q2_gather(const uint64_t *__restrict__ map_keys, const uint64_t 
 //              (scan order); a nation is visited at most once (it has one region key, region
 //              keys are unique), so at most kNationScan visits, found through an LDS hash;
 //   sel      = every SUPPLIER record of each visited nation, visit by visit, in ScanLeafNode
-//              (slot dump) order: a stable counting sort by visit -- each wave counts its
-//              contiguous share of the slots per visit (one ballot per distinct visit of a
-//              64-slot chunk), one prefix over (visit, wave), then each wave places its records;
+//              (slot dump) order: a stable counting sort by visit.  The slots go through LDS in
+//              windows of kSelWin; in each, every lane finds its slots' visits (independent
+//              loads), then wave w ranks the window's w-th 1024 slots per visit (one ballot per
+//              distinct visit of a 64-slot chunk, LDS only) -- the visit and rank of every slot go
+//              to global scratch; one prefix over (visit, window, wave) gives each group's start,
+//              and a parallel pass places every selected supplier at start + rank;
 //   segments = src / cnt of each selected supplier's supp_stock_map entries (map_off, keys
 //              below 10000), dst = their exclusive prefix sum;
 //   counts   = {suppliers, stock keys}.
+// No loop of this kernel waits on a global load per iteration: the loads are issued side by side.
 constexpr int kVisits = kNationScan, kVisitHash = 256;
+constexpr uint32_t kSelWin = 16384, kSelMaxWin = 8;  // slots per LDS window, windows per call
 __global__ __launch_bounds__(1024) void q2_select(const uint8_t *__restrict__ regs, uint32_t rs,
                                                   const uint8_t *__restrict__ nats, uint32_t ns, uint64_t name0,
                                                   uint64_t name1, const uint64_t *__restrict__ pairs, uint64_t nslots,
-                                                  const uint32_t *__restrict__ map_off, uint64_t *__restrict__ sel,
+                                                  const uint32_t *__restrict__ map_off, int8_t *__restrict__ g_vis,
+                                                  uint16_t *__restrict__ g_rank, uint64_t *__restrict__ sel,
                                                   uint64_t *__restrict__ src, uint32_t *__restrict__ cnt,
                                                   uint64_t *__restrict__ dst, uint64_t *__restrict__ counts) {
     __shared__ uint8_t s_rmatch[kRegionScan];
     __shared__ uint8_t s_flag[kRegionScan * kNationScan];
-    __shared__ int64_t s_visit[kVisits];
     __shared__ uint32_t s_nvisit;
     __shared__ int64_t s_hkey[kVisitHash];
     __shared__ int32_t s_hval[kVisitHash];
-    __shared__ uint32_t s_cnt[16][kVisits];
+    __shared__ int8_t s_vis[kSelWin];
+    __shared__ uint32_t s_grp[kSelMaxWin * 16][kVisits];  // per (window, wave): counts, then starts
+    __shared__ uint32_t s_vstart[kVisits];
     __shared__ uint64_t s_wsum[16];
     __shared__ uint64_t s_n;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t nreg = *reinterpret_cast<const uint32_t *>(regs - 8);
     const uint32_t nnat = *reinterpret_cast<const uint32_t *>(nats - 8);
+    const uint32_t nwin = (uint32_t)((nslots + kSelWin - 1) / kSelWin);  // <= kSelMaxWin (host check)
     // 1. the visits
     if (tid < kRegionScan && tid < nreg) {  // R_NAME (55 bytes, NUL-terminated) == regions[target]
         const uint8_t *name = regs + (uint64_t)tid * rs + 8;
@@ -116,8 +124,7 @@ __global__ __launch_bounds__(1024) void q2_select(const uint8_t *__restrict__ re
         s_rmatch[tid] = eq;
     }
     for (uint32_t i = tid; i < kVisitHash; i += blockDim.x) s_hkey[i] = INT64_MIN, s_hval[i] = -1;
-    for (uint32_t w = 0; w < kVisits; ++w)
-        if (tid < 16) s_cnt[tid][w] = 0;
+    for (uint32_t i = tid; i < kSelMaxWin * 16 * kVisits; i += blockDim.x) (&s_grp[0][0])[i] = 0;
     __syncthreads();
     if (tid < nreg * nnat && tid < kRegionScan * kNationScan) {
         const uint32_t r = tid / nnat, a = tid % nnat;
@@ -134,8 +141,7 @@ __global__ __launch_bounds__(1024) void q2_select(const uint8_t *__restrict__ re
                 while (s_hkey[h] != INT64_MIN && s_hkey[h] != nk) h = (h + 1) & (kVisitHash - 1);
                 if (s_hkey[h] == nk) continue;  // (cannot happen: one region per nation)
                 s_hkey[h] = nk;
-                s_hval[h] = (int32_t)nv;
-                s_visit[nv++] = nk;
+                s_hval[h] = (int32_t)nv++;
             }
         s_nvisit = nv;
     }
@@ -150,65 +156,90 @@ __global__ __launch_bounds__(1024) void q2_select(const uint8_t *__restrict__ re
         }
         return -1;
     };
-    // 2. counting pass: wave w owns slots [w * per, (w + 1) * per)
-    const uint64_t per = ((nslots + 16 * 64 - 1) / (16 * 64)) * 64;
-    const uint64_t lo = wv * per, hi = lo + per < nslots ? lo + per : nslots;
-    for (uint64_t c0 = lo; c0 < hi; c0 += 64) {
-        const uint64_t i = c0 + lane;
-        const int v = i < hi ? visit_of(pairs[2 * i], pairs[2 * i + 1]) : -1;
-        uint64_t todo = ballot(v >= 0);
-        while (todo) {
-            const int vl = (int)rl32((uint32_t)v, (int)__builtin_ctzll(todo));
-            const uint64_t mm = ballot(v == vl);
-            if (lane == 0) s_cnt[wv][vl] += (uint32_t)__builtin_popcountll(mm);
-            todo &= ~mm;
+    // 2. per window: visits of its slots (A), per-wave counts and ranks (B)
+    for (uint32_t win = 0; win < nwin; ++win) {
+        const uint64_t w0 = (uint64_t)win * kSelWin;
+#pragma unroll 4
+        for (uint32_t j = tid; j < kSelWin; j += 1024) {
+            const uint64_t i = w0 + j;
+            int v = -1;
+            if (i < nslots) v = visit_of(pairs[2 * i], pairs[2 * i + 1]);
+            s_vis[j] = (int8_t)v;
         }
+        __syncthreads();
+        uint32_t *gc = s_grp[win * 16 + wv];
+        for (uint32_t c0 = wv * 1024; c0 < (wv + 1) * 1024; c0 += 64) {
+            const uint32_t j = c0 + lane;
+            const int v = s_vis[j];
+            uint32_t rank = 0;
+            uint64_t todo = ballot(v >= 0);
+            while (todo) {
+                const int vl = (int)rl32((uint32_t)v, (int)__builtin_ctzll(todo));
+                const uint64_t mm = ballot(v == vl);
+                const uint32_t before = gc[vl];
+                if (v == vl) rank = before + (uint32_t)__builtin_popcountll(mm & ((1ull << lane) - 1));
+                if (lane == 0) gc[vl] = before + (uint32_t)__builtin_popcountll(mm);
+                todo &= ~mm;
+            }
+            const uint64_t i = w0 + j;
+            if (i < nslots) {
+                g_vis[i] = (int8_t)v;
+                g_rank[i] = (uint16_t)rank;
+            }
+        }
+        __syncthreads();
+    }
+    // 3. group starts, visit-major, then window, then wave (slot order within a visit)
+    const uint32_t ngrp = nwin * 16;
+    if (tid < nv) {
+        uint32_t t = 0;
+        for (uint32_t g = 0; g < ngrp; ++g) t += s_grp[g][tid];
+        s_vstart[tid] = t;
     }
     __syncthreads();
-    if (tid == 0) {  // placement starts: visit-major, then wave (slot order)
+    if (tid == 0) {
         uint32_t pos = 0;
-        for (uint32_t v = 0; v < nv; ++v)
-            for (uint32_t w = 0; w < 16; ++w) {
-                const uint32_t c = s_cnt[w][v];
-                s_cnt[w][v] = pos;
-                pos += c;
-            }
+        for (uint32_t v = 0; v < nv; ++v) {
+            const uint32_t t = s_vstart[v];
+            s_vstart[v] = pos;
+            pos += t;
+        }
         counts[0] = pos;
         s_n = pos;
     }
     __syncthreads();
-    // 3. placement pass
-    for (uint64_t c0 = lo; c0 < hi; c0 += 64) {
-        const uint64_t i = c0 + lane;
-        const uint64_t key = i < hi ? pairs[2 * i] : ~0ull;
-        const int v = i < hi ? visit_of(key, pairs[2 * i + 1]) : -1;
-        uint64_t todo = ballot(v >= 0);
-        while (todo) {
-            const int vl = (int)rl32((uint32_t)v, (int)__builtin_ctzll(todo));
-            const uint64_t mm = ballot(v == vl);
-            const uint32_t base = s_cnt[wv][vl];
-            if (v == vl) sel[base + (uint32_t)__builtin_popcountll(mm & ((1ull << lane) - 1))] = key;
-            if (lane == 0) s_cnt[wv][vl] = base + (uint32_t)__builtin_popcountll(mm);
-            todo &= ~mm;
+    if (tid < nv) {
+        uint32_t pos = s_vstart[tid];
+        for (uint32_t g = 0; g < ngrp; ++g) {
+            const uint32_t c = s_grp[g][tid];
+            s_grp[g][tid] = pos;
+            pos += c;
         }
     }
     __syncthreads();
-    // 4. map segments: src / cnt per selected supplier, dst = exclusive prefix of cnt
+    // 4. placement and map segments, every slot independent
+#pragma unroll 4
+    for (uint64_t i = tid; i < nslots; i += 1024) {
+        const int v = g_vis[i];
+        if (v < 0) continue;
+        const uint32_t pos = s_grp[(uint32_t)(i / kSelWin) * 16 + (uint32_t)((i % kSelWin) >> 10)][v] + g_rank[i];
+        const uint64_t sk = pairs[2 * i];
+        uint64_t s0 = 0, c = 0;
+        if (sk < 10000) {
+            s0 = map_off[sk];
+            c = map_off[sk + 1] > map_off[sk] ? map_off[sk + 1] - map_off[sk] : 0;
+        }
+        sel[pos] = sk;
+        src[pos] = s0;
+        cnt[pos] = (uint32_t)c;
+    }
+    __syncthreads();
+    // 5. dst = exclusive prefix of cnt in selection order
     const uint64_t n = s_n;
     uint64_t carry = 0;
     for (uint64_t b = 0; b < n; b += blockDim.x) {
         const uint64_t i = b + tid;
-        uint64_t c = 0;
-        if (i < n) {
-            const uint64_t sk = sel[i];
-            uint64_t s0 = 0;
-            if (sk < 10000) {
-                s0 = map_off[sk];
-                c = map_off[sk + 1] > map_off[sk] ? map_off[sk + 1] - map_off[sk] : 0;
-            }
-            src[i] = s0;
-            cnt[i] = (uint32_t)c;
-        }
+        const uint64_t c = i < n ? cnt[i] : 0;
         uint64_t x = c;  // inclusive scan in the wave, then across the 16 waves
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -277,9 +308,20 @@ __global__ void q2_finish(const stage_probe_out_dev *__restrict__ iout, const ui
     if (!produced(st)) {
         atomicOr(abort_flag + s / n, 1);
     } else {
-        const uint8_t *d = iheap + (uint64_t)iout[s].w[6] * ihstride + ikpad + kIDataOff;
+        // I_DATA's 64 bytes in 16 word loads issued together (4-B aligned), scanned in registers
+        const uint32_t *d = reinterpret_cast<const uint32_t *>(iheap + (uint64_t)iout[s].w[6] * ihstride + ikpad +
+                                                               kIDataOff);
+        uint32_t w[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) w[k] = d[k];
         uint8_t has_b = 0;
-        for (int c = 0; c < 64 && d[c]; ++c) has_b |= d[c] == 'b';
+        bool end = false;
+#pragma unroll
+        for (int c = 0; c < 64; ++c) {
+            const uint8_t ch = (uint8_t)(w[c >> 2] >> (8 * (c & 3)));
+            end |= ch == 0;
+            has_b |= !end && ch == 'b';
+        }
         r.item_has_b = has_b;
         r.update = !has_b && r.s_quantity < 10;
         out[s] = r;
@@ -359,6 +401,8 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         for (uint32_t q = 0; q < nq; ++q) aborted[q] = 0;
         const DevTable &pv = supplier->dev.view, &sv = stock->dev.view, &iv = item->dev.view;
         const uint64_t nslots = (uint64_t)pv.nleaves * pv.cap;
+        if (nslots > (uint64_t)kSelWin * kSelMaxWin)
+            return fail(STAGE_E_UNSUPPORTED, "SUPPLIER has more slots than q2_select's windows hold (131072)");
         // upper bounds (buffer sizes, grids): every SUPPLIER slot visited, every map entry looked up
         constexpr uint32_t kMapKeys = 10000;
         uint64_t m_max = 0;
@@ -386,7 +430,8 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
                        o_src = take(n_max * 8), o_cnt = take(n_max * 4), o_dst = take(n_max * 8),
                        o_keys = take(std::max<uint64_t>(m_max, 1) * 16), o_sbase = take(std::max<uint64_t>(m_max, 1) * 32),
                        o_slast = take(n_max * 32 * nq), o_ik = take(n_max * 8 * nq), o_iout = take(n_max * 32 * nq),
-                       o_ibase = take(n_max * 32), o_rec = take(n_max * nq * sizeof(stage_q2_rec));
+                       o_ibase = take(n_max * 32), o_rec = take(n_max * nq * sizeof(stage_q2_rec)),
+                       o_vis = take(n_max), o_rank = take(n_max * 2);
         // the SUPPLIER table's scratch: REGION's and NATION's hold their scan rows (scan_rows)
         uint8_t *buf = scratch_bytes(supplier->dev, off), *mir = buf + o_mir;
         auto *d_map = (const uint32_t *)(mir + q_map);
@@ -426,7 +471,8 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         std::memcpy(&name0, tname, 8);
         std::memcpy(&name1, tname + 8, 8);
         q2_select<<<1, 1024, 0, s>>>(regs, region->dev.view.stride, nats, nation->dev.view.stride, name0, name1, d_pairs,
-                                     nslots, d_map, d_sel, d_src, d_cnt, d_dst, d_counts);
+                                     nslots, d_map, (int8_t *)(buf + o_vis), (uint16_t *)(buf + o_rank), d_sel, d_src,
+                                     d_cnt, d_dst, d_counts);
         hip_check(hipGetLastError(), "select");
         lap("selection enqueued");
         // 3. every visited supplier's STOCK keys, one probe of them all (the counts on the device)
@@ -457,7 +503,11 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         // `out` in page-locked memory (stage_host_alloc, stage.pinned_empty): the finishing kernel
         // writes the records into it directly; otherwise they are copied once the count is known
         stage_q2_rec *host_out = nullptr;
-        if (out && max_out) {  // page-locked memory has a device view; pageable memory has none
+        static const bool copy_out = [] {
+            const char *e = std::getenv("STAGE_Q2_OUT");  // "copy": records copied after the batch (A/B)
+            return e && std::strcmp(e, "copy") == 0;
+        }();
+        if (out && max_out && !copy_out) {  // page-locked memory has a device view; pageable memory has none
             void *dp = nullptr;
             if (hipHostGetDevicePointer(&dp, out, 0) == hipSuccess && dp) host_out = (stage_q2_rec *)dp;
             (void)hipGetLastError();  // a pageable pointer is not an error here

@@ -352,7 +352,8 @@ extern "C" {
 
 int stage_host_alloc(uint64_t bytes, void **ptr) {
     if (!ptr) return fail(STAGE_E_ARG, "null pointer");
-    return hip_rc(hipHostMalloc(ptr, bytes ? bytes : 16, hipHostMallocDefault), "hipHostMalloc");
+    // mapped: kernels may write results straight into it (stage_ch_query2_batch's `out`)
+    return hip_rc(hipHostMalloc(ptr, bytes ? bytes : 16, hipHostMallocMapped), "hipHostMalloc");
 }
 
 int stage_host_free(void *ptr) { return hip_rc(hipHostFree(ptr), "hipHostFree"); }
