@@ -12,9 +12,9 @@
 //      the supplier (:890-892); otherwise S_QUANTITY < 10 updates S_QUANTITY..S_REMOTE_CNT to
 //      (q + 50, ytd, order_cnt, remote_cnt) (:893-950), committed with the transaction.
 //
-// Here REGION / NATION run as device scans and SUPPLIER as a one-lane-per-slot leaf dump; one
-// workgroup (q2_select) filters them -- the region named regions[target], its nations, their
-// suppliers in visiting order -- and lays out each visited supplier's supp_stock_map segment; the
+// Here REGION / NATION run as device scans; four short kernels (q2_sel_*) read the SUPPLIER leaves
+// slot by slot and select -- the region named regions[target], its nations, their suppliers in
+// visiting order -- and lay out each visited supplier's supp_stock_map segment; the
 // hot part -- every visited supplier's stock lookups (W * I / 10^4 each, ~2600 suppliers for
 // EUROPE) and the item lookups -- is one gather kernel, one probe launch over all stock keys,
 // their visibility folded at every read id of the batch (aborts and each supplier's last
@@ -56,7 +56,7 @@ __device__ __forceinline__ int32_t ld_i32(const uint8_t *p) {
 __global__ void q2_set_u64(uint64_t *p, uint64_t v) { *p = v; }
 
 // blocks copy the visited suppliers' map entries (2 words each) to their segments; counts[0] =
-// the number of visited suppliers (q2_select); nothing is written past m_cap keys (the host
+// the number of visited suppliers (q2_sel_start); nothing is written past m_cap keys (the host
 // rejects counts above it after the batch)
 __global__ void q2_gather(const uint64_t *__restrict__ map_keys, const uint64_t *__restrict__ src,
                           const uint64_t *__restrict__ dst, const uint32_t *__restrict__ cnt,
@@ -69,194 +69,216 @@ __global__ void q2_gather(const uint64_t *__restrict__ map_keys, const uint64_t 
         }
 }
 
-// RunQuery2's selection (tpcc_new_order.cpp:650-797) in one workgroup, from the REGION / NATION
-// scan rows and the SUPPLIER slot dump:
+// RunQuery2's selection (tpcc_new_order.cpp:650-797) on the device, from the REGION / NATION scan
+// rows and the SUPPLIER leaves (TableScanExecutor::ScanLeafNode with scan_sz -1, executor.h:
+// 580-612: every slot of every leaf in leaf order, slots in slot order, raw records):
 //   visits   = for each REGION row named the target (scan order), each NATION row of that region
-//              (scan order); a nation is visited at most once (it has one region key, region
-//              keys are unique), so at most kNationScan visits, found through an LDS hash;
-//   sel      = every SUPPLIER record of each visited nation, visit by visit, in ScanLeafNode
-//              (slot dump) order: a stable counting sort by visit.  The slots go through LDS in
-//              windows of kSelWin; in each, every lane finds its slots' visits (independent
-//              loads), then wave w ranks the window's w-th 1024 slots per visit (one ballot per
-//              distinct visit of a 64-slot chunk, LDS only) -- the visit and rank of every slot go
-//              to global scratch; one prefix over (visit, window, wave) gives each group's start,
-//              and a parallel pass places every selected supplier at start + rank;
-//   segments = src / cnt of each selected supplier's supp_stock_map entries (map_off, keys
-//              below 10000), dst = their exclusive prefix sum;
+//              (scan order); a nation is visited at most once (one region key per nation, region
+//              keys unique), so at most kNationScan visits;
+//   sel      = every SUPPLIER record of each visited nation, visit by visit, in slot order: a
+//              stable counting sort by visit over 64-slot chunks --
+//                q2_sel_count  (a wave per chunk) the visits, each slot's visit and rank among
+//                              its chunk's slots of that visit, the chunk's count per visit;
+//                q2_sel_start  (one block) each (chunk, visit)'s start: visit-major, then chunk;
+//                q2_sel_place  (a lane per slot) sel[start + rank] and the supplier's map segment;
+//                q2_sel_seg    (one block) dst = exclusive prefix of the segment lengths;
 //   counts   = {suppliers, stock keys}.
-// No loop of this kernel waits on a global load per iteration: the loads are issued side by side.
-constexpr int kVisits = kNationScan, kVisitHash = 256;
-constexpr uint32_t kSelWin = 16384, kSelMaxWin = 8;  // slots per LDS window, windows per call
-__global__ __launch_bounds__(1024) void q2_select(const uint8_t *__restrict__ regs, uint32_t rs,
-                                                  const uint8_t *__restrict__ nats, uint32_t ns, uint64_t name0,
-                                                  uint64_t name1, const uint64_t *__restrict__ pairs, uint64_t nslots,
-                                                  const uint32_t *__restrict__ map_off, int8_t *__restrict__ g_vis,
-                                                  uint16_t *__restrict__ g_rank, uint64_t *__restrict__ sel,
-                                                  uint64_t *__restrict__ src, uint32_t *__restrict__ cnt,
-                                                  uint64_t *__restrict__ dst, uint64_t *__restrict__ counts) {
+// Every block derives the visits itself from the (L2-resident) scan rows, so no launch is spent
+// on them; no loop waits on one global load per iteration.
+constexpr int kVisits = kNationScan;
+constexpr uint32_t kDirect = 1024;  // nation keys below this: a direct LDS map, the rest searched
+
+struct VisitMap {  // nation key -> visit (LDS)
+    int8_t dir[kDirect];
+    int64_t big_key[kVisits];
+    int32_t big_val[kVisits];
+    uint32_t nbig, nv;
+};
+
+// the visit map of the target region, built by every block (blockDim.x >= 64)
+__device__ void build_visits(VisitMap &vm, const uint8_t *regs, uint32_t rs, const uint8_t *nats, uint32_t ns,
+                             uint64_t name0, uint64_t name1, uint64_t mask0, uint64_t mask1, uint8_t *s_rmatch,
+                             uint8_t *s_flag) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint32_t nreg = min(*reinterpret_cast<const uint32_t *>(regs - 8), (uint32_t)kRegionScan);
+    const uint32_t nnat = min(*reinterpret_cast<const uint32_t *>(nats - 8), (uint32_t)kNationScan);
+    for (uint32_t i = tid; i < kDirect; i += blockDim.x) vm.dir[i] = -1;
+    if (tid == 0) vm.nbig = 0;
+    // R_NAME == regions[target]: the bytes up to and including the target's NUL (< 16)
+    if (tid < nreg) {
+        const uint64_t *nm = reinterpret_cast<const uint64_t *>(regs + (uint64_t)tid * rs + 8);
+        s_rmatch[tid] = ((nm[0] ^ name0) & mask0) == 0 && ((nm[1] ^ name1) & mask1) == 0;
+    }
+    __syncthreads();
+    const uint32_t nf = nreg * nnat;  // flag f = (region row f / nnat, nation row f % nnat), visit order
+    for (uint32_t f = tid; f < nf; f += blockDim.x) {
+        const uint32_t r = f / nnat, a = f % nnat;
+        s_flag[f] = s_rmatch[r] && *reinterpret_cast<const int64_t *>(nats + (uint64_t)a * ns + 8) ==
+                                       *reinterpret_cast<const int64_t *>(regs + (uint64_t)r * rs);
+    }
+    __syncthreads();
+    if (tid < 64) {  // wave 0 numbers the flagged (region, nation) pairs in order
+        uint32_t base = 0;
+        for (uint32_t f0 = 0; f0 < nf; f0 += 64) {
+            const uint32_t f = f0 + lane;
+            const bool fl = f < nf && s_flag[f];
+            const uint64_t b = ballot(fl);
+            if (fl) {
+                const uint32_t idx = base + (uint32_t)__builtin_popcountll(b & ((1ull << lane) - 1));
+                const int64_t nk = *reinterpret_cast<const int64_t *>(nats + (uint64_t)(f % nnat) * ns);
+                if (idx < (uint32_t)kVisits) {
+                    if (nk >= 0 && nk < (int64_t)kDirect) {
+                        vm.dir[nk] = (int8_t)idx;
+                    } else {
+                        const uint32_t k = atomicAdd(&vm.nbig, 1u);
+                        vm.big_key[k] = nk;
+                        vm.big_val[k] = (int32_t)idx;
+                    }
+                }
+            }
+            base += (uint32_t)__builtin_popcountll(b);
+        }
+        if (lane == 0) vm.nv = min(base, (uint32_t)kVisits);
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ int visit_of(const VisitMap &vm, uint64_t nat) {
+    if ((int64_t)nat >= 0 && (int64_t)nat < (int64_t)kDirect) return vm.dir[nat];
+    for (uint32_t k = 0; k < vm.nbig; ++k)
+        if (vm.big_key[k] == (int64_t)nat) return vm.big_val[k];
+    return -1;
+}
+
+// a wave per 64-slot chunk of the SUPPLIER leaves (blocks of 4 waves)
+__global__ __launch_bounds__(256) void q2_sel_count(const uint8_t *__restrict__ regs, uint32_t rs,
+                                                    const uint8_t *__restrict__ nats, uint32_t ns, uint64_t name0,
+                                                    uint64_t name1, uint64_t mask0, uint64_t mask1, DevTable t,
+                                                    uint32_t kpad, uint64_t nchunks, int8_t *__restrict__ g_vis,
+                                                    uint8_t *__restrict__ g_rank, uint64_t *__restrict__ g_key,
+                                                    uint32_t *__restrict__ ccnt, uint32_t *__restrict__ g_nv) {
+    __shared__ VisitMap vm;
     __shared__ uint8_t s_rmatch[kRegionScan];
     __shared__ uint8_t s_flag[kRegionScan * kNationScan];
-    __shared__ uint32_t s_nvisit;
-    __shared__ int64_t s_hkey[kVisitHash];
-    __shared__ int32_t s_hval[kVisitHash];
-    __shared__ int8_t s_vis[kSelWin];
-    __shared__ uint32_t s_grp[kSelMaxWin * 16][kVisits];  // per (window, wave): counts, then starts
-    __shared__ uint32_t s_vstart[kVisits];
-    __shared__ uint64_t s_wsum[16];
-    __shared__ uint64_t s_n;
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const uint32_t nreg = *reinterpret_cast<const uint32_t *>(regs - 8);
-    const uint32_t nnat = *reinterpret_cast<const uint32_t *>(nats - 8);
-    const uint32_t nwin = (uint32_t)((nslots + kSelWin - 1) / kSelWin);  // <= kSelMaxWin (host check)
-    // 1. the visits
-    if (tid < kRegionScan && tid < nreg) {  // R_NAME (55 bytes, NUL-terminated) == regions[target]
-        const uint8_t *name = regs + (uint64_t)tid * rs + 8;
-        bool eq = true;
-        for (int i = 0; i < 55; ++i) {
-            const uint8_t c = name[i];
-            const uint8_t want = i < 8 ? (uint8_t)(name0 >> (8 * i)) : i < 16 ? (uint8_t)(name1 >> (8 * (i - 8))) : 0;
-            if (c != want) {
-                eq = false;
-                break;
-            }
-            if (c == 0) break;
-        }
-        s_rmatch[tid] = eq;
+    __shared__ uint32_t s_cnt[4][kVisits];
+    build_visits(vm, regs, rs, nats, ns, name0, name1, mask0, mask1, s_rmatch, s_flag);
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *g_nv = vm.nv;
+    const uint64_t c = (uint64_t)blockIdx.x * 4 + wv;
+    if (c >= nchunks) return;
+    for (uint32_t v = lane; v < (uint32_t)kVisits; v += 64) s_cnt[wv][v] = 0;
+    const uint64_t i = c * 64 + lane;
+    const SlotInfo si = t.slot[i];
+    uint64_t key = ~0ull;
+    int v = -1;
+    if (si.meta != 0) {
+        const uint8_t *row = t.heap + (uint64_t)si.image * t.hstride;
+        key = *reinterpret_cast<const uint64_t *>(row);
+        v = key == ~0ull ? -1 : visit_of(vm, *reinterpret_cast<const uint64_t *>(row + kpad));
     }
-    for (uint32_t i = tid; i < kVisitHash; i += blockDim.x) s_hkey[i] = INT64_MIN, s_hval[i] = -1;
-    for (uint32_t i = tid; i < kSelMaxWin * 16 * kVisits; i += blockDim.x) (&s_grp[0][0])[i] = 0;
-    __syncthreads();
-    if (tid < nreg * nnat && tid < kRegionScan * kNationScan) {
-        const uint32_t r = tid / nnat, a = tid % nnat;
-        const uint8_t *rr = regs + (uint64_t)r * rs, *nr = nats + (uint64_t)a * ns;
-        s_flag[tid] = s_rmatch[r] && *reinterpret_cast<const int64_t *>(nr + 8) == *reinterpret_cast<const int64_t *>(rr);
+    uint32_t rank = 0;
+    uint64_t todo = ballot(v >= 0);
+    while (todo) {
+        const int vl = (int)rl32((uint32_t)v, (int)__builtin_ctzll(todo));
+        const uint64_t mm = ballot(v == vl);
+        if (v == vl) rank = (uint32_t)__builtin_popcountll(mm & ((1ull << lane) - 1));
+        if (lane == 0) s_cnt[wv][vl] = (uint32_t)__builtin_popcountll(mm);
+        todo &= ~mm;
     }
-    __syncthreads();
-    if (tid == 0) {
-        uint32_t nv = 0;
-        for (uint32_t f = 0; f < nreg * nnat && f < kRegionScan * kNationScan; ++f)
-            if (s_flag[f] && nv < (uint32_t)kVisits) {
-                const int64_t nk = *reinterpret_cast<const int64_t *>(nats + (uint64_t)(f % nnat) * ns);
-                uint32_t h = (uint32_t)(((uint64_t)nk * 0x9E3779B97F4A7C15ull) >> 56);
-                while (s_hkey[h] != INT64_MIN && s_hkey[h] != nk) h = (h + 1) & (kVisitHash - 1);
-                if (s_hkey[h] == nk) continue;  // (cannot happen: one region per nation)
-                s_hkey[h] = nk;
-                s_hval[h] = (int32_t)nv++;
-            }
-        s_nvisit = nv;
-    }
-    __syncthreads();
-    const uint32_t nv = s_nvisit;
-    auto visit_of = [&](uint64_t key, uint64_t nat) -> int {
-        if (key == ~0ull || nv == 0) return -1;
-        uint32_t h = (uint32_t)((nat * 0x9E3779B97F4A7C15ull) >> 56);
-        while (s_hkey[h] != INT64_MIN) {
-            if (s_hkey[h] == (int64_t)nat) return s_hval[h];
-            h = (h + 1) & (kVisitHash - 1);
-        }
-        return -1;
-    };
-    // 2. per window: visits of its slots (A), per-wave counts and ranks (B)
-    for (uint32_t win = 0; win < nwin; ++win) {
-        const uint64_t w0 = (uint64_t)win * kSelWin;
-#pragma unroll 4
-        for (uint32_t j = tid; j < kSelWin; j += 1024) {
-            const uint64_t i = w0 + j;
-            int v = -1;
-            if (i < nslots) v = visit_of(pairs[2 * i], pairs[2 * i + 1]);
-            s_vis[j] = (int8_t)v;
-        }
-        __syncthreads();
-        uint32_t *gc = s_grp[win * 16 + wv];
-        for (uint32_t c0 = wv * 1024; c0 < (wv + 1) * 1024; c0 += 64) {
-            const uint32_t j = c0 + lane;
-            const int v = s_vis[j];
-            uint32_t rank = 0;
-            uint64_t todo = ballot(v >= 0);
-            while (todo) {
-                const int vl = (int)rl32((uint32_t)v, (int)__builtin_ctzll(todo));
-                const uint64_t mm = ballot(v == vl);
-                const uint32_t before = gc[vl];
-                if (v == vl) rank = before + (uint32_t)__builtin_popcountll(mm & ((1ull << lane) - 1));
-                if (lane == 0) gc[vl] = before + (uint32_t)__builtin_popcountll(mm);
-                todo &= ~mm;
-            }
-            const uint64_t i = w0 + j;
-            if (i < nslots) {
-                g_vis[i] = (int8_t)v;
-                g_rank[i] = (uint16_t)rank;
-            }
-        }
-        __syncthreads();
-    }
-    // 3. group starts, visit-major, then window, then wave (slot order within a visit)
-    const uint32_t ngrp = nwin * 16;
-    if (tid < nv) {
+    g_vis[i] = (int8_t)v;
+    g_rank[i] = (uint8_t)rank;
+    g_key[i] = key;
+    for (uint32_t w = lane; w < (uint32_t)kVisits; w += 64) ccnt[c * kVisits + w] = s_cnt[wv][w];
+}
+
+// one block: ccnt[c][v] (counts) -> starts, in place: visit-major, then chunk order
+__global__ __launch_bounds__(1024) void q2_sel_start(uint32_t *__restrict__ ccnt, uint64_t nchunks,
+                                                     const uint32_t *__restrict__ g_nv, uint64_t *__restrict__ counts) {
+    __shared__ uint32_t s_tot[kVisits];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const uint32_t nv = *g_nv;
+    for (uint32_t v = wv; v < nv; v += nw) {  // a wave per visit: its total
         uint32_t t = 0;
-        for (uint32_t g = 0; g < ngrp; ++g) t += s_grp[g][tid];
-        s_vstart[tid] = t;
+#pragma unroll 8
+        for (uint64_t c = lane; c < nchunks; c += 64) t += ccnt[c * kVisits + v];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+        if (lane == 0) s_tot[v] = t;
     }
     __syncthreads();
-    if (tid == 0) {
+    if (threadIdx.x == 0) {
         uint32_t pos = 0;
         for (uint32_t v = 0; v < nv; ++v) {
-            const uint32_t t = s_vstart[v];
-            s_vstart[v] = pos;
+            const uint32_t t = s_tot[v];
+            s_tot[v] = pos;
             pos += t;
         }
         counts[0] = pos;
-        s_n = pos;
     }
     __syncthreads();
-    if (tid < nv) {
-        uint32_t pos = s_vstart[tid];
-        for (uint32_t g = 0; g < ngrp; ++g) {
-            const uint32_t c = s_grp[g][tid];
-            s_grp[g][tid] = pos;
-            pos += c;
-        }
-    }
-    __syncthreads();
-    // 4. placement and map segments, every slot independent
-#pragma unroll 4
-    for (uint64_t i = tid; i < nslots; i += 1024) {
-        const int v = g_vis[i];
-        if (v < 0) continue;
-        const uint32_t pos = s_grp[(uint32_t)(i / kSelWin) * 16 + (uint32_t)((i % kSelWin) >> 10)][v] + g_rank[i];
-        const uint64_t sk = pairs[2 * i];
-        uint64_t s0 = 0, c = 0;
-        if (sk < 10000) {
-            s0 = map_off[sk];
-            c = map_off[sk + 1] > map_off[sk] ? map_off[sk + 1] - map_off[sk] : 0;
-        }
-        sel[pos] = sk;
-        src[pos] = s0;
-        cnt[pos] = (uint32_t)c;
-    }
-    __syncthreads();
-    // 5. dst = exclusive prefix of cnt in selection order
-    const uint64_t n = s_n;
-    uint64_t carry = 0;
-    for (uint64_t b = 0; b < n; b += blockDim.x) {
-        const uint64_t i = b + tid;
-        const uint64_t c = i < n ? cnt[i] : 0;
-        uint64_t x = c;  // inclusive scan in the wave, then across the 16 waves
+    for (uint32_t v = wv; v < nv; v += nw) {  // a wave per visit: exclusive scan over the chunks
+        uint32_t carry = s_tot[v];
+        for (uint64_t c0 = 0; c0 < nchunks; c0 += 64) {
+            const uint64_t c = c0 + lane;
+            const uint32_t x = c < nchunks ? ccnt[c * kVisits + v] : 0u;
+            uint32_t y = x;
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint64_t y = __shfl_up(x, o, 64);
-            if (lane >= (uint32_t)o) x += y;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t z = __shfl_up(y, o, 64);
+                if (lane >= (uint32_t)o) y += z;
+            }
+            if (c < nchunks) ccnt[c * kVisits + v] = carry + y - x;
+            carry += rl32(y, 63);
         }
-        if (lane == 63) s_wsum[wv] = x;
-        __syncthreads();
-        uint64_t before = carry;
-        for (uint32_t w = 0; w < wv; ++w) before += s_wsum[w];
-        if (i < n) dst[i] = before + x - c;
-        uint64_t total = 0;
-        for (uint32_t w = 0; w < 16; ++w) total += s_wsum[w];
-        carry += total;
-        __syncthreads();
     }
-    if (tid == 0) counts[1] = carry;
+}
+
+// a lane per slot: the selected suppliers at their places, with their supp_stock_map segments
+__global__ void q2_sel_place(const int8_t *__restrict__ g_vis, const uint8_t *__restrict__ g_rank,
+                             const uint64_t *__restrict__ g_key, const uint32_t *__restrict__ cstart, uint64_t nslots,
+                             const uint32_t *__restrict__ map_off, uint64_t *__restrict__ sel,
+                             uint64_t *__restrict__ src, uint32_t *__restrict__ cnt) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nslots) return;
+    const int v = g_vis[i];
+    if (v < 0) return;
+    const uint32_t pos = cstart[(i >> 6) * kVisits + v] + g_rank[i];
+    const uint64_t sk = g_key[i];
+    uint64_t s0 = 0, c = 0;
+    if (sk < 10000) {
+        const uint32_t a = map_off[sk], b = map_off[sk + 1];
+        s0 = a;
+        c = b > a ? b - a : 0;
+    }
+    sel[pos] = sk;
+    src[pos] = s0;
+    cnt[pos] = (uint32_t)c;
+}
+
+// one block: dst = exclusive prefix of cnt over the counts[0] selected suppliers, counts[1] = total
+__global__ __launch_bounds__(1024) void q2_sel_seg(const uint32_t *__restrict__ cnt, uint64_t *__restrict__ dst,
+                                                   uint64_t *__restrict__ counts) {
+    __shared__ uint64_t s_wsum[16];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint64_t n = counts[0];
+    const uint64_t per = (n + 1023) / 1024, lo = tid * per, hi = lo + per < n ? lo + per : n;
+    uint64_t own = 0;  // this thread's contiguous run
+    for (uint64_t i = lo; i < hi; ++i) own += cnt[i];
+    uint64_t x = own;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up(x, o, 64);
+        if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) s_wsum[wv] = x;
+    __syncthreads();
+    uint64_t before = x - own;
+    for (uint32_t w = 0; w < wv; ++w) before += s_wsum[w];
+    for (uint64_t i = lo; i < hi; ++i) {
+        dst[i] = before;
+        before += cnt[i];
+    }
+    if (tid == 1023) counts[1] = before;
 }
 
 // thread per (query q, supplier s): the abort for a stock lookup that produced no tuple is already
@@ -329,25 +351,6 @@ __global__ void q2_finish(const stage_probe_out_dev *__restrict__ iout, const ui
     if (host_out && s % n < max_out) host_out[(uint64_t)(s / n) * max_out + s % n] = r;
 }
 
-// SUPPLIER scan with scan_sz -1 (TableScanExecutor::ScanLeafNode, executor.h:580-612): every
-// slot of every leaf in leaf order, slots in slot order, raw records without a visibility
-// test -- one lane per slot; pairs[i] = {SU_SUPPKEY, SU_NATIONKEY} of slot i, or ~0 for a slot
-// holding no record
-__global__ void q2_dump_leaves(DevTable t, uint32_t kpad, uint64_t *__restrict__ pairs) {
-    const uint64_t n = (uint64_t)t.nleaves * t.cap;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-        const SlotInfo si = t.slot[i];
-        uint64_t k = ~0ull, nat = ~0ull;
-        if (si.meta != 0) {
-            const uint8_t *row = t.heap + (uint64_t)si.image * t.hstride;
-            k = *reinterpret_cast<const uint64_t *>(row);
-            nat = *reinterpret_cast<const uint64_t *>(row + kpad);
-        }
-        pairs[2 * i] = k;
-        pairs[2 * i + 1] = nat;
-    }
-}
-
 // TableScanExecutor rows of one scan from `start` (device scan) into the table's scratch: the
 // returned pointer is the first row, the row count (u32) 8 bytes before it
 const uint8_t *scan_rows(stage_table *t, uint64_t start, uint32_t scan_size, hipStream_t s) {
@@ -401,8 +404,8 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         for (uint32_t q = 0; q < nq; ++q) aborted[q] = 0;
         const DevTable &pv = supplier->dev.view, &sv = stock->dev.view, &iv = item->dev.view;
         const uint64_t nslots = (uint64_t)pv.nleaves * pv.cap;
-        if (nslots > (uint64_t)kSelWin * kSelMaxWin)
-            return fail(STAGE_E_UNSUPPORTED, "SUPPLIER has more slots than q2_select's windows hold (131072)");
+        if (pv.cap % 64) return fail(STAGE_E_UNSUPPORTED, "SUPPLIER leaves of a multiple of 64 slots");
+        const uint64_t nchunks = nslots / 64;
         // upper bounds (buffer sizes, grids): every SUPPLIER slot visited, every map entry looked up
         constexpr uint32_t kMapKeys = 10000;
         uint64_t m_max = 0;
@@ -431,14 +434,15 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
                        o_keys = take(std::max<uint64_t>(m_max, 1) * 16), o_sbase = take(std::max<uint64_t>(m_max, 1) * 32),
                        o_slast = take(n_max * 32 * nq), o_ik = take(n_max * 8 * nq), o_iout = take(n_max * 32 * nq),
                        o_ibase = take(n_max * 32), o_rec = take(n_max * nq * sizeof(stage_q2_rec)),
-                       o_vis = take(n_max), o_rank = take(n_max * 2);
+                       o_vis = take(n_max), o_rank = take(n_max), o_ccnt = take(std::max<uint64_t>(nchunks, 1) * kVisits * 4),
+                       o_nv = take(4);
         // the SUPPLIER table's scratch: REGION's and NATION's hold their scan rows (scan_rows)
         uint8_t *buf = scratch_bytes(supplier->dev, off), *mir = buf + o_mir;
         auto *d_map = (const uint32_t *)(mir + q_map);
         auto *d_rq = (const uint32_t *)(mir + q_rq);
         auto *d_counts = (uint64_t *)(mir + q_cn);
         auto *d_ab = (int32_t *)(mir + q_ab);
-        auto *d_pairs = (uint64_t *)(buf + o_pairs), *d_sel = (uint64_t *)(buf + o_sel);
+        auto *d_sel = (uint64_t *)(buf + o_sel);
         auto *d_src = (uint64_t *)(buf + o_src), *d_dst = (uint64_t *)(buf + o_dst);
         auto *d_cnt = (uint32_t *)(buf + o_cnt);
         auto *d_keys = (uint64_t *)(buf + o_keys), *d_ik = (uint64_t *)(buf + o_ik);
@@ -459,20 +463,30 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         const uint8_t *nats = scan_rows(nation, 0, kNationScan, ns_s);
         hip_check(hipEventRecord(ev[1], rs_s), "join");
         hip_check(hipEventRecord(ev[2], ns_s), "join");
-        q2_dump_leaves<<<(unsigned)std::min<uint64_t>((nslots + 255) / 256, 4096), 256, 0, s>>>(
-            pv, facts(supplier).key_pad(), d_pairs);
-        hip_check(hipGetLastError(), "dump leaves");
         hip_check(hipStreamWaitEvent(s, ev[1], 0), "join");
         hip_check(hipStreamWaitEvent(s, ev[2], 0), "join");
-        // 2. the selection and the map segments, on the device
+        // 2. the selection and the map segments, on the device (four kernels, no host wait)
         char tname[16] = {0};
         std::strncpy(tname, kRegions[target_region], 15);
-        uint64_t name0, name1;
+        uint64_t name0, name1, mask0 = 0, mask1 = 0;
         std::memcpy(&name0, tname, 8);
         std::memcpy(&name1, tname + 8, 8);
-        q2_select<<<1, 1024, 0, s>>>(regs, region->dev.view.stride, nats, nation->dev.view.stride, name0, name1, d_pairs,
-                                     nslots, d_map, (int8_t *)(buf + o_vis), (uint16_t *)(buf + o_rank), d_sel, d_src,
-                                     d_cnt, d_dst, d_counts);
+        for (size_t b = 0; b <= std::strlen(tname); ++b)  // the name and its NUL
+            (b < 8 ? mask0 : mask1) |= 0xFFull << (8 * (b % 8));
+        auto *g_key = (uint64_t *)(buf + o_pairs);
+        auto *g_vis = (int8_t *)(buf + o_vis);
+        auto *g_rank = (uint8_t *)(buf + o_rank);
+        auto *ccnt = (uint32_t *)(buf + o_ccnt);
+        auto *g_nv = (uint32_t *)(buf + o_nv);
+        if (nchunks) {
+            q2_sel_count<<<(unsigned)((nchunks + 3) / 4), 256, 0, s>>>(
+                regs, region->dev.view.stride, nats, nation->dev.view.stride, name0, name1, mask0, mask1, pv,
+                facts(supplier).key_pad(), nchunks, g_vis, g_rank, g_key, ccnt, g_nv);
+            q2_sel_start<<<1, 1024, 0, s>>>(ccnt, nchunks, g_nv, d_counts);
+            q2_sel_place<<<(unsigned)((nslots + 255) / 256), 256, 0, s>>>(g_vis, g_rank, g_key, ccnt, nslots, d_map,
+                                                                           d_sel, d_src, d_cnt);
+            q2_sel_seg<<<1, 1024, 0, s>>>(d_cnt, d_dst, d_counts);
+        }
         hip_check(hipGetLastError(), "select");
         lap("selection enqueued");
         // 3. every visited supplier's STOCK keys, one probe of them all (the counts on the device)
