@@ -449,23 +449,10 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         auto *d_iout = (stage_probe_out_dev *)(buf + o_iout), *d_slast = (stage_probe_out_dev *)(buf + o_slast);
         auto *d_sbase = (stage_probe_out_dev *)(buf + o_sbase), *d_ibase = (stage_probe_out_dev *)(buf + o_ibase);
         auto *d_rec = (stage_q2_rec *)(buf + o_rec);
-        hip_check(hipMemcpyAsync(mir, pq, q_end, hipMemcpyHostToDevice, s), "h2d");
-        // 1. REGION / NATION scans on their tables' own streams beside the SUPPLIER dump on s
-        // (forked from and joined back into s): three short dependent chains side by side
         hipEvent_t *ev = stock->dev.call_ev;
         for (int k = 0; k < 3; ++k)
             if (!ev[k]) hip_check(hipEventCreateWithFlags(&ev[k], hipEventDisableTiming), "call event");
         hipStream_t rs_s = region->dev.stream ? region->dev.stream : s, ns_s = nation->dev.stream ? nation->dev.stream : s;
-        hip_check(hipEventRecord(ev[0], s), "fork");
-        hip_check(hipStreamWaitEvent(rs_s, ev[0], 0), "fork");
-        hip_check(hipStreamWaitEvent(ns_s, ev[0], 0), "fork");
-        const uint8_t *regs = scan_rows(region, 0, kRegionScan, rs_s);
-        const uint8_t *nats = scan_rows(nation, 0, kNationScan, ns_s);
-        hip_check(hipEventRecord(ev[1], rs_s), "join");
-        hip_check(hipEventRecord(ev[2], ns_s), "join");
-        hip_check(hipStreamWaitEvent(s, ev[1], 0), "join");
-        hip_check(hipStreamWaitEvent(s, ev[2], 0), "join");
-        // 2. the selection and the map segments, on the device (four kernels, no host wait)
         char tname[16] = {0};
         std::strncpy(tname, kRegions[target_region], 15);
         uint64_t name0, name1, mask0 = 0, mask1 = 0;
@@ -478,42 +465,6 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         auto *g_rank = (uint8_t *)(buf + o_rank);
         auto *ccnt = (uint32_t *)(buf + o_ccnt);
         auto *g_nv = (uint32_t *)(buf + o_nv);
-        if (nchunks) {
-            q2_sel_count<<<(unsigned)((nchunks + 3) / 4), 256, 0, s>>>(
-                regs, region->dev.view.stride, nats, nation->dev.view.stride, name0, name1, mask0, mask1, pv,
-                facts(supplier).key_pad(), nchunks, g_vis, g_rank, g_key, ccnt, g_nv);
-            q2_sel_start<<<1, 1024, 0, s>>>(ccnt, nchunks, g_nv, d_counts);
-            q2_sel_place<<<(unsigned)((nslots + 255) / 256), 256, 0, s>>>(g_vis, g_rank, g_key, ccnt, nslots, d_map,
-                                                                           d_sel, d_src, d_cnt);
-            q2_sel_seg<<<1, 1024, 0, s>>>(d_cnt, d_dst, d_counts);
-        }
-        hip_check(hipGetLastError(), "select");
-        lap("selection enqueued");
-        // 3. every visited supplier's STOCK keys, one probe of them all (the counts on the device)
-        q2_gather<<<(unsigned)std::max<uint64_t>(std::min<uint64_t>(n_hint, 4096), 1), 256, 0, s>>>(
-            d_map_keys, d_src, d_dst, d_cnt, d_counts, m_max, d_keys);
-        // every query of the batch looks up the same STOCK keys (the visited suppliers and their
-        // supp_stock_map do not depend on the read id): each key is probed once, with no read id
-        // (the hit slot does not depend on it), and its visibility evaluated at every query's read
-        // id inside the per-supplier fold (launch_revisit_segments: the aborts and each
-        // supplier's last stock, per query)
-        if (m_max)
-            hip_check(launch_probe(sv, d_keys, nullptr, nullptr, nullptr, m_max, d_sbase, nullptr, s, stock->tune,
-                                   d_counts + 1, m_hint),
-                      "stock probe");
-        if (m_max)
-            hip_check(launch_revisit_segments(sv, d_sbase, m_max, d_dst, d_cnt, (uint32_t)n_max, d_rq, nq, d_slast, d_ab, s,
-                                              d_counts + 1, d_counts),
-                      "stock read ids");
-        q2_reduce<<<(unsigned)((n_max * nq + 255) / 256), 256, 0, s>>>(d_slast, d_keys, d_dst, d_cnt, d_sel, sv.heap,
-                                                                       sv.hstride, facts(stock).key_pad(), d_counts,
-                                                                       nq, d_rec, d_ik);
-        // 4. item lookups of the last stocks (the same keys in every query: probed once, as above),
-        // the I_DATA filter, the records into `out`
-        hip_check(launch_probe(iv, d_ik, nullptr, nullptr, nullptr, n_max, d_ibase, nullptr, s, item->tune, d_counts,
-                               n_hint),
-                  "item probe");
-        hip_check(launch_revisit(iv, d_ibase, n_max, d_rq, nq, nullptr, d_iout, s, d_counts), "item read ids");
         // `out` in page-locked memory (stage_host_alloc, stage.pinned_empty): the finishing kernel
         // writes the records into it directly; otherwise they are copied once the count is known
         stage_q2_rec *host_out = nullptr;
@@ -527,10 +478,125 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
             (void)hipGetLastError();  // a pageable pointer is not an error here
         }
         if (trace) std::fprintf(stderr, "[q2] out %s\n", host_out ? "page-locked: written by q2_finish" : "pageable: copied");
-        q2_finish<<<(unsigned)((n_max * nq + 255) / 256), 256, 0, s>>>(d_iout, iv.heap, iv.hstride, facts(item).key_pad(),
-                                                                       d_counts, nq, d_rec, d_ab, host_out, max_out);
-        hip_check(hipGetLastError(), "q2 kernels");
-        hip_check(hipMemcpyAsync(pq + q_cn, d_counts, 16 + nq * 4ull, hipMemcpyDeviceToHost, s), "d2h");
+        // the scan rows' scratch sized before any capture (scan_rows asks for the same size again)
+        (void)scratch_bytes(region->dev, 64 + (uint64_t)kRegionScan * region->dev.view.stride);
+        (void)scratch_bytes(nation->dev, 64 + (uint64_t)kNationScan * nation->dev.view.stride);
+        // everything up to the batch's one synchronisation, enqueued on s (and the REGION /
+        // NATION streams forked from it)
+        auto enqueue = [&] {
+            hip_check(hipMemcpyAsync(mir, pq, q_end, hipMemcpyHostToDevice, s), "h2d");
+            // 1. REGION / NATION scans on their tables' own streams beside the SUPPLIER dump on s
+            // (forked from and joined back into s): three short dependent chains side by side
+            hip_check(hipEventRecord(ev[0], s), "fork");
+            hip_check(hipStreamWaitEvent(rs_s, ev[0], 0), "fork");
+            hip_check(hipStreamWaitEvent(ns_s, ev[0], 0), "fork");
+            const uint8_t *regs = scan_rows(region, 0, kRegionScan, rs_s);
+            const uint8_t *nats = scan_rows(nation, 0, kNationScan, ns_s);
+            hip_check(hipEventRecord(ev[1], rs_s), "join");
+            hip_check(hipEventRecord(ev[2], ns_s), "join");
+            hip_check(hipStreamWaitEvent(s, ev[1], 0), "join");
+            hip_check(hipStreamWaitEvent(s, ev[2], 0), "join");
+            // 2. the selection and the map segments, on the device (four kernels, no host wait)
+            if (nchunks) {
+                q2_sel_count<<<(unsigned)((nchunks + 3) / 4), 256, 0, s>>>(
+                    regs, region->dev.view.stride, nats, nation->dev.view.stride, name0, name1, mask0, mask1, pv,
+                    facts(supplier).key_pad(), nchunks, g_vis, g_rank, g_key, ccnt, g_nv);
+                q2_sel_start<<<1, 1024, 0, s>>>(ccnt, nchunks, g_nv, d_counts);
+                q2_sel_place<<<(unsigned)((nslots + 255) / 256), 256, 0, s>>>(g_vis, g_rank, g_key, ccnt, nslots, d_map,
+                                                                               d_sel, d_src, d_cnt);
+                q2_sel_seg<<<1, 1024, 0, s>>>(d_cnt, d_dst, d_counts);
+            }
+            hip_check(hipGetLastError(), "select");
+            // 3. every visited supplier's STOCK keys, one probe of them all (the counts on the device)
+            q2_gather<<<(unsigned)std::max<uint64_t>(std::min<uint64_t>(n_hint, 4096), 1), 256, 0, s>>>(
+                d_map_keys, d_src, d_dst, d_cnt, d_counts, m_max, d_keys);
+            // every query of the batch looks up the same STOCK keys (the visited suppliers and their
+            // supp_stock_map do not depend on the read id): each key is probed once, with no read id
+            // (the hit slot does not depend on it), and its visibility evaluated at every query's read
+            // id inside the per-supplier fold (launch_revisit_segments: the aborts and each
+            // supplier's last stock, per query)
+            if (m_max)
+                hip_check(launch_probe(sv, d_keys, nullptr, nullptr, nullptr, m_max, d_sbase, nullptr, s, stock->tune,
+                                       d_counts + 1, m_hint),
+                          "stock probe");
+            if (m_max)
+                hip_check(launch_revisit_segments(sv, d_sbase, m_max, d_dst, d_cnt, (uint32_t)n_max, d_rq, nq, d_slast, d_ab, s,
+                                                  d_counts + 1, d_counts),
+                          "stock read ids");
+            q2_reduce<<<(unsigned)((n_max * nq + 255) / 256), 256, 0, s>>>(d_slast, d_keys, d_dst, d_cnt, d_sel, sv.heap,
+                                                                           sv.hstride, facts(stock).key_pad(), d_counts,
+                                                                           nq, d_rec, d_ik);
+            // 4. item lookups of the last stocks (the same keys in every query: probed once, as above),
+            // the I_DATA filter, the records into `out`
+            hip_check(launch_probe(iv, d_ik, nullptr, nullptr, nullptr, n_max, d_ibase, nullptr, s, item->tune, d_counts,
+                                   n_hint),
+                      "item probe");
+            hip_check(launch_revisit(iv, d_ibase, n_max, d_rq, nq, nullptr, d_iout, s, d_counts), "item read ids");
+            q2_finish<<<(unsigned)((n_max * nq + 255) / 256), 256, 0, s>>>(d_iout, iv.heap, iv.hstride, facts(item).key_pad(),
+                                                                           d_counts, nq, d_rec, d_ab, host_out, max_out);
+            hip_check(hipGetLastError(), "q2 kernels");
+            hip_check(hipMemcpyAsync(pq + q_cn, d_counts, 16 + nq * 4ull, hipMemcpyDeviceToHost, s), "d2h");
+        };
+        // A hipGraph of the enqueue: captured on the second call with the same arguments (every
+        // kernel argument, buffer, stream and launch shape is in the key), replayed while they
+        // stay the same -- one launch instead of ~20 (STAGE_Q2_GRAPH=0: always enqueue)
+        static const bool graphs = [] {
+            const char *e = std::getenv("STAGE_Q2_GRAPH");
+            return !(e && std::strcmp(e, "0") == 0);
+        }();
+        std::string key;
+        auto put = [&key](const void *p, size_t n) { key.append((const char *)p, n); };
+        auto putv = [&](auto v) { put(&v, sizeof v); };
+        for (stage_table *t : {region, nation, supplier, item, stock}) {
+            put(&t->dev.view, sizeof t->dev.view);
+            putv(t->dev.stream);
+            putv(t->dev.scratch.p);
+        }
+        put(&stock->tune, sizeof stock->tune);
+        put(&item->tune, sizeof item->tune);
+        put(&region->scan_tune, sizeof region->scan_tune);
+        put(&nation->scan_tune, sizeof nation->scan_tune);
+        for (uint64_t v : {(uint64_t)(uintptr_t)d_map_keys, (uint64_t)target_region, (uint64_t)nq, max_out,
+                           (uint64_t)(uintptr_t)host_out, (uint64_t)(uintptr_t)pq, (uint64_t)(uintptr_t)buf, q_end,
+                           n_max, m_max, n_hint, m_hint, (uint64_t)(uintptr_t)s})
+            putv(v);
+        Q2Graph &G = stock->q2g;
+        bool launched = false;
+        if (graphs && !G.failed) {
+            if (G.exec && G.key == key) {
+                hip_check(hipGraphLaunch(G.exec, s), "q2 graph launch");
+                launched = true;
+            } else if (G.last_key == key) {  // the same call twice: capture it
+                if (G.exec) (void)hipGraphExecDestroy(G.exec);
+                G.exec = nullptr;
+                G.key.clear();
+                hipGraph_t g = nullptr;
+                hip_check(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed), "q2 capture");
+                try {
+                    enqueue();
+                } catch (...) {
+                    (void)hipStreamEndCapture(s, &g);
+                    if (g) (void)hipGraphDestroy(g);
+                    (void)hipGetLastError();
+                    throw;
+                }
+                hipError_t e = hipStreamEndCapture(s, &g);
+                if (!e) e = hipGraphInstantiate(&G.exec, g, nullptr, nullptr, 0);
+                if (g) (void)hipGraphDestroy(g);
+                if (e) {  // no graph for this call shape: enqueue as before from now on
+                    (void)hipGetLastError();
+                    G.exec = nullptr;
+                    G.failed = true;
+                    if (trace) std::fprintf(stderr, "[q2] graph capture failed: %s\n", hipGetErrorString(e));
+                } else {
+                    G.key = key;
+                    hip_check(hipGraphLaunch(G.exec, s), "q2 graph launch");
+                    launched = true;
+                }
+            }
+            G.last_key = key;
+        }
+        if (!launched) enqueue();
         lap("enqueued");
         hip_check(hipStreamSynchronize(s), "q2 sync");  // the batch's one synchronisation
         lap("results back");

@@ -26,6 +26,14 @@ struct HostPipeDeleter {
 };
 }  // namespace stage
 
+// CH-Q2's captured batch (chq2.hip): replayed while its key -- every argument of the captured
+// launches -- stays the same
+struct Q2Graph {
+    hipGraphExec_t exec = nullptr;
+    std::string key, last_key;
+    bool failed = false;
+};
+
 struct stage_table {
     std::unique_ptr<stage::HostTable> host;
     stage::DeviceImage dev;
@@ -40,6 +48,7 @@ struct stage_table {
     int shard_key_bits = 64;                       // coalescing sort width (stage_set_shard_key_bits)
     int wp_overlap = 0;                            // stage_set_write_overlap
     uint64_t q2_hint[2] = {0, 0};                  // CH-Q2's last visited suppliers / STOCK keys (launch shapes)
+    Q2Graph q2g;
     std::mutex pipe_mu;  // serialises stage_probe_host calls on this table
     std::unique_ptr<stage::HostPipe, stage::HostPipeDeleter> pipe;
     // the device write path hands its epoch's bookkeeping (new copy / version headers, slot
@@ -89,6 +98,7 @@ struct stage_table {
     ~stage_table() {
         std::lock_guard<std::mutex> g(adopt_mu);
         if (adopt.joinable()) adopt.join();
+        if (q2g.exec) (void)hipGraphExecDestroy(q2g.exec);
     }
 };
 
