@@ -53,8 +53,6 @@ __device__ __forceinline__ int32_t ld_i32(const uint8_t *p) {
     return (int32_t)((uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24));
 }
 
-__global__ void q2_set_u64(uint64_t *p, uint64_t v) { *p = v; }
-
 // blocks copy the visited suppliers' map entries (2 words each) to their segments; counts[0] =
 // the number of visited suppliers (q2_sel_start); nothing is written past m_cap keys (the host
 // rejects counts above it after the batch)
@@ -79,9 +77,9 @@ __global__ void q2_gather(const uint64_t *__restrict__ map_keys, const uint64_t 
 //              stable counting sort by visit over 64-slot chunks --
 //                q2_sel_count  (a wave per chunk) the visits, each slot's visit and rank among
 //                              its chunk's slots of that visit, the chunk's count per visit;
-//                q2_sel_start  (one block) each (chunk, visit)'s start: visit-major, then chunk;
-//                q2_sel_place  (a lane per slot) sel[start + rank] and the supplier's map segment;
-//                q2_sel_seg    (one block) dst = exclusive prefix of the segment lengths;
+//                q2_sel_place  (one block) each (chunk, visit)'s start (visit-major, then chunk),
+//                              sel[start + rank] with the supplier's map segment, and dst =
+//                              the exclusive prefix of the segment lengths;
 //   counts   = {suppliers, stock keys}.
 // Every block derives the visits itself from the (L2-resident) scan rows, so no launch is spent
 // on them; no loop waits on one global load per iteration.
@@ -191,12 +189,22 @@ __global__ __launch_bounds__(256) void q2_sel_count(const uint8_t *__restrict__ 
     for (uint32_t w = lane; w < (uint32_t)kVisits; w += 64) ccnt[c * kVisits + w] = s_cnt[wv][w];
 }
 
-// one block: ccnt[c][v] (counts) -> starts, in place: visit-major, then chunk order
-__global__ __launch_bounds__(1024) void q2_sel_start(uint32_t *__restrict__ ccnt, uint64_t nchunks,
-                                                     const uint32_t *__restrict__ g_nv, uint64_t *__restrict__ counts) {
+// one block, after q2_sel_count: (1) ccnt[c][v] counts -> starts, in place (visit-major, then
+// chunk order); (2) every selected supplier at start + rank with its supp_stock_map segment
+// (src, cnt); (3) dst = exclusive prefix of the segment lengths; counts = {suppliers, stock keys}
+__global__ __launch_bounds__(1024) void q2_sel_place(uint32_t *__restrict__ ccnt, uint64_t nchunks,
+                                                     const uint32_t *__restrict__ g_nv, const int8_t *__restrict__ g_vis,
+                                                     const uint8_t *__restrict__ g_rank,
+                                                     const uint64_t *__restrict__ g_key, const uint32_t *__restrict__ map_off,
+                                                     uint64_t *__restrict__ sel, uint64_t *__restrict__ src,
+                                                     uint32_t *__restrict__ cnt, uint64_t *__restrict__ dst,
+                                                     uint64_t *__restrict__ counts) {
     __shared__ uint32_t s_tot[kVisits];
-    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    __shared__ uint64_t s_wsum[16];
+    __shared__ uint32_t s_n;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
     const uint32_t nv = *g_nv;
+    // 1. starts
     for (uint32_t v = wv; v < nv; v += nw) {  // a wave per visit: its total
         uint32_t t = 0;
 #pragma unroll 8
@@ -206,7 +214,7 @@ __global__ __launch_bounds__(1024) void q2_sel_start(uint32_t *__restrict__ ccnt
         if (lane == 0) s_tot[v] = t;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (tid == 0) {
         uint32_t pos = 0;
         for (uint32_t v = 0; v < nv; ++v) {
             const uint32_t t = s_tot[v];
@@ -214,6 +222,7 @@ __global__ __launch_bounds__(1024) void q2_sel_start(uint32_t *__restrict__ ccnt
             pos += t;
         }
         counts[0] = pos;
+        s_n = pos;
     }
     __syncthreads();
     for (uint32_t v = wv; v < nv; v += nw) {  // a wave per visit: exclusive scan over the chunks
@@ -231,38 +240,30 @@ __global__ __launch_bounds__(1024) void q2_sel_start(uint32_t *__restrict__ ccnt
             carry += rl32(y, 63);
         }
     }
-}
-
-// a lane per slot: the selected suppliers at their places, with their supp_stock_map segments
-__global__ void q2_sel_place(const int8_t *__restrict__ g_vis, const uint8_t *__restrict__ g_rank,
-                             const uint64_t *__restrict__ g_key, const uint32_t *__restrict__ cstart, uint64_t nslots,
-                             const uint32_t *__restrict__ map_off, uint64_t *__restrict__ sel,
-                             uint64_t *__restrict__ src, uint32_t *__restrict__ cnt) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nslots) return;
-    const int v = g_vis[i];
-    if (v < 0) return;
-    const uint32_t pos = cstart[(i >> 6) * kVisits + v] + g_rank[i];
-    const uint64_t sk = g_key[i];
-    uint64_t s0 = 0, c = 0;
-    if (sk < 10000) {
-        const uint32_t a = map_off[sk], b = map_off[sk + 1];
-        s0 = a;
-        c = b > a ? b - a : 0;
+    __syncthreads();
+    // 2. placement, every slot independent
+    const uint64_t nslots = nchunks * 64;
+#pragma unroll 4
+    for (uint64_t i = tid; i < nslots; i += 1024) {
+        const int v = g_vis[i];
+        if (v < 0) continue;
+        const uint32_t pos = ccnt[(i >> 6) * kVisits + v] + g_rank[i];
+        const uint64_t sk = g_key[i];
+        uint64_t s0 = 0, c = 0;
+        if (sk < 10000) {
+            const uint32_t a = map_off[sk], b = map_off[sk + 1];
+            s0 = a;
+            c = b > a ? b - a : 0;
+        }
+        sel[pos] = sk;
+        src[pos] = s0;
+        cnt[pos] = (uint32_t)c;
     }
-    sel[pos] = sk;
-    src[pos] = s0;
-    cnt[pos] = (uint32_t)c;
-}
-
-// one block: dst = exclusive prefix of cnt over the counts[0] selected suppliers, counts[1] = total
-__global__ __launch_bounds__(1024) void q2_sel_seg(const uint32_t *__restrict__ cnt, uint64_t *__restrict__ dst,
-                                                   uint64_t *__restrict__ counts) {
-    __shared__ uint64_t s_wsum[16];
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const uint64_t n = counts[0];
+    __syncthreads();
+    // 3. segment offsets: each thread a contiguous run, one block scan
+    const uint64_t n = s_n;
     const uint64_t per = (n + 1023) / 1024, lo = tid * per, hi = lo + per < n ? lo + per : n;
-    uint64_t own = 0;  // this thread's contiguous run
+    uint64_t own = 0;
     for (uint64_t i = lo; i < hi; ++i) own += cnt[i];
     uint64_t x = own;
 #pragma unroll
@@ -353,14 +354,13 @@ __global__ void q2_finish(const stage_probe_out_dev *__restrict__ iout, const ui
 
 // TableScanExecutor rows of one scan from `start` (device scan) into the table's scratch: the
 // returned pointer is the first row, the row count (u32) 8 bytes before it
-const uint8_t *scan_rows(stage_table *t, uint64_t start, uint32_t scan_size, hipStream_t s) {
+// (d_start: the start key, in device memory written before s reaches the scan)
+const uint8_t *scan_rows(stage_table *t, const uint64_t *d_start, uint32_t scan_size, hipStream_t s) {
     const DevTable &v = t->dev.view;
     const uint64_t rows = (uint64_t)scan_size * v.stride;
     uint8_t *buf = scratch_bytes(t->dev, 64 + rows);
-    auto *key = (uint64_t *)buf;
     auto *cnt = (uint32_t *)(buf + 56);  // 8 bytes before the rows
-    q2_set_u64<<<1, 1, 0, s>>>(key, start);  // no host buffer outlives the call
-    hip_check(launch_scan(v, key, nullptr, 1, scan_size, cnt, buf + 64, s, t->scan_tune), "scan");
+    hip_check(launch_scan(v, d_start, nullptr, 1, scan_size, cnt, buf + 64, s, t->scan_tune), "scan");
     return buf + 64;
 }
 
@@ -418,11 +418,13 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         // [aborted] go down in one copy; [counts][aborted] come back in one copy
         auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
         const uint64_t q_map = 0, q_rq = q_map + al((kMapKeys + 1) * 4ull), q_cn = q_rq + al(nq * 4ull),
-                       q_ab = q_cn + 16, q_end = q_ab + al(nq * 4ull);
+                       q_ab = q_cn + 16, q_zero = q_ab + al(nq * 4ull), q_end = q_zero + 16;
         uint8_t *pq = pinned_bytes(stock->dev, q_end, 2);
         std::memcpy(pq + q_map, map_off, (kMapKeys + 1) * 4ull);
         std::memcpy(pq + q_rq, rq, nq * 4ull);
         std::memset(pq + q_cn, 0, 16 + nq * 4ull);
+        std::memset(pq + q_zero, 0, 16);  // the REGION / NATION scans' start key: 0 (:653, :734)
+        lap("staged");
         uint64_t off = 0;
         auto take = [&](uint64_t bytes) {
             const uint64_t o = off;
@@ -478,6 +480,7 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
             (void)hipGetLastError();  // a pageable pointer is not an error here
         }
         if (trace) std::fprintf(stderr, "[q2] out %s\n", host_out ? "page-locked: written by q2_finish" : "pageable: copied");
+        lap("buffers");
         // the scan rows' scratch sized before any capture (scan_rows asks for the same size again)
         (void)scratch_bytes(region->dev, 64 + (uint64_t)kRegionScan * region->dev.view.stride);
         (void)scratch_bytes(nation->dev, 64 + (uint64_t)kNationScan * nation->dev.view.stride);
@@ -490,8 +493,9 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
             hip_check(hipEventRecord(ev[0], s), "fork");
             hip_check(hipStreamWaitEvent(rs_s, ev[0], 0), "fork");
             hip_check(hipStreamWaitEvent(ns_s, ev[0], 0), "fork");
-            const uint8_t *regs = scan_rows(region, 0, kRegionScan, rs_s);
-            const uint8_t *nats = scan_rows(nation, 0, kNationScan, ns_s);
+            const auto *d_zero = (const uint64_t *)(mir + q_zero);
+            const uint8_t *regs = scan_rows(region, d_zero, kRegionScan, rs_s);
+            const uint8_t *nats = scan_rows(nation, d_zero, kNationScan, ns_s);
             hip_check(hipEventRecord(ev[1], rs_s), "join");
             hip_check(hipEventRecord(ev[2], ns_s), "join");
             hip_check(hipStreamWaitEvent(s, ev[1], 0), "join");
@@ -501,10 +505,8 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
                 q2_sel_count<<<(unsigned)((nchunks + 3) / 4), 256, 0, s>>>(
                     regs, region->dev.view.stride, nats, nation->dev.view.stride, name0, name1, mask0, mask1, pv,
                     facts(supplier).key_pad(), nchunks, g_vis, g_rank, g_key, ccnt, g_nv);
-                q2_sel_start<<<1, 1024, 0, s>>>(ccnt, nchunks, g_nv, d_counts);
-                q2_sel_place<<<(unsigned)((nslots + 255) / 256), 256, 0, s>>>(g_vis, g_rank, g_key, ccnt, nslots, d_map,
-                                                                               d_sel, d_src, d_cnt);
-                q2_sel_seg<<<1, 1024, 0, s>>>(d_cnt, d_dst, d_counts);
+                q2_sel_place<<<1, 1024, 0, s>>>(ccnt, nchunks, g_nv, g_vis, g_rank, g_key, d_map, d_sel, d_src,
+                                                d_cnt, d_dst, d_counts);
             }
             hip_check(hipGetLastError(), "select");
             // 3. every visited supplier's STOCK keys, one probe of them all (the counts on the device)
@@ -560,6 +562,7 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
                            (uint64_t)(uintptr_t)host_out, (uint64_t)(uintptr_t)pq, (uint64_t)(uintptr_t)buf, q_end,
                            n_max, m_max, n_hint, m_hint, (uint64_t)(uintptr_t)s})
             putv(v);
+        lap("key");
         Q2Graph &G = stock->q2g;
         bool launched = false;
         if (graphs && !G.failed) {
