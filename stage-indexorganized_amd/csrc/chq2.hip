@@ -204,11 +204,12 @@ __global__ __launch_bounds__(1024) void q2_sel_place(uint32_t *__restrict__ ccnt
     __shared__ uint32_t s_n;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
     const uint32_t nv = *g_nv;
-    // 1. starts
-    for (uint32_t v = wv; v < nv; v += nw) {  // a wave per visit: its total
+    // 1. starts.  A wave per visit, a lane per contiguous run of `per` chunks: every load of a
+    // pass is issued before its results are used
+    const uint64_t per = (nchunks + 63) / 64, c_lo = lane * per, c_hi = c_lo + per < nchunks ? c_lo + per : nchunks;
+    for (uint32_t v = wv; v < nv; v += nw) {  // the visit's total
         uint32_t t = 0;
-#pragma unroll 8
-        for (uint64_t c = lane; c < nchunks; c += 64) t += ccnt[c * kVisits + v];
+        for (uint64_t c = c_lo; c < c_hi; ++c) t += ccnt[c * kVisits + v];
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
         if (lane == 0) s_tot[v] = t;
@@ -225,44 +226,67 @@ __global__ __launch_bounds__(1024) void q2_sel_place(uint32_t *__restrict__ ccnt
         s_n = pos;
     }
     __syncthreads();
-    for (uint32_t v = wv; v < nv; v += nw) {  // a wave per visit: exclusive scan over the chunks
-        uint32_t carry = s_tot[v];
-        for (uint64_t c0 = 0; c0 < nchunks; c0 += 64) {
-            const uint64_t c = c0 + lane;
-            const uint32_t x = c < nchunks ? ccnt[c * kVisits + v] : 0u;
-            uint32_t y = x;
+    for (uint32_t v = wv; v < nv; v += nw) {  // exclusive scan over the chunks, in place
+        uint32_t x[16], t = 0;
+        if (per <= 16) {
 #pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t z = __shfl_up(y, o, 64);
-                if (lane >= (uint32_t)o) y += z;
+            for (int k = 0; k < 16; ++k) x[k] = c_lo + k < c_hi ? ccnt[(c_lo + k) * kVisits + v] : 0u;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) t += x[k];
+        } else {
+            for (uint64_t c = c_lo; c < c_hi; ++c) t += ccnt[c * kVisits + v];
+        }
+        uint32_t y = t;  // inclusive scan of the lanes' runs
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t z = __shfl_up(y, o, 64);
+            if (lane >= (uint32_t)o) y += z;
+        }
+        uint32_t pos = s_tot[v] + y - t;
+        if (per <= 16) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                if (c_lo + k < c_hi) {
+                    ccnt[(c_lo + k) * kVisits + v] = pos;
+                    pos += x[k];
+                }
+        } else {
+            for (uint64_t c = c_lo; c < c_hi; ++c) {
+                const uint32_t xc = ccnt[c * kVisits + v];
+                ccnt[c * kVisits + v] = pos;
+                pos += xc;
             }
-            if (c < nchunks) ccnt[c * kVisits + v] = carry + y - x;
-            carry += rl32(y, 63);
         }
     }
     __syncthreads();
-    // 2. placement, every slot independent
+    // 2. placement: a thread per 16 consecutive slots, their visits in one 16-B load, then the
+    // selected slots' rank / key / start loads side by side, then their map offsets
     const uint64_t nslots = nchunks * 64;
-#pragma unroll 4
-    for (uint64_t i = tid; i < nslots; i += 1024) {
-        const int v = g_vis[i];
-        if (v < 0) continue;
-        const uint32_t pos = ccnt[(i >> 6) * kVisits + v] + g_rank[i];
-        const uint64_t sk = g_key[i];
-        uint64_t s0 = 0, c = 0;
-        if (sk < 10000) {
-            const uint32_t a = map_off[sk], b = map_off[sk + 1];
-            s0 = a;
-            c = b > a ? b - a : 0;
+    for (uint64_t i0 = (uint64_t)tid * 16; i0 < nslots; i0 += 1024 * 16) {
+        const uint4 vv = *reinterpret_cast<const uint4 *>(g_vis + i0);
+        const uint32_t vw[4] = {vv.x, vv.y, vv.z, vv.w};
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int v = (int8_t)(vw[k >> 2] >> (8 * (k & 3)));
+            if (v < 0) continue;
+            const uint64_t i = i0 + k;
+            const uint32_t pos = ccnt[(i >> 6) * kVisits + v] + g_rank[i];
+            const uint64_t sk = g_key[i];
+            uint64_t s0 = 0, c = 0;
+            if (sk < 10000) {
+                const uint32_t a = map_off[sk], b = map_off[sk + 1];
+                s0 = a;
+                c = b > a ? b - a : 0;
+            }
+            sel[pos] = sk;
+            src[pos] = s0;
+            cnt[pos] = (uint32_t)c;
         }
-        sel[pos] = sk;
-        src[pos] = s0;
-        cnt[pos] = (uint32_t)c;
     }
     __syncthreads();
     // 3. segment offsets: each thread a contiguous run, one block scan
     const uint64_t n = s_n;
-    const uint64_t per = (n + 1023) / 1024, lo = tid * per, hi = lo + per < n ? lo + per : n;
+    const uint64_t run = (n + 1023) / 1024, lo = tid * run, hi = lo + run < n ? lo + run : n;
     uint64_t own = 0;
     for (uint64_t i = lo; i < hi; ++i) own += cnt[i];
     uint64_t x = own;
