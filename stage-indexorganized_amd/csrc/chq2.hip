@@ -75,11 +75,13 @@ __global__ void q2_gather(const uint64_t *__restrict__ map_keys, const uint64_t 
 //              keys unique), so at most kNationScan visits;
 //   sel      = every SUPPLIER record of each visited nation, visit by visit, in slot order: a
 //              stable counting sort by visit over 64-slot chunks --
-//                q2_sel_count  (a wave per chunk) the visits, each slot's visit and rank among
-//                              its chunk's slots of that visit, the chunk's count per visit;
-//                q2_sel_place  (one block) each (chunk, visit)'s start (visit-major, then chunk),
-//                              sel[start + rank] with the supplier's map segment, and dst =
-//                              the exclusive prefix of the segment lengths;
+//                q2_sel_count  (a wave per chunk) the visits, each slot's visit, its rank and its
+//                              map entries' offset among its chunk's slots of that visit, the
+//                              chunk's supplier and entry counts per visit;
+//                q2_sel_start  (one block) each (chunk, visit)'s supplier and entry starts:
+//                              visit-major, then chunk;
+//                q2_sel_place  (a lane per slot) sel[start + rank], the supplier's map segment
+//                              (src, cnt) and its first STOCK key (dst = entry start + offset);
 //   counts   = {suppliers, stock keys}.
 // Every block derives the visits itself from the (L2-resident) scan rows, so no launch is spent
 // on them; no loop waits on one global load per iteration.
@@ -152,19 +154,21 @@ __device__ __forceinline__ int visit_of(const VisitMap &vm, uint64_t nat) {
 __global__ __launch_bounds__(256) void q2_sel_count(const uint8_t *__restrict__ regs, uint32_t rs,
                                                     const uint8_t *__restrict__ nats, uint32_t ns, uint64_t name0,
                                                     uint64_t name1, uint64_t mask0, uint64_t mask1, DevTable t,
-                                                    uint32_t kpad, uint64_t nchunks, int8_t *__restrict__ g_vis,
-                                                    uint8_t *__restrict__ g_rank, uint64_t *__restrict__ g_key,
-                                                    uint32_t *__restrict__ ccnt, uint32_t *__restrict__ g_nv) {
+                                                    uint32_t kpad, uint64_t nchunks, const uint32_t *__restrict__ map_off,
+                                                    int8_t *__restrict__ g_vis, uint8_t *__restrict__ g_rank,
+                                                    uint32_t *__restrict__ g_koff, uint64_t *__restrict__ g_key,
+                                                    uint32_t *__restrict__ ccnt, uint32_t *__restrict__ kcnt,
+                                                    uint32_t *__restrict__ g_nv) {
     __shared__ VisitMap vm;
     __shared__ uint8_t s_rmatch[kRegionScan];
     __shared__ uint8_t s_flag[kRegionScan * kNationScan];
-    __shared__ uint32_t s_cnt[4][kVisits];
+    __shared__ uint32_t s_cnt[4][kVisits], s_kcnt[4][kVisits];
     build_visits(vm, regs, rs, nats, ns, name0, name1, mask0, mask1, s_rmatch, s_flag);
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     if (blockIdx.x == 0 && threadIdx.x == 0) *g_nv = vm.nv;
     const uint64_t c = (uint64_t)blockIdx.x * 4 + wv;
     if (c >= nchunks) return;
-    for (uint32_t v = lane; v < (uint32_t)kVisits; v += 64) s_cnt[wv][v] = 0;
+    for (uint32_t v = lane; v < (uint32_t)kVisits; v += 64) s_cnt[wv][v] = 0, s_kcnt[wv][v] = 0;
     const uint64_t i = c * 64 + lane;
     const SlotInfo si = t.slot[i];
     uint64_t key = ~0ull;
@@ -174,136 +178,137 @@ __global__ __launch_bounds__(256) void q2_sel_count(const uint8_t *__restrict__ 
         key = *reinterpret_cast<const uint64_t *>(row);
         v = key == ~0ull ? -1 : visit_of(vm, *reinterpret_cast<const uint64_t *>(row + kpad));
     }
-    uint32_t rank = 0;
+    uint32_t mc = 0;  // the supplier's supp_stock_map entries (keys below 10000)
+    if (v >= 0 && key < 10000) {
+        const uint32_t a = map_off[key], b = map_off[key + 1];
+        mc = b > a ? b - a : 0;
+    }
+    // per visit present in the chunk: each slot's rank and its entries' offset among the
+    // chunk's slots of that visit, the visit's supplier and entry counts
+    uint32_t rank = 0, koff = 0;
     uint64_t todo = ballot(v >= 0);
     while (todo) {
         const int vl = (int)rl32((uint32_t)v, (int)__builtin_ctzll(todo));
-        const uint64_t mm = ballot(v == vl);
-        if (v == vl) rank = (uint32_t)__builtin_popcountll(mm & ((1ull << lane) - 1));
-        if (lane == 0) s_cnt[wv][vl] = (uint32_t)__builtin_popcountll(mm);
-        todo &= ~mm;
-    }
-    g_vis[i] = (int8_t)v;
-    g_rank[i] = (uint8_t)rank;
-    g_key[i] = key;
-    for (uint32_t w = lane; w < (uint32_t)kVisits; w += 64) ccnt[c * kVisits + w] = s_cnt[wv][w];
-}
-
-// one block, after q2_sel_count: (1) ccnt[c][v] counts -> starts, in place (visit-major, then
-// chunk order); (2) every selected supplier at start + rank with its supp_stock_map segment
-// (src, cnt); (3) dst = exclusive prefix of the segment lengths; counts = {suppliers, stock keys}
-__global__ __launch_bounds__(1024) void q2_sel_place(uint32_t *__restrict__ ccnt, uint64_t nchunks,
-                                                     const uint32_t *__restrict__ g_nv, const int8_t *__restrict__ g_vis,
-                                                     const uint8_t *__restrict__ g_rank,
-                                                     const uint64_t *__restrict__ g_key, const uint32_t *__restrict__ map_off,
-                                                     uint64_t *__restrict__ sel, uint64_t *__restrict__ src,
-                                                     uint32_t *__restrict__ cnt, uint64_t *__restrict__ dst,
-                                                     uint64_t *__restrict__ counts) {
-    __shared__ uint32_t s_tot[kVisits];
-    __shared__ uint64_t s_wsum[16];
-    __shared__ uint32_t s_n;
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
-    const uint32_t nv = *g_nv;
-    // 1. starts.  A wave per visit, a lane per contiguous run of `per` chunks: every load of a
-    // pass is issued before its results are used
-    const uint64_t per = (nchunks + 63) / 64, c_lo = lane * per, c_hi = c_lo + per < nchunks ? c_lo + per : nchunks;
-    for (uint32_t v = wv; v < nv; v += nw) {  // the visit's total
-        uint32_t t = 0;
-        for (uint64_t c = c_lo; c < c_hi; ++c) t += ccnt[c * kVisits + v];
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
-        if (lane == 0) s_tot[v] = t;
-    }
-    __syncthreads();
-    if (tid == 0) {
-        uint32_t pos = 0;
-        for (uint32_t v = 0; v < nv; ++v) {
-            const uint32_t t = s_tot[v];
-            s_tot[v] = pos;
-            pos += t;
-        }
-        counts[0] = pos;
-        s_n = pos;
-    }
-    __syncthreads();
-    for (uint32_t v = wv; v < nv; v += nw) {  // exclusive scan over the chunks, in place
-        uint32_t x[16], t = 0;
-        if (per <= 16) {
-#pragma unroll
-            for (int k = 0; k < 16; ++k) x[k] = c_lo + k < c_hi ? ccnt[(c_lo + k) * kVisits + v] : 0u;
-#pragma unroll
-            for (int k = 0; k < 16; ++k) t += x[k];
-        } else {
-            for (uint64_t c = c_lo; c < c_hi; ++c) t += ccnt[c * kVisits + v];
-        }
-        uint32_t y = t;  // inclusive scan of the lanes' runs
+        const bool in = v == vl;
+        const uint64_t mm = ballot(in);
+        const uint32_t x = in ? mc : 0u;
+        uint32_t y = x;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const uint32_t z = __shfl_up(y, o, 64);
             if (lane >= (uint32_t)o) y += z;
         }
-        uint32_t pos = s_tot[v] + y - t;
-        if (per <= 16) {
+        if (in) {
+            rank = (uint32_t)__builtin_popcountll(mm & ((1ull << lane) - 1));
+            koff = y - x;
+        }
+        const uint32_t ktot = rl32(y, 63);
+        if (lane == 0) {
+            s_cnt[wv][vl] = (uint32_t)__builtin_popcountll(mm);
+            s_kcnt[wv][vl] = ktot;
+        }
+        todo &= ~mm;
+    }
+    g_vis[i] = (int8_t)v;
+    g_rank[i] = (uint8_t)rank;
+    g_koff[i] = koff;
+    g_key[i] = key;
+    for (uint32_t w = lane; w < (uint32_t)kVisits; w += 64) {
+        ccnt[c * kVisits + w] = s_cnt[wv][w];
+        kcnt[c * kVisits + w] = s_kcnt[wv][w];
+    }
+}
+
+// one block, after q2_sel_count: the (chunk, visit) supplier counts ccnt and entry counts kcnt ->
+// their starts, in place (visit-major, then chunk order); counts = {suppliers, stock keys}.  A
+// wave per visit, a lane per contiguous run of chunks: every load of a pass issued first.
+__global__ __launch_bounds__(1024) void q2_sel_start(uint32_t *__restrict__ ccnt, uint32_t *__restrict__ kcnt,
+                                                     uint64_t nchunks, const uint32_t *__restrict__ g_nv,
+                                                     uint64_t *__restrict__ counts) {
+    __shared__ uint32_t s_tot[2][kVisits];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
+    const uint32_t nv = *g_nv;
+    const uint64_t per = (nchunks + 63) / 64, c_lo = lane * per, c_hi = c_lo + per < nchunks ? c_lo + per : nchunks;
+    uint32_t *arr[2] = {ccnt, kcnt};
+    for (uint32_t v = wv; v < nv; v += nw)
+        for (int a = 0; a < 2; ++a) {  // the visit's totals
+            uint32_t t = 0;
+            for (uint64_t c = c_lo; c < c_hi; ++c) t += arr[a][c * kVisits + v];
 #pragma unroll
-            for (int k = 0; k < 16; ++k)
-                if (c_lo + k < c_hi) {
-                    ccnt[(c_lo + k) * kVisits + v] = pos;
-                    pos += x[k];
+            for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+            if (lane == 0) s_tot[a][v] = t;
+        }
+    __syncthreads();
+    if (tid < 2) {
+        uint32_t pos = 0;
+        for (uint32_t v = 0; v < nv; ++v) {
+            const uint32_t t = s_tot[tid][v];
+            s_tot[tid][v] = pos;
+            pos += t;
+        }
+        counts[tid] = pos;
+    }
+    __syncthreads();
+    for (uint32_t v = wv; v < nv; v += nw)
+        for (int a = 0; a < 2; ++a) {  // exclusive scan over the chunks, in place
+            uint32_t *A = arr[a];
+            uint32_t x[16], t = 0;
+            if (per <= 16) {
+#pragma unroll
+                for (int k = 0; k < 16; ++k) x[k] = c_lo + k < c_hi ? A[(c_lo + k) * kVisits + v] : 0u;
+#pragma unroll
+                for (int k = 0; k < 16; ++k) t += x[k];
+            } else {
+                for (uint64_t c = c_lo; c < c_hi; ++c) t += A[c * kVisits + v];
+            }
+            uint32_t y = t;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t z = __shfl_up(y, o, 64);
+                if (lane >= (uint32_t)o) y += z;
+            }
+            uint32_t pos = s_tot[a][v] + y - t;
+            if (per <= 16) {
+#pragma unroll
+                for (int k = 0; k < 16; ++k)
+                    if (c_lo + k < c_hi) {
+                        A[(c_lo + k) * kVisits + v] = pos;
+                        pos += x[k];
+                    }
+            } else {
+                for (uint64_t c = c_lo; c < c_hi; ++c) {
+                    const uint32_t xc = A[c * kVisits + v];
+                    A[c * kVisits + v] = pos;
+                    pos += xc;
                 }
-        } else {
-            for (uint64_t c = c_lo; c < c_hi; ++c) {
-                const uint32_t xc = ccnt[c * kVisits + v];
-                ccnt[c * kVisits + v] = pos;
-                pos += xc;
             }
         }
+}
+
+// a lane per slot: each selected supplier at its place, with its supp_stock_map segment (src,
+// cnt) and the segment's offset among all looked-up STOCK keys (dst)
+__global__ void q2_sel_place(const uint32_t *__restrict__ ccnt, const uint32_t *__restrict__ kcnt, uint64_t nslots,
+                             const int8_t *__restrict__ g_vis, const uint8_t *__restrict__ g_rank,
+                             const uint32_t *__restrict__ g_koff, const uint64_t *__restrict__ g_key,
+                             const uint32_t *__restrict__ map_off, uint64_t *__restrict__ sel,
+                             uint64_t *__restrict__ src, uint32_t *__restrict__ cnt, uint64_t *__restrict__ dst) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nslots) return;
+    const int v = g_vis[i];
+    if (v < 0) return;
+    const uint64_t g = (i >> 6) * kVisits + v;
+    const uint32_t pos = ccnt[g] + g_rank[i];
+    const uint64_t sk = g_key[i];
+    uint64_t s0 = 0, c = 0;
+    if (sk < 10000) {
+        const uint32_t a = map_off[sk], b = map_off[sk + 1];
+        s0 = a;
+        c = b > a ? b - a : 0;
     }
-    __syncthreads();
-    // 2. placement: a thread per 16 consecutive slots, their visits in one 16-B load, then the
-    // selected slots' rank / key / start loads side by side, then their map offsets
-    const uint64_t nslots = nchunks * 64;
-    for (uint64_t i0 = (uint64_t)tid * 16; i0 < nslots; i0 += 1024 * 16) {
-        const uint4 vv = *reinterpret_cast<const uint4 *>(g_vis + i0);
-        const uint32_t vw[4] = {vv.x, vv.y, vv.z, vv.w};
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const int v = (int8_t)(vw[k >> 2] >> (8 * (k & 3)));
-            if (v < 0) continue;
-            const uint64_t i = i0 + k;
-            const uint32_t pos = ccnt[(i >> 6) * kVisits + v] + g_rank[i];
-            const uint64_t sk = g_key[i];
-            uint64_t s0 = 0, c = 0;
-            if (sk < 10000) {
-                const uint32_t a = map_off[sk], b = map_off[sk + 1];
-                s0 = a;
-                c = b > a ? b - a : 0;
-            }
-            sel[pos] = sk;
-            src[pos] = s0;
-            cnt[pos] = (uint32_t)c;
-        }
-    }
-    __syncthreads();
-    // 3. segment offsets: each thread a contiguous run, one block scan
-    const uint64_t n = s_n;
-    const uint64_t run = (n + 1023) / 1024, lo = tid * run, hi = lo + run < n ? lo + run : n;
-    uint64_t own = 0;
-    for (uint64_t i = lo; i < hi; ++i) own += cnt[i];
-    uint64_t x = own;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint64_t y = __shfl_up(x, o, 64);
-        if (lane >= (uint32_t)o) x += y;
-    }
-    if (lane == 63) s_wsum[wv] = x;
-    __syncthreads();
-    uint64_t before = x - own;
-    for (uint32_t w = 0; w < wv; ++w) before += s_wsum[w];
-    for (uint64_t i = lo; i < hi; ++i) {
-        dst[i] = before;
-        before += cnt[i];
-    }
-    if (tid == 1023) counts[1] = before;
+    sel[pos] = sk;
+    src[pos] = s0;
+    cnt[pos] = (uint32_t)c;
+    dst[pos] = (uint64_t)kcnt[g] + g_koff[i];
 }
 
 // thread per (query q, supplier s): the abort for a stock lookup that produced no tuple is already
@@ -460,8 +465,9 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
                        o_keys = take(std::max<uint64_t>(m_max, 1) * 16), o_sbase = take(std::max<uint64_t>(m_max, 1) * 32),
                        o_slast = take(n_max * 32 * nq), o_ik = take(n_max * 8 * nq), o_iout = take(n_max * 32 * nq),
                        o_ibase = take(n_max * 32), o_rec = take(n_max * nq * sizeof(stage_q2_rec)),
-                       o_vis = take(n_max), o_rank = take(n_max), o_ccnt = take(std::max<uint64_t>(nchunks, 1) * kVisits * 4),
-                       o_nv = take(4);
+                       o_vis = take(n_max), o_rank = take(n_max), o_koff = take(n_max * 4),
+                       o_ccnt = take(std::max<uint64_t>(nchunks, 1) * kVisits * 4),
+                       o_kcnt = take(std::max<uint64_t>(nchunks, 1) * kVisits * 4), o_nv = take(4);
         // the SUPPLIER table's scratch: REGION's and NATION's hold their scan rows (scan_rows)
         uint8_t *buf = scratch_bytes(supplier->dev, off), *mir = buf + o_mir;
         auto *d_map = (const uint32_t *)(mir + q_map);
@@ -489,7 +495,8 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         auto *g_key = (uint64_t *)(buf + o_pairs);
         auto *g_vis = (int8_t *)(buf + o_vis);
         auto *g_rank = (uint8_t *)(buf + o_rank);
-        auto *ccnt = (uint32_t *)(buf + o_ccnt);
+        auto *ccnt = (uint32_t *)(buf + o_ccnt), *kcnt = (uint32_t *)(buf + o_kcnt);
+        auto *g_koff = (uint32_t *)(buf + o_koff);
         auto *g_nv = (uint32_t *)(buf + o_nv);
         // `out` in page-locked memory (stage_host_alloc, stage.pinned_empty): the finishing kernel
         // writes the records into it directly; otherwise they are copied once the count is known
@@ -528,9 +535,10 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
             if (nchunks) {
                 q2_sel_count<<<(unsigned)((nchunks + 3) / 4), 256, 0, s>>>(
                     regs, region->dev.view.stride, nats, nation->dev.view.stride, name0, name1, mask0, mask1, pv,
-                    facts(supplier).key_pad(), nchunks, g_vis, g_rank, g_key, ccnt, g_nv);
-                q2_sel_place<<<1, 1024, 0, s>>>(ccnt, nchunks, g_nv, g_vis, g_rank, g_key, d_map, d_sel, d_src,
-                                                d_cnt, d_dst, d_counts);
+                    facts(supplier).key_pad(), nchunks, d_map, g_vis, g_rank, g_koff, g_key, ccnt, kcnt, g_nv);
+                q2_sel_start<<<1, 1024, 0, s>>>(ccnt, kcnt, nchunks, g_nv, d_counts);
+                q2_sel_place<<<(unsigned)((nslots + 255) / 256), 256, 0, s>>>(ccnt, kcnt, nslots, g_vis, g_rank, g_koff,
+                                                                               g_key, d_map, d_sel, d_src, d_cnt, d_dst);
             }
             hip_check(hipGetLastError(), "select");
             // 3. every visited supplier's STOCK keys, one probe of them all (the counts on the device)
