@@ -1557,6 +1557,115 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void p
     }
 }
 
+// Point probes of the same instances as probe_split_kernel with a lane per probe throughout
+// (STAGE_PROBE_WIDE=2; leaves of up to 128 slots): each lane descends, loads its leaf head's
+// fingerprint bytes itself (SPL x 4 16-B loads, all in flight), finds its candidate slots in slot
+// order with byte-wise compares in registers, and confirms the first three candidates in up to
+// three rounds of loads that every lane of the wave issues together -- 64 probes' dependent
+// loads in flight per wave at every step instead of 4-16 (SearchRecordMeta's first hit; a probe
+// with more than three candidates falls back to a walk of the rest).  Then visibility() and the
+// rows, wave-wide, as probe_split_kernel.
+template <int SPL, int KW>
+__global__ __launch_bounds__(256) void probe_lane_kernel(DevTable t, const uint64_t *__restrict__ keys,
+                                                         const uint32_t *__restrict__ rids,
+                                                         const uint32_t *__restrict__ leaf_in, uint64_t n,
+                                                         stage_probe_out_dev *__restrict__ out,
+                                                         uint8_t *__restrict__ recs, const uint64_t *__restrict__ dn) {
+    static_assert(SPL <= 2, "head of at most 128 slots in registers");
+    if (dn) n = *dn < n ? *dn : n;
+    const uint32_t lane = lane_id(), wv = uni32(threadIdx.x >> 6);
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint32_t out_chunks = t.stride >> 4;
+    const uint32_t len = t.key_width;
+    for (uint64_t base = wave * 64; base < n; base += nwaves * 64) {
+        const uint64_t i = base + lane;
+        const bool valid = i < n;
+        const uint32_t rid = rids ? (valid ? rids[i] : 0u) : 0xFFFFFFFEu;
+        uint64_t ok[KW];
+        load_okey<KW>(keys, i, valid, len, ok);
+        uint32_t leaf = 0;
+        if (valid) leaf = leaf_in ? leaf_in[i] : resolve_leaf<false, KW>(t, ok, len, true);
+        if (leaf > t.nseps) leaf = t.nseps;
+        const uint32_t rep = (key_fp_words(ok, KW) & 0xFFu) * 0x01010101u;
+        // the head: fingerprint byte j = slot j
+        u32x4 hv[SPL * 4];
+        const u32x4 *hp = reinterpret_cast<const u32x4 *>(t.head + (uint64_t)leaf * t.head_bytes);
+#pragma unroll
+        for (int q = 0; q < SPL * 4; ++q) hv[q] = valid ? hp[q] : u32x4{0, 0, 0, 0};
+        // candidates in slot order: the first three kept, the count of all
+        uint32_t c0 = 0, c1 = 0, c2 = 0, nc = 0;
+#pragma unroll
+        for (int q = 0; q < SPL * 4; ++q) {
+            const uint32_t wq[4] = {hv[q].x, hv[q].y, hv[q].z, hv[q].w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const uint32_t w = wq[e] ^ rep;
+                uint32_t zm = ~(((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w) & 0x80808080u;  // bytes equal to the fingerprint
+                while (zm) {
+                    const uint32_t sl = (uint32_t)(q * 16 + e * 4) + ((uint32_t)__builtin_ctz(zm) >> 3);
+                    c0 = nc == 0 ? sl : c0;
+                    c1 = nc == 1 ? sl : c1;
+                    c2 = nc == 2 ? sl : c2;
+                    ++nc;
+                    zm &= zm - 1;
+                }
+            }
+        }
+        if (!valid) nc = 0;
+        int slot = -1;
+        uint64_t m = 0;
+        uint32_t nx = 0, im = 0;
+        const uint64_t lb = (uint64_t)leaf * t.cap;
+        auto confirm = [&](uint32_t sl) {
+            const u32x4 *w = reinterpret_cast<const u32x4 *>(t.slot + lb + sl);
+            const u32x4 w0 = w[0], w1 = w[1];
+            bool eq = (((uint64_t)w0.y << 32) | w0.x) == ok[0];
+#pragma unroll
+            for (int k = 1; k < KW; ++k) eq = eq && t.okey[((uint64_t)leaf * KW + k) * t.cap + sl] == ok[k];
+            if (eq) {
+                slot = (int)sl;
+                m = ((uint64_t)w0.w << 32) | w0.z;
+                nx = w1.x;
+                im = w1.y;
+            }
+            return eq;
+        };
+        // rounds: every lane still looking confirms its next candidate, the loads together
+        if (nc > 0) confirm(c0);
+        if (slot < 0 && nc > 1) confirm(c1);
+        if (slot < 0 && nc > 2) confirm(c2);
+        if (slot < 0 && nc > 3) {  // rare: walk the rest of the head in slot order
+            const uint8_t *h = t.head + (uint64_t)leaf * t.head_bytes;
+            const uint8_t fx = (uint8_t)rep;
+            for (uint32_t sl = c2 + 1; sl < t.cap; ++sl)
+                if (h[sl] == fx && confirm(sl)) break;
+        }
+        ProbeRes r;
+        visibility(t, slot, m, nx, im, rid, r);
+        if (recs) {  // rows: wave-wide, probe by probe
+            const int cnt = (int)((n - base) < 64 ? (n - base) : 64);
+            for (int j = 0; j < cnt; ++j) {
+                const uint32_t img = rl32(r.image, j);
+                for (uint32_t cc0 = 0; cc0 < out_chunks; cc0 += 64) {
+                    const uint32_t c = cc0 + lane;
+                    if (c >= out_chunks) continue;
+                    u32x4 v = u32x4{0, 0, 0, 0};
+                    if (img != 0xFFFFFFFFu) v = reinterpret_cast<const u32x4 *>(t.heap + (uint64_t)img * t.hstride)[c];
+                    st16<1>(v, recs + (base + j) * (uint64_t)t.stride, c * 16u);
+                }
+            }
+        }
+        if (valid) {
+            u32x4 a, b;
+            pack_out(leaf, r, a, b);
+            uint8_t *ob = reinterpret_cast<uint8_t *>(out + base);
+            st16<1>(a, ob, lane * 32u);
+            st16<1>(b, ob, lane * 32u + 16u);
+        }
+    }
+}
+
 // Chunk-cooperative lower bound of kFirstChunk fixed-width start keys: lane L works for scan
 // L/4 and compares a quarter of each node (4 of the 16 inner entries, 2 of the 8 bottom ones);
 // two xor-shuffles sum the quarter counts.  Same result as tree_lower_bound (le_child = true),
@@ -2827,10 +2936,13 @@ hipError_t launch_probe(const DevTable &t, const uint64_t *keys, const uint16_t 
         const uint64_t sn = d_n && shape_n ? std::min(shape_n, n) : n;
         const bool small = (sn + 63) / 64 < (uint64_t)tune.small_below;  // fewer 64-probe chunks than the chip holds waves
         const int wblocks = small ? grid_for((sn + 15) / 16, 4, tune.max_blocks > 0 ? tune.max_blocks : 16384) : blocks;
-        // default: probe_split_kernel; STAGE_PROBE_WIDE=1: probe_kernel's one-probe-in-flight form
+        // default: probe_split_kernel; STAGE_PROBE_WIDE=1: probe_kernel's one-probe-in-flight form;
+        // STAGE_PROBE_WIDE=2: probe_lane_kernel for leaves of up to 128 slots
         const bool split = tune.wide != 1 && tune.status_bytes != 16;
 #define STAGE_PROBE_W(S, KW)                                                                                  \
-    if (split && small)                                                                                       \
+    if (tune.wide == 2 && S <= 2 && tune.status_bytes != 16)                                                   \
+        probe_lane_kernel<(S <= 2 ? S : 2), KW><<<blocks, 256, 0, s>>>(t, keys, rids, leaf_in, n, out, recs, d_n); \
+    else if (split && small)                                                                                  \
         probe_split_kernel<S, KW, 16><<<wblocks, 256, 0, s>>>(t, keys, rids, leaf_in, n, out, recs, d_n);      \
     else if (split)                                                                                           \
         probe_split_kernel<S, KW, 64><<<blocks, 256, 0, s>>>(t, keys, rids, leaf_in, n, out, recs, d_n);       \
