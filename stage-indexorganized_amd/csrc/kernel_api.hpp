@@ -26,7 +26,8 @@ struct ProbeTuning {
     int max_blocks = 0;    // 0 = default grid cap (16384 blocks of 256 threads)
     int store = 1;         // output stores: 0 temporal, 1 nontemporal, 2 write-through (sc1)
     int status_bytes = 32; // status record: 32 (stage_probe_out) or 16 (stage_probe_out16)
-    int wide = 0;          // wide-key / large-leaf probes: 0 = probe_split_kernel, 1 = probe_kernel<.., G = 1>
+    int wide = 0;          // wide-key / large-leaf probes: 0 = probe_lane_kernel up to 256 slots per leaf, else
+                           // probe_split_kernel; 1 = probe_kernel<.., G = 1>; 3 = probe_split_kernel always
     int small_below = 16384;  // wide-key probes: 16-probe wave chunks below this many 64-probe chunks
 };
 

@@ -1558,7 +1558,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void p
 }
 
 // Point probes of the same instances as probe_split_kernel with a lane per probe throughout
-// (STAGE_PROBE_WIDE=2; leaves of up to 256 slots): each lane descends, loads its leaf head's
+// (the default for leaves of up to 256 slots): each lane descends, loads its leaf head's
 // fingerprint bytes itself (SPL x 4 16-B loads, all in flight), finds its candidate slots in slot
 // order with byte-wise compares in registers, and confirms the first three candidates in up to
 // three rounds of loads that every lane of the wave issues together -- 64 probes' dependent
@@ -2936,11 +2936,11 @@ hipError_t launch_probe(const DevTable &t, const uint64_t *keys, const uint16_t 
         const uint64_t sn = d_n && shape_n ? std::min(shape_n, n) : n;
         const bool small = (sn + 63) / 64 < (uint64_t)tune.small_below;  // fewer 64-probe chunks than the chip holds waves
         const int wblocks = small ? grid_for((sn + 15) / 16, 4, tune.max_blocks > 0 ? tune.max_blocks : 16384) : blocks;
-        // default: probe_split_kernel; STAGE_PROBE_WIDE=1: probe_kernel's one-probe-in-flight form;
-        // STAGE_PROBE_WIDE=2: probe_lane_kernel for leaves of up to 256 slots
+        // default: probe_lane_kernel for leaves of up to 256 slots, probe_split_kernel above;
+        // STAGE_PROBE_WIDE=1: probe_kernel's one-probe-in-flight form; =3: probe_split_kernel always
         const bool split = tune.wide != 1 && tune.status_bytes != 16;
 #define STAGE_PROBE_W(S, KW)                                                                                  \
-    if (tune.wide == 2 && S <= 4 && tune.status_bytes != 16)                                                   \
+    if (tune.wide != 3 && S <= 4 && split)                                                                    \
         probe_lane_kernel<(S <= 4 ? S : 4), KW><<<blocks, 256, 0, s>>>(t, keys, rids, leaf_in, n, out, recs, d_n); \
     else if (split && small)                                                                                  \
         probe_split_kernel<S, KW, 16><<<wblocks, 256, 0, s>>>(t, keys, rids, leaf_in, n, out, recs, d_n);      \
