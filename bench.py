@@ -1369,7 +1369,9 @@ def c3_leg(tab, args, stream, nthreads, steps, warmup):
     rows = d_rec.to_numpy(np.uint8, ns * tab.stride).reshape(ns, tab.stride)
     st = last["d"]["out"].to_numpy(stage.PROBE_OUT_DTYPE, ns)["status"]
     check_sample = (last["reads"][:ns].copy(), last["rids"][:ns].copy(), st, rows)
-    ok = bool(hist[stage.ST_LATEST] > 0 and hist[stage.ST_OLD] > 0 and hist[stage.ST_COPY] > 0)
+    # every outcome the read-id model produces occurred (no OLD reads when every read is at the
+    # newest id: --old-share 0)
+    ok = bool(hist[stage.ST_LATEST] > 0 and hist[stage.ST_COPY] > 0 and (hist[stage.ST_OLD] > 0 or args.old_share == 0))
     per_unit = BYTES_PER_LOOKUP + HOP_BYTES * mean_hops
     # value: the YCSB-B ops/s of configs[2] -- reads and successful updates over the whole loop
     # (write path + probes); reads_per_s: the read probes alone (their stream time), the figure
