@@ -915,11 +915,22 @@ static void peer_exchange(ShardComm &c, hipStream_t s) {
                                 : std::string("another rank could not map the row buffers")));
 }
 
+// A system-scope acquire on every XCD (256 one-wave workgroups land on all 8): the peers' row
+// buffers are mapped non-coherently, so a line this device's L2 kept from an earlier call with
+// the same buffer parity could be stale; `buffer_inv sc0 sc1` drops such lines before the
+// fan-out reads the rows the owners wrote since (their kernels' end released them to memory,
+// and the status records that precede this fan-out were sent after those kernels).
+__global__ void peer_acquire_kernel() {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate has completed
+}
+
 // peer reply, chunk i: the status records that came back from every other rank, with each row read
 // where its owner left it (peer_row) and stored at the caller positions
 static void chunk_return_peer(ShardComm &c, const Plan &P, const PeerCounts &pc, int i, uint32_t stride,
                               stage_probe_out_dev *d_out, uint8_t *d_recs, hipStream_t s) {
     const int W = P.W, me = c.rank;
+    peer_acquire_kernel<<<256, 64, 0, s>>>();
     const stage_probe_out_dev *bout = (const stage_probe_out_dev *)c.bout;
     for (int q = 0; q < W; ++q) {
         if (q == me) continue;  // own requests: probed straight to their caller positions
