@@ -880,8 +880,19 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
             reserve_device_rows(h, dv, 8 * n, 8 * n, 8 * n, s);
         }
         const double t_reserve = ms(t0);
-        if (t->wp_overlap && !dv.wp_stream)
-            hip_check(hipStreamCreateWithFlags(&dv.wp_stream, hipStreamNonBlocking), "write stream");
+        if (t->wp_overlap && !dv.wp_stream) {
+            // STAGE_WP_PRIO=1: the overlapped write kernels on a high-priority stream, so their
+            // workgroups are dispatched as the probe's retire instead of after all of them
+            static const bool prio = [] {
+                const char *e = std::getenv("STAGE_WP_PRIO");
+                return e && std::atoi(e) == 1;
+            }();
+            int lo = 0, hi = 0;
+            if (prio) hip_check(hipDeviceGetStreamPriorityRange(&lo, &hi), "stream priorities");
+            hip_check(prio ? hipStreamCreateWithPriority(&dv.wp_stream, hipStreamNonBlocking, hi)
+                           : hipStreamCreateWithFlags(&dv.wp_stream, hipStreamNonBlocking),
+                      "write stream");
+        }
         for (hipEvent_t *e : {&dv.wp_pub_ev, &dv.wp_pre_ev})
             if (!*e) hip_check(hipEventCreateWithFlags(e, hipEventDisableTiming), "write event");
         if (!dv.adopt_stream) {  // high priority: the export gets its CUs beside the next probe
