@@ -889,30 +889,10 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
                 return !(e && std::atoi(e) == 0);
             }();
             int lo = 0, hi = 0;
-            // STAGE_WP_CUS=N (experiment): the write stream limited to N CUs, spread over the
-            // XCDs (CU i of XCD x = bit 32 x + i), in place of the priority
-            static const int cus = [] {
-                const char *e = std::getenv("STAGE_WP_CUS");
-                return e ? std::atoi(e) : 0;
-            }();
-            hipDeviceProp_t prop;
-            hip_check(hipGetDeviceProperties(&prop, dv.device), "device properties");
-            const int ncu = prop.multiProcessorCount, nx = ncu >= 256 ? 8 : 1;
-            if (cus > 0 && cus < ncu) {
-                std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-                for (int x = 0; x < nx; ++x)
-                    for (int k = 0; k < cus / nx; ++k) {
-                        const int b = x * (ncu / nx) + k;
-                        mask[b / 32] |= 1u << (b % 32);
-                    }
-                hip_check(hipExtStreamCreateWithCUMask(&dv.wp_stream, (uint32_t)mask.size(), mask.data()),
-                          "write stream (CU mask)");
-            } else {
-                if (prio) hip_check(hipDeviceGetStreamPriorityRange(&lo, &hi), "stream priorities");
-                hip_check(prio ? hipStreamCreateWithPriority(&dv.wp_stream, hipStreamNonBlocking, hi)
-                               : hipStreamCreateWithFlags(&dv.wp_stream, hipStreamNonBlocking),
-                          "write stream");
-            }
+            if (prio) hip_check(hipDeviceGetStreamPriorityRange(&lo, &hi), "stream priorities");
+            hip_check(prio ? hipStreamCreateWithPriority(&dv.wp_stream, hipStreamNonBlocking, hi)
+                           : hipStreamCreateWithFlags(&dv.wp_stream, hipStreamNonBlocking),
+                      "write stream");
         }
         for (hipEvent_t *e : {&dv.wp_pub_ev, &dv.wp_pre_ev})
             if (!*e) hip_check(hipEventCreateWithFlags(e, hipEventDisableTiming), "write event");
