@@ -161,8 +161,18 @@ int stage_settle(stage_table *t);
  * published, beside whatever the caller enqueued on `stream` after that (e.g. the previous
  * epoch's read probes); only the publish waits for `stream`.  Results are the same.  Contract:
  * the epoch's inputs (keys, deltas, ids) are complete when the call is made -- not produced by
- * work still pending on `stream`. */
+ * work still pending on `stream`.
+ * Mode 2 (deferred publish): stage_update_batch_device enqueues the epoch's kernels up to the
+ * publish and returns; the publish follows at stage_publish_epoch(t, stream) -- or at the next
+ * stage_update_batch_device, or at the first call that reads or writes the host table.  Probes
+ * enqueued in between see the table as it was before the epoch: a driver may prepare epoch e + 1
+ * before enqueuing epoch e's reads, so that e + 1's kernels reach the device first and run beside
+ * those reads, then publish it (n_ok != NULL publishes at once). */
 int stage_set_write_overlap(stage_table *t, int on);
+/* publishes the epoch that write-overlap mode 2 left prepared (a no-op when none is): its slot
+ * words on `stream` (NULL: the stream the epoch was prepared on) behind the work enqueued there,
+ * then the export and the host table's adoption (background) */
+int stage_publish_epoch(stage_table *t, void *stream);
 
 /* byte-key forms, for every key width a table takes: 1..8 bytes (key_width 1..8 or 0 =
  * variable) or a fixed width of 9..32 bytes (TPC-C composite keys, tpcc_record.h: int64

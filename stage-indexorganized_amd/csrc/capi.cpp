@@ -725,9 +725,20 @@ int stage_set_shard_dedupe(stage_table *t, int on) {
 }
 
 int stage_set_write_overlap(stage_table *t, int on) {
+    if (!t || on < 0 || on > 2) return fail(STAGE_E_ARG, "write overlap must be 0, 1 or 2");
+    return guarded([&] {
+        t->flush_publish(t->pending_stream);
+        t->wp_overlap = on;
+        return STAGE_OK;
+    });
+}
+
+int stage_publish_epoch(stage_table *t, void *stream) {
     if (!t) return fail(STAGE_E_ARG, "null table");
-    t->wp_overlap = on ? 1 : 0;
-    return STAGE_OK;
+    return guarded([&] {
+        t->flush_publish(stream ? (hipStream_t)stream : t->pending_stream);
+        return STAGE_OK;
+    });
 }
 
 int stage_set_shard_key_bits(stage_table *t, int bits) {

@@ -828,6 +828,9 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         const auto t0 = clk::now();
         static const auto g0 = t0;  // trace: the first call's start
         auto ms = [&](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
+        // a previous epoch prepared under write-overlap mode 2 and not yet published: publish it
+        // now (in stream order before this epoch)
+        t->flush_publish(s);
         // epoch e uses output buffers e % 2: epoch e - 2's adoption must be done with them
         const uint64_t epoch = ++t->wp_started;
         const int par = (int)(epoch & 1);
@@ -1058,93 +1061,111 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         // 5. write, 6. publish
         const int wblocks = (int)std::min<uint64_t>(blocks_for(n, 256 / kRowTeam), 32768);
         wp_write<<<wblocks, 256, 0, ks>>>(a, view, (uint8_t *)dv.heap.p, wrec, tot);
-        if (ks != s) {
-            hip_check(hipEventRecord(dv.wp_pre_ev, ks), "write event");
-            hip_check(hipStreamWaitEvent(s, dv.wp_pre_ev, 0), "publish wait");
-        }
-        wp_publish<<<blocks_for(n, 256), 256, 0, s>>>(a, (SlotInfo *)dv.slot.p, rcs, succ, prev, ranks, ls, tot, fin,
-                                                      d_rc);
-        hip_check(hipGetLastError(), "write-path kernels");
-        hip_check(hipEventRecord(dv.wp_pub_ev, s), "write event");  // the next epoch starts after it
-        dv.wp_pub_valid = true;
+        if (ks != s) hip_check(hipEventRecord(dv.wp_pre_ev, ks), "write event");
+        // the publish and everything after it (the slot words, the export to the host, the host
+        // table's adoption) -- now, or, under write-overlap mode 2, at the caller's
+        // stage_publish_epoch (or the next call that needs the epoch) on the stream it names
+        auto finish = [=, &h, &dv](hipStream_t s, bool want_n) -> uint64_t {
+            if (ks != s) hip_check(hipStreamWaitEvent(s, dv.wp_pre_ev, 0), "publish wait");
+            wp_publish<<<blocks_for(n, 256), 256, 0, s>>>(a, (SlotInfo *)dv.slot.p, rcs, succ, prev, ranks, ls, tot, fin,
+                                                          d_rc);
+            hip_check(hipGetLastError(), "write-path kernels");
+            hip_check(hipEventRecord(dv.wp_pub_ev, s), "write event");  // the next epoch starts after it
+            dv.wp_pub_valid = true;
 
-        // the host adopts the epoch.  The headers and slot words come back on a stream of their
-        // own into pinned staging (full PCIe rate) and the host adopts them on a background
-        // thread (stage_table::start_adoption) while the caller's stream goes on (the next probe
-        // -- and the next epoch's write path -- overlap the copies); the next call that needs the
-        // host table waits for it (host() / settle).
-        const double t_enqueue = ms(t0);
-        const double t_events = ms(t0);
-        hip_check(hipEventRecord(dv.adopt_ev[par], s), "adopt event");
-        auto *totals = reinterpret_cast<uint64_t *>(pin);
-        auto *fr = reinterpret_cast<FinRec *>(pin + 64 + bmax);
-        auto *writers = reinterpret_cast<const uint32_t *>(pin + 64 + bmax + bf);
-        const double t_pinned = ms(t0);
-        void *pin_dev = nullptr;
-        hip_check(hipHostGetDevicePointer(&pin_dev, pin, 0), "pinned device pointer");
-        hip_check(hipStreamWaitEvent(dv.adopt_stream, dv.adopt_ev[par], 0), "export wait");
-        static const int export_blocks = std::getenv("STAGE_WP_EXPORT_BLOCKS") ? std::atoi(std::getenv("STAGE_WP_EXPORT_BLOCKS")) : 32;
-        wp_export<<<export_blocks, 256, 0, dv.adopt_stream>>>(tot, fin, (const CopyHdr *)dv.chdr.p, (const VersionHdr *)dv.vhdr.p,
-                                                    cwriter, (uint8_t *)pin_dev, 64 + bmax, 64 + bmax + bf);
-        hip_check(hipGetLastError(), "export");
-        hip_check(hipEventRecord(dv.export_ev[par], dv.adopt_stream), "export event");
-        uint64_t ns = 0;
-        if (n_ok) {  // the caller wants the count now: wait for the kernels
-            uint64_t tv[2] = {0, 0};
-            hip_check(hipMemcpyAsync(tv, tot, 16, hipMemcpyDeviceToHost, s), "totals");
-            hip_check(hipStreamSynchronize(s), "write path");
-            ns = tv[0];
-        }
-        const double t_kernels = ms(t0);
-        // FinRec and HostTable::SlotWords share a layout: device slot locations become host slot
-        // indices in place (ops that published nothing keep ~0 and are skipped by the adoption)
-        static_assert(sizeof(FinRec) == sizeof(HostTable::SlotWords) &&
-                          offsetof(FinRec, meta) == offsetof(HostTable::SlotWords, meta) &&
-                          offsetof(FinRec, next) == offsetof(HostTable::SlotWords, next) &&
-                          offsetof(FinRec, image) == offsetof(HostTable::SlotWords, image),
-                      "FinRec / SlotWords layout");
-        t->start_adoption(epoch, [t, &h, &dv, par, epoch, cap = view.cap, n, pin, totals, fr, writers, t0, t_kernels, t_enqueue,
-                           t_reserve, t_events, t_pinned]() {
-            const double t_join = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
-            hip_check(hipSetDevice(dv.device), "hipSetDevice");
-            hip_check(hipEventSynchronize(dv.export_ev[par]), "adopt export");
-            const uint64_t ns = totals[0], nv = totals[1], cbase = totals[2], vbase = totals[3];
-            if (ns > n) throw std::runtime_error("write path: more successes than ops");
-            // the epochs are adopted in order: the host's counts are this epoch's bases
-            if (h.copies_.size() != cbase || h.versions_.size() != vbase || h.images_.size() != totals[4])
-                throw std::runtime_error("write path: device append counters disagree with the host table");
-            auto *copies = reinterpret_cast<CopyHdr *>(pin + 64);
-            auto *versions = reinterpret_cast<VersionHdr *>(pin + 64 + ns * sizeof(CopyHdr));
-            const double t_d2h = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
-            const std::vector<uint32_t> &d2h = dv.dev_to_host;
-            std::atomic<uint64_t> bad{0};
-            HostTable::parallel_chunks(ns, [&](uint64_t b, uint64_t e) {
-                for (uint64_t k = b; k < e; ++k) {
-                    if (fr[k].loc == ~0ull) continue;
-                    if (fr[k].loc / cap >= d2h.size()) {
-                        bad.fetch_add(1);
-                        fr[k].loc = ~0ull;
-                        continue;
+            // the host adopts the epoch.  The headers and slot words come back on a stream of their
+            // own into pinned staging (full PCIe rate) and the host adopts them on a background
+            // thread (stage_table::start_adoption) while the caller's stream goes on (the next probe
+            // -- and the next epoch's write path -- overlap the copies); the next call that needs the
+            // host table waits for it (host() / settle).
+            const double t_enqueue = ms(t0);
+            const double t_events = ms(t0);
+            hip_check(hipEventRecord(dv.adopt_ev[par], s), "adopt event");
+            auto *totals = reinterpret_cast<uint64_t *>(pin);
+            auto *fr = reinterpret_cast<FinRec *>(pin + 64 + bmax);
+            auto *writers = reinterpret_cast<const uint32_t *>(pin + 64 + bmax + bf);
+            const double t_pinned = ms(t0);
+            void *pin_dev = nullptr;
+            hip_check(hipHostGetDevicePointer(&pin_dev, pin, 0), "pinned device pointer");
+            hip_check(hipStreamWaitEvent(dv.adopt_stream, dv.adopt_ev[par], 0), "export wait");
+            static const int export_blocks = std::getenv("STAGE_WP_EXPORT_BLOCKS") ? std::atoi(std::getenv("STAGE_WP_EXPORT_BLOCKS")) : 32;
+            wp_export<<<export_blocks, 256, 0, dv.adopt_stream>>>(tot, fin, (const CopyHdr *)dv.chdr.p, (const VersionHdr *)dv.vhdr.p,
+                                                        cwriter, (uint8_t *)pin_dev, 64 + bmax, 64 + bmax + bf);
+            hip_check(hipGetLastError(), "export");
+            hip_check(hipEventRecord(dv.export_ev[par], dv.adopt_stream), "export event");
+            uint64_t ns = 0;
+            if (want_n) {  // the caller wants the count now: wait for the kernels
+                uint64_t tv[2] = {0, 0};
+                hip_check(hipMemcpyAsync(tv, tot, 16, hipMemcpyDeviceToHost, s), "totals");
+                hip_check(hipStreamSynchronize(s), "write path");
+                ns = tv[0];
+            }
+            const double t_kernels = ms(t0);
+            // FinRec and HostTable::SlotWords share a layout: device slot locations become host slot
+            // indices in place (ops that published nothing keep ~0 and are skipped by the adoption)
+            static_assert(sizeof(FinRec) == sizeof(HostTable::SlotWords) &&
+                              offsetof(FinRec, meta) == offsetof(HostTable::SlotWords, meta) &&
+                              offsetof(FinRec, next) == offsetof(HostTable::SlotWords, next) &&
+                              offsetof(FinRec, image) == offsetof(HostTable::SlotWords, image),
+                          "FinRec / SlotWords layout");
+            t->start_adoption(epoch, [t, &h, &dv, par, epoch, cap = view.cap, n, pin, totals, fr, writers, t0, t_kernels, t_enqueue,
+                               t_reserve, t_events, t_pinned]() {
+                const double t_join = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+                hip_check(hipSetDevice(dv.device), "hipSetDevice");
+                hip_check(hipEventSynchronize(dv.export_ev[par]), "adopt export");
+                const uint64_t ns = totals[0], nv = totals[1], cbase = totals[2], vbase = totals[3];
+                if (ns > n) throw std::runtime_error("write path: more successes than ops");
+                // the epochs are adopted in order: the host's counts are this epoch's bases
+                if (h.copies_.size() != cbase || h.versions_.size() != vbase || h.images_.size() != totals[4])
+                    throw std::runtime_error("write path: device append counters disagree with the host table");
+                auto *copies = reinterpret_cast<CopyHdr *>(pin + 64);
+                auto *versions = reinterpret_cast<VersionHdr *>(pin + 64 + ns * sizeof(CopyHdr));
+                const double t_d2h = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+                const std::vector<uint32_t> &d2h = dv.dev_to_host;
+                std::atomic<uint64_t> bad{0};
+                HostTable::parallel_chunks(ns, [&](uint64_t b, uint64_t e) {
+                    for (uint64_t k = b; k < e; ++k) {
+                        if (fr[k].loc == ~0ull) continue;
+                        if (fr[k].loc / cap >= d2h.size()) {
+                            bad.fetch_add(1);
+                            fr[k].loc = ~0ull;
+                            continue;
+                        }
+                        fr[k].loc = (uint64_t)d2h[fr[k].loc / cap] * cap + fr[k].loc % cap;
                     }
-                    fr[k].loc = (uint64_t)d2h[fr[k].loc / cap] * cap + fr[k].loc % cap;
-                }
+                });
+                if (bad.load())
+                    throw std::runtime_error("write path: " + std::to_string(bad.load()) +
+                                             " slot words outside the table (ns " + std::to_string(ns) + ")");
+                h.adopt_device_epoch(copies, writers, ns, versions, nv, ns, reinterpret_cast<const HostTable::SlotWords *>(fr), ns);
+                t->adopted_sz[0].store(h.copies_.size(), std::memory_order_release);
+                t->adopted_sz[1].store(h.versions_.size(), std::memory_order_release);
+                t->adopted_sz[2].store(h.images_.size(), std::memory_order_release);
+                if (trace)
+                    std::fprintf(stderr,
+                                 "[wp] epoch %llu at %.2f ms: n=%llu ok=%llu reserve %.2f enqueue %.2f events %.2f pinned %.2f kernels %.2f "
+                                 "previous adopted %.2f exported %.2f adopted %.2f ms (background)\n",
+                                 (unsigned long long)epoch,
+                                 std::chrono::duration<double, std::milli>(t0 - g0).count(), (unsigned long long)n,
+                                 (unsigned long long)ns, t_reserve, t_enqueue, t_events, t_pinned, t_kernels, t_join, t_d2h,
+                                 std::chrono::duration<double, std::milli>(clk::now() - t0).count());
             });
-            if (bad.load())
-                throw std::runtime_error("write path: " + std::to_string(bad.load()) +
-                                         " slot words outside the table (ns " + std::to_string(ns) + ")");
-            h.adopt_device_epoch(copies, writers, ns, versions, nv, ns, reinterpret_cast<const HostTable::SlotWords *>(fr), ns);
-            t->adopted_sz[0].store(h.copies_.size(), std::memory_order_release);
-            t->adopted_sz[1].store(h.versions_.size(), std::memory_order_release);
-            t->adopted_sz[2].store(h.images_.size(), std::memory_order_release);
-            if (trace)
-                std::fprintf(stderr,
-                             "[wp] epoch %llu at %.2f ms: n=%llu ok=%llu reserve %.2f enqueue %.2f events %.2f pinned %.2f kernels %.2f "
-                             "previous adopted %.2f exported %.2f adopted %.2f ms (background)\n",
-                             (unsigned long long)epoch,
-                             std::chrono::duration<double, std::milli>(t0 - g0).count(), (unsigned long long)n,
-                             (unsigned long long)ns, t_reserve, t_enqueue, t_events, t_pinned, t_kernels, t_join, t_d2h,
-                             std::chrono::duration<double, std::milli>(clk::now() - t0).count());
-        });
+            return ns;
+        };
+        if (t->wp_overlap == 2 && !n_ok) {
+            guard.started = true;  // the pending publish carries the epoch from here on
+            t->pending_pub = [t, epoch, finish](hipStream_t ps) {
+                try {
+                    finish(ps, false);
+                } catch (...) {  // the host table missed the epoch: every later call reports it
+                    t->start_adoption(epoch, [] { throw std::runtime_error("a deferred write-path publish failed"); });
+                    throw;
+                }
+            };
+            t->pending_stream = s;
+            return STAGE_OK;
+        }
+        const uint64_t ns = finish(s, n_ok != nullptr);
         guard.started = true;
         if (n_ok) *n_ok = ns;
         return STAGE_OK;

@@ -381,3 +381,75 @@ def test_write_overlap_epochs_with_probes_between(gpu):
         assert not (rows[:, :orc.row] != o_rec).any(axis=1).any(), keys.size
     check_all(tab, orc, probe_keys, rng, counter)
     assert_same_images(tab, orc)
+
+
+def test_deferred_publish_probes_before_and_after(gpu):
+    """stage_set_write_overlap(2): stage_update_batch_device prepares epoch e and returns; a probe
+    enqueued before stage_publish_epoch reads the state after epoch e - 1 (the prepared epoch is
+    invisible), one enqueued after it the state after epoch e -- the order the YCSB-B driver uses
+    (prepare e + 1, probe e, publish e + 1).  Codes, statuses and rows equal the oracle's; a host
+    write between epochs settles the pending publish first; the host table agrees at the end."""
+    n = 30000
+    tab = stage.Table(key_width=8)
+    tab.load_ycsb(0, n, 8, mode=1)
+    tab.sync()
+    tab.set_write_overlap(2)
+    orc = O.OracleTree()
+    orc.load_ycsb(0, n, 8, 1)
+    rng = np.random.default_rng(37)
+    s = stage.Stream()
+    base, hot = np.arange(0, n, 2, dtype=np.uint64), np.arange(0, 40, dtype=np.uint64)
+    counter, epochs = 10, []
+    probe_keys = np.concatenate([hot, rng.integers(0, n + 50, 5000)]).astype(np.uint64)
+
+    def enqueue_probe():
+        rids = np.where(rng.random(probe_keys.size) < 0.5, rng.integers(0, counter, probe_keys.size),
+                        0xFFFFFFFE).astype(np.uint32)
+        pk, pr = stage.DeviceBuffer.from_numpy(probe_keys), stage.DeviceBuffer.from_numpy(rids)
+        pout, prow = stage.DeviceBuffer(probe_keys.size * 32), stage.DeviceBuffer(probe_keys.size * tab.stride)
+        tab.probe_device(pk.ptr, probe_keys.size, pout.ptr, prow.ptr, d_read_ids=pr.ptr, stream=s.ptr)
+        return rids, (pk, pr), pout, prow
+
+    for e, m in enumerate((3000, 800, 9000, 60000, 1500, 4000, 2)):
+        keys, deltas, wid, cid = epoch_ops(rng, base, hot, m, counter)
+        counter += 2 * m + 2
+        ep_host = None
+        if e == 5:  # a host-side write between epochs (nothing pending: the last epoch was published)
+            s.sync()
+            k0 = int(hot[3])
+            dd = rng.integers(0, 256, 8, dtype=np.uint8)
+            ep_host = (k0, dd, counter, tab.update(k0, 3, dd, counter))
+            counter += 2
+            tab.sync()
+        d = [stage.DeviceBuffer.from_numpy(x) for x in (keys, deltas.reshape(-1), wid, cid)]
+        rcb = stage.DeviceBuffer(m)
+        check(stage.lib().stage_update_batch_device(tab.h, d[0].ptr, None, m, 16, d[1].ptr, 24, d[2].ptr, d[3].ptr,
+                                                    None, rcb.ptr, None, s.ptr), "update_batch_device")
+        before = enqueue_probe()  # the prepared epoch is not visible yet
+        tab.publish_epoch(s.ptr)
+        after = enqueue_probe()
+        epochs.append((keys, deltas, wid, cid, rcb, d, ep_host, before, after))
+    s.sync()
+
+    def compare(probe):
+        rids, _, pout, prow = probe
+        out = pout.to_numpy(stage.PROBE_OUT_DTYPE, probe_keys.size)
+        rows = prow.to_numpy(np.uint8, probe_keys.size * tab.stride).reshape(probe_keys.size, tab.stride)
+        o_out, o_rec = orc.read_batch(probe_keys, 8, rids)
+        for f in ("status", "hops", "cstamp", "rec_cstamp", "copy_sstamp"):
+            badf = np.nonzero(out[f] != o_out[f])[0]
+            assert badf.size == 0, (f, badf[:5], out[f][badf[:5]], o_out[f][badf[:5]])
+        assert not (rows[:, :orc.row] != o_rec).any(axis=1).any()
+
+    for keys, deltas, wid, cid, rcb, _, ep_host, before, after in epochs:
+        if ep_host is not None:
+            k0, dd, c0, rc0 = ep_host
+            assert orc.update(k0, 8, 3, dd.tobytes(), c0) == rc0
+        compare(before)
+        exp = oracle_epoch(orc, keys, 8, 16, deltas, wid, cid)
+        rc = rcb.to_numpy(np.uint8, keys.size)
+        bad = np.nonzero(rc != exp)[0]
+        assert bad.size == 0, (keys.size, bad[:5], rc[bad[:5]], exp[bad[:5]])
+        compare(after)
+    check_all(tab, orc, probe_keys, rng, counter)
+    assert_same_images(tab, orc)
