@@ -110,7 +110,7 @@ def parse(argv=None):
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extras", action="store_true", help="c2: skip the nested C4 / C3 legs")
     p.add_argument("--host-traversal", action="store_true", help="leaf ids from the host router instead")
-    p.add_argument("--write-overlap", type=int, choices=[0, 1, 2], default=2,
+    p.add_argument("--write-overlap", type=int, choices=[0, 1, 2], default=1,
                    help="device write path: 1 = an epoch's kernels up to its publish run beside the previous "
                         "epoch's read probe (stage_set_write_overlap; the epoch inputs are resident beforehand); "
                         "2 = the next epoch is prepared before this epoch's probe is enqueued and published "
