@@ -524,22 +524,42 @@ __global__ __launch_bounds__(1024) void wp_finish_jump(WpArgs a, WpCls kc, DevTa
             __syncthreads();
             continue;
         }
-        // B. the chain, chunk to chunk (wave 0; the loop is wave-uniform)
+        // B. the chain, chunk to chunk (wave 0; the loop is wave-uniform).  The chunks' exits and
+        // masks come in kPre chunks at a time, a lane per op, all loads in flight together (they
+        // do not depend on where the chain enters); the chain then picks its entry's values by
+        // readlane -- one load round trip per kPre chunks instead of one per chunk
         if (wv == 0) {
+            constexpr int kPre = 16;
             uint64_t e = start;
             int64_t carry = f > g ? (start > g ? (int64_t)start - 1 : -1) : -1;
-            for (uint64_t c = 0; c < nch; ++c) {
-                const uint64_t cb = start + 64 * c;
-                uint64_t entry = kNone;
-                int64_t next_carry = carry;
-                if (e != kNone && e < cb + 64) {
-                    entry = e;
-                    const uint64_t m = jm[e];
-                    next_carry = (int64_t)(cb + 63 - __builtin_clzll(m));
-                    e = jx[e];
+            for (uint64_t c0 = 0; c0 < nch; c0 += kPre) {
+                uint32_t xr[kPre];
+                uint64_t mr[kPre];
+#pragma unroll
+                for (int k = 0; k < kPre; ++k) {
+                    const uint64_t p = start + 64 * (c0 + k) + lane;
+                    const bool ok = c0 + k < nch && p < end;
+                    xr[k] = ok ? jx[p] : kNone;
+                    mr[k] = ok ? jm[p] : 0ull;
                 }
-                if (lane == 0) ci[cb] = entry | ((uint64_t)(uint32_t)(int32_t)carry << 32);
-                carry = next_carry;
+#pragma unroll
+                for (int k = 0; k < kPre; ++k) {
+                    if (c0 + k >= nch) break;
+                    const uint64_t cb = start + 64 * (c0 + k);
+                    uint64_t entry = kNone;
+                    int64_t next_carry = carry;
+                    if (e != kNone && e < cb + 64) {  // wave-uniform
+                        entry = e;
+                        const int el = (int)(e - cb);
+                        const uint64_t m = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(mr[k] >> 32), el)
+                                            << 32) |
+                                           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mr[k], el);
+                        next_carry = (int64_t)(cb + 63 - __builtin_clzll(m));
+                        e = (uint32_t)__builtin_amdgcn_readlane((int)xr[k], el);
+                    }
+                    if (lane == 0) ci[cb] = entry | ((uint64_t)(uint32_t)(int32_t)carry << 32);
+                    carry = next_carry;
+                }
             }
         }
         __syncthreads();
