@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-5 profile passes on one box, from one tree; each pass its own run, PMC never combined
 # with trace domains.  Output: gpurun_out/prof_r05/<pass>/...
+#   c2_trace / c2_fetch / c2_write -> pmc_probe.json (probe_kernel, round-4 calibration)
 #   c4_trace / c4_fetch / c4_write -> pmc_scan.json (scan_kernel, calibrated as pmc_probe.json)
 #   c3_trace                       -> the C3 write-path kernels on this tree
 #   q2_trace                       -> CH-Q2 step kernels
@@ -22,6 +23,9 @@ run() {  # name limit cmd...
   if [ $rc -ne 0 ]; then exit $rc; fi
 }
 B="python3 -u bench.py --no-cpu-baseline"
+run c2_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/c2_trace -o c2 -- $B --steps 5 --warmup 1 --no-extras
+run c2_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/c2_fetch -o c2 -- python3 scripts/profile_probe.py
+run c2_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/c2_write -o c2 -- python3 scripts/profile_probe.py
 run c4_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/c4_trace -o c4 -- $B --config c4 --steps 5 --warmup 1
 run c4_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/c4_fetch -o c4 -- python3 scripts/profile_scan.py
 run c4_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/c4_write -o c4 -- python3 scripts/profile_scan.py
@@ -43,6 +47,12 @@ json.dump(p, open(path, "w"), indent=1)
 print(json.dumps(p["profiled"]))
 PY
 }
+# C2: the probe's heap rows as 1024-B wide reads (as round 4), the rest counted once
+if [ -f $OUT/c2_fetch/c2_counter_collection.csv ] && [ -f $OUT/c2_write/c2_counter_collection.csv ]; then
+  python3 scripts/pmc_summary.py $OUT/c2_fetch/c2_counter_collection.csv $OUT/c2_write/c2_counter_collection.csv \
+    probe_kernel 16777216 100000000 $OUT/pmc_probe.json 0 1024 > $OUT/pmc_summary_c2.log 2>&1 &&
+    stamp $OUT/pmc_probe.json "prof_r05/c2_trace (same call)"
+fi
 # wide bytes per scan (whole 128-B lines): 100 heap rows of 1024 B + the key columns (512 B) of
 # about 3 leaves visited; the rest of FETCH_SIZE (heads, separator nodes) is counted 1x
 if [ -f $OUT/c4_fetch/c4_counter_collection.csv ] && [ -f $OUT/c4_write/c4_counter_collection.csv ]; then
