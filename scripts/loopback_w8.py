@@ -5,7 +5,8 @@ stage_probe_sharded_loopback -- the same plan as the RCCL path with device copie
 transfers.  One loopback step does the HBM work all W ranks do (probes, fan-out probes of own
 requests, result copies, fan-out of returned results) for BATCH lookups in total, i.e. what ONE
 rank does per step at W ranks for its BATCH lookups (trees of ROWS / W rows instead of ROWS;
-no xGMI).  Prints one JSON line: step ms (hipEvents), full reply and owner reply, and the
+no xGMI).  Prints one JSON line: step ms (hipEvents), full reply (rows copied back), peer reply
+(rows read from the owners' buffers) and owner reply, and the
 request counts.  Env: ROWS (100M), W (8), BATCH (2^24), STEPS (5), CHUNKS (4)."""
 import ctypes
 import json
@@ -44,7 +45,7 @@ hs = (ctypes.c_void_p * W)(*[t.h for t in tabs])
 n_arr = (ctypes.c_uint64 * W)(*([per] * W))
 s = stage.Stream()
 res = {"rows": rows, "world": W, "batch_total": batch, "chunks": chunks, "steps": steps}
-for name, reply in (("full_reply", stage.REPLY_ROWS), ("owner_reply", stage.REPLY_OWNER)):
+for name, reply in (("full_reply", stage.REPLY_ROWS), ("peer_reply", stage.REPLY_PEER), ("owner_reply", stage.REPLY_OWNER)):
     ms = []
     for it in range(steps + 1):
         e0, e1 = stage.Event(), stage.Event()
