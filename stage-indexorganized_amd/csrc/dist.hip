@@ -69,6 +69,16 @@ constexpr int kDefaultChunks = 4;  // sharded batches are exchanged in this many
 // caller positions served by one coalesced request at most: a hot key's run is cut into
 // requests of <= 64 callers, so no single probe or fan-out copy stores more than 64 rows
 constexpr uint32_t kFanCap = 64;
+// callers per coalesced request: kFanCap, or STAGE_SHARD_FANCAP (1..64) -- a smaller cap splits a
+// hot key's callers over more requests (more row reads, shorter per-request fan-outs)
+static uint32_t fan_cap() {
+    static const uint32_t v = [] {
+        const char *e = std::getenv("STAGE_SHARD_FANCAP");
+        const int x = e ? std::atoi(e) : 0;
+        return x >= 1 && x <= (int)kFanCap ? (uint32_t)x : kFanCap;
+    }();
+    return v;
+}
 
 // chunk i of C over the routed items [0, total): [total*i/C, total*(i+1)/C); total is the batch
 // size, or the coalesced request count read on the device (total_dev)
@@ -208,11 +218,11 @@ struct SortedKeys {
 };
 
 __global__ void dd_heads(SortedKeys sk, const uint32_t *__restrict__ sidx,
-                         const uint32_t *__restrict__ rids, uint64_t n, uint32_t *__restrict__ flag) {
+                         const uint32_t *__restrict__ rids, uint64_t n, uint32_t cap, uint32_t *__restrict__ flag) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n) return;
     const bool wide = !sk.k64 && *sk.hi != 0;
-    bool head = j % kFanCap == 0 || sk.at(j, sidx, wide) != sk.at(j - 1, sidx, wide);
+    bool head = j % cap == 0 || sk.at(j, sidx, wide) != sk.at(j - 1, sidx, wide);
     if (!head && rids) head = rids[sidx[j]] != rids[sidx[j - 1]];
     flag[j] = head ? 1u : 0u;
 }
@@ -636,7 +646,7 @@ static void plan_route(ShardComm &c, Plan &P, const uint64_t *d_keys, const uint
             chk(hipcub::DeviceRadixSort::SortPairs(c.dd_cub, bytes, d_keys, skeys, iota, sidx, (int)n, 0, bits, s),
                 "dedupe sort");
         }
-        dd_heads<<<nb, 256, 0, s>>>(sk, sidx, d_rids, n, flag);
+        dd_heads<<<nb, 256, 0, s>>>(sk, sidx, d_rids, n, fan_cap(), flag);
         bytes = c.dd_cub_bytes;
         chk(hipcub::DeviceScan::InclusiveSum(c.dd_cub, bytes, flag, useq, (int)n, s), "dedupe scan");
         dd_pack<<<nb, 256, 0, s>>>(sk, sidx, d_rids, flag, useq, n, 0u, owner ? (uint32_t *)c.uidx : nullptr,
