@@ -45,7 +45,9 @@ hs = (ctypes.c_void_p * W)(*[t.h for t in tabs])
 n_arr = (ctypes.c_uint64 * W)(*([per] * W))
 s = stage.Stream()
 res = {"rows": rows, "world": W, "batch_total": batch, "chunks": chunks, "steps": steps}
-for name, reply in (("full_reply", stage.REPLY_ROWS), ("peer_reply", stage.REPLY_PEER), ("owner_reply", stage.REPLY_OWNER)):
+modes = (("full_reply", stage.REPLY_ROWS), ("peer_reply", stage.REPLY_PEER), ("owner_reply", stage.REPLY_OWNER))
+only = os.environ.get("MODES")  # e.g. MODES=peer_reply
+for name, reply in [m for m in modes if not only or m[0] in only.split(",")]:
     ms = []
     for it in range(steps + 1):
         e0, e1 = stage.Event(), stage.Event()
