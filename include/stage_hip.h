@@ -510,6 +510,15 @@ int stage_ch_query2_batch(stage_table *region, stage_table *nation, stage_table 
                           stage_table *stock, const uint32_t *map_off, const uint64_t *d_map_keys,
                           int32_t target_region, const uint32_t *read_ids, uint32_t nq, stage_q2_rec *out,
                           uint64_t max_per_query, uint64_t *n_out, int32_t *aborted, void *stream);
+/* the same batch without waiting for it: enqueued on `stream` into slot 0 or 1 (two batches
+ * may be in flight, the host enqueueing one while the device runs the other); `out` must be
+ * page-locked (stage_host_alloc) and stay untouched until stage_ch_query2_wait(slot) returns
+ * *n_out and aborted[nq].  STAGE_E_STATE: the slot still holds a batch not waited for. */
+int stage_ch_query2_batch_async(stage_table *region, stage_table *nation, stage_table *supplier,
+                                stage_table *item, stage_table *stock, const uint32_t *map_off,
+                                const uint64_t *d_map_keys, int32_t target_region, const uint32_t *read_ids,
+                                uint32_t nq, stage_q2_rec *out, uint64_t max_per_query, int slot, void *stream);
+int stage_ch_query2_wait(stage_table *stock, int slot, uint64_t *n_out, int32_t *aborted);
 
 /* ---- multi-GPU: hash-sharded probe front-end over RCCL (one process per GPU) ------------
  * stage_comm_unique_id fills 128 bytes on rank 0 (broadcast them out of band);

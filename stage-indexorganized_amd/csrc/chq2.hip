@@ -400,13 +400,15 @@ const uint8_t *scan_rows(stage_table *t, const uint64_t *d_start, uint32_t scan_
 static int q2_run(stage_table *region, stage_table *nation, stage_table *supplier, stage_table *item,
                   stage_table *stock, const uint32_t *map_off, const uint64_t *d_map_keys, int32_t target_region,
                   const uint32_t *rq, uint32_t nq, uint32_t commit_id, stage_q2_rec *out, uint64_t max_out,
-                  uint64_t *n_out, int32_t *aborted, void *stream) {
+                  uint64_t *n_out, int32_t *aborted, void *stream, int slot = 0, bool async = false) {
     for (stage_table *t : {region, nation, supplier, item, stock}) {
         int rc = need_synced(t);
         if (rc) return rc;
     }
-    if (!map_off || !d_map_keys || !n_out || !aborted || (max_out && !out))
+    if (!map_off || !d_map_keys || (!async && (!n_out || !aborted)) || (max_out && !out))
         return fail(STAGE_E_ARG, "null argument");
+    if (slot < 0 || slot > 1) return fail(STAGE_E_ARG, "slot must be 0 or 1");
+    if (stock->q2p[slot].active) return fail(STAGE_E_STATE, "CH-Q2 slot still in flight: stage_ch_query2_wait first");
     if (target_region < 0 || target_region > 4) return fail(STAGE_E_ARG, "target_region must be 0..4");
     for (stage_table *t : {region, nation, supplier, item})
         if (facts(t).params().key_width != 8) return fail(STAGE_E_ARG, "REGION/NATION/SUPPLIER/ITEM keys are 8 bytes");
@@ -429,8 +431,10 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
                 std::fprintf(stderr, "[q2] %s %.1f us\n", what,
                              std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
         };
-        *n_out = 0;
-        for (uint32_t q = 0; q < nq; ++q) aborted[q] = 0;
+        if (!async) {
+            *n_out = 0;
+            for (uint32_t q = 0; q < nq; ++q) aborted[q] = 0;
+        }
         const DevTable &pv = supplier->dev.view, &sv = stock->dev.view, &iv = item->dev.view;
         const uint64_t nslots = (uint64_t)pv.nleaves * pv.cap;
         if (pv.cap % 64) return fail(STAGE_E_UNSUPPORTED, "SUPPLIER leaves of a multiple of 64 slots");
@@ -448,7 +452,7 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
         const uint64_t q_map = 0, q_rq = q_map + al((kMapKeys + 1) * 4ull), q_cn = q_rq + al(nq * 4ull),
                        q_ab = q_cn + 16, q_zero = q_ab + al(nq * 4ull), q_end = q_zero + 16;
-        uint8_t *pq = pinned_bytes(stock->dev, q_end, 2);
+        uint8_t *pq = pinned_bytes(stock->dev, q_end, 2 + slot);
         std::memcpy(pq + q_map, map_off, (kMapKeys + 1) * 4ull);
         std::memcpy(pq + q_rq, rq, nq * 4ull);
         std::memset(pq + q_cn, 0, 16 + nq * 4ull);
@@ -468,6 +472,13 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
                        o_vis = take(n_max), o_rank = take(n_max), o_koff = take(n_max * 4),
                        o_ccnt = take(std::max<uint64_t>(nchunks, 1) * kVisits * 4),
                        o_kcnt = take(std::max<uint64_t>(nchunks, 1) * kVisits * 4), o_nv = take(4);
+        // a batch still in flight uses these scratch buffers: growing one (a reallocation) waits
+        // for it first
+        const uint64_t reg_rows = 64 + (uint64_t)kRegionScan * region->dev.view.stride,
+                       nat_rows = 64 + (uint64_t)kNationScan * nation->dev.view.stride;
+        if ((stock->q2p[0].active || stock->q2p[1].active) &&
+            (supplier->dev.scratch.cap < off || region->dev.scratch.cap < reg_rows || nation->dev.scratch.cap < nat_rows))
+            hip_check(hipDeviceSynchronize(), "q2 drain");
         // the SUPPLIER table's scratch: REGION's and NATION's hold their scan rows (scan_rows)
         uint8_t *buf = scratch_bytes(supplier->dev, off), *mir = buf + o_mir;
         auto *d_map = (const uint32_t *)(mir + q_map);
@@ -511,10 +522,12 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
             (void)hipGetLastError();  // a pageable pointer is not an error here
         }
         if (trace) std::fprintf(stderr, "[q2] out %s\n", host_out ? "page-locked: written by q2_finish" : "pageable: copied");
+        if (async && out && max_out && !host_out)
+            return fail(STAGE_E_ARG, "stage_ch_query2_batch_async needs a page-locked out (stage_host_alloc)");
         lap("buffers");
         // the scan rows' scratch sized before any capture (scan_rows asks for the same size again)
-        (void)scratch_bytes(region->dev, 64 + (uint64_t)kRegionScan * region->dev.view.stride);
-        (void)scratch_bytes(nation->dev, 64 + (uint64_t)kNationScan * nation->dev.view.stride);
+        (void)scratch_bytes(region->dev, reg_rows);
+        (void)scratch_bytes(nation->dev, nat_rows);
         // everything up to the batch's one synchronisation, enqueued on s (and the REGION /
         // NATION streams forked from it)
         auto enqueue = [&] {
@@ -595,7 +608,7 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
                            n_max, m_max, n_hint, m_hint, (uint64_t)(uintptr_t)s})
             putv(v);
         lap("key");
-        Q2Graph &G = stock->q2g;
+        Q2Graph &G = stock->q2g[slot];
         bool launched = false;
         if (graphs && !G.failed) {
             if (G.exec && G.key == key) {
@@ -633,6 +646,19 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         }
         if (!launched) enqueue();
         lap("enqueued");
+        if (async) {  // the results are read by stage_ch_query2_wait
+            Q2Pending &P = stock->q2p[slot];
+            if (!P.ev) hip_check(hipEventCreateWithFlags(&P.ev, hipEventDisableTiming), "q2 event");
+            hip_check(hipEventRecord(P.ev, s), "q2 event");
+            P.pq = pq;
+            P.q_cn = q_cn;
+            P.q_ab = q_ab;
+            P.nq = nq;
+            P.n_max = n_max;
+            P.m_max = m_max;
+            P.active = true;
+            return STAGE_OK;
+        }
         hip_check(hipStreamSynchronize(s), "q2 sync");  // the batch's one synchronisation
         lap("results back");
         uint64_t cn[2];
@@ -713,6 +739,37 @@ extern "C" int stage_ch_query2(stage_table *region, stage_table *nation, stage_t
                                uint64_t max_out, uint64_t *n_out, int32_t *aborted, void *stream) {
     return q2_run(region, nation, supplier, item, stock, map_off, d_map_keys, target_region, &read_id, 1, commit_id,
                   out, max_out, n_out, aborted, stream);
+}
+
+extern "C" int stage_ch_query2_batch_async(stage_table *region, stage_table *nation, stage_table *supplier,
+                                           stage_table *item, stage_table *stock, const uint32_t *map_off,
+                                           const uint64_t *d_map_keys, int32_t target_region, const uint32_t *read_ids,
+                                           uint32_t nq, stage_q2_rec *out, uint64_t max_per_query, int slot,
+                                           void *stream) {
+    if (nq == 0 || !read_ids || nq > 4096) return fail(STAGE_E_ARG, "read_ids: 1..4096 queries");
+    if (!out || !max_per_query) return fail(STAGE_E_ARG, "an out array is required");
+    return q2_run(region, nation, supplier, item, stock, map_off, d_map_keys, target_region, read_ids, nq, 0, out,
+                  max_per_query, nullptr, nullptr, stream, slot, true);
+}
+
+extern "C" int stage_ch_query2_wait(stage_table *stock, int slot, uint64_t *n_out, int32_t *aborted) {
+    if (!stock || slot < 0 || slot > 1 || !n_out || !aborted) return fail(STAGE_E_ARG, "bad arguments");
+    Q2Pending &P = stock->q2p[slot];
+    if (!P.active) return fail(STAGE_E_STATE, "no CH-Q2 batch in flight in this slot");
+    return guarded([&] {
+        P.active = false;
+        stage::hip_check(hipEventSynchronize(P.ev), "q2 wait");
+        uint64_t cn[2];
+        std::memcpy(cn, P.pq + P.q_cn, 16);
+        std::memcpy(aborted, P.pq + P.q_ab, 4ull * P.nq);
+        if (cn[0] > P.n_max || cn[1] > P.m_max) throw std::runtime_error("q2: device counts out of range");
+        stock->q2_hint[0] = cn[0];
+        stock->q2_hint[1] = cn[1];
+        *n_out = cn[0];
+        if (cn[0] == 0)
+            for (uint32_t q = 0; q < P.nq; ++q) aborted[q] = 0;
+        return STAGE_OK;
+    });
 }
 
 extern "C" int stage_ch_query2_batch(stage_table *region, stage_table *nation, stage_table *supplier,

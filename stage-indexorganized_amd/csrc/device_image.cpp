@@ -34,7 +34,7 @@ void DeviceImage::release() {
         b->p = nullptr;
         b->cap = 0;
     }
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < 4; ++k) {
         if (pinned[k]) (void)hipHostFree(pinned[k]);
         pinned[k] = nullptr;
         pinned_cap[k] = 0;

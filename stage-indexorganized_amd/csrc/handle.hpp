@@ -34,6 +34,14 @@ struct Q2Graph {
     std::string key, last_key;
     bool failed = false;
 };
+// a CH-Q2 batch enqueued by stage_ch_query2_batch_async and not yet waited for (per slot)
+struct Q2Pending {
+    bool active = false;
+    hipEvent_t ev = nullptr;  // after the batch's last copy
+    uint8_t *pq = nullptr;    // its page-locked staging: counts at q_cn, aborted flags at q_ab
+    uint64_t q_cn = 0, q_ab = 0, n_max = 0, m_max = 0;
+    uint32_t nq = 0;
+};
 
 struct stage_table {
     std::unique_ptr<stage::HostTable> host;
@@ -59,7 +67,8 @@ struct stage_table {
         f(s);
     }
     uint64_t q2_hint[2] = {0, 0};                  // CH-Q2's last visited suppliers / STOCK keys (launch shapes)
-    Q2Graph q2g;
+    Q2Graph q2g[2];     // per CH-Q2 slot (stage_ch_query2_batch_async); slot 0 also serves the synchronous calls
+    Q2Pending q2p[2];
     std::mutex pipe_mu;  // serialises stage_probe_host calls on this table
     std::unique_ptr<stage::HostPipe, stage::HostPipeDeleter> pipe;
     // the device write path hands its epoch's bookkeeping (new copy / version headers, slot
@@ -114,7 +123,11 @@ struct stage_table {
         }
         std::lock_guard<std::mutex> g(adopt_mu);
         if (adopt.joinable()) adopt.join();
-        if (q2g.exec) (void)hipGraphExecDestroy(q2g.exec);
+        for (int k = 0; k < 2; ++k) {
+            if (q2p[k].active && q2p[k].ev) (void)hipEventSynchronize(q2p[k].ev);
+            if (q2p[k].ev) (void)hipEventDestroy(q2p[k].ev);
+            if (q2g[k].exec) (void)hipGraphExecDestroy(q2g[k].exec);
+        }
     }
 };
 

@@ -65,6 +65,9 @@ SIGNATURES = {
     "stage_ch_query2_batch": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_int32, c_vp,
                                              ctypes.c_uint32, c_vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64),
                                              c_vp, c_vp]),
+    "stage_ch_query2_batch_async": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_int32, c_vp,
+                                                   ctypes.c_uint32, c_vp, ctypes.c_uint64, ctypes.c_int, c_vp]),
+    "stage_ch_query2_wait": (ctypes.c_int, [c_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), c_vp]),
     "stage_ch_query2": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_int32, ctypes.c_uint32,
                                        ctypes.c_uint32, c_vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64),
                                        ctypes.POINTER(ctypes.c_int32), c_vp]),

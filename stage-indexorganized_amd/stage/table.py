@@ -878,3 +878,34 @@ def ch_query2_batch(region, nation, supplier, item, stock, map_off, d_map_keys, 
                                       d_map_keys, int(target_region), rids.ctypes.data, nq, out.ctypes.data,
                                       max_per_query, ctypes.byref(n), ab.ctypes.data, stream), "ch_query2_batch")
     return out[:, :min(n.value, max_per_query)], ab.astype(bool)
+
+
+class Q2Batch:
+    """An enqueued stage_ch_query2_batch_async batch (slot 0 or 1); wait() -> (records [nq, n],
+    aborted[nq]).  `out` is a page-locked [nq, max_per_query] Q2_REC_DTYPE array (pinned_empty)
+    left untouched until wait() returns."""
+
+    def __init__(self, stock, slot, out, nq):
+        self.stock, self.slot, self.out, self.nq, self.done = stock, slot, out, nq, None
+
+    def wait(self):
+        if self.done is None:
+            n = ctypes.c_uint64()
+            ab = np.zeros(self.nq, np.int32)
+            check(lib().stage_ch_query2_wait(self.stock.h, self.slot, ctypes.byref(n), ab.ctypes.data),
+                  "ch_query2_wait")
+            self.done = (self.out[:, :min(n.value, self.out.shape[1])], ab.astype(bool))
+        return self.done
+
+
+def ch_query2_batch_async(region, nation, supplier, item, stock, map_off, d_map_keys, read_ids, out, slot=0,
+                          target_region=3, stream=None):
+    """stage_ch_query2_batch_async: ch_query2_batch without the wait (two slots may be in flight)."""
+    map_off = np.ascontiguousarray(map_off, np.uint32)
+    rids = np.ascontiguousarray(read_ids, np.uint32)
+    nq = rids.size
+    assert out.dtype == Q2_REC_DTYPE and out.flags.c_contiguous and out.ndim == 2 and out.shape[0] == nq
+    check(lib().stage_ch_query2_batch_async(region.h, nation.h, supplier.h, item.h, stock.h, map_off.ctypes.data,
+                                            d_map_keys, int(target_region), rids.ctypes.data, nq, out.ctypes.data,
+                                            out.shape[1], int(slot), stream), "ch_query2_batch_async")
+    return Q2Batch(stock, slot, out, nq)

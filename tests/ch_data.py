@@ -119,6 +119,11 @@ class ChTables:
         return stage.ch_query2_batch(t["region"], t["nation"], t["supplier"], t["item"], t["stock"], self.map_off,
                                      self.d_map.ptr, read_ids, target, out=out)
 
+    def query2_batch_async(self, read_ids, out, slot=0, target=3):
+        t = self.tables
+        return stage.ch_query2_batch_async(t["region"], t["nation"], t["supplier"], t["item"], t["stock"],
+                                           self.map_off, self.d_map.ptr, read_ids, out, slot, target)
+
     def query2_oracle(self, target=3, read_id=0xFFFFFFFE):
         import ctypes
 

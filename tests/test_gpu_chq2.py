@@ -135,3 +135,30 @@ def test_q2_batch_many_read_ids(ch):
         assert ab[q] == ab1, (q, r)
         if not ab1:
             same(recs[q], one)
+
+
+def test_q2_batch_async_two_in_flight(ch):
+    """stage_ch_query2_batch_async: two batches in flight (slots 0 and 1, different targets and
+    read ids), waited for out of order, each equal to the synchronous batch of the same queries;
+    a busy slot, a pageable `out` and a wait on an idle slot are refused."""
+    ra = np.array([10, 0xFFFFFFFE, 25], np.uint32)
+    rb = np.array([40, 3, 0xFFFFFFFE, 60], np.uint32)
+    oa = stage.pinned_empty((ra.size, 1 << 14), stage.Q2_REC_DTYPE)
+    ob = stage.pinned_empty((rb.size, 1 << 14), stage.Q2_REC_DTYPE)
+    for rep in range(3):  # the third round replays both slots' graphs
+        ja = ch.query2_batch_async(ra, oa, 0, 3)
+        jb = ch.query2_batch_async(rb, ob, 1, 0)
+        with pytest.raises(stage.StageError):
+            ch.query2_batch_async(ra, oa, 0, 3)
+        recs_b, ab_b = jb.wait()
+        recs_a, ab_a = ja.wait()
+        for rids, target, recs, ab in ((ra, 3, recs_a, ab_a), (rb, 0, recs_b, ab_b)):
+            srecs, sab = ch.query2_batch(rids, target)
+            assert (ab == sab).all() and recs.shape == srecs.shape, rep
+            for q in range(rids.size):
+                if not ab[q]:
+                    same(recs[q], srecs[q])
+    with pytest.raises(stage.StageError):
+        ch.query2_batch_async(ra, np.zeros((ra.size, 1 << 14), stage.Q2_REC_DTYPE), 0, 3)
+    with pytest.raises(stage.StageError):
+        stage.table.Q2Batch(ch.tables["stock"], 1, ob, rb.size).wait()
