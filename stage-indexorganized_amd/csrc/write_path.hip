@@ -205,13 +205,24 @@ __device__ __forceinline__ uint64_t lanes_between(uint32_t from, uint32_t lane) 
     return below & ~skip;
 }
 
+// the sort's input, and the epoch's position-indexed state initialised on the way (no fills on
+// the stream later): first failures none, last-success marks 0, FinRecs all ones (24 B each),
+// the big-group count 0
 __global__ void wp_keys(const stage_probe_out_dev *__restrict__ pout, uint64_t n, uint32_t cap, uint64_t none,
-                        uint64_t *__restrict__ loc, uint32_t *__restrict__ op) {
+                        uint64_t *__restrict__ loc, uint32_t *__restrict__ op, uint32_t *__restrict__ first_fail,
+                        uint32_t *__restrict__ last_succ, uint64_t *__restrict__ fin_words,
+                        uint32_t *__restrict__ big_count) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) *big_count = 0;
     if (i >= n) return;
     const uint32_t slot = pout[i].w[2] & 0xFFFF;
     loc[i] = slot == 0xFFFF ? none : (uint64_t)pout[i].w[1] * cap + slot;
     op[i] = (uint32_t)i;
+    first_fail[i] = 0xFFFFFFFFu;
+    last_succ[i] = 0;
+    fin_words[3 * i] = ~0ull;
+    fin_words[3 * i + 1] = ~0ull;
+    fin_words[3 * i + 2] = ~0ull;
 }
 
 __global__ void wp_heads(const uint64_t *__restrict__ loc, uint64_t n, uint32_t *__restrict__ head) {
@@ -220,14 +231,23 @@ __global__ void wp_heads(const uint64_t *__restrict__ loc, uint64_t n, uint32_t 
     head[q] = (q == 0 || loc[q] != loc[q - 1]) ? (uint32_t)q : 0u;
 }
 
-// step 3a: every op evaluated against its predecessor-as-success
+// step 3a: every op evaluated against its predecessor-as-success; on the way the group extents
+// (gend[g] = one past the group's last position) and the first position of every delta class
+// (cfirst; cls = inclusive sum of wp_classify's breaks, cfirst[last class + 1] = n, so the run
+// after a group's last run starts at or past the group's end)
 __global__ void wp_speculate(WpArgs a, WpCls k, DevTable t, uint8_t *__restrict__ rcs, uint8_t *__restrict__ succ,
-                             int32_t *__restrict__ prev, uint32_t *__restrict__ first_fail) {
+                             int32_t *__restrict__ prev, uint32_t *__restrict__ first_fail, uint32_t *__restrict__ gend,
+                             const uint32_t *__restrict__ brk, uint32_t *__restrict__ cfirst) {
     const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // blockDim: a multiple of 64
     if (q >= a.n) return;
     const uint32_t lane = threadIdx.x & 63;
-    const bool found = a.loc[q] != a.none;
+    const uint64_t lq = a.loc[q];
+    const bool found = lq != a.none;
     const uint32_t g = a.gs[q];
+    const uint32_t cq = k.cls[q];
+    if (q + 1 == a.n || a.loc[q + 1] != lq) gend[g] = (uint32_t)(q + 1);
+    if (brk[q]) cfirst[cq] = (uint32_t)q;
+    if (q + 1 == a.n) cfirst[cq + 1] = (uint32_t)a.n;
     const int64_t last = q > g ? (int64_t)q - 1 : -1;
     uint8_t r = STAGE_RC_NOT_FOUND;
     if (found) {
@@ -254,15 +274,23 @@ __global__ void wp_speculate(WpArgs a, WpCls k, DevTable t, uint8_t *__restrict_
 constexpr int kFinishChunks = 8;
 constexpr uint32_t kBigGroup = 2048;  // ops from the first failure on: a workgroup finishes it (wp_finish_big)
 constexpr uint32_t kJumpFrom = 256;   // ... by pointer jumping (wp_finish_jump)
+// Groups with at least big_from ops from their first failure on go to `list` instead (one
+// atomic per big group; their finishing kernels follow).
 __global__ __launch_bounds__(256) void wp_finish_groups(WpArgs a, WpCls kc, DevTable t, uint8_t *__restrict__ rcs,
                                                         uint8_t *__restrict__ succ, int32_t *__restrict__ prev,
                                                         const uint32_t *__restrict__ first_fail,
-                                                        const uint32_t *__restrict__ gend, uint32_t big_from) {
+                                                        const uint32_t *__restrict__ gend, uint32_t big_from,
+                                                        uint32_t *__restrict__ list, uint32_t *__restrict__ count,
+                                                        uint8_t *__restrict__ junr) {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t base_q = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64;
     const uint64_t mine = base_q + lane;
-    const bool start = mine < a.n && a.loc[mine] != a.none && a.gs[mine] == mine && first_fail[mine] != 0xFFFFFFFFu &&
-                       gend[mine] - first_fail[mine] < big_from;
+    const bool failing = mine < a.n && a.loc[mine] != a.none && a.gs[mine] == mine && first_fail[mine] != 0xFFFFFFFFu;
+    const bool start = failing && gend[mine] - first_fail[mine] < big_from;
+    if (failing && !start) {
+        list[atomicAdd(count, 1u)] = (uint32_t)mine;
+        if (junr) junr[mine] = 0;  // wp_jump_links: no unresolved candidate yet
+    }
     uint64_t groups = __builtin_amdgcn_ballot_w64(start);
     while (groups) {
         const uint64_t g = base_q + __builtin_ctzll(groups);
@@ -330,22 +358,6 @@ __global__ __launch_bounds__(256) void wp_finish_groups(WpArgs a, WpCls kc, DevT
             pos += 64 * kFinishChunks;
         }
     }
-}
-
-// group extents: gend[g] = one past the last sorted position of the group starting at g
-__global__ void wp_group_ends(WpArgs a, uint32_t *__restrict__ gend) {
-    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= a.n) return;
-    if (q + 1 == a.n || a.loc[q + 1] != a.loc[q]) gend[a.gs[q]] = (uint32_t)(q + 1);
-}
-
-// failing groups with at least kBigGroup ops from their first failure on (a hot key's run of
-// NotNeededUpdate / DIRTY ops) -> list
-__global__ void wp_big_groups(WpArgs a, const uint32_t *__restrict__ first_fail, const uint32_t *__restrict__ gend,
-                              uint32_t *__restrict__ list, uint32_t *__restrict__ count, uint32_t big_from) {
-    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= a.n || a.loc[q] == a.none || a.gs[q] != q || first_fail[q] == 0xFFFFFFFFu) return;
-    if (gend[q] - first_fail[q] >= big_from) list[atomicAdd(count, 1u)] = (uint32_t)q;
 }
 
 // step 3b for big groups, the walk (round 4; now the fallback of wp_finish_jump): one
@@ -584,6 +596,229 @@ __global__ __launch_bounds__(1024) void wp_finish_jump(WpArgs a, WpCls kc, DevTa
     }
 }
 
+// wp_finish_jump with its per-op phases grid-wide (STAGE_WP_FINISH unset; "jump1": the kernel
+// above).  In wp_finish_jump a group's phases A (nxt / exit / mask) and C (return codes) run
+// inside its one workgroup, a 64-op chunk per wave and pass: a Zipf-0.99 hot key (~44 K ops)
+// takes ~43 dependent passes per wave in each.  Here A and C run over every big group at once, a
+// wave per absolute 64-position chunk (wp_jump_links, wp_jump_codes), and the per-group workgroup
+// keeps the start search and the chain walk B (wp_jump_chain).  A chunk may hold the end of one
+// group and the start of the next: the chain's per-chunk record is keyed by max(chunk start,
+// group head), distinct for the two.  Phase A starts at the chain's earliest possible node (f - 1
+// when the head succeeded, else the head), so an unresolved candidate before the actual start
+// (the head-failed case) only sends the group to the walk, which is exact either way.
+__device__ __forceinline__ bool jump_member(const WpArgs &a, const uint32_t *__restrict__ first_fail,
+                                            const uint32_t *__restrict__ gend, uint32_t big_from, uint64_t p,
+                                            uint64_t &g, uint64_t &f, uint64_t &end) {
+    if (p >= a.n || a.loc[p] == a.none) return false;
+    g = a.gs[p];
+    const uint32_t ff = first_fail[g];
+    if (ff == 0xFFFFFFFFu || gend[g] - ff < big_from) return false;
+    f = ff;
+    end = gend[g];
+    return true;
+}
+
+__global__ __launch_bounds__(256) void wp_jump_links(WpArgs a, WpCls kc, const uint32_t *__restrict__ first_fail,
+                                                     const uint32_t *__restrict__ gend, uint32_t big_from,
+                                                     const uint32_t *__restrict__ cfirst, uint32_t *__restrict__ jx,
+                                                     uint64_t *__restrict__ jm, uint8_t *__restrict__ junr) {
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // blockDim: a multiple of 64
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t cb = p - lane;
+    uint64_t g = 0, f = 0, end = 0;
+    bool in = jump_member(a, first_fail, gend, big_from, p, g, f, end);
+    in = in && p >= (f > g ? f - 1 : g);
+    if (!__builtin_amdgcn_ballot_w64(in)) return;  // wave-uniform
+    uint32_t J = kNone;
+    uint64_t M = 0;
+    if (in) {
+        M = 1ull << lane;
+        const uint32_t cp = commit_of(a, a.op[p]);
+        if (cp != 0) {  // an uncommitted success leaves every later op DIRTY
+            const uint32_t cl = kc.cls[p];
+            const uint64_t cand = (p + 1 < end && kc.cls[p + 1] == cl) ? cfirst[cl + 1] : p + 1;
+            if (cand < end) {
+                if (a.writer[a.op[cand]] >= cp) J = (uint32_t)cand;
+                else junr[g] = 1;  // (benign race: every writer stores 1)
+            }
+        }
+    }
+    const uint32_t cend = (uint32_t)(cb + 64);
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {  // doubling inside the chunk: J = f^(2^r)(p), M = its path
+        const bool hop = J < cend;
+        const int src = hop ? (int)(J - (uint32_t)cb) : (int)lane;
+        const uint32_t Jn = (uint32_t)__shfl((int)J, src, 64);
+        const uint64_t Mn = __shfl(M, src, 64);
+        if (hop) {
+            J = Jn;
+            M |= Mn;
+        }
+    }
+    if (in) {
+        jx[p] = J;
+        jm[p] = M;
+    }
+}
+
+__global__ __launch_bounds__(1024) void wp_jump_chain(WpArgs a, WpCls kc, DevTable t, uint8_t *__restrict__ rcs,
+                                                      uint8_t *__restrict__ succ, int32_t *__restrict__ prev,
+                                                      const uint32_t *__restrict__ first_fail,
+                                                      const uint32_t *__restrict__ gend,
+                                                      const uint32_t *__restrict__ list,
+                                                      const uint32_t *__restrict__ count,
+                                                      const uint32_t *__restrict__ jx, const uint64_t *__restrict__ jm,
+                                                      uint64_t *__restrict__ ci, uint32_t *__restrict__ gst,
+                                                      const uint8_t *__restrict__ junr) {
+    constexpr uint32_t kSpanChunks = 64, kSpan = kSpanChunks * 64;  // 4096 positions, 48 KB a buffer
+    __shared__ uint32_t s_jx[2][kSpan];
+    __shared__ uint64_t s_jm[2][kSpan];
+    __shared__ uint64_t s_first[16];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t nbig = *count;
+    for (uint32_t i = blockIdx.x; i < nbig; i += gridDim.x) {
+        const uint64_t g = list[i];
+        const uint64_t l = a.loc[g], end = gend[g];
+        const SlotInfo base = t.slot[l];
+        const uint64_t f = first_fail[g];
+        uint64_t start;
+        if (f > g) {
+            start = f - 1;
+        } else {  // the head failed: the first op that succeeds against the epoch-start state
+            start = ~0ull;
+            for (uint64_t done = g; done < end && start == ~0ull; done += 1024) {
+                const uint64_t q = done + (uint64_t)wv * 64 + lane;
+                const uint8_t r = q < end ? wp_eval(a, kc, t, q, g, -1, base) : (uint8_t)0xFF;
+                uint64_t wf = r == STAGE_RC_OK ? q : ~0ull;
+                for (int o = 32; o > 0; o >>= 1) {
+                    const uint64_t x = __shfl_xor(wf, o, 64);
+                    wf = x < wf ? x : wf;
+                }
+                __syncthreads();
+                if (lane == 0) s_first[wv] = wf;
+                __syncthreads();
+                uint64_t bf = ~0ull;
+#pragma unroll
+                for (int w = 0; w < 16; ++w) bf = s_first[w] < bf ? s_first[w] : bf;
+                if (q < end && q <= bf) {
+                    rcs[q] = r;
+                    succ[q] = q == bf;
+                    prev[q] = -1;
+                }
+                start = bf;
+            }
+        }
+        if (threadIdx.x == 0) gst[g] = start == ~0ull ? kNone : (uint32_t)start;
+        if (start == ~0ull) continue;  // nothing succeeds: every op was evaluated above
+        if (junr[g]) {  // a candidate's writer is older than the commit: walk the group instead
+            finish_big_walk(a, kc, t, rcs, succ, prev, g, end, f, base, s_first);
+            __syncthreads();
+            continue;
+        }
+        // B. the chain, chunk to chunk, as in wp_finish_jump but over absolute chunks, the
+        // exits and masks staged through LDS a span of kSpanChunks chunks at a time: waves 1-15
+        // fill the next span while wave 0 walks this one (from registers, kPre chunks per LDS
+        // batch, by readlane)
+        const uint64_t c_lo = start & ~63ull, nch = (end - c_lo + 63) / 64;
+        const uint64_t nspan = (nch + kSpanChunks - 1) / kSpanChunks;
+        auto fill = [&](uint64_t sp, int buf, uint32_t t0, uint32_t nt) {
+            const uint64_t pbase = c_lo + sp * kSpan;
+            for (uint32_t j0 = t0; j0 < kSpan; j0 += 4 * nt) {
+                uint32_t x[4];
+                uint64_t m[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const uint32_t j = j0 + u * nt;
+                    const uint64_t p = pbase + j;
+                    const bool ok = j < kSpan && p >= start && p < end;
+                    x[u] = ok ? jx[p] : kNone;
+                    m[u] = ok ? jm[p] : 0ull;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const uint32_t j = j0 + u * nt;
+                    if (j < kSpan) {
+                        s_jx[buf][j] = x[u];
+                        s_jm[buf][j] = m[u];
+                    }
+                }
+            }
+        };
+        fill(0, 0, threadIdx.x, blockDim.x);
+        __syncthreads();
+        uint64_t e = start;
+        int64_t carry = f > g ? (start > g ? (int64_t)start - 1 : -1) : -1;
+        for (uint64_t sp = 0; sp < nspan; ++sp) {
+            const int buf = (int)(sp & 1);
+            if (wv != 0) {
+                if (sp + 1 < nspan) fill(sp + 1, buf ^ 1, threadIdx.x - 64, blockDim.x - 64);
+            } else {
+                constexpr int kPre = 16;
+                const uint64_t ch0 = sp * kSpanChunks;
+                for (uint32_t k0 = 0; k0 < (uint32_t)kSpanChunks && ch0 + k0 < nch; k0 += kPre) {
+                    uint32_t xr[kPre];
+                    uint64_t mr[kPre];
+#pragma unroll
+                    for (int k = 0; k < kPre; ++k) {
+                        xr[k] = s_jx[buf][(k0 + k) * 64 + lane];
+                        mr[k] = s_jm[buf][(k0 + k) * 64 + lane];
+                    }
+#pragma unroll
+                    for (int k = 0; k < kPre; ++k) {
+                        if (ch0 + k0 + k >= nch) break;
+                        const uint64_t cb = c_lo + 64 * (ch0 + k0 + k);
+                        uint64_t entry = kNone;
+                        int64_t next_carry = carry;
+                        if (e != kNone && e < cb + 64) {  // wave-uniform
+                            entry = e;
+                            const int el = (int)(e - cb);
+                            const uint64_t m =
+                                ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(mr[k] >> 32), el) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mr[k], el);
+                            next_carry = (int64_t)(cb + 63 - __builtin_clzll(m));
+                            e = (uint32_t)__builtin_amdgcn_readlane((int)xr[k], el);
+                        }
+                        if (lane == 0) ci[cb > g ? cb : g] = entry | ((uint64_t)(uint32_t)(int32_t)carry << 32);
+                        carry = next_carry;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void wp_jump_codes(WpArgs a, WpCls kc, DevTable t, uint8_t *__restrict__ rcs,
+                                                     uint8_t *__restrict__ succ, int32_t *__restrict__ prev,
+                                                     const uint32_t *__restrict__ first_fail,
+                                                     const uint32_t *__restrict__ gend, uint32_t big_from,
+                                                     const uint32_t *__restrict__ gst, const uint8_t *__restrict__ junr,
+                                                     const uint64_t *__restrict__ jm, const uint64_t *__restrict__ ci) {
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t lane = (uint32_t)(p & 63);
+    const uint64_t cb = p - lane;
+    uint64_t g = 0, f = 0, end = 0;
+    if (!jump_member(a, first_fail, gend, big_from, p, g, f, end) || junr[g]) return;
+    const uint32_t st = gst[g];
+    if (st == kNone || p < st) return;
+    const uint64_t info = ci[cb > g ? cb : g];
+    const uint32_t entry = (uint32_t)info;
+    const int32_t carry = (int32_t)(uint32_t)(info >> 32);
+    const uint64_t M = entry != kNone ? jm[entry] : 0ull;
+    const bool s = (M >> lane) & 1ull;
+    const uint64_t below = M & (lane ? ~0ull >> (64 - lane) : 0ull);
+    const int64_t ps = below ? (int64_t)(cb + 63 - __builtin_clzll(below)) : (int64_t)carry;
+    succ[p] = s;
+    prev[p] = (int32_t)ps;
+    if (s) {
+        rcs[p] = (uint8_t)STAGE_RC_OK;
+    } else {
+        SlotInfo base{};
+        if (ps < 0) base = t.slot[a.loc[g]];  // the epoch-start state matters only against no success
+        rcs[p] = wp_eval(a, kc, t, p, g, ps, base);
+    }
+}
+
 __global__ __launch_bounds__(1024) void wp_finish_big(WpArgs a, WpCls kc, DevTable t, uint8_t *__restrict__ rcs,
                                                       uint8_t *__restrict__ succ, int32_t *__restrict__ prev,
                                                       const uint32_t *__restrict__ first_fail,
@@ -597,16 +832,6 @@ __global__ __launch_bounds__(1024) void wp_finish_big(WpArgs a, WpCls kc, DevTab
         finish_big_walk(a, kc, t, rcs, succ, prev, g, gend[g], first_fail[g], t.slot[a.loc[g]], s_first);
         __syncthreads();
     }
-}
-
-// first position of every delta class (cls = inclusive sum of wp_classify's breaks); cfirst[last
-// class + 1] = n, so the run after a group's last run starts at or past the group's end
-__global__ void wp_class_first(const uint32_t *__restrict__ brk, const uint32_t *__restrict__ cls, uint64_t n,
-                               uint32_t *__restrict__ cfirst) {
-    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= n) return;
-    if (brk[q]) cfirst[cls[q]] = (uint32_t)q;
-    if (q + 1 == n) cfirst[cls[q] + 1] = (uint32_t)n;
 }
 
 // step 4 input: successes in the low word, committed successes in the high word
@@ -742,6 +967,7 @@ struct FinRec {
     uint64_t loc, meta;
     uint32_t next, image;
 };
+static_assert(sizeof(FinRec) == 24, "wp_keys initialises a FinRec as three 8-byte words");
 
 // step 6: the last success of each group publishes the slot word; every op gets its code
 __global__ void wp_publish(WpArgs a, SlotInfo *__restrict__ slot, const uint8_t *__restrict__ rcs,
@@ -959,6 +1185,7 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
                        o_ranks = take(n * 8), o_brk = take(n * 4), o_cls = take(n * 4),
                        o_fp = take(n * 8), o_wfp = take(n * 8), o_eqw = take(n), o_wrec = take(n * sizeof(WRec)),
                        o_cfirst = take((n + 2) * 4), o_jx = take(n * 4), o_jm = take(n * 8), o_ci = take(n * 8),
+                       o_gst = take(n * 4), o_junr = take(n),
                        o_cub = take(cub_bytes);
         // the write path's own scratch: an overlapped epoch runs beside the caller's later work,
         // which may use the table's shared scratch (stock-level, CH-Q2, scans)
@@ -989,6 +1216,8 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         auto *jx = (uint32_t *)(buf + o_jx);
         auto *jm = (uint64_t *)(buf + o_jm);
         auto *ci = (uint64_t *)(buf + o_ci);
+        auto *gst = (uint32_t *)(buf + o_gst);
+        auto *junr = buf + o_junr;
         // slot words + totals: read back after this call returns (background adoption)
         // both parities are sized together when no adoption is reading the other one: a first
         // use inside a run of epochs would allocate (and drain the device) in the middle of it
@@ -1035,7 +1264,8 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
 
         // 1. locate
         hip_check(launch_probe(view, d_keys, d_lens, nullptr, nullptr, n, pout, nullptr, ks, t->tune), "locate");
-        wp_keys<<<blocks_for(n, 256), 256, 0, ks>>>(pout, n, view.cap, none, loc0, op0);
+        wp_keys<<<blocks_for(n, 256), 256, 0, ks>>>(pout, n, view.cap, none, loc0, op0, ff, ls, (uint64_t *)fin,
+                                                    (uint32_t *)(tot + 1));
         // 2. group
         hip_check(sort_pairs(cub, cb, (const uint64_t *)loc0, loc, (const uint32_t *)op0, op, n, 0, end_bit, ks), "sort");
         wp_heads<<<blocks_for(n, 256), 256, 0, ks>>>(loc, n, head);
@@ -1045,31 +1275,34 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         WpArgs a{loc, op, gs, d_deltas, d_writer_ids, d_commit_ids, d_sstamps, n, none, delta_len,
                  facts(t).key_pad() + payload_off,
                  (uint64_t)payload_off + delta_len > facts(t).params().payload_size ? 1u : 0u};
-        hip_check(hipMemsetAsync(ff, 0xFF, n * 4, ks), "memset");
-        hip_check(hipMemsetAsync(ls, 0, n * 4, ks), "memset");
-        hip_check(hipMemsetAsync(fin, 0xFF, n * sizeof(FinRec), ks), "memset");
         wp_classify<<<blocks_for(n * kTeam, 256), 256, 0, ks>>>(a, view, brk, fpd, wfp, eqw);
         cb = cub_bytes;
         hip_check(hipcub::DeviceScan::InclusiveSum(cub, cb, brk, cls, (int)n, ks), "delta classes");
         const WpCls kc{cls, fpd, wfp, eqw};
-        wp_speculate<<<blocks_for(n, 256), 256, 0, ks>>>(a, kc, view, rcs, succ, prev, ff);
-        wp_group_ends<<<blocks_for(n, 256), 256, 0, ks>>>(a, gend);
-        hip_check(hipMemsetAsync(tot + 1, 0, 4, ks), "memset");  // big-group count (tot is rewritten in step 4)
+        wp_speculate<<<blocks_for(n, 256), 256, 0, ks>>>(a, kc, view, rcs, succ, prev, ff, gend, brk, cfirst);
         // big failing groups: pointer jumping (STAGE_WP_FINISH=walk: the round-4 walk, for A/B);
         // groups with at least big_from ops from their first failure on (STAGE_WP_BIG) take it,
         // smaller ones a wave each (wp_finish_groups)
-        static const bool walk = std::getenv("STAGE_WP_FINISH") && std::string(std::getenv("STAGE_WP_FINISH")) == "walk";
+        // (STAGE_WP_FINISH=jump1: wp_finish_jump, phases A and C inside the group's workgroup)
+        static const std::string finish_mode = std::getenv("STAGE_WP_FINISH") ? std::getenv("STAGE_WP_FINISH") : "";
+        static const bool walk = finish_mode == "walk", jump1 = finish_mode == "jump1";
         static const uint32_t big_from = walk ? kBigGroup
                                               : (std::getenv("STAGE_WP_BIG") ? (uint32_t)std::atoi(std::getenv("STAGE_WP_BIG"))
                                                                               : kJumpFrom);
-        wp_big_groups<<<blocks_for(n, 256), 256, 0, ks>>>(a, ff, gend, big, (uint32_t *)(tot + 1), big_from);
-        wp_finish_groups<<<blocks_for(n, 256), 256, 0, ks>>>(a, kc, view, rcs, succ, prev, ff, gend, big_from);
+        // (the big-group count, tot[1]'s low word, was zeroed by wp_keys; tot is rewritten in step 4)
+        wp_finish_groups<<<blocks_for(n, 256), 256, 0, ks>>>(a, kc, view, rcs, succ, prev, ff, gend, big_from, big,
+                                                             (uint32_t *)(tot + 1), walk || jump1 ? nullptr : junr);
         if (walk) {
             wp_finish_big<<<256, 1024, 0, ks>>>(a, kc, view, rcs, succ, prev, ff, gend, big, (uint32_t *)(tot + 1));
-        } else {
-            wp_class_first<<<blocks_for(n, 256), 256, 0, ks>>>(brk, cls, n, cfirst);
+        } else if (jump1) {
             wp_finish_jump<<<256, 1024, 0, ks>>>(a, kc, view, rcs, succ, prev, ff, gend, big, (uint32_t *)(tot + 1),
                                                  cfirst, jx, jm, ci);
+        } else {
+            wp_jump_links<<<blocks_for(n, 256), 256, 0, ks>>>(a, kc, ff, gend, big_from, cfirst, jx, jm, junr);
+            wp_jump_chain<<<256, 1024, 0, ks>>>(a, kc, view, rcs, succ, prev, ff, gend, big, (uint32_t *)(tot + 1), jx, jm,
+                                                ci, gst, junr);
+            wp_jump_codes<<<blocks_for(n, 256), 256, 0, ks>>>(a, kc, view, rcs, succ, prev, ff, gend, big_from, gst, junr,
+                                                              jm, ci);
         }
         // 4. number
         wp_flags<<<blocks_for(n, 256), 256, 0, ks>>>(a, succ, flags);

@@ -192,19 +192,22 @@ def test_device_epoch_edge_cases(gpu):
         check_probe(tab, orc, keys, 8, read_ids=np.full(keys.size, rid, np.uint32))
 
 
-@pytest.mark.parametrize("alphabet,old_writers,head_fails", [(3, True, False), (256, True, False),
-                                                              (3, False, False), (256, False, False),
-                                                              (62, False, True)])
-def test_hot_key_groups_finished_by_workgroups(gpu, alphabet, old_writers, head_fails):
+@pytest.mark.parametrize("alphabet,old_writers,head_fails,adjacent", [(3, True, False, False), (256, True, False, False),
+                                                                       (3, False, False, False), (256, False, False, False),
+                                                                       (62, False, True, False), (3, False, False, True),
+                                                                       (62, False, True, True)])
+def test_hot_key_groups_finished_by_workgroups(gpu, alphabet, old_writers, head_fails, adjacent):
     """Groups longer than the workgroup finisher's threshold (2048 ops from the first failure):
     three hot keys hammered ~6000 times each in one epoch with a 3-letter delta alphabet
     (NotNeededUpdate and successes interleave) or RunMixed's 256 / 62 (successes with sparse
     failures), a few left in flight (the rest of that group DIRTY) -- return codes, versions and
     reads equal to the oracle applied op by op.  Without writers older than the record the groups
-    are finished by pointer jumping (wp_finish_jump); with them (NotNeededUpdate by cstamp) the
+    are finished by pointer jumping (wp_jump_links / _chain / _codes); with them (NotNeededUpdate by cstamp) the
     chain is not known locally and the walk finishes them.  head_fails: every hot group's first op
     repeats the record's current column (NotNeededUpdate against the epoch-start state), so the
-    chain starts behind a failed head."""
+    chain starts behind a failed head.  adjacent: two hot keys in neighbouring slots, so their
+    groups meet inside one 64-position chunk (the grid-wide jump phases key the chain's per-chunk
+    record by group)."""
     n = 20000
     tab = stage.Table(key_width=8)
     tab.load_ycsb(0, n, 8, mode=1)
@@ -215,7 +218,7 @@ def test_hot_key_groups_finished_by_workgroups(gpu, alphabet, old_writers, head_
     counter = 10
     for epoch in range(2):
         m = 24000
-        hot = np.array([3, 1000, 19999], np.uint64)
+        hot = np.array([3, 4, 19999] if adjacent else [3, 1000, 19999], np.uint64)
         keys = np.where(rng.random(m) < 0.75, rng.choice(hot, m), rng.integers(0, n + 50, m)).astype(np.uint64)
         deltas = rng.integers(0, alphabet, (m, 1), dtype=np.uint8).repeat(16, 1)
         if head_fails:  # the first op of each hot key writes what its row already holds there
