@@ -142,34 +142,46 @@ __device__ __forceinline__ uint64_t word_fp(uint32_t w, uint32_t k) {
     return fmix64(((uint64_t)k << 32 | w) ^ 0x9e3779b97f4a7c15ull);
 }
 
-// step 3 preparation: a team of kTeam lanes per sorted position reads its delta (and its
-// predecessor's, or at a group head the epoch-start window) with word loads, 4 per lane in
-// flight together
+// step 3 preparation, in op order before the sort (so it runs beside the read probe rather
+// than after it): a team of kTeam lanes per op reads its delta and, for a found key, its slot's
+// epoch-start window with word loads, 4 per lane in flight together -> the delta's fingerprint,
+// the window's, and whether the two are equal.  The sort's input and the epoch's
+// position-indexed state (first failures none, last-success marks 0, FinRecs all ones -- 24 B
+// each -- and the big-group count 0) are written on the way, so no fills follow on the stream.
 constexpr uint32_t kTeam = 8;
-__global__ __launch_bounds__(256) void wp_classify(WpArgs a, DevTable t, uint32_t *__restrict__ brk,
-                                                   uint64_t *__restrict__ fp, uint64_t *__restrict__ wfp,
-                                                   uint8_t *__restrict__ eqw) {
+__global__ __launch_bounds__(256) void wp_keys(const stage_probe_out_dev *__restrict__ pout, uint64_t n, uint64_t none,
+                                               DevTable t, const uint8_t *__restrict__ deltas, uint32_t delta_len,
+                                               uint32_t win_off, uint32_t bad_range, uint64_t *__restrict__ loc,
+                                               uint32_t *__restrict__ op,
+                                               uint64_t *__restrict__ fp_op, uint64_t *__restrict__ wfp_op,
+                                               uint8_t *__restrict__ eqw_op, uint32_t *__restrict__ first_fail,
+                                               uint32_t *__restrict__ last_succ, uint64_t *__restrict__ fin_words,
+                                               uint32_t *__restrict__ big_count) {
+    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63, tl = lane & (kTeam - 1);
-    const uint64_t q = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / kTeam;
-    const bool live = q < a.n && a.loc[q] != a.none;
-    const bool head = live && a.gs[q] == q;
-    const uint8_t *d = nullptr, *p = nullptr;
-    if (live) {
-        d = a.deltas + (uint64_t)a.op[q] * a.delta_len;
-        p = head ? t.heap + (uint64_t)t.slot[a.loc[q]].image * t.hstride + a.win_off
-                 : a.deltas + (uint64_t)a.op[q - 1] * a.delta_len;
+    const uint64_t i = gid / kTeam;
+    if (gid == 0) *big_count = 0;
+    const bool valid = i < n;
+    uint64_t l = none;
+    if (valid) {
+        const uint32_t slot = pout[i].w[2] & 0xFFFF;
+        l = slot == 0xFFFF ? none : (uint64_t)pout[i].w[1] * t.cap + slot;
     }
-    const bool al = live && ((((uintptr_t)d | (uintptr_t)p) & 3u) == 0);
+    const bool found = valid && l != none;
+    const uint8_t *d = valid ? deltas + i * delta_len : nullptr;
+    // (a window past the payload: every op is INVALID, wp_eval never compares with it)
+    const uint8_t *w = found && !bad_range ? t.heap + (uint64_t)t.slot[l].image * t.hstride + win_off : nullptr;
+    const bool al = found && ((((uintptr_t)d | (uintptr_t)w) & 3u) == 0);
     uint64_t h = 0, hw = 0;
     bool ne = false;
-    const uint32_t words = live ? (a.delta_len + 3) / 4 : 0u;
+    const uint32_t words = found ? (delta_len + 3) / 4 : 0u;
     for (uint32_t k0 = 0; k0 < words; k0 += 4 * kTeam) {
         uint32_t x[4], y[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const uint32_t k = k0 + u * kTeam + tl;
-            x[u] = k < words ? ld_word(d, k, a.delta_len, al) : 0u;
-            y[u] = k < words ? ld_word(p, k, a.delta_len, al) : 0u;
+            x[u] = k < words ? ld_word(d, k, delta_len, al) : 0u;
+            y[u] = k < words && w ? ld_word(w, k, delta_len, al) : 0u;
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -188,13 +200,48 @@ __global__ __launch_bounds__(256) void wp_classify(WpArgs a, DevTable t, uint32_
         h ^= __shfl_xor(h, o, 64);
         hw ^= __shfl_xor(hw, o, 64);
     }
-    if (tl == 0 && q < a.n) {
-        brk[q] = !live || head || team_ne ? 1u : 0u;
-        fp[q] = h;
-        if (head) {
-            wfp[q] = hw;
-            eqw[q] = team_ne ? 0 : 1;
+    if (tl == 0 && valid) {
+        loc[i] = l;
+        op[i] = (uint32_t)i;
+        fp_op[i] = h;
+        if (found) {
+            wfp_op[i] = hw;
+            eqw_op[i] = team_ne ? 0 : 1;
         }
+        first_fail[i] = 0xFFFFFFFFu;
+        last_succ[i] = 0;
+        fin_words[3 * i] = ~0ull;
+        fin_words[3 * i + 1] = ~0ull;
+        fin_words[3 * i + 2] = ~0ull;
+    }
+}
+
+// step 3 preparation after the sort, a thread per sorted position: the op's fingerprints
+// gathered; a break where the group starts or the delta differs from its predecessor's (a
+// fingerprint mismatch, or equal fingerprints and unequal bytes)
+__global__ void wp_classify(WpArgs a, const uint64_t *__restrict__ fp_op, const uint64_t *__restrict__ wfp_op,
+                            const uint8_t *__restrict__ eqw_op, uint32_t *__restrict__ brk, uint64_t *__restrict__ fp,
+                            uint64_t *__restrict__ wfp, uint8_t *__restrict__ eqw) {
+    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= a.n) return;
+    const bool live = a.loc[q] != a.none;
+    const bool head = live && a.gs[q] == q;
+    const uint32_t o = a.op[q];
+    const uint64_t h = live ? fp_op[o] : 0ull;
+    uint32_t b = 1;
+    if (live && !head) {
+        const uint32_t po = a.op[q - 1];
+        b = h != fp_op[po] ? 1u
+                           : (bytes_equal(a.deltas + (uint64_t)o * a.delta_len, a.deltas + (uint64_t)po * a.delta_len,
+                                          a.delta_len)
+                                  ? 0u
+                                  : 1u);
+    }
+    brk[q] = b;
+    fp[q] = h;
+    if (head) {
+        wfp[q] = wfp_op[o];
+        eqw[q] = eqw_op[o];
     }
 }
 
@@ -203,26 +250,6 @@ __device__ __forceinline__ uint64_t lanes_between(uint32_t from, uint32_t lane) 
     const uint64_t below = lane ? ~0ull >> (64 - lane) : 0ull;
     const uint64_t skip = from ? ~0ull >> (64 - from) : 0ull;
     return below & ~skip;
-}
-
-// the sort's input, and the epoch's position-indexed state initialised on the way (no fills on
-// the stream later): first failures none, last-success marks 0, FinRecs all ones (24 B each),
-// the big-group count 0
-__global__ void wp_keys(const stage_probe_out_dev *__restrict__ pout, uint64_t n, uint32_t cap, uint64_t none,
-                        uint64_t *__restrict__ loc, uint32_t *__restrict__ op, uint32_t *__restrict__ first_fail,
-                        uint32_t *__restrict__ last_succ, uint64_t *__restrict__ fin_words,
-                        uint32_t *__restrict__ big_count) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i == 0) *big_count = 0;
-    if (i >= n) return;
-    const uint32_t slot = pout[i].w[2] & 0xFFFF;
-    loc[i] = slot == 0xFFFF ? none : (uint64_t)pout[i].w[1] * cap + slot;
-    op[i] = (uint32_t)i;
-    first_fail[i] = 0xFFFFFFFFu;
-    last_succ[i] = 0;
-    fin_words[3 * i] = ~0ull;
-    fin_words[3 * i + 1] = ~0ull;
-    fin_words[3 * i + 2] = ~0ull;
 }
 
 __global__ void wp_heads(const uint64_t *__restrict__ loc, uint64_t n, uint32_t *__restrict__ head) {
@@ -1185,7 +1212,8 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
                        o_ranks = take(n * 8), o_brk = take(n * 4), o_cls = take(n * 4),
                        o_fp = take(n * 8), o_wfp = take(n * 8), o_eqw = take(n), o_wrec = take(n * sizeof(WRec)),
                        o_cfirst = take((n + 2) * 4), o_jx = take(n * 4), o_jm = take(n * 8), o_ci = take(n * 8),
-                       o_gst = take(n * 4), o_junr = take(n),
+                       o_gst = take(n * 4), o_junr = take(n), o_fpo = take(n * 8), o_wfpo = take(n * 8),
+                       o_eqwo = take(n),
                        o_cub = take(cub_bytes);
         // the write path's own scratch: an overlapped epoch runs beside the caller's later work,
         // which may use the table's shared scratch (stock-level, CH-Q2, scans)
@@ -1218,6 +1246,8 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         auto *ci = (uint64_t *)(buf + o_ci);
         auto *gst = (uint32_t *)(buf + o_gst);
         auto *junr = buf + o_junr;
+        auto *fp_op = (uint64_t *)(buf + o_fpo), *wfp_op = (uint64_t *)(buf + o_wfpo);
+        auto *eqw_op = buf + o_eqwo;
         // slot words + totals: read back after this call returns (background adoption)
         // both parities are sized together when no adoption is reading the other one: a first
         // use inside a run of epochs would allocate (and drain the device) in the middle of it
@@ -1264,8 +1294,11 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
 
         // 1. locate
         hip_check(launch_probe(view, d_keys, d_lens, nullptr, nullptr, n, pout, nullptr, ks, t->tune), "locate");
-        wp_keys<<<blocks_for(n, 256), 256, 0, ks>>>(pout, n, view.cap, none, loc0, op0, ff, ls, (uint64_t *)fin,
-                                                    (uint32_t *)(tot + 1));
+        wp_keys<<<blocks_for(n * kTeam, 256), 256, 0, ks>>>(pout, n, none, view, d_deltas, delta_len,
+                                                            facts(t).key_pad() + payload_off,
+                                                            (uint64_t)payload_off + delta_len > facts(t).params().payload_size,
+                                                            loc0, op0, fp_op, wfp_op,
+                                                            eqw_op, ff, ls, (uint64_t *)fin, (uint32_t *)(tot + 1));
         // 2. group
         hip_check(sort_pairs(cub, cb, (const uint64_t *)loc0, loc, (const uint32_t *)op0, op, n, 0, end_bit, ks), "sort");
         wp_heads<<<blocks_for(n, 256), 256, 0, ks>>>(loc, n, head);
@@ -1275,7 +1308,7 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         WpArgs a{loc, op, gs, d_deltas, d_writer_ids, d_commit_ids, d_sstamps, n, none, delta_len,
                  facts(t).key_pad() + payload_off,
                  (uint64_t)payload_off + delta_len > facts(t).params().payload_size ? 1u : 0u};
-        wp_classify<<<blocks_for(n * kTeam, 256), 256, 0, ks>>>(a, view, brk, fpd, wfp, eqw);
+        wp_classify<<<blocks_for(n, 256), 256, 0, ks>>>(a, fp_op, wfp_op, eqw_op, brk, fpd, wfp, eqw);
         cb = cub_bytes;
         hip_check(hipcub::DeviceScan::InclusiveSum(cub, cb, brk, cls, (int)n, ks), "delta classes");
         const WpCls kc{cls, fpd, wfp, eqw};
