@@ -750,11 +750,11 @@ __global__ __launch_bounds__(1024) void wp_jump_chain(WpArgs a, WpCls kc, DevTab
         const uint64_t nspan = (nch + kSpanChunks - 1) / kSpanChunks;
         auto fill = [&](uint64_t sp, int buf, uint32_t t0, uint32_t nt) {
             const uint64_t pbase = c_lo + sp * kSpan;
-            for (uint32_t j0 = t0; j0 < kSpan; j0 += 4 * nt) {
-                uint32_t x[4];
-                uint64_t m[4];
+            for (uint32_t j0 = t0; j0 < kSpan; j0 += 8 * nt) {  // one round trip for 512+ threads
+                uint32_t x[8];
+                uint64_t m[8];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
+                for (int u = 0; u < 8; ++u) {
                     const uint32_t j = j0 + u * nt;
                     const uint64_t p = pbase + j;
                     const bool ok = j < kSpan && p >= start && p < end;
@@ -762,7 +762,7 @@ __global__ __launch_bounds__(1024) void wp_jump_chain(WpArgs a, WpCls kc, DevTab
                     m[u] = ok ? jm[p] : 0ull;
                 }
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
+                for (int u = 0; u < 8; ++u) {
                     const uint32_t j = j0 + u * nt;
                     if (j < kSpan) {
                         s_jx[buf][j] = x[u];
