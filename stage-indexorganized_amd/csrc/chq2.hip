@@ -472,6 +472,16 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
                        o_vis = take(n_max), o_rank = take(n_max), o_koff = take(n_max * 4),
                        o_ccnt = take(std::max<uint64_t>(nchunks, 1) * kVisits * 4),
                        o_kcnt = take(std::max<uint64_t>(nchunks, 1) * kVisits * 4), o_nv = take(4);
+        // NATION's scan (scan_sz 65) is past the compact scan kernel's 63 records; a table of fewer
+        // slots than that returns the same records for every scan size of at least its slot count
+        // (the scan ends at the table's end), so such a table is scanned with that size instead
+        uint32_t nat_scan = kNationScan;
+        if (nation->dev.view.nleaves <= 4) {
+            uint64_t slots = 0;
+            for (const auto &L : host(nation).leaves_)
+                if (L.live) slots += L.count;
+            if (slots < (uint64_t)kNationScan) nat_scan = (uint32_t)std::max<uint64_t>(slots, 1);
+        }
         // a batch still in flight uses these scratch buffers: growing one (a reallocation) waits
         // for it first
         const uint64_t reg_rows = 64 + (uint64_t)kRegionScan * region->dev.view.stride,
@@ -539,7 +549,7 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
             hip_check(hipStreamWaitEvent(ns_s, ev[0], 0), "fork");
             const auto *d_zero = (const uint64_t *)(mir + q_zero);
             const uint8_t *regs = scan_rows(region, d_zero, kRegionScan, rs_s);
-            const uint8_t *nats = scan_rows(nation, d_zero, kNationScan, ns_s);
+            const uint8_t *nats = scan_rows(nation, d_zero, nat_scan, ns_s);
             hip_check(hipEventRecord(ev[1], rs_s), "join");
             hip_check(hipEventRecord(ev[2], ns_s), "join");
             hip_check(hipStreamWaitEvent(s, ev[1], 0), "join");
@@ -605,7 +615,7 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         put(&nation->scan_tune, sizeof nation->scan_tune);
         for (uint64_t v : {(uint64_t)(uintptr_t)d_map_keys, (uint64_t)target_region, (uint64_t)nq, max_out,
                            (uint64_t)(uintptr_t)host_out, (uint64_t)(uintptr_t)pq, (uint64_t)(uintptr_t)buf, q_end,
-                           n_max, m_max, n_hint, m_hint, (uint64_t)(uintptr_t)s})
+                           n_max, m_max, n_hint, m_hint, (uint64_t)(uintptr_t)s, (uint64_t)nat_scan})
             putv(v);
         lap("key");
         Q2Graph &G = stock->q2g[slot];
