@@ -773,8 +773,13 @@ __global__ __launch_bounds__(1024) void wp_jump_chain(WpArgs a, WpCls kc, DevTab
         };
         fill(0, 0, threadIdx.x, blockDim.x);
         __syncthreads();
-        uint64_t e = start;
-        int64_t carry = f > g ? (start > g ? (int64_t)start - 1 : -1) : -1;
+        // the walk's state is wave-uniform and kept in scalar registers (32-bit positions, values
+        // taken by readlane), so each chunk step is a few scalar instructions and no exec-mask
+        // branches; lane kk collects chunk kk's record and the span's records are stored at once
+        // (start comes through LDS in the head-failed case: readfirstlane tells the compiler it is
+        // uniform, so the walk stays on the scalar unit)
+        uint32_t e = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)start);
+        int32_t carry = __builtin_amdgcn_readfirstlane(f > g ? (start > g ? (int32_t)(start - 1) : -1) : -1);
         for (uint64_t sp = 0; sp < nspan; ++sp) {
             const int buf = (int)(sp & 1);
             if (wv != 0) {
@@ -782,32 +787,42 @@ __global__ __launch_bounds__(1024) void wp_jump_chain(WpArgs a, WpCls kc, DevTab
             } else {
                 constexpr int kPre = 16;
                 const uint64_t ch0 = sp * kSpanChunks;
-                for (uint32_t k0 = 0; k0 < (uint32_t)kSpanChunks && ch0 + k0 < nch; k0 += kPre) {
-                    uint32_t xr[kPre];
-                    uint64_t mr[kPre];
+                const uint32_t nin = (uint32_t)(nch - ch0 < kSpanChunks ? nch - ch0 : kSpanChunks);
+                const uint32_t cs = (uint32_t)(c_lo + 64 * ch0);  // the span's first chunk start
+                int rec_lo = 0, rec_hi = 0;  // lane kk: chunk kk's record
+                for (uint32_t k0 = 0; k0 < nin; k0 += kPre) {
+                    uint32_t xr[kPre], ml[kPre], mh[kPre];
 #pragma unroll
                     for (int k = 0; k < kPre; ++k) {
-                        xr[k] = s_jx[buf][(k0 + k) * 64 + lane];
-                        mr[k] = s_jm[buf][(k0 + k) * 64 + lane];
+                        const uint32_t j = (k0 + k) * 64 + lane;
+                        xr[k] = s_jx[buf][j];
+                        const uint64_t m = s_jm[buf][j];
+                        ml[k] = (uint32_t)m;
+                        mh[k] = (uint32_t)(m >> 32);
                     }
 #pragma unroll
                     for (int k = 0; k < kPre; ++k) {
-                        if (ch0 + k0 + k >= nch) break;
-                        const uint64_t cb = c_lo + 64 * (ch0 + k0 + k);
-                        uint64_t entry = kNone;
-                        int64_t next_carry = carry;
-                        if (e != kNone && e < cb + 64) {  // wave-uniform
-                            entry = e;
+                        const uint32_t kk = k0 + k, cb = cs + 64 * kk;
+                        e = (uint32_t)__builtin_amdgcn_readfirstlane((int)e);  // scalar compares below
+                        carry = __builtin_amdgcn_readfirstlane(carry);
+                        uint32_t entry = kNone;
+                        int32_t next_carry = carry;
+                        if (kk < nin && e != kNone && e - cb < 64u) {
                             const int el = (int)(e - cb);
-                            const uint64_t m =
-                                ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(mr[k] >> 32), el) << 32) |
-                                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mr[k], el);
-                            next_carry = (int64_t)(cb + 63 - __builtin_clzll(m));
+                            const uint64_t m = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)mh[k], el) << 32) |
+                                               (uint32_t)__builtin_amdgcn_readlane((int)ml[k], el);
+                            next_carry = (int32_t)(cb + 63 - (uint32_t)__builtin_clzll(m));
+                            entry = e;
                             e = (uint32_t)__builtin_amdgcn_readlane((int)xr[k], el);
                         }
-                        if (lane == 0) ci[cb > g ? cb : g] = entry | ((uint64_t)(uint32_t)(int32_t)carry << 32);
+                        rec_lo = lane == kk ? (int)entry : rec_lo;
+                        rec_hi = lane == kk ? carry : rec_hi;
                         carry = next_carry;
                     }
+                }
+                if (lane < nin) {
+                    const uint64_t cb = (uint64_t)cs + 64ull * lane;
+                    ci[cb > g ? cb : g] = (uint64_t)(uint32_t)rec_lo | ((uint64_t)(uint32_t)rec_hi << 32);
                 }
             }
             __syncthreads();
