@@ -1,6 +1,7 @@
 #!/bin/bash
 # wp_jump_chain's phase-B timing (STAGE_WP_CHAIN_DEBUG: the hottest group's first fill, walk and
-# span totals from wall_clock64, printed per epoch)
+# span totals from wall_clock64, printed per epoch).  The instrumentation was a temporary
+# build (wp_finish_jump follow-up); on later trees this only runs C3.
 set -e
 out=gpurun_out/chaindbg
 mkdir -p $out
