@@ -83,3 +83,24 @@ def test_zipf_draws_deterministic_and_threads_agree():
     counts = np.bincount(a.astype(np.int64))
     assert counts.argmax() == 1
     assert 0.01 < counts[1] / a.size < 0.2
+
+
+def test_q2_async_arguments():
+    """stage_ch_query2_batch_async / _wait refuse bad calls before anything reaches a device:
+    a slot outside 0..1, an empty batch, no `out`, a wait on a slot with nothing in flight, and
+    unsynced tables (no device image: STAGE_E_STATE, as every device entry point)."""
+    L = stage.lib()
+    t = stage.Table(key_width=8)
+    n = ctypes.c_uint64()
+    ab = (ctypes.c_int32 * 4)()
+    assert L.stage_ch_query2_wait(t.h, 2, ctypes.byref(n), ab) == -1
+    assert L.stage_ch_query2_wait(t.h, 0, ctypes.byref(n), ab) == -4
+    assert b"in flight" in L.stage_last_error()
+    rids = (ctypes.c_uint32 * 4)(1, 2, 3, 4)
+    out = ctypes.create_string_buffer(4 * 48 * 8)
+    moff = (ctypes.c_uint32 * 10001)()
+    h = t.h
+    assert L.stage_ch_query2_batch_async(h, h, h, h, h, moff, None, 3, rids, 0, out, 8, 0, None) == -1
+    assert L.stage_ch_query2_batch_async(h, h, h, h, h, moff, None, 3, rids, 4, None, 8, 0, None) == -1
+    assert L.stage_ch_query2_batch_async(h, h, h, h, h, moff, ctypes.c_void_p(16), 3, rids, 4, out, 8, 0,
+                                         None) == -4
