@@ -85,8 +85,10 @@ def parse(argv=None):
     p.add_argument("--warehouses", type=int, default=16, help="tpcc: warehouses (10 districts, 3000 orders each)")
     p.add_argument("--items", type=int, default=100_000, help="tpcc: items (stock rows per warehouse)")
     p.add_argument("--q2-batch", type=int, default=16, help="chq2: Q2 transactions per step (stage_ch_query2_batch)")
-    p.add_argument("--q2-async", type=int, default=0, choices=[0, 1],
-                   help="chq2: 1 = two batches in flight (stage_ch_query2_batch_async, slots 0/1 alternating)")
+    p.add_argument("--q2-async", type=int, default=1, choices=[0, 1],
+                   help="chq2: 1 = two batches in flight (stage_ch_query2_batch_async, slots 0/1 alternating: "
+                        "the host stages batch k+1 while the device runs batch k); 0 = one synchronous batch "
+                        "per step (stage_ch_query2_batch)")
     p.add_argument("--rows", type=int, default=100_000_000, help="rows per GPU")
     p.add_argument("--batch", type=int, default=None, help="lookups (c2/c3) or scans (c4) per GPU per step")
     p.add_argument("--theta", type=float, default=None)

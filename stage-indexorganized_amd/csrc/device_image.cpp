@@ -38,8 +38,6 @@ void DeviceImage::release() {
         if (pinned[k]) (void)hipHostFree(pinned[k]);
         pinned[k] = nullptr;
         pinned_cap[k] = 0;
-        if (call_ev[k]) (void)hipEventDestroy(call_ev[k]);
-        call_ev[k] = nullptr;
     }
     for (int k = 0; k < 2; ++k) {
         if (adopt_ev[k]) (void)hipEventDestroy(adopt_ev[k]);

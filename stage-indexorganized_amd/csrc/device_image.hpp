@@ -41,7 +41,6 @@ struct DeviceImage {
     std::vector<uint8_t> staging;  // host staging of incremental patches
     // pinned host staging: [0], [1] the write path's epoch results (by epoch parity); [2] the
     // host copies of one synchronous call (CH-Q2's scan rows, supplier list, records)
-    hipEvent_t call_ev[3] = {nullptr, nullptr, nullptr};  // fork / join events of one synchronous call (CH-Q2)
     void *pinned[4] = {nullptr, nullptr, nullptr, nullptr};  // 0 / 1: write-path adoption; 2 / 3: CH-Q2 slots
     uint64_t pinned_cap[4] = {0, 0, 0, 0};
     uint64_t heap_rows = 0;  // rows the heap buffer can hold
