@@ -300,7 +300,7 @@ __global__ void wp_speculate(WpArgs a, WpCls k, DevTable t, uint8_t *__restrict_
 // key's long run of NotNeededUpdate / DIRTY ops goes 512 ops per pass.
 constexpr int kFinishChunks = 8;
 constexpr uint32_t kBigGroup = 2048;  // ops from the first failure on: a workgroup finishes it (wp_finish_big)
-constexpr uint32_t kJumpFrom = 256;   // ... by pointer jumping (wp_finish_jump)
+constexpr uint32_t kJumpFrom = 128;   // ... by pointer jumping (wp_jump_*; 128 from the r05 sweep)
 // Groups with at least big_from ops from their first failure on go to `list` instead (one
 // atomic per big group; their finishing kernels follow).
 __global__ __launch_bounds__(256) void wp_finish_groups(WpArgs a, WpCls kc, DevTable t, uint8_t *__restrict__ rcs,
