@@ -1770,6 +1770,45 @@ static orc_rmeta *find_meta(orc_tree *t, const uint8_t *key, uint16_t ks, uint8_
     return slot < 0 ? NULL : l_meta(leaf, (uint32_t)slot);
 }
 
+/* Allocations of one writer thread of orc_update_batch_mt: the reference's EphemeralPool and
+ * VersionStore are concurrent pools (ephemeral_pool.cpp:17-44, version_store.cpp); here each
+ * writer keeps its own list and the lists join the tree's registry after the writers end. */
+typedef struct {
+    orc_copy **copies;
+    uint32_t ncopies, capcopies;
+    orc_th **ths;
+    uint32_t nths, capths;
+} alloc_sink;
+static __thread alloc_sink *tl_sink;
+
+static void sink_push(void ***arr, uint32_t *n, uint32_t *cap, void *p) {
+    if (*n == *cap) {
+        *cap = *cap ? 2 * *cap : 1024;
+        *arr = realloc(*arr, sizeof(void *) * *cap);
+        if (!*arr) abort();
+    }
+    (*arr)[(*n)++] = p;
+}
+
+static void register_copy(orc_tree *t, orc_copy *c) {
+    c->reg_next = t->copies;
+    t->copies = c;
+    if (t->ncopies == t->capcopies) {
+        t->capcopies = t->capcopies ? 2 * t->capcopies : 1024;
+        t->copy_by_id = realloc(t->copy_by_id, sizeof(orc_copy *) * t->capcopies);
+        if (!t->copy_by_id) abort();
+    }
+    c->id = t->ncopies;
+    t->copy_by_id[t->ncopies++] = c;
+}
+
+static void register_th(orc_tree *t, orc_th *th) {
+    th->reg_next = t->ths;
+    t->ths = th;
+    th->id = t->nths++;
+    t->retired++;
+}
+
 static orc_copy *copy_alloc(orc_tree *t, const uint8_t *src_key, uint16_t klen, uint64_t next, uint32_t cstamp,
                             uint32_t rstamp) {
     /* EphemeralPool::Allocate, ephemeral_pool.cpp:17-44 */
@@ -1786,15 +1825,10 @@ static orc_copy *copy_alloc(orc_tree *t, const uint8_t *src_key, uint16_t klen, 
     c->image = xmalloc(klen + t->payload_size);
     memcpy(c->image, src_key, klen);                                   /* b_tree.cpp:1143 */
     memcpy(c->image + klen, src_key + pad_key(klen), t->payload_size); /* b_tree.cpp:1144 */
-    c->reg_next = t->copies;
-    t->copies = c;
-    if (t->ncopies == t->capcopies) {
-        t->capcopies = t->capcopies ? 2 * t->capcopies : 1024;
-        t->copy_by_id = realloc(t->copy_by_id, sizeof(orc_copy *) * t->capcopies);
-        if (!t->copy_by_id) abort();
-    }
-    c->id = t->ncopies;
-    t->copy_by_id[t->ncopies++] = c;
+    if (tl_sink)
+        sink_push((void ***)&tl_sink->copies, &tl_sink->ncopies, &tl_sink->capcopies, c);
+    else
+        register_copy(t, c);
     return c;
 }
 
@@ -1856,10 +1890,10 @@ int orc_commit_update(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32
     th->key_len = c->key_len;
     th->slot = xmalloc(c->key_len + t->payload_size);
     memcpy(th->slot, c->image, c->key_len + t->payload_size);
-    th->reg_next = t->ths;
-    t->ths = th;
-    th->id = t->nths++;
-    t->retired++;
+    if (tl_sink)
+        sink_push((void ***)&tl_sink->ths, &tl_sink->nths, &tl_sink->capths, th);
+    else
+        register_th(t, th);
     c->pre = (uint64_t)(uintptr_t)th;
     uint64_t m = mp->meta;
     m = (m & ~M_TXN) | commit_id; /* FinalizeForUpdate(t_cstamp), record_meta.h:146-151 */
@@ -1926,6 +1960,79 @@ uint64_t orc_update_batch(orc_tree *t, const uint64_t *keys, uint32_t key_size, 
         if (rc) rc[i] = (uint8_t)r;
         ok += r == ORC_RET_OK;
     }
+    return ok;
+}
+
+/* The same epoch with T concurrent writers (the CPU baseline of C3's write share).  RunMixed's
+ * writer threads each run LeafNode::Update with CASes on the record's own meta and next words
+ * (b_tree.cpp:1061-1163) and commit their own records (transaction_manager.cpp:610-676): no
+ * update touches another record's bytes, splits never happen on this path, and the leaf status
+ * word is CASed to its own value.  Writer g takes the ops whose key hashes to g, in batch order,
+ * so every key's op sequence -- hence every rc and the final state of every record -- is the
+ * single writer's.  Copy and version allocations go to per-writer lists (alloc_sink) joined to
+ * the tree after the writers end; copy / version ids then follow writer order, not batch order
+ * (ids are handles only; no read result depends on them). */
+typedef struct {
+    orc_tree *t;
+    const uint64_t *keys;
+    uint32_t key_size, payload_off, delta_len, g, T;
+    uint64_t n;
+    const uint8_t *deltas;
+    const uint32_t *wid, *cid;
+    uint8_t *rc;
+    uint64_t ok;
+    alloc_sink sink;
+} upd_job;
+
+static inline uint32_t writer_of(uint64_t k, uint32_t T) { return (uint32_t)(splitmix64(k) % T); }
+
+static void *upd_worker(void *arg) {
+    upd_job *j = arg;
+    tl_sink = &j->sink;
+    uint64_t ok = 0;
+    for (uint64_t i = 0; i < j->n; i++) {
+        uint64_t k = j->keys[i];
+        if (writer_of(k, j->T) != j->g) continue;
+        int r = orc_update(j->t, (const uint8_t *)&k, j->key_size, j->payload_off, j->deltas + i * j->delta_len,
+                           j->delta_len, j->wid[i]);
+        if (r == ORC_RET_OK && j->cid[i])
+            r = orc_commit_update(j->t, (const uint8_t *)&k, j->key_size, j->cid[i], j->cid[i]);
+        if (j->rc) j->rc[i] = (uint8_t)r;
+        ok += r == ORC_RET_OK;
+    }
+    tl_sink = NULL;
+    j->ok = ok;
+    return NULL;
+}
+
+uint64_t orc_update_batch_mt(orc_tree *t, const uint64_t *keys, uint32_t key_size, uint64_t n, uint32_t payload_off,
+                             const uint8_t *deltas, uint32_t delta_len, const uint32_t *wid, const uint32_t *cid,
+                             uint8_t *rc, int nthreads, double *seconds) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    upd_job *jobs = calloc((size_t)nthreads, sizeof(upd_job));
+    pthread_t th[256];
+    if (!jobs) abort();
+    struct timespec a, b;
+    clock_gettime(CLOCK_MONOTONIC, &a);
+    for (int g = 0; g < nthreads; g++) {
+        jobs[g] = (upd_job){t, keys, key_size, payload_off, delta_len, (uint32_t)g, (uint32_t)nthreads, n,
+                            deltas, wid, cid, rc, 0, {0}};
+        pthread_create(&th[g], NULL, upd_worker, &jobs[g]);
+    }
+    for (int g = 0; g < nthreads; g++) pthread_join(th[g], NULL);
+    clock_gettime(CLOCK_MONOTONIC, &b);
+    if (seconds) *seconds = (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
+    uint64_t ok = 0;
+    for (int g = 0; g < nthreads; g++) {
+        alloc_sink *s = &jobs[g].sink;
+        for (uint32_t i = 0; i < s->ncopies; i++) register_copy(t, s->copies[i]);
+        for (uint32_t i = 0; i < s->nths; i++) register_th(t, s->ths[i]);
+        free(s->copies);
+        free(s->ths);
+        ok += jobs[g].ok;
+    }
+    free(jobs);
     return ok;
 }
 

@@ -131,6 +131,11 @@ int orc_commit_update(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32
 uint64_t orc_update_batch(orc_tree *t, const uint64_t *keys, uint32_t key_size, uint64_t n, uint32_t payload_off,
                           const uint8_t *deltas, uint32_t delta_len, const uint32_t *wid, const uint32_t *cid,
                           uint8_t *rc);
+/* the same epoch with nthreads concurrent writers, each key's ops on one writer in batch order
+ * (rc and every record's final state equal orc_update_batch's); seconds = wall time of the writers */
+uint64_t orc_update_batch_mt(orc_tree *t, const uint64_t *keys, uint32_t key_size, uint64_t n, uint32_t payload_off,
+                             const uint8_t *deltas, uint32_t delta_len, const uint32_t *wid, const uint32_t *cid,
+                             uint8_t *rc, int nthreads, double *seconds);
 /* AbortTransaction UPDATE / INSERT entries (transaction_manager.cpp:846-921, 949-979) */
 int orc_abort_update(orc_tree *t, const uint8_t *key, uint32_t key_size);
 int orc_abort_insert(orc_tree *t, const uint8_t *key, uint32_t key_size);

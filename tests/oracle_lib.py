@@ -62,6 +62,8 @@ _SIG = {
     "orc_abort_update": (ctypes.c_int, [vp, vp, u32]),
     "orc_abort_insert": (ctypes.c_int, [vp, vp, u32]),
     "orc_update_batch": (u64, [vp, vp, u32, u64, u32, vp, u32, vp, vp, vp]),
+    "orc_update_batch_mt": (u64, [vp, vp, u32, u64, u32, vp, u32, vp, vp, vp, ctypes.c_int,
+                                  ctypes.POINTER(ctypes.c_double)]),
     "orc_tree_set_bulk": (None, [vp, ctypes.c_int]),
     "orc_load_ycsb_parallel": (u64, [vp, u64, u64, u32, ctypes.c_int, ctypes.c_int]),
     "orc_resolve_locations": (None, [vp, vp, u64, vp, vp]),
@@ -291,6 +293,19 @@ class OracleTree:
         ok = lib().orc_update_batch(self.t, keys.ctypes.data, key_size, keys.size, payload_off, deltas.ctypes.data,
                                     deltas.shape[1], wid.ctypes.data, cid.ctypes.data, rc.ctypes.data)
         return rc, int(ok)
+
+    def update_batch_mt(self, keys, key_size, payload_off, deltas, wid, cid, nthreads):
+        """orc_update_batch_mt (nthreads concurrent writers): returns (rc[n], n_ok, seconds)"""
+        keys = np.ascontiguousarray(keys, np.uint64)
+        deltas = np.ascontiguousarray(deltas, np.uint8).reshape(keys.size, -1)
+        wid = np.ascontiguousarray(wid, np.uint32)
+        cid = np.ascontiguousarray(cid, np.uint32)
+        rc = np.zeros(keys.size, np.uint8)
+        sec = ctypes.c_double()
+        ok = lib().orc_update_batch_mt(self.t, keys.ctypes.data, key_size, keys.size, payload_off, deltas.ctypes.data,
+                                       deltas.shape[1], wid.ctypes.data, cid.ctypes.data, rc.ctypes.data,
+                                       int(nthreads), ctypes.byref(sec))
+        return rc, int(ok), sec.value
 
     def commit_update(self, key, key_size, commit_id, sstamp):
         return lib().orc_commit_update(self.t, key_bytes(key, key_size), key_size, commit_id, sstamp)

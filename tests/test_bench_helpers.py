@@ -51,3 +51,35 @@ def test_sharded_hbm_bytes_counts_what_moves():
     b, parts = bench.sharded_hbm_bytes(st, 1024)
     assert parts["remote_results"] == 480 * 2 * 1012 and parts["returned_results"] == 500 * 2 * 1012
     assert parts["key_records"] == (500 + 480) * 32 and b == sum(parts.values())
+
+
+def test_cpu_legs_c3_times_concurrent_writers():
+    """The C3 CPU leg replays the GPU's epochs on the oracle and times the last epoch's updates
+    on T concurrent writers (orc_update_batch_mt) beside its reads: the fields the line carries,
+    no one-thread update timing left."""
+    import types
+
+    import numpy as np
+    rows = 30_000
+    orc = bench.CpuOracle(rows, 4)
+    args = types.SimpleNamespace(seed=3, cpu_seconds=0.05, scan_size=100, rows=rows)
+    rng = np.random.default_rng(0)
+    record = []
+    counter = 1
+    for ep in range(3):
+        m = 3000
+        keys = rng.integers(0, rows, m).astype(np.uint64)
+        rid = (counter + 2 * np.arange(m)).astype(np.uint32)
+        counter += 2 * m
+        record.append({"keys": keys, "colb": rng.integers(0, 4, m).astype(np.uint8), "rid": rid,
+                       "cid": (rid + 1).astype(np.uint32)})
+    reads = rng.integers(0, rows, 20_000).astype(np.uint64)
+    rids = np.full(reads.size, counter, np.uint32)
+    res = {"cpu_model": "test", "nproc": 8}
+    out = bench.cpu_legs(orc, args, res, 4, c3={"record": record, "reads": reads, "rids": rids})
+    c3 = out["c3"]
+    assert "last_epoch_update_s_1_thread" not in c3
+    assert c3["update_writers"] == 4 and c3["last_epoch_update_ops"] == 3000
+    assert 0 < c3["last_epoch_updates_ok"] <= 3000 and c3["updates_per_s"] > 0
+    assert c3["updates_replayed"] >= c3["last_epoch_updates_ok"]
+    assert c3["value"] > 0 and c3["reads_per_s"] > 0

@@ -99,3 +99,35 @@ def test_update_batch_equals_op_by_op():
     oa, ra = a.read_batch(probe, 8, rids)
     ob, rb = b.read_batch(probe, 8, rids)
     assert (oa == ob).all() and (ra == rb).all()
+
+
+@pytest.mark.parametrize("threads", [2, 7, 16])
+def test_update_batch_mt_equals_single_writer(threads):
+    """bench.py's C3 CPU leg runs the last epoch's updates on T writers (orc_update_batch_mt):
+    every rc, every later read (latest / copy / old versions at any read id) and the number of
+    retired versions equal the single writer's replay of the same epoch."""
+    n = 60_000
+    a, b = O.OracleTree(), O.OracleTree()
+    a.load_ycsb(0, n, 8, 1)
+    b.load_ycsb(0, n, 8, 1)
+    rng = np.random.default_rng(threads)
+    for ep in range(3):
+        m = 6000
+        # hot keys repeated many times in one epoch (RunMixed's Zipf stream), absent keys too
+        keys = np.concatenate([rng.integers(0, n + 100, m - 1500), rng.integers(0, 40, 1500)]).astype(np.uint64)
+        rng.shuffle(keys)
+        deltas = np.repeat(rng.integers(0, 4, (m, 1), dtype=np.uint8), 100, 1)
+        wid = (10 + 2 * m * ep + 2 * np.arange(m)).astype(np.uint32)
+        cid = (wid + 1).astype(np.uint32)
+        cid[(rng.random(m) < 0.05) & (keys > 40)] = 0  # left in flight
+        rc1, ok1 = a.update_batch(keys, 8, 0, deltas, wid, cid)
+        rc2, ok2, sec = b.update_batch_mt(keys, 8, 0, deltas, wid, cid, threads)
+        assert (rc1 == rc2).all() and ok1 == ok2 and sec > 0
+        assert len(set(rc1.tolist())) >= 3
+    assert a.stats()["versions"] == b.stats()["versions"] > 0
+    probe = np.concatenate([rng.integers(0, n, 4000), rng.integers(0, 40, 2000)]).astype(np.uint64)
+    rids = rng.integers(0, 2 * 6000 * 3 + 20, probe.size).astype(np.uint32)
+    oa, ra = a.read_batch(probe, 8, rids)
+    ob, rb = b.read_batch(probe, 8, rids)
+    assert (oa["status"] == ob["status"]).all() and (ra == rb).all()
+    assert len(set(oa["status"].tolist())) >= 3
