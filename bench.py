@@ -114,6 +114,8 @@ def parse(argv=None):
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extras", action="store_true", help="c2: skip the nested C4 / C3 legs")
     p.add_argument("--host-traversal", action="store_true", help="leaf ids from the host router instead")
+    p.add_argument("--no-e2e", action="store_true", help="c2: skip the end-to-end (host-buffer) leg")
+    p.add_argument("--e2e-passes", type=int, default=2, help="c2: passes over the batch of the end-to-end leg")
     p.add_argument("--write-overlap", type=int, choices=[0, 1, 2], default=1,
                    help="device write path: 1 = an epoch's kernels up to its publish run beside the previous "
                         "epoch's read probe (stage_set_write_overlap; the epoch inputs are resident beforehand); "
@@ -1301,6 +1303,57 @@ def run_chq2(args):
     return 0 if ok else 1
 
 
+PCIE_PEAK_GBS = 63.0  # PCIe Gen5 x16 per direction (MI355X_MICROARCH.md, host link)
+
+
+def end_to_end_leg(tab, args, draws, d_out, d_rec):
+    """C2 delivered to host memory (SURVEY §8(d) timing rule: H2D / D2H included): the same 2^24
+    Zipf keys through stage_probe_host from a pinned key array, each call's status records and
+    rows landing in a pinned result ring the caller consumes (2^22 lookups per call), for
+    --e2e-passes passes over the batch.  Two output layouts: the default (32-B stage_probe_out,
+    1024-B rows) and the lean one a host caller asks for with stage_set_output_layout(1008, 16)
+    (16-B stage_probe_out16, packed 1008-B [key][payload] rows: what IndexScanExecutor copies
+    out, executor.h:396-397).  The last call's first 4096 results are compared with the
+    device-resident probe of the same keys (d_out / d_rec, themselves oracle-checked)."""
+    B = draws.size
+    chunk = min(B, 1 << 22)
+    keys = stage.pinned_empty(B, np.uint64)
+    keys[:] = draws
+    layouts = (("default", 0, 32), ("lean", 1008, 16))
+    res = {}
+    last = (B // chunk - 1) * chunk
+    k = min(4096, chunk)
+    ref_st = d_out.to_numpy(stage.PROBE_OUT_DTYPE, k, offset=last * 32)["status"]
+    ref_rows = d_rec.to_numpy(np.uint8, k * tab.stride, offset=last * tab.stride).reshape(k, tab.stride)[:, :1008]
+    for name, stride, sb in layouts:
+        tab.set_output_layout(stride, sb)
+        dt = stage.PROBE_OUT16_DTYPE if sb == 16 else stage.PROBE_OUT_DTYPE
+        out = stage.pinned_empty(chunk, dt)
+        rows = stage.pinned_empty((chunk, tab.stride), np.uint8)
+        tab.probe_host(keys[:chunk], out=out, rows=rows)  # warm: the pipe's device buffers
+        t0 = time.perf_counter()
+        for _ in range(args.e2e_passes):
+            for b in range(0, B - chunk + 1, chunk):
+                tab.probe_host(keys[b:b + chunk], out=out, rows=rows)
+        sec = time.perf_counter() - t0
+        n = args.e2e_passes * (B // chunk) * chunk
+        d2h = sb + tab.stride
+        eq = bool((out["status"][:k] == ref_st).all() and (rows[:k, :1008] == ref_rows).all())
+        res[name] = {"value": round(n / sec, 1), "unit": "ops/s", "lookups": n, "seconds": round(sec, 4),
+                     "bytes_per_lookup": {"h2d": 8, "d2h": d2h}, "status_bytes": sb, "row_stride": tab.stride,
+                     "pcie_d2h_gbs": round(n * d2h / sec / 1e9, 2), "pcie_h2d_gbs": round(n * 8 / sec / 1e9, 3),
+                     "pcie_d2h_frac": round(n * d2h / sec / 1e9 / PCIE_PEAK_GBS, 3), "check_equal": eq}
+        del out, rows
+    tab.set_output_layout(args.out_stride or 0, 32)
+    del keys
+    lean = res["lean"]
+    return {**lean, "layout": "stage_set_output_layout(1008, 16): 16-B status records + packed 1008-B rows",
+            "pcie_peak_gbs": PCIE_PEAK_GBS, "default_layout": res["default"],
+            "timed": f"{args.e2e_passes} passes over the C2 batch, {chunk} lookups per stage_probe_host call, keys "
+                     "in pinned host memory before the timed region, results into a pinned ring the caller "
+                     "reuses; H2D of keys, probe and D2H of status records + rows all inside"}
+
+
 def c4_leg(tab, args, total_rows, rank, stream, steps, warmup):
     """configs[3]: B uniform start keys, L-key range scans (stage_scan_batch); returns the leg's
     measured dict and a sample for the oracle check."""
@@ -1604,6 +1657,10 @@ def main(argv=None):
                 "ms_per_step": round(elapsed / args.steps * 1e3, 4), "self_check": ok, "roofline": roof,
                 "config": {"workload": WORKLOADS["c2"], "theta": args.theta,
                            "traversal": "host" if d_leaf else "device"}}
+        if not args.no_e2e:
+            head["end_to_end"] = end_to_end_leg(tab, args, draws, d_out, d_rec)
+            log(f"[rank {rank}] C2 end to end (host buffers): {head['end_to_end']['value'] / 1e6:.1f} M lookups/s, "
+                f"{head['end_to_end']['pcie_d2h_gbs']} GB/s D2H")
         for b in (d_keys, d_out, d_rec) + ((d_leaf,) if d_leaf else ()):
             b.free()
         if not args.no_extras:
@@ -1624,6 +1681,8 @@ def main(argv=None):
                         c3=samples.get("c3"))
         legs["c2"]["calibration"] = cpu_calibration(orc.O, nthreads)
         cpu = legs[args.config]
+        if "end_to_end" in head:
+            head["end_to_end"]["vs_cpu_baseline"] = round(head["end_to_end"]["value"] / cpu["value"], 2)
         for k, v in extras.items():
             v["cpu_baseline"] = legs.get(k)
     config = {**head["config"], "rows_per_gpu": args.rows, "rows_total": total_rows,
@@ -1636,6 +1695,7 @@ def main(argv=None):
         "config": config, "roofline": head["roofline"], "cpu_baseline": cpu, "self_check": head["self_check"],
         **({k: head[k] for k in ("value_is", "reads_per_s", "read_probe_ms_per_step", "ops_per_s_incl_writes")
             if k in head}),
+        **({"end_to_end": head["end_to_end"]} if "end_to_end" in head else {}),
         **({"extras": extras} if extras else {}),
         "setup_s": {"load": round(t_load, 1), "sync": round(t_sync, 1)},
         "host_peak_rss_gib": round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20, 1),

@@ -356,8 +356,9 @@ int stage_copy_update_ps(stage_table *t, uint32_t copy_id, uint32_t pstamp);
  *   stage_record_stride's default (the row rounded to 128 B above 128 B), else any multiple of
  *   16 of at least key pad + payload (e.g. 1008 for YCSB rows: no pad bytes written);
  *   status_bytes 32 = stage_probe_out, 16 = stage_probe_out16 records in d_out (fixed-width
- *   keys of <= 8 bytes in 64-slot leaves).  The row stride also applies to stage_probe_host;
- *   every other entry point keeps 32-B records. */
+ *   keys of <= 8 bytes in 64-slot leaves).  Both apply to stage_probe_host too (its `out`
+ *   then holds n packed stage_probe_out16 records); every other entry point keeps 32-B
+ *   records. */
 int stage_set_output_layout(stage_table *t, uint32_t row_stride, uint32_t status_bytes);
 int stage_probe_batch(stage_table *t, const uint64_t *d_keys, const uint16_t *d_lens,
                       const uint32_t *d_read_ids, const uint32_t *d_leaf_ids, uint64_t n,

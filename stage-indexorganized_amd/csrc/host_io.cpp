@@ -98,10 +98,12 @@ hipError_t pipe_chunk(stage_table *t, stage::PipeLane &l, uint64_t stride, uint3
     if (e) return e;
     stage::DevTable view = t->dev.view;
     view.stride = (uint32_t)stride;
+    stage::ProbeTuning tune = t->tune;
+    tune.status_bytes = t->status_bytes;  // 16: stage_probe_out16 records, packed
     e = stage::launch_probe(view, (const uint64_t *)dk, lens ? (const uint16_t *)dl : nullptr,
                             rids ? (const uint32_t *)dr : nullptr, nullptr, n, (stage::stage_probe_out_dev *)dout,
-                            rows ? drow : nullptr, l.s, t->tune);
-    if (!e) e = hipMemcpyAsync(out, dout, 32 * n, hipMemcpyDeviceToHost, l.s);
+                            rows ? drow : nullptr, l.s, tune);
+    if (!e) e = hipMemcpyAsync(out, dout, (uint64_t)tune.status_bytes * n, hipMemcpyDeviceToHost, l.s);
     if (!e && rows) e = hipMemcpyAsync(rows, drow, stride * n, hipMemcpyDeviceToHost, l.s);
     return e;
 }

@@ -562,13 +562,20 @@ class Table:
         check(lib().stage_set_output_layout(self.h, row_stride, status_bytes), "set_output_layout")
         self.status_bytes = status_bytes
 
-    def probe_host(self, keys, read_ids=None, lens=None, records=True):
-        """stage_probe_host: the same probe with host-memory inputs and outputs (pipelined)."""
+    def probe_host(self, keys, read_ids=None, lens=None, records=True, out=None, rows=None):
+        """stage_probe_host: the same probe with host-memory inputs and outputs (pipelined).
+        `out` / `rows`: caller-owned result arrays (e.g. pinned_empty) to fill instead of new ones;
+        status records are 16 B after set_output_layout(.., 16)."""
         keys, n = self.key_buffer(keys)
         rids = None if read_ids is None else np.ascontiguousarray(read_ids, np.uint32)
         ln = None if lens is None else np.ascontiguousarray(lens, np.uint16)
-        out = np.zeros(n, PROBE_OUT_DTYPE)
-        rows = np.zeros((n, self.stride), np.uint8) if records else None
+        dt = PROBE_OUT16_DTYPE if getattr(self, "status_bytes", 32) == 16 else PROBE_OUT_DTYPE
+        if out is None:
+            out = np.zeros(n, dt)
+        assert out.dtype == dt and out.size >= n, "out: n status records of the table's layout"
+        if rows is None and records:
+            rows = np.zeros((n, self.stride), np.uint8)
+        assert rows is None or (rows.shape[0] >= n and rows.shape[1] == self.stride and rows.flags.c_contiguous)
         check(lib().stage_probe_host(self.h, keys.ctypes.data, _ptr(ln), _ptr(rids), n, out.ctypes.data, _ptr(rows)),
               "probe_host")
         return out, rows

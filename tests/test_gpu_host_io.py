@@ -52,6 +52,35 @@ def test_probe_host_matches_device_and_oracle(chains):
     assert none is None and (out2 == out_h[:1000]).all()
 
 
+def test_probe_host_lean_layout_into_pinned_buffers(chains):
+    """bench.py's end-to-end leg: stage_set_output_layout(1008, 16) applies to stage_probe_host
+    (packed 16-B stage_probe_out16 records, 1008-B rows) and the results land in caller-owned
+    pinned arrays; equal to the device-buffer probe of the same keys in the same layout and, in
+    the fields both layouts carry, to the default layout."""
+    tab, orc, hot, n = chains
+    rng = np.random.default_rng(44)
+    keys = np.concatenate([rng.integers(0, n + 1000, 300000), hot]).astype(np.uint64)
+    rids = rng.integers(0, 45, keys.size).astype(np.uint32)
+    out32, rows32 = tab.probe_host(keys, read_ids=rids)
+    try:
+        tab.set_output_layout(1008, 16)
+        assert tab.stride == 1008
+        pk = stage.pinned_empty(keys.size, np.uint64)
+        pk[:] = keys
+        out = stage.pinned_empty(keys.size, stage.PROBE_OUT16_DTYPE)
+        rows = stage.pinned_empty((keys.size, 1008), np.uint8)
+        o2, r2 = tab.probe_host(pk, read_ids=rids, out=out, rows=rows)
+        assert o2 is out and r2 is rows
+        od, rd = tab.probe(keys, read_ids=rids)
+        assert od.dtype == stage.PROBE_OUT16_DTYPE
+        assert (out == od).all() and (rows == rd).all()
+        for f in ("status", "flags", "hops", "cstamp", "rec_cstamp", "copy_sstamp"):
+            assert (out[f] == out32[f]).all(), f
+        assert (rows == rows32[:, :1008]).all()
+    finally:
+        tab.set_output_layout(0, 32)
+
+
 @pytest.mark.parametrize("resident", [False, True])
 def test_reader_concurrent_threads_match_oracle(chains, resident):
     tab, orc, hot, n = chains
