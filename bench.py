@@ -116,11 +116,9 @@ def parse(argv=None):
     p.add_argument("--host-traversal", action="store_true", help="leaf ids from the host router instead")
     p.add_argument("--no-e2e", action="store_true", help="c2: skip the end-to-end (host-buffer) leg")
     p.add_argument("--e2e-passes", type=int, default=2, help="c2: passes over the batch of the end-to-end leg")
-    p.add_argument("--write-overlap", type=int, choices=[0, 1, 2], default=1,
+    p.add_argument("--write-overlap", type=int, choices=[0, 1], default=1,
                    help="device write path: 1 = an epoch's kernels up to its publish run beside the previous "
-                        "epoch's read probe (stage_set_write_overlap; the epoch inputs are resident beforehand); "
-                        "2 = the next epoch is prepared before this epoch's probe is enqueued and published "
-                        "after it (stage_publish_epoch), so its kernels reach the device first")
+                        "epoch's read probe (stage_set_write_overlap; the epoch inputs are resident beforehand)")
     p.add_argument("--out-stride", type=int, default=0,
                    help="caller row stride in bytes (stage_set_output_layout; 0 = the 1008-B canonical row)")
     p.add_argument("--reply", choices=["auto", "rows", "peer"], default="auto",
@@ -1438,33 +1436,17 @@ def c3_leg(tab, args, stream, nthreads, steps, warmup):
     elapsed, write_s, updates, ops_done = 0.0, 0.0, 0, 0
     t_loop = time.perf_counter()
     timed = epochs[warm:]
-    deferred = device_wp and args.write_overlap == 2
-    if deferred:  # the first timed epoch prepared and published before its reads
-        tw = time.perf_counter()
-        ycsb_b.apply(timed[0], stream)
-        tab.publish_epoch(stream.ptr)
-        write_s += time.perf_counter() - tw
     for i, ep in enumerate(timed):
         tw = time.perf_counter()
         # device write path: the epoch's kernels are enqueued on the probe's stream (the reads
         # follow the epoch's writes in stream order; no host wait in between); host write path:
-        # applied and published before the probe.  Deferred publish (write overlap 2): epoch
-        # i + 1 is prepared before epoch i's probe is enqueued -- its kernels reach the device
-        # first and run beside the probe -- and published after it (same results)
-        if deferred:
-            if i + 1 < len(timed):
-                ycsb_b.apply(timed[i + 1], stream)
-        else:
-            updates += ycsb_b.apply(ep, stream if device_wp else None)
+        # applied and published before the probe
+        updates += ycsb_b.apply(ep, stream if device_wp else None)
         write_s += time.perf_counter() - tw
         tr = time.perf_counter()
         evs[2 * i].record(stream)
         probe(ep)
         evs[2 * i + 1].record(stream)
-        if deferred and i + 1 < len(timed):
-            tw = time.perf_counter()
-            tab.publish_epoch(stream.ptr)
-            write_s += time.perf_counter() - tw
         if not device_wp:
             stream.sync()
             elapsed += time.perf_counter() - tr

@@ -161,18 +161,10 @@ int stage_settle(stage_table *t);
  * published, beside whatever the caller enqueued on `stream` after that (e.g. the previous
  * epoch's read probes); only the publish waits for `stream`.  Results are the same.  Contract:
  * the epoch's inputs (keys, deltas, ids) are complete when the call is made -- not produced by
- * work still pending on `stream`.
- * Mode 2 (deferred publish): stage_update_batch_device enqueues the epoch's kernels up to the
- * publish and returns; the publish follows at stage_publish_epoch(t, stream) -- or at the next
- * stage_update_batch_device, or at the first call that reads or writes the host table.  Probes
- * enqueued in between see the table as it was before the epoch: a driver may prepare epoch e + 1
- * before enqueuing epoch e's reads, so that e + 1's kernels reach the device first and run beside
- * those reads, then publish it (n_ok != NULL publishes at once). */
+ * work still pending on `stream` -- and stay unmodified until the work enqueued on `stream`
+ * behind the call has run (stream order, as for every device entry point).  A deferred-publish
+ * mode 2 was measured and retired. */
 int stage_set_write_overlap(stage_table *t, int on);
-/* publishes the epoch that write-overlap mode 2 left prepared (a no-op when none is): its slot
- * words on `stream` (NULL: the stream the epoch was prepared on) behind the work enqueued there,
- * then the export and the host table's adoption (background) */
-int stage_publish_epoch(stage_table *t, void *stream);
 
 /* byte-key forms, for every key width a table takes: 1..8 bytes (key_width 1..8 or 0 =
  * variable) or a fixed width of 9..32 bytes (TPC-C composite keys, tpcc_record.h: int64
@@ -449,7 +441,7 @@ int stage_set_probe_tuning(stage_table *t, int group, int max_blocks);
 /* cache policy of stage_probe_batch's output stores (rows + status records), 8-probe launch
  * shape: STAGE_STORE_TEMPORAL, STAGE_STORE_NONTEMPORAL (default) or STAGE_STORE_WRITE_THROUGH
  * (the output lines leave the GPU's L2 at once, which keeps hot rows and index lines cached).
- * A tuning knob, not a semantic one; env STAGE_PROBE_STORE sets the initial value. */
+ * A tuning knob, not a semantic one. */
 #define STAGE_STORE_TEMPORAL 0
 #define STAGE_STORE_NONTEMPORAL 1
 #define STAGE_STORE_WRITE_THROUGH 2
@@ -514,7 +506,11 @@ int stage_ch_query2_batch(stage_table *region, stage_table *nation, stage_table 
 /* the same batch without waiting for it: enqueued on `stream` into slot 0 or 1 (two batches
  * may be in flight, the host enqueueing one while the device runs the other); `out` must be
  * page-locked (stage_host_alloc) and stay untouched until stage_ch_query2_wait(slot) returns
- * *n_out and aborted[nq].  STAGE_E_STATE: the slot still holds a batch not waited for. */
+ * *n_out and aborted[nq].  STAGE_E_STATE: the slot still holds a batch not waited for.
+ * The two slots (and a synchronous batch) share the tables' device scratch: a batch enqueued on
+ * another stream than a batch still in flight first waits for it on the device
+ * (hipStreamWaitEvent), so batches on different streams are correct but do not overlap; on one
+ * stream they overlap the host's staging of the next batch with the device's run of the last. */
 int stage_ch_query2_batch_async(stage_table *region, stage_table *nation, stage_table *supplier,
                                 stage_table *item, stage_table *stock, const uint32_t *map_off,
                                 const uint64_t *d_map_keys, int32_t target_region, const uint32_t *read_ids,

@@ -53,14 +53,6 @@ int stage_table_create(const stage_params *params, stage_table **out) {
         auto t = std::make_unique<stage_table>();
         t->host = std::make_unique<stage::HostTable>(*params);
         t->dev.device = params->device;
-        if (const char *g = std::getenv("STAGE_PROBE_GROUP")) t->tune.group = std::atoi(g);
-        if (const char *g = std::getenv("STAGE_PROBE_MAX_BLOCKS")) t->tune.max_blocks = std::atoi(g);
-        if (const char *g = std::getenv("STAGE_PROBE_STORE")) t->tune.store = std::atoi(g);
-        if (const char *g = std::getenv("STAGE_PROBE_WIDE")) t->tune.wide = std::atoi(g);
-        if (const char *g = std::getenv("STAGE_PROBE_SMALL_BELOW")) t->tune.small_below = std::atoi(g);
-        if (const char *g = std::getenv("STAGE_SCAN_ROWS")) t->scan_tune.rows = std::atoi(g);
-        if (const char *g = std::getenv("STAGE_SL_SCANS")) t->scan_tune.first_scans = std::atoi(g);
-        if (const char *g = std::getenv("STAGE_SCAN_MAX_BLOCKS")) t->scan_tune.max_blocks = std::atoi(g);
         if (const char *g = std::getenv("STAGE_OUT_STRIDE")) {
             uint32_t v = (uint32_t)std::atoi(g);
             if (v >= ((t->host->key_pad() + t->host->params().payload_size + 15) & ~15u) && v % 16 == 0)
@@ -725,20 +717,9 @@ int stage_set_shard_dedupe(stage_table *t, int on) {
 }
 
 int stage_set_write_overlap(stage_table *t, int on) {
-    if (!t || on < 0 || on > 2) return fail(STAGE_E_ARG, "write overlap must be 0, 1 or 2");
-    return guarded([&] {
-        t->flush_publish(t->pending_stream);
-        t->wp_overlap = on;
-        return STAGE_OK;
-    });
-}
-
-int stage_publish_epoch(stage_table *t, void *stream) {
-    if (!t) return fail(STAGE_E_ARG, "null table");
-    return guarded([&] {
-        t->flush_publish(stream ? (hipStream_t)stream : t->pending_stream);
-        return STAGE_OK;
-    });
+    if (!t || on < 0 || on > 1) return fail(STAGE_E_ARG, "write overlap must be 0 or 1");
+    t->wp_overlap = on;
+    return STAGE_OK;
 }
 
 int stage_set_shard_key_bits(stage_table *t, int bits) {

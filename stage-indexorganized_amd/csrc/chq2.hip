@@ -518,11 +518,7 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         // `out` in page-locked memory (stage_host_alloc, stage.pinned_empty): the finishing kernel
         // writes the records into it directly; otherwise they are copied once the count is known
         stage_q2_rec *host_out = nullptr;
-        static const bool copy_out = [] {
-            const char *e = std::getenv("STAGE_Q2_OUT");  // "copy": records copied after the batch (A/B)
-            return e && std::strcmp(e, "copy") == 0;
-        }();
-        if (out && max_out && !copy_out) {  // page-locked memory has a device view; pageable memory has none
+        if (out && max_out) {  // page-locked memory has a device view; pageable memory has none
             void *dp = nullptr;
             if (hipHostGetDevicePointer(&dp, out, 0) == hipSuccess && dp) host_out = (stage_q2_rec *)dp;
             (void)hipGetLastError();  // a pageable pointer is not an error here
@@ -540,6 +536,11 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         // the ~35 µs the scans took, against ~10 µs for the two scans back to back on s.)
         for (stage_table *d : {region, nation})
             if (d->dev.stream && d->dev.stream != s) hip_check(hipStreamSynchronize(d->dev.stream), "dimension stream");
+        // both slots share the SUPPLIER scratch and the REGION / NATION scan rows: a batch still in
+        // flight on another stream is waited for on the device before this one is enqueued (on its
+        // own stream, stream order already keeps them apart)
+        for (const Q2Pending &o : stock->q2p)
+            if (o.active && o.stream != s) hip_check(hipStreamWaitEvent(s, o.ev, 0), "q2 other slot");
         // everything up to the batch's one synchronisation, enqueued on s
         auto enqueue = [&] {
             hip_check(hipMemcpyAsync(mir, pq, q_end, hipMemcpyHostToDevice, s), "h2d");
@@ -657,6 +658,7 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
             P.q_cn = q_cn;
             P.q_ab = q_ab;
             P.nq = nq;
+            P.stream = s;
             P.n_max = n_max;
             P.m_max = m_max;
             P.active = true;

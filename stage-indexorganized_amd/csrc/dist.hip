@@ -69,16 +69,6 @@ constexpr int kDefaultChunks = 4;  // sharded batches are exchanged in this many
 // caller positions served by one coalesced request at most: a hot key's run is cut into
 // requests of <= 64 callers, so no single probe or fan-out copy stores more than 64 rows
 constexpr uint32_t kFanCap = 64;
-// callers per coalesced request: kFanCap, or STAGE_SHARD_FANCAP (1..64) -- a smaller cap splits a
-// hot key's callers over more requests (more row reads, shorter per-request fan-outs)
-static uint32_t fan_cap() {
-    static const uint32_t v = [] {
-        const char *e = std::getenv("STAGE_SHARD_FANCAP");
-        const int x = e ? std::atoi(e) : 0;
-        return x >= 1 && x <= (int)kFanCap ? (uint32_t)x : kFanCap;
-    }();
-    return v;
-}
 
 // chunk i of C over the routed items [0, total): [total*i/C, total*(i+1)/C); total is the batch
 // size, or the coalesced request count read on the device (total_dev)
@@ -366,34 +356,12 @@ void grow(void *&p, uint64_t bytes) {
 
 unsigned blocks_for(uint64_t n, unsigned per_block) { return (unsigned)std::max<uint64_t>(1, (n + per_block - 1) / per_block); }
 
-// The 32-bit coalescing sort (u32 keys, u32 positions): hipcub's onesweep (8 bits a pass), or
-// rocprim's onesweep at RB bits a pass -- 3 passes instead of 4 over 25-30 key bits
-// (STAGE_DD_RADIX_BITS = 10 / 11).  temp == nullptr: storage size query.
-template <unsigned RB>
-using Onesweep32 = rocprim::radix_sort_config<
-    rocprim::default_config, rocprim::default_config,
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<512, 8>, rocprim::kernel_config<512, 8>, RB,
-                                        rocprim::block_radix_rank_algorithm::match>>;
-
-int dd_radix_bits() {
-    static const int rb = [] {
-        const char *e = std::getenv("STAGE_DD_RADIX_BITS");
-        const int v = e ? std::atoi(e) : 8;
-        return v == 10 || v == 11 ? v : 8;
-    }();
-    return rb;
-}
-
+// The 32-bit coalescing sort (u32 keys, u32 positions): hipcub's onesweep, 8 bits a pass
+// (rocprim's onesweep at 10 / 11 bits a pass -- 3 passes instead of 4 over 25-30 key bits -- was
+// measured no faster, DESIGN §6, and retired).  temp == nullptr: storage size query.
 hipError_t sort32(void *temp, size_t &bytes, const uint32_t *kin, uint32_t *kout, const uint32_t *vin,
                   uint32_t *vout, int n, int bits, hipStream_t s) {
-    switch (dd_radix_bits()) {
-        case 10:
-            return rocprim::radix_sort_pairs<Onesweep32<10>>(temp, bytes, kin, kout, vin, vout, n, 0u, (unsigned)bits, s);
-        case 11:
-            return rocprim::radix_sort_pairs<Onesweep32<11>>(temp, bytes, kin, kout, vin, vout, n, 0u, (unsigned)bits, s);
-        default:
-            return hipcub::DeviceRadixSort::SortPairs(temp, bytes, kin, kout, vin, vout, n, 0, bits, s);
-    }
+    return hipcub::DeviceRadixSort::SortPairs(temp, bytes, kin, kout, vin, vout, n, 0, bits, s);
 }
 
 }  // namespace
@@ -646,7 +614,7 @@ static void plan_route(ShardComm &c, Plan &P, const uint64_t *d_keys, const uint
             chk(hipcub::DeviceRadixSort::SortPairs(c.dd_cub, bytes, d_keys, skeys, iota, sidx, (int)n, 0, bits, s),
                 "dedupe sort");
         }
-        dd_heads<<<nb, 256, 0, s>>>(sk, sidx, d_rids, n, fan_cap(), flag);
+        dd_heads<<<nb, 256, 0, s>>>(sk, sidx, d_rids, n, kFanCap, flag);
         bytes = c.dd_cub_bytes;
         chk(hipcub::DeviceScan::InclusiveSum(c.dd_cub, bytes, flag, useq, (int)n, s), "dedupe scan");
         dd_pack<<<nb, 256, 0, s>>>(sk, sidx, d_rids, flag, useq, n, 0u, owner ? (uint32_t *)c.uidx : nullptr,
@@ -770,10 +738,7 @@ static void chunk_probe(ShardComm &c, const Plan &P, int i, const DevTable &t, c
     probe(r1, e);
     if (r1 == r0) return;
     if (d_recs && probe_fanout_supported(t)) {
-        // STAGE_SHARD_OWN_STREAM=0: on the caller's stream after the remote probes (A/B)
-        static const bool own_stream = !(std::getenv("STAGE_SHARD_OWN_STREAM") &&
-                                         std::getenv("STAGE_SHARD_OWN_STREAM")[0] == '0');
-        hipStream_t os = own_stream ? c.ps : s;
+        hipStream_t os = c.ps;  // beside the remote probes (on s: slower)
         chk(hipEventRecord(c.ev_fork, s), "fork");  // the unpacked keys
         chk(hipStreamWaitEvent(os, c.ev_fork, 0), "fork");
         chk(launch_probe_fanout(t, lk + r0, lr + r0, r1 - r0, (const FanRange *)c.fan + q0,
@@ -842,9 +807,16 @@ struct PeerCounts {
     }
 };
 
-// the growth rule every rank applies to every rank's row buffers; true when one of them grows
-static bool peer_grow_plan(ShardComm &c, const PeerCounts &pc) {
-    if ((int)c.peer_cap.size() != pc.W) c.peer_cap.assign(pc.W, 0);
+// the growth rule every rank applies to every rank's row buffers; true when one of them grows.
+// The buffers hold rows of the call's stride (every rank's table has the same output stride, as
+// the rows reply's transfers assume): a stride change (stage_set_output_layout between calls)
+// re-plans every rank's buffers from zero, so they are reallocated and their handles exchanged
+// again on every rank together.
+static bool peer_grow_plan(ShardComm &c, const PeerCounts &pc, uint32_t stride) {
+    if ((int)c.peer_cap.size() != pc.W || c.peer_stride != stride) {
+        c.peer_cap.assign(pc.W, 0);
+        c.peer_stride = stride;
+    }
     bool grew = false;
     for (int q = 0; q < pc.W; ++q) {
         const uint64_t m = pc.received(q);
@@ -860,9 +832,10 @@ static bool peer_grow_plan(ShardComm &c, const PeerCounts &pc) {
 // done -- every rank's fan-out of the previous call ended before this call's count exchange)
 static void peer_alloc_own(ShardComm &c, uint32_t stride) {
     const uint64_t cap = c.peer_cap[c.rank];
-    if (cap == c.prow_cap && c.prow[0]) return;
+    if (cap == c.prow_cap && stride == c.prow_stride && c.prow[0]) return;
     for (int k = 0; k < 2; ++k) grow(c.prow[k], cap * stride);
     c.prow_cap = cap;
+    c.prow_stride = stride;
 }
 
 static void *hbuf(ShardComm &c, uint64_t bytes) {
@@ -935,6 +908,15 @@ __global__ void peer_acquire_kernel() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate has completed
 }
 
+// The owner side's counterpart: a system-scope release on every XCD after the chunk's probe has
+// stored its rows into this rank's IPC-exported row buffer, before the status records leave over
+// RCCL -- each XCD's L2 writes its dirty lines of the buffer back to HBM, where the peers' reads
+// over xGMI find them (kernel-boundary fences alone give device scope only).
+__global__ void peer_release_kernel() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+}
+
 // peer reply, chunk i: the status records that came back from every other rank, with each row read
 // where its owner left it (peer_row) and stored at the caller positions
 static void chunk_return_peer(ShardComm &c, const Plan &P, const PeerCounts &pc, int i, uint32_t stride,
@@ -1004,7 +986,7 @@ int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const 
         P.rc.resize((size_t)C * W);
         for (int i = 0; i < C; ++i)
             for (int r = 0; r < W; ++r) P.rc[(size_t)i * W + r] = pc.at(r, i, c.rank);
-        if (peer_grow_plan(c, pc)) {  // the same decision on every rank
+        if (peer_grow_plan(c, pc, stride)) {  // the same decision on every rank
             peer_alloc_own(c, stride);
             peer_exchange(c, s);
         }
@@ -1049,6 +1031,7 @@ int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const 
     for (int i = 0; i < C; ++i) {
         chk(hipStreamWaitEvent(s, ev_keys[i], 0), "wait keys");
         chunk_probe(c, P, i, t, tune, owner, d_out, d_recs, s, peer ? (uint8_t *)c.prow[c.parity] : nullptr);
+        if (peer) peer_release_kernel<<<256, 64, 0, s>>>();
         chk(hipEventRecord(ev_probe[i], s), "event");
         chk(hipStreamWaitEvent(c.cs, ev_probe[i], 0), "wait probe");
         nchk(ncclGroupStart(), "group");
@@ -1129,7 +1112,7 @@ int shard_probe_loopback(const std::vector<ShardComm *> &cs, const std::vector<c
         pc.S.resize((size_t)W * C * W);
         for (int q = 0; q < W; ++q) std::copy(P[q].sc.begin(), P[q].sc.end(), pc.S.begin() + (size_t)q * C * W);
         for (int r = 0; r < W; ++r)
-            if (peer_grow_plan(*cs[r], pc)) peer_alloc_own(*cs[r], stride);
+            if (peer_grow_plan(*cs[r], pc, stride)) peer_alloc_own(*cs[r], stride);
         for (int r = 0; r < W; ++r) {
             for (int k = 0; k < 2; ++k) {
                 cs[r]->peer_row[k].resize(W);

@@ -46,7 +46,9 @@ struct ShardComm {
     // through the owner's buffers opened by IPC handle (loopback: the other shard's pointers)
     void *prow[2] = {nullptr, nullptr};  // this rank's row buffers
     uint64_t prow_cap = 0;               // rows each of them holds
+    uint32_t prow_stride = 0;            // ... of this many bytes
     std::vector<uint64_t> peer_cap;      // every rank's prow_cap, as every rank computes it
+    uint32_t peer_stride = 0;            // the row stride peer_cap was planned for
     std::vector<void *> peer_row[2];     // [parity][rank]: where rank's row buffers are here
     std::vector<void *> opened;          // IPC mappings to close
     void *hbuf = nullptr;                // handle / count exchange scratch

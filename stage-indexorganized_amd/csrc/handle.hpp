@@ -38,6 +38,7 @@ struct Q2Graph {
 struct Q2Pending {
     bool active = false;
     hipEvent_t ev = nullptr;  // after the batch's last copy
+    hipStream_t stream = nullptr;  // the stream it was enqueued on
     uint8_t *pq = nullptr;    // its page-locked staging: counts at q_cn, aborted flags at q_ab
     uint64_t q_cn = 0, q_ab = 0, n_max = 0, m_max = 0;
     uint32_t nq = 0;
@@ -55,17 +56,7 @@ struct stage_table {
     int shard_chunks = 0;                          // 0 = STAGE_SHARD_CHUNKS or the default
     int shard_dedupe = -1;                         // -1 = STAGE_SHARD_DEDUPE or on
     int shard_key_bits = 64;                       // coalescing sort width (stage_set_shard_key_bits)
-    int wp_overlap = 0;                            // stage_set_write_overlap (0, 1, 2 = deferred publish)
-    // write-overlap mode 2: the publish of the last prepared epoch, run by stage_publish_epoch,
-    // by the next epoch, or by the first call that needs the host table (on the epoch's stream)
-    std::function<void(hipStream_t)> pending_pub;
-    hipStream_t pending_stream = nullptr;
-    void flush_publish(hipStream_t s) {
-        if (!pending_pub) return;
-        auto f = std::move(pending_pub);
-        pending_pub = nullptr;
-        f(s);
-    }
+    int wp_overlap = 0;                            // stage_set_write_overlap (0 or 1)
     uint64_t q2_hint[2] = {0, 0};                  // CH-Q2's last visited suppliers / STOCK keys (launch shapes)
     Q2Graph q2g[2];     // per CH-Q2 slot (stage_ch_query2_batch_async); slot 0 also serves the synchronous calls
     Q2Pending q2p[2];
@@ -89,7 +80,6 @@ struct stage_table {
     std::atomic<uint64_t> adopted_sz[3] = {{0}, {0}, {0}};  // host copies / versions / images after the last adoption
     uint64_t wp_epoch_n[2] = {0, 0};                          // ops of the writer's last two epochs (by parity)
     void settle() {
-        flush_publish(pending_stream);
         std::lock_guard<std::mutex> g(adopt_mu);
         if (adopt.joinable()) adopt.join();
         if (adopt_err) std::rethrow_exception(adopt_err);
@@ -117,10 +107,6 @@ struct stage_table {
         while (wp_adopted.load(std::memory_order_acquire) < epoch) std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
     ~stage_table() {
-        try {
-            flush_publish(pending_stream);
-        } catch (...) {
-        }
         std::lock_guard<std::mutex> g(adopt_mu);
         if (adopt.joinable()) adopt.join();
         for (int k = 0; k < 2; ++k) {

@@ -26,9 +26,6 @@ struct ProbeTuning {
     int max_blocks = 0;    // 0 = default grid cap (16384 blocks of 256 threads)
     int store = 1;         // output stores: 0 temporal, 1 nontemporal, 2 write-through (sc1)
     int status_bytes = 32; // status record: 32 (stage_probe_out) or 16 (stage_probe_out16)
-    int wide = 0;          // wide-key / large-leaf probes: 0 = probe_lane_kernel up to 256 slots per leaf, else
-                           // probe_split_kernel; 1 = probe_kernel<.., G = 1>; 3 = probe_split_kernel always
-    int small_below = 16384;  // wide-key probes: 16-probe wave chunks below this many 64-probe chunks
 };
 
 hipError_t launch_resolve(const DevTable &t, const uint64_t *keys, const uint16_t *lens, uint64_t n, int le_child,
@@ -50,9 +47,7 @@ hipError_t launch_probe_fanout(const DevTable &t, const uint64_t *keys, const ui
                                const FanRange *fan, const uint32_t *flist, stage_probe_out_dev *out, uint8_t *recs,
                                hipStream_t s, const ProbeTuning &tune);
 struct ScanTuning {
-    int rows = 4;        // tuple rows in flight per wave (2, 4 or 8)
     int max_blocks = 0;  // 0 = default grid cap (16384 blocks of 256 threads)
-    int first_scans = 0; // first-tuple scans: 0 = scan_first_fast_kernel, 1 = general single-scan kernel, 2 / 4 = lockstep
 };
 
 // row_status != nullptr: IndexScanExecutor range semantics (per-record visibility for

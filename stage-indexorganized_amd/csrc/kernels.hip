@@ -1170,257 +1170,6 @@ __global__ __launch_bounds__(256) void scan_kernel_compact(DevTable t, const uin
 // (FirstPrefixSink); img_out[i] / st_out[i] = that tuple's heap row and status.
 constexpr int kFirstChunk = 16;
 constexpr uint8_t kFirstUndecided = 0xFE;  // scan_first_split_kernel -> scan_first_rest_kernel
-template <int SPL, int KW>
-__global__ __launch_bounds__(256) void scan_first_kernel(DevTable t, const uint64_t *__restrict__ keys, uint64_t n,
-                                                         uint32_t scan_size, const uint32_t *__restrict__ rids,
-                                                         uint32_t words, uint32_t *__restrict__ img_out,
-                                                         uint8_t *__restrict__ st_out) {
-    __shared__ uint64_t s_keys[4][64 * KW];
-    __shared__ uint32_t s_len[4][64], s_slot[4][64];
-    const uint32_t lane = lane_id(), wv = uni32(threadIdx.x >> 6);
-    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wv;
-    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    const uint32_t len = t.key_width;
-    // chunks of kFirstChunk scans per wave: lane j descends the tree for scan j of the chunk
-    // (independent descents in flight together), then the wave runs the chunk's scans
-    for (uint64_t c0 = wave * kFirstChunk; c0 < n; c0 += nwaves * kFirstChunk) {
-        const uint64_t i = c0 + lane;
-        const bool valid = lane < (uint32_t)kFirstChunk && i < n;
-        uint64_t ok[KW];
-        load_okey<KW>(keys, i, valid, len, ok);
-        const uint32_t leafv = valid ? resolve_leaf<false, KW>(t, ok, len, true) : 0u;
-        const uint32_t ridv = valid && rids ? rids[i] : 0xFFFFFFFEu;
-        const int cnt = (int)((n - c0) < (uint64_t)kFirstChunk ? (n - c0) : (uint64_t)kFirstChunk);
-        uint32_t my_img = 0xFFFFFFFFu, my_st = ST_NOT_FOUND;
-        for (int j = 0; j < cnt; ++j) {
-            FirstPrefixSink<KW> sink;
-            uint64_t x[KW];
-#pragma unroll
-            for (int w = 0; w < KW; ++w) x[w] = sink.pre[w] = rl64(ok[w], j);
-            sink.words = words;
-            sink.rid = rl32(ridv, j);
-            sink.img = 0xFFFFFFFFu;
-            sink.st = ST_NOT_FOUND;
-            scan_one_compact<false, SPL, KW>(t, x, len, rl32(leafv, j), scan_size, lane, sink, s_keys[wv], s_len[wv],
-                                             s_slot[wv]);
-            if (lane == (uint32_t)j) {
-                my_img = sink.img;
-                my_st = sink.st;
-            }
-        }
-        if (valid) {
-            img_out[i] = my_img;
-            st_out[i] = (uint8_t)my_st;
-        }
-    }
-}
-
-// scan_first_kernel with NS scans of a chunk run in lockstep by one wave: every dependent load
-// step (group max keys, a slot group's visibility mask + key columns, the kept records' slot
-// words, the next leaf's separator) is issued for the NS scans together, so a wave keeps NS
-// times the loads in flight (the single-scan form is latency-bound: 61 % of wave cycles parked
-// on s_waitcnt, profiles/r02).  The visibility mask and key columns of a group are loaded
-// together (one round trip per group instead of two).  Semantics per scan are those of
-// scan_one_compact + FirstPrefixSink (fixed-width keys): RangeScanBySize's first to_scan+1
-// qualifying records in slot order, sorted; the first visible tuple with the start key's
-// prefix among the first `remaining` of them; the Iterator continuation (le_child = false from
-// the last popped key, a re-popped start key ends the scan).
-template <int SPL, int KW, int NS>
-__global__ __launch_bounds__(256) void scan_first_multi_kernel(DevTable t, const uint64_t *__restrict__ keys,
-                                                               uint64_t n, uint32_t scan_size,
-                                                               const uint32_t *__restrict__ rids, uint32_t words,
-                                                               uint32_t *__restrict__ img_out,
-                                                               uint8_t *__restrict__ st_out) {
-    __shared__ uint64_t s_keys[4][NS][64 * KW];
-    __shared__ uint32_t s_slot[4][NS][64];
-    const uint32_t lane = lane_id(), wv = uni32(threadIdx.x >> 6);
-    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wv;
-    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    const uint32_t len = t.key_width;
-    for (uint64_t c0 = wave * kFirstChunk; c0 < n; c0 += nwaves * kFirstChunk) {
-        const uint64_t i = c0 + lane;
-        const bool valid = lane < (uint32_t)kFirstChunk && i < n;
-        uint64_t ok[KW];
-        load_okey<KW>(keys, i, valid, len, ok);
-        const uint32_t leafv = valid ? resolve_leaf<false, KW>(t, ok, len, true) : 0u;
-        const uint32_t ridv = valid && rids ? rids[i] : 0xFFFFFFFEu;
-        const int cnt = (int)((n - c0) < (uint64_t)kFirstChunk ? (n - c0) : (uint64_t)kFirstChunk);
-        uint32_t my_img = 0xFFFFFFFFu, my_st = ST_NOT_FOUND;
-        for (int j0 = 0; j0 < cnt; j0 += NS) {
-            // per-scan state (wave-uniform)
-            uint64_t x[NS][KW], pre[NS][KW];
-            uint32_t leaf[NS], remaining[NS], rid[NS], img[NS], st[NS];
-            bool live[NS], cont[NS];
-#pragma unroll
-            for (int k = 0; k < NS; ++k) {
-                const int j = j0 + k < cnt ? j0 + k : j0;
-                live[k] = j0 + k < cnt && scan_size > 0;
-#pragma unroll
-                for (int w = 0; w < KW; ++w) x[k][w] = pre[k][w] = rl64(ok[w], j);
-                leaf[k] = rl32(leafv, j);
-                rid[k] = rl32(ridv, j);
-                remaining[k] = scan_size;
-                img[k] = 0xFFFFFFFFu;
-                st[k] = ST_NOT_FOUND;
-                cont[k] = false;
-            }
-            for (uint32_t guard = 0; guard < scan_size + 2; ++guard) {
-                bool any = false;
-#pragma unroll
-                for (int k = 0; k < NS; ++k) any = any || live[k];
-                if (!any) break;
-                // (A) slot groups that can hold a key >= x: lane g tests group g's max key
-                uint64_t gmx[NS][KW];
-#pragma unroll
-                for (int k = 0; k < NS; ++k) {
-                    const uint64_t *gm = reinterpret_cast<const uint64_t *>(t.head + (uint64_t)leaf[k] * t.head_bytes +
-                                                                            head_gmax_offset(t.cap)) +
-                                         (lane < (uint32_t)SPL ? lane : 0u) * KW;
-#pragma unroll
-                    for (int w = 0; w < KW; ++w) gmx[k][w] = live[k] && lane < (uint32_t)SPL ? gm[w] : 0ull;
-                }
-                uint64_t active[NS];
-                uint32_t kept[NS], to_scan[NS];
-#pragma unroll
-                for (int k = 0; k < NS; ++k) {
-                    active[k] = ballot(live[k] && lane < (uint32_t)SPL && !kw_lt<KW>(gmx[k], x[k]));
-                    kept[k] = 0;
-                    to_scan[k] = remaining[k];
-                }
-                // (B) the groups in slot order until to_scan+1 records are held; the NS scans'
-                // visibility masks and key columns load together
-                for (;;) {
-                    int s[NS];
-                    bool any_g = false;
-#pragma unroll
-                    for (int k = 0; k < NS; ++k) {
-                        s[k] = active[k] && kept[k] <= to_scan[k] ? __builtin_ctzll(active[k]) : -1;
-                        if (s[k] >= 0) active[k] &= active[k] - 1;
-                        any_g = any_g || s[k] >= 0;
-                    }
-                    if (!any_g) break;
-                    uint64_t vm[NS], col[NS][KW];
-#pragma unroll
-                    for (int k = 0; k < NS; ++k) {
-                        const int sg = s[k] >= 0 ? s[k] : 0;
-                        vm[k] = s[k] >= 0 ? head_vis(t, leaf[k], sg) : 0ull;
-#pragma unroll
-                        for (int w = 0; w < KW; ++w)
-                            col[k][w] = s[k] >= 0 ? t.okey[((uint64_t)leaf[k] * KW + w) * t.cap + sg * 64 + lane] : 0ull;
-                    }
-#pragma unroll
-                    for (int k = 0; k < NS; ++k) {
-                        if (s[k] < 0) continue;
-                        const bool vis = (vm[k] >> lane) & 1;
-                        const uint64_t q = ballot(vis && !kw_lt<KW>(col[k], x[k]));
-                        if (!q) continue;
-                        const uint32_t rank = kept[k] + count_below(q);
-                        const bool take = ((q >> lane) & 1) && rank <= to_scan[k];
-                        if (take) {
-#pragma unroll
-                            for (int w = 0; w < KW; ++w) s_keys[wv][k][rank * KW + w] = col[k][w];
-                            s_slot[wv][k][rank] = (uint32_t)(s[k] * 64) + lane;
-                        }
-                        kept[k] += (uint32_t)__builtin_popcountll(ballot(take));
-                    }
-                }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                // (C) rank the kept records (lane k < m holds record k); (D) their slot words
-                uint64_t mk[NS][KW];
-                uint32_t kr[NS], mslot[NS], e[NS];
-                bool on[NS];
-                SlotInfo si[NS];
-#pragma unroll
-                for (int k = 0; k < NS; ++k) {
-                    const uint32_t m = kept[k];
-                    if (live[k] && m == 0) live[k] = false;  // nothing left in range
-                    const bool mine = live[k] && lane < m;
-#pragma unroll
-                    for (int w = 0; w < KW; ++w) mk[k][w] = mine ? s_keys[wv][k][lane * KW + w] : 0ull;
-                    mslot[k] = mine ? s_slot[wv][k][lane] : 0u;
-                    uint32_t r = 0;
-                    for (uint32_t jj = 0; live[k] && jj < m; ++jj) {
-                        uint64_t kj[KW];
-#pragma unroll
-                        for (int w = 0; w < KW; ++w) kj[w] = s_keys[wv][k][jj * KW + w];
-                        r += (mine && kw_lt<KW>(kj, mk[k])) ? 1u : 0u;
-                    }
-                    kr[k] = r;
-                    if (live[k] && cont[k]) {  // the continuation re-popped the last key: the scan ends
-                        bool eq = true;
-#pragma unroll
-                        for (int w = 0; w < KW; ++w) eq = eq && mk[k][w] == x[k][w];
-                        if (ballot(mine && r == 0 && eq)) live[k] = false;
-                    }
-                    e[k] = m < remaining[k] ? m : remaining[k];
-                    on[k] = live[k] && mine && r < e[k];
-                    si[k] = on[k] ? t.slot[(uint64_t)leaf[k] * t.cap + mslot[k]] : SlotInfo{};
-                }
-                __builtin_amdgcn_wave_barrier();  // the LDS lists are rewritten on the next leaf
-#pragma unroll
-                for (int k = 0; k < NS; ++k) {
-                    if (!live[k]) continue;
-                    uint8_t sv = ST_NOT_FOUND;
-                    uint32_t im = 0xFFFFFFFFu;
-                    bool pass = false;
-                    if (on[k]) {
-                        im = scan_visible(t, si[k], rid[k], sv);
-                        pass = sv == ST_LATEST || sv == ST_OLD;
-#pragma unroll
-                        for (int w = 0; w < KW; ++w)
-                            if ((uint32_t)w < words) pass = pass && mk[k][w] == pre[k][w];
-                    }
-                    uint64_t pm = ballot(pass);
-                    if (pm) {  // the passing record of lowest rank
-                        uint32_t best = 0xFFFFFFFFu;
-                        int bl = 0;
-                        while (pm) {
-                            const int b = __builtin_ctzll(pm);
-                            pm &= pm - 1;
-                            const uint32_t rr = rl32(kr[k], b);
-                            if (rr < best) {
-                                best = rr;
-                                bl = b;
-                            }
-                        }
-                        img[k] = rl32(im, bl);
-                        st[k] = rl32((uint32_t)sv, bl);
-                        live[k] = false;
-                        continue;
-                    }
-                    remaining[k] -= e[k];
-                    if (e[k] < kept[k] || remaining[k] == 0) {
-                        live[k] = false;
-                        continue;
-                    }
-                    // last record popped: continue from its key with le_child = false
-                    const uint64_t lm = ballot(lane < kept[k] && kr[k] == kept[k] - 1);
-                    const int b = __builtin_ctzll(lm);
-#pragma unroll
-                    for (int w = 0; w < KW; ++w) x[k][w] = rl64(mk[k][w], b);
-                    cont[k] = true;
-                }
-                // (E) the continuing scans' next leaves, loads together
-#pragma unroll
-                for (int k = 0; k < NS; ++k)
-                    if (live[k]) leaf[k] = uni32(next_leaf_after<false, KW>(t, leaf[k], x[k], len));
-            }
-#pragma unroll
-            for (int k = 0; k < NS; ++k)
-                if (lane == (uint32_t)(j0 + k)) {
-                    my_img = img[k];
-                    my_st = st[k];
-                }
-        }
-        if (valid) {
-            img_out[i] = my_img;
-            st_out[i] = (uint8_t)my_st;
-        }
-    }
-}
-
 // Point probes of the one-probe-in-flight instances (fixed-width keys of 9..32 bytes, or
 // 8-byte keys in leaves above 128 slots) in two stages per chunk of CH probes -- the results of
 // probe_kernel<false, SPL, 1, .., KW, CH>:
@@ -1696,228 +1445,6 @@ __device__ __forceinline__ uint32_t chunk_lower_bound(const DevTable &t, const u
     return node < t.nseps ? node : t.nseps;
 }
 
-// scan_first_kernel's semantics (scan_one_compact + FirstPrefixSink, fixed-width keys) with
-// the per-scan instruction count cut (the single-scan kernel issues ~1070 instructions per scan
-// and is issue- as much as latency-bound: profiles/r02/prof/tpcc_insts):
-//  * the chunk's 16 start-leaf descents are chunk-cooperative (chunk_lower_bound);
-//  * a slot group's visibility mask and key columns load together (one round trip);
-//  * the kept records' ranks: when they are increasing in slot order (a start key in a leaf's
-//    sorted region -- the common case) rank = slot-order position, checked with one compare
-//    per record against its predecessor; otherwise the O(m) count of the general kernel;
-//  * visibility is resolved only for records carrying the start key's prefix (the sink keeps
-//    no other record), and the lowest-rank passing record is a ctz on the fast path.
-template <int SPL, int KW, int WPE, bool PF>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void scan_first_fast_kernel(DevTable t, const uint64_t *__restrict__ keys,
-                                                              uint64_t n, uint32_t scan_size,
-                                                              const uint32_t *__restrict__ rids, uint32_t words,
-                                                              uint32_t *__restrict__ img_out,
-                                                              uint8_t *__restrict__ st_out) {
-    __shared__ uint64_t s_keys[4][64 * KW];
-    __shared__ uint32_t s_slot[4][64];
-    const uint32_t lane = lane_id(), wv = uni32(threadIdx.x >> 6);
-    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wv;
-    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    const uint32_t len = t.key_width;
-    uint64_t *lk = s_keys[wv];
-    uint32_t *ls = s_slot[wv];
-    for (uint64_t c0 = wave * kFirstChunk; c0 < n; c0 += nwaves * kFirstChunk) {
-        const uint64_t i = c0 + (lane >> 2);  // the scan this lane descends for
-        const bool valid = i < n;
-        uint64_t ok[KW];
-        load_okey<KW>(keys, i, valid, len, ok);
-        const uint32_t leafv = chunk_lower_bound<KW>(t, ok, lane & 3);
-        const uint32_t ridv = valid && rids ? rids[i] : 0xFFFFFFFEu;
-        const int cnt = (int)((n - c0) < (uint64_t)kFirstChunk ? (n - c0) : (uint64_t)kFirstChunk);
-        // PF: the start leaves' active slot groups of all 16 scans in one round trip (lane L
-        // tests groups L%4, L%4+4, ... for scan L/4), and scan j+1's first active group (mask +
-        // key columns) in flight while scan j runs
-        uint32_t actv = 0;
-        uint64_t pf_vm = 0, pf_col[KW];
-        int pf_s = 0;
-        if (PF) {
-            const uint64_t *gm = reinterpret_cast<const uint64_t *>(t.head + (uint64_t)leafv * t.head_bytes +
-                                                                    head_gmax_offset(t.cap));
-#pragma unroll
-            for (int g = 0; g < SPL; g += 4) {
-                const uint32_t gg = (uint32_t)g + (lane & 3);
-                if (gg < (uint32_t)SPL) {
-                    uint64_t e[KW];
-#pragma unroll
-                    for (int w = 0; w < KW; ++w) e[w] = gm[gg * KW + w];
-                    actv |= kw_lt<KW>(e, ok) ? 0u : (1u << gg);
-                }
-            }
-            actv |= (uint32_t)__shfl_xor((int)actv, 1);
-            actv |= (uint32_t)__shfl_xor((int)actv, 2);
-            const uint32_t a0 = rl32(actv, 0), l0 = rl32(leafv, 0);
-            pf_s = a0 ? __builtin_ctz(a0) : 0;
-            pf_vm = head_vis(t, l0, pf_s);
-#pragma unroll
-            for (int w = 0; w < KW; ++w) pf_col[w] = t.okey[((uint64_t)l0 * KW + w) * t.cap + pf_s * 64 + lane];
-        }
-        uint32_t my_img = 0xFFFFFFFFu, my_st = ST_NOT_FOUND;
-        for (int j = 0; j < cnt; ++j) {
-            const int src = 4 * j;
-            uint64_t x[KW];
-#pragma unroll
-            for (int w = 0; w < KW; ++w) x[w] = rl64(ok[w], src);
-            uint32_t leaf = rl32(leafv, src);
-            const uint32_t rid = rl32(ridv, src);
-            uint32_t img = 0xFFFFFFFFu, st = ST_NOT_FOUND, remaining = scan_size;
-            bool cont = false;
-            // pf_* hold this scan's first group; once it is consumed the next scan's goes in flight
-            bool pf_pending = PF;
-            auto issue_next = [&]() {
-                pf_pending = false;
-                if (j + 1 < cnt) {
-                    const uint32_t an = rl32(actv, src + 4), ln = rl32(leafv, src + 4);
-                    pf_s = an ? __builtin_ctz(an) : 0;
-                    pf_vm = head_vis(t, ln, pf_s);
-#pragma unroll
-                    for (int w = 0; w < KW; ++w)
-                        pf_col[w] = t.okey[((uint64_t)ln * KW + w) * t.cap + pf_s * 64 + lane];
-                }
-            };
-            for (uint32_t guard = 0; guard < scan_size + 2 && remaining > 0; ++guard) {
-                const uint64_t base = (uint64_t)leaf * t.cap;
-                // slot groups that can hold a key >= x (lane g tests group g's max key)
-                bool act = false;
-                if (PF && guard == 0) {
-                    act = lane < (uint32_t)SPL && ((rl32(actv, src) >> lane) & 1);
-                } else if (lane < (uint32_t)SPL) {
-                    const uint64_t *gm =
-                        reinterpret_cast<const uint64_t *>(t.head + (uint64_t)leaf * t.head_bytes +
-                                                           head_gmax_offset(t.cap)) + lane * KW;
-                    uint64_t g[KW];
-#pragma unroll
-                    for (int w = 0; w < KW; ++w) g[w] = gm[w];
-                    act = !kw_lt<KW>(g, x);
-                }
-                uint64_t active = ballot(act);
-                const uint32_t to_scan = remaining;
-                uint32_t kept = 0;
-                while (active) {
-                    const int s = __builtin_ctzll(active);
-                    active &= active - 1;
-                    uint64_t vm, col[KW];
-                    const bool from_pf = PF && pf_pending && s == pf_s;
-                    if (from_pf) {  // the first visit's first group: prefetched
-                        vm = pf_vm;
-#pragma unroll
-                        for (int w = 0; w < KW; ++w) col[w] = pf_col[w];
-                    } else {
-                        vm = head_vis(t, leaf, s);
-#pragma unroll
-                        for (int w = 0; w < KW; ++w) col[w] = t.okey[((uint64_t)leaf * KW + w) * t.cap + s * 64 + lane];
-                    }
-                    const bool vis = (vm >> lane) & 1;
-                    const uint64_t q = ballot(vis && !kw_lt<KW>(col, x));
-                    const uint32_t rank = kept + count_below(q);
-                    const bool take = ((q >> lane) & 1) && rank <= to_scan;
-                    if (take) {
-#pragma unroll
-                        for (int w = 0; w < KW; ++w) lk[rank * KW + w] = col[w];
-                        ls[rank] = (uint32_t)(s * 64) + lane;
-                    }
-                    if (from_pf) issue_next();
-                    if (!q) continue;
-                    kept += (uint32_t)__builtin_popcountll(ballot(take));
-                    if (kept > to_scan) break;
-                }
-                if (PF && pf_pending) issue_next();
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                const uint32_t m = kept;
-                if (m == 0) break;
-                const bool mine = lane < m;
-                uint64_t mk[KW];
-                uint32_t mslot = 0;
-#pragma unroll
-                for (int w = 0; w < KW; ++w) mk[w] = mine ? lk[lane * KW + w] : 0ull;
-                bool ord = true;
-                if (mine) {
-                    mslot = ls[lane];
-                    if (lane > 0) {
-                        uint64_t pk[KW];
-#pragma unroll
-                        for (int w = 0; w < KW; ++w) pk[w] = lk[(lane - 1) * KW + w];
-                        ord = kw_lt<KW>(pk, mk);
-                    }
-                }
-                const bool sorted = ballot(!ord) == 0;
-                uint32_t kr = lane;
-                if (!sorted) {
-                    kr = 0;
-                    for (uint32_t jj = 0; jj < m; ++jj) {
-                        uint64_t kj[KW];
-#pragma unroll
-                        for (int w = 0; w < KW; ++w) kj[w] = lk[jj * KW + w];
-                        kr += (mine && kw_lt<KW>(kj, mk)) ? 1u : 0u;
-                    }
-                }
-                __builtin_amdgcn_wave_barrier();  // the LDS list is rewritten on the next leaf
-                if (cont) {  // the continuation re-popped the last key: the scan ends
-                    bool eq = true;
-#pragma unroll
-                    for (int w = 0; w < KW; ++w) eq = eq && mk[w] == x[w];
-                    if (ballot(mine && kr == 0 && eq)) break;
-                }
-                const uint32_t e = m < remaining ? m : remaining;
-                uint8_t sv = ST_NOT_FOUND;
-                uint32_t im = 0xFFFFFFFFu;
-                bool pass = false;
-                if (mine && kr < e) {
-                    bool pfx = true;
-#pragma unroll
-                    for (int w = 0; w < KW; ++w)
-                        if ((uint32_t)w < words) pfx = pfx && mk[w] == rl64(ok[w], src);  // start key prefix
-                    if (pfx) {
-                        im = scan_visible(t, t.slot[base + mslot], rid, sv);
-                        pass = sv == ST_LATEST || sv == ST_OLD;
-                    }
-                }
-                uint64_t pm = ballot(pass);
-                if (pm) {  // the passing record of lowest rank
-                    int bl = __builtin_ctzll(pm);
-                    if (!sorted) {
-                        uint32_t best = 0xFFFFFFFFu;
-                        while (pm) {
-                            const int b = __builtin_ctzll(pm);
-                            pm &= pm - 1;
-                            const uint32_t rr = rl32(kr, b);
-                            if (rr < best) {
-                                best = rr;
-                                bl = b;
-                            }
-                        }
-                    }
-                    img = rl32(im, bl);
-                    st = rl32((uint32_t)sv, bl);
-                    break;
-                }
-                remaining -= e;
-                if (e < m) break;
-                // last record popped: continue from its key with le_child = false
-                const uint64_t lm = ballot(mine && kr == m - 1);
-                const int b = __builtin_ctzll(lm);
-#pragma unroll
-                for (int w = 0; w < KW; ++w) x[w] = rl64(mk[w], b);
-                leaf = uni32(next_leaf_after<false, KW>(t, leaf, x, len));
-                cont = true;
-            }
-            if (lane == (uint32_t)j) {
-                my_img = img;
-                my_st = st;
-            }
-        }
-        if (lane < (uint32_t)cnt) {
-            img_out[c0 + lane] = my_img;
-            st_out[c0 + lane] = (uint8_t)my_st;
-        }
-    }
-}
-
 // The first-tuple scans split in two stages per chunk of 16 (same results as scan_first_kernel):
 //  A (wave per scan, in turn): the start leaf's first visit -- active groups (all 16 scans' in
 //    one round trip), the first group prefetched while the previous scan runs, the kept records
@@ -1930,9 +1457,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 //  a scan whose first visit decides nothing (no candidate passed, the visit held m <= e records
 //    and the scan has records left) is re-run by the general loop (scan_one_compact +
 //    FirstPrefixSink), which continues across leaves.
-// SKIP: a second pass behind scan_first_probe_kernel -- a chunk whose 16 scans that kernel
-// all decided is skipped (recomputing a decided scan would store the same result).
-template <int SPL, int KW, int WPE, bool SKIP = false>
+template <int SPL, int KW, int WPE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void scan_first_split_kernel(
     DevTable t, const uint64_t *__restrict__ keys, uint64_t n, uint32_t scan_size, const uint32_t *__restrict__ rids,
     uint32_t words, uint32_t *__restrict__ img_out, uint8_t *__restrict__ st_out) {
@@ -1947,10 +1472,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     uint32_t *ls = s_slot[wv];
     constexpr uint16_t kHole = 0xFFFF;
     for (uint64_t c0 = wave * kFirstChunk; c0 < n; c0 += nwaves * kFirstChunk) {
-        if constexpr (SKIP) {
-            const uint64_t q = c0 + lane;
-            if (!ballot(lane < (uint32_t)kFirstChunk && q < n && st_out[q] == kFirstUndecided)) continue;
-        }
         const uint64_t i = c0 + (lane >> 2);  // the scan this lane descends for
         const bool valid = i < n;
         uint64_t ok[KW];
@@ -2148,534 +1669,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         if (lane < (uint32_t)cnt) {
             img_out[c0 + lane] = my_img;
             st_out[c0 + lane] = (uint8_t)my_st;
-        }
-        __builtin_amdgcn_wave_barrier();  // s_cand is rewritten by the next chunk
-    }
-}
-
-// The first-tuple scans without the wave-serial stage of scan_first_split_kernel, for the
-// leaves' monotone prefix: the head info word carries the leaf's record count and the length mp
-// of its longest slot prefix whose keys increase (>= the sorted region, RangeScanBySize's
-// reference layout after a split; the whole leaf for a table loaded in key order).
-// RangeScanBySize keeps the first to_scan + 1 visible records with key >= x in slot order
-// (b_tree.cpp:1276-1302): when the monotone prefix alone holds that many from p =
-// lower_bound(x) on, they are its visible slots from p on, already in key order, so the first
-// candidates in rank order are the first visible slots >= p.  Per chunk of 16 scans, 4 lanes per
-// scan (lane L: scan L/4, part L%4), every step one round trip for all 16:
-//   1. the start leaf (chunk_lower_bound);
-//   2. the info word, group maxima and visible masks (a quarter per lane);
-//   3. p: the first full monotone group whose max key is >= x (or the partial one), then a 5-ary
-//      search in it, the 4 lanes comparing 4 pivots (64 -> 12 -> 2 -> 0 slots);
-//   4. the first 4 visible slots >= p, one per lane: key prefix and slot word, visibility
-//      (scan_visible); the lowest passing one in slot order is the scan's tuple.
-// Scans this does not decide -- fewer than to_scan + 1 visible records in [p, mp) while records
-// follow mp, or no pass among the first 4 candidates while more candidates or an Iterator
-// continuation remain -- are left to scan_first_rest_kernel (kFirstUndecided).
-template <int SPL, int KW, int WPE = 8>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void scan_first_mono_kernel(
-    DevTable t, const uint64_t *__restrict__ keys,
-                                                              uint64_t n, uint32_t scan_size,
-                                                              const uint32_t *__restrict__ rids, uint32_t words,
-                                                              uint32_t *__restrict__ img_out,
-                                                              uint8_t *__restrict__ st_out) {
-    static_assert(SPL <= 16, "visible masks: up to 4 words per lane");
-    const uint32_t lane = lane_id(), part = lane & 3, quad = lane & ~3u;
-    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + uni32(threadIdx.x >> 6);
-    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    const uint32_t len = t.key_width;
-    constexpr int VPL = SPL >= 4 ? SPL / 4 : 1;  // visible-mask words per lane
-    for (uint64_t c0 = wave * kFirstChunk; c0 < n; c0 += nwaves * kFirstChunk) {
-        const uint64_t i = c0 + (lane >> 2);
-        const bool valid = i < n;
-        uint64_t x[KW];
-        load_okey<KW>(keys, i, valid, len, x);
-        const uint32_t leaf = chunk_lower_bound<KW>(t, x, part);
-        const uint32_t rid = valid && rids ? rids[i] : 0xFFFFFFFEu;
-        // 2. info word, group maxima (groups part, part + 4, ...), visible masks (words part * VPL ..)
-        const uint8_t *hd = t.head + (uint64_t)leaf * t.head_bytes;
-        const uint32_t info = *reinterpret_cast<const uint32_t *>(hd + head_info_offset(t.cap, KW));
-        const uint64_t *gm = reinterpret_cast<const uint64_t *>(hd + head_gmax_offset(t.cap));
-        uint32_t actv = 0;
-#pragma unroll
-        for (int g = 0; g < SPL; g += 4) {
-            const uint32_t gg = (uint32_t)g + part;
-            if (gg < (uint32_t)SPL) {
-                uint64_t e[KW];
-#pragma unroll
-                for (int w = 0; w < KW; ++w) e[w] = gm[gg * KW + w];
-                actv |= kw_lt<KW>(e, x) ? 0u : (1u << gg);
-            }
-        }
-        uint64_t vis[VPL];
-#pragma unroll
-        for (int k = 0; k < VPL; ++k) {
-            const uint32_t wi = part * VPL + (uint32_t)k;
-            vis[k] = wi < (uint32_t)SPL ? head_vis(t, leaf, (int)wi) : 0ull;
-        }
-        actv |= (uint32_t)__shfl_xor((int)actv, 1);
-        actv |= (uint32_t)__shfl_xor((int)actv, 2);
-        const uint32_t count = info & 0xFFFFu, mp = info >> 16;
-        // 3. p = lower_bound(x) over the monotone prefix [0, mp).  Full groups inside it have
-        //    their last key as maximum: the first one >= x holds p; else p is in the partial group.
-        const uint32_t nfull = mp / 64u;
-        const uint32_t act_full = actv & (nfull >= 32u ? ~0u : ((1u << nfull) - 1u));
-        uint32_t lo = act_full ? 64u * (uint32_t)__builtin_ctz(act_full) : 64u * nfull;
-        uint32_t hi = act_full ? lo + 64u : mp;
-        const uint64_t *plane = t.okey + (uint64_t)leaf * KW * t.cap;
-        for (int step = 0; step < 4; ++step) {
-            const uint32_t span = hi > lo ? hi - lo : 0u;
-            // the 4 lanes of a scan share lo / hi (same inputs, same steps): quads go together
-            if (span == 0) continue;
-            const uint32_t piv = lo + ((part + 1u) * span) / 5u;
-            uint64_t k[KW];
-#pragma unroll
-            for (int w = 0; w < KW; ++w) k[w] = plane[(uint64_t)w * t.cap + piv];
-            int c = kw_lt<KW>(k, x) ? 1 : 0;
-            c += __shfl_xor(c, 1);
-            c += __shfl_xor(c, 2);
-            // pivots increase with the part and keys with the slot: parts [0, c) hold keys < x,
-            // so p lies in (piv[c-1], piv[c]]
-            const uint32_t plo = c > 0 ? (uint32_t)__shfl((int)piv, (int)(quad + (uint32_t)c - 1u)) + 1u : lo;
-            const uint32_t phi = c < 4 ? (uint32_t)__shfl((int)piv, (int)(quad + (uint32_t)c)) : hi;
-            lo = plo;
-            hi = phi;
-        }
-        const uint32_t p = lo;
-        // 4. visible slots in [p, mp): this lane's words masked and counted
-        uint32_t nv = 0;
-#pragma unroll
-        for (int k = 0; k < VPL; ++k) {
-            const uint32_t s0 = (part * VPL + (uint32_t)k) * 64u;
-            uint64_t v = vis[k];
-            if (s0 + 64u <= p || s0 >= mp) v = 0;
-            else {
-                if (s0 < p) v &= ~0ull << (p - s0);
-                if (mp < s0 + 64u) v &= (1ull << (mp - s0)) - 1ull;
-            }
-            vis[k] = v;
-            nv += (uint32_t)__builtin_popcountll(v);
-        }
-        const uint32_t n0 = (uint32_t)__shfl((int)nv, (int)quad), n1 = (uint32_t)__shfl((int)nv, (int)(quad + 1u)),
-                       n2 = (uint32_t)__shfl((int)nv, (int)(quad + 2u));
-        const uint32_t before = part == 0 ? 0u : part == 1 ? n0 : part == 2 ? n0 + n1 : n0 + n1 + n2;
-        uint32_t vs = nv;
-        vs += (uint32_t)__shfl_xor((int)vs, 1);
-        vs += (uint32_t)__shfl_xor((int)vs, 2);
-        // part r's candidate: the (r + 1)-th visible slot >= p, found by whichever lane's words
-        // hold it (each lane walks its own set bits), then OR-gathered over the scan's lanes
-        uint32_t cand[4] = {0u, 0u, 0u, 0u};  // slot + 1, 0 = none
-        {
-            uint32_t r = before;
-#pragma unroll
-            for (int k = 0; k < VPL; ++k) {
-                uint64_t v = vis[k];
-                while (v && r < 4u) {
-                    const uint32_t s = (part * VPL + (uint32_t)k) * 64u + (uint32_t)__builtin_ctzll(v);
-                    v &= v - 1;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        if (r == (uint32_t)q) cand[q] = s + 1u;
-                    ++r;
-                }
-            }
-        }
-        uint32_t my_cand = 0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            uint32_t v = cand[q];
-            v |= (uint32_t)__shfl_xor((int)v, 1);
-            v |= (uint32_t)__shfl_xor((int)v, 2);
-            if (part == (uint32_t)q) my_cand = v;
-        }
-        // the visit's kept records m and candidates e -- decided when the prefix alone supplies
-        // to_scan + 1 records, or when nothing follows it (then m is all it has)
-        const bool whole = mp >= count;
-        const bool decided = vs >= scan_size + 1u || whole;
-        const uint32_t m = vs < scan_size + 1u ? vs : scan_size + 1u;
-        const uint32_t e = m < scan_size ? m : scan_size;
-        // per candidate: 1 = has the prefix and resolves (LATEST / OLD), 2 = no prefix (a hole:
-        // its key, and every later candidate's, is past the prefix range, so the scan has no
-        // tuple), 3 = prefix but nothing visible for the read id, 0 = no candidate
-        uint32_t res = 0;
-        uint32_t img = 0xFFFFFFFFu;
-        uint8_t sv = ST_NOT_FOUND;
-        if (valid && decided && my_cand && part < e) {
-            const uint32_t sl = my_cand - 1u;
-            bool pfx = true;
-#pragma unroll
-            for (int w = 0; w < KW; ++w)
-                if ((uint32_t)w < words) pfx = pfx && plane[(uint64_t)w * t.cap + sl] == x[w];
-            const SlotInfo si = t.slot[(uint64_t)leaf * t.cap + sl];
-            if (pfx) {
-                img = scan_visible(t, si, rid, sv);
-                res = sv == ST_LATEST || sv == ST_OLD ? 1u : 3u;
-            } else {
-                res = 2u;
-            }
-        }
-        // the scan's outcome from its candidates in rank order (parts 0..3): the first that
-        // resolves or is a hole decides; candidates past the 4th are left to the general loop
-        uint32_t code = 0;  // 4 x 2 bits, part r at bits 2r
-#pragma unroll
-        for (int q = 0; q < 4; ++q) code |= (uint32_t)__shfl((int)res, (int)(quad + (uint32_t)q)) << (2 * q);
-        int first = -1;  // first part that resolves (1) or is a hole (2)
-        int stop = 4;    // first part without a candidate
-#pragma unroll
-        for (int q = 3; q >= 0; --q) {
-            const uint32_t c = (code >> (2 * q)) & 3u;
-            if (c == 1u || c == 2u) first = q;
-            if (c == 0u) stop = q;
-        }
-        const uint32_t wimg = (uint32_t)__shfl((int)img, (int)(quad + (uint32_t)(first < 0 ? 0 : first)));
-        const uint32_t wst = (uint32_t)__shfl((int)sv, (int)(quad + (uint32_t)(first < 0 ? 0 : first)));
-        if (valid && part == 0) {
-            uint8_t st = ST_NOT_FOUND;
-            uint32_t im = 0xFFFFFFFFu;
-            const bool reached = first >= 0 && first < stop;  // decided before the candidates ran out
-            if (!decided) {
-                st = kFirstUndecided;
-            } else if (reached && ((code >> (2 * first)) & 3u) == 1u) {
-                st = (uint8_t)wst;
-                im = wimg;
-            } else if (reached) {
-                st = ST_NOT_FOUND;  // a hole: no candidate from it on has the prefix
-            } else if (m == 0) {
-                st = ST_NOT_FOUND;  // the visit kept nothing: the Iterator ends
-            } else if (e > 4u || (e == m && scan_size > e)) {
-                st = kFirstUndecided;  // candidates past the 4th, or an Iterator continuation
-            }
-            img_out[i] = im;
-            st_out[i] = st;
-        }
-    }
-}
-
-// inclusive prefix sum within each row of 16 lanes (DPP row shifts; lanes shifted in from
-// outside the row read 0)
-__device__ __forceinline__ uint32_t row16_incl_scan(uint32_t v) {
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
-    return v;
-}
-__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
-    return ((uint64_t)(uint32_t)__shfl((int)(v >> 32), src) << 32) | (uint32_t)__shfl((int)(uint32_t)v, src);
-}
-
-// scan_first_split_kernel with stage A run for SUB scans at once: lane segment r (64/SUB lanes)
-// works for scan SUB*p + r of pass p, each lane tests SUB consecutive slots of a slot group, a
-// segmented DPP prefix sum ranks the qualifying slots in slot order, and lane k of the segment
-// then holds kept record k (scan_size < 64/SUB).  The uniform per-scan control of the
-// wave-per-scan stage A (~420 instructions per scan) is shared by SUB scans.  Stage B and the
-// undecided scans as in scan_first_split_kernel.
-template <int SPL, int KW, int WPE, int SUB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void scan_first_seg_kernel(
-    DevTable t, const uint64_t *__restrict__ keys, uint64_t n, uint32_t scan_size, const uint32_t *__restrict__ rids,
-    uint32_t words, uint32_t *__restrict__ img_out, uint8_t *__restrict__ st_out) {
-    static_assert(SUB == 2 || SUB == 4, "segments of 32 or 16 lanes");
-    constexpr uint32_t SEGW = 64 / SUB;
-    __shared__ uint64_t s_keys[4][SUB][SEGW * KW];
-    __shared__ uint32_t s_slot[4][SUB][SEGW];
-    __shared__ uint16_t s_cand[4][kFirstChunk][SEGW];
-    const uint32_t lane = lane_id(), wv = uni32(threadIdx.x >> 6);
-    const uint32_t seg = lane / SEGW, sl = lane % SEGW;
-    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wv;
-    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    const uint32_t len = t.key_width;
-    uint64_t *lk = s_keys[wv][seg];
-    uint32_t *ls = s_slot[wv][seg];
-    constexpr uint16_t kHole = 0xFFFF;
-    for (uint64_t c0 = wave * kFirstChunk; c0 < n; c0 += nwaves * kFirstChunk) {
-        const uint64_t i = c0 + (lane >> 2);  // the scan this lane descends for
-        const bool valid = i < n;
-        uint64_t ok[KW];
-        load_okey<KW>(keys, i, valid, len, ok);
-        const uint32_t leafv = chunk_lower_bound<KW>(t, ok, lane & 3);
-        const uint32_t ridv = valid && rids ? rids[i] : 0xFFFFFFFEu;
-        const int cnt = (int)((n - c0) < (uint64_t)kFirstChunk ? (n - c0) : (uint64_t)kFirstChunk);
-        uint32_t actv = 0;
-        {
-            const uint64_t *gm = reinterpret_cast<const uint64_t *>(t.head + (uint64_t)leafv * t.head_bytes +
-                                                                    head_gmax_offset(t.cap));
-#pragma unroll
-            for (int g = 0; g < SPL; g += 4) {
-                const uint32_t gg = (uint32_t)g + (lane & 3);
-                if (gg < (uint32_t)SPL) {
-                    uint64_t e[KW];
-#pragma unroll
-                    for (int w = 0; w < KW; ++w) e[w] = gm[gg * KW + w];
-                    actv |= kw_lt<KW>(e, ok) ? 0u : (1u << gg);
-                }
-            }
-            actv |= (uint32_t)__shfl_xor((int)actv, 1);
-            actv |= (uint32_t)__shfl_xor((int)actv, 2);
-        }
-        uint32_t my_info = 0;
-        // ---- stage A, SUB scans per pass
-#pragma unroll 1
-        for (int p = 0; p < (cnt + SUB - 1) / SUB; ++p) {
-            const int j = SUB * p + (int)seg;  // this segment's scan
-            const int src = 4 * (j < kFirstChunk ? j : 0);
-            uint64_t x[KW];
-#pragma unroll
-            for (int w = 0; w < KW; ++w) x[w] = shfl64(ok[w], src);
-            const uint32_t leaf = (uint32_t)__shfl((int)leafv, src);
-            uint32_t act = (uint32_t)__shfl((int)actv, src);
-            bool live = j < cnt && act != 0;
-            uint32_t kept = 0;
-#pragma unroll 1
-            while (ballot(live)) {
-                const int s = live ? __builtin_ctz(act) : 0;
-                if (live) act &= act - 1;
-                uint64_t vm = 0, col[SUB][KW];
-                const uint64_t gbase = (uint64_t)s * 64 + sl * SUB;
-                if (live) {
-                    vm = head_vis(t, leaf, s);
-#pragma unroll
-                    for (int w = 0; w < KW; ++w) {
-                        const uint64_t *cp = t.okey + ((uint64_t)leaf * KW + w) * t.cap + gbase;
-#pragma unroll
-                        for (int k = 0; k < SUB; ++k) col[k][w] = cp[k];
-                    }
-                }
-                uint32_t qb = 0;
-#pragma unroll
-                for (int k = 0; k < SUB; ++k)
-                    qb |= (live & (((vm >> (sl * SUB + k)) & 1) != 0) & !kw_lt_flat<KW>(col[k], x)) ? 1u << k : 0u;
-                const uint32_t c = (uint32_t)__builtin_popcount(qb);
-                uint32_t incl = row16_incl_scan(c);
-                if (SEGW == 32) {  // upper row of a 32-lane segment: + the lower row's total
-                    const uint32_t low = (uint32_t)__shfl((int)incl, (int)((lane & ~31u) | 15u));
-                    incl += (lane & 16) ? low : 0u;
-                }
-                const uint32_t total = (uint32_t)__shfl((int)incl, (int)(lane | (SEGW - 1)));
-                uint32_t r = kept + incl - c;
-#pragma unroll
-                for (int k = 0; k < SUB; ++k)
-                    if ((qb >> k) & 1) {
-                        if (r <= scan_size) {
-#pragma unroll
-                            for (int w = 0; w < KW; ++w) lk[r * KW + w] = col[k][w];
-                            ls[r] = (uint32_t)(gbase + k);
-                        }
-                        ++r;
-                    }
-                if (live) {
-                    kept += total;
-                    if (kept > scan_size || act == 0) live = false;
-                }
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const uint32_t m = kept < scan_size + 1 ? kept : scan_size + 1;  // records held (<= SEGW)
-            const uint64_t segmask = (SEGW == 32 ? 0xFFFFFFFFull : 0xFFFFull) << (seg * SEGW);
-            const bool mine = j < cnt && sl < m;
-            uint64_t mk[KW];
-            uint32_t mslot = 0;
-            bool ord = true;
-#pragma unroll
-            for (int w = 0; w < KW; ++w) mk[w] = mine ? lk[sl * KW + w] : 0ull;
-            if (mine) {
-                mslot = ls[sl];
-                if (sl > 0) {
-                    uint64_t pk[KW];
-#pragma unroll
-                    for (int w = 0; w < KW; ++w) pk[w] = lk[(sl - 1) * KW + w];
-                    ord = kw_lt<KW>(pk, mk);
-                }
-            }
-            const bool seg_sorted = (ballot(!ord) & segmask) == 0;
-            uint32_t kr = sl;
-            bool dup = false;
-            if (!seg_sorted) {
-                kr = 0;
-                for (uint32_t jj = 0; jj < m; ++jj) {
-                    bool eq = jj != sl;
-                    uint64_t kj[KW];
-#pragma unroll
-                    for (int w = 0; w < KW; ++w) {
-                        kj[w] = lk[jj * KW + w];
-                        eq = eq && kj[w] == mk[w];
-                    }
-                    kr += (mine && kw_lt<KW>(kj, mk)) ? 1u : 0u;
-                    dup = dup || (mine && eq);
-                }
-            }
-            const bool seg_dup = (ballot(dup) & segmask) != 0;
-            const uint32_t e = m < scan_size ? m : scan_size;
-            uint32_t info = 0;
-            if (j < cnt && m > 0) {
-                if (seg_dup) {
-                    info = 0x200u;  // equal keys share a rank: the general loop decides
-                } else {
-                    info = e | (e == m && scan_size > e ? 0x100u : 0u);
-                    if (sl < e) s_cand[wv][j][sl] = kHole;
-                    if (mine && kr < e) {
-                        bool pfx = true;
-#pragma unroll
-                        for (int w = 0; w < KW; ++w)
-                            if ((uint32_t)w < words) pfx = pfx && mk[w] == x[w];
-                        if (pfx) s_cand[wv][j][kr] = (uint16_t)mslot;
-                    }
-                }
-            }
-            __builtin_amdgcn_wave_barrier();  // the LDS lists are rewritten by the next pass
-            // lane q (< 16) keeps the info of scan q = SUB*p + r from segment r's lane 0
-            const uint32_t got = (uint32_t)__shfl((int)info, (int)((lane % SUB) * SEGW));
-            if (lane / SUB == (uint32_t)p && lane < 16) my_info = got;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // ---- stage B: lane j resolves scan j's candidates in rank order
-        const uint32_t my_leaf = (uint32_t)__shfl((int)leafv, (int)(4 * (lane & 15)));
-        const uint32_t my_rid = (uint32_t)__shfl((int)ridv, (int)(4 * (lane & 15)));
-        uint32_t my_img = 0xFFFFFFFFu, my_st = ST_NOT_FOUND;
-        bool found = false;
-        if (lane < (uint32_t)cnt) {
-            const uint32_t e = my_info & 0xFF;
-            const uint64_t base = (uint64_t)my_leaf * t.cap;
-            for (uint32_t c = 0; c < e; ++c) {
-                const uint16_t slo = s_cand[wv][lane][c];
-                if (slo == kHole) continue;
-                uint8_t sv;
-                const uint32_t im = scan_visible(t, t.slot[base + slo], my_rid, sv);
-                if (sv == ST_LATEST || sv == ST_OLD) {
-                    my_img = im;
-                    my_st = sv;
-                    found = true;
-                    break;
-                }
-            }
-        }
-        if (lane < (uint32_t)cnt && ((!found && (my_info & 0x100u)) || (my_info & 0x200u))) my_st = kFirstUndecided;
-        if (lane < (uint32_t)cnt) {
-            img_out[c0 + lane] = my_img;
-            st_out[c0 + lane] = (uint8_t)my_st;
-        }
-        __builtin_amdgcn_wave_barrier();  // s_cand is rewritten by the next chunk
-    }
-}
-
-// First-tuple scans decided as point probes of their start key.  RangeScanBySize keeps the
-// first to_scan + 1 visible records with key >= x in slot order and ranks them by key
-// (b_tree.cpp:1276-1302); the scan's result is the first LATEST / OLD record in rank order that
-// carries the start key's prefix (executor.h:459-490 with the predicate).  When a visible record
-// holds exactly x at slot p inside the leaf's monotone slot prefix (p < mp, the head's info
-// word), every visible slot before p holds a key below x, so p is the first record kept and --
-// x being the least key >= x -- rank 0, unless another visible record also holds x (only
-// possible beyond mp, where the key order is not known: such a candidate is confirmed).  Rank 0
-// carries every prefix of x, so if its visibility at the read id is LATEST / OLD it is the
-// result.  Everything else -- no exact record, p >= mp, an equal key beyond mp, more than
-// kProbeCand fingerprint candidates, rank 0 invisible to the reader -- is marked kFirstUndecided
-// for scan_first_rest_kernel's general loop.  A TPC-C stock-level scan starts at {w, d, o, 5},
-// the fifth line of an order of 5..15 lines, so the exact record is the usual case, and the scan
-// costs what a point probe costs: the probe_split_kernel structure (a lane-per-scan descent,
-// the fingerprint heads wave-serial with 4 in flight, the candidates' slot words lane-parallel)
-// instead of a slot group's key columns per scan.
-template <int SPL, int KW, int CH>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void scan_first_probe_kernel(
-    DevTable t, const uint64_t *__restrict__ keys, uint64_t n, const uint32_t *__restrict__ rids,
-    uint32_t *__restrict__ img_out, uint8_t *__restrict__ st_out) {
-    __shared__ uint16_t s_cand[4][64][kProbeCand];
-    const uint32_t lane = lane_id(), wv = uni32(threadIdx.x >> 6);
-    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wv;
-    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    const uint32_t len = t.key_width;
-    for (uint64_t base = wave * CH; base < n; base += nwaves * CH) {
-        const uint64_t i = base + lane;
-        const bool valid = lane < (uint32_t)CH && i < n;
-        const uint32_t rid = rids ? (valid ? rids[i] : 0u) : 0xFFFFFFFEu;
-        uint64_t ok[KW];
-        load_okey<KW>(keys, i, valid, len, ok);
-        uint32_t leaf = 0;
-        if (valid) leaf = resolve_leaf<false, KW>(t, ok, len, true);
-        // the leaf's monotone prefix length, in flight through stage A
-        const uint32_t mp = valid ? *reinterpret_cast<const uint32_t *>(t.head + (uint64_t)leaf * t.head_bytes +
-                                                                       head_info_offset(t.cap, KW)) >> 16
-                                  : 0u;
-        const uint32_t fx_mine = key_fp_words(ok, KW);
-        const int cnt = (int)((n - base) < CH ? (n - base) : CH);
-        // ---- stage A (probe_split_kernel's): fingerprint candidates in slot order to LDS
-        constexpr int PD = SPL <= 4 ? 4 : 1;
-        uint32_t pf[PD][SPL];
-#pragma unroll
-        for (int d = 0; d < PD; ++d) {
-            if (d < cnt) {
-                const uint8_t *h = t.head + (uint64_t)rl32(leaf, d) * t.head_bytes;
-#pragma unroll
-                for (int s = 0; s < SPL; ++s) pf[d][s] = h[s * 64 + lane];
-            }
-        }
-        uint32_t my_nc = 0;
-        for (int j0 = 0; j0 < cnt; j0 += PD) {
-#pragma unroll
-            for (int u = 0; u < PD; ++u) {
-                const int j = j0 + u;
-                if (j >= cnt) break;
-                uint32_t fpb[SPL];
-#pragma unroll
-                for (int s = 0; s < SPL; ++s) fpb[s] = pf[u][s];
-                if (j + PD < cnt) {
-                    const uint8_t *h = t.head + (uint64_t)rl32(leaf, j + PD) * t.head_bytes;
-#pragma unroll
-                    for (int s = 0; s < SPL; ++s) pf[u][s] = h[s * 64 + lane];
-                }
-                const uint32_t fx = rl32(fx_mine, j);
-                uint32_t nc = 0;
-#pragma unroll
-                for (int s = 0; s < SPL; ++s) {
-                    const bool c = fpb[s] == fx;
-                    const uint64_t cm = ballot(c);
-                    const uint32_t r = nc + count_below(cm);
-                    if (c && r < (uint32_t)kProbeCand) s_cand[wv][j][r] = (uint16_t)(s * 64 + lane);
-                    nc += (uint32_t)__builtin_popcountll(cm);
-                }
-                if (lane == (uint32_t)j) my_nc = nc;
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // ---- stage B: lane = scan
-        if (valid) {
-            const uint64_t lb = (uint64_t)leaf * t.cap;
-            int p = -1;
-            bool undecided = my_nc > (uint32_t)kProbeCand;
-            SlotInfo si{};
-            for (uint32_t c = 0; c < my_nc && !undecided; ++c) {
-                const uint32_t sl = s_cand[wv][lane][c];
-                if (p >= 0 && sl < mp) continue;  // after p inside the monotone prefix: key > x
-                const u32x4 *w = reinterpret_cast<const u32x4 *>(t.slot + lb + sl);
-                const u32x4 w0 = w[0], w1 = w[1];
-                bool eq = (((uint64_t)w0.y << 32) | w0.x) == ok[0];
-#pragma unroll
-                for (int k = 1; k < KW; ++k) eq = eq && t.okey[((uint64_t)leaf * KW + k) * t.cap + sl] == ok[k];
-                if (!eq) continue;
-                if (p >= 0 || sl >= mp) {
-                    undecided = true;  // a second record holding x, or x beyond the monotone prefix
-                } else {
-                    p = (int)sl;
-                    si.okey = ((uint64_t)w0.y << 32) | w0.x;
-                    si.meta = ((uint64_t)w0.w << 32) | w0.z;
-                    si.next = w1.x;
-                    si.image = w1.y;
-                }
-            }
-            uint32_t img = 0xFFFFFFFFu;
-            uint8_t st = kFirstUndecided;
-            if (!undecided && p >= 0) {
-                uint8_t sv;
-                const uint32_t im = scan_visible(t, si, rid, sv);
-                if (sv == ST_LATEST || sv == ST_OLD) {
-                    img = im;
-                    st = sv;
-                }
-            }
-            img_out[i] = img;
-            st_out[i] = st;
         }
         __builtin_amdgcn_wave_barrier();  // s_cand is rewritten by the next chunk
     }
@@ -2917,41 +1910,34 @@ hipError_t launch_resolve(const DevTable &t, const uint64_t *keys, const uint16_
     return hipGetLastError();
 }
 
+constexpr uint64_t kSmallBelow = 16384;  // 64-probe chunks: about the waves the chip holds at once
+
 hipError_t launch_probe(const DevTable &t, const uint64_t *keys, const uint16_t *lens, const uint32_t *rids,
                         const uint32_t *leaf_in, uint64_t n, stage_probe_out_dev *out, uint8_t *recs, hipStream_t s,
                         const ProbeTuning &tune, const uint64_t *d_n, uint64_t shape_n) {
     if (n == 0) return hipSuccess;
-    if (d_n) {  // device-sized batches: the split kernel only (wide keys / large leaves)
-        const bool split_path = (t.key_words > 1 || (t.key_width != 0 && t.cap > 128)) && tune.wide != 1 &&
-                                tune.status_bytes != 16;
-        if (!split_path) return hipErrorInvalidValue;
+    if (d_n) {  // device-sized batches: the wide-key / large-leaf kernels only
+        if (!(t.key_words > 1 || (t.key_width != 0 && t.cap > 128))) return hipErrorInvalidValue;
     }
     const uint64_t chunks = (n + 63) / 64;
     const int blocks = grid_for(chunks, 4, tune.max_blocks > 0 ? tune.max_blocks : 16384);
     const bool var = t.key_width == 0;
     // wide fixed-width keys, and 8-byte keys in leaves above 128 slots (small rows): leaves of
-    // up to 1024 slots, one probe in flight
+    // up to 1024 slots -- probe_lane_kernel for leaves of up to 256 slots, probe_split_kernel
+    // above (in 16-probe wave chunks when 64-probe ones cannot fill the chip).  Retired (DESIGN
+    // §4): probe_kernel's one-probe-in-flight form and the split kernel for every leaf size.
     if (t.key_words > 1 || (!var && t.cap > 128)) {
         // launch shape from the expected size (a device-sized batch's hint), the grid from n
         const uint64_t sn = d_n && shape_n ? std::min(shape_n, n) : n;
-        const bool small = (sn + 63) / 64 < (uint64_t)tune.small_below;  // fewer 64-probe chunks than the chip holds waves
+        const bool small = (sn + 63) / 64 < (uint64_t)kSmallBelow;  // fewer 64-probe chunks than the chip holds waves
         const int wblocks = small ? grid_for((sn + 15) / 16, 4, tune.max_blocks > 0 ? tune.max_blocks : 16384) : blocks;
-        // default: probe_lane_kernel for leaves of up to 256 slots, probe_split_kernel above;
-        // STAGE_PROBE_WIDE=1: probe_kernel's one-probe-in-flight form; =3: probe_split_kernel always
-        const bool split = tune.wide != 1 && tune.status_bytes != 16;
 #define STAGE_PROBE_W(S, KW)                                                                                  \
-    if (tune.wide != 3 && S <= 4 && split)                                                                    \
+    if (S <= 4)                                                                                               \
         probe_lane_kernel<(S <= 4 ? S : 4), KW><<<blocks, 256, 0, s>>>(t, keys, rids, leaf_in, n, out, recs, d_n); \
-    else if (split && small)                                                                                  \
-        probe_split_kernel<S, KW, 16><<<wblocks, 256, 0, s>>>(t, keys, rids, leaf_in, n, out, recs, d_n);      \
-    else if (split)                                                                                           \
-        probe_split_kernel<S, KW, 64><<<blocks, 256, 0, s>>>(t, keys, rids, leaf_in, n, out, recs, d_n);       \
     else if (small)                                                                                           \
-        probe_kernel<false, S, 1, 1, KW, 16><<<wblocks, 256, 0, s>>>(t, keys, lens, rids, leaf_in, n, out, recs, \
-                                                                     nullptr, nullptr);                        \
+        probe_split_kernel<S, KW, 16><<<wblocks, 256, 0, s>>>(t, keys, rids, leaf_in, n, out, recs, d_n);      \
     else                                                                                                      \
-        probe_kernel<false, S, 1, 1, KW><<<blocks, 256, 0, s>>>(t, keys, lens, rids, leaf_in, n, out, recs,      \
-                                                                nullptr, nullptr)
+        probe_split_kernel<S, KW, 64><<<blocks, 256, 0, s>>>(t, keys, rids, leaf_in, n, out, recs, d_n)
 #define STAGE_PROBE_WK(KW)                      \
     switch (t.cap / 64) {                       \
         case 1: STAGE_PROBE_W(1, KW); break;    \
@@ -3265,11 +2251,7 @@ hipError_t launch_scan(const DevTable &t, const uint64_t *keys, const uint16_t *
     const int blocks = grid_for(n, 4, tune.max_blocks > 0 ? tune.max_blocks : 16384);
     if (row_status) {  // IndexScanExecutor range branch: per-record visibility
         launch_scan_r<4, true>(t, keys, lens, n, scan_size, counts, recs, rids, row_status, s, blocks);
-    } else if (tune.rows == 8) {
-        launch_scan_r<8, false>(t, keys, lens, n, scan_size, counts, recs, nullptr, nullptr, s, blocks);
-    } else if (tune.rows == 2) {
-        launch_scan_r<2, false>(t, keys, lens, n, scan_size, counts, recs, nullptr, nullptr, s, blocks);
-    } else {
+    } else {  // 4 rows in flight per wave (2 and 8 measured no faster)
         launch_scan_r<4, false>(t, keys, lens, n, scan_size, counts, recs, nullptr, nullptr, s, blocks);
     }
     return hipGetLastError();
@@ -3281,75 +2263,16 @@ hipError_t launch_scan_first(const DevTable &t, const uint64_t *keys, uint64_t n
     if (n == 0) return hipSuccess;
     if (t.key_width == 0 || scan_size == 0 || scan_size > 63) return hipErrorInvalidValue;
     const int blocks = grid_for((n + kFirstChunk - 1) / kFirstChunk, 4, tune.max_blocks > 0 ? tune.max_blocks : 16384);
-    // default (STAGE_SL_SCANS unset or 0): scan_first_split_kernel + scan_first_rest_kernel.
-    // Variants: -8 / -9 scan_first_mono_kernel at 8 waves/SIMD / uncapped
-    // (round 3: a third of the instructions and of the HBM bytes, but per-lane scattered key
-    // loads -- no faster); -4 / -10 split at 7 / 6 waves/SIMD; -5 / -3 / -1 scan_first_fast_kernel with the
-    // prefetch at 8 / 7 / 6 waves, -2 without it; -6 / -7 scan_first_seg_kernel (4 / 2 scans per
-    // pass); 1 the general single-scan kernel; 2 / 4 NS scans per wave in lockstep; -11
-    // scan_first_probe_kernel (the start key's exact record as a point probe), then the split
-    // kernel on the chunks it left undecided, then the rest kernel
-    const int ns = tune.first_scans;
-    const uint64_t pchunks = (n + 63) / 64;
-    const bool psmall = pchunks < 16384;  // as launch_probe: 16-scan chunks when 64-scan ones cannot fill the chip
-    const int pblocks = psmall ? grid_for((n + 15) / 16, 4, tune.max_blocks > 0 ? tune.max_blocks : 16384)
-                               : grid_for(pchunks, 4, tune.max_blocks > 0 ? tune.max_blocks : 16384);
+    // scan_first_split_kernel decides the scans whose start leaf's first visit does, then
+    // scan_first_rest_kernel runs the general loop for the rest.  Retired variants (measured
+    // no faster): a single-scan kernel, NS scans in lockstep, the prefetching
+    // "fast" kernel, the lane-parallel "mono" kernel, segmented stage A, a point-probe first
+    // pass, the split kernel at 6 / 7 waves per SIMD.
 #define STAGE_FIRST(S, KW)                                                                                  \
-    if (ns == -11) {                                                                                        \
-        if (psmall)                                                                                         \
-            scan_first_probe_kernel<S, KW, 16><<<pblocks, 256, 0, s>>>(t, keys, n, rids, img_out, st_out);   \
-        else                                                                                                \
-            scan_first_probe_kernel<S, KW, 64><<<pblocks, 256, 0, s>>>(t, keys, n, rids, img_out, st_out);   \
-        scan_first_split_kernel<S, KW, 8, true><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words,   \
-                                                                       img_out, st_out);                    \
-        scan_first_rest_kernel<S, KW><<<grid_for((n + 63) / 64, 4, 4096), 256, 0, s>>>(t, keys, n, scan_size,  \
-                                                                                    rids, words, img_out,   \
-                                                                                    st_out);                \
-    } else if (ns == 0 || ns == -4 || ns == -6 || ns == -7 || ns == -8 || ns == -9 || ns == -10) {                 \
-        if (ns == -8)                                                                                       \
-            scan_first_mono_kernel<S, KW, 8><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words, img_out, \
-                                                                    st_out);                                \
-        else if (ns == -9)                                                                                  \
-            scan_first_mono_kernel<S, KW, 1><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words,      \
-                                                                    img_out, st_out);                       \
-        else if (ns == -6 && scan_size <= 15)                                                               \
-            scan_first_seg_kernel<S, KW, 4, 4><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words,    \
-                                                                      img_out, st_out);                     \
-        else if (ns == -7 && scan_size <= 31)                                                               \
-            scan_first_seg_kernel<S, KW, 1, 2><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words,    \
-                                                                      img_out, st_out);                     \
-        else if (ns == -10)                                                                                 \
-            scan_first_split_kernel<S, KW, 6><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words,     \
-                                                                     img_out, st_out);                      \
-        else if (ns != -4)                                                                                  \
-            scan_first_split_kernel<S, KW, 8><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words,     \
-                                                                     img_out, st_out);                      \
-        else                                                                                                \
-            scan_first_split_kernel<S, KW, 7><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words,     \
-                                                                     img_out, st_out);                      \
-        scan_first_rest_kernel<S, KW><<<grid_for((n + 63) / 64, 4, 4096), 256, 0, s>>>(t, keys, n, scan_size,  \
-                                                                                    rids, words, img_out,   \
-                                                                                    st_out);                \
-    } else if (ns == -5)                                                                                    \
-        scan_first_fast_kernel<S, KW, 8, true><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words,    \
-                                                                      img_out, st_out);                     \
-    else if (ns == -1)                                                                                      \
-        scan_first_fast_kernel<S, KW, 1, true><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words,    \
-                                                                      img_out, st_out);                     \
-    else if (ns == -2)                                                                                      \
-        scan_first_fast_kernel<S, KW, 8, false><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words,   \
-                                                                       img_out, st_out);                    \
-    else if (ns < 0)                                                                                        \
-        scan_first_fast_kernel<S, KW, 7, true><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words,    \
-                                                                      img_out, st_out);                     \
-    else if (ns == 1)                                                                                       \
-        scan_first_kernel<S, KW><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words, img_out, st_out); \
-    else if (ns == 4)                                                                                       \
-        scan_first_multi_kernel<S, KW, 4><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words, img_out,   \
-                                                                 st_out);                                   \
-    else                                                                                                    \
-        scan_first_multi_kernel<S, KW, 2><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words, img_out,   \
-                                                                 st_out)
+    scan_first_split_kernel<S, KW, 8><<<blocks, 256, 0, s>>>(t, keys, n, scan_size, rids, words, img_out,    \
+                                                             st_out);                                       \
+    scan_first_rest_kernel<S, KW><<<grid_for((n + 63) / 64, 4, 4096), 256, 0, s>>>(t, keys, n, scan_size, rids, \
+                                                                                words, img_out, st_out)
 #define STAGE_FIRST_K(KW)                      \
     switch (t.cap / 64) {                      \
         case 1: STAGE_FIRST(1, KW); break;     \

@@ -299,8 +299,7 @@ __global__ void wp_speculate(WpArgs a, WpCls k, DevTable t, uint8_t *__restrict_
 // loads independent), takes the first success in batch order and restarts behind it: a hot
 // key's long run of NotNeededUpdate / DIRTY ops goes 512 ops per pass.
 constexpr int kFinishChunks = 8;
-constexpr uint32_t kBigGroup = 2048;  // ops from the first failure on: a workgroup finishes it (wp_finish_big)
-constexpr uint32_t kJumpFrom = 128;   // ... by pointer jumping (wp_jump_*; 128 from the r05 sweep)
+constexpr uint32_t kJumpFrom = 128;  // ops from the first failure on: pointer jumping (wp_jump_*; 128 from the r05 sweep)
 // Groups with at least big_from ops from their first failure on go to `list` instead (one
 // atomic per big group; their finishing kernels follow).
 __global__ __launch_bounds__(256) void wp_finish_groups(WpArgs a, WpCls kc, DevTable t, uint8_t *__restrict__ rcs,
@@ -387,8 +386,8 @@ __global__ __launch_bounds__(256) void wp_finish_groups(WpArgs a, WpCls kc, DevT
     }
 }
 
-// step 3b for big groups, the walk (round 4; now the fallback of wp_finish_jump): one
-// 1024-thread workgroup per group, 16 waves x kFinishChunks x 64 = 8192 ops evaluated against
+// step 3b for big groups, the walk (round 4; now the fallback of the pointer jumping when a
+// candidate's writer is older than the commit): one 1024-thread workgroup per group, 16 waves x kFinishChunks x 64 = 8192 ops evaluated against
 // the last success per pass, the first success in batch order found across the waves through
 // LDS.  Serial in the group's failures: ~700 passes for a Zipf-0.99 hot key on RunMixed's stream.
 __device__ void finish_big_walk(const WpArgs &a, const WpCls &kc, const DevTable &t, uint8_t *__restrict__ rcs,
@@ -462,7 +461,7 @@ __device__ void finish_big_walk(const WpArgs &a, const WpCls &kc, const DevTable
 // p's delta, else p+1 -- provided its writer is not older than p's commit id.  When that
 // writer is older (NotNeededUpdate by cstamp) the candidate fails and the chain is not known
 // locally: the group is finished by finish_big_walk instead (never on RunMixed's stream, whose
-// writer ids grow with the batch).  One 1024-thread workgroup per group:
+// writer ids grow with the batch).  Per group:
 //   A. per 64-op chunk (a wave), nxt of every op, then exit(p) (the first chain node at or past
 //      the chunk's end) and mask(p) (the chain's nodes inside the chunk) by 6 doubling steps
 //      over the wave's lanes (shuffles, no memory);
@@ -472,167 +471,15 @@ __device__ void finish_big_walk(const WpArgs &a, const WpCls &kc, const DevTable
 //      before it (wp_eval) and its prev.
 // Scratch (position-indexed, disjoint between groups): jx (exit), jm (mask), ci (entry | carry).
 constexpr uint32_t kNone = 0xFFFFFFFFu;
-__global__ __launch_bounds__(1024) void wp_finish_jump(WpArgs a, WpCls kc, DevTable t, uint8_t *__restrict__ rcs,
-                                                       uint8_t *__restrict__ succ, int32_t *__restrict__ prev,
-                                                       const uint32_t *__restrict__ first_fail,
-                                                       const uint32_t *__restrict__ gend,
-                                                       const uint32_t *__restrict__ list,
-                                                       const uint32_t *__restrict__ count,
-                                                       const uint32_t *__restrict__ cfirst, uint32_t *__restrict__ jx,
-                                                       uint64_t *__restrict__ jm, uint64_t *__restrict__ ci) {
-    __shared__ uint64_t s_first[16];
-    __shared__ uint32_t s_unres;
-    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint32_t nbig = *count;
-    for (uint32_t i = blockIdx.x; i < nbig; i += gridDim.x) {
-        const uint64_t g = list[i];
-        const uint64_t l = a.loc[g], end = gend[g];
-        const SlotInfo base = t.slot[l];
-        const uint64_t f = first_fail[g];
-        // the chain's first node: f - 1 (a success of the leading run), or when the group's head
-        // already failed the first op that succeeds against the epoch-start state
-        uint64_t start;
-        if (f > g) {
-            start = f - 1;
-        } else {
-            start = ~0ull;
-            for (uint64_t done = g; done < end && start == ~0ull; done += 1024) {
-                const uint64_t q = done + (uint64_t)wv * 64 + lane;
-                const uint8_t r = q < end ? wp_eval(a, kc, t, q, g, -1, base) : (uint8_t)0xFF;
-                uint64_t wf = r == STAGE_RC_OK ? q : ~0ull;
-                for (int o = 32; o > 0; o >>= 1) {
-                    const uint64_t x = __shfl_xor(wf, o, 64);
-                    wf = x < wf ? x : wf;
-                }
-                __syncthreads();
-                if (lane == 0) s_first[wv] = wf;
-                __syncthreads();
-                uint64_t bf = ~0ull;
-#pragma unroll
-                for (int w = 0; w < 16; ++w) bf = s_first[w] < bf ? s_first[w] : bf;
-                if (q < end && q <= bf) {  // up to the first success: evaluated against the start state
-                    rcs[q] = r;
-                    succ[q] = q == bf;
-                    prev[q] = -1;
-                }
-                start = bf;
-            }
-            if (start == ~0ull) continue;  // nothing succeeds: every op was evaluated above
-        }
-        // A. nxt, exit and mask of every op from `start` on
-        if (threadIdx.x == 0) s_unres = 0;
-        __syncthreads();
-        const uint64_t nch = (end - start + 63) / 64;
-        for (uint64_t c = wv; c < nch; c += 16) {
-            const uint64_t cb = start + 64 * c;
-            const uint64_t p = cb + lane;
-            uint32_t J = kNone;
-            uint64_t M = 0;
-            if (p < end) {
-                M = 1ull << lane;
-                const uint32_t cp = commit_of(a, a.op[p]);
-                if (cp != 0) {  // an uncommitted success leaves every later op DIRTY
-                    const uint32_t cl = kc.cls[p];
-                    const uint64_t cand = (p + 1 < end && kc.cls[p + 1] == cl) ? cfirst[cl + 1] : p + 1;
-                    if (cand < end) {
-                        if (a.writer[a.op[cand]] >= cp) J = (uint32_t)cand;
-                        else s_unres = 1;  // (benign race: every writer stores 1)
-                    }
-                }
-            }
-            const uint32_t cend = (uint32_t)(cb + 64);
-#pragma unroll
-            for (int r = 0; r < 6; ++r) {  // doubling inside the chunk: J = f^(2^r)(p), M = its path
-                const bool in = J < cend;
-                const int src = in ? (int)(J - (uint32_t)cb) : (int)lane;
-                const uint32_t Jn = (uint32_t)__shfl((int)J, src, 64);
-                const uint64_t Mn = __shfl(M, src, 64);
-                if (in) {
-                    J = Jn;
-                    M |= Mn;
-                }
-            }
-            if (p < end) {
-                jx[p] = J;
-                jm[p] = M;
-            }
-        }
-        __syncthreads();
-        if (s_unres) {  // a candidate's writer is older than the commit: walk the group instead
-            finish_big_walk(a, kc, t, rcs, succ, prev, g, end, f, base, s_first);
-            __syncthreads();
-            continue;
-        }
-        // B. the chain, chunk to chunk (wave 0; the loop is wave-uniform).  The chunks' exits and
-        // masks come in kPre chunks at a time, a lane per op, all loads in flight together (they
-        // do not depend on where the chain enters); the chain then picks its entry's values by
-        // readlane -- one load round trip per kPre chunks instead of one per chunk
-        if (wv == 0) {
-            constexpr int kPre = 16;
-            uint64_t e = start;
-            int64_t carry = f > g ? (start > g ? (int64_t)start - 1 : -1) : -1;
-            for (uint64_t c0 = 0; c0 < nch; c0 += kPre) {
-                uint32_t xr[kPre];
-                uint64_t mr[kPre];
-#pragma unroll
-                for (int k = 0; k < kPre; ++k) {
-                    const uint64_t p = start + 64 * (c0 + k) + lane;
-                    const bool ok = c0 + k < nch && p < end;
-                    xr[k] = ok ? jx[p] : kNone;
-                    mr[k] = ok ? jm[p] : 0ull;
-                }
-#pragma unroll
-                for (int k = 0; k < kPre; ++k) {
-                    if (c0 + k >= nch) break;
-                    const uint64_t cb = start + 64 * (c0 + k);
-                    uint64_t entry = kNone;
-                    int64_t next_carry = carry;
-                    if (e != kNone && e < cb + 64) {  // wave-uniform
-                        entry = e;
-                        const int el = (int)(e - cb);
-                        const uint64_t m = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(mr[k] >> 32), el)
-                                            << 32) |
-                                           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mr[k], el);
-                        next_carry = (int64_t)(cb + 63 - __builtin_clzll(m));
-                        e = (uint32_t)__builtin_amdgcn_readlane((int)xr[k], el);
-                    }
-                    if (lane == 0) ci[cb] = entry | ((uint64_t)(uint32_t)(int32_t)carry << 32);
-                    carry = next_carry;
-                }
-            }
-        }
-        __syncthreads();
-        // C. return codes
-        for (uint64_t c = wv; c < nch; c += 16) {
-            const uint64_t cb = start + 64 * c;
-            const uint64_t q = cb + lane;
-            const uint64_t info = ci[cb];
-            const uint32_t entry = (uint32_t)info;
-            const int32_t carry = (int32_t)(uint32_t)(info >> 32);
-            const uint64_t M = entry != kNone ? jm[entry] : 0ull;
-            if (q < end) {
-                const bool s = (M >> lane) & 1ull;
-                const uint64_t below = M & (lane ? ~0ull >> (64 - lane) : 0ull);
-                const int64_t ps = below ? (int64_t)(cb + 63 - __builtin_clzll(below)) : (int64_t)carry;
-                succ[q] = s;
-                prev[q] = (int32_t)ps;
-                rcs[q] = s ? (uint8_t)STAGE_RC_OK : wp_eval(a, kc, t, q, g, ps, base);
-            }
-        }
-        __syncthreads();
-    }
-}
-
-// wp_finish_jump with its per-op phases grid-wide (STAGE_WP_FINISH unset; "jump1": the kernel
-// above).  In wp_finish_jump a group's phases A (nxt / exit / mask) and C (return codes) run
-// inside its one workgroup, a 64-op chunk per wave and pass: a Zipf-0.99 hot key (~44 K ops)
-// takes ~43 dependent passes per wave in each.  Here A and C run over every big group at once, a
-// wave per absolute 64-position chunk (wp_jump_links, wp_jump_codes), and the per-group workgroup
-// keeps the start search and the chain walk B (wp_jump_chain).  A chunk may hold the end of one
-// group and the start of the next: the chain's per-chunk record is keyed by max(chunk start,
-// group head), distinct for the two.  Phase A starts at the chain's earliest possible node (f - 1
-// when the head succeeded, else the head), so an unresolved candidate before the actual start
-// (the head-failed case) only sends the group to the walk, which is exact either way.
+// The phases run over every big group at once where they are per op: A and C a wave per absolute
+// 64-position chunk (wp_jump_links, wp_jump_codes), and the per-group workgroup keeps the start
+// search and the chain walk B (wp_jump_chain).  (Round 5 first ran A and C inside the group's
+// workgroup, a 64-op chunk per wave and pass: a Zipf-0.99 hot key (~44 K ops) took ~43 dependent
+// passes per wave in each -- retired)  A chunk may hold the end of one group and the
+// start of the next: the chain's per-chunk record is keyed by max(chunk start, group head),
+// distinct for the two.  Phase A starts at the chain's earliest possible node (f - 1 when the head
+// succeeded, else the head), so an unresolved candidate before the actual start (the head-failed
+// case) only sends the group to the walk, which is exact either way.
 __device__ __forceinline__ bool jump_member(const WpArgs &a, const uint32_t *__restrict__ first_fail,
                                             const uint32_t *__restrict__ gend, uint32_t big_from, uint64_t p,
                                             uint64_t &g, uint64_t &f, uint64_t &end) {
@@ -742,7 +589,7 @@ __global__ __launch_bounds__(1024) void wp_jump_chain(WpArgs a, WpCls kc, DevTab
             __syncthreads();
             continue;
         }
-        // B. the chain, chunk to chunk, as in wp_finish_jump but over absolute chunks, the
+        // B. the chain, chunk to chunk, over absolute chunks, the
         // exits and masks staged through LDS a span of kSpanChunks chunks at a time: waves 1-15
         // fill the next span while wave 0 walks this one (from registers, kPre chunks per LDS
         // batch, by readlane)
@@ -858,21 +705,6 @@ __global__ __launch_bounds__(256) void wp_jump_codes(WpArgs a, WpCls kc, DevTabl
         SlotInfo base{};
         if (ps < 0) base = t.slot[a.loc[g]];  // the epoch-start state matters only against no success
         rcs[p] = wp_eval(a, kc, t, p, g, ps, base);
-    }
-}
-
-__global__ __launch_bounds__(1024) void wp_finish_big(WpArgs a, WpCls kc, DevTable t, uint8_t *__restrict__ rcs,
-                                                      uint8_t *__restrict__ succ, int32_t *__restrict__ prev,
-                                                      const uint32_t *__restrict__ first_fail,
-                                                      const uint32_t *__restrict__ gend,
-                                                      const uint32_t *__restrict__ list,
-                                                      const uint32_t *__restrict__ count) {
-    __shared__ uint64_t s_first[16];
-    const uint32_t nbig = *count;
-    for (uint32_t i = blockIdx.x; i < nbig; i += gridDim.x) {
-        const uint64_t g = list[i];
-        finish_big_walk(a, kc, t, rcs, succ, prev, g, gend[g], first_fail[g], t.slot[a.loc[g]], s_first);
-        __syncthreads();
     }
 }
 
@@ -1116,9 +948,6 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         const auto t0 = clk::now();
         static const auto g0 = t0;  // trace: the first call's start
         auto ms = [&](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
-        // a previous epoch prepared under write-overlap mode 2 and not yet published: publish it
-        // now (in stream order before this epoch)
-        t->flush_publish(s);
         // epoch e uses output buffers e % 2: epoch e - 2's adoption must be done with them
         const uint64_t epoch = ++t->wp_started;
         const int par = (int)(epoch & 1);
@@ -1139,9 +968,6 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
                 t->start_adoption(epoch, [] { throw std::runtime_error("a device write-path epoch failed"); });
             }
         } guard{t, epoch};
-        // STAGE_WP_PIPELINE=0: every epoch waits for the previous one's adoption (A/B of the pipeline)
-        static const bool pipeline = !(std::getenv("STAGE_WP_PIPELINE") && std::getenv("STAGE_WP_PIPELINE")[0] == '0');
-        if (!pipeline) t->settle();
         if (epoch > 2) t->wait_adopted(epoch - 2);
         if (t->adopt_failed.load(std::memory_order_acquire)) t->settle();  // rethrows the adoption's error
         // pending: epoch e - 1 is still being adopted, so the device's append counters are ahead
@@ -1173,17 +999,10 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         const double t_reserve = ms(t0);
         if (t->wp_overlap && !dv.wp_stream) {
             // the overlapped write kernels on a high-priority stream, so their workgroups are
-            // dispatched as the probe's retire instead of after all of them (C3 +1.5-2.5 %;
-            // STAGE_WP_PRIO=0: normal priority)
-            static const bool prio = [] {
-                const char *e = std::getenv("STAGE_WP_PRIO");
-                return !(e && std::atoi(e) == 0);
-            }();
+            // dispatched as the probe's retire instead of after all of them (C3 +1.5-2.5 %)
             int lo = 0, hi = 0;
-            if (prio) hip_check(hipDeviceGetStreamPriorityRange(&lo, &hi), "stream priorities");
-            hip_check(prio ? hipStreamCreateWithPriority(&dv.wp_stream, hipStreamNonBlocking, hi)
-                           : hipStreamCreateWithFlags(&dv.wp_stream, hipStreamNonBlocking),
-                      "write stream");
+            hip_check(hipDeviceGetStreamPriorityRange(&lo, &hi), "stream priorities");
+            hip_check(hipStreamCreateWithPriority(&dv.wp_stream, hipStreamNonBlocking, hi), "write stream");
         }
         for (hipEvent_t *e : {&dv.wp_pub_ev, &dv.wp_pre_ev})
             if (!*e) hip_check(hipEventCreateWithFlags(e, hipEventDisableTiming), "write event");
@@ -1328,30 +1147,16 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         hip_check(hipcub::DeviceScan::InclusiveSum(cub, cb, brk, cls, (int)n, ks), "delta classes");
         const WpCls kc{cls, fpd, wfp, eqw};
         wp_speculate<<<blocks_for(n, 256), 256, 0, ks>>>(a, kc, view, rcs, succ, prev, ff, gend, brk, cfirst);
-        // big failing groups: pointer jumping (STAGE_WP_FINISH=walk: the round-4 walk, for A/B);
-        // groups with at least big_from ops from their first failure on (STAGE_WP_BIG) take it,
-        // smaller ones a wave each (wp_finish_groups)
-        // (STAGE_WP_FINISH=jump1: wp_finish_jump, phases A and C inside the group's workgroup)
-        static const std::string finish_mode = std::getenv("STAGE_WP_FINISH") ? std::getenv("STAGE_WP_FINISH") : "";
-        static const bool walk = finish_mode == "walk", jump1 = finish_mode == "jump1";
-        static const uint32_t big_from = walk ? kBigGroup
-                                              : (std::getenv("STAGE_WP_BIG") ? (uint32_t)std::atoi(std::getenv("STAGE_WP_BIG"))
-                                                                              : kJumpFrom);
+        // big failing groups (at least kJumpFrom ops from their first failure on) by pointer
+        // jumping, smaller ones a wave each (wp_finish_groups)
         // (the big-group count, tot[1]'s low word, was zeroed by wp_keys; tot is rewritten in step 4)
-        wp_finish_groups<<<blocks_for(n, 256), 256, 0, ks>>>(a, kc, view, rcs, succ, prev, ff, gend, big_from, big,
-                                                             (uint32_t *)(tot + 1), walk || jump1 ? nullptr : junr);
-        if (walk) {
-            wp_finish_big<<<256, 1024, 0, ks>>>(a, kc, view, rcs, succ, prev, ff, gend, big, (uint32_t *)(tot + 1));
-        } else if (jump1) {
-            wp_finish_jump<<<256, 1024, 0, ks>>>(a, kc, view, rcs, succ, prev, ff, gend, big, (uint32_t *)(tot + 1),
-                                                 cfirst, jx, jm, ci);
-        } else {
-            wp_jump_links<<<blocks_for(n, 256), 256, 0, ks>>>(a, kc, ff, gend, big_from, cfirst, jx, jm, junr);
-            wp_jump_chain<<<256, 1024, 0, ks>>>(a, kc, view, rcs, succ, prev, ff, gend, big, (uint32_t *)(tot + 1), jx, jm,
-                                                ci, gst, junr);
-            wp_jump_codes<<<blocks_for(n, 256), 256, 0, ks>>>(a, kc, view, rcs, succ, prev, ff, gend, big_from, gst, junr,
-                                                              jm, ci);
-        }
+        wp_finish_groups<<<blocks_for(n, 256), 256, 0, ks>>>(a, kc, view, rcs, succ, prev, ff, gend, kJumpFrom, big,
+                                                             (uint32_t *)(tot + 1), junr);
+        wp_jump_links<<<blocks_for(n, 256), 256, 0, ks>>>(a, kc, ff, gend, kJumpFrom, cfirst, jx, jm, junr);
+        wp_jump_chain<<<256, 1024, 0, ks>>>(a, kc, view, rcs, succ, prev, ff, gend, big, (uint32_t *)(tot + 1), jx, jm, ci,
+                                            gst, junr);
+        wp_jump_codes<<<blocks_for(n, 256), 256, 0, ks>>>(a, kc, view, rcs, succ, prev, ff, gend, kJumpFrom, gst, junr, jm,
+                                                          ci);
         // 4. number
         wp_flags<<<blocks_for(n, 256), 256, 0, ks>>>(a, succ, flags);
         cb = cub_bytes;
@@ -1364,8 +1169,7 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         wp_write<<<wblocks, 256, 0, ks>>>(a, view, (uint8_t *)dv.heap.p, wrec, tot);
         if (ks != s) hip_check(hipEventRecord(dv.wp_pre_ev, ks), "write event");
         // the publish and everything after it (the slot words, the export to the host, the host
-        // table's adoption) -- now, or, under write-overlap mode 2, at the caller's
-        // stage_publish_epoch (or the next call that needs the epoch) on the stream it names
+        // table's adoption)
         auto finish = [=, &h, &dv](hipStream_t s, bool want_n) -> uint64_t {
             if (ks != s) hip_check(hipStreamWaitEvent(s, dv.wp_pre_ev, 0), "publish wait");
             wp_publish<<<blocks_for(n, 256), 256, 0, s>>>(a, (SlotInfo *)dv.slot.p, rcs, succ, prev, ranks, ls, tot, fin,
@@ -1389,8 +1193,8 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
             void *pin_dev = nullptr;
             hip_check(hipHostGetDevicePointer(&pin_dev, pin, 0), "pinned device pointer");
             hip_check(hipStreamWaitEvent(dv.adopt_stream, dv.adopt_ev[par], 0), "export wait");
-            static const int export_blocks = std::getenv("STAGE_WP_EXPORT_BLOCKS") ? std::atoi(std::getenv("STAGE_WP_EXPORT_BLOCKS")) : 32;
-            wp_export<<<export_blocks, 256, 0, dv.adopt_stream>>>(tot, fin, (const CopyHdr *)dv.chdr.p, (const VersionHdr *)dv.vhdr.p,
+            constexpr int kExportBlocks = 32;  // beside the next probe: 32 was the best of the r05 sweep
+            wp_export<<<kExportBlocks, 256, 0, dv.adopt_stream>>>(tot, fin, (const CopyHdr *)dv.chdr.p, (const VersionHdr *)dv.vhdr.p,
                                                         cwriter, (uint8_t *)pin_dev, 64 + bmax, 64 + bmax + bf);
             hip_check(hipGetLastError(), "export");
             hip_check(hipEventRecord(dv.export_ev[par], dv.adopt_stream), "export event");
@@ -1453,19 +1257,6 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
             });
             return ns;
         };
-        if (t->wp_overlap == 2 && !n_ok) {
-            guard.started = true;  // the pending publish carries the epoch from here on
-            t->pending_pub = [t, epoch, finish](hipStream_t ps) {
-                try {
-                    finish(ps, false);
-                } catch (...) {  // the host table missed the epoch: every later call reports it
-                    t->start_adoption(epoch, [] { throw std::runtime_error("a deferred write-path publish failed"); });
-                    throw;
-                }
-            };
-            t->pending_stream = s;
-            return STAGE_OK;
-        }
         const uint64_t ns = finish(s, n_ok != nullptr);
         guard.started = true;
         if (n_ok) *n_ok = ns;

@@ -549,13 +549,8 @@ class Table:
 
     def set_write_overlap(self, on):
         """stage_set_write_overlap: a device write-path epoch's kernels up to its publish run beside
-        the caller's later work (inputs must be complete when update_batch_device is called);
-        2 = deferred publish (publish_epoch)."""
+        the caller's later work (inputs must be complete when update_batch_device is called)."""
         check(lib().stage_set_write_overlap(self.h, int(on)), "set_write_overlap")
-
-    def publish_epoch(self, stream=None):
-        """stage_publish_epoch: publish the epoch write-overlap mode 2 left prepared (on `stream`)."""
-        check(lib().stage_publish_epoch(self.h, stream), "publish_epoch")
 
     def set_output_layout(self, row_stride=0, status_bytes=32):
         """stage_set_output_layout: probe row stride (0 = default) and 32- or 16-B status records."""

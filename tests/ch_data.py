@@ -114,15 +114,15 @@ class ChTables:
                                    self.d_map.ptr, target, read_id, commit_id, out=self._out)
         return recs.copy(), ab
 
-    def query2_batch(self, read_ids, target=3, out=None):
+    def query2_batch(self, read_ids, target=3, out=None, stream=None):
         t = self.tables
         return stage.ch_query2_batch(t["region"], t["nation"], t["supplier"], t["item"], t["stock"], self.map_off,
-                                     self.d_map.ptr, read_ids, target, out=out)
+                                     self.d_map.ptr, read_ids, target, out=out, stream=stream)
 
-    def query2_batch_async(self, read_ids, out, slot=0, target=3):
+    def query2_batch_async(self, read_ids, out, slot=0, target=3, stream=None):
         t = self.tables
         return stage.ch_query2_batch_async(t["region"], t["nation"], t["supplier"], t["item"], t["stock"],
-                                           self.map_off, self.d_map.ptr, read_ids, out, slot, target)
+                                           self.map_off, self.d_map.ptr, read_ids, out, slot, target, stream=stream)
 
     def query2_oracle(self, target=3, read_id=0xFFFFFFFE):
         import ctypes

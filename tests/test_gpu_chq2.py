@@ -162,3 +162,27 @@ def test_q2_batch_async_two_in_flight(ch):
         ch.query2_batch_async(ra, np.zeros((ra.size, 1 << 14), stage.Q2_REC_DTYPE), 0, 3)
     with pytest.raises(stage.StageError):
         stage.table.Q2Batch(ch.tables["stock"], 1, ob, rb.size).wait()
+
+
+def test_q2_batches_on_different_streams(ch):
+    """The two async slots and a synchronous batch share the tables' device scratch:
+    batches enqueued on different streams while another is in flight wait for it on the device,
+    so each still equals its batch run alone."""
+    ra = np.array([10, 0xFFFFFFFE, 25], np.uint32)
+    rb = np.array([40, 3, 0xFFFFFFFE, 60], np.uint32)
+    rc = np.array([25, 0xFFFFFFFE], np.uint32)
+    ref = {k: ch.query2_batch(r, t) for k, (r, t) in {"a": (ra, 3), "b": (rb, 0), "c": (rc, 1)}.items()}
+    s1, s2, s3 = stage.Stream(), stage.Stream(), stage.Stream()
+    oa = stage.pinned_empty((ra.size, 1 << 14), stage.Q2_REC_DTYPE)
+    ob = stage.pinned_empty((rb.size, 1 << 14), stage.Q2_REC_DTYPE)
+    for rep in range(3):
+        ja = ch.query2_batch_async(ra, oa, 0, 3, stream=s1.ptr)
+        jb = ch.query2_batch_async(rb, ob, 1, 0, stream=s2.ptr)
+        got_c = ch.query2_batch(rc, 1, stream=s3.ptr)  # synchronous, a third stream, both slots busy
+        got = {"b": jb.wait(), "a": ja.wait(), "c": got_c}
+        for k, (recs, ab) in got.items():
+            srecs, sab = ref[k]
+            assert (ab == sab).all() and recs.shape == srecs.shape, (rep, k)
+            for q in range(ab.size):
+                if not ab[q]:
+                    same(recs[q], srecs[q])

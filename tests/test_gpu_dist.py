@@ -291,3 +291,33 @@ def test_narrow_coalescing_sort(gpu, bits, wide):
         for t in tabs:
             stage.set_shard_dedupe(t, -1)
             stage.set_shard_key_bits(t, 0)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_peer_reply_row_stride_raised_between_calls(gpu, world):
+    """STAGE_REPLY_PEER row buffers are sized in rows of the call's stride: raising the output
+    stride (stage_set_output_layout) between peer calls re-plans and reallocates every shard's
+    buffers, so the owners' rows never land past their end.  Each call also rewrites
+    the same buffer parity with different rows (the keys change), so a stale row would show."""
+    n = 200_000
+    keys = np.arange(n, dtype=np.uint64)
+    tabs, h = shard_tables(keys, world)
+    full = stage.Table(key_width=8)
+    full.load_keys(keys, 8, mode=1)
+    for t in tabs + [full]:
+        t.sync()
+    rng = np.random.default_rng(100 + world)
+    for call, stride in enumerate((0, 0, 1152, 1152, 1008, 2048)):
+        for t in tabs + [full]:
+            t.set_output_layout(stride, 32)
+        per_keys = [rng.integers(0, n + 5000, int(rng.integers(20_000, 60_000))).astype(np.uint64)
+                    for _ in range(world)]
+        res = stage.probe_sharded_loopback(tabs, per_keys, None, reply=stage.REPLY_PEER)
+        for r in range(world):
+            out, rows = res[r]
+            ref_out, ref_rows = full.probe(per_keys[r])
+            assert rows.shape[1] == full.stride == (stride or 1024)
+            assert (out["status"] == ref_out["status"]).all(), (call, r)
+            assert (rows == ref_rows).all(), (call, r, stride)
+    for t in tabs + [full]:
+        t.set_output_layout(0, 32)

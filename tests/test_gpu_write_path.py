@@ -386,17 +386,20 @@ def test_write_overlap_epochs_with_probes_between(gpu):
     assert_same_images(tab, orc)
 
 
-def test_deferred_publish_probes_before_and_after(gpu):
-    """stage_set_write_overlap(2): stage_update_batch_device prepares epoch e and returns; a probe
-    enqueued before stage_publish_epoch reads the state after epoch e - 1 (the prepared epoch is
-    invisible), one enqueued after it the state after epoch e -- the order the YCSB-B driver uses
-    (prepare e + 1, probe e, publish e + 1).  Codes, statuses and rows equal the oracle's; a host
-    write between epochs settles the pending publish first; the host table agrees at the end."""
+def test_overlap_epochs_reuse_input_buffers(gpu):
+    """Write-overlap mode 1 with ONE set of device input buffers (keys, deltas, writer and commit
+    ids) for every epoch: each next epoch's inputs are copied into them on the caller's stream
+    right behind the call -- after the epoch's publish in stream order, which is the header's
+    contract (inputs unmodified until the work enqueued behind the call has run; ADVICE r05 on
+    the retired deferred-publish mode) -- and probes enqueued between epochs see each epoch.
+    Codes, statuses and rows equal the oracle's; the host table agrees at the end."""
     n = 30000
     tab = stage.Table(key_width=8)
     tab.load_ycsb(0, n, 8, mode=1)
     tab.sync()
-    tab.set_write_overlap(2)
+    tab.set_write_overlap(1)
+    with pytest.raises(stage.StageError):
+        tab.set_write_overlap(2)  # retired
     orc = O.OracleTree()
     orc.load_ycsb(0, n, 8, 1)
     rng = np.random.default_rng(37)
@@ -404,6 +407,15 @@ def test_deferred_publish_probes_before_and_after(gpu):
     base, hot = np.arange(0, n, 2, dtype=np.uint64), np.arange(0, 40, dtype=np.uint64)
     counter, epochs = 10, []
     probe_keys = np.concatenate([hot, rng.integers(0, n + 50, 5000)]).astype(np.uint64)
+    cap = 60000
+    dk, dd, dw, dc = (stage.DeviceBuffer(cap * w) for w in (8, 24, 4, 4))
+    L = stage.lib()
+
+    def refill(keys, deltas, wid, cid):  # stream-ordered H2D into the shared input buffers
+        for buf, x in ((dk, keys), (dd, deltas.reshape(-1)), (dw, wid), (dc, cid)):
+            x = np.ascontiguousarray(x)
+            check(L.stage_memcpy_h2d(buf.ptr, x.ctypes.data, x.nbytes, s.ptr), "h2d")
+        return x
 
     def enqueue_probe():
         rids = np.where(rng.random(probe_keys.size) < 0.5, rng.integers(0, counter, probe_keys.size),
@@ -413,25 +425,23 @@ def test_deferred_publish_probes_before_and_after(gpu):
         tab.probe_device(pk.ptr, probe_keys.size, pout.ptr, prow.ptr, d_read_ids=pr.ptr, stream=s.ptr)
         return rids, (pk, pr), pout, prow
 
-    for e, m in enumerate((3000, 800, 9000, 60000, 1500, 4000, 2)):
-        keys, deltas, wid, cid = epoch_ops(rng, base, hot, m, counter)
+    sizes = (3000, 800, 9000, 60000, 1500, 4000, 2)
+    ops = []
+    for m in sizes:
+        ops.append(epoch_ops(rng, base, hot, m, counter))
         counter += 2 * m + 2
-        ep_host = None
-        if e == 5:  # a host-side write between epochs (nothing pending: the last epoch was published)
-            s.sync()
-            k0 = int(hot[3])
-            dd = rng.integers(0, 256, 8, dtype=np.uint8)
-            ep_host = (k0, dd, counter, tab.update(k0, 3, dd, counter))
-            counter += 2
-            tab.sync()
-        d = [stage.DeviceBuffer.from_numpy(x) for x in (keys, deltas.reshape(-1), wid, cid)]
+    host_src = [refill(*ops[0])]  # the first epoch's inputs; the arrays stay alive until s is done
+    s.sync()
+    for e, m in enumerate(sizes):
+        keys, deltas, wid, cid = ops[e]
         rcb = stage.DeviceBuffer(m)
-        check(stage.lib().stage_update_batch_device(tab.h, d[0].ptr, None, m, 16, d[1].ptr, 24, d[2].ptr, d[3].ptr,
-                                                    None, rcb.ptr, None, s.ptr), "update_batch_device")
-        before = enqueue_probe()  # the prepared epoch is not visible yet
-        tab.publish_epoch(s.ptr)
+        check(L.stage_update_batch_device(tab.h, dk.ptr, None, m, 16, dd.ptr, 24, dw.ptr, dc.ptr, None, rcb.ptr,
+                                          None, s.ptr), "update_batch_device")
         after = enqueue_probe()
-        epochs.append((keys, deltas, wid, cid, rcb, d, ep_host, before, after))
+        if e + 1 < len(sizes):
+            host_src.append(refill(*ops[e + 1]))  # behind the epoch's publish and probe on s
+            s.sync()  # the next call's inputs are complete when it is made
+        epochs.append((keys, deltas, wid, cid, rcb, after))
     s.sync()
 
     def compare(probe):
@@ -444,11 +454,7 @@ def test_deferred_publish_probes_before_and_after(gpu):
             assert badf.size == 0, (f, badf[:5], out[f][badf[:5]], o_out[f][badf[:5]])
         assert not (rows[:, :orc.row] != o_rec).any(axis=1).any()
 
-    for keys, deltas, wid, cid, rcb, _, ep_host, before, after in epochs:
-        if ep_host is not None:
-            k0, dd, c0, rc0 = ep_host
-            assert orc.update(k0, 8, 3, dd.tobytes(), c0) == rc0
-        compare(before)
+    for keys, deltas, wid, cid, rcb, after in epochs:
         exp = oracle_epoch(orc, keys, 8, 16, deltas, wid, cid)
         rc = rcb.to_numpy(np.uint8, keys.size)
         bad = np.nonzero(rc != exp)[0]
