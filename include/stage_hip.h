@@ -516,6 +516,14 @@ int stage_ch_query2_batch_async(stage_table *region, stage_table *nation, stage_
                                 const uint64_t *d_map_keys, int32_t target_region, const uint32_t *read_ids,
                                 uint32_t nq, stage_q2_rec *out, uint64_t max_per_query, int slot, void *stream);
 int stage_ch_query2_wait(stage_table *stock, int slot, uint64_t *n_out, int32_t *aborted);
+/* self-check of the multi-table operations' device scratch plans, no device work: op 0 = CH-Q2
+ * (users: the batch buffers, the REGION scan rows, the NATION scan rows, the stock-update
+ * staging; roles 0..4 = region, nation, supplier, item, stock), op 1 = TPC-C stock-level (its
+ * batch buffers, role 0 = district).  roles NULL: the library's own plan; else n roles, one per
+ * user (e.g. a past layout).  STAGE_OK when no two users share one table's per-call scratch,
+ * STAGE_E_ARG naming them otherwise.  Every CH-Q2 call runs the same check on the tables it is
+ * given and refuses one table passed for two roles whose scratch users would collide. */
+int stage_scratch_plan_check(int op, const int32_t *roles, int n);
 
 /* ---- multi-GPU: hash-sharded probe front-end over RCCL (one process per GPU) ------------
  * stage_comm_unique_id fills 128 bytes on rank 0 (broadcast them out of band);

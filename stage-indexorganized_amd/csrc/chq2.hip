@@ -396,11 +396,29 @@ const uint8_t *scan_rows(stage_table *t, const uint64_t *d_start, uint32_t scan_
 }  // namespace
 }  // namespace stage
 
+// CH-Q2's users of the tables' per-call scratch, by table role (check_scratch_uses)
+enum { kRoleRegion, kRoleNation, kRoleSupplier, kRoleItem, kRoleStock };
+static const stage::ScratchUse kQ2Scratch[] = {{kRoleSupplier, "the CH-Q2 batch buffers"},
+                                               {kRoleRegion, "the REGION scan rows"},
+                                               {kRoleNation, "the NATION scan rows"},
+                                               {kRoleItem, "the stock-update staging"}};
+constexpr int kQ2ScratchUses = (int)(sizeof(kQ2Scratch) / sizeof(kQ2Scratch[0]));
+
 // nq transactions at read ids rq[0..nq): out[q * max_out + k], aborted[q]; commit only for nq == 1
 static int q2_run(stage_table *region, stage_table *nation, stage_table *supplier, stage_table *item,
                   stage_table *stock, const uint32_t *map_off, const uint64_t *d_map_keys, int32_t target_region,
                   const uint32_t *rq, uint32_t nq, uint32_t commit_id, stage_q2_rec *out, uint64_t max_out,
                   uint64_t *n_out, int32_t *aborted, void *stream, int slot = 0, bool async = false) {
+    for (stage_table *t : {region, nation, supplier, item, stock})
+        if (!t) return fail(STAGE_E_ARG, "null table");
+    {
+        const void *roles[] = {region, nation, supplier, item, stock};
+        int rc = guarded([&] {
+            stage::check_scratch_uses(kQ2Scratch, kQ2ScratchUses, roles);
+            return STAGE_OK;
+        });
+        if (rc) return rc;
+    }
     for (stage_table *t : {region, nation, supplier, item, stock}) {
         int rc = need_synced(t);
         if (rc) return rc;
@@ -786,4 +804,23 @@ extern "C" int stage_ch_query2_batch(stage_table *region, stage_table *nation, s
     if (!read_ids || nq > 4096) return fail(STAGE_E_ARG, "read_ids: 1..4096 queries");
     return q2_run(region, nation, supplier, item, stock, map_off, d_map_keys, target_region, read_ids, nq, 0, out,
                   max_per_query, n_out, aborted, stream);
+}
+
+// the multi-table operations' scratch plans (stage_hip.h)
+static const stage::ScratchUse kStockLevelScratch[] = {{0, "the stock-level batch buffers (DISTRICT)"}};
+
+extern "C" int stage_scratch_plan_check(int op, const int32_t *roles, int n) {
+    const stage::ScratchUse *plan;
+    int np;
+    if (op == 0) plan = kQ2Scratch, np = kQ2ScratchUses;
+    else if (op == 1) plan = kStockLevelScratch, np = 1;
+    else return fail(STAGE_E_ARG, "op: 0 = CH-Q2, 1 = stock-level");
+    if (roles && n != np) return fail(STAGE_E_ARG, "roles: one per scratch user of the plan");
+    return guarded([&] {
+        std::vector<stage::ScratchUse> u(plan, plan + np);
+        if (roles)
+            for (int i = 0; i < np; ++i) u[i].role = roles[i];
+        stage::check_scratch_uses(u.data(), np);
+        return STAGE_OK;
+    });
 }

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime_api.h>
 
 #include <cstdint>
+#include <stdexcept>
+#include <string>
 #include <vector>
 
 #include "host_table.hpp"
@@ -66,6 +68,27 @@ void hip_check(hipError_t e, const char *what);
 // next call on the same table).  Stream-ordered pool memory (hipMallocAsync) is not used: on
 // gfx950 its reuse across calls showed stale reads on other XCDs between kernels of a stream.
 uint8_t *scratch_bytes(DeviceImage &d, uint64_t bytes);
+// A multi-table operation's users of the tables' per-call scratch: each table's scratch is one
+// buffer handed out from offset 0 (scratch_bytes), so within one operation it may have one user.
+// Round 5's fault (781d36d) broke exactly that: CH-Q2's batch buffers were carved from NATION's
+// scratch while it held the NATION scan rows.  An operation lists its users by the table role
+// they live in (kQ2Scratch, kStockLevelScratch); check_scratch_uses refuses two users on one
+// table -- the roles' tables when given (a caller passing one table for two roles), else the
+// roles themselves (the plan as written).
+struct ScratchUse {
+    int role;
+    const char *what;
+};
+inline void check_scratch_uses(const ScratchUse *u, int n, const void *const *tables = nullptr) {
+    for (int i = 0; i < n; ++i)
+        for (int j = i + 1; j < n; ++j) {
+            const bool same = tables ? tables[u[i].role] == tables[u[j].role] : u[i].role == u[j].role;
+            if (same)
+                throw std::invalid_argument(std::string("scratch alias: ") + u[i].what + " and " + u[j].what +
+                                            " would share one table's per-call scratch");
+        }
+}
+
 // the same for the device write path alone (write_path.hip)
 uint8_t *wp_scratch_bytes(DeviceImage &d, uint64_t bytes);
 // pinned host buffer `k` (0/1) of at least `bytes` (grown with hipHostMalloc; reused by later calls)

@@ -83,6 +83,7 @@ SIGNATURES = {
     "stage_set_shard_dedupe": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "stage_set_shard_key_bits": (ctypes.c_int, [c_vp, ctypes.c_int]),
     "stage_set_write_overlap": (ctypes.c_int, [c_vp, ctypes.c_int]),
+    "stage_scratch_plan_check": (ctypes.c_int, [ctypes.c_int, c_vp, ctypes.c_int]),
     "stage_settle": (ctypes.c_int, [c_vp]),
     "stage_rccl_info": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int), ctypes.c_char_p,
                                        ctypes.c_uint64]),

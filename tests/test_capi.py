@@ -102,5 +102,10 @@ def test_q2_async_arguments():
     h = t.h
     assert L.stage_ch_query2_batch_async(h, h, h, h, h, moff, None, 3, rids, 0, out, 8, 0, None) == -1
     assert L.stage_ch_query2_batch_async(h, h, h, h, h, moff, None, 3, rids, 4, None, 8, 0, None) == -1
+    # one table for every role: its scratch would serve the batch buffers and both scan rows
     assert L.stage_ch_query2_batch_async(h, h, h, h, h, moff, ctypes.c_void_p(16), 3, rids, 4, out, 8, 0,
+                                         None) == -1
+    assert b"scratch alias" in L.stage_last_error()
+    ts = [stage.Table(key_width=8) for _ in range(5)]
+    assert L.stage_ch_query2_batch_async(*[x.h for x in ts], moff, ctypes.c_void_p(16), 3, rids, 4, out, 8, 0,
                                          None) == -4
