@@ -176,9 +176,9 @@ def test_q2_batches_on_different_streams(ch):
     oa = stage.pinned_empty((ra.size, 1 << 14), stage.Q2_REC_DTYPE)
     ob = stage.pinned_empty((rb.size, 1 << 14), stage.Q2_REC_DTYPE)
     for rep in range(3):
-        ja = ch.query2_batch_async(ra, oa, 0, 3, stream=s1.ptr)
-        jb = ch.query2_batch_async(rb, ob, 1, 0, stream=s2.ptr)
-        got_c = ch.query2_batch(rc, 1, stream=s3.ptr)  # synchronous, a third stream, both slots busy
+        ja = ch.query2_batch_async(ra, oa, 1, 3, stream=s1.ptr)
+        got_c = ch.query2_batch(rc, 1, stream=s3.ptr)  # synchronous (slot 0), slot 1 busy on s1
+        jb = ch.query2_batch_async(rb, ob, 0, 0, stream=s2.ptr)  # slot 1 may still be busy on s1
         got = {"b": jb.wait(), "a": ja.wait(), "c": got_c}
         for k, (recs, ab) in got.items():
             srecs, sab = ref[k]
