@@ -67,6 +67,13 @@ __device__ __forceinline__ bool kw_lt(const uint64_t *a, const uint64_t *b) {
     return r != 0;
 }
 
+// chunk c (16 B) of heap row img; zeros past the heap row (an output stride above the heap
+// stride, stage_set_output_layout: the rest of the output row is zero, not the next heap row)
+__device__ __forceinline__ u32x4 heap_chunk(const DevTable &t, uint32_t img, uint32_t c) {
+    return c < (t.hstride >> 4) ? reinterpret_cast<const u32x4 *>(t.heap + (uint64_t)img * t.hstride)[c]
+                                : u32x4{0, 0, 0, 0};
+}
+
 // separators of one node (F entries) below x.  KW = 1: the node is F x 8 B (F/2 16-B loads
 // per lane); KW > 1: F entries of KW words each, compared lexicographically.
 template <bool VARLEN, int KW, int F>
@@ -496,7 +503,7 @@ __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *
                 for (int g = 0; g < G; ++g) {
                     v[g] = u32x4{0, 0, 0, 0};
                     if (lane < out_chunks && r[g].image != 0xFFFFFFFFu)
-                        v[g] = reinterpret_cast<const u32x4 *>(t.heap + (uint64_t)r[g].image * t.hstride)[lane];
+                        v[g] = heap_chunk(t, r[g].image, lane);
                     const int j = j0 + g;
                     const uint32_t lo = rl32(my_fan.lo, j & 63), hi = rl32(my_fan.hi, j & 63);
                     const uint32_t kk = lo + lane;
@@ -532,7 +539,7 @@ __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *
                     for (int g = 0; g < G; ++g) {
                         v[g] = u32x4{0, 0, 0, 0};
                         if (c < out_chunks && r[g].image != 0xFFFFFFFFu)
-                            v[g] = reinterpret_cast<const u32x4 *>(t.heap + (uint64_t)r[g].image * t.hstride)[c];
+                            v[g] = heap_chunk(t, r[g].image, c);
                     }
 #pragma unroll
                     for (int g = 0; g < G; ++g) {
@@ -629,7 +636,7 @@ __device__ __forceinline__ void ring_probe_one(const DevTable &t, uint32_t lane,
         const uint32_t c = c0 + lane;
         if (c < out_chunks) {
             u32x4 v = u32x4{0, 0, 0, 0};
-            if (r.image != 0xFFFFFFFFu) v = reinterpret_cast<const u32x4 *>(t.heap + (uint64_t)r.image * t.hstride)[c];
+            if (r.image != 0xFFFFFFFFu) v = heap_chunk(t, r.image, c);
             reinterpret_cast<u32x4 *>(row)[c] = v;
         }
     }
@@ -715,7 +722,7 @@ __device__ __forceinline__ void copy_rows(const DevTable &t, const uint32_t *img
         for (int k = 0; k < R; ++k) {
             v[k] = u32x4{0, 0, 0, 0};
             if (k < n && c < chunks && img[k] != 0xFFFFFFFFu)
-                v[k] = reinterpret_cast<const u32x4 *>(t.heap + (uint64_t)img[k] * t.hstride)[c];
+                v[k] = heap_chunk(t, img[k], c);
         }
 #pragma unroll
         for (int k = 0; k < R; ++k)
@@ -767,7 +774,7 @@ __device__ __forceinline__ void copy_rows_flat(const DevTable &t, uint64_t em, u
             const uint32_t im = (uint32_t)__shfl((int)img, src);
             d[u] = (uint32_t)__shfl((int)dst, src);
             v[u] = u32x4{0, 0, 0, 0};
-            if (ok[u] && im != 0xFFFFFFFFu) v[u] = reinterpret_cast<const u32x4 *>(t.heap + (uint64_t)im * t.hstride)[ck[u]];
+            if (ok[u] && im != 0xFFFFFFFFu) v[u] = heap_chunk(t, im, ck[u]);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -1290,7 +1297,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void p
                     const uint32_t c = c0 + lane;
                     if (c >= out_chunks) continue;
                     u32x4 v = u32x4{0, 0, 0, 0};
-                    if (img != 0xFFFFFFFFu) v = reinterpret_cast<const u32x4 *>(t.heap + (uint64_t)img * t.hstride)[c];
+                    if (img != 0xFFFFFFFFu) v = heap_chunk(t, img, c);
                     st16<1>(v, recs + (base + j) * (uint64_t)t.stride, c * 16u);
                 }
             }
@@ -1400,7 +1407,7 @@ __global__ __launch_bounds__(256) void probe_lane_kernel(DevTable t, const uint6
                     const uint32_t c = cc0 + lane;
                     if (c >= out_chunks) continue;
                     u32x4 v = u32x4{0, 0, 0, 0};
-                    if (img != 0xFFFFFFFFu) v = reinterpret_cast<const u32x4 *>(t.heap + (uint64_t)img * t.hstride)[c];
+                    if (img != 0xFFFFFFFFu) v = heap_chunk(t, img, c);
                     st16<1>(v, recs + (base + j) * (uint64_t)t.stride, c * 16u);
                 }
             }
@@ -2155,7 +2162,7 @@ __global__ __launch_bounds__(256) void for_update_kernel(DevTable t, const uint8
         if (recs) {
             for (uint32_t c = lane; c < chunks; c += 64) {
                 u32x4 v = u32x4{0, 0, 0, 0};
-                if (image != 0xFFFFFFFFu) v = reinterpret_cast<const u32x4 *>(t.heap + (uint64_t)image * t.hstride)[c];
+                if (image != 0xFFFFFFFFu) v = heap_chunk(t, image, c);
                 reinterpret_cast<u32x4 *>(recs + p * (uint64_t)t.stride)[c] = v;
             }
         }

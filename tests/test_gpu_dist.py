@@ -319,5 +319,7 @@ def test_peer_reply_row_stride_raised_between_calls(gpu, world):
             assert rows.shape[1] == full.stride == (stride or 1024)
             assert (out["status"] == ref_out["status"]).all(), (call, r)
             assert (rows == ref_rows).all(), (call, r, stride)
+            # past the 1024-B heap row the output row is zero (not the next heap row)
+            assert not rows[:, 1024:].any()
     for t in tabs + [full]:
         t.set_output_layout(0, 32)
