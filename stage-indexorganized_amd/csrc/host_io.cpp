@@ -375,8 +375,10 @@ int stage_probe_host(stage_table *t, const uint64_t *keys, const uint16_t *lens,
             stage::PipeLane &l = p->lane[c % stage::kPipeLanes];
             if (c >= (uint64_t)stage::kPipeLanes) stage::hip_check(hipStreamSynchronize(l.s), "pipe lane");
             const uint64_t b = c * stage::kPipeChunk, m = std::min<uint64_t>(stage::kPipeChunk, n - b);
+            // out: n records of the table's status layout (32 or 16 B)
+            auto *ob = reinterpret_cast<stage_probe_out *>(reinterpret_cast<uint8_t *>(out) + b * (uint64_t)t->status_bytes);
             stage::hip_check(pipe_chunk(t, l, p->stride, p->kw, keys + b * p->kw, lens ? lens + b : nullptr,
-                                        read_ids ? read_ids + b : nullptr, m, out + b,
+                                        read_ids ? read_ids + b : nullptr, m, ob,
                                         records ? records + b * p->stride : nullptr),
                              "probe_host chunk");
         }
