@@ -346,39 +346,61 @@ __global__ void q2_reduce(const stage_probe_out_dev *__restrict__ slast, const u
 
 // item outcome: no tuple aborts; I_DATA up to its first NUL containing 'b' skips; else a
 // quantity below 10 marks the update
-// ... and each record straight into the caller's page-locked records (host_out, row pitch
-// max_out; null: the records stay in `out` on the device)
-__global__ void q2_finish(const stage_probe_out_dev *__restrict__ iout, const uint8_t *__restrict__ iheap,
-                          uint32_t ihstride, uint32_t ikpad, const uint64_t *__restrict__ counts, uint32_t nq,
-                          stage_q2_rec *__restrict__ out, int32_t *__restrict__ abort_flag,
-                          stage_q2_rec *__restrict__ host_out, uint64_t max_out) {
+// ... and each record into the caller's page-locked records (host_out, row pitch max_out; null:
+// the records stay in `out` on the device).  The host writes cross PCIe: a block's 256 records
+// (48 B each) are staged in LDS and leave as 16-B chunks, consecutive lanes on consecutive
+// chunks (a wave's store is 1 KB of one run of records), not as 48-B-strided lane stores.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+static_assert(sizeof(stage_q2_rec) == 48, "three 16-B chunks per record");
+__global__ __launch_bounds__(256) void q2_finish(const stage_probe_out_dev *__restrict__ iout, const uint8_t *__restrict__ iheap,
+                                                 uint32_t ihstride, uint32_t ikpad, const uint64_t *__restrict__ counts,
+                                                 uint32_t nq, stage_q2_rec *__restrict__ out, int32_t *__restrict__ abort_flag,
+                                                 stage_q2_rec *__restrict__ host_out, uint64_t max_out) {
+    __shared__ u32x4 s_rec[256 * 3];
     const uint32_t n = (uint32_t)counts[0];
-    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;  // q * n + supplier
-    if (s >= n * nq) return;
-    const uint32_t st = iout[s].w[0] & 0xFF;
-    stage_q2_rec r = out[s];
-    if (!produced(st)) {
-        atomicOr(abort_flag + s / n, 1);
-    } else {
-        // I_DATA's 64 bytes in 16 word loads issued together (4-B aligned), scanned in registers
-        const uint32_t *d = reinterpret_cast<const uint32_t *>(iheap + (uint64_t)iout[s].w[6] * ihstride + ikpad +
-                                                               kIDataOff);
-        uint32_t w[16];
+    const uint64_t total = (uint64_t)n * nq;
+    const uint64_t g0 = (uint64_t)blockIdx.x * blockDim.x;
+    const uint64_t s = g0 + threadIdx.x;  // q * n + supplier
+    if (g0 >= total) return;  // block-uniform
+    if (s < total) {
+        const uint32_t st = iout[s].w[0] & 0xFF;
+        stage_q2_rec r = out[s];
+        if (!produced(st)) {
+            atomicOr(abort_flag + s / n, 1);
+        } else {
+            // I_DATA's 64 bytes in 16 word loads issued together (4-B aligned), scanned in registers
+            const uint32_t *d = reinterpret_cast<const uint32_t *>(iheap + (uint64_t)iout[s].w[6] * ihstride + ikpad +
+                                                                   kIDataOff);
+            uint32_t w[16];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) w[k] = d[k];
-        uint8_t has_b = 0;
-        bool end = false;
+            for (int k = 0; k < 16; ++k) w[k] = d[k];
+            uint8_t has_b = 0;
+            bool end = false;
 #pragma unroll
-        for (int c = 0; c < 64; ++c) {
-            const uint8_t ch = (uint8_t)(w[c >> 2] >> (8 * (c & 3)));
-            end |= ch == 0;
-            has_b |= !end && ch == 'b';
+            for (int c = 0; c < 64; ++c) {
+                const uint8_t ch = (uint8_t)(w[c >> 2] >> (8 * (c & 3)));
+                end |= ch == 0;
+                has_b |= !end && ch == 'b';
+            }
+            r.item_has_b = has_b;
+            r.update = !has_b && r.s_quantity < 10;
+            out[s] = r;
         }
-        r.item_has_b = has_b;
-        r.update = !has_b && r.s_quantity < 10;
-        out[s] = r;
+        u32x4 rv[3];
+        memcpy(rv, &r, sizeof(r));
+#pragma unroll
+        for (int k = 0; k < 3; ++k) s_rec[threadIdx.x * 3 + k] = rv[k];
     }
-    if (host_out && s % n < max_out) host_out[(uint64_t)(s / n) * max_out + s % n] = r;
+    if (!host_out) return;  // uniform
+    __syncthreads();
+    const uint64_t nrec = total - g0 < 256 ? total - g0 : 256;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const uint32_t c = k * 256 + threadIdx.x;  // chunk c: record c / 3, part c % 3
+        const uint64_t rec = g0 + c / 3;
+        if (c / 3 < nrec && rec % n < max_out)
+            reinterpret_cast<u32x4 *>(host_out + (rec / n) * max_out + rec % n)[c % 3] = s_rec[c];
+    }
 }
 
 // TableScanExecutor rows of one scan from `start` (device scan) into the table's scratch: the

@@ -1313,6 +1313,60 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void p
     }
 }
 
+// Wave-cooperative lower bound of the wave's 64 fixed-width keys (one per lane, le_child), for
+// the one-probe-in-flight tables whose separators are 2-4 words: per level a team of f lanes
+// (the node's fanout, 16 inner / 8 bottom) reads one key's node, one entry per lane -- 64 / f
+// keys per load instruction, each team's f entries contiguous -- instead of every lane reading
+// its own whole node (a lane's 16 loads of 16 B touch 64 different nodes per instruction: 4x the
+// cache lines for the texture addresser, CH-Q2's STOCK probe ran it 58-79 % busy, r05/lanepmc).
+// A team's ballot bits count its key's separators below the key; the keys and their nodes pass
+// through LDS (s_x: 64 keys, s_node: their nodes at this level).  All 64 lanes take part.
+template <int KW>
+__device__ __forceinline__ uint32_t coop_lower_bound(const DevTable &t, const uint64_t *ok, uint32_t lane,
+                                                     uint64_t *s_x, uint32_t *s_node) {
+#pragma unroll
+    for (int j = 0; j < KW; ++j) s_x[lane * KW + j] = ok[j];
+    uint32_t node = 0;
+    for (int lvl = (int)t.levels - 1; lvl >= 0; --lvl) {
+        const uint32_t f = lvl > 0 ? (uint32_t)kTreeFanout : (uint32_t)kLeafFanout;
+        const uint32_t sh = lvl > 0 ? 4u : 3u, kpr = 64u >> sh;  // keys per round: 4 / 8
+        const uint32_t rounds = 64u / kpr;                        // 16 / 8
+        s_node[lane] = node;
+        __builtin_amdgcn_wave_barrier();
+        const uint64_t lbase = t.level_off[lvl];
+        const uint32_t e = lane & (f - 1), kq = lane >> sh;  // entry of the node, key in the round
+        const uint32_t my_round = lane / kpr, my_team = lane % kpr;
+        uint64_t ball = 0;
+        // rounds in batches of 8 whose loads are in flight together (8 x KW x 8 B per lane)
+        constexpr int kBatch = 8;
+#pragma unroll
+        for (int r0 = 0; r0 < 16; r0 += kBatch) {
+            if ((uint32_t)r0 >= rounds) break;  // wave-uniform: the bottom level has 8 rounds
+            uint64_t w[kBatch][KW];
+#pragma unroll
+            for (int r = 0; r < kBatch; ++r) {
+                const uint32_t kk = (uint32_t)(r0 + r) * kpr + kq;
+                const uint64_t ent = lbase + (uint64_t)s_node[kk] * f + e;
+#pragma unroll
+                for (int j = 0; j < KW; ++j) w[r][j] = t.tree[ent * KW + j];
+            }
+#pragma unroll
+            for (int r = 0; r < kBatch; ++r) {
+                const uint32_t kk = (uint32_t)(r0 + r) * kpr + kq;
+                uint64_t x[KW];
+#pragma unroll
+                for (int j = 0; j < KW; ++j) x[j] = s_x[kk * KW + j];
+                const uint64_t b = __builtin_amdgcn_ballot_w64(kw_lt<KW>(w[r], x));
+                ball = (uint32_t)(r0 + r) == my_round ? b : ball;
+            }
+        }
+        const uint32_t cnt = (uint32_t)__builtin_popcountll((ball >> (my_team * f)) & ((1ull << f) - 1));
+        node = node * f + cnt;
+        __builtin_amdgcn_wave_barrier();  // s_node is rewritten by the next level
+    }
+    return node < t.nseps ? node : t.nseps;
+}
+
 // Point probes of the same instances as probe_split_kernel with a lane per probe throughout
 // (the default for leaves of up to 256 slots): each lane descends, loads its leaf head's
 // fingerprint bytes itself (SPL x 4 16-B loads, all in flight), finds its candidate slots in slot
@@ -1328,6 +1382,8 @@ __global__ __launch_bounds__(256) void probe_lane_kernel(DevTable t, const uint6
                                                          stage_probe_out_dev *__restrict__ out,
                                                          uint8_t *__restrict__ recs, const uint64_t *__restrict__ dn) {
     static_assert(SPL <= 4, "head of at most 256 slots in registers");
+    __shared__ uint64_t s_x[4][64 * KW];
+    __shared__ uint32_t s_node[4][64];
     if (dn) n = *dn < n ? *dn : n;
     const uint32_t lane = lane_id(), wv = uni32(threadIdx.x >> 6);
     const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wv;
@@ -1341,7 +1397,9 @@ __global__ __launch_bounds__(256) void probe_lane_kernel(DevTable t, const uint6
         uint64_t ok[KW];
         load_okey<KW>(keys, i, valid, len, ok);
         uint32_t leaf = 0;
-        if (valid) leaf = leaf_in ? leaf_in[i] : resolve_leaf<false, KW>(t, ok, len, true);
+        if (leaf_in) leaf = valid ? leaf_in[i] : 0u;
+        else leaf = coop_lower_bound<KW>(t, ok, lane, s_x[wv], s_node[wv]);  // every lane takes part
+        if (!valid) leaf = 0;
         if (leaf > t.nseps) leaf = t.nseps;
         const uint32_t rep = (key_fp_words(ok, KW) & 0xFFu) * 0x01010101u;
         // the head: fingerprint byte j = slot j
