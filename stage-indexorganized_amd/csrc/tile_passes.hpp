@@ -46,9 +46,6 @@ struct MaxOp {
     __device__ __forceinline__ static T identity() { return T(0); }  // unsigned values
 };
 
-template <class T, class Op>
-__device__ __forceinline__ T block_excl_scan(T x, T *lds4, T *block_total);
-
 // the lanes of the wave whose `valid` item carries digit d (8 ballots)
 __device__ __forceinline__ uint64_t digit_peers(uint32_t d, bool valid) {
     uint64_t m = __builtin_amdgcn_ballot_w64(valid);
@@ -90,27 +87,21 @@ __global__ __launch_bounds__(kThreads) void tile_hist(const uint64_t *__restrict
 }
 
 // stable scatter of tile b: offs[d * ntiles + b] = the exclusive-scanned histogram (where tile
-// b's first item of digit d goes).  The tile is first sorted by digit in LDS (ranks by wave,
-// round and lane), then written out run by run, consecutive lanes on consecutive positions of a
-// digit's run.  Written item by item, every lane's 8-B key and 4-B value landed on its own line:
-// beside the read probe (which keeps HBM saturated) those partial-line writes made the pass take
-// 3.7 ms instead of 20 µs (round-6 traces); the runs leave as whole lines.  The tile is read
-// twice (counts, then ranks; the second read hits L2) rather than held in registers.
+// b's first item of digit d goes).  The tile is read twice (counts, then the scatter; the second
+// read hits L2) rather than held in registers: a workgroup that holds its 16 items per lane
+// needed the whole register file of its SIMD and was dispatched beside the probe only once every
+// probe wave had left that SIMD (round-6 trace: a 4.9-ms pass).  Rounds are not unrolled for the
+// same reason.
 __global__ __launch_bounds__(kThreads) void tile_scatter(const uint64_t *__restrict__ kin, const uint32_t *__restrict__ vin,
                                                          uint64_t *__restrict__ kout, uint32_t *__restrict__ vout,
                                                          uint64_t n, uint32_t sh, const uint32_t *__restrict__ offs,
                                                          uint32_t ntiles) {
-    __shared__ uint64_t s_k[kTile];
-    __shared__ uint32_t s_v[kTile];
-    __shared__ uint32_t wbase[kThreads / 64][kDigits];  // per wave and digit: counts, then local bases
-    __shared__ uint32_t dstart[kDigits];                // the tile's first sorted position of each digit
-    __shared__ uint32_t goff[kDigits];                  // where the tile's run of each digit goes
-    __shared__ uint32_t lds4[kThreads / 64];
+    __shared__ uint32_t wbase[kThreads / 64][kDigits];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
     for (int w = 0; w < kThreads / 64; ++w) wbase[w][threadIdx.x] = 0;
     __syncthreads();
-    // 1. counts per wave (each wave writes only its own row; a round's leaders hold distinct digits)
+    // counts per wave (each wave writes only its own row; a round's leaders hold distinct digits)
 #pragma unroll 1
     for (int j = 0; j < kItems; ++j) {
         const uint64_t i = item_of(blockIdx.x, wv, j, lane);
@@ -121,27 +112,16 @@ __global__ __launch_bounds__(kThreads) void tile_scatter(const uint64_t *__restr
         __builtin_amdgcn_wave_barrier();
     }
     __syncthreads();
-    // 2. thread t owns digit t: the digit's start in the tile's sorted order (a block scan of the
-    //    digit totals) and each wave's local base
-    {
-        uint32_t c[kThreads / 64], tot = 0;
+    {  // per-wave bases: thread t owns digit t
+        uint32_t run = offs[(uint64_t)threadIdx.x * ntiles + blockIdx.x];
 #pragma unroll
         for (int w = 0; w < kThreads / 64; ++w) {
-            c[w] = wbase[w][threadIdx.x];
-            tot += c[w];
-        }
-        uint32_t all;
-        uint32_t run = block_excl_scan<uint32_t, SumOp>(tot, lds4, &all);
-        dstart[threadIdx.x] = run;
-        goff[threadIdx.x] = offs[(uint64_t)threadIdx.x * ntiles + blockIdx.x];
-#pragma unroll
-        for (int w = 0; w < kThreads / 64; ++w) {
+            const uint32_t c = wbase[w][threadIdx.x];
             wbase[w][threadIdx.x] = run;
-            run += c[w];
+            run += c;
         }
     }
     __syncthreads();
-    // 3. the tile sorted by digit into LDS
 #pragma unroll 1
     for (int j = 0; j < kItems; ++j) {
         const uint64_t i = item_of(blockIdx.x, wv, j, lane);
@@ -154,25 +134,13 @@ __global__ __launch_bounds__(kThreads) void tile_scatter(const uint64_t *__restr
         __builtin_amdgcn_wave_barrier();  // every lane has read its base before a leader moves it
         if (valid) {
             const uint32_t pos = base + (uint32_t)__builtin_popcountll(peers & lanes_below(lane));
-            s_k[pos] = k;
-            s_v[pos] = v;
+            if (pos < n) {  // always (the offsets partition [0, n)); a guard against a bad histogram
+                kout[pos] = k;
+                vout[pos] = v;
+            }
             if (lane == (uint32_t)__builtin_ctzll(peers)) wbase[wv][d] = base + (uint32_t)__builtin_popcountll(peers);
         }
         __builtin_amdgcn_wave_barrier();
-    }
-    __syncthreads();
-    // 4. the sorted tile out, run by run: item e of digit d goes to offs[d] + (e - dstart[d])
-    const uint64_t t0 = (uint64_t)blockIdx.x * kTile;
-    const uint32_t cnt = (uint32_t)(n - t0 < (uint64_t)kTile ? n - t0 : (uint64_t)kTile);
-#pragma unroll 1
-    for (uint32_t e = threadIdx.x; e < cnt; e += kThreads) {
-        const uint64_t k = s_k[e];
-        const uint32_t d = (uint32_t)(k >> sh) & (kDigits - 1);
-        const uint64_t pos = (uint64_t)goff[d] + (e - dstart[d]);
-        if (pos < n) {  // always (the offsets partition [0, n)); a guard against a bad histogram
-            kout[pos] = k;
-            vout[pos] = s_v[e];
-        }
     }
 }
 
