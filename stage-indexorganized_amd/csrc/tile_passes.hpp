@@ -87,11 +87,7 @@ __global__ __launch_bounds__(kThreads) void tile_hist(const uint64_t *__restrict
 }
 
 // stable scatter of tile b: offs[d * ntiles + b] = the exclusive-scanned histogram (where tile
-// b's first item of digit d goes).  The tile is read twice (counts, then the scatter; the second
-// read hits L2) rather than held in registers: a workgroup that holds its 16 items per lane
-// needed the whole register file of its SIMD and was dispatched beside the probe only once every
-// probe wave had left that SIMD (round-6 trace: a 4.9-ms pass).  Rounds are not unrolled for the
-// same reason.
+// b's first item of digit d goes)
 __global__ __launch_bounds__(kThreads) void tile_scatter(const uint64_t *__restrict__ kin, const uint32_t *__restrict__ vin,
                                                          uint64_t *__restrict__ kout, uint32_t *__restrict__ vout,
                                                          uint64_t n, uint32_t sh, const uint32_t *__restrict__ offs,
@@ -101,12 +97,16 @@ __global__ __launch_bounds__(kThreads) void tile_scatter(const uint64_t *__restr
 #pragma unroll
     for (int w = 0; w < kThreads / 64; ++w) wbase[w][threadIdx.x] = 0;
     __syncthreads();
+    uint64_t k[kItems];
+    uint32_t v[kItems];
     // counts per wave (each wave writes only its own row; a round's leaders hold distinct digits)
-#pragma unroll 1
+#pragma unroll
     for (int j = 0; j < kItems; ++j) {
         const uint64_t i = item_of(blockIdx.x, wv, j, lane);
         const bool valid = i < n;
-        const uint32_t d = valid ? (uint32_t)(kin[i] >> sh) & (kDigits - 1) : 0u;
+        k[j] = valid ? kin[i] : 0ull;
+        v[j] = valid ? vin[i] : 0u;
+        const uint32_t d = (uint32_t)(k[j] >> sh) & (kDigits - 1);
         const uint64_t peers = digit_peers(d, valid);
         if (valid && lane == (uint32_t)__builtin_ctzll(peers)) wbase[wv][d] += (uint32_t)__builtin_popcountll(peers);
         __builtin_amdgcn_wave_barrier();
@@ -122,21 +122,19 @@ __global__ __launch_bounds__(kThreads) void tile_scatter(const uint64_t *__restr
         }
     }
     __syncthreads();
-#pragma unroll 1
+#pragma unroll
     for (int j = 0; j < kItems; ++j) {
         const uint64_t i = item_of(blockIdx.x, wv, j, lane);
         const bool valid = i < n;
-        const uint64_t k = valid ? kin[i] : 0ull;
-        const uint32_t v = valid ? vin[i] : 0u;
-        const uint32_t d = (uint32_t)(k >> sh) & (kDigits - 1);
+        const uint32_t d = (uint32_t)(k[j] >> sh) & (kDigits - 1);
         const uint64_t peers = digit_peers(d, valid);
         const uint32_t base = valid ? wbase[wv][d] : 0u;
         __builtin_amdgcn_wave_barrier();  // every lane has read its base before a leader moves it
         if (valid) {
             const uint32_t pos = base + (uint32_t)__builtin_popcountll(peers & lanes_below(lane));
             if (pos < n) {  // always (the offsets partition [0, n)); a guard against a bad histogram
-                kout[pos] = k;
-                vout[pos] = v;
+                kout[pos] = k[j];
+                vout[pos] = v[j];
             }
             if (lane == (uint32_t)__builtin_ctzll(peers)) wbase[wv][d] = base + (uint32_t)__builtin_popcountll(peers);
         }
