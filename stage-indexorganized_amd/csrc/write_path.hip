@@ -35,6 +35,7 @@
 #include <atomic>
 #include <string>
 
+#include <hipcub/hipcub.hpp>
 
 #include <chrono>
 #include <cstdio>
@@ -42,7 +43,7 @@
 #include <vector>
 
 #include "handle.hpp"
-#include "tile_passes.hpp"
+#include "radix_sort.hpp"
 
 using namespace stage_capi;
 
@@ -1018,9 +1019,20 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         while (end_bit < 64 && (none >> end_bit)) ++end_bit;
 
         // scratch
-        // the sort's and scans' scratch (tile_passes.hpp: independent-workgroup passes, so the
-        // epoch's kernels progress beside the previous epoch's probe in write-overlap mode)
-        const size_t cub_bytes = std::max(tiles::sort_scratch(n), tiles::scan_scratch<uint64_t>(n));
+        size_t cub_sort = 0, cub_scan = 0, cub_sum = 0;
+        hip_check(sort_pairs(nullptr, cub_sort, (const uint64_t *)nullptr, (uint64_t *)nullptr, (const uint32_t *)nullptr,
+                             (uint32_t *)nullptr, n, 0, end_bit, s),
+                  "sort size");
+        hip_check(hipcub::DeviceScan::InclusiveScan(nullptr, cub_scan, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                                    hipcub::Max(), (int)n, s),
+                  "scan size");
+        hip_check(hipcub::DeviceScan::ExclusiveSum(nullptr, cub_sum, (uint64_t *)nullptr, (uint64_t *)nullptr, (int)n,
+                                                   s),
+                  "sum size");
+        size_t cub_cls = 0;
+        hip_check(hipcub::DeviceScan::InclusiveSum(nullptr, cub_cls, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)n, s),
+                  "class scan size");
+        const size_t cub_bytes = std::max(std::max(cub_sort, cub_cls), std::max(cub_scan, cub_sum));
         auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
         uint64_t off = 0;
         auto take = [&](uint64_t bytes) {
@@ -1080,6 +1092,7 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         auto *tot = (uint64_t *)(wo + al(n * sizeof(FinRec)));
         auto *cwriter = (uint32_t *)(wo + al(n * sizeof(FinRec)) + 256);  // writer id per new copy
         void *cub = buf + o_cub;
+        size_t cb = cub_bytes;
         // pinned staging of the adoption: [totals 64 B][copy headers][version headers][slot
         // words], sized for the worst case (one copy and one version per op); every part starts
         // on a 16-B boundary (the headers are 16-B aligned types: a misaligned source faults in
@@ -1121,18 +1134,17 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
                                                             loc0, op0, fp_op, wfp_op,
                                                             eqw_op, ff, ls, (uint64_t *)fin, (uint32_t *)(tot + 1));
         // 2. group
-        if (tiles::sort_pairs_tiles(loc0, op0, loc, op, n, end_bit, cub, ks) == false) {
-            std::swap(loc0, loc);  // the result is in the first pair of buffers
-            std::swap(op0, op);
-        }
+        hip_check(sort_pairs(cub, cb, (const uint64_t *)loc0, loc, (const uint32_t *)op0, op, n, 0, end_bit, ks), "sort");
         wp_heads<<<blocks_for(n, 256), 256, 0, ks>>>(loc, n, head);
-        tiles::scan<uint32_t, tiles::MaxOp, true>(head, gs, n, cub, ks);  // group starts
+        cb = cub_bytes;
+        hip_check(hipcub::DeviceScan::InclusiveScan(cub, cb, head, gs, hipcub::Max(), (int)n, ks), "group starts");
         // 3. decide
         WpArgs a{loc, op, gs, d_deltas, d_writer_ids, d_commit_ids, d_sstamps, n, none, delta_len,
                  facts(t).key_pad() + payload_off,
                  (uint64_t)payload_off + delta_len > facts(t).params().payload_size ? 1u : 0u};
         wp_classify<<<blocks_for(n, 256), 256, 0, ks>>>(a, fp_op, wfp_op, eqw_op, brk, fpd, wfp, eqw);
-        tiles::scan<uint32_t, tiles::SumOp, true>(brk, cls, n, cub, ks);  // delta classes
+        cb = cub_bytes;
+        hip_check(hipcub::DeviceScan::InclusiveSum(cub, cb, brk, cls, (int)n, ks), "delta classes");
         const WpCls kc{cls, fpd, wfp, eqw};
         wp_speculate<<<blocks_for(n, 256), 256, 0, ks>>>(a, kc, view, rcs, succ, prev, ff, gend, brk, cfirst);
         // big failing groups (at least kJumpFrom ops from their first failure on) by pointer
@@ -1147,7 +1159,8 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
                                                           ci);
         // 4. number
         wp_flags<<<blocks_for(n, 256), 256, 0, ks>>>(a, succ, flags);
-        tiles::scan<uint64_t, tiles::SumOp, false>(flags, ranks, n, cub, ks);  // ranks
+        cb = cub_bytes;
+        hip_check(hipcub::DeviceScan::ExclusiveSum(cub, cb, flags, ranks, (int)n, ks), "ranks");
         wp_totals<<<1, 1, 0, ks>>>(ranks, flags, n, tot, (uint64_t *)dv.wp_bases.p);
         wp_headers<<<blocks_for(n, 256), 256, 0, ks>>>(a, view, succ, prev, ranks, (CopyHdr *)dv.chdr.p,
                                                       (VersionHdr *)dv.vhdr.p, ls, wrec, tot, cwriter);
