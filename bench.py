@@ -1304,7 +1304,7 @@ def run_chq2(args):
 PCIE_PEAK_GBS = 63.0  # PCIe Gen5 x16 per direction (MI355X_MICROARCH.md, host link)
 
 
-def end_to_end_leg(tab, args, draws, d_out, d_rec):
+def end_to_end_leg(tab, args, draws):
     """C2 delivered to host memory (SURVEY §8(d) timing rule: H2D / D2H included): the same 2^24
     Zipf keys through stage_probe_host from a pinned key array, each call's status records and
     rows landing in a pinned result ring the caller consumes (2^22 lookups per call), for
@@ -1312,7 +1312,9 @@ def end_to_end_leg(tab, args, draws, d_out, d_rec):
     1024-B rows) and the lean one a host caller asks for with stage_set_output_layout(1008, 16)
     (16-B stage_probe_out16, packed 1008-B [key][payload] rows: what IndexScanExecutor copies
     out, executor.h:396-397).  The last call's first 4096 results are compared with the
-    device-resident probe of the same keys (d_out / d_rec, themselves oracle-checked)."""
+    device-buffer probe (stage_probe_batch) of the same keys on the same table state.  It runs
+    after the other device legs: pinning and releasing its 4-GB ring slowed the C3 leg that
+    followed it by ~7 % (round-6 A/B, profiles/r06/e2eorder)."""
     B = draws.size
     chunk = min(B, 1 << 22)
     keys = stage.pinned_empty(B, np.uint64)
@@ -1321,8 +1323,9 @@ def end_to_end_leg(tab, args, draws, d_out, d_rec):
     res = {}
     last = (B // chunk - 1) * chunk
     k = min(4096, chunk)
-    ref_st = d_out.to_numpy(stage.PROBE_OUT_DTYPE, k, offset=last * 32)["status"]
-    ref_rows = d_rec.to_numpy(np.uint8, k * tab.stride, offset=last * tab.stride).reshape(k, tab.stride)[:, :1008]
+    tab.set_output_layout(0, 32)
+    ref_out, ref_rows = tab.probe(draws[last:last + k])
+    ref_st, ref_rows = ref_out["status"], ref_rows[:, :1008]
     for name, stride, sb in layouts:
         tab.set_output_layout(stride, sb)
         dt = stage.PROBE_OUT16_DTYPE if sb == 16 else stage.PROBE_OUT_DTYPE
@@ -1639,10 +1642,6 @@ def main(argv=None):
                 "ms_per_step": round(elapsed / args.steps * 1e3, 4), "self_check": ok, "roofline": roof,
                 "config": {"workload": WORKLOADS["c2"], "theta": args.theta,
                            "traversal": "host" if d_leaf else "device"}}
-        if not args.no_e2e:
-            head["end_to_end"] = end_to_end_leg(tab, args, draws, d_out, d_rec)
-            log(f"[rank {rank}] C2 end to end (host buffers): {head['end_to_end']['value'] / 1e6:.1f} M lookups/s, "
-                f"{head['end_to_end']['pcie_d2h_gbs']} GB/s D2H")
         for b in (d_keys, d_out, d_rec) + ((d_leaf,) if d_leaf else ()):
             b.free()
         if not args.no_extras:
@@ -1653,6 +1652,12 @@ def main(argv=None):
             extras["c3"], samples["c3"] = c3_leg(tab, args, stream, nthreads, args.c3_epochs, 1)
             log(f"[rank {rank}] C3: {extras['c3']['value'] / 1e9:.3f} G ops/s incl. writes "
                 f"({extras['c3']['reads_per_s'] / 1e9:.3f} G reads/s)")
+        if not args.no_e2e:  # last: its pinned ring disturbs the legs after it
+            head["end_to_end"] = end_to_end_leg(tab, args, draws)
+            head["end_to_end"]["table_state"] = ("as the C4 and C3 legs left it (C3's updates applied)"
+                                                 if not args.no_extras else "as loaded (the C2 table)")
+            log(f"[rank {rank}] C2 end to end (host buffers): {head['end_to_end']['value'] / 1e6:.1f} M lookups/s, "
+                f"{head['end_to_end']['pcie_d2h_gbs']} GB/s D2H")
     if not head["self_check"]:
         log(f"[rank {rank}] SELF-CHECK FAILED")
 
