@@ -63,6 +63,23 @@ __global__ __launch_bounds__(256) void guest(uint32_t *__restrict__ out, uint32_
     if (i < n) out[i] = v;
 }
 
+// writer guests: 200 x 256 threads x 16 items of 8 B (the sort scatter's volume per pass) into a
+// 6.7-MB array -- at hashed (scattered) or consecutive positions, with ordinary or nontemporal
+// stores
+template <bool SCATTER, bool NT>
+__global__ __launch_bounds__(256) void writer(uint64_t *__restrict__ out, uint32_t m) {
+    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+#pragma unroll 1
+    for (int j = 0; j < 16; ++j) {
+        const uint32_t i = t * 16 + j;
+        uint64_t h = (uint64_t)i * 0x9E3779B97F4A7C15ull;
+        h ^= h >> 29;
+        const uint32_t pos = SCATTER ? (uint32_t)(h % m) : (i % m);
+        if (NT) __builtin_nontemporal_store((uint64_t)i, out + pos);
+        else out[pos] = i;
+    }
+}
+
 int main() {
     CK(hipSetDevice(0));
     const uint64_t nsrc = (6ull << 30) / 16;  // 6 GiB of 16-B items
@@ -91,7 +108,7 @@ int main() {
         else guest<3><<<200, 256, v.lds, s>>>(gout, 200 * 256);
     };
     // the hog alone
-    const uint64_t iters = 24;
+    const uint64_t iters = 6;  // ~9 ms
     hog<<<16384, 256, 0, sh>>>(src, dst, nsrc, iters);
     CK(hipStreamSynchronize(sh));
     CK(hipEventRecord(h0, sh));
@@ -128,6 +145,43 @@ int main() {
         CK(hipEventElapsedTime(&from_hog, h0, b));
         std::printf("guest barriers %d lds %6u B: alone %.3f ms, beside the hog %.3f ms (ends %.3f ms after the hog's start; hog %.3f ms)\n",
                     v.nb, v.lds, alone, beside, from_hog, hog2);
+        CK(hipEventDestroy(a));
+        CK(hipEventDestroy(b));
+    }
+    uint64_t *wout;
+    const uint32_t m = 838000;
+    CK(hipMalloc(&wout, (uint64_t)m * 8));
+    auto launch_writer = [&](int kind, hipStream_t s) {
+        if (kind == 0) writer<true, false><<<200, 256, 0, s>>>(wout, m);
+        else if (kind == 1) writer<true, true><<<200, 256, 0, s>>>(wout, m);
+        else writer<false, false><<<200, 256, 0, s>>>(wout, m);
+    };
+    const char *names[3] = {"scattered ordinary stores", "scattered nontemporal stores", "consecutive ordinary stores"};
+    for (int kind = 0; kind < 3; ++kind) {
+        hipEvent_t a, b;
+        CK(hipEventCreate(&a));
+        CK(hipEventCreate(&b));
+        launch_writer(kind, sg);
+        CK(hipEventRecord(a, sg));
+        launch_writer(kind, sg);
+        CK(hipEventRecord(b, sg));
+        CK(hipStreamSynchronize(sg));
+        float alone = 0;
+        CK(hipEventElapsedTime(&alone, a, b));
+        CK(hipEventRecord(h0, sh));
+        hog<<<16384, 256, 0, sh>>>(src, dst, nsrc, iters);
+        CK(hipEventRecord(h1, sh));
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+        CK(hipEventRecord(a, sg));
+        launch_writer(kind, sg);
+        CK(hipEventRecord(b, sg));
+        CK(hipDeviceSynchronize());
+        float beside = 0, hog2 = 0, from_hog = 0;
+        CK(hipEventElapsedTime(&beside, a, b));
+        CK(hipEventElapsedTime(&hog2, h0, h1));
+        CK(hipEventElapsedTime(&from_hog, h0, b));
+        std::printf("writer, %s: alone %.3f ms, beside the hog %.3f ms (ends %.3f ms after the hog's start; hog %.3f ms)\n",
+                    names[kind], alone, beside, from_hog, hog2);
         CK(hipEventDestroy(a));
         CK(hipEventDestroy(b));
     }
