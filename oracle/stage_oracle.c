@@ -422,12 +422,19 @@ static uint8_t *leaf_new(orc_tree *t) { /* LeafNode::New, b_tree.cpp:791-797 */
     return n;
 }
 
+/* A slot's meta word is read by every search of its leaf and, under orc_update_batch_mt,
+ * written by the writer that owns its key while other writers search the same leaf: relaxed
+ * atomic loads and stores (the reference CASes the word, b_tree.cpp:1106-1120) -- the other
+ * writers' searches only need its visible bit and key length, which an update never changes. */
+static inline uint64_t meta_load(const orc_rmeta *m) { return __atomic_load_n(&m->meta, __ATOMIC_RELAXED); }
+static inline void meta_store(orc_rmeta *m, uint64_t v) { __atomic_store_n(&m->meta, v, __ATOMIC_RELAXED); }
+
 /* BaseNode::SearchRecordMeta, b_tree.cpp:18-122 (called with check_concurrency == true by
  * LeafNode::Read because of the argument shift at b_tree.cpp:1044-1045). */
 static int64_t search_record_meta(uint8_t *n, const uint8_t *key, uint16_t ks, int check_concurrency) {
     uint32_t sorted = *l_sorted(n);
     for (uint32_t i = 0; i < sorted; i++) {
-        uint64_t m = l_meta(n, i)->meta;
+        uint64_t m = meta_load(l_meta(n, i));
         if (m == 0) continue;
         const uint8_t *ck = l_key(n, m);
         int cmp = orc_key_compare(key, ks, ck, m_keylen(m));
@@ -435,7 +442,7 @@ static int64_t search_record_meta(uint8_t *n, const uint8_t *key, uint16_t ks, i
     }
     uint32_t cnt = st_count(*l_status(n));
     for (uint32_t i = sorted; i < cnt; i++) {
-        uint64_t m = l_meta(n, i)->meta;
+        uint64_t m = meta_load(l_meta(n, i));
         if (m_visible(m)) {
             uint16_t cs = m_keylen(m);
             if (cs == ks && orc_key_compare(key, ks, l_key(n, m), cs) == 0) return i;
@@ -1849,7 +1856,7 @@ int orc_update(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32_t payl
     if (memcmp(col, delta, delta_len) == 0) return ORC_RET_NOT_NEEDED_UPDATE; /* ComparePayload */
     if (m_cstamp(mp->meta) > writer_id) return ORC_RET_NOT_NEEDED_UPDATE;
     uint64_t old = mp->meta;
-    mp->meta = old | M_CONTROL | M_VISIBLE; /* PrepareForUpdate */
+    meta_store(mp, old | M_CONTROL | M_VISIBLE); /* PrepareForUpdate */
     orc_copy *c = copy_alloc(t, rk, m_keylen(old), mp->next, writer_id, m_cstamp(old));
     mp->next = (uint64_t)(uintptr_t)c | NEXT_COPY;
     memcpy(col, delta, delta_len); /* CopyPayload */
@@ -1898,7 +1905,7 @@ int orc_commit_update(orc_tree *t, const uint8_t *key, uint32_t key_size, uint32
     uint64_t m = mp->meta;
     m = (m & ~M_TXN) | commit_id; /* FinalizeForUpdate(t_cstamp), record_meta.h:146-151 */
     m &= ~M_CONTROL;
-    mp->meta = m;
+    meta_store(mp, m);
     mp->next = (uint64_t)(uintptr_t)th | NEXT_TH;
     return ORC_RET_OK;
 }
