@@ -35,6 +35,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "handle.hpp"
+#include "visibility.hpp"
 
 using namespace stage_capi;
 
@@ -77,9 +78,10 @@ __global__ void q2_gather(const uint64_t *__restrict__ map_keys, const uint64_t 
 //              stable counting sort by visit over 64-slot chunks --
 //                q2_sel_count  (a wave per chunk) the visits, each slot's visit, its rank and its
 //                              map entries' offset among its chunk's slots of that visit, the
-//                              chunk's supplier and entry counts per visit;
-//                q2_sel_start  (one block) each (chunk, visit)'s supplier and entry starts:
-//                              visit-major, then chunk;
+//                              chunk's supplier and entry counts per visit (stored
+//                              visit-major: a visit's chunks side by side);
+//                q2_sel_start  (one block) each (visit, chunk)'s supplier and entry starts:
+//                              visit, then chunk order;
 //                q2_sel_place  (a lane per slot) sel[start + rank], the supplier's map segment
 //                              (src, cnt) and its first STOCK key (dst = entry start + offset);
 //   counts   = {suppliers, stock keys}.
@@ -163,26 +165,29 @@ __global__ __launch_bounds__(256) void q2_sel_count(const uint8_t *__restrict__ 
     __shared__ uint8_t s_rmatch[kRegionScan];
     __shared__ uint8_t s_flag[kRegionScan * kNationScan];
     __shared__ uint32_t s_cnt[4][kVisits], s_kcnt[4][kVisits];
-    build_visits(vm, regs, rs, nats, ns, name0, name1, mask0, mask1, s_rmatch, s_flag);
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *g_nv = vm.nv;
     const uint64_t c = (uint64_t)blockIdx.x * 4 + wv;
+    // the slot's record first -- slot word, key, nation key, map segment: none of it depends on
+    // the visits, so these dependent loads overlap build_visits' own (the scan rows)
+    const uint64_t i = c * 64 + lane;
+    uint64_t key = ~0ull, nat = 0;
+    uint32_t ma = 0, mb = 0;
+    if (c < nchunks) {
+        const SlotInfo si = t.slot[i];
+        if (si.meta != 0) {
+            const uint8_t *row = t.heap + (uint64_t)si.image * t.hstride;
+            key = *reinterpret_cast<const uint64_t *>(row);
+            nat = *reinterpret_cast<const uint64_t *>(row + kpad);
+        }
+        if (key < 10000) ma = map_off[key], mb = map_off[key + 1];
+    }
+    build_visits(vm, regs, rs, nats, ns, name0, name1, mask0, mask1, s_rmatch, s_flag);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *g_nv = vm.nv;
     if (c >= nchunks) return;
     for (uint32_t v = lane; v < (uint32_t)kVisits; v += 64) s_cnt[wv][v] = 0, s_kcnt[wv][v] = 0;
-    const uint64_t i = c * 64 + lane;
-    const SlotInfo si = t.slot[i];
-    uint64_t key = ~0ull;
-    int v = -1;
-    if (si.meta != 0) {
-        const uint8_t *row = t.heap + (uint64_t)si.image * t.hstride;
-        key = *reinterpret_cast<const uint64_t *>(row);
-        v = key == ~0ull ? -1 : visit_of(vm, *reinterpret_cast<const uint64_t *>(row + kpad));
-    }
-    uint32_t mc = 0;  // the supplier's supp_stock_map entries (keys below 10000)
-    if (v >= 0 && key < 10000) {
-        const uint32_t a = map_off[key], b = map_off[key + 1];
-        mc = b > a ? b - a : 0;
-    }
+    const int v = key == ~0ull ? -1 : visit_of(vm, nat);
+    // the supplier's supp_stock_map entries (keys below 10000)
+    const uint32_t mc = v >= 0 && key < 10000 && mb > ma ? mb - ma : 0;
     // per visit present in the chunk: each slot's rank and its entries' offset among the
     // chunk's slots of that visit, the visit's supplier and entry counts
     uint32_t rank = 0, koff = 0;
@@ -213,31 +218,64 @@ __global__ __launch_bounds__(256) void q2_sel_count(const uint8_t *__restrict__ 
     g_rank[i] = (uint8_t)rank;
     g_koff[i] = koff;
     g_key[i] = key;
-    for (uint32_t w = lane; w < (uint32_t)kVisits; w += 64) {
-        ccnt[c * kVisits + w] = s_cnt[wv][w];
-        kcnt[c * kVisits + w] = s_kcnt[wv][w];
+    for (uint32_t w = lane; w < vm.nv; w += 64) {  // visit-major: q2_sel_start reads a visit's chunks coalesced
+        ccnt[(uint64_t)w * nchunks + c] = s_cnt[wv][w];
+        kcnt[(uint64_t)w * nchunks + c] = s_kcnt[wv][w];
     }
 }
 
-// one block, after q2_sel_count: the (chunk, visit) supplier counts ccnt and entry counts kcnt ->
-// their starts, in place (visit-major, then chunk order); counts = {suppliers, stock keys}.  A
-// wave per visit, a lane per contiguous run of chunks: every load of a pass issued first.
+// one block, after q2_sel_count: the (visit, chunk) supplier counts ccnt and entry counts kcnt
+// (visit-major) -> their starts, in place (visit, then chunk order); counts = {suppliers, stock
+// keys}.  A wave per visit; lane l takes chunks l, l + 64, ... so each load and store of the
+// wave is 64 consecutive words; 16 chunks per lane in flight at once.  (Round 6: a lane per
+// contiguous run of chunks in the chunk-major layout made every load touch 64 lines -- ~10 K
+// line requests through the block's one CU, ~13 µs of the chain.)
+constexpr uint32_t kSelBatch = 16;
+__device__ __forceinline__ void load_batch(const uint32_t *__restrict__ ccnt, const uint32_t *__restrict__ kcnt,
+                                           uint64_t row, uint64_t nchunks, uint64_t c0, uint32_t lane,
+                                           uint32_t (&x0)[kSelBatch], uint32_t (&x1)[kSelBatch]) {
+#pragma unroll
+    for (uint32_t k = 0; k < kSelBatch; ++k) {  // unconditional loads (an index past the end re-reads chunk 0)
+        const uint64_t c = c0 + k * 64 + lane;
+        const uint64_t at = row + (c < nchunks ? c : 0);
+        x0[k] = ccnt[at];
+        x1[k] = kcnt[at];
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kSelBatch; ++k) {
+        const bool in = c0 + k * 64 + lane < nchunks;
+        x0[k] = in ? x0[k] : 0u;
+        x1[k] = in ? x1[k] : 0u;
+    }
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t y, uint32_t lane) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t z = __shfl_up(y, o, 64);
+        if (lane >= (uint32_t)o) y += z;
+    }
+    return y;
+}
+
 __global__ __launch_bounds__(1024) void q2_sel_start(uint32_t *__restrict__ ccnt, uint32_t *__restrict__ kcnt,
                                                      uint64_t nchunks, const uint32_t *__restrict__ g_nv,
                                                      uint64_t *__restrict__ counts) {
     __shared__ uint32_t s_tot[2][kVisits];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
     const uint32_t nv = *g_nv;
-    const uint64_t per = (nchunks + 63) / 64, c_lo = lane * per, c_hi = c_lo + per < nchunks ? c_lo + per : nchunks;
-    uint32_t *arr[2] = {ccnt, kcnt};
-    for (uint32_t v = wv; v < nv; v += nw)
-        for (int a = 0; a < 2; ++a) {  // the visit's totals
-            uint32_t t = 0;
-            for (uint64_t c = c_lo; c < c_hi; ++c) t += arr[a][c * kVisits + v];
+    for (uint32_t v = wv; v < nv; v += nw) {  // the visit's totals
+        uint32_t t0 = 0, t1 = 0;
+        for (uint64_t c0 = 0; c0 < nchunks; c0 += 64 * kSelBatch) {
+            uint32_t x0[kSelBatch], x1[kSelBatch];
+            load_batch(ccnt, kcnt, (uint64_t)v * nchunks, nchunks, c0, lane, x0, x1);
 #pragma unroll
-            for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
-            if (lane == 0) s_tot[a][v] = t;
+            for (uint32_t k = 0; k < kSelBatch; ++k) t0 += x0[k], t1 += x1[k];
         }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) t0 += __shfl_xor(t0, o, 64), t1 += __shfl_xor(t1, o, 64);
+        if (lane == 0) s_tot[0][v] = t0, s_tot[1][v] = t1;
+    }
     __syncthreads();
     if (tid < 2) {
         uint32_t pos = 0;
@@ -249,40 +287,22 @@ __global__ __launch_bounds__(1024) void q2_sel_start(uint32_t *__restrict__ ccnt
         counts[tid] = pos;
     }
     __syncthreads();
-    for (uint32_t v = wv; v < nv; v += nw)
-        for (int a = 0; a < 2; ++a) {  // exclusive scan over the chunks, in place
-            uint32_t *A = arr[a];
-            uint32_t x[16], t = 0;
-            if (per <= 16) {
+    for (uint32_t v = wv; v < nv; v += nw) {  // exclusive scan over the chunks, in place
+        uint32_t p0 = s_tot[0][v], p1 = s_tot[1][v];  // the start of the next 64 chunks
+        const uint64_t row = (uint64_t)v * nchunks;
+        for (uint64_t c0 = 0; c0 < nchunks; c0 += 64 * kSelBatch) {
+            uint32_t x0[kSelBatch], x1[kSelBatch];
+            load_batch(ccnt, kcnt, row, nchunks, c0, lane, x0, x1);
 #pragma unroll
-                for (int k = 0; k < 16; ++k) x[k] = c_lo + k < c_hi ? A[(c_lo + k) * kVisits + v] : 0u;
-#pragma unroll
-                for (int k = 0; k < 16; ++k) t += x[k];
-            } else {
-                for (uint64_t c = c_lo; c < c_hi; ++c) t += A[c * kVisits + v];
-            }
-            uint32_t y = t;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t z = __shfl_up(y, o, 64);
-                if (lane >= (uint32_t)o) y += z;
-            }
-            uint32_t pos = s_tot[a][v] + y - t;
-            if (per <= 16) {
-#pragma unroll
-                for (int k = 0; k < 16; ++k)
-                    if (c_lo + k < c_hi) {
-                        A[(c_lo + k) * kVisits + v] = pos;
-                        pos += x[k];
-                    }
-            } else {
-                for (uint64_t c = c_lo; c < c_hi; ++c) {
-                    const uint32_t xc = A[c * kVisits + v];
-                    A[c * kVisits + v] = pos;
-                    pos += xc;
-                }
+            for (uint32_t k = 0; k < kSelBatch; ++k) {
+                const uint64_t c = c0 + k * 64 + lane;
+                const uint32_t y0 = wave_incl_scan(x0[k], lane), y1 = wave_incl_scan(x1[k], lane);
+                if (c < nchunks) ccnt[row + c] = p0 + y0 - x0[k], kcnt[row + c] = p1 + y1 - x1[k];
+                p0 += rl32(y0, 63);
+                p1 += rl32(y1, 63);
             }
         }
+    }
 }
 
 // a lane per slot: each selected supplier at its place, with its supp_stock_map segment (src,
@@ -296,7 +316,7 @@ __global__ void q2_sel_place(const uint32_t *__restrict__ ccnt, const uint32_t *
     if (i >= nslots) return;
     const int v = g_vis[i];
     if (v < 0) return;
-    const uint64_t g = (i >> 6) * kVisits + v;
+    const uint64_t g = (uint64_t)v * (nslots >> 6) + (i >> 6);  // visit-major (q2_sel_start)
     const uint32_t pos = ccnt[g] + g_rank[i];
     const uint64_t sk = g_key[i];
     uint64_t s0 = 0, c = 0;
@@ -311,18 +331,130 @@ __global__ void q2_sel_place(const uint32_t *__restrict__ ccnt, const uint32_t *
     dst[pos] = (uint64_t)kcnt[g] + g_koff[i];
 }
 
+// q2_sel_start + q2_sel_place + q2_gather in one launch, for SUPPLIER tables of at most
+// kPlaceChunks 64-slot chunks.  A block of 16 waves per 4 chunks (sel_count's chunks of a block):
+//   1. per visit, a wave sums the (visit, chunk) counts of every chunk and of the chunks before
+//      the block's first (coalesced loads, L2-resident: ~26 KB per block at 256 chunks and 13
+//      visits) -- one load round when the visits fit the 16 waves -- and keeps the block's own
+//      chunks' counts in LDS; the visit totals are scanned in LDS (block 0 writes counts);
+//   2. a thread per slot of the 4 chunks places its supplier as q2_sel_place and lists it;
+//   3. the block's listed suppliers' map segments are copied as q2_gather, a wave per supplier,
+//      each segment's loads issued together (up to 256 entries of 16 B per round).
+// Removes two launches and the one-block scan from the chain (round 6).
+constexpr uint64_t kPlaceChunks = 1024;
+__global__ __launch_bounds__(1024) void q2_place(const uint32_t *__restrict__ ccnt, const uint32_t *__restrict__ kcnt,
+                                                 uint64_t nchunks, const uint32_t *__restrict__ g_nv,
+                                                 const int8_t *__restrict__ g_vis, const uint8_t *__restrict__ g_rank,
+                                                 const uint32_t *__restrict__ g_koff, const uint64_t *__restrict__ g_key,
+                                                 const uint32_t *__restrict__ map_off, const uint64_t *__restrict__ map_keys,
+                                                 uint64_t m_cap, uint64_t *__restrict__ sel, uint64_t *__restrict__ src,
+                                                 uint32_t *__restrict__ cnt, uint64_t *__restrict__ dst,
+                                                 uint64_t *__restrict__ counts, uint64_t *__restrict__ keys) {
+    __shared__ uint32_t s_base[2][kVisits];  // visit start + the counts of chunks before the block's first
+    __shared__ uint32_t s_tot[2][kVisits];
+    __shared__ uint32_t s_loc[2][4][kVisits];  // the block's own chunks' counts
+    __shared__ uint64_t s_a[256], s_d[256];    // listed suppliers: map segment start, first STOCK key
+    __shared__ uint32_t s_m[256], s_n;         // ... entry count; list length
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
+    const uint64_t c_first = (uint64_t)blockIdx.x * 4;
+    // the slot's selection (threads 0..255: the block's 4 chunks) first, its map segment next:
+    // independent of the counts, so these loads overlap the count pass below
+    const bool slot_thread = tid < 256 && c_first + (tid >> 6) < nchunks;
+    const uint64_t i = (c_first + (tid >> 6)) * 64 + lane;
+    int v_i = -1;
+    uint32_t rank_i = 0, koff_i = 0, lo_i = 0, hi_i = 0;
+    uint64_t key_i = ~0ull;
+    if (slot_thread) {
+        v_i = g_vis[i];
+        rank_i = g_rank[i];
+        koff_i = g_koff[i];
+        key_i = g_key[i];
+        if (key_i < 10000) lo_i = map_off[key_i], hi_i = map_off[key_i + 1];
+    }
+    const uint32_t nv = *g_nv;
+    if (tid == 0) s_n = 0;
+    for (uint32_t j = tid; j < 2 * 4 * kVisits; j += blockDim.x)  // chunks past the table's end
+        if (c_first + (j / kVisits) % 4 >= nchunks) (&s_loc[0][0][0])[j] = 0;
+    for (uint32_t v = wv; v < nv; v += nw) {
+        uint32_t t0 = 0, t1 = 0, p0 = 0, p1 = 0;
+        for (uint64_t c0 = 0; c0 < nchunks; c0 += 64 * kSelBatch) {
+            uint32_t x0[kSelBatch], x1[kSelBatch];
+            load_batch(ccnt, kcnt, (uint64_t)v * nchunks, nchunks, c0, lane, x0, x1);
+#pragma unroll
+            for (uint32_t k = 0; k < kSelBatch; ++k) {
+                const uint64_t c = c0 + k * 64 + lane;
+                t0 += x0[k], t1 += x1[k];
+                if (c < c_first) p0 += x0[k], p1 += x1[k];
+                if (c >= c_first && c < c_first + 4 && c < nchunks)
+                    s_loc[0][c - c_first][v] = x0[k], s_loc[1][c - c_first][v] = x1[k];
+            }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            t0 += __shfl_xor(t0, o, 64), t1 += __shfl_xor(t1, o, 64);
+            p0 += __shfl_xor(p0, o, 64), p1 += __shfl_xor(p1, o, 64);
+        }
+        if (lane == 0) s_tot[0][v] = t0, s_tot[1][v] = t1, s_base[0][v] = p0, s_base[1][v] = p1;
+    }
+    __syncthreads();
+    if (tid < 2) {
+        uint32_t pos = 0;
+        for (uint32_t v = 0; v < nv; ++v) {
+            s_base[tid][v] += pos;
+            pos += s_tot[tid][v];
+        }
+        if (blockIdx.x == 0) counts[tid] = pos;
+    }
+    __syncthreads();
+    if (slot_thread && v_i >= 0) {
+        const uint32_t j = tid >> 6, v = (uint32_t)v_i;  // the block's chunk, the slot's visit
+        uint32_t pos = s_base[0][v] + rank_i, kpos = s_base[1][v] + koff_i;
+        for (uint32_t jj = 0; jj < j; ++jj) pos += s_loc[0][jj][v], kpos += s_loc[1][jj][v];
+        const uint32_t m = key_i < 10000 && hi_i > lo_i ? hi_i - lo_i : 0;
+        sel[pos] = key_i;
+        src[pos] = lo_i;
+        cnt[pos] = m;
+        dst[pos] = kpos;
+        if (m) {
+            const uint32_t k = atomicAdd(&s_n, 1u);
+            s_a[k] = lo_i;
+            s_d[k] = kpos;
+            s_m[k] = m;
+        }
+    }
+    __syncthreads();
+    const uint32_t nl = s_n;
+    for (uint32_t k = wv; k < nl; k += nw) {  // a wave per listed supplier
+        const uint64_t a = s_a[k], d = s_d[k];
+        const uint32_t m = s_m[k];
+        for (uint32_t e0 = 0; e0 < m; e0 += 256) {
+            u32x4 x[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const uint32_t e = e0 + r * 64 + lane;
+                if (e < m && d + e < m_cap) x[r] = reinterpret_cast<const u32x4 *>(map_keys)[a + e];
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const uint32_t e = e0 + r * 64 + lane;
+                if (e < m && d + e < m_cap) reinterpret_cast<u32x4 *>(keys)[d + e] = x[r];
+            }
+        }
+    }
+}
+
 // thread per (query q, supplier s): the abort for a stock lookup that produced no tuple is already
-// in abort_flag (launch_revisit_segments); the last entry's stock row, at q's read id, gives
-// (w, i, quantity, ytd, order_cnt, remote_cnt) and the item key
-__global__ void q2_reduce(const stage_probe_out_dev *__restrict__ slast, const uint64_t *__restrict__ skeys,
-                          const uint64_t *__restrict__ dst, const uint32_t *__restrict__ cnt,
-                          const uint64_t *__restrict__ supp, const uint8_t *__restrict__ sheap, uint32_t shstride,
-                          uint32_t skpad, const uint64_t *__restrict__ counts, uint32_t nq,
-                          stage_q2_rec *__restrict__ out, uint64_t *__restrict__ ikeys) {
+// in abort_flag (launch_revisit_segments); the last entry's stock probe, its hit re-evaluated at
+// q's read id here (revisit_one), gives (w, i, quantity, ytd, order_cnt, remote_cnt) and the item key
+__global__ void q2_reduce(DevTable st, const stage_probe_out_dev *__restrict__ sbase, const uint32_t *__restrict__ rids,
+                          const uint64_t *__restrict__ skeys, const uint64_t *__restrict__ dst,
+                          const uint32_t *__restrict__ cnt, const uint64_t *__restrict__ supp, uint32_t skpad,
+                          const uint64_t *__restrict__ counts, uint32_t nq, stage_q2_rec *__restrict__ out,
+                          uint64_t *__restrict__ ikeys) {
     const uint32_t n = (uint32_t)counts[0];
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;  // q * n + s
     if (g >= n * nq) return;
-    const uint32_t s = g % n;
+    const uint32_t s = g % n, q = g / n;
     const uint64_t kb = dst[s];
     const uint32_t c = cnt[s];
     stage_q2_rec r;
@@ -332,8 +464,11 @@ __global__ void q2_reduce(const stage_probe_out_dev *__restrict__ slast, const u
         const uint64_t klast = kb + c - 1;
         r.s_w_id = (int64_t)skeys[2 * klast];
         r.s_i_id = (int64_t)skeys[2 * klast + 1];
-        if (produced(slast[g].w[0] & 0xFF)) {
-            const uint8_t *row = sheap + (uint64_t)slast[g].w[6] * shstride + skpad;
+        const u32x4 *bp = reinterpret_cast<const u32x4 *>(sbase + klast);
+        u32x4 a = bp[0], b = bp[1];
+        revisit_one(st, rids[q], a, b);
+        if (produced(a.x & 0xFF)) {
+            const uint8_t *row = st.heap + (uint64_t)b.z * st.hstride + skpad;
             r.s_quantity = ld_i32(row);
             r.s_ytd = ld_i32(row + 4);
             r.s_order_cnt = ld_i32(row + 8);
@@ -350,12 +485,16 @@ __global__ void q2_reduce(const stage_probe_out_dev *__restrict__ slast, const u
 // the records stay in `out` on the device).  The host writes cross PCIe: a block's 256 records
 // (48 B each) are staged in LDS and leave as 16-B chunks, consecutive lanes on consecutive
 // chunks (a wave's store is 1 KB of one run of records), not as 48-B-strided lane stores.
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+// slot_out (split emit, host_out null): the records into the batch slot's own device buffer, row
+// pitch slot_pitch (query q's supplier k at q * slot_pitch + k), for the side stream's copy to
+// the caller.
 static_assert(sizeof(stage_q2_rec) == 48, "three 16-B chunks per record");
-__global__ __launch_bounds__(256) void q2_finish(const stage_probe_out_dev *__restrict__ iout, const uint8_t *__restrict__ iheap,
-                                                 uint32_t ihstride, uint32_t ikpad, const uint64_t *__restrict__ counts,
+__global__ __launch_bounds__(256) void q2_finish(DevTable it, const stage_probe_out_dev *__restrict__ ibase,
+                                                 const uint32_t *__restrict__ rids, uint32_t ikpad,
+                                                 const uint64_t *__restrict__ counts,
                                                  uint32_t nq, stage_q2_rec *__restrict__ out, int32_t *__restrict__ abort_flag,
-                                                 stage_q2_rec *__restrict__ host_out, uint64_t max_out) {
+                                                 stage_q2_rec *__restrict__ host_out, uint64_t max_out,
+                                                 stage_q2_rec *__restrict__ slot_out, uint64_t slot_pitch) {
     __shared__ u32x4 s_rec[256 * 3];
     const uint32_t n = (uint32_t)counts[0];
     const uint64_t total = (uint64_t)n * nq;
@@ -363,14 +502,18 @@ __global__ __launch_bounds__(256) void q2_finish(const stage_probe_out_dev *__re
     const uint64_t s = g0 + threadIdx.x;  // q * n + supplier
     if (g0 >= total) return;  // block-uniform
     if (s < total) {
-        const uint32_t st = iout[s].w[0] & 0xFF;
+        // the supplier's item probe, its hit re-evaluated at the query's read id (revisit_one)
+        const u32x4 *bp = reinterpret_cast<const u32x4 *>(ibase + s % n);
+        u32x4 ia = bp[0], ib = bp[1];
+        revisit_one(it, rids[s / n], ia, ib);
+        const uint32_t st = ia.x & 0xFF;
         stage_q2_rec r = out[s];
         if (!produced(st)) {
             atomicOr(abort_flag + s / n, 1);
         } else {
             // I_DATA's 64 bytes in 16 word loads issued together (4-B aligned), scanned in registers
-            const uint32_t *d = reinterpret_cast<const uint32_t *>(iheap + (uint64_t)iout[s].w[6] * ihstride + ikpad +
-                                                                   kIDataOff);
+            const uint32_t *d =
+                reinterpret_cast<const uint32_t *>(it.heap + (uint64_t)ib.z * it.hstride + ikpad + kIDataOff);
             uint32_t w[16];
 #pragma unroll
             for (int k = 0; k < 16; ++k) w[k] = d[k];
@@ -390,6 +533,11 @@ __global__ __launch_bounds__(256) void q2_finish(const stage_probe_out_dev *__re
         memcpy(rv, &r, sizeof(r));
 #pragma unroll
         for (int k = 0; k < 3; ++k) s_rec[threadIdx.x * 3 + k] = rv[k];
+        if (slot_out) {
+            u32x4 *so = reinterpret_cast<u32x4 *>(slot_out + (s / n) * slot_pitch + s % n);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) so[k] = rv[k];
+        }
     }
     if (!host_out) return;  // uniform
     __syncthreads();
@@ -406,13 +554,24 @@ __global__ __launch_bounds__(256) void q2_finish(const stage_probe_out_dev *__re
 // TableScanExecutor rows of one scan from `start` (device scan) into the table's scratch: the
 // returned pointer is the first row, the row count (u32) 8 bytes before it
 // (d_start: the start key, in device memory written before s reaches the scan)
-const uint8_t *scan_rows(stage_table *t, const uint64_t *d_start, uint32_t scan_size, hipStream_t s) {
-    const DevTable &v = t->dev.view;
-    const uint64_t rows = (uint64_t)scan_size * v.stride;
-    uint8_t *buf = scratch_bytes(t->dev, 64 + rows);
-    auto *cnt = (uint32_t *)(buf + 56);  // 8 bytes before the rows
-    hip_check(launch_scan(v, d_start, nullptr, 1, scan_size, cnt, buf + 64, s, t->scan_tune), "scan");
-    return buf + 64;
+uint8_t *scan_rows_buf(stage_table *t, uint32_t scan_size) {
+    return scratch_bytes(t->dev, 64 + (uint64_t)scan_size * t->dev.view.stride) + 64;
+}
+// ... and both CH-Q2 dimension scans (REGION, NATION) from the same start key: one launch when
+// launch_scan_pair takes them, else one each
+void scan_dims(stage_table *a, uint32_t sa, stage_table *b, uint32_t sb, const uint64_t *d_start, hipStream_t s,
+               const uint8_t **ra, const uint8_t **rb) {
+    uint8_t *pa = scan_rows_buf(a, sa), *pb = scan_rows_buf(b, sb);
+    auto cnt = [](uint8_t *rows) { return (uint32_t *)(rows - 8); };  // 8 bytes before the rows
+    const DevTable &va = a->dev.view, &vb = b->dev.view;
+    if (scan_pair_supported(va, sa, vb, sb)) {
+        hip_check(launch_scan_pair(va, d_start, sa, cnt(pa), pa, vb, d_start, sb, cnt(pb), pb, s), "scan pair");
+    } else {
+        hip_check(launch_scan(va, d_start, nullptr, 1, sa, cnt(pa), pa, s, a->scan_tune), "scan");
+        hip_check(launch_scan(vb, d_start, nullptr, 1, sb, cnt(pb), pb, s, b->scan_tune), "scan");
+    }
+    *ra = pa;
+    *rb = pb;
 }
 
 }  // namespace
@@ -487,6 +646,10 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         // launch shapes from the previous call's counts (the visited set depends on the data only)
         const uint64_t n_hint = stock->q2_hint[0] ? std::min(stock->q2_hint[0], n_max) : n_max;
         const uint64_t m_hint = stock->q2_hint[1] ? std::min(stock->q2_hint[1], std::max<uint64_t>(m_max, 1)) : m_max;
+        // q2_place up to kPlaceChunks SUPPLIER chunks (STAGE_Q2_PLACE_CHUNKS: another limit, for
+        // the tests of the three-kernel form larger tables take)
+        const char *pe = std::getenv("STAGE_Q2_PLACE_CHUNKS");
+        const bool fused_place = nchunks <= (pe ? std::strtoull(pe, nullptr, 10) : kPlaceChunks);
         // pinned call staging mirrored at the head of the device scratch: [map_off][read ids]
         // [aborted] go down in one copy; [counts][aborted] come back in one copy
         auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
@@ -507,7 +670,7 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         const uint64_t o_mir = take(q_end), o_pairs = take(n_max * 16), o_sel = take(n_max * 8),
                        o_src = take(n_max * 8), o_cnt = take(n_max * 4), o_dst = take(n_max * 8),
                        o_keys = take(std::max<uint64_t>(m_max, 1) * 16), o_sbase = take(std::max<uint64_t>(m_max, 1) * 32),
-                       o_slast = take(n_max * 32 * nq), o_ik = take(n_max * 8 * nq), o_iout = take(n_max * 32 * nq),
+                       o_ik = take(n_max * 8 * nq),
                        o_ibase = take(n_max * 32), o_rec = take(n_max * nq * sizeof(stage_q2_rec)),
                        o_vis = take(n_max), o_rank = take(n_max), o_koff = take(n_max * 4),
                        o_ccnt = take(std::max<uint64_t>(nchunks, 1) * kVisits * 4),
@@ -529,7 +692,7 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         if ((stock->q2p[0].active || stock->q2p[1].active) &&
             (supplier->dev.scratch.cap < off || region->dev.scratch.cap < reg_rows || nation->dev.scratch.cap < nat_rows))
             hip_check(hipDeviceSynchronize(), "q2 drain");
-        // the SUPPLIER table's scratch: REGION's and NATION's hold their scan rows (scan_rows)
+        // the SUPPLIER table's scratch: REGION's and NATION's hold their scan rows (scan_dims)
         uint8_t *buf = scratch_bytes(supplier->dev, off), *mir = buf + o_mir;
         auto *d_map = (const uint32_t *)(mir + q_map);
         auto *d_rq = (const uint32_t *)(mir + q_rq);
@@ -539,7 +702,6 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         auto *d_src = (uint64_t *)(buf + o_src), *d_dst = (uint64_t *)(buf + o_dst);
         auto *d_cnt = (uint32_t *)(buf + o_cnt);
         auto *d_keys = (uint64_t *)(buf + o_keys), *d_ik = (uint64_t *)(buf + o_ik);
-        auto *d_iout = (stage_probe_out_dev *)(buf + o_iout), *d_slast = (stage_probe_out_dev *)(buf + o_slast);
         auto *d_sbase = (stage_probe_out_dev *)(buf + o_sbase), *d_ibase = (stage_probe_out_dev *)(buf + o_ibase);
         auto *d_rec = (stage_q2_rec *)(buf + o_rec);
         char tname[16] = {0};
@@ -566,8 +728,26 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         if (trace) std::fprintf(stderr, "[q2] out %s\n", host_out ? "page-locked: written by q2_finish" : "pageable: copied");
         if (async && out && max_out && !host_out)
             return fail(STAGE_E_ARG, "stage_ch_query2_batch_async needs a page-locked out (stage_host_alloc)");
+        // an async batch's records leave from the side stream (Q2Pending::split): finished into
+        // the slot's own device buffer, row pitch n_max
+        Q2Pending &P = stock->q2p[slot];
+        const bool split = async && host_out;
+        stage_q2_rec *slot_out = nullptr;
+        if (split) {
+            const uint64_t need = n_max * nq * sizeof(stage_q2_rec);
+            if (P.dcap < need) {  // the slot is idle (checked above): its old buffer is unused
+                if (P.dbuf) hip_check(hipFree(P.dbuf), "q2 slot buffer");
+                P.dbuf = nullptr;
+                P.dcap = 0;
+                hip_check(hipMalloc(&P.dbuf, need), "q2 slot buffer");
+                P.dcap = need;
+            }
+            if (!stock->q2_side) hip_check(hipStreamCreateWithFlags(&stock->q2_side, hipStreamNonBlocking), "q2 side stream");
+            if (!P.fin) hip_check(hipEventCreateWithFlags(&P.fin, hipEventDisableTiming), "q2 event");
+            slot_out = (stage_q2_rec *)P.dbuf;
+        }
         lap("buffers");
-        // the scan rows' scratch sized before any capture (scan_rows asks for the same size again)
+        // the scan rows' scratch sized before any capture (scan_dims asks for the same size again)
         (void)scratch_bytes(region->dev, reg_rows);
         (void)scratch_bytes(nation->dev, nat_rows);
         // work a caller left on the REGION / NATION tables' own streams (a call without a stream
@@ -579,52 +759,68 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         // both slots share the SUPPLIER scratch and the REGION / NATION scan rows: a batch still in
         // flight on another stream is waited for on the device before this one is enqueued (on its
         // own stream, stream order already keeps them apart)
-        for (const Q2Pending &o : stock->q2p)
-            if (o.active && o.stream != s) hip_check(hipStreamWaitEvent(s, o.ev, 0), "q2 other slot");
+        for (const Q2Pending &o : stock->q2p)  // (a split batch's kernels: its copy reads only its slot buffer)
+            if (o.active && o.stream != s) hip_check(hipStreamWaitEvent(s, o.split ? o.fin : o.ev, 0), "q2 other slot");
         // everything up to the batch's one synchronisation, enqueued on s
         auto enqueue = [&] {
             hip_check(hipMemcpyAsync(mir, pq, q_end, hipMemcpyHostToDevice, s), "h2d");
             // 1. the REGION / NATION scans
             const auto *d_zero = (const uint64_t *)(mir + q_zero);
-            const uint8_t *regs = scan_rows(region, d_zero, kRegionScan, s);
-            const uint8_t *nats = scan_rows(nation, d_zero, nat_scan, s);
+            const uint8_t *regs = nullptr, *nats = nullptr;
+            scan_dims(region, kRegionScan, nation, nat_scan, d_zero, s, &regs, &nats);
             // 2. the selection and the map segments, on the device (four kernels, no host wait)
             if (nchunks) {
                 q2_sel_count<<<(unsigned)((nchunks + 3) / 4), 256, 0, s>>>(
                     regs, region->dev.view.stride, nats, nation->dev.view.stride, name0, name1, mask0, mask1, pv,
                     facts(supplier).key_pad(), nchunks, d_map, g_vis, g_rank, g_koff, g_key, ccnt, kcnt, g_nv);
-                q2_sel_start<<<1, 1024, 0, s>>>(ccnt, kcnt, nchunks, g_nv, d_counts);
-                q2_sel_place<<<(unsigned)((nslots + 255) / 256), 256, 0, s>>>(ccnt, kcnt, nslots, g_vis, g_rank, g_koff,
-                                                                               g_key, d_map, d_sel, d_src, d_cnt, d_dst);
+                if (fused_place) {  // starts, places and the STOCK keys in one launch
+                    q2_place<<<(unsigned)((nchunks + 3) / 4), 1024, 0, s>>>(ccnt, kcnt, nchunks, g_nv, g_vis, g_rank,
+                                                                          g_koff, g_key, d_map, d_map_keys, m_max,
+                                                                          d_sel, d_src, d_cnt, d_dst, d_counts, d_keys);
+                } else {
+                    q2_sel_start<<<1, 1024, 0, s>>>(ccnt, kcnt, nchunks, g_nv, d_counts);
+                    q2_sel_place<<<(unsigned)((nslots + 255) / 256), 256, 0, s>>>(ccnt, kcnt, nslots, g_vis, g_rank,
+                                                                                   g_koff, g_key, d_map, d_sel, d_src,
+                                                                                   d_cnt, d_dst);
+                }
             }
             hip_check(hipGetLastError(), "select");
             // 3. every visited supplier's STOCK keys, one probe of them all (the counts on the device)
-            q2_gather<<<(unsigned)std::max<uint64_t>(std::min<uint64_t>(n_hint, 4096), 1), 256, 0, s>>>(
-                d_map_keys, d_src, d_dst, d_cnt, d_counts, m_max, d_keys);
+            if (!fused_place)
+                q2_gather<<<(unsigned)std::max<uint64_t>(std::min<uint64_t>(n_hint, 4096), 1), 256, 0, s>>>(
+                    d_map_keys, d_src, d_dst, d_cnt, d_counts, m_max, d_keys);
+
             // every query of the batch looks up the same STOCK keys (the visited suppliers and their
             // supp_stock_map do not depend on the read id): each key is probed once, with no read id
             // (the hit slot does not depend on it), and its visibility evaluated at every query's read
             // id inside the per-supplier fold (launch_revisit_segments: the aborts and each
             // supplier's last stock, per query)
-            if (m_max)
+            // (the misses at every read id folded into the probe where its kernel takes them;
+            // q2_reduce re-evaluates each supplier's last lookup)
+            if (m_max && probe_missed_supported(sv)) {
+                hip_check(launch_probe_missed(sv, d_keys, m_max, d_sbase, s, stock->tune, d_counts + 1, m_hint, d_rq, nq,
+                                              d_ab),
+                          "stock probe");
+            } else if (m_max) {
                 hip_check(launch_probe(sv, d_keys, nullptr, nullptr, nullptr, m_max, d_sbase, nullptr, s, stock->tune,
                                        d_counts + 1, m_hint),
                           "stock probe");
-            if (m_max)
-                hip_check(launch_revisit_segments(sv, d_sbase, m_max, d_dst, d_cnt, (uint32_t)n_max, d_rq, nq, d_slast, d_ab, s,
-                                                  d_counts + 1, d_counts),
+                hip_check(launch_revisit_segments(sv, d_sbase, m_max, nullptr, nullptr, 0, d_rq, nq, nullptr, d_ab, s,
+                                                  d_counts + 1, nullptr),
                           "stock read ids");
-            q2_reduce<<<(unsigned)((n_max * nq + 255) / 256), 256, 0, s>>>(d_slast, d_keys, d_dst, d_cnt, d_sel, sv.heap,
-                                                                           sv.hstride, facts(stock).key_pad(), d_counts,
-                                                                           nq, d_rec, d_ik);
+            }
+            q2_reduce<<<(unsigned)((n_max * nq + 255) / 256), 256, 0, s>>>(sv, d_sbase, d_rq, d_keys, d_dst, d_cnt, d_sel,
+                                                                           facts(stock).key_pad(), d_counts, nq, d_rec,
+                                                                           d_ik);
             // 4. item lookups of the last stocks (the same keys in every query: probed once, as above),
             // the I_DATA filter, the records into `out`
             hip_check(launch_probe(iv, d_ik, nullptr, nullptr, nullptr, n_max, d_ibase, nullptr, s, item->tune, d_counts,
                                    n_hint),
                       "item probe");
-            hip_check(launch_revisit(iv, d_ibase, n_max, d_rq, nq, nullptr, d_iout, s, d_counts), "item read ids");
-            q2_finish<<<(unsigned)((n_max * nq + 255) / 256), 256, 0, s>>>(d_iout, iv.heap, iv.hstride, facts(item).key_pad(),
-                                                                           d_counts, nq, d_rec, d_ab, host_out, max_out);
+            q2_finish<<<(unsigned)((n_max * nq + 255) / 256), 256, 0, s>>>(iv, d_ibase, d_rq, facts(item).key_pad(),
+                                                                           d_counts, nq, d_rec, d_ab,
+                                                                           split ? nullptr : host_out, max_out,
+                                                                           slot_out, n_max);
             hip_check(hipGetLastError(), "q2 kernels");
             hip_check(hipMemcpyAsync(pq + q_cn, d_counts, 16 + nq * 4ull, hipMemcpyDeviceToHost, s), "d2h");
         };
@@ -649,7 +845,8 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         put(&nation->scan_tune, sizeof nation->scan_tune);
         for (uint64_t v : {(uint64_t)(uintptr_t)d_map_keys, (uint64_t)target_region, (uint64_t)nq, max_out,
                            (uint64_t)(uintptr_t)host_out, (uint64_t)(uintptr_t)pq, (uint64_t)(uintptr_t)buf, q_end,
-                           n_max, m_max, n_hint, m_hint, (uint64_t)(uintptr_t)s, (uint64_t)nat_scan})
+                           n_max, m_max, n_hint, m_hint, (uint64_t)(uintptr_t)s, (uint64_t)nat_scan,
+                           (uint64_t)(uintptr_t)slot_out, (uint64_t)fused_place})
             putv(v);
         lap("key");
         Q2Graph &G = stock->q2g[slot];
@@ -691,9 +888,27 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         if (!launched) enqueue();
         lap("enqueued");
         if (async) {  // the results are read by stage_ch_query2_wait
-            Q2Pending &P = stock->q2p[slot];
             if (!P.ev) hip_check(hipEventCreateWithFlags(&P.ev, hipEventDisableTiming), "q2 event");
-            hip_check(hipEventRecord(P.ev, s), "q2 event");
+            P.split = split;
+            if (split) {  // the records cross PCIe from the side stream while s goes on
+                hip_check(hipEventRecord(P.fin, s), "q2 event");
+                hip_check(hipStreamWaitEvent(stock->q2_side, P.fin, 0), "q2 side wait");
+                // a 2-D copy (the DMA engine) of the expected count's columns -- the last call's
+                // count; wait() copies any more.  (A kernel writing the records over PCIe from the
+                // side stream slowed the next batch's kernels beside it ~4x, 0.153 ms a batch
+                // against 0.127 with the copy, r06q2emit.)
+                P.cols = std::min(n_hint, max_out);
+                if (P.cols)
+                    hip_check(hipMemcpy2DAsync(out, max_out * sizeof(stage_q2_rec), slot_out, n_max * sizeof(stage_q2_rec),
+                                               P.cols * sizeof(stage_q2_rec), nq, hipMemcpyDeviceToHost, stock->q2_side),
+                              "q2 records copy");
+                P.out = out;
+                P.max_out = max_out;
+                P.slot_out = slot_out;
+                hip_check(hipEventRecord(P.ev, stock->q2_side), "q2 event");
+            } else {
+                hip_check(hipEventRecord(P.ev, s), "q2 event");
+            }
             P.pq = pq;
             P.q_cn = q_cn;
             P.q_ab = q_ab;
@@ -808,6 +1023,12 @@ extern "C" int stage_ch_query2_wait(stage_table *stock, int slot, uint64_t *n_ou
         std::memcpy(cn, P.pq + P.q_cn, 16);
         std::memcpy(aborted, P.pq + P.q_ab, 4ull * P.nq);
         if (cn[0] > P.n_max || cn[1] > P.m_max) throw std::runtime_error("q2: device counts out of range");
+        const uint64_t want = std::min<uint64_t>(cn[0], P.max_out);
+        if (P.split && want > P.cols)  // more records than the copy expected
+            stage::hip_check(hipMemcpy2D(P.out + P.cols, P.max_out * sizeof(stage_q2_rec), P.slot_out + P.cols,
+                                         P.n_max * sizeof(stage_q2_rec), (want - P.cols) * sizeof(stage_q2_rec), P.nq,
+                                         hipMemcpyDeviceToHost),
+                             "q2 records rest");
         stock->q2_hint[0] = cn[0];
         stock->q2_hint[1] = cn[1];
         *n_out = cn[0];

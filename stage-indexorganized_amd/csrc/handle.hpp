@@ -37,11 +37,21 @@ struct Q2Graph {
 // a CH-Q2 batch enqueued by stage_ch_query2_batch_async and not yet waited for (per slot)
 struct Q2Pending {
     bool active = false;
-    hipEvent_t ev = nullptr;  // after the batch's last copy
+    hipEvent_t ev = nullptr;  // after the batch's last copy (its records' copy, when split)
     hipStream_t stream = nullptr;  // the stream it was enqueued on
     uint8_t *pq = nullptr;    // its page-locked staging: counts at q_cn, aborted flags at q_ab
     uint64_t q_cn = 0, q_ab = 0, n_max = 0, m_max = 0;
     uint32_t nq = 0;
+    // split emit (async batches into page-locked `out`): the records are finished into this
+    // slot's own device buffer and leave over PCIe by a copy on the table's q2_side stream, so
+    // the next batch's kernels run while they cross; `fin` marks the end of the batch's kernels
+    // (the shared scratch is free again), `ev` the end of the copy
+    bool split = false;
+    hipEvent_t fin = nullptr;
+    uint8_t *dbuf = nullptr;  // the records, row pitch n_max
+    uint64_t dcap = 0;
+    uint64_t cols = 0, max_out = 0;  // columns (records per query) the 2-D copy to `out` takes
+    stage_q2_rec *out = nullptr, *slot_out = nullptr;
 };
 
 struct stage_table {
@@ -60,6 +70,7 @@ struct stage_table {
     uint64_t q2_hint[2] = {0, 0};                  // CH-Q2's last visited suppliers / STOCK keys (launch shapes)
     Q2Graph q2g[2];     // per CH-Q2 slot (stage_ch_query2_batch_async); slot 0 also serves the synchronous calls
     Q2Pending q2p[2];
+    hipStream_t q2_side = nullptr;  // the split batches' record copies (created on first use)
     std::mutex pipe_mu;  // serialises stage_probe_host calls on this table
     std::unique_ptr<stage::HostPipe, stage::HostPipeDeleter> pipe;
     // the device write path hands its epoch's bookkeeping (new copy / version headers, slot
@@ -112,8 +123,13 @@ struct stage_table {
         for (int k = 0; k < 2; ++k) {
             if (q2p[k].active && q2p[k].ev) (void)hipEventSynchronize(q2p[k].ev);
             if (q2p[k].ev) (void)hipEventDestroy(q2p[k].ev);
+            if (q2p[k].fin) (void)hipEventDestroy(q2p[k].fin);
             if (q2g[k].exec) (void)hipGraphExecDestroy(q2g[k].exec);
         }
+        if (q2_side) (void)hipStreamSynchronize(q2_side);
+        for (int k = 0; k < 2; ++k)
+            if (q2p[k].dbuf) (void)hipFree(q2p[k].dbuf);
+        if (q2_side) (void)hipStreamDestroy(q2_side);
     }
 };
 

@@ -36,6 +36,15 @@ hipError_t launch_resolve(const DevTable &t, const uint64_t *keys, const uint16_
 hipError_t launch_probe(const DevTable &t, const uint64_t *keys, const uint16_t *lens, const uint32_t *rids,
                         const uint32_t *leaf_in, uint64_t n, stage_probe_out_dev *out, uint8_t *recs, hipStream_t s,
                         const ProbeTuning &tune, const uint64_t *d_n = nullptr, uint64_t shape_n = 0);
+// launch_probe with no read id (status records only) that also evaluates each hit at the read
+// ids mrids[0..mnq) and sets missed[q] when a probe produces no tuple at read id q (the miss pass
+// of launch_revisit_segments, folded in).  The lane-probe tables only (probe_missed_supported:
+// wide fixed-width keys or 8-byte keys in leaves above 128 slots, leaves of at most 256 slots);
+// otherwise hipErrorInvalidValue and nothing is launched.
+bool probe_missed_supported(const DevTable &t);
+hipError_t launch_probe_missed(const DevTable &t, const uint64_t *keys, uint64_t n, stage_probe_out_dev *out,
+                               hipStream_t s, const ProbeTuning &tune, const uint64_t *d_n, uint64_t shape_n,
+                               const uint32_t *mrids, uint32_t mnq, int32_t *missed);
 // fan-out probe (sharded front-end, dist.hip): probe i's status record and row are stored at
 // every caller position flist[k], k in [fan[i].lo, fan[i].hi) (flist null: k itself).  Tables of
 // the YCSB geometry only (fixed-width 8-byte keys, 64-slot leaves, rows <= 1024 B).
@@ -55,6 +64,13 @@ struct ScanTuning {
 hipError_t launch_scan(const DevTable &t, const uint64_t *keys, const uint16_t *lens, uint64_t n, uint32_t scan_size,
                        uint32_t *counts, uint8_t *recs, hipStream_t s, const ScanTuning &tune,
                        const uint32_t *rids = nullptr, uint8_t *row_status = nullptr);
+// two single scans (no read id) of two tables in one launch, the same records as launch_scan of
+// each (n = 1): 8-byte keys, leaves of the same size above 128 slots, 1..63 records each
+// (scan_pair_supported; otherwise hipErrorInvalidValue and nothing is launched)
+hipError_t launch_scan_pair(const DevTable &t0, const uint64_t *k0, uint32_t sz0, uint32_t *c0, uint8_t *r0,
+                            const DevTable &t1, const uint64_t *k1, uint32_t sz1, uint32_t *c1, uint8_t *r1,
+                            hipStream_t s);
+bool scan_pair_supported(const DevTable &t0, uint32_t sz0, const DevTable &t1, uint32_t sz1);
 // IndexScanExecutor range scan (fixed-width tables) kept only up to its first produced tuple
 // whose key starts with the start key's first `words` order words: img_out[i] = its heap row
 // (0xFFFFFFFF if none), st_out[i] = ST_LATEST / ST_OLD / ST_NOT_FOUND

@@ -20,10 +20,9 @@
 
 #include "kernel_api.hpp"
 #include "stage_core.hpp"
+#include "visibility.hpp"
 
 namespace stage {
-
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 __device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
@@ -230,97 +229,6 @@ __global__ __launch_bounds__(256) void resolve_kernel(DevTable t, const uint64_t
 
 // ----------------------------------------------------------------------------------------
 // point probe
-
-struct ProbeRes {
-    uint32_t status, flags, hops, slot, meta_hi, cstamp, rec_cstamp, copy_sstamp, image;  // meta_hi: meta >> 32
-};
-
-// BTree::Read + IndexScanExecutor visibility for one wave-uniform probe whose slot word
-// (meta, next, image) is already known.  FU: BTree::Read(..., is_for_update = true), the
-// writer's read of its own record: an in-flight record is read from the leaf, not from the
-// overwrite copy (b_tree.cpp:2087 takes the copy branch only when !is_for_update; the else
-// branch :2114-2120 is Record::New of the leaf image with cstamp = the reader's id and no
-// AddReader), and the executor skips PerformRead (executor.h:388) -- flag bit 2 says so.
-template <bool FU = false>
-__device__ __forceinline__ void visibility(const DevTable &t, int slot, uint64_t m, uint32_t next, uint32_t image,
-                                           uint32_t rid, ProbeRes &r) {
-    r.flags = FU ? 2u : 0u;
-    r.hops = 0;
-    r.copy_sstamp = kMaxCid;
-    r.image = 0xFFFFFFFFu;
-    r.cstamp = 0;
-    r.rec_cstamp = 0;
-    r.meta_hi = 0;
-    r.slot = 0xFFFF;
-    if (slot < 0) {
-        r.status = ST_NOT_FOUND;
-        return;
-    }
-    r.slot = (uint32_t)slot;
-    r.rec_cstamp = meta_cstamp(m);
-    r.meta_hi = (uint32_t)(m >> 32);
-    CopyHdr c = {0, kMaxCid, 0, 0};
-    const bool has_copy = (next & kNextKindMask) == kNextCopy;
-    if (has_copy) {  // PerformRead: GetOversionHeader(meta.next_ptr) != nullptr
-        c = t.chdr[next & kNextIndexMask];
-        r.flags |= 1u;
-        r.copy_sstamp = c.sstamp;
-    }
-    uint32_t img, chain;
-    bool from_copy = false;
-    if (!FU && meta_inserting(m)) {
-        if (!has_copy) {  // copy location 0 / header gone: Read returns nullptr
-            r.status = ST_NOT_FOUND;
-            return;
-        }
-        img = c.image;
-        r.cstamp = c.rstamp;
-        chain = c.next;
-        from_copy = true;
-    } else {
-        img = image;
-        r.cstamp = rid;
-        chain = next;
-    }
-    if (rid >= r.rec_cstamp) {
-        r.status = from_copy ? ST_COPY : ST_LATEST;
-        r.image = img;
-        return;
-    }
-    // older snapshot: TupleHeader chain (executor.h:407-449)
-    if ((chain & kNextKindMask) != kNextVersion) {
-        r.status = ST_CHAIN_MISS;
-        return;
-    }
-    for (uint32_t guard = 0; guard < (1u << 24); ++guard) {
-        const VersionHdr v = t.vhdr[chain & kNextIndexMask];
-        r.hops++;
-        if (v.begin_id == kInvalidCid || v.comm_id == kInvalidCid) {
-            r.status = ST_FAIL_INVALID_TS;
-            return;
-        }
-        if (rid >= v.begin_id && rid <= v.comm_id) {
-            r.status = ST_OLD;
-            r.cstamp = v.begin_id;
-            r.image = v.image;
-            return;
-        }
-        if ((v.next & kNextKindMask) != kNextVersion) break;
-        chain = v.next;
-    }
-    r.status = ST_CHAIN_MISS;
-}
-
-__device__ __forceinline__ void pack_out(uint32_t leaf, const ProbeRes &r, u32x4 &a, u32x4 &b) {
-    a.x = (r.status & 0xFF) | ((r.flags & 0xFF) << 8) | ((r.hops > 0xFFFF ? 0xFFFF : r.hops) << 16);
-    a.y = leaf;
-    a.z = (r.slot & 0xFFFF) | (meta_keylen((uint64_t)r.meta_hi << 32) << 16);
-    a.w = r.cstamp;
-    b.x = r.rec_cstamp;
-    b.y = r.copy_sstamp;
-    b.z = r.image;
-    b.w = r.meta_hi;
-}
 
 // 16-B output store at base + off (base wave-uniform).  POL 0: temporal; 1: nontemporal (the
 // line is still kept in the XCD's L2); 2: write-through (sc1 buffer store: the line leaves L2,
@@ -1145,6 +1053,23 @@ __device__ uint32_t scan_one_compact(const DevTable &t, const uint64_t *x0, uint
     return produced;
 }
 
+// one scan of scan_compact (a wave; the LDS buffers are the wave's)
+template <bool VARLEN, int SPL, int KW, bool VIS>
+__device__ __forceinline__ void scan_compact_one(const DevTable &t, const uint64_t *keys, const uint16_t *lens, uint64_t i,
+                                                 uint32_t scan_size, uint32_t *counts, uint8_t *recs,
+                                                 const uint32_t *rids, uint8_t *row_status, uint32_t lane,
+                                                 uint64_t *s_keys, uint32_t *s_len, uint32_t *s_slot) {
+    const uint32_t len = t.key_width ? t.key_width : (lens ? (uint32_t)lens[i] : 8u);
+    uint64_t ok[KW];
+    load_okey<KW>(keys, i, true, len, ok);
+    const uint32_t leaf = uni32(resolve_leaf_uniform<VARLEN, KW>(t, ok, len, true, lane));
+    RowSink<VIS> sink{recs + i * (uint64_t)scan_size * t.stride, VIS ? row_status + i * (uint64_t)scan_size : nullptr,
+                      VIS ? (rids ? rids[i] : 0xFFFFFFFEu) : 0u};
+    const uint32_t produced =
+        scan_one_compact<VARLEN, SPL, KW>(t, ok, len, leaf, scan_size, lane, sink, s_keys, s_len, s_slot);
+    if (lane == 0) counts[i] = produced;
+}
+
 template <bool VARLEN, int SPL, int KW, bool VIS>
 __global__ __launch_bounds__(256) void scan_kernel_compact(DevTable t, const uint64_t *__restrict__ keys,
                                                            const uint16_t *__restrict__ lens, uint64_t n,
@@ -1157,18 +1082,28 @@ __global__ __launch_bounds__(256) void scan_kernel_compact(DevTable t, const uin
     const uint32_t lane = lane_id(), wv = uni32(threadIdx.x >> 6);
     const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wv;
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    for (uint64_t i = wave; i < n; i += nwaves) {
-        const uint32_t len = t.key_width ? t.key_width : (lens ? (uint32_t)lens[i] : 8u);
-        uint64_t ok[KW];
-        load_okey<KW>(keys, i, true, len, ok);
-        const uint32_t leaf = uni32(resolve_leaf_uniform<VARLEN, KW>(t, ok, len, true, lane));
-        RowSink<VIS> sink{recs + i * (uint64_t)scan_size * t.stride,
-                          VIS ? row_status + i * (uint64_t)scan_size : nullptr,
-                          VIS ? (rids ? rids[i] : 0xFFFFFFFEu) : 0u};
-        const uint32_t produced = scan_one_compact<VARLEN, SPL, KW>(t, ok, len, leaf, scan_size, lane, sink,
-                                                                    s_keys[wv], s_len[wv], s_slot[wv]);
-        if (lane == 0) counts[i] = produced;
-    }
+    for (uint64_t i = wave; i < n; i += nwaves)
+        scan_compact_one<VARLEN, SPL, KW, VIS>(t, keys, lens, i, scan_size, counts, recs, rids, row_status, lane,
+                                               s_keys[wv], s_len[wv], s_slot[wv]);
+}
+
+// two single scans of two tables (the same leaf size, 8-byte keys, at most 63 records each) in
+// one launch: block 0 scans t0 from k0[0], block 1 t1 from k1[0] -- CH-Q2's REGION and NATION
+// scans, whose latency chains then overlap instead of running back to back
+template <int SPL>
+__global__ __launch_bounds__(64) void scan_pair_compact_kernel(DevTable t0, DevTable t1, const uint64_t *__restrict__ k0,
+                                                             const uint64_t *__restrict__ k1, uint32_t sz0, uint32_t sz1,
+                                                             uint32_t *__restrict__ c0, uint32_t *__restrict__ c1,
+                                                             uint8_t *__restrict__ r0, uint8_t *__restrict__ r1) {
+    __shared__ uint64_t s_keys[64];
+    __shared__ uint32_t s_len[64], s_slot[64];
+    const uint32_t lane = lane_id();
+    if (blockIdx.x == 0)
+        scan_compact_one<false, SPL, 1, false>(t0, k0, nullptr, 0, sz0, c0, r0, nullptr, nullptr, lane, s_keys, s_len,
+                                               s_slot);
+    else
+        scan_compact_one<false, SPL, 1, false>(t1, k1, nullptr, 0, sz1, c1, r1, nullptr, nullptr, lane, s_keys, s_len,
+                                               s_slot);
 }
 
 // The IndexScanExecutor range scan of `scan_size` records from key i (a wave per scan, the
@@ -1375,12 +1310,17 @@ __device__ __forceinline__ uint32_t coop_lower_bound(const DevTable &t, const ui
 // loads in flight per wave at every step instead of 4-16 (SearchRecordMeta's first hit; a probe
 // with more than three candidates falls back to a walk of the rest).  Then visibility() and the
 // rows, wave-wide, as probe_split_kernel.
-template <int SPL, int KW>
+// MISS (launch_probe_missed): the hit is also evaluated at every read id mrids[0..mnq) and a
+// probe that produces no tuple at read id q sets missed[q] -- launch_revisit_segments' miss pass
+// folded into the probe, whose slot word is already in registers.
+template <int SPL, int KW, bool MISS = false>
 __global__ __launch_bounds__(256) void probe_lane_kernel(DevTable t, const uint64_t *__restrict__ keys,
                                                          const uint32_t *__restrict__ rids,
                                                          const uint32_t *__restrict__ leaf_in, uint64_t n,
                                                          stage_probe_out_dev *__restrict__ out,
-                                                         uint8_t *__restrict__ recs, const uint64_t *__restrict__ dn) {
+                                                         uint8_t *__restrict__ recs, const uint64_t *__restrict__ dn,
+                                                         const uint32_t *__restrict__ mrids = nullptr,
+                                                         uint32_t mnq = 0, int32_t *__restrict__ missed = nullptr) {
     static_assert(SPL <= 4, "head of at most 256 slots in registers");
     __shared__ uint64_t s_x[4][64 * KW];
     __shared__ uint32_t s_node[4][64];
@@ -1457,6 +1397,12 @@ __global__ __launch_bounds__(256) void probe_lane_kernel(DevTable t, const uint6
         }
         ProbeRes r;
         visibility(t, slot, m, nx, im, rid, r);
+        if (MISS && valid)
+            for (uint32_t q = 0; q < mnq; ++q) {
+                ProbeRes rq;
+                visibility(t, slot, m, nx, im, mrids[q], rq);
+                if (rq.status != ST_LATEST && rq.status != ST_COPY && rq.status != ST_OLD) atomicOr(missed + q, 1);
+            }
         if (recs) {  // rows: wave-wide, probe by probe
             const int cnt = (int)((n - base) < 64 ? (n - base) : 64);
             for (int j = 0; j < cnt; ++j) {
@@ -1995,10 +1941,18 @@ hipError_t launch_probe(const DevTable &t, const uint64_t *keys, const uint16_t 
         // launch shape from the expected size (a device-sized batch's hint), the grid from n
         const uint64_t sn = d_n && shape_n ? std::min(shape_n, n) : n;
         const bool small = (sn + 63) / 64 < (uint64_t)kSmallBelow;  // fewer 64-probe chunks than the chip holds waves
-        const int wblocks = small ? grid_for((sn + 15) / 16, 4, tune.max_blocks > 0 ? tune.max_blocks : 16384) : blocks;
+        // tiny batches (fewer 16-probe chunks than a quarter of that, e.g. CH-Q2's ~2.5 K item
+        // lookups): 4-probe wave chunks, a quarter of the serial probes per wave
+        const bool tiny = (sn + 15) / 16 < (uint64_t)kSmallBelow / 4;
+        const int mb = tune.max_blocks > 0 ? tune.max_blocks : 16384;
+        const int wblocks = tiny ? grid_for((sn + 3) / 4, 4, mb) : small ? grid_for((sn + 15) / 16, 4, mb) : blocks;
+        // the lane kernel strides over the batch: its grid from the expected size too
+        const int lblocks = grid_for((sn + 63) / 64, 4, tune.max_blocks > 0 ? tune.max_blocks : 16384);
 #define STAGE_PROBE_W(S, KW)                                                                                  \
     if (S <= 4)                                                                                               \
-        probe_lane_kernel<(S <= 4 ? S : 4), KW><<<blocks, 256, 0, s>>>(t, keys, rids, leaf_in, n, out, recs, d_n); \
+        probe_lane_kernel<(S <= 4 ? S : 4), KW><<<lblocks, 256, 0, s>>>(t, keys, rids, leaf_in, n, out, recs, d_n); \
+    else if (tiny)                                                                                            \
+        probe_split_kernel<S, KW, 4><<<wblocks, 256, 0, s>>>(t, keys, rids, leaf_in, n, out, recs, d_n);       \
     else if (small)                                                                                           \
         probe_split_kernel<S, KW, 16><<<wblocks, 256, 0, s>>>(t, keys, rids, leaf_in, n, out, recs, d_n);      \
     else                                                                                                      \
@@ -2050,6 +2004,41 @@ hipError_t launch_probe(const DevTable &t, const uint64_t *keys, const uint16_t 
     return hipGetLastError();
 }
 
+hipError_t launch_probe_missed(const DevTable &t, const uint64_t *keys, uint64_t n, stage_probe_out_dev *out,
+                               hipStream_t s, const ProbeTuning &tune, const uint64_t *d_n, uint64_t shape_n,
+                               const uint32_t *mrids, uint32_t mnq, int32_t *missed) {
+    if (!probe_missed_supported(t)) return hipErrorInvalidValue;
+    if (n == 0) return hipSuccess;
+    const uint64_t sn = d_n && shape_n ? std::min(shape_n, n) : n;
+    const int blocks = grid_for((sn + 63) / 64, 4, tune.max_blocks > 0 ? tune.max_blocks : 16384);
+#define STAGE_PROBE_M(S, KW)                                                                                    \
+    probe_lane_kernel<S, KW, true><<<blocks, 256, 0, s>>>(t, keys, nullptr, nullptr, n, out, nullptr, d_n, mrids, \
+                                                          mnq, missed)
+#define STAGE_PROBE_MK(KW)                   \
+    switch (t.cap / 64) {                    \
+        case 1: STAGE_PROBE_M(1, KW); break; \
+        case 2: STAGE_PROBE_M(2, KW); break; \
+        default: STAGE_PROBE_M(4, KW); break; \
+    }
+    if (t.key_words == 1) {
+        STAGE_PROBE_MK(1)
+    } else if (t.key_words == 2) {
+        STAGE_PROBE_MK(2)
+    } else {
+        STAGE_PROBE_MK(4)
+    }
+#undef STAGE_PROBE_MK
+#undef STAGE_PROBE_M
+    return hipGetLastError();
+}
+
+bool probe_missed_supported(const DevTable &t) {
+    // the lane kernel's instances: wide fixed-width keys, or 8-byte keys in leaves above 128
+    // slots, in leaves of up to 256 slots
+    const bool wide = t.key_words > 1 || (t.key_width != 0 && t.cap > 128);
+    return wide && t.key_width != 0 && t.cap <= 256 && (t.cap == 64 || t.cap == 128 || t.cap == 256);
+}
+
 hipError_t launch_probe_fanout(const DevTable &t, const uint64_t *keys, const uint32_t *rids, uint64_t n,
                                const FanRange *fan, const uint32_t *flist, stage_probe_out_dev *out, uint8_t *recs,
                                hipStream_t s, const ProbeTuning &tune) {
@@ -2066,18 +2055,7 @@ bool probe_fanout_supported(const DevTable &t) {
     return t.key_width != 0 && t.key_words == 1 && t.cap == 64 && t.stride <= 1024;
 }
 
-// launch_revisit: thread per (key i, read id q); a NOT_FOUND result (no visible slot, or an
-// in-flight insert without a copy) holds for every read id and is copied as it is
-__device__ __forceinline__ void revisit_one(const DevTable &t, uint32_t rid, u32x4 &a, u32x4 &b) {
-    const uint32_t slot = a.z & 0xFFFF, leaf = a.y;
-    if ((a.x & 0xFF) != ST_NOT_FOUND && slot < t.cap && leaf < t.nleaves) {
-        const SlotInfo si = t.slot[(uint64_t)leaf * t.cap + slot];
-        ProbeRes r;
-        visibility(t, (int)slot, si.meta, si.next, si.image, rid, r);
-        pack_out(leaf, r, a, b);
-    }
-}
-
+// launch_revisit: thread per (key i, read id q), revisit_one (visibility.hpp)
 __global__ __launch_bounds__(256) void revisit_kernel(DevTable t, const stage_probe_out_dev *__restrict__ base,
                                                       uint64_t n, const uint32_t *__restrict__ rids, uint32_t nq,
                                                       const uint32_t *__restrict__ perm,
@@ -2320,6 +2298,29 @@ hipError_t launch_scan(const DevTable &t, const uint64_t *keys, const uint16_t *
         launch_scan_r<4, false>(t, keys, lens, n, scan_size, counts, recs, nullptr, nullptr, s, blocks);
     }
     return hipGetLastError();
+}
+
+hipError_t launch_scan_pair(const DevTable &t0, const uint64_t *k0, uint32_t sz0, uint32_t *c0, uint8_t *r0,
+                            const DevTable &t1, const uint64_t *k1, uint32_t sz1, uint32_t *c1, uint8_t *r1,
+                            hipStream_t s) {
+    if (!scan_pair_supported(t0, sz0, t1, sz1)) return hipErrorInvalidValue;
+#define STAGE_SCAN_P(S) scan_pair_compact_kernel<S><<<2, 64, 0, s>>>(t0, t1, k0, k1, sz0, sz1, c0, c1, r0, r1)
+    switch (t0.cap / 64) {
+        case 1: STAGE_SCAN_P(1); break;
+        case 2: STAGE_SCAN_P(2); break;
+        case 4: STAGE_SCAN_P(4); break;
+        case 8: STAGE_SCAN_P(8); break;
+        default: STAGE_SCAN_P(16);
+    }
+#undef STAGE_SCAN_P
+    return hipGetLastError();
+}
+
+bool scan_pair_supported(const DevTable &t0, uint32_t sz0, const DevTable &t1, uint32_t sz1) {
+    auto one = [](const DevTable &t, uint32_t sz) {
+        return t.key_width == 8 && t.key_words == 1 && t.cap > 128 && sz >= 1 && sz <= 63;
+    };
+    return one(t0, sz0) && one(t1, sz1) && t0.cap == t1.cap;
 }
 
 hipError_t launch_scan_first(const DevTable &t, const uint64_t *keys, uint64_t n, uint32_t scan_size,

@@ -146,6 +146,8 @@ def test_q2_batch_async_two_in_flight(ch):
     oa = stage.pinned_empty((ra.size, 1 << 14), stage.Q2_REC_DTYPE)
     ob = stage.pinned_empty((rb.size, 1 << 14), stage.Q2_REC_DTYPE)
     for rep in range(3):  # the third round replays both slots' graphs
+        oa[...] = np.zeros(1, stage.Q2_REC_DTYPE)[0]  # the records must come from this round's emit
+        ob[...] = np.zeros(1, stage.Q2_REC_DTYPE)[0]
         ja = ch.query2_batch_async(ra, oa, 0, 3)
         jb = ch.query2_batch_async(rb, ob, 1, 0)
         with pytest.raises(stage.StageError):
@@ -164,6 +166,42 @@ def test_q2_batch_async_two_in_flight(ch):
         stage.table.Q2Batch(ch.tables["stock"], 1, ob, rb.size).wait()
 
 
+def test_q2_async_split_emit_sizes(ch):
+    """Async batches finish their records into the slot's device buffer and emit them to the
+    page-locked `out` from a side stream, the emit's grid shaped by the last call's count: a batch
+    with more suppliers than the previous one (target 3 after 0 ... and back), one query and many,
+    and a narrow `out` (max_per_query below the count) each equal the synchronous batch."""
+    for rids, targets, width in ((np.array([25], np.uint32), (1, 3, 0, 3), 1 << 14),
+                                 (np.arange(3, 43, dtype=np.uint32), (3, 2), 1 << 14),
+                                 (np.array([10, 0xFFFFFFFE], np.uint32), (3,), 100)):
+        out = stage.pinned_empty((rids.size, width), stage.Q2_REC_DTYPE)
+        for t in targets:
+            out[...] = np.zeros(1, stage.Q2_REC_DTYPE)[0]
+            recs, ab = ch.query2_batch_async(rids, out, 1, t).wait()
+            srecs, sab = ch.query2_batch(rids, t)
+            assert (ab == sab).all()
+            n = min(srecs.shape[1], width)
+            assert recs.shape[1] == n and np.shares_memory(recs, out)
+            for q in range(rids.size):
+                if not ab[q]:  # the same records in the same (visit) order, the first n of them
+                    for f in FIELDS:
+                        assert (recs[q][f] == srecs[q][:n][f]).all(), (t, q, f)
+
+
+def test_q2_place_forms_agree(ch, monkeypatch):
+    """The one-launch selection placement (q2_place, SUPPLIER tables of up to 1024 chunks) and the
+    three-kernel form larger tables take (q2_sel_start, q2_sel_place, q2_gather;
+    STAGE_Q2_PLACE_CHUNKS=0 forces it here) give the same records, synchronous and batched."""
+    rids = np.array([10, 0xFFFFFFFE, 25], np.uint32)
+    got = {}
+    for lim in ("1024", "0"):
+        monkeypatch.setenv("STAGE_Q2_PLACE_CHUNKS", lim)
+        got[lim] = [ch.query2(t) for t in (0, 3)] + [ch.query2_batch(rids, 3)]
+    for (ra, aa), (rb, ab) in zip(got["1024"], got["0"]):
+        assert np.all(np.asarray(aa) == np.asarray(ab)) and ra.shape == rb.shape
+        assert (ra == rb).all()
+
+
 def test_q2_batches_on_different_streams(ch):
     """The two async slots and a synchronous batch share the tables' device scratch:
     batches enqueued on different streams while another is in flight wait for it on the device,
@@ -176,6 +214,8 @@ def test_q2_batches_on_different_streams(ch):
     oa = stage.pinned_empty((ra.size, 1 << 14), stage.Q2_REC_DTYPE)
     ob = stage.pinned_empty((rb.size, 1 << 14), stage.Q2_REC_DTYPE)
     for rep in range(3):
+        oa[...] = np.zeros(1, stage.Q2_REC_DTYPE)[0]
+        ob[...] = np.zeros(1, stage.Q2_REC_DTYPE)[0]
         ja = ch.query2_batch_async(ra, oa, 1, 3, stream=s1.ptr)
         got_c = ch.query2_batch(rc, 1, stream=s3.ptr)  # synchronous (slot 0), slot 1 busy on s1
         jb = ch.query2_batch_async(rb, ob, 0, 0, stream=s2.ptr)  # slot 1 may still be busy on s1
