@@ -510,7 +510,10 @@ int stage_ch_query2_batch(stage_table *region, stage_table *nation, stage_table 
  * The two slots (and a synchronous batch) share the tables' device scratch: a batch enqueued on
  * another stream than a batch still in flight first waits for it on the device
  * (hipStreamWaitEvent), so batches on different streams are correct but do not overlap; on one
- * stream they overlap the host's staging of the next batch with the device's run of the last. */
+ * stream they overlap the host's staging of the next batch with the device's run of the last.
+ * The records are finished into the slot's own device buffer and reach `out` by a copy on a
+ * side stream, beside the next batch's kernels; records past *n_out in a query's row of `out`
+ * are unspecified (the copy takes the previous batch's count per query, the wait the rest). */
 int stage_ch_query2_batch_async(stage_table *region, stage_table *nation, stage_table *supplier,
                                 stage_table *item, stage_table *stock, const uint32_t *map_off,
                                 const uint64_t *d_map_keys, int32_t target_region, const uint32_t *read_ids,
