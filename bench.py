@@ -121,11 +121,13 @@ def parse(argv=None):
                         "epoch's read probe (stage_set_write_overlap; the epoch inputs are resident beforehand)")
     p.add_argument("--out-stride", type=int, default=0,
                    help="caller row stride in bytes (stage_set_output_layout; 0 = the 1008-B canonical row)")
-    p.add_argument("--reply", choices=["auto", "rows", "peer"], default="auto",
+    p.add_argument("--reply", choices=["auto", "rows", "peer", "direct"], default="auto",
                    help="N > 1: how remote rows reach the caller -- rows: back over RCCL; peer: read by the caller's "
-                        "fan-out from the owners' IPC-mapped row buffers (STAGE_REPLY_PEER); auto: peer, falling back "
-                        "to rows when the runtime refuses the mapping; auto times both and reports the faster as the line's value, "
-                        "the other beside it (same results either way)")
+                        "fan-out from the owners' IPC-mapped row buffers (STAGE_REPLY_PEER); direct: written by the "
+                        "owners into the callers' IPC-mapped outputs (STAGE_REPLY_DIRECT); auto: peer, falling back "
+                        "to rows when the runtime refuses the mapping, then times rows and direct too and reports the "
+                        "fastest full reply whose sample check passed on every rank as the line's value, the others "
+                        "beside it (same results either way)")
     p.add_argument("--force-sharded", action="store_true",
                    help="run the multi-GPU (RCCL) code path even with one rank -- a rehearsal, not a config")
     p.add_argument("--dry-run", action="store_true",
@@ -440,19 +442,35 @@ def run_sharded(args, rank, world, local):
     # the reply mode of the headline: peer (rows read in place from the owners' exported buffers)
     # unless refused; the library makes every rank agree on a refusal, so all ranks fall back
     # together at the same call
-    reply_mode = {"rows": stage.REPLY_ROWS, "peer": stage.REPLY_PEER}.get(
+    reply_mode = {"rows": stage.REPLY_ROWS, "peer": stage.REPLY_PEER, "direct": stage.REPLY_DIRECT}.get(
         args.reply, stage.REPLY_PEER if world > 1 else stage.REPLY_ROWS)
     reply_note = None
-    if reply_mode == stage.REPLY_PEER:
+    if reply_mode in (stage.REPLY_PEER, stage.REPLY_DIRECT):
         rc = call(reply_mode)
         if rc != 0:
             err = L.stage_last_error().decode(errors="replace")
-            if args.reply == "peer":
-                raise SystemExit(f"[rank {rank}] peer reply: {err}")
+            if args.reply in ("peer", "direct"):
+                raise SystemExit(f"[rank {rank}] {args.reply} reply: {err}")
             reply_note = f"peer reply refused, rows over RCCL instead: {err}"
             log(f"[rank {rank}] {reply_note}")
             reply_mode = stage.REPLY_ROWS
         stream.sync()
+
+    def sample_check():
+        """8 windows of 8192 lookups spread over the batch (every exchange chunk), each against
+        its key's LoadYCSBRows row: (ok, status windows, row windows, key windows)"""
+        sample = min(B, 8192)
+        outs_w, rows_w, keys_w = [], [], []
+        for w in range(8 if B > 8 * sample else 1):
+            o = (B - sample) * w // 7 if B > 8 * sample else 0
+            outs_w.append(d_out.to_numpy(stage.PROBE_OUT_DTYPE, sample, offset=o * 32))
+            rows_w.append(d_rec.to_numpy(np.uint8, sample * tab.stride, offset=o * tab.stride).reshape(sample, tab.stride))
+            keys_w.append(draws[o:o + sample])
+        outs, rows, kw = np.concatenate(outs_w), np.concatenate(rows_w), np.concatenate(keys_w)
+        good = bool((outs["status"] == stage.ST_LATEST).all() and
+                    (rows[:, :8].copy().view(np.uint64).ravel() == kw).all() and
+                    (rows[:, 8:1008] == (kw & np.uint64(0xFF)).astype(np.uint8)[:, None]).all())
+        return good, outs_w, rows_w, keys_w
 
     def step(reply=None):
         check(call(reply_mode if reply is None else reply), "sharded")
@@ -489,6 +507,7 @@ def run_sharded(args, rank, world, local):
     owner = {"value": round(B * args.steps * world / t_own, 1), "ms_per_step": round(t_own / args.steps * 1e3, 4),
              "reply": "32-B status records to the caller, tuple rows materialised on the owner"}
     other_mode = None
+    others = {}  # the full-reply modes timed beside the line's, by name
     if reply_mode == stage.REPLY_PEER:  # the same steps with the rows back over RCCL, for comparison
         for _ in range(max(1, args.warmup)):
             step(stage.REPLY_ROWS)
@@ -512,6 +531,45 @@ def run_sharded(args, rank, world, local):
             reply_mode, elapsed, kern_ms, other_mode = stage.REPLY_ROWS, t_rows, kern_rows, ("peer_reply", peer_fig)
         else:
             other_mode = ("rows_reply", rows_fig)
+        others[other_mode[0]] = other_mode[1]
+        if args.reply == "auto" and world > 1:
+            # and the owners writing into the callers' outputs (STAGE_REPLY_DIRECT): timed, then
+            # checked on the sample windows; the line takes it only when every rank's check passed
+            d_out.memset(0)  # the check must see what the direct reply wrote (owners write only after
+            d_rec.memset(0)  # this rank's keys reached them, i.e. after these fills)
+            direct_rc = call(stage.REPLY_DIRECT)
+            stream.sync()
+            direct_ok = direct_rc == 0 and sample_check()[0]
+            if direct_rc != 0:
+                log(f"[rank {rank}] direct reply refused: {L.stage_last_error().decode(errors='replace')}")
+            if ctl.max(0.0 if direct_ok else 1.0) == 0.0:
+                for _ in range(max(1, args.warmup)):
+                    step(stage.REPLY_DIRECT)
+                stream.sync()
+                ctl.barrier()
+                t0 = time.perf_counter()
+                for i in range(args.steps):
+                    evs[2 * i].record(stream)
+                    step(stage.REPLY_DIRECT)
+                    evs[2 * i + 1].record(stream)
+                stream.sync()
+                t_dir = ctl.max(time.perf_counter() - t0)
+                kern_dir = float(np.mean([evs[2 * i].elapsed_ms(evs[2 * i + 1]) for i in range(args.steps)]))
+                direct_fig = {"value": round(B * args.steps * world / t_dir, 1),
+                              "ms_per_step": round(t_dir / args.steps * 1e3, 4),
+                              "reply": "owners write each remote row into the caller's IPC-mapped output, the "
+                                       "caller copies duplicates; 16-B tokens over RCCL"}
+                if t_dir < elapsed:
+                    mine = ("peer_reply" if reply_mode == stage.REPLY_PEER else "rows_reply",
+                            {"value": round(B * args.steps * world / elapsed, 1),
+                             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+                             "reply": peer_fig["reply"] if reply_mode == stage.REPLY_PEER else rows_fig["reply"]})
+                    others[mine[0]] = mine[1]
+                    reply_mode, elapsed, kern_ms = stage.REPLY_DIRECT, t_dir, kern_dir
+                else:
+                    others["direct_reply"] = direct_fig
+            else:
+                others["direct_reply"] = {"note": "not timed: refused or its sample check failed on some rank"}
     direct = None
     if world == 1:  # the one-rank rehearsal against the direct probe of the same batch on the same table
         for _ in range(max(1, args.warmup)):
@@ -522,21 +580,11 @@ def run_sharded(args, rank, world, local):
             tab.probe_device(d_keys.ptr, B, d_out.ptr, d_rec.ptr, stream=stream.ptr)
         stream.sync()
         direct = round((time.perf_counter() - t0) / args.steps * 1e3, 4)
+    d_out.memset(0)  # the self-check reads what the line's mode writes, not an earlier mode's rows
+    d_rec.memset(0)
     step()  # full reply again, so the self-check reads full rows
     stream.sync()
-    # self-check: 8 windows of 8192 lookups spread over the batch (every exchange chunk), each
-    # against its key's LoadYCSBRows row
-    sample = min(B, 8192)
-    outs_w, rows_w, keys_w = [], [], []
-    for w in range(8 if B > 8 * sample else 1):
-        o = (B - sample) * w // 7 if B > 8 * sample else 0
-        outs_w.append(d_out.to_numpy(stage.PROBE_OUT_DTYPE, sample, offset=o * 32))
-        rows_w.append(d_rec.to_numpy(np.uint8, sample * tab.stride, offset=o * tab.stride).reshape(sample, tab.stride))
-        keys_w.append(draws[o:o + sample])
-    outs, rows, kw = np.concatenate(outs_w), np.concatenate(rows_w), np.concatenate(keys_w)
-    ok = bool((outs["status"] == stage.ST_LATEST).all() and
-              (rows[:, :8].copy().view(np.uint64).ravel() == kw).all() and
-              (rows[:, 8:1008] == (kw & np.uint64(0xFF)).astype(np.uint8)[:, None]).all())
+    ok, outs_w, rows_w, keys_w = sample_check()
     c2_check = (draws[:4096].copy(), outs_w[0]["status"][:4096].copy(), rows_w[0][:4096].copy())
     reports = ctl.gather(rank_report(rank, loaded, setup, ok) + [float(st[k]) for k in
                                                                    ("keys", "routed", "remote", "received")])
@@ -554,7 +602,8 @@ def run_sharded(args, rank, world, local):
     step_s = elapsed / args.steps
     # HBM roofline of the step: the bytes that move on each rank (owners' probes, caller rows,
     # result copies), the busiest rank over the step time
-    hb = [sharded_hbm_bytes(sx, tab.stride, peer=reply_mode == stage.REPLY_PEER) for sx in stats]
+    hb = [sharded_hbm_bytes(sx, tab.stride, peer=reply_mode == stage.REPLY_PEER, direct=reply_mode == stage.REPLY_DIRECT)
+          for sx in stats]
     hmax = max(b for b, _ in hb)
     hbm = {"bound": "hbm", "achieved": round(hmax / step_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(hmax / step_s / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
@@ -581,9 +630,9 @@ def run_sharded(args, rank, world, local):
                    "exchange_chunks": int(os.environ.get("STAGE_SHARD_CHUNKS", 4 if world > 1 else 1)),
                    "control_plane": "the RCCL communicator (file rendezvous of the unique id)"},
         "roofline": roof, "cpu_baseline": cpu, "self_check": all(p["self_check"] for p in per_rank),
-        "reply": {stage.REPLY_PEER: "peer", stage.REPLY_ROWS: "rows"}[reply_mode],
+        "reply": {stage.REPLY_PEER: "peer", stage.REPLY_ROWS: "rows", stage.REPLY_DIRECT: "direct"}[reply_mode],
         **({"reply_note": reply_note} if reply_note else {}),
-        **({other_mode[0]: other_mode[1]} if other_mode else {}),
+        **others,
         "owner_reply": owner,
         **({"world1_vs_direct": {"sharded_ms_per_step": round(step_s * 1e3, 4), "owner_reply_ms_per_step":
                                  owner["ms_per_step"], "direct_probe_ms_per_step": direct,
@@ -712,7 +761,7 @@ def sharded_workload(world, rows_per_gpu, shared=False):
     return s
 
 
-def sharded_hbm_bytes(st, stride, row_bytes=1008, peer=False):
+def sharded_hbm_bytes(st, stride, row_bytes=1008, peer=False, direct=False):
     """Algorithmic HBM bytes of one sharded step on one rank, counting what actually moves
     (stage_sharded_stats_ex after the step: n caller keys, `routed` requests after coalescing,
     `remote` of them owned by other ranks, `received` requests this rank probed as owner):
@@ -725,11 +774,20 @@ def sharded_hbm_bytes(st, stride, row_bytes=1008, peer=False):
     row buffer and read once by the requesting rank's fan-out (from this rank's HBM, over the
     fabric) -- the same 2 x per row here; the returned results are only status records
     (remote x 2 x 32), their rows are read from the owners' HBM.
+    Direct reply (STAGE_REPLY_DIRECT): the owner writes each remote result once, straight into its
+    caller's output (counted there, in caller_rows) -- no result buffers, no returned rows; the
+    caller reads the first position's row once per duplicate caller of a remote request, estimated
+    as the batch's duplicates (n - routed) in the remote share of the requests.
     The coalescing sorts and the routing's own scratch traffic are not counted (not algorithmic)."""
     n, routed, remote, received = st["keys"], st["routed"], st["remote"], st["received"]
     own = routed - remote
     recv_remote = received - own
     out = row_bytes + 4
+    if direct:
+        parts = {"owner_probes": received * (8 + 64 + 16 + 1000), "caller_rows": n * out,
+                 "duplicate_reads": round((n - routed) * remote / max(routed, 1)) * out,
+                 "key_records": (remote + recv_remote) * 32}
+        return sum(parts.values()), parts
     parts = {"owner_probes": received * (8 + 64 + 16 + 1000), "caller_rows": n * out,
              "remote_results": recv_remote * 2 * out, "returned_results": remote * 2 * (32 if peer else out),
              "key_records": (remote + recv_remote) * 32}

@@ -558,6 +558,17 @@ int stage_probe_sharded(stage_table *t, const uint64_t *d_keys, const uint32_t *
  * rank's send counts (an allgather instead of the count all-to-all), hence where each owner put
  * each row.  d_records required; at world 1 the same as STAGE_REPLY_ROWS. */
 #define STAGE_REPLY_PEER 2
+/* STAGE_REPLY_DIRECT: what STAGE_REPLY_ROWS returns, with each owner probing a remote request
+ * straight into its caller's d_out / d_records -- status record and row at the request's first
+ * caller position, carried in the request record -- through the caller's buffers opened by IPC
+ * handle (each rank's (allocation handle, offset) pairs travel with the send counts every call;
+ * a mapping is reopened when its allocation changes).  Over RCCL only the keys go out and a 16-B
+ * token per chunk and peer comes back, after the owner's system-scope release; the caller then
+ * acquires and copies its coalesced requests' duplicates from their first positions.  The rows
+ * cross xGMI once and land once.  Tables of the YCSB geometry (8-byte keys, 64-slot leaves, rows
+ * <= 1024 B); d_records required; d_out and d_records must be IPC-exportable device memory
+ * (hipMalloc); at world 1 the same as STAGE_REPLY_ROWS. */
+#define STAGE_REPLY_DIRECT 3
 int stage_probe_sharded_ex(stage_table *t, const uint64_t *d_keys, const uint32_t *d_read_ids,
                            uint64_t n, stage_probe_out *d_out, uint8_t *d_records, int reply_mode,
                            void *stream);

@@ -6,8 +6,8 @@ transfers.  One loopback step does the HBM work all W ranks do (probes, fan-out 
 requests, result copies, fan-out of returned results) for BATCH lookups in total, i.e. what ONE
 rank does per step at W ranks for its BATCH lookups (trees of ROWS / W rows instead of ROWS;
 no xGMI).  Prints one JSON line: step ms (hipEvents), full reply (rows copied back), peer reply
-(rows read from the owners' buffers) and owner reply, and the
-request counts.  Env: ROWS (100M), W (8), BATCH (2^24), STEPS (5), CHUNKS (4)."""
+(rows read from the owners' buffers), direct reply (rows written by the owners into the callers'
+outputs, duplicates copied by the caller) and owner reply, and the request counts.  Env: ROWS (100M), W (8), BATCH (2^24), STEPS (5), CHUNKS (4)."""
 import ctypes
 import json
 import os
@@ -45,7 +45,8 @@ hs = (ctypes.c_void_p * W)(*[t.h for t in tabs])
 n_arr = (ctypes.c_uint64 * W)(*([per] * W))
 s = stage.Stream()
 res = {"rows": rows, "world": W, "batch_total": batch, "chunks": chunks, "steps": steps}
-modes = (("full_reply", stage.REPLY_ROWS), ("peer_reply", stage.REPLY_PEER), ("owner_reply", stage.REPLY_OWNER))
+modes = (("full_reply", stage.REPLY_ROWS), ("peer_reply", stage.REPLY_PEER), ("direct_reply", stage.REPLY_DIRECT),
+         ("owner_reply", stage.REPLY_OWNER))
 only = os.environ.get("MODES")  # e.g. MODES=peer_reply
 for name, reply in [m for m in modes if not only or m[0] in only.split(",")]:
     ms = []

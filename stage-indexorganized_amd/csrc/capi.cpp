@@ -807,7 +807,8 @@ int stage_probe_sharded_ex(stage_table *t, const uint64_t *d_keys, const uint32_
     int rc = need_synced(t);
     if (rc) return rc;
     if (!t->comm) return fail(STAGE_E_STATE, "stage_comm_init first");
-    if (reply_mode != STAGE_REPLY_ROWS && reply_mode != STAGE_REPLY_OWNER && reply_mode != STAGE_REPLY_PEER)
+    if (reply_mode != STAGE_REPLY_ROWS && reply_mode != STAGE_REPLY_OWNER && reply_mode != STAGE_REPLY_PEER &&
+        reply_mode != STAGE_REPLY_DIRECT)
         return fail(STAGE_E_ARG, "bad reply mode");
     return guarded([&] {
         (void)hipSetDevice(t->dev.device);
@@ -834,7 +835,8 @@ int stage_probe_sharded_loopback(stage_table *const *shards, int world, const ui
                                  const uint32_t *const *d_read_ids, const uint64_t *n, stage_probe_out *const *d_out,
                                  uint8_t *const *d_records, int reply_mode, void *stream) {
     if (!shards || world < 1 || !d_keys || !n || !d_out || !d_records) return fail(STAGE_E_ARG, "null argument");
-    if (reply_mode != STAGE_REPLY_ROWS && reply_mode != STAGE_REPLY_OWNER && reply_mode != STAGE_REPLY_PEER)
+    if (reply_mode != STAGE_REPLY_ROWS && reply_mode != STAGE_REPLY_OWNER && reply_mode != STAGE_REPLY_PEER &&
+        reply_mode != STAGE_REPLY_DIRECT)
         return fail(STAGE_E_ARG, "bad reply mode");
     for (int r = 0; r < world; ++r) {
         int rc = need_synced(shards[r]);

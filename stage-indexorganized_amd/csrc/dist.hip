@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <climits>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -40,7 +41,7 @@ __device__ __forceinline__ uint32_t rl32(uint32_t v, int l) { return (uint32_t)_
 struct alignas(16) SendRec {
     uint64_t key;
     uint32_t rid;
-    uint32_t pad;
+    uint32_t first;  // the request's first caller position (STAGE_REPLY_DIRECT's row destination)
 };
 
 __device__ __forceinline__ uint64_t mm64a_8(uint64_t k) {
@@ -130,15 +131,16 @@ __global__ __launch_bounds__(1024) void route_scan(const uint32_t *__restrict__ 
 }
 
 // send[lo + pos] = item i's key record (i in the chunk [lo, hi), pos its place in the chunk,
-// grouped by destination); perm[lo + pos] = i; fan[lo + pos] = the caller positions it serves:
-// urange[i] (coalesced: a run of flist) or {i, i + 1} (one caller, the item itself)
+// grouped by destination) with its first caller position; perm[lo + pos] = i; fan[lo + pos] =
+// the caller positions it serves: urange[i] (coalesced: a run of flist) or {i, i + 1} (one
+// caller, the item itself)
 __global__ __launch_bounds__(256) void route_scatter(const uint64_t *__restrict__ keys, const uint32_t *__restrict__ rids,
                                                      uint64_t total_max, const uint32_t *__restrict__ total_dev,
                                                      int chunk, int nchunks, int world,
                                                      const uint8_t *__restrict__ dest, const uint32_t *__restrict__ offs,
                                                      SendRec *__restrict__ send, uint32_t *__restrict__ perm,
                                                      uint32_t *__restrict__ upos, const FanRange *__restrict__ urange,
-                                                     FanRange *__restrict__ fan) {
+                                                     const uint32_t *__restrict__ flist, FanRange *__restrict__ fan) {
     __shared__ uint32_t cur[kMaxWorld];
     if (threadIdx.x < (unsigned)world) cur[threadIdx.x] = offs[threadIdx.x * gridDim.x + blockIdx.x];
     __syncthreads();
@@ -149,10 +151,11 @@ __global__ __launch_bounds__(256) void route_scatter(const uint64_t *__restrict_
     for (uint64_t i = cs.lo + b0 + threadIdx.x; i < cs.lo + b1; i += blockDim.x) {
         const uint32_t pos = (uint32_t)cs.lo + atomicAdd(&cur[dest[i]], 1u);
         const uint32_t idx = (uint32_t)i;
-        send[pos] = SendRec{keys[i], rids ? rids[i] : 0xFFFFFFFEu, 0};
+        const FanRange fr = urange ? urange[idx] : FanRange{idx, idx + 1};
+        send[pos] = SendRec{keys[i], rids ? rids[i] : 0xFFFFFFFEu, urange ? flist[fr.lo] : idx};
         perm[pos] = idx;
         if (upos) upos[idx] = pos;  // where request idx was sent (owner-reply expand)
-        fan[pos] = urange ? urange[idx] : FanRange{idx, idx + 1};
+        fan[pos] = fr;
     }
 }
 
@@ -241,11 +244,12 @@ __global__ void dd_pack(SortedKeys sk, const uint32_t *__restrict__ sidx,
 }
 
 __global__ void unpack_keys(const SendRec *__restrict__ recv, uint64_t n, uint64_t *__restrict__ keys,
-                            uint32_t *__restrict__ rids) {
+                            uint32_t *__restrict__ rids, uint32_t *__restrict__ firsts) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     keys[i] = recv[i].key;
     rids[i] = recv[i].rid;
+    if (firsts) firsts[i] = recv[i].first;
 }
 
 __device__ __forceinline__ void st_nt(u32x4 v, uint8_t *p) { __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p)); }
@@ -295,6 +299,65 @@ __global__ __launch_bounds__(256) void fan_copy(const stage_probe_out_dev *__res
                 for (uint32_t k0 = fr[r].lo; k0 < fr[r].hi; k0 += 64) {
                     const uint32_t kk = k0 + lane;
                     const uint32_t mine = k0 == fr[r].lo ? mine0[r] : kk < fr[r].hi ? (flist ? flist[kk] : kk) : 0u;
+                    const uint32_t kn = fr[r].hi - k0 < 64u ? fr[r].hi - k0 : 64u;
+                    for (uint32_t k = 0; k < kn; ++k) {
+                        const uint64_t pos = rl32(mine, (int)k);
+                        if (c < chunks) st_nt(v[r], recs + pos * stride + c * 16u);
+                        if (c0 == 0 && lane < 2) st_nt(so[r], reinterpret_cast<uint8_t *>(out + pos) + lane * 16u);
+                    }
+                }
+            }
+        }
+    }
+}
+
+// STAGE_REPLY_DIRECT, the caller's side: request p in [p0, p1) was probed by its owner straight
+// into caller position flist[fan[p].lo] (status record and row); its other caller positions
+// flist[k], k in (fan[p].lo, fan[p].hi), take copies of that position.  A wave per R requests,
+// their R rows in flight together as fan_copy; requests with one caller cost one load of fan.
+template <int R>
+__global__ __launch_bounds__(256) void dup_copy(uint64_t p0, uint64_t p1, const FanRange *__restrict__ fan,
+                                                const uint32_t *__restrict__ flist, uint32_t stride,
+                                                stage_probe_out_dev *__restrict__ out, uint8_t *__restrict__ recs) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint32_t chunks = stride >> 4;
+    for (uint64_t pb = p0 + w * R; pb < p1; pb += nw * R) {
+        FanRange fr[R];
+        uint32_t first[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            fr[r] = pb + r < p1 ? fan[pb + r] : FanRange{0u, 0u};
+            first[r] = fr[r].hi - fr[r].lo > 1 ? flist[fr[r].lo] : 0u;
+        }
+        bool any = false;
+#pragma unroll
+        for (int r = 0; r < R; ++r) any = any || fr[r].hi - fr[r].lo > 1;
+        if (!any) continue;  // wave-uniform
+        uint32_t mine0[R];
+        u32x4 so[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const bool dup = fr[r].hi - fr[r].lo > 1;
+            const uint32_t kk = fr[r].lo + 1 + lane;
+            mine0[r] = dup && kk < fr[r].hi ? flist[kk] : 0u;
+            so[r] = dup && lane < 2 ? reinterpret_cast<const u32x4 *>(out + first[r])[lane] : u32x4{0, 0, 0, 0};
+        }
+        for (uint32_t c0 = 0; c0 < chunks; c0 += 64) {
+            const uint32_t c = c0 + lane;
+            u32x4 v[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                v[r] = fr[r].hi - fr[r].lo > 1 && c < chunks
+                           ? reinterpret_cast<const u32x4 *>(recs + (uint64_t)first[r] * stride)[c]
+                           : u32x4{0, 0, 0, 0};
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                if (fr[r].hi - fr[r].lo <= 1) continue;
+                for (uint32_t k0 = fr[r].lo + 1; k0 < fr[r].hi; k0 += 64) {
+                    const uint32_t kk = k0 + lane;
+                    const uint32_t mine = k0 == fr[r].lo + 1 ? mine0[r] : kk < fr[r].hi ? flist[kk] : 0u;
                     const uint32_t kn = fr[r].hi - k0 < 64u ? fr[r].hi - k0 : 64u;
                     for (uint32_t k = 0; k < kn; ++k) {
                         const uint64_t pos = rl32(mine, (int)k);
@@ -368,6 +431,8 @@ hipError_t sort32(void *temp, size_t &bytes, const uint32_t *kin, uint32_t *kout
 
 ShardComm::~ShardComm() {
     for (void *p : opened) (void)hipIpcCloseMemHandle(p);
+    for (auto &v : dopen)
+        for (void *p : v) (void)hipIpcCloseMemHandle(p);
     for (void *p : {prow[0], prow[1], hbuf})
         if (p) (void)hipFree(p);
     if (cs) (void)hipStreamSynchronize(cs), (void)hipStreamDestroy(cs);
@@ -378,8 +443,10 @@ ShardComm::~ShardComm() {
     for (hipEvent_t e : evs) (void)hipEventDestroy(e);
     if (comm) ncclCommDestroy((ncclComm_t)comm);
     for (void *p : {dest, cursor, perm, send, recv, rout, rrec, bout, brec, cnt, lkeys, lrids, fan, dd_skeys, dd_iota,
-                    dd_sidx, dd_flag, dd_useq, uidx, ukeys, urids, upos, urange, flist, dd_cub, dd_nu, ctl})
+                    dd_sidx, dd_flag, dd_useq, uidx, ukeys, urids, upos, urange, flist, dd_cub, dd_nu, ctl, lpads,
+                    fdest})
         if (p) (void)hipFree(p);
+    if (fdest_h) (void)hipHostFree(fdest_h);
 }
 
 bool shard_default_dedupe() {
@@ -637,7 +704,8 @@ static void plan_route(ShardComm &c, Plan &P, const uint64_t *d_keys, const uint
         route_scatter<<<kRouteBlocks, 256, 0, s>>>(rkeys, rrids, n, nu, i, C, W, (const uint8_t *)c.dest, offs,
                                                    (SendRec *)c.send, (uint32_t *)c.perm,
                                                    P.dedupe && owner ? (uint32_t *)c.upos : nullptr,
-                                                   P.dedupe ? (const FanRange *)c.urange : nullptr, (FanRange *)c.fan);
+                                                   P.dedupe ? (const FanRange *)c.urange : nullptr,
+                                                   P.dedupe ? (const uint32_t *)c.flist : nullptr, (FanRange *)c.fan);
     }
     chk(hipGetLastError(), "route");
 }
@@ -683,6 +751,7 @@ static void plan_receive(ShardComm &c, Plan &P, uint32_t stride) {
         grow(c.rrec, cap * stride);
         grow(c.lkeys, cap * 8);
         grow(c.lrids, cap * 4);
+        grow(c.lpads, cap * 4);
         c.cap_remote = cap;
     }
 }
@@ -704,18 +773,21 @@ static void fan_launch(const stage_probe_out_dev *sout, const uint8_t *srec, uin
 // small launch whose latency the remote probes hide; joined by own_join); tables of other
 // geometries: probed into rout / rrec, then fanned out.  The remote segments are probed into
 // rout / rrec for the return transfer.  Owner reply: everything into rout / rrec, rows tagged
-// with their owner-local index.
+// with their owner-local index.  Direct reply: each remote segment (one per source rank q) is
+// probed in fan-out form straight into caller q's d_out / d_records (c.dpeer), each request at
+// its first caller position (c.lpads); own requests as in the full reply.
 static void chunk_probe(ShardComm &c, const Plan &P, int i, const DevTable &t, const ProbeTuning &tune, bool owner,
-                        stage_probe_out_dev *d_out, uint8_t *d_recs, hipStream_t s, uint8_t *rows_buf = nullptr) {
+                        stage_probe_out_dev *d_out, uint8_t *d_recs, hipStream_t s, uint8_t *rows_buf = nullptr,
+                        bool direct = false) {
     const int W = P.W, me = c.rank;
     const uint64_t b = P.rb[i], e = P.rb[i + 1];
     if (e == b) return;
     const uint64_t r0 = P.roff[(size_t)i * (W + 1) + me], r1 = P.roff[(size_t)i * (W + 1) + me + 1];
     const uint64_t q0 = P.soff[(size_t)i * (W + 1) + me];
     uint64_t *lk = (uint64_t *)c.lkeys;
-    uint32_t *lr = (uint32_t *)c.lrids;
+    uint32_t *lr = (uint32_t *)c.lrids, *lp = (uint32_t *)c.lpads;
     auto unpack = [&](const SendRec *src, uint64_t at, uint64_t m) {
-        if (m) unpack_keys<<<blocks_for(m, 256), 256, 0, s>>>(src, m, lk + at, lr + at);
+        if (m) unpack_keys<<<blocks_for(m, 256), 256, 0, s>>>(src, m, lk + at, lr + at, direct ? lp + at : nullptr);
     };
     unpack((const SendRec *)c.recv + b, b, r0 - b);
     unpack((const SendRec *)c.send + q0, r0, r1 - r0);
@@ -734,8 +806,18 @@ static void chunk_probe(ShardComm &c, const Plan &P, int i, const DevTable &t, c
         tag_rows<<<blocks_for(e - b, 256), 256, 0, s>>>(rout + b, e - b, (uint32_t)b);
         return;
     }
-    probe(b, r0);
-    probe(r1, e);
+    if (direct) {  // the ranks below this one, then the ranks above: one launch each (direct_tables)
+        const FanDest *fd = (const FanDest *)c.fdest + 2 * (size_t)i;
+        if (r0 > b)
+            chk(launch_probe_fanout(t, lk + b, lr + b, r0 - b, nullptr, lp + b, nullptr, nullptr, s, tune, fd),
+                "direct probe");
+        if (e > r1)
+            chk(launch_probe_fanout(t, lk + r1, lr + r1, e - r1, nullptr, lp + r1, nullptr, nullptr, s, tune, fd + 1),
+                "direct probe");
+    } else {
+        probe(b, r0);
+        probe(r1, e);
+    }
     if (r1 == r0) return;
     if (d_recs && probe_fanout_supported(t)) {
         hipStream_t os = c.ps;  // beside the remote probes (on s: slower)
@@ -933,6 +1015,154 @@ static void chunk_return_peer(ShardComm &c, const Plan &P, const PeerCounts &pc,
     }
 }
 
+// ---- STAGE_REPLY_DIRECT.  The caller's side of chunk i once every owner's token for it is in:
+// a system-scope acquire (its L2 may hold lines of d_out / d_records the owners have written
+// since), then the duplicates of each coalesced request copied from its first caller position.
+static void chunk_return_direct(ShardComm &c, const Plan &P, int i, uint32_t stride, stage_probe_out_dev *d_out,
+                                uint8_t *d_recs, hipStream_t s) {
+    const int W = P.W, me = c.rank;
+    peer_acquire_kernel<<<256, 64, 0, s>>>();
+    if (!P.dedupe) return;  // one caller per request: nothing to copy
+    constexpr int R = 4;
+    // the requests sent to other ranks: send positions [p0, q0) and [q1, pz) (own ones, [q0, q1),
+    // were probed straight to every caller position)
+    const uint64_t p0 = P.cb[i], pz = P.soff[(size_t)i * (W + 1) + W];
+    const uint64_t q0 = P.soff[(size_t)i * (W + 1) + me], q1 = P.soff[(size_t)i * (W + 1) + me + 1];
+    for (const auto &rg : {std::make_pair(p0, q0), std::make_pair(q1, pz)})
+        if (rg.second > rg.first)
+            dup_copy<R><<<(unsigned)std::min<uint64_t>((rg.second - rg.first + 4 * R - 1) / (4 * R), 8192), 256, 0, s>>>(
+                rg.first, rg.second, (const FanRange *)c.fan, (const uint32_t *)c.flist, stride, d_out, d_recs);
+    chk(hipGetLastError(), "direct duplicates");
+}
+
+// the FanDest tables of every chunk's two remote ranges -- receive positions [b, r0) from the
+// ranks below this one and [r1, e) from those above, one segment per source rank -- from the
+// plan and c.dpeer, staged in pinned memory and copied to the device on s (the staging is
+// rewritten only after the next call's count exchange has synchronised s)
+static void direct_tables(ShardComm &c, const Plan &P, hipStream_t s) {
+    const int W = P.W, C = P.C, me = c.rank;
+    const size_t bytes = (size_t)2 * kMaxChunks * sizeof(FanDest);
+    if (!c.fdest) {
+        grow(c.fdest, bytes);
+        chk(hipHostMalloc(&c.fdest_h, bytes, hipHostMallocDefault), "hipHostMalloc");
+    }
+    FanDest *h = (FanDest *)c.fdest_h;
+    for (int i = 0; i < C; ++i)
+        for (int side = 0; side < 2; ++side) {
+            FanDest &d = h[2 * i + side];
+            d.nseg = 0;
+            const int qa = side ? me + 1 : 0, qz = side ? W : me;
+            const uint64_t start = P.roff[(size_t)i * (W + 1) + qa];
+            for (int q = qa; q < qz; ++q) {
+                d.end[d.nseg] = (uint32_t)(P.roff[(size_t)i * (W + 1) + q + 1] - start);
+                d.out[d.nseg] = (stage_probe_out_dev *)c.dpeer[0][q];
+                d.recs[d.nseg] = (uint8_t *)c.dpeer[1][q];
+                ++d.nseg;
+            }
+        }
+    chk(hipMemcpyAsync(c.fdest, h, (size_t)2 * C * sizeof(FanDest), hipMemcpyHostToDevice, s), "direct tables");
+}
+
+// this rank's d_out / d_records as another process opens it: the allocation's IPC handle and the
+// buffer's offset in it; off = ~0 when the runtime refuses (reported on every rank once the pairs
+// are exchanged).  Taken on every call, not cached per pointer: memory freed and allocated again
+// at the same address gets a new handle (hipIpcGetMemHandle), which is how the other ranks see
+// that their mapping of it is stale.
+static ShardComm::DirectBuf direct_export(const void *p) {
+    ShardComm::DirectBuf b{};
+    b.off = ~0ull;
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    hipIpcMemHandle_t h;
+    if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)p) == hipSuccess && base &&
+        hipIpcGetMemHandle(&h, (void *)base) == hipSuccess) {
+        std::memcpy(b.handle, &h, sizeof b.handle);
+        b.off = (uint64_t)((const uint8_t *)p - (const uint8_t *)base);
+    } else {
+        (void)hipGetLastError();
+    }
+    return b;
+}
+
+// every rank's pairs (all[2 * q + k], the same table on every rank) -> c.dpeer.  A rank whose
+// allocation handles changed since the last call has its mappings reopened (an offset change
+// alone reuses them); when any rank's changed, every rank takes part in agreeing on the outcome
+// (an allreduce, as peer_exchange), so a refusal on one rank fails the call on all of them.
+static void direct_map(ShardComm &c, const std::vector<ShardComm::DirectBuf> &all, stage_probe_out_dev *d_out,
+                       uint8_t *d_recs, hipStream_t s) {
+    const int W = c.world;
+    for (int j = 0; j < 2 * W; ++j)
+        if (all[j].off == ~0ull)
+            throw std::runtime_error("direct reply unavailable: rank " + std::to_string(j / 2) +
+                                     " could not export its output buffers (hipIpcGetMemHandle)");
+    auto same_h = [](const ShardComm::DirectBuf &a, const ShardComm::DirectBuf &b) {
+        return std::memcmp(a.handle, b.handle, sizeof a.handle) == 0;
+    };
+    if ((int)c.dseen.size() != 2 * W) {  // nothing mapped yet
+        for (auto &v : c.dopen)
+            for (void *p : v) (void)hipIpcCloseMemHandle(p);
+        c.dopen.assign(W, {});
+        c.dbase.assign(2 * W, nullptr);
+        c.dseen.assign(2 * W, ShardComm::DirectBuf{});
+        for (auto &b : c.dseen) b.off = ~0ull;  // matches no handle below
+    }
+    std::vector<char> moved(W, 0);
+    bool any = false;
+    for (int q = 0; q < W; ++q) {
+        moved[q] = c.dseen[2 * q].off == ~0ull || !same_h(all[2 * q], c.dseen[2 * q]) ||
+                   !same_h(all[2 * q + 1], c.dseen[2 * q + 1]);
+        any = any || moved[q];
+    }
+    hipError_t e = hipSuccess;
+    for (int q = 0; q < W && !e; ++q) {
+        if (!moved[q] || q == c.rank) continue;
+        for (void *p : c.dopen[q]) (void)hipIpcCloseMemHandle(p);
+        c.dopen[q].clear();
+        c.dbase[2 * q] = c.dbase[2 * q + 1] = nullptr;
+        for (int k = 0; k < 2 && !e; ++k) {
+            if (k == 1 && same_h(all[2 * q + 1], all[2 * q])) {  // both buffers in one allocation
+                c.dbase[2 * q + 1] = c.dbase[2 * q];
+                break;
+            }
+            hipIpcMemHandle_t h;
+            std::memcpy(&h, all[2 * q + k].handle, sizeof h);
+            void *b = nullptr;
+            e = hipIpcOpenMemHandle(&b, h, hipIpcMemLazyEnablePeerAccess);
+            if (!e) {
+                c.dopen[q].push_back(b);
+                c.dbase[2 * q + k] = b;
+            } else {
+                std::fprintf(stderr, "[direct] rank %d: hipIpcOpenMemHandle(rank %d, %s) failed: %s\n", c.rank, q,
+                             k ? "d_records" : "d_out", hipGetErrorString(e));
+            }
+        }
+    }
+    if (e) (void)hipGetLastError();
+    if (any) {
+        int32_t ok = e ? 0 : 1, all_ok = 0;
+        int32_t *dok = (int32_t *)hbuf(c, 8);
+        chk(hipMemcpyAsync(dok, &ok, 4, hipMemcpyHostToDevice, s), "ok h2d");
+        nchk(ncclAllReduce(dok, dok, 1, ncclInt32, ncclMin, (ncclComm_t)c.comm, s), "ncclAllReduce ok");
+        chk(hipMemcpyAsync(&all_ok, dok, 4, hipMemcpyDeviceToHost, s), "ok d2h");
+        chk(hipStreamSynchronize(s), "ok sync");
+        if (!all_ok) {
+            for (auto &v : c.dopen)
+                for (void *p : v) (void)hipIpcCloseMemHandle(p);
+            c.dopen.assign(W, {});
+            c.dseen.clear();  // every rank: the next direct call maps afresh
+            throw std::runtime_error(std::string("direct reply unavailable: ") +
+                                     (e ? std::string("hipIpcOpenMemHandle failed on this rank: ") + hipGetErrorString(e)
+                                        : std::string("another rank could not map the output buffers")));
+        }
+    }
+    c.dseen = all;
+    for (int k = 0; k < 2; ++k) c.dpeer[k].assign(W, nullptr);
+    for (int q = 0; q < W; ++q)
+        for (int k = 0; k < 2; ++k)
+            c.dpeer[k][q] = q == c.rank ? (k ? (void *)d_recs : (void *)d_out)
+                                        : (void *)((uint8_t *)c.dbase[2 * q + k] + all[2 * q + k].off);
+}
+
 static void owner_expand(ShardComm &c, const Plan &P, stage_probe_out_dev *d_out, hipStream_t s) {
     if (!P.dedupe || P.n == 0) return;
     const int W = P.W, me = c.rank;
@@ -962,6 +1192,9 @@ int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const 
     if (!c.comm) throw std::invalid_argument("not an RCCL communicator");
     const bool owner = reply == STAGE_REPLY_OWNER;
     const bool peer = reply == STAGE_REPLY_PEER && c.world > 1 && d_recs != nullptr;
+    const bool direct = reply == STAGE_REPLY_DIRECT && c.world > 1 && d_recs != nullptr;
+    if (direct && !probe_fanout_supported(t))
+        throw std::invalid_argument("STAGE_REPLY_DIRECT: tables of the YCSB geometry (8-byte keys, 64-slot leaves, rows <= 1024 B)");
     if (owner) d_recs = nullptr;  // rows stay on the owner
     c.owner_rows = 0;
     const int W = c.world, C = c.chunks;
@@ -969,6 +1202,9 @@ int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const 
     ncclComm_t comm = (ncclComm_t)c.comm;
     Plan P;
     plan_route(c, P, d_keys, d_rids, n, stride, owner, s);
+    // direct: this device's L2 writes back its dirty lines of d_out / d_records before any owner
+    // writes them over xGMI (done before the count exchange's synchronisation below)
+    if (direct) peer_release_kernel<<<256, 64, 0, s>>>();
     uint32_t *cnt = (uint32_t *)c.cnt, *sendT = cnt + (uint64_t)C * W, *recvT = sendT + (uint64_t)C * W;
     PeerCounts pc{W, C, {}};
     if (peer) {
@@ -991,6 +1227,37 @@ int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const 
             peer_exchange(c, s);
         }
         c.parity ^= 1;
+    } else if (direct) {
+        // every rank's [C][W] send counts and its (handle, offset) of d_out / d_records in one
+        // allgather, then the coalesced request count
+        const ShardComm::DirectBuf mine[2] = {direct_export(d_out), direct_export(d_recs)};
+        const uint64_t cw = (uint64_t)C * W * 4, rec = (cw + sizeof mine + 15) & ~15ull;
+        uint8_t *d = (uint8_t *)hbuf(c, (uint64_t)(W + 1) * rec);
+        chk(hipMemcpyAsync(d, cnt, cw, hipMemcpyDeviceToDevice, s), "counts");
+        chk(hipMemcpyAsync(d + cw, mine, sizeof mine, hipMemcpyHostToDevice, s), "buffers h2d");
+        nchk(ncclAllGather(d, d + rec, rec, ncclUint8, comm, s), "ncclAllGather counts + buffers");
+        std::vector<uint8_t> h((size_t)W * rec + 4);
+        chk(hipMemcpyAsync(h.data(), d + rec, (size_t)W * rec, hipMemcpyDeviceToHost, s), "counts d2h");
+        chk(hipMemcpyAsync(h.data() + (size_t)W * rec, c.dd_nu, 4, hipMemcpyDeviceToHost, s), "nu d2h");
+        chk(hipStreamSynchronize(s), "sync");
+        auto S = [&](int q, int i, int r) {
+            uint32_t v;
+            std::memcpy(&v, h.data() + (size_t)q * rec + ((size_t)i * W + r) * 4, 4);
+            return v;
+        };
+        P.sc.resize((size_t)C * W);
+        P.rc.resize((size_t)C * W);
+        for (int i = 0; i < C; ++i)
+            for (int r = 0; r < W; ++r) {
+                P.sc[(size_t)i * W + r] = S(c.rank, i, r);
+                P.rc[(size_t)i * W + r] = S(r, i, c.rank);
+            }
+        uint32_t nu;
+        std::memcpy(&nu, h.data() + (size_t)W * rec, 4);
+        P.total = nu;
+        std::vector<ShardComm::DirectBuf> all((size_t)2 * W);
+        for (int q = 0; q < W; ++q) std::memcpy(&all[(size_t)2 * q], h.data() + (size_t)q * rec + cw, sizeof mine);
+        direct_map(c, all, d_out, d_recs, s);
     } else {
         transpose_counts<<<1, 256, 0, s>>>(cnt, C, W, sendT);
         nchk(ncclAllToAll(sendT, recvT, (size_t)C, ncclUint32, comm, s), "ncclAllToAll counts");
@@ -1008,6 +1275,7 @@ int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const 
     }
     plan_send(c, P);
     plan_receive(c, P, stride);
+    if (direct) direct_tables(c, P, s);
     hipEvent_t *ev_keys = c.evs.data(), *ev_probe = ev_keys + C, *ev_res = ev_probe + C, ev_start = ev_res[C];
     // the comm stream starts after the routing (done: s was synchronised) -- keys of all chunks
     for (int i = 0; i < C; ++i) {
@@ -1030,8 +1298,10 @@ int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const 
     const uint64_t ob = sizeof(stage_probe_out_dev);
     for (int i = 0; i < C; ++i) {
         chk(hipStreamWaitEvent(s, ev_keys[i], 0), "wait keys");
-        chunk_probe(c, P, i, t, tune, owner, d_out, d_recs, s, peer ? (uint8_t *)c.prow[c.parity] : nullptr);
-        if (peer) peer_release_kernel<<<256, 64, 0, s>>>();
+        chunk_probe(c, P, i, t, tune, owner, d_out, d_recs, s, peer ? (uint8_t *)c.prow[c.parity] : nullptr, direct);
+        // peer / direct: the rows this device stored for other ranks leave its L2 (system-scope
+        // release on every XCD) before the status records / tokens that announce them
+        if (peer || direct) peer_release_kernel<<<256, 64, 0, s>>>();
         chk(hipEventRecord(ev_probe[i], s), "event");
         chk(hipStreamWaitEvent(c.cs, ev_probe[i], 0), "wait probe");
         nchk(ncclGroupStart(), "group");
@@ -1040,6 +1310,11 @@ int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const 
             const uint32_t sn = P.sc[(size_t)i * W + r], rn = P.rc[(size_t)i * W + r];
             const uint64_t so = P.soff[(size_t)i * (W + 1) + r], ro = P.roff[(size_t)i * (W + 1) + r];
             const bool send_rows = d_recs && !peer;  // peer reply: the rows stay here, read in place
+            if (direct) {  // the results are in the callers' buffers already: a 16-B token each way
+                if (rn) nchk(ncclSend((const uint8_t *)c.rout + ro * ob, 16, ncclUint8, r, comm, c.cs), "send token");
+                if (sn) nchk(ncclRecv((uint8_t *)c.bout + so * ob, 16, ncclUint8, r, comm, c.cs), "recv token");
+                continue;
+            }
             if (rn) {
                 nchk(ncclSend((const uint8_t *)c.rout + ro * ob, (uint64_t)rn * ob, ncclUint8, r, comm, c.cs), "send out");
                 if (send_rows)
@@ -1057,6 +1332,7 @@ int shard_probe(ShardComm &c, const DevTable &t, const ProbeTuning &tune, const 
         chk(hipEventRecord(ev_res[i], c.cs), "event");
         chk(hipStreamWaitEvent(c.us, ev_res[i], 0), "wait results");
         if (peer) chunk_return_peer(c, P, pc, i, stride, d_out, d_recs, c.us);
+        else if (direct) chunk_return_direct(c, P, i, stride, d_out, d_recs, c.us);
         else chunk_return(c, P, i, stride, owner, d_out, d_recs, c.us);
     }
     if (owner) owner_expand(c, P, d_out, c.us);
@@ -1079,6 +1355,9 @@ int shard_probe_loopback(const std::vector<ShardComm *> &cs, const std::vector<c
     const uint32_t stride = ts[0]->stride;
     const bool owner = reply == STAGE_REPLY_OWNER;
     const bool peer = reply == STAGE_REPLY_PEER && W > 1 && recs[0] != nullptr;
+    const bool direct = reply == STAGE_REPLY_DIRECT && W > 1 && recs[0] != nullptr;
+    if (direct && !probe_fanout_supported(*ts[0]))
+        throw std::invalid_argument("STAGE_REPLY_DIRECT: tables of the YCSB geometry (8-byte keys, 64-slot leaves, rows <= 1024 B)");
     if (owner)
         for (auto &r : recs) r = nullptr;
     for (int r = 0; r < W; ++r)
@@ -1121,6 +1400,14 @@ int shard_probe_loopback(const std::vector<ShardComm *> &cs, const std::vector<c
             cs[r]->parity ^= 1;
         }
     }
+    if (direct)  // one process: the callers' buffers themselves
+        for (int r = 0; r < W; ++r) {
+            for (int k = 0; k < 2; ++k) {
+                cs[r]->dpeer[k].resize(W);
+                for (int q = 0; q < W; ++q) cs[r]->dpeer[k][q] = k ? (void *)recs[q] : (void *)outs[q];
+            }
+            direct_tables(*cs[r], P[r], s);
+        }
     auto copy = [&](void *dst, const void *src, uint64_t bytes, const char *what) {
         if (bytes) chk(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s), what);
     };
@@ -1136,8 +1423,8 @@ int shard_probe_loopback(const std::vector<ShardComm *> &cs, const std::vector<c
     for (int i = 0; i < C; ++i) {
         for (int r = 0; r < W; ++r)
             chunk_probe(*cs[r], P[r], i, *ts[r], tune, owner, outs[r], recs[r], s,
-                        peer ? (uint8_t *)cs[r]->prow[cs[r]->parity] : nullptr);
-        for (int q = 0; q < W; ++q)  // results: owner q's chunk-i segment for r -> r's chunk-i slots of q
+                        peer ? (uint8_t *)cs[r]->prow[cs[r]->parity] : nullptr, direct);
+        for (int q = 0; q < W && !direct; ++q)  // results: owner q's chunk-i segment for r -> r's chunk-i slots of q
             for (int r = 0; r < W; ++r) {
                 if (r == q) continue;  // as shard_probe: own results are already in place
                 const uint64_t cnt = P[q].rc[(size_t)i * W + r];
@@ -1149,6 +1436,7 @@ int shard_probe_loopback(const std::vector<ShardComm *> &cs, const std::vector<c
             }
         for (int r = 0; r < W; ++r) {
             if (peer) chunk_return_peer(*cs[r], P[r], pc, i, stride, outs[r], recs[r], s);
+            else if (direct) chunk_return_direct(*cs[r], P[r], i, stride, outs[r], recs[r], s);
             else chunk_return(*cs[r], P[r], i, stride, owner, outs[r], recs[r], s);
         }
     }

@@ -54,6 +54,22 @@ struct ShardComm {
     void *hbuf = nullptr;                // handle / count exchange scratch
     uint64_t hbuf_cap = 0;
     int parity = 0;
+    // STAGE_REPLY_DIRECT: each owner probes a remote request straight into its caller's output
+    // (status record and row at the first caller position of the request's run, carried in the
+    // request record) through the caller's d_out / d_records opened by IPC handle; the caller
+    // copies only the duplicates of its coalesced requests.  The callers' buffers change from
+    // call to call: their (handle, offset) pairs travel with the counts, and a peer's mapping is
+    // reopened when its pair changes (loopback: the other shard's pointers).
+    void *lpads = nullptr;               // [received request] its first caller position
+    void *fdest = nullptr, *fdest_h = nullptr;  // per chunk, the two remote ranges' FanDest tables (device, pinned)
+    struct DirectBuf {                   // one caller buffer as exported: allocation handle + offset
+        uint8_t handle[64];
+        uint64_t off;
+    };
+    std::vector<DirectBuf> dseen;        // [2 * rank + {out, rec}] the handles the mappings were opened for
+    std::vector<void *> dbase;           // [2 * rank + {out, rec}] their mapped allocation bases
+    std::vector<std::vector<void *>> dopen;  // [rank] its IPC mappings to close
+    std::vector<void *> dpeer[2];        // [{out, rec}][rank]: the caller buffers as mapped here
     ~ShardComm();
 };
 

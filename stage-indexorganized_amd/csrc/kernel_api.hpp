@@ -46,15 +46,26 @@ hipError_t launch_probe_missed(const DevTable &t, const uint64_t *keys, uint64_t
                                hipStream_t s, const ProbeTuning &tune, const uint64_t *d_n, uint64_t shape_n,
                                const uint32_t *mrids, uint32_t mnq, int32_t *missed);
 // fan-out probe (sharded front-end, dist.hip): probe i's status record and row are stored at
-// every caller position flist[k], k in [fan[i].lo, fan[i].hi) (flist null: k itself).  Tables of
-// the YCSB geometry only (fixed-width 8-byte keys, 64-slot leaves, rows <= 1024 B).
+// every caller position flist[k], k in [fan[i].lo, fan[i].hi) (flist null: k itself; fan null:
+// the one position flist[i]).  Tables of the YCSB geometry only (fixed-width 8-byte keys, 64-slot
+// leaves, rows <= 1024 B).
 struct alignas(8) FanRange {
     uint32_t lo, hi;
+};
+// dest (device memory, optional): the probes fall in dest->nseg consecutive segments (segment g
+// ends at probe dest->end[g], launch-relative), each with its own output buffers out[g] / recs[g]
+// in place of out / recs -- one launch for the requests of several callers (STAGE_REPLY_DIRECT)
+constexpr int kFanDests = 64;
+struct FanDest {
+    uint32_t nseg;
+    uint32_t end[kFanDests];
+    stage_probe_out_dev *out[kFanDests];
+    uint8_t *recs[kFanDests];
 };
 bool probe_fanout_supported(const DevTable &t);
 hipError_t launch_probe_fanout(const DevTable &t, const uint64_t *keys, const uint32_t *rids, uint64_t n,
                                const FanRange *fan, const uint32_t *flist, stage_probe_out_dev *out, uint8_t *recs,
-                               hipStream_t s, const ProbeTuning &tune);
+                               hipStream_t s, const ProbeTuning &tune, const FanDest *dest = nullptr);
 struct ScanTuning {
     int max_blocks = 0;  // 0 = default grid cap (16384 blocks of 256 threads)
 };

@@ -256,17 +256,32 @@ __device__ __forceinline__ void st16(u32x4 v, uint8_t *base, uint32_t off) {
 // flags | hops, cstamp, copy_sstamp, rec_cstamp -- what IndexScanExecutor and PerformRead use)
 // FAN: fan-out probes (the sharded front-end's coalesced requests, dist.hip): probe i's status
 // record and row go to every caller position flist[k], k in [fan[i].lo, fan[i].hi) (flist null:
-// the positions k themselves) instead of position i -- the row leaves registers once per
-// caller and no second pass copies it (rows of at most 1024 B, recs required).
-template <bool VARLEN, int SPL, int G, int POL = 1, int KW = 1, int CH = 64, int ST = 32, bool FAN = false>
+// the positions k themselves; fan null: {i, i + 1}, probe i's one position flist[i]) instead of
+// position i -- the row leaves registers once per caller and no second pass copies it (rows of
+// at most 1024 B, recs required).
+template <bool VARLEN, int SPL, int G, int POL = 1, int KW = 1, int CH = 64, int ST = 32, bool FAN = false,
+          bool DEST = false>
 __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *__restrict__ keys,
                                                     const uint16_t *__restrict__ lens,
                                                     const uint32_t *__restrict__ rids,
                                                     const uint32_t *__restrict__ leaf_in, uint64_t n,
                                                     stage_probe_out_dev *__restrict__ out,
                                                     uint8_t *__restrict__ recs, const FanRange *__restrict__ fan,
-                                                    const uint32_t *__restrict__ flist) {
+                                                    const uint32_t *__restrict__ flist,
+                                                    const FanDest *__restrict__ dest = nullptr) {
     const uint32_t lane = lane_id();
+    // FAN with per-segment destinations: the segment table in LDS (every thread reaches this
+    // barrier: nothing returns before it)
+    __shared__ uint32_t s_dend[DEST ? kFanDests : 1];
+    __shared__ stage_probe_out_dev *s_dout[DEST ? kFanDests : 1];
+    __shared__ uint8_t *s_drec[DEST ? kFanDests : 1];
+    uint32_t nseg = 0;
+    if constexpr (DEST) {
+        nseg = dest->nseg;
+        for (uint32_t g = threadIdx.x; g < nseg; g += blockDim.x)
+            s_dend[g] = dest->end[g], s_dout[g] = dest->out[g], s_drec[g] = dest->recs[g];
+        __syncthreads();
+    }
     // threadIdx.x / 64 made provably wave-uniform: the chunk base and the output row addresses
     // live in SGPRs (probe_kernel<.., 8>: 78 VGPRs, 6 waves/SIMD, instead of 95 and 5)
     const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + uni32(threadIdx.x >> 6);
@@ -279,7 +294,14 @@ __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *
         const uint32_t len = t.key_width ? t.key_width : (lens && valid ? (uint32_t)lens[i] : 8u);
         const uint32_t rid = rids ? (valid ? rids[i] : 0u) : 0xFFFFFFFEu;
         FanRange my_fan = FanRange{0u, 0u};
-        if (FAN && valid) my_fan = fan[i];
+        if (FAN && valid) my_fan = fan ? fan[i] : FanRange{(uint32_t)i, (uint32_t)i + 1u};
+        uint64_t my_o = 0, my_r = 0;  // DEST: this lane's probe's segment's buffers
+        if constexpr (DEST) {
+            uint32_t sg = 0;
+            for (uint32_t g = 0; g + 1 < nseg; ++g) sg += i >= s_dend[g] ? 1u : 0u;
+            my_o = (uint64_t)s_dout[sg];
+            my_r = (uint64_t)s_drec[sg];
+        }
         uint64_t ok[KW];
         load_okey<KW>(keys, i, valid, len, ok);
         uint32_t leaf = 0;
@@ -425,14 +447,20 @@ __global__ __launch_bounds__(256) void probe_kernel(DevTable t, const uint64_t *
                     pack_out(lf[g], r[g], a, b);
                     const u32x4 half = lane == 0 ? a : b;
                     const uint32_t lo = rl32(my_fan.lo, j), hi = rl32(my_fan.hi, j);
+                    stage_probe_out_dev *o_j = out;
+                    uint8_t *r_j = recs;
+                    if constexpr (DEST) {  // probe j's segment's buffers (wave-uniform: scalar registers)
+                        o_j = reinterpret_cast<stage_probe_out_dev *>(rl64(my_o, j));
+                        r_j = reinterpret_cast<uint8_t *>(rl64(my_r, j));
+                    }
                     for (uint32_t k0 = lo; k0 < hi; k0 += 64) {
                         const uint32_t kk = k0 + lane;
                         const uint32_t mine = k0 == lo ? mine0[g] : kk < hi ? (flist ? flist[kk] : kk) : 0u;
                         const uint32_t kn = hi - k0 < 64u ? hi - k0 : 64u;
                         for (uint32_t k = 0; k < kn; ++k) {
                             const uint64_t pos = rl32(mine, (int)k);
-                            if (lane < out_chunks) st16<POL>(v[g], recs + pos * (uint64_t)t.stride, lane * 16u);
-                            if (lane < 2) st16<POL>(half, reinterpret_cast<uint8_t *>(out + pos), lane * 16u);
+                            if (lane < out_chunks) st16<POL>(v[g], r_j + pos * (uint64_t)t.stride, lane * 16u);
+                            if (lane < 2) st16<POL>(half, reinterpret_cast<uint8_t *>(o_j + pos), lane * 16u);
                         }
                     }
                 }
@@ -2041,13 +2069,17 @@ bool probe_missed_supported(const DevTable &t) {
 
 hipError_t launch_probe_fanout(const DevTable &t, const uint64_t *keys, const uint32_t *rids, uint64_t n,
                                const FanRange *fan, const uint32_t *flist, stage_probe_out_dev *out, uint8_t *recs,
-                               hipStream_t s, const ProbeTuning &tune) {
+                               hipStream_t s, const ProbeTuning &tune, const FanDest *dest) {
     if (!probe_fanout_supported(t)) return hipErrorInvalidValue;
     if (n == 0) return hipSuccess;
-    if (!recs || !fan) return hipErrorInvalidValue;
+    if ((!recs && !dest) || (!fan && !flist)) return hipErrorInvalidValue;
     const int blocks = grid_for((n + 63) / 64, 4, tune.max_blocks > 0 ? tune.max_blocks : 16384);
-    probe_kernel<false, 1, 8, 1, 1, 64, 32, true><<<blocks, 256, 0, s>>>(t, keys, nullptr, rids, nullptr, n, out, recs,
-                                                                         fan, flist);
+    if (dest)
+        probe_kernel<false, 1, 4, 1, 1, 64, 32, true, true><<<blocks, 256, 0, s>>>(t, keys, nullptr, rids, nullptr, n,
+                                                                                   out, recs, fan, flist, dest);
+    else
+        probe_kernel<false, 1, 8, 1, 1, 64, 32, true><<<blocks, 256, 0, s>>>(t, keys, nullptr, rids, nullptr, n, out,
+                                                                             recs, fan, flist);
     return hipGetLastError();
 }
 

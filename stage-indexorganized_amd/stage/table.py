@@ -699,7 +699,7 @@ class Reader:
             pass
 
 
-REPLY_ROWS, REPLY_OWNER, REPLY_PEER = 0, 1, 2  # stage_hip.h STAGE_REPLY_*
+REPLY_ROWS, REPLY_OWNER, REPLY_PEER, REPLY_DIRECT = 0, 1, 2, 3  # stage_hip.h STAGE_REPLY_*
 
 
 def owner_rows(table, loopback=True):

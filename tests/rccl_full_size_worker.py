@@ -89,8 +89,8 @@ def main():
     d_out = stage.DeviceBuffer(nk * 32)
     d_rec = stage.DeviceBuffer(nk * shard.stride)
     ok = True
-    for reply in (stage.REPLY_ROWS, stage.REPLY_OWNER, stage.REPLY_PEER):
-        name = {stage.REPLY_OWNER: "owner", stage.REPLY_PEER: "peer"}.get(reply, "rows")
+    for reply in (stage.REPLY_ROWS, stage.REPLY_OWNER, stage.REPLY_PEER, stage.REPLY_DIRECT):
+        name = {stage.REPLY_OWNER: "owner", stage.REPLY_PEER: "peer", stage.REPLY_DIRECT: "direct"}.get(reply, "rows")
         times = []
         for it in range(3):  # the first call grows the exchange buffers; all three are checked alike
             stage.comm_allreduce(shard, [1.0])  # barrier

@@ -91,12 +91,16 @@ def main():
     # (chunks, dedupe, read ids, reply, batch size): rank world-1 probes nothing in one case (it
     # still takes part in every exchange)
     # STAGE_REPLY_PEER: rows read through the owners' IPC-mapped row buffers (two parities: the
-    # case runs its probe twice, as every case does)
+    # case runs its probe twice, as every case does); STAGE_REPLY_DIRECT: the owners write into
+    # the callers' IPC-mapped outputs (each case allocates new ones: the mappings move with them)
     cases = [(1, 1, True, stage.REPLY_ROWS, 60_000), (4, 1, True, stage.REPLY_ROWS, 90_000),
              (3, 0, False, stage.REPLY_ROWS, 40_000), (4, 1, False, stage.REPLY_OWNER, 50_000),
              (2, 1, True, stage.REPLY_ROWS, 0 if rank == world - 1 else 30_000),
-             (4, 1, True, stage.REPLY_PEER, 80_000), (2, 0, False, stage.REPLY_PEER, 0 if rank == 0 else 35_000)]
+             (4, 1, True, stage.REPLY_PEER, 80_000), (2, 0, False, stage.REPLY_PEER, 0 if rank == 0 else 35_000),
+             (4, 1, True, stage.REPLY_DIRECT, 80_000), (2, 0, False, stage.REPLY_DIRECT, 0 if rank == 1 else 35_000),
+             (3, 1, False, stage.REPLY_DIRECT, 45_000)]
     for ci, (chunks, dedupe, use_rids, reply, size) in enumerate(cases):
+        print(f"[case {ci}] reply {reply}, chunks {chunks}, dedupe {dedupe}, keys {size}", flush=True)
         check(L.stage_set_shard_chunks(shard.h, chunks), "chunks")
         stage.set_shard_dedupe(shard, dedupe)
         if size:
@@ -117,7 +121,8 @@ def main():
             check(L.stage_device_sync(), "sync")
         st = stage.sharded_stats_ex(shard)
         case = {"case": ci, "chunks": chunks, "dedupe": dedupe, "read_ids": use_rids,
-                "reply": {stage.REPLY_OWNER: "owner", stage.REPLY_PEER: "peer"}.get(reply, "rows"), "keys": nk,
+                "reply": {stage.REPLY_OWNER: "owner", stage.REPLY_PEER: "peer",
+                          stage.REPLY_DIRECT: "direct"}.get(reply, "rows"), "keys": nk,
                 "stats": {kk: int(v) for kk, v in st.items()} if isinstance(st, dict) else str(st)}
         good = True
         if nk:

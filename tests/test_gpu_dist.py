@@ -55,10 +55,13 @@ def shard_tables(keys, world, mode=1, payload=1000):
 
 
 @pytest.mark.parametrize("world,chunks,dedupe,reply", [(2, 1, 1, 0), (3, 4, 1, 0), (8, 7, 1, 0), (3, 4, 0, 0),
-                                                        (2, 1, 1, 2), (3, 4, 1, 2), (8, 7, 1, 2), (3, 4, 0, 2)])
+                                                        (2, 1, 1, 2), (3, 4, 1, 2), (8, 7, 1, 2), (3, 4, 0, 2),
+                                                        (2, 1, 1, 3), (3, 4, 1, 3), (8, 7, 1, 3), (3, 4, 0, 3)])
 def test_sharded_data_path_loopback_equals_single_table(gpu, world, chunks, dedupe, reply):
     # reply 2 = STAGE_REPLY_PEER: status records travel back, each row is read by the caller's
-    # fan-out where its owner left it (here: the other shard's row buffer in place of an IPC map)
+    # fan-out where its owner left it (here: the other shard's row buffer in place of an IPC map);
+    # reply 3 = STAGE_REPLY_DIRECT: each owner probes a remote request straight into its
+    # caller's output at the request's first caller position, the caller copies the duplicates
     # the multi-GPU data path (routing, count exchange, all-to-all-v offsets, local probes,
     # reverse exchange, un-permutation) with W shards on one device, against one table
     # holding every key; version chains on some keys so statuses and rows vary
@@ -89,7 +92,7 @@ def test_sharded_data_path_loopback_equals_single_table(gpu, world, chunks, dedu
                 if s else np.zeros(0, np.uint64) for s in sizes]
     per_rids = [rng.integers(0, 14, k.size).astype(np.uint32) for k in per_keys]
     res = stage.probe_sharded_loopback(tabs, per_keys, per_rids, reply=reply)
-    if reply == stage.REPLY_PEER:  # a second call: the other parity of the row buffers
+    if reply in (stage.REPLY_PEER, stage.REPLY_DIRECT):  # a second call: the other parity / fresh buffers
         res = stage.probe_sharded_loopback(tabs, per_keys, per_rids, reply=reply)
     for r in range(world):
         out, rows = res[r]
@@ -208,7 +211,8 @@ def test_request_coalescing_zipf_batch(gpu, read_ids):
 
 
 @pytest.mark.parametrize("world,chunks,payload,reply", [(2, 1, 1000, 0), (3, 3, 1000, 0), (3, 2, 100, 0),
-                                                         (3, 3, 1000, 2), (3, 2, 100, 2)])
+                                                         (3, 3, 1000, 2), (3, 2, 100, 2), (2, 1, 1000, 3),
+                                                         (3, 3, 1000, 3), (3, 2, 100, 3)])
 def test_hot_keys_and_other_geometries_loopback(gpu, world, chunks, payload, reply):
     # one key asked 10,000 times in a batch (its run is cut into requests of <= 64 callers, each
     # fanned out), a few keys a few hundred times, read ids interleaved; payload 100 = leaves of
@@ -231,6 +235,12 @@ def test_hot_keys_and_other_geometries_loopback(gpu, world, chunks, payload, rep
         perm = rng.permutation(k.size)
         per_keys.append(k[perm])
         per_rids.append(rng.integers(1, 4, k.size).astype(np.uint32))
+    if reply == stage.REPLY_DIRECT and payload != 1000:  # outside the fan-out probe's geometry: refused
+        with pytest.raises(stage.StageError):
+            stage.probe_sharded_loopback(tabs, per_keys, per_rids, reply=reply)
+        for t in tabs:
+            stage.set_shard_dedupe(t, -1)
+        return
     res = stage.probe_sharded_loopback(tabs, per_keys, per_rids, reply=reply)
     for r in range(world):
         out, rows = res[r]

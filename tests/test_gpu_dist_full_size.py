@@ -90,6 +90,16 @@ def test_c5_loopback_at_size_equals_one_table(gpu):
             assert (out[f] == ref_out[f]).all(), (r, f)
         assert (rows == ref_rows).all(), r
     del res
+    # 3c. direct reply: each owner writes its rows into the callers' outputs (STAGE_REPLY_DIRECT)
+    res = stage.probe_sharded_loopback(tabs, per_keys, None, reply=stage.REPLY_DIRECT)
+    _say(t0, "sharded probe, direct mode")
+    for r in range(W):
+        out, rows = res[r]
+        ref_out, ref_rows = ref[r]
+        for f in fields:
+            assert (out[f] == ref_out[f]).all(), (r, f)
+        assert (rows == ref_rows).all(), r
+    del res
     # 4. rows left at their owners, status records back (each carries the owner-local row index)
     res = stage.probe_sharded_loopback(tabs, per_keys, None, records=True, reply=stage.REPLY_OWNER)
     _say(t0, "sharded probe, owner mode")

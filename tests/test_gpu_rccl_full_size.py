@@ -5,9 +5,10 @@ one MI355X allows -- the data path at C5's per-rank batch over a REAL 8-rank RCC
 interface, tests/rccl_rank_worker.py) and form one communicator; rank r holds the 12.5M rows of
 a 100M-key table with MurmurHash64A(key, 8, 0) % 8 == r and probes its 2^21-key Zipf-0.9 batch
 (drawn over all 100M keys) with stage_probe_sharded_ex -- the counts ncclAllToAll, the 8-peer
-grouped ncclSend / ncclRecv and the fan-out of returned rows all execute -- in the three reply
+grouped ncclSend / ncclRecv and the fan-out of returned rows all execute -- in the four reply
 modes (rows back over RCCL, rows left at the owner, rows read by the caller from the owner's
-IPC-mapped row buffers: STAGE_REPLY_PEER).
+IPC-mapped row buffers: STAGE_REPLY_PEER, rows written by the owner into the caller's
+IPC-mapped output: STAGE_REPLY_DIRECT).
 The reference is ONE 100M-row table's direct probe of the same keys, taken first (in this
 process, then released) and saved: every status field and every row (64-bit digest) must match.
 Per-rank step times are in the reports; they are not a scaling point (8 ranks share one GPU and
@@ -69,7 +70,7 @@ def test_c5_rccl_8_ranks_at_size(gpu):
                                    outs[r][-2000:])
             assert rep["all_ranks_ok"] and rcs[r] == 0
         for rep in reports:
-            assert [c["reply"] for c in rep["cases"]] == ["rows", "owner", "peer"]
+            assert [c["reply"] for c in rep["cases"]] == ["rows", "owner", "peer", "direct"]
             rows_case = rep["cases"][0]
             assert rows_case["stats"]["remote"] > 0 and rows_case["stats"]["received"] > 0
             print(json.dumps({"rank": rep["rank"], "rows": rep["rows"],

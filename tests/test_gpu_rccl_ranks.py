@@ -64,9 +64,12 @@ def test_sharded_probe_over_rccl_ranks(gpu, world):
             path = os.path.join(d, f"rank{r}.json")
             assert os.path.exists(path), f"rank {r} wrote no report (exit {rcs[r]}):\n{outs[r][-3000:]}"
             reports.append(json.load(open(path)))
+        # every failing rank's last error line and its library diagnostics, not only the first rank's
+        bad = [(r, (rep.get("error") or "").strip().splitlines()[-1:], [c for c in rep.get("cases", []) if not c["ok"]],
+                [ln for ln in outs[r].splitlines() if ln.startswith("[") or "IPC" in ln][-6:])
+               for r, rep in enumerate(reports) if not rep.get("ok")]
+        assert not bad, bad
         for r, rep in enumerate(reports):
-            assert rep.get("ok"), (r, rep.get("error"), [c for c in rep.get("cases", []) if not c["ok"]],
-                                   outs[r][-2000:])
             assert rep["all_ranks_ok"]
             assert rcs[r] == 0
         # the exchange carried requests between the processes
@@ -94,4 +97,8 @@ def test_bench_multi_rank_line_over_rccl(gpu):
     assert [p["rank"] for p in line["per_rank"]] == [0, 1] and all(p["self_check"] for p in line["per_rank"])
     assert line["coalescing"]["remote_requests"] > 0
     assert line["rccl"]["runtime"] > 0
-    print(json.dumps({k: line[k] for k in ("value", "ms_per_step", "owner_reply", "coalescing", "rccl")}))
+    # auto: every full-reply mode was timed (or its refusal noted); the line names the fastest
+    replies = {"peer": "peer_reply", "rows": "rows_reply", "direct": "direct_reply"}
+    assert line["reply"] in replies and all(v in line for k, v in replies.items() if k != line["reply"]), line
+    print(json.dumps({k: line.get(k) for k in ("value", "ms_per_step", "reply", "peer_reply", "rows_reply",
+                                               "direct_reply", "owner_reply", "coalescing", "rccl")}))
