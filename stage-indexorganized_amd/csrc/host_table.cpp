@@ -16,6 +16,7 @@
 #include <cstring>
 #include <stdexcept>
 #include <thread>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -235,7 +236,7 @@ void HostTable::adopt_device_epoch(const CopyHdr *copies, const uint32_t *writer
         room(ssn_.e, nc);  // not reserve(c0 + nc): an exact reserve reallocates every epoch
         // the epoch's copies are c0 .. c0 + nc - 1: their SSN state goes at the same ids
         if (ssn_.e.size() > c0) throw std::runtime_error("adopt_device_epoch: SSN state ahead of the copies");
-        ssn_.e.resize(c0 + nc, CopySsn{0, 0, 0, kMaxCid, 0, 0, 0});
+        ssn_.e.resize(c0 + nc);  // uninitialised (HugeAllocNoInit): every entry is written below, in parallel
         CopySsn *dst = ssn_.e.data() + c0;
         parallel_chunks(nc, [&](uint64_t b, uint64_t e) {
             for (uint64_t k = b; k < e; ++k) {
@@ -254,10 +255,15 @@ void HostTable::adopt_device_epoch(const CopyHdr *copies, const uint32_t *writer
         });
     }
     lap("images");
-    // one slot word per touched record (distinct indices): scattered writes in parallel
-    for (uint64_t k = 0; k < nslots; ++k)
-        if (slots[k].idx != ~0ull && slots[k].idx >= meta_.size())
-            throw std::runtime_error("adopt_device_epoch: slot index outside the table");
+    // one slot word per touched record (distinct indices): scattered writes in parallel, after a
+    // parallel bounds check of every index
+    std::atomic<bool> bad{false};
+    const uint64_t nmeta = meta_.size();
+    parallel_chunks(nslots, [&](uint64_t b, uint64_t e) {
+        for (uint64_t k = b; k < e; ++k)
+            if (slots[k].idx != ~0ull && slots[k].idx >= nmeta) bad.store(true, std::memory_order_relaxed);
+    });
+    if (bad.load()) throw std::runtime_error("adopt_device_epoch: slot index outside the table");
     parallel_chunks(nslots, [&](uint64_t b, uint64_t e) {
         for (uint64_t k = b; k < e; ++k) {
             const SlotWords &w = slots[k];

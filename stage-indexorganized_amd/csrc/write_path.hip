@@ -302,7 +302,9 @@ constexpr int kFinishChunks = 8;
 constexpr uint32_t kJumpFrom = 128;  // ops from the first failure on: pointer jumping (wp_jump_*; 128 from the r05 sweep)
 // Groups with at least big_from ops from their first failure on go to `list` instead (one
 // atomic per big group; their finishing kernels follow).
-__global__ __launch_bounds__(256) void wp_finish_groups(WpArgs a, WpCls kc, DevTable t, uint8_t *__restrict__ rcs,
+// (<= 80 VGPRs, amdgpu_waves_per_eu(6): a retired read-probe wave's registers fit one of its
+// waves, so it runs beside C3's probe -- at 91 VGPRs it waited for the probe's last dispatch)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void wp_finish_groups(WpArgs a, WpCls kc, DevTable t, uint8_t *__restrict__ rcs,
                                                         uint8_t *__restrict__ succ, int32_t *__restrict__ prev,
                                                         const uint32_t *__restrict__ first_fail,
                                                         const uint32_t *__restrict__ gend, uint32_t big_from,
@@ -386,19 +388,26 @@ __global__ __launch_bounds__(256) void wp_finish_groups(WpArgs a, WpCls kc, DevT
     }
 }
 
+// The big-group kernels' workgroups (wp_jump_chain, finish_big_walk inside it): 256 threads, so
+// that they are dispatched beside C3's read probe, whose 256-thread workgroups fill every CU --
+// a larger workgroup needs several retired probe workgroups on one CU at once and waits for the
+// probe's last dispatch (round 6; 1024 threads before).
+constexpr uint32_t kJumpThreads = 256, kJumpWaves = kJumpThreads / 64;
+
 // step 3b for big groups, the walk (round 4; now the fallback of the pointer jumping when a
-// candidate's writer is older than the commit): one 1024-thread workgroup per group, 16 waves x kFinishChunks x 64 = 8192 ops evaluated against
-// the last success per pass, the first success in batch order found across the waves through
-// LDS.  Serial in the group's failures: ~700 passes for a Zipf-0.99 hot key on RunMixed's stream.
+// candidate's writer is older than the commit): one workgroup per group, kJumpWaves waves x
+// kFinishChunks x 64 ops evaluated against the last success per pass, the first success in batch
+// order found across the waves through LDS.  Serial in the group's failures: ~700 passes for a
+// Zipf-0.99 hot key on RunMixed's stream.
 __device__ void finish_big_walk(const WpArgs &a, const WpCls &kc, const DevTable &t, uint8_t *__restrict__ rcs,
                                 uint8_t *__restrict__ succ, int32_t *__restrict__ prev, uint64_t g, uint64_t end,
                                 uint64_t f, const SlotInfo &base, uint64_t *s_first) {
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    constexpr uint64_t kPass = 16ull * kFinishChunks * 64;
+    constexpr uint64_t kPass = (uint64_t)kJumpWaves * kFinishChunks * 64;
     int64_t last = f > g ? (int64_t)f - 1 : -1;  // [g, f) all succeeded
     uint64_t pos = f;
     while (pos < end) {
-        // a pass: up to kFinishChunks slices of 1024 ops (one 64-op chunk per wave), evaluated
+        // a pass: up to kFinishChunks slices of kJumpThreads ops (one 64-op chunk per wave), evaluated
         // against the last success slice by slice until one holds a success -- behind a
         // single failure the next op usually succeeds, so most passes take one slice
         uint64_t bf = ~0ull, done = pos;
@@ -414,13 +423,13 @@ __device__ void finish_big_walk(const WpArgs &a, const WpCls &kc, const DevTable
             if (lane == 0) s_first[wv] = wf;
             __syncthreads();
 #pragma unroll
-            for (int w = 0; w < 16; ++w) bf = s_first[w] < bf ? s_first[w] : bf;
+            for (uint32_t w = 0; w < kJumpWaves; ++w) bf = s_first[w] < bf ? s_first[w] : bf;
             if (q < end && q <= bf) {
                 rcs[q] = r;
                 succ[q] = q == bf;
                 prev[q] = (int32_t)last;
             }
-            done += 1024;
+            done += kJumpThreads;
         }
         if (bf != ~0ull) {
             // as wp_finish_groups: the speculative outcomes behind a success stand up to
@@ -441,7 +450,7 @@ __device__ void finish_big_walk(const WpArgs &a, const WpCls &kc, const DevTable
                 if (lane == 0) s_first[wv] = mf;
                 __syncthreads();
 #pragma unroll
-                for (int w = 0; w < 16; ++w) nf = s_first[w] < nf ? s_first[w] : nf;
+                for (uint32_t w = 0; w < kJumpWaves; ++w) nf = s_first[w] < nf ? s_first[w] : nf;
             }
             if (nf == ~0ull) break;
             last = (int64_t)nf - 1;
@@ -535,7 +544,7 @@ __global__ __launch_bounds__(256) void wp_jump_links(WpArgs a, WpCls kc, const u
     }
 }
 
-__global__ __launch_bounds__(1024) void wp_jump_chain(WpArgs a, WpCls kc, DevTable t, uint8_t *__restrict__ rcs,
+__global__ __launch_bounds__(kJumpThreads) __attribute__((amdgpu_waves_per_eu(6))) void wp_jump_chain(WpArgs a, WpCls kc, DevTable t, uint8_t *__restrict__ rcs,
                                                       uint8_t *__restrict__ succ, int32_t *__restrict__ prev,
                                                       const uint32_t *__restrict__ first_fail,
                                                       const uint32_t *__restrict__ gend,
@@ -544,10 +553,10 @@ __global__ __launch_bounds__(1024) void wp_jump_chain(WpArgs a, WpCls kc, DevTab
                                                       const uint32_t *__restrict__ jx, const uint64_t *__restrict__ jm,
                                                       uint64_t *__restrict__ ci, uint32_t *__restrict__ gst,
                                                       const uint8_t *__restrict__ junr) {
-    constexpr uint32_t kSpanChunks = 64, kSpan = kSpanChunks * 64;  // 4096 positions, 48 KB a buffer
+    constexpr uint32_t kSpanChunks = 16, kSpan = kSpanChunks * 64;  // 1024 positions, 12 KB a buffer
     __shared__ uint32_t s_jx[2][kSpan];
     __shared__ uint64_t s_jm[2][kSpan];
-    __shared__ uint64_t s_first[16];
+    __shared__ uint64_t s_first[kJumpWaves];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t nbig = *count;
     for (uint32_t i = blockIdx.x; i < nbig; i += gridDim.x) {
@@ -560,7 +569,7 @@ __global__ __launch_bounds__(1024) void wp_jump_chain(WpArgs a, WpCls kc, DevTab
             start = f - 1;
         } else {  // the head failed: the first op that succeeds against the epoch-start state
             start = ~0ull;
-            for (uint64_t done = g; done < end && start == ~0ull; done += 1024) {
+            for (uint64_t done = g; done < end && start == ~0ull; done += kJumpThreads) {
                 const uint64_t q = done + (uint64_t)wv * 64 + lane;
                 const uint8_t r = q < end ? wp_eval(a, kc, t, q, g, -1, base) : (uint8_t)0xFF;
                 uint64_t wf = r == STAGE_RC_OK ? q : ~0ull;
@@ -573,7 +582,7 @@ __global__ __launch_bounds__(1024) void wp_jump_chain(WpArgs a, WpCls kc, DevTab
                 __syncthreads();
                 uint64_t bf = ~0ull;
 #pragma unroll
-                for (int w = 0; w < 16; ++w) bf = s_first[w] < bf ? s_first[w] : bf;
+                for (uint32_t w = 0; w < kJumpWaves; ++w) bf = s_first[w] < bf ? s_first[w] : bf;
                 if (q < end && q <= bf) {
                     rcs[q] = r;
                     succ[q] = q == bf;
@@ -590,7 +599,7 @@ __global__ __launch_bounds__(1024) void wp_jump_chain(WpArgs a, WpCls kc, DevTab
             continue;
         }
         // B. the chain, chunk to chunk, over absolute chunks, the
-        // exits and masks staged through LDS a span of kSpanChunks chunks at a time: waves 1-15
+        // exits and masks staged through LDS a span of kSpanChunks chunks at a time: waves 1..
         // fill the next span while wave 0 walks this one (from registers, kPre chunks per LDS
         // batch, by readlane)
         const uint64_t c_lo = start & ~63ull, nch = (end - c_lo + 63) / 64;
@@ -1153,7 +1162,7 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         wp_finish_groups<<<blocks_for(n, 256), 256, 0, ks>>>(a, kc, view, rcs, succ, prev, ff, gend, kJumpFrom, big,
                                                              (uint32_t *)(tot + 1), junr);
         wp_jump_links<<<blocks_for(n, 256), 256, 0, ks>>>(a, kc, ff, gend, kJumpFrom, cfirst, jx, jm, junr);
-        wp_jump_chain<<<256, 1024, 0, ks>>>(a, kc, view, rcs, succ, prev, ff, gend, big, (uint32_t *)(tot + 1), jx, jm, ci,
+        wp_jump_chain<<<1024, kJumpThreads, 0, ks>>>(a, kc, view, rcs, succ, prev, ff, gend, big, (uint32_t *)(tot + 1), jx, jm, ci,
                                             gst, junr);
         wp_jump_codes<<<blocks_for(n, 256), 256, 0, ks>>>(a, kc, view, rcs, succ, prev, ff, gend, kJumpFrom, gst, junr, jm,
                                                           ci);
