@@ -103,7 +103,9 @@ def parse(argv=None):
     p.add_argument("--inflight-share", type=float, default=0.02,
                    help="c3: share of the update ops left in flight (uncommitted; keys beyond the 10^4 hottest) "
                         "so reads of them take the overwrite-copy (COPY) branch")
-    p.add_argument("--c3-epochs", type=int, default=8, help="timed YCSB-B epochs of the nested C3 leg")
+    p.add_argument("--c3-epochs", type=int, default=16,
+                   help="timed YCSB-B epochs of the nested C3 leg (the write pipeline's fill and the last "
+                        "epoch's host adoption are inside the timed loop, amortised over these; round 6: 8 -> 16)")
     p.add_argument("--write-path", choices=["device", "host"], default="device",
                    help="c3: apply each epoch's updates on the device (stage_update_batch_device) or on the "
                         "host write path + incremental publish (stage_update_batch + stage_sync)")
