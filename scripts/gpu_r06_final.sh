@@ -4,7 +4,7 @@
 # N > 1 line, then the profile set (scripts/profile_r06.sh).  Each step has its own time limit;
 # the first failure ends it.
 set -e
-out=gpurun_out/final6
+out=gpurun_out/final6b
 mkdir -p $out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests --durations=20 > $out/tests.log 2>&1
