@@ -219,7 +219,7 @@ __global__ __launch_bounds__(256) void wp_keys(const stage_probe_out_dev *__rest
 // step 3 preparation after the sort, a thread per sorted position: the op's fingerprints
 // gathered; a break where the group starts or the delta differs from its predecessor's (a
 // fingerprint mismatch, or equal fingerprints and unequal bytes)
-__global__ void wp_classify(WpArgs a, const uint64_t *__restrict__ fp_op, const uint64_t *__restrict__ wfp_op,
+__global__ __launch_bounds__(256) void wp_classify(WpArgs a, const uint64_t *__restrict__ fp_op, const uint64_t *__restrict__ wfp_op,
                             const uint8_t *__restrict__ eqw_op, uint32_t *__restrict__ brk, uint64_t *__restrict__ fp,
                             uint64_t *__restrict__ wfp, uint8_t *__restrict__ eqw) {
     const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -252,7 +252,7 @@ __device__ __forceinline__ uint64_t lanes_between(uint32_t from, uint32_t lane) 
     return below & ~skip;
 }
 
-__global__ void wp_heads(const uint64_t *__restrict__ loc, uint64_t n, uint32_t *__restrict__ head) {
+__global__ __launch_bounds__(256) void wp_heads(const uint64_t *__restrict__ loc, uint64_t n, uint32_t *__restrict__ head) {
     const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= n) return;
     head[q] = (q == 0 || loc[q] != loc[q - 1]) ? (uint32_t)q : 0u;
@@ -262,7 +262,7 @@ __global__ void wp_heads(const uint64_t *__restrict__ loc, uint64_t n, uint32_t 
 // (gend[g] = one past the group's last position) and the first position of every delta class
 // (cfirst; cls = inclusive sum of wp_classify's breaks, cfirst[last class + 1] = n, so the run
 // after a group's last run starts at or past the group's end)
-__global__ void wp_speculate(WpArgs a, WpCls k, DevTable t, uint8_t *__restrict__ rcs, uint8_t *__restrict__ succ,
+__global__ __launch_bounds__(256) void wp_speculate(WpArgs a, WpCls k, DevTable t, uint8_t *__restrict__ rcs, uint8_t *__restrict__ succ,
                              int32_t *__restrict__ prev, uint32_t *__restrict__ first_fail, uint32_t *__restrict__ gend,
                              const uint32_t *__restrict__ brk, uint32_t *__restrict__ cfirst) {
     const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // blockDim: a multiple of 64
@@ -718,7 +718,7 @@ __global__ __launch_bounds__(256) void wp_jump_codes(WpArgs a, WpCls kc, DevTabl
 }
 
 // step 4 input: successes in the low word, committed successes in the high word
-__global__ void wp_flags(WpArgs a, const uint8_t *__restrict__ succ, uint64_t *__restrict__ flags) {
+__global__ __launch_bounds__(256) void wp_flags(WpArgs a, const uint8_t *__restrict__ succ, uint64_t *__restrict__ flags) {
     const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= a.n) return;
     const uint64_t s = succ[q] ? 1ull : 0ull;
@@ -727,7 +727,7 @@ __global__ void wp_flags(WpArgs a, const uint8_t *__restrict__ succ, uint64_t *_
 
 // tot = {successes, committed successes, this epoch's copy / version / image bases}; the
 // device's append counters (bases) move past this epoch's entries
-__global__ void wp_totals(const uint64_t *__restrict__ ranks, const uint64_t *__restrict__ flags, uint64_t n,
+__global__ __launch_bounds__(256) void wp_totals(const uint64_t *__restrict__ ranks, const uint64_t *__restrict__ flags, uint64_t n,
                           uint64_t *__restrict__ tot, uint64_t *__restrict__ bases) {
     const uint64_t v = ranks[n - 1] + flags[n - 1];
     const uint64_t ns = v & 0xFFFFFFFFull, nv = v >> 32;
@@ -741,7 +741,7 @@ __global__ void wp_totals(const uint64_t *__restrict__ ranks, const uint64_t *__
     bases[2] += ns;
 }
 
-__global__ void wp_set_bases(uint64_t *__restrict__ bases, uint64_t c, uint64_t v, uint64_t i) {
+__global__ __launch_bounds__(256) void wp_set_bases(uint64_t *__restrict__ bases, uint64_t c, uint64_t v, uint64_t i) {
     bases[0] = c;
     bases[1] = v;
     bases[2] = i;
@@ -755,7 +755,7 @@ struct WRec {
 // step 5a, one thread per sorted position: a success writes its overwrite-copy header, the
 // retired-version header when committed, and its WRec; the last success of each group is
 // marked (last_succ; one atomic per group per wave)
-__global__ void wp_headers(WpArgs a, DevTable t, const uint8_t *__restrict__ succ, const int32_t *__restrict__ prev,
+__global__ __launch_bounds__(256) void wp_headers(WpArgs a, DevTable t, const uint8_t *__restrict__ succ, const int32_t *__restrict__ prev,
                            const uint64_t *__restrict__ ranks, CopyHdr *__restrict__ chdr, VersionHdr *__restrict__ vhdr,
                            uint32_t *__restrict__ last_succ, WRec *__restrict__ wrec, const uint64_t *__restrict__ tot,
                            uint32_t *__restrict__ cwriter) {
