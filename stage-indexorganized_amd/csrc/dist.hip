@@ -773,9 +773,9 @@ static void fan_launch(const stage_probe_out_dev *sout, const uint8_t *srec, uin
 // small launch whose latency the remote probes hide; joined by own_join); tables of other
 // geometries: probed into rout / rrec, then fanned out.  The remote segments are probed into
 // rout / rrec for the return transfer.  Owner reply: everything into rout / rrec, rows tagged
-// with their owner-local index.  Direct reply: each remote segment (one per source rank q) is
-// probed in fan-out form straight into caller q's d_out / d_records (c.dpeer), each request at
-// its first caller position (c.lpads); own requests as in the full reply.
+// with their owner-local index.  Direct reply: the whole chunk, one segment per source rank q
+// (this rank's own requests included), is probed in one fan-out launch straight into caller q's
+// d_out / d_records (c.dpeer), each request at its first caller position (c.lpads).
 static void chunk_probe(ShardComm &c, const Plan &P, int i, const DevTable &t, const ProbeTuning &tune, bool owner,
                         stage_probe_out_dev *d_out, uint8_t *d_recs, hipStream_t s, uint8_t *rows_buf = nullptr,
                         bool direct = false) {
@@ -806,18 +806,14 @@ static void chunk_probe(ShardComm &c, const Plan &P, int i, const DevTable &t, c
         tag_rows<<<blocks_for(e - b, 256), 256, 0, s>>>(rout + b, e - b, (uint32_t)b);
         return;
     }
-    if (direct) {  // the ranks below this one, then the ranks above: one launch each (direct_tables)
-        const FanDest *fd = (const FanDest *)c.fdest + 2 * (size_t)i;
-        if (r0 > b)
-            chk(launch_probe_fanout(t, lk + b, lr + b, r0 - b, nullptr, lp + b, nullptr, nullptr, s, tune, fd),
-                "direct probe");
-        if (e > r1)
-            chk(launch_probe_fanout(t, lk + r1, lr + r1, e - r1, nullptr, lp + r1, nullptr, nullptr, s, tune, fd + 1),
-                "direct probe");
-    } else {
-        probe(b, r0);
-        probe(r1, e);
+    if (direct) {  // every source rank's segment in one launch (direct_tables)
+        chk(launch_probe_fanout(t, lk + b, lr + b, e - b, nullptr, lp + b, nullptr, nullptr, s, tune,
+                                (const FanDest *)c.fdest + i),
+            "direct probe");
+        return;
     }
+    probe(b, r0);
+    probe(r1, e);
     if (r1 == r0) return;
     if (d_recs && probe_fanout_supported(t)) {
         hipStream_t os = c.ps;  // beside the remote probes (on s: slower)
@@ -1020,47 +1016,42 @@ static void chunk_return_peer(ShardComm &c, const Plan &P, const PeerCounts &pc,
 // since), then the duplicates of each coalesced request copied from its first caller position.
 static void chunk_return_direct(ShardComm &c, const Plan &P, int i, uint32_t stride, stage_probe_out_dev *d_out,
                                 uint8_t *d_recs, hipStream_t s) {
-    const int W = P.W, me = c.rank;
+    const int W = P.W;
     peer_acquire_kernel<<<256, 64, 0, s>>>();
     if (!P.dedupe) return;  // one caller per request: nothing to copy
     constexpr int R = 4;
-    // the requests sent to other ranks: send positions [p0, q0) and [q1, pz) (own ones, [q0, q1),
-    // were probed straight to every caller position)
+    // every request of the chunk, this rank's own ones included: send positions [p0, pz)
     const uint64_t p0 = P.cb[i], pz = P.soff[(size_t)i * (W + 1) + W];
-    const uint64_t q0 = P.soff[(size_t)i * (W + 1) + me], q1 = P.soff[(size_t)i * (W + 1) + me + 1];
-    for (const auto &rg : {std::make_pair(p0, q0), std::make_pair(q1, pz)})
-        if (rg.second > rg.first)
-            dup_copy<R><<<(unsigned)std::min<uint64_t>((rg.second - rg.first + 4 * R - 1) / (4 * R), 8192), 256, 0, s>>>(
-                rg.first, rg.second, (const FanRange *)c.fan, (const uint32_t *)c.flist, stride, d_out, d_recs);
+    if (pz > p0)
+        dup_copy<R><<<(unsigned)std::min<uint64_t>((pz - p0 + 4 * R - 1) / (4 * R), 8192), 256, 0, s>>>(
+            p0, pz, (const FanRange *)c.fan, (const uint32_t *)c.flist, stride, d_out, d_recs);
     chk(hipGetLastError(), "direct duplicates");
 }
 
-// the FanDest tables of every chunk's two remote ranges -- receive positions [b, r0) from the
-// ranks below this one and [r1, e) from those above, one segment per source rank -- from the
-// plan and c.dpeer, staged in pinned memory and copied to the device on s (the staging is
-// rewritten only after the next call's count exchange has synchronised s)
+// the FanDest table of every chunk -- receive positions [b, e), one segment per source rank q
+// (the own one, read from the send buffer, in its place between the ranks below and above) --
+// from the plan and c.dpeer, staged in pinned memory and copied to the device on s (the staging
+// is rewritten only after the next call's count exchange has synchronised s)
 static void direct_tables(ShardComm &c, const Plan &P, hipStream_t s) {
-    const int W = P.W, C = P.C, me = c.rank;
-    const size_t bytes = (size_t)2 * kMaxChunks * sizeof(FanDest);
+    const int W = P.W, C = P.C;
+    static_assert(kMaxWorld <= kFanDests, "a segment per source rank");
+    const size_t bytes = (size_t)kMaxChunks * sizeof(FanDest);
     if (!c.fdest) {
         grow(c.fdest, bytes);
         chk(hipHostMalloc(&c.fdest_h, bytes, hipHostMallocDefault), "hipHostMalloc");
     }
     FanDest *h = (FanDest *)c.fdest_h;
-    for (int i = 0; i < C; ++i)
-        for (int side = 0; side < 2; ++side) {
-            FanDest &d = h[2 * i + side];
-            d.nseg = 0;
-            const int qa = side ? me + 1 : 0, qz = side ? W : me;
-            const uint64_t start = P.roff[(size_t)i * (W + 1) + qa];
-            for (int q = qa; q < qz; ++q) {
-                d.end[d.nseg] = (uint32_t)(P.roff[(size_t)i * (W + 1) + q + 1] - start);
-                d.out[d.nseg] = (stage_probe_out_dev *)c.dpeer[0][q];
-                d.recs[d.nseg] = (uint8_t *)c.dpeer[1][q];
-                ++d.nseg;
-            }
+    for (int i = 0; i < C; ++i) {
+        FanDest &d = h[i];
+        d.nseg = (uint32_t)W;
+        const uint64_t start = P.roff[(size_t)i * (W + 1)];
+        for (int q = 0; q < W; ++q) {
+            d.end[q] = (uint32_t)(P.roff[(size_t)i * (W + 1) + q + 1] - start);
+            d.out[q] = (stage_probe_out_dev *)c.dpeer[0][q];
+            d.recs[q] = (uint8_t *)c.dpeer[1][q];
         }
-    chk(hipMemcpyAsync(c.fdest, h, (size_t)2 * C * sizeof(FanDest), hipMemcpyHostToDevice, s), "direct tables");
+    }
+    chk(hipMemcpyAsync(c.fdest, h, (size_t)C * sizeof(FanDest), hipMemcpyHostToDevice, s), "direct tables");
 }
 
 // this rank's d_out / d_records as another process opens it: the allocation's IPC handle and the
