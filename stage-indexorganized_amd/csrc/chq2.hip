@@ -655,7 +655,7 @@ static int q2_run(stage_table *region, stage_table *nation, stage_table *supplie
         auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
         const uint64_t q_map = 0, q_rq = q_map + al((kMapKeys + 1) * 4ull), q_cn = q_rq + al(nq * 4ull),
                        q_ab = q_cn + 16, q_zero = q_ab + al(nq * 4ull), q_end = q_zero + 16;
-        uint8_t *pq = pinned_bytes(stock->dev, q_end, 2 + slot);
+        uint8_t *pq = pinned_bytes(stock->dev, q_end, kQ2Pinned + slot);
         std::memcpy(pq + q_map, map_off, (kMapKeys + 1) * 4ull);
         std::memcpy(pq + q_rq, rq, nq * 4ull);
         std::memset(pq + q_cn, 0, 16 + nq * 4ull);

@@ -28,18 +28,22 @@ DeviceImage::~DeviceImage() { release(); }
 
 void DeviceImage::release() {
     for (DevBuf *b :
-         {&head, &okey, &slot, &tree, &tree_len, &heap, &chdr, &vhdr, &arena, &descs, &patch, &scratch, &wp_scratch, &wp_out[0],
-          &wp_out[1], &wp_bases}) {
+         {&head, &okey, &slot, &tree, &tree_len, &heap, &chdr, &vhdr, &arena, &descs, &patch, &scratch, &wp_scratch, &wp_bases}) {
         if (b->p) (void)hipFree(b->p);
         b->p = nullptr;
         b->cap = 0;
     }
-    for (int k = 0; k < 4; ++k) {
+    for (DevBuf *b = wp_out; b != wp_out + kWpDepth; ++b) {
+        if (b->p) (void)hipFree(b->p);
+        b->p = nullptr;
+        b->cap = 0;
+    }
+    for (int k = 0; k < kQ2Pinned + 2; ++k) {
         if (pinned[k]) (void)hipHostFree(pinned[k]);
         pinned[k] = nullptr;
         pinned_cap[k] = 0;
     }
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < kWpDepth; ++k) {
         if (adopt_ev[k]) (void)hipEventDestroy(adopt_ev[k]);
         adopt_ev[k] = nullptr;
         if (export_ev[k]) (void)hipEventDestroy(export_ev[k]);

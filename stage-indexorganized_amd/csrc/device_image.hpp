@@ -18,6 +18,14 @@ struct DevBuf {
     uint64_t cap = 0;
 };
 
+// device write-path epochs in flight: epoch e's outputs are reused by epoch e + kWpDepth, whose
+// call waits for e's host adoption.  Three: an epoch is adopted ~2.7 epochs after its call starts
+// (its kernels run beside the previous epoch's probe, its export beside its own, then ~3.7 ms
+// of host work), so with two the next-but-one call waited for it and its kernels reached the
+// device too late to hide under the probe (§5r6)
+constexpr int kWpDepth = 3;
+constexpr int kQ2Pinned = kWpDepth;  // first pinned staging slot of CH-Q2
+
 struct DeviceImage {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -25,14 +33,14 @@ struct DeviceImage {
     DevBuf scratch;     // per-call scratch of stock-level / CH-Q2 / scans (scratch_bytes)
     DevBuf wp_scratch;  // the device write path's own scratch (wp_scratch_bytes): an overlapped
                         // epoch runs beside the caller's later work on the shared scratch
-    // the device write path's per-epoch outputs, double-buffered by epoch parity: epoch e's
-    // background adoption reads wp_out[e % 2] / pinned[e % 2] while epoch e + 1 runs
-    DevBuf wp_out[2];  // slot words + totals
+    // the device write path's per-epoch outputs, kWpDepth-buffered by epoch: epoch e's background
+    // adoption reads wp_out[e % kWpDepth] / pinned[e % kWpDepth] while epochs e + 1, e + 2 run
+    DevBuf wp_out[kWpDepth];  // slot words + totals
     DevBuf wp_bases;   // the next epoch's copy / version / image indices (device-side append counters)
     uint64_t wp_ub[3] = {0, 0, 0};       // upper bounds of those counters (copies, versions, images)
     hipStream_t adopt_stream = nullptr;  // the adoption's D2H copies (beside the caller's stream)
-    hipEvent_t adopt_ev[2] = {nullptr, nullptr};  // end of an epoch's write-path kernels
-    hipEvent_t export_ev[2] = {nullptr, nullptr}; // end of its export into pinned host memory
+    hipEvent_t adopt_ev[kWpDepth] = {};   // end of an epoch's write-path kernels
+    hipEvent_t export_ev[kWpDepth] = {};  // end of its export into pinned host memory
     // write-overlap mode (stage_set_write_overlap): an epoch's kernels up to the publish run on
     // wp_stream after the previous epoch's publish (wp_pub_ev), beside the caller's later work;
     // the publish joins the caller's stream (wp_pre_ev).  wp_pub_valid: wp_pub_ev marks the
@@ -41,10 +49,10 @@ struct DeviceImage {
     hipEvent_t wp_pub_ev = nullptr, wp_pre_ev = nullptr;
     bool wp_pub_valid = false;
     std::vector<uint8_t> staging;  // host staging of incremental patches
-    // pinned host staging: [0], [1] the write path's epoch results (by epoch parity); [2] the
-    // host copies of one synchronous call (CH-Q2's scan rows, supplier list, records)
-    void *pinned[4] = {nullptr, nullptr, nullptr, nullptr};  // 0 / 1: write-path adoption; 2 / 3: CH-Q2 slots
-    uint64_t pinned_cap[4] = {0, 0, 0, 0};
+    // pinned host staging: [0, kWpDepth) the write path's epoch results (by epoch % kWpDepth);
+    // [kQ2Pinned, kQ2Pinned + 2) CH-Q2's two batch slots (scan rows, supplier list, records)
+    void *pinned[kQ2Pinned + 2] = {};
+    uint64_t pinned_cap[kQ2Pinned + 2] = {};
     uint64_t heap_rows = 0;  // rows the heap buffer can hold
     DevTable view{};
     std::vector<uint32_t> host_to_dev;  // host leaf id -> leaf index in key order

@@ -89,7 +89,7 @@ struct stage_table {
     std::atomic<uint64_t> wp_adopted{0}; // device epochs adopted (or failed) -- in order
     std::atomic<bool> adopt_failed{false};
     std::atomic<uint64_t> adopted_sz[3] = {{0}, {0}, {0}};  // host copies / versions / images after the last adoption
-    uint64_t wp_epoch_n[2] = {0, 0};                          // ops of the writer's last two epochs (by parity)
+    uint64_t wp_epoch_n[stage::kWpDepth] = {};                       // ops of the writer's last epochs (by epoch % kWpDepth)
     void settle() {
         std::lock_guard<std::mutex> g(adopt_mu);
         if (adopt.joinable()) adopt.join();
@@ -113,7 +113,7 @@ struct stage_table {
             wp_adopted.store(epoch, std::memory_order_release);
         });
     }
-    // the writer waits until epoch `epoch` is adopted (its double-buffered outputs are free)
+    // the writer waits until epoch `epoch` is adopted (its kWpDepth-buffered outputs are free)
     void wait_adopted(uint64_t epoch) {
         while (wp_adopted.load(std::memory_order_acquire) < epoch) std::this_thread::sleep_for(std::chrono::microseconds(20));
     }

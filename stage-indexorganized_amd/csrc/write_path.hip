@@ -957,9 +957,9 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         const auto t0 = clk::now();
         static const auto g0 = t0;  // trace: the first call's start
         auto ms = [&](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
-        // epoch e uses output buffers e % 2: epoch e - 2's adoption must be done with them
+        // epoch e uses output buffers e % kWpDepth: epoch e - kWpDepth's adoption must be done with them
         const uint64_t epoch = ++t->wp_started;
-        const int par = (int)(epoch & 1);
+        const int par = (int)(epoch % kWpDepth);
         // an epoch that fails before its adoption starts still counts as adopted -- with a
         // sticky error (the device may hold part of it): later calls neither hang nor go on
         // -- unless nothing of it reached the device yet (an allocation or stream / event creation
@@ -977,11 +977,14 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
                 t->start_adoption(epoch, [] { throw std::runtime_error("a device write-path epoch failed"); });
             }
         } guard{t, epoch};
-        if (epoch > 2) t->wait_adopted(epoch - 2);
+        if (epoch > (uint64_t)kWpDepth) t->wait_adopted(epoch - kWpDepth);
         if (t->adopt_failed.load(std::memory_order_acquire)) t->settle();  // rethrows the adoption's error
-        // pending: epoch e - 1 is still being adopted, so the device's append counters are ahead
-        // of the host table; otherwise (no epoch in flight) they are set from the host's counts
-        bool pending = t->wp_adopted.load(std::memory_order_acquire) + 1 < epoch;
+        // pending: epochs (adopted, e) are still being adopted, so the device's append counters
+        // are ahead of the host table; otherwise (no epoch in flight) they are set from the
+        // host's counts.  wp_adopted is read before adopted_sz (stored after it): the bound below
+        // can only come out high
+        const uint64_t adopted = t->wp_adopted.load(std::memory_order_acquire);
+        bool pending = adopted + 1 < epoch;
         if (!dv.wp_bases.p) {
             hip_check(hipMalloc(&dv.wp_bases.p, 64), "wp bases");
             dv.wp_bases.cap = 64;
@@ -996,7 +999,9 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
             ub[0] = h.copies_.size(), ub[1] = h.versions_.size(), ub[2] = h.images_.size();
             for (int k = 0; k < 3; ++k) t->adopted_sz[k].store(ub[k], std::memory_order_relaxed);
         } else {
-            for (int k = 0; k < 3; ++k) ub[k] = t->adopted_sz[k].load(std::memory_order_acquire) + t->wp_epoch_n[par ^ 1];
+            uint64_t inflight = 0;  // the ops of epochs adopted + 1 .. e - 1 (at most kWpDepth - 1 of them)
+            for (uint64_t j = adopted + 1; j < epoch; ++j) inflight += t->wp_epoch_n[j % kWpDepth];
+            for (int k = 0; k < 3; ++k) ub[k] = t->adopted_sz[k].load(std::memory_order_acquire) + inflight;
         }
         const bool fits = dv.heap_rows >= ub[2] + n && dv.chdr.cap >= (ub[0] + n) * sizeof(CopyHdr) &&
                           dv.vhdr.cap >= (ub[1] + n) * sizeof(VersionHdr) && dv.chdr.p && dv.vhdr.p && dv.heap.p;
@@ -1020,8 +1025,9 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
             hip_check(hipDeviceGetStreamPriorityRange(&lo, &hi), "stream priorities");
             hip_check(hipStreamCreateWithPriority(&dv.adopt_stream, hipStreamNonBlocking, hi), "adopt stream");
         }
-        for (hipEvent_t *e : {&dv.adopt_ev[0], &dv.adopt_ev[1], &dv.export_ev[0], &dv.export_ev[1]})
-            if (!*e) hip_check(hipEventCreateWithFlags(e, hipEventDisableTiming), "adopt event");
+        for (int k = 0; k < kWpDepth; ++k)
+            for (hipEvent_t *e : {&dv.adopt_ev[k], &dv.export_ev[k]})
+                if (!*e) hip_check(hipEventCreateWithFlags(e, hipEventDisableTiming), "adopt event");
         const DevTable &view = dv.view;
         const uint64_t none = (uint64_t)view.nleaves * view.cap;
         int end_bit = 1;
@@ -1092,11 +1098,11 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         auto *fp_op = (uint64_t *)(buf + o_fpo), *wfp_op = (uint64_t *)(buf + o_wfpo);
         auto *eqw_op = buf + o_eqwo;
         // slot words + totals: read back after this call returns (background adoption)
-        // both parities are sized together when no adoption is reading the other one: a first
-        // use inside a run of epochs would allocate (and drain the device) in the middle of it
+        // every epoch's buffers are sized together when no adoption is reading another one: a
+        // first use inside a run of epochs would allocate (and drain the device) in the middle of it
         const uint64_t wo_bytes = al(n * sizeof(FinRec)) + 256 + al(n * 4);
         uint8_t *wo = wp_out_bytes(dv, wo_bytes, par);
-        if (!pending) wp_out_bytes(dv, wo_bytes, par ^ 1);
+        for (int k = 0; k < kWpDepth && !pending; ++k) wp_out_bytes(dv, wo_bytes, k);
         auto *fin = (FinRec *)wo;
         auto *tot = (uint64_t *)(wo + al(n * sizeof(FinRec)));
         auto *cwriter = (uint32_t *)(wo + al(n * sizeof(FinRec)) + 256);  // writer id per new copy
@@ -1110,7 +1116,7 @@ extern "C" int stage_update_batch_device(stage_table *t, const uint64_t *d_keys,
         const uint64_t bf = n * sizeof(FinRec), bmax = 2 * n * sizeof(CopyHdr), bw = n * 4;
         static_assert(sizeof(CopyHdr) == sizeof(VersionHdr) && sizeof(CopyHdr) % 16 == 0, "header sizes");
         uint8_t *pin = pinned_bytes(dv, 64 + bmax + bf + bw, par);
-        if (!pending) pinned_bytes(dv, 64 + bmax + bf + bw, par ^ 1);
+        for (int k = 0; k < kWpDepth && !pending; ++k) pinned_bytes(dv, 64 + bmax + bf + bw, k);
         // write-overlap mode: the kernels up to the publish go on the table's write stream ks,
         // which waits for the previous epoch's publish only (or, when the device image changed
         // otherwise since, for all of s) -- not for the caller's work enqueued after it, such as
