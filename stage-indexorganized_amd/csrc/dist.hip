@@ -766,6 +766,13 @@ static void fan_launch(const stage_probe_out_dev *sout, const uint8_t *srec, uin
     chk(hipGetLastError(), "fan copy");
 }
 
+// STAGE_REPLY_DIRECT: from this many ranks on, a rank's own requests (1/W of a chunk) are probed
+// in the chunk's one launch with the remote ones; below it, on their own stream beside the remote
+// probes, where they overlap the key exchange.  Measured: W = 8 loopback 16.6 → 12.8
+// ms per 2^24 lookups merged; the 2-rank RCCL rehearsal 26.7-28.7 merged vs 24.2-25.4 ms apart
+constexpr int kDirectMergeFrom = 4;
+static inline bool direct_merge(int W) { return W >= kDirectMergeFrom; }
+
 // Probe what chunk i holds for this rank.  The remote segments arrived in recv; this rank's own
 // requests never left the device (no self transfer): they are read from the send buffer.
 // Full reply: own requests are probed in fan-out form, straight to their caller positions in
@@ -773,9 +780,11 @@ static void fan_launch(const stage_probe_out_dev *sout, const uint8_t *srec, uin
 // small launch whose latency the remote probes hide; joined by own_join); tables of other
 // geometries: probed into rout / rrec, then fanned out.  The remote segments are probed into
 // rout / rrec for the return transfer.  Owner reply: everything into rout / rrec, rows tagged
-// with their owner-local index.  Direct reply: the whole chunk, one segment per source rank q
-// (this rank's own requests included), is probed in one fan-out launch straight into caller q's
-// d_out / d_records (c.dpeer), each request at its first caller position (c.lpads).
+// with their owner-local index.  Direct reply: the chunk, one segment per source rank q, is probed
+// in fan-out form straight into caller q's d_out / d_records (c.dpeer), each request at its first
+// caller position (c.lpads) -- from kDirectMergeFrom ranks on in one launch with this rank's own
+// requests as one more segment, below it in two (the ranks below / above this one) with the own
+// requests as in the full reply.
 static void chunk_probe(ShardComm &c, const Plan &P, int i, const DevTable &t, const ProbeTuning &tune, bool owner,
                         stage_probe_out_dev *d_out, uint8_t *d_recs, hipStream_t s, uint8_t *rows_buf = nullptr,
                         bool direct = false) {
@@ -806,14 +815,23 @@ static void chunk_probe(ShardComm &c, const Plan &P, int i, const DevTable &t, c
         tag_rows<<<blocks_for(e - b, 256), 256, 0, s>>>(rout + b, e - b, (uint32_t)b);
         return;
     }
-    if (direct) {  // every source rank's segment in one launch (direct_tables)
-        chk(launch_probe_fanout(t, lk + b, lr + b, e - b, nullptr, lp + b, nullptr, nullptr, s, tune,
-                                (const FanDest *)c.fdest + i),
-            "direct probe");
-        return;
+    if (direct) {  // direct_tables: [2i] the whole chunk (merged) or the ranks below, [2i + 1] those above
+        const FanDest *fd = (const FanDest *)c.fdest + 2 * (size_t)i;
+        if (direct_merge(W)) {
+            chk(launch_probe_fanout(t, lk + b, lr + b, e - b, nullptr, lp + b, nullptr, nullptr, s, tune, fd),
+                "direct probe");
+            return;
+        }
+        if (r0 > b)
+            chk(launch_probe_fanout(t, lk + b, lr + b, r0 - b, nullptr, lp + b, nullptr, nullptr, s, tune, fd),
+                "direct probe");
+        if (e > r1)
+            chk(launch_probe_fanout(t, lk + r1, lr + r1, e - r1, nullptr, lp + r1, nullptr, nullptr, s, tune, fd + 1),
+                "direct probe");
+    } else {
+        probe(b, r0);
+        probe(r1, e);
     }
-    probe(b, r0);
-    probe(r1, e);
     if (r1 == r0) return;
     if (d_recs && probe_fanout_supported(t)) {
         hipStream_t os = c.ps;  // beside the remote probes (on s: slower)
@@ -1020,38 +1038,48 @@ static void chunk_return_direct(ShardComm &c, const Plan &P, int i, uint32_t str
     peer_acquire_kernel<<<256, 64, 0, s>>>();
     if (!P.dedupe) return;  // one caller per request: nothing to copy
     constexpr int R = 4;
-    // every request of the chunk, this rank's own ones included: send positions [p0, pz)
+    // the requests of the chunk, send positions [p0, pz) -- without this rank's own ones, [q0, q1),
+    // when they were probed straight to every caller position (below kDirectMergeFrom ranks)
     const uint64_t p0 = P.cb[i], pz = P.soff[(size_t)i * (W + 1) + W];
-    if (pz > p0)
-        dup_copy<R><<<(unsigned)std::min<uint64_t>((pz - p0 + 4 * R - 1) / (4 * R), 8192), 256, 0, s>>>(
-            p0, pz, (const FanRange *)c.fan, (const uint32_t *)c.flist, stride, d_out, d_recs);
+    uint64_t q0 = P.soff[(size_t)i * (W + 1) + c.rank], q1 = P.soff[(size_t)i * (W + 1) + c.rank + 1];
+    if (direct_merge(W)) q0 = q1 = pz;
+    for (const auto &rg : {std::make_pair(p0, q0), std::make_pair(q1, pz)})
+        if (rg.second > rg.first)
+            dup_copy<R><<<(unsigned)std::min<uint64_t>((rg.second - rg.first + 4 * R - 1) / (4 * R), 8192), 256, 0, s>>>(
+                rg.first, rg.second, (const FanRange *)c.fan, (const uint32_t *)c.flist, stride, d_out, d_recs);
     chk(hipGetLastError(), "direct duplicates");
 }
 
-// the FanDest table of every chunk -- receive positions [b, e), one segment per source rank q
-// (the own one, read from the send buffer, in its place between the ranks below and above) --
-// from the plan and c.dpeer, staged in pinned memory and copied to the device on s (the staging
-// is rewritten only after the next call's count exchange has synchronised s)
+// the FanDest tables of every chunk, one segment per source rank q -- from kDirectMergeFrom ranks
+// on [2i] covers receive positions [b, e) (the own segment, read from the send buffer, in its
+// place between the ranks below and above); below it [2i] covers [b, r0) from the ranks below
+// this one and [2i + 1] [r1, e) from those above -- from the plan and c.dpeer, staged in pinned
+// memory and copied to the device on s (the staging is rewritten only after the next call's count
+// exchange has synchronised s)
 static void direct_tables(ShardComm &c, const Plan &P, hipStream_t s) {
-    const int W = P.W, C = P.C;
+    const int W = P.W, C = P.C, me = c.rank;
     static_assert(kMaxWorld <= kFanDests, "a segment per source rank");
-    const size_t bytes = (size_t)kMaxChunks * sizeof(FanDest);
+    const size_t bytes = (size_t)2 * kMaxChunks * sizeof(FanDest);
     if (!c.fdest) {
         grow(c.fdest, bytes);
         chk(hipHostMalloc(&c.fdest_h, bytes, hipHostMallocDefault), "hipHostMalloc");
     }
     FanDest *h = (FanDest *)c.fdest_h;
-    for (int i = 0; i < C; ++i) {
-        FanDest &d = h[i];
-        d.nseg = (uint32_t)W;
-        const uint64_t start = P.roff[(size_t)i * (W + 1)];
-        for (int q = 0; q < W; ++q) {
-            d.end[q] = (uint32_t)(P.roff[(size_t)i * (W + 1) + q + 1] - start);
-            d.out[q] = (stage_probe_out_dev *)c.dpeer[0][q];
-            d.recs[q] = (uint8_t *)c.dpeer[1][q];
+    const bool merge = direct_merge(W);
+    for (int i = 0; i < C; ++i)
+        for (int side = 0; side < 2; ++side) {
+            FanDest &d = h[2 * i + side];
+            d.nseg = 0;
+            const int qa = merge ? (side ? W : 0) : (side ? me + 1 : 0), qz = merge ? W : (side ? W : me);
+            const uint64_t start = P.roff[(size_t)i * (W + 1) + qa];
+            for (int q = qa; q < qz; ++q) {
+                d.end[d.nseg] = (uint32_t)(P.roff[(size_t)i * (W + 1) + q + 1] - start);
+                d.out[d.nseg] = (stage_probe_out_dev *)c.dpeer[0][q];
+                d.recs[d.nseg] = (uint8_t *)c.dpeer[1][q];
+                ++d.nseg;
+            }
         }
-    }
-    chk(hipMemcpyAsync(c.fdest, h, (size_t)C * sizeof(FanDest), hipMemcpyHostToDevice, s), "direct tables");
+    chk(hipMemcpyAsync(c.fdest, h, (size_t)2 * C * sizeof(FanDest), hipMemcpyHostToDevice, s), "direct tables");
 }
 
 // this rank's d_out / d_records as another process opens it: the allocation's IPC handle and the
